@@ -1,0 +1,170 @@
+"""Single-GPU (per rank) Ape-X engine: actor shard + HBM replay + fused learner.
+
+This is the MI355X-native replacement for the reference's three process kinds
+(actor / replay server / learner talking ZeroMQ + pickle) on one GPU:
+
+* actor shard: ``n_envs`` GPU envs with the global epsilon ladder (ActorShard)
+* replay: HBM frame ring + fanout-64 priority tree (HBMReplay)
+* learner: fused double-DQN step (DQNLearner)
+
+Each is a static sequence of kernels captured once into a hipGraph (via
+``torch.cuda.CUDAGraph``) and replayed; the host only replays graphs and counts
+steps.  Reference cadences are kept: params published to the actors every
+``publish_param_interval`` learner steps (learner.py:169, 25), target sync every
+``target_update_interval`` (learner.py:163, 2500), learning starts after
+``threshold_size`` transitions (replay.py:104, 50,000).  In data-parallel mode (one
+rank per GPU, ``apex_amd.parallel``), the flat gradient is all-reduced over RCCL
+between the two learner graphs.
+"""
+from __future__ import annotations
+
+import copy
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models.dqn import DuelingDQN
+from .actor_shard import ActorShard
+from .hbm_replay import HBMReplay
+from .learner import DQNLearner, LearnerConfig, forward_q
+
+
+@dataclass
+class EngineConfig:
+    n_envs: int = 256                    # actors (envs) on this GPU
+    n_actions: int = 18                  # Seaquest (the reference's published run)
+    replay_capacity: int = 2_000_000     # arguments.py --replay_buffer_size
+    alpha: float = 0.6
+    threshold_size: int = 50_000
+    actor_steps_per_learner_step: int = 1
+    publish_param_interval: int = 25
+    target_update_interval: int = 2500
+    nstep_mode: str = "reference"
+    eps_base: float = 0.4
+    eps_alpha: float = 7.0
+    actor_offset: int = 0
+    total_actors: int | None = None
+    use_graphs: bool = True
+    exact_mass: bool = True
+    seed: int = 1122
+    learner: LearnerConfig = field(default_factory=LearnerConfig)
+
+
+class ApexEngine:
+    def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", allreduce=None,
+                 model: DuelingDQN | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        lc = cfg.learner
+        torch.manual_seed(cfg.seed)
+        self.replay = HBMReplay(cfg.replay_capacity, cfg.n_envs, lc.n_step, cfg.alpha, self.device,
+                                exact_mass=cfg.exact_mass, seed=cfg.seed)
+        self.actor = ActorShard(self.replay, cfg.n_envs, cfg.n_actions, lc.n_step, lc.gamma, cfg.eps_base,
+                                cfg.eps_alpha, cfg.actor_offset, cfg.total_actors, cfg.seed, cfg.nstep_mode)
+        model = model if model is not None else DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions)
+        self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce)
+        self.actor_model = copy.deepcopy(self.learner.model)
+        self.actor_model._flat = None
+        self.actor_flat = self.actor_model.flatten_parameters()
+        for p in self.actor_model.parameters():
+            p.requires_grad_(False)
+            p.grad = None
+        self.learner.copy_params_to(self.actor_flat)
+        self.learn_steps = 0
+        self.actor_steps = 0
+        self._g_actor = self._g_learn_a = self._g_learn_b = None
+        self._pool = None
+        self._allreduce = allreduce
+
+    # ------------------------------------------------------------------ eager bodies
+    def _actor_body(self):
+        obs = self.actor.observe()
+        with torch.no_grad():
+            q = forward_q(self.actor_model, obs)
+        self.actor.act_and_step(q)
+
+    def _learn_a(self):
+        self.learner.sample_and_forward()
+
+    def _learn_b(self):
+        self.learner.optimize()
+
+    # ------------------------------------------------------------------ graphs
+    def capture(self, warmup_iters: int = 3) -> None:
+        """Warm up on a side stream, then capture actor and learner steps as hipGraphs."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup_iters):
+                self._actor_body()
+                self._learn_a()
+                if self._allreduce is not None:
+                    self._allreduce(self.learner.flat_grad)
+                self._learn_b()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._pool = torch.cuda.graph_pool_handle()
+        self._g_actor = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_actor, pool=self._pool):
+            self._actor_body()
+        self._g_learn_a = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_learn_a, pool=self._pool):
+            self._learn_a()
+        self._g_learn_b = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_learn_b, pool=self._pool):
+            self._learn_b()
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ steps
+    def actor_step(self) -> None:
+        if self._g_actor is not None:
+            self._g_actor.replay()
+        else:
+            self._actor_body()
+        self.actor_steps += 1
+
+    def learner_step(self) -> None:
+        if self._g_learn_a is not None:
+            self._g_learn_a.replay()
+            if self._allreduce is not None:
+                self._allreduce(self.learner.flat_grad)
+            self._g_learn_b.replay()
+        else:
+            self._learn_a()
+            if self._allreduce is not None:
+                self._allreduce(self.learner.flat_grad)
+            self._learn_b()
+        self.learn_steps += 1
+        if self.learn_steps % self.cfg.publish_param_interval == 0:
+            self.learner.copy_params_to(self.actor_flat)
+        if self.learn_steps % self.cfg.target_update_interval == 0:
+            self.learner.sync_target()
+
+    def fill(self, min_transitions: int | None = None) -> None:
+        """Run actor steps until the replay holds ``threshold_size`` slots."""
+        need = self.cfg.threshold_size if min_transitions is None else min_transitions
+        steps = -(-need // self.cfg.n_envs)
+        for _ in range(max(steps, 4)):
+            self.actor_step()
+
+    def train_step(self) -> None:
+        """One Ape-X step of this rank: one learner SGD step + its actor steps."""
+        self.learner_step()
+        for _ in range(self.cfg.actor_steps_per_learner_step):
+            self.actor_step()
+
+    def run(self, n_steps: int) -> float:
+        torch.cuda.synchronize(self.device)
+        t0 = time.perf_counter()
+        for _ in range(n_steps):
+            self.train_step()
+        torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
+    @property
+    def frames_per_actor_step(self) -> int:
+        return self.cfg.n_envs * 4  # action repeat 4 (MaxAndSkipEnv)
+
+    def save(self, path: str) -> None:
+        torch.save(self.learner.model.state_dict(), path)

@@ -1,0 +1,144 @@
+"""HBM-resident prioritized replay.
+
+Layout on the GPU (all ``torch`` allocations on one device):
+
+* ``frames``  u8 [F, 84*84]  -- every observed frame stored once (frame ring)
+* ``s_ids`` / ``s2_ids`` int32 [C, 4] -- frame ids of the stacked s / s'
+* ``action`` int32 [C], ``reward`` f32 [C] (n-step return), ``done`` f32 [C]
+* the fanout-64 priority tree (``_apex_hip`` ``per_*`` kernels): fp32 leaves
+  (sum + min), fp64 internal sums, fp32 internal mins
+* ``max_prio`` f32 [1]; ``filled`` i64 [1] (slots written, read on device by the
+  sampler so a captured graph sees the live fill level)
+
+Frame dedup makes 1M transitions ~7.1 GB and 10M ~71 GB (fits 288 GB of HBM3E); the
+reference's Python list of LazyFrames under one lock is replaced by device kernels
+that never sync with the host.
+
+API mirrors the reference buffer (``sample(B, beta)``, ``update_priorities``) but
+everything stays on device: ``sample`` returns device tensors, priorities are
+device tensors, nothing is copied to the host.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+
+FRAME_BYTES = 84 * 84
+
+
+def tree_level_sizes(capacity: int) -> list[int]:
+    sizes = [int(capacity)]
+    while sizes[-1] > 1:
+        sizes.append((sizes[-1] + 63) // 64)
+    if len(sizes) == 1:  # capacity 1: still need one internal level
+        sizes.append(1)
+    return sizes
+
+
+class HBMReplay:
+    def __init__(self, capacity: int, n_envs: int, n_step: int = 3, alpha: float = 0.6,
+                 device: str | torch.device = "cuda", frame_bytes: int = FRAME_BYTES,
+                 frame_capacity: int | None = None, exact_mass: bool = True, seed: int = 0):
+        self.hip = ops.hip()
+        self.device = torch.device(device)
+        self.capacity = int(capacity)
+        self.n_envs = int(n_envs)
+        self.alpha = float(alpha)
+        self.frame_bytes = int(frame_bytes)
+        # frames must outlive every transition that references them (see actor_kernels.hip)
+        self.frame_capacity = int(frame_capacity or (self.capacity + (2 * n_step + 8) * self.n_envs))
+        self.exact_mass = exact_mass
+        self.seed = int(seed)
+        dev = self.device
+        C = self.capacity
+        self.frames = torch.zeros(self.frame_capacity, self.frame_bytes, dtype=torch.uint8, device=dev)
+        self.s_ids = torch.zeros(C, 4, dtype=torch.int32, device=dev)
+        self.s2_ids = torch.zeros(C, 4, dtype=torch.int32, device=dev)
+        self.action = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.reward = torch.zeros(C, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(C, dtype=torch.float32, device=dev)
+        sizes = tree_level_sizes(C)
+        self.level_sizes = sizes
+        self.leaf_sum = torch.zeros(C, dtype=torch.float32, device=dev)
+        self.leaf_min = torch.full((C,), math.inf, dtype=torch.float32, device=dev)
+        self.node_sum = [torch.zeros(n, dtype=torch.float64, device=dev) for n in sizes[1:]]
+        self.node_min = [torch.full((n,), math.inf, dtype=torch.float32, device=dev) for n in sizes[1:]]
+        self.max_prio = torch.ones(1, dtype=torch.float32, device=dev)
+        self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
+                                       [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
+                                       sizes)
+
+    # ------------------------------------------------------------------ bytes
+    def nbytes(self) -> int:
+        tensors = [self.frames, self.s_ids, self.s2_ids, self.action, self.reward, self.done, self.leaf_sum,
+                   self.leaf_min, *self.node_sum, *self.node_min]
+        return sum(t.numel() * t.element_size() for t in tensors)
+
+    def trans_ptrs(self) -> dict:
+        return {"s_ids": self.s_ids.data_ptr(), "s2_ids": self.s2_ids.data_ptr(), "action": self.action.data_ptr(),
+                "reward": self.reward.data_ptr(), "done": self.done.data_ptr()}
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    # ------------------------------------------------------------------ priorities
+    def write_priorities(self, idx: torch.Tensor, prio: torch.Tensor | None, dedup: bool = True) -> None:
+        """Set leaves for ``idx`` (int32) to prio**alpha (None = current max priority),
+        then recompute all dirty ancestors level by level."""
+        B = idx.numel()
+        s = self._stream()
+        self.hip.per_write_leaves(self.tree, idx.data_ptr(), 0 if prio is None else prio.data_ptr(), B, self.alpha,
+                                  self.max_prio.data_ptr(), int(dedup), s)
+        self.hip.per_update_levels(self.tree, idx.data_ptr(), B, s)
+
+    update_priorities = write_priorities
+
+    def sample_indices(self, B: int, out_idx: torch.Tensor, out_w: torch.Tensor, counter: torch.Tensor,
+                       beta: float | torch.Tensor = 0.4, exclude_last: bool | None = None) -> None:
+        excl = (not self.exact_mass) if exclude_last is None else exclude_last
+        beta_ptr = beta.data_ptr() if isinstance(beta, torch.Tensor) else 0
+        beta_c = 0.0 if isinstance(beta, torch.Tensor) else float(beta)
+        self.hip.per_sample(self.tree, B, self.filled.data_ptr(), 0, beta_ptr, beta_c, self.seed, counter.data_ptr(),
+                            out_idx.data_ptr(), out_w.data_ptr(), int(excl), self._stream())
+
+    def gather(self, idx: torch.Tensor, out_s, out_s2, out_a, out_r, out_d) -> None:
+        self.hip.gather_transitions(self.frames.data_ptr(), self.frame_bytes, self.s_ids.data_ptr(),
+                                    self.s2_ids.data_ptr(), self.action.data_ptr(), self.reward.data_ptr(),
+                                    self.done.data_ptr(), idx.data_ptr(), idx.numel(), out_s.data_ptr(),
+                                    out_s2.data_ptr(), out_a.data_ptr(), out_r.data_ptr(), out_d.data_ptr(),
+                                    self._stream())
+
+    def gather_frames(self, ids: torch.Tensor, out: torch.Tensor) -> None:
+        N, stack = ids.shape
+        self.hip.gather_frames(self.frames.data_ptr(), self.frame_bytes, ids.data_ptr(), N, stack, out.data_ptr(),
+                               self._stream())
+
+    # ------------------------------------------------------------------ convenience (allocating)
+    def sample(self, batch_size: int, beta: float, counter: torch.Tensor | None = None):
+        """Allocating convenience API: (s u8, a i64, r, s2 u8, d, w, idx) on device."""
+        dev = self.device
+        counter = counter if counter is not None else torch.zeros(1, dtype=torch.int64, device=dev)
+        idx = torch.empty(batch_size, dtype=torch.int32, device=dev)
+        w = torch.empty(batch_size, dtype=torch.float32, device=dev)
+        self.sample_indices(batch_size, idx, w, counter, beta)
+        s = torch.empty(batch_size, 4, 84, 84, dtype=torch.uint8, device=dev)
+        s2 = torch.empty_like(s)
+        a = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        r = torch.empty(batch_size, dtype=torch.float32, device=dev)
+        d = torch.empty(batch_size, dtype=torch.float32, device=dev)
+        self.gather(idx, s, s2, a, r, d)
+        return s, a, r, s2, d, w, idx
+
+    def total_priority(self) -> float:
+        return float(self.node_sum[-1][0].item())
+
+    def min_priority(self) -> float:
+        return float(self.node_min[-1][0].item())
+
+    def __len__(self) -> int:
+        return int(min(self.filled.item(), self.capacity))

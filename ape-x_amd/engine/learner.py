@@ -1,0 +1,178 @@
+"""Fused, host-sync-free DQN learner step.
+
+One learner step (reference: learner.py:152-175 + utils.py:64-97 + the replay
+server's sample/update round trips over TCP) is, entirely on one HIP stream:
+
+  per_sample (stratified PER, IS weights)  ->  gather s/s' u8 stacks from the frame ring
+  -> Q(s) with grad, Q(s'), Q_target(s')   (bf16 conv trunk, fp32 heads)
+  -> dqn_loss (double-DQN n-step Huber + IS weights + priorities + dL/dQ, one kernel)
+  -> backward into ONE flat fp32 grad buffer  (-> optional RCCL all-reduce, DP)
+  -> grad_sumsq + clip + centered RMSprop over the flat buffer (two kernels)
+  -> priority write-back into the tree (leaf write + level recompute)
+
+No ``.cpu()``/``.item()`` anywhere: priorities, indices, weights, loss and the grad
+norms stay on device, so the step is capturable as a hipGraph and replayed.
+The model keeps the reference state_dict (parameters are views of the flat buffer).
+"""
+from __future__ import annotations
+
+import copy
+from dataclasses import dataclass
+
+import torch
+
+from .. import ops
+from ..models.dqn import DuelingDQN
+from .hbm_replay import HBMReplay
+
+
+@dataclass
+class LearnerConfig:
+    batch_size: int = 512
+    n_step: int = 3
+    gamma: float = 0.99
+    lr: float = 6.25e-5
+    rms_alpha: float = 0.95
+    rms_eps: float = 1.5e-7
+    centered: bool = True
+    max_norm: float = 40.0
+    lr_gamma: float = 1.0          # StepLR gamma (ApeX.py: 0.99 every 1000 steps)
+    lr_step_size: int = 0
+    lr_step_offset: int = 0
+    beta: float = 0.4
+    optimizer: str = "rmsprop"     # or "adam"
+    forward: str = "torch"         # "torch" (MIOpen bf16 trunk) | "hip" (MFMA kernels)
+    seed: int = 0
+
+
+def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = True) -> torch.Tensor:
+    """Q = V + A - mean(A) with the conv trunk in bf16 (u8 frames are exact in bf16, the
+    reference feeds raw 0..255 values) and fp32 heads/output."""
+    if bf16:
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            h = model.features(x_u8.to(torch.bfloat16))
+        h = h.float().flatten(1)
+    else:
+        h = model.features(x_u8.float()).flatten(1)
+    adv = model.advantage(h)
+    val = model.value(h)
+    return val + adv - adv.mean(1, keepdim=True)
+
+
+class DQNLearner:
+    BLOCKS_PER_SEG = 16
+
+    def __init__(self, model: DuelingDQN, replay: HBMReplay, cfg: LearnerConfig, allreduce=None):
+        self.hip = ops.hip()
+        self.cfg = cfg
+        self.replay = replay
+        self.device = replay.device
+        self.model = model.to(self.device)
+        self.flat = self.model.flatten_parameters()
+        self.target = copy.deepcopy(self.model)
+        self.target._flat = None
+        self.tflat = self.target.flatten_parameters()
+        for p in self.target.parameters():
+            p.requires_grad_(False)
+        self.P = self.flat.numel()
+        dev = self.device
+        self.flat_grad = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.model.parameters():
+            n = p.numel()
+            p.grad = self.flat_grad[off:off + n].view_as(p)
+            off += n
+        segs = self.model.param_segments()
+        self.segments = self.hip.make_segments([o for _, o, _ in segs], [n for _, _, n in segs])
+        self.n_segs = len(segs)
+        self.partials = torch.zeros(self.n_segs * self.BLOCKS_PER_SEG, dtype=torch.float64, device=dev)
+        self.opt_s1 = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        self.opt_s2 = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        if cfg.optimizer == "rmsprop":
+            self.hp = self.hip.RMSpropParams(cfg.lr, cfg.rms_alpha, cfg.rms_eps, cfg.max_norm, cfg.lr_gamma,
+                                             cfg.lr_step_size, cfg.lr_step_offset, cfg.centered)
+        elif cfg.optimizer == "adam":
+            self.hp = self.hip.AdamParams(cfg.lr, max_norm=cfg.max_norm, lr_gamma=cfg.lr_gamma,
+                                          lr_step_size=cfg.lr_step_size, lr_step_offset=cfg.lr_step_offset)
+        else:
+            raise ValueError(cfg.optimizer)
+        B, A = cfg.batch_size, self.model.num_actions
+        self.B, self.A = B, A
+        self.idx = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.w = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.s = torch.zeros(B, 4, 84, 84, dtype=torch.uint8, device=dev)
+        self.s2 = torch.zeros_like(self.s)
+        self.a = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.r = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.d = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.dq = torch.zeros(B, A, dtype=torch.float32, device=dev)
+        self.prio = torch.zeros(B, dtype=torch.float32, device=dev)
+        self.norms = torch.zeros(4, dtype=torch.float32, device=dev)   # l2, reference norm, clip coef, lr
+        self.step_counter = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.beta = torch.full((1,), cfg.beta, dtype=torch.float32, device=dev)
+        self.gamma_n = float(cfg.gamma ** cfg.n_step)
+        self.allreduce = allreduce  # callable(flat_grad) for data-parallel learners
+        self.host_steps = 0
+
+    @staticmethod
+    def _stream() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    # ------------------------------------------------------------------ phases
+    def sample_and_forward(self) -> None:
+        """Sample, gather, forward x3, loss, backward (grads in ``flat_grad``)."""
+        s = self._stream()
+        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta)
+        self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
+        q = forward_q(self.model, self.s)
+        with torch.no_grad():
+            q2 = forward_q(self.model, self.s2)
+            q2t = forward_q(self.target, self.s2)
+        q2 = q2.contiguous()
+        q2t = q2t.contiguous()
+        qd = q.detach().contiguous()
+        self.hip.dqn_loss(qd.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, self.a.data_ptr(), self.r.data_ptr(),
+                          self.d.data_ptr(), self.w.data_ptr(), self.B, self.A, self.gamma_n, self.loss.data_ptr(),
+                          self.dq.data_ptr(), self.prio.data_ptr(), s)
+        self.flat_grad.zero_()
+        q.backward(self.dq)
+
+    def optimize(self) -> None:
+        s = self._stream()
+        h = self.hip
+        h.grad_sumsq(self.flat_grad.data_ptr(), self.segments, self.partials.data_ptr(), self.BLOCKS_PER_SEG, s)
+        if self.cfg.optimizer == "rmsprop":
+            h.rmsprop_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
+                           self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(),
+                           self.segments, self.BLOCKS_PER_SEG, self.hp, self.step_counter.data_ptr(),
+                           self.norms.data_ptr(), s)
+        else:
+            h.adam_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
+                        self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(),
+                        self.segments, self.BLOCKS_PER_SEG, self.hp, self.step_counter.data_ptr(),
+                        self.norms.data_ptr(), s)
+        self.replay.write_priorities(self.idx, self.prio, dedup=True)
+        h.bump_counter(self.step_counter.data_ptr(), 1, 1, s)
+
+    def step(self) -> None:
+        self.sample_and_forward()
+        if self.allreduce is not None:
+            self.allreduce(self.flat_grad)
+        self.optimize()
+        self.host_steps += 1
+
+    # ------------------------------------------------------------------ target / params
+    def sync_target(self) -> None:
+        self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
+
+    def copy_params_to(self, dst_flat: torch.Tensor) -> None:
+        self.hip.copy_f32(dst_flat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
+
+    def state_dict(self):
+        return self.model.state_dict()
+
+    def stats(self) -> dict:
+        """Host-side view of the last step's scalars (forces a sync; call rarely)."""
+        n = self.norms.tolist()
+        return {"loss": float(self.loss.item()), "grad_norm_l2": n[0], "grad_norm": n[1], "clip": n[2], "lr": n[3]}

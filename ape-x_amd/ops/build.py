@@ -1,0 +1,163 @@
+"""In-tree native build driver (no torch.utils.cpp_extension, no hipify).
+
+Builds two pybind11 extension modules next to this file:
+
+* ``_apex_cpu``  -- host C++17 (g++): segment trees / PER batch ops used by the
+  reference-compatible replay buffers (reference memory.py:10-320).
+* ``_apex_hip``  -- HIP C++ for gfx950 only (``hipcc --offload-arch=gfx950``): the
+  HBM replay, n-step batcher, synthetic vector env, fused loss / optimizer and the
+  MFMA conv/FC kernels of the Nature-CNN dueling network.
+
+Neither module links libtorch: kernels take raw device pointers and the HIP stream
+handle of the caller, so they are captured by ``torch.cuda.CUDAGraph`` like any
+other work on that stream.  ``libamdhip64.so.7`` resolves to the copy torch has
+already loaded (same SONAME), so ``import torch`` must precede the import of
+``_apex_hip`` (``apex_amd.ops`` does that).
+
+Usage: ``python -m apex_amd.ops.build [--force] [--jobs N] [--only cpu|hip]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+BUILD = HERE / "_build"
+ARCH = "gfx950"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+
+CPU_SOURCES = ["cpu_replay.cpp"]
+HIP_SOURCES = [
+    "hip_bindings.cpp",
+    "replay_kernels.hip",
+    "actor_kernels.hip",
+    "learner_kernels.hip",
+    "conv_kernels.hip",
+]
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _py_includes() -> list[str]:
+    import pybind11
+
+    return [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}", f"-I{CSRC}"]
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.cuh")) + sorted(CSRC.glob("*.hpp"))
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def _run(cmd: list[str]) -> None:
+    proc = subprocess.run(cmd, capture_output=True, text=True)
+    if proc.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + proc.stdout + proc.stderr)
+        raise RuntimeError(f"native build failed: {cmd[-1] if cmd else ''}")
+    if proc.stderr.strip() and os.environ.get("APEX_BUILD_VERBOSE"):
+        sys.stderr.write(proc.stderr)
+
+
+def cpu_target() -> Path:
+    return HERE / f"_apex_cpu{_ext_suffix()}"
+
+
+def hip_target() -> Path:
+    return HERE / f"_apex_hip{_ext_suffix()}"
+
+
+def build_cpu(force: bool = False) -> Path:
+    target = cpu_target()
+    srcs = [CSRC / s for s in CPU_SOURCES]
+    if not force and not _stale(target, srcs + _headers()):
+        return target
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", "-fvisibility=hidden",
+           *_py_includes(), *map(str, srcs), "-o", str(target)]
+    _run(cmd)
+    return target
+
+
+def _hipcc() -> str:
+    cand = ROCM / "bin" / "hipcc"
+    return str(cand) if cand.exists() else (shutil.which("hipcc") or "hipcc")
+
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-fvisibility=hidden",
+    "-ffp-contract=fast",
+    "-munsafe-fp-atomics",
+    "-mcode-object-version=5",
+    "-Wno-unused-result",
+]
+
+
+def build_hip(force: bool = False, jobs: int | None = None) -> Path:
+    target = hip_target()
+    BUILD.mkdir(exist_ok=True)
+    srcs = [CSRC / s for s in HIP_SOURCES]
+    hdrs = _headers()
+    objs = []
+    todo = []
+    for s in srcs:
+        o = BUILD / (s.name + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            if s.suffix == ".hip":
+                cmd = [_hipcc(), *HIP_FLAGS, "-x", "hip", *_py_includes(), "-c", str(s), "-o", str(o)]
+            else:
+                # host-only translation unit (pybind11 glue); still compiled by hipcc so
+                # hip_runtime types resolve, but with no device code of its own.
+                cmd = [_hipcc(), *HIP_FLAGS, *_py_includes(), "-c", str(s), "-o", str(o)]
+            todo.append(cmd)
+    if todo:
+        jobs = jobs or min(len(todo), max(1, (os.cpu_count() or 4) // 2))
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_run, todo))
+    if force or todo or _stale(target, objs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
+               f"-L{ROCM / 'lib'}", "-lamdhip64", "-o", str(target)]
+        _run(cmd)
+    return target
+
+
+def build_all(force: bool = False, only: str | None = None, jobs: int | None = None) -> list[Path]:
+    out = []
+    if only in (None, "cpu"):
+        out.append(build_cpu(force))
+    if only in (None, "hip"):
+        out.append(build_hip(force, jobs))
+    return out
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--only", choices=["cpu", "hip"], default=None)
+    ap.add_argument("--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    for p in build_all(a.force, a.only, a.jobs):
+        print(p)
+
+
+if __name__ == "__main__":
+    main()

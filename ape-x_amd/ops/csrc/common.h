@@ -1,0 +1,118 @@
+// Shared device helpers for the gfx950 kernels (wave64 reductions, Philox RNG,
+// bf16 packing, launch checking).  CDNA4 only: wave width is hard-coded to 64.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#define APEX_WAVE 64
+
+#define HIP_CHECK(expr)                                                                      \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                   \
+  } while (0)
+
+#define LAUNCH_CHECK() HIP_CHECK(hipGetLastError())
+
+namespace apex {
+
+// ---------------------------------------------------------------- wave reductions
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w = __shfl_xor(v, o, 64);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// inclusive prefix sum across the 64 lanes (Hillis-Steele, fixed order => deterministic)
+template <typename T>
+__device__ __forceinline__ T wave_inclusive_scan(T v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T w = __shfl_up(v, o, 64);
+    if (lane >= o) v += w;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+
+__device__ __forceinline__ u32x4 philox4x32(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(0xD2511F53u, c.x, &hi0);
+    uint32_t lo1 = mulhilo(0xCD9E8D57u, c.z, &hi1);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 4 uniforms in [0,1) for (seed, stream, counter).
+__device__ __forceinline__ void uniform4(uint64_t seed, uint64_t stream, uint64_t counter, float out[4]) {
+  u32x4 c{(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
+  u32x4 r = philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float s = 5.9604644775390625e-08f;  // 2^-24
+  out[0] = (r.x >> 8) * s;
+  out[1] = (r.y >> 8) * s;
+  out[2] = (r.z >> 8) * s;
+  out[3] = (r.w >> 8) * s;
+}
+
+__device__ __forceinline__ double uniform_double(uint64_t seed, uint64_t stream, uint64_t counter) {
+  u32x4 c{(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
+  u32x4 r = philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  uint64_t bits = ((uint64_t)r.x << 21) ^ (uint64_t)r.y;  // 53 random bits
+  return (double)(bits & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0);
+}
+
+// ---------------------------------------------------------------- bf16
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ void atomic_max_pos_float(float* addr, float v) {
+  // valid for non-negative floats: IEEE order == signed-int order
+  atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));
+}
+
+}  // namespace apex

@@ -1,0 +1,210 @@
+// pybind11 bindings for the gfx950 kernel library `_apex_hip`.
+//
+// Pointers cross the boundary as integers (torch `tensor.data_ptr()`) and the stream
+// as `torch.cuda.current_stream().cuda_stream`; descriptor structs are built once in
+// Python and held by small handle classes so each per-step call is a plain function
+// call with scalars (sub-microsecond binding overhead, graph-capturable launches).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <vector>
+
+#include "kernels.h"
+
+namespace py = pybind11;
+using namespace apex;
+
+namespace {
+
+template <typename T>
+T* P(uint64_t v) {
+  return reinterpret_cast<T*>(static_cast<uintptr_t>(v));
+}
+hipStream_t S(uint64_t v) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(v)); }
+
+struct TreeHandle {
+  TreeDesc d{};
+};
+
+TreeHandle make_tree(uint64_t leaf_sum, uint64_t leaf_min, const std::vector<uint64_t>& node_sum,
+                     const std::vector<uint64_t>& node_min, const std::vector<int>& sizes) {
+  TreeHandle h;
+  if (node_sum.size() != node_min.size() || sizes.size() != node_sum.size() + 1)
+    throw std::invalid_argument("tree: inconsistent level lists");
+  if ((int)node_sum.size() > kMaxTreeLevels || node_sum.empty()) throw std::invalid_argument("tree: bad level count");
+  h.d.leaf_sum = P<float>(leaf_sum);
+  h.d.leaf_min = P<float>(leaf_min);
+  h.d.levels = (int)node_sum.size();
+  for (size_t i = 0; i < node_sum.size(); ++i) {
+    h.d.node_sum[i] = P<double>(node_sum[i]);
+    h.d.node_min[i] = P<float>(node_min[i]);
+  }
+  for (size_t i = 0; i < sizes.size(); ++i) h.d.size[i] = sizes[i];
+  for (size_t i = 1; i < sizes.size(); ++i)
+    if (sizes[i] != (sizes[i - 1] + kTreeFanout - 1) / kTreeFanout) throw std::invalid_argument("tree: bad sizes");
+  if (sizes.back() != 1) throw std::invalid_argument("tree: top level must have one node");
+  return h;
+}
+
+struct SegHandle {
+  OptSegments s{};
+};
+SegHandle make_segments(const std::vector<int64_t>& offsets, const std::vector<int64_t>& numels) {
+  SegHandle h;
+  if (offsets.size() != numels.size() || offsets.size() > 64 || offsets.empty())
+    throw std::invalid_argument("segments: 1..64 tensors");
+  h.s.n = (int)offsets.size();
+  for (size_t i = 0; i < offsets.size(); ++i) {
+    h.s.offset[i] = offsets[i];
+    h.s.numel[i] = numels[i];
+  }
+  return h;
+}
+
+struct NStepHandle {
+  NStepParams p{};
+  NStepState st{};
+  TransTable tt{};
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_apex_hip, m) {
+  m.doc() = "apex_amd gfx950 kernels (HBM replay, actor shard, fused learner)";
+  m.attr("arch") = "gfx950";
+
+  py::class_<TreeHandle>(m, "TreeHandle").def_property_readonly("levels", [](const TreeHandle& h) {
+    return h.d.levels;
+  });
+  m.def("make_tree", &make_tree);
+  py::class_<SegHandle>(m, "SegHandle").def_property_readonly("n", [](const SegHandle& h) { return h.s.n; });
+  m.def("make_segments", &make_segments);
+
+  // ---- replay
+  m.def("per_write_leaves", [](const TreeHandle& t, uint64_t idx, uint64_t prio, int B, float alpha,
+                               uint64_t max_prio, int dedup, uint64_t s) {
+    per_write_leaves(t.d, P<const int>(idx), P<const float>(prio), B, alpha, P<float>(max_prio), dedup, S(s));
+  });
+  m.def("per_update_levels", [](const TreeHandle& t, uint64_t idx, int B, uint64_t s) {
+    per_update_levels(t.d, P<const int>(idx), B, S(s));
+  });
+  m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
+                         float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
+                         int exclude_last, uint64_t s) {
+    per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
+               P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, S(s));
+  });
+  m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
+                                 uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
+                                 uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {
+    gather_transitions(P<const uint8_t>(frames), frame_bytes, P<const int>(s_ids), P<const int>(s2_ids),
+                       P<const int>(act), P<const float>(rew), P<const float>(done), P<const int>(idx), B,
+                       P<uint8_t>(out_s), P<uint8_t>(out_s2), P<int64_t>(out_a), P<float>(out_r), P<float>(out_d),
+                       S(s));
+  });
+  m.def("gather_frames", [](uint64_t frames, int frame_bytes, uint64_t ids, int N, int stack, uint64_t out,
+                            uint64_t s) {
+    gather_frames(P<const uint8_t>(frames), frame_bytes, P<const int>(ids), N, stack, P<uint8_t>(out), S(s));
+  });
+  m.def("bump_counter", [](uint64_t c, int n, int64_t by, uint64_t s) { bump_counter(P<int64_t>(c), n, by, S(s)); });
+
+  // ---- actor shard
+  py::class_<VecEnvParams>(m, "VecEnvParams")
+      .def(py::init([](int E, int A, int frame_bytes, int F, int repeat, int clip, int life, int max_steps) {
+             VecEnvParams p{E, A, frame_bytes, F, repeat, clip, life, max_steps};
+             return p;
+           }),
+           py::arg("E"), py::arg("n_actions"), py::arg("frame_bytes"), py::arg("F"), py::arg("action_repeat") = 4,
+           py::arg("clip_rewards") = 1, py::arg("episode_life") = 1, py::arg("max_episode_steps") = 50000)
+      .def_readonly("E", &VecEnvParams::E)
+      .def_readonly("F", &VecEnvParams::F);
+  m.def("vec_env_reset", [](uint64_t state, uint64_t seed, uint64_t frames, const VecEnvParams& p, uint64_t step,
+                            uint64_t new_frame, uint64_t hist, uint64_t ep_log, uint64_t s) {
+    vec_env_reset(P<float>(state), seed, P<uint8_t>(frames), p, P<const int64_t>(step), P<int>(new_frame),
+                  P<int>(hist), P<float>(ep_log), S(s));
+  });
+  m.def("vec_env_step", [](uint64_t state, uint64_t actions, uint64_t seed, uint64_t step, uint64_t frames,
+                           const VecEnvParams& p, uint64_t reward, uint64_t done, uint64_t new_frame, uint64_t ep_log,
+                           uint64_t s) {
+    vec_env_step(P<float>(state), P<const int>(actions), seed, P<const int64_t>(step), P<uint8_t>(frames), p,
+                 P<float>(reward), P<float>(done), P<int>(new_frame), P<float>(ep_log), S(s));
+  });
+  m.def("select_actions", [](uint64_t q, int E, int A, uint64_t eps, uint64_t seed, uint64_t counter,
+                             uint64_t actions, uint64_t s) {
+    select_actions(P<const float>(q), E, A, P<const float>(eps), seed, P<const int64_t>(counter), P<int>(actions),
+                   S(s));
+  });
+
+  py::class_<NStepHandle>(m, "NStepHandle");
+  m.def("make_nstep", [](int E, int A, int n, int C, float gamma, int mode, py::dict st, py::dict tt) {
+    NStepHandle h;
+    h.p = NStepParams{E, A, n, C, gamma, mode};
+    auto g = [&](py::dict d, const char* k) { return d[k].cast<uint64_t>(); };
+    h.st.win_ids = P<int>(g(st, "win_ids"));
+    h.st.win_a = P<int>(g(st, "win_a"));
+    h.st.win_r = P<float>(g(st, "win_r"));
+    h.st.win_q = P<float>(g(st, "win_q"));
+    h.st.win_meta = P<int>(g(st, "win_meta"));
+    h.st.hist = P<int>(g(st, "hist"));
+    h.st.drain_ids = P<int>(g(st, "drain_ids"));
+    h.st.drain_a = P<int>(g(st, "drain_a"));
+    h.st.drain_r = P<float>(g(st, "drain_r"));
+    h.st.drain_q = P<float>(g(st, "drain_q"));
+    h.st.drain_meta = P<int>(g(st, "drain_meta"));
+    h.st.drain_s2 = P<int>(g(st, "drain_s2"));
+    h.tt.s_ids = P<int>(g(tt, "s_ids"));
+    h.tt.s2_ids = P<int>(g(tt, "s2_ids"));
+    h.tt.action = P<int>(g(tt, "action"));
+    h.tt.reward = P<float>(g(tt, "reward"));
+    h.tt.done = P<float>(g(tt, "done"));
+    return h;
+  });
+  m.def("nstep_emit", [](const NStepHandle& h, uint64_t q, uint64_t actions, uint64_t reward, uint64_t done,
+                         uint64_t new_frame, uint64_t step, uint64_t slot_out, uint64_t prio_out, uint64_t s) {
+    nstep_emit(h.p, h.st, h.tt, P<const float>(q), P<const int>(actions), P<const float>(reward),
+               P<const float>(done), P<const int>(new_frame), P<const int64_t>(step), P<int>(slot_out),
+               P<float>(prio_out), S(s));
+  });
+
+  // ---- learner
+  m.def("dqn_loss", [](uint64_t q, uint64_t q2, uint64_t q2t, int ldq, uint64_t a, uint64_t r, uint64_t d,
+                       uint64_t w, int B, int A, float gamma_n, uint64_t loss, uint64_t dq, uint64_t prio,
+                       uint64_t s) {
+    dqn_loss(P<const float>(q), P<const float>(q2), P<const float>(q2t), ldq, P<const int64_t>(a), P<const float>(r),
+             P<const float>(d), P<const float>(w), B, A, gamma_n, P<float>(loss), P<float>(dq), P<float>(prio), S(s));
+  });
+  m.def("grad_sumsq", [](uint64_t g, const SegHandle& seg, uint64_t partials, int bps, uint64_t s) {
+    grad_sumsq(P<const float>(g), seg.s, P<double>(partials), bps, S(s));
+  });
+  py::class_<RMSpropParams>(m, "RMSpropParams")
+      .def(py::init([](float lr, float alpha, float eps, float max_norm, float lr_gamma, int lr_step_size,
+                       int lr_step_offset, bool centered) {
+             return RMSpropParams{lr, alpha, eps, max_norm, lr_gamma, lr_step_size, lr_step_offset, centered ? 1 : 0};
+           }),
+           py::arg("lr"), py::arg("alpha") = 0.99f, py::arg("eps") = 1e-8f, py::arg("max_norm") = 0.f,
+           py::arg("lr_gamma") = 1.f, py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0,
+           py::arg("centered") = false);
+  m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
+                           int n_partials, const SegHandle& seg, int bps, const RMSpropParams& hp, uint64_t step,
+                           uint64_t norms, uint64_t s) {
+    rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
+                 n_partials, seg.s, bps, hp, P<const int64_t>(step), P<float>(norms), S(s));
+  });
+  py::class_<AdamParams>(m, "AdamParams")
+      .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
+                       int lr_step_size, int lr_step_offset) {
+             return AdamParams{lr, b1, b2, eps, wd, max_norm, lr_gamma, lr_step_size, lr_step_offset};
+           }),
+           py::arg("lr"), py::arg("beta1") = 0.9f, py::arg("beta2") = 0.999f, py::arg("eps") = 1e-8f,
+           py::arg("weight_decay") = 0.f, py::arg("max_norm") = 0.f, py::arg("lr_gamma") = 1.f,
+           py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0);
+  m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
+                        int n_partials, const SegHandle& seg, int bps, const AdamParams& hp, uint64_t step,
+                        uint64_t norms, uint64_t s) {
+    adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
+              seg.s, bps, hp, P<const int64_t>(step), P<float>(norms), S(s));
+  });
+  m.def("copy_f32", [](uint64_t dst, uint64_t src, int64_t n, uint64_t s) {
+    copy_f32(P<float>(dst), P<const float>(src), n, S(s));
+  });
+}

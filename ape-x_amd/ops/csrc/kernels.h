@@ -1,0 +1,122 @@
+// Host-visible launcher declarations for the gfx950 kernels.  Every launcher takes
+// raw device pointers and the caller's hipStream_t (torch's current stream), never
+// allocates and never synchronises, so a sequence of them can be captured into a
+// hipGraph (cdna_hip_programming.md Guideline 9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace apex {
+
+constexpr int kTreeFanout = 64;       // one child per lane of a wave64
+constexpr int kTreeLog2Fanout = 6;
+constexpr int kMaxTreeLevels = 8;     // 64^8 leaves >> any HBM capacity
+
+// Wide prioritized-replay tree: level 0 = leaves (fp32 sum / fp32 min), levels
+// 1..levels = internal nodes (fp64 sum / fp32 min), level `levels` has one node.
+struct TreeDesc {
+  float* leaf_sum;
+  float* leaf_min;
+  double* node_sum[kMaxTreeLevels];
+  float* node_min[kMaxTreeLevels];
+  int size[kMaxTreeLevels + 1];
+  int levels;
+};
+
+// ---- replay_kernels.hip
+void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
+                      int dedup, hipStream_t s);
+void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
+// length/beta are read from device memory when the pointers are non-null (so a captured
+// graph sees the live replay fill level and annealed beta), else the constants are used.
+void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
+                float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
+                int exclude_last, hipStream_t s);
+void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
+                        const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
+                        uint8_t* out_s2, int64_t* out_a, float* out_r, float* out_d, hipStream_t s);
+void gather_frames(const uint8_t* frames, int frame_bytes, const int* ids, int N, int stack, uint8_t* out,
+                   hipStream_t s);
+void bump_counter(int64_t* counter, int n, int64_t by, hipStream_t s);
+
+// ---- actor_kernels.hip
+struct VecEnvParams {
+  int E;              // envs in this shard
+  int n_actions;
+  int frame_bytes;    // 84*84
+  int F;              // frame-ring capacity (frames)
+  int action_repeat;  // 4 (MaxAndSkip)
+  int clip_rewards;
+  int episode_life;
+  int max_episode_steps;
+};
+void vec_env_reset(float* state, uint64_t seed, uint8_t* frames, const VecEnvParams& p,
+                   const int64_t* step_counter, int* new_frame, int* hist, float* ep_log, hipStream_t s);
+void vec_env_step(float* state, const int* actions, uint64_t seed, const int64_t* step_counter, uint8_t* frames,
+                  const VecEnvParams& p, float* reward, float* done, int* new_frame, float* ep_log, hipStream_t s);
+void select_actions(const float* q, int E, int A, const float* eps, uint64_t seed, const int64_t* counter,
+                    int* actions, hipStream_t s);
+
+struct NStepParams {
+  int E, A, n, C;   // envs, actions, n-step, transition capacity
+  float gamma;
+  int mode;         // 0 = reference, 1 = textbook
+};
+struct NStepState {
+  int* win_ids;     // [E][n][4]
+  int* win_a;       // [E][n]
+  float* win_r;     // [E][n]
+  float* win_q;     // [E][n][A]
+  int* win_meta;    // [E][4]: start, len, q_start, q_len
+  int* hist;        // [E][4]  current observation stack (frame ids)
+  int* drain_ids;   // [E][n][4]   textbook-mode tail
+  int* drain_a;     // [E][n]
+  float* drain_r;   // [E][n]
+  float* drain_q;   // [E][n]      Q(s, a) only
+  int* drain_meta;  // [E][2]: start, len
+  int* drain_s2;    // [E][4]
+};
+struct TransTable {
+  int* s_ids;       // [C][4]
+  int* s2_ids;      // [C][4]
+  int* action;      // [C]
+  float* reward;    // [C]
+  float* done;      // [C]
+};
+void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float* q, const int* actions,
+                const float* reward, const float* done, const int* new_frame, const int64_t* step_counter,
+                int* slot_out, float* prio_out, hipStream_t s);
+
+// ---- learner_kernels.hip
+void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int64_t* a, const float* r,
+              const float* d, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
+              hipStream_t s);
+struct OptSegments {
+  int n;                 // number of parameter tensors (<= 64)
+  int64_t offset[64];
+  int64_t numel[64];
+};
+void grad_sumsq(const float* g, const OptSegments& seg, double* partials, int blocks_per_seg, hipStream_t s);
+struct RMSpropParams {
+  float lr0, alpha, eps, max_norm;
+  float lr_gamma;        // StepLR gamma (1 = constant)
+  int lr_step_size;      // StepLR step size
+  int lr_step_offset;    // 1 reproduces scheduler.step() before optimizer.step()
+  int centered;
+};
+void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
+                  int n_partials, const OptSegments& seg, int blocks_per_seg, const RMSpropParams& hp,
+                  const int64_t* step, float* norms_out, hipStream_t s);
+struct AdamParams {
+  float lr0, beta1, beta2, eps, weight_decay, max_norm;
+  float lr_gamma;
+  int lr_step_size, lr_step_offset;
+};
+void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
+               const OptSegments& seg, int blocks_per_seg, const AdamParams& hp, const int64_t* step,
+               float* norms_out, hipStream_t s);
+void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
+
+}  // namespace apex

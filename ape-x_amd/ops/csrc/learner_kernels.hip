@@ -1,0 +1,221 @@
+// Learner-side fused kernels for gfx950.
+//
+// * dqn_loss: double-DQN n-step target + Huber(1) * IS weight + batch-max priority
+//   mixing + dL/dQ in ONE workgroup (reference utils.py:64-81 runs ~15 torch ops and a
+//   device->host copy of the priorities every step).
+// * grad_sumsq + rmsprop_step / adam_step: global-L2 clip (torch clip_grad_norm_
+//   semantics) fused into a single pass of the optimizer over the flat fp32 parameter
+//   buffer.  The norm is reduced deterministically: per-(tensor, block) fp64 partials,
+//   re-reduced in fixed order by every update block, so no atomics and no host sync.
+//   The same partials give the reference's logged 'grad_norm' formula.
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+__device__ __forceinline__ float block_sum_f(float v, float* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += smem[i];  // fixed order
+  return t;
+}
+
+__device__ __forceinline__ float block_max_f(float v, float* smem) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  float t = -INFINITY;
+  for (int i = 0; i < nw; ++i) t = fmaxf(t, smem[i]);
+  return t;
+}
+
+// ------------------------------------------------------------------ loss
+__global__ void dqn_loss_k(const float* __restrict__ q, const float* __restrict__ q2, const float* __restrict__ q2t,
+                           int ldq, const int64_t* __restrict__ act, const float* __restrict__ rew,
+                           const float* __restrict__ done, const float* __restrict__ w, int B, int A, float gamma_n,
+                           float* __restrict__ loss_out, float* __restrict__ dq, float* __restrict__ prio) {
+  __shared__ float red[16];
+  const int b = threadIdx.x;
+  float delta = 0.f, lw = 0.f, g = 0.f;
+  int a = 0;
+  if (b < B) {
+    const float* qr = q + (size_t)b * ldq;
+    const float* q2r = q2 + (size_t)b * ldq;
+    const float* q2tr = q2t + (size_t)b * ldq;
+    a = (int)act[b];
+    int astar = 0;
+    float best = q2r[0];
+    for (int k = 1; k < A; ++k)
+      if (q2r[k] > best) { best = q2r[k]; astar = k; }
+    const float y = rew[b] + gamma_n * q2tr[astar] * (1.f - done[b]);
+    const float qa = qr[a];
+    delta = fabsf(y - qa);
+    const float h = delta < 1.f ? 0.5f * delta * delta : delta - 0.5f;
+    lw = w[b] * h;
+    g = w[b] / (float)B * fminf(fmaxf(qa - y, -1.f), 1.f);
+  }
+  const float total = block_sum_f(lw, red);
+  const float dmax = block_max_f(b < B ? delta : -INFINITY, red);
+  if (b < B) {
+    prio[b] = 0.9f * dmax + 0.1f * delta + 1e-6f;
+    float* dr = dq + (size_t)b * ldq;
+    for (int k = 0; k < A; ++k) dr[k] = (k == a) ? g : 0.f;
+  }
+  if (b == 0) loss_out[0] = total / (float)B;
+}
+
+void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int64_t* a, const float* r,
+              const float* d, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
+              hipStream_t s) {
+  if (B < 1 || B > 1024) throw std::invalid_argument("dqn_loss: batch must be in [1, 1024]");
+  const int threads = ((B + 63) / 64) * 64;
+  dqn_loss_k<<<1, threads, 0, s>>>(q, q2, q2t, ldq, a, r, d, w, B, A, gamma_n, loss_out, dq, prio);
+  LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ grad norm partials
+__global__ void grad_sumsq_k(const float* __restrict__ g, OptSegments seg, double* __restrict__ partials) {
+  __shared__ double red[16];
+  const int sidx = blockIdx.y;
+  const int64_t off = seg.offset[sidx], n = seg.numel[sidx];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = g[off + i];
+    acc += (double)v * (double)v;
+  }
+  acc = wave_sum(acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) red[wid] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    partials[sidx * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+void grad_sumsq(const float* g, const OptSegments& seg, double* partials, int blocks_per_seg, hipStream_t s) {
+  grad_sumsq_k<<<dim3(blocks_per_seg, seg.n), 256, 0, s>>>(g, seg, partials);
+  LAUNCH_CHECK();
+}
+
+// Every update block re-reduces the partials in the same fixed order.
+struct NormInfo {
+  float clip, l2, ref;
+};
+__device__ NormInfo reduce_norms(const double* partials, int n_partials, const OptSegments& seg, int bps,
+                                 float max_norm) {
+  __shared__ double segsum[64];
+  for (int sidx = threadIdx.x; sidx < seg.n; sidx += blockDim.x) {
+    double t = 0.0;
+    for (int k = 0; k < bps; ++k) t += partials[sidx * bps + k];
+    segsum[sidx] = t;
+  }
+  __syncthreads();
+  double total = 0.0, ref = 0.0;
+  for (int sidx = 0; sidx < seg.n; ++sidx) {
+    total += segsum[sidx];
+    ref += sqrt(sqrt(segsum[sidx]));  // ||g_p||^(1/2)
+  }
+  NormInfo ni;
+  ni.l2 = (float)sqrt(total);
+  ni.ref = (float)sqrt(ref);
+  const float coef = max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f;
+  ni.clip = fminf(coef, 1.f);
+  return ni;
+}
+
+__device__ __forceinline__ float step_lr(float lr0, float gamma, int step_size, int offset, int64_t step) {
+  if (gamma == 1.f || step_size <= 0) return lr0;
+  const int64_t k = (step + offset) / step_size;
+  return lr0 * powf(gamma, (float)k);
+}
+
+__global__ void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sq,
+                               float* __restrict__ gavg, int64_t n, const double* __restrict__ partials,
+                               int n_partials, OptSegments seg, int bps, RMSpropParams hp,
+                               const int64_t* __restrict__ step, float* __restrict__ norms_out) {
+  const NormInfo ni = reduce_norms(partials, n_partials, seg, bps, hp.max_norm);
+  const int64_t st = step ? step[0] : 0;
+  const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
+    norms_out[0] = ni.l2;
+    norms_out[1] = ni.ref;
+    norms_out[2] = ni.clip;
+    norms_out[3] = lr;
+  }
+  const float a = hp.alpha, oma = 1.f - hp.alpha;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * ni.clip;
+    const float s2 = sq[i] * a + oma * gi * gi;
+    sq[i] = s2;
+    float avg;
+    if (hp.centered) {
+      float ga = gavg[i];
+      ga = ga + oma * (gi - ga);
+      gavg[i] = ga;
+      avg = sqrtf(fmaxf(s2 - ga * ga, 0.f)) + hp.eps;
+    } else {
+      avg = sqrtf(s2) + hp.eps;
+    }
+    p[i] -= lr * gi / avg;
+  }
+}
+
+void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
+                  int n_partials, const OptSegments& seg, int blocks_per_seg, const RMSpropParams& hp,
+                  const int64_t* step, float* norms_out, hipStream_t s) {
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, seg, blocks_per_seg, hp, step,
+                                         norms_out);
+  LAUNCH_CHECK();
+}
+
+__global__ void adam_step_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t n, const double* __restrict__ partials, int n_partials,
+                            OptSegments seg, int bps, AdamParams hp, const int64_t* __restrict__ step,
+                            float* __restrict__ norms_out) {
+  const NormInfo ni = reduce_norms(partials, n_partials, seg, bps, hp.max_norm);
+  const int64_t st = step ? step[0] : 0;
+  const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
+  const float t = (float)(st + 1);
+  const float bc1 = 1.f - powf(hp.beta1, t), bc2 = 1.f - powf(hp.beta2, t);
+  const float step_size = lr / bc1, rbc2 = 1.f / sqrtf(bc2);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
+    norms_out[0] = ni.l2;
+    norms_out[1] = ni.ref;
+    norms_out[2] = ni.clip;
+    norms_out[3] = lr;
+  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * ni.clip;
+    if (hp.weight_decay != 0.f) gi += hp.weight_decay * p[i];
+    float mi = m[i];
+    mi = mi + (1.f - hp.beta1) * (gi - mi);
+    const float vi = v[i] * hp.beta2 + (1.f - hp.beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] -= step_size * mi / (sqrtf(vi) * rbc2 + hp.eps);
+  }
+}
+
+void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
+               const OptSegments& seg, int blocks_per_seg, const AdamParams& hp, const int64_t* step,
+               float* norms_out, hipStream_t s) {
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, seg, blocks_per_seg, hp, step,
+                                      norms_out);
+  LAUNCH_CHECK();
+}
+
+void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s) {
+  HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s));
+}
+
+}  // namespace apex

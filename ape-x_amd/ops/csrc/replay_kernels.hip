@@ -1,0 +1,223 @@
+// HBM-resident prioritized replay for gfx950.
+//
+// Instead of the reference's binary segment tree walked in Python under a lock
+// (memory.py:10-143, origin_repo/replay.py:92-143), the tree here has fanout 64 =
+// one child per lane of a wave64:
+//   * a prefix descent is ceil(log64 C) dependent 64-wide loads + a wave prefix scan
+//     (2M leaves -> 4 levels instead of 21),
+//   * a batched priority update recomputes each dirty node with ONE wave reading its
+//     64 children (coalesced 256-512 B) and a fixed-order reduction, so results are
+//     deterministic and independent of arrival order.  Duplicate indices resolve
+//     last-write-wins like the reference's sequential loop; parents are recomputed
+//     level-synchronously (one launch per level), never incrementally, so there is
+//     no fp drift and no race on shared ancestors.
+// Leaves are fp32, internal sums fp64, mins fp32 (+inf neutral).
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+// ------------------------------------------------------------------ leaf writes
+__global__ void per_write_leaves_k(TreeDesc t, const int* __restrict__ idx, const float* __restrict__ prio, int B,
+                                   float alpha, float* max_prio, int dedup) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const int id = idx[i];
+  if (id < 0 || id >= t.size[0]) return;
+  if (dedup) {  // last write wins (memory.py:313-320 applies updates sequentially)
+    for (int j = i + 1; j < B; ++j)
+      if (idx[j] == id) return;
+  }
+  float p = prio ? prio[i] : *max_prio;
+  if (p > 0.f && isfinite(p)) {
+    const float v = powf(p, alpha);
+    t.leaf_sum[id] = v;
+    t.leaf_min[id] = v;
+    if (prio) atomic_max_pos_float(max_prio, p);
+  } else {  // empty / invalid slot: no sampling mass, neutral for the min
+    t.leaf_sum[id] = 0.f;
+    t.leaf_min[id] = INFINITY;
+  }
+}
+
+// ------------------------------------------------------------------ level recompute
+// One wave per update; a wave whose parent was already claimed by an earlier update
+// exits, so each dirty node is recomputed exactly once per level.
+__global__ void per_update_level_k(TreeDesc t, const int* __restrict__ idx, int B, int level) {
+  const int lane = threadIdx.x & 63;
+  const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w >= B) return;
+  const int id = idx[w];
+  if (id < 0 || id >= t.size[0]) return;
+  const int shift = kTreeLog2Fanout * level;
+  const int node = id >> shift;
+  for (int j0 = 0; j0 < w; j0 += 64) {
+    const int j = j0 + lane;
+    int other = (j < w) ? idx[j] : -1;
+    const bool dup = (j < w) && other >= 0 && other < t.size[0] && (other >> shift) == node;
+    if (__ballot(dup)) return;  // wave-uniform
+  }
+  const int child = node * kTreeFanout + lane;
+  const int csize = t.size[level - 1];
+  double s = 0.0;
+  float m = INFINITY;
+  if (child < csize) {
+    if (level == 1) {
+      s = (double)t.leaf_sum[child];
+      m = t.leaf_min[child];
+    } else {
+      s = t.node_sum[level - 2][child];
+      m = t.node_min[level - 2][child];
+    }
+  }
+  s = wave_sum(s);
+  m = wave_min(m);
+  if (lane == 0) {
+    t.node_sum[level - 1][node] = s;
+    t.node_min[level - 1][node] = m;
+  }
+}
+
+// ------------------------------------------------------------------ stratified sampling
+// One wave per sample: mass_i = (u_i + i) * total / B, descend levels with a wave-wide
+// inclusive scan of the 64 child sums; IS weight = (p_i / p_min)^-beta
+// ( == (p_i N / S)^-beta / (p_min N / S)^-beta, memory.py:284-298 ).
+__global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64_t length_const,
+                             const float* beta_ptr, float beta_const, uint64_t seed,
+                             const int64_t* __restrict__ counter, int* __restrict__ out_idx,
+                             float* __restrict__ out_w, int exclude_last) {
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (i >= B) return;
+  int64_t len64 = length_ptr ? length_ptr[0] : length_const;
+  const int length = (int)(len64 < (int64_t)t.size[0] ? len64 : (int64_t)t.size[0]);
+  const float beta = beta_ptr ? beta_ptr[0] : beta_const;
+  const int L = t.levels;
+  double total = t.node_sum[L - 1][0];
+  if (exclude_last && length > 0 && length <= t.size[0]) total -= (double)t.leaf_sum[length - 1];
+  const uint64_t ctr = counter ? (uint64_t)counter[0] : 0ull;
+  const double u = uniform_double(seed, (uint64_t)i, ctr);
+  double mass = (u + (double)i) * total / (double)B;
+  int node = 0;
+  for (int level = L; level >= 1; --level) {
+    const int child = node * kTreeFanout + lane;
+    const int csize = t.size[level - 1];
+    double v = 0.0;
+    if (child < csize) v = (level == 1) ? (double)t.leaf_sum[child] : t.node_sum[level - 2][child];
+    if (exclude_last && level == 1 && child == length - 1) v = 0.0;
+    const double incl = wave_inclusive_scan(v, lane);
+    unsigned long long hit = __ballot(incl > mass);
+    int k;
+    if (hit) {
+      k = __ffsll((long long)hit) - 1;
+    } else {  // rounding at the top end: take the last child with mass
+      unsigned long long nz = __ballot(v > 0.0);
+      k = nz ? 63 - __clzll((long long)nz) : 0;
+    }
+    const double before = __shfl(incl - v, k, 64);
+    mass -= before;
+    if (mass < 0.0) mass = 0.0;
+    node = node * kTreeFanout + k;
+  }
+  if (lane == 0) {
+    const float p = t.leaf_sum[node];
+    const float pmin = t.node_min[L - 1][0];
+    out_idx[i] = node;
+    out_w[i] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
+  }
+}
+
+// ------------------------------------------------------------------ gathers
+// Frames are stored once in a u8 ring; a transition holds 4+4 frame ids, so a
+// sampled (s, s') pair is assembled by id (7,056 B per frame, not 2x28 KB
+// per transition).  One workgroup copies one 84x84 frame with 16-B loads/stores.
+__global__ void gather_transitions_k(const uint8_t* __restrict__ frames, int frame_bytes,
+                                     const int* __restrict__ s_ids, const int* __restrict__ s2_ids,
+                                     const int* __restrict__ act, const float* __restrict__ rew,
+                                     const float* __restrict__ done, const int* __restrict__ idx,
+                                     uint8_t* __restrict__ out_s, uint8_t* __restrict__ out_s2,
+                                     int64_t* __restrict__ out_a, float* __restrict__ out_r,
+                                     float* __restrict__ out_d) {
+  const int b = blockIdx.x;
+  const int which = blockIdx.y;  // 0..3: s frames, 4..7: s' frames
+  const int slot = idx[b];
+  const int f = (which < 4 ? s_ids : s2_ids)[slot * 4 + (which & 3)];
+  const uint4* src = reinterpret_cast<const uint4*>(frames + (size_t)f * frame_bytes);
+  uint8_t* dst_base = (which < 4 ? out_s : out_s2) + ((size_t)b * 4 + (which & 3)) * frame_bytes;
+  uint4* dst = reinterpret_cast<uint4*>(dst_base);
+  const int n16 = frame_bytes >> 4;
+  for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+  if (which == 0 && threadIdx.x == 0) {
+    out_a[b] = act[slot];
+    out_r[b] = rew[slot];
+    out_d[b] = done[slot];
+  }
+}
+
+__global__ void gather_frames_k(const uint8_t* __restrict__ frames, int frame_bytes, const int* __restrict__ ids,
+                                int stack, uint8_t* __restrict__ out) {
+  const int n = blockIdx.x, c = blockIdx.y;
+  const int f = ids[n * stack + c];
+  const uint4* src = reinterpret_cast<const uint4*>(frames + (size_t)f * frame_bytes);
+  uint4* dst = reinterpret_cast<uint4*>(out + ((size_t)n * stack + c) * frame_bytes);
+  const int n16 = frame_bytes >> 4;
+  for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+}
+
+__global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
+  const int i = threadIdx.x;
+  if (i < n) c[i] += by;
+}
+
+// ------------------------------------------------------------------ launchers
+void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
+                      int dedup, hipStream_t s) {
+  if (B <= 0) return;
+  per_write_leaves_k<<<(B + 255) / 256, 256, 0, s>>>(t, idx, prio, B, alpha, max_prio, dedup);
+  LAUNCH_CHECK();
+}
+
+void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) {
+  if (B <= 0) return;
+  const int waves_per_block = 4;
+  const int grid = (B + waves_per_block - 1) / waves_per_block;
+  for (int level = 1; level <= t.levels; ++level) {
+    per_update_level_k<<<grid, 64 * waves_per_block, 0, s>>>(t, idx, B, level);
+    LAUNCH_CHECK();
+  }
+}
+
+void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
+                float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
+                int exclude_last, hipStream_t s) {
+  if (B <= 0) return;
+  const int waves_per_block = 4;
+  per_sample_k<<<(B + waves_per_block - 1) / waves_per_block, 64 * waves_per_block, 0, s>>>(
+      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last);
+  LAUNCH_CHECK();
+}
+
+void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
+                        const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
+                        uint8_t* out_s2, int64_t* out_a, float* out_r, float* out_d, hipStream_t s) {
+  if (B <= 0) return;
+  if (frame_bytes % 16) throw std::invalid_argument("frame_bytes must be a multiple of 16");
+  gather_transitions_k<<<dim3(B, 8), 256, 0, s>>>(frames, frame_bytes, s_ids, s2_ids, act, rew, done, idx, out_s,
+                                                  out_s2, out_a, out_r, out_d);
+  LAUNCH_CHECK();
+}
+
+void gather_frames(const uint8_t* frames, int frame_bytes, const int* ids, int N, int stack, uint8_t* out,
+                   hipStream_t s) {
+  if (N <= 0) return;
+  if (frame_bytes % 16) throw std::invalid_argument("frame_bytes must be a multiple of 16");
+  gather_frames_k<<<dim3(N, stack), 256, 0, s>>>(frames, frame_bytes, ids, stack, out);
+  LAUNCH_CHECK();
+}
+
+void bump_counter(int64_t* counter, int n, int64_t by, hipStream_t s) {
+  bump_counter_k<<<1, 64, 0, s>>>(counter, n, by);
+  LAUNCH_CHECK();
+}
+
+}  // namespace apex

@@ -1,0 +1,160 @@
+#!/usr/bin/env python
+"""Headline benchmark: Ape-X DQN learner SGD steps/s + actor frames/s on MI355X.
+
+Metric and config come from BASELINE.json: learner SGD steps/sec (+ actor frames/sec)
+for Ape-X dueling double DQN on Atari-shaped 84x84x4 synthetic frames, batch 512,
+n-step 3, PER alpha 0.6 / beta 0.4, centered RMSprop (lr 6.25e-5), grad clip 40,
+target sync 2500, 18 actions (Seaquest, the reference's published run), random-init
+weights.  The reference publishes 10-12 batches/s (its implementation, V100 learner)
+and quotes 19 batches/s for the Ape-X paper (origin_repo/README.md:42).
+
+Every rank (one per GPU) runs an actor shard (``--envs`` GPU envs with the global
+Ape-X epsilon ladder), its HBM replay shard (``--capacity`` transitions) and a
+learner replica; learner replicas are data-parallel (flat-gradient RCCL all-reduce),
+so per-GPU work is fixed as N grows (weak scaling) and the global batch is 512*N.
+One timed step = one learner SGD step (sample 512 -> 3 forwards -> backward ->
+clip -> RMSprop -> priority update) + ``--actor-steps`` actor steps of all envs.
+
+``value`` = sum over ranks of learner SGD steps/s (= batches of 512 per second, the
+unit of the reference's number); actor frames/s (4 emulator frames per env step) is
+reported alongside.  Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1
+under torch.distributed.run, one process per GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REFERENCE_BATCHES_PER_S = 12.0   # upper end of the reference's 10-12 batches/s
+PAPER_BATCHES_PER_S = 19.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=256, help="GPU envs (actors) per GPU")
+    ap.add_argument("--actor-steps", type=int, default=1, help="actor steps per learner step")
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--capacity", type=int, default=2_000_000)
+    ap.add_argument("--threshold", type=int, default=50_000)
+    ap.add_argument("--actions", type=int, default=18)
+    ap.add_argument("--forward", default="torch", choices=["torch", "hip"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=1122)
+    ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    from apex_amd.engine.apex import ApexEngine, EngineConfig
+    from apex_amd.engine.learner import LearnerConfig
+    from apex_amd.parallel.dp import FlatGradAllReduce
+
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank)
+    cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
+                       threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
+                       actor_offset=rank * args.envs, total_actors=world * args.envs,
+                       use_graphs=not args.no_graphs, seed=args.seed + 7919 * rank, learner=lc)
+    allreduce = FlatGradAllReduce(world) if world > 1 else None
+    eng = ApexEngine(cfg, device, allreduce=allreduce)
+    if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
+        from apex_amd.parallel.broadcast import broadcast_flat
+
+        broadcast_flat(eng.learner.flat, src=0)
+        eng.learner.sync_target()
+        eng.learner.copy_params_to(eng.actor_flat)
+
+    t_fill = time.perf_counter()
+    eng.fill(args.threshold)
+    torch.cuda.synchronize(device)
+    t_fill = time.perf_counter() - t_fill
+    if not args.no_graphs:
+        eng.capture()
+    for _ in range(args.warmup):
+        eng.train_step()
+    torch.cuda.synchronize(device)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    for _ in range(args.profile_steps):
+        eng.train_step()
+    torch.cuda.synchronize(device)
+
+    stats = eng.learner.stats()
+    steps_per_s = world * args.steps / dt
+    frames_per_s = world * args.steps * args.actor_steps * eng.frames_per_actor_step / dt
+    if rank == 0:
+        out = {
+            "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
+            "value": round(steps_per_s, 3),
+            "unit": "learner SGD steps/s (batch 512 each, summed over GPUs)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
+            "config": {
+                "model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
+                "global_batch": args.batch * world,
+                "seq_len": 3,
+                "seq_len_meaning": "n-step return horizon (frame stack 4)",
+                "parallelism": f"dp{world}",
+                "replay_capacity_per_gpu": args.capacity,
+                "envs_per_gpu": args.envs,
+                "actor_steps_per_learner_step": args.actor_steps,
+                "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
+                "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
+                "forward": args.forward,
+                "hip_graphs": not args.no_graphs,
+            },
+            "actor_frames_per_sec": round(frames_per_s, 1),
+            "learner_samples_per_sec": round(steps_per_s * args.batch, 1),
+            "vs_paper_19_batches_per_s": round(steps_per_s / PAPER_BATCHES_PER_S, 2),
+            "replay_fill_seconds": round(t_fill, 3),
+            "last_loss": round(stats["loss"], 6),
+            "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+"""HBM replay kernels vs host references (fp64 numpy oracles)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _tree_oracle(leaf_sum, sizes):
+    levels = [np.asarray(leaf_sum, dtype=np.float64)]
+    for n in sizes[1:]:
+        prev = levels[-1]
+        pad = np.zeros(n * 64)
+        pad[:len(prev)] = prev
+        levels.append(pad.reshape(n, 64).sum(1))
+    return levels
+
+
+def test_tree_write_update_dedup(cuda):
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 5000
+    rp = HBMReplay(C, n_envs=16, device=cuda, alpha=0.6)
+    rng = np.random.RandomState(0)
+    host = np.zeros(C)
+    hmin = np.full(C, np.inf)
+    for _ in range(5):
+        idx = rng.randint(0, C, size=700).astype(np.int32)
+        pr = rng.uniform(0.01, 3.0, size=700).astype(np.float32)
+        for i, p in zip(idx, pr):  # sequential => last write wins
+            host[i] = float(np.float32(p) ** np.float32(0.6))
+            hmin[i] = host[i]
+        rp.write_priorities(torch.from_numpy(idx).to(cuda), torch.from_numpy(pr).to(cuda), dedup=True)
+    torch.cuda.synchronize()
+    leaf = rp.leaf_sum.cpu().numpy()
+    np.testing.assert_allclose(leaf, host, rtol=2e-6, atol=1e-7)
+    levels = _tree_oracle(leaf, rp.level_sizes)
+    for k, t in enumerate(rp.node_sum):
+        np.testing.assert_allclose(t.cpu().numpy(), levels[k + 1], rtol=1e-12, atol=1e-9)
+    assert rp.min_priority() == pytest.approx(np.min(leaf[leaf > 0]), rel=1e-6)
+    assert rp.total_priority() == pytest.approx(leaf.astype(np.float64).sum(), rel=1e-12)
+
+
+def test_sample_stratified_and_weights(cuda):
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 3000
+    rp = HBMReplay(C, n_envs=8, device=cuda, alpha=1.0)
+    rng = np.random.RandomState(1)
+    pr = rng.uniform(0.1, 5.0, size=C).astype(np.float32)
+    pr[::7] = 0.0  # empty slots: no mass
+    idx = torch.arange(C, dtype=torch.int32, device=cuda)
+    rp.write_priorities(idx, torch.from_numpy(pr).to(cuda), dedup=False)
+    rp.filled.fill_(C)
+    B = 256
+    out_i = torch.empty(B, dtype=torch.int32, device=cuda)
+    out_w = torch.empty(B, dtype=torch.float32, device=cuda)
+    counts = np.zeros(C)
+    leaf = rp.leaf_sum.cpu().numpy().astype(np.float64)
+    cum = np.cumsum(leaf)
+    total = cum[-1]
+    pmin = leaf[leaf > 0].min()
+    for c in range(200):
+        ctr = torch.tensor([c], dtype=torch.int64, device=cuda)
+        rp.sample_indices(B, out_i, out_w, ctr, beta=0.4)
+        ii = out_i.cpu().numpy()
+        ww = out_w.cpu().numpy()
+        assert (leaf[ii] > 0).all(), "sampled an empty slot"
+        # stratification: sample i falls in stratum i of the cumulative mass
+        lo = np.where(ii > 0, cum[ii - 1], 0.0)
+        hi = cum[ii]
+        seg = total / B
+        k = np.arange(B)
+        assert np.all(hi >= k * seg - 1e-6 * total) and np.all(lo <= (k + 1) * seg + 1e-6 * total)
+        np.testing.assert_allclose(ww, (leaf[ii] / pmin) ** -0.4, rtol=1e-5)
+        np.add.at(counts, ii, 1)
+    expected = leaf / total * B * 200
+    big = expected > 20
+    rel = np.abs(counts[big] - expected[big]).sum() / expected[big].sum()
+    assert rel < 0.08, rel
+
+
+def test_gather_transitions(cuda):
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    rp = HBMReplay(512, n_envs=4, device=cuda)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    rp.frames.copy_(torch.randint(0, 256, rp.frames.shape, generator=g, dtype=torch.uint8).to(cuda))
+    F = rp.frame_capacity
+    rp.s_ids.copy_(torch.randint(0, F, (512, 4), generator=g, dtype=torch.int32).to(cuda))
+    rp.s2_ids.copy_(torch.randint(0, F, (512, 4), generator=g, dtype=torch.int32).to(cuda))
+    rp.action.copy_(torch.randint(0, 18, (512,), generator=g, dtype=torch.int32).to(cuda))
+    rp.reward.copy_(torch.randn(512, generator=g).to(cuda))
+    rp.done.copy_((torch.rand(512, generator=g) < 0.1).float().to(cuda))
+    idx = torch.randint(0, 512, (64,), generator=g, dtype=torch.int32).to(cuda)
+    s = torch.empty(64, 4, 84, 84, dtype=torch.uint8, device=cuda)
+    s2 = torch.empty_like(s)
+    a = torch.empty(64, dtype=torch.int64, device=cuda)
+    r = torch.empty(64, device=cuda)
+    d = torch.empty(64, device=cuda)
+    rp.gather(idx, s, s2, a, r, d)
+    il = idx.long()
+    ref_s = rp.frames[rp.s_ids[il].long()].view(64, 4, 84, 84)
+    ref_s2 = rp.frames[rp.s2_ids[il].long()].view(64, 4, 84, 84)
+    assert torch.equal(s, ref_s) and torch.equal(s2, ref_s2)
+    assert torch.equal(a, rp.action[il].long())
+    assert torch.equal(r, rp.reward[il]) and torch.equal(d, rp.done[il])
+
+
+def test_large_tree_levels(cuda):
+    """2^21-leaf (reference replay size 2M) tree: 4 levels, sums exact vs fp64."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 2_000_000
+    rp = HBMReplay(C, n_envs=256, device=cuda, alpha=0.6)
+    assert len(rp.level_sizes) == 5
+    idx = torch.arange(0, C, 3, dtype=torch.int32, device=cuda)
+    pr = torch.rand(idx.numel(), device=cuda) + 0.05
+    rp.write_priorities(idx, pr, dedup=False)
+    leaf = rp.leaf_sum.double()
+    assert math.isclose(rp.total_priority(), float(leaf.sum()), rel_tol=1e-10)
