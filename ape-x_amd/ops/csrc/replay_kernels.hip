@@ -18,15 +18,25 @@
 namespace apex {
 
 // ------------------------------------------------------------------ leaf writes
+// The batch's indices are staged in LDS so the last-write-wins scan (memory.py:313-320
+// applies updates sequentially) reads LDS, not L2 (B <= kStageMax; larger batches must
+// be unique, e.g. actor slots, and run with dedup = 0).
+constexpr int kStageMax = 4096;
+
 __global__ void per_write_leaves_k(TreeDesc t, const int* __restrict__ idx, const float* __restrict__ prio, int B,
                                    float alpha, float* max_prio, int dedup) {
+  __shared__ int sidx[kStageMax];
+  if (dedup) {
+    for (int j = threadIdx.x; j < B; j += blockDim.x) sidx[j] = idx[j];
+    __syncthreads();
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const int id = idx[i];
   if (id < 0 || id >= t.size[0]) return;
-  if (dedup) {  // last write wins (memory.py:313-320 applies updates sequentially)
+  if (dedup) {
     for (int j = i + 1; j < B; ++j)
-      if (idx[j] == id) return;
+      if (sidx[j] == id) return;
   }
   float p = prio ? prio[i] : *max_prio;
   if (p > 0.f && isfinite(p)) {
@@ -42,10 +52,18 @@ __global__ void per_write_leaves_k(TreeDesc t, const int* __restrict__ idx, cons
 
 // ------------------------------------------------------------------ level recompute
 // One wave per update; a wave whose parent was already claimed by an earlier update
-// exits, so each dirty node is recomputed exactly once per level.
+// exits, so each dirty node is recomputed exactly once per level.  The earlier
+// updates' indices are scanned from an LDS copy (64 per ballot).
 __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ idx, int B, int level) {
+  __shared__ int sidx[kStageMax];
   const int lane = threadIdx.x & 63;
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int wmax = min(B, (int)((blockIdx.x + 1) * blockDim.x) >> 6);
+  const bool staged = B <= kStageMax;
+  if (staged) {
+    for (int j = threadIdx.x; j < wmax; j += blockDim.x) sidx[j] = idx[j];
+    __syncthreads();
+  }
   if (w >= B) return;
   const int id = idx[w];
   if (id < 0 || id >= t.size[0]) return;
@@ -53,8 +71,8 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ idx, int 
   const int node = id >> shift;
   for (int j0 = 0; j0 < w; j0 += 64) {
     const int j = j0 + lane;
-    int other = (j < w) ? idx[j] : -1;
-    const bool dup = (j < w) && other >= 0 && other < t.size[0] && (other >> shift) == node;
+    const int other = (j < w) ? (staged ? sidx[j] : idx[j]) : -1;
+    const bool dup = other >= 0 && other < t.size[0] && (other >> shift) == node;
     if (__ballot(dup)) return;  // wave-uniform
   }
   const int child = node * kTreeFanout + lane;
@@ -173,6 +191,7 @@ __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
                       int dedup, hipStream_t s) {
   if (B <= 0) return;
+  if (dedup && B > kStageMax) throw std::invalid_argument("per_write_leaves: dedup batch too large");
   per_write_leaves_k<<<(B + 255) / 256, 256, 0, s>>>(t, idx, prio, B, alpha, max_prio, dedup);
   LAUNCH_CHECK();
 }

@@ -76,10 +76,13 @@ def test_sample_stratified_and_weights(cuda):
         assert np.all(hi >= k * seg - 1e-6 * total) and np.all(lo <= (k + 1) * seg + 1e-6 * total)
         np.testing.assert_allclose(ww, (leaf[ii] / pmin) ** -0.4, rtol=1e-5)
         np.add.at(counts, ii, 1)
+    # stratified sampling makes bin counts nearly deterministic: compare 64-leaf bins
     expected = leaf / total * B * 200
-    big = expected > 20
-    rel = np.abs(counts[big] - expected[big]).sum() / expected[big].sum()
-    assert rel < 0.08, rel
+    nb = C // 64
+    cb = counts[:nb * 64].reshape(nb, 64).sum(1)
+    eb = expected[:nb * 64].reshape(nb, 64).sum(1)
+    rel = np.abs(cb - eb).sum() / eb.sum()
+    assert rel < 0.03, rel
 
 
 def test_gather_transitions(cuda):
