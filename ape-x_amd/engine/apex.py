@@ -25,6 +25,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ..models.dqn import DuelingDQN
+from ..models.fused import HipDuelingNet, NetWorkspace
 from .actor_shard import ActorShard
 from .hbm_replay import HBMReplay
 from .learner import DQNLearner, LearnerConfig, forward_q
@@ -70,7 +71,11 @@ class ApexEngine:
         for p in self.actor_model.parameters():
             p.requires_grad_(False)
             p.grad = None
-        self.learner.copy_params_to(self.actor_flat)
+        self.hip_net = lc.forward == "hip"
+        if self.hip_net:
+            self.actor_net = HipDuelingNet(self.actor_model)
+            self.actor_ws = NetWorkspace(cfg.n_envs, cfg.n_actions, self.device)
+        self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
         self._g_actor = self._g_learn_a = self._g_learn_b = None
@@ -78,10 +83,19 @@ class ApexEngine:
         self._allreduce = allreduce
 
     # ------------------------------------------------------------------ eager bodies
+    def publish_params(self) -> None:
+        """Learner -> local actor weights (the on-GPU analogue of learner.py:169-170)."""
+        self.learner.copy_params_to(self.actor_flat)
+        if self.hip_net:
+            self.actor_net.repack()
+
     def _actor_body(self):
         obs = self.actor.observe()
-        with torch.no_grad():
-            q = forward_q(self.actor_model, obs)
+        if self.hip_net:
+            q = self.actor_net(obs, self.actor_ws)
+        else:
+            with torch.no_grad():
+                q = forward_q(self.actor_model, obs)
         self.actor.act_and_step(q)
 
     def _learn_a(self):
@@ -137,7 +151,7 @@ class ApexEngine:
             self._learn_b()
         self.learn_steps += 1
         if self.learn_steps % self.cfg.publish_param_interval == 0:
-            self.learner.copy_params_to(self.actor_flat)
+            self.publish_params()
         if self.learn_steps % self.cfg.target_update_interval == 0:
             self.learner.sync_target()
 

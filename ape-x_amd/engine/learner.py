@@ -23,6 +23,7 @@ import torch
 
 from .. import ops
 from ..models.dqn import DuelingDQN
+from ..models.fused import HipDuelingNet, NetWorkspace
 from .hbm_replay import HBMReplay
 
 
@@ -114,6 +115,13 @@ class DQNLearner:
         self.gamma_n = float(cfg.gamma ** cfg.n_step)
         self.allreduce = allreduce  # callable(flat_grad) for data-parallel learners
         self.host_steps = 0
+        self.hip_net = cfg.forward == "hip"
+        if self.hip_net:
+            self.net = HipDuelingNet(self.model)
+            self.tnet = HipDuelingNet(self.target)
+            self.ws_s = NetWorkspace(B, A, dev, keep_for_backward=True)
+            self.ws_s2 = NetWorkspace(B, A, dev)
+            self.ws_t = NetWorkspace(B, A, dev)
 
     @staticmethod
     def _stream() -> int:
@@ -125,6 +133,15 @@ class DQNLearner:
         s = self._stream()
         self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta)
         self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
+        if self.hip_net:
+            q = self.net(self.s, self.ws_s)
+            q2 = self.net(self.s2, self.ws_s2)
+            q2t = self.tnet(self.s2, self.ws_t)
+            self.hip.dqn_loss(q.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, self.a.data_ptr(),
+                              self.r.data_ptr(), self.d.data_ptr(), self.w.data_ptr(), self.B, self.A, self.gamma_n,
+                              self.loss.data_ptr(), self.dq.data_ptr(), self.prio.data_ptr(), s)
+            self.net.backward(self.dq, self.s, self.ws_s)
+            return
         q = forward_q(self.model, self.s)
         with torch.no_grad():
             q2 = forward_q(self.model, self.s2)
@@ -152,6 +169,8 @@ class DQNLearner:
                         self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(),
                         self.segments, self.BLOCKS_PER_SEG, self.hp, self.step_counter.data_ptr(),
                         self.norms.data_ptr(), s)
+        if self.hip_net:
+            self.net.repack()
         self.replay.write_priorities(self.idx, self.prio, dedup=True)
         h.bump_counter(self.step_counter.data_ptr(), 1, 1, s)
 
@@ -165,6 +184,8 @@ class DQNLearner:
     # ------------------------------------------------------------------ target / params
     def sync_target(self) -> None:
         self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
+        if self.hip_net:
+            self.tnet.repack()
 
     def copy_params_to(self, dst_flat: torch.Tensor) -> None:
         self.hip.copy_f32(dst_flat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())

@@ -1,0 +1,147 @@
+"""HIP fast path of the dueling Q-network (forward on hand-written MFMA kernels).
+
+``HipDuelingNet`` wraps a :class:`DuelingDQN` (fp32 master parameters, reference
+state_dict, flat buffer) and keeps a packed bf16 copy of its weights in the layouts the
+gfx950 kernels want (conv weights [N][KH][KW][C], FC1 repacked to the channels-last
+flatten order).  ``repack()`` refreshes the packed copy after every optimizer step /
+target sync / actor publish (4 tiny kernels).
+
+Forward (per pass, no autograd):
+  conv_fwd x3  (u8 frames -> bf16 NHWC activations; MFMA 32x32x16, bias+ReLU fused)
+  FC1          (hipBLASLt GEMM, bf16 x bf16 -> fp32; a plain library GEMM)
+  heads_fwd    (bias + ReLU + adv/value heads + dueling combine, one wave per row)
+Backward (explicit, writes every parameter gradient into the flat fp32 grad buffer
+exactly once, so no zeroing pass is needed):
+  heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (hipBLASLt) ->
+  ReLU masks + conv backward (MIOpen NHWC bf16 igemm, channels-last views of our
+  buffers) for conv3 -> conv2 -> conv1 (weight grad only).
+
+Numerics: bf16 operands, fp32 accumulation, fp32 heads and Q.  Checked against the
+fp32 PyTorch module in tests/test_gpu_fused_net.py.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .dqn import DuelingDQN
+
+P3, C3 = 49, 64
+FEAT = P3 * C3  # 3136
+
+
+class NetWorkspace:
+    """Activation buffers for one forward pass of batch ``B``."""
+
+    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False):
+        self.B, self.A = B, A
+        bf = dict(dtype=torch.bfloat16, device=device)
+        f32 = dict(dtype=torch.float32, device=device)
+        self.a1 = torch.empty(B, 400, 32, **bf)
+        self.a2 = torch.empty(B, 81, 64, **bf)
+        self.a3 = torch.empty(B, FEAT, **bf)
+        self.z = torch.empty(B, 256, **f32)
+        self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
+        self.q = torch.empty(B, A, **f32)
+        if keep_for_backward:
+            self.dA = torch.empty(B, A + 1, **f32)
+            self.dz = torch.empty(B, 256, **f32)
+            self.dz_bf = torch.empty(B, 256, **bf)
+            self.da3 = torch.empty(B, FEAT, **bf)
+            self.x_nhwc = torch.empty(B, 84, 84, 4, **bf)
+            self.dy3 = torch.empty(B, P3, C3, **bf)
+            self.dy2 = torch.empty(B, 81, 64, **bf)
+            self.dy1 = torch.empty(B, 400, 32, **bf)
+
+
+def _cl_view(t: torch.Tensor, B: int, C: int, H: int, W: int) -> torch.Tensor:
+    """[B][H][W][C] memory viewed as a channels-last [B, C, H, W] tensor."""
+    return t.as_strided((B, C, H, W), (H * W * C, 1, W * C, C))
+
+
+class HipDuelingNet:
+    def __init__(self, model: DuelingDQN):
+        assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
+        self.hip = ops.hip()
+        self.model = model
+        self.A = model.num_actions
+        dev = next(model.parameters()).device
+        self.device = dev
+        bf = dict(dtype=torch.bfloat16, device=dev)
+        self.w1p = torch.empty(32, 8, 8, 4, **bf)
+        self.w2p = torch.empty(64, 4, 4, 32, **bf)
+        self.w3p = torch.empty(64, 3, 3, 64, **bf)
+        self.wfc1p = torch.empty(256, FEAT, **bf)
+        f = model.features
+        self.b1, self.b2, self.b3 = f[0].bias, f[2].bias, f[4].bias
+        self.repack()
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def repack(self) -> None:
+        h, s, f, m = self.hip, self._s(), self.model.features, self.model
+        h.pack_conv_w(f[0].weight.data_ptr(), self.w1p.data_ptr(), 32, 4, 8, 8, s)
+        h.pack_conv_w(f[2].weight.data_ptr(), self.w2p.data_ptr(), 64, 32, 4, 4, s)
+        h.pack_conv_w(f[4].weight.data_ptr(), self.w3p.data_ptr(), 64, 64, 3, 3, s)
+        h.pack_fc1(m.advantage[0].weight.data_ptr(), m.value[0].weight.data_ptr(), self.wfc1p.data_ptr(), P3, C3, s)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x_u8: torch.Tensor, ws: NetWorkspace) -> torch.Tensor:
+        B = x_u8.shape[0]
+        assert x_u8.dtype == torch.uint8 and x_u8.is_contiguous() and tuple(x_u8.shape[1:]) == (4, 84, 84)
+        assert B == ws.B
+        h, s, m = self.hip, self._s(), self.model
+        h.conv_fwd(1, x_u8.data_ptr(), self.w1p.data_ptr(), self.b1.data_ptr(), ws.a1.data_ptr(), B, s)
+        h.conv_fwd(2, ws.a1.data_ptr(), self.w2p.data_ptr(), self.b2.data_ptr(), ws.a2.data_ptr(), B, s)
+        h.conv_fwd(3, ws.a2.data_ptr(), self.w3p.data_ptr(), self.b3.data_ptr(), ws.a3.data_ptr(), B, s)
+        torch.mm(ws.a3, self.wfc1p.t(), out_dtype=torch.float32, out=ws.z)
+        h.heads_fwd(ws.z.data_ptr(), m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
+                    m.advantage[2].weight.data_ptr(), m.advantage[2].bias.data_ptr(), m.value[2].weight.data_ptr(),
+                    m.value[2].bias.data_ptr(), ws.h.data_ptr() if ws.h is not None else 0, ws.q.data_ptr(), B,
+                    self.A, s)
+        return ws.q
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dq: torch.Tensor, x_u8: torch.Tensor, ws: NetWorkspace) -> None:
+        """Write dL/dparam for the pass held in ``ws`` into the model's ``.grad`` views."""
+        B, A = ws.B, self.A
+        h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        h.heads_bwd(dq.data_ptr(), ws.h.data_ptr(), m.advantage[2].weight.data_ptr(), m.value[2].weight.data_ptr(),
+                    ws.dA.data_ptr(), ws.dz.data_ptr(), ws.dz_bf.data_ptr(), B, A, s)
+        dadv, dv = ws.dA[:, :A], ws.dA[:, A:]
+        torch.mm(dadv.t(), ws.h[:, :128], out=m.advantage[2].weight.grad)
+        torch.sum(dadv, 0, out=m.advantage[2].bias.grad)
+        torch.mm(dv.t(), ws.h[:, 128:], out=m.value[2].weight.grad)
+        torch.sum(dv, 0, out=m.value[2].bias.grad)
+        torch.sum(ws.dz[:, :128], 0, out=m.advantage[0].bias.grad)
+        torch.sum(ws.dz[:, 128:], 0, out=m.value[0].bias.grad)
+        gfc1 = torch.mm(ws.dz_bf.t(), ws.a3, out_dtype=torch.float32)
+        h.unpack_fc1_grad(gfc1.data_ptr(), m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(),
+                          P3, C3, s)
+        torch.mm(ws.dz_bf, self.wfc1p, out=ws.da3)
+        # conv3
+        h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
+        dx2, dw3, db3 = torch.ops.aten.convolution_backward(
+            _cl_view(ws.dy3, B, 64, 7, 7), _cl_view(ws.a2, B, 64, 9, 9), _cl_view(self.w3p, 64, 64, 3, 3), [64],
+            [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
+        f[4].weight.grad.copy_(dw3)
+        f[4].bias.grad.copy_(db3)
+        dx2 = dx2.contiguous(memory_format=torch.channels_last)
+        h.relu_mask_bf16(dx2.data_ptr(), ws.a2.data_ptr(), ws.dy2.data_ptr(), ws.dy2.numel(), s)
+        dx1, dw2, db2 = torch.ops.aten.convolution_backward(
+            _cl_view(ws.dy2, B, 64, 9, 9), _cl_view(ws.a1, B, 32, 20, 20), _cl_view(self.w2p, 64, 32, 4, 4), [64],
+            [2, 2], [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
+        f[2].weight.grad.copy_(dw2)
+        f[2].bias.grad.copy_(db2)
+        dx1 = dx1.contiguous(memory_format=torch.channels_last)
+        h.relu_mask_bf16(dx1.data_ptr(), ws.a1.data_ptr(), ws.dy1.data_ptr(), ws.dy1.numel(), s)
+        h.u8_to_bf16_nhwc(x_u8.data_ptr(), ws.x_nhwc.data_ptr(), B, 84 * 84, s)
+        _, dw1, db1 = torch.ops.aten.convolution_backward(
+            _cl_view(ws.dy1, B, 32, 20, 20), _cl_view(ws.x_nhwc, B, 4, 84, 84), _cl_view(self.w1p, 32, 4, 8, 8), [32],
+            [4, 4], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
+        f[0].weight.grad.copy_(dw1)
+        f[0].bias.grad.copy_(db1)

@@ -1,6 +1,378 @@
-// MFMA implicit-GEMM kernels for the Nature-CNN dueling network.
-// (filled in by the conv milestone; this translation unit is part of the library build)
+// MFMA kernels for the Nature-CNN dueling Q-network on gfx950.
+//
+// Layouts (chosen for CDNA4, not copied from any NCHW/cuDNN convention):
+//   * activations are channels-last bf16: a1 [B][400][32], a2 [B][81][64], a3 [B][49][64]
+//     (a3 flattened as p*64+c; the FC1 weight is repacked to that order);
+//   * conv weights are packed bf16 [N][KH][KW][C] (== channels_last of [N][C][KH][KW]), so
+//     the implicit-GEMM K index is (ky, kx, c) with c fastest and every MFMA A/B fragment
+//     (8 consecutive k) is ONE 16-byte LDS read.
+//   * the u8 frames of the replay are converted to bf16 (exact for 0..255) while
+//     being staged into LDS -- no separate cast kernel, no NCHW->NHWC transpose kernel.
+//
+// conv_fwd: persistent workgroups (4 waves) stage the packed weights into LDS once, then
+// loop over sample pairs: stage both samples' input into LDS (padded pixel stride to break
+// the 2-4 way ds_read_b128 bank conflicts of stride-S pixel rows), and each wave runs whole
+// 32x32 output tiles as a chain of v_mfma_f32_32x32x16_bf16 over K, with the bias + ReLU +
+// bf16 pack fused into the epilogue.
 #include "common.h"
 #include "kernels.h"
 
-namespace apex {}  // namespace apex
+namespace apex {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_>
+struct ConvGeo {
+  static constexpr int H = H_, W = W_, C = C_, KH = KH_, KW = KW_, S = S_, N = N_;
+  static constexpr int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1, P = OH * OW;
+  static constexpr int K = KH * KW * C, KSTEPS = K / 16;
+  static constexpr int MT = (P + 31) / 32, NT = N / 32;
+  static constexpr int PIX = (C == 4) ? 8 : (C * 2 + 16);  // LDS bytes per input pixel (padded)
+  static constexpr int X_BYTES = H * W * PIX;
+  static constexpr int W_ROW = K * 2 + 16;                 // LDS bytes per weight row (padded)
+  static constexpr int W_BYTES = N * W_ROW;
+  static constexpr int SPW = 2;                             // samples per workgroup iteration
+  static constexpr int LDS = SPW * X_BYTES + W_BYTES;
+  static_assert(K % 16 == 0, "K must be a multiple of 16");
+  static_assert(N % 32 == 0, "N must be a multiple of 32");
+};
+
+using Conv1 = ConvGeo<84, 84, 4, 8, 8, 4, 32>;
+using Conv2 = ConvGeo<20, 20, 32, 4, 4, 2, 64>;
+using Conv3 = ConvGeo<9, 9, 64, 3, 3, 1, 64>;
+static_assert(Conv1::P == 400 && Conv2::P == 81 && Conv3::P == 49, "Nature-CNN geometry");
+static_assert(Conv1::LDS <= 160 * 1024 && Conv2::LDS <= 160 * 1024 && Conv3::LDS <= 160 * 1024, "LDS");
+
+__device__ __forceinline__ uint32_t pack_bf16x2_u8(uint32_t b0, uint32_t b1) {
+  // integers 0..255 are exact in bf16: bf16 = high half of the f32
+  const uint32_t f0 = __float_as_uint((float)b0), f1 = __float_as_uint((float)b1);
+  return (f0 >> 16) | (f1 & 0xFFFF0000u);
+}
+
+// Stage one sample's input into LDS as padded NHWC bf16.
+template <class G, bool U8IN>
+__device__ __forceinline__ void stage_input(const void* __restrict__ in, int b, char* xs) {
+  if constexpr (U8IN) {
+    // u8 NCHW [4][84][84] -> bf16 NHWC; thread = 4 consecutive x of one row
+    static_assert(G::C == 4 && G::W % 4 == 0, "u8 path is the 4-frame stack");
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(in) + (size_t)b * G::C * G::H * G::W;
+    constexpr int GROUPS = G::H * G::W / 4;
+    for (int g = threadIdx.x; g < GROUPS; g += blockDim.x) {
+      const int off = g * 4;
+      uint32_t v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const uint32_t*>(src + c * G::H * G::W + off);
+      uint4 lo, hi;  // pixels x..x+1 and x+2..x+3, 4 channels each
+      lo.x = pack_bf16x2_u8(v[0] & 0xFF, v[1] & 0xFF);
+      lo.y = pack_bf16x2_u8(v[2] & 0xFF, v[3] & 0xFF);
+      lo.z = pack_bf16x2_u8((v[0] >> 8) & 0xFF, (v[1] >> 8) & 0xFF);
+      lo.w = pack_bf16x2_u8((v[2] >> 8) & 0xFF, (v[3] >> 8) & 0xFF);
+      hi.x = pack_bf16x2_u8((v[0] >> 16) & 0xFF, (v[1] >> 16) & 0xFF);
+      hi.y = pack_bf16x2_u8((v[2] >> 16) & 0xFF, (v[3] >> 16) & 0xFF);
+      hi.z = pack_bf16x2_u8(v[0] >> 24, v[1] >> 24);
+      hi.w = pack_bf16x2_u8(v[2] >> 24, v[3] >> 24);
+      uint4* d = reinterpret_cast<uint4*>(xs + off * G::PIX);
+      d[0] = lo;
+      d[1] = hi;
+    }
+  } else {
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) +
+                                                      (size_t)b * G::H * G::W * G::C * 2);
+    constexpr int CH16 = G::C / 8;  // 16-byte chunks per pixel
+    constexpr int TOTAL = G::H * G::W * CH16;
+    for (int q = threadIdx.x; q < TOTAL; q += blockDim.x) {
+      const int pix = q / CH16, cc = q % CH16;
+      *reinterpret_cast<uint4*>(xs + pix * G::PIX + cc * 16) = src[q];
+    }
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void stage_weights(const uint16_t* __restrict__ wp, char* ws) {
+  constexpr int CH16 = G::K / 8;
+  const uint4* src = reinterpret_cast<const uint4*>(wp);
+  for (int q = threadIdx.x; q < G::N * CH16; q += blockDim.x) {
+    const int n = q / CH16, kk = q % CH16;
+    *reinterpret_cast<uint4*>(ws + n * G::W_ROW + kk * 16) = src[q];
+  }
+}
+
+// LDS byte offset (relative to the output pixel's window origin) of implicit-GEMM k index kk
+// (8 consecutive k starting at kk are contiguous: one tap x 8 channels, or for the 4-channel
+// frame stack two adjacent taps x 4 channels).
+template <class G>
+__device__ __forceinline__ constexpr int a_off(int kk) {
+  if constexpr (G::C == 4) {
+    const int ky = kk / (4 * G::KW), kx = (kk / 4) % G::KW;
+    return (ky * G::W + kx) * G::PIX;
+  } else {
+    const int tap = kk / G::C, c0 = kk % G::C;
+    return ((tap / G::KW) * G::W + tap % G::KW) * G::PIX + c0 * 2;
+  }
+}
+
+template <class G, bool U8IN>
+__global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, const uint16_t* __restrict__ wp,
+                                                  const float* __restrict__ bias, uint16_t* __restrict__ out,
+                                                  int B) {
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  char* ws = smem + G::SPW * G::X_BYTES;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  stage_weights<G>(wp, ws);
+  for (int b0 = blockIdx.x * G::SPW; b0 < B; b0 += gridDim.x * G::SPW) {
+    __syncthreads();
+#pragma unroll
+    for (int sw = 0; sw < G::SPW; ++sw)
+      if (b0 + sw < B) stage_input<G, U8IN>(in, b0 + sw, smem + sw * G::X_BYTES);
+    __syncthreads();
+    constexpr int ITEMS = G::SPW * G::MT * G::NT;
+    for (int it = wave; it < ITEMS; it += 4) {
+      const int sw = it / (G::MT * G::NT);
+      const int mt = (it / G::NT) % G::MT;
+      const int nt = it % G::NT;
+      const int b = b0 + sw;
+      if (b >= B) continue;  // wave-uniform
+      const char* xs = smem + sw * G::X_BYTES;
+      int p = mt * 32 + r32;
+      const int pc = p < G::P ? p : G::P - 1;
+      const int oy = pc / G::OW, ox = pc % G::OW;
+      const char* abase = xs + ((G::S * oy) * G::W + G::S * ox) * G::PIX;
+      const char* bbase = ws + (nt * 32 + r32) * G::W_ROW + h * 16;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < G::KSTEPS; ++s) {
+        // after unrolling, both candidate offsets are compile-time constants
+        const int off = h ? a_off<G>(16 * s + 8) : a_off<G>(16 * s);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase + off);
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + 32 * s);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      }
+      const int n = nt * 32 + r32;
+      const float bn = bias[n];
+      uint16_t* ob = out + (size_t)b * G::P * G::N + n;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int pp = mt * 32 + row;
+        if (pp < G::P) ob[(size_t)pp * G::N] = f2bf(fmaxf(acc[r] + bn, 0.f));
+      }
+    }
+  }
+}
+
+template <class G, bool U8IN>
+static void launch_conv_fwd(const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B,
+                            hipStream_t s) {
+  if (B <= 0) return;
+  const int grid = std::min((B + G::SPW - 1) / G::SPW, 512);
+  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(in, wp, bias, out, B);
+  LAUNCH_CHECK();
+}
+
+void conv_fwd(int layer, const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B, hipStream_t s) {
+  switch (layer) {
+    case 1: launch_conv_fwd<Conv1, true>(in, wp, bias, out, B, s); break;
+    case 2: launch_conv_fwd<Conv2, false>(in, wp, bias, out, B, s); break;
+    case 3: launch_conv_fwd<Conv3, false>(in, wp, bias, out, B, s); break;
+    default: throw std::invalid_argument("conv_fwd: layer must be 1, 2 or 3");
+  }
+}
+
+// ------------------------------------------------------------------ dueling heads
+// z [B][256] = FC1 pre-activation (adv hidden 0..127 | value hidden 128..255, no bias).
+// One wave per row: h = relu(z + b1) -> LDS; lanes a < A compute adv_a, lane A the value;
+// q = V + A - mean(A) (model.py:60-68).  h is kept (fp32) for the backward.
+__global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, const float* __restrict__ b_adv1,
+                                                   const float* __restrict__ b_val1, const float* __restrict__ w_adv2,
+                                                   const float* __restrict__ b_adv2, const float* __restrict__ w_val2,
+                                                   const float* __restrict__ b_val2, float* __restrict__ hout,
+                                                   float* __restrict__ q, int B, int A) {
+  __shared__ float hs[4][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const float* zr = z + (size_t)b * 256;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = lane + 64 * k;
+    const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
+    const float v = fmaxf(zr[j] + bias, 0.f);
+    hs[wave][j] = v;
+    if (hout) hout[(size_t)b * 256 + j] = v;
+  }
+  __syncthreads();  // uniform: rows beyond B returned before any wave of this block waits? see guard below
+  float o = 0.f;
+  if (lane < A) {
+    const float* wr = w_adv2 + lane * 128;
+    for (int j = 0; j < 128; ++j) o += hs[wave][j] * wr[j];
+    o += b_adv2[lane];
+  } else if (lane == A) {
+    for (int j = 0; j < 128; ++j) o += hs[wave][128 + j] * w_val2[j];
+    o += b_val2[0];
+  }
+  const float adv_sum = wave_sum(lane < A ? o : 0.f);
+  const float v = __shfl(o, A, 64);
+  if (lane < A) q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
+}
+
+void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
+               const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s) {
+  if (A < 1 || A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
+  if (B % 4) throw std::invalid_argument("heads_fwd: batch must be a multiple of 4");
+  heads_fwd_k<<<B / 4, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout, q, B, A);
+  LAUNCH_CHECK();
+}
+
+// Backward of the heads for one row per wave:
+//   dv = sum_a dq_a ; dadv_a = dq_a - mean(dq) ; dh_j = sum_a dadv_a W_adv2[a][j] (j<128),
+//   dh_{128+j} = dv W_val2[j] ; dz = dh * (h > 0).
+// Writes dz as fp32 (bias grads) and bf16 (FC1 GEMMs), and dA = [dadv | dv] for the head
+// weight gradients.
+__global__ __launch_bounds__(256) void heads_bwd_k(const float* __restrict__ dq, const float* __restrict__ h,
+                                                   const float* __restrict__ w_adv2, const float* __restrict__ w_val2,
+                                                   float* __restrict__ dA, float* __restrict__ dz,
+                                                   uint16_t* __restrict__ dz_bf, int B, int A) {
+  __shared__ float da_s[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + wave;
+  if (b >= B) return;
+  const float g = lane < A ? dq[(size_t)b * A + lane] : 0.f;
+  const float tot = wave_sum(g);
+  const float dadv = lane < A ? g - tot / (float)A : 0.f;
+  if (lane < A) {
+    da_s[wave][lane] = dadv;
+    dA[(size_t)b * (A + 1) + lane] = dadv;
+  }
+  if (lane == 0) dA[(size_t)b * (A + 1) + A] = tot;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int j = lane + 64 * k;
+    float d;
+    if (j < 128) {
+      d = 0.f;
+      for (int a = 0; a < A; ++a) d += da_s[wave][a] * w_adv2[a * 128 + j];
+    } else {
+      d = tot * w_val2[j - 128];
+    }
+    d = h[(size_t)b * 256 + j] > 0.f ? d : 0.f;
+    dz[(size_t)b * 256 + j] = d;
+    dz_bf[(size_t)b * 256 + j] = f2bf(d);
+  }
+}
+
+void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
+               uint16_t* dz_bf, int B, int A, hipStream_t s) {
+  if (A < 1 || A > 63) throw std::invalid_argument("heads_bwd: 1 <= A <= 63");
+  if (B % 4) throw std::invalid_argument("heads_bwd: batch must be a multiple of 4");
+  heads_bwd_k<<<B / 4, 256, 0, s>>>(dq, h, w_adv2, w_val2, dA, dz, dz_bf, B, A);
+  LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ packing / masks
+// conv weight fp32 [N][C][KH][KW] (reference layout) -> bf16 [N][KH][KW][C]
+__global__ void pack_conv_w_k(const float* __restrict__ src, uint16_t* __restrict__ dst, int N, int C, int KH,
+                              int KW) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // dst index
+  const int total = N * C * KH * KW;
+  if (i >= total) return;
+  const int c = i % C, kx = (i / C) % KW, ky = (i / (C * KW)) % KH, n = i / (C * KW * KH);
+  dst[i] = f2bf(src[((n * C + c) * KH + ky) * KW + kx]);
+}
+
+// FC1 weights: adv.0.weight / value.0.weight fp32 [128][C*P] (order c*P+p) -> bf16 [256][P*C]
+__global__ void pack_fc1_k(const float* __restrict__ adv, const float* __restrict__ val, uint16_t* __restrict__ dst,
+                           int P, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int F = P * C;
+  if (i >= 256 * F) return;
+  const int n = i / F, r = i % F, p = r / C, c = r % C;
+  const float* src = n < 128 ? adv + (size_t)n * F : val + (size_t)(n - 128) * F;
+  dst[i] = f2bf(src[c * P + p]);
+}
+
+// gradient of the packed FC1 weight (fp32 [256][P*C]) -> reference-layout grads (assign)
+__global__ void unpack_fc1_grad_k(const float* __restrict__ gp, float* __restrict__ g_adv, float* __restrict__ g_val,
+                                  int P, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // reference index
+  const int F = P * C;
+  if (i >= 256 * F) return;
+  const int n = i / F, r = i % F, c = r / P, p = r % P;
+  const float v = gp[(size_t)n * F + p * C + c];
+  if (n < 128) g_adv[(size_t)n * F + r] = v; else g_val[(size_t)(n - 128) * F + r] = v;
+}
+
+// y = x * (a > 0) for bf16 tensors (ReLU backward through the stored activation)
+__global__ void relu_mask_bf16_k(const uint16_t* __restrict__ g, const uint16_t* __restrict__ a,
+                                 uint16_t* __restrict__ out, int64_t n8) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  uint4 gv = reinterpret_cast<const uint4*>(g)[i];
+  const uint4 av = reinterpret_cast<const uint4*>(a)[i];
+  uint32_t* gw = reinterpret_cast<uint32_t*>(&gv);
+  const uint32_t* aw = reinterpret_cast<const uint32_t*>(&av);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    // bf16 > 0  <=>  sign bit clear and not +0
+    const uint32_t lo = aw[k] & 0xFFFF, hi = aw[k] >> 16;
+    const uint32_t mlo = (lo != 0 && !(lo & 0x8000)) ? 0xFFFFu : 0u;
+    const uint32_t mhi = (hi != 0 && !(hi & 0x8000)) ? 0xFFFF0000u : 0u;
+    gw[k] &= (mlo | mhi);
+  }
+  reinterpret_cast<uint4*>(out)[i] = gv;
+}
+
+// u8 NCHW [B][4][84][84] -> bf16 NHWC [B][84][84][4] (the conv1 input for its weight gradient)
+__global__ void u8_to_bf16_nhwc_k(const uint8_t* __restrict__ in, uint16_t* __restrict__ out, int B, int HW) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // group of 4 pixels
+  const int64_t groups = (int64_t)B * HW / 4;
+  if (g >= groups) return;
+  const int64_t b = g / (HW / 4), off = (g % (HW / 4)) * 4;
+  const uint8_t* src = in + b * 4 * HW + off;
+  uint32_t v[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const uint32_t*>(src + c * HW);
+  uint4 lo, hi;
+  lo.x = pack_bf16x2_u8(v[0] & 0xFF, v[1] & 0xFF);
+  lo.y = pack_bf16x2_u8(v[2] & 0xFF, v[3] & 0xFF);
+  lo.z = pack_bf16x2_u8((v[0] >> 8) & 0xFF, (v[1] >> 8) & 0xFF);
+  lo.w = pack_bf16x2_u8((v[2] >> 8) & 0xFF, (v[3] >> 8) & 0xFF);
+  hi.x = pack_bf16x2_u8((v[0] >> 16) & 0xFF, (v[1] >> 16) & 0xFF);
+  hi.y = pack_bf16x2_u8((v[2] >> 16) & 0xFF, (v[3] >> 16) & 0xFF);
+  hi.z = pack_bf16x2_u8(v[0] >> 24, v[1] >> 24);
+  hi.w = pack_bf16x2_u8(v[2] >> 24, v[3] >> 24);
+  uint4* d = reinterpret_cast<uint4*>(out + (b * HW + off) * 4);
+  d[0] = lo;
+  d[1] = hi;
+}
+
+void pack_conv_w(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s) {
+  const int total = N * C * KH * KW;
+  pack_conv_w_k<<<(total + 255) / 256, 256, 0, s>>>(src, dst, N, C, KH, KW);
+  LAUNCH_CHECK();
+}
+void pack_fc1(const float* adv, const float* val, uint16_t* dst, int P, int C, hipStream_t s) {
+  const int total = 256 * P * C;
+  pack_fc1_k<<<(total + 255) / 256, 256, 0, s>>>(adv, val, dst, P, C);
+  LAUNCH_CHECK();
+}
+void unpack_fc1_grad(const float* gp, float* g_adv, float* g_val, int P, int C, hipStream_t s) {
+  const int total = 256 * P * C;
+  unpack_fc1_grad_k<<<(total + 255) / 256, 256, 0, s>>>(gp, g_adv, g_val, P, C);
+  LAUNCH_CHECK();
+}
+void relu_mask_bf16(const uint16_t* g, const uint16_t* a, uint16_t* out, int64_t n, hipStream_t s) {
+  if (n % 8) throw std::invalid_argument("relu_mask_bf16: n must be a multiple of 8");
+  const int64_t n8 = n / 8;
+  relu_mask_bf16_k<<<(unsigned)((n8 + 255) / 256), 256, 0, s>>>(g, a, out, n8);
+  LAUNCH_CHECK();
+}
+void u8_to_bf16_nhwc(const uint8_t* in, uint16_t* out, int B, int HW, hipStream_t s) {
+  if (HW % 4) throw std::invalid_argument("u8_to_bf16_nhwc: HW must be a multiple of 4");
+  const int64_t groups = (int64_t)B * HW / 4;
+  u8_to_bf16_nhwc_k<<<(unsigned)((groups + 255) / 256), 256, 0, s>>>(in, out, B, HW);
+  LAUNCH_CHECK();
+}
+
+}  // namespace apex

@@ -204,6 +204,35 @@ PYBIND11_MODULE(_apex_hip, m) {
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
               seg.s, bps, hp, P<const int64_t>(step), P<float>(norms), S(s));
   });
+  // ---- network kernels
+  m.def("conv_fwd", [](int layer, uint64_t in, uint64_t wp, uint64_t bias, uint64_t out, int B, uint64_t s) {
+    conv_fwd(layer, P<const void>(in), P<const uint16_t>(wp), P<const float>(bias), P<uint16_t>(out), B, S(s));
+  });
+  m.def("heads_fwd", [](uint64_t z, uint64_t ba1, uint64_t bv1, uint64_t wa2, uint64_t ba2, uint64_t wv2, uint64_t bv2,
+                        uint64_t hout, uint64_t q, int B, int A, uint64_t s) {
+    heads_fwd(P<const float>(z), P<const float>(ba1), P<const float>(bv1), P<const float>(wa2), P<const float>(ba2),
+              P<const float>(wv2), P<const float>(bv2), P<float>(hout), P<float>(q), B, A, S(s));
+  });
+  m.def("heads_bwd", [](uint64_t dq, uint64_t h, uint64_t wa2, uint64_t wv2, uint64_t dA, uint64_t dz, uint64_t dzb,
+                        int B, int A, uint64_t s) {
+    heads_bwd(P<const float>(dq), P<const float>(h), P<const float>(wa2), P<const float>(wv2), P<float>(dA),
+              P<float>(dz), P<uint16_t>(dzb), B, A, S(s));
+  });
+  m.def("pack_conv_w", [](uint64_t src, uint64_t dst, int N, int C, int KH, int KW, uint64_t s) {
+    pack_conv_w(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));
+  });
+  m.def("pack_fc1", [](uint64_t adv, uint64_t val, uint64_t dst, int Pp, int C, uint64_t s) {
+    pack_fc1(P<const float>(adv), P<const float>(val), P<uint16_t>(dst), Pp, C, S(s));
+  });
+  m.def("unpack_fc1_grad", [](uint64_t gp, uint64_t ga, uint64_t gv, int Pp, int C, uint64_t s) {
+    unpack_fc1_grad(P<const float>(gp), P<float>(ga), P<float>(gv), Pp, C, S(s));
+  });
+  m.def("relu_mask_bf16", [](uint64_t g, uint64_t a, uint64_t out, int64_t n, uint64_t s) {
+    relu_mask_bf16(P<const uint16_t>(g), P<const uint16_t>(a), P<uint16_t>(out), n, S(s));
+  });
+  m.def("u8_to_bf16_nhwc", [](uint64_t in, uint64_t out, int B, int HW, uint64_t s) {
+    u8_to_bf16_nhwc(P<const uint8_t>(in), P<uint16_t>(out), B, HW, S(s));
+  });
   m.def("copy_f32", [](uint64_t dst, uint64_t src, int64_t n, uint64_t s) {
     copy_f32(P<float>(dst), P<const float>(src), n, S(s));
   });

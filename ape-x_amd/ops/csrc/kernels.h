@@ -119,4 +119,16 @@ void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const do
                float* norms_out, hipStream_t s);
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
 
+// ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)
+void conv_fwd(int layer, const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B, hipStream_t s);
+void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
+               const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s);
+void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
+               uint16_t* dz_bf, int B, int A, hipStream_t s);
+void pack_conv_w(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
+void pack_fc1(const float* adv, const float* val, uint16_t* dst, int P, int C, hipStream_t s);
+void unpack_fc1_grad(const float* gp, float* g_adv, float* g_val, int P, int C, hipStream_t s);
+void relu_mask_bf16(const uint16_t* g, const uint16_t* a, uint16_t* out, int64_t n, hipStream_t s);
+void u8_to_bf16_nhwc(const uint8_t* in, uint16_t* out, int B, int HW, hipStream_t s);
+
 }  // namespace apex
