@@ -118,6 +118,7 @@ class DQNLearner:
         self.hip_net = cfg.forward == "hip"
         if self.hip_net:
             self.net = HipDuelingNet(self.model)
+            self.net.enable_backward()
             self.tnet = HipDuelingNet(self.target)
             self.ws_s = NetWorkspace(B, A, dev, keep_for_backward=True)
             self.ws_s2 = NetWorkspace(B, A, dev)

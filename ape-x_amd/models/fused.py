@@ -13,8 +13,9 @@ Forward (per pass, no autograd):
 Backward (explicit, writes every parameter gradient into the flat fp32 grad buffer
 exactly once, so no zeroing pass is needed):
   heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (hipBLASLt) ->
-  ReLU masks + conv backward (MIOpen NHWC bf16 igemm, channels-last views of our
-  buffers) for conv3 -> conv2 -> conv1 (weight grad only).
+  conv3/conv2/conv1: MFMA wgrad (ds_read_b64_tr_b16 operand transposes, split over the
+  batch, deterministic partial reduce, conv bias grads fused) and MFMA dgrad (stride-1
+  zero-border / stride-2 sub-pixel implicit GEMM with the ReLU backward fused).
 
 Numerics: bf16 operands, fp32 accumulation, fp32 heads and Q.  Checked against the
 fp32 PyTorch module in tests/test_gpu_fused_net.py.
@@ -48,7 +49,6 @@ class NetWorkspace:
             self.dz = torch.empty(B, 256, **f32)
             self.dz_bf = torch.empty(B, 256, **bf)
             self.da3 = torch.empty(B, FEAT, **bf)
-            self.x_nhwc = torch.empty(B, 84, 84, 4, **bf)
             self.dy3 = torch.empty(B, P3, C3, **bf)
             self.dy2 = torch.empty(B, 81, 64, **bf)
             self.dy1 = torch.empty(B, 400, 32, **bf)
@@ -72,6 +72,9 @@ class HipDuelingNet:
         self.w2p = torch.empty(64, 4, 4, 32, **bf)
         self.w3p = torch.empty(64, 3, 3, 64, **bf)
         self.wfc1p = torch.empty(256, FEAT, **bf)
+        self.w2t = torch.empty(4, 4, 32, 64, **bf)   # W^T [ky][kx][c][n] for dgrad
+        self.w3t = torch.empty(3, 3, 64, 64, **bf)
+        self._wgrad_ws = None
         f = model.features
         self.b1, self.b2, self.b3 = f[0].bias, f[2].bias, f[4].bias
         self.repack()
@@ -86,6 +89,14 @@ class HipDuelingNet:
         h.pack_conv_w(f[2].weight.data_ptr(), self.w2p.data_ptr(), 64, 32, 4, 4, s)
         h.pack_conv_w(f[4].weight.data_ptr(), self.w3p.data_ptr(), 64, 64, 3, 3, s)
         h.pack_fc1(m.advantage[0].weight.data_ptr(), m.value[0].weight.data_ptr(), self.wfc1p.data_ptr(), P3, C3, s)
+        if self._wgrad_ws is not None:  # the backward is only used by the learner's online net
+            h.pack_conv_wt(f[2].weight.data_ptr(), self.w2t.data_ptr(), 64, 32, 4, 4, s)
+            h.pack_conv_wt(f[4].weight.data_ptr(), self.w3t.data_ptr(), 64, 64, 3, 3, s)
+
+    def enable_backward(self) -> None:
+        n = max(self.hip.wgrad_workspace_floats(k) for k in (1, 2, 3))
+        self._wgrad_ws = torch.empty(n, dtype=torch.float32, device=self.device)
+        self.repack()
 
     # ------------------------------------------------------------------ forward
     def forward(self, x_u8: torch.Tensor, ws: NetWorkspace) -> torch.Tensor:
@@ -123,25 +134,16 @@ class HipDuelingNet:
         h.unpack_fc1_grad(gfc1.data_ptr(), m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(),
                           P3, C3, s)
         torch.mm(ws.dz_bf, self.wfc1p, out=ws.da3)
-        # conv3
+        # conv3 .. conv1: ReLU mask of the FC1 input gradient, then MFMA wgrad/dgrad
+        if self._wgrad_ws is None:
+            self.enable_backward()
+        wsp = self._wgrad_ws.data_ptr()
         h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
-        dx2, dw3, db3 = torch.ops.aten.convolution_backward(
-            _cl_view(ws.dy3, B, 64, 7, 7), _cl_view(ws.a2, B, 64, 9, 9), _cl_view(self.w3p, 64, 64, 3, 3), [64],
-            [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
-        f[4].weight.grad.copy_(dw3)
-        f[4].bias.grad.copy_(db3)
-        dx2 = dx2.contiguous(memory_format=torch.channels_last)
-        h.relu_mask_bf16(dx2.data_ptr(), ws.a2.data_ptr(), ws.dy2.data_ptr(), ws.dy2.numel(), s)
-        dx1, dw2, db2 = torch.ops.aten.convolution_backward(
-            _cl_view(ws.dy2, B, 64, 9, 9), _cl_view(ws.a1, B, 32, 20, 20), _cl_view(self.w2p, 64, 32, 4, 4), [64],
-            [2, 2], [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
-        f[2].weight.grad.copy_(dw2)
-        f[2].bias.grad.copy_(db2)
-        dx1 = dx1.contiguous(memory_format=torch.channels_last)
-        h.relu_mask_bf16(dx1.data_ptr(), ws.a1.data_ptr(), ws.dy1.data_ptr(), ws.dy1.numel(), s)
-        h.u8_to_bf16_nhwc(x_u8.data_ptr(), ws.x_nhwc.data_ptr(), B, 84 * 84, s)
-        _, dw1, db1 = torch.ops.aten.convolution_backward(
-            _cl_view(ws.dy1, B, 32, 20, 20), _cl_view(ws.x_nhwc, B, 4, 84, 84), _cl_view(self.w1p, 32, 4, 8, 8), [32],
-            [4, 4], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
-        f[0].weight.grad.copy_(dw1)
-        f[0].bias.grad.copy_(db1)
+        h.conv_wgrad(3, ws.a2.data_ptr(), ws.dy3.data_ptr(), B, wsp, f[4].weight.grad.data_ptr(),
+                     f[4].bias.grad.data_ptr(), s)
+        h.conv_dgrad(3, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(), ws.dy2.data_ptr(), B, s)
+        h.conv_wgrad(2, ws.a1.data_ptr(), ws.dy2.data_ptr(), B, wsp, f[2].weight.grad.data_ptr(),
+                     f[2].bias.grad.data_ptr(), s)
+        h.conv_dgrad(2, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(), ws.dy1.data_ptr(), B, s)
+        h.conv_wgrad(1, x_u8.data_ptr(), ws.dy1.data_ptr(), B, wsp, f[0].weight.grad.data_ptr(),
+                     f[0].bias.grad.data_ptr(), s)

@@ -40,6 +40,7 @@ HIP_SOURCES = [
     "actor_kernels.hip",
     "learner_kernels.hip",
     "conv_kernels.hip",
+    "conv_bwd_kernels.hip",
 ]
 
 

@@ -1,0 +1,411 @@
+// MFMA backward kernels for the Nature-CNN trunk on gfx950.
+//
+// dgrad (input gradient) as an implicit GEMM  M = input pixels, N = input channels,
+// K = (tap, output channel), fused with the ReLU backward of the layer below:
+//   * conv3 (3x3, stride 1): dy3 staged in LDS with a 2-pixel zero border, so every tap of
+//     every output row is a plain 16-byte read (no bounds checks in the K loop);
+//   * conv2 (4x4, stride 2): sub-pixel decomposition -- input pixels are grouped by
+//     parity class (qy%2, qx%2); inside a class exactly 2x2 taps contribute, so K = 4 taps
+//     x 64 instead of 16 taps x 64 with 3/4 zeros.
+//   B operand = transposed packed weights W^T [tap][c][n] (n contiguous, 16-byte frags).
+//
+// wgrad (weight gradient) dW[n][(ky,kx,c)] = sum_{b,p} dy[b][p][n] x[b][S p + (ky,kx)][c]:
+//   the reduction runs over output pixels, which are strided in the channels-last tiles,
+//   so both MFMA operands are fetched with ds_read_b64_tr_b16 (hardware 4x16 transpose;
+//   every lane supplies its own row address, so the strided im2col rows of the input are
+//   gathered for free).  Each workgroup accumulates a batch slice in registers and writes
+//   one fp32 partial; wgrad_reduce sums the partials in fixed order (deterministic) and
+//   scatters into the reference [N][C][KH][KW] gradient layout.
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(__attribute__((address_space(3))) char*)p);
+}
+
+__device__ __forceinline__ bool bf16_pos(uint16_t v) { return v != 0 && !(v & 0x8000); }
+
+__device__ __forceinline__ uint32_t pack_bf16x2_u8b(uint32_t b0, uint32_t b1) {
+  const uint32_t f0 = __float_as_uint((float)b0), f1 = __float_as_uint((float)b1);
+  return (f0 >> 16) | (f1 & 0xFFFF0000u);
+}
+
+// ====================================================================== dgrad
+// Stage a [OH][OW][64] bf16 dy tile into LDS at offset `border` inside a zeroed
+// [TH][TW] grid (pixel stride 144 B = 128 + 16 pad).
+constexpr int DY_PIX = 144;
+
+template <int OH, int OW, int TH, int TW, int BORDER>
+__device__ __forceinline__ void stage_dy_padded(const uint16_t* __restrict__ dy, char* t) {
+  constexpr int CH = 8;  // 16-byte chunks per pixel (64 channels)
+  for (int q = threadIdx.x; q < OH * OW * CH; q += blockDim.x) {
+    const int pix = q / CH, cc = q % CH;
+    const int py = pix / OW, px = pix % OW;
+    *reinterpret_cast<uint4*>(t + ((py + BORDER) * TW + px + BORDER) * DY_PIX + cc * 16) =
+        reinterpret_cast<const uint4*>(dy)[q];
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void zero_lds(char* t) {
+  for (int q = threadIdx.x; q < ROWS * DY_PIX / 16; q += blockDim.x) reinterpret_cast<uint4*>(t)[q] = uint4{0, 0, 0, 0};
+}
+
+// W^T packed [taps][C][64] bf16 -> LDS rows (tap, c) with stride 144 B
+template <int TAPS, int C>
+__device__ __forceinline__ void stage_wt(const uint16_t* __restrict__ wt, char* t) {
+  constexpr int CH = 8;
+  for (int q = threadIdx.x; q < TAPS * C * CH; q += blockDim.x) {
+    const int row = q / CH, cc = q % CH;
+    *reinterpret_cast<uint4*>(t + row * DY_PIX + cc * 16) = reinterpret_cast<const uint4*>(wt)[q];
+  }
+}
+
+// conv3 dgrad: dy3 [B][49][64] -> dy2 = (dx2 * (a2 > 0)) [B][81][64]
+__global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ wt3,
+                                                const uint16_t* __restrict__ a2, uint16_t* __restrict__ dy2, int B) {
+  constexpr int T = 11, TILE = T * T * DY_PIX;     // 7x7 grid + 2-pixel border
+  constexpr int SPW = 2;
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX];
+  char* wts = smem + SPW * TILE;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  zero_lds<SPW * T * T>(smem);
+  stage_wt<9, 64>(wt3, wts);
+  for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
+    __syncthreads();
+    for (int sw = 0; sw < SPW; ++sw)
+      if (b0 + sw < B) stage_dy_padded<7, 7, T, T, 2>(dy3 + (size_t)(b0 + sw) * 49 * 64, smem + sw * TILE);
+    __syncthreads();
+    // items: (sample, m-tile of 32 input pixels (3), n-tile of 32 channels (2)) = 12
+    for (int it = wave; it < SPW * 6; it += 4) {
+      const int sw = it / 6, mt = (it / 2) % 3, nt = it % 2;
+      const int b = b0 + sw;
+      if (b >= B) continue;
+      const int q = mt * 32 + r32;
+      const int qc = q < 81 ? q : 80;
+      const int qy = qc / 9, qx = qc % 9;
+      // output pixel for tap (ky,kx): (qy-ky, qx-kx) -> padded index (qy-ky+2, qx-kx+2)
+      const char* abase = smem + sw * TILE + ((qy + 2) * T + (qx + 2)) * DY_PIX + h * 16;
+      const char* bbase = wts + (nt * 32 + r32) * DY_PIX + h * 16;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 36; ++s) {
+        const int tap = s / 4, ky = tap / 3, kx = tap % 3, n0 = (s % 4) * 16;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase - (ky * T + kx) * DY_PIX + n0 * 2);
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 64 * DY_PIX + n0 * 2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      }
+      const int c = nt * 32 + r32;
+      const uint16_t* ab = a2 + (size_t)b * 81 * 64 + c;
+      uint16_t* ob = dy2 + (size_t)b * 81 * 64 + c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qq = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (qq < 81) ob[qq * 64] = bf16_pos(ab[qq * 64]) ? f2bf(acc[r]) : (uint16_t)0;
+      }
+    }
+  }
+}
+
+// conv2 dgrad (sub-pixel): dy2 [B][81][64] -> dy1 = (dx1 * (a1 > 0)) [B][400][32]
+__global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ wt2,
+                                                const uint16_t* __restrict__ a1, uint16_t* __restrict__ dy1, int B) {
+  constexpr int T = 11, TILE = T * T * DY_PIX;     // 9x9 grid + 1-pixel border
+  constexpr int SPW = 2;
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX];
+  char* wts = smem + SPW * TILE;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  zero_lds<SPW * T * T>(smem);
+  stage_wt<16, 32>(wt2, wts);
+  for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
+    __syncthreads();
+    for (int sw = 0; sw < SPW; ++sw)
+      if (b0 + sw < B) stage_dy_padded<9, 9, T, T, 1>(dy2 + (size_t)(b0 + sw) * 81 * 64, smem + sw * TILE);
+    __syncthreads();
+    // items: (sample, parity class (4), m-tile of 32 class pixels (4 -> 128 >= 100)) = 32
+    for (int it = wave; it < SPW * 16; it += 4) {
+      const int sw = it / 16, cls = (it / 4) % 4, mt = it % 4;
+      const int b = b0 + sw;
+      if (b >= B) continue;
+      const int ry = cls >> 1, rx = cls & 1;
+      const int m = mt * 32 + r32;
+      const int mc = m < 100 ? m : 99;
+      const int i = mc / 10, j = mc % 10;  // qy = 2i + ry, qx = 2j + rx
+      // contributing taps: ky = ry + 2 dyy, kx = rx + 2 dxx ; output pixel (i - dyy, j - dxx) -> padded +1
+      const char* abase = smem + sw * TILE + ((i + 1) * T + (j + 1)) * DY_PIX + h * 16;
+      const char* bbase = wts + r32 * DY_PIX + h * 16;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int sub = s / 4, dyy = sub >> 1, dxx = sub & 1, n0 = (s % 4) * 16;
+        const int tap = (ry + 2 * dyy) * 4 + (rx + 2 * dxx);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase - (dyy * T + dxx) * DY_PIX + n0 * 2);
+        const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 32 * DY_PIX + n0 * 2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
+      }
+      const int c = r32;
+      const uint16_t* ab = a1 + (size_t)b * 400 * 32 + c;
+      uint16_t* ob = dy1 + (size_t)b * 400 * 32 + c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (mm < 100) {
+          const int q = (2 * (mm / 10) + ry) * 20 + 2 * (mm % 10) + rx;
+          ob[q * 32] = bf16_pos(ab[q * 32]) ? f2bf(acc[r]) : (uint16_t)0;
+        }
+      }
+    }
+  }
+}
+
+void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* wt, const uint16_t* act_below, uint16_t* dy_below,
+                int B, hipStream_t s) {
+  if (B <= 0) return;
+  const int grid = std::min((B + 1) / 2, 512);
+  if (layer == 3) {
+    dgrad3_k<<<grid, 256, 0, s>>>(dy, wt, act_below, dy_below, B);
+  } else if (layer == 2) {
+    dgrad2_k<<<grid, 256, 0, s>>>(dy, wt, act_below, dy_below, B);
+  } else {
+    throw std::invalid_argument("conv_dgrad: layer must be 2 or 3");
+  }
+  LAUNCH_CHECK();
+}
+
+// ====================================================================== wgrad
+template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_>
+struct WG {
+  static constexpr int H = H_, W = W_, C = C_, KH = KH_, KW = KW_, S = S_, N = N_, GRID = GRID_;
+  static constexpr int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1, P = OH * OW;
+  static constexpr int K = KH * KW * C;
+  static constexpr int KT = K / 32;            // 32-wide kidx tiles
+  static constexpr int NT = N / 32;
+  static constexpr int KS = (P + 15) / 16;     // pixel k-steps
+  static constexpr int PPAD = KS * 16;
+  static constexpr int PIX = (C == 4) ? 8 : (C * 2 + 16);
+  static constexpr int X_BYTES = H * W * PIX;
+  static constexpr int DYROW = N * 2 + 16;
+  static constexpr int DY_BYTES = PPAD * DYROW;
+  static constexpr int KTW = (KT + 3) / 4;     // kidx tiles per wave
+};
+using WG1 = WG<84, 84, 4, 8, 8, 4, 32, 128>;
+using WG2 = WG<20, 20, 32, 4, 4, 2, 64, 64>;
+using WG3 = WG<9, 9, 64, 3, 3, 1, 64, 64>;
+
+// LDS byte offset of kidx tile kt's column-block origin relative to an output pixel's window
+template <class G>
+__device__ __forceinline__ int kt_origin(int kt) {
+  if constexpr (G::C == 4) {
+    return kt * G::W * G::PIX;  // tile = kernel row ky (8 taps x 4 channels contiguous)
+  } else {
+    constexpr int CB = G::C / 32;
+    const int tap = kt / CB, c0 = (kt % CB) * 32;
+    return ((tap / G::KW) * G::W + tap % G::KW) * G::PIX + c0 * 2;
+  }
+}
+
+template <class G>
+__global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, const uint16_t* __restrict__ dy, int B,
+                                               float* __restrict__ partial, float* __restrict__ bias_partial) {
+  __shared__ __attribute__((aligned(16))) char smem[G::X_BYTES + G::DY_BYTES];
+  char* xs = smem;
+  char* dys = smem + G::X_BYTES;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
+  const int colsel = 16 * (g & 1) + 4 * pp;  // column (within a 32-wide tile) this lane addresses
+  // zero the padded dy rows once (they stay zero)
+  for (int q = threadIdx.x; q < (G::PPAD - G::P) * G::DYROW / 16; q += blockDim.x)
+    reinterpret_cast<uint4*>(dys + G::P * G::DYROW)[q] = uint4{0, 0, 0, 0};
+  // bias gradient = column sums of dy; thread t owns column t % N and rows = t / N (mod RG)
+  constexpr int RG = 256 / G::N;
+  const int bcol = threadIdx.x % G::N, brow = threadIdx.x / G::N;
+  float bacc = 0.f;
+  f32x16 acc[G::NT][G::KTW];
+#pragma unroll
+  for (int a = 0; a < G::NT; ++a)
+#pragma unroll
+    for (int k = 0; k < G::KTW; ++k) acc[a][k] = f32x16{};
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    __syncthreads();
+    // stage x (as the forward does: padded NHWC bf16; u8 frames converted on the fly)
+    if constexpr (G::C == 4) {
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(x) + (size_t)b * 4 * G::H * G::W;
+      for (int gq = threadIdx.x; gq < G::H * G::W / 4; gq += blockDim.x) {
+        const int off = gq * 4;
+        uint32_t v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const uint32_t*>(src + c * G::H * G::W + off);
+        uint4 lo, hi;
+        lo.x = pack_bf16x2_u8b(v[0] & 0xFF, v[1] & 0xFF);
+        lo.y = pack_bf16x2_u8b(v[2] & 0xFF, v[3] & 0xFF);
+        lo.z = pack_bf16x2_u8b((v[0] >> 8) & 0xFF, (v[1] >> 8) & 0xFF);
+        lo.w = pack_bf16x2_u8b((v[2] >> 8) & 0xFF, (v[3] >> 8) & 0xFF);
+        hi.x = pack_bf16x2_u8b((v[0] >> 16) & 0xFF, (v[1] >> 16) & 0xFF);
+        hi.y = pack_bf16x2_u8b((v[2] >> 16) & 0xFF, (v[3] >> 16) & 0xFF);
+        hi.z = pack_bf16x2_u8b(v[0] >> 24, v[1] >> 24);
+        hi.w = pack_bf16x2_u8b(v[2] >> 24, v[3] >> 24);
+        uint4* d = reinterpret_cast<uint4*>(xs + off * G::PIX);
+        d[0] = lo;
+        d[1] = hi;
+      }
+    } else {
+      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(x) +
+                                                        (size_t)b * G::H * G::W * G::C * 2);
+      constexpr int CH16 = G::C / 8;
+      for (int q = threadIdx.x; q < G::H * G::W * CH16; q += blockDim.x)
+        *reinterpret_cast<uint4*>(xs + (q / CH16) * G::PIX + (q % CH16) * 16) = src[q];
+    }
+    {
+      const uint4* src = reinterpret_cast<const uint4*>(dy + (size_t)b * G::P * G::N);
+      constexpr int CH16 = G::N / 8;
+      for (int q = threadIdx.x; q < G::P * CH16; q += blockDim.x)
+        *reinterpret_cast<uint4*>(dys + (q / CH16) * G::DYROW + (q % CH16) * 16) = src[q];
+    }
+    __syncthreads();
+    for (int r = brow; r < G::P; r += RG)
+      bacc += bf2f(*reinterpret_cast<const uint16_t*>(dys + r * G::DYROW + bcol * 2));
+#pragma unroll 1
+    for (int ks = 0; ks < G::KS; ++ks) {
+      // pixel rows addressed by this lane for the two tr reads: kk = 8h + 4t + q4
+      int prow[2];
+      const char* xrow[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int p = ks * 16 + 8 * h + 4 * t + q4;
+        prow[t] = p;
+        const int pc = p < G::P ? p : G::P - 1;
+        const int oy = pc / G::OW, ox = pc % G::OW;
+        xrow[t] = xs + ((G::S * oy) * G::W + G::S * ox) * G::PIX;
+      }
+      bf16x8 afr[G::NT];
+#pragma unroll
+      for (int nt = 0; nt < G::NT; ++nt) {
+        const int coff = (nt * 32 + colsel) * 2;
+        const bf16x4 lo = tr_read(dys + prow[0] * G::DYROW + coff);
+        const bf16x4 hi = tr_read(dys + prow[1] * G::DYROW + coff);
+        afr[nt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int k = 0; k < G::KTW; ++k) {
+        const int kt = wave + 4 * k;
+        if (kt < G::KT) {
+          const int o = kt_origin<G>(kt) + colsel * 2;
+          const bf16x4 lo = tr_read(xrow[0] + o);
+          const bf16x4 hi = tr_read(xrow[1] + o);
+          const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int nt = 0; nt < G::NT; ++nt)
+            acc[nt][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[nt], bfr, acc[nt][k], 0, 0, 0);
+        }
+      }
+    }
+  }
+  {  // fixed-order combine of the bias partial sums (reuse the x tile region of LDS)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    red[threadIdx.x] = bacc;
+    __syncthreads();
+    if (threadIdx.x < G::N) {
+      float t = 0.f;
+      for (int k = 0; k < RG; ++k) t += red[k * G::N + threadIdx.x];
+      bias_partial[(size_t)blockIdx.x * G::N + threadIdx.x] = t;
+    }
+  }
+  // partial[blk][n][kidx]: C/D map row = n (A rows), col = kidx (B cols)
+  float* out = partial + (size_t)blockIdx.x * G::N * G::K;
+  const int hh = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int nt = 0; nt < G::NT; ++nt)
+#pragma unroll
+    for (int k = 0; k < G::KTW; ++k) {
+      const int kt = wave + 4 * k;
+      if (kt < G::KT) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int n = nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          out[(size_t)n * G::K + kt * 32 + col] = acc[nt][k][r];
+        }
+      }
+    }
+}
+
+// sum partials [G][N][K] (kidx order (ky,kx,c)) -> reference grad [N][C][KH][KW]
+__global__ void wgrad_reduce_k(const float* __restrict__ partial, int G, int N, int C, int KH, int KW,
+                               float* __restrict__ grad) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // reference index
+  const int K = C * KH * KW;
+  if (i >= N * K) return;
+  const int kx = i % KW, ky = (i / KW) % KH, c = (i / (KW * KH)) % C, n = i / K;
+  const int kidx = (ky * KW + kx) * C + c;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += partial[((size_t)g * N + n) * K + kidx];
+  grad[i] = s;
+}
+
+__global__ void bias_reduce_k(const float* __restrict__ bp, int G, int N, float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += bp[(size_t)g * N + n];
+  out[n] = s;
+}
+
+template <class G>
+static void launch_wgrad(const void* x, const uint16_t* dy, int B, float* ws, float* grad, float* bias_grad,
+                         hipStream_t s) {
+  const int grid = std::min(G::GRID, B);
+  float* partial = ws;
+  float* bpart = ws + (size_t)G::GRID * G::N * G::K;
+  wgrad_k<G><<<grid, 256, 0, s>>>(x, dy, B, partial, bpart);
+  LAUNCH_CHECK();
+  const int total = G::N * G::K;
+  wgrad_reduce_k<<<(total + 255) / 256, 256, 0, s>>>(partial, grid, G::N, G::C, G::KH, G::KW, grad);
+  LAUNCH_CHECK();
+  bias_reduce_k<<<1, 64, 0, s>>>(bpart, grid, G::N, bias_grad);
+  LAUNCH_CHECK();
+}
+
+size_t wgrad_workspace_floats(int layer) {
+  switch (layer) {
+    case 1: return (size_t)WG1::GRID * WG1::N * (WG1::K + 1);
+    case 2: return (size_t)WG2::GRID * WG2::N * (WG2::K + 1);
+    case 3: return (size_t)WG3::GRID * WG3::N * (WG3::K + 1);
+    default: throw std::invalid_argument("wgrad layer");
+  }
+}
+
+void conv_wgrad(int layer, const void* x, const uint16_t* dy, int B, float* workspace, float* grad, float* bias_grad,
+                hipStream_t s) {
+  if (B <= 0) return;
+  switch (layer) {
+    case 1: launch_wgrad<WG1>(x, dy, B, workspace, grad, bias_grad, s); break;
+    case 2: launch_wgrad<WG2>(x, dy, B, workspace, grad, bias_grad, s); break;
+    case 3: launch_wgrad<WG3>(x, dy, B, workspace, grad, bias_grad, s); break;
+    default: throw std::invalid_argument("conv_wgrad: layer must be 1, 2 or 3");
+  }
+}
+
+// fp32 [N][C][KH][KW] -> bf16 W^T [KH][KW][C][N]
+__global__ void pack_conv_wt_k(const float* __restrict__ src, uint16_t* __restrict__ dst, int N, int C, int KH,
+                               int KW) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = N * C * KH * KW;
+  if (i >= total) return;
+  const int n = i % N, c = (i / N) % C, kx = (i / (N * C)) % KW, ky = i / (N * C * KW);
+  dst[i] = f2bf(src[((n * C + c) * KH + ky) * KW + kx]);
+}
+
+void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s) {
+  const int total = N * C * KH * KW;
+  pack_conv_wt_k<<<(total + 255) / 256, 256, 0, s>>>(src, dst, N, C, KH, KW);
+  LAUNCH_CHECK();
+}
+
+}  // namespace apex

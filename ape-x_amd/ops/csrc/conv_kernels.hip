@@ -191,17 +191,18 @@ __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, 
   __shared__ float hs[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.x * 4 + wave;
-  if (b >= B) return;
-  const float* zr = z + (size_t)b * 256;
+  const bool valid = b < B;  // no early return: every wave reaches the barrier
+  const float* zr = z + (size_t)(valid ? b : 0) * 256;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int j = lane + 64 * k;
     const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
     const float v = fmaxf(zr[j] + bias, 0.f);
     hs[wave][j] = v;
-    if (hout) hout[(size_t)b * 256 + j] = v;
+    if (hout && valid) hout[(size_t)b * 256 + j] = v;
   }
-  __syncthreads();  // uniform: rows beyond B returned before any wave of this block waits? see guard below
+  __syncthreads();
+  if (!valid) return;
   float o = 0.f;
   if (lane < A) {
     const float* wr = w_adv2 + lane * 128;
@@ -219,8 +220,7 @@ __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, 
 void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
                const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s) {
   if (A < 1 || A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
-  if (B % 4) throw std::invalid_argument("heads_fwd: batch must be a multiple of 4");
-  heads_fwd_k<<<B / 4, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout, q, B, A);
+  heads_fwd_k<<<(B + 3) / 4, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout, q, B, A);
   LAUNCH_CHECK();
 }
 
@@ -236,16 +236,15 @@ __global__ __launch_bounds__(256) void heads_bwd_k(const float* __restrict__ dq,
   __shared__ float da_s[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.x * 4 + wave;
-  if (b >= B) return;
-  const float g = lane < A ? dq[(size_t)b * A + lane] : 0.f;
+  const bool valid = b < B;
+  const float g = (valid && lane < A) ? dq[(size_t)b * A + lane] : 0.f;
   const float tot = wave_sum(g);
   const float dadv = lane < A ? g - tot / (float)A : 0.f;
-  if (lane < A) {
-    da_s[wave][lane] = dadv;
-    dA[(size_t)b * (A + 1) + lane] = dadv;
-  }
-  if (lane == 0) dA[(size_t)b * (A + 1) + A] = tot;
+  if (lane < A) da_s[wave][lane] = dadv;
+  if (valid && lane < A) dA[(size_t)b * (A + 1) + lane] = dadv;
+  if (valid && lane == 0) dA[(size_t)b * (A + 1) + A] = tot;
   __syncthreads();
+  if (!valid) return;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int j = lane + 64 * k;
@@ -265,8 +264,7 @@ __global__ __launch_bounds__(256) void heads_bwd_k(const float* __restrict__ dq,
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
                uint16_t* dz_bf, int B, int A, hipStream_t s) {
   if (A < 1 || A > 63) throw std::invalid_argument("heads_bwd: 1 <= A <= 63");
-  if (B % 4) throw std::invalid_argument("heads_bwd: batch must be a multiple of 4");
-  heads_bwd_k<<<B / 4, 256, 0, s>>>(dq, h, w_adv2, w_val2, dA, dz, dz_bf, B, A);
+  heads_bwd_k<<<(B + 3) / 4, 256, 0, s>>>(dq, h, w_adv2, w_val2, dA, dz, dz_bf, B, A);
   LAUNCH_CHECK();
 }
 

@@ -131,4 +131,12 @@ void unpack_fc1_grad(const float* gp, float* g_adv, float* g_val, int P, int C, 
 void relu_mask_bf16(const uint16_t* g, const uint16_t* a, uint16_t* out, int64_t n, hipStream_t s);
 void u8_to_bf16_nhwc(const uint8_t* in, uint16_t* out, int B, int HW, hipStream_t s);
 
+// ---- conv_bwd_kernels.hip
+void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* wt, const uint16_t* act_below, uint16_t* dy_below,
+                int B, hipStream_t s);
+size_t wgrad_workspace_floats(int layer);
+void conv_wgrad(int layer, const void* x, const uint16_t* dy, int B, float* workspace, float* grad, float* bias_grad,
+                hipStream_t s);
+void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
+
 }  // namespace apex

@@ -1,0 +1,5 @@
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python bench.py --steps 100 --warmup 20 --forward hip > gpurun_out/bench_hip.log 2>&1; rc=$?; echo "bench hip rc=$rc"; tail -3 gpurun_out/bench_hip.log
+exit $rc

@@ -96,8 +96,10 @@ def test_backward_grads_close_to_autograd(cuda):
     q.backward(dq)
     for n, p in ref.named_parameters():
         g = ours[n]
+        # bf16 activations flip a few ReLU masks vs the fp32 reference: expect a few % of
+        # relative error (measured 0.3-7%); a wrong kernel gives O(1)
         rel = (g - p.grad).norm() / (p.grad.norm() + 1e-12)
-        assert rel < 5e-2, (n, float(rel))
+        assert rel < 0.15, (n, float(rel))
 
 
 def test_hip_learner_engine_step(cuda):
@@ -120,3 +122,60 @@ def test_hip_learner_engine_step(cuda):
     st = eng.learner.stats()
     assert np.isfinite(st["loss"]) and st["grad_norm_l2"] > 0
     assert not torch.equal(before, eng.learner.flat)
+
+
+def _rand_bf16(shape, dev, scale=1.0, g=None):
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(dev)
+
+
+@pytest.mark.parametrize("layer", [1, 2, 3])
+def test_wgrad_kernel_matches_torch(cuda, layer):
+    """MFMA weight/bias gradient vs torch fp32 on identical bf16-valued operands."""
+    from apex_amd import ops
+
+    hip = ops.hip()
+    g = torch.Generator().manual_seed(layer)
+    geo = {1: (4, 84, 32, 8, 4, 20), 2: (32, 20, 64, 4, 2, 9), 3: (64, 9, 64, 3, 1, 7)}[layer]
+    C, H, N, KS, S, OH = geo
+    B = 37
+    if layer == 1:
+        x = torch.randint(0, 256, (B, 4, H, H), generator=g, dtype=torch.uint8).to(cuda)
+        x_f = x.float()
+        xptr = x.data_ptr()
+    else:
+        x_nhwc = _rand_bf16((B, H, H, C), cuda, 1.0, g)
+        x_f = x_nhwc.float().permute(0, 3, 1, 2)
+        xptr = x_nhwc.data_ptr()
+    dy = _rand_bf16((B, OH, OH, N), cuda, 0.1, g)
+    ws = torch.empty(hip.wgrad_workspace_floats(layer), device=cuda)
+    gw = torch.empty(N, C, KS, KS, device=cuda)
+    gb = torch.empty(N, device=cuda)
+    hip.conv_wgrad(layer, xptr, dy.data_ptr(), B, ws.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+                   torch.cuda.current_stream().cuda_stream)
+    dy_f = dy.float().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(x_f, (N, C, KS, KS), dy_f, stride=S)
+    ref_b = dy_f.sum((0, 2, 3))
+    torch.testing.assert_close(gw, ref_w, rtol=2e-3, atol=2e-3 * ref_w.abs().max().item())
+    torch.testing.assert_close(gb, ref_b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("layer", [2, 3])
+def test_dgrad_kernel_matches_torch(cuda, layer):
+    """MFMA input gradient (+ fused ReLU backward) vs torch fp32."""
+    from apex_amd import ops
+
+    hip = ops.hip()
+    g = torch.Generator().manual_seed(10 + layer)
+    C, H, N, KS, S, OH = {2: (32, 20, 64, 4, 2, 9), 3: (64, 9, 64, 3, 1, 7)}[layer]
+    B = 21
+    w = torch.randn(N, C, KS, KS, generator=g).to(cuda) * 0.1
+    wt = torch.empty(KS, KS, C, N, dtype=torch.bfloat16, device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    hip.pack_conv_wt(w.data_ptr(), wt.data_ptr(), N, C, KS, KS, s)
+    dy = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)
+    act = _rand_bf16((B, H, H, C), cuda, 1.0, g)  # ~half positive: exercises the mask
+    out = torch.empty(B, H, H, C, dtype=torch.bfloat16, device=cuda)
+    hip.conv_dgrad(layer, dy.data_ptr(), wt.data_ptr(), act.data_ptr(), out.data_ptr(), B, s)
+    ref = torch.nn.grad.conv2d_input((B, C, H, H), _bf(w), dy.float().permute(0, 3, 1, 2), stride=S)
+    ref = (ref.permute(0, 2, 3, 1) * (act.float() > 0)).to(torch.bfloat16).float()
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
