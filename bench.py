@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--capacity", type=int, default=2_000_000)
     ap.add_argument("--threshold", type=int, default=50_000)
     ap.add_argument("--actions", type=int, default=18)
-    ap.add_argument("--forward", default="torch", choices=["torch", "hip"])
+    ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
