@@ -101,9 +101,8 @@ class ActorShard:
         h.nstep_emit(self.nstep, self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                      self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
                      self.slot.data_ptr(), self.prio.data_ptr(), s)
-        self.replay.write_priorities(self.slot, self.prio, dedup=False)
-        h.bump_counter(self.step_counter.data_ptr(), 1, 1, s)
-        h.bump_counter(self.replay.filled.data_ptr(), 1, E, s)
+        self.replay.write_priorities(self.slot, self.prio, dedup=False,
+                                     bumps=((self.step_counter, 1), (self.replay.filled, E)))
 
     def step(self, policy) -> None:
         """One full actor step with ``policy(obs_u8) -> Q f32 [E, A]``."""

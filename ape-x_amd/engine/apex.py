@@ -90,10 +90,10 @@ class ApexEngine:
             self.actor_net.repack()
 
     def _actor_body(self):
-        obs = self.actor.observe()
-        if self.hip_net:
-            q = self.actor_net(obs, self.actor_ws)
+        if self.hip_net:  # conv1 reads the current stacks straight from the frame ring
+            q = self.actor_net(self.replay.frames, self.actor_ws, self.actor.st["hist"])
         else:
+            obs = self.actor.observe()
             with torch.no_grad():
                 q = forward_q(self.actor_model, obs)
         self.actor.act_and_step(q)

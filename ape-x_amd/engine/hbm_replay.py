@@ -68,6 +68,7 @@ class HBMReplay:
         self.node_min = [torch.full((n,), math.inf, dtype=torch.float32, device=dev) for n in sizes[1:]]
         self.max_prio = torch.ones(1, dtype=torch.float32, device=dev)
         self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.sorted_scratch = torch.zeros(1024, dtype=torch.int32, device=dev)
         self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
                                        [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
                                        sizes)
@@ -87,14 +88,19 @@ class HBMReplay:
         return torch.cuda.current_stream().cuda_stream
 
     # ------------------------------------------------------------------ priorities
-    def write_priorities(self, idx: torch.Tensor, prio: torch.Tensor | None, dedup: bool = True) -> None:
+    def write_priorities(self, idx: torch.Tensor, prio: torch.Tensor | None, dedup: bool = True,
+                         bumps: tuple = ()) -> None:
         """Set leaves for ``idx`` (int32) to prio**alpha (None = current max priority),
-        then recompute all dirty ancestors level by level."""
+        then recompute all dirty ancestors level by level.  ``dedup`` resolves duplicate
+        indices last-write-wins (B <= 1024); without it ``idx`` must be unique slots in
+        ring order.  ``bumps``: up to two (int64 device counter, delta) pairs advanced by
+        the same launch."""
         B = idx.numel()
-        s = self._stream()
+        b = list(bumps) + [(None, 0)] * (2 - len(bumps))
+        ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         self.hip.per_write_leaves(self.tree, idx.data_ptr(), 0 if prio is None else prio.data_ptr(), B, self.alpha,
-                                  self.max_prio.data_ptr(), int(dedup), s)
-        self.hip.per_update_levels(self.tree, idx.data_ptr(), B, s)
+                                  self.max_prio.data_ptr(), int(dedup), self.sorted_scratch.data_ptr(), ptr(b[0][0]),
+                                  int(b[0][1]), ptr(b[1][0]), int(b[1][1]), self._stream())
 
     update_priorities = write_priorities
 

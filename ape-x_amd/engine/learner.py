@@ -83,10 +83,8 @@ class DQNLearner:
             n = p.numel()
             p.grad = self.flat_grad[off:off + n].view_as(p)
             off += n
-        segs = self.model.param_segments()
-        self.segments = self.hip.make_segments([o for _, o, _ in segs], [n for _, _, n in segs])
-        self.n_segs = len(segs)
-        self.partials = torch.zeros(self.n_segs * self.BLOCKS_PER_SEG, dtype=torch.float64, device=dev)
+        self.segments = self.model.param_segments()
+        self.partials = torch.zeros(self.hip.grad_norm_partials(), dtype=torch.float64, device=dev)
         self.opt_s1 = torch.zeros(self.P, dtype=torch.float32, device=dev)
         self.opt_s2 = torch.zeros(self.P, dtype=torch.float32, device=dev)
         if cfg.optimizer == "rmsprop":
@@ -103,13 +101,13 @@ class DQNLearner:
         self.w = torch.zeros(B, dtype=torch.float32, device=dev)
         self.s = torch.zeros(B, 4, 84, 84, dtype=torch.uint8, device=dev)
         self.s2 = torch.zeros_like(self.s)
-        self.a = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.a = torch.zeros(B, dtype=torch.int32, device=dev)
         self.r = torch.zeros(B, dtype=torch.float32, device=dev)
         self.d = torch.zeros(B, dtype=torch.float32, device=dev)
         self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self.dq = torch.zeros(B, A, dtype=torch.float32, device=dev)
         self.prio = torch.zeros(B, dtype=torch.float32, device=dev)
-        self.norms = torch.zeros(4, dtype=torch.float32, device=dev)   # l2, reference norm, clip coef, lr
+        self.norms = torch.zeros(4, dtype=torch.float32, device=dev)   # l2, (unused), clip coef, lr
         self.step_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.beta = torch.full((1,), cfg.beta, dtype=torch.float32, device=dev)
         self.gamma_n = float(cfg.gamma ** cfg.n_step)
@@ -133,16 +131,19 @@ class DQNLearner:
         """Sample, gather, forward x3, loss, backward (grads in ``flat_grad``)."""
         s = self._stream()
         self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta)
-        self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
         if self.hip_net:
-            q = self.net(self.s, self.ws_s)
-            q2 = self.net(self.s2, self.ws_s2)
-            q2t = self.tnet(self.s2, self.ws_t)
-            self.hip.dqn_loss(q.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, self.a.data_ptr(),
-                              self.r.data_ptr(), self.d.data_ptr(), self.w.data_ptr(), self.B, self.A, self.gamma_n,
-                              self.loss.data_ptr(), self.dq.data_ptr(), self.prio.data_ptr(), s)
-            self.net.backward(self.dq, self.s, self.ws_s)
+            # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
+            # the loss reads (a, r, d) straight out of the transition table.
+            rp = self.replay
+            q = self.net(rp.frames, self.ws_s, rp.s_ids, self.idx)
+            q2 = self.net(rp.frames, self.ws_s2, rp.s2_ids, self.idx)
+            q2t = self.tnet(rp.frames, self.ws_t, rp.s2_ids, self.idx)
+            self.hip.dqn_loss(q.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, rp.action.data_ptr(),
+                              rp.reward.data_ptr(), rp.done.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), self.B,
+                              self.A, self.gamma_n, self.loss.data_ptr(), self.dq.data_ptr(), self.prio.data_ptr(), s)
+            self.net.backward(self.dq, rp.frames, self.ws_s, rp.s_ids, self.idx)
             return
+        self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
         q = forward_q(self.model, self.s)
         with torch.no_grad():
             q2 = forward_q(self.model, self.s2)
@@ -151,7 +152,7 @@ class DQNLearner:
         q2t = q2t.contiguous()
         qd = q.detach().contiguous()
         self.hip.dqn_loss(qd.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, self.a.data_ptr(), self.r.data_ptr(),
-                          self.d.data_ptr(), self.w.data_ptr(), self.B, self.A, self.gamma_n, self.loss.data_ptr(),
+                          self.d.data_ptr(), 0, self.w.data_ptr(), self.B, self.A, self.gamma_n, self.loss.data_ptr(),
                           self.dq.data_ptr(), self.prio.data_ptr(), s)
         self.flat_grad.zero_()
         q.backward(self.dq)
@@ -159,21 +160,18 @@ class DQNLearner:
     def optimize(self) -> None:
         s = self._stream()
         h = self.hip
-        h.grad_sumsq(self.flat_grad.data_ptr(), self.segments, self.partials.data_ptr(), self.BLOCKS_PER_SEG, s)
+        h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
         if self.cfg.optimizer == "rmsprop":
             h.rmsprop_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
-                           self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(),
-                           self.segments, self.BLOCKS_PER_SEG, self.hp, self.step_counter.data_ptr(),
-                           self.norms.data_ptr(), s)
+                           self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(), self.hp,
+                           self.step_counter.data_ptr(), self.norms.data_ptr(), s)
         else:
             h.adam_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
-                        self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(),
-                        self.segments, self.BLOCKS_PER_SEG, self.hp, self.step_counter.data_ptr(),
-                        self.norms.data_ptr(), s)
+                        self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(), self.hp,
+                        self.step_counter.data_ptr(), self.norms.data_ptr(), s)
         if self.hip_net:
             self.net.repack()
-        self.replay.write_priorities(self.idx, self.prio, dedup=True)
-        h.bump_counter(self.step_counter.data_ptr(), 1, 1, s)
+        self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 
     def step(self) -> None:
         self.sample_and_forward()
@@ -195,6 +193,9 @@ class DQNLearner:
         return self.model.state_dict()
 
     def stats(self) -> dict:
-        """Host-side view of the last step's scalars (forces a sync; call rarely)."""
+        """Host-side view of the last step's scalars (forces a sync; call rarely).
+        ``grad_norm`` is the reference's logged value (sum_p ||g_p||^(1/2))^(1/2) of the last
+        step's (pre-clip) gradient, ``grad_norm_l2`` the true global L2 used for clipping."""
         n = self.norms.tolist()
-        return {"loss": float(self.loss.item()), "grad_norm_l2": n[0], "grad_norm": n[1], "clip": n[2], "lr": n[3]}
+        ref = sum(self.flat_grad[o:o + k].norm().item() ** 0.5 for _, o, k in self.segments) ** 0.5
+        return {"loss": float(self.loss.item()), "grad_norm_l2": n[0], "grad_norm": ref, "clip": n[2], "lr": n[3]}

@@ -94,19 +94,35 @@ class HipDuelingNet:
             h.pack_conv_wt(f[4].weight.data_ptr(), self.w3t.data_ptr(), 64, 64, 3, 3, s)
 
     def enable_backward(self) -> None:
+        """Allocate backward workspaces + transposed weights (call before graph capture)."""
         n = max(self.hip.wgrad_workspace_floats(k) for k in (1, 2, 3))
         self._wgrad_ws = torch.empty(n, dtype=torch.float32, device=self.device)
+        self._heads_ws = torch.empty(self.hip.heads_wgrad_workspace_floats(self.A), dtype=torch.float32,
+                                     device=self.device)
         self.repack()
 
     # ------------------------------------------------------------------ forward
-    def forward(self, x_u8: torch.Tensor, ws: NetWorkspace) -> torch.Tensor:
-        B = x_u8.shape[0]
-        assert x_u8.dtype == torch.uint8 and x_u8.is_contiguous() and tuple(x_u8.shape[1:]) == (4, 84, 84)
-        assert B == ws.B
+    @staticmethod
+    def _src(x: torch.Tensor, ids, idx, B: int):
+        """(ptr, ids_ptr, idx_ptr) of a conv1 input: a dense u8 [B,4,84,84] stack, or the
+        HBM frame ring ``x`` addressed by frame ids ``ids`` [*,4] (rows picked by ``idx``)."""
+        assert x.dtype == torch.uint8 and x.is_contiguous()
+        if ids is None:
+            assert tuple(x.shape) == (B, 4, 84, 84)
+            return x.data_ptr(), 0, 0
+        assert ids.dtype == torch.int32 and ids.shape[-1] == 4 and x.shape[-1] == 84 * 84
+        if idx is None:
+            assert ids.shape[0] == B
+        return x.data_ptr(), ids.data_ptr(), 0 if idx is None else idx.data_ptr()
+
+    def forward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
+                idx: torch.Tensor | None = None) -> torch.Tensor:
+        B = ws.B
+        xp, ip, jp = self._src(x, ids, idx, B)
         h, s, m = self.hip, self._s(), self.model
-        h.conv_fwd(1, x_u8.data_ptr(), self.w1p.data_ptr(), self.b1.data_ptr(), ws.a1.data_ptr(), B, s)
-        h.conv_fwd(2, ws.a1.data_ptr(), self.w2p.data_ptr(), self.b2.data_ptr(), ws.a2.data_ptr(), B, s)
-        h.conv_fwd(3, ws.a2.data_ptr(), self.w3p.data_ptr(), self.b3.data_ptr(), ws.a3.data_ptr(), B, s)
+        h.conv_fwd(1, xp, ip, jp, self.w1p.data_ptr(), self.b1.data_ptr(), ws.a1.data_ptr(), B, s)
+        h.conv_fwd(2, ws.a1.data_ptr(), 0, 0, self.w2p.data_ptr(), self.b2.data_ptr(), ws.a2.data_ptr(), B, s)
+        h.conv_fwd(3, ws.a2.data_ptr(), 0, 0, self.w3p.data_ptr(), self.b3.data_ptr(), ws.a3.data_ptr(), B, s)
         torch.mm(ws.a3, self.wfc1p.t(), out_dtype=torch.float32, out=ws.z)
         h.heads_fwd(ws.z.data_ptr(), m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
                     m.advantage[2].weight.data_ptr(), m.advantage[2].bias.data_ptr(), m.value[2].weight.data_ptr(),
@@ -117,33 +133,33 @@ class HipDuelingNet:
     __call__ = forward
 
     # ------------------------------------------------------------------ backward
-    def backward(self, dq: torch.Tensor, x_u8: torch.Tensor, ws: NetWorkspace) -> None:
-        """Write dL/dparam for the pass held in ``ws`` into the model's ``.grad`` views."""
+    def backward(self, dq: torch.Tensor, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
+                 idx: torch.Tensor | None = None) -> None:
+        """Write dL/dparam for the pass held in ``ws`` (input ``x``/``ids``/``idx`` as in
+        :meth:`forward`) into the model's ``.grad`` views."""
         B, A = ws.B, self.A
+        xp, ip, jp = self._src(x, ids, idx, B)
         h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        if self._wgrad_ws is None:
+            self.enable_backward()
         h.heads_bwd(dq.data_ptr(), ws.h.data_ptr(), m.advantage[2].weight.data_ptr(), m.value[2].weight.data_ptr(),
                     ws.dA.data_ptr(), ws.dz.data_ptr(), ws.dz_bf.data_ptr(), B, A, s)
-        dadv, dv = ws.dA[:, :A], ws.dA[:, A:]
-        torch.mm(dadv.t(), ws.h[:, :128], out=m.advantage[2].weight.grad)
-        torch.sum(dadv, 0, out=m.advantage[2].bias.grad)
-        torch.mm(dv.t(), ws.h[:, 128:], out=m.value[2].weight.grad)
-        torch.sum(dv, 0, out=m.value[2].bias.grad)
-        torch.sum(ws.dz[:, :128], 0, out=m.advantage[0].bias.grad)
-        torch.sum(ws.dz[:, 128:], 0, out=m.value[0].bias.grad)
+        h.heads_wgrad(ws.dA.data_ptr(), ws.h.data_ptr(), ws.dz.data_ptr(), B, A, self._heads_ws.data_ptr(),
+                      m.advantage[2].weight.grad.data_ptr(), m.advantage[2].bias.grad.data_ptr(),
+                      m.value[2].weight.grad.data_ptr(), m.value[2].bias.grad.data_ptr(),
+                      m.advantage[0].bias.grad.data_ptr(), m.value[0].bias.grad.data_ptr(), s)
         gfc1 = torch.mm(ws.dz_bf.t(), ws.a3, out_dtype=torch.float32)
         h.unpack_fc1_grad(gfc1.data_ptr(), m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(),
                           P3, C3, s)
         torch.mm(ws.dz_bf, self.wfc1p, out=ws.da3)
         # conv3 .. conv1: ReLU mask of the FC1 input gradient, then MFMA wgrad/dgrad
-        if self._wgrad_ws is None:
-            self.enable_backward()
         wsp = self._wgrad_ws.data_ptr()
         h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
-        h.conv_wgrad(3, ws.a2.data_ptr(), ws.dy3.data_ptr(), B, wsp, f[4].weight.grad.data_ptr(),
+        h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), B, wsp, f[4].weight.grad.data_ptr(),
                      f[4].bias.grad.data_ptr(), s)
         h.conv_dgrad(3, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(), ws.dy2.data_ptr(), B, s)
-        h.conv_wgrad(2, ws.a1.data_ptr(), ws.dy2.data_ptr(), B, wsp, f[2].weight.grad.data_ptr(),
+        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), B, wsp, f[2].weight.grad.data_ptr(),
                      f[2].bias.grad.data_ptr(), s)
         h.conv_dgrad(2, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(), ws.dy1.data_ptr(), B, s)
-        h.conv_wgrad(1, x_u8.data_ptr(), ws.dy1.data_ptr(), B, wsp, f[0].weight.grad.data_ptr(),
+        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), B, wsp, f[0].weight.grad.data_ptr(),
                      f[0].bias.grad.data_ptr(), s)

@@ -115,4 +115,92 @@ __device__ __forceinline__ void atomic_max_pos_float(float* addr, float v) {
   atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));
 }
 
+// Where a conv1 input sample lives.  With `ids`, sample b's frame c is frame
+// ids[(idx ? idx[b] : b) * 4 + c] of the HBM frame ring (the replay / actor stack is read
+// in place, no gather); without, the input is a dense u8 [B][4][84][84] tensor.
+struct FrameSrc {
+  const uint8_t* frames;
+  const int* ids;
+  const int* idx;
+};
+
+__device__ __forceinline__ const uint8_t* frame_plane(const FrameSrc& f, int b, int c, int plane_bytes) {
+  if (f.ids) {
+    const int row = f.idx ? f.idx[b] : b;
+    return f.frames + (size_t)f.ids[row * 4 + c] * plane_bytes;
+  }
+  return f.frames + ((size_t)b * 4 + c) * plane_bytes;
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2_u8(uint32_t b0, uint32_t b1) {
+  // integers 0..255 are exact in bf16: bf16 = high half of the f32
+  const uint32_t f0 = __float_as_uint((float)b0), f1 = __float_as_uint((float)b1);
+  return (f0 >> 16) | (f1 & 0xFFFF0000u);
+}
+
+// 4 channel planes x 16 consecutive u8 pixels -> 16 pixels x 4 channels bf16 (128 B)
+__device__ __forceinline__ void u8x4planes_to_bf16_nhwc(const uint4 (&v)[4], uint4 (&o)[8]) {
+  const uint32_t* w[4] = {&v[0].x, &v[1].x, &v[2].x, &v[3].x};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {      // 4 words of 4 pixels each
+#pragma unroll
+    for (int bb = 0; bb < 4; bb += 2) {  // pixel pairs within the word
+      const int sh0 = 8 * bb, sh1 = 8 * (bb + 1);
+      uint4 q;
+      q.x = pack_bf16x2_u8((w[0][k] >> sh0) & 0xFF, (w[1][k] >> sh0) & 0xFF);
+      q.y = pack_bf16x2_u8((w[2][k] >> sh0) & 0xFF, (w[3][k] >> sh0) & 0xFF);
+      q.z = pack_bf16x2_u8((w[0][k] >> sh1) & 0xFF, (w[1][k] >> sh1) & 0xFF);
+      q.w = pack_bf16x2_u8((w[2][k] >> sh1) & 0xFF, (w[3][k] >> sh1) & 0xFF);
+      o[2 * k + bb / 2] = q;
+    }
+  }
+}
+
+// Stage a 4-frame u8 stack (84x84) into LDS as NHWC bf16 with 8-byte pixels: every
+// thread issues all of its 16-byte global loads before the first LDS write.
+template <int HW>
+__device__ __forceinline__ void stage_frames_bf16(const FrameSrc& f, int b, char* xs) {
+  constexpr int GROUPS = HW / 16;                 // 16-pixel groups
+  constexpr int PER = (GROUPS + 255) / 256;
+  const uint8_t* pl[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) pl[c] = frame_plane(f, b, c, HW);
+  uint4 v[PER][4];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int g = threadIdx.x + 256 * k;
+    if (g < GROUPS)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[k][c] = reinterpret_cast<const uint4*>(pl[c])[g];
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int g = threadIdx.x + 256 * k;
+    if (g < GROUPS) {
+      uint4 o[8];
+      u8x4planes_to_bf16_nhwc(v[k], o);
+      uint4* d = reinterpret_cast<uint4*>(xs + g * 16 * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = o[j];
+    }
+  }
+}
+
+// Pipelined 16-byte copy global -> LDS of TOTAL chunks with a destination remap.
+template <int TOTAL, class DstOff>
+__device__ __forceinline__ void stage_chunks(const uint4* __restrict__ src, char* dst, DstOff dst_off) {
+  constexpr int PER = (TOTAL + 255) / 256;
+  uint4 v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    if (q < TOTAL) v[k] = src[q];
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    if (q < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q)) = v[k];
+  }
+}
+
 }  // namespace apex

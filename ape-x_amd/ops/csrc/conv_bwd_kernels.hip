@@ -32,10 +32,6 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
 
 __device__ __forceinline__ bool bf16_pos(uint16_t v) { return v != 0 && !(v & 0x8000); }
 
-__device__ __forceinline__ uint32_t pack_bf16x2_u8b(uint32_t b0, uint32_t b1) {
-  const uint32_t f0 = __float_as_uint((float)b0), f1 = __float_as_uint((float)b1);
-  return (f0 >> 16) | (f1 & 0xFFFF0000u);
-}
 
 // ====================================================================== dgrad
 // Stage a [OH][OW][64] bf16 dy tile into LDS at offset `border` inside a zeroed
@@ -45,12 +41,10 @@ constexpr int DY_PIX = 144;
 template <int OH, int OW, int TH, int TW, int BORDER>
 __device__ __forceinline__ void stage_dy_padded(const uint16_t* __restrict__ dy, char* t) {
   constexpr int CH = 8;  // 16-byte chunks per pixel (64 channels)
-  for (int q = threadIdx.x; q < OH * OW * CH; q += blockDim.x) {
+  stage_chunks<OH * OW * CH>(reinterpret_cast<const uint4*>(dy), t, [](int q) {
     const int pix = q / CH, cc = q % CH;
-    const int py = pix / OW, px = pix % OW;
-    *reinterpret_cast<uint4*>(t + ((py + BORDER) * TW + px + BORDER) * DY_PIX + cc * 16) =
-        reinterpret_cast<const uint4*>(dy)[q];
-  }
+    return ((pix / OW + BORDER) * TW + pix % OW + BORDER) * DY_PIX + cc * 16;
+  });
 }
 
 template <int ROWS>
@@ -62,10 +56,8 @@ __device__ __forceinline__ void zero_lds(char* t) {
 template <int TAPS, int C>
 __device__ __forceinline__ void stage_wt(const uint16_t* __restrict__ wt, char* t) {
   constexpr int CH = 8;
-  for (int q = threadIdx.x; q < TAPS * C * CH; q += blockDim.x) {
-    const int row = q / CH, cc = q % CH;
-    *reinterpret_cast<uint4*>(t + row * DY_PIX + cc * 16) = reinterpret_cast<const uint4*>(wt)[q];
-  }
+  stage_chunks<TAPS * C * CH>(reinterpret_cast<const uint4*>(wt), t,
+                              [](int q) { return (q / CH) * DY_PIX + (q % CH) * 16; });
 }
 
 // conv3 dgrad: dy3 [B][49][64] -> dy2 = (dx2 * (a2 > 0)) [B][81][64]
@@ -212,8 +204,9 @@ __device__ __forceinline__ int kt_origin(int kt) {
 }
 
 template <class G>
-__global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, const uint16_t* __restrict__ dy, int B,
-                                               float* __restrict__ partial, float* __restrict__ bias_partial) {
+__global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
+                                               const uint16_t* __restrict__ dy, int B, float* __restrict__ partial,
+                                               float* __restrict__ bias_partial) {
   __shared__ __attribute__((aligned(16))) char smem[G::X_BYTES + G::DY_BYTES];
   char* xs = smem;
   char* dys = smem + G::X_BYTES;
@@ -234,39 +227,20 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, const
     for (int k = 0; k < G::KTW; ++k) acc[a][k] = f32x16{};
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     __syncthreads();
-    // stage x (as the forward does: padded NHWC bf16; u8 frames converted on the fly)
+    // stage x (as the forward does: padded NHWC bf16; u8 frames read in place from the
+    // frame ring and converted on the fly) and dy (rows of N channels, padded)
     if constexpr (G::C == 4) {
-      const uint8_t* src = reinterpret_cast<const uint8_t*>(x) + (size_t)b * 4 * G::H * G::W;
-      for (int gq = threadIdx.x; gq < G::H * G::W / 4; gq += blockDim.x) {
-        const int off = gq * 4;
-        uint32_t v[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const uint32_t*>(src + c * G::H * G::W + off);
-        uint4 lo, hi;
-        lo.x = pack_bf16x2_u8b(v[0] & 0xFF, v[1] & 0xFF);
-        lo.y = pack_bf16x2_u8b(v[2] & 0xFF, v[3] & 0xFF);
-        lo.z = pack_bf16x2_u8b((v[0] >> 8) & 0xFF, (v[1] >> 8) & 0xFF);
-        lo.w = pack_bf16x2_u8b((v[2] >> 8) & 0xFF, (v[3] >> 8) & 0xFF);
-        hi.x = pack_bf16x2_u8b((v[0] >> 16) & 0xFF, (v[1] >> 16) & 0xFF);
-        hi.y = pack_bf16x2_u8b((v[2] >> 16) & 0xFF, (v[3] >> 16) & 0xFF);
-        hi.z = pack_bf16x2_u8b(v[0] >> 24, v[1] >> 24);
-        hi.w = pack_bf16x2_u8b(v[2] >> 24, v[3] >> 24);
-        uint4* d = reinterpret_cast<uint4*>(xs + off * G::PIX);
-        d[0] = lo;
-        d[1] = hi;
-      }
+      stage_frames_bf16<G::H * G::W>(fs, b, xs);
     } else {
-      const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(x) +
-                                                        (size_t)b * G::H * G::W * G::C * 2);
       constexpr int CH16 = G::C / 8;
-      for (int q = threadIdx.x; q < G::H * G::W * CH16; q += blockDim.x)
-        *reinterpret_cast<uint4*>(xs + (q / CH16) * G::PIX + (q % CH16) * 16) = src[q];
+      stage_chunks<G::H * G::W * CH16>(
+          reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(x) + (size_t)b * G::H * G::W * G::C * 2), xs,
+          [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
     }
     {
-      const uint4* src = reinterpret_cast<const uint4*>(dy + (size_t)b * G::P * G::N);
       constexpr int CH16 = G::N / 8;
-      for (int q = threadIdx.x; q < G::P * CH16; q += blockDim.x)
-        *reinterpret_cast<uint4*>(dys + (q / CH16) * G::DYROW + (q % CH16) * 16) = src[q];
+      stage_chunks<G::P * CH16>(reinterpret_cast<const uint4*>(dy + (size_t)b * G::P * G::N), dys,
+                                [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
     }
     __syncthreads();
     for (int r = brow; r < G::P; r += RG)
@@ -336,39 +310,49 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, const
     }
 }
 
-// sum partials [G][N][K] (kidx order (ky,kx,c)) -> reference grad [N][C][KH][KW]
-__global__ void wgrad_reduce_k(const float* __restrict__ partial, int G, int N, int C, int KH, int KW,
-                               float* __restrict__ grad) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // reference index
+// Sum the [G][N][K] partials (kidx order (ky,kx,c)) and the [G][N] bias partials.
+// Block = 64 outputs x 4 waves; wave w sums partials g = w, w+4, ... (coalesced, 4x the
+// loads in flight), fixed-order combine in LDS; writes the reference [N][C][KH][KW] grad.
+__global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ partial,
+                                                      const float* __restrict__ bpart, int G, int N, int C, int KH,
+                                                      int KW, float* __restrict__ grad, float* __restrict__ bias_grad) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int K = C * KH * KW;
-  if (i >= N * K) return;
-  const int kx = i % KW, ky = (i / KW) % KH, c = (i / (KW * KH)) % C, n = i / K;
-  const int kidx = (ky * KW + kx) * C + c;
+  const int e = blockIdx.x * 64 + lane;
+  const int total = N * K + N;
   float s = 0.f;
-  for (int g = 0; g < G; ++g) s += partial[((size_t)g * N + n) * K + kidx];
-  grad[i] = s;
-}
-
-__global__ void bias_reduce_k(const float* __restrict__ bp, int G, int N, float* __restrict__ out) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += bp[(size_t)g * N + n];
-  out[n] = s;
+  if (e < N * K) {
+#pragma unroll 4
+    for (int g = wave; g < G; g += 4) s += partial[(size_t)g * N * K + e];
+  } else if (e < total) {
+#pragma unroll 4
+    for (int g = wave; g < G; g += 4) s += bpart[(size_t)g * N + (e - N * K)];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && e < total) {
+    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (e < N * K) {
+      const int n = e / K, kidx = e % K;
+      const int c = kidx % C, tap = kidx / C;
+      grad[((n * C + c) * KH + tap / KW) * KW + tap % KW] = t;
+    } else {
+      bias_grad[e - N * K] = t;
+    }
+  }
 }
 
 template <class G>
-static void launch_wgrad(const void* x, const uint16_t* dy, int B, float* ws, float* grad, float* bias_grad,
-                         hipStream_t s) {
+static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, int B, float* ws, float* grad,
+                         float* bias_grad, hipStream_t s) {
   const int grid = std::min(G::GRID, B);
   float* partial = ws;
   float* bpart = ws + (size_t)G::GRID * G::N * G::K;
-  wgrad_k<G><<<grid, 256, 0, s>>>(x, dy, B, partial, bpart);
+  wgrad_k<G><<<grid, 256, 0, s>>>(x, fs, dy, B, partial, bpart);
   LAUNCH_CHECK();
-  const int total = G::N * G::K;
-  wgrad_reduce_k<<<(total + 255) / 256, 256, 0, s>>>(partial, grid, G::N, G::C, G::KH, G::KW, grad);
-  LAUNCH_CHECK();
-  bias_reduce_k<<<1, 64, 0, s>>>(bpart, grid, G::N, bias_grad);
+  const int total = G::N * G::K + G::N;
+  wgrad_reduce_k<<<(total + 63) / 64, 256, 0, s>>>(partial, bpart, grid, G::N, G::C, G::KH, G::KW, grad, bias_grad);
   LAUNCH_CHECK();
 }
 
@@ -381,13 +365,14 @@ size_t wgrad_workspace_floats(int layer) {
   }
 }
 
-void conv_wgrad(int layer, const void* x, const uint16_t* dy, int B, float* workspace, float* grad, float* bias_grad,
-                hipStream_t s) {
+void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const uint16_t* dy, int B, float* workspace,
+                float* grad, float* bias_grad, hipStream_t s) {
   if (B <= 0) return;
+  const FrameSrc fs{reinterpret_cast<const uint8_t*>(x), ids, idx};
   switch (layer) {
-    case 1: launch_wgrad<WG1>(x, dy, B, workspace, grad, bias_grad, s); break;
-    case 2: launch_wgrad<WG2>(x, dy, B, workspace, grad, bias_grad, s); break;
-    case 3: launch_wgrad<WG3>(x, dy, B, workspace, grad, bias_grad, s); break;
+    case 1: launch_wgrad<WG1>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
+    case 2: launch_wgrad<WG2>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
+    case 3: launch_wgrad<WG3>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
     default: throw std::invalid_argument("conv_wgrad: layer must be 1, 2 or 3");
   }
 }

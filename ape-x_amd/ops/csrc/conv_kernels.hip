@@ -44,58 +44,25 @@ using Conv3 = ConvGeo<9, 9, 64, 3, 3, 1, 64>;
 static_assert(Conv1::P == 400 && Conv2::P == 81 && Conv3::P == 49, "Nature-CNN geometry");
 static_assert(Conv1::LDS <= 160 * 1024 && Conv2::LDS <= 160 * 1024 && Conv3::LDS <= 160 * 1024, "LDS");
 
-__device__ __forceinline__ uint32_t pack_bf16x2_u8(uint32_t b0, uint32_t b1) {
-  // integers 0..255 are exact in bf16: bf16 = high half of the f32
-  const uint32_t f0 = __float_as_uint((float)b0), f1 = __float_as_uint((float)b1);
-  return (f0 >> 16) | (f1 & 0xFFFF0000u);
-}
-
-// Stage one sample's input into LDS as padded NHWC bf16.
+// Stage one sample's input into LDS as padded NHWC bf16 (blockDim must be 256).
 template <class G, bool U8IN>
-__device__ __forceinline__ void stage_input(const void* __restrict__ in, int b, char* xs) {
+__device__ __forceinline__ void stage_input(const void* __restrict__ in, const FrameSrc& fs, int b, char* xs) {
   if constexpr (U8IN) {
-    // u8 NCHW [4][84][84] -> bf16 NHWC; thread = 4 consecutive x of one row
-    static_assert(G::C == 4 && G::W % 4 == 0, "u8 path is the 4-frame stack");
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(in) + (size_t)b * G::C * G::H * G::W;
-    constexpr int GROUPS = G::H * G::W / 4;
-    for (int g = threadIdx.x; g < GROUPS; g += blockDim.x) {
-      const int off = g * 4;
-      uint32_t v[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[c] = *reinterpret_cast<const uint32_t*>(src + c * G::H * G::W + off);
-      uint4 lo, hi;  // pixels x..x+1 and x+2..x+3, 4 channels each
-      lo.x = pack_bf16x2_u8(v[0] & 0xFF, v[1] & 0xFF);
-      lo.y = pack_bf16x2_u8(v[2] & 0xFF, v[3] & 0xFF);
-      lo.z = pack_bf16x2_u8((v[0] >> 8) & 0xFF, (v[1] >> 8) & 0xFF);
-      lo.w = pack_bf16x2_u8((v[2] >> 8) & 0xFF, (v[3] >> 8) & 0xFF);
-      hi.x = pack_bf16x2_u8((v[0] >> 16) & 0xFF, (v[1] >> 16) & 0xFF);
-      hi.y = pack_bf16x2_u8((v[2] >> 16) & 0xFF, (v[3] >> 16) & 0xFF);
-      hi.z = pack_bf16x2_u8(v[0] >> 24, v[1] >> 24);
-      hi.w = pack_bf16x2_u8(v[2] >> 24, v[3] >> 24);
-      uint4* d = reinterpret_cast<uint4*>(xs + off * G::PIX);
-      d[0] = lo;
-      d[1] = hi;
-    }
+    static_assert(G::C == 4 && G::PIX == 8, "u8 path is the 4-frame stack");
+    stage_frames_bf16<G::H * G::W>(fs, b, xs);
   } else {
+    constexpr int CH16 = G::C / 8;  // 16-byte chunks per pixel
     const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) +
                                                       (size_t)b * G::H * G::W * G::C * 2);
-    constexpr int CH16 = G::C / 8;  // 16-byte chunks per pixel
-    constexpr int TOTAL = G::H * G::W * CH16;
-    for (int q = threadIdx.x; q < TOTAL; q += blockDim.x) {
-      const int pix = q / CH16, cc = q % CH16;
-      *reinterpret_cast<uint4*>(xs + pix * G::PIX + cc * 16) = src[q];
-    }
+    stage_chunks<G::H * G::W * CH16>(src, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
   }
 }
 
 template <class G>
 __device__ __forceinline__ void stage_weights(const uint16_t* __restrict__ wp, char* ws) {
   constexpr int CH16 = G::K / 8;
-  const uint4* src = reinterpret_cast<const uint4*>(wp);
-  for (int q = threadIdx.x; q < G::N * CH16; q += blockDim.x) {
-    const int n = q / CH16, kk = q % CH16;
-    *reinterpret_cast<uint4*>(ws + n * G::W_ROW + kk * 16) = src[q];
-  }
+  stage_chunks<G::N * CH16>(reinterpret_cast<const uint4*>(wp), ws,
+                            [](int q) { return (q / CH16) * G::W_ROW + (q % CH16) * 16; });
 }
 
 // LDS byte offset (relative to the output pixel's window origin) of implicit-GEMM k index kk
@@ -113,9 +80,9 @@ __device__ __forceinline__ constexpr int a_off(int kk) {
 }
 
 template <class G, bool U8IN>
-__global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, const uint16_t* __restrict__ wp,
-                                                  const float* __restrict__ bias, uint16_t* __restrict__ out,
-                                                  int B) {
+__global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, FrameSrc fs,
+                                                  const uint16_t* __restrict__ wp, const float* __restrict__ bias,
+                                                  uint16_t* __restrict__ out, int B) {
   __shared__ __attribute__((aligned(16))) char smem[G::LDS];
   char* ws = smem + G::SPW * G::X_BYTES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
@@ -124,7 +91,7 @@ __global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, c
     __syncthreads();
 #pragma unroll
     for (int sw = 0; sw < G::SPW; ++sw)
-      if (b0 + sw < B) stage_input<G, U8IN>(in, b0 + sw, smem + sw * G::X_BYTES);
+      if (b0 + sw < B) stage_input<G, U8IN>(in, fs, b0 + sw, smem + sw * G::X_BYTES);
     __syncthreads();
     constexpr int ITEMS = G::SPW * G::MT * G::NT;
     for (int it = wave; it < ITEMS; it += 4) {
@@ -162,65 +129,78 @@ __global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, c
 }
 
 template <class G, bool U8IN>
-static void launch_conv_fwd(const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B,
+static void launch_conv_fwd(const void* in, FrameSrc fs, const uint16_t* wp, const float* bias, uint16_t* out, int B,
                             hipStream_t s) {
   if (B <= 0) return;
   const int grid = std::min((B + G::SPW - 1) / G::SPW, 512);
-  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(in, wp, bias, out, B);
+  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(in, fs, wp, bias, out, B);
   LAUNCH_CHECK();
 }
 
-void conv_fwd(int layer, const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B, hipStream_t s) {
+void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const uint16_t* wp, const float* bias,
+              uint16_t* out, int B, hipStream_t s) {
+  const FrameSrc fs{reinterpret_cast<const uint8_t*>(in), ids, idx};
   switch (layer) {
-    case 1: launch_conv_fwd<Conv1, true>(in, wp, bias, out, B, s); break;
-    case 2: launch_conv_fwd<Conv2, false>(in, wp, bias, out, B, s); break;
-    case 3: launch_conv_fwd<Conv3, false>(in, wp, bias, out, B, s); break;
+    case 1: launch_conv_fwd<Conv1, true>(in, fs, wp, bias, out, B, s); break;
+    case 2: launch_conv_fwd<Conv2, false>(in, fs, wp, bias, out, B, s); break;
+    case 3: launch_conv_fwd<Conv3, false>(in, fs, wp, bias, out, B, s); break;
     default: throw std::invalid_argument("conv_fwd: layer must be 1, 2 or 3");
   }
 }
 
 // ------------------------------------------------------------------ dueling heads
 // z [B][256] = FC1 pre-activation (adv hidden 0..127 | value hidden 128..255, no bias).
-// One wave per row: h = relu(z + b1) -> LDS; lanes a < A compute adv_a, lane A the value;
+// A workgroup stages the head weights (A+1)x128 in LDS once and walks 16 rows (4 per
+// wave): h = relu(z + b1) -> LDS; lane a < A computes adv_a, lane A the value;
 // q = V + A - mean(A) (model.py:60-68).  h is kept (fp32) for the backward.
+constexpr int kHeadRows = 16;
+
 __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, const float* __restrict__ b_adv1,
                                                    const float* __restrict__ b_val1, const float* __restrict__ w_adv2,
                                                    const float* __restrict__ b_adv2, const float* __restrict__ w_val2,
                                                    const float* __restrict__ b_val2, float* __restrict__ hout,
                                                    float* __restrict__ q, int B, int A) {
+  __shared__ float ws[64 * 129];  // row a (a < A: adv, a == A: value), padded to break bank conflicts
   __shared__ float hs[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + wave;
-  const bool valid = b < B;  // no early return: every wave reaches the barrier
-  const float* zr = z + (size_t)(valid ? b : 0) * 256;
+  for (int e = threadIdx.x; e < (A + 1) * 128; e += 256) {
+    const int a = e / 128, j = e % 128;
+    ws[a * 129 + j] = a < A ? w_adv2[a * 128 + j] : w_val2[j];
+  }
+  const float bo = lane < A ? b_adv2[lane] : (lane == A ? b_val2[0] : 0.f);
+  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
+    const int b = blockIdx.x * kHeadRows + rr * 4 + wave;
+    const bool valid = b < B;
+    const float* zr = z + (size_t)(valid ? b : 0) * 256;
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int j = lane + 64 * k;
-    const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
-    const float v = fmaxf(zr[j] + bias, 0.f);
-    hs[wave][j] = v;
-    if (hout && valid) hout[(size_t)b * 256 + j] = v;
+    for (int k = 0; k < 4; ++k) {
+      const int j = lane + 64 * k;
+      const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
+      const float v = fmaxf(zr[j] + bias, 0.f);
+      hs[wave][j] = v;
+      if (hout && valid) hout[(size_t)b * 256 + j] = v;
+    }
+    __syncthreads();
+    float o = 0.f;
+    if (lane <= A) {
+      const float* wr = ws + lane * 129;
+      const float* hr = hs[wave] + (lane < A ? 0 : 128);
+#pragma unroll 8
+      for (int j = 0; j < 128; ++j) o += hr[j] * wr[j];
+      o += bo;
+    }
+    const float adv_sum = wave_sum(lane < A ? o : 0.f);
+    const float v = __shfl(o, A, 64);
+    if (valid && lane < A) q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
   }
-  __syncthreads();
-  if (!valid) return;
-  float o = 0.f;
-  if (lane < A) {
-    const float* wr = w_adv2 + lane * 128;
-    for (int j = 0; j < 128; ++j) o += hs[wave][j] * wr[j];
-    o += b_adv2[lane];
-  } else if (lane == A) {
-    for (int j = 0; j < 128; ++j) o += hs[wave][128 + j] * w_val2[j];
-    o += b_val2[0];
-  }
-  const float adv_sum = wave_sum(lane < A ? o : 0.f);
-  const float v = __shfl(o, A, 64);
-  if (lane < A) q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
 }
 
 void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
                const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s) {
   if (A < 1 || A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
-  heads_fwd_k<<<(B + 3) / 4, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout, q, B, A);
+  heads_fwd_k<<<(B + kHeadRows - 1) / kHeadRows, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout,
+                                                             q, B, A);
   LAUNCH_CHECK();
 }
 
@@ -267,6 +247,88 @@ void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float
   heads_bwd_k<<<(B + 3) / 4, 256, 0, s>>>(dq, h, w_adv2, w_val2, dA, dz, dz_bf, B, A);
   LAUNCH_CHECK();
 }
+
+// Head/FC1-bias gradients as one batch reduction (replaces 2 GEMMs + 4 sums):
+//   dW_adv2[a][j] = sum_b dadv[b][a] h[b][j]   dW_val2[j] = sum_b dv[b] h[b][128+j]
+//   db_adv2[a] = sum_b dadv[b][a]   db_val2 = sum_b dv[b]   db_fc1[n] = sum_b dz[b][n]
+// Stage 1: HG_SPLIT blocks x 256 threads (thread = hidden column j) over row slices ->
+// fp32 partials; stage 2 sums the partials in fixed order (deterministic).
+constexpr int HG_SPLIT = 16;
+constexpr int HG_MAXA = 32;
+
+__global__ __launch_bounds__(256) void heads_wgrad_partial_k(const float* __restrict__ dA, const float* __restrict__ h,
+                                                             const float* __restrict__ dz, int B, int A,
+                                                             float* __restrict__ part) {
+  __shared__ float da_s[64][HG_MAXA + 1];
+  const int j = threadIdx.x;
+  const int rows = (B + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows, r1 = min(B, r0 + rows);
+  float acc[HG_MAXA];
+#pragma unroll
+  for (int a = 0; a < HG_MAXA; ++a) acc[a] = 0.f;
+  float dsum = 0.f, bsum = 0.f;  // db_fc1[j]; bias of head output (threads j <= A)
+  for (int c0 = r0; c0 < r1; c0 += 64) {
+    const int cn = min(64, r1 - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < cn * (A + 1); e += 256) da_s[e / (A + 1)][e % (A + 1)] = dA[(size_t)(c0 + e / (A + 1)) * (A + 1) + e % (A + 1)];
+    __syncthreads();
+    for (int r = 0; r < cn; ++r) {
+      const float hj = h[(size_t)(c0 + r) * 256 + j];
+      dsum += dz[(size_t)(c0 + r) * 256 + j];
+      if (j <= A) bsum += da_s[r][j];
+      if (j < 128) {
+#pragma unroll
+        for (int a = 0; a < HG_MAXA; ++a)
+          if (a < A) acc[a] += da_s[r][a] * hj;
+      } else {
+        acc[0] += da_s[r][A] * hj;
+      }
+    }
+  }
+  // partial layout per block: [A][128] adv, [128] val, [A] db_adv2, [1] db_val2, [256] db_fc1
+  const int stride = (A + 1) * 128 + (A + 1) + 256;
+  float* p = part + (size_t)blockIdx.x * stride;
+  if (j < 128) {
+    for (int a = 0; a < A; ++a) p[a * 128 + j] = acc[a];
+  } else {
+    p[A * 128 + (j - 128)] = acc[0];
+  }
+  if (j <= A) p[(A + 1) * 128 + j] = bsum;
+  p[(A + 1) * 129 + j] = dsum;
+}
+
+__global__ void heads_wgrad_reduce_k(const float* __restrict__ part, int G, int A, float* __restrict__ g_wadv2,
+                                     float* __restrict__ g_badv2, float* __restrict__ g_wval2,
+                                     float* __restrict__ g_bval2, float* __restrict__ g_badv1,
+                                     float* __restrict__ g_bval1) {
+  const int stride = (A + 1) * 128 + (A + 1) + 256;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= stride) return;
+  float s = 0.f;
+  for (int g = 0; g < G; ++g) s += part[(size_t)g * stride + e];
+  if (e < A * 128) g_wadv2[e] = s;
+  else if (e < (A + 1) * 128) g_wval2[e - A * 128] = s;
+  else if (e < (A + 1) * 128 + A) g_badv2[e - (A + 1) * 128] = s;
+  else if (e < (A + 1) * 129) g_bval2[0] = s;
+  else {
+    const int n = e - (A + 1) * 129;
+    if (n < 128) g_badv1[n] = s; else g_bval1[n - 128] = s;
+  }
+}
+
+void heads_wgrad(const float* dA, const float* h, const float* dz, int B, int A, float* ws, float* g_wadv2,
+                 float* g_badv2, float* g_wval2, float* g_bval2, float* g_badv1, float* g_bval1, hipStream_t s) {
+  if (A < 1 || A > HG_MAXA) throw std::invalid_argument("heads_wgrad: 1 <= A <= 32");
+  const int G = std::min(HG_SPLIT, B);
+  heads_wgrad_partial_k<<<G, 256, 0, s>>>(dA, h, dz, B, A, ws);
+  LAUNCH_CHECK();
+  const int stride = (A + 1) * 128 + (A + 1) + 256;
+  heads_wgrad_reduce_k<<<(stride + 255) / 256, 256, 0, s>>>(ws, G, A, g_wadv2, g_badv2, g_wval2, g_bval2, g_badv1,
+                                                           g_bval1);
+  LAUNCH_CHECK();
+}
+
+size_t heads_wgrad_workspace_floats(int A) { return (size_t)HG_SPLIT * ((A + 1) * 128 + (A + 1) + 256); }
 
 // ------------------------------------------------------------------ packing / masks
 // conv weight fp32 [N][C][KH][KW] (reference layout) -> bf16 [N][KH][KW][C]

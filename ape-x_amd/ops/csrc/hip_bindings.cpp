@@ -46,21 +46,6 @@ TreeHandle make_tree(uint64_t leaf_sum, uint64_t leaf_min, const std::vector<uin
   return h;
 }
 
-struct SegHandle {
-  OptSegments s{};
-};
-SegHandle make_segments(const std::vector<int64_t>& offsets, const std::vector<int64_t>& numels) {
-  SegHandle h;
-  if (offsets.size() != numels.size() || offsets.size() > 64 || offsets.empty())
-    throw std::invalid_argument("segments: 1..64 tensors");
-  h.s.n = (int)offsets.size();
-  for (size_t i = 0; i < offsets.size(); ++i) {
-    h.s.offset[i] = offsets[i];
-    h.s.numel[i] = numels[i];
-  }
-  return h;
-}
-
 struct NStepHandle {
   NStepParams p{};
   NStepState st{};
@@ -77,16 +62,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     return h.d.levels;
   });
   m.def("make_tree", &make_tree);
-  py::class_<SegHandle>(m, "SegHandle").def_property_readonly("n", [](const SegHandle& h) { return h.s.n; });
-  m.def("make_segments", &make_segments);
 
   // ---- replay
   m.def("per_write_leaves", [](const TreeHandle& t, uint64_t idx, uint64_t prio, int B, float alpha,
-                               uint64_t max_prio, int dedup, uint64_t s) {
-    per_write_leaves(t.d, P<const int>(idx), P<const float>(prio), B, alpha, P<float>(max_prio), dedup, S(s));
-  });
-  m.def("per_update_levels", [](const TreeHandle& t, uint64_t idx, int B, uint64_t s) {
-    per_update_levels(t.d, P<const int>(idx), B, S(s));
+                               uint64_t max_prio, int dedup, uint64_t sorted_scratch, uint64_t bump0, int64_t d0,
+                               uint64_t bump1, int64_t d1, uint64_t s) {
+    per_write_leaves(t.d, P<const int>(idx), P<const float>(prio), B, alpha, P<float>(max_prio), dedup,
+                     P<int>(sorted_scratch), P<int64_t>(bump0), d0, P<int64_t>(bump1), d1, S(s));
   });
   m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
@@ -99,7 +81,7 @@ PYBIND11_MODULE(_apex_hip, m) {
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {
     gather_transitions(P<const uint8_t>(frames), frame_bytes, P<const int>(s_ids), P<const int>(s2_ids),
                        P<const int>(act), P<const float>(rew), P<const float>(done), P<const int>(idx), B,
-                       P<uint8_t>(out_s), P<uint8_t>(out_s2), P<int64_t>(out_a), P<float>(out_r), P<float>(out_d),
+                       P<uint8_t>(out_s), P<uint8_t>(out_s2), P<int>(out_a), P<float>(out_r), P<float>(out_d),
                        S(s));
   });
   m.def("gather_frames", [](uint64_t frames, int frame_bytes, uint64_t ids, int N, int stack, uint64_t out,
@@ -168,14 +150,16 @@ PYBIND11_MODULE(_apex_hip, m) {
 
   // ---- learner
   m.def("dqn_loss", [](uint64_t q, uint64_t q2, uint64_t q2t, int ldq, uint64_t a, uint64_t r, uint64_t d,
-                       uint64_t w, int B, int A, float gamma_n, uint64_t loss, uint64_t dq, uint64_t prio,
-                       uint64_t s) {
-    dqn_loss(P<const float>(q), P<const float>(q2), P<const float>(q2t), ldq, P<const int64_t>(a), P<const float>(r),
-             P<const float>(d), P<const float>(w), B, A, gamma_n, P<float>(loss), P<float>(dq), P<float>(prio), S(s));
+                       uint64_t idx, uint64_t w, int B, int A, float gamma_n, uint64_t loss, uint64_t dq,
+                       uint64_t prio, uint64_t s) {
+    dqn_loss(P<const float>(q), P<const float>(q2), P<const float>(q2t), ldq, P<const int>(a), P<const float>(r),
+             P<const float>(d), P<const int>(idx), P<const float>(w), B, A, gamma_n, P<float>(loss), P<float>(dq),
+             P<float>(prio), S(s));
   });
-  m.def("grad_sumsq", [](uint64_t g, const SegHandle& seg, uint64_t partials, int bps, uint64_t s) {
-    grad_sumsq(P<const float>(g), seg.s, P<double>(partials), bps, S(s));
+  m.def("grad_sumsq", [](uint64_t g, int64_t n, uint64_t partials, uint64_t s) {
+    grad_sumsq(P<const float>(g), n, P<double>(partials), S(s));
   });
+  m.def("grad_norm_partials", &grad_norm_partials);
   py::class_<RMSpropParams>(m, "RMSpropParams")
       .def(py::init([](float lr, float alpha, float eps, float max_norm, float lr_gamma, int lr_step_size,
                        int lr_step_offset, bool centered) {
@@ -185,10 +169,9 @@ PYBIND11_MODULE(_apex_hip, m) {
            py::arg("lr_gamma") = 1.f, py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0,
            py::arg("centered") = false);
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
-                           int n_partials, const SegHandle& seg, int bps, const RMSpropParams& hp, uint64_t step,
-                           uint64_t norms, uint64_t s) {
+                           int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s) {
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
-                 n_partials, seg.s, bps, hp, P<const int64_t>(step), P<float>(norms), S(s));
+                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s));
   });
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
@@ -199,15 +182,22 @@ PYBIND11_MODULE(_apex_hip, m) {
            py::arg("weight_decay") = 0.f, py::arg("max_norm") = 0.f, py::arg("lr_gamma") = 1.f,
            py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0);
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
-                        int n_partials, const SegHandle& seg, int bps, const AdamParams& hp, uint64_t step,
-                        uint64_t norms, uint64_t s) {
+                        int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s) {
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
-              seg.s, bps, hp, P<const int64_t>(step), P<float>(norms), S(s));
+              hp, P<const int64_t>(step), P<float>(norms), S(s));
   });
   // ---- network kernels
-  m.def("conv_fwd", [](int layer, uint64_t in, uint64_t wp, uint64_t bias, uint64_t out, int B, uint64_t s) {
-    conv_fwd(layer, P<const void>(in), P<const uint16_t>(wp), P<const float>(bias), P<uint16_t>(out), B, S(s));
+  m.def("conv_fwd", [](int layer, uint64_t in, uint64_t ids, uint64_t idx, uint64_t wp, uint64_t bias, uint64_t out,
+                       int B, uint64_t s) {
+    conv_fwd(layer, P<const void>(in), P<const int>(ids), P<const int>(idx), P<const uint16_t>(wp),
+             P<const float>(bias), P<uint16_t>(out), B, S(s));
   });
+  m.def("heads_wgrad", [](uint64_t dA, uint64_t h, uint64_t dz, int B, int A, uint64_t ws, uint64_t gwa, uint64_t gba,
+                          uint64_t gwv, uint64_t gbv, uint64_t gba1, uint64_t gbv1, uint64_t s) {
+    heads_wgrad(P<const float>(dA), P<const float>(h), P<const float>(dz), B, A, P<float>(ws), P<float>(gwa),
+                P<float>(gba), P<float>(gwv), P<float>(gbv), P<float>(gba1), P<float>(gbv1), S(s));
+  });
+  m.def("heads_wgrad_workspace_floats", &heads_wgrad_workspace_floats);
   m.def("heads_fwd", [](uint64_t z, uint64_t ba1, uint64_t bv1, uint64_t wa2, uint64_t ba2, uint64_t wv2, uint64_t bv2,
                         uint64_t hout, uint64_t q, int B, int A, uint64_t s) {
     heads_fwd(P<const float>(z), P<const float>(ba1), P<const float>(bv1), P<const float>(wa2), P<const float>(ba2),
@@ -237,9 +227,10 @@ PYBIND11_MODULE(_apex_hip, m) {
     conv_dgrad(layer, P<const uint16_t>(dy), P<const uint16_t>(wt), P<const uint16_t>(act), P<uint16_t>(out), B, S(s));
   });
   m.def("wgrad_workspace_floats", &wgrad_workspace_floats);
-  m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t dy, int B, uint64_t ws, uint64_t grad, uint64_t bgrad,
-                         uint64_t s) {
-    conv_wgrad(layer, P<const void>(x), P<const uint16_t>(dy), B, P<float>(ws), P<float>(grad), P<float>(bgrad), S(s));
+  m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, int B, uint64_t ws,
+                         uint64_t grad, uint64_t bgrad, uint64_t s) {
+    conv_wgrad(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const uint16_t>(dy), B, P<float>(ws),
+               P<float>(grad), P<float>(bgrad), S(s));
   });
   m.def("pack_conv_wt", [](uint64_t src, uint64_t dst, int N, int C, int KH, int KW, uint64_t s) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));

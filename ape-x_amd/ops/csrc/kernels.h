@@ -26,8 +26,13 @@ struct TreeDesc {
 };
 
 // ---- replay_kernels.hip
+// Write prio**alpha into the leaves of `idx` AND recompute every dirty ancestor.
+// dedup = 1: duplicates resolve last-write-wins (B <= 1024, needs `sorted_scratch` [B]);
+// dedup = 0: `idx` must be unique ring-ordered slots (actor inserts).
+// bump0/bump1: optional device counters advanced by d0/d1 (fused counter updates).
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
-                      int dedup, hipStream_t s);
+                      int dedup, int* sorted_scratch, int64_t* bump0, int64_t d0, int64_t* bump1, int64_t d1,
+                      hipStream_t s);
 void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 // length/beta are read from device memory when the pointers are non-null (so a captured
 // graph sees the live replay fill level and annealed beta), else the constants are used.
@@ -36,7 +41,7 @@ void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t len
                 int exclude_last, hipStream_t s);
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
-                        uint8_t* out_s2, int64_t* out_a, float* out_r, float* out_d, hipStream_t s);
+                        uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s);
 void gather_frames(const uint8_t* frames, int frame_bytes, const int* ids, int N, int stack, uint8_t* out,
                    hipStream_t s);
 void bump_counter(int64_t* counter, int n, int64_t by, hipStream_t s);
@@ -90,15 +95,12 @@ void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float*
                 int* slot_out, float* prio_out, hipStream_t s);
 
 // ---- learner_kernels.hip
-void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int64_t* a, const float* r,
-              const float* d, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
+// (a, r, d) are read through idx (the sampled replay slots) when idx != nullptr.
+void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int* a, const float* r, const float* d,
+              const int* idx, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
               hipStream_t s);
-struct OptSegments {
-  int n;                 // number of parameter tensors (<= 64)
-  int64_t offset[64];
-  int64_t numel[64];
-};
-void grad_sumsq(const float* g, const OptSegments& seg, double* partials, int blocks_per_seg, hipStream_t s);
+void grad_sumsq(const float* g, int64_t n, double* partials, hipStream_t s);
+int grad_norm_partials();
 struct RMSpropParams {
   float lr0, alpha, eps, max_norm;
   float lr_gamma;        // StepLR gamma (1 = constant)
@@ -107,20 +109,23 @@ struct RMSpropParams {
   int centered;
 };
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
-                  int n_partials, const OptSegments& seg, int blocks_per_seg, const RMSpropParams& hp,
-                  const int64_t* step, float* norms_out, hipStream_t s);
+                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s);
 struct AdamParams {
   float lr0, beta1, beta2, eps, weight_decay, max_norm;
   float lr_gamma;
   int lr_step_size, lr_step_offset;
 };
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
-               const OptSegments& seg, int blocks_per_seg, const AdamParams& hp, const int64_t* step,
-               float* norms_out, hipStream_t s);
+               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s);
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
 
 // ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)
-void conv_fwd(int layer, const void* in, const uint16_t* wp, const float* bias, uint16_t* out, int B, hipStream_t s);
+// layer 1: `in` is the u8 frame ring (ids/idx: FrameSrc, see common.h) or a dense u8 stack
+void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const uint16_t* wp, const float* bias,
+              uint16_t* out, int B, hipStream_t s);
+void heads_wgrad(const float* dA, const float* h, const float* dz, int B, int A, float* ws, float* g_wadv2,
+                 float* g_badv2, float* g_wval2, float* g_bval2, float* g_badv1, float* g_bval1, hipStream_t s);
+size_t heads_wgrad_workspace_floats(int A);
 void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
                const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s);
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
@@ -135,8 +140,8 @@ void u8_to_bf16_nhwc(const uint8_t* in, uint16_t* out, int B, int HW, hipStream_
 void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* wt, const uint16_t* act_below, uint16_t* dy_below,
                 int B, hipStream_t s);
 size_t wgrad_workspace_floats(int layer);
-void conv_wgrad(int layer, const void* x, const uint16_t* dy, int B, float* workspace, float* grad, float* bias_grad,
-                hipStream_t s);
+void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const uint16_t* dy, int B, float* workspace,
+                float* grad, float* bias_grad, hipStream_t s);
 void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
 
 }  // namespace apex

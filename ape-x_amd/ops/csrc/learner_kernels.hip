@@ -37,9 +37,10 @@ __device__ __forceinline__ float block_max_f(float v, float* smem) {
 
 // ------------------------------------------------------------------ loss
 __global__ void dqn_loss_k(const float* __restrict__ q, const float* __restrict__ q2, const float* __restrict__ q2t,
-                           int ldq, const int64_t* __restrict__ act, const float* __restrict__ rew,
-                           const float* __restrict__ done, const float* __restrict__ w, int B, int A, float gamma_n,
-                           float* __restrict__ loss_out, float* __restrict__ dq, float* __restrict__ prio) {
+                           int ldq, const int* __restrict__ act, const float* __restrict__ rew,
+                           const float* __restrict__ done, const int* __restrict__ idx, const float* __restrict__ w,
+                           int B, int A, float gamma_n, float* __restrict__ loss_out, float* __restrict__ dq,
+                           float* __restrict__ prio) {
   __shared__ float red[16];
   const int b = threadIdx.x;
   float delta = 0.f, lw = 0.f, g = 0.f;
@@ -48,12 +49,13 @@ __global__ void dqn_loss_k(const float* __restrict__ q, const float* __restrict_
     const float* qr = q + (size_t)b * ldq;
     const float* q2r = q2 + (size_t)b * ldq;
     const float* q2tr = q2t + (size_t)b * ldq;
-    a = (int)act[b];
+    const int row = idx ? idx[b] : b;  // read (a, r, d) straight from the replay's transition table
+    a = act[row];
     int astar = 0;
     float best = q2r[0];
     for (int k = 1; k < A; ++k)
       if (q2r[k] > best) { best = q2r[k]; astar = k; }
-    const float y = rew[b] + gamma_n * q2tr[astar] * (1.f - done[b]);
+    const float y = rew[row] + gamma_n * q2tr[astar] * (1.f - done[row]);
     const float qa = qr[a];
     delta = fabsf(y - qa);
     const float h = delta < 1.f ? 0.5f * delta * delta : delta - 0.5f;
@@ -70,62 +72,61 @@ __global__ void dqn_loss_k(const float* __restrict__ q, const float* __restrict_
   if (b == 0) loss_out[0] = total / (float)B;
 }
 
-void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int64_t* a, const float* r,
-              const float* d, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
+void dqn_loss(const float* q, const float* q2, const float* q2t, int ldq, const int* a, const float* r, const float* d,
+              const int* idx, const float* w, int B, int A, float gamma_n, float* loss_out, float* dq, float* prio,
               hipStream_t s) {
   if (B < 1 || B > 1024) throw std::invalid_argument("dqn_loss: batch must be in [1, 1024]");
   const int threads = ((B + 63) / 64) * 64;
-  dqn_loss_k<<<1, threads, 0, s>>>(q, q2, q2t, ldq, a, r, d, w, B, A, gamma_n, loss_out, dq, prio);
+  dqn_loss_k<<<1, threads, 0, s>>>(q, q2, q2t, ldq, a, r, d, idx, w, B, A, gamma_n, loss_out, dq, prio);
   LAUNCH_CHECK();
 }
 
 // ------------------------------------------------------------------ grad norm partials
-__global__ void grad_sumsq_k(const float* __restrict__ g, OptSegments seg, double* __restrict__ partials) {
-  __shared__ double red[16];
-  const int sidx = blockIdx.y;
-  const int64_t off = seg.offset[sidx], n = seg.numel[sidx];
+// kNormBlocks blocks cover the flat gradient in contiguous chunks (all CUs busy no matter
+// how the parameters are split into tensors); each writes one fp64 partial.
+constexpr int kNormBlocks = 256;
+
+__global__ void grad_sumsq_k(const float* __restrict__ g, int64_t n, double* __restrict__ partials) {
+  __shared__ double red[4];
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = blockIdx.x * chunk, hi = min(n, lo + chunk);
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float v = g[off + i];
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const float v = g[i];
     acc += (double)v * (double)v;
   }
   acc = wave_sum(acc);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (lane == 0) red[wid] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double t = 0.0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
-    partials[sidx * gridDim.x + blockIdx.x] = t;
-  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-void grad_sumsq(const float* g, const OptSegments& seg, double* partials, int blocks_per_seg, hipStream_t s) {
-  grad_sumsq_k<<<dim3(blocks_per_seg, seg.n), 256, 0, s>>>(g, seg, partials);
+void grad_sumsq(const float* g, int64_t n, double* partials, hipStream_t s) {
+  grad_sumsq_k<<<kNormBlocks, 256, 0, s>>>(g, n, partials);
   LAUNCH_CHECK();
 }
 
-// Every update block re-reduces the partials in the same fixed order.
+int grad_norm_partials() { return kNormBlocks; }
+
+// Every update block re-reduces the partials in the same fixed order (deterministic,
+// identical in all blocks).  The reference's per-tensor 'grad_norm' log value is computed
+// on demand on the host side (DQNLearner.stats), not on every step.
 struct NormInfo {
-  float clip, l2, ref;
+  float clip, l2;
 };
-__device__ NormInfo reduce_norms(const double* partials, int n_partials, const OptSegments& seg, int bps,
-                                 float max_norm) {
-  __shared__ double segsum[64];
-  for (int sidx = threadIdx.x; sidx < seg.n; sidx += blockDim.x) {
-    double t = 0.0;
-    for (int k = 0; k < bps; ++k) t += partials[sidx * bps + k];
-    segsum[sidx] = t;
-  }
+__device__ NormInfo reduce_norms(const double* partials, int n_partials, float max_norm) {
+  __shared__ double red[256];
+  double t = 0.0;
+  for (int k = threadIdx.x; k < n_partials; k += blockDim.x) t += partials[k];
+  red[threadIdx.x] = t;
   __syncthreads();
-  double total = 0.0, ref = 0.0;
-  for (int sidx = 0; sidx < seg.n; ++sidx) {
-    total += segsum[sidx];
-    ref += sqrt(sqrt(segsum[sidx]));  // ||g_p||^(1/2)
+  for (int off = blockDim.x >> 1; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
   }
   NormInfo ni;
-  ni.l2 = (float)sqrt(total);
-  ni.ref = (float)sqrt(ref);
+  ni.l2 = (float)sqrt(red[0]);
   const float coef = max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f;
   ni.clip = fminf(coef, 1.f);
   return ni;
@@ -137,16 +138,16 @@ __device__ __forceinline__ float step_lr(float lr0, float gamma, int step_size, 
   return lr0 * powf(gamma, (float)k);
 }
 
-__global__ void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ sq,
-                               float* __restrict__ gavg, int64_t n, const double* __restrict__ partials,
-                               int n_partials, OptSegments seg, int bps, RMSpropParams hp,
-                               const int64_t* __restrict__ step, float* __restrict__ norms_out) {
-  const NormInfo ni = reduce_norms(partials, n_partials, seg, bps, hp.max_norm);
+__global__ __launch_bounds__(256) void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ g,
+                                                      float* __restrict__ sq, float* __restrict__ gavg, int64_t n,
+                                                      const double* __restrict__ partials, int n_partials,
+                                                      RMSpropParams hp, const int64_t* __restrict__ step,
+                                                      float* __restrict__ norms_out) {
+  const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
   const int64_t st = step ? step[0] : 0;
   const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
   if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
     norms_out[0] = ni.l2;
-    norms_out[1] = ni.ref;
     norms_out[2] = ni.clip;
     norms_out[3] = lr;
   }
@@ -169,19 +170,17 @@ __global__ void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ 
 }
 
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
-                  int n_partials, const OptSegments& seg, int blocks_per_seg, const RMSpropParams& hp,
-                  const int64_t* step, float* norms_out, hipStream_t s) {
+                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, seg, blocks_per_seg, hp, step,
-                                         norms_out);
+  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out);
   LAUNCH_CHECK();
 }
 
-__global__ void adam_step_k(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, const double* __restrict__ partials, int n_partials,
-                            OptSegments seg, int bps, AdamParams hp, const int64_t* __restrict__ step,
-                            float* __restrict__ norms_out) {
-  const NormInfo ni = reduce_norms(partials, n_partials, seg, bps, hp.max_norm);
+__global__ __launch_bounds__(256) void adam_step_k(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                   const double* __restrict__ partials, int n_partials, AdamParams hp,
+                                                   const int64_t* __restrict__ step, float* __restrict__ norms_out) {
+  const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
   const int64_t st = step ? step[0] : 0;
   const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
   const float t = (float)(st + 1);
@@ -189,7 +188,6 @@ __global__ void adam_step_k(float* __restrict__ p, const float* __restrict__ g, 
   const float step_size = lr / bc1, rbc2 = 1.f / sqrtf(bc2);
   if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
     norms_out[0] = ni.l2;
-    norms_out[1] = ni.ref;
     norms_out[2] = ni.clip;
     norms_out[3] = lr;
   }
@@ -206,11 +204,9 @@ __global__ void adam_step_k(float* __restrict__ p, const float* __restrict__ g, 
 }
 
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
-               const OptSegments& seg, int blocks_per_seg, const AdamParams& hp, const int64_t* step,
-               float* norms_out, hipStream_t s) {
+               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, seg, blocks_per_seg, hp, step,
-                                      norms_out);
+  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, hp, step, norms_out);
   LAUNCH_CHECK();
 }
 

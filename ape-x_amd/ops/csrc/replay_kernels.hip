@@ -18,27 +18,76 @@
 namespace apex {
 
 // ------------------------------------------------------------------ leaf writes
-// The batch's indices are staged in LDS so the last-write-wins scan (memory.py:313-320
-// applies updates sequentially) reads LDS, not L2 (B <= kStageMax; larger batches must
-// be unique, e.g. actor slots, and run with dedup = 0).
-constexpr int kStageMax = 4096;
+// Learner updates (dedup = 1, B <= 1024): one workgroup bitonic-sorts the (slot, position)
+// pairs in LDS; the last position of every run of equal slots wins (the reference applies
+// updates sequentially, memory.py:313-320), and the sorted slot list is written out so the
+// level kernels dedup parents by comparing with their predecessor (O(1)).
+// Actor inserts (dedup = 0) are unique, already ordered ring slots.
+// `bump*` are device counters advanced by this kernel (it never reads them), which saves
+// a separate counter launch per step.
+constexpr int kSortMax = 1024;
+
+__global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, const int* __restrict__ idx,
+                                                                  const float* __restrict__ prio, int B, float alpha,
+                                                                  float* max_prio, int* __restrict__ sorted_out,
+                                                                  int64_t* bump0, int64_t d0, int64_t* bump1,
+                                                                  int64_t d1) {
+  __shared__ unsigned long long key[kSortMax];
+  int n = 1;
+  while (n < B) n <<= 1;
+  for (int k = threadIdx.x; k < n; k += blockDim.x)
+    key[k] = k < B ? (((unsigned long long)(unsigned)idx[k]) << 32) | (unsigned)k : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const int o = k ^ stride;
+        if (o > k) {
+          const bool up = (k & size) == 0;
+          const unsigned long long a = key[k], b = key[o];
+          if ((a > b) == up) {
+            key[k] = b;
+            key[o] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int k = threadIdx.x; k < B; k += blockDim.x) {
+    const int id = (int)(key[k] >> 32);
+    sorted_out[k] = id;
+    const bool last = (k == B - 1) || ((int)(key[k + 1] >> 32) != id);
+    if (!last || id < 0 || id >= t.size[0]) continue;
+    const float p = prio ? prio[(int)(key[k] & 0xFFFFFFFFu)] : *max_prio;
+    if (p > 0.f && isfinite(p)) {
+      const float v = powf(p, alpha);
+      t.leaf_sum[id] = v;
+      t.leaf_min[id] = v;
+      if (prio) atomic_max_pos_float(max_prio, p);
+    } else {
+      t.leaf_sum[id] = 0.f;
+      t.leaf_min[id] = INFINITY;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (bump0) *bump0 += d0;
+    if (bump1) *bump1 += d1;
+  }
+}
 
 __global__ void per_write_leaves_k(TreeDesc t, const int* __restrict__ idx, const float* __restrict__ prio, int B,
-                                   float alpha, float* max_prio, int dedup) {
-  __shared__ int sidx[kStageMax];
-  if (dedup) {
-    for (int j = threadIdx.x; j < B; j += blockDim.x) sidx[j] = idx[j];
-    __syncthreads();
-  }
+                                   float alpha, float* max_prio, int64_t* bump0, int64_t d0, int64_t* bump1,
+                                   int64_t d1) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    if (bump0) *bump0 += d0;
+    if (bump1) *bump1 += d1;
+  }
   if (i >= B) return;
   const int id = idx[i];
   if (id < 0 || id >= t.size[0]) return;
-  if (dedup) {
-    for (int j = i + 1; j < B; ++j)
-      if (sidx[j] == id) return;
-  }
-  float p = prio ? prio[i] : *max_prio;
+  const float p = prio ? prio[i] : *max_prio;
   if (p > 0.f && isfinite(p)) {
     const float v = powf(p, alpha);
     t.leaf_sum[id] = v;
@@ -51,29 +100,19 @@ __global__ void per_write_leaves_k(TreeDesc t, const int* __restrict__ idx, cons
 }
 
 // ------------------------------------------------------------------ level recompute
-// One wave per update; a wave whose parent was already claimed by an earlier update
-// exits, so each dirty node is recomputed exactly once per level.  The earlier
-// updates' indices are scanned from an LDS copy (64 per ballot).
-__global__ void per_update_level_k(TreeDesc t, const int* __restrict__ idx, int B, int level) {
-  __shared__ int sidx[kStageMax];
+// One wave per (sorted or ring-ordered) slot; children of a node are a contiguous id
+// range, so equal parents form runs and only the first of a run recomputes the node.
+__global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int B, int level) {
   const int lane = threadIdx.x & 63;
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int wmax = min(B, (int)((blockIdx.x + 1) * blockDim.x) >> 6);
-  const bool staged = B <= kStageMax;
-  if (staged) {
-    for (int j = threadIdx.x; j < wmax; j += blockDim.x) sidx[j] = idx[j];
-    __syncthreads();
-  }
   if (w >= B) return;
-  const int id = idx[w];
+  const int id = ids[w];
   if (id < 0 || id >= t.size[0]) return;
   const int shift = kTreeLog2Fanout * level;
   const int node = id >> shift;
-  for (int j0 = 0; j0 < w; j0 += 64) {
-    const int j = j0 + lane;
-    const int other = (j < w) ? (staged ? sidx[j] : idx[j]) : -1;
-    const bool dup = other >= 0 && other < t.size[0] && (other >> shift) == node;
-    if (__ballot(dup)) return;  // wave-uniform
+  if (w > 0) {
+    const int prev = ids[w - 1];
+    if (prev >= 0 && prev < t.size[0] && (prev >> shift) == node) return;  // wave-uniform
   }
   const int child = node * kTreeFanout + lane;
   const int csize = t.size[level - 1];
@@ -154,7 +193,7 @@ __global__ void gather_transitions_k(const uint8_t* __restrict__ frames, int fra
                                      const int* __restrict__ act, const float* __restrict__ rew,
                                      const float* __restrict__ done, const int* __restrict__ idx,
                                      uint8_t* __restrict__ out_s, uint8_t* __restrict__ out_s2,
-                                     int64_t* __restrict__ out_a, float* __restrict__ out_r,
+                                     int* __restrict__ out_a, float* __restrict__ out_r,
                                      float* __restrict__ out_d) {
   const int b = blockIdx.x;
   const int which = blockIdx.y;  // 0..3: s frames, 4..7: s' frames
@@ -189,11 +228,21 @@ __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
 
 // ------------------------------------------------------------------ launchers
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
-                      int dedup, hipStream_t s) {
+                      int dedup, int* sorted_scratch, int64_t* bump0, int64_t d0, int64_t* bump1, int64_t d1,
+                      hipStream_t s) {
   if (B <= 0) return;
-  if (dedup && B > kStageMax) throw std::invalid_argument("per_write_leaves: dedup batch too large");
-  per_write_leaves_k<<<(B + 255) / 256, 256, 0, s>>>(t, idx, prio, B, alpha, max_prio, dedup);
-  LAUNCH_CHECK();
+  if (dedup) {
+    if (B > kSortMax) throw std::invalid_argument("per_write_leaves: dedup batch must be <= 1024");
+    if (!sorted_scratch) throw std::invalid_argument("per_write_leaves: dedup needs a sorted scratch buffer");
+    per_write_leaves_sorted_k<<<1, 1024, 0, s>>>(t, idx, prio, B, alpha, max_prio, sorted_scratch, bump0, d0, bump1,
+                                                  d1);
+    LAUNCH_CHECK();
+    per_update_levels(t, sorted_scratch, B, s);
+  } else {
+    per_write_leaves_k<<<(B + 255) / 256, 256, 0, s>>>(t, idx, prio, B, alpha, max_prio, bump0, d0, bump1, d1);
+    LAUNCH_CHECK();
+    per_update_levels(t, idx, B, s);
+  }
 }
 
 void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) {
@@ -218,7 +267,7 @@ void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t len
 
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
-                        uint8_t* out_s2, int64_t* out_a, float* out_r, float* out_d, hipStream_t s) {
+                        uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s) {
   if (B <= 0) return;
   if (frame_bytes % 16) throw std::invalid_argument("frame_bytes must be a multiple of 16");
   gather_transitions_k<<<dim3(B, 8), 256, 0, s>>>(frames, frame_bytes, s_ids, s2_ids, act, rew, done, idx, out_s,

@@ -150,7 +150,7 @@ def test_wgrad_kernel_matches_torch(cuda, layer):
     ws = torch.empty(hip.wgrad_workspace_floats(layer), device=cuda)
     gw = torch.empty(N, C, KS, KS, device=cuda)
     gb = torch.empty(N, device=cuda)
-    hip.conv_wgrad(layer, xptr, dy.data_ptr(), B, ws.data_ptr(), gw.data_ptr(), gb.data_ptr(),
+    hip.conv_wgrad(layer, xptr, 0, 0, dy.data_ptr(), B, ws.data_ptr(), gw.data_ptr(), gb.data_ptr(),
                    torch.cuda.current_stream().cuda_stream)
     dy_f = dy.float().permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x_f, (N, C, KS, KS), dy_f, stride=S)
@@ -179,3 +179,20 @@ def test_dgrad_kernel_matches_torch(cuda, layer):
     ref = torch.nn.grad.conv2d_input((B, C, H, H), _bf(w), dy.float().permute(0, 3, 1, 2), stride=S)
     ref = (ref.permute(0, 2, 3, 1) * (act.float() > 0)).to(torch.bfloat16).float()
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_frame_ring_input_matches_dense(cuda):
+    """conv1 reading stacks in place from the frame ring (ids + idx) == dense input."""
+    from apex_amd.models.fused import HipDuelingNet, NetWorkspace
+
+    m = _model(cuda, A=18, seed=3)
+    net = HipDuelingNet(m)
+    g = torch.Generator().manual_seed(0)
+    frames = torch.randint(0, 256, (50, 84 * 84), generator=g, dtype=torch.uint8).to(cuda)
+    table = torch.randint(0, 50, (30, 4), generator=g, dtype=torch.int32).to(cuda)
+    idx = torch.randint(0, 30, (12,), generator=g, dtype=torch.int32).to(cuda)
+    dense = frames[table[idx.long()].long()].view(12, 4, 84, 84).contiguous()
+    ws1, ws2 = NetWorkspace(12, 18, cuda), NetWorkspace(12, 18, cuda)
+    q1 = net(dense, ws1).clone()
+    q2 = net(frames, ws2, table, idx).clone()
+    assert torch.equal(q1, q2)

@@ -100,7 +100,7 @@ def test_gather_transitions(cuda):
     idx = torch.randint(0, 512, (64,), generator=g, dtype=torch.int32).to(cuda)
     s = torch.empty(64, 4, 84, 84, dtype=torch.uint8, device=cuda)
     s2 = torch.empty_like(s)
-    a = torch.empty(64, dtype=torch.int64, device=cuda)
+    a = torch.empty(64, dtype=torch.int32, device=cuda)
     r = torch.empty(64, device=cuda)
     d = torch.empty(64, device=cuda)
     rp.gather(idx, s, s2, a, r, d)
@@ -108,7 +108,7 @@ def test_gather_transitions(cuda):
     ref_s = rp.frames[rp.s_ids[il].long()].view(64, 4, 84, 84)
     ref_s2 = rp.frames[rp.s2_ids[il].long()].view(64, 4, 84, 84)
     assert torch.equal(s, ref_s) and torch.equal(s2, ref_s2)
-    assert torch.equal(a, rp.action[il].long())
+    assert torch.equal(a, rp.action[il])
     assert torch.equal(r, rp.reward[il]) and torch.equal(d, rp.done[il])
 
 
