@@ -138,22 +138,24 @@ __device__ __forceinline__ uint32_t pack_bf16x2_u8(uint32_t b0, uint32_t b1) {
   return (f0 >> 16) | (f1 & 0xFFFF0000u);
 }
 
-// 4 channel planes x 16 consecutive u8 pixels -> 16 pixels x 4 channels bf16 (128 B)
-__device__ __forceinline__ void u8x4planes_to_bf16_nhwc(const uint4 (&v)[4], uint4 (&o)[8]) {
-  const uint32_t* w[4] = {&v[0].x, &v[1].x, &v[2].x, &v[3].x};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {      // 4 words of 4 pixels each
-#pragma unroll
-    for (int bb = 0; bb < 4; bb += 2) {  // pixel pairs within the word
-      const int sh0 = 8 * bb, sh1 = 8 * (bb + 1);
-      uint4 q;
-      q.x = pack_bf16x2_u8((w[0][k] >> sh0) & 0xFF, (w[1][k] >> sh0) & 0xFF);
-      q.y = pack_bf16x2_u8((w[2][k] >> sh0) & 0xFF, (w[3][k] >> sh0) & 0xFF);
-      q.z = pack_bf16x2_u8((w[0][k] >> sh1) & 0xFF, (w[1][k] >> sh1) & 0xFF);
-      q.w = pack_bf16x2_u8((w[2][k] >> sh1) & 0xFF, (w[3][k] >> sh1) & 0xFF);
-      o[2 * k + bb / 2] = q;
-    }
-  }
+__device__ __forceinline__ uint32_t word_of(const uint4& v, int k) {
+  return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));  // k is a compile-time constant
+}
+
+// 4 channel planes x 4 consecutive u8 pixels (one 32-bit word each) -> 4 pixels x 4
+// channels bf16 = 32 bytes (two uint4), written straight to LDS.
+__device__ __forceinline__ void u8x4words_to_lds(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint4* d) {
+  uint4 a, b;
+  a.x = pack_bf16x2_u8(w0 & 0xFF, w1 & 0xFF);
+  a.y = pack_bf16x2_u8(w2 & 0xFF, w3 & 0xFF);
+  a.z = pack_bf16x2_u8((w0 >> 8) & 0xFF, (w1 >> 8) & 0xFF);
+  a.w = pack_bf16x2_u8((w2 >> 8) & 0xFF, (w3 >> 8) & 0xFF);
+  b.x = pack_bf16x2_u8((w0 >> 16) & 0xFF, (w1 >> 16) & 0xFF);
+  b.y = pack_bf16x2_u8((w2 >> 16) & 0xFF, (w3 >> 16) & 0xFF);
+  b.z = pack_bf16x2_u8(w0 >> 24, w1 >> 24);
+  b.w = pack_bf16x2_u8(w2 >> 24, w3 >> 24);
+  d[0] = a;
+  d[1] = b;
 }
 
 // Stage a 4-frame u8 stack (84x84) into LDS as NHWC bf16 with 8-byte pixels: every
@@ -162,44 +164,54 @@ template <int HW>
 __device__ __forceinline__ void stage_frames_bf16(const FrameSrc& f, int b, char* xs) {
   constexpr int GROUPS = HW / 16;                 // 16-pixel groups
   constexpr int PER = (GROUPS + 255) / 256;
-  const uint8_t* pl[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) pl[c] = frame_plane(f, b, c, HW);
-  uint4 v[PER][4];
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int g = threadIdx.x + 256 * k;
-    if (g < GROUPS)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[k][c] = reinterpret_cast<const uint4*>(pl[c])[g];
+  const uint8_t* const pl[4] = {frame_plane(f, b, 0, HW), frame_plane(f, b, 1, HW), frame_plane(f, b, 2, HW),
+                                frame_plane(f, b, 3, HW)};
+  static_assert(PER <= 2, "frame staging keeps <= 8 loads in flight per thread");
+  const int g0 = threadIdx.x, g1 = threadIdx.x + 256;
+  const bool ok1 = PER > 1 && g1 < GROUPS;
+  uint4 a0 = {}, a1 = {}, a2 = {}, a3 = {}, b0 = {}, b1 = {}, b2 = {}, b3 = {};
+  if (g0 < GROUPS) {
+    a0 = reinterpret_cast<const uint4*>(pl[0])[g0];
+    a1 = reinterpret_cast<const uint4*>(pl[1])[g0];
+    a2 = reinterpret_cast<const uint4*>(pl[2])[g0];
+    a3 = reinterpret_cast<const uint4*>(pl[3])[g0];
   }
+  if (ok1) {
+    b0 = reinterpret_cast<const uint4*>(pl[0])[g1];
+    b1 = reinterpret_cast<const uint4*>(pl[1])[g1];
+    b2 = reinterpret_cast<const uint4*>(pl[2])[g1];
+    b3 = reinterpret_cast<const uint4*>(pl[3])[g1];
+  }
+  if (g0 < GROUPS) {
+    uint4* d = reinterpret_cast<uint4*>(xs + g0 * 16 * 8);
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int g = threadIdx.x + 256 * k;
-    if (g < GROUPS) {
-      uint4 o[8];
-      u8x4planes_to_bf16_nhwc(v[k], o);
-      uint4* d = reinterpret_cast<uint4*>(xs + g * 16 * 8);
+    for (int k = 0; k < 4; ++k) u8x4words_to_lds(word_of(a0, k), word_of(a1, k), word_of(a2, k), word_of(a3, k), d + 2 * k);
+  }
+  if (ok1) {
+    uint4* d = reinterpret_cast<uint4*>(xs + g1 * 16 * 8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = o[j];
-    }
+    for (int k = 0; k < 4; ++k) u8x4words_to_lds(word_of(b0, k), word_of(b1, k), word_of(b2, k), word_of(b3, k), d + 2 * k);
   }
 }
 
-// Pipelined 16-byte copy global -> LDS of TOTAL chunks with a destination remap.
+// Pipelined 16-byte copy global -> LDS of TOTAL chunks with a destination remap: rounds
+// of 4 loads issued back to back before their LDS writes (bounded register footprint,
+// no private-memory arrays).
 template <int TOTAL, class DstOff>
 __device__ __forceinline__ void stage_chunks(const uint4* __restrict__ src, char* dst, DstOff dst_off) {
   constexpr int PER = (TOTAL + 255) / 256;
-  uint4 v[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (q < TOTAL) v[k] = src[q];
-  }
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (q < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q)) = v[k];
+  for (int k0 = 0; k0 < PER; k0 += 4) {
+    const int q0 = threadIdx.x + 256 * k0, q1 = q0 + 256, q2 = q0 + 512, q3 = q0 + 768;
+    uint4 v0 = {}, v1 = {}, v2 = {}, v3 = {};
+    if (q0 < TOTAL) v0 = src[q0];
+    if (k0 + 1 < PER && q1 < TOTAL) v1 = src[q1];
+    if (k0 + 2 < PER && q2 < TOTAL) v2 = src[q2];
+    if (k0 + 3 < PER && q3 < TOTAL) v3 = src[q3];
+    if (q0 < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q0)) = v0;
+    if (k0 + 1 < PER && q1 < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q1)) = v1;
+    if (k0 + 2 < PER && q2 < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q2)) = v2;
+    if (k0 + 3 < PER && q3 < TOTAL) *reinterpret_cast<uint4*>(dst + dst_off(q3)) = v3;
   }
 }
 
