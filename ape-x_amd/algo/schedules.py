@@ -28,3 +28,14 @@ def beta_by_frame(frame_idx: int, beta_start: float = 0.4, horizon: float = 1000
 
 def epsilon_by_frame(frame_idx: int, eps_start: float = 1.0, eps_final: float = 0.01, decay: float = 500.0) -> float:
     return eps_final + (eps_start - eps_final) * math.exp(-1.0 * frame_idx / decay)
+
+
+def step_scheduler_early(scheduler) -> None:
+    """``scheduler.step()`` before ``optimizer.step()`` (the reference decays
+    the LR one step early, ApeX.py:60-61 / DQN.py:71-73); torch's ordering warning is
+    expected here and silenced."""
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message="Detected call of `lr_scheduler.step()`")
+        scheduler.step()
