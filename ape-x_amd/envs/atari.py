@@ -301,10 +301,14 @@ class LazyFrames:
         self._out = None
 
     def _force(self):
+        # ``_frames`` is kept after forcing (unlike wrapper.py:230) so the role actors can
+        # ship each frame once (frame-id dedup, apex_amd.roles.common.FrameDedup)
         if self._out is None:
             self._out = np.concatenate(self._frames, axis=self._axis)
-            self._frames = None
         return self._out
+
+    def frames(self):
+        return self._frames
 
     def __array__(self, dtype=None, copy=None):
         out = self._force()
