@@ -14,7 +14,9 @@ steps.  Reference cadences are kept: params published to the actors every
 ``target_update_interval`` (learner.py:163, 2500), learning starts after
 ``threshold_size`` transitions (replay.py:104, 50,000).  In data-parallel mode (one
 rank per GPU, ``apex_amd.parallel``), the flat gradient is all-reduced over RCCL
-between the two learner graphs.
+between the two learner graphs, and with ``sharded=True`` the replay shards are
+sampled as one global prioritized buffer (``parallel.sharded``: shard masses are
+all-gathered before the learner graph).
 """
 from __future__ import annotations
 
@@ -54,7 +56,7 @@ class EngineConfig:
 
 class ApexEngine:
     def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", allreduce=None,
-                 model: DuelingDQN | None = None):
+                 model: DuelingDQN | None = None, sharded: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         lc = cfg.learner
@@ -64,7 +66,12 @@ class ApexEngine:
         self.actor = ActorShard(self.replay, cfg.n_envs, cfg.n_actions, lc.n_step, lc.gamma, cfg.eps_base,
                                 cfg.eps_alpha, cfg.actor_offset, cfg.total_actors, cfg.seed, cfg.nstep_mode)
         model = model if model is not None else DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions)
-        self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce)
+        self._sharded = None
+        if sharded:
+            from ..parallel.sharded import ShardedSampling
+
+            self._sharded = ShardedSampling(self.replay)
+        self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce, sharded=self._sharded)
         self.actor_model = copy.deepcopy(self.learner.model)
         self.actor_model._flat = None
         self.actor_flat = self.actor_model.flatten_parameters()
@@ -112,6 +119,8 @@ class ApexEngine:
         with torch.cuda.stream(s):
             for _ in range(warmup_iters):
                 self._actor_body()
+                if self._sharded is not None:
+                    self._sharded.exchange()
                 self._learn_a()
                 if self._allreduce is not None:
                     self._allreduce(self.learner.flat_grad)
@@ -139,6 +148,8 @@ class ApexEngine:
         self.actor_steps += 1
 
     def learner_step(self) -> None:
+        if self._sharded is not None:  # 16 B/rank all-gather of shard masses (eager collective)
+            self._sharded.exchange()
         if self._g_learn_a is not None:
             self._g_learn_a.replay()
             if self._allreduce is not None:

@@ -105,12 +105,16 @@ class HBMReplay:
     update_priorities = write_priorities
 
     def sample_indices(self, B: int, out_idx: torch.Tensor, out_w: torch.Tensor, counter: torch.Tensor,
-                       beta: float | torch.Tensor = 0.4, exclude_last: bool | None = None) -> None:
+                       beta: float | torch.Tensor = 0.4, exclude_last: bool | None = None,
+                       glob: torch.Tensor | None = None) -> None:
+        """``glob`` (sharded replay): f32 [2] device tensor = (global min priority, this
+        shard's IS-weight scale), see :mod:`apex_amd.parallel.sharded`."""
         excl = (not self.exact_mass) if exclude_last is None else exclude_last
         beta_ptr = beta.data_ptr() if isinstance(beta, torch.Tensor) else 0
         beta_c = 0.0 if isinstance(beta, torch.Tensor) else float(beta)
         self.hip.per_sample(self.tree, B, self.filled.data_ptr(), 0, beta_ptr, beta_c, self.seed, counter.data_ptr(),
-                            out_idx.data_ptr(), out_w.data_ptr(), int(excl), self._stream())
+                            out_idx.data_ptr(), out_w.data_ptr(), int(excl), self._stream(),
+                            0 if glob is None else glob.data_ptr())
 
     def gather(self, idx: torch.Tensor, out_s, out_s2, out_a, out_r, out_d) -> None:
         self.hip.gather_transitions(self.frames.data_ptr(), self.frame_bytes, self.s_ids.data_ptr(),

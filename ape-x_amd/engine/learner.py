@@ -63,7 +63,7 @@ def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = True) -> torch
 class DQNLearner:
     BLOCKS_PER_SEG = 16
 
-    def __init__(self, model: DuelingDQN, replay: HBMReplay, cfg: LearnerConfig, allreduce=None):
+    def __init__(self, model: DuelingDQN, replay: HBMReplay, cfg: LearnerConfig, allreduce=None, sharded=None):
         self.hip = ops.hip()
         self.cfg = cfg
         self.replay = replay
@@ -112,6 +112,7 @@ class DQNLearner:
         self.beta = torch.full((1,), cfg.beta, dtype=torch.float32, device=dev)
         self.gamma_n = float(cfg.gamma ** cfg.n_step)
         self.allreduce = allreduce  # callable(flat_grad) for data-parallel learners
+        self.sharded = sharded      # parallel.sharded.ShardedSampling (global PER over shards)
         self.host_steps = 0
         self.hip_net = cfg.forward == "hip"
         if self.hip_net:
@@ -130,7 +131,11 @@ class DQNLearner:
     def sample_and_forward(self) -> None:
         """Sample, gather, forward x3, loss, backward (grads in ``flat_grad``)."""
         s = self._stream()
-        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta)
+        glob = None
+        if self.sharded is not None:  # gathered shard masses -> global pmin + shard weight scale
+            self.sharded.finalize()
+            glob = self.sharded.glob
+        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.
@@ -174,6 +179,8 @@ class DQNLearner:
         self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 
     def step(self) -> None:
+        if self.sharded is not None:
+            self.sharded.exchange()
         self.sample_and_forward()
         if self.allreduce is not None:
             self.allreduce(self.flat_grad)

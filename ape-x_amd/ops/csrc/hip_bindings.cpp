@@ -72,10 +72,12 @@ PYBIND11_MODULE(_apex_hip, m) {
   });
   m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
-                         int exclude_last, uint64_t s) {
+                         int exclude_last, uint64_t s, uint64_t glob) {
     per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
-               P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, S(s));
-  });
+               P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s));
+  }, py::arg("t"), py::arg("B"), py::arg("length_ptr"), py::arg("length"), py::arg("beta_ptr"), py::arg("beta"),
+     py::arg("seed"), py::arg("counter"), py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"),
+     py::arg("s"), py::arg("glob") = 0);
   m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
                                  uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {

@@ -36,9 +36,11 @@ void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int 
 void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 // length/beta are read from device memory when the pointers are non-null (so a captured
 // graph sees the live replay fill level and annealed beta), else the constants are used.
+// ``glob`` (sharded replay, nullable): glob[0] = global min priority used for the IS
+// weights, glob[1] = this shard's weight scale (apex_amd.parallel.sharded).
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, hipStream_t s);
+                int exclude_last, const float* glob, hipStream_t s);
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
                         uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s);

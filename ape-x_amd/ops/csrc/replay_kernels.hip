@@ -142,7 +142,7 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
 __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64_t length_const,
                              const float* beta_ptr, float beta_const, uint64_t seed,
                              const int64_t* __restrict__ counter, int* __restrict__ out_idx,
-                             float* __restrict__ out_w, int exclude_last) {
+                             float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob) {
   const int lane = threadIdx.x & 63;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (i >= B) return;
@@ -178,9 +178,10 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
   }
   if (lane == 0) {
     const float p = t.leaf_sum[node];
-    const float pmin = t.node_min[L - 1][0];
+    const float pmin = glob ? glob[0] : t.node_min[L - 1][0];
+    const float wscale = glob ? glob[1] : 1.f;
     out_idx[i] = node;
-    out_w[i] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
+    out_w[i] = wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
   }
 }
 
@@ -257,11 +258,11 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) 
 
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, hipStream_t s) {
+                int exclude_last, const float* glob, hipStream_t s) {
   if (B <= 0) return;
   const int waves_per_block = 4;
   per_sample_k<<<(B + waves_per_block - 1) / waves_per_block, 64 * waves_per_block, 0, s>>>(
-      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last);
+      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob);
   LAUNCH_CHECK();
 }
 

@@ -10,8 +10,10 @@ and quotes 19 batches/s for the Ape-X paper (origin_repo/README.md:42).
 
 Every rank (one per GPU) runs an actor shard (``--envs`` GPU envs with the global
 Ape-X epsilon ladder), its HBM replay shard (``--capacity`` transitions) and a
-learner replica; learner replicas are data-parallel (flat-gradient RCCL all-reduce),
-so per-GPU work is fixed as N grows (weak scaling) and the global batch is 512*N.
+learner replica; learner replicas are data-parallel (flat-gradient RCCL all-reduce)
+and sample the shards as one global prioritized buffer (shard-mass all-gather,
+``apex_amd.parallel.sharded``), so per-GPU work is fixed as N grows (weak scaling)
+and the global batch is 512*N.
 One timed step = one learner SGD step (sample 512 -> 3 forwards -> backward ->
 clip -> RMSprop -> priority update) + ``--actor-steps`` actor steps of all envs.
 
@@ -47,6 +49,8 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
+    ap.add_argument("--local-sampling", action="store_true",
+                    help="N>1: sample each replay shard on its own (default: global PER over shards)")
     return ap.parse_args()
 
 
@@ -76,7 +80,8 @@ def main():
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
                        use_graphs=not args.no_graphs, seed=args.seed + 7919 * rank, learner=lc)
     allreduce = FlatGradAllReduce(world) if world > 1 else None
-    eng = ApexEngine(cfg, device, allreduce=allreduce)
+    sharded = world > 1 and not args.local_sampling
+    eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
         from apex_amd.parallel.broadcast import broadcast_flat
 
@@ -136,6 +141,7 @@ def main():
                 "seq_len": 3,
                 "seq_len_meaning": "n-step return horizon (frame stack 4)",
                 "parallelism": f"dp{world}",
+                "replay_sampling": "global PER over shards (mass all-gather)" if sharded else "per-shard PER",
                 "replay_capacity_per_gpu": args.capacity,
                 "envs_per_gpu": args.envs,
                 "actor_steps_per_learner_step": args.actor_steps,

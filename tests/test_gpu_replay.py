@@ -85,6 +85,34 @@ def test_sample_stratified_and_weights(cuda):
     assert rel < 0.03, rel
 
 
+def test_sample_glob_override_sharded(cuda):
+    """glob = (global pmin, shard scale) changes only the IS weights, not the indices;
+    ShardedSampling at world 1 reproduces plain sampling exactly."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+    from apex_amd.parallel.sharded import ShardedSampling
+
+    C = 5000
+    rp = HBMReplay(C, n_envs=8, device=cuda, alpha=1.0)
+    pr = torch.rand(C, device=cuda) + 0.2
+    rp.write_priorities(torch.arange(C, dtype=torch.int32, device=cuda), pr, dedup=False)
+    rp.filled.fill_(C)
+    B = 128
+    ctr = torch.zeros(1, dtype=torch.int64, device=cuda)
+    i0, w0 = torch.empty(B, dtype=torch.int32, device=cuda), torch.empty(B, device=cuda)
+    rp.sample_indices(B, i0, w0, ctr, beta=0.4)
+    sh = ShardedSampling(rp)
+    glob = sh()
+    i1, w1 = torch.empty_like(i0), torch.empty_like(w0)
+    rp.sample_indices(B, i1, w1, ctr, beta=0.4, glob=glob)
+    assert torch.equal(i0, i1)
+    torch.testing.assert_close(w1, w0, rtol=1e-6, atol=0)
+    forced = torch.tensor([0.1, 2.5], device=cuda)
+    rp.sample_indices(B, i1, w1, ctr, beta=0.4, glob=forced)
+    assert torch.equal(i0, i1)
+    leaf = rp.leaf_sum[i1.long()]
+    torch.testing.assert_close(w1, 2.5 * (leaf / 0.1) ** -0.4, rtol=1e-5, atol=0)
+
+
 def test_gather_transitions(cuda):
     from apex_amd.engine.hbm_replay import HBMReplay
 
