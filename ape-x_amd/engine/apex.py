@@ -94,7 +94,7 @@ class ApexEngine:
         """Learner -> local actor weights (the on-GPU analogue of learner.py:169-170)."""
         self.learner.copy_params_to(self.actor_flat)
         if self.hip_net:
-            self.actor_net.repack()
+            self.actor_net.copy_packed_from(self.learner.net)
 
     def _actor_body(self):
         if self.hip_net:  # conv1 reads the current stacks straight from the frame ring

@@ -119,6 +119,7 @@ class DQNLearner:
             self.net = HipDuelingNet(self.model)
             self.net.enable_backward()
             self.tnet = HipDuelingNet(self.target)
+            self.pmap1, self.pmap2 = self.net.pack_maps()  # optimizer refreshes the packed bf16 weights
             self.ws_s = NetWorkspace(B, A, dev, keep_for_backward=True)
             self.ws_s2 = NetWorkspace(B, A, dev)
             self.ws_t = NetWorkspace(B, A, dev)
@@ -166,16 +167,11 @@ class DQNLearner:
         s = self._stream()
         h = self.hip
         h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
-        if self.cfg.optimizer == "rmsprop":
-            h.rmsprop_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
-                           self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(), self.hp,
-                           self.step_counter.data_ptr(), self.norms.data_ptr(), s)
-        else:
-            h.adam_step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(),
-                        self.opt_s2.data_ptr(), self.P, self.partials.data_ptr(), self.partials.numel(), self.hp,
-                        self.step_counter.data_ptr(), self.norms.data_ptr(), s)
-        if self.hip_net:
-            self.net.repack()
+        pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if self.hip_net else (0, 0, 0)
+        step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
+        step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(), self.opt_s2.data_ptr(), self.P,
+             self.partials.data_ptr(), self.partials.numel(), self.hp, self.step_counter.data_ptr(),
+             self.norms.data_ptr(), s, *pk)
         self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 
     def step(self) -> None:
@@ -188,10 +184,16 @@ class DQNLearner:
         self.host_steps += 1
 
     # ------------------------------------------------------------------ target / params
+    def refresh_packed(self) -> None:
+        """Re-derive the packed bf16 weights from the fp32 master (after the flat buffer
+        was written outside the optimizer, e.g. a DP broadcast or a checkpoint load)."""
+        if self.hip_net:
+            self.net.repack()
+
     def sync_target(self) -> None:
         self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
         if self.hip_net:
-            self.tnet.repack()
+            self.tnet.copy_packed_from(self.net)
 
     def copy_params_to(self, dst_flat: torch.Tensor) -> None:
         self.hip.copy_f32(dst_flat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())

@@ -2,9 +2,11 @@
 
 ``HipDuelingNet`` wraps a :class:`DuelingDQN` (fp32 master parameters, reference
 state_dict, flat buffer) and keeps a packed bf16 copy of its weights in the layouts the
-gfx950 kernels want (conv weights [N][KH][KW][C], FC1 repacked to the channels-last
-flatten order).  ``repack()`` refreshes the packed copy after every optimizer step /
-target sync / actor publish (4 tiny kernels).
+gfx950 kernels want (conv weights [N][KH][KW][C] and their transposes for dgrad, FC1
+repacked to the channels-last flatten order), all in one bf16 arena.  The learner's
+fused optimizer rewrites the arena in the same pass as the fp32 update (``pack_maps``
+-> PackMap), target sync / actor publish copy arenas, and ``repack()`` re-derives it
+from scratch (init, after a broadcast or checkpoint load).
 
 Forward (per pass, no autograd):
   conv_fwd x3  (u8 frames -> bf16 NHWC activations; MFMA 32x32x16, bias+ReLU fused)
@@ -60,6 +62,10 @@ def _cl_view(t: torch.Tensor, B: int, C: int, H: int, W: int) -> torch.Tensor:
 
 
 class HipDuelingNet:
+    # packed bf16 weights live in one arena: [w1p | w2p | w3p | wfc1p | w2t | w3t]
+    LAYOUT = (("w1p", (32, 8, 8, 4)), ("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, FEAT)),
+              ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)))
+
     def __init__(self, model: DuelingDQN):
         assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
         self.hip = ops.hip()
@@ -67,17 +73,55 @@ class HipDuelingNet:
         self.A = model.num_actions
         dev = next(model.parameters()).device
         self.device = dev
-        bf = dict(dtype=torch.bfloat16, device=dev)
-        self.w1p = torch.empty(32, 8, 8, 4, **bf)
-        self.w2p = torch.empty(64, 4, 4, 32, **bf)
-        self.w3p = torch.empty(64, 3, 3, 64, **bf)
-        self.wfc1p = torch.empty(256, FEAT, **bf)
-        self.w2t = torch.empty(4, 4, 32, 64, **bf)   # W^T [ky][kx][c][n] for dgrad
-        self.w3t = torch.empty(3, 3, 64, 64, **bf)
+        sizes = [int(torch.Size(sh).numel()) for _, sh in self.LAYOUT]
+        self.arena = torch.empty(sum(sizes), dtype=torch.bfloat16, device=dev)
+        self.arena_offsets = {}
+        off = 0
+        for (name, sh), n in zip(self.LAYOUT, sizes):
+            setattr(self, name, self.arena[off:off + n].view(sh))
+            self.arena_offsets[name] = off
+            off += n
+        self.fwd_numel = self.arena_offsets["w2t"]   # forward-only part of the arena
         self._wgrad_ws = None
+        self._maps = None
         f = model.features
         self.b1, self.b2, self.b3 = f[0].bias, f[2].bias, f[4].bias
         self.repack()
+
+    def pack_maps(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """int32 (dst1, dst2) over the model's flat parameter order: the arena positions
+        that hold bf16 copies of each parameter (-1 = not packed, e.g. biases and the
+        fp32 head weights).  Used by the fused optimizer (PackMap)."""
+        if self._maps is not None:
+            return self._maps
+        m, f = self.model, self.model.features
+        seg = {name: (o, n) for name, o, n in m.param_segments()}
+        P = sum(n for _, n in seg.values())
+        dst1 = torch.full((P,), -1, dtype=torch.int64)
+        dst2 = torch.full((P,), -1, dtype=torch.int64)
+        ao = self.arena_offsets
+
+        def place(dst, pname, ref_of_pos, base):
+            o, n = seg[pname]
+            assert ref_of_pos.numel() == n
+            dst[o + ref_of_pos] = base + torch.arange(n)
+
+        for li, pname, N, C, K in ((0, "features.0.weight", 32, 4, 8), (1, "features.2.weight", 64, 32, 4),
+                                   (2, "features.4.weight", 64, 64, 3)):
+            ref = torch.arange(N * C * K * K).view(N, C, K, K)
+            place(dst1, pname, ref.permute(0, 2, 3, 1).reshape(-1), ao[("w1p", "w2p", "w3p")[li]])
+            if li > 0:
+                place(dst2, pname, ref.permute(2, 3, 1, 0).reshape(-1), ao[("w2t", "w3t")[li - 1]])
+        ref = torch.arange(128 * FEAT).view(128, C3, P3).permute(0, 2, 1).reshape(-1)
+        place(dst1, "advantage.0.weight", ref, ao["wfc1p"])
+        place(dst1, "value.0.weight", ref, ao["wfc1p"] + 128 * FEAT)
+        self._maps = (dst1.to(torch.int32).to(self.device), dst2.to(torch.int32).to(self.device))
+        return self._maps
+
+    def copy_packed_from(self, other: "HipDuelingNet", forward_only: bool = True) -> None:
+        """Device copy of another net's packed weights (same architecture)."""
+        n = self.fwd_numel if forward_only else self.arena.numel()
+        self.arena[:n].copy_(other.arena[:n])
 
     @staticmethod
     def _s() -> int:

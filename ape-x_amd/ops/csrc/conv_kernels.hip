@@ -150,10 +150,11 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
 
 // ------------------------------------------------------------------ dueling heads
 // z [B][256] = FC1 pre-activation (adv hidden 0..127 | value hidden 128..255, no bias).
-// A workgroup stages the head weights (A+1)x128 in LDS once and walks 16 rows (4 per
-// wave): h = relu(z + b1) -> LDS; lane a < A computes adv_a, lane A the value;
-// q = V + A - mean(A) (model.py:60-68).  h is kept (fp32) for the backward.
-constexpr int kHeadRows = 16;
+// A workgroup stages the head weights (A+1)x128 in LDS and handles 4 rows (one per
+// wave, B/4 workgroups so a 512-row batch spreads over 128 CUs): h = relu(z + b1) ->
+// LDS; lane a < A computes adv_a, lane A the value; q = V + A - mean(A)
+// (model.py:60-68).  h is kept (fp32) for the backward.
+constexpr int kHeadRows = 4;
 
 __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, const float* __restrict__ b_adv1,
                                                    const float* __restrict__ b_val1, const float* __restrict__ w_adv2,
@@ -253,7 +254,7 @@ void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float
 //   db_adv2[a] = sum_b dadv[b][a]   db_val2 = sum_b dv[b]   db_fc1[n] = sum_b dz[b][n]
 // Stage 1: HG_SPLIT blocks x 256 threads (thread = hidden column j) over row slices ->
 // fp32 partials; stage 2 sums the partials in fixed order (deterministic).
-constexpr int HG_SPLIT = 16;
+constexpr int HG_SPLIT = 64;  // 8 rows per block at B = 512: latency-bound, so spread wide
 constexpr int HG_MAXA = 32;
 
 __global__ __launch_bounds__(256) void heads_wgrad_partial_k(const float* __restrict__ dA, const float* __restrict__ h,
@@ -304,8 +305,16 @@ __global__ void heads_wgrad_reduce_k(const float* __restrict__ part, int G, int 
   const int stride = (A + 1) * 128 + (A + 1) + 256;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= stride) return;
-  float s = 0.f;
-  for (int g = 0; g < G; ++g) s += part[(size_t)g * stride + e];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains: loads stay in flight
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {
+    s0 += part[(size_t)g * stride + e];
+    s1 += part[(size_t)(g + 1) * stride + e];
+    s2 += part[(size_t)(g + 2) * stride + e];
+    s3 += part[(size_t)(g + 3) * stride + e];
+  }
+  for (; g < G; ++g) s0 += part[(size_t)g * stride + e];
+  const float s = (s0 + s1) + (s2 + s3);
   if (e < A * 128) g_wadv2[e] = s;
   else if (e < (A + 1) * 128) g_wval2[e - A * 128] = s;
   else if (e < (A + 1) * 128 + A) g_badv2[e - (A + 1) * 128] = s;

@@ -171,10 +171,14 @@ PYBIND11_MODULE(_apex_hip, m) {
            py::arg("lr_gamma") = 1.f, py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0,
            py::arg("centered") = false);
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
-                           int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s) {
+                           int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s,
+                           uint64_t dst1, uint64_t dst2, uint64_t arena) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
-                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s));
-  });
+                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr);
+  }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("gavg"), py::arg("n"), py::arg("partials"),
+     py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
+     py::arg("dst2") = 0, py::arg("arena") = 0);
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
                        int lr_step_size, int lr_step_offset) {
@@ -184,10 +188,14 @@ PYBIND11_MODULE(_apex_hip, m) {
            py::arg("weight_decay") = 0.f, py::arg("max_norm") = 0.f, py::arg("lr_gamma") = 1.f,
            py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0);
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
-                        int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s) {
+                        int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s,
+                        uint64_t dst1, uint64_t dst2, uint64_t arena) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
-              hp, P<const int64_t>(step), P<float>(norms), S(s));
-  });
+              hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr);
+  }, py::arg("p"), py::arg("g"), py::arg("mm"), py::arg("v"), py::arg("n"), py::arg("partials"),
+     py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
+     py::arg("dst2") = 0, py::arg("arena") = 0);
   // ---- network kernels
   m.def("conv_fwd", [](int layer, uint64_t in, uint64_t ids, uint64_t idx, uint64_t wp, uint64_t bias, uint64_t out,
                        int B, uint64_t s) {

@@ -110,15 +110,25 @@ struct RMSpropParams {
   int lr_step_offset;    // 1 reproduces scheduler.step() before optimizer.step()
   int centered;
 };
+// ``pack`` (nullable): after the update, bf16(p[i]) is also written to pack->arena at
+// pack->dst1[i] and pack->dst2[i] (-1 = none): the MFMA kernels' packed weight layouts
+// are refreshed inside the optimizer pass instead of by separate pack kernels.
+struct PackMap {
+  const int* dst1;
+  const int* dst2;
+  uint16_t* arena;
+};
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
-                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s);
+                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
+                  const PackMap* pack = nullptr);
 struct AdamParams {
   float lr0, beta1, beta2, eps, weight_decay, max_norm;
   float lr_gamma;
   int lr_step_size, lr_step_offset;
 };
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
-               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s);
+               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
+               const PackMap* pack = nullptr);
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
 
 // ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)

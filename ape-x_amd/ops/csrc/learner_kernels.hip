@@ -138,11 +138,19 @@ __device__ __forceinline__ float step_lr(float lr0, float gamma, int step_size, 
   return lr0 * powf(gamma, (float)k);
 }
 
+__device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v) {
+  if (!pk.arena) return;
+  const uint16_t b = f2bf(v);
+  const int d1 = pk.dst1[i], d2 = pk.dst2[i];
+  if (d1 >= 0) pk.arena[d1] = b;
+  if (d2 >= 0) pk.arena[d2] = b;
+}
+
 __global__ __launch_bounds__(256) void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ g,
                                                       float* __restrict__ sq, float* __restrict__ gavg, int64_t n,
                                                       const double* __restrict__ partials, int n_partials,
                                                       RMSpropParams hp, const int64_t* __restrict__ step,
-                                                      float* __restrict__ norms_out) {
+                                                      float* __restrict__ norms_out, PackMap pk) {
   const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
   const int64_t st = step ? step[0] : 0;
   const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
@@ -165,21 +173,26 @@ __global__ __launch_bounds__(256) void rmsprop_step_k(float* __restrict__ p, con
     } else {
       avg = sqrtf(s2) + hp.eps;
     }
-    p[i] -= lr * gi / avg;
+    const float np = p[i] - lr * gi / avg;
+    p[i] = np;
+    pack_store(pk, i, np);
   }
 }
 
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
-                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s) {
+                  int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
+                  const PackMap* pack) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out);
+  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
+  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out, pk);
   LAUNCH_CHECK();
 }
 
 __global__ __launch_bounds__(256) void adam_step_k(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                    const double* __restrict__ partials, int n_partials, AdamParams hp,
-                                                   const int64_t* __restrict__ step, float* __restrict__ norms_out) {
+                                                   const int64_t* __restrict__ step, float* __restrict__ norms_out,
+                                                   PackMap pk) {
   const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
   const int64_t st = step ? step[0] : 0;
   const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
@@ -199,14 +212,17 @@ __global__ __launch_bounds__(256) void adam_step_k(float* __restrict__ p, const 
     const float vi = v[i] * hp.beta2 + (1.f - hp.beta2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    p[i] -= step_size * mi / (sqrtf(vi) * rbc2 + hp.eps);
+    const float np = p[i] - step_size * mi / (sqrtf(vi) * rbc2 + hp.eps);
+    p[i] = np;
+    pack_store(pk, i, np);
   }
 }
 
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
-               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s) {
+               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s, const PackMap* pack) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, hp, step, norms_out);
+  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
+  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, hp, step, norms_out, pk);
   LAUNCH_CHECK();
 }
 

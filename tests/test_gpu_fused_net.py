@@ -196,3 +196,41 @@ def test_frame_ring_input_matches_dense(cuda):
     q1 = net(dense, ws1).clone()
     q2 = net(frames, ws2, table, idx).clone()
     assert torch.equal(q1, q2)
+
+
+@pytest.mark.parametrize("opt", ["rmsprop", "adam"])
+def test_fused_optimizer_packing_matches_repack(cuda, opt):
+    """The optimizer's PackMap stores leave the bf16 arena exactly as repack() would."""
+    from apex_amd import ops
+    from apex_amd.models.fused import HipDuelingNet
+
+    hip = ops.hip()
+    m = _model(cuda)
+    flat = m.flatten_parameters()
+    net = HipDuelingNet(m)
+    net.enable_backward()
+    d1, d2 = net.pack_maps()
+    P = flat.numel()
+    assert int((d1 >= 0).sum()) == net.fwd_numel
+    assert int((d2 >= 0).sum()) == net.arena.numel() - net.fwd_numel
+    g = torch.randn(P, device=cuda)
+    s1, s2 = torch.zeros(P, device=cuda), torch.zeros(P, device=cuda)
+    partials = torch.zeros(hip.grad_norm_partials(), dtype=torch.float64, device=cuda)
+    norms = torch.zeros(4, device=cuda)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.arena.zero_()
+    hip.grad_sumsq(g.data_ptr(), P, partials.data_ptr(), s)
+    if opt == "rmsprop":
+        hp = hip.RMSpropParams(1e-3, 0.95, 1.5e-7, 40.0, 1.0, 0, 0, True)
+        hip.rmsprop_step(flat.data_ptr(), g.data_ptr(), s1.data_ptr(), s2.data_ptr(), P, partials.data_ptr(),
+                         partials.numel(), hp, step.data_ptr(), norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
+                         net.arena.data_ptr())
+    else:
+        hp = hip.AdamParams(1e-3, max_norm=40.0)
+        hip.adam_step(flat.data_ptr(), g.data_ptr(), s1.data_ptr(), s2.data_ptr(), P, partials.data_ptr(),
+                      partials.numel(), hp, step.data_ptr(), norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
+                      net.arena.data_ptr())
+    fused = net.arena.clone()
+    net.repack()
+    assert torch.equal(fused.view(torch.int16), net.arena.view(torch.int16))
