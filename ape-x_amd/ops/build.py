@@ -41,6 +41,7 @@ HIP_SOURCES = [
     "learner_kernels.hip",
     "conv_kernels.hip",
     "conv_bwd_kernels.hip",
+    "aql_kernels.hip",
 ]
 
 

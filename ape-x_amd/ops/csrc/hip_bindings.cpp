@@ -248,4 +248,43 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("copy_f32", [](uint64_t dst, uint64_t src, int64_t n, uint64_t s) {
     copy_f32(P<float>(dst), P<const float>(src), n, S(s));
   });
+
+  // ---- AQL kernels
+  py::class_<AQLNet>(m, "AQLNet");
+  m.def("make_aql_net", [](py::dict ints, py::dict ptrs) {
+    AQLNet n{};
+    auto gi = [&](const char* k) { return ints[k].cast<int>(); };
+    n.obs = gi("obs"); n.adim = gi("adim"); n.cont = gi("cont"); n.T = gi("T"); n.na = gi("na");
+    n.uniform = gi("uniform"); n.propose = gi("propose"); n.noisy = gi("noisy");
+    auto gp = [&](const char* k) -> const float* {
+      return ptrs.contains(k) ? reinterpret_cast<const float*>(ptrs[k].cast<uint64_t>()) : nullptr;
+    };
+    n.qf_w1 = gp("qf_w1"); n.qf_b1 = gp("qf_b1"); n.qf_w2 = gp("qf_w2"); n.qf_b2 = gp("qf_b2");
+    n.ao_w1 = gp("ao_w1"); n.ao_b1 = gp("ao_b1"); n.ao_w2 = gp("ao_w2"); n.ao_b2 = gp("ao_b2");
+    n.a1_wmu = gp("a1_wmu"); n.a1_wsig = gp("a1_wsig"); n.a1_weps = gp("a1_weps");
+    n.a1_bmu = gp("a1_bmu"); n.a1_bsig = gp("a1_bsig"); n.a1_beps = gp("a1_beps");
+    n.a2_wmu = gp("a2_wmu"); n.a2_wsig = gp("a2_wsig"); n.a2_weps = gp("a2_weps");
+    n.a2_bmu = gp("a2_bmu"); n.a2_bsig = gp("a2_bsig"); n.a2_beps = gp("a2_beps");
+    n.f_w = gp("f_w"); n.f_b = gp("f_b");
+    n.df_w1 = gp("df_w1"); n.df_b1 = gp("df_b1"); n.df_w2 = gp("df_w2"); n.df_b2 = gp("df_b2");
+    if (!n.qf_w1 || !n.ao_w1 || !n.a1_wmu || !n.a2_wmu) throw std::invalid_argument("make_aql_net: missing weights");
+    if (n.cont && (!n.ao_w2 || n.adim < 1)) throw std::invalid_argument("make_aql_net: continuous encoder");
+    return n;
+  });
+  m.def("aql_workspace_floats", &aql_workspace_floats);
+  m.def("aql_candidate_q", [](const AQLNet& n, uint64_t ws, uint64_t state, uint64_t a_mu, int B, uint64_t q,
+                              uint64_t s) {
+    aql_candidate_q(n, P<float>(ws), P<const float>(state), P<const float>(a_mu), B, P<float>(q), S(s));
+  });
+  m.def("aql_propose", [](const AQLNet& n, uint64_t state, int B, uint64_t low, uint64_t high, uint64_t var,
+                          uint64_t seed, uint64_t counter, uint64_t a_mu, uint64_t mu_out, uint64_t s) {
+    if (!n.f_w || !n.df_w1 || !n.df_w2) throw std::invalid_argument("aql_propose: proposal weights missing");
+    aql_propose(n, P<const float>(state), B, P<const float>(low), P<const float>(high), P<const float>(var), seed,
+                P<const int64_t>(counter), P<float>(a_mu), P<float>(mu_out), S(s));
+  });
+  m.def("aql_select", [](uint64_t q, uint64_t a_mu, int B, int T, int adim, uint64_t eps, uint64_t seed,
+                         uint64_t counter, uint64_t act_idx, uint64_t env_act, uint64_t s) {
+    aql_select(P<const float>(q), P<const float>(a_mu), B, T, adim, P<const float>(eps), seed,
+               P<const int64_t>(counter), P<int>(act_idx), P<float>(env_act), S(s));
+  });
 }

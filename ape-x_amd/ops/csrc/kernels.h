@@ -156,4 +156,23 @@ void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const 
                 float* grad, float* bias_grad, hipStream_t s);
 void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
 
+
+// ---- aql_kernels.hip (AQL candidate critic / proposal)
+struct AQLNet {
+  int obs, adim, cont, T, na, uniform, propose, noisy;
+  const float *qf_w1, *qf_b1, *qf_w2, *qf_b2;        // q_feature: obs->64->64
+  const float *ao_w1, *ao_b1, *ao_w2, *ao_b2;        // action_out: adim->128->64 (cont) | 1->64
+  const float *a1_wmu, *a1_wsig, *a1_weps, *a1_bmu, *a1_bsig, *a1_beps;  // NoisyLinear 128->64
+  const float *a2_wmu, *a2_wsig, *a2_weps, *a2_bmu, *a2_bsig, *a2_beps;  // NoisyLinear 64->1
+  const float *f_w, *f_b;                            // q.features: obs->128 (state embedding)
+  const float *df_w1, *df_b1, *df_w2, *df_b2;        // proposal.dist_feature: 128->128->na
+};
+size_t aql_workspace_floats();
+void aql_candidate_q(const AQLNet& net, float* ws, const float* state, const float* a_mu, int B, float* q,
+                     hipStream_t s);
+void aql_propose(const AQLNet& net, const float* state, int B, const float* low, const float* high, const float* var,
+                 uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s);
+void aql_select(const float* q, const float* a_mu, int B, int T, int adim, const float* eps, uint64_t seed,
+                const int64_t* counter, int* act_idx, float* env_act, hipStream_t s);
+
 }  // namespace apex

@@ -46,7 +46,7 @@ def sample_aql_batch(buffer, batch_size, beta, device):
 
 
 def aql_update(model, target_model, buffer, optimizer_q, optimizer_proposal, batch_size, beta, gamma, n_steps,
-               ent_lam, device, copy_proposal_to_target=False, reset_noise=False, max_norm=40.0):
+               ent_lam, device, copy_proposal_to_target=False, reset_noise=False, max_norm=40.0, fused=None):
     batch = sample_aql_batch(buffer, batch_size, beta, device)
     (state, action, reward, next_state, done, a_mu, weights), indices = batch
     # proposal loss: imitate the critic's best candidate, entropy bonus
@@ -64,8 +64,11 @@ def aql_update(model, target_model, buffer, optimizer_q, optimizer_proposal, bat
     if copy_proposal_to_target:
         target_model.proposal.load_state_dict(model.proposal.state_dict())
     # critic loss
-    loss_q, prios = compute_loss_AQL(model, target_model, (state, action, reward, next_state, done, a_mu, weights),
-                                     n_steps=n_steps, gamma=gamma)
+    batch_t = (state, action, reward, next_state, done, a_mu, weights)
+    if fused is not None:  # (FusedAQL online, FusedAQL target): no-grad s' critics on the HIP kernel
+        loss_q, prios = compute_loss_AQL_fused(model, target_model, fused[0], fused[1], batch_t, n_steps, gamma)
+    else:
+        loss_q, prios = compute_loss_AQL(model, target_model, batch_t, n_steps=n_steps, gamma=gamma)
     optimizer_q.zero_grad()
     loss_q.backward()
     torch.nn.utils.clip_grad_norm_(model.q.parameters(), max_norm)
@@ -75,6 +78,80 @@ def aql_update(model, target_model, buffer, optimizer_q, optimizer_proposal, bat
         model.reset_noise()
         target_model.reset_noise()
     return loss_q, loss_p
+
+
+def compute_loss_AQL_fused(model, target_model, fused, fused_tgt, batch, n_steps, gamma=0.99):
+    """``compute_loss_AQL`` with the two no-grad critic evaluations at s' (online and
+    target, utils.py:48-49) on the fused HIP kernel; Q(s, a_mu) keeps autograd."""
+    from ..algo.losses import _td_terms, huber_weighted, priorities_from_td
+
+    states, actions, rewards, next_states, dones, a_mu, weights = batch
+    q_values = model(states, a_mu)
+    with torch.no_grad():
+        next_q = fused.candidate_q(next_states, a_mu)
+        tgt_next_q = fused_tgt.candidate_q(next_states, a_mu)
+    td = _td_terms(q_values, next_q, tgt_next_q, actions, rewards, dones, n_steps, gamma)
+    return huber_weighted(td, weights), priorities_from_td(td).detach().cpu().numpy()
+
+
+class VectorAQLActors:
+    """GPU-batched AQL acting for ``n_envs`` host envs: one proposal + candidate-Q +
+    epsilon-greedy launch sequence per env step for all envs (FusedAQL), instead of one
+    CPU process and ~20 small ops + ``.cpu()`` per env per step (batchrecoder_AQL.py).
+    Same recording contract as ``BatchRecorder.record_batch``: every env plays one
+    episode, raw (s, a, r, s', d, a_mu) transitions go into the buffer."""
+
+    def __init__(self, env_id, n_envs, buffer, model, seed=0, max_episode_length=50000, writer=None,
+                 eps_base=0.4, eps_alpha=7.0):
+        from ..algo.schedules import actor_epsilon
+        from ..models.aql_fused import FusedAQL
+
+        self.envs = [envs.make(env_id) for _ in range(n_envs)]
+        for i, e in enumerate(self.envs):
+            e.seed(seed + i)
+        self.buffer = buffer
+        self.model = model
+        self.fused = FusedAQL(model, seed=seed)
+        self.max_episode_length = int(max_episode_length)
+        self.writer = writer
+        self.episode_idx = 0
+        eps = actor_epsilon(np.arange(n_envs), n_envs, eps_base, eps_alpha)
+        self.eps = torch.as_tensor(np.atleast_1d(eps), dtype=torch.float32, device=self.fused.device)
+
+    def record_batch(self) -> int:
+        E = len(self.envs)
+        states = [e.reset() for e in self.envs]
+        active = np.ones(E, dtype=bool)
+        ep_r, ep_len = np.zeros(E), np.zeros(E, dtype=np.int64)
+        while active.any():
+            ids = np.nonzero(active)[0]
+            st = np.stack([np.asarray(states[i], dtype=np.float32) for i in ids])
+            with torch.no_grad():
+                idx, am, act = self.fused.act(st, self.eps[torch.as_tensor(ids, device=self.eps.device)])
+            idx, am, act = idx.cpu().numpy(), am.cpu().numpy(), act.cpu().numpy()
+            for j, i in enumerate(ids):
+                a_env = act[j] if self.fused.cont else int(act[j])
+                s2, r, d, _ = self.envs[i].step(a_env)
+                a_mu = am[j] if self.fused.cont else am[j].astype(np.int64)
+                self.buffer.add(states[i], int(idx[j]), r, s2, d, a_mu)
+                states[i] = s2
+                ep_r[i] += r
+                ep_len[i] += 1
+                if d or ep_len[i] >= self.max_episode_length:
+                    active[i] = False
+                    if self.writer is not None:
+                        self.writer.add_scalar("actor/episode_reward", float(ep_r[i]), self.episode_idx)
+                        self.writer.add_scalar("actor/episode_length", int(ep_len[i]), self.episode_idx)
+                    self.episode_idx += 1
+        return int(ep_len.sum())
+
+    def set_worker_weights(self, model) -> None:
+        if model is not self.model:
+            self.model.load_state_dict(model.state_dict())
+
+    def cleanup(self) -> None:
+        for e in self.envs:
+            e.close()
 
 
 class _AQLBase:
@@ -133,6 +210,11 @@ class train_AQL(_AQLBase):  # AQL.py train_DQN
         device = device if device is not None else ("cuda:0" if torch.cuda.is_available() else "cpu")
         self._build(env_id, propose_sample, uniform_sample, action_var, device, buffer_size, prior_alpha, lr, seed,
                     writer)
+        self.fused = None
+        if self.device.type == "cuda":  # no-grad s' critics on the fused HIP kernel
+            from ..models.aql_fused import FusedAQL
+
+            self.fused = (FusedAQL(self.model), FusedAQL(self.target_model))
         self.scheduler_q = torch.optim.lr_scheduler.CosineAnnealingLR(self.optimizer_q, T_max=self.max_step,
                                                                       eta_min=lr / 1000)
         self.scheduler_proposal = torch.optim.lr_scheduler.CosineAnnealingLR(self.optimizer_proposal,
@@ -145,7 +227,7 @@ class train_AQL(_AQLBase):  # AQL.py train_DQN
     def compute_td_loss(self, batch_size, beta):
         loss_q, loss_p = aql_update(self.model, self.target_model, self.replay_buffer, self.optimizer_q,
                                     self.optimizer_proposal, batch_size, beta, self.gamma, 1, self.ent_lam,
-                                    self.device)
+                                    self.device, fused=self.fused)
         self.scheduler_proposal.step()
         self.scheduler_q.step()
         return loss_q, loss_p
@@ -187,7 +269,7 @@ class train_AQL_dis(_AQLBase):  # AQL_dis.py train_DQN
                  device=None, n_steps=1, batch_size=32, gamma=0.99, target_update_interval=20, save_interval=200,
                  propose_sample=1, uniform_sample=50, action_var=0.25, ent_lam=0.8, n_workers=10, lr=1e-3, seed=0,
                  save_dir=".", writer=None, buffer_size=1e7, start_method="spawn", aql_dup_by_obs_dim=False,
-                 max_episode_length=50000):
+                 max_episode_length=50000, gpu_actors: int = 0, fused: bool | None = None):
         from .batchrecorder import KIND_AQL, BatchRecorder
 
         self.prior_beta_start = prior_beta_start
@@ -206,6 +288,19 @@ class train_AQL_dis(_AQLBase):  # AQL_dis.py train_DQN
                     writer)
         self.scheduler_q = torch.optim.lr_scheduler.StepLR(self.optimizer_q, step_size=100, gamma=0.99)
         self.scheduler_proposal = torch.optim.lr_scheduler.StepLR(self.optimizer_proposal, step_size=100, gamma=0.99)
+        use_fused = (self.device.type == "cuda") if fused is None else fused
+        self.fused = None
+        if use_fused:
+            from ..models.aql_fused import FusedAQL
+
+            self.fused = (FusedAQL(self.model), FusedAQL(self.target_model))
+        if gpu_actors:
+            actor_model = AQL(env=self.env, propose_sample=propose_sample, uniform_sample=uniform_sample,
+                              action_var=action_var, device=self.device).to(self.device)
+            self.recoder = VectorAQLActors(env_id, gpu_actors, self.replay_buffer, actor_model, seed=0,
+                                           max_episode_length=max_episode_length, writer=self.writer)
+            self.learn_idx = 0
+            return
         cpu_model = AQL(env=self.env, propose_sample=propose_sample, uniform_sample=uniform_sample,
                         action_var=action_var, device="cpu")
         self.recoder = BatchRecorder(env_id, env_seed=0, n_workers=self.n_workers, buffer=self.replay_buffer,
@@ -223,7 +318,7 @@ class train_AQL_dis(_AQLBase):  # AQL_dis.py train_DQN
     def compute_td_loss(self, batch_size, beta):
         return aql_update(self.model, self.target_model, self.replay_buffer, self.optimizer_q, self.optimizer_proposal,
                           batch_size, beta, self.gamma, self.n_steps, self.ent_lam, self.device,
-                          copy_proposal_to_target=True, reset_noise=True)
+                          copy_proposal_to_target=True, reset_noise=True, fused=self.fused)
 
     def train(self):
         try:
@@ -245,7 +340,7 @@ class train_AQL_dis(_AQLBase):  # AQL_dis.py train_DQN
         finally:
             self.recoder.cleanup()
             self.writer.flush()
-        return self.recoder.episodes
+        return getattr(self.recoder, "episodes", self.recoder.episode_idx)
 
 
 def main(argv=None):

@@ -86,6 +86,7 @@ def main():
         from apex_amd.parallel.broadcast import broadcast_flat
 
         broadcast_flat(eng.learner.flat, src=0)
+        eng.learner.refresh_packed()
         eng.learner.sync_target()
         eng.learner.copy_params_to(eng.actor_flat)
 
