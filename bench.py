@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
+    ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
+                    help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="gloo: host-staged (tests)")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal, gloo)")
     ap.add_argument("--local-sampling", action="store_true",
                     help="N>1: sample each replay shard on its own (default: global PER over shards)")
     return ap.parse_args()
@@ -64,11 +68,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    if args.same_device:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.topology == "central":
+        return central(args, rank, world, device)
 
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
@@ -161,6 +172,65 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def central(args, rank, world, device):
+    """Central-replay topology: rank 0 = learner + the one replay, ranks 1.. = actor GPUs
+    pushing experience over RCCL.  ``value`` = learner SGD steps/s (one learner);
+    actor frames/s summed over the actor GPUs."""
+    import torch
+    import torch.distributed as dist
+
+    from apex_amd.engine.apex import EngineConfig
+    from apex_amd.engine.central import CentralApexEngine
+    from apex_amd.engine.learner import LearnerConfig
+
+    if world < 2:
+        raise SystemExit("--topology central needs >= 2 ranks")
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed)
+    cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
+                       threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
+                       use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
+    eng = CentralApexEngine(cfg, device, rank, world)
+    t_fill = time.perf_counter()
+    eng.fill()
+    torch.cuda.synchronize(device)
+    t_fill = time.perf_counter() - t_fill
+    if not args.no_graphs:
+        eng.capture()
+    for _ in range(args.warmup):
+        eng.train_step()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.train_step()
+    torch.cuda.synchronize(device)
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank == 0:
+        st = eng.learner.stats()
+        steps_per_s = args.steps / dt
+        frames_per_s = (world - 1) * args.steps * args.actor_steps * eng.frames_per_actor_step / dt
+        print(json.dumps({
+            "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
+            "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": "bf16",
+            "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
+            "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
+                       "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",
+                       "topology": "central replay on rank 0, experience pushed over " + args.backend,
+                       "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": args.envs},
+            "actor_frames_per_sec": round(frames_per_s, 1), "replay_fill_seconds": round(t_fill, 3),
+            "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
+        }), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

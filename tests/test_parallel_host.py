@@ -195,3 +195,59 @@ def test_sharded_estimator_matches_single_buffer_expectation():
         w_plain = w_sh[r] / (k * M[r] / M.sum())
         i0 = sum(len(s) for s in shards[:r])
         assert np.allclose(w_plain, w_single[i0:i0 + len(shards[r])])
+
+
+def _packet(rank, k, E, FB, n_slots, n_frames):
+    g = torch.Generator().manual_seed(1000 * rank + k)
+    frames = torch.randint(0, 256, (E, FB), dtype=torch.uint8, generator=g)
+    slot = (torch.arange(E) + k * E) % n_slots
+    fslot = (torch.arange(E) + (k + 1) * E) % n_frames
+    s_ids = torch.randint(0, n_frames, (E, 4), generator=g, dtype=torch.int32)
+    s2_ids = torch.randint(0, n_frames, (E, 4), generator=g, dtype=torch.int32)
+    a = torch.randint(0, 18, (E,), generator=g, dtype=torch.int32)
+    r = torch.randn(E, generator=g)
+    d = (torch.rand(E, generator=g) < 0.1).float()
+    p = torch.rand(E, generator=g)
+    return frames, (s_ids, s2_ids, a, r, d, p, slot.int(), fslot.int())
+
+
+def _experience_body(rank, world, E, FB, steps):
+    from apex_amd.parallel.experience import ExperienceReceiver, ExperienceSender, Region, apply_packet, pack_meta
+
+    n_slots, n_frames = 4 * E, 6 * E
+    if rank > 0:
+        snd = ExperienceSender(E, FB, "cpu", dst=0)
+        for k in range(steps):
+            frames, fields = _packet(rank, k, E, FB, n_slots, n_frames)
+            snd.send(frames, pack_meta(*fields, out=snd.meta.clone()))
+            snd.wait()
+        return "sent"
+    R = world - 1
+    tables = {"frames": torch.zeros(R * n_frames, FB, dtype=torch.uint8),
+              "s_ids": torch.zeros(R * n_slots, 4, dtype=torch.int32),
+              "s2_ids": torch.zeros(R * n_slots, 4, dtype=torch.int32),
+              "action": torch.zeros(R * n_slots, dtype=torch.int32), "reward": torch.zeros(R * n_slots),
+              "done": torch.zeros(R * n_slots)}
+    regions = {r: Region((r - 1) * n_slots, n_slots, (r - 1) * n_frames, n_frames) for r in range(1, world)}
+    rcv = ExperienceReceiver(E, FB, "cpu", range(1, world))
+    bad = 0
+    for k in range(steps):
+        rcv.post()
+        for r, (frames, meta) in rcv.take("cpu").items():
+            slots, prio = apply_packet(tables, regions[r], frames, meta)
+            ef, (s_ids, s2_ids, a, rew, d, p, slot, fslot) = _packet(r, k, E, FB, n_slots, n_frames)
+            reg = regions[r]
+            bad += int(not torch.equal(slots, (slot + reg.slot_base).int()))
+            bad += int(not torch.equal(prio, p))
+            bad += int(not torch.equal(tables["frames"][(fslot + reg.frame_base).long()], ef))
+            sl = (slot + reg.slot_base).long()
+            bad += int(not torch.equal(tables["s_ids"][sl], s_ids + reg.frame_base))
+            bad += int(not torch.equal(tables["s2_ids"][sl], s2_ids + reg.frame_base))
+            bad += int(not torch.equal(tables["action"][sl], a))
+            bad += int(not torch.equal(tables["reward"][sl], rew) or not torch.equal(tables["done"][sl], d))
+    return bad
+
+
+def test_central_experience_push_regions():
+    out = _spawn(_experience_body, 3, 32, 112, 7)
+    assert out[0] == 0 and out[1] == "sent" and out[2] == "sent"
