@@ -63,7 +63,8 @@ def _cl_view(t: torch.Tensor, B: int, C: int, H: int, W: int) -> torch.Tensor:
 
 class HipDuelingNet:
     # packed bf16 weights live in one arena: [w1p | w2p | w3p | wfc1p | w2t | w3t]
-    LAYOUT = (("w1p", (32, 8, 8, 4)), ("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, FEAT)),
+    # (conv1 keeps the reference layout [n][c][ky][kx]: its kernel's K order is (c, ky, kx))
+    LAYOUT = (("w1p", (32, 4, 8, 8)), ("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, FEAT)),
               ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)))
 
     def __init__(self, model: DuelingDQN):
@@ -109,7 +110,8 @@ class HipDuelingNet:
         for li, pname, N, C, K in ((0, "features.0.weight", 32, 4, 8), (1, "features.2.weight", 64, 32, 4),
                                    (2, "features.4.weight", 64, 64, 3)):
             ref = torch.arange(N * C * K * K).view(N, C, K, K)
-            place(dst1, pname, ref.permute(0, 2, 3, 1).reshape(-1), ao[("w1p", "w2p", "w3p")[li]])
+            order = ref.reshape(-1) if li == 0 else ref.permute(0, 2, 3, 1).reshape(-1)
+            place(dst1, pname, order, ao[("w1p", "w2p", "w3p")[li]])
             if li > 0:
                 place(dst2, pname, ref.permute(2, 3, 1, 0).reshape(-1), ao[("w2t", "w3t")[li - 1]])
         ref = torch.arange(128 * FEAT).view(128, C3, P3).permute(0, 2, 1).reshape(-1)
@@ -129,7 +131,7 @@ class HipDuelingNet:
 
     def repack(self) -> None:
         h, s, f, m = self.hip, self._s(), self.model.features, self.model
-        h.pack_conv_w(f[0].weight.data_ptr(), self.w1p.data_ptr(), 32, 4, 8, 8, s)
+        self.w1p.copy_(f[0].weight.detach().reshape(self.w1p.shape))  # bf16 cast, reference layout
         h.pack_conv_w(f[2].weight.data_ptr(), self.w2p.data_ptr(), 64, 32, 4, 4, s)
         h.pack_conv_w(f[4].weight.data_ptr(), self.w3p.data_ptr(), 64, 64, 3, 3, s)
         h.pack_fc1(m.advantage[0].weight.data_ptr(), m.value[0].weight.data_ptr(), self.wfc1p.data_ptr(), P3, C3, s)

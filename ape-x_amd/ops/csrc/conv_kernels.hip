@@ -141,7 +141,7 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
               uint16_t* out, int B, hipStream_t s) {
   const FrameSrc fs{reinterpret_cast<const uint8_t*>(in), ids, idx};
   switch (layer) {
-    case 1: launch_conv_fwd<Conv1, true>(in, fs, wp, bias, out, B, s); break;
+    case 1: conv1_fwd(fs.frames, ids, idx, wp, bias, out, B, s); break;  // conv1_kernels.hip
     case 2: launch_conv_fwd<Conv2, false>(in, fs, wp, bias, out, B, s); break;
     case 3: launch_conv_fwd<Conv3, false>(in, fs, wp, bias, out, B, s); break;
     default: throw std::invalid_argument("conv_fwd: layer must be 1, 2 or 3");

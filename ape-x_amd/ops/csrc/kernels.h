@@ -157,6 +157,10 @@ void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const 
 void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
 
 
+// ---- conv1_kernels.hip: conv1 forward from raw u8 planes; w = bf16 [32][4][8][8] (reference layout)
+void conv1_fwd(const uint8_t* frames, const int* ids, const int* idx, const uint16_t* w, const float* bias,
+               uint16_t* out, int B, hipStream_t s);
+
 // ---- aql_kernels.hip (AQL candidate critic / proposal)
 struct AQLNet {
   int obs, adim, cont, T, na, uniform, propose, noisy;

@@ -18,6 +18,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=100)
 ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
+ap.add_argument("--graph", type=int, default=1, help="time a captured graph of --iters launches (no launch overhead)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -74,10 +75,26 @@ for name, fn in cases.items():
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    e0.record()
-    for _ in range(a.iters):
-        fn()
-    e1.record()
+    if a.graph:
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream()
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            s = torch.cuda.current_stream().cuda_stream
+            with torch.cuda.graph(g, stream=cs):
+                for _ in range(a.iters):
+                    fn()
+        torch.cuda.current_stream().wait_stream(cs)
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+    else:
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1000
     fl = flops.get(name[:5], 0) * B
