@@ -216,3 +216,42 @@ __device__ __forceinline__ void stage_chunks(const uint4* __restrict__ src, char
 }
 
 }  // namespace apex
+
+namespace apex {
+
+// ---------------------------------------------------------------- register prefetch
+// Up to 8 x 256 16-byte chunks per workgroup held in NAMED registers (a uint4 array here
+// is demoted to scratch: SROA runs before the unroller), so a persistent kernel can issue
+// the global loads of its NEXT sample before computing the current one, and commit them
+// to LDS after the compute (one LDS buffer, global latency hidden behind the MFMAs).
+typedef unsigned int u32v4 __attribute__((ext_vector_type(4)));  // native vector: SROA-friendly
+struct Pf8 {
+  u32v4 r0, r1, r2, r3, r4, r5, r6, r7;
+};
+
+#define APEX_PF_SLOTS(X) X(0, r0) X(1, r1) X(2, r2) X(3, r3) X(4, r4) X(5, r5) X(6, r6) X(7, r7)
+
+template <int TOTAL>
+__device__ __forceinline__ void pf_load(Pf8& p, const uint4* __restrict__ src4) {
+  static_assert(TOTAL <= 8 * 256, "Pf8 holds at most 2048 chunks per workgroup");
+  const u32v4* src = reinterpret_cast<const u32v4*>(src4);
+  const int t = threadIdx.x;
+#define APEX_PF_LD(K, R) \
+  if constexpr (K * 256 < TOTAL) p.R = src[min(t + K * 256, TOTAL - 1)];  /* always assigned */
+  APEX_PF_SLOTS(APEX_PF_LD)
+#undef APEX_PF_LD
+}
+
+template <int TOTAL, class DstOff>
+__device__ __forceinline__ void pf_store(const Pf8& p, char* dst, DstOff dst_off) {
+  const int t = threadIdx.x;
+#define APEX_PF_ST(K, R) \
+  if constexpr (K * 256 < TOTAL) {                                  \
+    if ((K + 1) * 256 <= TOTAL || t + K * 256 < TOTAL)              \
+      *reinterpret_cast<u32v4*>(dst + dst_off(t + K * 256)) = p.R;  \
+  }
+  APEX_PF_SLOTS(APEX_PF_ST)
+#undef APEX_PF_ST
+}
+
+}  // namespace apex

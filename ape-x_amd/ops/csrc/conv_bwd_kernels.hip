@@ -172,9 +172,13 @@ void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* wt, const uint16_
 }
 
 // ====================================================================== wgrad
-template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_>
+// GRID batch slices x KSPLIT kidx-tile groups = workgroups (256: one per CU).  Splitting
+// the kidx tiles (instead of more batch slices) keeps the fp32 partial workspace
+// [GRID][N][K] -- and the reduce that reads it -- small.
+template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_, int KSPLIT_>
 struct WG {
   static constexpr int H = H_, W = W_, C = C_, KH = KH_, KW = KW_, S = S_, N = N_, GRID = GRID_;
+  static constexpr int KSPLIT = KSPLIT_;
   static constexpr int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1, P = OH * OW;
   static constexpr int K = KH * KW * C;
   static constexpr int KT = K / 32;            // 32-wide kidx tiles
@@ -182,20 +186,63 @@ struct WG {
   static constexpr int KS = (P + 15) / 16;     // pixel k-steps
   static constexpr int PPAD = KS * 16;
   static constexpr int PIX = (C == 4) ? 8 : (C * 2 + 16);
-  static constexpr int X_BYTES = H * W * PIX;
+  // C == 4 (the u8 frame stack): 8-B pixels plus 16 B of padding after every 16 pixels,
+  // so the staging threads' 128-B runs land on distinct banks (conflict-free b128 writes)
+  static constexpr int X_BYTES = (C == 4) ? H * W * PIX + (H * W / 16) * 16 : H * W * PIX;
   static constexpr int DYROW = N * 2 + 16;
   static constexpr int DY_BYTES = PPAD * DYROW;
-  static constexpr int KTW = (KT + 3) / 4;     // kidx tiles per wave
+  static constexpr int KTB = (KT + KSPLIT - 1) / KSPLIT;  // kidx tiles per workgroup
+  static constexpr int KTW = (KTB + 3) / 4;               // kidx tiles per wave
 };
-using WG1 = WG<84, 84, 4, 8, 8, 4, 32, 128>;
-using WG2 = WG<20, 20, 32, 4, 4, 2, 64, 64>;
-using WG3 = WG<9, 9, 64, 3, 3, 1, 64, 64>;
+using WG1 = WG<84, 84, 4, 8, 8, 4, 32, 128, 2>;
+using WG2 = WG<20, 20, 32, 4, 4, 2, 64, 64, 4>;
+using WG3 = WG<9, 9, 64, 3, 3, 1, 64, 64, 4>;
+
+// LDS byte address of input pixel `pix` in the wgrad x tile
+template <class G>
+__device__ __forceinline__ int x_pix_off(int pix) {
+  if constexpr (G::C == 4) return pix * G::PIX + (pix >> 4) * 16;
+  else return pix * G::PIX;
+}
+
+// Frame stack -> padded NHWC bf16 (16 pixels per thread-chunk, 16-B pad after each chunk),
+// split into a register prefetch (4 planes x <= 2 groups per thread) and an LDS commit.
+template <class G>
+__device__ __forceinline__ void frames_load(const FrameSrc& f, int b, Pf8& p) {
+  constexpr int HW = G::H * G::W, GROUPS = HW / 16;
+  static_assert(GROUPS <= 512, "two 16-pixel groups per thread");
+  const uint4* p0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, HW));
+  const uint4* p1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, HW));
+  const uint4* p2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, HW));
+  const uint4* p3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, HW));
+  const int g0 = threadIdx.x, g1 = threadIdx.x + 256;
+  auto ld = [](const uint4* q, int i) { return reinterpret_cast<const u32v4*>(q)[i]; };
+  p.r0 = ld(p0, g0); p.r1 = ld(p1, g0); p.r2 = ld(p2, g0); p.r3 = ld(p3, g0);
+  const int g1c = g1 < GROUPS ? g1 : GROUPS - 1;  // always assigned (stores are guarded)
+  p.r4 = ld(p0, g1c); p.r5 = ld(p1, g1c); p.r6 = ld(p2, g1c); p.r7 = ld(p3, g1c);
+}
+
+template <class G>
+__device__ __forceinline__ void frames_store(const Pf8& p, char* xs) {
+  constexpr int GROUPS = G::H * G::W / 16;
+  const int g0 = threadIdx.x, g1 = threadIdx.x + 256;
+  uint4* d = reinterpret_cast<uint4*>(xs + g0 * 144);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    u8x4words_to_lds(p.r0[k], p.r1[k], p.r2[k], p.r3[k], d + 2 * k);
+  if (g1 < GROUPS) {
+    d = reinterpret_cast<uint4*>(xs + g1 * 144);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      u8x4words_to_lds(p.r4[k], p.r5[k], p.r6[k], p.r7[k], d + 2 * k);
+  }
+}
 
 // LDS byte offset of kidx tile kt's column-block origin relative to an output pixel's window
 template <class G>
 __device__ __forceinline__ int kt_origin(int kt) {
   if constexpr (G::C == 4) {
-    return kt * G::W * G::PIX;  // tile = kernel row ky (8 taps x 4 channels contiguous)
+    return kt * G::W;  // PIXEL delta: tile = kernel row ky (8 taps x 4 channels); see x_pix_off
   } else {
     constexpr int CB = G::C / 32;
     const int tap = kt / CB, c0 = (kt % CB) * 32;
@@ -204,15 +251,30 @@ __device__ __forceinline__ int kt_origin(int kt) {
 }
 
 template <class G>
+__device__ __forceinline__ void wg_issue(const void* __restrict__ x, const FrameSrc& fs,
+                                         const uint16_t* __restrict__ dy, int bb, Pf8& px, Pf8& pd) {
+  if constexpr (G::C == 4) {
+    frames_load<G>(fs, bb, px);
+  } else {
+    pf_load<G::H * G::W * G::C / 8>(px, reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(x) +
+                                                                       (size_t)bb * G::H * G::W * G::C * 2));
+  }
+  pf_load<G::P * G::N / 8>(pd, reinterpret_cast<const uint4*>(dy + (size_t)bb * G::P * G::N));
+}
+
+template <class G>
 __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
-                                               const uint16_t* __restrict__ dy, int B, float* __restrict__ partial,
-                                               float* __restrict__ bias_partial) {
+                                               const uint16_t* __restrict__ dy, int B, int gridb,
+                                               float* __restrict__ partial, float* __restrict__ bias_partial) {
   __shared__ __attribute__((aligned(16))) char smem[G::X_BYTES + G::DY_BYTES];
   char* xs = smem;
   char* dys = smem + G::X_BYTES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
   const int colsel = 16 * (g & 1) + 4 * pp;  // column (within a 32-wide tile) this lane addresses
+  const int bg = blockIdx.x / G::KSPLIT, kg = blockIdx.x % G::KSPLIT;
+  const int kt0 = kg * G::KTB;
+  const bool do_bias = kg == 0;  // block-uniform: one kidx group owns the bias gradient
   // zero the padded dy rows once (they stay zero)
   for (int q = threadIdx.x; q < (G::PPAD - G::P) * G::DYROW / 16; q += blockDim.x)
     reinterpret_cast<uint4*>(dys + G::P * G::DYROW)[q] = uint4{0, 0, 0, 0};
@@ -225,38 +287,40 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   for (int a = 0; a < G::NT; ++a)
 #pragma unroll
     for (int k = 0; k < G::KTW; ++k) acc[a][k] = f32x16{};
-  for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    __syncthreads();
-    // stage x (as the forward does: padded NHWC bf16; u8 frames read in place from the
-    // frame ring and converted on the fly) and dy (rows of N channels, padded)
+  // register prefetch: the next sample's x and dy loads are in flight during this
+  // sample's MFMA loop (one LDS buffer; committed after the compute)
+  constexpr int XCH = (G::C == 4) ? 0 : G::H * G::W * G::C / 8;
+  constexpr int DCH = G::P * G::N / 8;
+  Pf8 px, pd;
+  if (bg < B) wg_issue<G>(x, fs, dy, bg, px, pd);
+  for (int b = bg; b < B; b += gridb) {
+    __syncthreads();  // the previous sample's compute is done with LDS
     if constexpr (G::C == 4) {
-      stage_frames_bf16<G::H * G::W>(fs, b, xs);
+      frames_store<G>(px, xs);
     } else {
       constexpr int CH16 = G::C / 8;
-      stage_chunks<G::H * G::W * CH16>(
-          reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(x) + (size_t)b * G::H * G::W * G::C * 2), xs,
-          [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
+      pf_store<XCH>(px, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
     }
     {
       constexpr int CH16 = G::N / 8;
-      stage_chunks<G::P * CH16>(reinterpret_cast<const uint4*>(dy + (size_t)b * G::P * G::N), dys,
-                                [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
+      pf_store<DCH>(pd, dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
     }
     __syncthreads();
-    for (int r = brow; r < G::P; r += RG)
-      bacc += bf2f(*reinterpret_cast<const uint16_t*>(dys + r * G::DYROW + bcol * 2));
+    if (b + gridb < B) wg_issue<G>(x, fs, dy, b + gridb, px, pd);  // block-uniform
+    if (do_bias)
+      for (int r = brow; r < G::P; r += RG)
+        bacc += bf2f(*reinterpret_cast<const uint16_t*>(dys + r * G::DYROW + bcol * 2));
 #pragma unroll 1
     for (int ks = 0; ks < G::KS; ++ks) {
       // pixel rows addressed by this lane for the two tr reads: kk = 8h + 4t + q4
-      int prow[2];
-      const char* xrow[2];
+      int prow[2], xpix[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int p = ks * 16 + 8 * h + 4 * t + q4;
         prow[t] = p;
         const int pc = p < G::P ? p : G::P - 1;
         const int oy = pc / G::OW, ox = pc % G::OW;
-        xrow[t] = xs + ((G::S * oy) * G::W + G::S * ox) * G::PIX;
+        xpix[t] = (G::S * oy) * G::W + G::S * ox;
       }
       bf16x8 afr[G::NT];
 #pragma unroll
@@ -268,11 +332,19 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
       }
 #pragma unroll
       for (int k = 0; k < G::KTW; ++k) {
-        const int kt = wave + 4 * k;
-        if (kt < G::KT) {
-          const int o = kt_origin<G>(kt) + colsel * 2;
-          const bf16x4 lo = tr_read(xrow[0] + o);
-          const bf16x4 hi = tr_read(xrow[1] + o);
+        const int kl = wave + 4 * k;
+        const int kt = kt0 + kl;
+        if (kl < G::KTB && kt < G::KT) {
+          bf16x4 lo, hi;
+          if constexpr (G::C == 4) {  // 32-k tile = 8 pixels x 4 channels of kernel row kt
+            const int dp = kt_origin<G>(kt) + colsel / 4;
+            lo = tr_read(xs + x_pix_off<G>(xpix[0] + dp));
+            hi = tr_read(xs + x_pix_off<G>(xpix[1] + dp));
+          } else {
+            const int o = kt_origin<G>(kt) + colsel * 2;
+            lo = tr_read(xs + xpix[0] * G::PIX + o);
+            hi = tr_read(xs + xpix[1] * G::PIX + o);
+          }
           const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
           for (int nt = 0; nt < G::NT; ++nt)
@@ -281,7 +353,7 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
       }
     }
   }
-  {  // fixed-order combine of the bias partial sums (reuse the x tile region of LDS)
+  if (do_bias) {  // fixed-order combine of the bias partial sums (reuse the x tile region of LDS)
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
     red[threadIdx.x] = bacc;
@@ -289,18 +361,19 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
     if (threadIdx.x < G::N) {
       float t = 0.f;
       for (int k = 0; k < RG; ++k) t += red[k * G::N + threadIdx.x];
-      bias_partial[(size_t)blockIdx.x * G::N + threadIdx.x] = t;
+      bias_partial[(size_t)bg * G::N + threadIdx.x] = t;
     }
   }
-  // partial[blk][n][kidx]: C/D map row = n (A rows), col = kidx (B cols)
-  float* out = partial + (size_t)blockIdx.x * G::N * G::K;
+  // partial[bg][n][kidx]: C/D map row = n (A rows), col = kidx (B cols)
+  float* out = partial + (size_t)bg * G::N * G::K;
   const int hh = lane >> 5, col = lane & 31;
 #pragma unroll
   for (int nt = 0; nt < G::NT; ++nt)
 #pragma unroll
     for (int k = 0; k < G::KTW; ++k) {
-      const int kt = wave + 4 * k;
-      if (kt < G::KT) {
+      const int kl = wave + 4 * k;
+      const int kt = kt0 + kl;
+      if (kl < G::KTB && kt < G::KT) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int n = nt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -346,10 +419,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ 
 template <class G>
 static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, int B, float* ws, float* grad,
                          float* bias_grad, hipStream_t s) {
-  const int grid = std::min(G::GRID, B);
+  const int grid = std::min(G::GRID, B);  // batch slices; x KSPLIT kidx groups
   float* partial = ws;
   float* bpart = ws + (size_t)G::GRID * G::N * G::K;
-  wgrad_k<G><<<grid, 256, 0, s>>>(x, fs, dy, B, partial, bpart);
+  wgrad_k<G><<<grid * G::KSPLIT, 256, 0, s>>>(x, fs, dy, B, grid, partial, bpart);
   LAUNCH_CHECK();
   const int total = G::N * G::K + G::N;
   wgrad_reduce_k<<<(total + 63) / 64, 256, 0, s>>>(partial, bpart, grid, G::N, G::C, G::KH, G::KW, grad, bias_grad);
