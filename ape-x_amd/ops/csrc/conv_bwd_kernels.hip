@@ -263,6 +263,85 @@ __device__ __forceinline__ void wg_issue(const void* __restrict__ x, const Frame
 }
 
 template <class G>
+struct WgFrags {
+  bf16x8 a[G::NT];   // dy^T fragments (rows n, k = 16 pixels)
+  bf16x8 b[G::KTW];  // im2col x fragments (k = 16 pixels, cols kidx)
+};
+
+// Fragments of pixel k-step ks: rows p = 16 ks + 8 h + 4 t + q4 for the two tr reads t
+template <class G>
+__device__ __forceinline__ void wg_frags(const char* xs, const char* dys, int ks, int h, int q4, int colsel,
+                                         int wave, int kt0, WgFrags<G>& f) {
+  int prow[2], xpix[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int p = ks * 16 + 8 * h + 4 * t + q4;
+    prow[t] = p;
+    const int pc = p < G::P ? p : G::P - 1;
+    const int oy = pc / G::OW, ox = pc % G::OW;
+    xpix[t] = (G::S * oy) * G::W + G::S * ox;
+  }
+#pragma unroll
+  for (int nt = 0; nt < G::NT; ++nt) {
+    const int coff = (nt * 32 + colsel) * 2;
+    const bf16x4 lo = tr_read(dys + prow[0] * G::DYROW + coff);
+    const bf16x4 hi = tr_read(dys + prow[1] * G::DYROW + coff);
+    f.a[nt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+#pragma unroll
+  for (int k = 0; k < G::KTW; ++k) {
+    const int kl = wave + 4 * k;
+    const int kt = kt0 + kl;
+    if (kl < G::KTB && kt < G::KT) {
+      bf16x4 lo, hi;
+      if constexpr (G::C == 4) {  // 32-k tile = 8 pixels x 4 channels of kernel row kt
+        const int dp = kt_origin<G>(kt) + colsel / 4;
+        lo = tr_read(xs + x_pix_off<G>(xpix[0] + dp));
+        hi = tr_read(xs + x_pix_off<G>(xpix[1] + dp));
+      } else {
+        const int o = kt_origin<G>(kt) + colsel * 2;
+        lo = tr_read(xs + xpix[0] * G::PIX + o);
+        hi = tr_read(xs + xpix[1] * G::PIX + o);
+      }
+      f.b[k] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void wg_mfma(const WgFrags<G>& f, int wave, int kt0, f32x16 (&acc)[G::NT][G::KTW]) {
+#pragma unroll
+  for (int k = 0; k < G::KTW; ++k) {
+    const int kl = wave + 4 * k;
+    if (kl < G::KTB && kt0 + kl < G::KT) {
+#pragma unroll
+      for (int nt = 0; nt < G::NT; ++nt)
+        acc[nt][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[nt], f.b[k], acc[nt][k], 0, 0, 0);
+    }
+  }
+}
+
+// bias gradient from the prefetched dy registers: chunk q = 8 channels (group q % (N/8))
+// of pixel q / (N/8); a thread's chunks all have group t % (N/8)
+template <class G>
+__device__ __forceinline__ void wg_bias_acc(const Pf8& pd, float (&bs)[8]) {
+  constexpr int DCH = G::P * G::N / 8;
+  const int t = threadIdx.x;
+#define APEX_WG_BIAS(K, R)                                     \
+  if constexpr (K * 256 < DCH) {                               \
+    if (t + K * 256 < DCH) {                                   \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j) {          \
+        const uint32_t w = pd.R[j];                            \
+        bs[2 * j] += __uint_as_float(w << 16);                 \
+        bs[2 * j + 1] += __uint_as_float(w & 0xFFFF0000u);     \
+      }                                                        \
+    }                                                          \
+  }
+  APEX_PF_SLOTS(APEX_WG_BIAS)
+#undef APEX_WG_BIAS
+}
+
+template <class G>
 __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
                                                const uint16_t* __restrict__ dy, int B, int gridb,
                                                float* __restrict__ partial, float* __restrict__ bias_partial) {
@@ -278,10 +357,7 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   // zero the padded dy rows once (they stay zero)
   for (int q = threadIdx.x; q < (G::PPAD - G::P) * G::DYROW / 16; q += blockDim.x)
     reinterpret_cast<uint4*>(dys + G::P * G::DYROW)[q] = uint4{0, 0, 0, 0};
-  // bias gradient = column sums of dy; thread t owns column t % N and rows = t / N (mod RG)
-  constexpr int RG = 256 / G::N;
-  const int bcol = threadIdx.x % G::N, brow = threadIdx.x / G::N;
-  float bacc = 0.f;
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 acc[G::NT][G::KTW];
 #pragma unroll
   for (int a = 0; a < G::NT; ++a)
@@ -305,63 +381,34 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
       constexpr int CH16 = G::N / 8;
       pf_store<DCH>(pd, dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
     }
+    if (do_bias) wg_bias_acc<G>(pd, bs);
     __syncthreads();
     if (b + gridb < B) wg_issue<G>(x, fs, dy, b + gridb, px, pd);  // block-uniform
-    if (do_bias)
-      for (int r = brow; r < G::P; r += RG)
-        bacc += bf2f(*reinterpret_cast<const uint16_t*>(dys + r * G::DYROW + bcol * 2));
+    // software-pipelined pixel k-steps: fragments of ks + 1 are read while ks multiplies
+    WgFrags<G> f0, f1;
+    wg_frags<G>(xs, dys, 0, h, q4, colsel, wave, kt0, f0);
 #pragma unroll 1
-    for (int ks = 0; ks < G::KS; ++ks) {
-      // pixel rows addressed by this lane for the two tr reads: kk = 8h + 4t + q4
-      int prow[2], xpix[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int p = ks * 16 + 8 * h + 4 * t + q4;
-        prow[t] = p;
-        const int pc = p < G::P ? p : G::P - 1;
-        const int oy = pc / G::OW, ox = pc % G::OW;
-        xpix[t] = (G::S * oy) * G::W + G::S * ox;
-      }
-      bf16x8 afr[G::NT];
-#pragma unroll
-      for (int nt = 0; nt < G::NT; ++nt) {
-        const int coff = (nt * 32 + colsel) * 2;
-        const bf16x4 lo = tr_read(dys + prow[0] * G::DYROW + coff);
-        const bf16x4 hi = tr_read(dys + prow[1] * G::DYROW + coff);
-        afr[nt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int k = 0; k < G::KTW; ++k) {
-        const int kl = wave + 4 * k;
-        const int kt = kt0 + kl;
-        if (kl < G::KTB && kt < G::KT) {
-          bf16x4 lo, hi;
-          if constexpr (G::C == 4) {  // 32-k tile = 8 pixels x 4 channels of kernel row kt
-            const int dp = kt_origin<G>(kt) + colsel / 4;
-            lo = tr_read(xs + x_pix_off<G>(xpix[0] + dp));
-            hi = tr_read(xs + x_pix_off<G>(xpix[1] + dp));
-          } else {
-            const int o = kt_origin<G>(kt) + colsel * 2;
-            lo = tr_read(xs + xpix[0] * G::PIX + o);
-            hi = tr_read(xs + xpix[1] * G::PIX + o);
-          }
-          const bf16x8 bfr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-          for (int nt = 0; nt < G::NT; ++nt)
-            acc[nt][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afr[nt], bfr, acc[nt][k], 0, 0, 0);
-        }
+    for (int ks = 0; ks < G::KS; ks += 2) {
+      if (ks + 1 < G::KS) wg_frags<G>(xs, dys, ks + 1, h, q4, colsel, wave, kt0, f1);
+      wg_mfma<G>(f0, wave, kt0, acc);
+      if (ks + 1 < G::KS) {
+        if (ks + 2 < G::KS) wg_frags<G>(xs, dys, ks + 2, h, q4, colsel, wave, kt0, f0);
+        wg_mfma<G>(f1, wave, kt0, acc);
       }
     }
   }
-  if (do_bias) {  // fixed-order combine of the bias partial sums (reuse the x tile region of LDS)
+  if (do_bias) {  // fixed-order combine of the per-thread bias sums (reuse the x tile region of LDS)
+    constexpr int NG = G::N / 8;  // channel groups; thread t owns group t % NG
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
-    red[threadIdx.x] = bacc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = bs[j];
     __syncthreads();
     if (threadIdx.x < G::N) {
+      const int n = threadIdx.x, grp = n / 8, j = n % 8;
       float t = 0.f;
-      for (int k = 0; k < RG; ++k) t += red[k * G::N + threadIdx.x];
-      bias_partial[(size_t)bg * G::N + threadIdx.x] = t;
+      for (int src = grp; src < 256; src += NG) t += red[src * 8 + j];
+      bias_partial[(size_t)bg * G::N + n] = t;
     }
   }
   // partial[bg][n][kidx]: C/D map row = n (A rows), col = kidx (B cols)
