@@ -231,27 +231,103 @@ struct Pf8 {
 
 #define APEX_PF_SLOTS(X) X(0, r0) X(1, r1) X(2, r2) X(3, r3) X(4, r4) X(5, r5) X(6, r6) X(7, r7)
 
-template <int TOTAL>
+// pf_load / pf_store: chunks q = t + 256 (BASE + K), K = 0..7, of a TOTAL-chunk copy
+template <int TOTAL, int BASE = 0>
 __device__ __forceinline__ void pf_load(Pf8& p, const uint4* __restrict__ src4) {
-  static_assert(TOTAL <= 8 * 256, "Pf8 holds at most 2048 chunks per workgroup");
+  static_assert(TOTAL <= 32 * 256, "at most 4 Pf8 blocks per copy");
   const u32v4* src = reinterpret_cast<const u32v4*>(src4);
   const int t = threadIdx.x;
 #define APEX_PF_LD(K, R) \
-  if constexpr (K * 256 < TOTAL) p.R = src[min(t + K * 256, TOTAL - 1)];  /* always assigned */
+  if constexpr ((BASE + K) * 256 < TOTAL) p.R = src[min(t + (BASE + K) * 256, TOTAL - 1)];  /* always assigned */
   APEX_PF_SLOTS(APEX_PF_LD)
 #undef APEX_PF_LD
 }
 
-template <int TOTAL, class DstOff>
+template <int TOTAL, int BASE = 0, class DstOff>
 __device__ __forceinline__ void pf_store(const Pf8& p, char* dst, DstOff dst_off) {
   const int t = threadIdx.x;
 #define APEX_PF_ST(K, R) \
-  if constexpr (K * 256 < TOTAL) {                                  \
-    if ((K + 1) * 256 <= TOTAL || t + K * 256 < TOTAL)              \
-      *reinterpret_cast<u32v4*>(dst + dst_off(t + K * 256)) = p.R;  \
+  if constexpr ((BASE + K) * 256 < TOTAL) {                                     \
+    const int q = t + (BASE + K) * 256;                                         \
+    if (((BASE + K) + 1) * 256 <= TOTAL || q < TOTAL)                           \
+      *reinterpret_cast<u32v4*>(dst + dst_off(q)) = p.R;                        \
   }
   APEX_PF_SLOTS(APEX_PF_ST)
 #undef APEX_PF_ST
+}
+
+// Global -> LDS copy of TOTAL 16-byte chunks with every load of the copy issued before
+// the first LDS store (up to 32 per thread in flight, named vector registers): the
+// latency is paid once per copy, not once per round of loads.
+template <int TOTAL, class DstOff>
+__device__ __forceinline__ void stage_all(const uint4* __restrict__ src, char* dst, DstOff dst_off) {
+  Pf8 a, b, c, d;
+  pf_load<TOTAL, 0>(a, src);
+  if constexpr (TOTAL > 8 * 256) pf_load<TOTAL, 8>(b, src);
+  if constexpr (TOTAL > 16 * 256) pf_load<TOTAL, 16>(c, src);
+  if constexpr (TOTAL > 24 * 256) pf_load<TOTAL, 24>(d, src);
+  pf_store<TOTAL, 0>(a, dst, dst_off);
+  if constexpr (TOTAL > 8 * 256) pf_store<TOTAL, 8>(b, dst, dst_off);
+  if constexpr (TOTAL > 16 * 256) pf_store<TOTAL, 16>(c, dst, dst_off);
+  if constexpr (TOTAL > 24 * 256) pf_store<TOTAL, 24>(d, dst, dst_off);
+}
+
+}  // namespace apex
+
+namespace apex {
+
+// ---------------------------------------------------------------- ReLU-backward mask
+// keep bf16 element of v where the matching element of m (a post-ReLU activation) is > 0
+__device__ __forceinline__ uint32_t relu_mask_bf16x2(uint32_t v, uint32_t m) {
+  const uint32_t lo = ((m & 0xFFFFu) != 0u && !(m & 0x8000u)) ? 0x0000FFFFu : 0u;
+  const uint32_t hi = ((m >> 16) != 0u && !(m & 0x80000000u)) ? 0xFFFF0000u : 0u;
+  return v & (lo | hi);
+}
+
+__device__ __forceinline__ u32v4 relu_mask_chunk(u32v4 v, u32v4 m) {
+  return u32v4{relu_mask_bf16x2(v[0], m[0]), relu_mask_bf16x2(v[1], m[1]), relu_mask_bf16x2(v[2], m[2]),
+               relu_mask_bf16x2(v[3], m[3])};
+}
+
+// mask every prefetched chunk of p by the matching chunk of m (same TOTAL / BASE geometry)
+template <int TOTAL, int BASE = 0>
+__device__ __forceinline__ void pf_mask(Pf8& p, const Pf8& m) {
+#define APEX_PF_MK(K, R) \
+  if constexpr ((BASE + K) * 256 < TOTAL) p.R = relu_mask_chunk(p.R, m.R);
+  APEX_PF_SLOTS(APEX_PF_MK)
+#undef APEX_PF_MK
+}
+
+// ---------------------------------------------------------------- MFMA tile epilogue
+// Store a 32x32 fp32 MFMA tile (C/D map: row = (r&3) + 8(r>>2) + 4h, col = lane&31) as bf16
+// rows of 64 contiguous bytes through a per-wave LDS scratch (32 x 80 B): 16 two-byte LDS
+// writes + 2 coalesced 16-byte global stores per lane instead of 16 strided 2-byte global
+// stores.  cvt(r, row, v) -> bf16 bits; row_ptr(row) -> destination of the 32-column row
+// (nullptr: skip).  Wave-synchronous (LDS ops of one wave complete in order).
+constexpr int TILE_EP_PITCH = 80;
+constexpr int TILE_EP_BYTES = 32 * TILE_EP_PITCH;
+
+template <class Acc, class Cvt, class RowPtr>
+__device__ __forceinline__ void tile_store_bf16(const Acc& acc, char* ep, Cvt cvt, RowPtr row_ptr) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+    *reinterpret_cast<uint16_t*>(ep + row * TILE_EP_PITCH + col * 2) = cvt(r, row, acc[r]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int id = lane + 64 * i, row = id >> 2, ch = id & 3;
+    const u32v4 v = *reinterpret_cast<const u32v4*>(ep + row * TILE_EP_PITCH + ch * 16);
+    uint16_t* dst = row_ptr(row);
+    if (dst) *reinterpret_cast<u32v4*>(dst + ch * 8) = v;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();  // the scratch is reused by the wave's next tile
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace apex

@@ -39,12 +39,29 @@ __device__ __forceinline__ bool bf16_pos(uint16_t v) { return v != 0 && !(v & 0x
 constexpr int DY_PIX = 144;
 
 template <int OH, int OW, int TH, int TW, int BORDER>
-__device__ __forceinline__ void stage_dy_padded(const uint16_t* __restrict__ dy, char* t) {
+__device__ __forceinline__ int dy_pad_off(int q) {
   constexpr int CH = 8;  // 16-byte chunks per pixel (64 channels)
-  stage_chunks<OH * OW * CH>(reinterpret_cast<const uint4*>(dy), t, [](int q) {
-    const int pix = q / CH, cc = q % CH;
-    return ((pix / OW + BORDER) * TW + pix % OW + BORDER) * DY_PIX + cc * 16;
-  });
+  const int pix = q / CH, cc = q % CH;
+  return ((pix / OW + BORDER) * TW + pix % OW + BORDER) * DY_PIX + cc * 16;
+}
+
+// Stage a [OH][OW][64] bf16 dy tile into a zero-bordered LDS grid; with `mask` (the
+// post-ReLU activation of the same shape) the ReLU backward is applied on the way in
+// (coalesced 16-B reads of both, instead of a strided gather in a producer's epilogue).
+template <int OH, int OW, int TH, int TW, int BORDER>
+__device__ __forceinline__ void stage_dy_padded(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ mask,
+                                                char* t) {
+  constexpr int TOTAL = OH * OW * 8;
+  static_assert(TOTAL <= 8 * 256, "one Pf8 block");
+  auto off = [](int q) { return dy_pad_off<OH, OW, TH, TW, BORDER>(q); };
+  Pf8 v;
+  pf_load<TOTAL>(v, reinterpret_cast<const uint4*>(dy));
+  if (mask) {  // block-uniform
+    Pf8 m;
+    pf_load<TOTAL>(m, reinterpret_cast<const uint4*>(mask));
+    pf_mask<TOTAL>(v, m);
+  }
+  pf_store<TOTAL>(v, t, off);
 }
 
 template <int ROWS>
@@ -56,24 +73,28 @@ __device__ __forceinline__ void zero_lds(char* t) {
 template <int TAPS, int C>
 __device__ __forceinline__ void stage_wt(const uint16_t* __restrict__ wt, char* t) {
   constexpr int CH = 8;
-  stage_chunks<TAPS * C * CH>(reinterpret_cast<const uint4*>(wt), t,
-                              [](int q) { return (q / CH) * DY_PIX + (q % CH) * 16; });
+  stage_all<TAPS * C * CH>(reinterpret_cast<const uint4*>(wt), t,
+                           [](int q) { return (q / CH) * DY_PIX + (q % CH) * 16; });
 }
 
-// conv3 dgrad: dy3 [B][49][64] -> dy2 = (dx2 * (a2 > 0)) [B][81][64]
-__global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ wt3,
-                                                const uint16_t* __restrict__ a2, uint16_t* __restrict__ dy2, int B) {
+// conv3 dgrad: dy3 [B][49][64] (already ReLU-masked) -> dx2 [B][81][64] (raw; the
+// consumers apply the a2 mask when they stage it)
+__global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ mask3,
+                                                const uint16_t* __restrict__ wt3, uint16_t* __restrict__ dx2, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 7x7 grid + 2-pixel border
   constexpr int SPW = 2;
-  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX];
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX + 4 * TILE_EP_BYTES];
   char* wts = smem + SPW * TILE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  char* ep = wts + 9 * 64 * DY_PIX + wave * TILE_EP_BYTES;
   zero_lds<SPW * T * T>(smem);
   stage_wt<9, 64>(wt3, wts);
   for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
     __syncthreads();
     for (int sw = 0; sw < SPW; ++sw)
-      if (b0 + sw < B) stage_dy_padded<7, 7, T, T, 2>(dy3 + (size_t)(b0 + sw) * 49 * 64, smem + sw * TILE);
+      if (b0 + sw < B)
+        stage_dy_padded<7, 7, T, T, 2>(dy3 + (size_t)(b0 + sw) * 49 * 64,
+                                       mask3 ? mask3 + (size_t)(b0 + sw) * 49 * 64 : nullptr, smem + sw * TILE);
     __syncthreads();
     // items: (sample, m-tile of 32 input pixels (3), n-tile of 32 channels (2)) = 12
     for (int it = wave; it < SPW * 6; it += 4) {
@@ -94,32 +115,34 @@ __global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3
         const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 64 * DY_PIX + n0 * 2);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
-      const int c = nt * 32 + r32;
-      const uint16_t* ab = a2 + (size_t)b * 81 * 64 + c;
-      uint16_t* ob = dy2 + (size_t)b * 81 * 64 + c;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qq = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (qq < 81) ob[qq * 64] = bf16_pos(ab[qq * 64]) ? f2bf(acc[r]) : (uint16_t)0;
-      }
+      uint16_t* ob = dx2 + (size_t)b * 81 * 64 + nt * 32;
+      tile_store_bf16(acc, ep, [](int, int, float v) { return f2bf(v); },
+                      [&](int row) -> uint16_t* {
+                        const int qq = mt * 32 + row;
+                        return qq < 81 ? ob + qq * 64 : nullptr;
+                      });
     }
   }
 }
 
-// conv2 dgrad (sub-pixel): dy2 [B][81][64] -> dy1 = (dx1 * (a1 > 0)) [B][400][32]
-__global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ wt2,
-                                                const uint16_t* __restrict__ a1, uint16_t* __restrict__ dy1, int B) {
+// conv2 dgrad (sub-pixel): dy2 = dx2 * (a2 > 0) (masked while staging) -> dx1 [B][400][32]
+// (raw; wgrad1 applies the a1 mask when it stages it)
+__global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dx2, const uint16_t* __restrict__ mask2,
+                                                const uint16_t* __restrict__ wt2, uint16_t* __restrict__ dx1, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 9x9 grid + 1-pixel border
   constexpr int SPW = 2;
-  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX];
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX + 4 * TILE_EP_BYTES];
   char* wts = smem + SPW * TILE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  char* ep = wts + 16 * 32 * DY_PIX + wave * TILE_EP_BYTES;
   zero_lds<SPW * T * T>(smem);
   stage_wt<16, 32>(wt2, wts);
   for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
     __syncthreads();
     for (int sw = 0; sw < SPW; ++sw)
-      if (b0 + sw < B) stage_dy_padded<9, 9, T, T, 1>(dy2 + (size_t)(b0 + sw) * 81 * 64, smem + sw * TILE);
+      if (b0 + sw < B)
+        stage_dy_padded<9, 9, T, T, 1>(dx2 + (size_t)(b0 + sw) * 81 * 64,
+                                       mask2 ? mask2 + (size_t)(b0 + sw) * 81 * 64 : nullptr, smem + sw * TILE);
     __syncthreads();
     // items: (sample, parity class (4), m-tile of 32 class pixels (4 -> 128 >= 100)) = 32
     for (int it = wave; it < SPW * 16; it += 4) {
@@ -142,29 +165,26 @@ __global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dy2
         const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 32 * DY_PIX + n0 * 2);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
-      const int c = r32;
-      const uint16_t* ab = a1 + (size_t)b * 400 * 32 + c;
-      uint16_t* ob = dy1 + (size_t)b * 400 * 32 + c;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (mm < 100) {
-          const int q = (2 * (mm / 10) + ry) * 20 + 2 * (mm % 10) + rx;
-          ob[q * 32] = bf16_pos(ab[q * 32]) ? f2bf(acc[r]) : (uint16_t)0;
-        }
-      }
+      uint16_t* ob = dx1 + (size_t)b * 400 * 32;
+      tile_store_bf16(acc, ep, [](int, int, float v) { return f2bf(v); },
+                      [&](int row) -> uint16_t* {
+                        const int mm = mt * 32 + row;
+                        if (mm >= 100) return nullptr;
+                        const int q = (2 * (mm / 10) + ry) * 20 + 2 * (mm % 10) + rx;
+                        return ob + q * 32;
+                      });
     }
   }
 }
 
-void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* wt, const uint16_t* act_below, uint16_t* dy_below,
-                int B, hipStream_t s) {
+void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const uint16_t* wt, uint16_t* dx, int B,
+                hipStream_t s) {
   if (B <= 0) return;
   const int grid = std::min((B + 1) / 2, 512);
   if (layer == 3) {
-    dgrad3_k<<<grid, 256, 0, s>>>(dy, wt, act_below, dy_below, B);
+    dgrad3_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, B);
   } else if (layer == 2) {
-    dgrad2_k<<<grid, 256, 0, s>>>(dy, wt, act_below, dy_below, B);
+    dgrad2_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, B);
   } else {
     throw std::invalid_argument("conv_dgrad: layer must be 2 or 3");
   }
@@ -252,7 +272,8 @@ __device__ __forceinline__ int kt_origin(int kt) {
 
 template <class G>
 __device__ __forceinline__ void wg_issue(const void* __restrict__ x, const FrameSrc& fs,
-                                         const uint16_t* __restrict__ dy, int bb, Pf8& px, Pf8& pd) {
+                                         const uint16_t* __restrict__ dy, const uint16_t* __restrict__ mask, int bb,
+                                         Pf8& px, Pf8& pd, Pf8& pm) {
   if constexpr (G::C == 4) {
     frames_load<G>(fs, bb, px);
   } else {
@@ -260,6 +281,7 @@ __device__ __forceinline__ void wg_issue(const void* __restrict__ x, const Frame
                                                                        (size_t)bb * G::H * G::W * G::C * 2));
   }
   pf_load<G::P * G::N / 8>(pd, reinterpret_cast<const uint4*>(dy + (size_t)bb * G::P * G::N));
+  if (mask) pf_load<G::P * G::N / 8>(pm, reinterpret_cast<const uint4*>(mask + (size_t)bb * G::P * G::N));
 }
 
 template <class G>
@@ -343,7 +365,8 @@ __device__ __forceinline__ void wg_bias_acc(const Pf8& pd, float (&bs)[8]) {
 
 template <class G>
 __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
-                                               const uint16_t* __restrict__ dy, int B, int gridb,
+                                               const uint16_t* __restrict__ dy, const uint16_t* __restrict__ mask,
+                                               int B, int gridb,
                                                float* __restrict__ partial, float* __restrict__ bias_partial) {
   __shared__ __attribute__((aligned(16))) char smem[G::X_BYTES + G::DY_BYTES];
   char* xs = smem;
@@ -367,8 +390,8 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   // sample's MFMA loop (one LDS buffer; committed after the compute)
   constexpr int XCH = (G::C == 4) ? 0 : G::H * G::W * G::C / 8;
   constexpr int DCH = G::P * G::N / 8;
-  Pf8 px, pd;
-  if (bg < B) wg_issue<G>(x, fs, dy, bg, px, pd);
+  Pf8 px, pd, pm;
+  if (bg < B) wg_issue<G>(x, fs, dy, mask, bg, px, pd, pm);
   for (int b = bg; b < B; b += gridb) {
     __syncthreads();  // the previous sample's compute is done with LDS
     if constexpr (G::C == 4) {
@@ -379,11 +402,12 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
     }
     {
       constexpr int CH16 = G::N / 8;
+      if (mask) pf_mask<DCH>(pd, pm);  // ReLU backward of the layer output, applied at staging
       pf_store<DCH>(pd, dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
     }
     if (do_bias) wg_bias_acc<G>(pd, bs);
     __syncthreads();
-    if (b + gridb < B) wg_issue<G>(x, fs, dy, b + gridb, px, pd);  // block-uniform
+    if (b + gridb < B) wg_issue<G>(x, fs, dy, mask, b + gridb, px, pd, pm);  // block-uniform
     // software-pipelined pixel k-steps: fragments of ks + 1 are read while ks multiplies
     WgFrags<G> f0, f1;
     wg_frags<G>(xs, dys, 0, h, q4, colsel, wave, kt0, f0);
@@ -464,12 +488,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_k(const float* __restrict__ 
 }
 
 template <class G>
-static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, int B, float* ws, float* grad,
-                         float* bias_grad, hipStream_t s) {
+static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, const uint16_t* mask, int B, float* ws,
+                         float* grad, float* bias_grad, hipStream_t s) {
   const int grid = std::min(G::GRID, B);  // batch slices; x KSPLIT kidx groups
   float* partial = ws;
   float* bpart = ws + (size_t)G::GRID * G::N * G::K;
-  wgrad_k<G><<<grid * G::KSPLIT, 256, 0, s>>>(x, fs, dy, B, grid, partial, bpart);
+  wgrad_k<G><<<grid * G::KSPLIT, 256, 0, s>>>(x, fs, dy, mask, B, grid, partial, bpart);
   LAUNCH_CHECK();
   const int total = G::N * G::K + G::N;
   wgrad_reduce_k<<<(total + 63) / 64, 256, 0, s>>>(partial, bpart, grid, G::N, G::C, G::KH, G::KW, grad, bias_grad);
@@ -485,14 +509,14 @@ size_t wgrad_workspace_floats(int layer) {
   }
 }
 
-void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const uint16_t* dy, int B, float* workspace,
-                float* grad, float* bias_grad, hipStream_t s) {
+void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const uint16_t* dy, const uint16_t* dy_mask,
+                int B, float* workspace, float* grad, float* bias_grad, hipStream_t s) {
   if (B <= 0) return;
   const FrameSrc fs{reinterpret_cast<const uint8_t*>(x), ids, idx};
   switch (layer) {
-    case 1: launch_wgrad<WG1>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
-    case 2: launch_wgrad<WG2>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
-    case 3: launch_wgrad<WG3>(x, fs, dy, B, workspace, grad, bias_grad, s); break;
+    case 1: launch_wgrad<WG1>(x, fs, dy, dy_mask, B, workspace, grad, bias_grad, s); break;
+    case 2: launch_wgrad<WG2>(x, fs, dy, dy_mask, B, workspace, grad, bias_grad, s); break;
+    case 3: launch_wgrad<WG3>(x, fs, dy, dy_mask, B, workspace, grad, bias_grad, s); break;
     default: throw std::invalid_argument("conv_wgrad: layer must be 1, 2 or 3");
   }
 }

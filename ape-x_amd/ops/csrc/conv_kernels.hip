@@ -54,14 +54,14 @@ __device__ __forceinline__ void stage_input(const void* __restrict__ in, const F
     constexpr int CH16 = G::C / 8;  // 16-byte chunks per pixel
     const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(in) +
                                                       (size_t)b * G::H * G::W * G::C * 2);
-    stage_chunks<G::H * G::W * CH16>(src, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
+    stage_all<G::H * G::W * CH16>(src, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
   }
 }
 
 template <class G>
 __device__ __forceinline__ void stage_weights(const uint16_t* __restrict__ wp, char* ws) {
   constexpr int CH16 = G::K / 8;
-  stage_chunks<G::N * CH16>(reinterpret_cast<const uint4*>(wp), ws,
+  stage_all<G::N * CH16>(reinterpret_cast<const uint4*>(wp), ws,
                             [](int q) { return (q / CH16) * G::W_ROW + (q % CH16) * 16; });
 }
 

@@ -233,14 +233,15 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("u8_to_bf16_nhwc", [](uint64_t in, uint64_t out, int B, int HW, uint64_t s) {
     u8_to_bf16_nhwc(P<const uint8_t>(in), P<uint16_t>(out), B, HW, S(s));
   });
-  m.def("conv_dgrad", [](int layer, uint64_t dy, uint64_t wt, uint64_t act, uint64_t out, int B, uint64_t s) {
-    conv_dgrad(layer, P<const uint16_t>(dy), P<const uint16_t>(wt), P<const uint16_t>(act), P<uint16_t>(out), B, S(s));
+  m.def("conv_dgrad", [](int layer, uint64_t dy, uint64_t dy_mask, uint64_t wt, uint64_t dx, int B, uint64_t s) {
+    conv_dgrad(layer, P<const uint16_t>(dy), P<const uint16_t>(dy_mask), P<const uint16_t>(wt), P<uint16_t>(dx), B,
+               S(s));
   });
   m.def("wgrad_workspace_floats", &wgrad_workspace_floats);
-  m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, int B, uint64_t ws,
-                         uint64_t grad, uint64_t bgrad, uint64_t s) {
-    conv_wgrad(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const uint16_t>(dy), B, P<float>(ws),
-               P<float>(grad), P<float>(bgrad), S(s));
+  m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t dy_mask, int B,
+                         uint64_t ws, uint64_t grad, uint64_t bgrad, uint64_t s) {
+    conv_wgrad(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const uint16_t>(dy),
+               P<const uint16_t>(dy_mask), B, P<float>(ws), P<float>(grad), P<float>(bgrad), S(s));
   });
   m.def("pack_conv_wt", [](uint64_t src, uint64_t dst, int N, int C, int KH, int KW, uint64_t s) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));

@@ -128,9 +128,10 @@ def _rand_bf16(shape, dev, scale=1.0, g=None):
     return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16).to(dev)
 
 
-@pytest.mark.parametrize("layer", [1, 2, 3])
-def test_wgrad_kernel_matches_torch(cuda, layer):
-    """MFMA weight/bias gradient vs torch fp32 on identical bf16-valued operands."""
+@pytest.mark.parametrize("layer,masked", [(1, False), (2, False), (3, False), (1, True), (2, True)])
+def test_wgrad_kernel_matches_torch(cuda, layer, masked):
+    """MFMA weight/bias gradient vs torch fp32 on identical bf16-valued operands (with the
+    optional ReLU mask of dy applied while staging)."""
     from apex_amd import ops
 
     hip = ops.hip()
@@ -147,12 +148,14 @@ def test_wgrad_kernel_matches_torch(cuda, layer):
         x_f = x_nhwc.float().permute(0, 3, 1, 2)
         xptr = x_nhwc.data_ptr()
     dy = _rand_bf16((B, OH, OH, N), cuda, 0.1, g)
+    mask = _rand_bf16((B, OH, OH, N), cuda, 1.0, g) if masked else None
     ws = torch.empty(hip.wgrad_workspace_floats(layer), device=cuda)
     gw = torch.empty(N, C, KS, KS, device=cuda)
     gb = torch.empty(N, device=cuda)
-    hip.conv_wgrad(layer, xptr, 0, 0, dy.data_ptr(), B, ws.data_ptr(), gw.data_ptr(), gb.data_ptr(),
-                   torch.cuda.current_stream().cuda_stream)
-    dy_f = dy.float().permute(0, 3, 1, 2)
+    hip.conv_wgrad(layer, xptr, 0, 0, dy.data_ptr(), 0 if mask is None else mask.data_ptr(), B, ws.data_ptr(),
+                   gw.data_ptr(), gb.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    dy_eff = dy.float() if mask is None else dy.float() * (mask.float() > 0)
+    dy_f = dy_eff.permute(0, 3, 1, 2)
     ref_w = torch.nn.grad.conv2d_weight(x_f, (N, C, KS, KS), dy_f, stride=S)
     ref_b = dy_f.sum((0, 2, 3))
     torch.testing.assert_close(gw, ref_w, rtol=2e-3, atol=2e-3 * ref_w.abs().max().item())
@@ -161,7 +164,8 @@ def test_wgrad_kernel_matches_torch(cuda, layer):
 
 @pytest.mark.parametrize("layer", [2, 3])
 def test_dgrad_kernel_matches_torch(cuda, layer):
-    """MFMA input gradient (+ fused ReLU backward) vs torch fp32."""
+    """MFMA input gradient vs torch fp32; dy is ReLU-masked by its activation while staged
+    and the raw input gradient is written."""
     from apex_amd import ops
 
     hip = ops.hip()
@@ -173,11 +177,12 @@ def test_dgrad_kernel_matches_torch(cuda, layer):
     s = torch.cuda.current_stream().cuda_stream
     hip.pack_conv_wt(w.data_ptr(), wt.data_ptr(), N, C, KS, KS, s)
     dy = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)
-    act = _rand_bf16((B, H, H, C), cuda, 1.0, g)  # ~half positive: exercises the mask
+    act = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)  # ~half positive: exercises the mask
     out = torch.empty(B, H, H, C, dtype=torch.bfloat16, device=cuda)
-    hip.conv_dgrad(layer, dy.data_ptr(), wt.data_ptr(), act.data_ptr(), out.data_ptr(), B, s)
-    ref = torch.nn.grad.conv2d_input((B, C, H, H), _bf(w), dy.float().permute(0, 3, 1, 2), stride=S)
-    ref = (ref.permute(0, 2, 3, 1) * (act.float() > 0)).to(torch.bfloat16).float()
+    hip.conv_dgrad(layer, dy.data_ptr(), act.data_ptr(), wt.data_ptr(), out.data_ptr(), B, s)
+    dy_m = dy.float() * (act.float() > 0)
+    ref = torch.nn.grad.conv2d_input((B, C, H, H), _bf(w), dy_m.permute(0, 3, 1, 2), stride=S)
+    ref = ref.permute(0, 2, 3, 1).to(torch.bfloat16).float()
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
 
 
