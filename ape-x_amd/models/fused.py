@@ -203,11 +203,11 @@ class HipDuelingNet:
         h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
         h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, wsp, f[4].weight.grad.data_ptr(),
                      f[4].bias.grad.data_ptr(), s)
-        # dgrad writes the RAW input gradient; each consumer applies the ReLU mask of the
-        # activation while staging it (coalesced), so ws.dy2 / ws.dy1 hold dx2 / dx1
-        h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), B, s)
-        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), ws.a2.data_ptr(), B, wsp,
-                     f[2].weight.grad.data_ptr(), f[2].bias.grad.data_ptr(), s)
-        h.conv_dgrad(2, ws.dy2.data_ptr(), ws.a2.data_ptr(), self.w2t.data_ptr(), ws.dy1.data_ptr(), B, s)
-        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), ws.a1.data_ptr(), B, wsp, f[0].weight.grad.data_ptr(),
+        # dgrad applies the ReLU backward of the layer below in its coalesced epilogue, so
+        # ws.dy2 / ws.dy1 hold the masked gradients every consumer reads as-is
+        h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
+        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, wsp, f[2].weight.grad.data_ptr(),
+                     f[2].bias.grad.data_ptr(), s)
+        h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
+        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, wsp, f[0].weight.grad.data_ptr(),
                      f[0].bias.grad.data_ptr(), s)

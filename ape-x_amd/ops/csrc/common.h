@@ -302,13 +302,16 @@ __device__ __forceinline__ void pf_mask(Pf8& p, const Pf8& m) {
 // Store a 32x32 fp32 MFMA tile (C/D map: row = (r&3) + 8(r>>2) + 4h, col = lane&31) as bf16
 // rows of 64 contiguous bytes through a per-wave LDS scratch (32 x 80 B): 16 two-byte LDS
 // writes + 2 coalesced 16-byte global stores per lane instead of 16 strided 2-byte global
-// stores.  cvt(r, row, v) -> bf16 bits; row_ptr(row) -> destination of the 32-column row
-// (nullptr: skip).  Wave-synchronous (LDS ops of one wave complete in order).
+// stores.  cvt(r, row, v) -> bf16 bits.  Wave-synchronous (LDS ops of one wave complete
+// in order).
 constexpr int TILE_EP_PITCH = 80;
 constexpr int TILE_EP_BYTES = 32 * TILE_EP_PITCH;
 
-template <class Acc, class Cvt, class RowPtr>
-__device__ __forceinline__ void tile_store_bf16(const Acc& acc, char* ep, Cvt cvt, RowPtr row_ptr) {
+template <class Acc, class Cvt, class RowOff>
+__device__ __forceinline__ void tile_store_bf16(const Acc& acc, char* ep, Cvt cvt, RowOff row_off, uint16_t* out,
+                                                const uint16_t* mask = nullptr) {
+  // row_off(row) -> element offset of the row in `out` (< 0: skip); `mask` (optional): a
+  // ReLU-backward mask with the layout of `out`, applied per 16-B chunk (coalesced read)
   const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -321,9 +324,12 @@ __device__ __forceinline__ void tile_store_bf16(const Acc& acc, char* ep, Cvt cv
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int id = lane + 64 * i, row = id >> 2, ch = id & 3;
-    const u32v4 v = *reinterpret_cast<const u32v4*>(ep + row * TILE_EP_PITCH + ch * 16);
-    uint16_t* dst = row_ptr(row);
-    if (dst) *reinterpret_cast<u32v4*>(dst + ch * 8) = v;
+    u32v4 v = *reinterpret_cast<const u32v4*>(ep + row * TILE_EP_PITCH + ch * 16);
+    const long off = row_off(row);
+    if (off >= 0) {
+      if (mask) v = relu_mask_chunk(v, *reinterpret_cast<const u32v4*>(mask + off + ch * 8));
+      *reinterpret_cast<u32v4*>(out + off + ch * 8) = v;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();  // the scratch is reused by the wave's next tile

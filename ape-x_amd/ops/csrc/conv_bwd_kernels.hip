@@ -77,10 +77,11 @@ __device__ __forceinline__ void stage_wt(const uint16_t* __restrict__ wt, char* 
                            [](int q) { return (q / CH) * DY_PIX + (q % CH) * 16; });
 }
 
-// conv3 dgrad: dy3 [B][49][64] (already ReLU-masked) -> dx2 [B][81][64] (raw; the
-// consumers apply the a2 mask when they stage it)
+// conv3 dgrad: dy3 [B][49][64] (already ReLU-masked) -> dx2 [B][81][64]; with out_mask
+// (= a2) the ReLU backward is applied in the coalesced epilogue (writes dy2)
 __global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ mask3,
-                                                const uint16_t* __restrict__ wt3, uint16_t* __restrict__ dx2, int B) {
+                                                const uint16_t* __restrict__ wt3, uint16_t* __restrict__ dx2,
+                                                const uint16_t* __restrict__ out_mask, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 7x7 grid + 2-pixel border
   constexpr int SPW = 2;
   __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX + 4 * TILE_EP_BYTES];
@@ -115,20 +116,21 @@ __global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3
         const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 64 * DY_PIX + n0 * 2);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
-      uint16_t* ob = dx2 + (size_t)b * 81 * 64 + nt * 32;
+      const long base = (long)b * 81 * 64 + nt * 32;
       tile_store_bf16(acc, ep, [](int, int, float v) { return f2bf(v); },
-                      [&](int row) -> uint16_t* {
+                      [&](int row) -> long {
                         const int qq = mt * 32 + row;
-                        return qq < 81 ? ob + qq * 64 : nullptr;
-                      });
+                        return qq < 81 ? base + qq * 64 : -1;
+                      }, dx2, out_mask);
     }
   }
 }
 
-// conv2 dgrad (sub-pixel): dy2 = dx2 * (a2 > 0) (masked while staging) -> dx1 [B][400][32]
-// (raw; wgrad1 applies the a1 mask when it stages it)
+// conv2 dgrad (sub-pixel): dy2 (optionally masked while staging) -> dx1 [B][400][32];
+// with out_mask (= a1) the ReLU backward is applied in the coalesced epilogue (writes dy1)
 __global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dx2, const uint16_t* __restrict__ mask2,
-                                                const uint16_t* __restrict__ wt2, uint16_t* __restrict__ dx1, int B) {
+                                                const uint16_t* __restrict__ wt2, uint16_t* __restrict__ dx1,
+                                                const uint16_t* __restrict__ out_mask, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 9x9 grid + 1-pixel border
   constexpr int SPW = 2;
   __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX + 4 * TILE_EP_BYTES];
@@ -165,26 +167,26 @@ __global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dx2
         const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + tap * 32 * DY_PIX + n0 * 2);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
-      uint16_t* ob = dx1 + (size_t)b * 400 * 32;
+      const long base = (long)b * 400 * 32;
       tile_store_bf16(acc, ep, [](int, int, float v) { return f2bf(v); },
-                      [&](int row) -> uint16_t* {
+                      [&](int row) -> long {
                         const int mm = mt * 32 + row;
-                        if (mm >= 100) return nullptr;
+                        if (mm >= 100) return -1;
                         const int q = (2 * (mm / 10) + ry) * 20 + 2 * (mm % 10) + rx;
-                        return ob + q * 32;
-                      });
+                        return base + q * 32;
+                      }, dx1, out_mask);
     }
   }
 }
 
-void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const uint16_t* wt, uint16_t* dx, int B,
-                hipStream_t s) {
+void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const uint16_t* wt, uint16_t* dx,
+                const uint16_t* dx_mask, int B, hipStream_t s) {
   if (B <= 0) return;
   const int grid = std::min((B + 1) / 2, 512);
   if (layer == 3) {
-    dgrad3_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, B);
+    dgrad3_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
   } else if (layer == 2) {
-    dgrad2_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, B);
+    dgrad2_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
   } else {
     throw std::invalid_argument("conv_dgrad: layer must be 2 or 3");
   }

@@ -233,9 +233,10 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("u8_to_bf16_nhwc", [](uint64_t in, uint64_t out, int B, int HW, uint64_t s) {
     u8_to_bf16_nhwc(P<const uint8_t>(in), P<uint16_t>(out), B, HW, S(s));
   });
-  m.def("conv_dgrad", [](int layer, uint64_t dy, uint64_t dy_mask, uint64_t wt, uint64_t dx, int B, uint64_t s) {
-    conv_dgrad(layer, P<const uint16_t>(dy), P<const uint16_t>(dy_mask), P<const uint16_t>(wt), P<uint16_t>(dx), B,
-               S(s));
+  m.def("conv_dgrad", [](int layer, uint64_t dy, uint64_t dy_mask, uint64_t wt, uint64_t dx, uint64_t dx_mask, int B,
+                         uint64_t s) {
+    conv_dgrad(layer, P<const uint16_t>(dy), P<const uint16_t>(dy_mask), P<const uint16_t>(wt), P<uint16_t>(dx),
+               P<const uint16_t>(dx_mask), B, S(s));
   });
   m.def("wgrad_workspace_floats", &wgrad_workspace_floats);
   m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t dy_mask, int B,

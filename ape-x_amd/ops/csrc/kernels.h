@@ -149,10 +149,10 @@ void relu_mask_bf16(const uint16_t* g, const uint16_t* a, uint16_t* out, int64_t
 void u8_to_bf16_nhwc(const uint8_t* in, uint16_t* out, int B, int HW, hipStream_t s);
 
 // ---- conv_bwd_kernels.hip
-// dgrad of layer 2/3 from dy (optionally ReLU-masked by dy_mask while staging); writes the
-// RAW input gradient dx (the layer below's consumers apply its mask)
-void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const uint16_t* wt, uint16_t* dx, int B,
-                hipStream_t s);
+// dgrad of layer 2/3: dy (optionally ReLU-masked by dy_mask while staging) -> dx,
+// optionally ReLU-masked by dx_mask in the (coalesced) epilogue
+void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const uint16_t* wt, uint16_t* dx,
+                const uint16_t* dx_mask, int B, hipStream_t s);
 size_t wgrad_workspace_floats(int layer);
 void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const uint16_t* dy, const uint16_t* dy_mask,
                 int B, float* workspace, float* grad, float* bias_grad, hipStream_t s);

@@ -58,12 +58,13 @@ cases = {
                                        ws.q.data_ptr(), B, 18, s),
     "wgrad3": lambda: hip.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, wsp,
                                      f[4].weight.grad.data_ptr(), f[4].bias.grad.data_ptr(), s),
-    "dgrad3": lambda: hip.conv_dgrad(3, ws.dy3.data_ptr(), 0, net.w3t.data_ptr(), ws.dy2.data_ptr(), B, s),
-    "wgrad2": lambda: hip.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), ws.a2.data_ptr(), B, wsp,
+    "dgrad3": lambda: hip.conv_dgrad(3, ws.dy3.data_ptr(), 0, net.w3t.data_ptr(), ws.dy2.data_ptr(),
+                                     ws.a2.data_ptr(), B, s),
+    "wgrad2": lambda: hip.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, wsp,
                                      f[2].weight.grad.data_ptr(), f[2].bias.grad.data_ptr(), s),
-    "dgrad2": lambda: hip.conv_dgrad(2, ws.dy2.data_ptr(), ws.a2.data_ptr(), net.w2t.data_ptr(), ws.dy1.data_ptr(),
-                                     B, s),
-    "wgrad1": lambda: hip.conv_wgrad(1, x.data_ptr(), 0, 0, ws.dy1.data_ptr(), ws.a1.data_ptr(), B, wsp,
+    "dgrad2": lambda: hip.conv_dgrad(2, ws.dy2.data_ptr(), 0, net.w2t.data_ptr(), ws.dy1.data_ptr(),
+                                     ws.a1.data_ptr(), B, s),
+    "wgrad1": lambda: hip.conv_wgrad(1, x.data_ptr(), 0, 0, ws.dy1.data_ptr(), 0, B, wsp,
                                      f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr(), s),
 }
 flops = {"conv1": 2 * 3.28e6, "conv2": 2 * 2.65e6, "conv3": 2 * 1.81e6}

@@ -164,8 +164,8 @@ def test_wgrad_kernel_matches_torch(cuda, layer, masked):
 
 @pytest.mark.parametrize("layer", [2, 3])
 def test_dgrad_kernel_matches_torch(cuda, layer):
-    """MFMA input gradient vs torch fp32; dy is ReLU-masked by its activation while staged
-    and the raw input gradient is written."""
+    """MFMA input gradient vs torch fp32, with both optional ReLU masks (dy while staged,
+    the output in the epilogue)."""
     from apex_amd import ops
 
     hip = ops.hip()
@@ -177,12 +177,13 @@ def test_dgrad_kernel_matches_torch(cuda, layer):
     s = torch.cuda.current_stream().cuda_stream
     hip.pack_conv_wt(w.data_ptr(), wt.data_ptr(), N, C, KS, KS, s)
     dy = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)
-    act = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)  # ~half positive: exercises the mask
+    act = _rand_bf16((B, OH, OH, N), cuda, 1.0, g)  # ~half positive: exercises the input mask
+    act_below = _rand_bf16((B, H, H, C), cuda, 1.0, g)  # epilogue (output) mask
     out = torch.empty(B, H, H, C, dtype=torch.bfloat16, device=cuda)
-    hip.conv_dgrad(layer, dy.data_ptr(), act.data_ptr(), wt.data_ptr(), out.data_ptr(), B, s)
+    hip.conv_dgrad(layer, dy.data_ptr(), act.data_ptr(), wt.data_ptr(), out.data_ptr(), act_below.data_ptr(), B, s)
     dy_m = dy.float() * (act.float() > 0)
     ref = torch.nn.grad.conv2d_input((B, C, H, H), _bf(w), dy_m.permute(0, 3, 1, 2), stride=S)
-    ref = ref.permute(0, 2, 3, 1).to(torch.bfloat16).float()
+    ref = (ref.permute(0, 2, 3, 1) * (act_below.float() > 0)).to(torch.bfloat16).float()
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
 
 
