@@ -120,6 +120,7 @@ __global__ __launch_bounds__(256, 1) void conv1_fwd_k(FrameSrc fs, const uint16_
                                                       const float* __restrict__ bias, uint16_t* __restrict__ out,
                                                       int B) {
   __shared__ __attribute__((aligned(16))) char smem[2][C1_STAGE];
+  __shared__ __attribute__((aligned(16))) char eps[4][TILE_EP_BYTES];  // per-wave epilogue scratch
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
   // B operand (weights, reference layout [n][c][ky][kx] = [n][k]): lane holds column n = r32,
   // k = 16 s + 8 h + j, for all 16 k-steps -- the whole B stays in 64 VGPRs
@@ -165,13 +166,12 @@ __global__ __launch_bounds__(256, 1) void conv1_fwd_k(FrameSrc fs, const uint16_
 #pragma unroll
       for (int s = 0; s < 16; ++s)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ar[s]), wb[s], acc, 0, 0, 0);
-      uint16_t* ob = out + (size_t)b * C1_P * C1_N + r32;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int pp = mt * 32 + row;
-        if (pp < C1_P) ob[(size_t)pp * C1_N] = f2bf(fmaxf(acc[r] + bn, 0.f));
-      }
+      const long base = (long)b * C1_P * C1_N;
+      tile_store_bf16(acc, eps[wave], [bn](int, int, float v) { return f2bf(fmaxf(v + bn, 0.f)); },
+                      [&](int row) -> long {
+                        const int pp = mt * 32 + row;
+                        return pp < C1_P ? base + (long)pp * C1_N : -1;
+                      }, out);
     }
     tile0 = (tile0 + 4 * ((C1_MT - tile0 + 3) / 4)) - C1_MT;  // next sample continues the rotation
     if (more) store_sample(smem[stage ^ 1], v);

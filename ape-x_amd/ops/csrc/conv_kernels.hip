@@ -42,7 +42,7 @@ using Conv1 = ConvGeo<84, 84, 4, 8, 8, 4, 32>;
 using Conv2 = ConvGeo<20, 20, 32, 4, 4, 2, 64>;
 using Conv3 = ConvGeo<9, 9, 64, 3, 3, 1, 64>;
 static_assert(Conv1::P == 400 && Conv2::P == 81 && Conv3::P == 49, "Nature-CNN geometry");
-static_assert(Conv1::LDS <= 160 * 1024 && Conv2::LDS <= 160 * 1024 && Conv3::LDS <= 160 * 1024, "LDS");
+static_assert(Conv2::LDS + 4 * TILE_EP_BYTES <= 160 * 1024 && Conv3::LDS + 4 * TILE_EP_BYTES <= 160 * 1024, "LDS");
 
 // Stage one sample's input into LDS as padded NHWC bf16 (blockDim must be 256).
 template <class G, bool U8IN>
@@ -83,9 +83,10 @@ template <class G, bool U8IN>
 __global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, FrameSrc fs,
                                                   const uint16_t* __restrict__ wp, const float* __restrict__ bias,
                                                   uint16_t* __restrict__ out, int B) {
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS];
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS + 4 * TILE_EP_BYTES];
   char* ws = smem + G::SPW * G::X_BYTES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  char* ep = smem + G::LDS + wave * TILE_EP_BYTES;  // per-wave epilogue scratch
   stage_weights<G>(wp, ws);
   for (int b0 = blockIdx.x * G::SPW; b0 < B; b0 += gridDim.x * G::SPW) {
     __syncthreads();
@@ -115,15 +116,13 @@ __global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, F
         const bf16x8 bb = *reinterpret_cast<const bf16x8*>(bbase + 32 * s);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bb, acc, 0, 0, 0);
       }
-      const int n = nt * 32 + r32;
-      const float bn = bias[n];
-      uint16_t* ob = out + (size_t)b * G::P * G::N + n;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int pp = mt * 32 + row;
-        if (pp < G::P) ob[(size_t)pp * G::N] = f2bf(fmaxf(acc[r] + bn, 0.f));
-      }
+      const float bn = bias[nt * 32 + r32];
+      const long base = (long)b * G::P * G::N + nt * 32;
+      tile_store_bf16(acc, ep, [bn](int, int, float v) { return f2bf(fmaxf(v + bn, 0.f)); },
+                      [&](int row) -> long {
+                        const int pp = mt * 32 + row;
+                        return pp < G::P ? base + (long)pp * G::N : -1;
+                      }, out);
     }
   }
 }
