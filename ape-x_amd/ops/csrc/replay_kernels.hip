@@ -135,6 +135,96 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
   }
 }
 
+// ------------------------------------------------------------------ fused small updates
+// Node recompute by one wave, reading through L2 (the children may have been written by
+// other waves of this workgroup earlier in the same kernel).
+__device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int node, int lane) {
+  const int child = node * kTreeFanout + lane;
+  const int csize = t.size[level - 1];
+  double s = 0.0;
+  float m = INFINITY;
+  if (child < csize) {
+    if (level == 1) {
+      s = (double)__hip_atomic_load(t.leaf_sum + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      m = __hip_atomic_load(t.leaf_min + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      s = __hip_atomic_load(t.node_sum[level - 2] + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      m = __hip_atomic_load(t.node_min[level - 2] + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  s = wave_sum(s);
+  m = wave_min(m);
+  if (lane == 0) {
+    t.node_sum[level - 1][node] = s;
+    t.node_min[level - 1][node] = m;
+  }
+}
+
+// Recompute levels lo..hi of the dirty paths of `ids` (run order, staged in LDS) inside
+// ONE workgroup: each wave checks 64 candidates at once (lane-parallel run detection,
+// ballot) and recomputes the first-of-run nodes; level-synchronous via the barrier.
+__device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int* sids, int B, int lo, int hi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int level = lo; level <= hi; ++level) {
+    __threadfence();
+    __syncthreads();
+    const int shift = kTreeLog2Fanout * level;
+    for (int base = wave * 64; base < B; base += nw * 64) {  // wave-uniform
+      const int w = base + lane;
+      const int id = w < B ? sids[w] : -1;
+      const bool ok = id >= 0 && id < t.size[0];
+      const int node = ok ? id >> shift : -1;
+      bool first = ok;
+      if (ok && w > 0) {
+        const int prev = sids[w - 1];
+        if (prev >= 0 && prev < t.size[0] && (prev >> shift) == node) first = false;
+      }
+      unsigned long long m = __ballot(first);
+      while (m) {
+        const int k = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        recompute_node(t, level, __shfl(node, k, 64), lane);
+      }
+    }
+  }
+}
+
+// Actor inserts: B (<= 1024) unique ring-ordered slots -> leaves AND every level in one
+// launch (a ring chunk dirties only a handful of nodes per level).
+__global__ __launch_bounds__(1024) void per_write_ring_fused_k(TreeDesc t, const int* __restrict__ idx,
+                                                               const float* __restrict__ prio, int B, float alpha,
+                                                               float* max_prio, int64_t* bump0, int64_t d0,
+                                                               int64_t* bump1, int64_t d1) {
+  __shared__ int sids[1024];
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const int id = idx[i];
+    sids[i] = id;
+    if (id < 0 || id >= t.size[0]) continue;
+    const float p = prio ? prio[i] : *max_prio;
+    if (p > 0.f && isfinite(p)) {
+      const float v = powf(p, alpha);
+      t.leaf_sum[id] = v;
+      t.leaf_min[id] = v;
+      if (prio) atomic_max_pos_float(max_prio, p);
+    } else {
+      t.leaf_sum[id] = 0.f;
+      t.leaf_min[id] = INFINITY;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (bump0) *bump0 += d0;
+    if (bump1) *bump1 += d1;
+  }
+  update_levels_block(t, sids, B, 1, t.levels);
+}
+
+// The small top levels of a batched (random-slot) update in one workgroup.
+__global__ __launch_bounds__(1024) void per_update_top_k(TreeDesc t, const int* __restrict__ ids, int B, int lo) {
+  __shared__ int sids[1024];
+  for (int i = threadIdx.x; i < B; i += blockDim.x) sids[i] = ids[i];
+  update_levels_block(t, sids, B, lo, t.levels);
+}
+
 // ------------------------------------------------------------------ stratified sampling
 // One wave per sample: mass_i = (u_i + i) * total / B, descend levels with a wave-wide
 // inclusive scan of the 64 child sums; IS weight = (p_i / p_min)^-beta
@@ -239,6 +329,9 @@ void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int 
                                                   d1);
     LAUNCH_CHECK();
     per_update_levels(t, sorted_scratch, B, s);
+  } else if (B <= 1024) {
+    per_write_ring_fused_k<<<1, 1024, 0, s>>>(t, idx, prio, B, alpha, max_prio, bump0, d0, bump1, d1);
+    LAUNCH_CHECK();
   } else {
     per_write_leaves_k<<<(B + 255) / 256, 256, 0, s>>>(t, idx, prio, B, alpha, max_prio, bump0, d0, bump1, d1);
     LAUNCH_CHECK();
@@ -246,12 +339,20 @@ void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int 
   }
 }
 
+// Random-slot batches: one wide launch per level while the level is big, then the
+// remaining top levels (<= 64 nodes each) in a single workgroup launch.
 void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) {
   if (B <= 0) return;
   const int waves_per_block = 4;
   const int grid = (B + waves_per_block - 1) / waves_per_block;
-  for (int level = 1; level <= t.levels; ++level) {
+  int level = 1;
+  for (; level <= t.levels; ++level) {
+    if (level > 1 && t.size[level] <= 64 && B <= 1024) break;
     per_update_level_k<<<grid, 64 * waves_per_block, 0, s>>>(t, idx, B, level);
+    LAUNCH_CHECK();
+  }
+  if (level <= t.levels) {
+    per_update_top_k<<<1, 1024, 0, s>>>(t, idx, B, level);
     LAUNCH_CHECK();
   }
 }

@@ -43,6 +43,31 @@ def test_tree_write_update_dedup(cuda):
     assert rp.total_priority() == pytest.approx(leaf.astype(np.float64).sum(), rel=1e-12)
 
 
+def test_tree_ring_writes_fused(cuda):
+    """Actor-style unique ring-ordered chunks (incl. the wrap) take the single-launch path
+    (leaves + every level in one workgroup); tree must equal the fp64 oracle."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C, E = 70000, 256
+    rp = HBMReplay(C, n_envs=E, device=cuda, alpha=1.0)
+    rng = np.random.RandomState(3)
+    host = np.zeros(C)
+    start = C - 3 * E + 17  # the 4th chunk wraps around the ring end
+    for k in range(9):
+        idx = ((start + k * E + np.arange(E)) % C).astype(np.int32)
+        pr = rng.uniform(0.0, 2.0, size=E).astype(np.float32)
+        pr[::11] = 0.0  # "no transition emitted": zero mass
+        host[idx] = pr
+        rp.write_priorities(torch.from_numpy(idx).to(cuda), torch.from_numpy(pr).to(cuda), dedup=False)
+    torch.cuda.synchronize()
+    leaf = rp.leaf_sum.cpu().numpy()
+    np.testing.assert_allclose(leaf, host, rtol=1e-6, atol=0)
+    levels = _tree_oracle(leaf, rp.level_sizes)
+    for k, t in enumerate(rp.node_sum):
+        np.testing.assert_allclose(t.cpu().numpy(), levels[k + 1], rtol=1e-12, atol=1e-9)
+    assert rp.min_priority() == pytest.approx(np.min(leaf[leaf > 0]), rel=1e-6)
+
+
 def test_sample_stratified_and_weights(cuda):
     from apex_amd.engine.hbm_replay import HBMReplay
 
