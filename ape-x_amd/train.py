@@ -1,0 +1,209 @@
+"""GPU-resident Ape-X training CLI: ``python -m apex_amd.train [arguments.py flags]``.
+
+The production entry point for the MI355X engine (one process per GPU).  It replaces
+the reference's replay.py + learner.py + N x actor.py deployment with
+one rank per GPU, launched directly (1 GPU) or under ``torch.distributed.run`` (any
+number of GPUs and nodes; RCCL over xGMI inside a node):
+
+* ``--topology sharded`` (default for N > 1): every rank runs an actor shard, its HBM
+  replay shard and a data-parallel learner replica; gradients are all-reduced and the
+  shards are sampled as one global prioritized buffer (``apex_amd.parallel.sharded``).
+* ``--topology central``: rank 0 is the learner with the one replay; ranks 1.. are
+  actor GPUs pushing experience over RCCL (``apex_amd.engine.central``).
+
+Reference cadences and tags are kept: target sync every ``--target_update_interval``
+(learner.py:163-165), weights published every ``--publish_param_interval``
+(learner.py:169-170), ``model.pth`` written every ``--save_interval`` (learner.py:166-168)
+plus a ``model.pth.train.pt`` sidecar (optimizer moments, step counters, target net)
+for a true resume (``--resume``), ``learner/loss``, ``learner/grad_norm``,
+``learner/BPS`` every ``--bps_interval`` (learner.py:151-175), ``actor/episode_reward``
+and ``actor/episode_length`` (actor.py:91-92), plus ``learner/steps_per_sec``,
+``actor/frames_per_sec`` and ``replay/size``.  The envs are the GPU
+synthetic Atari-shaped envs of ``ActorShard`` (no emulator in this image).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+from .config import args_to_config, build_parser, preset
+from .utils.checkpoint import save_model, sidecar_path
+
+
+def parser():
+    p = build_parser(preset("origin"), description="Ape-X DQN on MI355X (GPU-resident engine)")
+    p.add_argument("--actions", type=int, default=18, help="action count of the synthetic env (Seaquest: 18)")
+    p.add_argument("--actor-steps", type=int, default=1, help="actor steps per learner step")
+    p.add_argument("--save-path", default="model.pth")
+    p.add_argument("--resume", default=None, help="model.pth (+ .train.pt sidecar) to resume from")
+    p.add_argument("--log-dir", default=None, help="event-file directory (default runs/<time>-<env>-learner)")
+    p.add_argument("--no-tb", action="store_true")
+    p.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal with gloo)")
+    return p
+
+
+# ------------------------------------------------------------------ checkpoint
+def _learner_state(learner, counters: dict) -> dict:
+    return {"opt_s1": learner.opt_s1.cpu(), "opt_s2": learner.opt_s2.cpu(),
+            "step_counter": learner.step_counter.cpu(), "target_flat": learner.tflat.cpu(),
+            "counters": dict(counters)}
+
+
+def save_engine(learner, path: str, counters: dict) -> None:
+    """model.pth (the reference state_dict: enjoy.py / load_model read it) + sidecar."""
+    save_model(learner.model, path)
+    torch.save(_learner_state(learner, counters), sidecar_path(path))
+
+
+def load_engine(learner, path: str) -> dict:
+    """Load weights (+ sidecar if present) into a DQNLearner; returns the counters."""
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    learner.model.load_state_dict(sd)   # parameters are views of the flat buffer
+    counters = {}
+    side = sidecar_path(path)
+    if os.path.exists(side):
+        st = torch.load(side, map_location="cpu", weights_only=True)
+        learner.opt_s1.copy_(st["opt_s1"])
+        learner.opt_s2.copy_(st["opt_s2"])
+        learner.step_counter.copy_(st["step_counter"])
+        learner.tflat.copy_(st["target_flat"])
+        counters = dict(st.get("counters", {}))
+    else:
+        learner.tflat.copy_(learner.flat)
+    if getattr(learner, "hip_net", False):
+        learner.refresh_packed()
+        learner.tnet.repack()
+    return counters
+
+
+# ------------------------------------------------------------------ main
+def main(argv=None) -> int:
+    args = parser().parse_args(argv)
+    cfg = args_to_config(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("apex_amd.train runs the GPU engine; use apex_amd.trainers.* or the roles on CPU")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    backend = cfg.dist.backend if cfg.dist.backend != "auto" else "nccl"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {"device_id": device} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    topology = cfg.replay.topology if world > 1 else "single"
+
+    from .engine.apex import ApexEngine, EngineConfig
+    from .engine.learner import LearnerConfig
+
+    L, R = cfg.learner, cfg.replay
+    lc = LearnerConfig(batch_size=R.batch_size, n_step=cfg.n_steps, gamma=cfg.gamma, lr=L.lr, rms_alpha=L.rms_alpha,
+                       rms_eps=L.rms_eps, centered=L.centered, max_norm=L.max_norm, lr_gamma=L.lr_gamma,
+                       lr_step_size=L.lr_step_size, beta=R.beta, optimizer=L.optimizer, forward=cfg.kernel.forward,
+                       seed=cfg.seed + (rank if topology == "sharded" else 0))
+    E = cfg.actor.n_envs
+    ecfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=R.replay_buffer_size, alpha=R.alpha,
+                        threshold_size=R.threshold_size, actor_steps_per_learner_step=args.actor_steps,
+                        publish_param_interval=L.publish_param_interval,
+                        target_update_interval=L.target_update_interval, nstep_mode=cfg.actor.nstep_mode,
+                        eps_base=cfg.actor.eps_base, eps_alpha=cfg.actor.eps_alpha, exact_mass=R.exact_mass,
+                        use_graphs=cfg.kernel.use_graphs, seed=cfg.seed, learner=lc)
+    counters = {}
+    if topology == "central":
+        from .engine.central import CentralApexEngine
+
+        eng = CentralApexEngine(ecfg, device, rank, world)
+        learner = eng.learner if rank == 0 else None
+        if args.resume and rank == 0:
+            counters = load_engine(learner, args.resume)
+        if args.resume:
+            eng.broadcast_params()
+        n_actor_gpus = world - 1
+    else:
+        from .parallel.dp import FlatGradAllReduce
+
+        ecfg.actor_offset, ecfg.total_actors = rank * E, world * E
+        ecfg.seed = cfg.seed + 7919 * rank
+        eng = ApexEngine(ecfg, device, allreduce=FlatGradAllReduce(world) if world > 1 else None,
+                         sharded=world > 1)
+        learner = eng.learner
+        if args.resume:
+            counters = load_engine(learner, args.resume)
+        if world > 1:
+            from .parallel.broadcast import broadcast_flat
+
+            broadcast_flat(learner.flat, src=0)
+            broadcast_flat(learner.tflat, src=0)
+            learner.refresh_packed()
+            if learner.hip_net:
+                learner.tnet.repack()
+        eng.publish_params()
+        n_actor_gpus = world
+    start = int(counters.get("learn_steps", 0))
+    eng.learn_steps = start
+
+    writer = None
+    if rank == 0 and not args.no_tb:
+        from .utils.tb import SummaryWriter
+
+        writer = SummaryWriter(args.log_dir, comment=f"-{cfg.env.env}-learner")
+    t_fill = time.perf_counter()
+    eng.fill()
+    if cfg.kernel.use_graphs:
+        eng.capture()
+    torch.cuda.synchronize(device)
+    if rank == 0:
+        print(f"replay warm ({time.perf_counter() - t_fill:.1f}s); training from step {start}", flush=True)
+
+    max_step = int(L.max_step)
+    bps_every = max(1, L.bps_interval)
+    frames_per_round = n_actor_gpus * args.actor_steps * eng.frames_per_actor_step
+    t_last, step_last = time.perf_counter(), start
+    step = start
+    while not max_step or step < max_step:
+        eng.train_step()
+        step += 1
+        if step % bps_every == 0:
+            torch.cuda.synchronize(device)
+            now = time.perf_counter()
+            sps = (step - step_last) / (now - t_last)
+            t_last, step_last = now, step
+            if learner is not None and rank == 0:
+                st = learner.stats()
+                line = {"learner/loss": st["loss"], "learner/grad_norm": st["grad_norm"],
+                        "learner/grad_norm_l2": st["grad_norm_l2"], "learner/BPS": sps,
+                        "learner/steps_per_sec": sps * (world if topology == "sharded" else 1),
+                        "actor/frames_per_sec": sps * frames_per_round}
+                shard = getattr(eng, "actor", None)
+                if shard is not None:
+                    ret, length, count = shard.episode_stats()
+                    done = count > 0
+                    if bool(done.any()):
+                        line["actor/episode_reward"] = float(ret[done].mean())
+                        line["actor/episode_length"] = float(length[done].float().mean())
+                line["replay/size"] = float(len(eng.replay))
+                print(f"Step: {step} " + " ".join(f"{k}={v:.4g}" for k, v in line.items()), flush=True)
+                if writer is not None:
+                    for k, v in line.items():
+                        writer.add_scalar(k, v, step)
+        if L.save_interval and step % L.save_interval == 0 and rank == 0 and learner is not None:
+            print("Saving Model..", flush=True)
+            save_engine(learner, args.save_path, {"learn_steps": step, "actor_steps": eng.actor_steps})
+    torch.cuda.synchronize(device)
+    if rank == 0 and learner is not None:
+        save_engine(learner, args.save_path, {"learn_steps": step, "actor_steps": eng.actor_steps})
+    if writer is not None:
+        writer.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
