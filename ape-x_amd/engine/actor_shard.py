@@ -29,7 +29,7 @@ class ActorShard:
     def __init__(self, replay: HBMReplay, n_envs: int, n_actions: int, n_step: int = 3, gamma: float = 0.99,
                  eps_base: float = 0.4, eps_alpha: float = 7.0, actor_offset: int = 0, total_actors: int | None = None,
                  seed: int = 0, mode: str = "reference", clip_rewards: bool = True, episode_life: bool = True,
-                 max_episode_steps: int = 50000, action_repeat: int = 4):
+                 max_episode_steps: int = 50000, action_repeat: int = 4, staged: int = 0):
         self.hip = ops.hip()
         self.replay = replay
         self.E, self.A, self.n = int(n_envs), int(n_actions), int(n_step)
@@ -65,8 +65,22 @@ class ActorShard:
         }
         if mode not in ("reference", "textbook"):
             raise ValueError("mode must be 'reference' or 'textbook'")
-        self.nstep = self.hip.make_nstep(E, A, n, replay.capacity, float(gamma), 0 if mode == "reference" else 1,
-                                         {k: v.data_ptr() for k, v in self.st.items()}, replay.trans_ptrs())
+        st_ptrs = {k: v.data_ptr() for k, v in self.st.items()}
+        nmode = 0 if mode == "reference" else 1
+        self.nstep = self.hip.make_nstep(E, A, n, replay.capacity, float(gamma), nmode, st_ptrs, replay.trans_ptrs())
+        # staged mode (overlapped actor/learner streams): ``staged`` sets of [E] rows +
+        # slots + priorities; the learner stream applies one half while the actor fills
+        # the other
+        self.staged = int(staged)
+        if staged:
+            self.stage = [{"s_ids": torch.zeros(E, 4, **i32), "s2_ids": torch.zeros(E, 4, **i32),
+                           "action": torch.zeros(E, **i32), "reward": torch.zeros(E, **f32),
+                           "done": torch.zeros(E, **f32)} for _ in range(self.staged)]
+            self.stage_ptrs = [{k: v.data_ptr() for k, v in t.items()} for t in self.stage]
+            self.stage_nstep = [self.hip.make_nstep(E, A, n, replay.capacity, float(gamma), nmode, st_ptrs, sp,
+                                                    stage=1) for sp in self.stage_ptrs]
+            self.stage_slot = [torch.zeros(E, **i32) for _ in range(self.staged)]
+            self.stage_prio = [torch.zeros(E, **f32) for _ in range(self.staged)]
         self.env_params = self.hip.VecEnvParams(E, A, replay.frame_bytes, replay.frame_capacity, action_repeat,
                                                 int(clip_rewards), int(episode_life), int(max_episode_steps))
         self.reset()
@@ -85,9 +99,10 @@ class ActorShard:
         self.replay.gather_frames(self.st["hist"], self.obs)
         return self.obs
 
-    def act_and_step(self, q: torch.Tensor | None = None) -> None:
+    def act_and_step(self, q: torch.Tensor | None = None, parity: int | None = None) -> None:
         """Given Q for the current observations (in ``self.q`` or ``q``), act, step the
-        envs and push the emitted transitions into the replay."""
+        envs and push the emitted transitions into the replay (staged mode: into staging
+        set ``parity``; :meth:`apply_staged` moves them into the replay)."""
         if q is not None and q.data_ptr() != self.q.data_ptr():
             self.q.copy_(q)
         s = self._stream()
@@ -98,11 +113,27 @@ class ActorShard:
         h.vec_env_step(self.env_state.data_ptr(), self.actions.data_ptr(), self.seed, self.step_counter.data_ptr(),
                        self.replay.frames.data_ptr(), self.env_params, self.reward.data_ptr(), self.done.data_ptr(),
                        self.new_frame.data_ptr(), self.ep_log.data_ptr(), s)
+        if parity is not None:
+            assert 0 <= parity < self.staged, "staging set out of range"
+            h.nstep_emit(self.stage_nstep[parity], self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
+                         self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
+                         self.stage_slot[parity].data_ptr(), self.stage_prio[parity].data_ptr(), s)
+            self.step_counter.add_(1)
+            return
         h.nstep_emit(self.nstep, self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                      self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
                      self.slot.data_ptr(), self.prio.data_ptr(), s)
         self.replay.write_priorities(self.slot, self.prio, dedup=False,
                                      bumps=((self.step_counter, 1), (self.replay.filled, E)))
+
+    def apply_staged(self, parity: int) -> None:
+        """Scatter staging set ``parity`` into the replay tables and write its
+        priorities into the tree (the learner stream's half of a staged actor step)."""
+        self.hip.apply_staged_rows(self.stage_ptrs[parity], self.replay.trans_ptrs(),
+                                   self.stage_slot[parity].data_ptr(), self.stage_prio[parity].data_ptr(), self.E,
+                                   self._stream())
+        self.replay.write_priorities(self.stage_slot[parity], self.stage_prio[parity], dedup=False,
+                                     bumps=((self.replay.filled, self.E),))
 
     def step(self, policy) -> None:
         """One full actor step with ``policy(obs_u8) -> Q f32 [E, A]``."""

@@ -49,6 +49,7 @@ class EngineConfig:
     actor_offset: int = 0
     total_actors: int | None = None
     use_graphs: bool = True
+    overlap: bool = False                # actor graph on its own stream, concurrent with the learner
     exact_mass: bool = True
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
@@ -63,8 +64,11 @@ class ApexEngine:
         torch.manual_seed(cfg.seed)
         self.replay = HBMReplay(cfg.replay_capacity, cfg.n_envs, lc.n_step, cfg.alpha, self.device,
                                 exact_mass=cfg.exact_mass, seed=cfg.seed)
+        k = cfg.actor_steps_per_learner_step
+        self.overlap = bool(cfg.overlap)
         self.actor = ActorShard(self.replay, cfg.n_envs, cfg.n_actions, lc.n_step, lc.gamma, cfg.eps_base,
-                                cfg.eps_alpha, cfg.actor_offset, cfg.total_actors, cfg.seed, cfg.nstep_mode)
+                                cfg.eps_alpha, cfg.actor_offset, cfg.total_actors, cfg.seed, cfg.nstep_mode,
+                                staged=2 * k if self.overlap else 0)
         model = model if model is not None else DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions)
         self._sharded = None
         if sharded:
@@ -88,6 +92,12 @@ class ApexEngine:
         self._g_actor = self._g_learn_a = self._g_learn_b = None
         self._pool = None
         self._allreduce = allreduce
+        # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
+        # train step while the learner applies the other half (the previous step's)
+        self._half = 0
+        self._astream = torch.cuda.Stream(device=self.device) if self.overlap else None
+        self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()] if self.overlap else None
+        self._ev_learn = torch.cuda.Event() if self.overlap else None
 
     # ------------------------------------------------------------------ eager bodies
     def publish_params(self) -> None:
@@ -96,16 +106,28 @@ class ApexEngine:
         if self.hip_net:
             self.actor_net.copy_packed_from(self.learner.net)
 
-    def _actor_body(self):
+    def _actor_body(self, stage: int | None = None):
         if self.hip_net:  # conv1 reads the current stacks straight from the frame ring
             q = self.actor_net(self.replay.frames, self.actor_ws, self.actor.st["hist"])
         else:
             obs = self.actor.observe()
             with torch.no_grad():
                 q = forward_q(self.actor_model, obs)
-        self.actor.act_and_step(q)
+        self.actor.act_and_step(q, stage)
 
-    def _learn_a(self):
+    def _actor_half(self, half: int):
+        k = self.cfg.actor_steps_per_learner_step
+        for i in range(k):
+            self._actor_body(half * k + i)
+
+    def _apply_half(self, half: int):
+        k = self.cfg.actor_steps_per_learner_step
+        for i in range(k):
+            self.actor.apply_staged(half * k + i)
+
+    def _learn_a(self, apply_half: int | None = None):
+        if apply_half is not None and self._sharded is None:
+            self._apply_half(apply_half)  # sharded: applied before the mass exchange instead
         self.learner.sample_and_forward()
 
     def _learn_b(self):
@@ -113,7 +135,12 @@ class ApexEngine:
 
     # ------------------------------------------------------------------ graphs
     def capture(self, warmup_iters: int = 3) -> None:
-        """Warm up on a side stream, then capture actor and learner steps as hipGraphs."""
+        """Warm up on a side stream, then capture actor and learner steps as hipGraphs.
+        The warm-up iterations are real train steps and are counted as such."""
+        self.learn_steps += warmup_iters
+        self.actor_steps += warmup_iters * self.cfg.actor_steps_per_learner_step
+        if self.overlap:
+            return self._capture_overlap(warmup_iters)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -138,6 +165,86 @@ class ApexEngine:
         with torch.cuda.graph(self._g_learn_b, pool=self._pool):
             self._learn_b()
         torch.cuda.synchronize(self.device)
+
+    def _capture_overlap(self, warmup_iters: int) -> None:
+        """Overlap mode: graphs per staging half (actor: fill half h; learner: apply half
+        1-h, sample, forward, backward) + the optimizer graph.  Warm-up runs real
+        sequential train steps, keeping the one-step-behind staging invariant."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup_iters):
+                self._train_step_eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self._pool = torch.cuda.graph_pool_handle()
+        apool = torch.cuda.graph_pool_handle()  # actor graphs run concurrently: never share memory
+        self._g_actor, self._g_learn_a, self._g_apply = [], [], []
+        for h in (0, 1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=apool):
+                self._actor_half(h)
+            self._g_actor.append(g)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._pool):
+                self._learn_a(1 - h)
+            self._g_learn_a.append(g)
+            if self._sharded is not None:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._pool):
+                    self._apply_half(1 - h)
+                self._g_apply.append(g)
+        self._g_learn_b = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_learn_b, pool=self._pool):
+            self._learn_b()
+        torch.cuda.synchronize(self.device)
+        self._ev_learn.record(torch.cuda.current_stream(self.device))
+
+    def _train_step_eager(self) -> None:
+        """Overlap-mode semantics, run sequentially on the current stream."""
+        h = self._half
+        self._actor_half(h)
+        if self._sharded is not None:
+            self._apply_half(1 - h)
+            self._sharded.exchange()
+        self._learn_a(1 - h)
+        if self._allreduce is not None:
+            self._allreduce(self.learner.flat_grad)
+        self._learn_b()
+        self._half ^= 1
+
+    def _train_step_overlap(self) -> None:
+        """Actor half h on the actor stream || learner step on the current stream.
+
+        Ordering (events): actor step t waits for learner step t-1 (which applied the
+        staging half this actor step refills, and published weights); learner step t
+        waits for actor step t-1 (whose half it applies).  The frame ring's margin
+        ((2n+8)E frames beyond the transition capacity) keeps every frame the actor
+        overwrites unreferenced by any sampleable transition."""
+        h = self._half
+        L = torch.cuda.current_stream(self.device)
+        A = self._astream
+        A.wait_event(self._ev_learn)
+        with torch.cuda.stream(A):
+            self._g_actor[h].replay()
+        self._ev_actor[h].record(A)
+        L.wait_event(self._ev_actor[1 - h])
+        if self._sharded is not None:
+            self._g_apply[h].replay()
+            self._sharded.exchange()
+        self._g_learn_a[h].replay()
+        if self._allreduce is not None:
+            self._allreduce(self.learner.flat_grad)
+        self._g_learn_b.replay()
+        self.learn_steps += 1
+        self.actor_steps += self.cfg.actor_steps_per_learner_step
+        if self.learn_steps % self.cfg.publish_param_interval == 0:
+            L.wait_event(self._ev_actor[h])  # the actor is not reading its weights
+            self.publish_params()
+        if self.learn_steps % self.cfg.target_update_interval == 0:
+            self.learner.sync_target()
+        self._ev_learn.record(L)
+        self._half ^= 1
 
     # ------------------------------------------------------------------ steps
     def actor_step(self) -> None:
@@ -169,12 +276,34 @@ class ApexEngine:
     def fill(self, min_transitions: int | None = None) -> None:
         """Run actor steps until the replay holds ``threshold_size`` slots."""
         need = self.cfg.threshold_size if min_transitions is None else min_transitions
-        steps = -(-need // self.cfg.n_envs)
-        for _ in range(max(steps, 4)):
+        steps = max(-(-need // self.cfg.n_envs), 4)
+        if self.overlap:  # whole halves; the last one stays staged for the first learner step
+            k = self.cfg.actor_steps_per_learner_step
+            halves = max(2, -(-steps // k))
+            for i in range(halves):
+                self._actor_half(self._half)
+                if i < halves - 1:
+                    self._apply_half(self._half)
+                self._half ^= 1
+                self.actor_steps += k
+            return
+        for _ in range(steps):
             self.actor_step()
 
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""
+        if self.overlap:
+            if self._g_learn_b is not None:
+                self._train_step_overlap()
+            else:
+                self._train_step_eager()
+                self.learn_steps += 1
+                self.actor_steps += self.cfg.actor_steps_per_learner_step
+                if self.learn_steps % self.cfg.publish_param_interval == 0:
+                    self.publish_params()
+                if self.learn_steps % self.cfg.target_update_interval == 0:
+                    self.learner.sync_target()
+            return
         self.learner_step()
         for _ in range(self.cfg.actor_steps_per_learner_step):
             self.actor_step()

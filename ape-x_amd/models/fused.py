@@ -10,8 +10,9 @@ from scratch (init, after a broadcast or checkpoint load).
 
 Forward (per pass, no autograd):
   conv_fwd x3  (u8 frames -> bf16 NHWC activations; MFMA 32x32x16, bias+ReLU fused)
-  FC1          (hipBLASLt GEMM, bf16 x bf16 -> fp32; a plain library GEMM)
-  heads_fwd    (bias + ReLU + adv/value heads + dueling combine, one wave per row)
+  fc1_fwd      (split-K MFMA GEMM, 4 fp32 partials; the M x N-tiled library GEMM left
+               half the CUs idle on this skinny K = 3136 shape)
+  heads_fwd    (partial sum + bias + ReLU + adv/value heads + dueling combine, one wave per row)
 Backward (explicit, writes every parameter gradient into the flat fp32 grad buffer
 exactly once, so no zeroing pass is needed):
   heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (hipBLASLt) ->
@@ -31,6 +32,7 @@ from .dqn import DuelingDQN
 
 P3, C3 = 49, 64
 FEAT = P3 * C3  # 3136
+FC1_SPLITS = 4  # split-K partials of the FC1 kernel (fc_kernels.hip, checked against fc1_splits())
 
 
 class NetWorkspace:
@@ -43,7 +45,7 @@ class NetWorkspace:
         self.a1 = torch.empty(B, 400, 32, **bf)
         self.a2 = torch.empty(B, 81, 64, **bf)
         self.a3 = torch.empty(B, FEAT, **bf)
-        self.z = torch.empty(B, 256, **f32)
+        self.z = torch.empty(FC1_SPLITS, B, 256, **f32)  # FC1 split-K partials
         self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
         self.q = torch.empty(B, A, **f32)
         if keep_for_backward:
@@ -70,6 +72,7 @@ class HipDuelingNet:
     def __init__(self, model: DuelingDQN):
         assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
         self.hip = ops.hip()
+        assert self.hip.fc1_splits() == FC1_SPLITS, "fc_kernels.hip split-K factor changed"
         self.model = model
         self.A = model.num_actions
         dev = next(model.parameters()).device
@@ -169,8 +172,8 @@ class HipDuelingNet:
         h.conv_fwd(1, xp, ip, jp, self.w1p.data_ptr(), self.b1.data_ptr(), ws.a1.data_ptr(), B, s)
         h.conv_fwd(2, ws.a1.data_ptr(), 0, 0, self.w2p.data_ptr(), self.b2.data_ptr(), ws.a2.data_ptr(), B, s)
         h.conv_fwd(3, ws.a2.data_ptr(), 0, 0, self.w3p.data_ptr(), self.b3.data_ptr(), ws.a3.data_ptr(), B, s)
-        torch.mm(ws.a3, self.wfc1p.t(), out_dtype=torch.float32, out=ws.z)
-        h.heads_fwd(ws.z.data_ptr(), m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
+        h.fc1_fwd(ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.z.data_ptr(), B, s)
+        h.heads_fwd(ws.z.data_ptr(), FC1_SPLITS, m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
                     m.advantage[2].weight.data_ptr(), m.advantage[2].bias.data_ptr(), m.value[2].weight.data_ptr(),
                     m.value[2].bias.data_ptr(), ws.h.data_ptr() if ws.h is not None else 0, ws.q.data_ptr(), B,
                     self.A, s)

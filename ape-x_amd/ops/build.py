@@ -43,6 +43,7 @@ HIP_SOURCES = [
     "conv_bwd_kernels.hip",
     "aql_kernels.hip",
     "conv1_kernels.hip",
+    "fc_kernels.hip",
 ]
 
 

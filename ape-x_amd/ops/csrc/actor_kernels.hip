@@ -221,6 +221,7 @@ __global__ void nstep_emit_k(NStepParams p, NStepState st, TransTable tt, const 
   const int n = p.n, A = p.A;
   const int64_t step = step_counter ? step_counter[0] : 0;
   const int slot = (int)(((int64_t)step * p.E + e) % p.C);
+  const int row = p.stage ? e : slot;  // staged: the learner scatters the row later
   int* meta = st.win_meta + e * 4;
   int start = meta[0], len = meta[1], qstart = meta[2], qlen = meta[3];
   int* hist = st.hist + e * 4;
@@ -236,12 +237,12 @@ __global__ void nstep_emit_k(NStepParams p, NStepState st, TransTable tt, const 
   float prio = 0.f;
   auto write_trans = [&](const int* s0, int a0, float R, float d) {
     for (int c = 0; c < 4; ++c) {
-      tt.s_ids[slot * 4 + c] = s0[c];
-      tt.s2_ids[slot * 4 + c] = hist[c];
+      tt.s_ids[row * 4 + c] = s0[c];
+      tt.s2_ids[row * 4 + c] = hist[c];
     }
-    tt.action[slot] = a0;
-    tt.reward[slot] = R;
-    tt.done[slot] = d;
+    tt.action[row] = a0;
+    tt.reward[row] = R;
+    tt.done[row] = d;
   };
 
   if (p.mode == 0) {
@@ -323,12 +324,12 @@ __global__ void nstep_emit_k(NStepParams p, NStepState st, TransTable tt, const 
     } else if (!emitted && dmeta[1] > 0) {
       const int k = dmeta[0];
       for (int c = 0; c < 4; ++c) {
-        tt.s_ids[slot * 4 + c] = st.drain_ids[(e * n + k) * 4 + c];
-        tt.s2_ids[slot * 4 + c] = st.drain_s2[e * 4 + c];
+        tt.s_ids[row * 4 + c] = st.drain_ids[(e * n + k) * 4 + c];
+        tt.s2_ids[row * 4 + c] = st.drain_s2[e * 4 + c];
       }
-      tt.action[slot] = st.drain_a[e * n + k];
-      tt.reward[slot] = st.drain_r[e * n + k];
-      tt.done[slot] = 1.f;
+      tt.action[row] = st.drain_a[e * n + k];
+      tt.reward[row] = st.drain_r[e * n + k];
+      tt.done[row] = 1.f;
       prio = st.drain_q[e * n + k];
       emitted = true;
       dmeta[0] = k + 1;
@@ -347,6 +348,21 @@ __global__ void nstep_emit_k(NStepParams p, NStepState st, TransTable tt, const 
   }
   slot_out[e] = slot;
   prio_out[e] = emitted ? prio : 0.f;
+}
+
+// staged rows -> replay tables (overlapped actor/learner: the learner stream applies the
+// previous actor step's rows right before its tree write, so a row is never rewritten
+// while the learner can still sample its slot)
+__global__ void apply_staged_rows_k(TransTable st, TransTable dst, const int* __restrict__ slot,
+                                    const float* __restrict__ prio, int E) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= E || !(prio[e] > 0.f)) return;
+  const int j = slot[e];
+  reinterpret_cast<int4*>(dst.s_ids)[j] = reinterpret_cast<const int4*>(st.s_ids)[e];
+  reinterpret_cast<int4*>(dst.s2_ids)[j] = reinterpret_cast<const int4*>(st.s2_ids)[e];
+  dst.action[j] = st.action[e];
+  dst.reward[j] = st.reward[e];
+  dst.done[j] = st.done[e];
 }
 
 // ------------------------------------------------------------------ launchers
@@ -377,6 +393,12 @@ void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float*
   if (p.n < 1 || p.n > 16) throw std::invalid_argument("n-step must be in [1, 16]");
   nstep_emit_k<<<(p.E + 127) / 128, 128, 0, s>>>(p, st, tt, q, actions, reward, done, new_frame, step_counter,
                                                  slot_out, prio_out);
+  LAUNCH_CHECK();
+}
+
+void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s) {
+  if (E <= 0) return;
+  apply_staged_rows_k<<<(E + 255) / 256, 256, 0, s>>>(stage, dst, slot, prio, E);
   LAUNCH_CHECK();
 }
 

@@ -148,14 +148,15 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
 }
 
 // ------------------------------------------------------------------ dueling heads
-// z [B][256] = FC1 pre-activation (adv hidden 0..127 | value hidden 128..255, no bias).
+// z [nsplit][B][256] = FC1 pre-activation split-K partials (fc_kernels.hip; adv hidden
+// 0..127 | value hidden 128..255, no bias), summed here in fixed order.
 // A workgroup stages the head weights (A+1)x128 in LDS and handles 4 rows (one per
 // wave, B/4 workgroups so a 512-row batch spreads over 128 CUs): h = relu(z + b1) ->
 // LDS; lane a < A computes adv_a, lane A the value; q = V + A - mean(A)
 // (model.py:60-68).  h is kept (fp32) for the backward.
 constexpr int kHeadRows = 4;
 
-__global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, const float* __restrict__ b_adv1,
+__global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, int nsplit, const float* __restrict__ b_adv1,
                                                    const float* __restrict__ b_val1, const float* __restrict__ w_adv2,
                                                    const float* __restrict__ b_adv2, const float* __restrict__ w_val2,
                                                    const float* __restrict__ b_val2, float* __restrict__ hout,
@@ -177,7 +178,9 @@ __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, 
     for (int k = 0; k < 4; ++k) {
       const int j = lane + 64 * k;
       const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
-      const float v = fmaxf(zr[j] + bias, 0.f);
+      float zs = zr[j];
+      for (int sp = 1; sp < nsplit; ++sp) zs += zr[(size_t)sp * B * 256 + j];
+      const float v = fmaxf(zs + bias, 0.f);
       hs[wave][j] = v;
       if (hout && valid) hout[(size_t)b * 256 + j] = v;
     }
@@ -196,10 +199,12 @@ __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, 
   }
 }
 
-void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
-               const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s) {
+void heads_fwd(const float* z, int nsplit, const float* b_adv1, const float* b_val1, const float* w_adv2,
+               const float* b_adv2, const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A,
+               hipStream_t s) {
   if (A < 1 || A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
-  heads_fwd_k<<<(B + kHeadRows - 1) / kHeadRows, 256, 0, s>>>(z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout,
+  if (nsplit < 1) throw std::invalid_argument("heads_fwd: nsplit >= 1");
+  heads_fwd_k<<<(B + kHeadRows - 1) / kHeadRows, 256, 0, s>>>(z, nsplit, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout,
                                                              q, B, A);
   LAUNCH_CHECK();
 }

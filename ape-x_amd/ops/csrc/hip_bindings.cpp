@@ -120,9 +120,9 @@ PYBIND11_MODULE(_apex_hip, m) {
   });
 
   py::class_<NStepHandle>(m, "NStepHandle");
-  m.def("make_nstep", [](int E, int A, int n, int C, float gamma, int mode, py::dict st, py::dict tt) {
+  m.def("make_nstep", [](int E, int A, int n, int C, float gamma, int mode, py::dict st, py::dict tt, int stage) {
     NStepHandle h;
-    h.p = NStepParams{E, A, n, C, gamma, mode};
+    h.p = NStepParams{E, A, n, C, gamma, mode, stage};
     auto g = [&](py::dict d, const char* k) { return d[k].cast<uint64_t>(); };
     h.st.win_ids = P<int>(g(st, "win_ids"));
     h.st.win_a = P<int>(g(st, "win_a"));
@@ -142,6 +142,15 @@ PYBIND11_MODULE(_apex_hip, m) {
     h.tt.reward = P<float>(g(tt, "reward"));
     h.tt.done = P<float>(g(tt, "done"));
     return h;
+  }, py::arg("E"), py::arg("A"), py::arg("n"), py::arg("C"), py::arg("gamma"), py::arg("mode"), py::arg("st"),
+     py::arg("tt"), py::arg("stage") = 0);
+  m.def("apply_staged_rows", [](py::dict st, py::dict dst, uint64_t slot, uint64_t prio, int E, uint64_t s) {
+    auto tab = [](py::dict d) {
+      auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+      return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
+                        P<float>(g("done"))};
+    };
+    apply_staged_rows(tab(st), tab(dst), P<const int>(slot), P<const float>(prio), E, S(s));
   });
   m.def("nstep_emit", [](const NStepHandle& h, uint64_t q, uint64_t actions, uint64_t reward, uint64_t done,
                          uint64_t new_frame, uint64_t step, uint64_t slot_out, uint64_t prio_out, uint64_t s) {
@@ -208,9 +217,13 @@ PYBIND11_MODULE(_apex_hip, m) {
                 P<float>(gba), P<float>(gwv), P<float>(gbv), P<float>(gba1), P<float>(gbv1), S(s));
   });
   m.def("heads_wgrad_workspace_floats", &heads_wgrad_workspace_floats);
-  m.def("heads_fwd", [](uint64_t z, uint64_t ba1, uint64_t bv1, uint64_t wa2, uint64_t ba2, uint64_t wv2, uint64_t bv2,
-                        uint64_t hout, uint64_t q, int B, int A, uint64_t s) {
-    heads_fwd(P<const float>(z), P<const float>(ba1), P<const float>(bv1), P<const float>(wa2), P<const float>(ba2),
+  m.def("fc1_splits", &fc1_splits);
+  m.def("fc1_fwd", [](uint64_t a, uint64_t w, uint64_t part, int B, uint64_t s) {
+    fc1_fwd(P<const uint16_t>(a), P<const uint16_t>(w), P<float>(part), B, S(s));
+  });
+  m.def("heads_fwd", [](uint64_t z, int nsplit, uint64_t ba1, uint64_t bv1, uint64_t wa2, uint64_t ba2, uint64_t wv2,
+                        uint64_t bv2, uint64_t hout, uint64_t q, int B, int A, uint64_t s) {
+    heads_fwd(P<const float>(z), nsplit, P<const float>(ba1), P<const float>(bv1), P<const float>(wa2), P<const float>(ba2),
               P<const float>(wv2), P<const float>(bv2), P<float>(hout), P<float>(q), B, A, S(s));
   });
   m.def("heads_bwd", [](uint64_t dq, uint64_t h, uint64_t wa2, uint64_t wv2, uint64_t dA, uint64_t dz, uint64_t dzb,

@@ -70,6 +70,7 @@ struct NStepParams {
   int E, A, n, C;   // envs, actions, n-step, transition capacity
   float gamma;
   int mode;         // 0 = reference, 1 = textbook
+  int stage;        // 1: rows go to staging row e (TransTable of E rows), slot_out = ring slot
 };
 struct NStepState {
   int* win_ids;     // [E][n][4]
@@ -95,6 +96,8 @@ struct TransTable {
 void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float* q, const int* actions,
                 const float* reward, const float* done, const int* new_frame, const int64_t* step_counter,
                 int* slot_out, float* prio_out, hipStream_t s);
+// staged actor rows [E] -> replay tables at slot[e] (emitted rows only: prio[e] > 0)
+void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s);
 
 // ---- learner_kernels.hip
 // (a, r, d) are read through idx (the sampled replay slots) when idx != nullptr.
@@ -138,8 +141,12 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
 void heads_wgrad(const float* dA, const float* h, const float* dz, int B, int A, float* ws, float* g_wadv2,
                  float* g_badv2, float* g_wval2, float* g_bval2, float* g_badv1, float* g_bval1, hipStream_t s);
 size_t heads_wgrad_workspace_floats(int A);
-void heads_fwd(const float* z, const float* b_adv1, const float* b_val1, const float* w_adv2, const float* b_adv2,
-               const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A, hipStream_t s);
+void heads_fwd(const float* z, int nsplit, const float* b_adv1, const float* b_val1, const float* w_adv2,
+               const float* b_adv2, const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A,
+               hipStream_t s);
+// fc_kernels.hip: split-K FC1 (a3 [B][3136] bf16 . W [256][3136]^T) -> fp32 partials [fc1_splits()][B][256]
+int fc1_splits();
+void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s);
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
                uint16_t* dz_bf, int B, int A, hipStream_t s);
 void pack_conv_w(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);

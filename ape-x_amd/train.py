@@ -163,11 +163,11 @@ def main(argv=None) -> int:
     max_step = int(L.max_step)
     bps_every = max(1, L.bps_interval)
     frames_per_round = n_actor_gpus * args.actor_steps * eng.frames_per_actor_step
-    t_last, step_last = time.perf_counter(), start
-    step = start
+    step = eng.learn_steps  # capture's warm-up steps are real training steps
+    t_last, step_last = time.perf_counter(), step
     while not max_step or step < max_step:
         eng.train_step()
-        step += 1
+        step = eng.learn_steps
         if step % bps_every == 0:
             torch.cuda.synchronize(device)
             now = time.perf_counter()

@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--actions", type=int, default=18)
     ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="actor graph on its own HIP stream, concurrent with the learner step")
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
@@ -89,7 +91,8 @@ def main():
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
-                       use_graphs=not args.no_graphs, seed=args.seed + 7919 * rank, learner=lc)
+                       use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
+                       learner=lc)
     allreduce = FlatGradAllReduce(world) if world > 1 else None
     sharded = world > 1 and not args.local_sampling
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded)
@@ -161,6 +164,7 @@ def main():
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
                 "forward": args.forward,
                 "hip_graphs": not args.no_graphs,
+                "actor_learner_overlap": args.overlap,
             },
             "actor_frames_per_sec": round(frames_per_s, 1),
             "learner_samples_per_sec": round(steps_per_s * args.batch, 1),

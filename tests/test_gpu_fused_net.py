@@ -240,3 +240,23 @@ def test_fused_optimizer_packing_matches_repack(cuda, opt):
     fused = net.arena.clone()
     net.repack()
     assert torch.equal(fused.view(torch.int16), net.arena.view(torch.int16))
+
+
+@pytest.mark.parametrize("B", [512, 256, 37])
+def test_fc1_splitk_matches_torch(cuda, B):
+    """Split-K FC1 partials sum to the fp32 GEMM of the same bf16 operands (ragged batch
+    included: the last 32-row tile is clamped on load and masked on store)."""
+    from apex_amd import ops
+    from apex_amd.models.fused import FC1_SPLITS, FEAT
+
+    hip = ops.hip()
+    g = torch.Generator().manual_seed(B)
+    a = _rand_bf16((B, FEAT), cuda, g=g)
+    w = _rand_bf16((256, FEAT), cuda, scale=0.02, g=g)
+    part = torch.full((FC1_SPLITS, B, 256), float("nan"), device=cuda)
+    hip.fc1_fwd(a.data_ptr(), w.data_ptr(), part.data_ptr(), B, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = a.float() @ w.float().t()
+    got = part.sum(0)
+    assert torch.isfinite(part).all()
+    assert (got - want).abs().max().item() <= 1e-4 * max(1.0, want.abs().max().item())
