@@ -23,7 +23,7 @@ import torch
 
 from .. import ops
 from ..models.dqn import DuelingDQN
-from ..models.fused import HipDuelingNet, NetWorkspace
+from ..models.fused import HipDuelingNet, NetWorkspace, forward_multi
 from .hbm_replay import HBMReplay
 
 
@@ -140,10 +140,12 @@ class DQNLearner:
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.
+            # The three passes share each layer's launch (5 kernels, not 15).
             rp = self.replay
-            q = self.net(rp.frames, self.ws_s, rp.s_ids, self.idx)
-            q2 = self.net(rp.frames, self.ws_s2, rp.s2_ids, self.idx)
-            q2t = self.tnet(rp.frames, self.ws_t, rp.s2_ids, self.idx)
+            forward_multi([(self.net, rp.frames, self.ws_s, rp.s_ids, self.idx),
+                           (self.net, rp.frames, self.ws_s2, rp.s2_ids, self.idx),
+                           (self.tnet, rp.frames, self.ws_t, rp.s2_ids, self.idx)])
+            q, q2, q2t = self.ws_s.q, self.ws_s2.q, self.ws_t.q
             self.hip.dqn_loss(q.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, rp.action.data_ptr(),
                               rp.reward.data_ptr(), rp.done.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), self.B,
                               self.A, self.gamma_n, self.loss.data_ptr(), self.dq.data_ptr(), self.prio.data_ptr(), s)

@@ -114,35 +114,50 @@ __device__ __forceinline__ void store_sample(char* xs, const Stage14& st) {
   if (t + 3328 < C1_Q) d[t + 3328] = u8x8_to_bf16(st.v13);
 }
 
+__device__ __forceinline__ FrameSrc frames_of(const ConvProb& p) {
+  return FrameSrc{reinterpret_cast<const uint8_t*>(p.in), p.ids, p.idx};
+}
+
+// B operand (weights, reference layout [n][c][ky][kx] = [n][k]): lane holds column n = r32,
+// k = 16 s + 8 h + j, for all 16 k-steps -- the whole B stays in 64 VGPRs
+__device__ __forceinline__ void load_wb(const uint16_t* w, int r32, int h, bf16x8 (&wb)[16]) {
+  const uint4* wr = reinterpret_cast<const uint4*>(w + (size_t)r32 * C1_K + 8 * h);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wb[s] = __builtin_bit_cast(bf16x8, wr[2 * s]);
+}
+
 }  // namespace
 
-__global__ __launch_bounds__(256, 1) void conv1_fwd_k(FrameSrc fs, const uint16_t* __restrict__ w,
-                                                      const float* __restrict__ bias, uint16_t* __restrict__ out,
-                                                      int B) {
+// Samples i in [0, n*B) of the problem set (problem i / B), grid-strided; a workgroup
+// reloads its register-resident weights only when the problem's weights change.
+__global__ __launch_bounds__(256, 1) void conv1_fwd_k(ConvSet set) {
   __shared__ __attribute__((aligned(16))) char smem[2][C1_STAGE];
   __shared__ __attribute__((aligned(16))) char eps[4][TILE_EP_BYTES];  // per-wave epilogue scratch
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
-  // B operand (weights, reference layout [n][c][ky][kx] = [n][k]): lane holds column n = r32,
-  // k = 16 s + 8 h + j, for all 16 k-steps -- the whole B stays in 64 VGPRs
+  const int B = set.B, total = set.n * B;
+  int i = blockIdx.x;
+  if (i >= total) return;  // block-uniform
   bf16x8 wb[16];
-  {
-    const uint4* wr = reinterpret_cast<const uint4*>(w + (size_t)r32 * C1_K + 8 * h);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) wb[s] = __builtin_bit_cast(bf16x8, wr[2 * s]);
-  }
-  const float bn = bias[r32];
-  int b = blockIdx.x;
-  if (b >= B) return;  // block-uniform
+  const uint16_t* wcur = set.p[i / B].w;
+  load_wb(wcur, r32, h, wb);
+  float bn = set.p[i / B].bias[r32];
   Stage14 v;
-  load_sample(fs, b, v);
+  load_sample(frames_of(set.p[i / B]), i % B, v);
   store_sample(smem[0], v);
   __syncthreads();
   int stage = 0;
   int tile0 = wave;  // round-robin tiles across samples keeps the 4 waves balanced
-  for (; b < B; b += gridDim.x) {
-    const int b_next = b + gridDim.x;
-    const bool more = b_next < B;  // block-uniform
-    if (more) load_sample(fs, b_next, v);
+  for (; i < total; i += gridDim.x) {
+    const int pb = i / B, b = i - pb * B;
+    const int i_next = i + gridDim.x;
+    const bool more = i_next < total;  // block-uniform
+    if (more) load_sample(frames_of(set.p[i_next / B]), i_next % B, v);
+    if (set.p[pb].w != wcur) {  // block-uniform
+      wcur = set.p[pb].w;
+      load_wb(wcur, r32, h, wb);
+      bn = set.p[pb].bias[r32];
+    }
+    uint16_t* out = set.p[pb].out;
     const char* xs = smem[stage];
     for (int mt = tile0; mt < C1_MT; mt += 4) {
       const int p = mt * 32 + r32;
@@ -180,15 +195,23 @@ __global__ __launch_bounds__(256, 1) void conv1_fwd_k(FrameSrc fs, const uint16_
   }
 }
 
+void conv1_fwd_multi(const ConvSet& set, hipStream_t s) {
+  const int total = set.n * set.B;
+  if (total <= 0) return;
+  if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("conv1_fwd: 1..3 problems");
+  // >= two samples per workgroup: the next sample's load overlaps the current MFMA loop
+  const int grid = std::min(std::max(1, (total + 1) / 2), 256);  // one workgroup per CU (113 KB LDS)
+  conv1_fwd_k<<<grid, 256, 0, s>>>(set);
+  LAUNCH_CHECK();
+}
+
 void conv1_fwd(const uint8_t* frames, const int* ids, const int* idx, const uint16_t* w, const float* bias,
                uint16_t* out, int B, hipStream_t s) {
-  if (B <= 0) return;
-  const FrameSrc fs{frames, ids, idx};
-  // two samples per workgroup at the learner batch: the second sample's load overlaps
-  // the first one's MFMA loop
-  const int grid = std::min(std::max(1, (B + 1) / 2), 256);  // one workgroup per CU (113 KB LDS)
-  conv1_fwd_k<<<grid, 256, 0, s>>>(fs, w, bias, out, B);
-  LAUNCH_CHECK();
+  ConvSet set{};
+  set.p[0] = ConvProb{frames, ids, idx, w, bias, out};
+  set.n = 1;
+  set.B = B;
+  conv1_fwd_multi(set, s);
 }
 
 }  // namespace apex

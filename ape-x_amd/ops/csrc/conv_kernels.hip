@@ -79,21 +79,32 @@ __device__ __forceinline__ constexpr int a_off(int kk) {
   }
 }
 
+// Problem set (kernels.h ConvSet): sample pairs never straddle two problems (a problem of
+// B samples has ceil(B/2) pairs); the weights are restaged only when the problem's weight
+// pointer changes (the learner's Q(s) and Q(s') passes share the online weights).
 template <class G, bool U8IN>
-__global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, FrameSrc fs,
-                                                  const uint16_t* __restrict__ wp, const float* __restrict__ bias,
-                                                  uint16_t* __restrict__ out, int B) {
+__global__ __launch_bounds__(256) void conv_fwd_k(ConvSet set) {
   __shared__ __attribute__((aligned(16))) char smem[G::LDS + 4 * TILE_EP_BYTES];
   char* ws = smem + G::SPW * G::X_BYTES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
   char* ep = smem + G::LDS + wave * TILE_EP_BYTES;  // per-wave epilogue scratch
-  stage_weights<G>(wp, ws);
-  for (int b0 = blockIdx.x * G::SPW; b0 < B; b0 += gridDim.x * G::SPW) {
+  const int B = set.B, PP = (B + G::SPW - 1) / G::SPW, pairs = set.n * PP;
+  const uint16_t* wcur = nullptr;
+  for (int q = blockIdx.x; q < pairs; q += gridDim.x) {
+    const int pb = q / PP, b0 = (q - pb * PP) * G::SPW;
+    const ConvProb& pr = set.p[pb];
+    const FrameSrc fs{reinterpret_cast<const uint8_t*>(pr.in), pr.ids, pr.idx};
     __syncthreads();
+    if (pr.w != wcur) {  // block-uniform
+      wcur = pr.w;
+      stage_weights<G>(wcur, ws);
+    }
 #pragma unroll
     for (int sw = 0; sw < G::SPW; ++sw)
-      if (b0 + sw < B) stage_input<G, U8IN>(in, fs, b0 + sw, smem + sw * G::X_BYTES);
+      if (b0 + sw < B) stage_input<G, U8IN>(pr.in, fs, b0 + sw, smem + sw * G::X_BYTES);
     __syncthreads();
+    const float* bias = pr.bias;
+    uint16_t* out = pr.out;
     constexpr int ITEMS = G::SPW * G::MT * G::NT;
     for (int it = wave; it < ITEMS; it += 4) {
       const int sw = it / (G::MT * G::NT);
@@ -128,23 +139,32 @@ __global__ __launch_bounds__(256) void conv_fwd_k(const void* __restrict__ in, F
 }
 
 template <class G, bool U8IN>
-static void launch_conv_fwd(const void* in, FrameSrc fs, const uint16_t* wp, const float* bias, uint16_t* out, int B,
-                            hipStream_t s) {
-  if (B <= 0) return;
-  const int grid = std::min((B + G::SPW - 1) / G::SPW, 512);
-  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(in, fs, wp, bias, out, B);
+static void launch_conv_fwd(const ConvSet& set, hipStream_t s) {
+  const int pairs = set.n * ((set.B + G::SPW - 1) / G::SPW);
+  if (pairs <= 0) return;
+  // one workgroup per CU (the LDS footprint allows no more): 256 persistent workgroups
+  const int grid = std::min(pairs, 256);
+  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(set);
   LAUNCH_CHECK();
+}
+
+void conv_fwd_multi(int layer, const ConvSet& set, hipStream_t s) {
+  if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("conv_fwd: 1..3 problems");
+  switch (layer) {
+    case 1: conv1_fwd_multi(set, s); break;  // conv1_kernels.hip
+    case 2: launch_conv_fwd<Conv2, false>(set, s); break;
+    case 3: launch_conv_fwd<Conv3, false>(set, s); break;
+    default: throw std::invalid_argument("conv_fwd: layer must be 1, 2 or 3");
+  }
 }
 
 void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const uint16_t* wp, const float* bias,
               uint16_t* out, int B, hipStream_t s) {
-  const FrameSrc fs{reinterpret_cast<const uint8_t*>(in), ids, idx};
-  switch (layer) {
-    case 1: conv1_fwd(fs.frames, ids, idx, wp, bias, out, B, s); break;  // conv1_kernels.hip
-    case 2: launch_conv_fwd<Conv2, false>(in, fs, wp, bias, out, B, s); break;
-    case 3: launch_conv_fwd<Conv3, false>(in, fs, wp, bias, out, B, s); break;
-    default: throw std::invalid_argument("conv_fwd: layer must be 1, 2 or 3");
-  }
+  ConvSet set{};
+  set.p[0] = ConvProb{in, ids, idx, wp, bias, out};
+  set.n = 1;
+  set.B = B;
+  conv_fwd_multi(layer, set, s);
 }
 
 // ------------------------------------------------------------------ dueling heads
@@ -156,33 +176,39 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
 // (model.py:60-68).  h is kept (fp32) for the backward.
 constexpr int kHeadRows = 4;
 
-__global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, int nsplit, const float* __restrict__ b_adv1,
-                                                   const float* __restrict__ b_val1, const float* __restrict__ w_adv2,
-                                                   const float* __restrict__ b_adv2, const float* __restrict__ w_val2,
-                                                   const float* __restrict__ b_val2, float* __restrict__ hout,
-                                                   float* __restrict__ q, int B, int A) {
+__global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
   __shared__ float ws[64 * 129];  // row a (a < A: adv, a == A: value), padded to break bank conflicts
   __shared__ float hs[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int B = set.B, A = set.A, nsplit = set.nsplit, RB = (B + kHeadRows - 1) / kHeadRows;
+  const int pb = blockIdx.x / RB, rb = blockIdx.x - pb * RB;
+  const HeadsProb& pr = set.p[pb];
+  const float* __restrict__ z = pr.z;
   for (int e = threadIdx.x; e < (A + 1) * 128; e += 256) {
     const int a = e / 128, j = e % 128;
-    ws[a * 129 + j] = a < A ? w_adv2[a * 128 + j] : w_val2[j];
+    ws[a * 129 + j] = a < A ? pr.w_adv2[a * 128 + j] : pr.w_val2[j];
   }
-  const float bo = lane < A ? b_adv2[lane] : (lane == A ? b_val2[0] : 0.f);
+  const float bo = lane < A ? pr.b_adv2[lane] : (lane == A ? pr.b_val2[0] : 0.f);
   for (int rr = 0; rr < kHeadRows / 4; ++rr) {
-    const int b = blockIdx.x * kHeadRows + rr * 4 + wave;
+    const int b = rb * kHeadRows + rr * 4 + wave;
     const bool valid = b < B;
     const float* zr = z + (size_t)(valid ? b : 0) * 256;
+    // all split-K partial loads first (independent), then the fixed-order sums
+    float zv[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int sp = 0; sp < 4; ++sp) zv[k][sp] = sp < nsplit ? zr[(size_t)sp * B * 256 + lane + 64 * k] : 0.f;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int j = lane + 64 * k;
-      const float bias = j < 128 ? b_adv1[j] : b_val1[j - 128];
-      float zs = zr[j];
-      for (int sp = 1; sp < nsplit; ++sp) zs += zr[(size_t)sp * B * 256 + j];
+      const float bias = j < 128 ? pr.b_adv1[j] : pr.b_val1[j - 128];
+      float zs = zv[k][0];
+      for (int sp = 1; sp < 4; ++sp) zs += zv[k][sp];
       const float v = fmaxf(zs + bias, 0.f);
       hs[wave][j] = v;
-      if (hout && valid) hout[(size_t)b * 256 + j] = v;
+      if (pr.hout && valid) pr.hout[(size_t)b * 256 + j] = v;
     }
     __syncthreads();
     float o = 0.f;
@@ -195,18 +221,29 @@ __global__ __launch_bounds__(256) void heads_fwd_k(const float* __restrict__ z, 
     }
     const float adv_sum = wave_sum(lane < A ? o : 0.f);
     const float v = __shfl(o, A, 64);
-    if (valid && lane < A) q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
+    if (valid && lane < A) pr.q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
   }
+}
+
+void heads_fwd_multi(const HeadsSet& set, hipStream_t s) {
+  if (set.A < 1 || set.A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
+  if (set.nsplit < 1 || set.nsplit > 4) throw std::invalid_argument("heads_fwd: 1 <= nsplit <= 4");
+  if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("heads_fwd: 1..3 problems");
+  if (set.B <= 0) return;
+  heads_fwd_k<<<set.n * ((set.B + kHeadRows - 1) / kHeadRows), 256, 0, s>>>(set);
+  LAUNCH_CHECK();
 }
 
 void heads_fwd(const float* z, int nsplit, const float* b_adv1, const float* b_val1, const float* w_adv2,
                const float* b_adv2, const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A,
                hipStream_t s) {
-  if (A < 1 || A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
-  if (nsplit < 1) throw std::invalid_argument("heads_fwd: nsplit >= 1");
-  heads_fwd_k<<<(B + kHeadRows - 1) / kHeadRows, 256, 0, s>>>(z, nsplit, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout,
-                                                             q, B, A);
-  LAUNCH_CHECK();
+  HeadsSet set{};
+  set.p[0] = HeadsProb{z, b_adv1, b_val1, w_adv2, b_adv2, w_val2, b_val2, hout, q};
+  set.n = 1;
+  set.B = B;
+  set.A = A;
+  set.nsplit = nsplit;
+  heads_fwd_multi(set, s);
 }
 
 // Backward of the heads for one row per wave:

@@ -28,11 +28,15 @@ static_assert(FC_KSTEPS % FC_KSPLIT == 0, "K split");
 
 int fc1_splits() { return FC_KSPLIT; }
 
-__global__ __launch_bounds__(256) void fc1_fwd_k(const uint16_t* __restrict__ a, const uint16_t* __restrict__ w,
-                                                 float* __restrict__ part, int B) {
+// grid.x runs over the M tiles of all problems of the set (problem = tile / ceil(B/32))
+__global__ __launch_bounds__(256) void fc1_fwd_k(FcSet set) {
   __shared__ float red[4][32 * 65];  // per-wave 32 x 64 tiles, padded rows
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
-  const int mtile = blockIdx.x, ntile = blockIdx.y, split = blockIdx.z;
+  const int B = set.B, MT = (B + 31) / 32;
+  const int pb = blockIdx.x / MT, mtile = blockIdx.x - pb * MT, ntile = blockIdx.y, split = blockIdx.z;
+  const uint16_t* __restrict__ a = set.p[pb].a;
+  const uint16_t* __restrict__ w = set.p[pb].w;
+  float* __restrict__ part = set.p[pb].part;
   const int row = mtile * 32 + r32;
   const int rowc = row < B ? row : B - 1;
   // this wave's k-steps: split * 49 + [wave * 13, min(49, wave * 13 + 13))
@@ -84,11 +88,20 @@ __global__ __launch_bounds__(256) void fc1_fwd_k(const uint16_t* __restrict__ a,
   }
 }
 
-void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s) {
-  if (B <= 0) return;
-  const dim3 grid((B + 31) / 32, FC_N / 64, FC_KSPLIT);
-  fc1_fwd_k<<<grid, 256, 0, s>>>(a, w, part, B);
+void fc1_fwd_multi(const FcSet& set, hipStream_t s) {
+  if (set.B <= 0) return;
+  if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("fc1_fwd: 1..3 problems");
+  const dim3 grid(set.n * ((set.B + 31) / 32), FC_N / 64, FC_KSPLIT);
+  fc1_fwd_k<<<grid, 256, 0, s>>>(set);
   LAUNCH_CHECK();
+}
+
+void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s) {
+  FcSet set{};
+  set.p[0] = FcProb{a, w, part};
+  set.n = 1;
+  set.B = B;
+  fc1_fwd_multi(set, s);
 }
 
 }  // namespace apex

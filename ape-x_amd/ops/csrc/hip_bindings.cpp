@@ -7,6 +7,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <array>
 #include <vector>
 
 #include "kernels.h"
@@ -217,6 +218,44 @@ PYBIND11_MODULE(_apex_hip, m) {
                 P<float>(gba), P<float>(gwv), P<float>(gbv), P<float>(gba1), P<float>(gbv1), S(s));
   });
   m.def("heads_wgrad_workspace_floats", &heads_wgrad_workspace_floats);
+  // multi-problem forward launches: lists of per-problem pointer tuples (<= 3 problems)
+  m.def("conv_fwd_multi", [](int layer, const std::vector<std::array<uint64_t, 6>>& probs, int B, uint64_t s) {
+    if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
+    ConvSet set{};
+    for (size_t i = 0; i < probs.size(); ++i) {
+      const auto& t = probs[i];
+      set.p[i] = ConvProb{P<const void>(t[0]), P<const int>(t[1]), P<const int>(t[2]), P<const uint16_t>(t[3]),
+                          P<const float>(t[4]), P<uint16_t>(t[5])};
+    }
+    set.n = (int)probs.size();
+    set.B = B;
+    conv_fwd_multi(layer, set, S(s));
+  });
+  m.def("fc1_fwd_multi", [](const std::vector<std::array<uint64_t, 3>>& probs, int B, uint64_t s) {
+    if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
+    FcSet set{};
+    for (size_t i = 0; i < probs.size(); ++i)
+      set.p[i] = FcProb{P<const uint16_t>(probs[i][0]), P<const uint16_t>(probs[i][1]), P<float>(probs[i][2])};
+    set.n = (int)probs.size();
+    set.B = B;
+    fc1_fwd_multi(set, S(s));
+  });
+  m.def("heads_fwd_multi", [](const std::vector<std::array<uint64_t, 9>>& probs, int nsplit, int B, int A,
+                              uint64_t s) {
+    if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
+    HeadsSet set{};
+    for (size_t i = 0; i < probs.size(); ++i) {
+      const auto& t = probs[i];
+      set.p[i] = HeadsProb{P<const float>(t[0]), P<const float>(t[1]), P<const float>(t[2]), P<const float>(t[3]),
+                           P<const float>(t[4]), P<const float>(t[5]), P<const float>(t[6]), P<float>(t[7]),
+                           P<float>(t[8])};
+    }
+    set.n = (int)probs.size();
+    set.B = B;
+    set.A = A;
+    set.nsplit = nsplit;
+    heads_fwd_multi(set, S(s));
+  });
   m.def("fc1_splits", &fc1_splits);
   m.def("fc1_fwd", [](uint64_t a, uint64_t w, uint64_t part, int B, uint64_t s) {
     fc1_fwd(P<const uint16_t>(a), P<const uint16_t>(w), P<float>(part), B, S(s));

@@ -136,6 +136,24 @@ void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
 
 // ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)
 // layer 1: `in` is the u8 frame ring (ids/idx: FrameSrc, see common.h) or a dense u8 stack
+// Multi-problem forward launches: up to kMaxProbs independent passes of the same layer
+// (the learner's Q(s), Q(s') and Q_target(s')) in ONE launch -- every kernel boundary
+// costs ~4.5 us on MI355X, and the 3x larger grid amortises weight staging.  All
+// problems share the batch size B; problem i covers samples [i*B, (i+1)*B).
+constexpr int kMaxProbs = 3;
+struct ConvProb {
+  const void* in;       // layer 1: u8 frames (dense [B][4][84][84] or the frame ring)
+  const int* ids;       // layer 1 frame-ring ids [*][4] (nullptr = dense)
+  const int* idx;       // row map into ids (nullptr = identity)
+  const uint16_t* w;    // packed bf16 weights
+  const float* bias;
+  uint16_t* out;        // channels-last bf16 activations
+};
+struct ConvSet {
+  ConvProb p[kMaxProbs];
+  int n, B;
+};
+void conv_fwd_multi(int layer, const ConvSet& set, hipStream_t s);
 void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const uint16_t* wp, const float* bias,
               uint16_t* out, int B, hipStream_t s);
 void heads_wgrad(const float* dA, const float* h, const float* dz, int B, int A, float* ws, float* g_wadv2,
@@ -147,6 +165,27 @@ void heads_fwd(const float* z, int nsplit, const float* b_adv1, const float* b_v
 // fc_kernels.hip: split-K FC1 (a3 [B][3136] bf16 . W [256][3136]^T) -> fp32 partials [fc1_splits()][B][256]
 int fc1_splits();
 void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s);
+struct FcProb {
+  const uint16_t* a;  // a3 [B][3136] bf16
+  const uint16_t* w;  // [256][3136] bf16
+  float* part;        // [fc1_splits()][B][256]
+};
+struct FcSet {
+  FcProb p[kMaxProbs];
+  int n, B;
+};
+void fc1_fwd_multi(const FcSet& set, hipStream_t s);
+struct HeadsProb {
+  const float* z;  // FC1 split-K partials [nsplit][B][256]
+  const float *b_adv1, *b_val1, *w_adv2, *b_adv2, *w_val2, *b_val2;
+  float* hout;     // [B][256] post-ReLU hidden (nullptr: not kept)
+  float* q;        // [B][A]
+};
+struct HeadsSet {
+  HeadsProb p[kMaxProbs];
+  int n, B, A, nsplit;
+};
+void heads_fwd_multi(const HeadsSet& set, hipStream_t s);
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
                uint16_t* dz_bf, int B, int A, hipStream_t s);
 void pack_conv_w(const float* src, uint16_t* dst, int N, int C, int KH, int KW, hipStream_t s);
@@ -167,6 +206,7 @@ void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW,
 
 
 // ---- conv1_kernels.hip: conv1 forward from raw u8 planes; w = bf16 [32][4][8][8] (reference layout)
+void conv1_fwd_multi(const ConvSet& set, hipStream_t s);
 void conv1_fwd(const uint8_t* frames, const int* ids, const int* idx, const uint16_t* w, const float* bias,
                uint16_t* out, int B, hipStream_t s);
 

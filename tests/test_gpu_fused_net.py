@@ -260,3 +260,30 @@ def test_fc1_splitk_matches_torch(cuda, B):
     got = part.sum(0)
     assert torch.isfinite(part).all()
     assert (got - want).abs().max().item() <= 1e-4 * max(1.0, want.abs().max().item())
+
+
+@pytest.mark.parametrize("B", [512, 37])
+def test_forward_multi_equals_single_passes(cuda, B):
+    """One launch per layer for 3 passes (two nets, ring input via ids/idx) gives the
+    same bits as three single-pass forwards."""
+    from apex_amd.models.fused import HipDuelingNet, NetWorkspace, forward_multi
+
+    m1, m2 = _model(cuda, seed=1), _model(cuda, seed=2)
+    n1, n2 = HipDuelingNet(m1), HipDuelingNet(m2)
+    F = 4 * B + 8
+    g = torch.Generator(device=cuda).manual_seed(B)
+    frames = torch.randint(0, 256, (F, 84 * 84), dtype=torch.uint8, device=cuda, generator=g)
+    s_ids = torch.randint(0, F, (3 * B, 4), dtype=torch.int32, device=cuda, generator=g)
+    s2_ids = torch.randint(0, F, (3 * B, 4), dtype=torch.int32, device=cuda, generator=g)
+    idx = torch.randperm(3 * B, device=cuda)[:B].int()
+    ws = [NetWorkspace(B, 18, cuda, keep_for_backward=(i == 0)) for i in range(6)]
+    forward_multi([(n1, frames, ws[0], s_ids, idx), (n1, frames, ws[1], s2_ids, idx),
+                   (n2, frames, ws[2], s2_ids, idx)])
+    n1(frames, ws[3], s_ids, idx)
+    n1(frames, ws[4], s2_ids, idx)
+    n2(frames, ws[5], s2_ids, idx)
+    torch.cuda.synchronize()
+    for a, b in ((0, 3), (1, 4), (2, 5)):
+        assert torch.equal(ws[a].q, ws[b].q)
+        assert torch.equal(ws[a].a1, ws[b].a1) and torch.equal(ws[a].a3, ws[b].a3)
+    assert not torch.equal(ws[1].q, ws[2].q)  # different nets really ran
