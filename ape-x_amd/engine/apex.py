@@ -91,6 +91,7 @@ class ApexEngine:
         self.actor_steps = 0
         self._g_actor = self._g_learn_a = self._g_learn_b = None
         self._pool = None
+        self._captured = False
         self._allreduce = allreduce
         # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
         # train step while the learner applies the other half (the previous step's)
@@ -161,10 +162,22 @@ class ApexEngine:
         self._g_learn_a = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_learn_a, pool=self._pool):
             self._learn_a()
-        self._g_learn_b = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_learn_b, pool=self._pool):
-            self._learn_b()
+            if self._allreduce is None:  # no host collective in between: one graph per step
+                self._learn_b()
+        self._g_learn_b = self._capture_learn_b()
+        self._captured = True
         torch.cuda.synchronize(self.device)
+
+    def _capture_learn_b(self):
+        """The optimizer graph, needed only when an eager RCCL all-reduce sits between the
+        backward and the optimizer (data-parallel); otherwise it is part of learn_a (each
+        graph boundary costs ~8 us of launch gap, rocprofv3 trace)."""
+        if self._allreduce is None:
+            return None
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._pool):
+            self._learn_b()
+        return g
 
     def _capture_overlap(self, warmup_iters: int) -> None:
         """Overlap mode: graphs per staging half (actor: fill half h; learner: apply half
@@ -188,15 +201,16 @@ class ApexEngine:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self._pool):
                 self._learn_a(1 - h)
+                if self._allreduce is None:
+                    self._learn_b()
             self._g_learn_a.append(g)
             if self._sharded is not None:
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=self._pool):
                     self._apply_half(1 - h)
                 self._g_apply.append(g)
-        self._g_learn_b = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_learn_b, pool=self._pool):
-            self._learn_b()
+        self._g_learn_b = self._capture_learn_b()
+        self._captured = True
         torch.cuda.synchronize(self.device)
         self._ev_learn.record(torch.cuda.current_stream(self.device))
 
@@ -235,7 +249,7 @@ class ApexEngine:
         self._g_learn_a[h].replay()
         if self._allreduce is not None:
             self._allreduce(self.learner.flat_grad)
-        self._g_learn_b.replay()
+            self._g_learn_b.replay()
         self.learn_steps += 1
         self.actor_steps += self.cfg.actor_steps_per_learner_step
         if self.learn_steps % self.cfg.publish_param_interval == 0:
@@ -261,7 +275,7 @@ class ApexEngine:
             self._g_learn_a.replay()
             if self._allreduce is not None:
                 self._allreduce(self.learner.flat_grad)
-            self._g_learn_b.replay()
+                self._g_learn_b.replay()
         else:
             self._learn_a()
             if self._allreduce is not None:
@@ -293,7 +307,7 @@ class ApexEngine:
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""
         if self.overlap:
-            if self._g_learn_b is not None:
+            if self._captured:
                 self._train_step_overlap()
             else:
                 self._train_step_eager()

@@ -89,18 +89,21 @@ class HBMReplay:
 
     # ------------------------------------------------------------------ priorities
     def write_priorities(self, idx: torch.Tensor, prio: torch.Tensor | None, dedup: bool = True,
-                         bumps: tuple = ()) -> None:
+                         bumps: tuple = (), mix: tuple | None = None) -> None:
         """Set leaves for ``idx`` (int32) to prio**alpha (None = current max priority),
         then recompute all dirty ancestors level by level.  ``dedup`` resolves duplicate
         indices last-write-wins (B <= 1024); without it ``idx`` must be unique slots in
         ring order.  ``bumps``: up to two (int64 device counter, delta) pairs advanced by
-        the same launch."""
+        the same launch.  ``mix`` = (delta, lw, prio_out, loss_out): priorities derived
+        in-kernel from TD errors, 0.9 max(delta) + 0.1 delta + 1e-6 (utils.py:77), and the
+        loss mean of lw written to loss_out (dedup only)."""
         B = idx.numel()
         b = list(bumps) + [(None, 0)] * (2 - len(bumps))
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         self.hip.per_write_leaves(self.tree, idx.data_ptr(), 0 if prio is None else prio.data_ptr(), B, self.alpha,
                                   self.max_prio.data_ptr(), int(dedup), self.sorted_scratch.data_ptr(), ptr(b[0][0]),
-                                  int(b[0][1]), ptr(b[1][0]), int(b[1][1]), self._stream())
+                                  int(b[0][1]), ptr(b[1][0]), int(b[1][1]), self._stream(),
+                                  *((0, 0, 0, 0) if mix is None else tuple(ptr(t) for t in mix)))
 
     update_priorities = write_priorities
 

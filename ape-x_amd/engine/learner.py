@@ -123,6 +123,16 @@ class DQNLearner:
             self.ws_s = NetWorkspace(B, A, dev, keep_for_backward=True)
             self.ws_s2 = NetWorkspace(B, A, dev)
             self.ws_t = NetWorkspace(B, A, dev)
+            # fused loss + heads backward (dqn_heads_bwd) outputs; the priority-tree write
+            # (which mixes the TD errors into priorities and forms the loss mean) runs on
+            # a forked stream concurrently with the trunk backward
+            self.delta = torch.zeros(B, dtype=torch.float32, device=dev)
+            self.lw = torch.zeros(B, dtype=torch.float32, device=dev)
+            self.lh_blocks = self.hip.dqn_heads_bwd_blocks(B)
+            self.lh_part = torch.zeros(self.lh_blocks * ((A + 1) * 128 + (A + 1) + 256), dtype=torch.float32,
+                                       device=dev)
+            self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.tree_stream = torch.cuda.Stream(device=dev)
 
     @staticmethod
     def _stream() -> int:
@@ -145,11 +155,24 @@ class DQNLearner:
             forward_multi([(self.net, rp.frames, self.ws_s, rp.s_ids, self.idx),
                            (self.net, rp.frames, self.ws_s2, rp.s2_ids, self.idx),
                            (self.tnet, rp.frames, self.ws_t, rp.s2_ids, self.idx)])
-            q, q2, q2t = self.ws_s.q, self.ws_s2.q, self.ws_t.q
-            self.hip.dqn_loss(q.data_ptr(), q2.data_ptr(), q2t.data_ptr(), self.A, rp.action.data_ptr(),
-                              rp.reward.data_ptr(), rp.done.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), self.B,
-                              self.A, self.gamma_n, self.loss.data_ptr(), self.dq.data_ptr(), self.prio.data_ptr(), s)
-            self.net.backward(self.dq, rp.frames, self.ws_s, rp.s_ids, self.idx)
+            m = self.model
+            self.hip.dqn_heads_bwd(
+                {"q": self.ws_s.q.data_ptr(), "q2": self.ws_s2.q.data_ptr(), "q2t": self.ws_t.q.data_ptr(),
+                 "act": rp.action.data_ptr(), "rew": rp.reward.data_ptr(), "done": rp.done.data_ptr(),
+                 "idx": self.idx.data_ptr(), "w": self.w.data_ptr(), "h": self.ws_s.h.data_ptr(),
+                 "w_adv2": m.advantage[2].weight.data_ptr(), "w_val2": m.value[2].weight.data_ptr(),
+                 "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(), "dz_bf": self.ws_s.dz_bf.data_ptr(),
+                 "part": self.lh_part.data_ptr(), "step": self.step_counter.data_ptr(),
+                 "step_snap": self.step_snap.data_ptr()}, self.B, self.A, self.gamma_n, s)
+            # fork: priority mix + loss mean + tree write (+ step bump) beside the backward
+            main = torch.cuda.current_stream()
+            self.tree_stream.wait_stream(main)
+            with torch.cuda.stream(self.tree_stream):
+                self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
+                                             mix=(self.delta, self.lw, self.prio, self.loss))
+            self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
+                                    extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)])
+            main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
             return
         self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
         q = forward_q(self.model, self.s)
@@ -171,10 +194,13 @@ class DQNLearner:
         h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
         pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if self.hip_net else (0, 0, 0)
         step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
+        # the fused path already bumped step_counter on the tree stream: the optimizer reads
+        # this step's snapshot instead
+        stp = self.step_snap if self.hip_net else self.step_counter
         step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(), self.opt_s2.data_ptr(), self.P,
-             self.partials.data_ptr(), self.partials.numel(), self.hp, self.step_counter.data_ptr(),
-             self.norms.data_ptr(), s, *pk)
-        self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
+             self.partials.data_ptr(), self.partials.numel(), self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk)
+        if not self.hip_net:
+            self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 
     def step(self) -> None:
         if self.sharded is not None:

@@ -16,7 +16,9 @@ Forward (per pass, no autograd):
                half the CUs idle on this skinny K = 3136 shape)
   heads_fwd    (partial sum + bias + ReLU + adv/value heads + dueling combine, one wave per row)
 Backward (explicit, writes every parameter gradient into the flat fp32 grad buffer
-exactly once, so no zeroing pass is needed):
+exactly once, so no zeroing pass is needed; the learner fuses the loss and heads part
+into one launch, ``dqn_heads_bwd``, and all batch-sliced reductions into one
+``grad_finalize``):
   heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (hipBLASLt) ->
   conv3/conv2/conv1: MFMA wgrad (ds_read_b64_tr_b16 operand transposes, split over the
   batch, deterministic partial reduce, conv bias grads fused) and MFMA dgrad (stride-1
@@ -145,9 +147,12 @@ class HipDuelingNet:
             h.pack_conv_wt(f[4].weight.data_ptr(), self.w3t.data_ptr(), 64, 64, 3, 3, s)
 
     def enable_backward(self) -> None:
-        """Allocate backward workspaces + transposed weights (call before graph capture)."""
-        n = max(self.hip.wgrad_workspace_floats(k) for k in (1, 2, 3))
-        self._wgrad_ws = torch.empty(n, dtype=torch.float32, device=self.device)
+        """Allocate backward workspaces + transposed weights (call before graph capture).
+        One wgrad partial workspace per conv layer: the three layers' partials are reduced
+        together by one grad_finalize launch at the end of the backward."""
+        self._wgrad_wss = [torch.empty(self.hip.wgrad_workspace_floats(k), dtype=torch.float32, device=self.device)
+                           for k in (1, 2, 3)]
+        self._wgrad_ws = self._wgrad_wss[0]
         self._heads_ws = torch.empty(self.hip.heads_wgrad_workspace_floats(self.A), dtype=torch.float32,
                                      device=self.device)
         self.repack()
@@ -183,10 +188,9 @@ class HipDuelingNet:
     def backward(self, dq: torch.Tensor, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
                  idx: torch.Tensor | None = None) -> None:
         """Write dL/dparam for the pass held in ``ws`` (input ``x``/``ids``/``idx`` as in
-        :meth:`forward`) into the model's ``.grad`` views."""
+        :meth:`forward`) into the model's ``.grad`` views, given dL/dQ ``dq``."""
         B, A = ws.B, self.A
-        xp, ip, jp = self._src(x, ids, idx, B)
-        h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        h, s, m = self.hip, self._s(), self.model
         if self._wgrad_ws is None:
             self.enable_backward()
         h.heads_bwd(dq.data_ptr(), ws.h.data_ptr(), m.advantage[2].weight.data_ptr(), m.value[2].weight.data_ptr(),
@@ -195,23 +199,43 @@ class HipDuelingNet:
                       m.advantage[2].weight.grad.data_ptr(), m.advantage[2].bias.grad.data_ptr(),
                       m.value[2].weight.grad.data_ptr(), m.value[2].bias.grad.data_ptr(),
                       m.advantage[0].bias.grad.data_ptr(), m.value[0].bias.grad.data_ptr(), s)
+        self.trunk_backward(x, ws, ids, idx)
+
+    def heads_finalize_job(self, part: torch.Tensor, G: int):
+        """grad_finalize job reducing ``G`` head/FC1-bias partial slabs (dqn_heads_bwd) into
+        the model's head gradients."""
+        m = self.model
+        return self.hip.heads_finalize_job(G, self.A, part.data_ptr(), m.advantage[2].weight.grad.data_ptr(),
+                                           m.advantage[2].bias.grad.data_ptr(), m.value[2].weight.grad.data_ptr(),
+                                           m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
+                                           m.value[0].bias.grad.data_ptr())
+
+    def trunk_backward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
+                       idx: torch.Tensor | None = None, extra_jobs=()) -> None:
+        """FC1 + conv backward from ``ws.dz_bf`` (dL/dz, bf16); the conv weight-gradient
+        partials of all three layers (+ ``extra_jobs``) are reduced by ONE grad_finalize."""
+        B = ws.B
+        xp, ip, jp = self._src(x, ids, idx, B)
+        h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        if self._wgrad_ws is None:
+            self.enable_backward()
         gfc1 = torch.mm(ws.dz_bf.t(), ws.a3, out_dtype=torch.float32)
         h.unpack_fc1_grad(gfc1.data_ptr(), m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(),
                           P3, C3, s)
         torch.mm(ws.dz_bf, self.wfc1p, out=ws.da3)
-        # conv3 .. conv1: ReLU mask of the FC1 input gradient, then MFMA wgrad/dgrad
-        wsp = self._wgrad_ws.data_ptr()
+        # conv3 .. conv1: ReLU mask of the FC1 input gradient, then MFMA wgrad (partials
+        # only) / dgrad; dgrad applies the ReLU backward of the layer below in its
+        # coalesced epilogue, so ws.dy2 / ws.dy1 hold the masked gradients as-is
+        w1, w2, w3 = (t.data_ptr() for t in self._wgrad_wss)
         h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
-        h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, wsp, f[4].weight.grad.data_ptr(),
-                     f[4].bias.grad.data_ptr(), s)
-        # dgrad applies the ReLU backward of the layer below in its coalesced epilogue, so
-        # ws.dy2 / ws.dy1 hold the masked gradients every consumer reads as-is
+        h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, s)
         h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
-        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, wsp, f[2].weight.grad.data_ptr(),
-                     f[2].bias.grad.data_ptr(), s)
+        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, s)
         h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
-        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, wsp, f[0].weight.grad.data_ptr(),
-                     f[0].bias.grad.data_ptr(), s)
+        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
+        jobs = [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
+                for k, wsp in ((3, w3), (2, w2), (1, w1))]
+        h.grad_finalize(jobs + list(extra_jobs), s)
 
 
 def forward_multi(passes) -> None:

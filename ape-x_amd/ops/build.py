@@ -44,6 +44,7 @@ HIP_SOURCES = [
     "aql_kernels.hip",
     "conv1_kernels.hip",
     "fc_kernels.hip",
+    "loss_heads_kernels.hip",
 ]
 
 

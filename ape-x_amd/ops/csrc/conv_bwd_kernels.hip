@@ -497,6 +497,7 @@ static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, const u
   float* bpart = ws + (size_t)G::GRID * G::N * G::K;
   wgrad_k<G><<<grid * G::KSPLIT, 256, 0, s>>>(x, fs, dy, mask, B, grid, partial, bpart);
   LAUNCH_CHECK();
+  if (!grad) return;  // partials only: grad_finalize reduces them with the other layers'
   const int total = G::N * G::K + G::N;
   wgrad_reduce_k<<<(total + 63) / 64, 256, 0, s>>>(partial, bpart, grid, G::N, G::C, G::KH, G::KW, grad, bias_grad);
   LAUNCH_CHECK();
@@ -521,6 +522,120 @@ void conv_wgrad(int layer, const void* x, const int* ids, const int* idx, const 
     case 3: launch_wgrad<WG3>(x, fs, dy, dy_mask, B, workspace, grad, bias_grad, s); break;
     default: throw std::invalid_argument("conv_wgrad: layer must be 1, 2 or 3");
   }
+}
+
+// ------------------------------------------------------------------ grad finalize
+// One launch for every batch-sliced gradient reduction of the learner step: the three conv
+// wgrad partial sets and the dqn_heads_bwd head/FC1-bias partials (previously four launches).
+// Each workgroup owns 64 outputs of one job; its 4 waves split the partial slices and the
+// slices are summed in a fixed order (deterministic).
+int wgrad_grid(int layer, int B) {
+  switch (layer) {
+    case 1: return std::min(WG1::GRID, B);
+    case 2: return std::min(WG2::GRID, B);
+    case 3: return std::min(WG3::GRID, B);
+    default: throw std::invalid_argument("wgrad layer");
+  }
+}
+
+__global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int j = 0;
+  while (j + 1 < fs.n && (int)blockIdx.x >= fs.job[j + 1].block0) ++j;
+  const FinalizeJob& jb = fs.job[j];
+  const int e = ((int)blockIdx.x - jb.block0) * 64 + lane;
+  const int total = jb.n_main + jb.n_bias;
+  float s = 0.f;
+  if (e < jb.n_main) {
+#pragma unroll 4
+    for (int g = wave; g < jb.G; g += 4) s += jb.part[(size_t)g * jb.pstride + e];
+  } else if (e < total) {
+#pragma unroll 4
+    for (int g = wave; g < jb.G; g += 4) s += jb.bpart[(size_t)g * jb.bstride + (e - jb.n_main)];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || e >= total) return;
+  const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (jb.kind == 0) {  // conv: [N][KH*KW*C] (c fastest) -> reference [N][C][KH][KW]
+    if (e < jb.n_main) {
+      const int K = jb.C * jb.KH * jb.KW, n = e / K, kidx = e % K, c = kidx % jb.C, tap = kidx / jb.C;
+      jb.out[0][((n * jb.C + c) * jb.KH + tap / jb.KW) * jb.KW + tap % jb.KW] = t;
+    } else {
+      jb.out[1][e - jb.n_main] = t;
+    }
+  } else {  // heads: [A][128] W_adv2 | [128] W_val2 | [A] b_adv2 | [1] b_val2 | [128] b_adv1 | [128] b_val1
+    const int A = jb.C;
+    if (e < A * 128) jb.out[0][e] = t;
+    else if (e < (A + 1) * 128) jb.out[2][e - A * 128] = t;
+    else if (e < (A + 1) * 128 + A) jb.out[1][e - (A + 1) * 128] = t;
+    else if (e < (A + 1) * 129) jb.out[3][0] = t;
+    else {
+      const int n = e - (A + 1) * 129;
+      if (n < 128) jb.out[4][n] = t; else jb.out[5][n - 128] = t;
+    }
+  }
+}
+
+void grad_finalize(FinalizeSet fs, hipStream_t s) {
+  if (fs.n < 1 || fs.n > kMaxFinalizeJobs) throw std::invalid_argument("grad_finalize: 1..4 jobs");
+  int blocks = 0;
+  for (int j = 0; j < fs.n; ++j) {
+    fs.job[j].block0 = blocks;
+    blocks += (fs.job[j].n_main + fs.job[j].n_bias + 63) / 64;
+  }
+  grad_finalize_k<<<blocks, 256, 0, s>>>(fs);
+  LAUNCH_CHECK();
+}
+
+FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad) {
+  FinalizeJob j{};
+  auto fill = [&](auto geo) {
+    using G = decltype(geo);
+    j.kind = 0;
+    j.G = std::min(G::GRID, B);
+    j.part = ws;
+    j.pstride = G::N * G::K;
+    j.bpart = ws + (size_t)G::GRID * G::N * G::K;
+    j.bstride = G::N;
+    j.n_main = G::N * G::K;
+    j.n_bias = G::N;
+    j.C = G::C;
+    j.KH = G::KH;
+    j.KW = G::KW;
+  };
+  switch (layer) {
+    case 1: fill(WG1{}); break;
+    case 2: fill(WG2{}); break;
+    case 3: fill(WG3{}); break;
+    default: throw std::invalid_argument("conv_finalize_job: layer");
+  }
+  j.out[0] = grad;
+  j.out[1] = bias_grad;
+  return j;
+}
+
+FinalizeJob heads_finalize_job(int G, int A, const float* part, float* g_wadv2, float* g_badv2, float* g_wval2,
+                               float* g_bval2, float* g_badv1, float* g_bval1) {
+  FinalizeJob j{};
+  const int stride = (A + 1) * 128 + (A + 1) + 256;
+  j.kind = 1;
+  j.G = G;
+  j.part = part;
+  j.pstride = stride;
+  j.bpart = part;
+  j.bstride = stride;
+  j.n_main = stride;
+  j.n_bias = 0;
+  j.C = A;
+  j.out[0] = g_wadv2;
+  j.out[1] = g_badv2;
+  j.out[2] = g_wval2;
+  j.out[3] = g_bval2;
+  j.out[4] = g_badv1;
+  j.out[5] = g_bval1;
+  return j;
 }
 
 // fp32 [N][C][KH][KW] -> bf16 W^T [KH][KW][C][N]

@@ -67,10 +67,15 @@ PYBIND11_MODULE(_apex_hip, m) {
   // ---- replay
   m.def("per_write_leaves", [](const TreeHandle& t, uint64_t idx, uint64_t prio, int B, float alpha,
                                uint64_t max_prio, int dedup, uint64_t sorted_scratch, uint64_t bump0, int64_t d0,
-                               uint64_t bump1, int64_t d1, uint64_t s) {
+                               uint64_t bump1, int64_t d1, uint64_t s, uint64_t mix_delta, uint64_t mix_lw,
+                               uint64_t mix_prio_out, uint64_t mix_loss_out) {
     per_write_leaves(t.d, P<const int>(idx), P<const float>(prio), B, alpha, P<float>(max_prio), dedup,
-                     P<int>(sorted_scratch), P<int64_t>(bump0), d0, P<int64_t>(bump1), d1, S(s));
-  });
+                     P<int>(sorted_scratch), P<int64_t>(bump0), d0, P<int64_t>(bump1), d1, S(s),
+                     P<const float>(mix_delta), P<const float>(mix_lw), P<float>(mix_prio_out), P<float>(mix_loss_out));
+  }, py::arg("t"), py::arg("idx"), py::arg("prio"), py::arg("B"), py::arg("alpha"), py::arg("max_prio"),
+     py::arg("dedup"), py::arg("sorted_scratch"), py::arg("bump0"), py::arg("d0"), py::arg("bump1"), py::arg("d1"),
+     py::arg("s"), py::arg("mix_delta") = 0, py::arg("mix_lw") = 0, py::arg("mix_prio_out") = 0,
+     py::arg("mix_loss_out") = 0);
   m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
                          int exclude_last, uint64_t s, uint64_t glob) {
@@ -291,6 +296,52 @@ PYBIND11_MODULE(_apex_hip, m) {
                P<const uint16_t>(dx_mask), B, S(s));
   });
   m.def("wgrad_workspace_floats", &wgrad_workspace_floats);
+  py::class_<FinalizeJob>(m, "FinalizeJob");
+  m.def("conv_finalize_job", [](int layer, int B, uint64_t ws, uint64_t grad, uint64_t bias_grad) {
+    return conv_finalize_job(layer, B, P<const float>(ws), P<float>(grad), P<float>(bias_grad));
+  });
+  m.def("heads_finalize_job", [](int G, int A, uint64_t part, uint64_t wadv2, uint64_t badv2, uint64_t wval2,
+                                 uint64_t bval2, uint64_t badv1, uint64_t bval1) {
+    return heads_finalize_job(G, A, P<const float>(part), P<float>(wadv2), P<float>(badv2), P<float>(wval2),
+                              P<float>(bval2), P<float>(badv1), P<float>(bval1));
+  });
+  m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s) {
+    if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..4 jobs");
+    FinalizeSet fs{};
+    for (size_t i = 0; i < jobs.size(); ++i) fs.job[i] = jobs[i];
+    fs.n = (int)jobs.size();
+    grad_finalize(fs, S(s));
+  });
+  m.def("wgrad_grid", &wgrad_grid);
+  m.def("dqn_heads_bwd_blocks", &dqn_heads_bwd_blocks);
+  m.def("dqn_heads_bwd", [](py::dict d, int B, int A, float gamma_n, uint64_t s) {
+    auto g = [&](const char* k) { return d.contains(k) ? d[k].cast<uint64_t>() : (uint64_t)0; };
+    LossHeadsArgs a{};
+    a.q = P<const float>(g("q"));
+    a.q2 = P<const float>(g("q2"));
+    a.q2t = P<const float>(g("q2t"));
+    a.act = P<const int>(g("act"));
+    a.rew = P<const float>(g("rew"));
+    a.done = P<const float>(g("done"));
+    a.idx = P<const int>(g("idx"));
+    a.w = P<const float>(g("w"));
+    a.h = P<const float>(g("h"));
+    a.w_adv2 = P<const float>(g("w_adv2"));
+    a.w_val2 = P<const float>(g("w_val2"));
+    a.B = B;
+    a.A = A;
+    a.gamma_n = gamma_n;
+    a.delta = P<float>(g("delta"));
+    a.lw = P<float>(g("lw"));
+    a.dz_bf = P<uint16_t>(g("dz_bf"));
+    a.part = P<float>(g("part"));
+    a.step = P<const int64_t>(g("step"));
+    a.step_snap = P<int64_t>(g("step_snap"));
+    if (!a.q || !a.q2 || !a.q2t || !a.act || !a.rew || !a.done || !a.w || !a.h || !a.w_adv2 || !a.w_val2 ||
+        !a.delta || !a.lw || !a.dz_bf || !a.part || !a.step)
+      throw std::invalid_argument("dqn_heads_bwd: missing pointer");
+    dqn_heads_bwd(a, S(s));
+  });
   m.def("conv_wgrad", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t dy_mask, int B,
                          uint64_t ws, uint64_t grad, uint64_t bgrad, uint64_t s) {
     conv_wgrad(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const uint16_t>(dy),

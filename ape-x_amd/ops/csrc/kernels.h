@@ -30,9 +30,12 @@ struct TreeDesc {
 // dedup = 1: duplicates resolve last-write-wins (B <= 1024, needs `sorted_scratch` [B]);
 // dedup = 0: `idx` must be unique ring-ordered slots (actor inserts).
 // bump0/bump1: optional device counters advanced by d0/d1 (fused counter updates).
+// mix_* (optional, dedup only): priorities from per-row TD errors with the batch-max mix
+// of utils.py:77, and the loss mean (see replay_kernels.hip PrioMix)
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
                       int dedup, int* sorted_scratch, int64_t* bump0, int64_t d0, int64_t* bump1, int64_t d1,
-                      hipStream_t s);
+                      hipStream_t s, const float* mix_delta = nullptr, const float* mix_lw = nullptr,
+                      float* mix_prio_out = nullptr, float* mix_loss_out = nullptr);
 void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 // length/beta are read from device memory when the pointers are non-null (so a captured
 // graph sees the live replay fill level and annealed beta), else the constants are used.
@@ -98,6 +101,48 @@ void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float*
                 int* slot_out, float* prio_out, hipStream_t s);
 // staged actor rows [E] -> replay tables at slot[e] (emitted rows only: prio[e] > 0)
 void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s);
+
+// ---- conv_bwd_kernels.hip: one launch for all batch-sliced gradient reductions
+constexpr int kMaxFinalizeJobs = 4;
+struct FinalizeJob {
+  int kind;                 // 0: conv wgrad (C, KH, KW), 1: heads (C = A)
+  const float* part;        // [G][pstride]
+  const float* bpart;       // [G][bstride] (conv bias partials)
+  int G, pstride, bstride, n_main, n_bias;
+  int C, KH, KW;
+  float* out[6];
+  int block0;               // set by grad_finalize
+};
+struct FinalizeSet {
+  FinalizeJob job[kMaxFinalizeJobs];
+  int n;
+};
+int wgrad_grid(int layer, int B);
+void grad_finalize(FinalizeSet fs, hipStream_t s);
+FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
+FinalizeJob heads_finalize_job(int G, int A, const float* part, float* g_wadv2, float* g_badv2, float* g_wval2,
+                               float* g_bval2, float* g_badv1, float* g_bval1);
+
+// ---- loss_heads_kernels.hip: dqn_loss + heads_bwd + head weight-grad partials, fused
+struct LossHeadsArgs {
+  const float *q, *q2, *q2t;       // [B][A] Q(s), Q(s'), Q_target(s')
+  const int* act;                  // replay transition table, read through idx
+  const float *rew, *done;
+  const int* idx;                  // sampled slots (nullptr: row b)
+  const float* w;                  // [B] IS weights
+  const float* h;                  // [B][256] post-ReLU hidden of the Q(s) pass
+  const float *w_adv2, *w_val2;    // head weights [A][128], [128]
+  int B, A;
+  float gamma_n;
+  float* delta;                    // [B] out: |y - Q(s,a)|
+  float* lw;                       // [B] out: w * Huber(delta)
+  uint16_t* dz_bf;                 // [B][256] out: dL/dz (FC1 pre-activation), bf16
+  float* part;                     // [blocks][(A+1)*128 + (A+1) + 256] out: gradient partials
+  const int64_t* step;             // learner step counter (read)
+  int64_t* step_snap;              // out: its value for this step's optimizer (may be null)
+};
+int dqn_heads_bwd_blocks(int B);
+void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s);
 
 // ---- learner_kernels.hip
 // (a, r, d) are read through idx (the sampled replay slots) when idx != nullptr.

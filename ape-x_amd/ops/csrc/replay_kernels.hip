@@ -27,12 +27,49 @@ namespace apex {
 // a separate counter launch per step.
 constexpr int kSortMax = 1024;
 
+// `mix` (optional, the learner's fused loss path): prio is derived here from the per-row
+// TD errors, prio_i = 0.9 max_j delta_j + 0.1 delta_i + 1e-6 (utils.py:77), and the loss
+// mean sum_i lw_i / B is written -- the batch-wide max/sum the row-parallel loss kernel
+// cannot do without another launch.  Reductions in the same fixed order as dqn_loss_k.
+struct PrioMix {
+  const float* delta;  // [B] |y - Q(s,a)|
+  const float* lw;     // [B] w_i * Huber(delta_i)
+  float* prio_out;     // [B] mixed priorities (as dqn_loss writes them)
+  float* loss_out;     // [1]
+};
+
+__device__ __forceinline__ float block_reduce_1024(float v, float* red, bool is_max) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = is_max ? -INFINITY : 0.f;
+  for (int i = 0; i < nw; ++i) t = is_max ? fmaxf(t, red[i]) : t + red[i];  // fixed order
+  return t;
+}
+
 __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, const int* __restrict__ idx,
                                                                   const float* __restrict__ prio, int B, float alpha,
                                                                   float* max_prio, int* __restrict__ sorted_out,
                                                                   int64_t* bump0, int64_t d0, int64_t* bump1,
-                                                                  int64_t d1) {
+                                                                  int64_t d1, PrioMix mix) {
   __shared__ unsigned long long key[kSortMax];
+  __shared__ float pmix[kSortMax];
+  __shared__ float red[16];
+  if (mix.delta) {
+    const int k = threadIdx.x;  // B <= blockDim.x
+    const float dl = k < B ? mix.delta[k] : 0.f;
+    const float total = block_reduce_1024(k < B ? mix.lw[k] : 0.f, red, false);
+    const float dmax = block_reduce_1024(k < B ? dl : -INFINITY, red, true);
+    if (k < B) {
+      const float p = 0.9f * dmax + 0.1f * dl + 1e-6f;
+      pmix[k] = p;
+      if (mix.prio_out) mix.prio_out[k] = p;
+    }
+    if (k == 0 && mix.loss_out) mix.loss_out[0] = total / (float)B;
+    prio = nullptr;
+  }
   int n = 1;
   while (n < B) n <<= 1;
   for (int k = threadIdx.x; k < n; k += blockDim.x)
@@ -59,12 +96,13 @@ __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, co
     sorted_out[k] = id;
     const bool last = (k == B - 1) || ((int)(key[k + 1] >> 32) != id);
     if (!last || id < 0 || id >= t.size[0]) continue;
-    const float p = prio ? prio[(int)(key[k] & 0xFFFFFFFFu)] : *max_prio;
+    const int src = (int)(key[k] & 0xFFFFFFFFu);
+    const float p = mix.delta ? pmix[src] : (prio ? prio[src] : *max_prio);
     if (p > 0.f && isfinite(p)) {
       const float v = powf(p, alpha);
       t.leaf_sum[id] = v;
       t.leaf_min[id] = v;
-      if (prio) atomic_max_pos_float(max_prio, p);
+      if (prio || mix.delta) atomic_max_pos_float(max_prio, p);
     } else {
       t.leaf_sum[id] = 0.f;
       t.leaf_min[id] = INFINITY;
@@ -320,13 +358,16 @@ __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
 // ------------------------------------------------------------------ launchers
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
                       int dedup, int* sorted_scratch, int64_t* bump0, int64_t d0, int64_t* bump1, int64_t d1,
-                      hipStream_t s) {
+                      hipStream_t s, const float* mix_delta, const float* mix_lw, float* mix_prio_out,
+                      float* mix_loss_out) {
   if (B <= 0) return;
+  if (mix_delta && (!dedup || !mix_lw)) throw std::invalid_argument("per_write_leaves: mixing needs dedup + lw");
   if (dedup) {
     if (B > kSortMax) throw std::invalid_argument("per_write_leaves: dedup batch must be <= 1024");
     if (!sorted_scratch) throw std::invalid_argument("per_write_leaves: dedup needs a sorted scratch buffer");
+    const PrioMix mix{mix_delta, mix_lw, mix_prio_out, mix_loss_out};
     per_write_leaves_sorted_k<<<1, 1024, 0, s>>>(t, idx, prio, B, alpha, max_prio, sorted_scratch, bump0, d0, bump1,
-                                                  d1);
+                                                  d1, mix);
     LAUNCH_CHECK();
     per_update_levels(t, sorted_scratch, B, s);
   } else if (B <= 1024) {

@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--actions", type=int, default=18)
     ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--overlap", action="store_true",
-                    help="actor graph on its own HIP stream, concurrent with the learner step")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="run the actor graph after the learner step on the same stream (default: the actor "
+                         "graph runs on its own HIP stream, concurrent with the learner step)")
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],

@@ -40,7 +40,7 @@ f = m.features
 net(x, ws)
 dq = torch.randn(B, 18, device=dev)
 net.backward(dq, x, ws)
-wsp = net._wgrad_ws.data_ptr()
+wsp = net._wgrad_wss[2].data_ptr()
 
 cases = {
     "conv1_fwd_dense": lambda: hip.conv_fwd(1, x.data_ptr(), 0, 0, net.w1p.data_ptr(), net.b1.data_ptr(),
