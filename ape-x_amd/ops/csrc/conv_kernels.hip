@@ -193,20 +193,26 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
     const int b = rb * kHeadRows + rr * 4 + wave;
     const bool valid = b < B;
     const float* zr = z + (size_t)(valid ? b : 0) * 256;
-    // all split-K partial loads first (independent), then the fixed-order sums
-    float zv[4][4];
+    // split-K slabs summed in fixed order; 4 columns per lane, loads of 2 slabs in flight
+    // per column ahead of the adds
+    float zs[4] = {0.f, 0.f, 0.f, 0.f};
+    const size_t sstride = (size_t)B * 256;
+    for (int sp = 0; sp < nsplit; sp += 2) {
+      float v0[4], v1[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+      for (int k = 0; k < 4; ++k) {
+        v0[k] = zr[(size_t)sp * sstride + lane + 64 * k];
+        v1[k] = sp + 1 < nsplit ? zr[(size_t)(sp + 1) * sstride + lane + 64 * k] : 0.f;
+      }
 #pragma unroll
-      for (int sp = 0; sp < 4; ++sp) zv[k][sp] = sp < nsplit ? zr[(size_t)sp * B * 256 + lane + 64 * k] : 0.f;
+      for (int k = 0; k < 4; ++k) zs[k] = (zs[k] + v0[k]) + v1[k];
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int j = lane + 64 * k;
       const float bias = j < 128 ? pr.b_adv1[j] : pr.b_val1[j - 128];
-      float zs = zv[k][0];
-      for (int sp = 1; sp < 4; ++sp) zs += zv[k][sp];
-      const float v = fmaxf(zs + bias, 0.f);
+      const float v = fmaxf(zs[k] + bias, 0.f);
       hs[wave][j] = v;
       if (pr.hout && valid) pr.hout[(size_t)b * 256 + j] = v;
     }
@@ -227,7 +233,7 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
 
 void heads_fwd_multi(const HeadsSet& set, hipStream_t s) {
   if (set.A < 1 || set.A > 63) throw std::invalid_argument("heads_fwd: 1 <= A <= 63");
-  if (set.nsplit < 1 || set.nsplit > 4) throw std::invalid_argument("heads_fwd: 1 <= nsplit <= 4");
+  if (set.nsplit < 1 || set.nsplit > 64) throw std::invalid_argument("heads_fwd: 1 <= nsplit <= 64");
   if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("heads_fwd: 1..3 problems");
   if (set.B <= 0) return;
   heads_fwd_k<<<set.n * ((set.B + kHeadRows - 1) / kHeadRows), 256, 0, s>>>(set);

@@ -1,17 +1,19 @@
 // FC1 of the dueling heads (Linear 3136 -> 2 x 128, adv | value hidden) for gfx950.
 //
-// z[B][256] = a3[B][3136] . W[256][3136]^T is skinny (M = batch, N = 256, K = 3136): a
-// library GEMM tiles only M x N (at B = 512: 128 32x32 tiles for 256 CUs) and walks the
-// long K serially.  Here K is split 4 ways and, inside a workgroup, across its 4 waves:
+// z[M][256] = a3[M][3136] . W[256][3136]^T is skinny (N = 256) with a long K; at the
+// learner's M = 3 x 512 (one launch for Q(s), Q(s'), Q_target(s')) the limit is the
+// per-CU L2 -> CU read rate (~70 GB/s per CU, MI355X_MICROARCH.md 'Indexed rows'), so
+// the tiling minimises bytes per CU rather than maximising workgroups:
 //
-//   * workgroup = 32 rows x 64 columns x K/4 (49 k-steps of 16); grid = B/32 x 4 x 4
-//     (256 workgroups at B = 512, 128 for the 256-env actor batch);
-//   * both MFMA operands are read straight from global memory into registers (A rows and
-//     W rows are K-contiguous: one 16-byte load per lane per fragment, L2-resident), all
-//     of a wave's loads issued before its MFMA chain -- no LDS staging;
-//   * the 4 waves' partial tiles are summed in LDS in fixed order and written as one fp32
-//     split-K partial [4][B][256]; heads_fwd sums the 4 partials (fixed order, so the
-//     result is deterministic) before bias + ReLU + the dueling heads.
+//   * workgroup = 128 rows x all 256 columns x one K slice (S slices, S adaptive so the
+//     grid is ~170-250 workgroups); W bytes per CU = 256 x K/S x 2 -- the W slice is read
+//     ONCE per workgroup into LDS (115 KB at S = 14), shared by the 4 waves, and each
+//     wave streams its own 32 A rows straight into registers (all loads issued first);
+//   * each wave computes 32 rows x 256 columns (8 accumulator tiles of
+//     v_mfma_f32_32x32x16_bf16), writing its fp32 split-K partial slab [S][M][256];
+//     heads_fwd sums the S slabs in fixed order (deterministic) before bias + ReLU.
+//   * LDS W rows are padded by 16 B (464 / 240 B): 16 consecutive lanes' ds_read_b128 hit
+//     16 distinct 4-bank groups (conflict free).
 #include "common.h"
 #include "kernels.h"
 
@@ -20,88 +22,105 @@ namespace apex {
 namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int FC_K = 3136, FC_N = 256, FC_KSTEPS = FC_K / 16;  // 196
-constexpr int FC_KSPLIT = 4, FC_KS_PER_SPLIT = FC_KSTEPS / FC_KSPLIT;  // 49
-constexpr int FC_KS_PER_WAVE = (FC_KS_PER_SPLIT + 3) / 4;            // 13
-static_assert(FC_KSTEPS % FC_KSPLIT == 0, "K split");
+constexpr int FC_K = 3136, FC_N = 256;
+constexpr int FC_TM = 128;                       // rows per workgroup
 }  // namespace
 
-int fc1_splits() { return FC_KSPLIT; }
+int fc1_splits() { return 28; }  // the most any launch uses (workspace sizing)
 
-// grid.x runs over the M tiles of all problems of the set (problem = tile / ceil(B/32))
+int fc1_splits_for(int total_rows) {
+  // 196 k-steps split 14 ways (14 k-steps per slice) when that already gives ~160+
+  // workgroups, else 28 ways (fewer bytes per CU, more partial slabs)
+  const int mt = (total_rows + FC_TM - 1) / FC_TM;
+  return mt * 14 >= 160 ? 14 : 28;
+}
+
+template <int KS>  // k-steps per slice
 __global__ __launch_bounds__(256) void fc1_fwd_k(FcSet set) {
-  __shared__ float red[4][32 * 65];  // per-wave 32 x 64 tiles, padded rows
+  constexpr int FC_WPITCH = KS * 32 + 16;  // LDS bytes per W row: 464 (KS 14) / 240 (KS 7)
+  __shared__ __attribute__((aligned(16))) char wsm[FC_N * FC_WPITCH];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
-  const int B = set.B, MT = (B + 31) / 32;
-  const int pb = blockIdx.x / MT, mtile = blockIdx.x - pb * MT, ntile = blockIdx.y, split = blockIdx.z;
+  const int B = set.B, MT = (B + FC_TM - 1) / FC_TM;
+  const int pb = blockIdx.x / MT, mtile = blockIdx.x - pb * MT, split = blockIdx.y;
   const uint16_t* __restrict__ a = set.p[pb].a;
   const uint16_t* __restrict__ w = set.p[pb].w;
   float* __restrict__ part = set.p[pb].part;
-  const int row = mtile * 32 + r32;
+  const int k0 = split * KS * 16;
+  // A fragments of this wave's 32 rows for the whole slice (row clamped; stores masked)
+  const int row = mtile * FC_TM + wave * 32 + r32;
   const int rowc = row < B ? row : B - 1;
-  // this wave's k-steps: split * 49 + [wave * 13, min(49, wave * 13 + 13))
-  const int ks0 = split * FC_KS_PER_SPLIT + wave * FC_KS_PER_WAVE;
-  const int nks = min(FC_KS_PER_WAVE, FC_KS_PER_SPLIT - wave * FC_KS_PER_WAVE);  // 13, 13, 13, 10
-  const uint16_t* ar = a + (size_t)rowc * FC_K + 8 * h;
-  const uint16_t* w0 = w + (size_t)(ntile * 64 + r32) * FC_K + 8 * h;
-  const uint16_t* w1 = w0 + (size_t)32 * FC_K;
-  bf16x8 fa[FC_KS_PER_WAVE], fb0[FC_KS_PER_WAVE], fb1[FC_KS_PER_WAVE];
+  const bf16x8* ar = reinterpret_cast<const bf16x8*>(a + (size_t)rowc * FC_K + k0 + 8 * h);
+  bf16x8 fa[KS];
 #pragma unroll
-  for (int i = 0; i < FC_KS_PER_WAVE; ++i) {
-    if (i < nks) {
-      const int k = (ks0 + i) * 16;
-      fa[i] = *reinterpret_cast<const bf16x8*>(ar + k);
-      fb0[i] = *reinterpret_cast<const bf16x8*>(w0 + k);
-      fb1[i] = *reinterpret_cast<const bf16x8*>(w1 + k);
+  for (int i = 0; i < KS; ++i) fa[i] = ar[2 * i];
+  // W slice [256][KS*16] -> LDS in 16-byte chunks, loads issued in rounds of 7
+  constexpr int CPR = KS * 2;        // 16-byte chunks per W row
+  constexpr int TOTAL = FC_N * CPR;
+  constexpr int PER = TOTAL / 256;
+  static_assert(TOTAL % 256 == 0 && PER % 7 == 0, "W slice chunking");
+#pragma unroll
+  for (int r0 = 0; r0 < PER; r0 += 7) {
+    u32v4 v[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int q = threadIdx.x + 256 * (r0 + j);
+      const int n = q / CPR, c = q % CPR;
+      v[j] = *reinterpret_cast<const u32v4*>(w + (size_t)n * FC_K + k0 + c * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int q = threadIdx.x + 256 * (r0 + j);
+      const int n = q / CPR, c = q % CPR;
+      *reinterpret_cast<u32v4*>(wsm + n * FC_WPITCH + c * 16) = v[j];
     }
   }
-  f32x16 acc0 = {}, acc1 = {};
+  __syncthreads();
+  f32x16 acc[8];
 #pragma unroll
-  for (int i = 0; i < FC_KS_PER_WAVE; ++i) {
-    if (i < nks) {
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb0[i], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb1[i], acc1, 0, 0, 0);
-    }
+  for (int t = 0; t < 8; ++t) acc[t] = f32x16{};
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    bf16x8 fb[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      fb[t] = *reinterpret_cast<const bf16x8*>(wsm + (t * 32 + r32) * FC_WPITCH + i * 32 + h * 16);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[t], acc[t], 0, 0, 0);
   }
-  // fixed-order sum of the 4 waves' tiles: rows = M (the C/D row map), cols = N
-  float* rw = red[wave];
+  // partial slab rows (r&3)+8(r>>2)+4h of the wave's 32, column t*32 + r32
+  const int rbase = mtile * FC_TM + wave * 32;
+  float* dst = part + ((size_t)split * B + rbase) * FC_N;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = (r & 3) + 8 * (r >> 2) + 4 * h;
-    rw[m * 65 + r32] = acc0[r];
-    rw[m * 65 + 32 + r32] = acc1[r];
-  }
-  __syncthreads();
-  // 32 x 64 outputs / 256 threads = 8 per thread: row = t / 8, 8 consecutive columns
-  const int orow = threadIdx.x >> 3, oc = (threadIdx.x & 7) * 8;
-  const int grow = mtile * 32 + orow;
-  if (grow < B) {
-    float v[8];
+    if (rbase + m < B) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int e = orow * 65 + oc + j;
-      v[j] = (red[0][e] + red[1][e]) + (red[2][e] + red[3][e]);
+      for (int t = 0; t < 8; ++t) dst[(size_t)m * FC_N + t * 32 + r32] = acc[t][r];
     }
-    float4* dst = reinterpret_cast<float4*>(part + ((size_t)split * B + grow) * FC_N + ntile * 64 + oc);
-    dst[0] = make_float4(v[0], v[1], v[2], v[3]);
-    dst[1] = make_float4(v[4], v[5], v[6], v[7]);
   }
 }
 
-void fc1_fwd_multi(const FcSet& set, hipStream_t s) {
-  if (set.B <= 0) return;
+int fc1_fwd_multi(const FcSet& set, hipStream_t s) {
+  if (set.B <= 0) return 0;
   if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("fc1_fwd: 1..3 problems");
-  const dim3 grid(set.n * ((set.B + 31) / 32), FC_N / 64, FC_KSPLIT);
-  fc1_fwd_k<<<grid, 256, 0, s>>>(set);
+  const int MT = (set.B + FC_TM - 1) / FC_TM;
+  const int S = fc1_splits_for(set.n * set.B);
+  const dim3 grid(set.n * MT, S);
+  if (S == 14) {
+    fc1_fwd_k<14><<<grid, 256, 0, s>>>(set);
+  } else {
+    fc1_fwd_k<7><<<grid, 256, 0, s>>>(set);
+  }
   LAUNCH_CHECK();
+  return S;
 }
 
-void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s) {
+int fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s) {
   FcSet set{};
   set.p[0] = FcProb{a, w, part};
   set.n = 1;
   set.B = B;
-  fc1_fwd_multi(set, s);
+  return fc1_fwd_multi(set, s);
 }
 
 }  // namespace apex

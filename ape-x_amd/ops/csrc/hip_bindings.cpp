@@ -236,14 +236,14 @@ PYBIND11_MODULE(_apex_hip, m) {
     set.B = B;
     conv_fwd_multi(layer, set, S(s));
   });
-  m.def("fc1_fwd_multi", [](const std::vector<std::array<uint64_t, 3>>& probs, int B, uint64_t s) {
+  m.def("fc1_fwd_multi", [](const std::vector<std::array<uint64_t, 3>>& probs, int B, uint64_t s) -> int {
     if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
     FcSet set{};
     for (size_t i = 0; i < probs.size(); ++i)
       set.p[i] = FcProb{P<const uint16_t>(probs[i][0]), P<const uint16_t>(probs[i][1]), P<float>(probs[i][2])};
     set.n = (int)probs.size();
     set.B = B;
-    fc1_fwd_multi(set, S(s));
+    return fc1_fwd_multi(set, S(s));
   });
   m.def("heads_fwd_multi", [](const std::vector<std::array<uint64_t, 9>>& probs, int nsplit, int B, int A,
                               uint64_t s) {
@@ -263,8 +263,9 @@ PYBIND11_MODULE(_apex_hip, m) {
   });
   m.def("fc1_splits", &fc1_splits);
   m.def("fc1_fwd", [](uint64_t a, uint64_t w, uint64_t part, int B, uint64_t s) {
-    fc1_fwd(P<const uint16_t>(a), P<const uint16_t>(w), P<float>(part), B, S(s));
+    return fc1_fwd(P<const uint16_t>(a), P<const uint16_t>(w), P<float>(part), B, S(s));
   });
+  m.def("fc1_splits_for", &fc1_splits_for);
   m.def("heads_fwd", [](uint64_t z, int nsplit, uint64_t ba1, uint64_t bv1, uint64_t wa2, uint64_t ba2, uint64_t wv2,
                         uint64_t bv2, uint64_t hout, uint64_t q, int B, int A, uint64_t s) {
     heads_fwd(P<const float>(z), nsplit, P<const float>(ba1), P<const float>(bv1), P<const float>(wa2), P<const float>(ba2),

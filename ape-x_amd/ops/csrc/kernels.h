@@ -208,18 +208,19 @@ void heads_fwd(const float* z, int nsplit, const float* b_adv1, const float* b_v
                const float* b_adv2, const float* w_val2, const float* b_val2, float* hout, float* q, int B, int A,
                hipStream_t s);
 // fc_kernels.hip: split-K FC1 (a3 [B][3136] bf16 . W [256][3136]^T) -> fp32 partials [fc1_splits()][B][256]
-int fc1_splits();
-void fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s);
+int fc1_splits();                   // max slabs any launch writes (workspace sizing)
+int fc1_splits_for(int total_rows);  // slabs a launch over total_rows rows writes
+int fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_t s);  // returns slabs
 struct FcProb {
   const uint16_t* a;  // a3 [B][3136] bf16
   const uint16_t* w;  // [256][3136] bf16
-  float* part;        // [fc1_splits()][B][256]
+  float* part;        // [slabs][B][256] fp32 split-K partials
 };
 struct FcSet {
   FcProb p[kMaxProbs];
   int n, B;
 };
-void fc1_fwd_multi(const FcSet& set, hipStream_t s);
+int fc1_fwd_multi(const FcSet& set, hipStream_t s);  // returns the slab count
 struct HeadsProb {
   const float* z;  // FC1 split-K partials [nsplit][B][256]
   const float *b_adv1, *b_val1, *w_adv2, *b_adv2, *w_val2, *b_val2;

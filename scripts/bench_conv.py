@@ -53,7 +53,7 @@ cases = {
                                       ws.a3.data_ptr(), B, s),
     "fc1_fwd": lambda: hip.fc1_fwd(ws.a3.data_ptr(), net.wfc1p.data_ptr(), ws.z.data_ptr(), B, s),
     "fc1_fwd_blaslt": lambda: torch.mm(ws.a3, net.wfc1p.t(), out_dtype=torch.float32, out=ws.z[0]),
-    "heads_fwd": lambda: hip.heads_fwd(ws.z.data_ptr(), 4, m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
+    "heads_fwd": lambda: hip.heads_fwd(ws.z.data_ptr(), hip.fc1_splits_for(B), m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
                                        m.advantage[2].weight.data_ptr(), m.advantage[2].bias.data_ptr(),
                                        m.value[2].weight.data_ptr(), m.value[2].bias.data_ptr(), ws.h.data_ptr(),
                                        ws.q.data_ptr(), B, 18, s),

@@ -242,7 +242,7 @@ def test_fused_optimizer_packing_matches_repack(cuda, opt):
     assert torch.equal(fused.view(torch.int16), net.arena.view(torch.int16))
 
 
-@pytest.mark.parametrize("B", [512, 256, 37])
+@pytest.mark.parametrize("B", [1536, 512, 256, 37])
 def test_fc1_splitk_matches_torch(cuda, B):
     """Split-K FC1 partials sum to the fp32 GEMM of the same bf16 operands (ragged batch
     included: the last 32-row tile is clamped on load and masked on store)."""
@@ -254,18 +254,19 @@ def test_fc1_splitk_matches_torch(cuda, B):
     a = _rand_bf16((B, FEAT), cuda, g=g)
     w = _rand_bf16((256, FEAT), cuda, scale=0.02, g=g)
     part = torch.full((FC1_SPLITS, B, 256), float("nan"), device=cuda)
-    hip.fc1_fwd(a.data_ptr(), w.data_ptr(), part.data_ptr(), B, torch.cuda.current_stream().cuda_stream)
+    S = hip.fc1_fwd(a.data_ptr(), w.data_ptr(), part.data_ptr(), B, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
+    assert S == hip.fc1_splits_for(B) and 1 <= S <= FC1_SPLITS
     want = a.float() @ w.float().t()
-    got = part.sum(0)
-    assert torch.isfinite(part).all()
+    got = part[:S].sum(0)
+    assert torch.isfinite(part[:S]).all()
     assert (got - want).abs().max().item() <= 1e-4 * max(1.0, want.abs().max().item())
 
 
 @pytest.mark.parametrize("B", [512, 37])
 def test_forward_multi_equals_single_passes(cuda, B):
     """One launch per layer for 3 passes (two nets, ring input via ids/idx) gives the
-    same bits as three single-pass forwards."""
+    same activations as three single-pass forwards."""
     from apex_amd.models.fused import HipDuelingNet, NetWorkspace, forward_multi
 
     m1, m2 = _model(cuda, seed=1), _model(cuda, seed=2)
@@ -284,6 +285,8 @@ def test_forward_multi_equals_single_passes(cuda, B):
     n2(frames, ws[5], s2_ids, idx)
     torch.cuda.synchronize()
     for a, b in ((0, 3), (1, 4), (2, 5)):
-        assert torch.equal(ws[a].q, ws[b].q)
+        # conv activations bit-identical; FC1's split-K slab count follows the launch's
+        # total rows, so Q may differ by fp32 summation order only
         assert torch.equal(ws[a].a1, ws[b].a1) and torch.equal(ws[a].a3, ws[b].a3)
+        torch.testing.assert_close(ws[a].q, ws[b].q, rtol=1e-5, atol=1e-6 * ws[b].q.abs().max().item())
     assert not torch.equal(ws[1].q, ws[2].q)  # different nets really ran
