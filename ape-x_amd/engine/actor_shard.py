@@ -129,9 +129,15 @@ class ActorShard:
     def apply_staged(self, parity: int) -> None:
         """Scatter staging set ``parity`` into the replay tables and write its
         priorities into the tree (the learner stream's half of a staged actor step)."""
+        self.apply_rows(parity)
+        self.apply_prios(parity)
+
+    def apply_rows(self, parity: int) -> None:
         self.hip.apply_staged_rows(self.stage_ptrs[parity], self.replay.trans_ptrs(),
                                    self.stage_slot[parity].data_ptr(), self.stage_prio[parity].data_ptr(), self.E,
                                    self._stream())
+
+    def apply_prios(self, parity: int) -> None:
         self.replay.write_priorities(self.stage_slot[parity], self.stage_prio[parity], dedup=False,
                                      bumps=((self.replay.filled, self.E),))
 

@@ -128,7 +128,14 @@ class ApexEngine:
 
     def _learn_a(self, apply_half: int | None = None):
         if apply_half is not None and self._sharded is None:
-            self._apply_half(apply_half)  # sharded: applied before the mass exchange instead
+            # rows now (before sampling: a sampled slot never changes under the learner);
+            # their priorities on the learner's tree stream, beside the backward (the new
+            # transitions become sampleable one learner step later).  Sharded: applied in
+            # full before the shard-mass exchange instead.
+            k = self.cfg.actor_steps_per_learner_step
+            for i in range(k):
+                self.actor.apply_rows(apply_half * k + i)
+            self.learner.tree_hooks = [lambda i=i: self.actor.apply_prios(apply_half * k + i) for i in range(k)]
         self.learner.sample_and_forward()
 
     def _learn_b(self):

@@ -133,6 +133,9 @@ class DQNLearner:
                                        device=dev)
             self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
             self.tree_stream = torch.cuda.Stream(device=dev)
+        # one-shot callables run on the tree stream before this step's priority write
+        # (the overlapped engine's deferred actor-row priorities)
+        self.tree_hooks = []
 
     @staticmethod
     def _stream() -> int:
@@ -168,12 +171,18 @@ class DQNLearner:
             main = torch.cuda.current_stream()
             self.tree_stream.wait_stream(main)
             with torch.cuda.stream(self.tree_stream):
+                hooks, self.tree_hooks = self.tree_hooks, []
+                for fn in hooks:
+                    fn()
                 self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
                                              mix=(self.delta, self.lw, self.prio, self.loss))
             self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
                                     extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)])
             main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
             return
+        hooks, self.tree_hooks = self.tree_hooks, []
+        for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
+            fn()
         self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
         q = forward_q(self.model, self.s)
         with torch.no_grad():
