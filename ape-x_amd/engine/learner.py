@@ -44,6 +44,7 @@ class LearnerConfig:
     optimizer: str = "rmsprop"     # or "adam"
     forward: str = "torch"         # "torch" (MIOpen bf16 trunk) | "hip" (MFMA kernels)
     seed: int = 0
+    tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = True) -> torch.Tensor:
@@ -169,8 +170,10 @@ class DQNLearner:
                  "step_snap": self.step_snap.data_ptr()}, self.B, self.A, self.gamma_n, s)
             # fork: priority mix + loss mean + tree write (+ step bump) beside the backward
             main = torch.cuda.current_stream()
-            self.tree_stream.wait_stream(main)
-            with torch.cuda.stream(self.tree_stream):
+            fork = self.cfg.tree_fork
+            if fork:
+                self.tree_stream.wait_stream(main)
+            with torch.cuda.stream(self.tree_stream if fork else main):
                 hooks, self.tree_hooks = self.tree_hooks, []
                 for fn in hooks:
                     fn()
@@ -178,7 +181,8 @@ class DQNLearner:
                                              mix=(self.delta, self.lw, self.prio, self.loss))
             self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
                                     extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)])
-            main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
+            if fork:
+                main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling

@@ -51,6 +51,8 @@ def parse():
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
     ap.add_argument("--seed", type=int, default=1122)
+    ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
+                    help="priority-tree writes on the learner stream instead of a forked stream")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
                     help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
@@ -88,7 +90,7 @@ def main():
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
-    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank)
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
@@ -121,6 +123,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.train_step()
+    t_host = time.perf_counter() - t0  # host enqueue time (the GPU may still be running)
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -171,6 +174,7 @@ def main():
             "learner_samples_per_sec": round(steps_per_s * args.batch, 1),
             "vs_paper_19_batches_per_s": round(steps_per_s / PAPER_BATCHES_PER_S, 2),
             "replay_fill_seconds": round(t_fill, 3),
+            "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
             "last_loss": round(stats["loss"], 6),
             "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
         }
