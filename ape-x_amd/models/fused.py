@@ -72,7 +72,7 @@ class HipDuelingNet:
     # packed bf16 weights live in one arena: [w1p | w2p | w3p | wfc1p | w2t | w3t]
     # (conv1 keeps the reference layout [n][c][ky][kx]: its kernel's K order is (c, ky, kx))
     LAYOUT = (("w1p", (32, 4, 8, 8)), ("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, FEAT)),
-              ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)))
+              ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)), ("wfc1t", (FEAT, 256)))
 
     def __init__(self, model: DuelingDQN):
         assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
@@ -125,6 +125,15 @@ class HipDuelingNet:
         ref = torch.arange(128 * FEAT).view(128, C3, P3).permute(0, 2, 1).reshape(-1)
         place(dst1, "advantage.0.weight", ref, ao["wfc1p"])
         place(dst1, "value.0.weight", ref, ao["wfc1p"] + 128 * FEAT)
+        # W^T [k = p*64 + c][n] for the FC1 input-gradient GEMM (value rows at n + 128):
+        # reference element (n, c*49 + p) -> wfc1t[(p*64 + c)*256 + n]
+        n_i = torch.arange(128).view(128, 1, 1)
+        c_i = torch.arange(C3).view(1, C3, 1)
+        p_i = torch.arange(P3).view(1, 1, P3)
+        post = ((p_i * C3 + c_i) * 256 + n_i).reshape(-1)  # in reference (n, c, p) order
+        for pname, n0 in (("advantage.0.weight", 0), ("value.0.weight", 128)):
+            o, n = seg[pname]
+            dst2[o:o + n] = ao["wfc1t"] + n0 + post
         self._maps = (dst1.to(torch.int32).to(self.device), dst2.to(torch.int32).to(self.device))
         return self._maps
 
@@ -146,6 +155,7 @@ class HipDuelingNet:
         if self._wgrad_ws is not None:  # the backward is only used by the learner's online net
             h.pack_conv_wt(f[2].weight.data_ptr(), self.w2t.data_ptr(), 64, 32, 4, 4, s)
             h.pack_conv_wt(f[4].weight.data_ptr(), self.w3t.data_ptr(), 64, 64, 3, 3, s)
+            self.wfc1t.copy_(self.wfc1p.t())
 
     def enable_backward(self) -> None:
         """Allocate backward workspaces + transposed weights (call before graph capture).
@@ -156,6 +166,7 @@ class HipDuelingNet:
         self._wgrad_ws = self._wgrad_wss[0]
         self._heads_ws = torch.empty(self.hip.heads_wgrad_workspace_floats(self.A), dtype=torch.float32,
                                      device=self.device)
+        self._fc1_ws = torch.empty(self.hip.fc1_bwd_workspace_floats(), dtype=torch.float32, device=self.device)
         self.repack()
 
     # ------------------------------------------------------------------ forward
@@ -220,15 +231,12 @@ class HipDuelingNet:
         h, s, m, f = self.hip, self._s(), self.model, self.model.features
         if self._wgrad_ws is None:
             self.enable_backward()
-        gfc1 = torch.mm(ws.dz_bf.t(), ws.a3, out_dtype=torch.float32)
-        h.unpack_fc1_grad(gfc1.data_ptr(), m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(),
-                          P3, C3, s)
-        torch.mm(ws.dz_bf, self.wfc1p, out=ws.da3)
-        # conv3 .. conv1: ReLU mask of the FC1 input gradient, then MFMA wgrad (partials
-        # only) / dgrad; dgrad applies the ReLU backward of the layer below in its
-        # coalesced epilogue, so ws.dy2 / ws.dy1 hold the masked gradients as-is
+        # FC1: dy3 = relu_mask(dz . W) and dW slabs in one launch; then conv3 .. conv1 MFMA
+        # wgrad (partials only) / dgrad, where dgrad applies the ReLU backward of the
+        # layer below in its coalesced epilogue (ws.dy2 / ws.dy1 are the masked gradients)
+        h.fc1_bwd(ws.dz_bf.data_ptr(), ws.a3.data_ptr(), self.wfc1t.data_ptr(), ws.dy3.data_ptr(),
+                  self._fc1_ws.data_ptr(), B, s)
         w1, w2, w3 = (t.data_ptr() for t in self._wgrad_wss)
-        h.relu_mask_bf16(ws.da3.data_ptr(), ws.a3.data_ptr(), ws.dy3.data_ptr(), ws.dy3.numel(), s)
         h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, s)
         h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
         h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, s)
@@ -236,6 +244,8 @@ class HipDuelingNet:
         h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
         jobs = [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
+        jobs += [h.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
+                 h.fc1_finalize_job(1, self._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
         h.grad_finalize(jobs + list(extra_jobs), s)
 
 

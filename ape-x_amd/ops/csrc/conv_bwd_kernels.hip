@@ -538,26 +538,50 @@ int wgrad_grid(int layer, int B) {
   }
 }
 
+// outputs per workgroup: 64 when the 4 waves split many slices (G >= kWideG), 256 (one per
+// thread, 4 independent chains) when the job has few slices and many outputs (FC1)
+constexpr int kWideG = 16;
+__host__ __device__ inline int finalize_outputs_per_block(int G) { return G >= kWideG ? 64 : 256; }
+
 __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int j = 0;
   while (j + 1 < fs.n && (int)blockIdx.x >= fs.job[j + 1].block0) ++j;
   const FinalizeJob& jb = fs.job[j];
-  const int e = ((int)blockIdx.x - jb.block0) * 64 + lane;
   const int total = jb.n_main + jb.n_bias;
-  float s = 0.f;
-  if (e < jb.n_main) {
+  int e;
+  float t;
+  if (jb.G >= kWideG) {
+    e = ((int)blockIdx.x - jb.block0) * 64 + lane;
+    float s = 0.f;
+    if (e < jb.n_main) {
 #pragma unroll 4
-    for (int g = wave; g < jb.G; g += 4) s += jb.part[(size_t)g * jb.pstride + e];
-  } else if (e < total) {
+      for (int g = wave; g < jb.G; g += 4) s += jb.part[(size_t)g * jb.pstride + e];
+    } else if (e < total) {
 #pragma unroll 4
-    for (int g = wave; g < jb.G; g += 4) s += jb.bpart[(size_t)g * jb.bstride + (e - jb.n_main)];
+      for (int g = wave; g < jb.G; g += 4) s += jb.bpart[(size_t)g * jb.bstride + (e - jb.n_main)];
+    }
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave != 0 || e >= total) return;
+    t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  } else {
+    e = ((int)blockIdx.x - jb.block0) * 256 + threadIdx.x;
+    if (e >= total) return;
+    const float* src = e < jb.n_main ? jb.part + e : jb.bpart + (e - jb.n_main);
+    const size_t st = e < jb.n_main ? (size_t)jb.pstride : (size_t)jb.bstride;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int g = 0;
+    for (; g + 4 <= jb.G; g += 4) {
+      s0 += src[(size_t)g * st];
+      s1 += src[(size_t)(g + 1) * st];
+      s2 += src[(size_t)(g + 2) * st];
+      s3 += src[(size_t)(g + 3) * st];
+    }
+    for (; g < jb.G; ++g) s0 += src[(size_t)g * st];
+    t = (s0 + s1) + (s2 + s3);
   }
-  red[wave][lane] = s;
-  __syncthreads();
-  if (wave != 0 || e >= total) return;
-  const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   if (jb.kind == 0) {  // conv: [N][KH*KW*C] (c fastest) -> reference [N][C][KH][KW]
     if (e < jb.n_main) {
       const int K = jb.C * jb.KH * jb.KW, n = e / K, kidx = e % K, c = kidx % jb.C, tap = kidx / jb.C;
@@ -579,11 +603,12 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
 }
 
 void grad_finalize(FinalizeSet fs, hipStream_t s) {
-  if (fs.n < 1 || fs.n > kMaxFinalizeJobs) throw std::invalid_argument("grad_finalize: 1..4 jobs");
+  if (fs.n < 1 || fs.n > kMaxFinalizeJobs) throw std::invalid_argument("grad_finalize: 1..6 jobs");
   int blocks = 0;
   for (int j = 0; j < fs.n; ++j) {
     fs.job[j].block0 = blocks;
-    blocks += (fs.job[j].n_main + fs.job[j].n_bias + 63) / 64;
+    const int per = finalize_outputs_per_block(fs.job[j].G);
+    blocks += (fs.job[j].n_main + fs.job[j].n_bias + per - 1) / per;
   }
   grad_finalize_k<<<blocks, 256, 0, s>>>(fs);
   LAUNCH_CHECK();
@@ -613,6 +638,26 @@ FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, fl
   }
   j.out[0] = grad;
   j.out[1] = bias_grad;
+  return j;
+}
+
+FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad) {
+  // [G][256][7*7*64] natural (p, c) order == a 7x7 conv with C = 64 -> [n][c][7][7]
+  constexpr int K = 49 * 64;
+  FinalizeJob j{};
+  j.kind = 0;
+  j.G = fc1_bwd_slices();
+  j.part = ws + (size_t)half * 128 * K;
+  j.pstride = 256 * K;
+  j.bpart = nullptr;
+  j.bstride = 0;
+  j.n_main = 128 * K;
+  j.n_bias = 0;
+  j.C = 64;
+  j.KH = 7;
+  j.KW = 7;
+  j.out[0] = grad;
+  j.out[1] = nullptr;
   return j;
 }
 

@@ -306,8 +306,17 @@ PYBIND11_MODULE(_apex_hip, m) {
     return heads_finalize_job(G, A, P<const float>(part), P<float>(wadv2), P<float>(badv2), P<float>(wval2),
                               P<float>(bval2), P<float>(badv1), P<float>(bval1));
   });
+  m.def("fc1_finalize_job", [](int half, uint64_t ws, uint64_t grad) {
+    return fc1_finalize_job(half, P<const float>(ws), P<float>(grad));
+  });
+  m.def("fc1_bwd_slices", &fc1_bwd_slices);
+  m.def("fc1_bwd_workspace_floats", &fc1_bwd_workspace_floats);
+  m.def("fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wt, uint64_t dy3, uint64_t part, int B, uint64_t s) {
+    fc1_bwd(P<const uint16_t>(dz), P<const uint16_t>(a3), P<const uint16_t>(wt), P<uint16_t>(dy3), P<float>(part), B,
+            S(s));
+  });
   m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s) {
-    if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..4 jobs");
+    if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..6 jobs");
     FinalizeSet fs{};
     for (size_t i = 0; i < jobs.size(); ++i) fs.job[i] = jobs[i];
     fs.n = (int)jobs.size();

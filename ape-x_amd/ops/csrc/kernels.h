@@ -103,7 +103,7 @@ void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float*
 void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s);
 
 // ---- conv_bwd_kernels.hip: one launch for all batch-sliced gradient reductions
-constexpr int kMaxFinalizeJobs = 4;
+constexpr int kMaxFinalizeJobs = 6;
 struct FinalizeJob {
   int kind;                 // 0: conv wgrad (C, KH, KW), 1: heads (C = A)
   const float* part;        // [G][pstride]
@@ -120,6 +120,8 @@ struct FinalizeSet {
 int wgrad_grid(int layer, int B);
 void grad_finalize(FinalizeSet fs, hipStream_t s);
 FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
+// FC1 weight half (0: advantage rows 0..127, 1: value rows 128..255) of fc1_bwd's slabs
+FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad);
 FinalizeJob heads_finalize_job(int G, int A, const float* part, float* g_wadv2, float* g_badv2, float* g_wval2,
                                float* g_bval2, float* g_badv1, float* g_bval1);
 
@@ -221,6 +223,12 @@ struct FcSet {
   int n, B;
 };
 int fc1_fwd_multi(const FcSet& set, hipStream_t s);  // returns the slab count
+// FC1 backward: dy3 = relu_mask(dz . W, a3) (bf16) and dW partial slabs [fc1_bwd_slices()]
+// [256][3136] (natural k order; reduce + scatter with two grad_finalize conv-style jobs)
+int fc1_bwd_slices();
+size_t fc1_bwd_workspace_floats();
+void fc1_bwd(const uint16_t* dz, const uint16_t* a3, const uint16_t* wt, uint16_t* dy3, float* part, int B,
+             hipStream_t s);
 struct HeadsProb {
   const float* z;  // FC1 split-K partials [nsplit][B][256]
   const float *b_adv1, *b_val1, *w_adv2, *b_adv2, *w_val2, *b_val2;

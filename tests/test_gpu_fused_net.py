@@ -290,3 +290,34 @@ def test_forward_multi_equals_single_passes(cuda, B):
         assert torch.equal(ws[a].a1, ws[b].a1) and torch.equal(ws[a].a3, ws[b].a3)
         torch.testing.assert_close(ws[a].q, ws[b].q, rtol=1e-5, atol=1e-6 * ws[b].q.abs().max().item())
     assert not torch.equal(ws[1].q, ws[2].q)  # different nets really ran
+
+
+@pytest.mark.parametrize("B", [512, 100])
+def test_fc1_backward_matches_torch(cuda, B):
+    """fc1_bwd: dy3 = relu_mask(dz . W, a3) in bf16 and the dW slabs reduced + scattered by
+    grad_finalize into the reference [n][c*49+p] layout, vs torch fp32 on the same
+    bf16-valued operands."""
+    from apex_amd import ops
+    from apex_amd.models.fused import C3, FEAT, P3
+
+    hip = ops.hip()
+    g = torch.Generator().manual_seed(B)
+    dz = _rand_bf16((B, 256), cuda, scale=0.1, g=g)
+    a3 = torch.relu(_rand_bf16((B, FEAT), cuda, g=g))  # post-ReLU activations (zeros included)
+    w = _rand_bf16((256, FEAT), cuda, scale=0.05, g=g)  # packed [n][p*64+c]
+    wt = w.t().contiguous()
+    dy3 = torch.full((B, FEAT), 7.0, dtype=torch.bfloat16, device=cuda)
+    ws = torch.full((hip.fc1_bwd_workspace_floats(),), float("nan"), device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    hip.fc1_bwd(dz.data_ptr(), a3.data_ptr(), wt.data_ptr(), dy3.data_ptr(), ws.data_ptr(), B, s)
+    ga = torch.zeros(128, FEAT, device=cuda)
+    gv = torch.zeros(128, FEAT, device=cuda)
+    hip.grad_finalize([hip.fc1_finalize_job(0, ws.data_ptr(), ga.data_ptr()),
+                       hip.fc1_finalize_job(1, ws.data_ptr(), gv.data_ptr())], s)
+    torch.cuda.synchronize()
+    dx = (dz.float() @ w.float()) * (a3.float() > 0)
+    torch.testing.assert_close(dy3.float(), dx, rtol=1e-2, atol=1e-3)
+    gw = dz.float().t() @ a3.float()  # [256][p*64+c]
+    ref = gw.view(256, P3, C3).permute(0, 2, 1).reshape(256, FEAT)  # -> [n][c*49+p]
+    torch.testing.assert_close(ga, ref[:128], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gv, ref[128:], rtol=1e-4, atol=1e-4)
