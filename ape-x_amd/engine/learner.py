@@ -116,6 +116,7 @@ class DQNLearner:
         self.sharded = sharded      # parallel.sharded.ShardedSampling (global PER over shards)
         self.host_steps = 0
         self.hip_net = cfg.forward == "hip"
+        self.n_fin_partials = 0
         if self.hip_net:
             self.net = HipDuelingNet(self.model)
             self.net.enable_backward()
@@ -134,6 +135,11 @@ class DQNLearner:
                                        device=dev)
             self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
             self.tree_stream = torch.cuda.Stream(device=dev)
+            # single-process learner: grad_finalize writes the grad-norm partials (every
+            # gradient passes through it), so no separate sum-of-squares pass; with an
+            # all-reduce the norm must be taken after it (grad_sumsq)
+            self.fin_partials = torch.zeros(8192, dtype=torch.float64, device=dev)
+            self.n_fin_partials = 0
         # one-shot callables run on the tree stream before this step's priority write
         # (the overlapped engine's deferred actor-row priorities)
         self.tree_hooks = []
@@ -179,8 +185,13 @@ class DQNLearner:
                     fn()
                 self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
                                              mix=(self.delta, self.lw, self.prio, self.loss))
-            self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
-                                    extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)])
+            fused_norm = self.allreduce is None
+            n = self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
+                                        extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)],
+                                        sumsq=self.fin_partials if fused_norm else None)
+            if fused_norm:
+                assert n <= self.fin_partials.numel()
+                self.n_fin_partials = n
             if fork:
                 main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
             return
@@ -204,14 +215,18 @@ class DQNLearner:
     def optimize(self) -> None:
         s = self._stream()
         h = self.hip
-        h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
+        if self.hip_net and self.n_fin_partials:
+            parts, nparts = self.fin_partials, self.n_fin_partials  # from grad_finalize
+        else:
+            h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
+            parts, nparts = self.partials, self.partials.numel()
         pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if self.hip_net else (0, 0, 0)
         step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
         # the fused path already bumped step_counter on the tree stream: the optimizer reads
         # this step's snapshot instead
         stp = self.step_snap if self.hip_net else self.step_counter
         step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(), self.opt_s2.data_ptr(), self.P,
-             self.partials.data_ptr(), self.partials.numel(), self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk)
+             parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk)
         if not self.hip_net:
             self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 

@@ -223,9 +223,11 @@ class HipDuelingNet:
                                            m.value[0].bias.grad.data_ptr())
 
     def trunk_backward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
-                       idx: torch.Tensor | None = None, extra_jobs=()) -> None:
-        """FC1 + conv backward from ``ws.dz_bf`` (dL/dz, bf16); the conv weight-gradient
-        partials of all three layers (+ ``extra_jobs``) are reduced by ONE grad_finalize."""
+                       idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None) -> int:
+        """FC1 + conv backward from ``ws.dz_bf`` (dL/dz, bf16); the weight-gradient partials
+        of all layers (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes
+        per-workgroup sum-of-squares partials into ``sumsq`` (fp64) when given; returns
+        their count."""
         B = ws.B
         xp, ip, jp = self._src(x, ids, idx, B)
         h, s, m, f = self.hip, self._s(), self.model, self.model.features
@@ -246,7 +248,7 @@ class HipDuelingNet:
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
         jobs += [h.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
                  h.fc1_finalize_job(1, self._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
-        h.grad_finalize(jobs + list(extra_jobs), s)
+        return h.grad_finalize(jobs + list(extra_jobs), s, 0 if sumsq is None else sumsq.data_ptr())
 
 
 def forward_multi(passes) -> None:

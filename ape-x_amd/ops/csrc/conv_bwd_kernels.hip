@@ -539,19 +539,61 @@ int wgrad_grid(int layer, int B) {
 }
 
 // outputs per workgroup: 64 when the 4 waves split many slices (G >= kWideG), 256 (one per
-// thread, 4 independent chains) when the job has few slices and many outputs (FC1)
+// thread, 4 independent chains) when the job has few slices; kind 2 (FC1 rows): one row of
+// 3136 per workgroup, transposed through LDS so reads and writes are both coalesced
 constexpr int kWideG = 16;
-__host__ __device__ inline int finalize_outputs_per_block(int G) { return G >= kWideG ? 64 : 256; }
+constexpr int kRowLen = 49 * 64;
+__host__ __device__ inline int finalize_blocks(const FinalizeJob& j) {
+  if (j.kind == 2) return j.n_main / kRowLen;
+  const int per = j.G >= kWideG ? 64 : 256;
+  return (j.n_main + j.n_bias + per - 1) / per;
+}
+
+__device__ __forceinline__ void finalize_sumsq(float v, double* sumsq, bool active) {
+  // block-wide fixed-order sum of v^2 (all 256 threads call this)
+  __shared__ double red[4];
+  double q = active ? (double)v * (double)v : 0.0;
+  q = wave_sum(q);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) red[wave] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) sumsq[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
 
 __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   __shared__ float red[4][64];
+  __shared__ float row[kRowLen];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int j = 0;
   while (j + 1 < fs.n && (int)blockIdx.x >= fs.job[j + 1].block0) ++j;
   const FinalizeJob& jb = fs.job[j];
+  if (jb.kind == 2) {  // FC1 weight rows: natural [n][p*64 + c] -> reference [n][c*49 + p]
+    const int n = (int)blockIdx.x - jb.block0;
+    const float* src = jb.part + (size_t)n * kRowLen;
+    float q = 0.f;
+    for (int k = threadIdx.x; k < kRowLen; k += 256) {
+      float t = 0.f;
+      for (int g = 0; g < jb.G; ++g) t += src[(size_t)g * jb.pstride + k];
+      row[(k & 63) * 49 + (k >> 6)] = t;
+      q += t * t;
+    }
+    __syncthreads();
+    float* dst = jb.out[0] + (size_t)n * kRowLen;
+    for (int e = threadIdx.x; e < kRowLen; e += 256) dst[e] = row[e];
+    if (fs.sumsq) {
+      // per-thread fp32 partial of <= 13 squares, then the fixed-order fp64 block sum
+      __shared__ double rq[4];
+      double d = wave_sum((double)q);
+      if (lane == 0) rq[wave] = d;
+      __syncthreads();
+      if (threadIdx.x == 0) fs.sumsq[blockIdx.x] = (rq[0] + rq[1]) + (rq[2] + rq[3]);
+    }
+    return;
+  }
   const int total = jb.n_main + jb.n_bias;
   int e;
-  float t;
+  float t = 0.f;
+  bool have = false;
   if (jb.G >= kWideG) {
     e = ((int)blockIdx.x - jb.block0) * 64 + lane;
     float s = 0.f;
@@ -564,24 +606,28 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
     }
     red[wave][lane] = s;
     __syncthreads();
-    if (wave != 0 || e >= total) return;
-    t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    have = wave == 0 && e < total;
+    if (have) t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   } else {
     e = ((int)blockIdx.x - jb.block0) * 256 + threadIdx.x;
-    if (e >= total) return;
-    const float* src = e < jb.n_main ? jb.part + e : jb.bpart + (e - jb.n_main);
-    const size_t st = e < jb.n_main ? (size_t)jb.pstride : (size_t)jb.bstride;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int g = 0;
-    for (; g + 4 <= jb.G; g += 4) {
-      s0 += src[(size_t)g * st];
-      s1 += src[(size_t)(g + 1) * st];
-      s2 += src[(size_t)(g + 2) * st];
-      s3 += src[(size_t)(g + 3) * st];
+    have = e < total;
+    if (have) {
+      const float* src = e < jb.n_main ? jb.part + e : jb.bpart + (e - jb.n_main);
+      const size_t st = e < jb.n_main ? (size_t)jb.pstride : (size_t)jb.bstride;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int g = 0;
+      for (; g + 4 <= jb.G; g += 4) {
+        s0 += src[(size_t)g * st];
+        s1 += src[(size_t)(g + 1) * st];
+        s2 += src[(size_t)(g + 2) * st];
+        s3 += src[(size_t)(g + 3) * st];
+      }
+      for (; g < jb.G; ++g) s0 += src[(size_t)g * st];
+      t = (s0 + s1) + (s2 + s3);
     }
-    for (; g < jb.G; ++g) s0 += src[(size_t)g * st];
-    t = (s0 + s1) + (s2 + s3);
   }
+  if (fs.sumsq) finalize_sumsq(t, fs.sumsq, have);
+  if (!have) return;
   if (jb.kind == 0) {  // conv: [N][KH*KW*C] (c fastest) -> reference [N][C][KH][KW]
     if (e < jb.n_main) {
       const int K = jb.C * jb.KH * jb.KW, n = e / K, kidx = e % K, c = kidx % jb.C, tap = kidx / jb.C;
@@ -602,16 +648,22 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   }
 }
 
-void grad_finalize(FinalizeSet fs, hipStream_t s) {
+int grad_finalize(FinalizeSet fs, hipStream_t s) {
   if (fs.n < 1 || fs.n > kMaxFinalizeJobs) throw std::invalid_argument("grad_finalize: 1..6 jobs");
   int blocks = 0;
   for (int j = 0; j < fs.n; ++j) {
     fs.job[j].block0 = blocks;
-    const int per = finalize_outputs_per_block(fs.job[j].G);
-    blocks += (fs.job[j].n_main + fs.job[j].n_bias + per - 1) / per;
+    blocks += finalize_blocks(fs.job[j]);
   }
   grad_finalize_k<<<blocks, 256, 0, s>>>(fs);
   LAUNCH_CHECK();
+  return blocks;
+}
+
+int grad_finalize_blocks(const FinalizeSet& fs) {
+  int blocks = 0;
+  for (int j = 0; j < fs.n; ++j) blocks += finalize_blocks(fs.job[j]);
+  return blocks;
 }
 
 FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad) {
@@ -642,10 +694,10 @@ FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, fl
 }
 
 FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad) {
-  // [G][256][7*7*64] natural (p, c) order == a 7x7 conv with C = 64 -> [n][c][7][7]
+  // [G][256][7*7*64] natural (p, c) order -> reference [n][c*49 + p] (row-transpose job)
   constexpr int K = 49 * 64;
   FinalizeJob j{};
-  j.kind = 0;
+  j.kind = 2;
   j.G = fc1_bwd_slices();
   j.part = ws + (size_t)half * 128 * K;
   j.pstride = 256 * K;

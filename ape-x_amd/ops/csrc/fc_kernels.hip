@@ -131,11 +131,12 @@ int fc1_fwd(const uint16_t* a, const uint16_t* w, float* part, int B, hipStream_
 //    the ReLU backward of conv3 (a3 > 0) and the bf16 cast are fused into the coalesced
 //    tile epilogue, writing dy3 (what wgrad3 / dgrad3 read) directly;
 //  * dW (blocks [DXB, ...)): dW[n][k] = sum_b dz[b][n] a3[b][k] -- the reduction runs over
-//    rows of both operands, so a batch slice of dz and a3 is staged in LDS and both
+//    rows of both operands, so 128-row batch chunks of dz and a3 are staged in LDS and both
 //    fragments are gathered with ds_read_b64_tr_b16 (padded pitches: conflict free per
-//    32-lane half); each workgroup writes an fp32 partial slab [G][256][3136] in natural
-//    (p, c) column order and grad_finalize reduces the G slabs and scatters them into the
-//    reference [n][c*49+p] layout (FC1 is a 7x7 "conv" over a3's 7x7x64).
+//    32-lane half; the next chunk is prefetched into registers); each workgroup owns a
+//    complete 64 x 64 tile (no split-K slabs, 48 KB LDS: 3 workgroups per CU), written
+//    in natural (p, c) column order; grad_finalize's row-transpose job scatters it into the
+//    reference [n][c*49+p] layout through LDS (coalesced both ways).
 // Replaces two hipBLASLt GEMMs + the unpack and ReLU-mask kernels (four launches).
 namespace {
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -144,15 +145,13 @@ __device__ __forceinline__ bf16x4 tr_read4(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(__attribute__((address_space(3))) char*)p);
 }
 constexpr int FB_DX_TM = 128, FB_DX_TN = 64;      // dX workgroup tile (4 waves x 32 rows, 2 N tiles)
-constexpr int FB_DW_TN = 128, FB_DW_TK = 64;      // dW workgroup tile: 128 n x 64 k
-constexpr int FB_G = 2;                           // batch slices of the dW reduction
-constexpr int FB_DZ_PITCH = FB_DW_TN * 2 + 64;    // 320 B: tr-read rows 16 banks apart
-constexpr int FB_A3_PITCH = FB_DW_TK * 2 + 64;    // 192 B
-constexpr int FB_MAXB = 256;                      // batch rows per dW slice held in LDS
-constexpr int FB_LDS = FB_MAXB * (FB_DZ_PITCH + FB_A3_PITCH);  // 128 KB
+constexpr int FB_DW_TN = 64, FB_DW_TK = 64;       // dW workgroup tile: 64 n x 64 k (one 32x32 per wave)
+constexpr int FB_PITCH = 64 * 2 + 64;             // 192 B LDS rows: tr-read rows 16 banks apart
+constexpr int FB_CH = 128;                        // batch rows per LDS chunk
+constexpr int FB_LDS = 2 * FB_CH * FB_PITCH;      // dz + a3 chunk = 48 KB (3 workgroups per CU)
 }  // namespace
 
-int fc1_bwd_slices() { return FB_G; }
+int fc1_bwd_slices() { return 1; }  // dW is complete per workgroup (one slab)
 
 __global__ __launch_bounds__(256) void fc1_bwd_k(const uint16_t* __restrict__ dz, const uint16_t* __restrict__ a3,
                                                  const uint16_t* __restrict__ wt, uint16_t* __restrict__ dy3,
@@ -195,79 +194,68 @@ __global__ __launch_bounds__(256) void fc1_bwd_k(const uint16_t* __restrict__ dz
   // ---------------------------------------------------------------- dW role
   const int blk = blockIdx.x - dxb;
   const int KB = FC_K / FB_DW_TK;  // 49
-  const int g = blk / (2 * KB), rem = blk % (2 * KB), nbk = rem / KB, kb = rem % KB;
-  const int rows = (B + FB_G - 1) / FB_G, b0 = g * rows, nrows = min(rows, B - b0);
+  const int nbk = blk / KB, kb = blk % KB;
   char* dzs = smem;
-  char* a3s = smem + FB_MAXB * FB_DZ_PITCH;
-  // stage dz[b0 .. +256][nbk*128 .. +128] and a3[b0 .. +256][kb*64 .. +64] in 16-B chunks,
-  // every load of the thread issued before the first LDS store (rows past nrows are zero)
-  const int nr16 = (nrows + 15) & ~15;
-  {
-    constexpr int DZC = FB_MAXB * 16 / 256, A3C = FB_MAXB * 8 / 256;  // 16 + 8 chunks per thread
-    u32v4 vd[DZC], va[A3C];
-#pragma unroll
-    for (int j = 0; j < DZC; ++j) {
-      const int q = threadIdx.x + 256 * j, r = q >> 4, c = q & 15;
-      const int rr = r < nrows ? r : nrows - 1;
-      vd[j] = *reinterpret_cast<const u32v4*>(dz + (size_t)(b0 + rr) * FC_N + nbk * FB_DW_TN + c * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < A3C; ++j) {
-      const int q = threadIdx.x + 256 * j, r = q >> 3, c = q & 7;
-      const int rr = r < nrows ? r : nrows - 1;
-      va[j] = *reinterpret_cast<const u32v4*>(a3 + (size_t)(b0 + rr) * FC_K + kb * FB_DW_TK + c * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < DZC; ++j) {
-      const int q = threadIdx.x + 256 * j, r = q >> 4, c = q & 15;
-      if (r < nr16) *reinterpret_cast<u32v4*>(dzs + r * FB_DZ_PITCH + c * 16) = r < nrows ? vd[j] : u32v4{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int j = 0; j < A3C; ++j) {
-      const int q = threadIdx.x + 256 * j, r = q >> 3, c = q & 7;
-      if (r < nr16) *reinterpret_cast<u32v4*>(a3s + r * FB_A3_PITCH + c * 16) = r < nrows ? va[j] : u32v4{0u, 0u, 0u, 0u};
-    }
-  }
-  __syncthreads();
-  // wave (wn, wk): n tiles 2 wn, 2 wn + 1 (of 4), k tile wk (of 2)
-  const int wn = wave >> 1, wk = wave & 1;
+  char* a3s = smem + FB_CH * FB_PITCH;
+  const int wn = wave >> 1, wk = wave & 1;  // the wave's 32 x 32 tile
   const int q4 = (lane & 15) >> 2, p4 = lane & 3, grp = (lane >> 4) & 1;
   const int colsel = 16 * grp + 4 * p4;
-  f32x16 acc0 = {}, acc1 = {};
-  for (int s = 0; s < nr16 / 16; ++s) {
-    const int r0 = 16 * s + 8 * h + q4;
-    const char* d0 = dzs + r0 * FB_DZ_PITCH + (64 * wn + colsel) * 2;
-    const char* x0 = a3s + r0 * FB_A3_PITCH + (32 * wk + colsel) * 2;
-    const bf16x4 al0 = tr_read4(d0), ah0 = tr_read4(d0 + 4 * FB_DZ_PITCH);
-    const bf16x4 al1 = tr_read4(d0 + 64), ah1 = tr_read4(d0 + 64 + 4 * FB_DZ_PITCH);
-    const bf16x4 bl = tr_read4(x0), bh = tr_read4(x0 + 4 * FB_A3_PITCH);
-    const bf16x8 fa0{al0[0], al0[1], al0[2], al0[3], ah0[0], ah0[1], ah0[2], ah0[3]};
-    const bf16x8 fa1{al1[0], al1[1], al1[2], al1[3], ah1[0], ah1[1], ah1[2], ah1[3]};
-    const bf16x8 fb{bl[0], bl[1], bl[2], bl[3], bh[0], bh[1], bh[2], bh[3]};
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb, acc1, 0, 0, 0);
+  f32x16 acc = {};
+  // the whole batch in 128-row chunks through LDS; the next chunk's loads are in flight
+  // (registers) while the current one is multiplied.  Thread t moves 16-byte chunk
+  // q = t + 256 j (j < 4) of each operand: row q >> 3, column chunk q & 7.
+  u32v4 vd[4], va[4];
+  auto load = [&](int b0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = threadIdx.x + 256 * j, r = q >> 3, c = q & 7;
+      const int rr = min(b0 + r, B - 1);
+      vd[j] = *reinterpret_cast<const u32v4*>(dz + (size_t)rr * FC_N + nbk * FB_DW_TN + c * 8);
+      va[j] = *reinterpret_cast<const u32v4*>(a3 + (size_t)rr * FC_K + kb * FB_DW_TK + c * 8);
+    }
+  };
+  load(0);
+  for (int b0 = 0; b0 < B; b0 += FB_CH) {
+    const int nrows = min(FB_CH, B - b0), nr16 = (nrows + 15) & ~15;
+    if (b0) __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = threadIdx.x + 256 * j, r = q >> 3, c = q & 7;
+      const u32v4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32v4*>(dzs + r * FB_PITCH + c * 16) = r < nrows ? vd[j] : z;
+      *reinterpret_cast<u32v4*>(a3s + r * FB_PITCH + c * 16) = r < nrows ? va[j] : z;
+    }
+    __syncthreads();
+    if (b0 + FB_CH < B) load(b0 + FB_CH);
+    for (int s = 0; s < nr16 / 16; ++s) {
+      const int r0 = 16 * s + 8 * h + q4;
+      const char* d0 = dzs + r0 * FB_PITCH + (32 * wn + colsel) * 2;
+      const char* x0 = a3s + r0 * FB_PITCH + (32 * wk + colsel) * 2;
+      const bf16x4 al = tr_read4(d0), ah = tr_read4(d0 + 4 * FB_PITCH);
+      const bf16x4 bl = tr_read4(x0), bh = tr_read4(x0 + 4 * FB_PITCH);
+      const bf16x8 fa{al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3]};
+      const bf16x8 fb{bl[0], bl[1], bl[2], bl[3], bh[0], bh[1], bh[2], bh[3]};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc, 0, 0, 0);
+    }
   }
-  // partial slab g: [256][3136], rows n = C/D row map, columns k = lane
-  float* dst = part + (size_t)g * FC_N * FC_K;
+  // dW [256][3136] in natural (p, c) column order: rows n = C/D row map, columns k = lane
   const int ncol = kb * FB_DW_TK + 32 * wk + r32;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int m = (r & 3) + 8 * (r >> 2) + 4 * h;
-    dst[(size_t)(nbk * FB_DW_TN + 64 * wn + m) * FC_K + ncol] = acc0[r];
-    dst[(size_t)(nbk * FB_DW_TN + 64 * wn + 32 + m) * FC_K + ncol] = acc1[r];
+    part[(size_t)(nbk * FB_DW_TN + 32 * wn + m) * FC_K + ncol] = acc[r];
   }
 }
 
 void fc1_bwd(const uint16_t* dz, const uint16_t* a3, const uint16_t* wt, uint16_t* dy3, float* part, int B,
              hipStream_t s) {
   if (B <= 0) return;
-  if ((B + FB_G - 1) / FB_G > FB_MAXB) throw std::invalid_argument("fc1_bwd: batch <= 512");
   const int dxb = ((B + FB_DX_TM - 1) / FB_DX_TM) * (FC_K / FB_DX_TN);
-  const int dwb = FB_G * 2 * (FC_K / FB_DW_TK);
+  const int dwb = (FC_N / FB_DW_TN) * (FC_K / FB_DW_TK);
   fc1_bwd_k<<<dxb + dwb, 256, 0, s>>>(dz, a3, wt, dy3, part, B, dxb);
   LAUNCH_CHECK();
 }
 
-size_t fc1_bwd_workspace_floats() { return (size_t)FB_G * FC_N * FC_K; }
+size_t fc1_bwd_workspace_floats() { return (size_t)FC_N * FC_K; }
 
 }  // namespace apex

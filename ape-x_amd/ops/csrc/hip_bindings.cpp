@@ -315,13 +315,14 @@ PYBIND11_MODULE(_apex_hip, m) {
     fc1_bwd(P<const uint16_t>(dz), P<const uint16_t>(a3), P<const uint16_t>(wt), P<uint16_t>(dy3), P<float>(part), B,
             S(s));
   });
-  m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s) {
+  m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s, uint64_t sumsq) {
     if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..6 jobs");
     FinalizeSet fs{};
     for (size_t i = 0; i < jobs.size(); ++i) fs.job[i] = jobs[i];
     fs.n = (int)jobs.size();
-    grad_finalize(fs, S(s));
-  });
+    fs.sumsq = P<double>(sumsq);
+    return grad_finalize(fs, S(s));
+  }, py::arg("jobs"), py::arg("s"), py::arg("sumsq") = 0);
   m.def("wgrad_grid", &wgrad_grid);
   m.def("dqn_heads_bwd_blocks", &dqn_heads_bwd_blocks);
   m.def("dqn_heads_bwd", [](py::dict d, int B, int A, float gamma_n, uint64_t s) {

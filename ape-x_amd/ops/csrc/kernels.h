@@ -105,7 +105,7 @@ void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const 
 // ---- conv_bwd_kernels.hip: one launch for all batch-sliced gradient reductions
 constexpr int kMaxFinalizeJobs = 6;
 struct FinalizeJob {
-  int kind;                 // 0: conv wgrad (C, KH, KW), 1: heads (C = A)
+  int kind;                 // 0: conv wgrad (C, KH, KW), 1: heads (C = A), 2: FC1 weight rows
   const float* part;        // [G][pstride]
   const float* bpart;       // [G][bstride] (conv bias partials)
   int G, pstride, bstride, n_main, n_bias;
@@ -116,9 +116,11 @@ struct FinalizeJob {
 struct FinalizeSet {
   FinalizeJob job[kMaxFinalizeJobs];
   int n;
+  double* sumsq;            // optional: one fp64 partial of sum(g^2) per workgroup (grad norm)
 };
 int wgrad_grid(int layer, int B);
-void grad_finalize(FinalizeSet fs, hipStream_t s);
+int grad_finalize(FinalizeSet fs, hipStream_t s);  // returns the workgroup (= sumsq partial) count
+int grad_finalize_blocks(const FinalizeSet& fs);
 FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
 // FC1 weight half (0: advantage rows 0..127, 1: value rows 128..255) of fc1_bwd's slabs
 FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad);

@@ -41,6 +41,10 @@ net(x, ws)
 dq = torch.randn(B, 18, device=dev)
 net.backward(dq, x, ws)
 wsp = net._wgrad_wss[2].data_ptr()
+fin_jobs = [hip.conv_finalize_job(k, B, net._wgrad_wss[k - 1].data_ptr(), m.features[2 * k - 2].weight.grad.data_ptr(),
+                                  m.features[2 * k - 2].bias.grad.data_ptr()) for k in (3, 2, 1)]
+fin_jobs += [hip.fc1_finalize_job(0, net._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
+             hip.fc1_finalize_job(1, net._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
 
 cases = {
     "conv1_fwd_dense": lambda: hip.conv_fwd(1, x.data_ptr(), 0, 0, net.w1p.data_ptr(), net.b1.data_ptr(),
@@ -67,6 +71,9 @@ cases = {
                                      ws.a1.data_ptr(), B, s),
     "wgrad1": lambda: hip.conv_wgrad(1, x.data_ptr(), 0, 0, ws.dy1.data_ptr(), 0, B, wsp,
                                      f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr(), s),
+    "fc1_bwd": lambda: hip.fc1_bwd(ws.dz_bf.data_ptr(), ws.a3.data_ptr(), net.wfc1t.data_ptr(), ws.dy3.data_ptr(),
+                                   net._fc1_ws.data_ptr(), B, s),
+    "finalize_all": lambda: hip.grad_finalize(fin_jobs, s),
 }
 flops = {"conv1": 2 * 3.28e6, "conv2": 2 * 2.65e6, "conv3": 2 * 1.81e6}
 for name, fn in cases.items():
