@@ -316,6 +316,7 @@ __device__ __forceinline__ void wg_frags(const char* xs, const char* dys, int ks
   for (int k = 0; k < G::KTW; ++k) {
     const int kl = wave + 4 * k;
     const int kt = kt0 + kl;
+    f.b[k] = bf16x8{};  // out-of-range tiles multiply zeros (see wg_mfma)
     if (kl < G::KTB && kt < G::KT) {
       bf16x4 lo, hi;
       if constexpr (G::C == 4) {  // 32-k tile = 8 pixels x 4 channels of kernel row kt
@@ -332,16 +333,17 @@ __device__ __forceinline__ void wg_frags(const char* xs, const char* dys, int ks
   }
 }
 
+// Unconditional: a tile past the workgroup's kidx range has zero B fragments (acc + 0 is
+// exact) and is never stored.  A wave-uniform `if` around the MFMAs made the compiler keep
+// the accumulators in VGPRs and copy them to and from AGPRs around every MFMA (64 moves
+// per MFMA pair, measured: the bulk of the kernels' VALU).
 template <class G>
-__device__ __forceinline__ void wg_mfma(const WgFrags<G>& f, int wave, int kt0, f32x16 (&acc)[G::NT][G::KTW]) {
+__device__ __forceinline__ void wg_mfma(const WgFrags<G>& f, int, int, f32x16 (&acc)[G::NT][G::KTW]) {
 #pragma unroll
   for (int k = 0; k < G::KTW; ++k) {
-    const int kl = wave + 4 * k;
-    if (kl < G::KTB && kt0 + kl < G::KT) {
 #pragma unroll
-      for (int nt = 0; nt < G::NT; ++nt)
-        acc[nt][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[nt], f.b[k], acc[nt][k], 0, 0, 0);
-    }
+    for (int nt = 0; nt < G::NT; ++nt)
+      acc[nt][k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[nt], f.b[k], acc[nt][k], 0, 0, 0);
   }
 }
 
