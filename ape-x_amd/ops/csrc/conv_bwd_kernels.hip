@@ -292,51 +292,45 @@ struct WgFrags {
   bf16x8 b[G::KTW];  // im2col x fragments (k = 16 pixels, cols kidx)
 };
 
-// Fragments of pixel k-step ks: rows p = 16 ks + 8 h + 4 t + q4 for the two tr reads t
+// LDS byte offset of the B (im2col x) fragment of pixel k-step ks, half t, kidx tile kt
+// for this lane: sample-independent, so computed once per workgroup (the integer
+// division by OW per k-step was most of the kernels' VALU, PMC)
 template <class G>
-__device__ __forceinline__ void wg_frags(const char* xs, const char* dys, int ks, int h, int q4, int colsel,
-                                         int wave, int kt0, WgFrags<G>& f) {
-  int prow[2], xpix[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int p = ks * 16 + 8 * h + 4 * t + q4;
-    prow[t] = p;
-    const int pc = p < G::P ? p : G::P - 1;
-    const int oy = pc / G::OW, ox = pc % G::OW;
-    xpix[t] = (G::S * oy) * G::W + G::S * ox;
-  }
+__device__ __forceinline__ int wg_boff(int ks, int t, int h, int q4, int colsel, int kt) {
+  const int p = ks * 16 + 8 * h + 4 * t + q4;
+  const int pc = p < G::P ? p : G::P - 1;
+  const int oy = pc / G::OW, ox = pc % G::OW;
+  const int xpix = (G::S * oy) * G::W + G::S * ox;
+  if constexpr (G::C == 4) return x_pix_off<G>(xpix + kt_origin<G>(kt) + colsel / 4);
+  else return xpix * G::PIX + kt_origin<G>(kt) + colsel * 2;
+}
+
+template <class G>
+struct WgAddr {
+  int b[G::KS][2][G::KTW];
+  bool ok[G::KTW];
+};
+
+template <class G>
+__device__ __forceinline__ void wg_frags_pre(const char* xs, const char* dys, int ks, int arow, int colsel,
+                                             const WgAddr<G>& ad, WgFrags<G>& f) {
+  // A (dy^T): rows p = 16 ks + 8 h + 4 t + q4 (arow = 8 h + q4), columns n
 #pragma unroll
   for (int nt = 0; nt < G::NT; ++nt) {
-    const int coff = (nt * 32 + colsel) * 2;
-    const bf16x4 lo = tr_read(dys + prow[0] * G::DYROW + coff);
-    const bf16x4 hi = tr_read(dys + prow[1] * G::DYROW + coff);
+    const char* a0 = dys + (ks * 16 + arow) * G::DYROW + (nt * 32 + colsel) * 2;
+    const bf16x4 lo = tr_read(a0), hi = tr_read(a0 + 4 * G::DYROW);
     f.a[nt] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   }
 #pragma unroll
   for (int k = 0; k < G::KTW; ++k) {
-    const int kl = wave + 4 * k;
-    const int kt = kt0 + kl;
-    f.b[k] = bf16x8{};  // out-of-range tiles multiply zeros (see wg_mfma)
-    if (kl < G::KTB && kt < G::KT) {
-      bf16x4 lo, hi;
-      if constexpr (G::C == 4) {  // 32-k tile = 8 pixels x 4 channels of kernel row kt
-        const int dp = kt_origin<G>(kt) + colsel / 4;
-        lo = tr_read(xs + x_pix_off<G>(xpix[0] + dp));
-        hi = tr_read(xs + x_pix_off<G>(xpix[1] + dp));
-      } else {
-        const int o = kt_origin<G>(kt) + colsel * 2;
-        lo = tr_read(xs + xpix[0] * G::PIX + o);
-        hi = tr_read(xs + xpix[1] * G::PIX + o);
-      }
+    f.b[k] = bf16x8{};
+    if (ad.ok[k]) {
+      const bf16x4 lo = tr_read(xs + ad.b[ks][0][k]), hi = tr_read(xs + ad.b[ks][1][k]);
       f.b[k] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   }
 }
 
-// Unconditional: a tile past the workgroup's kidx range has zero B fragments (acc + 0 is
-// exact) and is never stored.  A wave-uniform `if` around the MFMAs made the compiler keep
-// the accumulators in VGPRs and copy them to and from AGPRs around every MFMA (64 moves
-// per MFMA pair, measured: the bulk of the kernels' VALU).
 template <class G>
 __device__ __forceinline__ void wg_mfma(const WgFrags<G>& f, int, int, f32x16 (&acc)[G::NT][G::KTW]) {
 #pragma unroll
@@ -390,6 +384,19 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   for (int a = 0; a < G::NT; ++a)
 #pragma unroll
     for (int k = 0; k < G::KTW; ++k) acc[a][k] = f32x16{};
+  // sample-independent fragment addresses (B: im2col x rows for every pixel k-step)
+  WgAddr<G> ad;
+  const int arow = 8 * h + q4;
+#pragma unroll
+  for (int k = 0; k < G::KTW; ++k) {
+    const int kl = wave + 4 * k, kt = kt0 + kl;
+    ad.ok[k] = kl < G::KTB && kt < G::KT;
+    const int ktc = kt < G::KT ? kt : G::KT - 1;
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) ad.b[ks][t][k] = wg_boff<G>(ks, t, h, q4, colsel, ktc);
+  }
   // register prefetch: the next sample's x and dy loads are in flight during this
   // sample's MFMA loop (one LDS buffer; committed after the compute)
   constexpr int XCH = (G::C == 4) ? 0 : G::H * G::W * G::C / 8;
@@ -412,17 +419,16 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
     if (do_bias) wg_bias_acc<G>(pd, bs);
     __syncthreads();
     if (b + gridb < B) wg_issue<G>(x, fs, dy, mask, b + gridb, px, pd, pm);  // block-uniform
-    // software-pipelined pixel k-steps: fragments of ks + 1 are read while ks multiplies
-    WgFrags<G> f0, f1;
-    wg_frags<G>(xs, dys, 0, h, q4, colsel, wave, kt0, f0);
-#pragma unroll 1
-    for (int ks = 0; ks < G::KS; ks += 2) {
-      if (ks + 1 < G::KS) wg_frags<G>(xs, dys, ks + 1, h, q4, colsel, wave, kt0, f1);
-      wg_mfma<G>(f0, wave, kt0, acc);
-      if (ks + 1 < G::KS) {
-        if (ks + 2 < G::KS) wg_frags<G>(xs, dys, ks + 2, h, q4, colsel, wave, kt0, f0);
-        wg_mfma<G>(f1, wave, kt0, acc);
-      }
+    // fully unrolled pixel k-steps on precomputed fragment addresses, software pipelined:
+    // the fragments of ks + 1 are read while ks multiplies
+    WgFrags<G> cur;
+    wg_frags_pre<G>(xs, dys, 0, arow, colsel, ad, cur);
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks) {
+      WgFrags<G> nxt;
+      if (ks + 1 < G::KS) wg_frags_pre<G>(xs, dys, ks + 1, arow, colsel, ad, nxt);
+      wg_mfma<G>(cur, wave, kt0, acc);
+      if (ks + 1 < G::KS) cur = nxt;
     }
   }
   if (do_bias) {  // fixed-order combine of the per-thread bias sums (reuse the x tile region of LDS)
