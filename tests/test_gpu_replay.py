@@ -170,10 +170,68 @@ def test_large_tree_levels(cuda):
     from apex_amd.engine.hbm_replay import HBMReplay
 
     C = 2_000_000
-    rp = HBMReplay(C, n_envs=256, device=cuda, alpha=0.6)
+    rp = HBMReplay(C, n_envs=256, device=cuda, alpha=0.6, frame_capacity=4096)
     assert len(rp.level_sizes) == 5
     idx = torch.arange(0, C, 3, dtype=torch.int32, device=cuda)
     pr = torch.rand(idx.numel(), device=cuda) + 0.05
     rp.write_priorities(idx, pr, dedup=False)
     leaf = rp.leaf_sum.double()
     assert math.isclose(rp.total_priority(), float(leaf.sum()), rel_tol=1e-10)
+
+
+@pytest.mark.parametrize("log2c", [20, 24])
+def test_large_tree_sampling_distribution(cuda, log2c):
+    """2^20 / 2^24 leaves: stratified proportional sampling matches the leaf masses
+    (chi-square over 256 equal-mass-index bins)."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 1 << log2c
+    rp = HBMReplay(C, n_envs=256, device=cuda, alpha=1.0, frame_capacity=4096)  # tree only: no frame ring
+    g = torch.Generator(device=cuda).manual_seed(log2c)
+    pr = torch.rand(C, device=cuda, generator=g) ** 4 + 1e-3  # skewed masses
+    rp.write_priorities(torch.arange(C, dtype=torch.int32, device=cuda), pr, dedup=False)
+    rp.filled.fill_(C)
+    B, rounds, bins = 512, 400, 256
+    out_i = torch.empty(B, dtype=torch.int32, device=cuda)
+    out_w = torch.empty(B, dtype=torch.float32, device=cuda)
+    counts = torch.zeros(bins, dtype=torch.float64, device=cuda)
+    for c in range(rounds):
+        rp.sample_indices(B, out_i, out_w, torch.tensor([c], dtype=torch.int64, device=cuda), beta=0.4)
+        counts += torch.bincount(out_i.long() * bins // C, minlength=bins).double()
+    leaf = rp.leaf_sum.double()
+    expected = leaf.view(bins, -1).sum(1) / leaf.sum() * B * rounds
+    chi2 = float(((counts - expected) ** 2 / expected).sum())
+    # stratified sampling is far tighter than multinomial: chi2 well under its dof (255)
+    assert chi2 < 255, chi2
+    assert math.isclose(rp.total_priority(), float(leaf.sum()), rel_tol=1e-9)
+
+
+def test_interleaved_sample_update_keeps_tree_consistent(cuda):
+    """Learner-style interleaving: sample, then write new priorities for the sampled
+    (duplicate-containing) indices, repeatedly; every level stays the exact sum of its
+    children and the min tree the min of the leaves."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 1 << 18
+    rp = HBMReplay(C, n_envs=256, device=cuda, alpha=0.6, frame_capacity=4096)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    rp.write_priorities(torch.arange(C, dtype=torch.int32, device=cuda), torch.rand(C, device=cuda, generator=g) + 0.01,
+                        dedup=False)
+    rp.filled.fill_(C)
+    B = 512
+    out_i = torch.empty(B, dtype=torch.int32, device=cuda)
+    out_w = torch.empty(B, dtype=torch.float32, device=cuda)
+    for c in range(50):
+        rp.sample_indices(B, out_i, out_w, torch.tensor([c], dtype=torch.int64, device=cuda), beta=0.4)
+        rp.write_priorities(out_i, torch.rand(B, device=cuda, generator=g) * 5 + 1e-3, dedup=True)
+    torch.cuda.synchronize()
+    below = rp.leaf_sum.double()
+    below_min = rp.leaf_min
+    for k, (s, m) in enumerate(zip(rp.node_sum, rp.node_min)):
+        n = s.numel()
+        pad = n * 64 - below.numel()
+        want = torch.nn.functional.pad(below, (0, pad)).view(n, 64).sum(1)
+        torch.testing.assert_close(s, want, rtol=1e-12, atol=1e-9)
+        want_min = torch.nn.functional.pad(below_min, (0, pad), value=float("inf")).view(n, 64).min(1).values
+        assert torch.equal(m, want_min), k
+        below, below_min = s, m

@@ -143,12 +143,14 @@ def test_flat_grad_allreduce_mean():
         assert out[r][0] == pytest.approx(want) and out[r][1] == pytest.approx(want)
 
 
-def test_dp_gradient_equals_single_big_batch():
-    out = _spawn(_dp_body, 2, 16)
-    for r in (0, 1):
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gradient_equals_single_big_batch(world):
+    out = _spawn(_dp_body, world, 16)
+    for r in range(world):
         err, scale, head = out[r]
         assert err <= 1e-5 * max(1.0, scale)
-    assert out[0][2] == pytest.approx(out[1][2])  # replicas start identical
+    for r in range(1, world):
+        assert out[0][2] == pytest.approx(out[r][2])  # replicas start identical
 
 
 def test_param_publisher_versions_and_conflation():
@@ -160,15 +162,16 @@ def test_param_publisher_versions_and_conflation():
         assert seen[3] == (False, 3, 12.0)
 
 
-def test_sharded_sampling_global_weights():
-    rng = np.random.default_rng(0)
-    shards = [rng.random(50) + 0.05, rng.random(80) * 3 + 0.5]
-    out = _spawn(_sharded_body, 2, shards)
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_sampling_global_weights(world):
+    rng = np.random.default_rng(world)
+    shards = [rng.random(50 + 10 * r) * (r + 1) + 0.05 for r in range(world)]
+    out = _spawn(_sharded_body, world, shards)
     M = [s.sum() for s in shards]
     pmin = min(s.min() for s in shards)
-    for r in (0, 1):
+    for r in range(world):
         assert out[r][0] == pytest.approx(pmin, rel=1e-6)
-        assert out[r][1] == pytest.approx(2 * M[r] / sum(M), rel=1e-6)
+        assert out[r][1] == pytest.approx(world * M[r] / sum(M), rel=1e-6)
 
 
 def test_sharded_estimator_matches_single_buffer_expectation():
