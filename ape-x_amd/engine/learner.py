@@ -45,6 +45,7 @@ class LearnerConfig:
     forward: str = "torch"         # "torch" (MIOpen bf16 trunk) | "hip" (MFMA kernels)
     seed: int = 0
     tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
+    bwd_fork: bool = False         # hip path: wgrad3/wgrad2 on a forked stream (measured slower: off)
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = True) -> torch.Tensor:
@@ -119,6 +120,7 @@ class DQNLearner:
         self.n_fin_partials = 0
         if self.hip_net:
             self.net = HipDuelingNet(self.model)
+            self.net.bwd_fork = cfg.bwd_fork
             self.net.enable_backward()
             self.tnet = HipDuelingNet(self.target)
             self.pmap1, self.pmap2 = self.net.pack_maps()  # optimizer refreshes the packed bf16 weights

@@ -93,6 +93,7 @@ class HipDuelingNet:
         self.fwd_numel = self.arena_offsets["w2t"]   # forward-only part of the arena
         self._wgrad_ws = None
         self._maps = None
+        self.bwd_fork = False  # wgrad3 / wgrad2 on a forked stream (A/B: 3095 vs 3236 steps/s, off)
         f = model.features
         self.b1, self.b2, self.b3 = f[0].bias, f[2].bias, f[4].bias
         self.repack()
@@ -167,6 +168,7 @@ class HipDuelingNet:
         self._heads_ws = torch.empty(self.hip.heads_wgrad_workspace_floats(self.A), dtype=torch.float32,
                                      device=self.device)
         self._fc1_ws = torch.empty(self.hip.fc1_bwd_workspace_floats(), dtype=torch.float32, device=self.device)
+        self._bwd_stream = torch.cuda.Stream(device=self.device)
         self.repack()
 
     # ------------------------------------------------------------------ forward
@@ -239,11 +241,27 @@ class HipDuelingNet:
         h.fc1_bwd(ws.dz_bf.data_ptr(), ws.a3.data_ptr(), self.wfc1t.data_ptr(), ws.dy3.data_ptr(),
                   self._fc1_ws.data_ptr(), B, s)
         w1, w2, w3 = (t.data_ptr() for t in self._wgrad_wss)
-        h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, s)
+        # the dgrad chain (dy3 -> dy2 -> dy1 -> wgrad1) is the critical path; wgrad3 and
+        # wgrad2 hang off it and run on a forked stream beside it (joined before finalize)
+        fork = self.bwd_fork
+        main = torch.cuda.current_stream()
+        side = self._bwd_stream if fork else main
+        ev = None
+        if fork:
+            side.wait_stream(main)
+        with torch.cuda.stream(side):
+            h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, side.cuda_stream)
         h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
-        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, s)
+        if fork:
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+        with torch.cuda.stream(side):
+            h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, side.cuda_stream)
         h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
         h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
+        if fork:
+            main.wait_stream(side)
         jobs = [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
         jobs += [h.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),

@@ -51,6 +51,8 @@ def parse():
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
     ap.add_argument("--seed", type=int, default=1122)
+    ap.add_argument("--bwd-fork", action="store_true",
+                    help="wgrad3/wgrad2 on a forked stream beside the dgrad chain (measured slower)")
     ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
                     help="priority-tree writes on the learner stream instead of a forked stream")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
@@ -90,7 +92,8 @@ def main():
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
-    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork)
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork,
+                       bwd_fork=args.bwd_fork)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
