@@ -16,7 +16,9 @@ steps.  Reference cadences are kept: params published to the actors every
 rank per GPU, ``apex_amd.parallel``), the flat gradient is all-reduced over RCCL
 between the two learner graphs, and with ``sharded=True`` the replay shards are
 sampled as one global prioritized buffer (``parallel.sharded``: shard masses are
-all-gathered before the learner graph).
+all-gathered before the learner graph).  The data-parallel step is split into three
+phase graphs so the FC1/head gradient all-reduce overlaps the conv backward
+(``ApexEngine._learn``).
 """
 from __future__ import annotations
 
@@ -89,8 +91,9 @@ class ApexEngine:
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
-        self._g_actor = self._g_learn_a = self._g_learn_b = None
+        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = None
         self._pool = None
+        self._mass_work, self._mass_pending = None, False  # pipelined shard-mass all-gather
         self._captured = False
         self._allreduce = allreduce
         # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
@@ -127,111 +130,139 @@ class ApexEngine:
             self.actor.apply_staged(half * k + i)
 
     def _learn_a(self, apply_half: int | None = None):
-        if apply_half is not None and self._sharded is None:
-            # rows now (before sampling: a sampled slot never changes under the learner);
-            # their priorities on the learner's tree stream, beside the backward (the new
-            # transitions become sampleable one learner step later).  Sharded: applied in
-            # full before the shard-mass exchange instead.
+        """Overlap mode: apply the staged actor rows of ``apply_half`` (before sampling: a
+        sampled slot never changes under the learner) and defer their priorities to the
+        learner's tree stream, beside the backward (the new transitions become sampleable
+        one learner step later -- which also keeps a sharded rank's exchanged shard mass
+        equal to the tree it samples).  Then the forward phase (single-process: the whole
+        learner step up to the optimizer)."""
+        if apply_half is not None:
             k = self.cfg.actor_steps_per_learner_step
             for i in range(k):
                 self.actor.apply_rows(apply_half * k + i)
             self.learner.tree_hooks = [lambda i=i: self.actor.apply_prios(apply_half * k + i) for i in range(k)]
-        self.learner.sample_and_forward()
+        self.learner.forward_phase()
 
     def _learn_b(self):
         self.learner.optimize()
 
+    @property
+    def _dp(self) -> bool:
+        return self._allreduce is not None and self.learner.dp_split
+
+    def _learn(self, a1, a2, b, pipelined_mass: bool) -> None:
+        """One learner step from its phases (graph replays or eager bodies).
+
+        Data-parallel (one rank per GPU, RCCL over xGMI)::
+
+            [wait shard-mass all-gather] a1 | start all-reduce(FC1+heads grads) | a2 (conv
+            backward) | start all-reduce(conv grads) [| start next step's mass all-gather]
+            | wait both | b (optimizer, 1/world mean folded in)
+
+        The FC1/head slice (~3.2 of 3.5 MB) travels while the conv backward computes; the
+        mass all-gather of step t+1 travels while the optimizer of step t runs
+        (``pipelined_mass``: only when no actor writes the tree between steps, i.e. in
+        overlap mode where actor rows are staged and applied by the learner).
+        Single-process: ``a1`` is the whole step and ``a2``/``b`` are None."""
+        sh = self._sharded
+        if sh is not None:
+            if self._mass_pending:
+                w = self._mass_work
+                self._mass_pending, self._mass_work = False, None
+            else:
+                w = sh.start_exchange()
+            sh.wait(w)
+        a1()
+        if a2 is None:
+            return
+        ar = self._allreduce
+        fc, conv = self.learner.grad_slices()
+        w1 = ar.start(fc)
+        a2()
+        w2 = ar.start(conv)
+        if sh is not None and pipelined_mass:
+            self._mass_work, self._mass_pending = sh.start_exchange(), True
+        ar.wait(w1, w2)
+        b()
+
+    def _drain_mass(self) -> None:
+        """Drop a pipelined mass exchange (something other than a train step is about to
+        touch the tree): wait for it so the buffers are quiet, re-exchange next step."""
+        if self._mass_pending:
+            self._sharded.wait(self._mass_work)
+            self._mass_pending, self._mass_work = False, None
+
     # ------------------------------------------------------------------ graphs
+    @staticmethod
+    def _graph(fn, pool):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=pool):
+            fn()
+        return g
+
     def capture(self, warmup_iters: int = 3) -> None:
         """Warm up on a side stream, then capture actor and learner steps as hipGraphs.
-        The warm-up iterations are real train steps and are counted as such."""
-        self.learn_steps += warmup_iters
-        self.actor_steps += warmup_iters * self.cfg.actor_steps_per_learner_step
+        The warm-up iterations are real train steps and are counted as such.  Collectives
+        stay eager, between the learner's phase graphs."""
+        self._drain_mass()
         if self.overlap:
             return self._capture_overlap(warmup_iters)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(warmup_iters):
-                self._actor_body()
-                if self._sharded is not None:
-                    self._sharded.exchange()
-                self._learn_a()
-                if self._allreduce is not None:
-                    self._allreduce(self.learner.flat_grad)
-                self._learn_b()
+            for _ in range(warmup_iters):  # full eager train steps (counters, publish/target cadence)
+                self.train_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
-        self._g_actor = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_actor, pool=self._pool):
-            self._actor_body()
-        self._g_learn_a = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_learn_a, pool=self._pool):
-            self._learn_a()
-            if self._allreduce is None:  # no host collective in between: one graph per step
-                self._learn_b()
-        self._g_learn_b = self._capture_learn_b()
+        self._g_actor = self._graph(self._actor_body, self._pool)
+        if self._dp:
+            self._g_learn_a = self._graph(self.learner.forward_phase, self._pool)
+            self._g_learn_a2 = self._graph(self.learner.backward_phase, self._pool)
+            self._g_learn_b = self._graph(self._learn_b, self._pool)
+        else:  # no host collective in between: one graph per step
+            self._g_learn_a = self._graph(lambda: (self.learner.forward_phase(), self._learn_b()), self._pool)
         self._captured = True
         torch.cuda.synchronize(self.device)
 
-    def _capture_learn_b(self):
-        """The optimizer graph, needed only when an eager RCCL all-reduce sits between the
-        backward and the optimizer (data-parallel); otherwise it is part of learn_a (each
-        graph boundary costs ~8 us of launch gap, rocprofv3 trace)."""
-        if self._allreduce is None:
-            return None
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self._pool):
-            self._learn_b()
-        return g
-
     def _capture_overlap(self, warmup_iters: int) -> None:
         """Overlap mode: graphs per staging half (actor: fill half h; learner: apply half
-        1-h, sample, forward, backward) + the optimizer graph.  Warm-up runs real
-        sequential train steps, keeping the one-step-behind staging invariant."""
+        1-h, sample, forward, backward [, optimizer]); data-parallel: the learner's three
+        phase graphs per half.  Warm-up runs real sequential train steps, keeping the
+        one-step-behind staging invariant."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
-            for _ in range(warmup_iters):
-                self._train_step_eager()
+            for _ in range(warmup_iters):  # full eager train steps (counters, publish/target cadence)
+                self.train_step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
         apool = torch.cuda.graph_pool_handle()  # actor graphs run concurrently: never share memory
-        self._g_actor, self._g_learn_a, self._g_apply = [], [], []
+        self._g_actor, self._g_learn_a, self._g_learn_a2 = [], [], []
         for h in (0, 1):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=apool):
-                self._actor_half(h)
-            self._g_actor.append(g)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self._pool):
-                self._learn_a(1 - h)
-                if self._allreduce is None:
-                    self._learn_b()
-            self._g_learn_a.append(g)
-            if self._sharded is not None:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self._pool):
-                    self._apply_half(1 - h)
-                self._g_apply.append(g)
-        self._g_learn_b = self._capture_learn_b()
+            self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+            if self._dp:
+                self._g_learn_a.append(self._graph(lambda h=h: self._learn_a(1 - h), self._pool))
+                self._g_learn_a2.append(self._graph(self.learner.backward_phase, self._pool))
+            else:
+                self._g_learn_a.append(self._graph(lambda h=h: (self._learn_a(1 - h), self._learn_b()), self._pool))
+        self._g_learn_b = self._graph(self._learn_b, self._pool) if self._dp else None
         self._captured = True
         torch.cuda.synchronize(self.device)
         self._ev_learn.record(torch.cuda.current_stream(self.device))
+
+    def _learner_eager(self, apply_half: int | None = None) -> None:
+        if self._dp:
+            self._learn(lambda: self._learn_a(apply_half), self.learner.backward_phase, self._learn_b, False)
+        else:
+            self._learn(lambda: (self._learn_a(apply_half), self._learn_b()), None, None, False)
 
     def _train_step_eager(self) -> None:
         """Overlap-mode semantics, run sequentially on the current stream."""
         h = self._half
         self._actor_half(h)
-        if self._sharded is not None:
-            self._apply_half(1 - h)
-            self._sharded.exchange()
-        self._learn_a(1 - h)
-        if self._allreduce is not None:
-            self._allreduce(self.learner.flat_grad)
-        self._learn_b()
+        self._learner_eager(1 - h)
         self._half ^= 1
 
     def _train_step_overlap(self) -> None:
@@ -250,13 +281,10 @@ class ApexEngine:
             self._g_actor[h].replay()
         self._ev_actor[h].record(A)
         L.wait_event(self._ev_actor[1 - h])
-        if self._sharded is not None:
-            self._g_apply[h].replay()
-            self._sharded.exchange()
-        self._g_learn_a[h].replay()
-        if self._allreduce is not None:
-            self._allreduce(self.learner.flat_grad)
-            self._g_learn_b.replay()
+        if self._dp:
+            self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, self._g_learn_b.replay, True)
+        else:
+            self._learn(self._g_learn_a[h].replay, None, None, False)
         self.learn_steps += 1
         self.actor_steps += self.cfg.actor_steps_per_learner_step
         if self.learn_steps % self.cfg.publish_param_interval == 0:
@@ -269,6 +297,7 @@ class ApexEngine:
 
     # ------------------------------------------------------------------ steps
     def actor_step(self) -> None:
+        self._drain_mass()
         if self._g_actor is not None:
             self._g_actor.replay()
         else:
@@ -276,18 +305,12 @@ class ApexEngine:
         self.actor_steps += 1
 
     def learner_step(self) -> None:
-        if self._sharded is not None:  # 16 B/rank all-gather of shard masses (eager collective)
-            self._sharded.exchange()
-        if self._g_learn_a is not None:
-            self._g_learn_a.replay()
-            if self._allreduce is not None:
-                self._allreduce(self.learner.flat_grad)
-                self._g_learn_b.replay()
+        if self._g_learn_a is None:
+            self._learner_eager()
+        elif self._dp:
+            self._learn(self._g_learn_a.replay, self._g_learn_a2.replay, self._g_learn_b.replay, False)
         else:
-            self._learn_a()
-            if self._allreduce is not None:
-                self._allreduce(self.learner.flat_grad)
-            self._learn_b()
+            self._learn(self._g_learn_a.replay, None, None, False)
         self.learn_steps += 1
         if self.learn_steps % self.cfg.publish_param_interval == 0:
             self.publish_params()
@@ -296,6 +319,7 @@ class ApexEngine:
 
     def fill(self, min_transitions: int | None = None) -> None:
         """Run actor steps until the replay holds ``threshold_size`` slots."""
+        self._drain_mass()
         need = self.cfg.threshold_size if min_transitions is None else min_transitions
         steps = max(-(-need // self.cfg.n_envs), 4)
         if self.overlap:  # whole halves; the last one stays staged for the first learner step

@@ -113,7 +113,11 @@ class DQNLearner:
         self.step_counter = torch.zeros(1, dtype=torch.int64, device=dev)
         self.beta = torch.full((1,), cfg.beta, dtype=torch.float32, device=dev)
         self.gamma_n = float(cfg.gamma ** cfg.n_step)
-        self.allreduce = allreduce  # callable(flat_grad) for data-parallel learners
+        # data-parallel learners: parallel.dp.FlatGradAllReduce (async SUM; the optimizer
+        # applies the 1/world mean through grad_scale)
+        self.allreduce = allreduce
+        if allreduce is not None:
+            self.hp.grad_scale = 1.0 / allreduce.world
         self.sharded = sharded      # parallel.sharded.ShardedSampling (global PER over shards)
         self.host_steps = 0
         self.hip_net = cfg.forward == "hip"
@@ -151,8 +155,35 @@ class DQNLearner:
         return torch.cuda.current_stream().cuda_stream
 
     # ------------------------------------------------------------------ phases
+    @property
+    def dp_split(self) -> bool:
+        """Data-parallel HIP learner: the backward runs as two phases so the FC1/head
+        gradients (the tail of the flat buffer, ~91% of its bytes) are all-reduced while
+        the conv backward runs (:meth:`forward_phase` / :meth:`backward_phase`)."""
+        return self.allreduce is not None and self.hip_net
+
+    def grad_slices(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """(FC1 + heads tail, conv head) views of the flat gradient, in all-reduce order."""
+        fc_off = self.fc_grad_offset
+        return self.flat_grad[fc_off:], self.flat_grad[:fc_off]
+
+    @property
+    def fc_grad_offset(self) -> int:
+        seg = {name: (o, n) for name, o, n in self.segments}
+        off = seg["advantage.0.weight"][0]
+        assert all((o + n <= off) == name.startswith("features.") for name, (o, n) in seg.items()), \
+            "flat layout: conv parameters first, then the dueling heads"
+        return off
+
     def sample_and_forward(self) -> None:
         """Sample, gather, forward x3, loss, backward (grads in ``flat_grad``)."""
+        self.forward_phase()
+        if self.dp_split:
+            self.backward_phase()
+
+    def forward_phase(self) -> None:
+        """Sample, forward x3, loss + heads backward; single-process: the whole backward
+        too; data-parallel split: up to the FC1 backward and its finalize."""
         s = self._stream()
         glob = None
         if self.sharded is not None:  # gathered shard masses -> global pmin + shard weight scale
@@ -176,26 +207,17 @@ class DQNLearner:
                  "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(), "dz_bf": self.ws_s.dz_bf.data_ptr(),
                  "part": self.lh_part.data_ptr(), "step": self.step_counter.data_ptr(),
                  "step_snap": self.step_snap.data_ptr()}, self.B, self.A, self.gamma_n, s)
-            # fork: priority mix + loss mean + tree write (+ step bump) beside the backward
-            main = torch.cuda.current_stream()
-            fork = self.cfg.tree_fork
-            if fork:
-                self.tree_stream.wait_stream(main)
-            with torch.cuda.stream(self.tree_stream if fork else main):
-                hooks, self.tree_hooks = self.tree_hooks, []
-                for fn in hooks:
-                    fn()
-                self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
-                                             mix=(self.delta, self.lw, self.prio, self.loss))
-            fused_norm = self.allreduce is None
-            n = self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx,
-                                        extra_jobs=[self.net.heads_finalize_job(self.lh_part, self.lh_blocks)],
-                                        sumsq=self.fin_partials if fused_norm else None)
-            if fused_norm:
+            heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
+            if self.dp_split:
+                self.net.fc_backward(self.ws_s, extra_jobs=[heads_job])
+                return
+            self._tree_fork_begin()
+            n = self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, extra_jobs=[heads_job],
+                                        sumsq=self.fin_partials if self.allreduce is None else None)
+            if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n
-            if fork:
-                main.wait_stream(self.tree_stream)  # join: the next sample reads the tree
+            self._tree_fork_end()
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
@@ -214,6 +236,33 @@ class DQNLearner:
         self.flat_grad.zero_()
         q.backward(self.dq)
 
+    def backward_phase(self) -> None:
+        """Data-parallel split, part 2: priority-tree writes on the forked tree stream beside
+        the conv backward (+ its finalize); joined before returning."""
+        assert self.dp_split
+        rp = self.replay
+        self._tree_fork_begin()
+        self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx)
+        self._tree_fork_end()
+
+    def _tree_fork_begin(self) -> None:
+        """Fork: deferred actor-row priorities, then the priority mix + loss mean + tree
+        write (+ step bump) of this step's samples, beside the backward."""
+        main = torch.cuda.current_stream()
+        fork = self.cfg.tree_fork
+        if fork:
+            self.tree_stream.wait_stream(main)
+        with torch.cuda.stream(self.tree_stream if fork else main):
+            hooks, self.tree_hooks = self.tree_hooks, []
+            for fn in hooks:
+                fn()
+            self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
+                                         mix=(self.delta, self.lw, self.prio, self.loss))
+
+    def _tree_fork_end(self) -> None:
+        if self.cfg.tree_fork:
+            torch.cuda.current_stream().wait_stream(self.tree_stream)  # join: the next sample reads the tree
+
     def optimize(self) -> None:
         s = self._stream()
         h = self.hip
@@ -223,21 +272,31 @@ class DQNLearner:
             h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
             parts, nparts = self.partials, self.partials.numel()
         pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if self.hip_net else (0, 0, 0)
+        fc = self.net.fc_pack_args() if self.hip_net else {}
         step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
         # the fused path already bumped step_counter on the tree stream: the optimizer reads
         # this step's snapshot instead
         stp = self.step_snap if self.hip_net else self.step_counter
         step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(), self.opt_s2.data_ptr(), self.P,
-             parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk)
+             parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk, **fc)
         if not self.hip_net:
             self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
 
     def step(self) -> None:
+        """One eager learner step (the engine runs the same phases as hipGraphs)."""
         if self.sharded is not None:
             self.sharded.exchange()
-        self.sample_and_forward()
-        if self.allreduce is not None:
-            self.allreduce(self.flat_grad)
+        self.forward_phase()
+        if self.allreduce is None:
+            pass
+        elif self.dp_split:
+            fc, conv = self.grad_slices()
+            w1 = self.allreduce.start(fc)
+            self.backward_phase()
+            w2 = self.allreduce.start(conv)
+            self.allreduce.wait(w1, w2)
+        else:
+            self.allreduce.wait(self.allreduce.start(self.flat_grad))
         self.optimize()
         self.host_steps += 1
 

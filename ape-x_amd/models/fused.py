@@ -138,6 +138,13 @@ class HipDuelingNet:
         self._maps = (dst1.to(torch.int32).to(self.device), dst2.to(torch.int32).to(self.device))
         return self._maps
 
+    def fc_pack_args(self) -> dict:
+        """Keyword arguments of the fused optimizer's FC1 tile path (FcPack): the flat
+        offsets of both FC1 weights and the two packed layouts they refresh."""
+        seg = {name: o for name, o, _ in self.model.param_segments()}
+        return {"fc_off0": seg["advantage.0.weight"], "fc_off1": seg["value.0.weight"],
+                "fc_wp": self.wfc1p.data_ptr(), "fc_wt": self.wfc1t.data_ptr()}
+
     def copy_packed_from(self, other: "HipDuelingNet", forward_only: bool = True) -> None:
         """Device copy of another net's packed weights (same architecture)."""
         n = self.fwd_numel if forward_only else self.arena.numel()
@@ -230,23 +237,48 @@ class HipDuelingNet:
         of all layers (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes
         per-workgroup sum-of-squares partials into ``sumsq`` (fp64) when given; returns
         their count."""
-        B = ws.B
-        xp, ip, jp = self._src(x, ids, idx, B)
-        h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        self._fc1_bwd(ws)
+        jobs = self._conv_chain(x, ws, ids, idx) + self._fc_jobs()
+        return self.hip.grad_finalize(jobs + list(extra_jobs), self._s(), 0 if sumsq is None else sumsq.data_ptr())
+
+    def fc_backward(self, ws: NetWorkspace, extra_jobs=()) -> None:
+        """Data-parallel split, part 1: FC1 backward and the finalize of the FC1 (+ head,
+        via ``extra_jobs``) gradients -- everything past conv3 in the flat buffer, ~91% of
+        its bytes -- so their all-reduce can start while :meth:`conv_backward` runs."""
+        self._fc1_bwd(ws)
+        self.hip.grad_finalize(self._fc_jobs() + list(extra_jobs), self._s(), 0)
+
+    def conv_backward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
+                      idx: torch.Tensor | None = None) -> None:
+        """Data-parallel split, part 2: conv3..conv1 backward + their finalize (needs
+        ``ws.dy3`` from :meth:`fc_backward`)."""
+        self.hip.grad_finalize(self._conv_chain(x, ws, ids, idx), self._s(), 0)
+
+    def _fc1_bwd(self, ws: NetWorkspace) -> None:
+        # FC1: dy3 = relu_mask(dz . W) and dW slabs in one launch
         if self._wgrad_ws is None:
             self.enable_backward()
-        # FC1: dy3 = relu_mask(dz . W) and dW slabs in one launch; then conv3 .. conv1 MFMA
-        # wgrad (partials only) / dgrad, where dgrad applies the ReLU backward of the
-        # layer below in its coalesced epilogue (ws.dy2 / ws.dy1 are the masked gradients)
-        h.fc1_bwd(ws.dz_bf.data_ptr(), ws.a3.data_ptr(), self.wfc1t.data_ptr(), ws.dy3.data_ptr(),
-                  self._fc1_ws.data_ptr(), B, s)
+        self.hip.fc1_bwd(ws.dz_bf.data_ptr(), ws.a3.data_ptr(), self.wfc1t.data_ptr(), ws.dy3.data_ptr(),
+                         self._fc1_ws.data_ptr(), ws.B, self._s())
+
+    def _fc_jobs(self) -> list:
+        m = self.model
+        return [self.hip.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
+                self.hip.fc1_finalize_job(1, self._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
+
+    def _conv_chain(self, x, ws: NetWorkspace, ids, idx) -> list:
+        """conv3 .. conv1 MFMA wgrad (partials only) / dgrad, where dgrad applies the ReLU
+        backward of the layer below in its coalesced epilogue (ws.dy2 / ws.dy1 are the
+        masked gradients); returns the finalize jobs of the three layers."""
+        B = ws.B
+        xp, ip, jp = self._src(x, ids, idx, B)
+        h, s, f = self.hip, self._s(), self.model.features
         w1, w2, w3 = (t.data_ptr() for t in self._wgrad_wss)
         # the dgrad chain (dy3 -> dy2 -> dy1 -> wgrad1) is the critical path; wgrad3 and
-        # wgrad2 hang off it and run on a forked stream beside it (joined before finalize)
+        # wgrad2 hang off it and can run on a forked stream beside it (joined before finalize)
         fork = self.bwd_fork
         main = torch.cuda.current_stream()
         side = self._bwd_stream if fork else main
-        ev = None
         if fork:
             side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -262,11 +294,8 @@ class HipDuelingNet:
         h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
         if fork:
             main.wait_stream(side)
-        jobs = [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
+        return [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
-        jobs += [h.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
-                 h.fc1_finalize_job(1, self._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
-        return h.grad_finalize(jobs + list(extra_jobs), s, 0 if sumsq is None else sumsq.data_ptr())
 
 
 def forward_multi(passes) -> None:

@@ -184,16 +184,21 @@ PYBIND11_MODULE(_apex_hip, m) {
            }),
            py::arg("lr"), py::arg("alpha") = 0.99f, py::arg("eps") = 1e-8f, py::arg("max_norm") = 0.f,
            py::arg("lr_gamma") = 1.f, py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0,
-           py::arg("centered") = false);
+           py::arg("centered") = false)
+      .def_readwrite("grad_scale", &RMSpropParams::grad_scale);
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
                            int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s,
-                           uint64_t dst1, uint64_t dst2, uint64_t arena) {
+                           uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
+                           uint64_t fc_wp, uint64_t fc_wt) {
     const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt)};
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
-                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr);
+                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr,
+                 fc_wp ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("gavg"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
-     py::arg("dst2") = 0, py::arg("arena") = 0);
+     py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0);
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
                        int lr_step_size, int lr_step_offset) {
@@ -201,16 +206,20 @@ PYBIND11_MODULE(_apex_hip, m) {
            }),
            py::arg("lr"), py::arg("beta1") = 0.9f, py::arg("beta2") = 0.999f, py::arg("eps") = 1e-8f,
            py::arg("weight_decay") = 0.f, py::arg("max_norm") = 0.f, py::arg("lr_gamma") = 1.f,
-           py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0);
+           py::arg("lr_step_size") = 0, py::arg("lr_step_offset") = 0)
+      .def_readwrite("grad_scale", &AdamParams::grad_scale);
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
                         int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s,
-                        uint64_t dst1, uint64_t dst2, uint64_t arena) {
+                        uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
+                        uint64_t fc_wp, uint64_t fc_wt) {
     const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt)};
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
-              hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr);
+              hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr, fc_wp ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("mm"), py::arg("v"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
-     py::arg("dst2") = 0, py::arg("arena") = 0);
+     py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0);
   // ---- network kernels
   m.def("conv_fwd", [](int layer, uint64_t in, uint64_t ids, uint64_t idx, uint64_t wp, uint64_t bias, uint64_t out,
                        int B, uint64_t s) {

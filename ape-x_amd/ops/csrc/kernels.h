@@ -161,6 +161,7 @@ struct RMSpropParams {
   int lr_step_size;      // StepLR step size
   int lr_step_offset;    // 1 reproduces scheduler.step() before optimizer.step()
   int centered;
+  float grad_scale = 1.f;  // gradient multiplier (1/world: the DP all-reduce sums)
 };
 // ``pack`` (nullable): after the update, bf16(p[i]) is also written to pack->arena at
 // pack->dst1[i] and pack->dst2[i] (-1 = none): the MFMA kernels' packed weight layouts
@@ -170,17 +171,28 @@ struct PackMap {
   const int* dst2;
   uint16_t* arena;
 };
+// FC1 weights (Nature-CNN dueling net): flat offsets of advantage.0.weight and
+// value.0.weight ([128][64*49] each) and the two packed bf16 layouts they refresh,
+// wp = wfc1p [256][49*64] and wt = wfc1t [49*64][256].  With it the optimizer updates
+// FC1 in LDS-transposed tiles (coalesced packed stores) instead of through the scatter
+// maps (whose FC1 entries are then ignored).
+struct FcPack {
+  int64_t off[2];
+  uint16_t* wp;
+  uint16_t* wt;
+};
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
-                  const PackMap* pack = nullptr);
+                  const PackMap* pack = nullptr, const FcPack* fc = nullptr);
 struct AdamParams {
   float lr0, beta1, beta2, eps, weight_decay, max_norm;
   float lr_gamma;
   int lr_step_size, lr_step_offset;
+  float grad_scale = 1.f;
 };
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
                const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
-               const PackMap* pack = nullptr);
+               const PackMap* pack = nullptr, const FcPack* fc = nullptr);
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
 
 // ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)

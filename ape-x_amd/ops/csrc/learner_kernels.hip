@@ -110,25 +110,25 @@ void grad_sumsq(const float* g, int64_t n, double* partials, hipStream_t s) {
 int grad_norm_partials() { return kNormBlocks; }
 
 // Every update block re-reduces the partials in the same fixed order (deterministic,
-// identical in all blocks).  The reference's per-tensor 'grad_norm' log value is computed
-// on demand on the host side (DQNLearner.stats), not on every step.
+// identical in all blocks): strided per-thread sums, a wave64 butterfly, then the 4 wave
+// sums in order -- one __syncthreads instead of a 256-wide LDS tree.  The reference's
+// per-tensor 'grad_norm' log value is computed on demand on the host side
+// (DQNLearner.stats), not on every step.  ``grad_scale`` (1/world for data-parallel
+// replicas) turns the all-reduced SUM into the mean inside this pass (no scaling kernel).
 struct NormInfo {
   float clip, l2;
 };
-__device__ NormInfo reduce_norms(const double* partials, int n_partials, float max_norm) {
-  __shared__ double red[256];
+__device__ NormInfo reduce_norms(const double* partials, int n_partials, float max_norm, float grad_scale) {
+  __shared__ double red[4];
   double t = 0.0;
   for (int k = threadIdx.x; k < n_partials; k += blockDim.x) t += partials[k];
-  red[threadIdx.x] = t;
+  t = wave_sum(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
-  for (int off = blockDim.x >> 1; off > 0; off >>= 1) {
-    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-    __syncthreads();
-  }
   NormInfo ni;
-  ni.l2 = (float)sqrt(red[0]);
+  ni.l2 = (float)(sqrt((red[0] + red[1]) + (red[2] + red[3])) * (double)grad_scale);
   const float coef = max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f;
-  ni.clip = fminf(coef, 1.f);
+  ni.clip = fminf(coef, 1.f) * grad_scale;  // applied to the raw (summed) gradient
   return ni;
 }
 
@@ -146,84 +146,181 @@ __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v
   if (d2 >= 0) pk.arena[d2] = b;
 }
 
-__global__ __launch_bounds__(256) void rmsprop_step_k(float* __restrict__ p, const float* __restrict__ g,
-                                                      float* __restrict__ sq, float* __restrict__ gavg, int64_t n,
-                                                      const double* __restrict__ partials, int n_partials,
-                                                      RMSpropParams hp, const int64_t* __restrict__ step,
-                                                      float* __restrict__ norms_out, PackMap pk) {
-  const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
-  const int64_t st = step ? step[0] : 0;
-  const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
+// Per-element update rules: (param, clipped grad, state1, state2) -> new param, written
+// with explicit fmaf so every call site -- the FC1 tile path and the generic path --
+// rounds identically.  The build uses -ffp-contract=fast, under which the backend may
+// fuse a multiply into a later add differently per call site (the source pragma does
+// not stop that): the clipped gradient is therefore passed through ``opaque`` (an
+// empty asm that hides the multiply from the combiner, no instruction emitted).
+__device__ __forceinline__ float opaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+struct RmsRule {
+  float lr, a, oma, eps;
+  int centered;
+  __device__ __forceinline__ float operator()(float p, float gi, float& s1, float& s2) const {
+#pragma clang fp contract(off)
+    s1 = fmaf(s1, a, oma * gi * gi);  // square average
+    float avg;
+    if (centered) {
+      s2 = fmaf(oma, gi - s2, s2);  // grad average
+      avg = sqrtf(fmaxf(fmaf(-s2, s2, s1), 0.f)) + eps;
+    } else {
+      avg = sqrtf(s1) + eps;
+    }
+    return fmaf(-lr, gi / avg, p);
+  }
+};
+struct AdamRule {
+  float b1, b2, eps, wd, step_size, rbc2;
+  __device__ __forceinline__ float operator()(float p, float gi, float& m, float& v) const {
+#pragma clang fp contract(off)
+    if (wd != 0.f) gi = fmaf(wd, p, gi);
+    m = fmaf(1.f - b1, gi - m, m);
+    v = fmaf(v, b2, (1.f - b2) * gi * gi);
+    return fmaf(-step_size, m / fmaf(sqrtf(v), rbc2, eps), p);
+  }
+};
+
+// FC1 weights (advantage.0 / value.0, reference [128][C3*P3] with column c*P3 + p) are
+// updated in tiles of 8 rows x 8 channels x all 49 positions: fp32 reads/writes stay
+// coalesced in the reference order, the bf16 results are staged in LDS and leave as
+// 16-byte runs in both packed layouts -- wfc1p [256][p*64 + c] (forward) and wfc1t
+// [p*64 + c][256] (FC1 input-gradient GEMM).  Writing them element by element through
+// the scatter maps cost ~1.6M scattered 2-byte stores per step (the old 20 us pass).
+constexpr int kFcN = 128, kFcC = 64, kFcP = 49, kFcTn = 8, kFcTc = 8;
+constexpr int kFcTile = kFcTn * kFcTc * kFcP;                                       // 3136
+constexpr int kFcTilesPerMat = (kFcN / kFcTn) * (kFcC / kFcTc);                      // 128
+constexpr int kOptThreads = 256, kOptGenBlocksMax = 160;
+
+template <class Rule>
+__device__ __forceinline__ void opt_elem(float* p, const float* g, float* s1, float* s2, int64_t i, float clip,
+                                         const Rule& rule, const PackMap& pk) {
+  float a = s1[i], b = s2[i];
+  const float np = rule(p[i], opaque(g[i] * clip), a, b);
+  s1[i] = a;
+  s2[i] = b;
+  p[i] = np;
+  pack_store(pk, i, np);
+}
+
+__device__ __forceinline__ RmsRule make_rule(const RMSpropParams& hp, int64_t st, float& lr) {
+  lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
+  return RmsRule{lr, hp.alpha, 1.f - hp.alpha, hp.eps, hp.centered};
+}
+__device__ __forceinline__ AdamRule make_rule(const AdamParams& hp, int64_t st, float& lr) {
+  lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
+  const float t = (float)(st + 1);
+  const float bc1 = 1.f - powf(hp.beta1, t), bc2 = 1.f - powf(hp.beta2, t);
+  return AdamRule{hp.beta1, hp.beta2, hp.eps, hp.weight_decay, lr / bc1, 1.f / sqrtf(bc2)};
+}
+
+template <class Params>
+__global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ s1, float* __restrict__ s2, int64_t n,
+                                                          const double* __restrict__ partials, int n_partials,
+                                                          Params hp, const int64_t* __restrict__ step,
+                                                          float* __restrict__ norms_out, PackMap pk, FcPack fc,
+                                                          int n_fc_blocks) {
+  const float max_norm = hp.max_norm;
+  const NormInfo ni = reduce_norms(partials, n_partials, max_norm, hp.grad_scale);
+  float lr;
+  const auto rule = make_rule(hp, step ? step[0] : 0, lr);
   if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
     norms_out[0] = ni.l2;
-    norms_out[2] = ni.clip;
+    norms_out[2] = fminf(max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f, 1.f);
     norms_out[3] = lr;
   }
-  const float a = hp.alpha, oma = 1.f - hp.alpha;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const float gi = g[i] * ni.clip;
-    const float s2 = sq[i] * a + oma * gi * gi;
-    sq[i] = s2;
-    float avg;
-    if (hp.centered) {
-      float ga = gavg[i];
-      ga = ga + oma * (gi - ga);
-      gavg[i] = ga;
-      avg = sqrtf(fmaxf(s2 - ga * ga, 0.f)) + hp.eps;
-    } else {
-      avg = sqrtf(s2) + hp.eps;
+  const int bid = blockIdx.x;
+  if (bid < n_fc_blocks) {
+    __shared__ uint16_t tile[kFcTn][kFcTc * kFcP];
+    const int mat = bid / kFcTilesPerMat, t = bid % kFcTilesPerMat;
+    const int n0 = (t / (kFcC / kFcTc)) * kFcTn, c0 = (t % (kFcC / kFcTc)) * kFcTc;
+    const int64_t base = fc.off[mat];
+    for (int e = threadIdx.x; e < kFcTile; e += kOptThreads) {
+      const int r = e / (kFcTc * kFcP), col = e - r * (kFcTc * kFcP);
+      const int64_t i = base + (int64_t)(n0 + r) * (kFcC * kFcP) + c0 * kFcP + col;
+      float a = s1[i], b = s2[i];
+      const float np = rule(p[i], opaque(g[i] * ni.clip), a, b);
+      s1[i] = a;
+      s2[i] = b;
+      p[i] = np;
+      tile[r][col] = f2bf(np);
     }
-    const float np = p[i] - lr * gi / avg;
-    p[i] = np;
-    pack_store(pk, i, np);
+    __syncthreads();
+    const int nrow = mat * kFcN + n0;
+    for (int e = threadIdx.x; e < 2 * kFcTn * kFcP; e += kOptThreads) {
+      union { uint16_t h[8]; uint4 v; } u;
+      if (e < kFcTn * kFcP) {  // wfc1p row nrow + r, positions p*64 + c0 .. +7
+        const int r = e / kFcP, pp = e - r * kFcP;
+#pragma unroll
+        for (int c = 0; c < kFcTc; ++c) u.h[c] = tile[r][c * kFcP + pp];
+        *reinterpret_cast<uint4*>(fc.wp + (size_t)(nrow + r) * (kFcC * kFcP) + pp * kFcC + c0) = u.v;
+      } else {  // wfc1t row p*64 + c0 + c, columns nrow .. +7
+        const int e2 = e - kFcTn * kFcP, c = e2 / kFcP, pp = e2 - c * kFcP;
+#pragma unroll
+        for (int r = 0; r < kFcTn; ++r) u.h[r] = tile[r][c * kFcP + pp];
+        *reinterpret_cast<uint4*>(fc.wt + (size_t)(pp * kFcC + c0 + c) * (2 * kFcN) + nrow) = u.v;
+      }
+    }
+    return;
   }
+  // generic part: every element outside the FC1 ranges, scalar, through the scatter maps
+  const int gb = bid - n_fc_blocks, ngb = gridDim.x - n_fc_blocks;
+  const int64_t stride = (int64_t)ngb * kOptThreads;
+  int64_t lo[3], hi[3];
+  int nr = 0;
+  if (n_fc_blocks) {
+    const int64_t F = (int64_t)kFcN * kFcC * kFcP;
+    const int64_t a0 = min(fc.off[0], fc.off[1]), a1 = max(fc.off[0], fc.off[1]);
+    lo[0] = 0;      hi[0] = a0;
+    lo[1] = a0 + F; hi[1] = a1;
+    lo[2] = a1 + F; hi[2] = n;
+    nr = 3;
+  } else {
+    lo[0] = 0; hi[0] = n; nr = 1;
+  }
+  for (int k = 0; k < nr; ++k)
+    for (int64_t i = lo[k] + (int64_t)gb * kOptThreads + threadIdx.x; i < hi[k]; i += stride)
+      opt_elem(p, g, s1, s2, i, ni.clip, rule, pk);
+}
+
+template <class Params>
+static void launch_opt(float* p, const float* g, float* s1, float* s2, int64_t n, const double* partials,
+                       int n_partials, const Params& hp, const int64_t* step, float* norms_out, const PackMap* pack,
+                       const FcPack* fc, hipStream_t s) {
+  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
+  FcPack f{};
+  int nfc = 0;
+  if (fc && fc->wp) {
+    const int64_t F = (int64_t)kFcN * kFcC * kFcP;
+    if (fc->off[0] < 0 || fc->off[1] < 0 || fc->off[0] + F > n || fc->off[1] + F > n ||
+        std::llabs(fc->off[0] - fc->off[1]) < F)
+      throw std::invalid_argument("opt_step: FC1 ranges out of bounds / overlapping");
+    if ((reinterpret_cast<uintptr_t>(fc->wp) | reinterpret_cast<uintptr_t>(fc->wt)) & 15)
+      throw std::invalid_argument("opt_step: packed FC1 layouts must be 16-byte aligned");
+    f = *fc;
+    nfc = 2 * kFcTilesPerMat;
+  }
+  const int64_t gen = n - (nfc ? 2 * (int64_t)kFcN * kFcC * kFcP : 0);
+  const int ngb = (int)std::max<int64_t>(1, std::min<int64_t>((gen + 4 * kOptThreads - 1) / (4 * kOptThreads),
+                                                               kOptGenBlocksMax));
+  opt_step_k<Params><<<nfc + ngb, kOptThreads, 0, s>>>(p, g, s1, s2, n, partials, n_partials, hp, step, norms_out,
+                                                       pk, f, nfc);
+  LAUNCH_CHECK();
 }
 
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
-                  const PackMap* pack) {
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
-  rmsprop_step_k<<<blocks, 256, 0, s>>>(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out, pk);
-  LAUNCH_CHECK();
-}
-
-__global__ __launch_bounds__(256) void adam_step_k(float* __restrict__ p, const float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v, int64_t n,
-                                                   const double* __restrict__ partials, int n_partials, AdamParams hp,
-                                                   const int64_t* __restrict__ step, float* __restrict__ norms_out,
-                                                   PackMap pk) {
-  const NormInfo ni = reduce_norms(partials, n_partials, hp.max_norm);
-  const int64_t st = step ? step[0] : 0;
-  const float lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
-  const float t = (float)(st + 1);
-  const float bc1 = 1.f - powf(hp.beta1, t), bc2 = 1.f - powf(hp.beta2, t);
-  const float step_size = lr / bc1, rbc2 = 1.f / sqrtf(bc2);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
-    norms_out[0] = ni.l2;
-    norms_out[2] = ni.clip;
-    norms_out[3] = lr;
-  }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float gi = g[i] * ni.clip;
-    if (hp.weight_decay != 0.f) gi += hp.weight_decay * p[i];
-    float mi = m[i];
-    mi = mi + (1.f - hp.beta1) * (gi - mi);
-    const float vi = v[i] * hp.beta2 + (1.f - hp.beta2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float np = p[i] - step_size * mi / (sqrtf(vi) * rbc2 + hp.eps);
-    p[i] = np;
-    pack_store(pk, i, np);
-  }
+                  const PackMap* pack, const FcPack* fc) {
+  launch_opt(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out, pack, fc, s);
 }
 
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
-               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s, const PackMap* pack) {
-  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
-  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
-  adam_step_k<<<blocks, 256, 0, s>>>(p, g, m, v, n, partials, n_partials, hp, step, norms_out, pk);
-  LAUNCH_CHECK();
+               const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s, const PackMap* pack,
+               const FcPack* fc) {
+  launch_opt(p, g, m, v, n, partials, n_partials, hp, step, norms_out, pack, fc, s);
 }
 
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s) {

@@ -15,7 +15,15 @@ import torch.distributed as dist
 
 
 class FlatGradAllReduce:
-    """Callable: average a flat gradient buffer across the process group in place."""
+    """Flat-gradient all-reduce across the process group.
+
+    ``__call__(flat)`` averages in place (synchronous w.r.t. the current stream).  The
+    learner uses the split, asynchronous form instead: ``start(t)`` enqueues an RCCL SUM
+    of ``t`` on the process group's own stream and returns at once (the current stream
+    does NOT wait), ``wait(*works)`` makes the current stream wait for them, and the
+    optimizer applies the 1/world mean (``grad_scale``) -- so the FC1/head slice's
+    all-reduce overlaps the conv backward, and no scaling kernel runs.
+    """
 
     def __init__(self, world_size: int | None = None, group=None, bucket_bytes: int | None = None):
         self.group = group
@@ -32,6 +40,24 @@ class FlatGradAllReduce:
             for off in range(0, flat.numel(), self.bucket_elems):
                 dist.all_reduce(flat[off:off + self.bucket_elems], group=self.group)
         flat.mul_(self.scale)
+
+    def start(self, t: torch.Tensor):
+        """Asynchronous in-place SUM of ``t``; returns the work handle(s) (None: world 1)."""
+        if self.world == 1:
+            return None
+        if self.bucket_elems is None or t.numel() <= self.bucket_elems:
+            return dist.all_reduce(t, group=self.group, async_op=True)
+        return [dist.all_reduce(t[off:off + self.bucket_elems], group=self.group, async_op=True)
+                for off in range(0, t.numel(), self.bucket_elems)]
+
+    @staticmethod
+    def wait(*works) -> None:
+        """Current stream waits for the given start() handles (no host block on RCCL)."""
+        for w in works:
+            if w is None:
+                continue
+            for x in (w if isinstance(w, list) else [w]):
+                x.wait()
 
 
 def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:

@@ -43,13 +43,25 @@ class ShardedSampling:
     def exchange(self) -> None:
         """Pack this shard's (mass, min priority) and all-gather them (eager: collectives
         stay outside the captured graphs)."""
+        self.wait(self.start_exchange())
+
+    def start_exchange(self):
+        """Asynchronous form: the pack runs on the current stream, the all-gather on the
+        process group's stream without making the current stream wait -- the engine
+        issues the NEXT step's exchange right after this step's backward (the tree is
+        final by then) so it overlaps the optimizer.  Returns the work handle."""
         mass, pmin = self._root()
         self.local[0:1].copy_(mass)
         self.local[1:2].copy_(pmin)
         if self.world > 1:
-            dist.all_gather_into_tensor(self.gathered, self.local, group=self.group)
-        else:
-            self.gathered.copy_(self.local)
+            return dist.all_gather_into_tensor(self.gathered, self.local, group=self.group, async_op=True)
+        self.gathered.copy_(self.local)
+        return None
+
+    @staticmethod
+    def wait(work) -> None:
+        if work is not None:
+            work.wait()
 
     def finalize(self) -> None:
         """Device-side: glob = (global pmin, k * M_r / sum M).  Graph-capturable."""

@@ -204,9 +204,11 @@ def test_frame_ring_input_matches_dense(cuda):
     assert torch.equal(q1, q2)
 
 
+@pytest.mark.parametrize("tiles", [False, True])
 @pytest.mark.parametrize("opt", ["rmsprop", "adam"])
-def test_fused_optimizer_packing_matches_repack(cuda, opt):
-    """The optimizer's PackMap stores leave the bf16 arena exactly as repack() would."""
+def test_fused_optimizer_packing_matches_repack(cuda, opt, tiles):
+    """The optimizer's PackMap stores (and, with ``tiles``, the LDS-transposed FC1 tile
+    path) leave the bf16 arena exactly as repack() would."""
     from apex_amd import ops
     from apex_amd.models.fused import HipDuelingNet
 
@@ -227,19 +229,56 @@ def test_fused_optimizer_packing_matches_repack(cuda, opt):
     s = torch.cuda.current_stream().cuda_stream
     net.arena.zero_()
     hip.grad_sumsq(g.data_ptr(), P, partials.data_ptr(), s)
+    fc = net.fc_pack_args() if tiles else {}
     if opt == "rmsprop":
         hp = hip.RMSpropParams(1e-3, 0.95, 1.5e-7, 40.0, 1.0, 0, 0, True)
         hip.rmsprop_step(flat.data_ptr(), g.data_ptr(), s1.data_ptr(), s2.data_ptr(), P, partials.data_ptr(),
                          partials.numel(), hp, step.data_ptr(), norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
-                         net.arena.data_ptr())
+                         net.arena.data_ptr(), **fc)
     else:
         hp = hip.AdamParams(1e-3, max_norm=40.0)
         hip.adam_step(flat.data_ptr(), g.data_ptr(), s1.data_ptr(), s2.data_ptr(), P, partials.data_ptr(),
                       partials.numel(), hp, step.data_ptr(), norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
-                      net.arena.data_ptr())
+                      net.arena.data_ptr(), **fc)
     fused = net.arena.clone()
     net.repack()
     assert torch.equal(fused.view(torch.int16), net.arena.view(torch.int16))
+
+
+def test_optimizer_tiles_and_grad_scale_bit_exact(cuda):
+    """FC1 tile path == scatter-map path elementwise, and grad_scale=1/k on a k-times
+    gradient (the DP all-reduce SUM) == the plain update, bit for bit."""
+    from apex_amd import ops
+    from apex_amd.models.fused import HipDuelingNet
+
+    hip = ops.hip()
+    m = _model(cuda)
+    flat0 = m.flatten_parameters().clone()
+    net = HipDuelingNet(m)
+    net.enable_backward()
+    d1, d2 = net.pack_maps()
+    P = flat0.numel()
+    g = torch.randn(P, device=cuda) * 0.3
+    s = torch.cuda.current_stream().cuda_stream
+    s10, s20 = torch.rand(P, device=cuda), torch.randn(P, device=cuda) * 0.1
+    outs = []
+    for tiles, k in ((False, 1), (True, 1), (True, 4)):
+        flat, s1, s2 = flat0.clone(), s10.clone(), s20.clone()
+        gk = g * k
+        partials = torch.zeros(hip.grad_norm_partials(), dtype=torch.float64, device=cuda)
+        norms = torch.zeros(4, device=cuda)
+        step = torch.zeros(1, dtype=torch.int64, device=cuda)
+        hip.grad_sumsq(gk.data_ptr(), P, partials.data_ptr(), s)
+        hp = hip.RMSpropParams(1e-3, 0.95, 1.5e-7, 1.0, 1.0, 0, 0, True)  # clipping active
+        hp.grad_scale = 1.0 / k
+        hip.rmsprop_step(flat.data_ptr(), gk.data_ptr(), s1.data_ptr(), s2.data_ptr(), P, partials.data_ptr(),
+                         partials.numel(), hp, step.data_ptr(), norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
+                         net.arena.data_ptr(), **(net.fc_pack_args() if tiles else {}))
+        outs.append((flat, s1, s2, norms.clone()))
+    for j, o in enumerate(outs[1:], 1):
+        for name, a, b in zip(("param", "s1", "s2", "norms"), outs[0], o):
+            bad = (a != b).nonzero().flatten()
+            assert bad.numel() == 0, (j, name, bad.numel(), bad[:8].tolist(), (a - b).abs().max().item())
 
 
 @pytest.mark.parametrize("B", [1536, 512, 256, 37])

@@ -38,15 +38,18 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs):
+def _engine(dev, overlap, graphs, dp=False, sharded=False):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
+    from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=4096, threshold_size=2048, overlap=overlap, use_graphs=graphs,
                        publish_param_interval=4, target_update_interval=6,
                        learner=LearnerConfig(batch_size=256, forward="hip"))
     torch.manual_seed(0)
-    return ApexEngine(cfg, dev)
+    # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
+    # pipelined shard-mass exchange) with a world-1 all-reduce -- same code path, 1 GPU
+    return ApexEngine(cfg, dev, allreduce=FlatGradAllReduce(1) if dp else None, sharded=sharded)
 
 
 def test_overlapped_graphs_equal_sequential_schedule(cuda):
@@ -65,6 +68,38 @@ def test_overlapped_graphs_equal_sequential_schedule(cuda):
     assert torch.equal(eng_g.replay.frames, eng_e.replay.frames)
     assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
     assert torch.equal(eng_g.replay.s_ids, eng_e.replay.s_ids)
+    assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
+    assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
+    assert torch.isfinite(eng_g.learner.flat).all()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("sharded", [False, True])
+def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded):
+    """The data-parallel step (three phase graphs, async all-reduce slices, pipelined
+    shard-mass exchange) replays exactly like its eager schedule, and its first step
+    matches the single-process fused step (different grad-norm summation order only)."""
+    eng_g = _engine(cuda, overlap, True, dp=True, sharded=sharded)
+    eng_e = _engine(cuda, overlap, False, dp=True, sharded=sharded)
+    eng_1 = _engine(cuda, overlap, False)
+    assert eng_g.learner.dp_split and eng_g._dp and not eng_1._dp
+    for eng in (eng_g, eng_e, eng_1):
+        eng.fill()
+    eng_e.train_step()
+    eng_1.train_step()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(eng_e.learner.flat, eng_1.learner.flat, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(eng_e.learner.loss, eng_1.learner.loss, rtol=1e-5, atol=1e-7)
+    eng_g.train_step()                # same first step, then capture (3 counted warm-up steps)
+    eng_g.capture()
+    for _ in range(3):
+        eng_e.train_step()
+    for _ in range(30):
+        eng_g.train_step()
+        eng_e.train_step()
+    torch.cuda.synchronize()
+    assert eng_g.learn_steps == eng_e.learn_steps == 34
+    assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
     assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
     assert torch.isfinite(eng_g.learner.flat).all()
