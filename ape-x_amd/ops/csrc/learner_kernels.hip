@@ -192,7 +192,7 @@ struct AdamRule {
 constexpr int kFcN = 128, kFcC = 64, kFcP = 49, kFcTn = 8, kFcTc = 8;
 constexpr int kFcTile = kFcTn * kFcTc * kFcP;                                       // 3136
 constexpr int kFcTilesPerMat = (kFcN / kFcTn) * (kFcC / kFcTc);                      // 128
-constexpr int kOptThreads = 256, kOptGenBlocksMax = 160;
+constexpr int kOptThreads = 256, kOptGenBlocksMax = 1024;
 
 template <class Rule>
 __device__ __forceinline__ void opt_elem(float* p, const float* g, float* s1, float* s2, int64_t i, float clip,
@@ -238,15 +238,33 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
     const int mat = bid / kFcTilesPerMat, t = bid % kFcTilesPerMat;
     const int n0 = (t / (kFcC / kFcTc)) * kFcTn, c0 = (t % (kFcC / kFcTc)) * kFcTc;
     const int64_t base = fc.off[mat];
-    for (int e = threadIdx.x; e < kFcTile; e += kOptThreads) {
-      const int r = e / (kFcTc * kFcP), col = e - r * (kFcTc * kFcP);
-      const int64_t i = base + (int64_t)(n0 + r) * (kFcC * kFcP) + c0 * kFcP + col;
-      float a = s1[i], b = s2[i];
-      const float np = rule(p[i], opaque(g[i] * ni.clip), a, b);
-      s1[i] = a;
-      s2[i] = b;
-      p[i] = np;
-      tile[r][col] = f2bf(np);
+    // all loads of the thread's ~12 elements issued up front (memory-level parallelism:
+    // one workgroup per CU), then the updates, then the stores
+    constexpr int kIt = (kFcTile + kOptThreads - 1) / kOptThreads;
+    float vp[kIt], vg[kIt], va[kIt], vb[kIt];
+    int64_t vi[kIt];
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+      const int e = threadIdx.x + k * kOptThreads;
+      const int ec = e < kFcTile ? e : kFcTile - 1;  // clamp: the tail lanes reload a valid element
+      const int r = ec / (kFcTc * kFcP), col = ec - r * (kFcTc * kFcP);
+      vi[k] = base + (int64_t)(n0 + r) * (kFcC * kFcP) + c0 * kFcP + col;
+      vp[k] = p[vi[k]];
+      vg[k] = g[vi[k]];
+      va[k] = s1[vi[k]];
+      vb[k] = s2[vi[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < kIt; ++k) {
+      const int e = threadIdx.x + k * kOptThreads;
+      const float np = rule(vp[k], opaque(vg[k] * ni.clip), va[k], vb[k]);
+      if (e < kFcTile) {
+        const int r = e / (kFcTc * kFcP), col = e - r * (kFcTc * kFcP);
+        s1[vi[k]] = va[k];
+        s2[vi[k]] = vb[k];
+        p[vi[k]] = np;
+        tile[r][col] = f2bf(np);
+      }
     }
     __syncthreads();
     const int nrow = mat * kFcN + n0;

@@ -75,6 +75,28 @@ cases = {
                                    net._fc1_ws.data_ptr(), B, s),
     "finalize_all": lambda: hip.grad_finalize(fin_jobs, s),
 }
+flat = m._flat if getattr(m, "_flat", None) is not None else m.flatten_parameters()
+P = flat.numel()
+gflat = torch.randn(P, device=dev) * 1e-3
+s1o, s2o = torch.zeros(P, device=dev), torch.zeros(P, device=dev)
+parts = torch.rand(1518, dtype=torch.float64, device=dev)
+norms = torch.zeros(4, device=dev)
+stp = torch.zeros(1, dtype=torch.int64, device=dev)
+d1, d2 = net.pack_maps()
+hp = hip.RMSpropParams(6.25e-5, 0.95, 1.5e-7, 40.0, 1.0, 0, 0, True)
+fcargs = net.fc_pack_args()
+cases["opt_rmsprop_tiles"] = lambda: hip.rmsprop_step(flat.data_ptr(), gflat.data_ptr(), s1o.data_ptr(), s2o.data_ptr(), P,
+                                                      parts.data_ptr(), parts.numel(), hp, stp.data_ptr(),
+                                                      norms.data_ptr(), s, d1.data_ptr(), d2.data_ptr(),
+                                                      net.arena.data_ptr(), **fcargs)
+cases["opt_rmsprop_scatter"] = lambda: hip.rmsprop_step(flat.data_ptr(), gflat.data_ptr(), s1o.data_ptr(),
+                                                        s2o.data_ptr(), P, parts.data_ptr(), parts.numel(), hp,
+                                                        stp.data_ptr(), norms.data_ptr(), s, d1.data_ptr(),
+                                                        d2.data_ptr(), net.arena.data_ptr())
+cases["opt_rmsprop_nopack"] = lambda: hip.rmsprop_step(flat.data_ptr(), gflat.data_ptr(), s1o.data_ptr(),
+                                                       s2o.data_ptr(), P, parts.data_ptr(), parts.numel(), hp,
+                                                       stp.data_ptr(), norms.data_ptr(), s)
+cases["grad_sumsq"] = lambda: hip.grad_sumsq(gflat.data_ptr(), P, parts.data_ptr(), s)
 flops = {"conv1": 2 * 3.28e6, "conv2": 2 * 2.65e6, "conv3": 2 * 1.81e6}
 for name, fn in cases.items():
     if a.only and a.only not in name:
