@@ -99,7 +99,8 @@ class DistCfg:
 class KernelCfg:
     forward: str = "hip"             # "hip" (MFMA kernels) | "torch" (autocast/MIOpen path)
     use_graphs: bool = True
-    profile: bool = False
+    profile: bool = False            # roctx ranges around the engine phases (utils.trace)
+    hip_debug: int = 0               # >0: AMD_LOG_LEVEL=<n> + blocking/serialised launches
 
 
 @dataclass
@@ -225,6 +226,7 @@ EXTRA_FLAGS = [
     ("backend", "dist.backend", str), ("master-port", "dist.master_port", int),
     ("heartbeat-timeout", "dist.heartbeat_timeout", float),
     ("forward", "kernel.forward", str), ("no-graphs", None, None), ("profile", "kernel.profile", int),
+    ("hip-debug", "kernel.hip_debug", int),
 ]
 
 

@@ -29,6 +29,7 @@ from dataclasses import dataclass, field
 import torch
 
 from ..models.dqn import DuelingDQN
+from ..utils import trace
 from ..models.fused import HipDuelingNet, NetWorkspace
 from .actor_shard import ActorShard
 from .hbm_replay import HBMReplay
@@ -106,6 +107,7 @@ class ApexEngine:
     # ------------------------------------------------------------------ eager bodies
     def publish_params(self) -> None:
         """Learner -> local actor weights (the on-GPU analogue of learner.py:169-170)."""
+        trace.mark("apex.publish_params")
         self.learner.copy_params_to(self.actor_flat)
         if self.hip_net:
             self.actor_net.copy_packed_from(self.learner.net)
@@ -164,6 +166,10 @@ class ApexEngine:
         (``pipelined_mass``: only when no actor writes the tree between steps, i.e. in
         overlap mode where actor rows are staged and applied by the learner).
         Single-process: ``a1`` is the whole step and ``a2``/``b`` are None."""
+        with trace.range("apex.learner"):
+            self._learn_phases(a1, a2, b, pipelined_mass)
+
+    def _learn_phases(self, a1, a2, b, pipelined_mass: bool) -> None:
         sh = self._sharded
         if sh is not None:
             if self._mass_pending:
@@ -337,6 +343,12 @@ class ApexEngine:
 
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""
+        if trace.enabled():
+            with trace.range(f"apex.train_step {self.learn_steps}"):
+                return self._train_step()
+        return self._train_step()
+
+    def _train_step(self) -> None:
         if self.overlap:
             if self._captured:
                 self._train_step_overlap()

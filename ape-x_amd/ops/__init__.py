@@ -8,6 +8,7 @@ PyTorch fallback for the engine's hot ops.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import sys
 import threading
@@ -36,8 +37,19 @@ def _load(name: str, builder):
 
 
 def cpu():
+    """``APEX_CPU_EXT_DIR`` loads the module from another directory instead (the
+    ASan/UBSan build of the sanitizer test, ``build.build_cpu(sanitize=True)``)."""
     from . import build
 
+    alt = os.environ.get("APEX_CPU_EXT_DIR")
+    if alt:
+        with _lock:
+            if "_apex_cpu" not in _mods:
+                spec = importlib.util.spec_from_file_location("_apex_cpu", os.path.join(alt, build.cpu_target().name))
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+                _mods["_apex_cpu"] = mod
+            return _mods["_apex_cpu"]
     return _load("_apex_cpu", lambda: build.build_cpu())
 
 

@@ -86,16 +86,35 @@ def hip_target() -> Path:
     return HERE / f"_apex_hip{_ext_suffix()}"
 
 
-def build_cpu(force: bool = False) -> Path:
-    target = cpu_target()
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=undefined"]
+
+
+def build_cpu(force: bool = False, out_dir: Path | None = None, sanitize: bool = False) -> Path:
+    """``sanitize``: an ASan + UBSan build of the host replay core into
+    ``out_dir`` -- load it with libasan preloaded (``sanitizer_env``)."""
+    target = cpu_target() if out_dir is None else Path(out_dir) / cpu_target().name
     srcs = [CSRC / s for s in CPU_SOURCES]
     if not force and not _stale(target, srcs + _headers()):
         return target
     cxx = os.environ.get("CXX", "g++")
-    cmd = [cxx, "-O3", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", "-fvisibility=hidden",
+    opt = SANITIZE_FLAGS if sanitize else ["-O3"]
+    cmd = [cxx, *opt, "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", "-fvisibility=hidden",
            *_py_includes(), *map(str, srcs), "-o", str(target)]
     _run(cmd)
     return target
+
+
+def sanitizer_env(ext_dir: Path) -> dict:
+    """Environment for a Python child that imports the sanitized ``_apex_cpu`` from
+    ``ext_dir`` (``APEX_CPU_EXT_DIR``): libasan must be the first DSO loaded."""
+    cxx = os.environ.get("CXX", "g++")
+    asan = subprocess.run([cxx, "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    env = dict(os.environ)
+    env.update(LD_PRELOAD=asan, APEX_CPU_EXT_DIR=str(ext_dir), APEX_NO_AUTOBUILD="1",
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    return env
 
 
 def _hipcc() -> str:

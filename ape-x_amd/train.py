@@ -87,6 +87,12 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    from .utils import trace
+
+    if cfg.kernel.hip_debug:  # before the HIP runtime starts
+        trace.hip_debug_env(cfg.kernel.hip_debug)
+    if cfg.kernel.profile:
+        trace.enable(True)
     if not torch.cuda.is_available():
         raise SystemExit("apex_amd.train runs the GPU engine; use apex_amd.trainers.* or the roles on CPU")
     torch.cuda.set_device(local_rank)

@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
                     help="priority-tree writes on the learner stream instead of a forked stream")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
+    ap.add_argument("--roctx", action="store_true", help="roctx ranges around engine phases (rocprofv3 --marker-trace)")
     ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
                     help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="gloo: host-staged (tests)")
@@ -72,6 +73,10 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.roctx:
+        from apex_amd.utils import trace
+
+        trace.enable(True)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)

@@ -186,3 +186,26 @@ def test_aql_trainers(tmp_path):
     assert len(eps) == 6 and d.learn_idx > 0
     sd = torch.load(tmp_path / "model2.pth", weights_only=True)
     assert "q.advantage1.weight_epsilon" in sd and "proposal.dist_feature.0.weight" in sd
+
+
+def test_trace_ranges_and_hip_debug_flags(monkeypatch):
+    """roctx ranges load libroctx64 (host library, no GPU needed) and nest; the
+    --profile / --hip-debug flags reach the config; hip_debug_env sets the runtime knobs."""
+    from apex_amd.config import args_to_config, build_parser
+    from apex_amd.utils import trace
+
+    if trace.enable(True):
+        with trace.range("outer"):
+            with trace.range("inner"):
+                trace.mark("m")
+    trace.enable(False)
+    with trace.range("disabled"):
+        pass
+    cfg = args_to_config(build_parser().parse_args(["--profile", "1", "--hip-debug", "4"]), environ={})
+    assert cfg.kernel.profile and cfg.kernel.hip_debug == 4
+    for k in ("AMD_LOG_LEVEL", "HIP_LAUNCH_BLOCKING", "AMD_SERIALIZE_KERNEL", "AMD_SERIALIZE_COPY"):
+        monkeypatch.delenv(k, raising=False)
+    env = trace.hip_debug_env(4)
+    import os
+
+    assert os.environ["AMD_LOG_LEVEL"] == "4" and os.environ["HIP_LAUNCH_BLOCKING"] == "1" and env
