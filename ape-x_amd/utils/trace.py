@@ -3,7 +3,7 @@
 The reference has no tracing at all (its only instrumentation is the learner's BPS
 print, learner.py:171-175).  Here:
 
-* ``range(name)`` / ``mark(name)``: roctx ranges (``libroctx64``, via ctypes) around
+* ``range(name)`` / ``mark(name)``: roctx ranges (rocprofiler-sdk roctx, via ctypes) around
   the engine's host-side phases -- actor step, learner step, parameter publish, target
   sync -- so ``rocprofv3 --marker-trace --kernel-trace`` lines kernels up with the
   Ape-X loop.  Off unless ``enable()`` was called (``--profile 1`` / ``APEX_ROCTX=1``);
@@ -25,7 +25,10 @@ _enabled = False
 def _load():
     global _lib
     if _lib is None:
-        for name in ("libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"):
+        # rocprofiler-sdk's roctx first: rocprofv3 --marker-trace records that one (the
+        # legacy roctracer libroctx64 is only seen by the old rocprof)
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                     "libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"):
             try:
                 _lib = ctypes.CDLL(name)
                 break
