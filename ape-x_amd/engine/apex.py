@@ -54,13 +54,42 @@ class EngineConfig:
     use_graphs: bool = True
     overlap: bool = False                # actor graph on its own stream, concurrent with the learner
     exact_mass: bool = True
+    # overlap mode: how the actor and learner streams reach separate hardware queues.
+    # HIP spreads the streams of one priority over GPU_MAX_HW_QUEUES (4) shared queues,
+    # so with enough streams in the process (RCCL/PG streams, torch's stream pools) the
+    # actor and learner streams can share one queue and serialise.
+    #   "none": the next torch pool stream, or the one ``reserve_actor_stream`` took
+    #           before the process group existed (default)
+    #   "pool": both on torch pool streams (the learner off the null stream)
+    #   "probe": the first pool stream that a measured concurrency probe shows running
+    #            beside the learner's stream (experimental)
+    #   "dedicated": CU-masked streams (own HSA queues; measured 2x slower: queue
+    #                oversubscription)
+    #   "priority-actor" / "priority-learner": a high-priority stream (measured slower in
+    #                the single-process step: preemption of the other queue's waves)
+    streams: str = "none"
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
 
 
+_RESERVED: dict = {}
+
+
+def reserve_actor_stream(device) -> None:
+    """Take the actor's stream from torch's stream pool NOW -- call it before
+    ``init_process_group`` and anything else that draws pool streams.  Pool streams are
+    spread round-robin over the GPU's hardware queues (GPU_MAX_HW_QUEUES = 4); the
+    process group's RCCL stream drawn first shifts the actor's stream onto the learner's
+    queue (rocprofv3: actor and learner kernels strictly interleaved on one queue, 0.51
+    vs 0.31 ms/step).  Reserving first gives every rank the single-process layout."""
+    dev = torch.device(device)
+    if dev not in _RESERVED:
+        _RESERVED[dev] = torch.cuda.Stream(device=dev)
+
+
 class ApexEngine:
     def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", allreduce=None,
-                 model: DuelingDQN | None = None, sharded: bool = False):
+                 model: DuelingDQN | None = None, sharded: bool = False, force_collectives: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
         lc = cfg.learner
@@ -77,7 +106,7 @@ class ApexEngine:
         if sharded:
             from ..parallel.sharded import ShardedSampling
 
-            self._sharded = ShardedSampling(self.replay)
+            self._sharded = ShardedSampling(self.replay, force=force_collectives)
         self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce, sharded=self._sharded)
         self.actor_model = copy.deepcopy(self.learner.model)
         self.actor_model._flat = None
@@ -100,7 +129,8 @@ class ApexEngine:
         # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
         # train step while the learner applies the other half (the previous step's)
         self._half = 0
-        self._astream = torch.cuda.Stream(device=self.device) if self.overlap else None
+        self.stream_probe = None
+        self._astream, self._lstream = self._make_streams(cfg.streams) if self.overlap else (None, None)
         self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()] if self.overlap else None
         self._ev_learn = torch.cuda.Event() if self.overlap else None
 
@@ -170,26 +200,35 @@ class ApexEngine:
             self._learn_phases(a1, a2, b, pipelined_mass)
 
     def _learn_phases(self, a1, a2, b, pipelined_mass: bool) -> None:
+        R = trace.range
         sh = self._sharded
         if sh is not None:
-            if self._mass_pending:
-                w = self._mass_work
-                self._mass_pending, self._mass_work = False, None
-            else:
-                w = sh.start_exchange()
-            sh.wait(w)
-        a1()
+            with R("mass.wait"):
+                if self._mass_pending:
+                    w = self._mass_work
+                    self._mass_pending, self._mass_work = False, None
+                else:
+                    w = sh.start_exchange()
+                sh.wait(w)
+        with R("learn.a1"):
+            a1()
         if a2 is None:
             return
         ar = self._allreduce
         fc, conv = self.learner.grad_slices()
-        w1 = ar.start(fc)
-        a2()
-        w2 = ar.start(conv)
+        with R("ar.fc.start"):
+            w1 = ar.start(fc)
+        with R("learn.a2"):
+            a2()
+        with R("ar.conv.start"):
+            w2 = ar.start(conv)
         if sh is not None and pipelined_mass:
-            self._mass_work, self._mass_pending = sh.start_exchange(), True
-        ar.wait(w1, w2)
-        b()
+            with R("mass.start"):
+                self._mass_work, self._mass_pending = sh.start_exchange(), True
+        with R("ar.wait"):
+            ar.wait(w1, w2)
+        with R("learn.b"):
+            b()
 
     def _drain_mass(self) -> None:
         """Drop a pipelined mass exchange (something other than a train step is about to
@@ -201,12 +240,21 @@ class ApexEngine:
     # ------------------------------------------------------------------ graphs
     @staticmethod
     def _graph(fn, pool):
+        # thread_local capture: the process group's watchdog thread polls RCCL work events
+        # while we capture; in the default (global) mode that call invalidates the capture
+        # ("operation not permitted when stream is capturing", seen with --force-dp)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=pool):
+        with torch.cuda.graph(g, pool=pool, capture_error_mode="thread_local"):
             fn()
         return g
 
     def capture(self, warmup_iters: int = 3) -> None:
+        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
+            with self._on_lstream():
+                return self.capture(warmup_iters)
+        return self._capture(warmup_iters)
+
+    def _capture(self, warmup_iters: int) -> None:
         """Warm up on a side stream, then capture actor and learner steps as hipGraphs.
         The warm-up iterations are real train steps and are counted as such.  Collectives
         stay eager, between the learner's phase graphs."""
@@ -325,6 +373,9 @@ class ApexEngine:
 
     def fill(self, min_transitions: int | None = None) -> None:
         """Run actor steps until the replay holds ``threshold_size`` slots."""
+        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
+            with self._on_lstream():
+                return self.fill(min_transitions)
         self._drain_mass()
         need = self.cfg.threshold_size if min_transitions is None else min_transitions
         steps = max(-(-need // self.cfg.n_envs), 4)
@@ -341,10 +392,84 @@ class ApexEngine:
         for _ in range(steps):
             self.actor_step()
 
+    def _make_streams(self, mode: str):
+        """(actor stream, learner stream or None = the caller's stream), see
+        EngineConfig.streams."""
+        dev = self.device
+        if mode == "probe":
+            return self._probe_actor_stream(), None
+        if mode == "dedicated":
+            from .. import ops
+
+            h = ops.hip()
+            mk = lambda: torch.cuda.ExternalStream(h.create_dedicated_stream(dev.index or 0), device=dev)  # noqa: E731
+            return mk(), mk()
+        if mode == "pool":  # learner off the null stream too (no legacy null-stream syncs)
+            return _RESERVED.pop(dev, None) or torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+        if mode == "priority-actor":
+            return torch.cuda.Stream(device=dev, priority=-1), None
+        if mode == "priority-learner":
+            return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev, priority=-1)
+        if mode == "none":
+            return _RESERVED.pop(dev, None) or torch.cuda.Stream(device=dev), None
+        raise ValueError(f"streams={mode!r}")
+
+    def _probe_actor_stream(self, tries: int = 8):
+        """Pick an actor stream that really runs concurrently with the learner's stream
+        (the caller's current stream): a 300 us one-wave spin on the learner stream, a
+        tiny one on the candidate; concurrent iff the candidate's finishes first.  Pool
+        streams cycle over the hardware queues, so a few candidates cover them all."""
+        from .. import ops
+
+        h = ops.hip()
+        L = torch.cuda.current_stream(self.device)
+        first = None
+        for _ in range(tries):
+            A = torch.cuda.Stream(device=self.device)
+            first = first or A
+            torch.cuda.synchronize(self.device)
+            e0, e1, ea = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(L)
+            h.spin_us(300, L.cuda_stream)
+            e1.record(L)
+            h.spin_us(1, A.cuda_stream)
+            ea.record(A)
+            torch.cuda.synchronize(self.device)
+            if e0.elapsed_time(ea) < 0.5 * e0.elapsed_time(e1):
+                self.stream_probe = {"tries": _ + 1, "concurrent": True}
+                return A
+        self.stream_probe = {"tries": tries, "concurrent": False}
+        import warnings
+
+        warnings.warn("no pool stream ran concurrently with the learner stream; actor/learner overlap may serialise")
+        return first
+
+    def _on_lstream(self):
+        """Context: the learner's stream (high priority) when configured, else a no-op.
+        Entering it makes that stream wait for the caller's stream (ordering with work
+        the caller enqueued, e.g. a weight broadcast)."""
+        import contextlib
+
+        if self._lstream is None:
+            return contextlib.nullcontext()
+
+        @contextlib.contextmanager
+        def ctx():
+            cur = torch.cuda.current_stream(self.device)
+            self._lstream.wait_stream(cur)
+            with torch.cuda.stream(self._lstream):
+                yield
+            cur.wait_stream(self._lstream)  # results visible to the caller's stream
+
+        return ctx()
+
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""
+        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
+            with self._on_lstream():
+                return self.train_step()
         if trace.enabled():
-            with trace.range(f"apex.train_step {self.learn_steps}"):
+            with trace.range("apex.train_step"):
                 return self._train_step()
         return self._train_step()
 

@@ -187,12 +187,12 @@ class CentralApexEngine:
         pool = torch.cuda.graph_pool_handle()
         if self.is_learner:
             self._g_learn = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_learn, pool=pool):
+            with torch.cuda.graph(self._g_learn, pool=pool, capture_error_mode="thread_local"):
                 self.learner.step()
         else:
             self.sender.wait()
             self._g_actor = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_actor, pool=pool):
+            with torch.cuda.graph(self._g_actor, pool=pool, capture_error_mode="thread_local"):
                 self._actor_body()
         torch.cuda.synchronize(self.device)
 

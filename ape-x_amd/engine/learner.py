@@ -185,11 +185,14 @@ class DQNLearner:
         """Sample, forward x3, loss + heads backward; single-process: the whole backward
         too; data-parallel split: up to the FC1 backward and its finalize."""
         s = self._stream()
-        glob = None
+        glob = shard = None
         if self.sharded is not None:  # gathered shard masses -> global pmin + shard weight scale
-            self.sharded.finalize()
-            glob = self.sharded.glob
-        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob)
+            if self.sharded.in_kernel:
+                shard = self.sharded.sample_args()
+            else:
+                self.sharded.finalize()
+                glob = self.sharded.glob
+        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.

@@ -28,8 +28,9 @@ struct TreeHandle {
 };
 
 TreeHandle make_tree(uint64_t leaf_sum, uint64_t leaf_min, const std::vector<uint64_t>& node_sum,
-                     const std::vector<uint64_t>& node_min, const std::vector<int>& sizes) {
+                     const std::vector<uint64_t>& node_min, const std::vector<int>& sizes, uint64_t root_out) {
   TreeHandle h;
+  h.d.root_out = P<double>(root_out);
   if (node_sum.size() != node_min.size() || sizes.size() != node_sum.size() + 1)
     throw std::invalid_argument("tree: inconsistent level lists");
   if ((int)node_sum.size() > kMaxTreeLevels || node_sum.empty()) throw std::invalid_argument("tree: bad level count");
@@ -62,7 +63,8 @@ PYBIND11_MODULE(_apex_hip, m) {
   py::class_<TreeHandle>(m, "TreeHandle").def_property_readonly("levels", [](const TreeHandle& h) {
     return h.d.levels;
   });
-  m.def("make_tree", &make_tree);
+  m.def("make_tree", &make_tree, py::arg("leaf_sum"), py::arg("leaf_min"), py::arg("node_sum"), py::arg("node_min"),
+        py::arg("sizes"), py::arg("root_out") = 0);
 
   // ---- replay
   m.def("per_write_leaves", [](const TreeHandle& t, uint64_t idx, uint64_t prio, int B, float alpha,
@@ -78,12 +80,13 @@ PYBIND11_MODULE(_apex_hip, m) {
      py::arg("mix_loss_out") = 0);
   m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
-                         int exclude_last, uint64_t s, uint64_t glob) {
+                         int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank) {
     per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
-               P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s));
+               P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s),
+               ShardGlob{P<const double>(gathered), world, rank});
   }, py::arg("t"), py::arg("B"), py::arg("length_ptr"), py::arg("length"), py::arg("beta_ptr"), py::arg("beta"),
      py::arg("seed"), py::arg("counter"), py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"),
-     py::arg("s"), py::arg("glob") = 0);
+     py::arg("s"), py::arg("glob") = 0, py::arg("gathered") = 0, py::arg("world") = 0, py::arg("rank") = 0);
   m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
                                  uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {
@@ -370,6 +373,28 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("pack_conv_wt", [](uint64_t src, uint64_t dst, int N, int C, int KH, int KW, uint64_t s) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));
   });
+  // A stream on its OWN hardware queue: a CU-masked stream always gets a dedicated HSA
+  // queue (the mask is a queue property), here with every CU enabled.  Plain streams of
+  // one priority are spread round-robin over GPU_MAX_HW_QUEUES (4) shared queues, where
+  // two logically concurrent streams (actor / learner) can land on one queue and
+  // serialise.  Returns the hipStream_t as an integer (torch.cuda.ExternalStream).
+  m.def("create_dedicated_stream", [](int device) {
+    auto hip_ok = [](hipError_t e) {
+      if (e != hipSuccess) throw std::runtime_error(std::string("create_dedicated_stream: ") + hipGetErrorString(e));
+    };
+    int cus = 0;
+    hip_ok(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    std::vector<uint32_t> mask((cus + 31) / 32, 0xFFFFFFFFu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+    int prev = 0;
+    hip_ok(hipGetDevice(&prev));
+    hip_ok(hipSetDevice(device));
+    hipStream_t st = nullptr;
+    hip_ok(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    hip_ok(hipSetDevice(prev));
+    return (uint64_t)reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("spin_us", [](int us, uint64_t s) { spin_us(us, S(s)); });
   m.def("copy_f32", [](uint64_t dst, uint64_t src, int64_t n, uint64_t s) {
     copy_f32(P<float>(dst), P<const float>(src), n, S(s));
   });

@@ -23,6 +23,16 @@ struct TreeDesc {
   float* node_min[kMaxTreeLevels];
   int size[kMaxTreeLevels + 1];
   int levels;
+  // optional: every root recompute also writes (total mass, min priority) here as fp64
+  // -- the sharded replay's all-gather send buffer, so no copy kernels per step
+  double* root_out;
+};
+// Sharded replay (parallel.sharded): the all-gathered per-shard (mass, min priority)
+// pairs; the sampler derives the global min priority and this shard's IS-weight scale
+// world * M_rank / sum_r M_r in-kernel (no host-side or torch-op finalize).
+struct ShardGlob {
+  const double* gathered;  // [world][2]
+  int world, rank;
 };
 
 // ---- replay_kernels.hip
@@ -43,7 +53,7 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 // weights, glob[1] = this shard's weight scale (apex_amd.parallel.sharded).
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, const float* glob, hipStream_t s);
+                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg = ShardGlob{nullptr, 0, 0});
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
                         uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s);
@@ -194,6 +204,9 @@ void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const do
                const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
                const PackMap* pack = nullptr, const FcPack* fc = nullptr);
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s);
+// One wave busy-waits `us` microseconds on the constant-rate wall clock (bounded; used by
+// the engine's stream-concurrency probe).
+void spin_us(int us, hipStream_t s);
 
 // ---- conv_kernels.hip (Nature-CNN dueling net, bf16 MFMA)
 // layer 1: `in` is the u8 frame ring (ids/idx: FrameSrc, see common.h) or a dense u8 stack

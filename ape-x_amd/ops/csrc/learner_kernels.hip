@@ -341,6 +341,21 @@ void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const do
   launch_opt(p, g, m, v, n, partials, n_partials, hp, step, norms_out, pack, fc, s);
 }
 
+__global__ void spin_k(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+void spin_us(int us, hipStream_t s) {
+  if (us < 0 || us > 100000) throw std::invalid_argument("spin_us: 0..100000 us");
+  int dev = 0, khz = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+  if (khz <= 0) khz = 100000;  // 100 MHz
+  spin_k<<<1, 64, 0, s>>>((uint64_t)khz * (uint64_t)us / 1000ull);
+  LAUNCH_CHECK();
+}
+
 void copy_f32(float* dst, const float* src, int64_t n, hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s));
 }

@@ -170,6 +170,10 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;
+    if (level == t.levels && t.root_out) {  // the root: also the shard-mass send buffer
+      t.root_out[0] = s;
+      t.root_out[1] = (double)m;
+    }
   }
 }
 
@@ -195,6 +199,10 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;
+    if (level == t.levels && t.root_out) {  // the root: also the shard-mass send buffer
+      t.root_out[0] = s;
+      t.root_out[1] = (double)m;
+    }
   }
 }
 
@@ -270,7 +278,8 @@ __global__ __launch_bounds__(1024) void per_update_top_k(TreeDesc t, const int* 
 __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64_t length_const,
                              const float* beta_ptr, float beta_const, uint64_t seed,
                              const int64_t* __restrict__ counter, int* __restrict__ out_idx,
-                             float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob) {
+                             float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob,
+                             ShardGlob sg) {
   const int lane = threadIdx.x & 63;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (i >= B) return;
@@ -304,10 +313,16 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
     if (mass < 0.0) mass = 0.0;
     node = node * kTreeFanout + k;
   }
+  float pmin = glob ? glob[0] : t.node_min[L - 1][0];
+  float wscale = glob ? glob[1] : 1.f;
+  if (sg.gathered) {  // global min priority + k M_rank / sum M over the shards (world <= 64)
+    const bool ok = lane < sg.world;
+    const double m = wave_sum(ok ? sg.gathered[2 * lane] : 0.0);
+    pmin = wave_min(ok ? (float)sg.gathered[2 * lane + 1] : INFINITY);
+    wscale = (float)((double)sg.world * sg.gathered[2 * sg.rank] / fmax(m, 1e-300));
+  }
   if (lane == 0) {
     const float p = t.leaf_sum[node];
-    const float pmin = glob ? glob[0] : t.node_min[L - 1][0];
-    const float wscale = glob ? glob[1] : 1.f;
     out_idx[i] = node;
     out_w[i] = wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
   }
@@ -400,11 +415,13 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) 
 
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, const float* glob, hipStream_t s) {
+                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg) {
   if (B <= 0) return;
+  if (sg.gathered && (sg.world < 1 || sg.world > 64 || sg.rank < 0 || sg.rank >= sg.world))
+    throw std::invalid_argument("per_sample: sharded world must be in [1, 64] with 0 <= rank < world");
   const int waves_per_block = 4;
   per_sample_k<<<(B + waves_per_block - 1) / waves_per_block, 64 * waves_per_block, 0, s>>>(
-      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob);
+      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob, sg);
   LAUNCH_CHECK();
 }
 

@@ -25,8 +25,12 @@ class FlatGradAllReduce:
     all-reduce overlaps the conv backward, and no scaling kernel runs.
     """
 
-    def __init__(self, world_size: int | None = None, group=None, bucket_bytes: int | None = None):
+    def __init__(self, world_size: int | None = None, group=None, bucket_bytes: int | None = None,
+                 force: bool = False):
+        """``force``: issue the collectives even in a 1-rank group (measures the RCCL call
+        path and host cost of the data-parallel step on a single GPU)."""
         self.group = group
+        self.force = force
         self.world = world_size or dist.get_world_size(group)
         self.scale = 1.0 / self.world
         self.bucket_elems = None if bucket_bytes is None else max(1, bucket_bytes // 4)
@@ -43,7 +47,7 @@ class FlatGradAllReduce:
 
     def start(self, t: torch.Tensor):
         """Asynchronous in-place SUM of ``t``; returns the work handle(s) (None: world 1)."""
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return None
         if self.bucket_elems is None or t.numel() <= self.bucket_elems:
             return dist.all_reduce(t, group=self.group, async_op=True)

@@ -27,9 +27,10 @@ import torch.distributed as dist
 
 
 class ShardedSampling:
-    def __init__(self, replay, group=None):
+    def __init__(self, replay, group=None, force: bool = False):
         self.replay = replay
         self.group = group
+        self.force = force  # collective even in a 1-rank group (single-GPU measurement of the DP path)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         dev = replay.device if hasattr(replay, "device") else torch.device("cpu")
@@ -39,6 +40,15 @@ class ShardedSampling:
 
     def _root(self):
         return self.replay.node_sum[-1][:1], self.replay.node_min[-1][:1]
+
+    @property
+    def in_kernel(self) -> bool:
+        """HBM replay: the tree kernels keep ``root_stats`` (the send buffer) current and
+        the sampler reads ``gathered`` itself -- no pack copies, no finalize ops."""
+        return hasattr(self.replay, "root_stats")
+
+    def sample_args(self) -> tuple:
+        return self.gathered, self.world, self.rank
 
     def exchange(self) -> None:
         """Pack this shard's (mass, min priority) and all-gather them (eager: collectives
@@ -50,12 +60,16 @@ class ShardedSampling:
         process group's stream without making the current stream wait -- the engine
         issues the NEXT step's exchange right after this step's backward (the tree is
         final by then) so it overlaps the optimizer.  Returns the work handle."""
-        mass, pmin = self._root()
-        self.local[0:1].copy_(mass)
-        self.local[1:2].copy_(pmin)
-        if self.world > 1:
-            return dist.all_gather_into_tensor(self.gathered, self.local, group=self.group, async_op=True)
-        self.gathered.copy_(self.local)
+        if self.in_kernel:
+            local = self.replay.root_stats
+        else:
+            mass, pmin = self._root()
+            self.local[0:1].copy_(mass)
+            self.local[1:2].copy_(pmin)
+            local = self.local
+        if self.world > 1 or self.force:
+            return dist.all_gather_into_tensor(self.gathered, local, group=self.group, async_op=True)
+        self.gathered.copy_(local)
         return None
 
     @staticmethod

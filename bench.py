@@ -56,11 +56,19 @@ def parse():
     ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
                     help="priority-tree writes on the learner stream instead of a forked stream")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
+    ap.add_argument("--no-reserve", dest="reserve", action="store_false",
+                    help="do not take the actor stream from the pool before the process group")
+    ap.add_argument("--streams", default="none",
+                    choices=["none", "pool", "probe", "dedicated", "priority-actor", "priority-learner"],
+                    help="overlap mode: how the actor and learner streams get separate HW queues")
     ap.add_argument("--roctx", action="store_true", help="roctx ranges around engine phases (rocprofv3 --marker-trace)")
     ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
                     help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="gloo: host-staged (tests)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal, gloo)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="run the data-parallel step (RCCL collectives, sharded sampling) even with 1 rank "
+                         "(under torch.distributed.run --nproc-per-node 1): measures its single-GPU overhead")
     ap.add_argument("--local-sampling", action="store_true",
                     help="N>1: sample each replay shard on its own (default: global PER over shards)")
     return ap.parse_args()
@@ -84,7 +92,11 @@ def main():
         local_rank = 0
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    if args.reserve and args.topology == "sharded":
+        from apex_amd.engine.apex import reserve_actor_stream
+
+        reserve_actor_stream(device)  # before the process group draws its pool streams
+    if world > 1 or args.force_dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
@@ -103,10 +115,11 @@ def main():
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
                        use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
-                       learner=lc)
-    allreduce = FlatGradAllReduce(world) if world > 1 else None
-    sharded = world > 1 and not args.local_sampling
-    eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded)
+                       streams=args.streams, learner=lc)
+    dp = world > 1 or args.force_dp
+    allreduce = FlatGradAllReduce(world, force=args.force_dp) if dp else None
+    sharded = dp and not args.local_sampling
+    eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
         from apex_amd.parallel.broadcast import broadcast_flat
 
@@ -167,7 +180,7 @@ def main():
                 "global_batch": args.batch * world,
                 "seq_len": 3,
                 "seq_len_meaning": "n-step return horizon (frame stack 4)",
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{world}" + ("-forced" if args.force_dp and world == 1 else ""),
                 "replay_sampling": "global PER over shards (mass all-gather)" if sharded else "per-shard PER",
                 "replay_capacity_per_gpu": args.capacity,
                 "envs_per_gpu": args.envs,
@@ -177,17 +190,19 @@ def main():
                 "forward": args.forward,
                 "hip_graphs": not args.no_graphs,
                 "actor_learner_overlap": args.overlap,
+                "actor_stream": args.streams,
             },
             "actor_frames_per_sec": round(frames_per_s, 1),
             "learner_samples_per_sec": round(steps_per_s * args.batch, 1),
             "vs_paper_19_batches_per_s": round(steps_per_s / PAPER_BATCHES_PER_S, 2),
             "replay_fill_seconds": round(t_fill, 3),
             "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
+            "stream_probe": eng.stream_probe,
             "last_loss": round(stats["loss"], 6),
             "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
