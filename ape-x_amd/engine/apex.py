@@ -90,6 +90,9 @@ def reserve_actor_stream(device) -> None:
 class ApexEngine:
     def __init__(self, cfg: EngineConfig, device: str | torch.device = "cuda", allreduce=None,
                  model: DuelingDQN | None = None, sharded: bool = False, force_collectives: bool = False):
+        """``allreduce``: data-parallel gradient all-reduce (``parallel.dp.FlatGradAllReduce``
+        over torch.distributed, or ``parallel.rccl.RcclGradAllReduce``, direct RCCL); the
+        shard-mass exchange uses the same object."""
         self.cfg = cfg
         self.device = torch.device(device)
         lc = cfg.learner
@@ -106,7 +109,7 @@ class ApexEngine:
         if sharded:
             from ..parallel.sharded import ShardedSampling
 
-            self._sharded = ShardedSampling(self.replay, force=force_collectives)
+            self._sharded = ShardedSampling(self.replay, force=force_collectives, comm=allreduce)
         self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce, sharded=self._sharded)
         self.actor_model = copy.deepcopy(self.learner.model)
         self.actor_model._flat = None
@@ -123,7 +126,7 @@ class ApexEngine:
         self.actor_steps = 0
         self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = None
         self._pool = None
-        self._mass_work, self._mass_pending = None, False  # pipelined shard-mass all-gather
+        self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
         self._captured = False
         self._allreduce = allreduce
         # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
@@ -202,14 +205,10 @@ class ApexEngine:
     def _learn_phases(self, a1, a2, b, pipelined_mass: bool) -> None:
         R = trace.range
         sh = self._sharded
-        if sh is not None:
-            with R("mass.wait"):
-                if self._mass_pending:
-                    w = self._mass_work
-                    self._mass_pending, self._mass_work = False, None
-                else:
-                    w = sh.start_exchange()
-                sh.wait(w)
+        if sh is not None and not self._mass_pending:
+            with R("mass.exchange"):
+                sh.exchange()
+        self._mass_pending = False
         with R("learn.a1"):
             a1()
         if a2 is None:
@@ -219,23 +218,21 @@ class ApexEngine:
         with R("ar.fc.start"):
             w1 = ar.start(fc)
         with R("learn.a2"):
-            a2()
+            a2()  # (sharded: ends by packing this shard's slot in front of the conv grads)
         with R("ar.conv.start"):
             w2 = ar.start(conv)
-        if sh is not None and pipelined_mass:
-            with R("mass.start"):
-                self._mass_work, self._mass_pending = sh.start_exchange(), True
+        # the slots travelled with the conv grads: the next step's masses are exchanged
+        # (valid when no actor writes the tree in between: overlap mode)
+        self._mass_pending = sh is not None and pipelined_mass and self.learner.grad_prefix > 0
         with R("ar.wait"):
             ar.wait(w1, w2)
         with R("learn.b"):
             b()
 
     def _drain_mass(self) -> None:
-        """Drop a pipelined mass exchange (something other than a train step is about to
-        touch the tree): wait for it so the buffers are quiet, re-exchange next step."""
-        if self._mass_pending:
-            self._sharded.wait(self._mass_work)
-            self._mass_pending, self._mass_work = False, None
+        """Something other than a train step is about to touch the tree: the pipelined
+        shard masses are stale, re-exchange at the next step."""
+        self._mass_pending = False
 
     # ------------------------------------------------------------------ graphs
     @staticmethod

@@ -69,12 +69,9 @@ class HBMReplay:
         self.max_prio = torch.ones(1, dtype=torch.float32, device=dev)
         self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sorted_scratch = torch.zeros(1024, dtype=torch.int32, device=dev)
-        # (total mass, min priority) of the root as fp64, rewritten by every root recompute
-        # (the sharded replay's all-gather send buffer)
-        self.root_stats = torch.zeros(2, dtype=torch.float64, device=dev)
         self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
                                        [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
-                                       sizes, self.root_stats.data_ptr())
+                                       sizes)
 
     # ------------------------------------------------------------------ bytes
     def nbytes(self) -> int:
@@ -115,8 +112,8 @@ class HBMReplay:
                        glob: torch.Tensor | None = None, shard: tuple | None = None) -> None:
         """``glob`` (sharded replay): f32 [2] device tensor = (global min priority, this
         shard's IS-weight scale), see :mod:`apex_amd.parallel.sharded`; or ``shard`` =
-        (gathered fp64 [world, 2] (mass, min priority) per shard, world, rank): the
-        sampler derives both in-kernel."""
+        (exchanged fp32 slots [world, 2] = (mass, min priority) per shard, world, rank):
+        the sampler derives both in-kernel."""
         excl = (not self.exact_mass) if exclude_last is None else exclude_last
         beta_ptr = beta.data_ptr() if isinstance(beta, torch.Tensor) else 0
         beta_c = 0.0 if isinstance(beta, torch.Tensor) else float(beta)
@@ -124,6 +121,11 @@ class HBMReplay:
                             out_idx.data_ptr(), out_w.data_ptr(), int(excl), self._stream(),
                             0 if glob is None else glob.data_ptr(),
                             *((0, 0, 0) if shard is None else (shard[0].data_ptr(), int(shard[1]), int(shard[2]))))
+
+    def pack_shard_slots(self, slots: torch.Tensor, world: int, rank: int) -> None:
+        """slots[:] = 0 except slot ``rank`` = (root mass, root min priority) (fp32)."""
+        assert slots.dtype == torch.float32 and slots.numel() >= 2 * world
+        self.hip.pack_shard_slots(self.tree, slots.data_ptr(), world, rank, self._stream())
 
     def gather(self, idx: torch.Tensor, out_s, out_s2, out_a, out_r, out_d) -> None:
         self.hip.gather_transitions(self.frames.data_ptr(), self.frame_bytes, self.s_ids.data_ptr(),

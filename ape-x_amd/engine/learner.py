@@ -79,7 +79,16 @@ class DQNLearner:
             p.requires_grad_(False)
         self.P = self.flat.numel()
         dev = self.device
-        self.flat_grad = torch.zeros(self.P, dtype=torch.float32, device=dev)
+        # gradient buffer = [shard slots (sharded DP) + padding | flat gradient]: the slots
+        # ride the conv-gradient all-reduce (parallel.sharded); the padding keeps the flat
+        # gradient 256-byte aligned
+        self.dp_split_possible = allreduce is not None and cfg.forward == "hip"
+        ns = 2 * sharded.world if (sharded is not None and self.dp_split_possible) else 0
+        self.grad_prefix = -(-ns // 64) * 64
+        self.grad_buf = torch.zeros(self.grad_prefix + self.P, dtype=torch.float32, device=dev)
+        self.flat_grad = self.grad_buf[self.grad_prefix:]
+        if ns:
+            sharded.slots = self.grad_buf[:ns]
         off = 0
         for p in self.model.parameters():
             n = p.numel()
@@ -160,12 +169,13 @@ class DQNLearner:
         """Data-parallel HIP learner: the backward runs as two phases so the FC1/head
         gradients (the tail of the flat buffer, ~91% of its bytes) are all-reduced while
         the conv backward runs (:meth:`forward_phase` / :meth:`backward_phase`)."""
-        return self.allreduce is not None and self.hip_net
+        return self.dp_split_possible
 
     def grad_slices(self) -> tuple[torch.Tensor, torch.Tensor]:
-        """(FC1 + heads tail, conv head) views of the flat gradient, in all-reduce order."""
+        """(FC1 + heads tail, [shard slots +] conv head) views of the gradient buffer, in
+        all-reduce order."""
         fc_off = self.fc_grad_offset
-        return self.flat_grad[fc_off:], self.flat_grad[:fc_off]
+        return self.flat_grad[fc_off:], self.grad_buf[:self.grad_prefix + fc_off]
 
     @property
     def fc_grad_offset(self) -> int:
@@ -247,6 +257,10 @@ class DQNLearner:
         self._tree_fork_begin()
         self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx)
         self._tree_fork_end()
+        if self.sharded is not None and self.grad_prefix:
+            # the tree is final for the next sample: pack this shard's slot, which the
+            # conv-gradient all-reduce then exchanges (the next step's shard masses)
+            self.sharded.pack()
 
     def _tree_fork_begin(self) -> None:
         """Fork: deferred actor-row priorities, then the priority mix + loss mean + tree

@@ -45,6 +45,7 @@ HIP_SOURCES = [
     "conv1_kernels.hip",
     "fc_kernels.hip",
     "loss_heads_kernels.hip",
+    "comm.cpp",
 ]
 
 
@@ -159,7 +160,7 @@ def build_hip(force: bool = False, jobs: int | None = None) -> Path:
             list(ex.map(_run, todo))
     if force or todo or _stale(target, objs):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-               f"-L{ROCM / 'lib'}", "-lamdhip64", "-o", str(target)]
+               f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-o", str(target)]
         _run(cmd)
     return target
 

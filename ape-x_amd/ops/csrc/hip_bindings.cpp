@@ -28,9 +28,8 @@ struct TreeHandle {
 };
 
 TreeHandle make_tree(uint64_t leaf_sum, uint64_t leaf_min, const std::vector<uint64_t>& node_sum,
-                     const std::vector<uint64_t>& node_min, const std::vector<int>& sizes, uint64_t root_out) {
+                     const std::vector<uint64_t>& node_min, const std::vector<int>& sizes) {
   TreeHandle h;
-  h.d.root_out = P<double>(root_out);
   if (node_sum.size() != node_min.size() || sizes.size() != node_sum.size() + 1)
     throw std::invalid_argument("tree: inconsistent level lists");
   if ((int)node_sum.size() > kMaxTreeLevels || node_sum.empty()) throw std::invalid_argument("tree: bad level count");
@@ -56,15 +55,20 @@ struct NStepHandle {
 
 }  // namespace
 
+void register_comm(py::module_& m);  // comm.cpp (direct RCCL)
+
 PYBIND11_MODULE(_apex_hip, m) {
+  register_comm(m);
   m.doc() = "apex_amd gfx950 kernels (HBM replay, actor shard, fused learner)";
   m.attr("arch") = "gfx950";
 
   py::class_<TreeHandle>(m, "TreeHandle").def_property_readonly("levels", [](const TreeHandle& h) {
     return h.d.levels;
   });
-  m.def("make_tree", &make_tree, py::arg("leaf_sum"), py::arg("leaf_min"), py::arg("node_sum"), py::arg("node_min"),
-        py::arg("sizes"), py::arg("root_out") = 0);
+  m.def("make_tree", &make_tree);
+  m.def("pack_shard_slots", [](const TreeHandle& t, uint64_t slots, int world, int rank, uint64_t s) {
+    pack_shard_slots(t.d, P<float>(slots), world, rank, S(s));
+  });
 
   // ---- replay
   m.def("per_write_leaves", [](const TreeHandle& t, uint64_t idx, uint64_t prio, int B, float alpha,
@@ -83,10 +87,10 @@ PYBIND11_MODULE(_apex_hip, m) {
                          int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank) {
     per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
                P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s),
-               ShardGlob{P<const double>(gathered), world, rank});
+               ShardGlob{P<const float>(gathered), world, rank});
   }, py::arg("t"), py::arg("B"), py::arg("length_ptr"), py::arg("length"), py::arg("beta_ptr"), py::arg("beta"),
      py::arg("seed"), py::arg("counter"), py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"),
-     py::arg("s"), py::arg("glob") = 0, py::arg("gathered") = 0, py::arg("world") = 0, py::arg("rank") = 0);
+     py::arg("s"), py::arg("glob") = 0, py::arg("slots") = 0, py::arg("world") = 0, py::arg("rank") = 0);
   m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
                                  uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {

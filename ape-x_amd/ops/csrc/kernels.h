@@ -23,17 +23,18 @@ struct TreeDesc {
   float* node_min[kMaxTreeLevels];
   int size[kMaxTreeLevels + 1];
   int levels;
-  // optional: every root recompute also writes (total mass, min priority) here as fp64
-  // -- the sharded replay's all-gather send buffer, so no copy kernels per step
-  double* root_out;
 };
-// Sharded replay (parallel.sharded): the all-gathered per-shard (mass, min priority)
-// pairs; the sampler derives the global min priority and this shard's IS-weight scale
+// Sharded replay (parallel.sharded): the exchanged per-shard (mass, min priority) slots;
+// the sampler derives the global min priority and this shard's IS-weight scale
 // world * M_rank / sum_r M_r in-kernel (no host-side or torch-op finalize).
 struct ShardGlob {
-  const double* gathered;  // [world][2]
+  const float* slots;  // [world][2]
   int world, rank;
 };
+// Zero `slots` [world][2] and write this shard's (root mass, root min priority) into
+// slot `rank`: after a SUM all-reduce every rank holds all shards' pairs (an all-gather
+// folded into the learner's conv-gradient all-reduce).
+void pack_shard_slots(const TreeDesc& t, float* slots, int world, int rank, hipStream_t s);
 
 // ---- replay_kernels.hip
 // Write prio**alpha into the leaves of `idx` AND recompute every dirty ancestor.

@@ -170,10 +170,6 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;
-    if (level == t.levels && t.root_out) {  // the root: also the shard-mass send buffer
-      t.root_out[0] = s;
-      t.root_out[1] = (double)m;
-    }
   }
 }
 
@@ -199,10 +195,6 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;
-    if (level == t.levels && t.root_out) {  // the root: also the shard-mass send buffer
-      t.root_out[0] = s;
-      t.root_out[1] = (double)m;
-    }
   }
 }
 
@@ -315,11 +307,11 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
   }
   float pmin = glob ? glob[0] : t.node_min[L - 1][0];
   float wscale = glob ? glob[1] : 1.f;
-  if (sg.gathered) {  // global min priority + k M_rank / sum M over the shards (world <= 64)
+  if (sg.slots) {  // global min priority + k M_rank / sum M over the shards (world <= 64)
     const bool ok = lane < sg.world;
-    const double m = wave_sum(ok ? sg.gathered[2 * lane] : 0.0);
-    pmin = wave_min(ok ? (float)sg.gathered[2 * lane + 1] : INFINITY);
-    wscale = (float)((double)sg.world * sg.gathered[2 * sg.rank] / fmax(m, 1e-300));
+    const double m = wave_sum(ok ? (double)sg.slots[2 * lane] : 0.0);
+    pmin = wave_min(ok ? sg.slots[2 * lane + 1] : INFINITY);
+    wscale = (float)((double)sg.world * (double)sg.slots[2 * sg.rank] / fmax(m, 1e-300));
   }
   if (lane == 0) {
     const float p = t.leaf_sum[node];
@@ -417,11 +409,27 @@ void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t len
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
                 int exclude_last, const float* glob, hipStream_t s, ShardGlob sg) {
   if (B <= 0) return;
-  if (sg.gathered && (sg.world < 1 || sg.world > 64 || sg.rank < 0 || sg.rank >= sg.world))
+  if (sg.slots && (sg.world < 1 || sg.world > 64 || sg.rank < 0 || sg.rank >= sg.world))
     throw std::invalid_argument("per_sample: sharded world must be in [1, 64] with 0 <= rank < world");
   const int waves_per_block = 4;
   per_sample_k<<<(B + waves_per_block - 1) / waves_per_block, 64 * waves_per_block, 0, s>>>(
       t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob, sg);
+  LAUNCH_CHECK();
+}
+
+__global__ void pack_shard_slots_k(TreeDesc t, float* slots, int world, int rank) {
+  const int i = threadIdx.x;
+  if (i < 2 * world) {
+    float v = 0.f;
+    if (i == 2 * rank) v = (float)t.node_sum[t.levels - 1][0];
+    if (i == 2 * rank + 1) v = t.node_min[t.levels - 1][0];
+    slots[i] = v;
+  }
+}
+
+void pack_shard_slots(const TreeDesc& t, float* slots, int world, int rank, hipStream_t s) {
+  if (world < 1 || world > 64 || rank < 0 || rank >= world) throw std::invalid_argument("pack_shard_slots: bad world");
+  pack_shard_slots_k<<<1, 128, 0, s>>>(t, slots, world, rank);
   LAUNCH_CHECK();
 }
 

@@ -16,9 +16,13 @@ prioritized buffer holding all shards, each step exchanges two numbers per shard
   sampling over the union, with fixed per-rank batch shapes (graph-capturable).
 
 Priorities stay local (each shard updates the leaves it sampled), so no priority
-routing is needed.  ``exchange()`` is the eager collective (before the learner
-graph); ``finalize()`` is captured inside the learner graph and writes ``glob`` =
-(global pmin, weight scale) for the sampling kernel.
+routing is needed.  The exchange is a SUM all-reduce of fp32 slots [world][2] in which
+each rank fills only its own slot (an all-gather in all-reduce form): the data-parallel
+learner places the slots right before the conv gradients in one buffer, so the NEXT
+step's exchange rides the conv-gradient all-reduce of this step (no extra collective).
+The HBM replay packs its slot with one kernel from the tree root and the sampling
+kernel reads the slots directly (global pmin + shard weight scale in-kernel);
+``finalize()`` / ``glob`` is the generic (torch-op) form used by host replays.
 """
 from __future__ import annotations
 
@@ -27,15 +31,19 @@ import torch.distributed as dist
 
 
 class ShardedSampling:
-    def __init__(self, replay, group=None, force: bool = False):
+    def __init__(self, replay, group=None, force: bool = False, slots: torch.Tensor | None = None, comm=None):
+        """``slots``: fp32 [2*world] buffer to use (e.g. the learner's gradient-buffer
+        prefix); ``comm``: an all-reduce with ``start(t)``/``wait(w)`` (RCCL or torch);
+        default torch.distributed.  ``force``: collective even in a 1-rank group."""
         self.replay = replay
         self.group = group
-        self.force = force  # collective even in a 1-rank group (single-GPU measurement of the DP path)
+        self.force = force
+        self.comm = comm
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         dev = replay.device if hasattr(replay, "device") else torch.device("cpu")
-        self.local = torch.zeros(2, dtype=torch.float64, device=dev)
-        self.gathered = torch.zeros(self.world * 2, dtype=torch.float64, device=dev)
+        self.slots = slots if slots is not None else torch.zeros(2 * self.world, dtype=torch.float32, device=dev)
+        assert self.slots.dtype == torch.float32 and self.slots.numel() == 2 * self.world
         self.glob = torch.tensor([0.0, 1.0], dtype=torch.float32, device=dev)
 
     def _root(self):
@@ -43,43 +51,46 @@ class ShardedSampling:
 
     @property
     def in_kernel(self) -> bool:
-        """HBM replay: the tree kernels keep ``root_stats`` (the send buffer) current and
-        the sampler reads ``gathered`` itself -- no pack copies, no finalize ops."""
-        return hasattr(self.replay, "root_stats")
+        """HBM replay: one pack kernel, and the sampler reads the slots itself."""
+        return hasattr(self.replay, "pack_shard_slots")
 
     def sample_args(self) -> tuple:
-        return self.gathered, self.world, self.rank
+        return self.slots, self.world, self.rank
 
-    def exchange(self) -> None:
-        """Pack this shard's (mass, min priority) and all-gather them (eager: collectives
-        stay outside the captured graphs)."""
-        self.wait(self.start_exchange())
+    def pack(self) -> None:
+        """slots = 0 except this rank's (mass, min priority) -- on the current stream."""
+        if self.in_kernel:
+            self.replay.pack_shard_slots(self.slots, self.world, self.rank)
+            return
+        mass, pmin = self._root()
+        self.slots.zero_()
+        self.slots[2 * self.rank:2 * self.rank + 1].copy_(mass)
+        self.slots[2 * self.rank + 1:2 * self.rank + 2].copy_(pmin)
 
     def start_exchange(self):
-        """Asynchronous form: the pack runs on the current stream, the all-gather on the
-        process group's stream without making the current stream wait -- the engine
-        issues the NEXT step's exchange right after this step's backward (the tree is
-        final by then) so it overlaps the optimizer.  Returns the work handle."""
-        if self.in_kernel:
-            local = self.replay.root_stats
-        else:
-            mass, pmin = self._root()
-            self.local[0:1].copy_(mass)
-            self.local[1:2].copy_(pmin)
-            local = self.local
-        if self.world > 1 or self.force:
-            return dist.all_gather_into_tensor(self.gathered, local, group=self.group, async_op=True)
-        self.gathered.copy_(local)
-        return None
+        """Pack, then start the SUM all-reduce of the slots (the current stream does not
+        wait; ``wait(work)`` joins).  Returns the work handle (None: nothing to wait)."""
+        self.pack()
+        if self.world == 1 and not self.force:
+            return None
+        if self.comm is not None:
+            return self.comm.start(self.slots)
+        return dist.all_reduce(self.slots, group=self.group, async_op=True)
 
-    @staticmethod
-    def wait(work) -> None:
-        if work is not None:
+    def wait(self, work) -> None:
+        if work is None:
+            return
+        if self.comm is not None:
+            self.comm.wait(work)
+        else:
             work.wait()
 
+    def exchange(self) -> None:
+        self.wait(self.start_exchange())
+
     def finalize(self) -> None:
-        """Device-side: glob = (global pmin, k * M_r / sum M).  Graph-capturable."""
-        g = self.gathered.view(self.world, 2)
+        """Device-side torch ops: glob = (global pmin, k * M_r / sum M).  Graph-capturable."""
+        g = self.slots.view(self.world, 2).double()
         masses = g[:, 0]
         total = masses.sum().clamp_min(1e-300)
         self.glob[0:1].copy_(g[:, 1].min().reshape(1))

@@ -135,8 +135,14 @@ def main(argv=None) -> int:
 
         ecfg.actor_offset, ecfg.total_actors = rank * E, world * E
         ecfg.seed = cfg.seed + 7919 * rank
-        eng = ApexEngine(ecfg, device, allreduce=FlatGradAllReduce(world) if world > 1 else None,
-                         sharded=world > 1)
+        allreduce = None
+        if world > 1 and backend == "nccl":  # per-step gradients on a direct RCCL communicator
+            from .parallel.rccl import RcclGradAllReduce
+
+            allreduce = RcclGradAllReduce(device)
+        elif world > 1:
+            allreduce = FlatGradAllReduce(world)
+        eng = ApexEngine(ecfg, device, allreduce=allreduce, sharded=world > 1)
         learner = eng.learner
         if args.resume:
             counters = load_engine(learner, args.resume)

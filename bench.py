@@ -66,6 +66,8 @@ def parse():
                     help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="gloo: host-staged (tests)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal, gloo)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"],
+                    help="data-parallel gradient all-reduce: direct RCCL communicator (default) or torch.distributed")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (RCCL collectives, sharded sampling) even with 1 rank "
                          "(under torch.distributed.run --nproc-per-node 1): measures its single-GPU overhead")
@@ -117,7 +119,13 @@ def main():
                        use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
                        streams=args.streams, learner=lc)
     dp = world > 1 or args.force_dp
-    allreduce = FlatGradAllReduce(world, force=args.force_dp) if dp else None
+    allreduce = None
+    if dp and args.comm == "rccl" and args.backend == "nccl":
+        from apex_amd.parallel.rccl import RcclGradAllReduce
+
+        allreduce = RcclGradAllReduce(device, force=args.force_dp)
+    elif dp:
+        allreduce = FlatGradAllReduce(world, force=args.force_dp)
     sharded = dp and not args.local_sampling
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
@@ -181,6 +189,7 @@ def main():
                 "seq_len": 3,
                 "seq_len_meaning": "n-step return horizon (frame stack 4)",
                 "parallelism": f"dp{world}" + ("-forced" if args.force_dp and world == 1 else ""),
+                "dp_comm": (type(allreduce).__name__ if allreduce is not None else None),
                 "replay_sampling": "global PER over shards (mass all-gather)" if sharded else "per-shard PER",
                 "replay_capacity_per_gpu": args.capacity,
                 "envs_per_gpu": args.envs,
