@@ -123,8 +123,7 @@ class ActorShard:
         h.nstep_emit(self.nstep, self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                      self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
                      self.slot.data_ptr(), self.prio.data_ptr(), s)
-        self.replay.write_priorities(self.slot, self.prio, dedup=False,
-                                     bumps=((self.step_counter, 1), (self.replay.filled, E)))
+        self.replay.write_batch(pre=(self.slot, self.prio, self.replay.filled), bump=self.step_counter)
 
     def apply_staged(self, parity: int) -> None:
         """Scatter staging set ``parity`` into the replay tables and write its
@@ -138,8 +137,12 @@ class ActorShard:
                                    self._stream())
 
     def apply_prios(self, parity: int) -> None:
-        self.replay.write_priorities(self.stage_slot[parity], self.stage_prio[parity], dedup=False,
-                                     bumps=((self.replay.filled, self.E),))
+        self.replay.write_batch(pre=self.staged_prio_write(parity))
+
+    def staged_prio_write(self, parity: int) -> tuple:
+        """``HBMReplay.write_batch`` pre-write of staging set ``parity``: (slots, raw
+        priorities, ``replay.filled`` advanced by E)."""
+        return self.stage_slot[parity], self.stage_prio[parity], self.replay.filled
 
     def step(self, policy) -> None:
         """One full actor step with ``policy(obs_u8) -> Q f32 [E, A]``."""

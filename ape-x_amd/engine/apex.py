@@ -175,7 +175,7 @@ class ApexEngine:
             k = self.cfg.actor_steps_per_learner_step
             for i in range(k):
                 self.actor.apply_rows(apply_half * k + i)
-            self.learner.tree_hooks = [lambda i=i: self.actor.apply_prios(apply_half * k + i) for i in range(k)]
+            self.learner.pre_writes = [self.actor.staged_prio_write(apply_half * k + i) for i in range(k)]
         self.learner.forward_phase()
 
     def _learn_b(self):
@@ -327,11 +327,12 @@ class ApexEngine:
         h = self._half
         L = torch.cuda.current_stream(self.device)
         A = self._astream
-        A.wait_event(self._ev_learn)
-        with torch.cuda.stream(A):
-            self._g_actor[h].replay()
-        self._ev_actor[h].record(A)
-        L.wait_event(self._ev_actor[1 - h])
+        with trace.range("actor.launch"):
+            A.wait_event(self._ev_learn)
+            with torch.cuda.stream(A):
+                self._g_actor[h].replay()
+            self._ev_actor[h].record(A)
+            L.wait_event(self._ev_actor[1 - h])
         if self._dp:
             self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, self._g_learn_b.replay, True)
         else:

@@ -69,6 +69,11 @@ class HBMReplay:
         self.max_prio = torch.ones(1, dtype=torch.float32, device=dev)
         self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sorted_scratch = torch.zeros(1024, dtype=torch.int32, device=dev)
+        # batched-write scratch: per-slot dedup claims (all -1 between writes), the dirty
+        # slot list, the last-block ticket of the level kernels
+        self.owner = torch.full((C,), -1, dtype=torch.int32, device=dev)
+        self.wlist = torch.zeros(2048, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
                                        [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
                                        sizes)
@@ -104,6 +109,22 @@ class HBMReplay:
                                   self.max_prio.data_ptr(), int(dedup), self.sorted_scratch.data_ptr(), ptr(b[0][0]),
                                   int(b[0][1]), ptr(b[1][0]), int(b[1][1]), self._stream(),
                                   *((0, 0, 0, 0) if mix is None else tuple(ptr(t) for t in mix)))
+
+    def write_batch(self, pre: tuple | None = None, idx: torch.Tensor | None = None, prio: torch.Tensor | None = None,
+                    mix: tuple | None = None, bump: torch.Tensor | None = None) -> None:
+        """Fast batched tree update: ``pre`` = (slots int32 [E], raw priorities [E],
+        counter advanced by E) -- an actor step's unique ring slots -- written first; then
+        ``idx`` (int32 [B], duplicates last-write-wins) with ``prio`` or ``mix`` =
+        (delta, lw, prio_out, loss_out) as in :meth:`write_priorities`; ``bump`` advanced
+        by 1.  One leaves kernel + one wide kernel per big tree level."""
+        ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        E = 0 if pre is None else pre[0].numel()
+        B = 0 if idx is None else idx.numel()
+        m = (None, None, None, None) if mix is None else mix
+        self.hip.per_write_batch(self.tree, ptr(pre[0]) if pre else 0, ptr(pre[1]) if pre else 0, E,
+                                 ptr(pre[2]) if pre else 0, ptr(idx), ptr(prio), B, ptr(m[0]), ptr(m[1]), ptr(m[2]),
+                                 ptr(m[3]), ptr(bump), self.owner.data_ptr(), self.wlist.data_ptr(),
+                                 self.max_prio.data_ptr(), self.alpha, self.ticket.data_ptr(), self._stream())
 
     update_priorities = write_priorities
 

@@ -66,6 +66,26 @@ PYBIND11_MODULE(_apex_hip, m) {
     return h.d.levels;
   });
   m.def("make_tree", &make_tree);
+  m.def("per_write_batch", [](const TreeHandle& t, uint64_t pre_idx, uint64_t pre_prio, int E, uint64_t pre_bump,
+                              uint64_t idx, uint64_t prio, int B, uint64_t mix_delta, uint64_t mix_lw,
+                              uint64_t mix_prio_out, uint64_t mix_loss_out, uint64_t bump, uint64_t owner,
+                              uint64_t list, uint64_t max_prio, float alpha, uint64_t ticket, uint64_t s) {
+    BatchWrite w{};
+    w.pre_idx = P<const int>(pre_idx);
+    w.pre_prio = P<const float>(pre_prio);
+    w.E = E;
+    w.pre_bump = P<int64_t>(pre_bump);
+    w.idx = P<const int>(idx);
+    w.prio = P<const float>(prio);
+    w.B = B;
+    w.mix = PrioMix{P<const float>(mix_delta), P<const float>(mix_lw), P<float>(mix_prio_out), P<float>(mix_loss_out)};
+    w.bump = P<int64_t>(bump);
+    w.owner = P<int>(owner);
+    w.list = P<int>(list);
+    w.max_prio = P<float>(max_prio);
+    w.alpha = alpha;
+    per_write_batch(t.d, w, P<int>(ticket), S(s));
+  });
   m.def("pack_shard_slots", [](const TreeHandle& t, uint64_t slots, int world, int rank, uint64_t s) {
     pack_shard_slots(t.d, P<float>(slots), world, rank, S(s));
   });

@@ -31,6 +31,30 @@ struct ShardGlob {
   const float* slots;  // [world][2]
   int world, rank;
 };
+// Fast batched tree update (replay_kernels.hip: BatchWrite, per_write_batch): staged
+// actor rows + learner priorities in one leaves kernel + one wide kernel per big level.
+struct PrioMix {
+  const float* delta;  // [B] |y - Q(s,a)|
+  const float* lw;     // [B] w_i * Huber(delta_i)
+  float* prio_out;     // [B] mixed priorities (as dqn_loss writes them)
+  float* loss_out;     // [1]
+};
+struct BatchWrite {
+  const int* pre_idx;     // [E] actor slots (unique) or null
+  const float* pre_prio;  // [E] raw priorities
+  int E;
+  int64_t* pre_bump;      // e.g. replay.filled += E (or null)
+  const int* idx;         // [B] learner slots (may repeat) or null
+  const float* prio;      // [B] raw priorities (ignored with mix)
+  int B;
+  PrioMix mix;
+  int64_t* bump;          // e.g. learner step counter += 1 (or null)
+  int* owner;             // [capacity] scratch, all -1 between calls
+  int* list;              // [E + B] out: slots whose ancestors are dirty
+  float* max_prio;
+  float alpha;
+};
+void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStream_t s);
 // Zero `slots` [world][2] and write this shard's (root mass, root min priority) into
 // slot `rank`: after a SUM all-reduce every rank holds all shards' pairs (an all-gather
 // folded into the learner's conv-gradient all-reduce).

@@ -31,12 +31,7 @@ constexpr int kSortMax = 1024;
 // TD errors, prio_i = 0.9 max_j delta_j + 0.1 delta_i + 1e-6 (utils.py:77), and the loss
 // mean sum_i lw_i / B is written -- the batch-wide max/sum the row-parallel loss kernel
 // cannot do without another launch.  Reductions in the same fixed order as dqn_loss_k.
-struct PrioMix {
-  const float* delta;  // [B] |y - Q(s,a)|
-  const float* lw;     // [B] w_i * Huber(delta_i)
-  float* prio_out;     // [B] mixed priorities (as dqn_loss writes them)
-  float* loss_out;     // [1]
-};
+
 
 __device__ __forceinline__ float block_reduce_1024(float v, float* red, bool is_max) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
@@ -360,6 +355,144 @@ __global__ void gather_frames_k(const uint8_t* __restrict__ frames, int frame_by
 __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
   const int i = threadIdx.x;
   if (i < n) c[i] += by;
+}
+
+// ------------------------------------------------------------------ fast batched writes
+// The learner step's whole tree update -- the staged actor rows of the previous actor
+// step (E unique ring slots, their initial priorities) followed by this step's B sampled
+// slots (mixed priorities, duplicates last-write-wins) -- in three short launches:
+//   K1 (one workgroup): actor leaves; learner priority mix + loss mean; dedup by claiming
+//      owner[slot] with atomicMax over the batch position (the largest position wins,
+//      like the reference's sequential loop) instead of a bitonic sort; winner leaves;
+//      the claims are released by the winners; counters bumped; the slot list (actor
+//      then learner) written for the level kernels.
+//   K2 (wide, per big level): one wave per listed slot recomputes its ancestor at this
+//      level from the 64 children.  Several waves may recompute the same node: each
+//      reads the same (final) children and writes the same value -- deterministic.
+//   The last big level's kernel also finishes the small top levels (<= 64 nodes): the
+//      last block to arrive (ticket counter, fenced) recomputes them.
+// vs the single-workgroup level walk (per_write_ring_fused_k + per_write_leaves_sorted_k
+// + per_update_top_k, ~60 us of latency per step on MI355X) this is ~3 short kernels.
+
+
+// Writes one leaf; returns the priority to fold into the running max (0 if none).
+__device__ __forceinline__ float write_leaf(const TreeDesc& t, int id, float p, float alpha) {
+  if (p > 0.f && isfinite(p)) {
+    const float v = powf(p, alpha);
+    t.leaf_sum[id] = v;
+    t.leaf_min[id] = v;
+    return p;
+  }
+  t.leaf_sum[id] = 0.f;
+  t.leaf_min[id] = INFINITY;
+  return 0.f;
+}
+
+__global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrite w, int small_levels_in_block) {
+  __shared__ float red[16];
+  __shared__ int sids[2048];
+  const int k = threadIdx.x;
+  // the running max priority: one block-reduced atomic (per-leaf atomics on one address
+  // serialise at L2: ~40 us for 768 leaves)
+  float pmax = 0.f;
+  // actor rows first (they precede this step's learner priorities in time)
+  for (int i = k; i < w.E; i += blockDim.x) {
+    const int id = w.pre_idx[i];
+    sids[i] = id;
+    w.list[i] = id;
+    if (id >= 0 && id < t.size[0]) pmax = fmaxf(pmax, write_leaf(t, id, w.pre_prio[i], w.alpha));
+  }
+  float p = 0.f;
+  if (w.B > 0) {
+    if (w.mix.delta) {
+      const float dl = k < w.B ? w.mix.delta[k] : 0.f;
+      const float total = block_reduce_1024(k < w.B ? w.mix.lw[k] : 0.f, red, false);
+      const float dmax = block_reduce_1024(k < w.B ? dl : -INFINITY, red, true);
+      p = 0.9f * dmax + 0.1f * dl + 1e-6f;
+      if (k < w.B && w.mix.prio_out) w.mix.prio_out[k] = p;
+      if (k == 0 && w.mix.loss_out) w.mix.loss_out[0] = total / (float)w.B;
+    } else if (k < w.B) {
+      p = w.prio ? w.prio[k] : *w.max_prio;
+    }
+  }
+  __threadfence();
+  __syncthreads();  // actor leaves land before any learner leaf (last write wins)
+  const int id = k < w.B ? w.idx[k] : -1;
+  const bool ok = id >= 0 && id < t.size[0];
+  if (k < w.B) {
+    sids[w.E + k] = id;
+    w.list[w.E + k] = id;
+  }
+  if (ok) atomicMax(w.owner + id, k);
+  __threadfence();
+  __syncthreads();
+  if (ok && __hip_atomic_load(w.owner + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
+    const float wp = write_leaf(t, id, p, w.alpha);
+    if (w.mix.delta != nullptr || w.prio != nullptr) pmax = fmaxf(pmax, wp);
+    w.owner[id] = -1;  // release the claim (only the winner writes; losers never touch it again)
+  }
+  pmax = block_reduce_1024(pmax, red, true);
+  if (k == 0 && pmax > 0.f) atomic_max_pos_float(w.max_prio, pmax);
+  if (k == 0) {
+    if (w.pre_bump) *w.pre_bump += w.E;
+    if (w.bump) *w.bump += 1;
+  }
+  if (small_levels_in_block) {  // tiny trees: every level in this block
+    __threadfence();
+    __syncthreads();
+    update_levels_block(t, sids, w.E + w.B, 1, t.levels);
+  }
+}
+
+// One wave per listed slot: recompute its level-`level` ancestor.  With `top_from` > 0
+// the last block to finish also recomputes every node of levels top_from..levels.
+__global__ __launch_bounds__(256) void per_batch_level_k(TreeDesc t, const int* __restrict__ list, int n, int level,
+                                                         int top_from, int* ticket) {
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (i < n) {
+    const int id = list[i];
+    if (id >= 0 && id < t.size[0]) recompute_node(t, level, id >> (kTreeLog2Fanout * level), lane);
+  }
+  if (top_from <= 0) return;
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ticket, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int lv = top_from; lv <= t.levels; ++lv) {
+    for (int node = wave; node < t.size[lv]; node += nw) recompute_node(t, lv, node, lane);
+    __threadfence();
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *ticket = 0;
+}
+
+void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStream_t s) {
+  const int n = w.E + w.B;
+  if (n <= 0) return;
+  if (w.B > 1024 || w.E > 1024) throw std::invalid_argument("per_write_batch: E, B must be <= 1024");
+  if (w.B > 0 && !w.idx) throw std::invalid_argument("per_write_batch: learner slots missing");
+  if (w.E > 0 && (!w.pre_idx || !w.pre_prio)) throw std::invalid_argument("per_write_batch: actor rows missing");
+  if (w.mix.delta && !w.mix.lw) throw std::invalid_argument("per_write_batch: mixing needs lw");
+  // big levels (> 64 nodes) get a wide launch each; the rest go to the last one's
+  // last block, or -- when no level is big -- to the leaves kernel itself
+  int last_big = 0;
+  for (int lv = 1; lv <= t.levels; ++lv)
+    if (t.size[lv] > 64) last_big = lv;
+  per_batch_leaves_k<<<1, 1024, 0, s>>>(t, w, last_big == 0 ? 1 : 0);
+  LAUNCH_CHECK();
+  if (last_big == 0) return;
+  const int waves_per_block = 4;
+  const int grid = (n + waves_per_block - 1) / waves_per_block;
+  for (int lv = 1; lv <= last_big; ++lv) {
+    const int top = (lv == last_big && last_big < t.levels) ? last_big + 1 : 0;
+    per_batch_level_k<<<grid, 64 * waves_per_block, 0, s>>>(t, w.list, n, lv, top, ticket);
+    LAUNCH_CHECK();
+  }
 }
 
 // ------------------------------------------------------------------ launchers

@@ -55,6 +55,8 @@ def parse():
                     help="wgrad3/wgrad2 on a forked stream beside the dgrad chain (measured slower)")
     ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
                     help="priority-tree writes on the learner stream instead of a forked stream")
+    ap.add_argument("--tree-write", default="legacy", choices=["batch", "legacy"],
+                    help="learner priority-tree update: batched wide kernels or the single-workgroup walks")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--no-reserve", dest="reserve", action="store_false",
                     help="do not take the actor stream from the pool before the process group")
@@ -112,7 +114,7 @@ def main():
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork,
-                       bwd_fork=args.bwd_fork)
+                       bwd_fork=args.bwd_fork, tree_write=args.tree_write)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,

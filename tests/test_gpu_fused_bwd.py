@@ -103,3 +103,42 @@ def test_tree_write_priority_mix(cuda):
     assert torch.equal(rp1.max_prio, rp2.max_prio)
     assert math.isclose(loss.item(), lw.sum().item() / B, rel_tol=1e-5)
     torch.testing.assert_close(out_p, prio, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("C", [4096, 8192, 1 << 21])
+def test_batched_tree_write_equals_sequential_writes(cuda, C):
+    """write_batch (actor rows + mixed learner priorities, dedup by claims, wide level
+    kernels + last-block top levels) leaves the tree bit-identical to the old sequential
+    path (ring write, then the sorted dedup write), repeatedly (claims released)."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    B, E = 512, 256
+    g = torch.Generator(device=cuda).manual_seed(11)
+    rp1 = HBMReplay(C, E, 3, 0.6, cuda)
+    rp2 = HBMReplay(C, E, 3, 0.6, cuda)
+    c1, c2 = torch.zeros(1, dtype=torch.int64, device=cuda), torch.zeros(1, dtype=torch.int64, device=cuda)
+    for it in range(4):
+        base = (it * E) % C
+        slots = (torch.arange(E, device=cuda, dtype=torch.int32) + base) % C
+        aprio = torch.rand(E, device=cuda, generator=g) * 2 + 0.05
+        idx = torch.randint(0, C, (B,), device=cuda, generator=g, dtype=torch.int32)
+        idx[:E // 4] = slots[:E // 4]            # learner samples that the actor rows just wrote
+        idx[E // 4:E // 2] = idx[:E // 4]        # and duplicates
+        delta = torch.rand(B, device=cuda, generator=g) * 3
+        lw = torch.rand(B, device=cuda, generator=g)
+        p1, p2 = torch.zeros(B, device=cuda), torch.zeros(B, device=cuda)
+        l1, l2 = torch.zeros(1, device=cuda), torch.zeros(1, device=cuda)
+        rp1.write_priorities(slots, aprio, dedup=False, bumps=((rp1.filled, E),))
+        rp1.write_priorities(idx, None, dedup=True, bumps=((c1, 1),), mix=(delta, lw, p1, l1))
+        rp2.write_batch(pre=(slots, aprio, rp2.filled), idx=idx, bump=c2, mix=(delta, lw, p2, l2))
+        torch.cuda.synchronize()
+        assert torch.equal(rp1.leaf_sum, rp2.leaf_sum) and torch.equal(rp1.leaf_min, rp2.leaf_min), it
+        for a, b in zip(rp1.node_sum + rp1.node_min, rp2.node_sum + rp2.node_min):
+            assert torch.equal(a, b), it
+        assert torch.equal(rp1.max_prio, rp2.max_prio) and torch.equal(rp1.filled, rp2.filled)
+        assert torch.equal(c1, c2) and torch.equal(p1, p2) and torch.equal(l1, l2)
+    assert int((rp2.owner != -1).sum()) == 0 and int(rp2.ticket.item()) == 0
+    # the root equals a full recomputation from the leaves
+    full = rp2.leaf_sum.double().sum()
+    torch.testing.assert_close(rp2.node_sum[-1][0], full, rtol=1e-12, atol=0)
+    assert rp2.node_min[-1][0].item() == rp2.leaf_min.min().item()
