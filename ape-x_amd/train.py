@@ -139,8 +139,11 @@ def main(argv=None) -> int:
         if world > 1 and backend == "nccl":  # per-step gradients on a direct RCCL communicator
             from .parallel.rccl import RcclGradAllReduce
 
-            allreduce = RcclGradAllReduce(device)
-        elif world > 1:
+            try:
+                allreduce = RcclGradAllReduce(device)
+            except RuntimeError as e:
+                print(f"rank {rank}: direct RCCL unavailable ({e}); torch.distributed collectives", flush=True)
+        if world > 1 and allreduce is None:
             allreduce = FlatGradAllReduce(world)
         eng = ApexEngine(ecfg, device, allreduce=allreduce, sharded=world > 1)
         learner = eng.learner

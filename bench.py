@@ -125,8 +125,11 @@ def main():
     if dp and args.comm == "rccl" and args.backend == "nccl":
         from apex_amd.parallel.rccl import RcclGradAllReduce
 
-        allreduce = RcclGradAllReduce(device, force=args.force_dp)
-    elif dp:
+        try:
+            allreduce = RcclGradAllReduce(device, force=args.force_dp)
+        except RuntimeError as e:  # every rank fails alike (bootstrap/config): torch collectives instead
+            print(f"rank {rank}: direct RCCL communicator unavailable ({e}); using torch.distributed", file=sys.stderr)
+    if dp and allreduce is None:
         allreduce = FlatGradAllReduce(world, force=args.force_dp)
     sharded = dp and not args.local_sampling
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
