@@ -197,10 +197,13 @@ void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const ui
 // GRID batch slices x KSPLIT kidx-tile groups = workgroups (256: one per CU).  Splitting
 // the kidx tiles (instead of more batch slices) keeps the fp32 partial workspace
 // [GRID][N][K] -- and the reduce that reads it -- small.
-template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_, int KSPLIT_>
+template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_, int KSPLIT_, int DEPTH_ = 1>
 struct WG {
   static constexpr int H = H_, W = W_, C = C_, KH = KH_, KW = KW_, S = S_, N = N_, GRID = GRID_;
   static constexpr int KSPLIT = KSPLIT_;
+  // samples in flight in the register prefetch (2 measured slower on MI355X: the loop is
+  // bandwidth-, not latency-bound; see the XCD-aware mapping in wgrad_k)
+  static constexpr int DEPTH = DEPTH_;
   static constexpr int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1, P = OH * OW;
   static constexpr int K = KH * KW * C;
   static constexpr int KT = K / 32;            // 32-wide kidx tiles
@@ -372,7 +375,19 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
   const int colsel = 16 * (g & 1) + 4 * pp;  // column (within a 32-wide tile) this lane addresses
-  const int bg = blockIdx.x / G::KSPLIT, kg = blockIdx.x % G::KSPLIT;
+  // XCD-aware mapping: workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8), and
+  // the KSPLIT workgroups of one batch slice read the same samples -- give them blockIdx
+  // values 8 apart so they share one XCD's L2 (one HBM/MALL read per sample instead of
+  // KSPLIT).  Needs gridDim.x % (8 * KSPLIT) == 0, else the plain mapping.
+  int bg, kg;
+  if (gridDim.x % (8 * G::KSPLIT) == 0) {
+    const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
+    kg = r % G::KSPLIT;
+    bg = (r / G::KSPLIT) * 8 + xcd;
+  } else {
+    bg = blockIdx.x / G::KSPLIT;
+    kg = blockIdx.x % G::KSPLIT;
+  }
   const int kt0 = kg * G::KTB;
   const bool do_bias = kg == 0;  // block-uniform: one kidx group owns the bias gradient
   // zero the padded dy rows once (they stay zero)
@@ -397,38 +412,48 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
 #pragma unroll
       for (int t = 0; t < 2; ++t) ad.b[ks][t][k] = wg_boff<G>(ks, t, h, q4, colsel, ktc);
   }
-  // register prefetch: the next sample's x and dy loads are in flight during this
-  // sample's MFMA loop (one LDS buffer; committed after the compute)
+  // register prefetch, G::DEPTH samples deep: while sample b multiplies, the x and dy
+  // loads of the next DEPTH samples are in flight (one LDS buffer, committed at the top
+  // of each sample).  A sample's MFMA loop is far shorter than an HBM round trip, so with
+  // one sample in flight the loop waited on memory every iteration.
   constexpr int XCH = (G::C == 4) ? 0 : G::H * G::W * G::C / 8;
   constexpr int DCH = G::P * G::N / 8;
-  Pf8 px, pd, pm;
-  if (bg < B) wg_issue<G>(x, fs, dy, mask, bg, px, pd, pm);
-  for (int b = bg; b < B; b += gridb) {
-    __syncthreads();  // the previous sample's compute is done with LDS
-    if constexpr (G::C == 4) {
-      frames_store<G>(px, xs);
-    } else {
-      constexpr int CH16 = G::C / 8;
-      pf_store<XCH>(px, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
-    }
-    {
-      constexpr int CH16 = G::N / 8;
-      if (mask) pf_mask<DCH>(pd, pm);  // ReLU backward of the layer output, applied at staging
-      pf_store<DCH>(pd, dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
-    }
-    if (do_bias) wg_bias_acc<G>(pd, bs);
-    __syncthreads();
-    if (b + gridb < B) wg_issue<G>(x, fs, dy, mask, b + gridb, px, pd, pm);  // block-uniform
-    // fully unrolled pixel k-steps on precomputed fragment addresses, software pipelined:
-    // the fragments of ks + 1 are read while ks multiplies
-    WgFrags<G> cur;
-    wg_frags_pre<G>(xs, dys, 0, arow, colsel, ad, cur);
+  constexpr int D = G::DEPTH;
+  Pf8 px[D], pd[D], pm[D];
 #pragma unroll
-    for (int ks = 0; ks < G::KS; ++ks) {
-      WgFrags<G> nxt;
-      if (ks + 1 < G::KS) wg_frags_pre<G>(xs, dys, ks + 1, arow, colsel, ad, nxt);
-      wg_mfma<G>(cur, wave, kt0, acc);
-      if (ks + 1 < G::KS) cur = nxt;
+  for (int u = 0; u < D; ++u)
+    if (bg + u * gridb < B) wg_issue<G>(x, fs, dy, mask, bg + u * gridb, px[u], pd[u], pm[u]);
+  for (int b0 = bg; b0 < B; b0 += D * gridb) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int b = b0 + u * gridb;
+      if (b >= B) break;  // block-uniform
+      __syncthreads();  // the previous sample's compute is done with LDS
+      if constexpr (G::C == 4) {
+        frames_store<G>(px[u], xs);
+      } else {
+        constexpr int CH16 = G::C / 8;
+        pf_store<XCH>(px[u], xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
+      }
+      {
+        constexpr int CH16 = G::N / 8;
+        if (mask) pf_mask<DCH>(pd[u], pm[u]);  // ReLU backward of the layer output, applied at staging
+        pf_store<DCH>(pd[u], dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
+      }
+      if (do_bias) wg_bias_acc<G>(pd[u], bs);
+      __syncthreads();
+      if (b + D * gridb < B) wg_issue<G>(x, fs, dy, mask, b + D * gridb, px[u], pd[u], pm[u]);  // block-uniform
+      // fully unrolled pixel k-steps on precomputed fragment addresses, software pipelined:
+      // the fragments of ks + 1 are read while ks multiplies
+      WgFrags<G> cur;
+      wg_frags_pre<G>(xs, dys, 0, arow, colsel, ad, cur);
+#pragma unroll
+      for (int ks = 0; ks < G::KS; ++ks) {
+        WgFrags<G> nxt;
+        if (ks + 1 < G::KS) wg_frags_pre<G>(xs, dys, ks + 1, arow, colsel, ad, nxt);
+        wg_mfma<G>(cur, wave, kt0, acc);
+        if (ks + 1 < G::KS) cur = nxt;
+      }
     }
   }
   if (do_bias) {  // fixed-order combine of the per-thread bias sums (reuse the x tile region of LDS)
