@@ -139,6 +139,10 @@ class ActorShard:
     def apply_prios(self, parity: int) -> None:
         self.replay.write_batch(pre=self.staged_prio_write(parity))
 
+    def staged_rows(self, parity: int) -> tuple:
+        """``HBMReplay.sample_indices(rows=...)`` of staging set ``parity``."""
+        return self.stage_ptrs[parity], self.stage_slot[parity], self.stage_prio[parity]
+
     def staged_prio_write(self, parity: int) -> tuple:
         """``HBMReplay.write_batch`` pre-write of staging set ``parity``: (slots, raw
         priorities, ``replay.filled`` advanced by E)."""

@@ -173,8 +173,11 @@ class ApexEngine:
         learner step up to the optimizer)."""
         if apply_half is not None:
             k = self.cfg.actor_steps_per_learner_step
-            for i in range(k):
-                self.actor.apply_rows(apply_half * k + i)
+            if self.hip_net:  # rows scattered by the sampling launch itself
+                self.learner.pre_rows = [self.actor.staged_rows(apply_half * k + i) for i in range(k)]
+            else:
+                for i in range(k):
+                    self.actor.apply_rows(apply_half * k + i)
             self.learner.pre_writes = [self.actor.staged_prio_write(apply_half * k + i) for i in range(k)]
         self.learner.forward_phase()
 

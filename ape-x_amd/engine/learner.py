@@ -164,6 +164,9 @@ class DQNLearner:
         # staged actor rows whose priorities go into this step's batched tree write:
         # (slots, raw priorities, counter advanced by the row count)
         self.pre_writes = []
+        # staged actor rows scattered into the tables by the sampling launch:
+        # (staged table ptr dict, slots, raw priorities)
+        self.pre_rows = []
 
     @staticmethod
     def _stream() -> int:
@@ -208,7 +211,12 @@ class DQNLearner:
             else:
                 self.sharded.finalize()
                 glob = self.sharded.glob
-        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard)
+        rows, self.pre_rows = self.pre_rows, []
+        for extra in rows[:-1]:  # more than one staged actor step per learner step
+            self.hip.apply_staged_rows(extra[0], self.replay.trans_ptrs(), extra[1].data_ptr(), extra[2].data_ptr(),
+                                       extra[1].numel(), s)
+        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
+                                   rows=rows[-1] if rows else None)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.

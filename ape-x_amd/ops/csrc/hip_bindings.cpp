@@ -104,13 +104,27 @@ PYBIND11_MODULE(_apex_hip, m) {
      py::arg("mix_loss_out") = 0);
   m.def("per_sample", [](const TreeHandle& t, int B, uint64_t length_ptr, int64_t length, uint64_t beta_ptr,
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
-                         int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank) {
+                         int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank,
+                         py::object rows_stage, py::object rows_dst, uint64_t rows_slot, uint64_t rows_prio,
+                         int rows_E) {
+    StagedRows rows{};
+    if (rows_E > 0) {
+      auto tab = [](py::dict d) {
+        auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+        return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
+                          P<float>(g("done"))};
+      };
+      rows = StagedRows{tab(rows_stage.cast<py::dict>()), tab(rows_dst.cast<py::dict>()), P<const int>(rows_slot),
+                        P<const float>(rows_prio), rows_E};
+    }
     per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
                P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s),
-               ShardGlob{P<const float>(gathered), world, rank});
+               ShardGlob{P<const float>(gathered), world, rank}, rows_E > 0 ? &rows : nullptr);
   }, py::arg("t"), py::arg("B"), py::arg("length_ptr"), py::arg("length"), py::arg("beta_ptr"), py::arg("beta"),
      py::arg("seed"), py::arg("counter"), py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"),
-     py::arg("s"), py::arg("glob") = 0, py::arg("slots") = 0, py::arg("world") = 0, py::arg("rank") = 0);
+     py::arg("s"), py::arg("glob") = 0, py::arg("slots") = 0, py::arg("world") = 0, py::arg("rank") = 0,
+     py::arg("rows_stage") = py::none(), py::arg("rows_dst") = py::none(), py::arg("rows_slot") = 0,
+     py::arg("rows_prio") = 0, py::arg("rows_E") = 0);
   m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
                                  uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {

@@ -78,7 +78,8 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 // weights, glob[1] = this shard's weight scale (apex_amd.parallel.sharded).
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg = ShardGlob{nullptr, 0, 0});
+                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg = ShardGlob{nullptr, 0, 0},
+                const struct StagedRows* rows = nullptr);
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
                         uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s);
@@ -134,7 +135,15 @@ struct TransTable {
 void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float* q, const int* actions,
                 const float* reward, const float* done, const int* new_frame, const int64_t* step_counter,
                 int* slot_out, float* prio_out, hipStream_t s);
-// staged actor rows [E] -> replay tables at slot[e] (emitted rows only: prio[e] > 0)
+// staged actor rows [E] -> replay tables at slot[e] (emitted rows only: prio[e] > 0);
+// also fused into per_sample's launch (extra blocks: the scatter writes table rows the
+// sampler never reads, and both must precede the learner's forward)
+struct StagedRows {
+  TransTable st, dst;
+  const int* slot;
+  const float* prio;
+  int E;
+};
 void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s);
 
 // ---- conv_bwd_kernels.hip: one launch for all batch-sliced gradient reductions

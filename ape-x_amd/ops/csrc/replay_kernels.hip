@@ -266,7 +266,18 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
                              const float* beta_ptr, float beta_const, uint64_t seed,
                              const int64_t* __restrict__ counter, int* __restrict__ out_idx,
                              float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob,
-                             ShardGlob sg) {
+                             ShardGlob sg, StagedRows rows, int sample_blocks) {
+  if ((int)blockIdx.x >= sample_blocks) {  // fused staged-row scatter (apply_staged_rows)
+    const int e = (blockIdx.x - sample_blocks) * blockDim.x + threadIdx.x;
+    if (e >= rows.E || !(rows.prio[e] > 0.f)) return;
+    const int j = rows.slot[e];
+    reinterpret_cast<int4*>(rows.dst.s_ids)[j] = reinterpret_cast<const int4*>(rows.st.s_ids)[e];
+    reinterpret_cast<int4*>(rows.dst.s2_ids)[j] = reinterpret_cast<const int4*>(rows.st.s2_ids)[e];
+    rows.dst.action[j] = rows.st.action[e];
+    rows.dst.reward[j] = rows.st.reward[e];
+    rows.dst.done[j] = rows.st.done[e];
+    return;
+  }
   const int lane = threadIdx.x & 63;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (i >= B) return;
@@ -540,13 +551,17 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) 
 
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg) {
+                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg, const StagedRows* rows) {
   if (B <= 0) return;
   if (sg.slots && (sg.world < 1 || sg.world > 64 || sg.rank < 0 || sg.rank >= sg.world))
     throw std::invalid_argument("per_sample: sharded world must be in [1, 64] with 0 <= rank < world");
   const int waves_per_block = 4;
-  per_sample_k<<<(B + waves_per_block - 1) / waves_per_block, 64 * waves_per_block, 0, s>>>(
-      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob, sg);
+  const int sblocks = (B + waves_per_block - 1) / waves_per_block;
+  const StagedRows r = rows ? *rows : StagedRows{};
+  const int rblocks = r.E > 0 ? (r.E + 64 * waves_per_block - 1) / (64 * waves_per_block) : 0;
+  per_sample_k<<<sblocks + rblocks, 64 * waves_per_block, 0, s>>>(
+      t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob, sg, r,
+      sblocks);
   LAUNCH_CHECK();
 }
 
