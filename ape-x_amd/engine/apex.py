@@ -68,6 +68,10 @@ class EngineConfig:
     #   "priority-actor" / "priority-learner": a high-priority stream (measured slower in
     #                the single-process step: preemption of the other queue's waves)
     streams: str = "none"
+    # data-parallel overlap mode: capture the whole learner step INCLUDING the two RCCL
+    # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
+    # staging half, instead of three phase graphs with eager collectives in between
+    dp_graph: bool = False
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
 
@@ -124,7 +128,7 @@ class ApexEngine:
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
-        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = None
+        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = None
         self._pool = None
         self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
         self._captured = False
@@ -294,6 +298,18 @@ class ApexEngine:
         self._pool = torch.cuda.graph_pool_handle()
         apool = torch.cuda.graph_pool_handle()  # actor graphs run concurrently: never share memory
         self._g_actor, self._g_learn_a, self._g_learn_a2 = [], [], []
+        self._g_dp = None
+        if self._dp and self.cfg.dp_graph and self._mass_pending_ok():
+            # the whole data-parallel learner step -- both gradient all-reduces included
+            # (RCCL kernels on the comm stream's branch of the graph) -- as ONE graph per half
+            self._g_dp = []
+            for h in (0, 1):
+                self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+                self._g_dp.append(self._graph(lambda h=h: self._dp_step_body(1 - h), self._pool))
+            self._captured = True
+            torch.cuda.synchronize(self.device)
+            self._ev_learn.record(torch.cuda.current_stream(self.device))
+            return
         for h in (0, 1):
             self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
             if self._dp:
@@ -305,6 +321,22 @@ class ApexEngine:
         self._captured = True
         torch.cuda.synchronize(self.device)
         self._ev_learn.record(torch.cuda.current_stream(self.device))
+
+    def _mass_pending_ok(self) -> bool:
+        """One-graph DP step: the shard masses must always arrive with the previous step's
+        conv-gradient all-reduce (overlap mode, slots in the gradient prefix)."""
+        return self._sharded is None or (self.overlap and self.learner.grad_prefix > 0)
+
+    def _dp_step_body(self, apply_half: int) -> None:
+        """Captured body of the one-graph DP step (EngineConfig.dp_graph)."""
+        ar = self._allreduce
+        self._learn_a(apply_half)
+        fc, conv = self.learner.grad_slices()
+        w1 = ar.start(fc)
+        self.learner.backward_phase()
+        w2 = ar.start(conv)
+        ar.wait(w1, w2)
+        self._learn_b()
 
     def _learner_eager(self, apply_half: int | None = None) -> None:
         if self._dp:
@@ -336,7 +368,13 @@ class ApexEngine:
                 self._g_actor[h].replay()
             self._ev_actor[h].record(A)
             L.wait_event(self._ev_actor[1 - h])
-        if self._dp:
+        if self._g_dp is not None:
+            if self._sharded is not None and not self._mass_pending:  # e.g. after fill(): re-exchange
+                self._sharded.exchange()
+            with trace.range("apex.learner"):
+                self._g_dp[h].replay()
+            self._mass_pending = self._sharded is not None  # the graph's conv all-reduce carried them
+        elif self._dp:
             self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, self._g_learn_b.replay, True)
         else:
             self._learn(self._g_learn_a[h].replay, None, None, False)

@@ -145,6 +145,10 @@ def main(argv=None) -> int:
                 print(f"rank {rank}: direct RCCL unavailable ({e}); torch.distributed collectives", flush=True)
         if world > 1 and allreduce is None:
             allreduce = FlatGradAllReduce(world)
+        from .parallel.rccl import RcclGradAllReduce
+
+        ecfg.overlap = True
+        ecfg.dp_graph = isinstance(allreduce, RcclGradAllReduce)  # all-reduces captured in the learner graph
         eng = ApexEngine(ecfg, device, allreduce=allreduce, sharded=world > 1)
         learner = eng.learner
         if args.resume:

@@ -73,3 +73,23 @@ def test_dp_engine_rccl_equals_no_collectives(pg):
     assert torch.equal(eng_r.replay.leaf_sum, eng_n.replay.leaf_sum)
     sl = eng_r._sharded.slots
     assert sl.numel() == 2 and float(sl[0]) > 0 and float(sl[1]) > 0  # (mass, min priority) exchanged
+
+
+def test_dp_one_graph_with_captured_rccl_equals_phase_graphs(pg):
+    """EngineConfig.dp_graph: the learner step with both RCCL all-reduces captured inside
+    one hipGraph replays bit-identically to the three phase graphs with eager RCCL."""
+    from apex_amd.parallel.rccl import RcclGradAllReduce
+
+    eng_p = _engine(pg, RcclGradAllReduce(pg, force=True), True)
+    eng_g = _engine(pg, RcclGradAllReduce(pg, force=True), True)
+    eng_g.cfg.dp_graph = True
+    for eng in (eng_p, eng_g):
+        eng.fill()
+        eng.capture()
+    assert eng_g._g_dp is not None and eng_p._g_dp is None
+    for _ in range(20):
+        eng_p.train_step()
+        eng_g.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(eng_g.learner.flat, eng_p.learner.flat)
+    assert torch.equal(eng_g.replay.leaf_sum, eng_p.replay.leaf_sum)
