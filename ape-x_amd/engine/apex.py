@@ -302,14 +302,23 @@ class ApexEngine:
         if self._dp and self.cfg.dp_graph and self._mass_pending_ok():
             # the whole data-parallel learner step -- both gradient all-reduces included
             # (RCCL kernels on the comm stream's branch of the graph) -- as ONE graph per half
-            self._g_dp = []
-            for h in (0, 1):
-                self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
-                self._g_dp.append(self._graph(lambda h=h: self._dp_step_body(1 - h), self._pool))
-            self._captured = True
-            torch.cuda.synchronize(self.device)
-            self._ev_learn.record(torch.cuda.current_stream(self.device))
-            return
+            try:
+                g_actor, g_dp = [], []
+                for h in (0, 1):
+                    g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+                    g_dp.append(self._graph(lambda h=h: self._dp_step_body(1 - h), self._pool))
+                self._g_actor, self._g_dp = g_actor, g_dp
+                self._captured = True
+                torch.cuda.synchronize(self.device)
+                self._ev_learn.record(torch.cuda.current_stream(self.device))
+                return
+            except RuntimeError as e:  # RCCL capture unsupported here: the phase graphs instead
+                import warnings
+
+                warnings.warn(f"capturing the RCCL all-reduces failed ({e}); using three phase graphs")
+                self._g_dp = None
+                torch.cuda.synchronize(self.device)
+                apool = torch.cuda.graph_pool_handle()
         for h in (0, 1):
             self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
             if self._dp:
