@@ -48,7 +48,7 @@ using Conv1 = ConvGeo<84, 84, 4, 8, 8, 4, 32>;
 using Conv2 = ConvGeo<20, 20, 32, 4, 4, 2, 64>;
 using Conv3 = ConvGeo<9, 9, 64, 3, 3, 1, 64>;
 static_assert(Conv1::P == 400 && Conv2::P == 81 && Conv3::P == 49, "Nature-CNN geometry");
-static_assert(Conv2::LDS + 4 * TILE_EP_BYTES <= 160 * 1024 && Conv3::LDS + 4 * TILE_EP_BYTES <= 160 * 1024, "LDS");
+static_assert(Conv2::LDS + 8 * TILE_EP_BYTES <= 160 * 1024 && Conv3::LDS + 8 * TILE_EP_BYTES <= 160 * 1024, "LDS");
 
 // Stage one sample's input into LDS as padded NHWC bf16 (blockDim must be 256).
 template <class G, bool U8IN>
@@ -91,11 +91,18 @@ __device__ __forceinline__ constexpr int a_off(int kk) {
 // Problem set (kernels.h ConvSet): sample pairs never straddle two problems (a problem of
 // B samples has ceil(B/2) pairs); the weights are restaged only when the problem's weight
 // pointer changes (the learner's Q(s) and Q(s') passes share the online weights).
+// Eight waves per workgroup: the LDS footprint (two samples + the weights) allows one
+// workgroup per CU, and with four waves each SIMD had a single wave to hide every LDS and
+// MFMA latency; waves 4-7 share the staged tiles (waves 0-3 stage: the copy helpers are
+// written for 256 threads).
+constexpr int kConvWaves = 8;
+
 template <class G, bool U8IN>
-__global__ __launch_bounds__(256) void conv_fwd_k(ConvSet set) {
-  __shared__ __attribute__((aligned(16))) char smem[G::LDS + 4 * TILE_EP_BYTES];
+__global__ __launch_bounds__(64 * kConvWaves) void conv_fwd_k(ConvSet set) {
+  __shared__ __attribute__((aligned(16))) char smem[G::LDS + kConvWaves * TILE_EP_BYTES];
   char* ws = smem + G::SPW * G::X_BYTES;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  const bool stager = threadIdx.x < 256;  // wave-uniform
   char* ep = smem + G::LDS + wave * TILE_EP_BYTES;  // per-wave epilogue scratch
   const int B = set.B, PP = (B + G::SPW - 1) / G::SPW, pairs = set.n * PP;
   const uint16_t* wcur = nullptr;
@@ -117,7 +124,7 @@ __global__ __launch_bounds__(256) void conv_fwd_k(ConvSet set) {
   };
   if constexpr (!U8IN) {
     static_assert(XCH <= 8 * 256, "one Pf8 per sample");
-    if ((int)blockIdx.x < pairs) issue(blockIdx.x);
+    if (stager && (int)blockIdx.x < pairs) issue(blockIdx.x);
   }
   for (int q = blockIdx.x; q < pairs; q += gridDim.x) {
     const int pb = q / PP, b0 = (q - pb * PP) * G::SPW;
@@ -126,28 +133,30 @@ __global__ __launch_bounds__(256) void conv_fwd_k(ConvSet set) {
     __syncthreads();
     if (pr.w != wcur) {  // block-uniform
       wcur = pr.w;
-      stage_weights<G>(wcur, ws);
+      if (stager) stage_weights<G>(wcur, ws);
     }
-    if constexpr (U8IN) {
+    if (stager) {
+      if constexpr (U8IN) {
 #pragma unroll
-      for (int sw = 0; sw < G::SPW; ++sw)
-        if (b0 + sw < B) stage_input<G, U8IN>(pr.in, fs, b0 + sw, smem + sw * G::X_BYTES);
-    } else {
-      auto off = [](int c) {
-        const int pi = c / CH16;
-        return (pi / G::W) * G::ROW + (pi % G::W) * G::PIX + (c % CH16) * 16;
-      };
-      pf_store<XCH>(nx0, smem, off);
-      if (b0 + 1 < B) pf_store<XCH>(nx1, smem + G::X_BYTES, off);
+        for (int sw = 0; sw < G::SPW; ++sw)
+          if (b0 + sw < B) stage_input<G, U8IN>(pr.in, fs, b0 + sw, smem + sw * G::X_BYTES);
+      } else {
+        auto off = [](int c) {
+          const int pi = c / CH16;
+          return (pi / G::W) * G::ROW + (pi % G::W) * G::PIX + (c % CH16) * 16;
+        };
+        pf_store<XCH>(nx0, smem, off);
+        if (b0 + 1 < B) pf_store<XCH>(nx1, smem + G::X_BYTES, off);
+      }
     }
     __syncthreads();
     if constexpr (!U8IN) {
-      if (q + (int)gridDim.x < pairs) issue(q + gridDim.x);  // block-uniform
+      if (stager && q + (int)gridDim.x < pairs) issue(q + gridDim.x);
     }
     const float* bias = pr.bias;
     uint16_t* out = pr.out;
     constexpr int ITEMS = G::SPW * G::MT * G::NT;
-    for (int it = wave; it < ITEMS; it += 4) {
+    for (int it = wave; it < ITEMS; it += kConvWaves) {
       const int sw = it / (G::MT * G::NT);
       const int mt = (it / G::NT) % G::MT;
       const int nt = it % G::NT;
@@ -185,7 +194,7 @@ static void launch_conv_fwd(const ConvSet& set, hipStream_t s) {
   if (pairs <= 0) return;
   // one workgroup per CU (the LDS footprint allows no more): 256 persistent workgroups
   const int grid = std::min(pairs, 256);
-  conv_fwd_k<G, U8IN><<<grid, 256, 0, s>>>(set);
+  conv_fwd_k<G, U8IN><<<grid, 64 * kConvWaves, 0, s>>>(set);
   LAUNCH_CHECK();
 }
 
