@@ -79,26 +79,32 @@ __device__ __forceinline__ void stage_wt(const uint16_t* __restrict__ wt, char* 
 
 // conv3 dgrad: dy3 [B][49][64] (already ReLU-masked) -> dx2 [B][81][64]; with out_mask
 // (= a2) the ReLU backward is applied in the coalesced epilogue (writes dy2)
-__global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ mask3,
+// dgrad kernels: 8 waves per workgroup (2 per SIMD at one LDS-limited workgroup per CU);
+// waves 0-3 stage (the copy helpers are written for 256 threads)
+constexpr int kDgWaves = 8;
+
+__global__ __launch_bounds__(64 * kDgWaves) void dgrad3_k(const uint16_t* __restrict__ dy3, const uint16_t* __restrict__ mask3,
                                                 const uint16_t* __restrict__ wt3, uint16_t* __restrict__ dx2,
                                                 const uint16_t* __restrict__ out_mask, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 7x7 grid + 2-pixel border
   constexpr int SPW = 2;
-  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX + 4 * TILE_EP_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 9 * 64 * DY_PIX + kDgWaves * TILE_EP_BYTES];
   char* wts = smem + SPW * TILE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  const bool stager = threadIdx.x < 256;  // wave-uniform
   char* ep = wts + 9 * 64 * DY_PIX + wave * TILE_EP_BYTES;
   zero_lds<SPW * T * T>(smem);
-  stage_wt<9, 64>(wt3, wts);
+  if (stager) stage_wt<9, 64>(wt3, wts);
   for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
     __syncthreads();
-    for (int sw = 0; sw < SPW; ++sw)
-      if (b0 + sw < B)
-        stage_dy_padded<7, 7, T, T, 2>(dy3 + (size_t)(b0 + sw) * 49 * 64,
-                                       mask3 ? mask3 + (size_t)(b0 + sw) * 49 * 64 : nullptr, smem + sw * TILE);
+    if (stager)
+      for (int sw = 0; sw < SPW; ++sw)
+        if (b0 + sw < B)
+          stage_dy_padded<7, 7, T, T, 2>(dy3 + (size_t)(b0 + sw) * 49 * 64,
+                                         mask3 ? mask3 + (size_t)(b0 + sw) * 49 * 64 : nullptr, smem + sw * TILE);
     __syncthreads();
     // items: (sample, m-tile of 32 input pixels (3), n-tile of 32 channels (2)) = 12
-    for (int it = wave; it < SPW * 6; it += 4) {
+    for (int it = wave; it < SPW * 6; it += kDgWaves) {
       const int sw = it / 6, mt = (it / 2) % 3, nt = it % 2;
       const int b = b0 + sw;
       if (b >= B) continue;
@@ -128,26 +134,28 @@ __global__ __launch_bounds__(256) void dgrad3_k(const uint16_t* __restrict__ dy3
 
 // conv2 dgrad (sub-pixel): dy2 (optionally masked while staging) -> dx1 [B][400][32];
 // with out_mask (= a1) the ReLU backward is applied in the coalesced epilogue (writes dy1)
-__global__ __launch_bounds__(256) void dgrad2_k(const uint16_t* __restrict__ dx2, const uint16_t* __restrict__ mask2,
+__global__ __launch_bounds__(64 * kDgWaves) void dgrad2_k(const uint16_t* __restrict__ dx2, const uint16_t* __restrict__ mask2,
                                                 const uint16_t* __restrict__ wt2, uint16_t* __restrict__ dx1,
                                                 const uint16_t* __restrict__ out_mask, int B) {
   constexpr int T = 11, TILE = T * T * DY_PIX;     // 9x9 grid + 1-pixel border
   constexpr int SPW = 2;
-  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX + 4 * TILE_EP_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[SPW * TILE + 16 * 32 * DY_PIX + kDgWaves * TILE_EP_BYTES];
   char* wts = smem + SPW * TILE;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5, r32 = lane & 31;
+  const bool stager = threadIdx.x < 256;  // wave-uniform
   char* ep = wts + 16 * 32 * DY_PIX + wave * TILE_EP_BYTES;
   zero_lds<SPW * T * T>(smem);
-  stage_wt<16, 32>(wt2, wts);
+  if (stager) stage_wt<16, 32>(wt2, wts);
   for (int b0 = blockIdx.x * SPW; b0 < B; b0 += gridDim.x * SPW) {
     __syncthreads();
-    for (int sw = 0; sw < SPW; ++sw)
-      if (b0 + sw < B)
-        stage_dy_padded<9, 9, T, T, 1>(dx2 + (size_t)(b0 + sw) * 81 * 64,
-                                       mask2 ? mask2 + (size_t)(b0 + sw) * 81 * 64 : nullptr, smem + sw * TILE);
+    if (stager)
+      for (int sw = 0; sw < SPW; ++sw)
+        if (b0 + sw < B)
+          stage_dy_padded<9, 9, T, T, 1>(dx2 + (size_t)(b0 + sw) * 81 * 64,
+                                         mask2 ? mask2 + (size_t)(b0 + sw) * 81 * 64 : nullptr, smem + sw * TILE);
     __syncthreads();
     // items: (sample, parity class (4), m-tile of 32 class pixels (4 -> 128 >= 100)) = 32
-    for (int it = wave; it < SPW * 16; it += 4) {
+    for (int it = wave; it < SPW * 16; it += kDgWaves) {
       const int sw = it / 16, cls = (it / 4) % 4, mt = it % 4;
       const int b = b0 + sw;
       if (b >= B) continue;
@@ -184,9 +192,9 @@ void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const ui
   if (B <= 0) return;
   const int grid = std::min((B + 1) / 2, 512);
   if (layer == 3) {
-    dgrad3_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
+    dgrad3_k<<<grid, 64 * kDgWaves, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
   } else if (layer == 2) {
-    dgrad2_k<<<grid, 256, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
+    dgrad2_k<<<grid, 64 * kDgWaves, 0, s>>>(dy, dy_mask, wt, dx, dx_mask, B);
   } else {
     throw std::invalid_argument("conv_dgrad: layer must be 2 or 3");
   }
