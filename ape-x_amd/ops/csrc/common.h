@@ -236,7 +236,7 @@ template <int TOTAL, int BASE = 0>
 __device__ __forceinline__ void pf_load(Pf8& p, const uint4* __restrict__ src4) {
   static_assert(TOTAL <= 32 * 256, "at most 4 Pf8 blocks per copy");
   const u32v4* src = reinterpret_cast<const u32v4*>(src4);
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 255;  /* local to a 256-thread staging group */
 #define APEX_PF_LD(K, R) \
   if constexpr ((BASE + K) * 256 < TOTAL) p.R = src[min(t + (BASE + K) * 256, TOTAL - 1)];  /* always assigned */
   APEX_PF_SLOTS(APEX_PF_LD)
@@ -245,7 +245,7 @@ __device__ __forceinline__ void pf_load(Pf8& p, const uint4* __restrict__ src4) 
 
 template <int TOTAL, int BASE = 0, class DstOff>
 __device__ __forceinline__ void pf_store(const Pf8& p, char* dst, DstOff dst_off) {
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 255;  /* local to a 256-thread staging group */
 #define APEX_PF_ST(K, R) \
   if constexpr ((BASE + K) * 256 < TOTAL) {                                     \
     const int q = t + (BASE + K) * 256;                                         \

@@ -205,13 +205,16 @@ void conv_dgrad(int layer, const uint16_t* dy, const uint16_t* dy_mask, const ui
 // GRID batch slices x KSPLIT kidx-tile groups = workgroups (256: one per CU).  Splitting
 // the kidx tiles (instead of more batch slices) keeps the fp32 partial workspace
 // [GRID][N][K] -- and the reduce that reads it -- small.
-template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_, int KSPLIT_, int DEPTH_ = 1>
+template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_, int GRID_, int KSPLIT_, int GROUPS_ = 1,
+          bool XCD_ = true>
 struct WG {
+  static constexpr bool XCD = XCD_;  // XCD-aware blockIdx mapping (see wgrad_k)
   static constexpr int H = H_, W = W_, C = C_, KH = KH_, KW = KW_, S = S_, N = N_, GRID = GRID_;
   static constexpr int KSPLIT = KSPLIT_;
-  // samples in flight in the register prefetch (2 measured slower on MI355X: the loop is
-  // bandwidth-, not latency-bound; see the XCD-aware mapping in wgrad_k)
-  static constexpr int DEPTH = DEPTH_;
+  // sample groups per workgroup: each group of 4 waves stages and multiplies its own
+  // sample (2 groups = 8 waves = 2 per SIMD at the LDS-limited one workgroup per CU), the
+  // groups' accumulators are summed before the one partial write (same workspace size)
+  static constexpr int GROUPS = GROUPS_;
   static constexpr int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1, P = OH * OW;
   static constexpr int K = KH * KW * C;
   static constexpr int KT = K / 32;            // 32-wide kidx tiles
@@ -227,9 +230,9 @@ struct WG {
   static constexpr int KTB = (KT + KSPLIT - 1) / KSPLIT;  // kidx tiles per workgroup
   static constexpr int KTW = (KTB + 3) / 4;               // kidx tiles per wave
 };
-using WG1 = WG<84, 84, 4, 8, 8, 4, 32, 128, 2>;
-using WG2 = WG<20, 20, 32, 4, 4, 2, 64, 64, 4>;
-using WG3 = WG<9, 9, 64, 3, 3, 1, 64, 64, 4>;
+using WG1 = WG<84, 84, 4, 8, 8, 4, 32, 128, 2, 1>;  // 95 KB of LDS per sample: one group
+using WG2 = WG<20, 20, 32, 4, 4, 2, 64, 64, 4, 2>;
+using WG3 = WG<9, 9, 64, 3, 3, 1, 64, 64, 4, 1, false>;
 
 // LDS byte address of input pixel `pix` in the wgrad x tile
 template <class G>
@@ -248,7 +251,7 @@ __device__ __forceinline__ void frames_load(const FrameSrc& f, int b, Pf8& p) {
   const uint4* p1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, HW));
   const uint4* p2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, HW));
   const uint4* p3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, HW));
-  const int g0 = threadIdx.x, g1 = threadIdx.x + 256;
+  const int g0 = threadIdx.x & 255, g1 = g0 + 256;
   auto ld = [](const uint4* q, int i) { return reinterpret_cast<const u32v4*>(q)[i]; };
   p.r0 = ld(p0, g0); p.r1 = ld(p1, g0); p.r2 = ld(p2, g0); p.r3 = ld(p3, g0);
   const int g1c = g1 < GROUPS ? g1 : GROUPS - 1;  // always assigned (stores are guarded)
@@ -258,7 +261,7 @@ __device__ __forceinline__ void frames_load(const FrameSrc& f, int b, Pf8& p) {
 template <class G>
 __device__ __forceinline__ void frames_store(const Pf8& p, char* xs) {
   constexpr int GROUPS = G::H * G::W / 16;
-  const int g0 = threadIdx.x, g1 = threadIdx.x + 256;
+  const int g0 = threadIdx.x & 255, g1 = g0 + 256;
   uint4* d = reinterpret_cast<uint4*>(xs + g0 * 144);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -357,7 +360,7 @@ __device__ __forceinline__ void wg_mfma(const WgFrags<G>& f, int, int, f32x16 (&
 template <class G>
 __device__ __forceinline__ void wg_bias_acc(const Pf8& pd, float (&bs)[8]) {
   constexpr int DCH = G::P * G::N / 8;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 255;  // local to the sample group
 #define APEX_WG_BIAS(K, R)                                     \
   if constexpr (K * 256 < DCH) {                               \
     if (t + K * 256 < DCH) {                                   \
@@ -373,14 +376,17 @@ __device__ __forceinline__ void wg_bias_acc(const Pf8& pd, float (&bs)[8]) {
 }
 
 template <class G>
-__global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
-                                               const uint16_t* __restrict__ dy, const uint16_t* __restrict__ mask,
-                                               int B, int gridb,
-                                               float* __restrict__ partial, float* __restrict__ bias_partial) {
-  __shared__ __attribute__((aligned(16))) char smem[G::X_BYTES + G::DY_BYTES];
-  char* xs = smem;
-  char* dys = smem + G::X_BYTES;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__global__ __launch_bounds__(256 * G::GROUPS) void wgrad_k(const void* __restrict__ x, FrameSrc fs,
+                                                          const uint16_t* __restrict__ dy,
+                                                          const uint16_t* __restrict__ mask, int B, int gridb,
+                                                          float* __restrict__ partial,
+                                                          float* __restrict__ bias_partial) {
+  constexpr int GB = G::X_BYTES + G::DY_BYTES;  // LDS bytes per sample group
+  __shared__ __attribute__((aligned(16))) char smem[G::GROUPS * GB];
+  const int grp = threadIdx.x >> 8;           // sample group (wave-uniform)
+  char* xs = smem + grp * GB;
+  char* dys = xs + G::X_BYTES;
+  const int lane = threadIdx.x & 63, wave = (threadIdx.x >> 6) & 3;  // wave within the group
   const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3, h = g >> 1;
   const int colsel = 16 * (g & 1) + 4 * pp;  // column (within a 32-wide tile) this lane addresses
   // XCD-aware mapping: workgroups are dealt round-robin to the 8 XCDs (blockIdx % 8), and
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   // values 8 apart so they share one XCD's L2 (one HBM/MALL read per sample instead of
   // KSPLIT).  Needs gridDim.x % (8 * KSPLIT) == 0, else the plain mapping.
   int bg, kg;
-  if (gridDim.x % (8 * G::KSPLIT) == 0) {
+  if (G::XCD && gridDim.x % (8 * G::KSPLIT) == 0) {
     const int xcd = blockIdx.x & 7, r = blockIdx.x >> 3;
     kg = r % G::KSPLIT;
     bg = (r / G::KSPLIT) * 8 + xcd;
@@ -399,7 +405,7 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
   const int kt0 = kg * G::KTB;
   const bool do_bias = kg == 0;  // block-uniform: one kidx group owns the bias gradient
   // zero the padded dy rows once (they stay zero)
-  for (int q = threadIdx.x; q < (G::PPAD - G::P) * G::DYROW / 16; q += blockDim.x)
+  for (int q = threadIdx.x & 255; q < (G::PPAD - G::P) * G::DYROW / 16; q += 256)
     reinterpret_cast<uint4*>(dys + G::P * G::DYROW)[q] = uint4{0, 0, 0, 0};
   float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16 acc[G::NT][G::KTW];
@@ -420,39 +426,36 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
 #pragma unroll
       for (int t = 0; t < 2; ++t) ad.b[ks][t][k] = wg_boff<G>(ks, t, h, q4, colsel, ktc);
   }
-  // register prefetch, G::DEPTH samples deep: while sample b multiplies, the x and dy
-  // loads of the next DEPTH samples are in flight (one LDS buffer, committed at the top
-  // of each sample).  A sample's MFMA loop is far shorter than an HBM round trip, so with
-  // one sample in flight the loop waited on memory every iteration.
+  // register prefetch: the group's next sample's x and dy loads are in flight during this
+  // sample's MFMA loop (one LDS buffer per group; committed after the compute)
   constexpr int XCH = (G::C == 4) ? 0 : G::H * G::W * G::C / 8;
   constexpr int DCH = G::P * G::N / 8;
-  constexpr int D = G::DEPTH;
-  Pf8 px[D], pd[D], pm[D];
-#pragma unroll
-  for (int u = 0; u < D; ++u)
-    if (bg + u * gridb < B) wg_issue<G>(x, fs, dy, mask, bg + u * gridb, px[u], pd[u], pm[u]);
-  for (int b0 = bg; b0 < B; b0 += D * gridb) {
-#pragma unroll
-    for (int u = 0; u < D; ++u) {
-      const int b = b0 + u * gridb;
-      if (b >= B) break;  // block-uniform
-      __syncthreads();  // the previous sample's compute is done with LDS
+  constexpr int STEP = G::GROUPS;  // samples of this batch slice per iteration
+  Pf8 px, pd, pm;
+  if (bg + grp * gridb < B) wg_issue<G>(x, fs, dy, mask, bg + grp * gridb, px, pd, pm);
+  for (int b0 = bg; b0 < B; b0 += STEP * gridb) {  // block-uniform trip count
+    const int b = b0 + grp * gridb;
+    const bool valid = b < B;  // group-uniform
+    __syncthreads();  // the previous sample's compute is done with LDS
+    if (valid) {
       if constexpr (G::C == 4) {
-        frames_store<G>(px[u], xs);
+        frames_store<G>(px, xs);
       } else {
         constexpr int CH16 = G::C / 8;
-        pf_store<XCH>(px[u], xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
+        pf_store<XCH>(px, xs, [](int q) { return (q / CH16) * G::PIX + (q % CH16) * 16; });
       }
       {
         constexpr int CH16 = G::N / 8;
-        if (mask) pf_mask<DCH>(pd[u], pm[u]);  // ReLU backward of the layer output, applied at staging
-        pf_store<DCH>(pd[u], dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
+        if (mask) pf_mask<DCH>(pd, pm);  // ReLU backward of the layer output, applied at staging
+        pf_store<DCH>(pd, dys, [](int q) { return (q / CH16) * G::DYROW + (q % CH16) * 16; });
       }
-      if (do_bias) wg_bias_acc<G>(pd[u], bs);
-      __syncthreads();
-      if (b + D * gridb < B) wg_issue<G>(x, fs, dy, mask, b + D * gridb, px[u], pd[u], pm[u]);  // block-uniform
-      // fully unrolled pixel k-steps on precomputed fragment addresses, software pipelined:
-      // the fragments of ks + 1 are read while ks multiplies
+      if (do_bias) wg_bias_acc<G>(pd, bs);
+    }
+    __syncthreads();
+    if (b + STEP * gridb < B) wg_issue<G>(x, fs, dy, mask, b + STEP * gridb, px, pd, pm);  // group-uniform
+    if (valid) {
+      // fully unrolled pixel k-steps on precomputed fragment addresses, software
+      // pipelined: the fragments of ks + 1 are read while ks multiplies
       WgFrags<G> cur;
       wg_frags_pre<G>(xs, dys, 0, arow, colsel, ad, cur);
 #pragma unroll
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
       }
     }
   }
-  if (do_bias) {  // fixed-order combine of the per-thread bias sums (reuse the x tile region of LDS)
+  if (do_bias) {  // fixed-order combine of the per-thread bias sums (reuse the LDS tiles)
     constexpr int NG = G::N / 8;  // channel groups; thread t owns group t % NG
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);
@@ -472,11 +475,34 @@ __global__ __launch_bounds__(256) void wgrad_k(const void* __restrict__ x, Frame
     for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = bs[j];
     __syncthreads();
     if (threadIdx.x < G::N) {
-      const int n = threadIdx.x, grp = n / 8, j = n % 8;
+      const int n = threadIdx.x, cg = n / 8, j = n % 8;
       float t = 0.f;
-      for (int src = grp; src < 256; src += NG) t += red[src * 8 + j];
+      for (int src = cg; src < 256 * G::GROUPS; src += NG) t += red[src * 8 + j];
       bias_partial[(size_t)bg * G::N + n] = t;
     }
+  }
+  if constexpr (G::GROUPS > 1) {  // group 1's accumulators into group 0's, one k-tile column at a time
+    static_assert(G::GROUPS == 2, "two sample groups");
+    static_assert(4 * G::NT * 16 * 64 * 4 <= G::GROUPS * GB, "accumulator exchange fits the tiles");
+    float* xch = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int k = 0; k < G::KTW; ++k) {
+      __syncthreads();
+      if (grp == 1) {
+#pragma unroll
+        for (int nt = 0; nt < G::NT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xch[((wave * G::NT + nt) * 16 + r) * 64 + lane] = acc[nt][k][r];
+      }
+      __syncthreads();
+      if (grp == 0) {
+#pragma unroll
+        for (int nt = 0; nt < G::NT; ++nt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[nt][k][r] += xch[((wave * G::NT + nt) * 16 + r) * 64 + lane];
+      }
+    }
+    if (grp != 0) return;
   }
   // partial[bg][n][kidx]: C/D map row = n (A rows), col = kidx (B cols)
   float* out = partial + (size_t)bg * G::N * G::K;
@@ -536,7 +562,7 @@ static void launch_wgrad(const void* x, FrameSrc fs, const uint16_t* dy, const u
   const int grid = std::min(G::GRID, B);  // batch slices; x KSPLIT kidx groups
   float* partial = ws;
   float* bpart = ws + (size_t)G::GRID * G::N * G::K;
-  wgrad_k<G><<<grid * G::KSPLIT, 256, 0, s>>>(x, fs, dy, mask, B, grid, partial, bpart);
+  wgrad_k<G><<<grid * G::KSPLIT, 256 * G::GROUPS, 0, s>>>(x, fs, dy, mask, B, grid, partial, bpart);
   LAUNCH_CHECK();
   if (!grad) return;  // partials only: grad_finalize reduces them with the other layers'
   const int total = G::N * G::K + G::N;
