@@ -22,10 +22,12 @@ namespace apex {
 
 namespace {
 constexpr int LH_ROWS = 8;   // rows per workgroup (B = 512 -> 64 workgroups)
+constexpr int LH_WAVES = 8;  // one row per wave: each row is a chain of dependent loads
+                             // (idx -> a, r, d; q rows), two rows per wave serialised them
 constexpr int LH_MAXA = 63;
 }  // namespace
 
-__global__ __launch_bounds__(256) void dqn_heads_bwd_k(LossHeadsArgs p) {
+__global__ __launch_bounds__(64 * LH_WAVES) void dqn_heads_bwd_k(LossHeadsArgs p) {
   __shared__ float colsum[128];
   __shared__ float gs[LH_ROWS];
   __shared__ int as[LH_ROWS];
@@ -40,10 +42,10 @@ __global__ __launch_bounds__(256) void dqn_heads_bwd_k(LossHeadsArgs p) {
     for (int a = 0; a < A; ++a) c += p.w_adv2[a * 128 + t];
     colsum[t] = c;
   }
-  for (int e = t; e < A * 128; e += 256) adv[e / 128][e % 128] = 0.f;
+  for (int e = t; e < A * 128; e += 64 * LH_WAVES) adv[e / 128][e % 128] = 0.f;
   __syncthreads();
   const float gn = p.gamma_n;
-  for (int rr = wave; rr < LH_ROWS; rr += 4) {
+  for (int rr = wave; rr < LH_ROWS; rr += LH_WAVES) {
     const int b = r0 + rr;
     if (rr >= nr) {  // wave-uniform
       if (lane == 0) {
@@ -96,6 +98,7 @@ __global__ __launch_bounds__(256) void dqn_heads_bwd_k(LossHeadsArgs p) {
     }
   }
   __syncthreads();
+  if (t >= 256) return;  // the partials below are one column per thread (no barriers follow)
   // workgroup partials: [A][128] dW_adv2, [128] dW_val2, [A] db_adv2, [1] db_val2, [256] db_fc1
   const int stride = (A + 1) * 128 + (A + 1) + 256;
   float* part = p.part + (size_t)blockIdx.x * stride;
@@ -128,7 +131,7 @@ int dqn_heads_bwd_blocks(int B) { return (B + LH_ROWS - 1) / LH_ROWS; }
 void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s) {
   if (args.A < 1 || args.A > LH_MAXA) throw std::invalid_argument("dqn_heads_bwd: 1 <= A <= 63");
   if (args.B <= 0) return;
-  dqn_heads_bwd_k<<<dqn_heads_bwd_blocks(args.B), 256, 0, s>>>(args);
+  dqn_heads_bwd_k<<<dqn_heads_bwd_blocks(args.B), 64 * LH_WAVES, 0, s>>>(args);
   LAUNCH_CHECK();
 }
 
