@@ -231,7 +231,21 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
   __shared__ float hs[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int B = set.B, A = set.A, nsplit = set.nsplit, RB = (B + kHeadRows - 1) / kHeadRows;
-  const int pb = blockIdx.x / RB, rb = blockIdx.x - pb * RB;
+  int pb, rb;
+  if (set.xcd_map) {
+    // The learner's 3 x 512 rows: fc1_fwd's grid (12 row tiles m, 14 splits s) puts slab
+    // (m, s) on XCD (m + 12 s) % 8, i.e. row tile m's partials live in the L2s of the two
+    // XCDs x == m (mod 4).  Deal this kernel's 384 row blocks so each reads its row tile
+    // from those L2s (workgroups go to XCD blockIdx % 8): XCD pair {c, c + 4} takes the
+    // 96 row blocks of tiles c, c + 4, c + 8 (48 each, balanced).
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, c = x & 3;
+    const int k = j + 48 * (x >> 2);
+    pb = k / 32;
+    rb = c * 32 + (k & 31);
+  } else {
+    pb = blockIdx.x / RB;
+    rb = blockIdx.x - pb * RB;
+  }
   const HeadsProb& pr = set.p[pb];
   const float* __restrict__ z = pr.z;
   for (int e = threadIdx.x; e < (A + 1) * 128; e += 256) {
@@ -243,19 +257,23 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
     const int b = rb * kHeadRows + rr * 4 + wave;
     const bool valid = b < B;
     const float* zr = z + (size_t)(valid ? b : 0) * 256;
-    // split-K slabs summed in fixed order; 4 columns per lane, loads of 2 slabs in flight
-    // per column ahead of the adds
+    // split-K slabs summed in fixed (slab) order; 4 columns per lane, 8 slabs (32 loads)
+    // in flight ahead of the adds: the sum is a chain of dependent L2/MALL round trips
+    // (the actor's 256-row FC1 uses 28 slabs: 2 in flight cost ~12 us)
     float zs[4] = {0.f, 0.f, 0.f, 0.f};
     const size_t sstride = (size_t)B * 256;
-    for (int sp = 0; sp < nsplit; sp += 2) {
-      float v0[4], v1[4];
+    constexpr int U = 8;
+    for (int sp = 0; sp < nsplit; sp += U) {
+      float v[U][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v0[k] = zr[(size_t)sp * sstride + lane + 64 * k];
-        v1[k] = sp + 1 < nsplit ? zr[(size_t)(sp + 1) * sstride + lane + 64 * k] : 0.f;
-      }
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) zs[k] = (zs[k] + v0[k]) + v1[k];
+        for (int k = 0; k < 4; ++k)
+          v[u][k] = sp + u < nsplit ? zr[(size_t)(sp + u) * sstride + lane + 64 * k] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) zs[k] += v[u][k];  // adding 0.f past nsplit is exact
     }
     __syncthreads();
 #pragma unroll
@@ -286,7 +304,10 @@ void heads_fwd_multi(const HeadsSet& set, hipStream_t s) {
   if (set.nsplit < 1 || set.nsplit > 64) throw std::invalid_argument("heads_fwd: 1 <= nsplit <= 64");
   if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("heads_fwd: 1..3 problems");
   if (set.B <= 0) return;
-  heads_fwd_k<<<set.n * ((set.B + kHeadRows - 1) / kHeadRows), 256, 0, s>>>(set);
+  HeadsSet hs = set;
+  // the mapping assumes fc1_fwd's 128-row tiles x 14 splits over 3 x 512 rows (FcSet)
+  hs.xcd_map = (set.n == 3 && set.B == 512 && set.nsplit == 14 && kHeadRows == 4) ? 1 : 0;
+  heads_fwd_k<<<set.n * ((set.B + kHeadRows - 1) / kHeadRows), 256, 0, s>>>(hs);
   LAUNCH_CHECK();
 }
 

@@ -299,6 +299,7 @@ struct HeadsProb {
 struct HeadsSet {
   HeadsProb p[kMaxProbs];
   int n, B, A, nsplit;
+  int xcd_map;  // set by heads_fwd_multi: XCD-aware row-block mapping (see heads_fwd_k)
 };
 void heads_fwd_multi(const HeadsSet& set, hipStream_t s);
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,
