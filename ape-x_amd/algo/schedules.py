@@ -34,8 +34,10 @@ def step_scheduler_early(scheduler) -> None:
     """``scheduler.step()`` before ``optimizer.step()`` (the reference decays
     the LR one step early, ApeX.py:60-61 / DQN.py:71-73); torch's ordering warning is
     expected here and silenced."""
+    import re
     import warnings
 
     with warnings.catch_warnings():
-        warnings.filterwarnings("ignore", message="Detected call of `lr_scheduler.step()`")
+        # ``message`` is a regex: escape the parentheses of "step()"
+        warnings.filterwarnings("ignore", message=re.escape("Detected call of `lr_scheduler.step()`"))
         scheduler.step()
