@@ -99,17 +99,25 @@ class ActorShard:
         self.replay.gather_frames(self.st["hist"], self.obs)
         return self.obs
 
-    def act_and_step(self, q: torch.Tensor | None = None, parity: int | None = None) -> None:
+    def act_args(self) -> tuple:
+        """(eps, rng seed, step counter, actions) pointers for an inference kernel that
+        picks the actions itself (``heads_fwd_multi``'s eps-greedy epilogue: the same
+        draw as ``select_actions``); then call :meth:`act_and_step` with ``selected=True``."""
+        return (self.eps.data_ptr(), self.seed ^ 0x5E1EC7, self.step_counter.data_ptr(), self.actions.data_ptr())
+
+    def act_and_step(self, q: torch.Tensor | None = None, parity: int | None = None, selected: bool = False) -> None:
         """Given Q for the current observations (in ``self.q`` or ``q``), act, step the
         envs and push the emitted transitions into the replay (staged mode: into staging
-        set ``parity``; :meth:`apply_staged` moves them into the replay)."""
+        set ``parity``; :meth:`apply_staged` moves them into the replay).  ``selected``:
+        ``self.actions`` already holds this step's eps-greedy actions (see :meth:`act_args`)."""
         if q is not None and q.data_ptr() != self.q.data_ptr():
             self.q.copy_(q)
         s = self._stream()
         h = self.hip
         E, A = self.E, self.A
-        h.select_actions(self.q.data_ptr(), E, A, self.eps.data_ptr(), self.seed ^ 0x5E1EC7, self.step_counter.data_ptr(),
-                         self.actions.data_ptr(), s)
+        if not selected:
+            h.select_actions(self.q.data_ptr(), E, A, self.eps.data_ptr(), self.seed ^ 0x5E1EC7,
+                             self.step_counter.data_ptr(), self.actions.data_ptr(), s)
         h.vec_env_step(self.env_state.data_ptr(), self.actions.data_ptr(), self.seed, self.step_counter.data_ptr(),
                        self.replay.frames.data_ptr(), self.env_params, self.reward.data_ptr(), self.done.data_ptr(),
                        self.new_frame.data_ptr(), self.ep_log.data_ptr(), s)
@@ -117,9 +125,8 @@ class ActorShard:
             assert 0 <= parity < self.staged, "staging set out of range"
             h.nstep_emit(self.stage_nstep[parity], self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                          self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
-                         self.stage_slot[parity].data_ptr(), self.stage_prio[parity].data_ptr(), s)
-            self.step_counter.add_(1)
-            return
+                         self.stage_slot[parity].data_ptr(), self.stage_prio[parity].data_ptr(), s, True)
+            return  # the kernel advanced step_counter
         h.nstep_emit(self.nstep, self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                      self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
                      self.slot.data_ptr(), self.prio.data_ptr(), s)

@@ -125,6 +125,7 @@ class ApexEngine:
         if self.hip_net:
             self.actor_net = HipDuelingNet(self.actor_model)
             self.actor_ws = NetWorkspace(cfg.n_envs, cfg.n_actions, self.device)
+            self.actor_ws.q = self.actor.q  # the heads kernel writes the actor's Q in place (no copy)
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
@@ -150,8 +151,11 @@ class ApexEngine:
             self.actor_net.copy_packed_from(self.learner.net)
 
     def _actor_body(self, stage: int | None = None):
-        if self.hip_net:  # conv1 reads the current stacks straight from the frame ring
-            q = self.actor_net(self.replay.frames, self.actor_ws, self.actor.st["hist"])
+        if self.hip_net:  # conv1 reads the current stacks straight from the frame ring; the
+            # heads kernel writes Q into the actor's buffer and picks the eps-greedy actions
+            self.actor_net(self.replay.frames, self.actor_ws, self.actor.st["hist"], act=self.actor.act_args())
+            self.actor.act_and_step(None, stage, selected=True)
+            return
         else:
             obs = self.actor.observe()
             with torch.no_grad():

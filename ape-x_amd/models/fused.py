@@ -199,8 +199,10 @@ class HipDuelingNet:
                 m.value[2].bias.data_ptr(), ws.h.data_ptr() if ws.h is not None else 0, ws.q.data_ptr())
 
     def forward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
-                idx: torch.Tensor | None = None) -> torch.Tensor:
-        forward_multi([(self, x, ws, ids, idx)])
+                idx: torch.Tensor | None = None, act: tuple | None = None) -> torch.Tensor:
+        """Q for ``x`` into ``ws.q``; ``act`` = ``ActorShard.act_args()``: the heads kernel
+        also writes the eps-greedy actions."""
+        forward_multi([(self, x, ws, ids, idx)], act=act)
         return ws.q
 
     __call__ = forward
@@ -298,7 +300,7 @@ class HipDuelingNet:
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
 
 
-def forward_multi(passes) -> None:
+def forward_multi(passes, act: tuple | None = None) -> None:
     """Run up to 3 forward passes ``(net, x, ws, ids, idx)`` (same batch size and action
     count; the nets may differ, e.g. online and target) with ONE launch per layer: conv1,
     conv2, conv3, FC1, heads = 5 kernels instead of 5 per pass.  Each kernel boundary
@@ -322,4 +324,4 @@ def forward_multi(passes) -> None:
     h.conv_fwd_multi(2, c2, B, s)
     h.conv_fwd_multi(3, c3, B, s)
     nsplit = h.fc1_fwd_multi(fc, B, s)
-    h.heads_fwd_multi(hd, nsplit, B, A, s)
+    h.heads_fwd_multi(hd, nsplit, B, A, s, act)

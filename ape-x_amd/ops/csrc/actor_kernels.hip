@@ -232,15 +232,37 @@ __global__ void select_actions_k(const float* __restrict__ q, int E, int A, cons
 }
 
 // ------------------------------------------------------------------ n-step batcher
+__device__ __forceinline__ void nstep_one(const NStepParams& p, const NStepState& st, const TransTable& tt,
+                                          const float* __restrict__ q, const int* __restrict__ actions,
+                                          const float* __restrict__ reward, const float* __restrict__ done,
+                                          const int* __restrict__ new_frame, int64_t step, int e,
+                                          int* __restrict__ slot_out, float* __restrict__ prio_out);
+
 __global__ void nstep_emit_k(NStepParams p, NStepState st, TransTable tt, const float* __restrict__ q,
                              const int* __restrict__ actions, const float* __restrict__ reward,
                              const float* __restrict__ done, const int* __restrict__ new_frame,
-                             const int64_t* step_counter, int* __restrict__ slot_out,
-                             float* __restrict__ prio_out) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= p.E) return;
-  const int n = p.n, A = p.A;
+                             int64_t* step_counter, int* __restrict__ slot_out,
+                             float* __restrict__ prio_out, int bump) {
   const int64_t step = step_counter ? step_counter[0] : 0;
+  if (bump) {
+    // one workgroup strides over all envs, then advances the step counter once every
+    // thread has read it (replaces a separate +1 launch on the actor stream)
+    for (int e = threadIdx.x; e < p.E; e += blockDim.x) nstep_one(p, st, tt, q, actions, reward, done, new_frame,
+                                                                  step, e, slot_out, prio_out);
+    __syncthreads();
+    if (threadIdx.x == 0) step_counter[0] = step + 1;
+    return;
+  }
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < p.E) nstep_one(p, st, tt, q, actions, reward, done, new_frame, step, e, slot_out, prio_out);
+}
+
+__device__ __forceinline__ void nstep_one(const NStepParams& p, const NStepState& st, const TransTable& tt,
+                                          const float* __restrict__ q, const int* __restrict__ actions,
+                                          const float* __restrict__ reward, const float* __restrict__ done,
+                                          const int* __restrict__ new_frame, int64_t step, int e,
+                                          int* __restrict__ slot_out, float* __restrict__ prio_out) {
+  const int n = p.n, A = p.A;
   const int slot = (int)(((int64_t)step * p.E + e) % p.C);
   const int row = p.stage ? e : slot;  // staged: the learner scatters the row later
   int* meta = st.win_meta + e * 4;
@@ -409,11 +431,18 @@ void select_actions(const float* q, int E, int A, const float* eps, uint64_t see
 }
 
 void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float* q, const int* actions,
-                const float* reward, const float* done, const int* new_frame, const int64_t* step_counter,
-                int* slot_out, float* prio_out, hipStream_t s) {
+                const float* reward, const float* done, const int* new_frame, int64_t* step_counter,
+                int* slot_out, float* prio_out, hipStream_t s, bool bump) {
   if (p.n < 1 || p.n > 16) throw std::invalid_argument("n-step must be in [1, 16]");
-  nstep_emit_k<<<(p.E + 127) / 128, 128, 0, s>>>(p, st, tt, q, actions, reward, done, new_frame, step_counter,
-                                                 slot_out, prio_out);
+  if (bump && !step_counter) throw std::invalid_argument("nstep_emit: bump needs a step counter");
+  if (bump) {  // one workgroup (see nstep_emit_k)
+    const int threads = std::min(1024, std::max(64, (p.E + 63) / 64 * 64));
+    nstep_emit_k<<<1, threads, 0, s>>>(p, st, tt, q, actions, reward, done, new_frame, step_counter, slot_out,
+                                       prio_out, 1);
+  } else {
+    nstep_emit_k<<<(p.E + 127) / 128, 128, 0, s>>>(p, st, tt, q, actions, reward, done, new_frame, step_counter,
+                                                   slot_out, prio_out, 0);
+  }
   LAUNCH_CHECK();
 }
 

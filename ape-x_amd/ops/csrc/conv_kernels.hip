@@ -295,7 +295,29 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
     }
     const float adv_sum = wave_sum(lane < A ? o : 0.f);
     const float v = __shfl(o, A, 64);
-    if (valid && lane < A) pr.q[(size_t)b * A + lane] = v + o - adv_sum / (float)A;
+    const float qv = v + o - adv_sum / (float)A;
+    if (valid && lane < A) pr.q[(size_t)b * A + lane] = qv;
+    if (pb == 0 && set.act.eps != nullptr && valid) {
+      // eps-greedy epilogue (select_actions_k's semantics and Philox draw): first argmax
+      // by a wave (value, index) reduction, ties to the lower index
+      float bv = lane < A ? qv : -INFINITY;
+      int bi = lane < A ? lane : 64;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (lane == 0) {
+        float u[4];
+        uniform4(set.act.seed, (uint64_t)b, set.act.counter ? (uint64_t)set.act.counter[0] : 0ull, u);
+        if (!(u[0] > set.act.eps[b])) {
+          const int r = (int)(u[1] * (float)A);
+          bi = r < A ? r : A - 1;
+        }
+        set.act.actions[b] = bi;
+      }
+    }
   }
 }
 

@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include <array>
+#include <optional>
 #include <vector>
 
 #include "kernels.h"
@@ -200,11 +201,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     apply_staged_rows(tab(st), tab(dst), P<const int>(slot), P<const float>(prio), E, S(s));
   });
   m.def("nstep_emit", [](const NStepHandle& h, uint64_t q, uint64_t actions, uint64_t reward, uint64_t done,
-                         uint64_t new_frame, uint64_t step, uint64_t slot_out, uint64_t prio_out, uint64_t s) {
+                         uint64_t new_frame, uint64_t step, uint64_t slot_out, uint64_t prio_out, uint64_t s,
+                         bool bump) {
     nstep_emit(h.p, h.st, h.tt, P<const float>(q), P<const int>(actions), P<const float>(reward),
-               P<const float>(done), P<const int>(new_frame), P<const int64_t>(step), P<int>(slot_out),
-               P<float>(prio_out), S(s));
-  });
+               P<const float>(done), P<const int>(new_frame), P<int64_t>(step), P<int>(slot_out),
+               P<float>(prio_out), S(s), bump);
+  }, py::arg("h"), py::arg("q"), py::arg("actions"), py::arg("reward"), py::arg("done"), py::arg("new_frame"),
+     py::arg("step"), py::arg("slot_out"), py::arg("prio_out"), py::arg("s"), py::arg("bump") = false);
 
   // ---- learner
   m.def("dqn_loss", [](uint64_t q, uint64_t q2, uint64_t q2t, int ldq, uint64_t a, uint64_t r, uint64_t d,
@@ -296,7 +299,7 @@ PYBIND11_MODULE(_apex_hip, m) {
     return fc1_fwd_multi(set, S(s));
   });
   m.def("heads_fwd_multi", [](const std::vector<std::array<uint64_t, 9>>& probs, int nsplit, int B, int A,
-                              uint64_t s) {
+                              uint64_t s, std::optional<std::array<uint64_t, 4>> act) {
     if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
     HeadsSet set{};
     for (size_t i = 0; i < probs.size(); ++i) {
@@ -309,8 +312,12 @@ PYBIND11_MODULE(_apex_hip, m) {
     set.B = B;
     set.A = A;
     set.nsplit = nsplit;
+    if (act) {  // (eps, rng seed, counter, actions): eps-greedy epilogue on problem 0
+      const auto& a = *act;
+      set.act = ActSel{P<const float>(a[0]), P<const int64_t>(a[2]), P<int>(a[3]), a[1]};
+    }
     heads_fwd_multi(set, S(s));
-  });
+  }, py::arg("probs"), py::arg("nsplit"), py::arg("B"), py::arg("A"), py::arg("s"), py::arg("act") = py::none());
   m.def("fc1_splits", &fc1_splits);
   m.def("fc1_fwd", [](uint64_t a, uint64_t w, uint64_t part, int B, uint64_t s) {
     return fc1_fwd(P<const uint16_t>(a), P<const uint16_t>(w), P<float>(part), B, S(s));

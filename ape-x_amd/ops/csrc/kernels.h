@@ -133,8 +133,8 @@ struct TransTable {
   float* done;      // [C]
 };
 void nstep_emit(const NStepParams& p, NStepState st, TransTable tt, const float* q, const int* actions,
-                const float* reward, const float* done, const int* new_frame, const int64_t* step_counter,
-                int* slot_out, float* prio_out, hipStream_t s);
+                const float* reward, const float* done, const int* new_frame, int64_t* step_counter,
+                int* slot_out, float* prio_out, hipStream_t s, bool bump = false);
 // staged actor rows [E] -> replay tables at slot[e] (emitted rows only: prio[e] > 0);
 // also fused into per_sample's launch (extra blocks: the scatter writes table rows the
 // sampler never reads, and both must precede the learner's forward)
@@ -296,10 +296,20 @@ struct HeadsProb {
   float* hout;     // [B][256] post-ReLU hidden (nullptr: not kept)
   float* q;        // [B][A]
 };
+// Optional epsilon-greedy epilogue of problem 0 (the actor's inference pass): the wave that
+// finishes row b's Q also picks its action (first argmax; uniform action with prob eps[b]),
+// drawing the same Philox numbers as select_actions_k, so the standalone launch goes away.
+struct ActSel {
+  const float* eps;        // [B] per-env epsilon (nullptr: no epilogue)
+  const int64_t* counter;  // actor step counter (RNG counter)
+  int* actions;            // [B]
+  uint64_t seed;
+};
 struct HeadsSet {
   HeadsProb p[kMaxProbs];
   int n, B, A, nsplit;
   int xcd_map;  // set by heads_fwd_multi: XCD-aware row-block mapping (see heads_fwd_k)
+  ActSel act;
 };
 void heads_fwd_multi(const HeadsSet& set, hipStream_t s);
 void heads_bwd(const float* dq, const float* h, const float* w_adv2, const float* w_val2, float* dA, float* dz,

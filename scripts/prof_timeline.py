@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--marker", default="dqn_heads_bwd")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--actor-kernels", default="vec_env_step,select_actions,nstep_emit,copyBuffer,elementwise")
+    ap.add_argument("--dump-step", action="store_true", help="print the kernels of the last full step")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -45,6 +46,19 @@ def main():
     ak = a.actor_kernels.split(",")
     learner = [(s, e) for s, e, r in win if not any(k in r["Kernel_Name"] for k in ak)]
     print(f"  non-actor-named kernels busy (union) {union(learner) / n / 1e3:.1f} us/step")
+    if a.dump_step:
+        # Gantt of the last full step: offset/duration (us) per kernel, per queue, and the idle
+        # gap before it on its queue (where that queue waits on another queue or the host).
+        s0, s1 = marks[-2], marks[-1]
+        ks = [(int(r["Start_Timestamp"]) - s0, int(r["End_Timestamp"]) - s0, r) for r in rows
+              if s0 <= int(r["Start_Timestamp"]) < s1]
+        last_end = {}
+        print(f"\nstep gantt ({(s1 - s0) / 1e3:.1f} us): start  dur  gap-on-queue  queue  kernel")
+        for s, e, r in ks:
+            q = r.get("Queue_Id", "?")
+            gap = s - last_end.get(q, s)
+            last_end[q] = max(e, last_end.get(q, e))
+            print(f"{s / 1e3:8.1f} {(e - s) / 1e3:6.1f} {gap / 1e3:7.1f}  q{q:>3}  {r['Kernel_Name'][:80]}")
 
 
 if __name__ == "__main__":

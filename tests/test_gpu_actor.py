@@ -70,3 +70,39 @@ def test_env_frames_and_episodes(cuda):
     assert int(rp.filled.item()) == 120 * E
     # all emitted slots have positive mass
     assert rp.total_priority() > 0
+
+
+def test_fused_eps_greedy_epilogue_matches_select_actions(cuda):
+    """heads_fwd's eps-greedy epilogue == the standalone select_actions kernel on the same Q
+    (first argmax, same Philox draw), and the staged n-step launch advances the counter."""
+    from apex_amd import ops
+    from apex_amd.engine.actor_shard import ActorShard
+    from apex_amd.engine.hbm_replay import HBMReplay
+    from apex_amd.models.dqn import DuelingDQN
+    from apex_amd.models.fused import HipDuelingNet, NetWorkspace
+
+    E, A = 256, 18
+    rp = HBMReplay(8192, n_envs=E, device=cuda)
+    act = ActorShard(rp, E, A, seed=5, staged=2)
+    net = HipDuelingNet(DuelingDQN.from_shapes((4, 84, 84), A).to(cuda))
+    ws = NetWorkspace(E, A, cuda)
+    ws.q = act.q
+    h = ops.hip()
+    s = torch.cuda.current_stream().cuda_stream
+    for t in range(6):
+        net(rp.frames, ws, act.st["hist"], act=act.act_args())
+        fused = act.actions.clone()
+        ref = torch.empty_like(fused)
+        h.select_actions(act.q.data_ptr(), E, A, act.eps.data_ptr(), act.seed ^ 0x5E1EC7, act.step_counter.data_ptr(),
+                         ref.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert torch.equal(fused, ref), (t, (fused != ref).sum().item())
+        c0 = int(act.step_counter.item())
+        act.act_and_step(None, t % 2, selected=True)
+        torch.cuda.synchronize()
+        assert int(act.step_counter.item()) == c0 + 1
+    # exploratory actions happen (eps ladder up to 0.4) and the greedy ones follow Q
+    net(rp.frames, ws, act.st["hist"], act=act.act_args())
+    torch.cuda.synchronize()
+    agree = (act.actions == act.q.argmax(1).to(torch.int32)).float().mean().item()
+    assert 0.5 < agree < 1.0, agree
