@@ -46,6 +46,7 @@ class LearnerConfig:
     seed: int = 0
     tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
     bwd_fork: bool = False         # hip path: wgrad3/wgrad2 on a forked stream (measured slower: off)
+    fork_late: bool = True         # capture the tree branch after the backward's first launch (see _fork_point)
     tree_write: str = "legacy"     # "legacy": single-workgroup walks on the tree fork (few CUs beside the
                                    # backward: 3315 vs 3195 steps/s) | "batch": HBMReplay.write_batch (wide
                                    # kernels; lower latency, better when the tree write is inline)
@@ -238,9 +239,10 @@ class DQNLearner:
             if self.dp_split:
                 self.net.fc_backward(self.ws_s, extra_jobs=[heads_job])
                 return
-            self._tree_fork_begin()
+            after = self._fork_point()
             n = self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, extra_jobs=[heads_job],
-                                        sumsq=self.fin_partials if self.allreduce is None else None)
+                                        sumsq=self.fin_partials if self.allreduce is None else None,
+                                        after_first=after)
             if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n
@@ -268,21 +270,38 @@ class DQNLearner:
         the conv backward (+ its finalize); joined before returning."""
         assert self.dp_split
         rp = self.replay
-        self._tree_fork_begin()
-        self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx)
+        after = self._fork_point()
+        self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, after_first=after)
         self._tree_fork_end()
         if self.sharded is not None and self.grad_prefix:
             # the tree is final for the next sample: pack this shard's slot, which the
             # conv-gradient all-reduce then exchanges (the next step's shard masses)
             self.sharded.pack()
 
-    def _tree_fork_begin(self) -> None:
+    def _fork_point(self):
+        """Fork the tree branch HERE (it depends on everything launched so far) but capture
+        it after the backward's first launch (``fork_late``): in the captured graph the
+        backward chain is then the first child of the fork and keeps the launch queue,
+        and only the tree branch pays the cross-queue hand-off.  Returns the callback for
+        ``after_first`` (None: the branch was forked right away)."""
+        if not (self.cfg.tree_fork and self.cfg.fork_late):
+            self._tree_fork_begin()
+            return None
+        self._ev_fork = ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        return lambda: self._tree_fork_begin(ev)
+
+    def _tree_fork_begin(self, ev: torch.cuda.Event | None = None) -> None:
         """Fork: deferred actor-row priorities, then the priority mix + loss mean + tree
-        write (+ step bump) of this step's samples, beside the backward."""
+        write (+ step bump) of this step's samples, beside the backward (``ev``: the fork
+        point, recorded earlier on the main stream)."""
         main = torch.cuda.current_stream()
         fork = self.cfg.tree_fork
         if fork:
-            self.tree_stream.wait_stream(main)
+            if ev is None:
+                self.tree_stream.wait_stream(main)
+            else:
+                self.tree_stream.wait_event(ev)
         with torch.cuda.stream(self.tree_stream if fork else main):
             hooks, self.tree_hooks = self.tree_hooks, []
             for fn in hooks:

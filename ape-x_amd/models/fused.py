@@ -234,12 +234,16 @@ class HipDuelingNet:
                                            m.value[0].bias.grad.data_ptr())
 
     def trunk_backward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
-                       idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None) -> int:
+                       idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None,
+                       after_first=None) -> int:
         """FC1 + conv backward from ``ws.dz_bf`` (dL/dz, bf16); the weight-gradient partials
         of all layers (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes
         per-workgroup sum-of-squares partials into ``sumsq`` (fp64) when given; returns
-        their count."""
+        their count.  ``after_first()`` runs right after the first launch (the FC1 backward):
+        a forked branch captured there keeps the backward chain the graph's first child."""
         self._fc1_bwd(ws)
+        if after_first is not None:
+            after_first()
         jobs = self._conv_chain(x, ws, ids, idx) + self._fc_jobs()
         return self.hip.grad_finalize(jobs + list(extra_jobs), self._s(), 0 if sumsq is None else sumsq.data_ptr())
 
@@ -251,10 +255,10 @@ class HipDuelingNet:
         self.hip.grad_finalize(self._fc_jobs() + list(extra_jobs), self._s(), 0)
 
     def conv_backward(self, x: torch.Tensor, ws: NetWorkspace, ids: torch.Tensor | None = None,
-                      idx: torch.Tensor | None = None) -> None:
+                      idx: torch.Tensor | None = None, after_first=None) -> None:
         """Data-parallel split, part 2: conv3..conv1 backward + their finalize (needs
-        ``ws.dy3`` from :meth:`fc_backward`)."""
-        self.hip.grad_finalize(self._conv_chain(x, ws, ids, idx), self._s(), 0)
+        ``ws.dy3`` from :meth:`fc_backward`); ``after_first`` as in :meth:`trunk_backward`."""
+        self.hip.grad_finalize(self._conv_chain(x, ws, ids, idx, after_first), self._s(), 0)
 
     def _fc1_bwd(self, ws: NetWorkspace) -> None:
         # FC1: dy3 = relu_mask(dz . W) and dW slabs in one launch
@@ -268,7 +272,7 @@ class HipDuelingNet:
         return [self.hip.fc1_finalize_job(0, self._fc1_ws.data_ptr(), m.advantage[0].weight.grad.data_ptr()),
                 self.hip.fc1_finalize_job(1, self._fc1_ws.data_ptr(), m.value[0].weight.grad.data_ptr())]
 
-    def _conv_chain(self, x, ws: NetWorkspace, ids, idx) -> list:
+    def _conv_chain(self, x, ws: NetWorkspace, ids, idx, after_first=None) -> list:
         """conv3 .. conv1 MFMA wgrad (partials only) / dgrad, where dgrad applies the ReLU
         backward of the layer below in its coalesced epilogue (ws.dy2 / ws.dy1 are the
         masked gradients); returns the finalize jobs of the three layers."""
@@ -285,6 +289,8 @@ class HipDuelingNet:
             side.wait_stream(main)
         with torch.cuda.stream(side):
             h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, side.cuda_stream)
+        if after_first is not None:
+            after_first()
         h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
         if fork:
             ev = torch.cuda.Event()
