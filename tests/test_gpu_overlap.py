@@ -38,14 +38,14 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False):
+def _engine(dev, overlap, graphs, dp=False, sharded=False, **lkw):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=4096, threshold_size=2048, overlap=overlap, use_graphs=graphs,
                        publish_param_interval=4, target_update_interval=6,
-                       learner=LearnerConfig(batch_size=256, forward="hip"))
+                       learner=LearnerConfig(batch_size=256, forward="hip", **lkw))
     torch.manual_seed(0)
     # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
     # pipelined shard-mass exchange) with a world-1 all-reduce -- same code path, 1 GPU
@@ -71,6 +71,24 @@ def test_overlapped_graphs_equal_sequential_schedule(cuda):
     assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
     assert torch.isfinite(eng_g.learner.flat).all()
+
+
+@pytest.mark.parametrize("lkw", [dict(bwd_fork=True), dict(fork_late=False), dict(tree_fork=False)])
+def test_graph_fork_layouts_equal_default(cuda, lkw):
+    """Where the captured graph forks (wgrad side stream, tree branch order, no tree
+    fork) changes the schedule only: the replayed steps are bit-identical to the default."""
+    eng_a = _engine(cuda, True, True)
+    eng_b = _engine(cuda, True, True, **lkw)
+    for eng in (eng_a, eng_b):
+        eng.fill()
+        eng.capture()
+    for _ in range(12):
+        eng_a.train_step()
+        eng_b.train_step()
+    torch.cuda.synchronize()
+    assert torch.equal(eng_a.learner.flat, eng_b.learner.flat)
+    assert torch.equal(eng_a.replay.leaf_sum, eng_b.replay.leaf_sum)
+    assert torch.isfinite(eng_a.learner.flat).all()
 
 
 @pytest.mark.parametrize("overlap", [True, False])
