@@ -46,6 +46,7 @@ class LearnerConfig:
     seed: int = 0
     tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
     bwd_fork: bool = False         # hip path: wgrad3/wgrad2 on a forked stream (measured slower: off)
+    late_join: bool = False        # single-process: join the tree branch after the optimizer (A/B 3555 vs 3633: off)
     fork_late: bool = True         # capture the tree branch after the backward's first launch (see _fork_point)
     tree_write: str = "legacy"     # "legacy": single-workgroup walks on the tree fork (few CUs beside the
                                    # backward: 3315 vs 3195 steps/s) | "batch": HBMReplay.write_batch (wide
@@ -76,6 +77,7 @@ class DQNLearner:
         self.device = replay.device
         self.model = model.to(self.device)
         self.flat = self.model.flatten_parameters()
+        self._join_pending = False
         self.target = copy.deepcopy(self.model)
         self.target._flat = None
         self.tflat = self.target.flatten_parameters()
@@ -246,7 +248,10 @@ class DQNLearner:
             if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n
-            self._tree_fork_end()
+            if self.cfg.late_join and self.allreduce is None:
+                self._join_pending = True  # joined after the optimizer (it reads nothing the branch writes)
+            else:
+                self._tree_fork_end()
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
@@ -340,6 +345,9 @@ class DQNLearner:
              parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk, **fc)
         if not self.hip_net:
             self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
+        if self._join_pending:
+            self._join_pending = False
+            self._tree_fork_end()
 
     def step(self) -> None:
         """One eager learner step (the engine runs the same phases as hipGraphs)."""

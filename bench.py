@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1122)
     ap.add_argument("--bwd-fork", action="store_true",
                     help="wgrad3/wgrad2 on a forked stream beside the dgrad chain (measured slower)")
+    ap.add_argument("--late-join", action="store_true",
+                    help="join the priority-tree branch after the optimizer instead of before it (measured slower)")
     ap.add_argument("--no-fork-late", dest="fork_late", action="store_false",
                     help="capture the priority-tree branch at its fork point, before the backward chain "
                          "(default: after the backward's first launch, so the chain keeps the graph's queue)")
@@ -121,7 +123,7 @@ def main():
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork,
-                       fork_late=args.fork_late,
+                       fork_late=args.fork_late, late_join=args.late_join,
                        bwd_fork=args.bwd_fork, tree_write=args.tree_write)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,

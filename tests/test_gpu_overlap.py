@@ -73,7 +73,8 @@ def test_overlapped_graphs_equal_sequential_schedule(cuda):
     assert torch.isfinite(eng_g.learner.flat).all()
 
 
-@pytest.mark.parametrize("lkw", [dict(bwd_fork=True), dict(fork_late=False), dict(tree_fork=False)])
+@pytest.mark.parametrize("lkw", [dict(bwd_fork=True), dict(fork_late=False), dict(tree_fork=False),
+                                 dict(late_join=True)])
 def test_graph_fork_layouts_equal_default(cuda, lkw):
     """Where the captured graph forks (wgrad side stream, tree branch order, no tree
     fork) changes the schedule only: the replayed steps are bit-identical to the default."""
