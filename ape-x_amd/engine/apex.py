@@ -72,6 +72,7 @@ class EngineConfig:
     # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
     # staging half, instead of three phase graphs with eager collectives in between
     dp_graph: bool = False
+    dp_comm_late: bool = True  # one-graph DP: capture the FC1 all-reduce branch after the backward's first launch
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
 
@@ -345,8 +346,15 @@ class ApexEngine:
         ar = self._allreduce
         self._learn_a(apply_half)
         fc, conv = self.learner.grad_slices()
-        w1 = ar.start(fc)
-        self.learner.backward_phase()
+        if self.cfg.dp_comm_late and hasattr(ar, "mark"):
+            # the FC1/head all-reduce depends on this point but is captured after the conv
+            # backward's first launch, so the backward chain keeps the graph's queue
+            ready, w = ar.mark(), []
+            self.learner.backward_phase(after_first=lambda: w.append(ar.start(fc, ready=ready)))
+            w1 = w[0]
+        else:
+            w1 = ar.start(fc)
+            self.learner.backward_phase()
         w2 = ar.start(conv)
         ar.wait(w1, w2)
         self._learn_b()

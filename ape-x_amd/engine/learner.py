@@ -270,12 +270,13 @@ class DQNLearner:
         self.flat_grad.zero_()
         q.backward(self.dq)
 
-    def backward_phase(self) -> None:
+    def backward_phase(self, after_first=None) -> None:
         """Data-parallel split, part 2: priority-tree writes on the forked tree stream beside
         the conv backward (+ its finalize); joined before returning."""
         assert self.dp_split
         rp = self.replay
-        after = self._fork_point()
+        tree = self._fork_point()
+        after = tree if after_first is None else (after_first if tree is None else (lambda: (tree(), after_first())))
         self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, after_first=after)
         self._tree_fork_end()
         if self.sharded is not None and self.grad_prefix:

@@ -73,12 +73,21 @@ class RcclGradAllReduce:
         self._k = (self._k + 1) % len(self._ring)
         return e
 
-    def start(self, t: torch.Tensor):
+    def mark(self):
+        """Record the point the next :meth:`start` depends on (``start(t, ready=...)`` may then
+        be issued later: in a captured graph the chain launched in between stays the fork's
+        first child and keeps the graph's queue; the collective branch takes the hand-off)."""
         if self.world == 1 and not self.force:
             return None
-        cur = torch.cuda.current_stream(self.device)
         ready = self._event()
-        ready.record(cur)
+        ready.record(torch.cuda.current_stream(self.device))
+        return ready
+
+    def start(self, t: torch.Tensor, ready=None):
+        if self.world == 1 and not self.force:
+            return None
+        if ready is None:
+            ready = self.mark()
         self.stream.wait_event(ready)
         self.comm.all_reduce_sum(t, self.stream)
         done = self._event()

@@ -79,6 +79,9 @@ def parse():
                     help="data-parallel: three phase graphs with eager RCCL all-reduces in between (default: the "
                          "all-reduces are captured inside ONE learner hipGraph per step; forced-DP 1-rank A/B 2615 -> "
                          "3050 steps/s)")
+    ap.add_argument("--dp-comm-early", dest="dp_comm_late", action="store_false",
+                    help="one-graph DP: capture the FC1 all-reduce at its fork point (default: after the conv "
+                         "backward's first launch)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (RCCL collectives, sharded sampling) even with 1 rank "
                          "(under torch.distributed.run --nproc-per-node 1): measures its single-GPU overhead")
@@ -144,6 +147,7 @@ def main():
     sharded = dp and not args.local_sampling
     from apex_amd.parallel.rccl import RcclGradAllReduce as _Rccl
 
+    cfg.dp_comm_late = args.dp_comm_late
     cfg.dp_graph = bool(args.dp_graph and isinstance(allreduce, _Rccl))  # capture needs the direct communicator
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
