@@ -72,6 +72,9 @@ class EngineConfig:
     # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
     # staging half, instead of three phase graphs with eager collectives in between
     dp_graph: bool = False
+    # overlap mode, single process: actor half and learner step as ONE graph per half (two
+    # branches: the learner captured first keeps the launch queue, the actor forks beside it)
+    step_graph: bool = False  # A/B 3320 vs 3647 steps/s: off
     dp_comm_late: bool = True  # one-graph DP: capture the FC1 all-reduce branch after the backward's first launch
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
@@ -130,7 +133,7 @@ class ApexEngine:
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
-        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = None
+        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = self._g_step = None
         self._pool = None
         self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
         self._captured = False
@@ -324,6 +327,12 @@ class ApexEngine:
                 self._g_dp = None
                 torch.cuda.synchronize(self.device)
                 apool = torch.cuda.graph_pool_handle()
+        if self.cfg.step_graph and not self._dp:
+            self._g_step = [self._graph(lambda h=h: self._fused_step_body(h), self._pool) for h in (0, 1)]
+            self._captured = True
+            torch.cuda.synchronize(self.device)
+            self._ev_learn.record(torch.cuda.current_stream(self.device))
+            return
         for h in (0, 1):
             self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
             if self._dp:
@@ -340,6 +349,23 @@ class ApexEngine:
         """One-graph DP step: the shard masses must always arrive with the previous step's
         conv-gradient all-reduce (overlap mode, slots in the gradient prefix)."""
         return self._sharded is None or (self.overlap and self.learner.grad_prefix > 0)
+
+    def _fused_step_body(self, h: int) -> None:
+        """Captured body of one overlapped train step (EngineConfig.step_graph): the learner
+        step (applying staging half 1-h) on the capture stream, and -- forked from the same
+        start point, captured second -- the actor half h on the actor stream, joined at the
+        end.  Replays serialise on the stream, which is the event protocol of
+        :meth:`_train_step_overlap` (actor t after learner t-1, learner t after actor t-1)."""
+        L, A = torch.cuda.current_stream(self.device), self._astream
+        start = torch.cuda.Event()
+        start.record(L)
+        self._learn_a(1 - h)
+        self._learn_b()
+        A.wait_event(start)
+        with torch.cuda.stream(A):
+            self._actor_half(h)
+        L.wait_stream(A)
+        self._step_events = start
 
     def _dp_step_body(self, apply_half: int) -> None:
         """Captured body of the one-graph DP step (EngineConfig.dp_graph)."""
@@ -383,6 +409,17 @@ class ApexEngine:
         h = self._half
         L = torch.cuda.current_stream(self.device)
         A = self._astream
+        if self._g_step is not None:
+            with trace.range("apex.step_graph"):
+                self._g_step[h].replay()
+            self.learn_steps += 1
+            self.actor_steps += self.cfg.actor_steps_per_learner_step
+            if self.learn_steps % self.cfg.publish_param_interval == 0:
+                self.publish_params()  # the graph joined its actor branch
+            if self.learn_steps % self.cfg.target_update_interval == 0:
+                self.learner.sync_target()
+            self._half ^= 1
+            return
         with trace.range("actor.launch"):
             A.wait_event(self._ev_learn)
             with torch.cuda.stream(A):

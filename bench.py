@@ -79,6 +79,8 @@ def parse():
                     help="data-parallel: three phase graphs with eager RCCL all-reduces in between (default: the "
                          "all-reduces are captured inside ONE learner hipGraph per step; forced-DP 1-rank A/B 2615 -> "
                          "3050 steps/s)")
+    ap.add_argument("--step-graph", action="store_true",
+                    help="single process, overlap: actor half + learner step as one hipGraph per step")
     ap.add_argument("--dp-comm-early", dest="dp_comm_late", action="store_false",
                     help="one-graph DP: capture the FC1 all-reduce at its fork point (default: after the conv "
                          "backward's first launch)")
@@ -148,6 +150,7 @@ def main():
     from apex_amd.parallel.rccl import RcclGradAllReduce as _Rccl
 
     cfg.dp_comm_late = args.dp_comm_late
+    cfg.step_graph = args.step_graph
     cfg.dp_graph = bool(args.dp_graph and isinstance(allreduce, _Rccl))  # capture needs the direct communicator
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)

@@ -52,8 +52,10 @@ def _engine(dev, overlap, graphs, dp=False, sharded=False, **lkw):
     return ApexEngine(cfg, dev, allreduce=FlatGradAllReduce(1) if dp else None, sharded=sharded)
 
 
-def test_overlapped_graphs_equal_sequential_schedule(cuda):
+@pytest.mark.parametrize("step_graph", [False, True])
+def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph):
     eng_g = _engine(cuda, True, True)
+    eng_g.cfg.step_graph = step_graph
     eng_e = _engine(cuda, True, False)
     for eng in (eng_g, eng_e):
         eng.fill()
