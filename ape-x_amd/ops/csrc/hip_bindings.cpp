@@ -11,6 +11,7 @@
 #include <optional>
 #include <vector>
 
+#include "common.h"
 #include "kernels.h"
 
 namespace py = pybind11;
@@ -440,6 +441,22 @@ PYBIND11_MODULE(_apex_hip, m) {
     return (uint64_t)reinterpret_cast<uintptr_t>(st);
   });
   m.def("spin_us", [](int us, uint64_t s) { spin_us(us, S(s)); });
+
+  // ---- stream-ordering events without the system-scope fence (device-local hand-offs
+  // between this process's streams: hipEventDisableSystemFence skips the L2 writeback /
+  // invalidate a default event's record and wait carry)
+  m.def("event_create", [](bool light) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming | (light ? hipEventDisableSystemFence : 0u)));
+    return reinterpret_cast<uint64_t>(e);
+  });
+  m.def("event_record", [](uint64_t e, uint64_t s) {
+    HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(s)));
+  });
+  m.def("stream_wait_event", [](uint64_t s, uint64_t e) {
+    HIP_CHECK(hipStreamWaitEvent(S(s), reinterpret_cast<hipEvent_t>(e), 0));
+  });
+  m.def("event_destroy", [](uint64_t e) { HIP_CHECK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e))); });
   m.def("copy_f32", [](uint64_t dst, uint64_t src, int64_t n, uint64_t s) {
     copy_f32(P<float>(dst), P<const float>(src), n, S(s));
   });

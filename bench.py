@@ -79,6 +79,8 @@ def parse():
                     help="data-parallel: three phase graphs with eager RCCL all-reduces in between (default: the "
                          "all-reduces are captured inside ONE learner hipGraph per step; forced-DP 1-rank A/B 2615 -> "
                          "3050 steps/s)")
+    ap.add_argument("--light-events", action="store_true",
+                    help="overlap: actor/learner hand-off events created with hipEventDisableSystemFence")
     ap.add_argument("--step-graph", action="store_true",
                     help="single process, overlap: actor half + learner step as one hipGraph per step")
     ap.add_argument("--dp-comm-early", dest="dp_comm_late", action="store_false",
@@ -151,6 +153,7 @@ def main():
 
     cfg.dp_comm_late = args.dp_comm_late
     cfg.step_graph = args.step_graph
+    cfg.light_events = args.light_events
     cfg.dp_graph = bool(args.dp_graph and isinstance(allreduce, _Rccl))  # capture needs the direct communicator
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)

@@ -38,13 +38,13 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False, **lkw):
+def _engine(dev, overlap, graphs, dp=False, sharded=False, light_events=False, **lkw):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=4096, threshold_size=2048, overlap=overlap, use_graphs=graphs,
-                       publish_param_interval=4, target_update_interval=6,
+                       publish_param_interval=4, target_update_interval=6, light_events=light_events,
                        learner=LearnerConfig(batch_size=256, forward="hip", **lkw))
     torch.manual_seed(0)
     # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
@@ -52,9 +52,9 @@ def _engine(dev, overlap, graphs, dp=False, sharded=False, **lkw):
     return ApexEngine(cfg, dev, allreduce=FlatGradAllReduce(1) if dp else None, sharded=sharded)
 
 
-@pytest.mark.parametrize("step_graph", [False, True])
-def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph):
-    eng_g = _engine(cuda, True, True)
+@pytest.mark.parametrize("step_graph,light", [(False, False), (True, False), (False, True)])
+def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph, light):
+    eng_g = _engine(cuda, True, True, light_events=light)
     eng_g.cfg.step_graph = step_graph
     eng_e = _engine(cuda, True, False)
     for eng in (eng_g, eng_e):
