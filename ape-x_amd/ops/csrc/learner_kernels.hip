@@ -224,14 +224,17 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
                                                           float* __restrict__ norms_out, PackMap pk, FcPack fc,
                                                           int n_fc_blocks) {
   const float max_norm = hp.max_norm;
-  const NormInfo ni = reduce_norms(partials, n_partials, max_norm, hp.grad_scale);
   float lr;
   const auto rule = make_rule(hp, step ? step[0] : 0, lr);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
-    norms_out[0] = ni.l2;
-    norms_out[2] = fminf(max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f, 1.f);
-    norms_out[3] = lr;
-  }
+  auto norms = [&]() {
+    const NormInfo ni = reduce_norms(partials, n_partials, max_norm, hp.grad_scale);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
+      norms_out[0] = ni.l2;
+      norms_out[2] = fminf(max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f, 1.f);
+      norms_out[3] = lr;
+    }
+    return ni;
+  };
   const int bid = blockIdx.x;
   if (bid < n_fc_blocks) {
     __shared__ uint16_t tile[kFcTn][kFcTc * kFcP];
@@ -254,6 +257,9 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
       va[k] = s1[vi[k]];
       vb[k] = s2[vi[k]];
     }
+    // the global grad norm (a reduction over the finalize partials) is reduced while the
+    // tile's loads above are in flight: the update needs it, the loads do not
+    const NormInfo ni = norms();
 #pragma unroll
     for (int k = 0; k < kIt; ++k) {
       const int e = threadIdx.x + k * kOptThreads;
@@ -285,6 +291,7 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
     return;
   }
   // generic part: every element outside the FC1 ranges, scalar, through the scatter maps
+  const NormInfo ni = norms();
   const int gb = bid - n_fc_blocks, ngb = gridDim.x - n_fc_blocks;
   const int64_t stride = (int64_t)ngb * kOptThreads;
   int64_t lo[3], hi[3];
