@@ -20,13 +20,14 @@ Backward (explicit, writes every parameter gradient into the flat fp32 grad buff
 exactly once, so no zeroing pass is needed; the learner fuses the loss and heads part
 into one launch, ``dqn_heads_bwd``, and all batch-sliced reductions into one
 ``grad_finalize``):
-  heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (hipBLASLt) ->
+  heads_bwd -> head weight/bias grads (small GEMMs/sums) -> FC1 dW/dX (fc1_bwd_k MFMA) ->
   conv3/conv2/conv1: MFMA wgrad (ds_read_b64_tr_b16 operand transposes, split over the
   batch, deterministic partial reduce, conv bias grads fused) and MFMA dgrad (stride-1
   zero-border / stride-2 sub-pixel implicit GEMM with the ReLU backward fused).
 
 Numerics: bf16 operands, fp32 accumulation, fp32 heads and Q.  Checked against the
-fp32 PyTorch module in tests/test_gpu_fused_net.py.
+fp32 PyTorch module in tests/test_gpu_fused_net.py.  This is the opt-in ``dtype="bf16"``
+mode; the reference-precision default is ``fused_f32.F32DuelingNet`` (fp32 MFMA).
 """
 from __future__ import annotations
 
@@ -69,6 +70,7 @@ def _cl_view(t: torch.Tensor, B: int, C: int, H: int, W: int) -> torch.Tensor:
 
 
 class HipDuelingNet:
+    fp32 = False
     # packed bf16 weights live in one arena: [w1p | w2p | w3p | wfc1p | w2t | w3t]
     # (conv1 keeps the reference layout [n][c][ky][kx]: its kernel's K order is (c, ky, kx))
     LAYOUT = (("w1p", (32, 4, 8, 8)), ("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, FEAT)),
@@ -324,6 +326,9 @@ def forward_multi(passes, act: tuple | None = None) -> None:
     costs ~4.5 us on MI355X (rocprofv3 trace), so the learner's three passes save ~45 us
     per step; the larger grids also amortise the per-workgroup weight staging."""
     passes = list(passes)
+    if getattr(passes[0][0], "fp32", False):
+        from .fused_f32 import forward_multi_f32
+        return forward_multi_f32(passes, act=act)
     assert 1 <= len(passes) <= 3
     net0 = passes[0][0]
     B, A = passes[0][2].B, net0.A
@@ -342,3 +347,26 @@ def forward_multi(passes, act: tuple | None = None) -> None:
     h.conv_fwd_multi(3, c3, B, s)
     nsplit = h.fc1_fwd_multi(fc, B, s)
     h.heads_fwd_multi(hd, nsplit, B, A, s, act)
+
+
+DTYPES = ("fp32", "bf16")
+
+
+def make_hip_net(model: DuelingDQN, dtype: str = "fp32"):
+    """The HIP network for ``dtype``: "fp32" (reference precision, fp32 MFMA, the default)
+    or "bf16" (bf16 MFMA operands, fp32 accumulation; opt-in fast mode)."""
+    if dtype == "fp32":
+        from .fused_f32 import F32DuelingNet
+        return F32DuelingNet(model)
+    if dtype == "bf16":
+        return HipDuelingNet(model)
+    raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
+
+
+def make_workspace(B: int, A: int, device, dtype: str = "fp32", keep_for_backward: bool = False):
+    if dtype == "fp32":
+        from .fused_f32 import F32Workspace
+        return F32Workspace(B, A, device, keep_for_backward)
+    if dtype == "bf16":
+        return NetWorkspace(B, A, device, keep_for_backward)
+    raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")

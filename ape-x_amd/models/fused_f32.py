@@ -1,0 +1,194 @@
+"""Reference-precision (fp32) HIP path of the dueling Q-network.
+
+The reference computes every forward, backward and optimizer step in fp32
+(origin_repo/learner.py:139-145, utils.py:64-97, model.py:31-68).  ``F32DuelingNet``
+runs the same Nature-CNN dueling network on gfx950's exact-f32 matrix instructions
+(``v_mfma_f32_32x32x2_f32``, a k-ordered fmaf chain) -- ``ops/csrc/f32_kernels.hip``:
+
+  forward (per layer ONE launch for up to 3 passes: Q(s), Q(s'), Q_target(s'))
+    conv1   u8 frames (frame ring by id, converted in the loader) -> a1 fp32 NHWC
+    conv2/3 implicit-GEMM, bias+ReLU fused -> a2, a3 fp32 NHWC
+    fc1     split-K (7 slabs) -> heads_fwd (fp32 heads + dueling combine, shared with bf16)
+  backward (4 GEMM launches + one grad_finalize)
+    fc1 dgrad (ReLU mask fused) + fc1 wgrad (reference layout, written in place)
+    conv3 wgrad partials + conv3 dgrad      (one launch)
+    conv2 wgrad partials + conv2 dgrad      (one launch, stride-2 sub-pixel classes)
+    conv1 wgrad partials from the u8 frames
+    grad_finalize: deterministic partial reduce -> reference layout + bias grads + grad-norm partials
+
+Weights are read straight from the fp32 master parameters in their reference layouts,
+so there is no packed copy to refresh: ``repack``/``copy_packed_from`` are no-ops and the
+optimizer is the plain fp32 centered RMSprop / Adam over the flat buffer.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .dqn import DuelingDQN
+
+P3, C3 = 49, 64
+FEAT = P3 * C3  # 3136
+F32_SPLITS = 7  # FC1 forward split-K slabs (f32_kernels.hip kFcSplits)
+
+
+class F32Workspace:
+    """fp32 activation buffers for one forward pass of batch ``B`` (+ backward buffers)."""
+
+    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False):
+        self.B, self.A = B, A
+        f32 = dict(dtype=torch.float32, device=device)
+        self.a1 = torch.empty(B, 400, 32, **f32)
+        self.a2 = torch.empty(B, 81, 64, **f32)
+        self.a3 = torch.empty(B, FEAT, **f32)
+        self.z = torch.empty(F32_SPLITS, B, 256, **f32)
+        self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
+        self.q = torch.empty(B, A, **f32)
+        if keep_for_backward:
+            self.dA = torch.empty(B, A + 1, **f32)
+            self.dz = torch.empty(B, 256, **f32)
+            self.dz_bf = torch.empty(B, 256, dtype=torch.bfloat16, device=device)  # heads_bwd writes both
+            self.dy3 = torch.empty(B, FEAT, **f32)
+            self.dy2 = torch.empty(B, 81, 64, **f32)
+            self.dy1 = torch.empty(B, 400, 32, **f32)
+
+
+class F32DuelingNet:
+    """fp32 MFMA kernels over a :class:`DuelingDQN` (fp32 master params, reference layout)."""
+
+    fp32 = True
+    arena = None
+
+    def __init__(self, model: DuelingDQN):
+        assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
+        self.hip = ops.hip()
+        assert self.hip.f32_fc1_splits() == F32_SPLITS
+        self.model = model
+        self.A = model.num_actions
+        self.device = next(model.parameters()).device
+        self._ws_B = None
+        self._heads_ws = None
+
+    # the weights are consumed in place: nothing to pack
+    def repack(self) -> None:
+        pass
+
+    def copy_packed_from(self, other, forward_only: bool = True) -> None:
+        pass
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def enable_backward(self, B: int = 512) -> None:
+        """Allocate the wgrad partial workspaces for batch ``B`` (call before graph capture)."""
+        if self._ws_B == B:
+            return
+        h = self.hip
+        self._wgrad_wss = [torch.empty(h.f32_wgrad_workspace_floats(k, B), dtype=torch.float32, device=self.device)
+                           for k in (1, 2, 3)]
+        self._heads_ws = torch.empty(h.heads_wgrad_workspace_floats(self.A), dtype=torch.float32, device=self.device)
+        self._ws_B = B
+
+    # ------------------------------------------------------------------ forward
+    @staticmethod
+    def _src(x: torch.Tensor, ids, idx, B: int):
+        assert x.dtype == torch.uint8 and x.is_contiguous()
+        if ids is None:
+            assert tuple(x.shape) == (B, 4, 84, 84)
+            return x.data_ptr(), 0, 0
+        assert ids.dtype == torch.int32 and ids.shape[-1] == 4 and x.shape[-1] == 84 * 84
+        if idx is None:
+            assert ids.shape[0] == B
+        return x.data_ptr(), ids.data_ptr(), 0 if idx is None else idx.data_ptr()
+
+    def _heads_tuple(self, ws: F32Workspace) -> tuple:
+        m = self.model
+        return (ws.z.data_ptr(), m.advantage[0].bias.data_ptr(), m.value[0].bias.data_ptr(),
+                m.advantage[2].weight.data_ptr(), m.advantage[2].bias.data_ptr(), m.value[2].weight.data_ptr(),
+                m.value[2].bias.data_ptr(), ws.h.data_ptr() if ws.h is not None else 0, ws.q.data_ptr())
+
+    def forward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
+                idx: torch.Tensor | None = None, act: tuple | None = None) -> torch.Tensor:
+        forward_multi_f32([(self, x, ws, ids, idx)], act=act)
+        return ws.q
+
+    __call__ = forward
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dq: torch.Tensor, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
+                 idx: torch.Tensor | None = None) -> None:
+        """dL/dparam for the pass held in ``ws`` into the model's ``.grad`` views, given dL/dQ."""
+        B, A = ws.B, self.A
+        h, s, m = self.hip, self._s(), self.model
+        self.enable_backward(B)
+        h.heads_bwd(dq.data_ptr(), ws.h.data_ptr(), m.advantage[2].weight.data_ptr(), m.value[2].weight.data_ptr(),
+                    ws.dA.data_ptr(), ws.dz.data_ptr(), ws.dz_bf.data_ptr(), B, A, s)
+        h.heads_wgrad(ws.dA.data_ptr(), ws.h.data_ptr(), ws.dz.data_ptr(), B, A, self._heads_ws.data_ptr(),
+                      m.advantage[2].weight.grad.data_ptr(), m.advantage[2].bias.grad.data_ptr(),
+                      m.value[2].weight.grad.data_ptr(), m.value[2].bias.grad.data_ptr(),
+                      m.advantage[0].bias.grad.data_ptr(), m.value[0].bias.grad.data_ptr(), s)
+        self.trunk_backward(x, ws, ids, idx)
+
+    def heads_finalize_job(self, part: torch.Tensor, G: int):
+        m = self.model
+        return self.hip.heads_finalize_job(G, self.A, part.data_ptr(), m.advantage[2].weight.grad.data_ptr(),
+                                           m.advantage[2].bias.grad.data_ptr(), m.value[2].weight.grad.data_ptr(),
+                                           m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
+                                           m.value[0].bias.grad.data_ptr())
+
+    def trunk_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
+                       idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None,
+                       after_first=None) -> int:
+        """FC1 + conv backward from ``ws.dz`` (fp32 dL/dz).  The conv weight-gradient
+        partials (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes the
+        per-workgroup sum-of-squares partials of EVERY gradient into ``sumsq`` (fp64) when
+        given (the FC1 weight gradients, written in place, join through norm-only jobs);
+        returns the partial count.  ``after_first()`` runs right after the first launch."""
+        B = ws.B
+        self.enable_backward(B)
+        h, s, m, f = self.hip, self._s(), self.model, self.model.features
+        ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+        h.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), m.advantage[0].weight.data_ptr(),
+                      m.value[0].weight.data_ptr(), ws.dy3.data_ptr(), ga.data_ptr(), gv.data_ptr(), B, s)
+        if after_first is not None:
+            after_first()
+        xp, ip, jp = self._src(x, ids, idx, B)
+        w1, w2, w3 = self._wgrad_wss
+        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), f[4].weight.data_ptr(), ws.a2.data_ptr(),
+                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
+        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), f[2].weight.data_ptr(), ws.a1.data_ptr(),
+                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
+        h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
+        jobs = [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
+                                        f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
+        jobs += list(extra_jobs)
+        if sumsq is not None:
+            jobs += [h.norm_only_job(ga.data_ptr(), ga.numel()), h.norm_only_job(gv.data_ptr(), gv.numel())]
+        return h.grad_finalize(jobs, s, 0 if sumsq is None else sumsq.data_ptr())
+
+
+def forward_multi_f32(passes, act: tuple | None = None) -> None:
+    """Up to 3 fp32 forward passes ``(net, x, ws, ids, idx)`` (common batch and action
+    count; the nets may differ, e.g. online and target) with ONE launch per layer."""
+    passes = list(passes)
+    assert 1 <= len(passes) <= 3
+    net0 = passes[0][0]
+    B, A = passes[0][2].B, net0.A
+    h, s = net0.hip, net0._s()
+    c1, c2, c3, fc, hd = [], [], [], [], []
+    for net, x, ws, ids, idx in passes:
+        assert ws.B == B and net.A == A, "one launch per layer needs a common batch and action count"
+        m, f = net.model, net.model.features
+        xp, ip, jp = net._src(x, ids, idx, B)
+        c1.append((xp, ip, jp, f[0].weight.data_ptr(), 0, f[0].bias.data_ptr(), ws.a1.data_ptr()))
+        c2.append((ws.a1.data_ptr(), 0, 0, f[2].weight.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
+        c3.append((ws.a2.data_ptr(), 0, 0, f[4].weight.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
+        fc.append((ws.a3.data_ptr(), 0, 0, m.advantage[0].weight.data_ptr(), m.value[0].weight.data_ptr(), 0,
+                   ws.z.data_ptr()))
+        hd.append(net._heads_tuple(ws))
+    h.f32_conv_fwd_multi(1, c1, B, s)
+    h.f32_conv_fwd_multi(2, c2, B, s)
+    h.f32_conv_fwd_multi(3, c3, B, s)
+    nsplit = h.f32_fc1_fwd_multi(fc, B, s)
+    h.heads_fwd_multi(hd, nsplit, B, A, s, act)

@@ -45,6 +45,7 @@ HIP_SOURCES = [
     "conv1_kernels.hip",
     "fc_kernels.hip",
     "loss_heads_kernels.hip",
+    "f32_kernels.hip",
     "comm.cpp",
 ]
 

@@ -612,6 +612,7 @@ constexpr int kWideG = 16;
 constexpr int kRowLen = 49 * 64;
 __host__ __device__ inline int finalize_blocks(const FinalizeJob& j) {
   if (j.kind == 2) return j.n_main / kRowLen;
+  if (j.kind == 3) return (j.n_main + 255) / 256;
   const int per = j.G >= kWideG ? 64 : 256;
   return (j.n_main + j.n_bias + per - 1) / per;
 }
@@ -634,6 +635,13 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   int j = 0;
   while (j + 1 < fs.n && (int)blockIdx.x >= fs.job[j + 1].block0) ++j;
   const FinalizeJob& jb = fs.job[j];
+  if (jb.kind == 3) {  // norm only: the gradient was written in place by its producer
+    if (!fs.sumsq) return;
+    const int e = ((int)blockIdx.x - jb.block0) * 256 + threadIdx.x;
+    const bool have = e < jb.n_main;
+    finalize_sumsq(have ? jb.part[e] : 0.f, fs.sumsq, have);
+    return;
+  }
   if (jb.kind == 2) {  // FC1 weight rows: natural [n][p*64 + c] -> reference [n][c*49 + p]
     const int n = (int)blockIdx.x - jb.block0;
     const float* src = jb.part + (size_t)n * kRowLen;

@@ -1,0 +1,830 @@
+// Reference-precision (fp32) Nature-CNN dueling network on CDNA4 fp32 MFMA (gfx950).
+//
+// The reference trains entirely in fp32 (origin_repo/learner.py:139-145, utils.py:64-97,
+// model.py:31-68).  gfx950 has exact-f32 matrix instructions -- v_mfma_f32_32x32x2_f32 is
+// bit-for-bit a k-ordered fmaf chain at 64 FLOP/clk/SIMD (157 TF chip) -- so every GEMM-shaped
+// op of the learner step (three forwards, the whole backward) runs on them here, with fp32
+// operands, fp32 activations and the fp32 master weights read in their REFERENCE layouts
+// (no packed copies: at 1/16 of the bf16 rate the kernels are MFMA-bound, and gathering a
+// weight chunk with four scalar loads from L2 is hidden behind the matrix work).
+//
+// One templated LDS-staged GEMM body serves all 13 GEMMs; a policy per layer supplies the
+// tile decode, the operand chunk loaders (implicit im2col / col2im / sub-pixel gathers,
+// u8 frames converted in the loader) and the epilogue (bias+ReLU, ReLU-backward mask,
+// split-K partials, conv bias column sums):
+//
+//   * C[M][N] = sum_k A(m,k) B(k,n); 256 threads = 4 waves on a WM x WN wave grid, each wave
+//     TM x TN 32x32 accumulators (16 fp32 each).
+//   * each operand tile is staged global -> registers -> LDS in its natural global layout:
+//     "K-major" [row][BK] (k contiguous) or "MN-major" [k][BM|BN] (m|n contiguous), 16-byte
+//     chunks; LDS double buffer + register prefetch of the next k-block (one barrier per
+//     k-block); pitches padded so the fragment reads are bank-conflict free.
+//   * k-chunk mapping: for a chunk of 8 k, lane (r = l & 31, h = l >> 5) holds elements
+//     k = 4h .. 4h+3 of its A row / B column (one ds_read_b128 when K-major, four ds_read_b32
+//     when MN-major); MFMA i of the chunk consumes element i of both -- the 32x32x2 MFMA's
+//     k-slot h is then k = 4h + i, and the four MFMAs together cover all 8.
+//
+// Layer GEMMs (B samples, activations channels-last fp32: a1 [B][400][32], a2 [B][81][64],
+// a3 [B][49][64]):
+//   fwd  conv1 M=B*400 N=32 K=256 (c,ky,kx; u8 frames)   conv2 M=B*81 N=64 K=512 (tap,ci)
+//        conv3 M=B*49 N=64 K=576                          fc1 M=B N=256 K=3136 (split-K 7)
+//   bwd  fc1 dgrad M=B N=3136 K=256 (+ReLU mask)          fc1 wgrad M=256 N=3136 K=B
+//        conv3/conv2 wgrad M=Cout N=taps*Cin K=B*P (split) conv3 dgrad M=B*81 N=64 K=576
+//        conv2 dgrad: 4 stride-2 sub-pixel classes, M=4*B*100 N=32 K=4*64
+//        conv1 wgrad M=32 N=256 K=B*400 (split, u8 frames)
+// Independent backward GEMMs share one launch (gemm2_k: fc1 dgrad+wgrad, conv3 wgrad+dgrad,
+// conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+// 4 u8 pixels (one dword) -> 4 floats (v_cvt_f32_ubyte0..3); 0..255 exact
+__device__ __forceinline__ f32x4 u8x4(uint32_t w) {
+  return f32x4{(float)(w & 0xFFu), (float)((w >> 8) & 0xFFu), (float)((w >> 16) & 0xFFu), (float)(w >> 24)};
+}
+
+constexpr int kPlane = 84 * 84;
+
+struct NoSmem {
+  int unused;
+};
+
+template <class P>
+struct Geo {
+  static constexpr int BM = P::BM, BN = P::BN, BK = P::BK, WM = P::WM, WN = 4 / P::WM;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  static constexpr int TM = WTM / 32, TN = WTN / 32;
+  static constexpr int PA = P::A_KMAJ ? BK + 4 : BM + 8;  // LDS pitches (floats)
+  static constexpr int PB = P::B_KMAJ ? BK + 4 : BN + 8;
+  static constexpr int RA = P::A_KMAJ ? BK / 4 : BM / 4;  // 16-byte chunks per LDS row
+  static constexpr int RB = P::B_KMAJ ? BK / 4 : BN / 4;
+  static constexpr int SA = (P::A_KMAJ ? BM : BK) * PA;
+  static constexpr int SB = (P::B_KMAJ ? BN : BK) * PB;
+  static constexpr int CA = BM * BK / 4, CB = BN * BK / 4;
+  static constexpr int NA = (CA + 255) / 256, NB = (CB + 255) / 256;
+  static constexpr int LDS_FLOATS = 2 * (SA + SB);
+  static_assert(WM * WN == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "32x32 wave blocks");
+  static_assert(BK % 8 == 0, "k-chunks of 8");
+  static_assert(LDS_FLOATS >= 4 * 256, "colsum reduction reuses the LDS tile");
+};
+
+// Policies may opt into an A column-sum (conv bias gradient = sum of dY over pixels):
+// only for MN-major A, where each thread's chunks always cover the same 4 columns.
+template <class P, class = void>
+struct HasColsum {
+  static constexpr bool value = false;
+};
+template <class P>
+struct HasColsum<P, decltype((void)P::A_COLSUM, void())> {
+  static constexpr bool value = P::A_COLSUM;
+};
+
+template <class P>
+__device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
+                                          typename P::Smem& sm) {
+  using G = Geo<P>;
+  constexpr bool COLSUM = HasColsum<P>::value;
+  static_assert(!COLSUM || (!P::A_KMAJ && 256 % G::RA == 0), "colsum needs MN-major A");
+  typename P::Ctx ctx;
+  P::decode(args, block, ctx, sm);
+  if constexpr (P::SMEM) __syncthreads();
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave % G::WM, wn = wave / G::WM;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  f32x4 ra[G::NA], rb[G::NB];
+  f32x4 csum = zero4();
+
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = t + 256 * j;
+      if (G::CA % 256 == 0 || q < G::CA) ra[j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
+    }
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = t + 256 * j;
+      if (G::CB % 256 == 0 || q < G::CB) rb[j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
+    }
+  };
+  auto sstore = [&](int buf) {
+    float* As = lds + buf * (G::SA + G::SB);
+    float* Bs = As + G::SA;
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = t + 256 * j;
+      if (G::CA % 256 == 0 || q < G::CA) {
+        *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[j];
+        if constexpr (COLSUM) csum += ra[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = t + 256 * j;
+      if (G::CB % 256 == 0 || q < G::CB) *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[j];
+    }
+  };
+  auto compute = [&](int buf) {
+    const float* As = lds + buf * (G::SA + G::SB);
+    const float* Bs = As + G::SA;
+#pragma unroll
+    for (int kc = 0; kc < G::BK / 8; ++kc) {
+      f32x4 a[G::TM], b[G::TN];
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi) {
+        const int m = wm * G::WTM + mi * 32 + r;
+        if constexpr (P::A_KMAJ) {
+          a[mi] = *reinterpret_cast<const f32x4*>(As + m * G::PA + kc * 8 + 4 * h);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[mi][i] = As[(kc * 8 + 4 * h + i) * G::PA + m];
+        }
+      }
+#pragma unroll
+      for (int ni = 0; ni < G::TN; ++ni) {
+        const int n = wn * G::WTN + ni * 32 + r;
+        if constexpr (P::B_KMAJ) {
+          b[ni] = *reinterpret_cast<const f32x4*>(Bs + n * G::PB + kc * 8 + 4 * h);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b[ni][i] = Bs[(kc * 8 + 4 * h + i) * G::PB + n];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < G::TN; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi][i], b[ni][i], acc[mi][ni], 0, 0, 0);
+    }
+  };
+
+  int kb = ctx.kb0;
+  if (kb < ctx.kb1) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; kb < ctx.kb1; ++kb) {
+    const bool more = kb + 1 < ctx.kb1;
+    if (more) gload(kb + 1);
+    compute(cur);
+    if (more) sstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+#pragma unroll
+  for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < G::TN; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+        P::store(args, ctx, wm * G::WTM + mi * 32 + row, wn * G::WTN + ni * 32 + r, acc[mi][ni][e]);
+      }
+
+  if constexpr (COLSUM) {
+    if (P::want_colsum(ctx)) {  // block-uniform
+      // the last loop barrier retired every LDS read: reuse the tile buffer
+      *reinterpret_cast<f32x4*>(lds + 4 * t) = csum;
+      __syncthreads();
+      if (t < G::BM) {
+        const int c4 = t >> 2, comp = t & 3;
+        float s = 0.f;
+        for (int g = 0; g < 256 / G::RA; ++g) s += lds[4 * (c4 + g * G::RA) + comp];  // fixed order
+        P::store_colsum(args, ctx, t, s);
+      }
+    }
+  }
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
+  __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
+  __shared__ typename P::Smem sm;
+  gemm_body<P>(args, blockIdx.x, lds, sm);
+}
+
+template <int A, int B>
+struct MaxI {
+  static constexpr int value = A > B ? A : B;
+};
+
+// Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
+// longer per-block problem starts early).
+template <class P1, class P2>
+__global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
+  __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
+  __shared__ union {
+    typename P1::Smem s1;
+    typename P2::Smem s2;
+  } sm;
+  if ((int)blockIdx.x < n1)
+    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
+  else
+    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+}
+
+__device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
+  return i == 0 ? s.p[0] : (i == 1 ? s.p[1] : s.p[2]);
+}
+
+// ------------------------------------------------------------------ forward policies
+struct Conv1Fwd {  // a1[m][n] = relu(sum_k frame(m, k) W1[n][k] + b1[n]), k = (c, ky, kx)
+  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = true;
+  using Args = F32Set;
+  struct Smem {
+    const uint8_t* pl[2][4];  // frame planes of the (<= 2) samples the tile touches
+  };
+  struct Ctx {
+    F32Prob p;
+    int M, m0, s0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return (B * 400 + BM - 1) / BM; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem& sm) {
+    const int tp = tiles(a.B);
+    c.p = pick(a, block / tp);
+    c.M = a.B * 400;
+    c.m0 = (block % tp) * BM;
+    c.s0 = c.m0 / 400;
+    c.kb0 = 0;
+    c.kb1 = 256 / BK;
+    const int t = threadIdx.x;
+    if (t < 8) {
+      const int b = c.s0 + (t >> 2), ch = t & 3;
+      const FrameSrc f{static_cast<const uint8_t*>(c.p.in), c.p.ids, c.p.idx};
+      sm.pl[t >> 2][ch] = b < a.B ? frame_plane(f, b, ch, kPlane) : nullptr;
+    }
+  }
+  static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem& sm, int kb, int row, int ch) {
+    const int m = c.m0 + row;
+    if (m >= c.M) return zero4();
+    const int b = m / 400, p = m - b * 400, oy = p / 20, ox = p - oy * 20;
+    const int k = kb * BK + 4 * ch, cc = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+    const uint8_t* pl = sm.pl[b - c.s0][cc];
+    return u8x4(*reinterpret_cast<const uint32_t*>(pl + (4 * oy + ky) * 84 + 4 * ox + kx));
+  }
+  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    return ld4(c.p.w + n * 256 + kb * BK + 4 * ch);
+  }
+  static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
+    const int m = c.m0 + ml;
+    if (m < c.M) c.p.out[(size_t)m * 32 + n] = fmaxf(v + c.p.bias[n], 0.f);
+  }
+};
+
+struct Conv2Fwd {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci), one tap per k-block
+  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = F32Set;
+  using Smem = NoSmem;
+  struct Ctx {
+    F32Prob p;
+    int M, m0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return (B * 81 + BM - 1) / BM; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tp = tiles(a.B);
+    c.p = pick(a, block / tp);
+    c.M = a.B * 81;
+    c.m0 = (block % tp) * BM;
+    c.kb0 = 0;
+    c.kb1 = 16;
+  }
+  static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int m = c.m0 + row;
+    if (m >= c.M) return zero4();
+    const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9, ky = kb >> 2, kx = kb & 3;
+    const float* in = static_cast<const float*>(c.p.in);
+    return ld4(in + ((size_t)b * 400 + (2 * oy + ky) * 20 + 2 * ox + kx) * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    const float* w = c.p.w + n * 512 + (4 * ch) * 16 + kb;  // reference [co][ci][ky][kx]
+    return f32x4{w[0], w[16], w[32], w[48]};
+  }
+  static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
+    const int m = c.m0 + ml;
+    if (m < c.M) c.p.out[(size_t)m * 64 + n] = fmaxf(v + c.p.bias[n], 0.f);
+  }
+};
+
+struct Conv3Fwd {  // a3 = relu(conv(a2, W3) + b3); k-block = half a tap (32 channels)
+  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = F32Set;
+  using Smem = NoSmem;
+  struct Ctx {
+    F32Prob p;
+    int M, m0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return (B * 49 + BM - 1) / BM; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tp = tiles(a.B);
+    c.p = pick(a, block / tp);
+    c.M = a.B * 49;
+    c.m0 = (block % tp) * BM;
+    c.kb0 = 0;
+    c.kb1 = 18;
+  }
+  static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int m = c.m0 + row;
+    if (m >= c.M) return zero4();
+    const int b = m / 49, p = m - b * 49, oy = p / 7, ox = p - oy * 7;
+    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3, ci = (kb & 1) * 32 + 4 * ch;
+    const float* in = static_cast<const float*>(c.p.in);
+    return ld4(in + ((size_t)b * 81 + (oy + ky) * 9 + ox + kx) * 64 + ci);
+  }
+  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    const int tap = kb >> 1, ci = (kb & 1) * 32 + 4 * ch;
+    const float* w = c.p.w + n * 576 + ci * 9 + tap;
+    return f32x4{w[0], w[9], w[18], w[27]};
+  }
+  static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
+    const int m = c.m0 + ml;
+    if (m < c.M) c.p.out[(size_t)m * 64 + n] = fmaxf(v + c.p.bias[n], 0.f);
+  }
+};
+
+constexpr int kFcSplits = 7;  // FC1 forward split-K: 3136 = 7 x 448
+struct Fc1Fwd {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] W[n][k'(ref)], k' = p*64 + c
+  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  static constexpr int KBS = 3136 / BK / kFcSplits;  // 14 k-blocks per split
+  using Args = F32Set;
+  using Smem = NoSmem;
+  struct Ctx {
+    F32Prob p;
+    int B, m0, n0, split, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * 4 * kFcSplits; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tp = tiles(a.B);
+    c.p = pick(a, block / tp);
+    int t = block % tp;
+    c.B = a.B;
+    c.n0 = (t & 3) * BN;
+    t >>= 2;
+    c.split = t % kFcSplits;
+    c.m0 = (t / kFcSplits) * BM;
+    c.kb0 = c.split * KBS;
+    c.kb1 = c.kb0 + KBS;
+  }
+  static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = c.m0 + row;
+    if (b >= c.B) return zero4();
+    return ld4(static_cast<const float*>(c.p.in) + (size_t)b * 3136 + kb * BK + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int nl, int ch) {
+    const int n = c.n0 + nl, k = kb * BK + 4 * ch, p = k >> 6, co = k & 63;
+    const float* w = (n < 128 ? c.p.w + n * 3136 : c.p.w2 + (n - 128) * 3136) + co * 49 + p;
+    return f32x4{w[0], w[49], w[98], w[147]};
+  }
+  static __device__ void store(const Args&, const Ctx& c, int ml, int nl, float v) {
+    const int b = c.m0 + ml;
+    if (b < c.B) c.p.out[((size_t)c.split * c.B + b) * 256 + c.n0 + nl] = v;
+  }
+};
+
+// ------------------------------------------------------------------ backward policies
+struct BwdArgs {
+  const void* x;        // layer input (u8 frames for conv1: FrameSrc fields)
+  const int* ids;
+  const int* idx;
+  const float* dy;      // gradient w.r.t. the layer's (post-ReLU-masked) output
+  const float* w;       // reference weights
+  const float* w2;      // FC1 value weights
+  const float* mask;    // post-ReLU activation of the layer below (dgrad ReLU backward)
+  float* out;           // dgrad output | wgrad partials / FC1 advantage grad
+  float* out2;          // wgrad bias partials | FC1 value grad
+  int B;
+  int kbps;             // wgrad: k-blocks per split
+  int splits;
+};
+
+struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] W[n][k'(ref)]
+  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = false, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int m0, n0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * 49; }
+  static __device__ void decode(const Args&, int block, Ctx& c, Smem&) {
+    c.n0 = (block % 49) * BN;
+    c.m0 = (block / 49) * BM;
+    c.kb0 = 0;
+    c.kb1 = 256 / BK;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = c.m0 + row;
+    if (b >= a.B) return zero4();
+    return ld4(a.dy + (size_t)b * 256 + kb * BK + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int n = kb * BK + row, k = c.n0 + 4 * ch, p = k >> 6, co = k & 63;
+    const float* w = (n < 128 ? a.w + n * 3136 : a.w2 + (n - 128) * 3136) + co * 49 + p;
+    return f32x4{w[0], w[49], w[98], w[147]};
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
+    const int b = c.m0 + ml;
+    if (b >= a.B) return;
+    const size_t o = (size_t)b * 3136 + c.n0 + nl;
+    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
+  }
+};
+
+struct Fc1Wgrad {  // dW[n][k(ref) = c*49 + p] = sum_b dz[b][n] a3[b][p*64 + c]
+  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int m0, n0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int) { return 4 * 49; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    c.n0 = (block % 49) * BN;
+    c.m0 = (block / 49) * BM;
+    c.kb0 = 0;
+    c.kb1 = (a.B + BK - 1) / BK;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = kb * BK + row;
+    if (b >= a.B) return zero4();
+    return ld4(a.dy + (size_t)b * 256 + c.m0 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = kb * BK + row;
+    if (b >= a.B) return zero4();
+    const float* a3 = static_cast<const float*>(a.x) + (size_t)b * 3136;
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = c.n0 + 4 * ch + i, co = k / 49, p = k - co * 49;
+      v[i] = a3[p * 64 + co];
+    }
+    return v;
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
+    const int n = c.m0 + ml, k = c.n0 + nl;
+    if (n < 128) a.out[n * 3136 + k] = v;
+    else a.out2[(n - 128) * 3136 + k] = v;
+  }
+};
+
+// conv wgrad (layers 2, 3): part[s][co][tap*C + ci] = sum_{r in split s} dy[r][co] x_col[r][tap, ci]
+template <int L>
+struct ConvWgrad {
+  static constexpr int C = L == 3 ? 64 : 32, K = L == 3 ? 3 : 4, S = L == 3 ? 1 : 2;
+  static constexpr int IH = L == 3 ? 9 : 20, OH = L == 3 ? 7 : 9, P = OH * OH;
+  static constexpr int N = K * K * C;
+  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false, A_COLSUM = true;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int n0, split, kb0, kb1, R;
+  };
+  static __host__ __device__ int tiles(int, int splits) { return (N / BN) * splits; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    c.split = block / (N / BN);
+    c.n0 = (block % (N / BN)) * BN;
+    c.R = a.B * P;
+    c.kb0 = c.split * a.kbps;
+    c.kb1 = min(c.kb0 + a.kbps, (c.R + BK - 1) / BK);
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int r = kb * BK + row;
+    if (r >= c.R) return zero4();
+    return ld4(a.dy + (size_t)r * 64 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int r = kb * BK + row;
+    if (r >= c.R) return zero4();
+    const int b = r / P, p = r - b * P, oy = p / OH, ox = p - oy * OH;
+    const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
+    const float* x = static_cast<const float*>(a.x);
+    return ld4(x + ((size_t)b * IH * IH + (S * oy + ky) * IH + S * ox + kx) * C + ci);
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
+    a.out[((size_t)c.split * 64 + m) * N + c.n0 + nl] = v;
+  }
+  static __device__ bool want_colsum(const Ctx& c) { return c.n0 == 0; }
+  static __device__ void store_colsum(const Args& a, const Ctx& c, int m, float v) {
+    a.out2[c.split * 64 + m] = v;
+  }
+};
+
+struct Conv1Wgrad {  // part[s][co][k = (c, ky, kx)] = sum_r dy1[r][co] frame(r, k)
+  static constexpr int BM = 32, BN = 128, BK = 32, WM = 1;
+  static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = true, A_COLSUM = true;
+  static constexpr int kMaxSamples = 8;
+  using Args = BwdArgs;
+  struct Smem {
+    const uint8_t* pl[kMaxSamples][4];
+  };
+  struct Ctx {
+    int n0, split, kb0, kb1, R, b0;
+  };
+  static __host__ __device__ int tiles(int, int splits) { return 2 * splits; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem& sm) {
+    c.split = block >> 1;
+    c.n0 = (block & 1) * BN;
+    c.R = a.B * 400;
+    c.kb0 = c.split * a.kbps;
+    c.kb1 = min(c.kb0 + a.kbps, (c.R + BK - 1) / BK);
+    c.b0 = (c.kb0 * BK) / 400;
+    const int t = threadIdx.x;
+    if (t < kMaxSamples * 4) {
+      const int b = c.b0 + (t >> 2), ch = t & 3;
+      const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
+      sm.pl[t >> 2][ch] = b < a.B ? frame_plane(f, b, ch, kPlane) : nullptr;
+    }
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int r = kb * BK + row;
+    if (r >= c.R) return zero4();
+    return ld4(a.dy + (size_t)r * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem& sm, int kb, int row, int ch) {
+    const int r = kb * BK + row;
+    if (r >= c.R) return zero4();
+    const int b = r / 400, p = r - b * 400, oy = p / 20, ox = p - oy * 20;
+    const int k = c.n0 + 4 * ch, cc = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
+    const uint8_t* pl = sm.pl[b - c.b0][cc];
+    return u8x4(*reinterpret_cast<const uint32_t*>(pl + (4 * oy + ky) * 84 + 4 * ox + kx));
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
+    a.out[((size_t)c.split * 32 + m) * 256 + c.n0 + nl] = v;
+  }
+  static __device__ bool want_colsum(const Ctx& c) { return c.n0 == 0; }
+  static __device__ void store_colsum(const Args& a, const Ctx& c, int m, float v) {
+    a.out2[c.split * 32 + m] = v;
+  }
+};
+
+struct Conv3Dgrad {  // dy2[b][pi][ci] = (a2 > 0) * sum_{tap, co} dy3[b][pi - tap][co] W3[co][ci][tap]
+  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int M, m0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return (B * 81 + BM - 1) / BM; }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    c.M = a.B * 81;
+    c.m0 = block * BM;
+    c.kb0 = 0;
+    c.kb1 = 18;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int m = c.m0 + row;
+    if (m >= c.M) return zero4();
+    const int b = m / 81, pi = m - b * 81, iy = pi / 9, ix = pi - iy * 9;
+    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3, oy = iy - ky, ox = ix - kx;
+    if (oy < 0 || oy >= 7 || ox < 0 || ox >= 7) return zero4();
+    return ld4(a.dy + ((size_t)b * 49 + oy * 7 + ox) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx&, const Smem&, int kb, int n, int ch) {
+    const int tap = kb >> 1, co = (kb & 1) * 32 + 4 * ch;
+    const float* w = a.w + co * 576 + n * 9 + tap;
+    return f32x4{w[0], w[576], w[1152], w[1728]};
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
+    const int m = c.m0 + ml;
+    if (m >= c.M) return;
+    const size_t o = (size_t)m * 64 + n;
+    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
+  }
+};
+
+// conv2 dgrad as 4 stride-1 sub-pixel problems: input pixel (iy, ix) = (2jy + py, 2jx + px)
+// receives taps ky = py + 2ty, kx = px + 2tx from output pixel (jy - ty, jx - tx)
+struct Conv2Dgrad {
+  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int M, m0, cls, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return 4 * ((B * 100 + BM - 1) / BM); }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tc = (a.B * 100 + BM - 1) / BM;
+    c.cls = block / tc;
+    c.m0 = (block % tc) * BM;
+    c.M = a.B * 100;
+    c.kb0 = 0;
+    c.kb1 = 8;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int m = c.m0 + row;
+    if (m >= c.M) return zero4();
+    const int b = m / 100, j = m - b * 100, jy = j / 10, jx = j - jy * 10;
+    const int t = kb >> 1, oy = jy - (t >> 1), ox = jx - (t & 1);
+    if (oy < 0 || oy >= 9 || ox < 0 || ox >= 9) return zero4();
+    return ld4(a.dy + ((size_t)b * 81 + oy * 9 + ox) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    const int t = kb >> 1, ky = (c.cls >> 1) + 2 * (t >> 1), kx = (c.cls & 1) + 2 * (t & 1);
+    const int co = (kb & 1) * 32 + 4 * ch;
+    const float* w = a.w + co * 512 + n * 16 + ky * 4 + kx;
+    return f32x4{w[0], w[512], w[1024], w[1536]};
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
+    const int m = c.m0 + ml;
+    if (m >= c.M) return;
+    const int b = m / 100, j = m - b * 100, jy = j / 10, jx = j - jy * 10;
+    const int iy = 2 * jy + (c.cls >> 1), ix = 2 * jx + (c.cls & 1);
+    const size_t o = ((size_t)b * 400 + iy * 20 + ix) * 32 + n;
+    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
+  }
+};
+
+// wgrad split sizing: ~target blocks over (n-tiles x splits)
+struct SplitPlan {
+  int splits, kbps;
+};
+SplitPlan plan_splits(int rows, int ntiles, int target_blocks, int max_kbps) {
+  const int kbt = (rows + 31) / 32;
+  int s = std::max(1, target_blocks / ntiles);
+  int kbps = (kbt + s - 1) / s;
+  if (kbps > max_kbps) kbps = max_kbps;
+  if (kbps < 1) kbps = 1;
+  s = (kbt + kbps - 1) / kbps;
+  return {s, kbps};
+}
+
+SplitPlan wgrad_plan(int layer, int B) {
+  switch (layer) {
+    case 1: return plan_splits(B * 400, 2, 512, 60);  // <= 60*32 rows -> <= 6 samples per split
+    case 2: return plan_splits(B * 81, 8, 256, 1 << 20);
+    case 3: return plan_splits(B * 49, 9, 252, 1 << 20);
+    default: throw std::invalid_argument("f32 wgrad layer");
+  }
+}
+
+template <class P>
+void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
+  if (blocks <= 0) return;
+  gemm_k<P><<<blocks, 256, 0, s>>>(a);
+  LAUNCH_CHECK();
+}
+
+template <class P1, class P2>
+void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
+  if (n1 + n2 <= 0) return;
+  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  LAUNCH_CHECK();
+}
+
+void check_set(const F32Set& set) {
+  if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("f32: 1..3 problems");
+  if (set.B <= 0) throw std::invalid_argument("f32: B must be positive");
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host launchers
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
+  check_set(set);
+  switch (layer) {
+    case 1: launch1<Conv1Fwd>(set, set.n * Conv1Fwd::tiles(set.B), s); break;
+    case 2: launch1<Conv2Fwd>(set, set.n * Conv2Fwd::tiles(set.B), s); break;
+    case 3: launch1<Conv3Fwd>(set, set.n * Conv3Fwd::tiles(set.B), s); break;
+    default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
+  }
+}
+
+int f32_fc1_splits() { return kFcSplits; }
+
+int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
+  check_set(set);
+  launch1<Fc1Fwd>(set, set.n * Fc1Fwd::tiles(set.B), s);
+  return kFcSplits;
+}
+
+void f32_fc1_bwd(const float* dz, const float* a3, const float* w_adv, const float* w_val, float* dy3, float* g_adv,
+                 float* g_val, int B, hipStream_t s) {
+  if (B <= 0) return;
+  BwdArgs d{};
+  d.dy = dz;
+  d.w = w_adv;
+  d.w2 = w_val;
+  d.mask = a3;
+  d.out = dy3;
+  d.B = B;
+  BwdArgs w{};
+  w.x = a3;
+  w.dy = dz;
+  w.out = g_adv;
+  w.out2 = g_val;
+  w.B = B;
+  launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B), d, Fc1Dgrad::tiles(B), s);
+}
+
+int f32_wgrad_splits(int layer, int B) { return wgrad_plan(layer, B).splits; }
+
+size_t f32_wgrad_workspace_floats(int layer, int B) {
+  const SplitPlan p = wgrad_plan(layer, B);
+  const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
+  const size_t cout = layer == 1 ? 32 : 64;
+  return (size_t)p.splits * (per + cout);
+}
+
+// wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
+void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s) {
+  if (B <= 0) return;
+  const SplitPlan p = wgrad_plan(layer, B);
+  const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
+  BwdArgs g{};
+  g.x = x;
+  g.ids = ids;
+  g.idx = idx;
+  g.dy = dy;
+  g.out = ws;
+  g.out2 = ws + (size_t)p.splits * per;
+  g.B = B;
+  g.kbps = p.kbps;
+  g.splits = p.splits;
+  BwdArgs d{};
+  d.dy = dy;
+  d.w = w;
+  d.mask = mask;
+  d.out = dx;
+  d.B = B;
+  switch (layer) {
+    case 3:
+      launch2<ConvWgrad<3>, Conv3Dgrad>(g, ConvWgrad<3>::tiles(B, p.splits), d, Conv3Dgrad::tiles(B), s);
+      break;
+    case 2:
+      launch2<ConvWgrad<2>, Conv2Dgrad>(g, ConvWgrad<2>::tiles(B, p.splits), d, Conv2Dgrad::tiles(B), s);
+      break;
+    case 1:
+      launch1<Conv1Wgrad>(g, Conv1Wgrad::tiles(B, p.splits), s);
+      break;
+    default: throw std::invalid_argument("f32_conv_bwd: layer must be 1, 2 or 3");
+  }
+}
+
+FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad) {
+  const SplitPlan p = wgrad_plan(layer, B);
+  FinalizeJob j{};
+  j.kind = 0;
+  j.G = p.splits;
+  j.part = ws;
+  const int cout = layer == 1 ? 32 : 64;
+  const int K = layer == 1 ? 256 : (layer == 2 ? 512 : 576);
+  j.pstride = cout * K;
+  j.bpart = ws + (size_t)p.splits * cout * K;
+  j.bstride = cout;
+  j.n_main = cout * K;
+  j.n_bias = cout;
+  if (layer == 1) {  // partials already in the reference [co][c][ky][kx] order
+    j.C = 1;
+    j.KH = 1;
+    j.KW = 256;
+  } else {  // [co][ky][kx][ci] -> reference [co][ci][ky][kx]
+    j.C = layer == 2 ? 32 : 64;
+    j.KH = j.KW = layer == 2 ? 4 : 3;
+  }
+  j.out[0] = grad;
+  j.out[1] = bias_grad;
+  return j;
+}
+
+FinalizeJob norm_only_job(const float* g, int n) {
+  FinalizeJob j{};
+  j.kind = 3;
+  j.G = 1;
+  j.part = g;
+  j.pstride = 0;
+  j.n_main = n;
+  j.n_bias = 0;
+  return j;
+}
+
+}  // namespace apex

@@ -403,11 +403,12 @@ PYBIND11_MODULE(_apex_hip, m) {
     a.delta = P<float>(g("delta"));
     a.lw = P<float>(g("lw"));
     a.dz_bf = P<uint16_t>(g("dz_bf"));
+    a.dz = P<float>(g("dz"));
     a.part = P<float>(g("part"));
     a.step = P<const int64_t>(g("step"));
     a.step_snap = P<int64_t>(g("step_snap"));
     if (!a.q || !a.q2 || !a.q2t || !a.act || !a.rew || !a.done || !a.w || !a.h || !a.w_adv2 || !a.w_val2 ||
-        !a.delta || !a.lw || !a.dz_bf || !a.part || !a.step)
+        !a.delta || !a.lw || !(a.dz_bf || a.dz) || !a.part || !a.step)
       throw std::invalid_argument("dqn_heads_bwd: missing pointer");
     dqn_heads_bwd(a, S(s));
   });
@@ -419,6 +420,43 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("pack_conv_wt", [](uint64_t src, uint64_t dst, int N, int C, int KH, int KW, uint64_t s) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));
   });
+  // ---- fp32 (reference-precision) network kernels (f32_kernels.hip)
+  auto f32set = [](const std::vector<std::array<uint64_t, 7>>& probs, int B) {
+    if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
+    F32Set set{};
+    for (size_t i = 0; i < probs.size(); ++i) {
+      const auto& t = probs[i];
+      set.p[i] = F32Prob{P<const void>(t[0]), P<const int>(t[1]), P<const int>(t[2]), P<const float>(t[3]),
+                         P<const float>(t[4]), P<const float>(t[5]), P<float>(t[6])};
+    }
+    set.n = (int)probs.size();
+    set.B = B;
+    return set;
+  };
+  // probs: (in, ids, idx, w, w2, bias, out)
+  m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::array<uint64_t, 7>>& probs, int B,
+                                       uint64_t s) { f32_conv_fwd_multi(layer, f32set(probs, B), S(s)); });
+  m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::array<uint64_t, 7>>& probs, int B, uint64_t s) {
+    return f32_fc1_fwd_multi(f32set(probs, B), S(s));
+  });
+  m.def("f32_fc1_splits", &f32_fc1_splits);
+  m.def("f32_fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wa, uint64_t wv, uint64_t dy3, uint64_t ga, uint64_t gv,
+                          int B, uint64_t s) {
+    f32_fc1_bwd(P<const float>(dz), P<const float>(a3), P<const float>(wa), P<const float>(wv), P<float>(dy3),
+                P<float>(ga), P<float>(gv), B, S(s));
+  });
+  m.def("f32_wgrad_splits", &f32_wgrad_splits);
+  m.def("f32_wgrad_workspace_floats", &f32_wgrad_workspace_floats);
+  m.def("f32_conv_bwd", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t w, uint64_t mask,
+                           uint64_t dx, uint64_t ws, int B, uint64_t s) {
+    f32_conv_bwd(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const float>(dy), P<const float>(w),
+                 P<const float>(mask), P<float>(dx), P<float>(ws), B, S(s));
+  });
+  m.def("f32_conv_finalize_job", [](int layer, int B, uint64_t ws, uint64_t grad, uint64_t bgrad) {
+    return f32_conv_finalize_job(layer, B, P<const float>(ws), P<float>(grad), P<float>(bgrad));
+  });
+  m.def("norm_only_job", [](uint64_t g, int n) { return norm_only_job(P<const float>(g), n); });
+
   // A stream on its OWN hardware queue: a CU-masked stream always gets a dedicated HSA
   // queue (the mask is a queue property), here with every CU enabled.  Plain streams of
   // one priority are spread round-robin over GPU_MAX_HW_QUEUES (4) shared queues, where

@@ -186,6 +186,7 @@ struct LossHeadsArgs {
   float* lw;                       // [B] out: w * Huber(delta)
   uint16_t* dz_bf;                 // [B][256] out: dL/dz (FC1 pre-activation), bf16
   float* part;                     // [blocks][(A+1)*128 + (A+1) + 256] out: gradient partials
+  float* dz;                       // [B][256] out (optional, replaces dz_bf): dL/dz in fp32
   const int64_t* step;             // learner step counter (read)
   int64_t* step_snap;              // out: its value for this step's optimizer (may be null)
 };
@@ -335,6 +336,38 @@ void pack_conv_wt(const float* src, uint16_t* dst, int N, int C, int KH, int KW,
 void conv1_fwd_multi(const ConvSet& set, hipStream_t s);
 void conv1_fwd(const uint8_t* frames, const int* ids, const int* idx, const uint16_t* w, const float* bias,
                uint16_t* out, int B, hipStream_t s);
+
+// ---- f32_kernels.hip: reference-precision (fp32 MFMA) dueling net, fp32 activations
+// channels-last, reference-layout fp32 weights (no packed copies)
+struct F32Prob {
+  const void* in;     // layer input: u8 frames (conv1, FrameSrc with ids/idx) or fp32 activations
+  const int* ids;
+  const int* idx;
+  const float* w;     // reference weights (FC1: advantage.0.weight)
+  const float* w2;    // FC1: value.0.weight
+  const float* bias;
+  float* out;         // activations (conv) | split-K partials [7][B][256] (FC1)
+};
+struct F32Set {
+  F32Prob p[kMaxProbs];
+  int n, B;
+};
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
+int f32_fc1_splits();
+int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
+// FC1 backward in one launch: dy3 = (a3 > 0) * dz . W (channels-last order) and the
+// reference-layout weight gradients written straight into g_adv / g_val
+void f32_fc1_bwd(const float* dz, const float* a3, const float* w_adv, const float* w_val, float* dy3, float* g_adv,
+                 float* g_val, int B, hipStream_t s);
+int f32_wgrad_splits(int layer, int B);
+size_t f32_wgrad_workspace_floats(int layer, int B);
+// conv backward: layers 3/2 = wgrad partials + dgrad (masked by `mask`) in one launch,
+// layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
+void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s);
+FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
+// grad_finalize job that only adds sum(g^2) of g[0..n) to the norm partials
+FinalizeJob norm_only_job(const float* g, int n);
 
 // ---- aql_kernels.hip (AQL candidate critic / proposal)
 struct AQLNet {

@@ -1,0 +1,151 @@
+"""Reference-precision (fp32 MFMA) network kernels vs plain PyTorch references.
+
+Every layer of ``F32DuelingNet`` (f32_kernels.hip) is compared with an fp64 PyTorch
+reference computed from the SAME layer input (the previous kernel's output), so each
+kernel's own error is measured: fp32 accumulation over K <= 3136 stays far below the
+rtol 1e-4 per layer / 1e-3 per parameter gradient required here."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, A=18, seed=0):
+    from apex_amd.models.dqn import DuelingDQN
+
+    torch.manual_seed(seed)
+    m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
+    with torch.no_grad():  # random biases: the reference init zeroes them
+        for mod in list(m.features) + list(m.advantage) + list(m.value):
+            if getattr(mod, "bias", None) is not None:
+                mod.bias.uniform_(-0.1, 0.1)
+    m.flatten_parameters()
+    return m
+
+
+def _rel(got, ref):
+    return float((got.double() - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+
+
+def _nchw(t, B, C, H):
+    return t.view(B, H, H, C).permute(0, 3, 1, 2).double()
+
+
+@pytest.mark.parametrize("B", [37, 64])
+def test_f32_layers_match_fp64(cuda, B):
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    m = _model(cuda)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, 18, cuda, keep_for_backward=True)
+    net(x, ws)
+    torch.cuda.synchronize()
+    f = m.features
+    d = lambda t: t.detach().double()  # noqa: E731
+    r1 = F.relu(F.conv2d(x.double(), d(f[0].weight), d(f[0].bias), stride=4))
+    g1 = _nchw(ws.a1, B, 32, 20)
+    assert _rel(g1, r1) < 1e-5
+    r2 = F.relu(F.conv2d(g1, d(f[2].weight), d(f[2].bias), stride=2))
+    g2 = _nchw(ws.a2, B, 64, 9)
+    assert _rel(g2, r2) < 1e-5
+    r3 = F.relu(F.conv2d(g2, d(f[4].weight), d(f[4].bias), stride=1))
+    g3 = _nchw(ws.a3, B, 64, 7)
+    assert _rel(g3, r3) < 1e-5
+    hflat = g3.reshape(B, -1)
+    ha = F.relu(F.linear(hflat, d(m.advantage[0].weight), d(m.advantage[0].bias)))
+    hv = F.relu(F.linear(hflat, d(m.value[0].weight), d(m.value[0].bias)))
+    assert _rel(ws.h[:, :128], ha) < 1e-5 and _rel(ws.h[:, 128:], hv) < 1e-5
+    adv = F.linear(ha, d(m.advantage[2].weight), d(m.advantage[2].bias))
+    val = F.linear(hv, d(m.value[2].weight), d(m.value[2].bias))
+    q_ref = val + adv - adv.mean(1, keepdim=True)
+    torch.testing.assert_close(ws.q.double(), q_ref, rtol=1e-4, atol=1e-4 * float(q_ref.abs().max()))
+    # end to end against the fp32 module itself
+    with torch.no_grad():
+        q32 = m(x.float())
+    assert float((ws.q - q32).norm() / q32.norm()) < 1e-5
+
+
+def test_f32_frame_ring_and_multi_pass(cuda):
+    """conv1 reading the HBM frame ring by id (rows picked by idx) == dense input, and the
+    3-problem launch == three single launches (bit-identical)."""
+    from apex_amd.models.fused import forward_multi
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    m, mt = _model(cuda, A=6, seed=1), _model(cuda, A=6, seed=2)
+    net, tnet = F32DuelingNet(m), F32DuelingNet(mt)
+    B, F_ = 48, 300
+    frames = torch.randint(0, 256, (F_, 84 * 84), dtype=torch.uint8, device=cuda)
+    ids = torch.randint(0, F_, (100, 4), dtype=torch.int32, device=cuda)
+    idx = torch.randint(0, 100, (B,), dtype=torch.int32, device=cuda)
+    dense = frames[ids[idx.long()].long()].view(B, 4, 84, 84).contiguous()
+    wss = [F32Workspace(B, 6, cuda) for _ in range(3)]
+    forward_multi([(net, frames, wss[0], ids, idx), (net, dense, wss[1], None, None),
+                   (tnet, frames, wss[2], ids, idx)])
+    single = F32Workspace(B, 6, cuda)
+    tnet(dense, single)
+    torch.cuda.synchronize()
+    assert torch.equal(wss[0].q, wss[1].q)
+    assert torch.equal(wss[2].q, single.q)
+    with torch.no_grad():
+        assert float((wss[0].q - m(dense.float())).norm() / m(dense.float()).norm()) < 1e-5
+
+
+@pytest.mark.parametrize("B", [29, 128])
+def test_f32_backward_matches_fp64_autograd(cuda, B):
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    A = 18
+    m = _model(cuda, A=A, seed=3)
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+    net(x, ws)
+    dq = torch.randn(B, A, device=cuda) / B
+    # poison the grads: every parameter gradient must be written (no accumulate / no zeroing pass)
+    for p in m.parameters():
+        p.grad.fill_(float("nan"))
+    net.backward(dq, x, ws)
+    torch.cuda.synchronize()
+    m64 = _model(cuda, A=A, seed=3).double()
+    m64.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+    q = m64(x.double())
+    (q * dq.double()).sum().backward()
+    for (name, p), p64 in zip(m.named_parameters(), m64.parameters()):
+        ref = p64.grad
+        err = float((p.grad.double() - ref).norm() / ref.norm().clamp_min(1e-30))
+        assert err < 1e-4, (name, err)
+        torch.testing.assert_close(p.grad.double(), ref, rtol=1e-3, atol=1e-4 * float(ref.abs().max()),
+                                   msg=lambda s, n=name: f"{n}: {s}")
+
+
+def test_f32_finalize_norm_partials(cuda):
+    """trunk_backward's grad_finalize sum-of-squares partials cover every trunk + FC1
+    weight gradient (the FC1 weights through norm-only jobs)."""
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    B, A = 64, 6
+    m = _model(cuda, A=A, seed=4)
+    flat = m.flatten_parameters()
+    g = torch.zeros_like(flat)
+    off = 0
+    for p in m.parameters():
+        p.grad = g[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+    net(x, ws)
+    ws.dz.normal_()
+    ws.dz.mul_((ws.h > 0).float())
+    sumsq = torch.zeros(8192, dtype=torch.float64, device=cuda)
+    n = net.trunk_backward(x, ws, sumsq=sumsq)
+    torch.cuda.synchronize()
+    trunk = [m.features[i].weight.grad for i in (0, 2, 4)] + [m.features[i].bias.grad for i in (0, 2, 4)]
+    trunk += [m.advantage[0].weight.grad, m.value[0].weight.grad]
+    want = sum(float(t.double().pow(2).sum()) for t in trunk)
+    got = float(sumsq[:n].sum())
+    assert abs(got - want) <= 1e-6 * want
