@@ -97,7 +97,8 @@ class DistCfg:
 
 @dataclass
 class KernelCfg:
-    forward: str = "hip"             # "hip" (MFMA kernels) | "torch" (autocast/MIOpen path)
+    forward: str = "hip"             # "hip" (MFMA kernels) | "torch" (PyTorch modules)
+    dtype: str = "fp32"              # "fp32" (reference precision, learner.py:139-145) | "bf16" (opt-in)
     use_graphs: bool = True
     profile: bool = False            # roctx ranges around the engine phases (utils.trace)
     hip_debug: int = 0               # >0: AMD_LOG_LEVEL=<n> + blocking/serialised launches
@@ -225,7 +226,7 @@ EXTRA_FLAGS = [
     ("lr-step-size", "learner.lr_step_size", int), ("lr-gamma", "learner.lr_gamma", float),
     ("backend", "dist.backend", str), ("master-port", "dist.master_port", int),
     ("heartbeat-timeout", "dist.heartbeat_timeout", float),
-    ("forward", "kernel.forward", str), ("no-graphs", None, None), ("profile", "kernel.profile", int),
+    ("forward", "kernel.forward", str), ("dtype", "kernel.dtype", str), ("no-graphs", None, None), ("profile", "kernel.profile", int),
     ("hip-debug", "kernel.hip_debug", int),
 ]
 

@@ -31,7 +31,7 @@ import torch
 from .. import ops
 from ..models.dqn import DuelingDQN
 from ..utils import trace
-from ..models.fused import HipDuelingNet, NetWorkspace
+from ..models.fused import make_hip_net, make_workspace
 from .actor_shard import ActorShard
 from .hbm_replay import HBMReplay
 from .learner import DQNLearner, LearnerConfig, forward_q
@@ -161,8 +161,9 @@ class ApexEngine:
             p.grad = None
         self.hip_net = lc.forward == "hip"
         if self.hip_net:
-            self.actor_net = HipDuelingNet(self.actor_model)
-            self.actor_ws = NetWorkspace(cfg.n_envs, cfg.n_actions, self.device)
+            # actors act at the learner's precision (the reference's actors are fp32 too)
+            self.actor_net = make_hip_net(self.actor_model, lc.dtype)
+            self.actor_ws = make_workspace(cfg.n_envs, cfg.n_actions, self.device, lc.dtype)
             self.actor_ws.q = self.actor.q  # the heads kernel writes the actor's Q in place (no copy)
         self.publish_params()
         self.learn_steps = 0
@@ -198,7 +199,7 @@ class ApexEngine:
         else:
             obs = self.actor.observe()
             with torch.no_grad():
-                q = forward_q(self.actor_model, obs)
+                q = forward_q(self.actor_model, obs, self.cfg.learner.dtype == "bf16")
         self.actor.act_and_step(q, stage)
 
     def _actor_half(self, half: int):

@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.dqn import DuelingDQN
-from ..models.fused import HipDuelingNet, NetWorkspace
+from ..models.fused import make_hip_net, make_workspace
 from ..parallel.experience import ExperienceReceiver, ExperienceSender, Region, apply_packet, pack_meta
 from .actor_shard import ActorShard
 from .apex import EngineConfig
@@ -80,8 +80,8 @@ class CentralApexEngine:
             for p in model.parameters():
                 p.requires_grad_(False)
             self.model = model
-            self.net = HipDuelingNet(model)
-            self.ws = NetWorkspace(E, cfg.n_actions, self.device)
+            self.net = make_hip_net(model, cfg.learner.dtype)
+            self.ws = make_workspace(E, cfg.n_actions, self.device, cfg.learner.dtype)
             self.sender = ExperienceSender(E, FRAME_BYTES, self.device, dst=0)
             self.pkt_frames = torch.empty(E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
         self.broadcast_params()

@@ -173,11 +173,11 @@ class HBMReplay:
         self.sample_indices(batch_size, idx, w, counter, beta)
         s = torch.empty(batch_size, 4, 84, 84, dtype=torch.uint8, device=dev)
         s2 = torch.empty_like(s)
-        a = torch.empty(batch_size, dtype=torch.int64, device=dev)
+        a = torch.empty(batch_size, dtype=torch.int32, device=dev)  # gather_transitions_k writes int32
         r = torch.empty(batch_size, dtype=torch.float32, device=dev)
         d = torch.empty(batch_size, dtype=torch.float32, device=dev)
         self.gather(idx, s, s2, a, r, d)
-        return s, a, r, s2, d, w, idx
+        return s, a.long(), r, s2, d, w, idx
 
     def total_priority(self) -> float:
         return float(self.node_sum[-1][0].item())

@@ -4,7 +4,8 @@ One learner step (reference: learner.py:152-175 + utils.py:64-97 + the replay
 server's sample/update round trips over TCP) is, entirely on one HIP stream:
 
   per_sample (stratified PER, IS weights)  ->  gather s/s' u8 stacks from the frame ring
-  -> Q(s) with grad, Q(s'), Q_target(s')   (bf16 conv trunk, fp32 heads)
+  -> Q(s) with grad, Q(s'), Q_target(s')   (fp32 MFMA trunk by default = the reference's
+                                            precision; bf16-operand MFMA trunk opt-in)
   -> dqn_loss (double-DQN n-step Huber + IS weights + priorities + dL/dQ, one kernel)
   -> backward into ONE flat fp32 grad buffer  (-> optional RCCL all-reduce, DP)
   -> grad_sumsq + clip + centered RMSprop over the flat buffer (two kernels)
@@ -23,7 +24,7 @@ import torch
 
 from .. import ops
 from ..models.dqn import DuelingDQN
-from ..models.fused import HipDuelingNet, NetWorkspace, forward_multi
+from ..models.fused import DTYPES, forward_multi, make_hip_net, make_workspace
 from .hbm_replay import HBMReplay
 
 
@@ -42,7 +43,9 @@ class LearnerConfig:
     lr_step_offset: int = 0
     beta: float = 0.4
     optimizer: str = "rmsprop"     # or "adam"
-    forward: str = "torch"         # "torch" (MIOpen bf16 trunk) | "hip" (MFMA kernels)
+    forward: str = "torch"         # "torch" (PyTorch/MIOpen modules) | "hip" (hand-written MFMA kernels)
+    dtype: str = "fp32"            # compute precision: "fp32" (reference, learner.py:139-145: fp32 MFMA on the
+                                   # hip path, no autocast on the torch path) | "bf16" (opt-in fast mode)
     seed: int = 0
     tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
     bwd_fork: bool = False         # hip path: wgrad3/wgrad2 on a forked stream (measured slower: off)
@@ -53,9 +56,9 @@ class LearnerConfig:
                                    # kernels; lower latency, better when the tree write is inline)
 
 
-def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = True) -> torch.Tensor:
-    """Q = V + A - mean(A) with the conv trunk in bf16 (u8 frames are exact in bf16, the
-    reference feeds raw 0..255 values) and fp32 heads/output."""
+def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
+    """Q = V + A - mean(A) in fp32 (the reference feeds raw 0..255 values, SURVEY Q10);
+    ``bf16``: the conv trunk under bf16 autocast (u8 frames are exact in bf16), fp32 heads."""
     if bf16:
         with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
             h = model.features(x_u8.to(torch.bfloat16))
@@ -73,6 +76,9 @@ class DQNLearner:
     def __init__(self, model: DuelingDQN, replay: HBMReplay, cfg: LearnerConfig, allreduce=None, sharded=None):
         self.hip = ops.hip()
         self.cfg = cfg
+        if cfg.dtype not in DTYPES:
+            raise ValueError(f"LearnerConfig.dtype must be one of {DTYPES}, got {cfg.dtype!r}")
+        self.fp32 = cfg.dtype == "fp32"
         self.replay = replay
         self.device = replay.device
         self.model = model.to(self.device)
@@ -138,14 +144,15 @@ class DQNLearner:
         self.hip_net = cfg.forward == "hip"
         self.n_fin_partials = 0
         if self.hip_net:
-            self.net = HipDuelingNet(self.model)
+            self.net = make_hip_net(self.model, cfg.dtype)
             self.net.bwd_fork = cfg.bwd_fork
-            self.net.enable_backward()
-            self.tnet = HipDuelingNet(self.target)
-            self.pmap1, self.pmap2 = self.net.pack_maps()  # optimizer refreshes the packed bf16 weights
-            self.ws_s = NetWorkspace(B, A, dev, keep_for_backward=True)
-            self.ws_s2 = NetWorkspace(B, A, dev)
-            self.ws_t = NetWorkspace(B, A, dev)
+            self.net.enable_backward(B)
+            self.tnet = make_hip_net(self.target, cfg.dtype)
+            # bf16: the optimizer refreshes the packed bf16 weights; fp32 reads the master in place
+            self.pmap1, self.pmap2 = (None, None) if self.fp32 else self.net.pack_maps()
+            self.ws_s = make_workspace(B, A, dev, cfg.dtype, keep_for_backward=True)
+            self.ws_s2 = make_workspace(B, A, dev, cfg.dtype)
+            self.ws_t = make_workspace(B, A, dev, cfg.dtype)
             # fused loss + heads backward (dqn_heads_bwd) outputs; the priority-tree write
             # (which mixes the TD errors into priorities and forms the loss mean) runs on
             # a forked stream concurrently with the trunk backward
@@ -234,7 +241,8 @@ class DQNLearner:
                  "act": rp.action.data_ptr(), "rew": rp.reward.data_ptr(), "done": rp.done.data_ptr(),
                  "idx": self.idx.data_ptr(), "w": self.w.data_ptr(), "h": self.ws_s.h.data_ptr(),
                  "w_adv2": m.advantage[2].weight.data_ptr(), "w_val2": m.value[2].weight.data_ptr(),
-                 "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(), "dz_bf": self.ws_s.dz_bf.data_ptr(),
+                 "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(),
+                 ("dz" if self.fp32 else "dz_bf"): (self.ws_s.dz if self.fp32 else self.ws_s.dz_bf).data_ptr(),
                  "part": self.lh_part.data_ptr(), "step": self.step_counter.data_ptr(),
                  "step_snap": self.step_snap.data_ptr()}, self.B, self.A, self.gamma_n, s)
             heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
@@ -257,10 +265,11 @@ class DQNLearner:
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
             fn()
         self.replay.gather(self.idx, self.s, self.s2, self.a, self.r, self.d)
-        q = forward_q(self.model, self.s)
+        bf = not self.fp32
+        q = forward_q(self.model, self.s, bf)
         with torch.no_grad():
-            q2 = forward_q(self.model, self.s2)
-            q2t = forward_q(self.target, self.s2)
+            q2 = forward_q(self.model, self.s2, bf)
+            q2t = forward_q(self.target, self.s2, bf)
         q2 = q2.contiguous()
         q2t = q2t.contiguous()
         qd = q.detach().contiguous()
@@ -336,8 +345,9 @@ class DQNLearner:
         else:
             h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
             parts, nparts = self.partials, self.partials.numel()
-        pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if self.hip_net else (0, 0, 0)
-        fc = self.net.fc_pack_args() if self.hip_net else {}
+        packed = self.hip_net and not self.fp32
+        pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if packed else (0, 0, 0)
+        fc = self.net.fc_pack_args() if packed else {}
         step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
         # the fused path already bumped step_counter on the tree stream: the optimizer reads
         # this step's snapshot instead
@@ -391,5 +401,8 @@ class DQNLearner:
         ``grad_norm`` is the reference's logged value (sum_p ||g_p||^(1/2))^(1/2) of the last
         step's (pre-clip) gradient, ``grad_norm_l2`` the true global L2 used for clipping."""
         n = self.norms.tolist()
-        ref = sum(self.flat_grad[o:o + k].norm().item() ** 0.5 for _, o, k in self.segments) ** 0.5
+        # under data parallelism flat_grad holds the all-reduced SUM; the optimizer applies
+        # the 1/world mean (grad_scale) in-kernel, so scale the logged norm the same way
+        sc = float(self.hp.grad_scale) if self.allreduce is not None else 1.0
+        ref = sum((sc * self.flat_grad[o:o + k].norm().item()) ** 0.5 for _, o, k in self.segments) ** 0.5
         return {"loss": float(self.loss.item()), "grad_norm_l2": n[0], "grad_norm": ref, "clip": n[2], "lr": n[3]}

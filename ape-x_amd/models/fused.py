@@ -167,8 +167,9 @@ class HipDuelingNet:
             h.pack_conv_wt(f[4].weight.data_ptr(), self.w3t.data_ptr(), 64, 64, 3, 3, s)
             self.wfc1t.copy_(self.wfc1p.t())
 
-    def enable_backward(self) -> None:
-        """Allocate backward workspaces + transposed weights (call before graph capture).
+    def enable_backward(self, B: int | None = None) -> None:
+        """Allocate backward workspaces + transposed weights (call before graph capture;
+        ``B`` is unused: the bf16 workspaces are sized for any batch).
         One wgrad partial workspace per conv layer: the three layers' partials are reduced
         together by one grad_finalize launch at the end of the backward."""
         self._wgrad_wss = [torch.empty(self.hip.wgrad_workspace_floats(k), dtype=torch.float32, device=self.device)

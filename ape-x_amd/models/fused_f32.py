@@ -58,6 +58,7 @@ class F32DuelingNet:
 
     fp32 = True
     arena = None
+    bwd_fork = False  # the bf16 net's side-stream wgrad option; the fp32 backward pairs wgrad+dgrad per launch
 
     def __init__(self, model: DuelingDQN):
         assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
@@ -137,6 +138,43 @@ class F32DuelingNet:
                                            m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
                                            m.value[0].bias.grad.data_ptr())
 
+    def _fc1_bwd(self, ws: F32Workspace) -> None:
+        m = self.model
+        self.hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), m.advantage[0].weight.data_ptr(),
+                             m.value[0].weight.data_ptr(), ws.dy3.data_ptr(), m.advantage[0].weight.grad.data_ptr(),
+                             m.value[0].weight.grad.data_ptr(), ws.B, self._s())
+
+    def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None) -> list:
+        """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch); returns the
+        finalize jobs of the three layers."""
+        B = ws.B
+        h, s, f = self.hip, self._s(), self.model.features
+        xp, ip, jp = self._src(x, ids, idx, B)
+        w1, w2, w3 = self._wgrad_wss
+        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), f[4].weight.data_ptr(), ws.a2.data_ptr(),
+                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
+        if after_first is not None:
+            after_first()
+        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), f[2].weight.data_ptr(), ws.a1.data_ptr(),
+                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
+        h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
+        return [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
+                                        f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
+
+    def fc_backward(self, ws: F32Workspace, extra_jobs=()) -> None:
+        """Data-parallel split, part 1: the FC1 backward (its weight gradients are written in
+        place) + the finalize of ``extra_jobs`` (the heads), so the FC1/head all-reduce can
+        start while :meth:`conv_backward` runs."""
+        self.enable_backward(ws.B)
+        self._fc1_bwd(ws)
+        if extra_jobs:
+            self.hip.grad_finalize(list(extra_jobs), self._s(), 0)
+
+    def conv_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
+                      idx: torch.Tensor | None = None, after_first=None) -> None:
+        """Data-parallel split, part 2: conv3..conv1 backward + their finalize."""
+        self.hip.grad_finalize(self._conv_chain(x, ws, ids, idx, after_first), self._s(), 0)
+
     def trunk_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
                        idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None,
                        after_first=None) -> int:
@@ -145,27 +183,16 @@ class F32DuelingNet:
         per-workgroup sum-of-squares partials of EVERY gradient into ``sumsq`` (fp64) when
         given (the FC1 weight gradients, written in place, join through norm-only jobs);
         returns the partial count.  ``after_first()`` runs right after the first launch."""
-        B = ws.B
-        self.enable_backward(B)
-        h, s, m, f = self.hip, self._s(), self.model, self.model.features
-        ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
-        h.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), m.advantage[0].weight.data_ptr(),
-                      m.value[0].weight.data_ptr(), ws.dy3.data_ptr(), ga.data_ptr(), gv.data_ptr(), B, s)
+        self.enable_backward(ws.B)
+        self._fc1_bwd(ws)
         if after_first is not None:
             after_first()
-        xp, ip, jp = self._src(x, ids, idx, B)
-        w1, w2, w3 = self._wgrad_wss
-        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), f[4].weight.data_ptr(), ws.a2.data_ptr(),
-                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
-        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), f[2].weight.data_ptr(), ws.a1.data_ptr(),
-                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
-        h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
-        jobs = [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
-                                        f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
-        jobs += list(extra_jobs)
+        h, m = self.hip, self.model
+        ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs)
         if sumsq is not None:
             jobs += [h.norm_only_job(ga.data_ptr(), ga.numel()), h.norm_only_job(gv.data_ptr(), gv.numel())]
-        return h.grad_finalize(jobs, s, 0 if sumsq is None else sumsq.data_ptr())
+        return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr())
 
 
 def forward_multi_f32(passes, act: tuple | None = None) -> None:

@@ -47,16 +47,30 @@ def parser():
 
 
 # ------------------------------------------------------------------ checkpoint
+def _weights_tag(flat: torch.Tensor) -> torch.Tensor:
+    """Cheap fingerprint of the model weights (fp64 sum, sum of squares, a strided sample)
+    stored in the sidecar: ``load_engine`` only restores optimizer moments / counters that
+    belong to the model file it loaded."""
+    f = flat.detach().double().cpu()
+    return torch.cat([f.sum().view(1), f.pow(2).sum().view(1), f[:: max(1, f.numel() // 61)][:61]])
+
+
 def _learner_state(learner, counters: dict) -> dict:
     return {"opt_s1": learner.opt_s1.cpu(), "opt_s2": learner.opt_s2.cpu(),
             "step_counter": learner.step_counter.cpu(), "target_flat": learner.tflat.cpu(),
-            "counters": dict(counters)}
+            "counters": dict(counters), "weights_tag": _weights_tag(learner.flat)}
 
 
 def save_engine(learner, path: str, counters: dict) -> None:
-    """model.pth (the reference state_dict: enjoy.py / load_model read it) + sidecar."""
+    """model.pth (the reference state_dict: enjoy.py / load_model read it) + sidecar.  The
+    sidecar goes first, through tmp + os.replace like the model file, and carries a
+    fingerprint of the weights: a kill between the two writes leaves a sidecar that
+    ``load_engine`` recognises as belonging to a different model file."""
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    side = sidecar_path(path)
+    torch.save(_learner_state(learner, counters), side + ".tmp")
+    os.replace(side + ".tmp", side)
     save_model(learner.model, path)
-    torch.save(_learner_state(learner, counters), sidecar_path(path))
 
 
 def load_engine(learner, path: str) -> dict:
@@ -65,8 +79,14 @@ def load_engine(learner, path: str) -> dict:
     learner.model.load_state_dict(sd)   # parameters are views of the flat buffer
     counters = {}
     side = sidecar_path(path)
-    if os.path.exists(side):
-        st = torch.load(side, map_location="cpu", weights_only=True)
+    st = torch.load(side, map_location="cpu", weights_only=True) if os.path.exists(side) else None
+    if st is not None and "weights_tag" in st and not torch.allclose(st["weights_tag"], _weights_tag(learner.flat),
+                                                                     rtol=1e-9, atol=0.0):
+        import warnings
+
+        warnings.warn(f"{side} does not belong to {path} (torn save?): resuming weights only")
+        st = None
+    if st is not None:
         learner.opt_s1.copy_(st["opt_s1"])
         learner.opt_s2.copy_(st["opt_s2"])
         learner.step_counter.copy_(st["step_counter"])
@@ -111,6 +131,7 @@ def main(argv=None) -> int:
     lc = LearnerConfig(batch_size=R.batch_size, n_step=cfg.n_steps, gamma=cfg.gamma, lr=L.lr, rms_alpha=L.rms_alpha,
                        rms_eps=L.rms_eps, centered=L.centered, max_norm=L.max_norm, lr_gamma=L.lr_gamma,
                        lr_step_size=L.lr_step_size, beta=R.beta, optimizer=L.optimizer, forward=cfg.kernel.forward,
+                       dtype=cfg.kernel.dtype,
                        seed=cfg.seed + (rank if topology == "sharded" else 0))
     E = cfg.actor.n_envs
     ecfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=R.replay_buffer_size, alpha=R.alpha,

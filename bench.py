@@ -17,9 +17,16 @@ and the global batch is 512*N.
 One timed step = one learner SGD step (sample 512 -> 3 forwards -> backward ->
 clip -> RMSprop -> priority update) + ``--actor-steps`` actor steps of all envs.
 
-``value`` = sum over ranks of learner SGD steps/s (= batches of 512 per second, the
-unit of the reference's number); actor frames/s (4 emulator frames per env step) is
-reported alongside.  Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1
+``value`` = learner sample throughput in batches of 512 per second (sampled transitions/s
+divided by 512: the unit of the reference's 10-12 batches/s).  With one GPU that is the
+optimizer-update rate; under ``--scaling weak`` (data parallel, global batch 512*N) one
+optimizer update consumes N such batches, so ``optimizer_updates_per_s`` (one synchronous
+update per step) and ``learner_samples_per_sec`` are reported separately; ``--scaling
+strong`` keeps the reference's single-learner global batch of 512 (512/N per rank), so
+``value`` equals the update rate.  Actor frames/s (4 emulator frames per env step) is
+reported alongside.  ``--dtype fp32`` (default) is the reference's precision
+(origin_repo/learner.py:139-145: fp32 modules, no autocast) on fp32 MFMA kernels;
+``--dtype bf16`` is the opt-in bf16-operand mode.  Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1
 under torch.distributed.run, one process per GPU).
 """
 from __future__ import annotations
@@ -41,7 +48,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=256, help="GPU envs (actors) per GPU")
     ap.add_argument("--actor-steps", type=int, default=1, help="actor steps per learner step")
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=512, help="global batch at N=1 (per-rank batch under weak scaling)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="learner/actor compute precision: fp32 = the reference's (fp32 MFMA kernels), bf16 = opt-in")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: batch per rank fixed (global batch batch*N); strong: global batch fixed (batch/N per rank)")
     ap.add_argument("--capacity", type=int, default=2_000_000)
     ap.add_argument("--threshold", type=int, default=50_000)
     ap.add_argument("--actions", type=int, default=18)
@@ -129,7 +140,11 @@ def main():
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
-    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed + rank, tree_fork=args.tree_fork,
+    if args.scaling == "strong" and args.batch % world:
+        raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
+    rank_batch = args.batch // world if args.scaling == "strong" else args.batch
+    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
+                       tree_fork=args.tree_fork,
                        fork_late=args.fork_late, late_join=args.late_join,
                        bwd_fork=args.bwd_fork, tree_write=args.tree_write)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
@@ -195,25 +210,28 @@ def main():
     torch.cuda.synchronize(device)
 
     stats = eng.learner.stats()
-    steps_per_s = world * args.steps / dt
+    updates_per_s = args.steps / dt                # synchronous optimizer updates (all ranks step together)
+    samples_per_s = world * rank_batch * args.steps / dt
+    batches_per_s = samples_per_s / 512.0          # the reference's unit: batches of 512 per second
     frames_per_s = world * args.steps * args.actor_steps * eng.frames_per_actor_step / dt
     if rank == 0:
         out = {
             "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
-            "value": round(steps_per_s, 3),
-            "unit": "learner SGD steps/s (batch 512 each, summed over GPUs)",
+            "value": round(batches_per_s, 3),
+            "unit": "learner batches of 512 sampled transitions per second, whole job (= SGD steps/s at N=1)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2),
-            "dtype": "bf16",
+            "scaling": args.scaling,
+            "vs_baseline": round(batches_per_s / REFERENCE_BATCHES_PER_S, 2),
+            "dtype": args.dtype,
             "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
             "config": {
                 "model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
-                "global_batch": args.batch * world,
+                "global_batch": rank_batch * world,
+                "batch_per_rank": rank_batch,
                 "seq_len": 3,
                 "seq_len_meaning": "n-step return horizon (frame stack 4)",
                 "parallelism": f"dp{world}" + ("-forced" if args.force_dp and world == 1 else ""),
@@ -230,9 +248,10 @@ def main():
                 "actor_stream": args.streams,
                 "dp_graph": eng._g_dp is not None,
             },
+            "optimizer_updates_per_s": round(updates_per_s, 3),
             "actor_frames_per_sec": round(frames_per_s, 1),
-            "learner_samples_per_sec": round(steps_per_s * args.batch, 1),
-            "vs_paper_19_batches_per_s": round(steps_per_s / PAPER_BATCHES_PER_S, 2),
+            "learner_samples_per_sec": round(samples_per_s, 1),
+            "vs_paper_19_batches_per_s": round(batches_per_s / PAPER_BATCHES_PER_S, 2),
             "replay_fill_seconds": round(t_fill, 3),
             "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
             "stream_probe": eng.stream_probe,
@@ -257,7 +276,7 @@ def central(args, rank, world, device):
 
     if world < 2:
         raise SystemExit("--topology central needs >= 2 ranks")
-    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, seed=args.seed)
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, dtype=args.dtype, seed=args.seed)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
@@ -291,7 +310,7 @@ def central(args, rank, world, device):
             "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": "bf16",
+            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": args.dtype,
             "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
             "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
                        "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",

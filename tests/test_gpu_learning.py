@@ -1,0 +1,122 @@
+"""The HIP learner learns like the reference's fp32 PyTorch learner.
+
+The reference learner step (origin_repo/learner.py:152-175, utils.py:64-97) is an fp32
+``DuelingDQN`` + ``compute_loss`` + ``clip_grad_norm_(40)`` + centered ``torch.optim.RMSprop``
+(lr 6.25e-5, alpha 0.95, eps 1.5e-7).  Here that learner is driven on EXACTLY the index /
+IS-weight stream the HIP learner sampled (same replay, same transitions) for 200 steps and
+the learners are compared step by step with an fp64 PyTorch learner on the same stream:
+loss, priorities and the parameter trajectory.  The
+reference ships no learning fixtures, so this pins self-consistency with the in-repo
+PyTorch reference of the same algorithm ("parity unpinned" against upstream numbers)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 200
+
+
+def _run(cuda, dtype: str, B: int = 256, steps: int = STEPS):
+    """HIP learner (``dtype``) + fp32 and fp64 PyTorch reference learners on the HIP
+    learner's sampled stream.  Returns per-step trajectories and parameter distances."""
+    from apex_amd.algo.losses import compute_loss_device, update_parameters_ex
+    from apex_amd.engine.apex import ApexEngine, EngineConfig
+    from apex_amd.engine.learner import LearnerConfig
+    from apex_amd.models.dqn import DuelingDQN
+
+    lc = LearnerConfig(batch_size=B, forward="hip", dtype=dtype)
+    cfg = EngineConfig(n_envs=64, replay_capacity=16384, threshold_size=8192, learner=lc)
+    eng = ApexEngine(cfg, cuda)
+    eng.fill()
+    L, rp = eng.learner, eng.replay
+
+    def clone(src, dt):
+        m = DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions).to(cuda)
+        m.load_state_dict(src.state_dict())
+        return m.to(dt)
+
+    refs = {}
+    for name, dt in (("t32", torch.float32), ("t64", torch.float64)):
+        m, t = clone(L.model, dt), clone(L.target, dt)
+        for p in t.parameters():
+            p.requires_grad_(False)
+        opt = torch.optim.RMSprop(m.parameters(), lc.lr, alpha=lc.rms_alpha, eps=lc.rms_eps, centered=True)
+        refs[name] = (m, t, opt, dt)
+    p0 = L.flat.detach().double().clone()
+    s = torch.empty(B, 4, 84, 84, dtype=torch.uint8, device=cuda)
+    s2 = torch.empty_like(s)
+    a = torch.empty(B, dtype=torch.int32, device=cuda)
+    r = torch.empty(B, device=cuda)
+    d = torch.empty(B, device=cuda)
+    flat = lambda m: torch.cat([p.detach().double().reshape(-1) for p in m.parameters()])  # noqa: E731
+    traj = []
+    for i in range(steps):
+        L.step()  # samples (idx, w) on device, 3 forwards, backward, clip, RMSprop, priority write
+        rp.gather(L.idx, s, s2, a, r, d)
+        row = {"hip_loss": float(L.loss.item()), "hip_prio": L.prio.double().clone()}
+        for name, (m, t, opt, dt) in refs.items():
+            batch = (s.to(dt), a.long(), r.to(dt), s2.to(dt), d.to(dt), L.w.to(dt))
+            loss, prios = compute_loss_device(m, t, batch, lc.n_step, lc.gamma)
+            update_parameters_ex(loss, m, opt, lc.max_norm)
+            row[name + "_loss"] = float(loss.item())
+            row[name + "_prio"] = prios.double()
+        p64 = flat(refs["t64"][0])
+        moved = float((p64 - p0).norm())
+        row["moved"] = moved
+        row["hip_vs_64"] = float((L.flat.double() - p64).norm()) / moved
+        row["t32_vs_64"] = float((flat(refs["t32"][0]) - p64).norm()) / moved
+        row["hip_vs_t32"] = float((L.flat.double() - flat(refs["t32"][0])).norm()) / moved
+        row["param_rel"] = float((L.flat.double() - p64).norm() / p64.norm())
+        row["t32_param_rel"] = float((flat(refs["t32"][0]) - p64).norm() / p64.norm())
+        for k in ("hip", "t32"):
+            row[k + "_prio_err"] = float(((row[k + "_prio"] - row["t64_prio"]).abs().max()
+                                          / row["t64_prio"].abs().max()))
+            row[k + "_loss_err"] = abs(row[k + "_loss"] - row["t64_loss"]) / max(abs(row["t64_loss"]), 1e-12)
+        traj.append(row)
+    return traj
+
+
+def _summary(traj):
+    keys = ("moved", "hip_vs_64", "t32_vs_64", "hip_vs_t32", "param_rel", "hip_loss_err", "t32_loss_err",
+            "hip_prio_err", "t32_prio_err")
+    for i in (0, 1, 2, 5, 10, 25, 50, 100, len(traj) - 1):
+        if i < len(traj):
+            print(i, {k: f"{traj[i][k]:.3g}" for k in keys})
+
+
+def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
+    """Measured (MI355X): step 0 HIP-vs-torch-fp32 parameter distance 2.2e-5 of the update
+    length, loss/priorities within 2e-7 of fp64.  Beyond ~10 steps BOTH fp32 learners drift
+    from the fp64 one at the same rate: the first centered-RMSprop steps are sign-like
+    (update ~ lr * g / sqrt(var)), so roundoff-sized gradients of either sign move weights by
+    a full lr -- an intrinsic property of the reference's algorithm, not of the kernels."""
+    traj = _run(cuda, "fp32")
+    _summary(traj)
+    assert traj[-1]["moved"] > 0
+    # first steps: kernel-level agreement with PyTorch fp32 and fp64
+    for row in traj[:3]:
+        assert row["hip_vs_t32"] < 1e-4, row["hip_vs_t32"]
+        assert row["hip_loss_err"] < 1e-4 and row["hip_prio_err"] < 1e-3
+    # whole run: the HIP fp32 learner is no farther from the fp64 learner than PyTorch's
+    # own fp32 learner (same fp32 roundoff class)
+    for row in traj:
+        assert row["hip_vs_64"] <= 1.25 * row["t32_vs_64"] + 0.02, row
+        assert row["param_rel"] <= 1.25 * row["t32_param_rel"] + 1e-4, row
+    tail = traj[len(traj) // 2:]
+    mean = lambda k: sum(r[k] for r in tail) / len(tail)  # noqa: E731
+    assert mean("hip_loss_err") <= 2.0 * mean("t32_loss_err") + 0.02
+    assert mean("hip_prio_err") <= 2.0 * mean("t32_prio_err") + 0.02
+
+
+def test_bf16_hip_learner_stays_in_band(cuda):
+    """The opt-in bf16 learner on the same stream: losses and priorities stay within a
+    stated band of the fp64 PyTorch learner (bf16 operands: ~3 significant digits)."""
+    traj = _run(cuda, "bf16")
+    _summary(traj)
+    # measured: step-1 loss 1.1e-3 / priorities 1.2e-2 from fp64; parameters within 2.8% of
+    # the fp64 learner's after 200 steps (the fp32 learners: 2.7%)
+    assert traj[0]["hip_loss_err"] < 1e-2
+    for row in traj:
+        assert row["param_rel"] <= 2.0 * row["t32_param_rel"] + 5e-3, row
+    tail = traj[len(traj) // 2:]
+    assert sum(r["hip_loss_err"] for r in tail) / len(tail) < 0.5

@@ -235,3 +235,31 @@ def test_interleaved_sample_update_keeps_tree_consistent(cuda):
         want_min = torch.nn.functional.pad(below_min, (0, pad), value=float("inf")).view(n, 64).min(1).values
         assert torch.equal(m, want_min), k
         below, below_min = s, m
+
+
+def test_sample_api_returns_the_sampled_transitions(cuda):
+    """HBMReplay.sample(): every returned column equals the transition table at the
+    returned idx (actions int64 like the reference buffer, no uninitialised halves)."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 1024
+    rp = HBMReplay(C, n_envs=4, device=cuda)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    rp.frames.copy_(torch.randint(0, 256, rp.frames.shape, generator=g, dtype=torch.uint8).to(cuda))
+    F = rp.frame_capacity
+    rp.s_ids.copy_(torch.randint(0, F, (C, 4), generator=g, dtype=torch.int32).to(cuda))
+    rp.s2_ids.copy_(torch.randint(0, F, (C, 4), generator=g, dtype=torch.int32).to(cuda))
+    rp.action.copy_(torch.randint(0, 18, (C,), generator=g, dtype=torch.int32).to(cuda))
+    rp.reward.copy_(torch.randn(C, generator=g).to(cuda))
+    rp.done.copy_((torch.rand(C, generator=g) < 0.1).float().to(cuda))
+    idx = torch.arange(C, dtype=torch.int32, device=cuda)
+    rp.write_priorities(idx, torch.rand(C, device=cuda) + 0.1)
+    rp.filled.fill_(C)
+    s, a, r, s2, d, w, sidx = rp.sample(256, 0.4)
+    torch.cuda.synchronize()
+    il = sidx.long()
+    assert a.dtype == torch.int64 and torch.equal(a, rp.action[il].long())
+    assert torch.equal(s, rp.frames[rp.s_ids[il].long()].view(256, 4, 84, 84))
+    assert torch.equal(s2, rp.frames[rp.s2_ids[il].long()].view(256, 4, 84, 84))
+    assert torch.equal(r, rp.reward[il]) and torch.equal(d, rp.done[il])
+    assert bool((w > 0).all()) and bool((w <= 1.0 + 1e-6).all())

@@ -97,3 +97,38 @@ def test_enjoy_plays_saved_checkpoint(tmp_path, capsys):
     res = main(["--env", "CartPole-v0", "--model", path, "--episodes", "2"])
     assert len(res) == 2 and all(n >= 1 and r == n for n, r in res)  # CartPole: +1 per step
     assert capsys.readouterr().out.count("Episode Length / Reward:") == 2
+
+
+def test_engine_checkpoint_sidecar_tagged(tmp_path):
+    """train.save_engine writes the sidecar atomically with a weights fingerprint; a
+    sidecar from a different save (torn save) is ignored by load_engine."""
+    import types
+    import warnings
+
+    import torch
+
+    from apex_amd.models.dqn import DuelingDQN
+    from apex_amd.train import load_engine, save_engine
+
+    def learner(seed):
+        torch.manual_seed(seed)
+        m = DuelingDQN.from_shapes((4,), 3)
+        flat = m.flatten_parameters()
+        return types.SimpleNamespace(model=m, flat=flat, opt_s1=torch.rand_like(flat), opt_s2=torch.rand_like(flat),
+                                     step_counter=torch.tensor([seed + 5]), tflat=flat.clone() + 1, hip_net=False)
+
+    a = learner(1)
+    path = str(tmp_path / "model.pth")
+    save_engine(a, path, {"learn_steps": 7})
+    b = learner(2)
+    assert load_engine(b, path) == {"learn_steps": 7}
+    assert torch.equal(b.flat, a.flat) and torch.equal(b.opt_s1, a.opt_s1) and int(b.step_counter) == 6
+    # torn save: the model file is newer than the sidecar
+    c = learner(3)
+    torch.save({k: v.clone() for k, v in c.model.state_dict().items()}, path)
+    d = learner(4)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert load_engine(d, path) == {}
+    assert any("torn" in str(x.message) for x in w)
+    assert torch.equal(d.flat, c.flat) and torch.equal(d.tflat, d.flat)
