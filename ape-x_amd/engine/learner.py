@@ -148,8 +148,8 @@ class DQNLearner:
             self.net.bwd_fork = cfg.bwd_fork
             self.net.enable_backward(B)
             self.tnet = make_hip_net(self.target, cfg.dtype)
-            # bf16: the optimizer refreshes the packed bf16 weights; fp32 reads the master in place
-            self.pmap1, self.pmap2 = (None, None) if self.fp32 else self.net.pack_maps()
+            # the optimizer refreshes the packed weight copies (bf16 or exact fp32) in its pass
+            self.pmap1, self.pmap2 = self.net.pack_maps()
             self.ws_s = make_workspace(B, A, dev, cfg.dtype, keep_for_backward=True)
             self.ws_s2 = make_workspace(B, A, dev, cfg.dtype)
             self.ws_t = make_workspace(B, A, dev, cfg.dtype)
@@ -345,15 +345,19 @@ class DQNLearner:
         else:
             h.grad_sumsq(self.flat_grad.data_ptr(), self.P, self.partials.data_ptr(), s)
             parts, nparts = self.partials, self.partials.numel()
-        packed = self.hip_net and not self.fp32
-        pk = (self.pmap1.data_ptr(), self.pmap2.data_ptr(), self.net.arena.data_ptr()) if packed else (0, 0, 0)
-        fc = self.net.fc_pack_args() if packed else {}
+        if not self.hip_net:
+            pk = {}
+        elif self.fp32:  # exact fp32 packed copies (PackMap.arena_f32 + FC1 tiles)
+            pk = self.net.opt_pack_args()
+        else:  # bf16 packed copies
+            pk = {"dst1": self.pmap1.data_ptr(), "dst2": self.pmap2.data_ptr(), "arena": self.net.arena.data_ptr(),
+                  **self.net.fc_pack_args()}
         step = h.rmsprop_step if self.cfg.optimizer == "rmsprop" else h.adam_step
         # the fused path already bumped step_counter on the tree stream: the optimizer reads
         # this step's snapshot instead
         stp = self.step_snap if self.hip_net else self.step_counter
         step(self.flat.data_ptr(), self.flat_grad.data_ptr(), self.opt_s1.data_ptr(), self.opt_s2.data_ptr(), self.P,
-             parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, *pk, **fc)
+             parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, **pk)
         if not self.hip_net:
             self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
         if self._join_pending:
@@ -380,7 +384,7 @@ class DQNLearner:
 
     # ------------------------------------------------------------------ target / params
     def refresh_packed(self) -> None:
-        """Re-derive the packed bf16 weights from the fp32 master (after the flat buffer
+        """Re-derive the packed weight copies from the fp32 master (after the flat buffer
         was written outside the optimizer, e.g. a DP broadcast or a checkpoint load)."""
         if self.hip_net:
             self.net.repack()

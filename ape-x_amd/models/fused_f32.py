@@ -16,9 +16,13 @@ runs the same Nature-CNN dueling network on gfx950's exact-f32 matrix instructio
     conv1 wgrad partials from the u8 frames
     grad_finalize: deterministic partial reduce -> reference layout + bias grads + grad-norm partials
 
-Weights are read straight from the fp32 master parameters in their reference layouts,
-so there is no packed copy to refresh: ``repack``/``copy_packed_from`` are no-ops and the
-optimizer is the plain fp32 centered RMSprop / Adam over the flat buffer.
+Weights are read from EXACT fp32 copies in GEMM layouts (one fp32 arena, see ``LAYOUT``):
+k-contiguous rows for the forward B operands, co-contiguous transposes for the conv input
+gradients.  The fused optimizer rewrites them in the same pass as the fp32 master update
+(``pack_maps`` -> PackMap.arena_f32, FC1 through the LDS-tiled FcPack path), target sync and
+actor publish copy arenas (``copy_packed_from``), and ``repack()`` re-derives the arena from
+the master (init, broadcast, checkpoint load).  The master parameters stay the reference
+state_dict; the arena only changes memory order, never a value.
 """
 from __future__ import annotations
 
@@ -57,8 +61,10 @@ class F32DuelingNet:
     """fp32 MFMA kernels over a :class:`DuelingDQN` (fp32 master params, reference layout)."""
 
     fp32 = True
-    arena = None
     bwd_fork = False  # the bf16 net's side-stream wgrad option; the fp32 backward pairs wgrad+dgrad per launch
+    # fp32 arena: forward layouts first (all an actor / target net needs), then the transposes
+    LAYOUT = (("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, P3, C3)),
+              ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)))
 
     def __init__(self, model: DuelingDQN):
         assert model.cnn and tuple(model.input_shape) == (4, 84, 84), "HIP path is the Atari Nature-CNN"
@@ -69,13 +75,65 @@ class F32DuelingNet:
         self.device = next(model.parameters()).device
         self._ws_B = None
         self._heads_ws = None
+        self._maps = None
+        sizes = [int(torch.Size(sh).numel()) for _, sh in self.LAYOUT]
+        self.arena = torch.empty(sum(sizes), dtype=torch.float32, device=self.device)
+        self.arena_offsets = {}
+        off = 0
+        for (name, sh), n in zip(self.LAYOUT, sizes):
+            setattr(self, name, self.arena[off:off + n].view(sh))
+            self.arena_offsets[name] = off
+            off += n
+        self.fwd_numel = self.arena_offsets["w2t"]
+        self.repack()
 
-    # the weights are consumed in place: nothing to pack
     def repack(self) -> None:
-        pass
+        """Re-derive every packed copy from the fp32 master (exact: a permutation)."""
+        f, m = self.model.features, self.model
+        with torch.no_grad():
+            self.w2p.copy_(f[2].weight.permute(0, 2, 3, 1))
+            self.w3p.copy_(f[4].weight.permute(0, 2, 3, 1))
+            self.wfc1p[:128].copy_(m.advantage[0].weight.view(128, C3, P3).permute(0, 2, 1))
+            self.wfc1p[128:].copy_(m.value[0].weight.view(128, C3, P3).permute(0, 2, 1))
+            self.w2t.copy_(f[2].weight.permute(2, 3, 1, 0))
+            self.w3t.copy_(f[4].weight.permute(2, 3, 1, 0))
 
-    def copy_packed_from(self, other, forward_only: bool = True) -> None:
-        pass
+    def copy_packed_from(self, other: "F32DuelingNet", forward_only: bool = True) -> None:
+        """Device copy of another net's packed weights (same architecture)."""
+        n = self.fwd_numel if forward_only else self.arena.numel()
+        self.arena[:n].copy_(other.arena[:n])
+
+    def pack_maps(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """int32 (dst1, dst2) over the flat parameter order: arena positions of the packed
+        copies of each conv weight element (-1: none; FC1 goes through ``fc_pack_args``)."""
+        if self._maps is not None:
+            return self._maps
+        seg = {name: (o, n) for name, o, n in self.model.param_segments()}
+        P = sum(n for _, n in seg.values())
+        dst1 = torch.full((P,), -1, dtype=torch.int64)
+        dst2 = torch.full((P,), -1, dtype=torch.int64)
+        ao = self.arena_offsets
+        for pname, N, C, K, fwd, bwd in (("features.2.weight", 64, 32, 4, "w2p", "w2t"),
+                                         ("features.4.weight", 64, 64, 3, "w3p", "w3t")):
+            o, n = seg[pname]
+            ref = torch.arange(N * C * K * K).view(N, C, K, K)  # reference position of each element
+            # packed position q holds reference element ref_order[q]
+            for dst, order, base in ((dst1, ref.permute(0, 2, 3, 1).reshape(-1), ao[fwd]),
+                                     (dst2, ref.permute(2, 3, 1, 0).reshape(-1), ao[bwd])):
+                dst[o + order] = base + torch.arange(n)
+        self._maps = (dst1.to(torch.int32).to(self.device), dst2.to(torch.int32).to(self.device))
+        return self._maps
+
+    def fc_pack_args(self) -> dict:
+        """Optimizer FC1 tile path (FcPack, fp32): flat offsets of both FC1 weights and wfc1p."""
+        seg = {name: o for name, o, _ in self.model.param_segments()}
+        return {"fc_off0": seg["advantage.0.weight"], "fc_off1": seg["value.0.weight"],
+                "fc_wp_f32": self.wfc1p.data_ptr()}
+
+    def opt_pack_args(self) -> dict:
+        d1, d2 = self.pack_maps()
+        return {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
+                **self.fc_pack_args()}
 
     @staticmethod
     def _s() -> int:
@@ -140,9 +198,8 @@ class F32DuelingNet:
 
     def _fc1_bwd(self, ws: F32Workspace) -> None:
         m = self.model
-        self.hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), m.advantage[0].weight.data_ptr(),
-                             m.value[0].weight.data_ptr(), ws.dy3.data_ptr(), m.advantage[0].weight.grad.data_ptr(),
-                             m.value[0].weight.grad.data_ptr(), ws.B, self._s())
+        self.hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
+                             m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(), ws.B, self._s())
 
     def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None) -> list:
         """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch); returns the
@@ -151,11 +208,11 @@ class F32DuelingNet:
         h, s, f = self.hip, self._s(), self.model.features
         xp, ip, jp = self._src(x, ids, idx, B)
         w1, w2, w3 = self._wgrad_wss
-        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), f[4].weight.data_ptr(), ws.a2.data_ptr(),
+        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
                        ws.dy2.data_ptr(), w3.data_ptr(), B, s)
         if after_first is not None:
             after_first()
-        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), f[2].weight.data_ptr(), ws.a1.data_ptr(),
+        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
                        ws.dy1.data_ptr(), w2.data_ptr(), B, s)
         h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
         return [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
@@ -209,10 +266,9 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
         m, f = net.model, net.model.features
         xp, ip, jp = net._src(x, ids, idx, B)
         c1.append((xp, ip, jp, f[0].weight.data_ptr(), 0, f[0].bias.data_ptr(), ws.a1.data_ptr()))
-        c2.append((ws.a1.data_ptr(), 0, 0, f[2].weight.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
-        c3.append((ws.a2.data_ptr(), 0, 0, f[4].weight.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
-        fc.append((ws.a3.data_ptr(), 0, 0, m.advantage[0].weight.data_ptr(), m.value[0].weight.data_ptr(), 0,
-                   ws.z.data_ptr()))
+        c2.append((ws.a1.data_ptr(), 0, 0, net.w2p.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
+        c3.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
+        fc.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
         hd.append(net._heads_tuple(ws))
     h.f32_conv_fwd_multi(1, c1, B, s)
     h.f32_conv_fwd_multi(2, c2, B, s)

@@ -4,9 +4,15 @@
 // model.py:31-68).  gfx950 has exact-f32 matrix instructions -- v_mfma_f32_32x32x2_f32 is
 // bit-for-bit a k-ordered fmaf chain at 64 FLOP/clk/SIMD (157 TF chip) -- so every GEMM-shaped
 // op of the learner step (three forwards, the whole backward) runs on them here, with fp32
-// operands, fp32 activations and the fp32 master weights read in their REFERENCE layouts
-// (no packed copies: at 1/16 of the bf16 rate the kernels are MFMA-bound, and gathering a
-// weight chunk with four scalar loads from L2 is hidden behind the matrix work).
+// operands and fp32 activations.  Weights are read from exact fp32 PACKED copies in GEMM
+// layouts (k-contiguous rows), which the optimizer rewrites in the same pass as the master
+// update (learner_kernels.hip PackMap / FcPack): gathering a weight chunk from the reference
+// layout took four strided dword loads per 16 bytes, and the texture-address work of those
+// scattered loads, not the MFMA pipe, bounded conv2/conv3/FC1 (MI355X: FC1 forward 60 -> 35 us,
+// conv2 114 -> 90 us per 1536-sample launch).  Packed layouts (models/fused_f32.py):
+//   conv1 W1 [32][c*64 + ky*8 + kx] (= reference)   w2p [64][tap*32 + ci]   w3p [64][tap*64 + ci]
+//   wfc1p [256][p*64 + c] (FC1 forward, and row-major the input-gradient B operand)
+//   w2t [ky][kx][ci][co], w3t [ky][kx][ci][co] (dgrad B operands, co contiguous)
 //
 // One templated LDS-staged GEMM body serves all 13 GEMMs; a policy per layer supplies the
 // tile decode, the operand chunk loaders (implicit im2col / col2im / sub-pixel gathers,
@@ -18,7 +24,9 @@
 //   * each operand tile is staged global -> registers -> LDS in its natural global layout:
 //     "K-major" [row][BK] (k contiguous) or "MN-major" [k][BM|BN] (m|n contiguous), 16-byte
 //     chunks; LDS double buffer + register prefetch of the next k-block (one barrier per
-//     k-block); pitches padded so the fragment reads are bank-conflict free.
+//     k-block; a sched_barrier pins the prefetch ahead of the MFMA block, otherwise the
+//     scheduler sinks late-needed loads next to their LDS store and exposes their latency);
+//     pitches padded so the fragment reads are bank-conflict free.
 //   * k-chunk mapping: for a chunk of 8 k, lane (r = l & 31, h = l >> 5) holds elements
 //     k = 4h .. 4h+3 of its A row / B column (one ds_read_b128 when K-major, four ds_read_b32
 //     when MN-major); MFMA i of the chunk consumes element i of both -- the 32x32x2 MFMA's
@@ -186,6 +194,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   for (; kb < ctx.kb1; ++kb) {
     const bool more = kb + 1 < ctx.kb1;
     if (more) gload(kb + 1);
+    __builtin_amdgcn_sched_barrier(0);
     compute(cur);
     if (more) sstore(cur ^ 1);
     __syncthreads();
@@ -249,9 +258,11 @@ __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
 }
 
 // ------------------------------------------------------------------ forward policies
-struct Conv1Fwd {  // a1[m][n] = relu(sum_k frame(m, k) W1[n][k] + b1[n]), k = (c, ky, kx)
-  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+template <int BM_, int BN_, int BK_, int WM_>
+struct Conv1FwdT {  // a1[m][n] = relu(sum_k frame(m, k) W1[n][k] + b1[n]), k = (c, ky, kx)
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = true;
+  static_assert(BM <= 400 && 256 % BK == 0, "a tile touches <= 2 samples");
   using Args = F32Set;
   struct Smem {
     const uint8_t* pl[2][4];  // frame planes of the (<= 2) samples the tile touches
@@ -293,97 +304,108 @@ struct Conv1Fwd {  // a1[m][n] = relu(sum_k frame(m, k) W1[n][k] + b1[n]), k = (
   }
 };
 
-struct Conv2Fwd {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci), one tap per k-block
-  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
+template <int BM_, int BN_, int BK_, int WM_>
+struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32 + ci; w = w2p
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  static_assert(512 % BK == 0 && BN <= 64, "k-blocks tile K = 512");
   using Args = F32Set;
   using Smem = NoSmem;
   struct Ctx {
     F32Prob p;
-    int M, m0, kb0, kb1;
+    int M, m0, n0, kb0, kb1;
   };
-  static __host__ __device__ int tiles(int B) { return (B * 81 + BM - 1) / BM; }
+  static constexpr int NT = 64 / BN;
+  static __host__ __device__ int tiles(int B) { return NT * ((B * 81 + BM - 1) / BM); }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     const int tp = tiles(a.B);
     c.p = pick(a, block / tp);
     c.M = a.B * 81;
-    c.m0 = (block % tp) * BM;
+    const int t = block % tp;
+    c.m0 = (t / NT) * BM;
+    c.n0 = (t % NT) * BN;
     c.kb0 = 0;
-    c.kb1 = 16;
+    c.kb1 = 512 / BK;
   }
   static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int m = c.m0 + row;
     if (m >= c.M) return zero4();
-    const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9, ky = kb >> 2, kx = kb & 3;
+    const int k = kb * BK + 4 * ch, tap = k >> 5, ci = k & 31, ky = tap >> 2, kx = tap & 3;
+    const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9;
     const float* in = static_cast<const float*>(c.p.in);
-    return ld4(in + ((size_t)b * 400 + (2 * oy + ky) * 20 + 2 * ox + kx) * 32 + 4 * ch);
+    return ld4(in + ((size_t)b * 400 + (2 * oy + ky) * 20 + 2 * ox + kx) * 32 + ci);
   }
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
-    const float* w = c.p.w + n * 512 + (4 * ch) * 16 + kb;  // reference [co][ci][ky][kx]
-    return f32x4{w[0], w[16], w[32], w[48]};
+    return ld4(c.p.w + (c.n0 + n) * 512 + kb * BK + 4 * ch);
   }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
-    if (m < c.M) c.p.out[(size_t)m * 64 + n] = fmaxf(v + c.p.bias[n], 0.f);
+    if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
   }
 };
 
-struct Conv3Fwd {  // a3 = relu(conv(a2, W3) + b3); k-block = half a tap (32 channels)
-  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
+template <int BM_, int BN_, int BK_, int WM_>
+struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  static_assert(576 % BK == 0 && 64 % BK == 0 || BK == 64, "a k-block stays inside one tap");
   using Args = F32Set;
   using Smem = NoSmem;
   struct Ctx {
     F32Prob p;
-    int M, m0, kb0, kb1;
+    int M, m0, n0, kb0, kb1;
   };
-  static __host__ __device__ int tiles(int B) { return (B * 49 + BM - 1) / BM; }
+  static constexpr int NT = 64 / BN;
+  static __host__ __device__ int tiles(int B) { return NT * ((B * 49 + BM - 1) / BM); }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     const int tp = tiles(a.B);
     c.p = pick(a, block / tp);
     c.M = a.B * 49;
-    c.m0 = (block % tp) * BM;
+    const int t = block % tp;
+    c.m0 = (t / NT) * BM;
+    c.n0 = (t % NT) * BN;
     c.kb0 = 0;
-    c.kb1 = 18;
+    c.kb1 = 576 / BK;
   }
   static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int m = c.m0 + row;
     if (m >= c.M) return zero4();
+    const int k = kb * BK + 4 * ch, tap = k >> 6, ci = k & 63, ky = tap / 3, kx = tap - ky * 3;
     const int b = m / 49, p = m - b * 49, oy = p / 7, ox = p - oy * 7;
-    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3, ci = (kb & 1) * 32 + 4 * ch;
     const float* in = static_cast<const float*>(c.p.in);
     return ld4(in + ((size_t)b * 81 + (oy + ky) * 9 + ox + kx) * 64 + ci);
   }
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
-    const int tap = kb >> 1, ci = (kb & 1) * 32 + 4 * ch;
-    const float* w = c.p.w + n * 576 + ci * 9 + tap;
-    return f32x4{w[0], w[9], w[18], w[27]};
+    return ld4(c.p.w + (c.n0 + n) * 576 + kb * BK + 4 * ch);
   }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
-    if (m < c.M) c.p.out[(size_t)m * 64 + n] = fmaxf(v + c.p.bias[n], 0.f);
+    if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
   }
 };
 
 constexpr int kFcSplits = 7;  // FC1 forward split-K: 3136 = 7 x 448
-struct Fc1Fwd {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] W[n][k'(ref)], k' = p*64 + c
-  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+template <int BM_, int BN_, int BK_, int WM_>
+struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k' = p*64 + c
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
-  static constexpr int KBS = 3136 / BK / kFcSplits;  // 14 k-blocks per split
+  static constexpr int KBS = 3136 / BK / kFcSplits;  // k-blocks per split
+  static_assert(KBS * BK * kFcSplits == 3136 && 256 % BN == 0, "split-K tiling");
+  static constexpr int NT = 256 / BN;
   using Args = F32Set;
   using Smem = NoSmem;
   struct Ctx {
     F32Prob p;
     int B, m0, n0, split, kb0, kb1;
   };
-  static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * 4 * kFcSplits; }
+  static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * NT * kFcSplits; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     const int tp = tiles(a.B);
     c.p = pick(a, block / tp);
     int t = block % tp;
     c.B = a.B;
-    c.n0 = (t & 3) * BN;
-    t >>= 2;
+    c.n0 = (t % NT) * BN;
+    t /= NT;
     c.split = t % kFcSplits;
     c.m0 = (t / kFcSplits) * BM;
     c.kb0 = c.split * KBS;
@@ -395,9 +417,7 @@ struct Fc1Fwd {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] W[n][k'(ref)], k'
     return ld4(static_cast<const float*>(c.p.in) + (size_t)b * 3136 + kb * BK + 4 * ch);
   }
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int nl, int ch) {
-    const int n = c.n0 + nl, k = kb * BK + 4 * ch, p = k >> 6, co = k & 63;
-    const float* w = (n < 128 ? c.p.w + n * 3136 : c.p.w2 + (n - 128) * 3136) + co * 49 + p;
-    return f32x4{w[0], w[49], w[98], w[147]};
+    return ld4(c.p.w + (size_t)(c.n0 + nl) * 3136 + kb * BK + 4 * ch);
   }
   static __device__ void store(const Args&, const Ctx& c, int ml, int nl, float v) {
     const int b = c.m0 + ml;
@@ -411,8 +431,7 @@ struct BwdArgs {
   const int* ids;
   const int* idx;
   const float* dy;      // gradient w.r.t. the layer's (post-ReLU-masked) output
-  const float* w;       // reference weights
-  const float* w2;      // FC1 value weights
+  const float* w;       // packed weights: wfc1p (FC1 dgrad), w3t / w2t (conv dgrad)
   const float* mask;    // post-ReLU activation of the layer below (dgrad ReLU backward)
   float* out;           // dgrad output | wgrad partials / FC1 advantage grad
   float* out2;          // wgrad bias partials | FC1 value grad
@@ -421,7 +440,7 @@ struct BwdArgs {
   int splits;
 };
 
-struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] W[n][k'(ref)]
+struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
   static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
   static constexpr bool A_KMAJ = true, B_KMAJ = false, SMEM = false;
   using Args = BwdArgs;
@@ -442,9 +461,7 @@ struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] W[n][k'(ref)]
     return ld4(a.dy + (size_t)b * 256 + kb * BK + 4 * ch);
   }
   static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int n = kb * BK + row, k = c.n0 + 4 * ch, p = k >> 6, co = k & 63;
-    const float* w = (n < 128 ? a.w + n * 3136 : a.w2 + (n - 128) * 3136) + co * 49 + p;
-    return f32x4{w[0], w[49], w[98], w[147]};
+    return ld4(a.w + (size_t)(kb * BK + row) * 3136 + c.n0 + 4 * ch);
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
     const int b = c.m0 + ml;
@@ -454,7 +471,7 @@ struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] W[n][k'(ref)]
   }
 };
 
-struct Fc1Wgrad {  // dW[n][k(ref) = c*49 + p] = sum_b dz[b][n] a3[b][p*64 + c]
+struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the reference [n][c*49 + p]
   static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false;
   using Args = BwdArgs;
@@ -477,19 +494,13 @@ struct Fc1Wgrad {  // dW[n][k(ref) = c*49 + p] = sum_b dz[b][n] a3[b][p*64 + c]
   static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int b = kb * BK + row;
     if (b >= a.B) return zero4();
-    const float* a3 = static_cast<const float*>(a.x) + (size_t)b * 3136;
-    f32x4 v;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = c.n0 + 4 * ch + i, co = k / 49, p = k - co * 49;
-      v[i] = a3[p * 64 + co];
-    }
-    return v;
+    return ld4(static_cast<const float*>(a.x) + (size_t)b * 3136 + c.n0 + 4 * ch);
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
-    const int n = c.m0 + ml, k = c.n0 + nl;
-    if (n < 128) a.out[n * 3136 + k] = v;
-    else a.out2[(n - 128) * 3136 + k] = v;
+    // scattered stores (write-combined in L2) instead of gathered operand loads
+    const int n = c.m0 + ml, k = c.n0 + nl, ref = (k & 63) * 49 + (k >> 6);
+    if (n < 128) a.out[n * 3136 + ref] = v;
+    else a.out2[(n - 128) * 3136 + ref] = v;
   }
 };
 
@@ -609,8 +620,7 @@ struct Conv3Dgrad {  // dy2[b][pi][ci] = (a2 > 0) * sum_{tap, co} dy3[b][pi - ta
   }
   static __device__ f32x4 load_b(const Args& a, const Ctx&, const Smem&, int kb, int n, int ch) {
     const int tap = kb >> 1, co = (kb & 1) * 32 + 4 * ch;
-    const float* w = a.w + co * 576 + n * 9 + tap;
-    return f32x4{w[0], w[576], w[1152], w[1728]};
+    return ld4(a.w + (tap * 64 + n) * 64 + co);  // w3t [tap][ci][co]
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
@@ -650,8 +660,7 @@ struct Conv2Dgrad {
   static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
     const int t = kb >> 1, ky = (c.cls >> 1) + 2 * (t >> 1), kx = (c.cls & 1) + 2 * (t & 1);
     const int co = (kb & 1) * 32 + 4 * ch;
-    const float* w = a.w + co * 512 + n * 16 + ky * 4 + kx;
-    return f32x4{w[0], w[512], w[1024], w[1536]};
+    return ld4(a.w + ((ky * 4 + kx) * 32 + n) * 64 + co);  // w2t [ky][kx][ci][co]
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
@@ -708,12 +717,32 @@ void check_set(const F32Set& set) {
 }  // namespace
 
 // ------------------------------------------------------------------ host launchers
+// conv1 forward tile variant (benchmark knob, f32_set_variant): 0 = BK 16 (default: the
+// smaller LDS footprint fits 4 workgroups per CU), 1 = BK 32
+int g_conv1_variant = 0;
+
+template <class P>
+void fwd_launch(const F32Set& set, hipStream_t s) {
+  launch1<P>(set, set.n * P::tiles(set.B), s);
+}
+
+void f32_set_variant(int layer, int v) {
+  if (layer != 1 || v < 0 || v > 1) throw std::invalid_argument("f32_set_variant: layer 1, v 0..1");
+  g_conv1_variant = v;
+}
+
+// Tiles (MI355X, 3 x 512-sample launches): 128 x 32 blocks, one 32x32 accumulator per wave,
+// beat 128 x 64 / 256-row blocks: 46-55 KB of LDS per workgroup gave 2-3 per CU, too few
+// waves to cover the operand-load latency.
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
   switch (layer) {
-    case 1: launch1<Conv1Fwd>(set, set.n * Conv1Fwd::tiles(set.B), s); break;
-    case 2: launch1<Conv2Fwd>(set, set.n * Conv2Fwd::tiles(set.B), s); break;
-    case 3: launch1<Conv3Fwd>(set, set.n * Conv3Fwd::tiles(set.B), s); break;
+    case 1:
+      if (g_conv1_variant) fwd_launch<Conv1FwdT<128, 32, 32, 4>>(set, s);
+      else fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
+      break;
+    case 2: fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s); break;
+    case 3: fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s); break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
   }
 }
@@ -722,17 +751,16 @@ int f32_fc1_splits() { return kFcSplits; }
 
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
-  launch1<Fc1Fwd>(set, set.n * Fc1Fwd::tiles(set.B), s);
+  fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
   return kFcSplits;
 }
 
-void f32_fc1_bwd(const float* dz, const float* a3, const float* w_adv, const float* w_val, float* dy3, float* g_adv,
-                 float* g_val, int B, hipStream_t s) {
+void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,
+                 hipStream_t s) {
   if (B <= 0) return;
   BwdArgs d{};
   d.dy = dz;
-  d.w = w_adv;
-  d.w2 = w_val;
+  d.w = wfc1p;
   d.mask = a3;
   d.out = dy3;
   d.B = B;

@@ -234,16 +234,16 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
                            int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                            uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                           uint64_t fc_wp, uint64_t fc_wt) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt)};
+                           uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
-                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr,
-                 fc_wp ? &fc : nullptr);
+                 n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
+                 (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("gavg"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
                        int lr_step_size, int lr_step_offset) {
@@ -256,15 +256,16 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
                         int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                         uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                        uint64_t fc_wp, uint64_t fc_wt) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena)};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt)};
+                        uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
-              hp, P<const int64_t>(step), P<float>(norms), S(s), arena ? &pk : nullptr, fc_wp ? &fc : nullptr);
+              hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
+              (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("mm"), py::arg("v"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
   // ---- network kernels
   m.def("conv_fwd", [](int layer, uint64_t in, uint64_t ids, uint64_t idx, uint64_t wp, uint64_t bias, uint64_t out,
                        int B, uint64_t s) {
@@ -440,10 +441,11 @@ PYBIND11_MODULE(_apex_hip, m) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
   m.def("f32_fc1_splits", &f32_fc1_splits);
-  m.def("f32_fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wa, uint64_t wv, uint64_t dy3, uint64_t ga, uint64_t gv,
-                          int B, uint64_t s) {
-    f32_fc1_bwd(P<const float>(dz), P<const float>(a3), P<const float>(wa), P<const float>(wv), P<float>(dy3),
-                P<float>(ga), P<float>(gv), B, S(s));
+  m.def("f32_set_variant", &f32_set_variant);
+  m.def("f32_fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ga, uint64_t gv, int B,
+                          uint64_t s) {
+    f32_fc1_bwd(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ga),
+                P<float>(gv), B, S(s));
   });
   m.def("f32_wgrad_splits", &f32_wgrad_splits);
   m.def("f32_wgrad_workspace_floats", &f32_wgrad_workspace_floats);

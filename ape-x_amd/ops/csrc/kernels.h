@@ -214,17 +214,20 @@ struct RMSpropParams {
 struct PackMap {
   const int* dst1;
   const int* dst2;
-  uint16_t* arena;
+  uint16_t* arena;      // bf16 packed copies (bf16 network) ...
+  float* arena_f32;     // ... or fp32 packed copies (reference-precision network)
 };
 // FC1 weights (Nature-CNN dueling net): flat offsets of advantage.0.weight and
 // value.0.weight ([128][64*49] each) and the two packed bf16 layouts they refresh,
 // wp = wfc1p [256][49*64] and wt = wfc1t [49*64][256].  With it the optimizer updates
 // FC1 in LDS-transposed tiles (coalesced packed stores) instead of through the scatter
-// maps (whose FC1 entries are then ignored).
+// maps (whose FC1 entries are then ignored).  fp32 network: wp_f32 = [256][49*64] fp32
+// (its forward B operand and, read row-major, the input-gradient GEMM's), no transpose.
 struct FcPack {
   int64_t off[2];
   uint16_t* wp;
   uint16_t* wt;
+  float* wp_f32;
 };
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
@@ -338,13 +341,13 @@ void conv1_fwd(const uint8_t* frames, const int* ids, const int* idx, const uint
                uint16_t* out, int B, hipStream_t s);
 
 // ---- f32_kernels.hip: reference-precision (fp32 MFMA) dueling net, fp32 activations
-// channels-last, reference-layout fp32 weights (no packed copies)
+// channels-last, weights from exact fp32 packed copies (models/fused_f32.py layouts)
 struct F32Prob {
   const void* in;     // layer input: u8 frames (conv1, FrameSrc with ids/idx) or fp32 activations
   const int* ids;
   const int* idx;
-  const float* w;     // reference weights (FC1: advantage.0.weight)
-  const float* w2;    // FC1: value.0.weight
+  const float* w;     // conv1: W1 (reference layout); conv2/conv3: w2p/w3p; FC1: wfc1p
+  const float* w2;    // unused
   const float* bias;
   float* out;         // activations (conv) | split-K partials [7][B][256] (FC1)
 };
@@ -353,16 +356,17 @@ struct F32Set {
   int n, B;
 };
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
+void f32_set_variant(int layer, int v);  // conv1 forward tile variant (benchmarks), 0 = default
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
-// FC1 backward in one launch: dy3 = (a3 > 0) * dz . W (channels-last order) and the
+// FC1 backward in one launch: dy3 = (a3 > 0) * dz . wfc1p (channels-last order) and the
 // reference-layout weight gradients written straight into g_adv / g_val
-void f32_fc1_bwd(const float* dz, const float* a3, const float* w_adv, const float* w_val, float* dy3, float* g_adv,
-                 float* g_val, int B, hipStream_t s);
+void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,
+                 hipStream_t s);
 int f32_wgrad_splits(int layer, int B);
 size_t f32_wgrad_workspace_floats(int layer, int B);
-// conv backward: layers 3/2 = wgrad partials + dgrad (masked by `mask`) in one launch,
-// layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
+// conv backward: layers 3/2 = wgrad partials + dgrad (w = w3t / w2t, masked by `mask`) in
+// one launch, layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
                   const float* mask, float* dx, float* ws, int B, hipStream_t s);
 FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);

@@ -139,6 +139,12 @@ __device__ __forceinline__ float step_lr(float lr0, float gamma, int step_size, 
 }
 
 __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v) {
+  if (pk.arena_f32) {  // fp32 network: exact copies in the GEMM layouts
+    const int d1 = pk.dst1[i], d2 = pk.dst2[i];
+    if (d1 >= 0) pk.arena_f32[d1] = v;
+    if (d2 >= 0) pk.arena_f32[d2] = v;
+    return;
+  }
   if (!pk.arena) return;
   const uint16_t b = f2bf(v);
   const int d1 = pk.dst1[i], d2 = pk.dst2[i];
@@ -238,6 +244,7 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
   const int bid = blockIdx.x;
   if (bid < n_fc_blocks) {
     __shared__ uint16_t tile[kFcTn][kFcTc * kFcP];
+    __shared__ float tile_f[kFcTn][kFcTc * kFcP];
     const int mat = bid / kFcTilesPerMat, t = bid % kFcTilesPerMat;
     const int n0 = (t / (kFcC / kFcTc)) * kFcTn, c0 = (t % (kFcC / kFcTc)) * kFcTc;
     const int64_t base = fc.off[mat];
@@ -269,11 +276,25 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
         s1[vi[k]] = va[k];
         s2[vi[k]] = vb[k];
         p[vi[k]] = np;
-        tile[r][col] = f2bf(np);
+        if (fc.wp_f32) tile_f[r][col] = np;
+        else tile[r][col] = f2bf(np);
       }
     }
-    __syncthreads();
     const int nrow = mat * kFcN + n0;
+    if (fc.wp_f32) {  // fp32 network: wfc1p rows only, 8 channels = two 16-byte runs per position
+      __syncthreads();
+      for (int e = threadIdx.x; e < kFcTn * kFcP * 2; e += kOptThreads) {
+        const int half = e & 1, rp = e >> 1, r = rp / kFcP, pp = rp - r * kFcP;
+        float4 v;
+        v.x = tile_f[r][(4 * half + 0) * kFcP + pp];
+        v.y = tile_f[r][(4 * half + 1) * kFcP + pp];
+        v.z = tile_f[r][(4 * half + 2) * kFcP + pp];
+        v.w = tile_f[r][(4 * half + 3) * kFcP + pp];
+        *reinterpret_cast<float4*>(fc.wp_f32 + (size_t)(nrow + r) * (kFcC * kFcP) + pp * kFcC + c0 + 4 * half) = v;
+      }
+      return;
+    }
+    __syncthreads();
     for (int e = threadIdx.x; e < 2 * kFcTn * kFcP; e += kOptThreads) {
       union { uint16_t h[8]; uint4 v; } u;
       if (e < kFcTn * kFcP) {  // wfc1p row nrow + r, positions p*64 + c0 .. +7
@@ -315,15 +336,16 @@ template <class Params>
 static void launch_opt(float* p, const float* g, float* s1, float* s2, int64_t n, const double* partials,
                        int n_partials, const Params& hp, const int64_t* step, float* norms_out, const PackMap* pack,
                        const FcPack* fc, hipStream_t s) {
-  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr};
+  const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr, nullptr};
   FcPack f{};
   int nfc = 0;
-  if (fc && fc->wp) {
+  if (fc && (fc->wp || fc->wp_f32)) {
     const int64_t F = (int64_t)kFcN * kFcC * kFcP;
     if (fc->off[0] < 0 || fc->off[1] < 0 || fc->off[0] + F > n || fc->off[1] + F > n ||
         std::llabs(fc->off[0] - fc->off[1]) < F)
       throw std::invalid_argument("opt_step: FC1 ranges out of bounds / overlapping");
-    if ((reinterpret_cast<uintptr_t>(fc->wp) | reinterpret_cast<uintptr_t>(fc->wt)) & 15)
+    if ((reinterpret_cast<uintptr_t>(fc->wp) | reinterpret_cast<uintptr_t>(fc->wt) |
+         reinterpret_cast<uintptr_t>(fc->wp_f32)) & 15)
       throw std::invalid_argument("opt_step: packed FC1 layouts must be 16-byte aligned");
     f = *fc;
     nfc = 2 * kFcTilesPerMat;

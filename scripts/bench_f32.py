@@ -1,0 +1,135 @@
+#!/usr/bin/env python
+"""Per-launch timing of the fp32 (reference-precision) network kernels at the learner's
+shapes: forward launches with 3 problems x B (Q(s), Q(s'), Q_target(s')), backward at B.
+
+``python scripts/bench_f32.py [--B 512] [--iters 50] [--only NAME] [--graph 1]`` prints
+us/launch and achieved TFLOP/s (157.3 TF = fp32 MFMA peak); ``--graph 0`` launches
+eagerly (for rocprofv3 --pmc, one dispatch per launch)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from apex_amd import ops  # noqa: E402
+from apex_amd.models.dqn import DuelingDQN  # noqa: E402
+from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--only", default=None)
+ap.add_argument("--B", type=int, default=512)
+ap.add_argument("--graph", type=int, default=1)
+ap.add_argument("--json", action="store_true")
+ap.add_argument("--variants", default=None, help="forward tile variants to sweep, e.g. 0,1,2,3 (f32_set_variant)")
+a = ap.parse_args()
+dev = torch.device("cuda")
+hip = ops.hip()
+B, A = a.B, 18
+m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
+m.flatten_parameters()
+for p in m.parameters():
+    p.grad = torch.zeros_like(p)
+net = F32DuelingNet(m)
+net.enable_backward(B)
+F = 4 * B
+frames = torch.randint(0, 256, (F, 84 * 84), dtype=torch.uint8, device=dev)
+ids = torch.randint(0, F, (B, 4), dtype=torch.int32, device=dev)
+idx = torch.randperm(B, device=dev).int()
+wss = [F32Workspace(B, A, dev, keep_for_backward=(i == 0)) for i in range(3)]
+f = m.features
+
+
+def S() -> int:  # the CURRENT stream at launch time (graph capture runs on a side stream)
+    return torch.cuda.current_stream().cuda_stream
+
+
+def set3(layer):
+    out = []
+    for ws in wss:
+        if layer == 1:
+            out.append((frames.data_ptr(), ids.data_ptr(), idx.data_ptr(), f[0].weight.data_ptr(), 0,
+                        f[0].bias.data_ptr(), ws.a1.data_ptr()))
+        elif layer == 2:
+            out.append((ws.a1.data_ptr(), 0, 0, net.w2p.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
+        elif layer == 3:
+            out.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
+        else:
+            out.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
+    return out
+
+
+from apex_amd.models.fused import forward_multi  # noqa: E402
+
+forward_multi([(net, frames, wss[0], ids, idx), (net, frames, wss[1], ids, idx), (net, frames, wss[2], ids, idx)])
+ws = wss[0]
+ws.dz.normal_()
+ws.dz.mul_((ws.h > 0).float())
+w1, w2, w3 = net._wgrad_wss
+P = 3 * B
+cases = {
+    "conv1_fwd": (lambda: hip.f32_conv_fwd_multi(1, set3(1), B, S()), 2 * P * 400 * 32 * 256),
+    "conv2_fwd": (lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S()), 2 * P * 81 * 64 * 512),
+    "conv3_fwd": (lambda: hip.f32_conv_fwd_multi(3, set3(3), B, S()), 2 * P * 49 * 64 * 576),
+    "fc1_fwd": (lambda: hip.f32_fc1_fwd_multi(set3(4), B, S()), 2 * P * 256 * 3136),
+    "fc1_bwd": (lambda: hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), net.wfc1p.data_ptr(), ws.dy3.data_ptr(),
+                                        m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(), B, S()),
+                2 * 2 * B * 256 * 3136),
+    "conv3_bwd": (lambda: hip.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), net.w3t.data_ptr(),
+                                           ws.a2.data_ptr(), ws.dy2.data_ptr(), w3.data_ptr(), B, S()),
+                  2 * 2 * B * 49 * 64 * 576),
+    "conv2_bwd": (lambda: hip.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), net.w2t.data_ptr(),
+                                           ws.a1.data_ptr(), ws.dy1.data_ptr(), w2.data_ptr(), B, S()),
+                  2 * 2 * B * 81 * 64 * 512),
+    "conv1_wgrad": (lambda: hip.f32_conv_bwd(1, frames.data_ptr(), ids.data_ptr(), idx.data_ptr(), ws.dy1.data_ptr(),
+                                             0, 0, 0, w1.data_ptr(), B, S()), 2 * B * 400 * 32 * 256),
+}
+res = {}
+FWD_LAYER = {"conv1_fwd": 1}
+runs, refs = [], {}
+for name, (fn, flop) in cases.items():
+    if a.only and a.only not in name:
+        continue
+    if a.variants and name in FWD_LAYER:
+        for v in map(int, a.variants.split(",")):
+            runs.append((f"{name}@v{v}", fn, flop, (FWD_LAYER[name], v)))
+    else:
+        runs.append((name, fn, flop, None))
+for name, fn, flop, var in runs:
+    if var is not None:
+        hip.f32_set_variant(*var)
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if a.graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(a.iters):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        g.replay()
+        e1.record()
+    else:
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+    torch.cuda.synchronize()
+    us = 1000.0 * e0.elapsed_time(e1) / a.iters
+    res[name] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1), "pct_peak": round(flop / us / 1e6 / 1.573, 1)}
+    if var is not None:
+        out = [getattr(w, ("a1", "a2", "a3", "z")[var[0] - 1]).clone() for w in wss]
+        ref0 = refs.setdefault(var[0], out)
+        same = all(torch.equal(x, y) for x, y in zip(out, ref0))
+        name += "" if same else " MISMATCH"
+        hip.f32_set_variant(var[0], 0)
+    if not a.json:
+        print(f"{name:12s} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)")
+if a.json:
+    print(json.dumps(res))
+tot = sum(r["us"] for r in res.values())
+print(f"total {tot:.1f} us")

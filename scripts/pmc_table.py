@@ -9,7 +9,8 @@ def main(paths):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for p in paths:
         for r in csv.DictReader(open(p)):
-            k = r["Kernel_Name"][:60]
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("apex::", "")
+            k = (k[5:] if k.startswith("void ") else k).split("(")[0][:70]
             key = (r.get("Dispatch_Id"), r["Counter_Name"])
             acc[k][r["Counter_Name"]].append((key, float(r["Counter_Value"])))
     names = sorted({c for k in acc for c in acc[k]})

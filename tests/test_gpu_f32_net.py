@@ -149,3 +149,31 @@ def test_f32_finalize_norm_partials(cuda):
     want = sum(float(t.double().pow(2).sum()) for t in trunk)
     got = float(sumsq[:n].sum())
     assert abs(got - want) <= 1e-6 * want
+
+
+def test_f32_packed_arena_stays_exact_under_training(cuda):
+    """The optimizer's fp32 PackMap / FcPack writes keep every packed copy EXACTLY equal to
+    a fresh permutation of the master weights (online net), and target sync / actor
+    publish copy the forward part (the kernels never see a stale or rounded weight)."""
+    from apex_amd.engine.apex import ApexEngine, EngineConfig
+    from apex_amd.engine.learner import LearnerConfig
+
+    cfg = EngineConfig(n_envs=64, replay_capacity=8192, threshold_size=2048, publish_param_interval=2,
+                       target_update_interval=3, learner=LearnerConfig(batch_size=64, forward="hip", dtype="fp32"))
+    eng = ApexEngine(cfg, cuda)
+    eng.fill()
+    for _ in range(2):
+        eng.train_step()
+    eng.capture()
+    for _ in range(4):
+        eng.train_step()
+    torch.cuda.synchronize()
+    L = eng.learner
+    got = L.net.arena.clone()
+    L.net.repack()
+    assert torch.equal(got, L.net.arena)
+    for net in (L.tnet, eng.actor_net):  # forward part matches its own master
+        fwd = net.arena[:net.fwd_numel].clone()
+        net.repack()
+        assert torch.equal(fwd, net.arena[:net.fwd_numel])
+    assert int(L.step_counter.item()) == 2 + 3 + 4
