@@ -425,6 +425,73 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
   }
 };
 
+// conv1 forward, sample-resident: one workgroup per (problem, sample).  The sample's four
+// 84x84 u8 planes (28 KB) are staged once into LDS with 16-byte loads (the GEMM-body
+// version gathered every 8x8 window from global memory, 4 bytes per load, each pixel four
+// times over); each wave keeps its half of W1 (16 output channels x K = 256) in registers
+// for the whole sample and sweeps output pixels in 16-row tiles on v_mfma_f32_16x16x4_f32:
+// 400 = 25 tiles exactly, waves {0,1} take channels 0-15 and {2,3} channels 16-31, each
+// pair splitting the 25 tiles 13/12.  A operand: lane (i = l & 15, q = l >> 4) reads ONE
+// dword of the plane row = 4 u8 pixels = k-slots 4q..4q+3 of a 16-k block (two ky rows x
+// 8 kx), converted with v_cvt_f32_ubyte*; MFMA i' of the block consumes element i', so its
+// k-slot q is k = 16 kb + 4q + i' and B (W1 row, reference k order) uses the same map.
+// Two accumulators (even / odd k-blocks) cover the 40-cycle dependent-MFMA latency.
+constexpr int kPlaneDw = kPlane / 4;  // 1764 dwords per plane
+__global__ __launch_bounds__(256) void f32_conv1_fwd_k(F32Set set) {
+  __shared__ __attribute__((aligned(16))) uint32_t pl[4 * kPlaneDw];
+  const int B = set.B, prob = blockIdx.x / B, b = blockIdx.x - prob * B;
+  const F32Prob p = pick(set, prob);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int j = lane & 15, q = lane >> 4, nh = wave >> 1;
+  // stage the planes: 4 x 441 16-byte chunks, all loads in flight before the first store
+  {
+    const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
+    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kChunks + 255) / 256;
+    const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
+    const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
+    const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
+    const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
+    uint4 v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {  // (no dynamically indexed pointer array: it would live in scratch)
+      const int e = min(t + 256 * i, kChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
+      const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
+      v[i] = sc[e - c * 441];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = t + 256 * i;
+      if (e < kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
+    }
+  }
+  // W1 fragments of this wave's 16 channels: breg[kb] = W1[nh*16 + j][16 kb + 4q .. +3]
+  f32x4 breg[16];
+  const float* wrow = p.w + (nh * 16 + j) * 256 + 4 * q;
+#pragma unroll
+  for (int kb = 0; kb < 16; ++kb) breg[kb] = ld4(wrow + 16 * kb);
+  __syncthreads();
+  const float bias = p.bias[nh * 16 + j];
+  float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + j;
+  for (int tile = wave & 1; tile < 25; tile += 2) {
+    const int m = tile * 16 + j, oy = m / 20, ox = m - oy * 20;
+    const uint32_t* a0 = pl + (4 * oy + (q >> 1)) * 21 + ox + (q & 1);
+    f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+    for (int kb = 0; kb < 16; kb += 2) {
+      // k-block kb: channel kb >> 2, rows ky = 2 (kb & 3) + (q >> 1)
+      const f32x4 x0 = u8x4(a0[(kb >> 2) * kPlaneDw + 2 * (kb & 3) * 21]);
+      const f32x4 x1 = u8x4(a0[((kb + 1) >> 2) * kPlaneDw + 2 * ((kb + 1) & 3) * 21]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[i], breg[kb][i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[i], breg[kb + 1][i], acc1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[(size_t)(tile * 16 + 4 * q + e) * 32] = fmaxf(acc0[e] + acc1[e] + bias, 0.f);
+  }
+}
+
 // ------------------------------------------------------------------ backward policies
 struct BwdArgs {
   const void* x;        // layer input (u8 frames for conv1: FrameSrc fields)
@@ -717,8 +784,8 @@ void check_set(const F32Set& set) {
 }  // namespace
 
 // ------------------------------------------------------------------ host launchers
-// conv1 forward tile variant (benchmark knob, f32_set_variant): 0 = BK 16 (default: the
-// smaller LDS footprint fits 4 workgroups per CU), 1 = BK 32
+// conv1 forward variant (benchmark knob, f32_set_variant): 0 = sample-resident kernel
+// (f32_conv1_fwd_k), 1 = generic GEMM body (128 x 32 x 16 tiles, windows gathered from global)
 int g_conv1_variant = 0;
 
 template <class P>
@@ -738,8 +805,12 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
   switch (layer) {
     case 1:
-      if (g_conv1_variant) fwd_launch<Conv1FwdT<128, 32, 32, 4>>(set, s);
-      else fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
+      if (g_conv1_variant == 1) {
+        fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
+      } else {
+        f32_conv1_fwd_k<<<set.n * set.B, 256, 0, s>>>(set);
+        LAUNCH_CHECK();
+      }
       break;
     case 2: fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s); break;
     case 3: fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s); break;
