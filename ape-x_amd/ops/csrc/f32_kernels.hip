@@ -39,9 +39,10 @@
 //   bwd  fc1 dgrad M=B N=3136 K=256 (+ReLU mask)          fc1 wgrad M=256 N=3136 K=B
 //        conv3/conv2 wgrad M=Cout N=taps*Cin K=B*P (split) conv3 dgrad M=B*81 N=64 K=576
 //        conv2 dgrad: 4 stride-2 sub-pixel classes, M=4*B*100 N=32 K=4*64
-//        conv1 wgrad M=32 N=256 K=B*400 (split, u8 frames)
+//        conv1 wgrad M=32 N=256 K=B*400 (sample-resident kernel, partial per 2 samples)
 // Independent backward GEMMs share one launch (gemm2_k: fc1 dgrad+wgrad, conv3 wgrad+dgrad,
-// conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.
+// conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.  conv1 (forward
+// and weight gradient) has its own sample-resident kernels: u8 frame planes staged in LDS.
 #include <algorithm>
 
 #include "common.h"
@@ -614,54 +615,6 @@ struct ConvWgrad {
   }
 };
 
-struct Conv1Wgrad {  // part[s][co][k = (c, ky, kx)] = sum_r dy1[r][co] frame(r, k)
-  static constexpr int BM = 32, BN = 128, BK = 32, WM = 1;
-  static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = true, A_COLSUM = true;
-  static constexpr int kMaxSamples = 8;
-  using Args = BwdArgs;
-  struct Smem {
-    const uint8_t* pl[kMaxSamples][4];
-  };
-  struct Ctx {
-    int n0, split, kb0, kb1, R, b0;
-  };
-  static __host__ __device__ int tiles(int, int splits) { return 2 * splits; }
-  static __device__ void decode(const Args& a, int block, Ctx& c, Smem& sm) {
-    c.split = block >> 1;
-    c.n0 = (block & 1) * BN;
-    c.R = a.B * 400;
-    c.kb0 = c.split * a.kbps;
-    c.kb1 = min(c.kb0 + a.kbps, (c.R + BK - 1) / BK);
-    c.b0 = (c.kb0 * BK) / 400;
-    const int t = threadIdx.x;
-    if (t < kMaxSamples * 4) {
-      const int b = c.b0 + (t >> 2), ch = t & 3;
-      const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
-      sm.pl[t >> 2][ch] = b < a.B ? frame_plane(f, b, ch, kPlane) : nullptr;
-    }
-  }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int r = kb * BK + row;
-    if (r >= c.R) return zero4();
-    return ld4(a.dy + (size_t)r * 32 + 4 * ch);
-  }
-  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem& sm, int kb, int row, int ch) {
-    const int r = kb * BK + row;
-    if (r >= c.R) return zero4();
-    const int b = r / 400, p = r - b * 400, oy = p / 20, ox = p - oy * 20;
-    const int k = c.n0 + 4 * ch, cc = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-    const uint8_t* pl = sm.pl[b - c.b0][cc];
-    return u8x4(*reinterpret_cast<const uint32_t*>(pl + (4 * oy + ky) * 84 + 4 * ox + kx));
-  }
-  static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
-    a.out[((size_t)c.split * 32 + m) * 256 + c.n0 + nl] = v;
-  }
-  static __device__ bool want_colsum(const Ctx& c) { return c.n0 == 0; }
-  static __device__ void store_colsum(const Args& a, const Ctx& c, int m, float v) {
-    a.out2[c.split * 32 + m] = v;
-  }
-};
-
 struct Conv3Dgrad {  // dy2[b][pi][ci] = (a2 > 0) * sum_{tap, co} dy3[b][pi - tap][co] W3[co][ci][tap]
   static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
@@ -739,6 +692,101 @@ struct Conv2Dgrad {
   }
 };
 
+// conv1 weight gradient, sample-resident: workgroup g (8 waves) holds samples 2g, 2g+1
+// (their frame planes staged in LDS once), wave w takes sample w >> 2 and input channel
+// c = w & 3, i.e. the 64 columns kk = c*64 + ky*8 + kx of dW1[32][256], as 2 (co halves) x 4
+// 16x16 tiles on v_mfma_f32_16x16x4_f32 with the PIXEL as the reduction index:
+//   A[i = co][slot q] = dy1[pixel p0 + q][co]              (one float per lane per 4 pixels)
+//   B[slot q][j]      = frame(pixel p0 + q, kk(j, i'))      with kk = c*64 + (j >> 1)*8 + 4 (j & 1) + i'
+// so ONE ds_read_b32 (4 u8 = kx 4(j&1)..+3 of row 4oy + (j >> 1)) feeds the 4 tiles i' and
+// both co halves: 8 independent accumulators per 4 pixels.  The two samples' partials are
+// added through LDS (fixed order) into partial g: ws[g][co][kk] + bias partials ws_b[g][co]
+// (sum of dy1 over the pixels), reduced over g by grad_finalize like the other layers.
+constexpr int kConv1WgradS = 2;  // samples per workgroup (partials = ceil(B / 2))
+__global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int j = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
+  const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
+  {  // stage both samples' planes: 2 x 4 x 441 16-byte chunks
+    const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
+    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
+    uint4 v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
+      v[i] = reinterpret_cast<const uint4*>(frame_plane(f, b0 + s2, ch, kPlane))[r - ch * 441];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = t + 512 * i;
+      if (e < ns * kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
+    }
+  }
+  __syncthreads();
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[h][i] = zero4();
+  float bs0 = 0.f, bs1 = 0.f;  // bias partials of co = j, 16 + j (wave c == 0)
+  if (sl < ns) {
+    const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
+    const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (j >> 1) * 21 + (j & 1);
+#pragma unroll 4
+    for (int p0 = 0; p0 < 400; p0 += 4) {
+      const int pix = p0 + q, oy = pix / 20, ox = pix - oy * 20;
+      const float x0 = dy[pix * 32 + j], x1 = dy[pix * 32 + 16 + j];
+      const f32x4 xb = u8x4(pc[4 * oy * 21 + ox]);
+      bs0 += x0;
+      bs1 += x1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[0][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, xb[i], acc[0][i], 0, 0, 0);
+        acc[1][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, xb[i], acc[1][i], 0, 0, 0);
+      }
+    }
+  }
+  // bias: sum the 4 pixel slots (lanes j, j+16, j+32, j+48)
+  bs0 += __shfl_xor(bs0, 16, 64);
+  bs0 += __shfl_xor(bs0, 32, 64);
+  bs1 += __shfl_xor(bs1, 16, 64);
+  bs1 += __shfl_xor(bs1, 32, 64);
+  // second sample's waves hand their tiles to the first's through LDS (planes are dead)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2][32]
+  if (sl == 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = acc[h][i][e];
+    if (c == 0 && q == 0) {
+      red[4 * 32 * 64 + j] = bs0;
+      red[4 * 32 * 64 + 16 + j] = bs1;
+    }
+  }
+  __syncthreads();
+  if (sl == 0) {
+    float* out = a.out + (size_t)blockIdx.x * 32 * 256;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = acc[h][i][e] + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
+          const int co = h * 16 + 4 * q + e, kk = c * 64 + (j >> 1) * 8 + 4 * (j & 1) + i;
+          out[co * 256 + kk] = v;
+        }
+    if (c == 0 && q == 0) {
+      a.out2[blockIdx.x * 32 + j] = bs0 + red[4 * 32 * 64 + j];
+      a.out2[blockIdx.x * 32 + 16 + j] = bs1 + red[4 * 32 * 64 + 16 + j];
+    }
+  }
+}
+
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
   int splits, kbps;
@@ -755,7 +803,7 @@ SplitPlan plan_splits(int rows, int ntiles, int target_blocks, int max_kbps) {
 
 SplitPlan wgrad_plan(int layer, int B) {
   switch (layer) {
-    case 1: return plan_splits(B * 400, 2, 512, 60);  // <= 60*32 rows -> <= 6 samples per split
+    case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_k workgroups
     case 2: return plan_splits(B * 81, 8, 256, 1 << 20);
     case 3: return plan_splits(B * 49, 9, 252, 1 << 20);
     default: throw std::invalid_argument("f32 wgrad layer");
@@ -883,7 +931,8 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
       launch2<ConvWgrad<2>, Conv2Dgrad>(g, ConvWgrad<2>::tiles(B, p.splits), d, Conv2Dgrad::tiles(B), s);
       break;
     case 1:
-      launch1<Conv1Wgrad>(g, Conv1Wgrad::tiles(B, p.splits), s);
+      f32_conv1_wgrad_k<<<p.splits, 512, 0, s>>>(g);
+      LAUNCH_CHECK();
       break;
     default: throw std::invalid_argument("f32_conv_bwd: layer must be 1, 2 or 3");
   }
