@@ -572,7 +572,11 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
   }
 };
 
-// conv wgrad (layers 2, 3): part[s][co][tap*C + ci] = sum_{r in split s} dy[r][co] x_col[r][tap, ci]
+// conv wgrad (layers 2, 3): part[s][co][tap*C + ci] = sum_{rows in split s} dy[row][co] x_col[row][tap, ci]
+// with POSITION-MAJOR rows: k-block kb = (output position p, block of 32 samples), so the
+// im2col address of a row is (sample) * plane + (position, tap) offset -- the position is
+// uniform per k-block (scalar), where sample-major rows paid ~30 VALU per 16-byte load
+// dividing the row index by P and OH (MI355X: conv3 wgrad 45 -> see profiles).
 template <int L>
 struct ConvWgrad {
   static constexpr int C = L == 3 ? 64 : 32, K = L == 3 ? 3 : 4, S = L == 3 ? 1 : 2;
@@ -583,25 +587,26 @@ struct ConvWgrad {
   using Args = BwdArgs;
   using Smem = NoSmem;
   struct Ctx {
-    int n0, split, kb0, kb1, R;
+    int n0, split, kb0, kb1, nbb, xoff;  // xoff: (tap, ci) offset of this thread's B chunk column
   };
+  static __host__ __device__ int kblocks(int B) { return P * ((B + BK - 1) / BK); }
   static __host__ __device__ int tiles(int, int splits) { return (N / BN) * splits; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     c.split = block / (N / BN);
     c.n0 = (block % (N / BN)) * BN;
-    c.R = a.B * P;
+    c.nbb = (a.B + BK - 1) / BK;
     c.kb0 = c.split * a.kbps;
-    c.kb1 = min(c.kb0 + a.kbps, (c.R + BK - 1) / BK);
+    c.kb1 = min(c.kb0 + a.kbps, kblocks(a.B));
   }
   static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int r = kb * BK + row;
-    if (r >= c.R) return zero4();
-    return ld4(a.dy + (size_t)r * 64 + 4 * ch);
+    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + row;
+    if (b >= a.B) return zero4();
+    return ld4(a.dy + ((size_t)b * P + p) * 64 + 4 * ch);
   }
   static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int r = kb * BK + row;
-    if (r >= c.R) return zero4();
-    const int b = r / P, p = r - b * P, oy = p / OH, ox = p - oy * OH;
+    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + row;
+    if (b >= a.B) return zero4();
+    const int oy = p / OH, ox = p - oy * OH;
     const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
     const float* x = static_cast<const float*>(a.x);
     return ld4(x + ((size_t)b * IH * IH + (S * oy + ky) * IH + S * ox + kx) * C + ci);
@@ -787,12 +792,121 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
   }
 }
 
+// Input-gradient GEMMs with POSITION-MAJOR rows: row m = (spatial position, sample), so all
+// rows of a tile share one input position and the same set of in-range taps.  The k loop runs
+// over exactly those taps -- the sample-major forms above multiply the zero border: 40% of
+// the conv3 dgrad MFMA work (21 of 27 (ky, iy) pairs in range per axis) and 19% of conv2's.
+struct Conv3DgradP {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b][pi - tap][co] w3t[tap][ci][co]
+  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int b0, pos, iy, ix, ky0, kx0, nkx, n0, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return 81 * 2 * ((B + BM - 1) / BM); }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tpp = (a.B + BM - 1) / BM;
+    c.n0 = (block & 1) * BN;
+    block >>= 1;
+    c.pos = block / tpp;
+    c.b0 = (block - c.pos * tpp) * BM;
+    c.iy = c.pos / 9;
+    c.ix = c.pos - c.iy * 9;
+    c.ky0 = max(0, c.iy - 6);
+    c.kx0 = max(0, c.ix - 6);
+    const int nky = min(2, c.iy) - c.ky0 + 1;
+    c.nkx = min(2, c.ix) - c.kx0 + 1;
+    c.kb0 = 0;
+    c.kb1 = 2 * nky * c.nkx;
+  }
+  static __device__ void tap_of(const Ctx& c, int kb, int& ky, int& kx) {
+    const int ti = kb >> 1, r = ti / c.nkx;
+    ky = c.ky0 + r;
+    kx = c.kx0 + ti - r * c.nkx;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = c.b0 + row;
+    if (b >= a.B) return zero4();
+    int ky, kx;
+    tap_of(c, kb, ky, kx);
+    return ld4(a.dy + ((size_t)b * 49 + (c.iy - ky) * 7 + c.ix - kx) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    int ky, kx;
+    tap_of(c, kb, ky, kx);
+    return ld4(a.w + ((ky * 3 + kx) * 64 + c.n0 + n) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
+    const int b = c.b0 + ml;
+    if (b >= a.B) return;
+    const size_t o = ((size_t)b * 81 + c.pos) * 64 + c.n0 + n;
+    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
+  }
+};
+
+// conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
+// output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
+struct Conv2DgradP {
+  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
+  using Args = BwdArgs;
+  using Smem = NoSmem;
+  struct Ctx {
+    int b0, cls, jy, jx, ty0, tx0, ntx, kb0, kb1;
+  };
+  static __host__ __device__ int tiles(int B) { return 400 * ((B + BM - 1) / BM); }
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
+    const int tpp = (a.B + BM - 1) / BM;
+    const int pos = block / tpp;  // cls * 100 + jy * 10 + jx
+    c.b0 = (block - pos * tpp) * BM;
+    c.cls = pos / 100;
+    const int jj = pos - c.cls * 100;
+    c.jy = jj / 10;
+    c.jx = jj - c.jy * 10;
+    c.ty0 = c.jy == 9 ? 1 : 0;
+    c.tx0 = c.jx == 9 ? 1 : 0;
+    const int nty = (c.jy == 0 ? 0 : 1) - c.ty0 + 1;
+    c.ntx = (c.jx == 0 ? 0 : 1) - c.tx0 + 1;
+    c.kb0 = 0;
+    c.kb1 = 2 * nty * c.ntx;
+  }
+  static __device__ void tap_of(const Ctx& c, int kb, int& ty, int& tx) {
+    const int ti = kb >> 1, r = c.ntx == 2 ? ti >> 1 : ti;
+    ty = c.ty0 + r;
+    tx = c.tx0 + ti - r * c.ntx;
+  }
+  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
+    const int b = c.b0 + row;
+    if (b >= a.B) return zero4();
+    int ty, tx;
+    tap_of(c, kb, ty, tx);
+    return ld4(a.dy + ((size_t)b * 81 + (c.jy - ty) * 9 + c.jx - tx) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
+    int ty, tx;
+    tap_of(c, kb, ty, tx);
+    const int ky = (c.cls >> 1) + 2 * ty, kx = (c.cls & 1) + 2 * tx;
+    return ld4(a.w + ((ky * 4 + kx) * 32 + n) * 64 + (kb & 1) * 32 + 4 * ch);
+  }
+  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
+    const int b = c.b0 + ml;
+    if (b >= a.B) return;
+    const int iy = 2 * c.jy + (c.cls >> 1), ix = 2 * c.jx + (c.cls & 1);
+    const size_t o = ((size_t)b * 400 + iy * 20 + ix) * 32 + n;
+    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
+  }
+};
+
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
   int splits, kbps;
 };
-SplitPlan plan_splits(int rows, int ntiles, int target_blocks, int max_kbps) {
-  const int kbt = (rows + 31) / 32;
+// conv2/conv3 weight-gradient workgroups per CU (256 CUs): more splits = more waves to hide
+// latency, but more partials for grad_finalize to reduce
+int g_wgrad_occ = 1;
+
+SplitPlan plan_splits(int kbt, int ntiles, int target_blocks, int max_kbps) {
   int s = std::max(1, target_blocks / ntiles);
   int kbps = (kbt + s - 1) / s;
   if (kbps > max_kbps) kbps = max_kbps;
@@ -804,8 +918,8 @@ SplitPlan plan_splits(int rows, int ntiles, int target_blocks, int max_kbps) {
 SplitPlan wgrad_plan(int layer, int B) {
   switch (layer) {
     case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_k workgroups
-    case 2: return plan_splits(B * 81, 8, 256, 1 << 20);
-    case 3: return plan_splits(B * 49, 9, 252, 1 << 20);
+    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 8, 256 * g_wgrad_occ, 1 << 20);
+    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 9, 252 * g_wgrad_occ, 1 << 20);
     default: throw std::invalid_argument("f32 wgrad layer");
   }
 }
@@ -841,9 +955,16 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
   launch1<P>(set, set.n * P::tiles(set.B), s);
 }
 
+// backward benchmark knobs: g_bwd_mode (0 both GEMMs of a conv backward launch, 1 weight
+// gradient only, 2 input gradient only), g_dgrad_variant (0 position-major, 1 sample-major)
+int g_bwd_mode = 0, g_dgrad_variant = 0;
+
 void f32_set_variant(int layer, int v) {
-  if (layer != 1 || v < 0 || v > 1) throw std::invalid_argument("f32_set_variant: layer 1, v 0..1");
-  g_conv1_variant = v;
+  if (layer == 1 && v >= 0 && v <= 1) g_conv1_variant = v;
+  else if (layer == 5 && v >= 0 && v <= 2) g_bwd_mode = v;
+  else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
+  else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
+  else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
 // Tiles (MI355X, 3 x 512-sample launches): 128 x 32 blocks, one 32x32 accumulator per wave,
@@ -923,12 +1044,20 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.mask = mask;
   d.out = dx;
   d.B = B;
+  const int mode = g_bwd_mode;  // benchmark knob: 0 both, 1 weight gradient only, 2 input gradient only
+  const int nw3 = mode == 2 ? 0 : ConvWgrad<3>::tiles(B, p.splits), nw2 = mode == 2 ? 0 : ConvWgrad<2>::tiles(B, p.splits);
   switch (layer) {
     case 3:
-      launch2<ConvWgrad<3>, Conv3Dgrad>(g, ConvWgrad<3>::tiles(B, p.splits), d, Conv3Dgrad::tiles(B), s);
+      if (g_dgrad_variant)
+        launch2<ConvWgrad<3>, Conv3Dgrad>(g, nw3, d, mode == 1 ? 0 : Conv3Dgrad::tiles(B), s);
+      else
+        launch2<ConvWgrad<3>, Conv3DgradP>(g, nw3, d, mode == 1 ? 0 : Conv3DgradP::tiles(B), s);
       break;
     case 2:
-      launch2<ConvWgrad<2>, Conv2Dgrad>(g, ConvWgrad<2>::tiles(B, p.splits), d, Conv2Dgrad::tiles(B), s);
+      if (g_dgrad_variant)
+        launch2<ConvWgrad<2>, Conv2Dgrad>(g, nw2, d, mode == 1 ? 0 : Conv2Dgrad::tiles(B), s);
+      else
+        launch2<ConvWgrad<2>, Conv2DgradP>(g, nw2, d, mode == 1 ? 0 : Conv2DgradP::tiles(B), s);
       break;
     case 1:
       f32_conv1_wgrad_k<<<p.splits, 512, 0, s>>>(g);

@@ -23,6 +23,8 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--wgrad-occ", type=int, default=0, help="conv2/3 wgrad workgroups per CU (knob 7; 0 = default)")
+ap.add_argument("--bwd-sweep", action="store_true", help="conv backward: wgrad / dgrad split and dgrad variants")
 ap.add_argument("--variants", default=None, help="forward tile variants to sweep, e.g. 0,1,2,3 (f32_set_variant)")
 a = ap.parse_args()
 dev = torch.device("cuda")
@@ -32,6 +34,8 @@ m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
 m.flatten_parameters()
 for p in m.parameters():
     p.grad = torch.zeros_like(p)
+if a.wgrad_occ:
+    hip.f32_set_variant(7, a.wgrad_occ)
 net = F32DuelingNet(m)
 net.enable_backward(B)
 F = 4 * B
@@ -83,6 +87,10 @@ cases = {
     "conv2_bwd": (lambda: hip.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), net.w2t.data_ptr(),
                                            ws.a1.data_ptr(), ws.dy1.data_ptr(), w2.data_ptr(), B, S()),
                   2 * 2 * B * 81 * 64 * 512),
+    "finalize": (lambda: hip.grad_finalize(
+        [hip.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
+                                   f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))],
+        S(), 0), 1),
     "conv1_wgrad": (lambda: hip.f32_conv_bwd(1, frames.data_ptr(), ids.data_ptr(), idx.data_ptr(), ws.dy1.data_ptr(),
                                              0, 0, 0, w1.data_ptr(), B, S()), 2 * B * 400 * 32 * 256),
 }
@@ -97,8 +105,18 @@ for name, (fn, flop) in cases.items():
             runs.append((f"{name}@v{v}", fn, flop, (FWD_LAYER[name], v)))
     else:
         runs.append((name, fn, flop, None))
+if a.bwd_sweep:  # (label, knob settings, flop scale); dgrad outputs checked against the sample-major form
+    for nm in ("conv3_bwd", "conv2_bwd"):
+        fn, flop = cases[nm]
+        for lab, knobs, fr in (("wgrad", ((5, 1),), 0.5), ("dgrad_pos", ((5, 2), (6, 0)), 0.5),
+                               ("both_pos", ((5, 0), (6, 0)), 1.0)):
+            runs.append((f"{nm}:{lab}", fn, flop * fr, knobs))
 for name, fn, flop, var in runs:
-    if var is not None:
+    if var is not None and isinstance(var[0], tuple):
+        for k in var:
+            hip.f32_set_variant(*k)
+        var = ("knobs", var)
+    elif var is not None:
         hip.f32_set_variant(*var)
     fn()
     torch.cuda.synchronize()
@@ -121,7 +139,15 @@ for name, fn, flop, var in runs:
     torch.cuda.synchronize()
     us = 1000.0 * e0.elapsed_time(e1) / a.iters
     res[name] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1), "pct_peak": round(flop / us / 1e6 / 1.573, 1)}
-    if var is not None:
+    if var is not None and var[0] == "knobs":
+        if "dgrad" in name or "both" in name:
+            dx = (ws.dy2 if name.startswith("conv3") else ws.dy1).clone()
+            key = name.split(":")[0]
+            ref0 = refs.setdefault(key, dx)
+            name += "" if torch.equal(dx, ref0) else " MISMATCH"
+        hip.f32_set_variant(5, 0)
+        hip.f32_set_variant(6, 0)
+    elif var is not None:
         out = [getattr(w, ("a1", "a2", "a3", "z")[var[0] - 1]).clone() for w in wss]
         ref0 = refs.setdefault(var[0], out)
         same = all(torch.equal(x, y) for x, y in zip(out, ref0))
