@@ -54,7 +54,7 @@ class EngineConfig:
     total_actors: int | None = None
     use_graphs: bool = True
     overlap: bool = False                # actor graph on its own stream, concurrent with the learner
-    exact_mass: bool = True
+    exact_mass: bool = False             # SURVEY Q5 parity: the newest slot is excluded from the sampled mass
     # overlap mode: how the actor and learner streams reach separate hardware queues.
     # HIP spreads the streams of one priority over GPU_MAX_HW_QUEUES (4) shared queues,
     # so with enough streams in the process (RCCL/PG streams, torch's stream pools) the

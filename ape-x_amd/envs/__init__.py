@@ -1,7 +1,7 @@
 """Environments: gym-API classic control, synthetic Atari + DeepMind wrappers.
 
 ``apex_amd.envs.make(id)`` is the ``gym.make`` of this framework.  The GPU-resident
-vectorised Atari env for the engine lives in :mod:`apex_amd.engine.vec_env`.
+vectorised Atari env for the engine is the `vec_env_*` HIP kernels (ops/csrc/actor_kernels.hip) driven by :mod:`apex_amd.engine.actor_shard`.
 """
 from . import spaces
 from .core import Env, EnvSpec, ObservationWrapper, RewardWrapper, TimeLimit, Wrapper, make, register, registered

@@ -11,7 +11,7 @@ wrap_atari_dqn), with WarpFrame's grayscale + INTER_AREA resize implemented as a
 separable area-averaging matrix product (no OpenCV).
 
 The GPU-resident vector env used by the high-throughput engine
-(:mod:`apex_amd.engine.vec_env`) renders the same game family straight to 84x84.
+(`vec_env_step_k`, ops/csrc/actor_kernels.hip, driven by :mod:`apex_amd.engine.actor_shard`) renders the same game family straight to 84x84.
 """
 from __future__ import annotations
 

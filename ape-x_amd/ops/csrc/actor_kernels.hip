@@ -408,7 +408,29 @@ __global__ void apply_staged_rows_k(TransTable st, TransTable dst, const int* __
   dst.done[j] = st.done[e];
 }
 
+// evaluator envs (no n-step batcher): advance each env's observation stack and the step
+// counter that seeds the env / action draws (lane 0 of block 0)
+__global__ void frame_hist_step_k(int* __restrict__ hist, const int* __restrict__ new_frame,
+                                  const float* __restrict__ done, int E, int64_t* counter) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0 && counter) counter[0] += 1;
+  if (e >= E) return;
+  const int f = new_frame[e];
+  int* h = hist + e * 4;
+  if (done[e] > 0.f) {
+    h[0] = h[1] = h[2] = h[3] = f;
+  } else {
+    h[0] = h[1]; h[1] = h[2]; h[2] = h[3]; h[3] = f;
+  }
+}
+
 // ------------------------------------------------------------------ launchers
+void frame_hist_step(int* hist, const int* new_frame, const float* done, int E, int64_t* counter, hipStream_t s) {
+  if (E <= 0) return;
+  frame_hist_step_k<<<(E + 255) / 256, 256, 0, s>>>(hist, new_frame, done, E, counter);
+  LAUNCH_CHECK();
+}
+
 void vec_env_reset(float* state, uint64_t seed, uint8_t* frames, const VecEnvParams& p,
                    const int64_t* step_counter, int* new_frame, int* hist, float* ep_log, hipStream_t s) {
   if (p.frame_bytes != kScreen * kScreen) throw std::invalid_argument("vec env renders 84x84 frames");

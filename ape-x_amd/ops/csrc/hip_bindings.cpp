@@ -139,6 +139,9 @@ PYBIND11_MODULE(_apex_hip, m) {
                             uint64_t s) {
     gather_frames(P<const uint8_t>(frames), frame_bytes, P<const int>(ids), N, stack, P<uint8_t>(out), S(s));
   });
+  m.def("frame_hist_step", [](uint64_t hist, uint64_t new_frame, uint64_t done, int E, uint64_t counter, uint64_t s) {
+    frame_hist_step(P<int>(hist), P<const int>(new_frame), P<const float>(done), E, P<int64_t>(counter), S(s));
+  });
   m.def("bump_counter", [](uint64_t c, int n, int64_t by, uint64_t s) { bump_counter(P<int64_t>(c), n, by, S(s)); });
 
   // ---- actor shard

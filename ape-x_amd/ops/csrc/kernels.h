@@ -86,6 +86,8 @@ void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids
 void gather_frames(const uint8_t* frames, int frame_bytes, const int* ids, int N, int stack, uint8_t* out,
                    hipStream_t s);
 void bump_counter(int64_t* counter, int n, int64_t by, hipStream_t s);
+// evaluator envs: FrameStack advance (done: the new frame repeated 4x) + counter += 1
+void frame_hist_step(int* hist, const int* new_frame, const float* done, int E, int64_t* counter, hipStream_t s);
 
 // ---- actor_kernels.hip
 struct VecEnvParams {

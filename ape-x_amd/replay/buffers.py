@@ -13,7 +13,7 @@ walk, no lock).  Sampling draws its B stratum offsets from Python's ``random`` i
 the reference's order, so for equal seeds indices/weights match the reference
 exactly.  ``exact_mass=False`` (default) reproduces the reference's exclusive-end
 mass (the newest slot excluded); ``exact_mass=True`` samples over the
-full mass.  The GPU/HBM replay used by the engine is :mod:`apex_amd.replay.gpu`.
+full mass.  The GPU/HBM replay used by the engine is :mod:`apex_amd.engine.hbm_replay`.
 """
 from __future__ import annotations
 

@@ -43,6 +43,10 @@ def parser():
     p.add_argument("--log-dir", default=None, help="event-file directory (default runs/<time>-<env>-learner)")
     p.add_argument("--no-tb", action="store_true")
     p.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal with gloo)")
+    p.add_argument("--eval-envs", type=int, default=8,
+                   help="greedy evaluator envs on rank 0 (eps 0, unclipped rewards, origin_repo/eval.py); 0 = off")
+    p.add_argument("--eval-interval", type=int, default=50, help="learner steps between evaluator chunks")
+    p.add_argument("--eval-steps", type=int, default=25, help="evaluator env steps per chunk")
     return p
 
 
@@ -200,14 +204,42 @@ def main(argv=None) -> int:
     if rank == 0:
         print(f"replay warm ({time.perf_counter() - t_fill:.1f}s); training from step {start}", flush=True)
 
+    evaluator = None
+    if rank == 0 and args.eval_envs > 0:
+        from .engine.evaluator import GPUEvaluator
+
+        src_model = eng.actor_model if hasattr(eng, "actor_model") else learner.model
+        evaluator = GPUEvaluator(src_model, args.eval_envs, args.actions, forward=cfg.kernel.forward,
+                                 dtype=cfg.kernel.dtype, device=device, seed=cfg.seed + 31337,
+                                 episode_life=bool(cfg.env.episode_life), max_episode_steps=cfg.env.max_episode_length)
+        eval_stream = torch.cuda.Stream(device=device)
+        ev_loaded = torch.cuda.Event()
+
+    def eval_chunk():
+        """Latest published weights -> evaluator (ordered after the publish on the training
+        stream, which in turn waits only for the copy), then greedy steps on the side stream."""
+        cur = torch.cuda.current_stream(device)
+        eval_stream.wait_stream(cur)
+        with torch.cuda.stream(eval_stream):
+            if hasattr(eng, "actor_flat"):
+                evaluator.load(eng.actor_flat, getattr(eng, "actor_net", None))
+            else:
+                evaluator.load(learner.flat, getattr(learner, "net", None))
+            ev_loaded.record(eval_stream)
+            evaluator.run(args.eval_steps)
+        cur.wait_event(ev_loaded)
+
     max_step = int(L.max_step)
     bps_every = max(1, L.bps_interval)
     frames_per_round = n_actor_gpus * args.actor_steps * eng.frames_per_actor_step
     step = eng.learn_steps  # capture's warm-up steps are real training steps
     t_last, step_last = time.perf_counter(), step
+    eval_rets, eval_lens = [], []
     while not max_step or step < max_step:
         eng.train_step()
         step = eng.learn_steps
+        if evaluator is not None and step % max(1, args.eval_interval) == 0:
+            eval_chunk()
         if step % bps_every == 0:
             torch.cuda.synchronize(device)
             now = time.perf_counter()
@@ -215,10 +247,22 @@ def main(argv=None) -> int:
             t_last, step_last = now, step
             if learner is not None and rank == 0:
                 st = learner.stats()
+                # sharded DP: one synchronous update per step over a global batch of B * world, so
+                # updates/s = sps and batches of B sampled per second = sps * world
                 line = {"learner/loss": st["loss"], "learner/grad_norm": st["grad_norm"],
                         "learner/grad_norm_l2": st["grad_norm_l2"], "learner/BPS": sps,
-                        "learner/steps_per_sec": sps * (world if topology == "sharded" else 1),
+                        "learner/updates_per_sec": sps,
+                        "learner/batches_per_sec": sps * (world if topology == "sharded" else 1),
                         "actor/frames_per_sec": sps * frames_per_round}
+                if evaluator is not None:
+                    for r, n in evaluator.poll():
+                        eval_rets.append(r)
+                        eval_lens.append(n)
+                    if eval_rets:  # episodes finished since the last log line
+                        line["evaluator/episode_reward"] = sum(eval_rets) / len(eval_rets)
+                        line["evaluator/episode_length"] = sum(eval_lens) / len(eval_lens)
+                        line["evaluator/episodes"] = float(evaluator.episodes)
+                        eval_rets, eval_lens = [], []
                 shard = getattr(eng, "actor", None)
                 if shard is not None:
                     ret, length, count = shard.episode_stats()
