@@ -1,0 +1,464 @@
+"""GPU AQL engine: distributed-actor Amortized Q-Learning with everything on one MI355X
+(BASELINE config 4; reference AQL_dis.py:18-170, batchrecoder_AQL.py:13-138,
+utils.py:44-61, model.py:112-390, memory.py:364-391).
+
+What runs where (all device-side, no host sync inside an iteration):
+
+* ``E`` vectorised GPU envs (``aql_env_step``: BipedalWalker-shaped / CartPole / Pendulum
+  dynamics of :mod:`apex_amd.envs.classic`) act with a published copy of the online
+  network: on-device candidate proposal (``aql_propose``: uniform + MVN / Categorical on
+  Philox), the fused candidate critic (``aql_candidate_q``) and per-env epsilon-greedy
+  selection (``aql_select``) with the reference worker ladder eps_i = 0.4^(1 + 7 i/(N-1))
+  (batchrecoder_AQL.py:97-99).  Each step inserts the raw (s, a, r, s', d, a_mu)
+  transitions into the HBM replay ring at max priority (no n-step, no actor priorities:
+  batchrecoder_AQL.py:48-51; the 24x duplicate insert of the reference, Q8, is not
+  reproduced).
+* :class:`AQLReplay`: tables ``[C, obs]`` x2, action/reward/done ``[C]``, the candidate
+  sets ``a_mu [C, T, adim]`` and the fanout-64 HBM priority tree shared with the DQN
+  engine (``per_*`` kernels).
+* One learner step (``AQLLearner.step``; AQL_dis.py:63-108) = stratified PER sample ->
+  ``aql_learn_fwd`` (online Q(s,.), Q(s',.), target Q(s',.) over the stored candidates,
+  fp32 MFMA) -> ``aql_learn_bwd`` (Double-Q Huber TD, proposal log-prob/entropy loss,
+  backward vectors) -> priority write (0.9 max + 0.1 |td| + 1e-6 mix, fused) ->
+  ``aql_grad`` (both losses' weight gradients + per-group norms) -> two Adam steps with
+  separate clip_grad_norm_(40) (critic, proposal) -> ``aql_post`` (reset_noise() of the
+  online and target NoisyNets + proposal hard copy online -> target, AQL_dis.py:92,104-105).
+  K learner steps are captured in one hipGraph.
+
+Iteration = one actor step of all E envs + ``E // batch`` learner steps: the reference's
+replay ratio (``total_ep_len // batch_size`` SGD steps per recorded batch, AQL_dis.py:118).
+Weights are published to the actors every iteration (set_worker_weights, AQL_dis.py:115)
+and the target network is synced every ``target_update_steps`` learner steps.
+
+Reference behaviours kept: q.features (the state embedding feeding the proposal) receives
+gradient only from the proposal loss, which optimizer_q zeroes before its own backward, so
+it never changes (its Adam step sees a None/zero gradient); the discrete proposal loss
+broadcasts log_prob([B,1]) against batch [B] (see aql_engine_kernels.hip).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import envs, ops
+from ..algo.schedules import actor_epsilon
+from ..models.aql import AQL
+from ..models.aql_fused import FusedAQL
+from .hbm_replay import tree_level_sizes
+
+ENV_KINDS = {"BipedalWalker-v3": 0, "CartPole-v0": 1, "CartPole-v1": 1, "Pendulum-v0": 2, "Pendulum-v1": 2}
+
+
+def flatten_module_params(module: torch.nn.Module) -> torch.Tensor:
+    """Re-seat every parameter of ``module`` as a view of one contiguous fp32 buffer
+    (named_parameters order); returns the buffer."""
+    params = list(module.parameters())
+    flat = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=params[0].device)
+    off = 0
+    for p in params:
+        n = p.numel()
+        flat[off:off + n].copy_(p.data.reshape(-1))
+        p.data = flat[off:off + n].view_as(p.data)
+        off += n
+    return flat
+
+
+def flatten_noise(model: AQL) -> torch.Tensor:
+    """Re-seat the four NoisyLinear epsilon buffers of ``model.q`` as views of one buffer:
+    [advantage1.weight_epsilon, advantage1.bias_epsilon, advantage2.weight_epsilon,
+    advantage2.bias_epsilon]."""
+    bufs = [model.q.advantage1.weight_epsilon, model.q.advantage1.bias_epsilon,
+            model.q.advantage2.weight_epsilon, model.q.advantage2.bias_epsilon]
+    flat = torch.empty(sum(b.numel() for b in bufs), dtype=torch.float32, device=bufs[0].device)
+    off = 0
+    for b in bufs:
+        n = b.numel()
+        flat[off:off + n].copy_(b.reshape(-1))
+        b.data = flat[off:off + n].view_as(b)
+        off += n
+    return flat
+
+
+class AQLReplay:
+    """HBM prioritized replay with candidate sets (reference CustomPrioritizedReplayBuffer_AQL,
+    memory.py:364-391): insert at max priority, proportional stratified sampling with IS
+    weights, priorities**alpha in the fanout-64 device tree."""
+
+    def __init__(self, capacity: int, obs: int, T: int, adim: int, alpha: float = 0.6,
+                 device: str | torch.device = "cuda", seed: int = 0):
+        self.hip = ops.hip()
+        self.device = torch.device(device)
+        self.capacity, self.obs, self.T, self.adim = int(capacity), int(obs), int(T), int(adim)
+        self.alpha, self.seed = float(alpha), int(seed)
+        C, dev = self.capacity, self.device
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.st = torch.zeros(C, obs, **f32)
+        self.st2 = torch.zeros(C, obs, **f32)
+        self.action = torch.zeros(C, dtype=torch.int32, device=dev)
+        self.reward = torch.zeros(C, **f32)
+        self.done = torch.zeros(C, **f32)
+        self.a_mu = torch.zeros(C, T, adim, **f32)
+        sizes = tree_level_sizes(C)
+        self.level_sizes = sizes
+        self.leaf_sum = torch.zeros(C, **f32)
+        self.leaf_min = torch.full((C,), math.inf, **f32)
+        self.node_sum = [torch.zeros(n, dtype=torch.float64, device=dev) for n in sizes[1:]]
+        self.node_min = [torch.full((n,), math.inf, **f32) for n in sizes[1:]]
+        self.max_prio = torch.ones(1, **f32)
+        self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.sorted_scratch = torch.zeros(1024, dtype=torch.int32, device=dev)
+        self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
+                                       [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
+                                       sizes)
+
+    def nbytes(self) -> int:
+        ts = [self.st, self.st2, self.action, self.reward, self.done, self.a_mu, self.leaf_sum, self.leaf_min,
+              *self.node_sum, *self.node_min]
+        return sum(t.numel() * t.element_size() for t in ts)
+
+    def table_ptrs(self) -> dict:
+        return {"st": self.st.data_ptr(), "st2": self.st2.data_ptr(), "rew": self.reward.data_ptr(),
+                "done": self.done.data_ptr(), "amu": self.a_mu.data_ptr(), "act": self.action.data_ptr()}
+
+    def __len__(self) -> int:
+        return int(min(self.filled.item(), self.capacity))
+
+    def total_priority(self) -> float:
+        return float(self.node_sum[-1][0].item())
+
+
+@dataclass
+class AQLEngineConfig:
+    env_id: str = "BipedalWalker-v3"
+    n_envs: int = 256
+    capacity: int = 1_000_000
+    batch_size: int = 32
+    gamma: float = 0.99
+    n_steps: int = 1
+    lr: float = 1e-3
+    ent_lam: float = 0.8
+    propose_sample: int = 1
+    uniform_sample: int = 50
+    action_var: float = 0.25
+    alpha: float = 0.6
+    beta_start: float = 0.4
+    max_step: int = 1_000_000      # beta annealing horizon, in iterations (AQL_dis.py:57)
+    n_workers: int = 10            # the reference's beta-annealing factor (AQL_dis.py:57)
+    max_norm: float = 40.0
+    learner_steps: int | None = None   # per iteration; None = n_envs // batch_size
+    target_update_steps: int = 2000    # learner steps between target syncs
+    eps_base: float = 0.4
+    eps_alpha: float = 7.0
+    total_actors: int | None = None    # epsilon ladder width (multi-GPU: all actors)
+    actor_offset: int = 0
+    threshold: int | None = None       # transitions before learning (default batch_size + 1)
+    exact_mass: bool = False           # False = reference sampling mass (Q5)
+    use_graphs: bool = True
+    seed: int = 0
+
+
+class AQLLearner:
+    """Device-resident AQL learner over an :class:`AQLReplay` (see module docstring)."""
+
+    def __init__(self, model: AQL, target: AQL, replay: AQLReplay, cfg: AQLEngineConfig):
+        self.hip = h = ops.hip()
+        self.cfg, self.model, self.target, self.replay = cfg, model, target, replay
+        dev = replay.device
+        self.device = dev
+        self.flat = flatten_module_params(model)
+        self.tflat = flatten_module_params(target)
+        self.eps = flatten_noise(model)
+        self.teps = flatten_noise(target)
+        names = [n for n, _ in model.named_parameters()]
+        self.P = self.flat.numel()
+        self.P_q = sum(p.numel() for n, p in model.named_parameters() if n.startswith("q."))
+        assert all(n.startswith("q.") for n in names[:sum(1 for n in names if n.startswith("q."))]), \
+            "critic parameters must precede the proposal's in the flat layout"
+        self.P_p = self.P - self.P_q
+        B, T = cfg.batch_size, model.total_sample
+        self.B, self.T = B, T
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.idx = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.w = torch.zeros(B, **f32)
+        self.q_s = torch.zeros(B, T, **f32)
+        self.q_s2 = torch.zeros(B, T, **f32)
+        self.qt_s2 = torch.zeros(B, T, **f32)
+        lay = h.aql_vec_layout()
+        self.lay = lay
+        self.vec = torch.zeros(B, lay["STRIDE"], **f32)
+        self.delta = torch.zeros(B, **f32)
+        self.lw = torch.zeros(B, **f32)
+        self.lossp = torch.zeros(B, **f32)
+        self.prio = torch.zeros(B, **f32)
+        self.loss_q = torch.zeros(1, **f32)
+        self.loss_p = torch.zeros(1, **f32)
+        self.grad = torch.zeros(self.P, **f32)
+        self.m = torch.zeros(self.P, **f32)
+        self.v = torch.zeros(self.P, **f32)
+        self.nblk = h.aql_grad_blocks(self.P)
+        self.part = torch.zeros(2 * self.nblk, dtype=torch.float64, device=dev)
+        self.norms_q = torch.zeros(4, **f32)
+        self.norms_p = torch.zeros(4, **f32)
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.beta = torch.full((1,), cfg.beta_start, **f32)
+        self.var = model.proposal.action_var.to(**f32).contiguous()
+        self.hp = h.AdamParams(cfg.lr, max_norm=cfg.max_norm)
+        self.fused_on = FusedAQL(model)
+        self.fused_tg = FusedAQL(target)
+        p = dict(replay.table_ptrs(), idx=self.idx.data_ptr(), w=self.w.data_ptr(), var=self.var.data_ptr(),
+                 q_s=self.q_s.data_ptr(), q_s2=self.q_s2.data_ptr(), qt_s2=self.qt_s2.data_ptr(),
+                 vec=self.vec.data_ptr(), delta=self.delta.data_ptr(), lw=self.lw.data_ptr(),
+                 lossp=self.lossp.data_ptr())
+        self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
+                                  float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
+        self.G = h.make_aql_grad(self._grad_jobs(), self.P, self.vec.data_ptr(), B, self.grad.data_ptr(),
+                                 self.part.data_ptr(), self.lossp.data_ptr(), self.loss_p.data_ptr())
+        layers = []
+        for m in (model, target):
+            for lin in (m.q.advantage1, m.q.advantage2):
+                layers.append((lin.weight_epsilon.data_ptr(), lin.bias_epsilon.data_ptr(), lin.out_features,
+                               lin.in_features))
+        self.post = h.make_aql_post(layers, self.flat[self.P_q:].data_ptr(), self.tflat[self.P_q:].data_ptr(),
+                                    self.P_p, self.step_ctr.data_ptr(), self.ticket.data_ptr(),
+                                    (cfg.seed * 0x9E3779B1 + 0x5EED) & 0xFFFFFFFFFFFF)
+
+    def _grad_jobs(self):
+        lay, m = self.lay, self.model
+        cont = m.env_iscontinuous
+        a1, a2 = m.q.advantage1, m.q.advantage2
+        spec = {
+            "q.q_feature.0.weight": ("GQFH", "S", None), "q.q_feature.0.bias": ("GQFH", None, None),
+            "q.q_feature.2.weight": ("GX+", "QFH", None), "q.q_feature.2.bias": ("GX+", None, None),
+            "q.action_out.0.weight": ("GAOH" if cont else "GX", "A", None),
+            "q.action_out.0.bias": ("GAOH" if cont else "GX", None, None),
+            "q.action_out.2.weight": ("GX", "AOH", None), "q.action_out.2.bias": ("GX", None, None),
+            "q.advantage1.weight_mu": ("GH", "X", None), "q.advantage1.weight_sigma": ("GH", "X", a1.weight_epsilon),
+            "q.advantage1.bias_mu": ("GH", None, None), "q.advantage1.bias_sigma": ("GH", None, a1.bias_epsilon),
+            "q.advantage2.weight_mu": ("GQ", "H", None), "q.advantage2.weight_sigma": ("GQ", "H", a2.weight_epsilon),
+            "q.advantage2.bias_mu": ("GQ", None, None), "q.advantage2.bias_sigma": ("GQ", None, a2.bias_epsilon),
+            "proposal.dist_feature.0.weight": ("GHID", "EMB", None), "proposal.dist_feature.0.bias": ("GHID", None, None),
+            "proposal.dist_feature.2.weight": ("GMU", "HID", None), "proposal.dist_feature.2.bias": ("GMU", None, None),
+        }
+        jobs, off = [], 0
+        for name, p in m.named_parameters():
+            rows = p.shape[0]
+            cols = p.numel() // rows
+            group = 1 if name.startswith("proposal.") else 0
+            if name.startswith("q.features."):
+                jobs.append((off, rows, cols, 0, -1, 0, group, 1))
+            else:
+                g, x, eps = spec[name]
+                goff = lay["GX"] + 64 if g == "GX+" else lay[g]
+                xoff = -1 if x is None else lay[x]
+                if xoff < 0:
+                    rows, cols = p.numel(), 1
+                jobs.append((off, rows, cols, goff, xoff, 0 if eps is None else eps.data_ptr(), group, 0))
+            off += p.numel()
+        return jobs
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def step(self) -> None:
+        h, r, s = self.hip, self.replay, self._s()
+        excl = 0 if self.cfg.exact_mass else 1
+        h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
+                     self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
+        h.aql_learn_fwd(self.L, s)
+        h.aql_learn_bwd(self.L, s)
+        h.per_write_leaves(r.tree, self.idx.data_ptr(), 0, self.B, r.alpha, r.max_prio.data_ptr(), 1,
+                           r.sorted_scratch.data_ptr(), 0, 0, 0, 0, s, self.delta.data_ptr(), self.lw.data_ptr(),
+                           self.prio.data_ptr(), self.loss_q.data_ptr())
+        h.aql_grad(self.G, s)
+        Pq = self.P_q
+        h.adam_step(self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
+                    self.part.data_ptr(), self.nblk, self.hp, self.step_ctr.data_ptr(), self.norms_q.data_ptr(), s)
+        o = 4 * Pq
+        h.adam_step(self.flat.data_ptr() + o, self.grad.data_ptr() + o, self.m.data_ptr() + o, self.v.data_ptr() + o,
+                    self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk, self.hp, self.step_ctr.data_ptr(),
+                    self.norms_p.data_ptr(), s)
+        h.aql_post(self.post, s)
+
+    def sync_target(self) -> None:
+        """update_target (AQL_dis.py:60-61): full state_dict copy, noise buffers included."""
+        s = self._s()
+        self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, s)
+        self.hip.copy_f32(self.teps.data_ptr(), self.eps.data_ptr(), self.eps.numel(), s)
+
+    def stats(self) -> dict:
+        return {"loss_q": float(self.loss_q.item()), "loss_proposal": float(self.loss_p.item()),
+                "grad_norm_q": float(self.norms_q[0].item()), "grad_norm_proposal": float(self.norms_p[0].item()),
+                "steps": int(self.step_ctr.item())}
+
+
+class AQLEngine:
+    """Actors + replay + learner of AQL_dis on one GPU (see module docstring)."""
+
+    def __init__(self, cfg: AQLEngineConfig, device: str | torch.device = "cuda"):
+        self.cfg = cfg
+        self.device = dev = torch.device(device)
+        self.hip = h = ops.hip()
+        if cfg.env_id not in ENV_KINDS:
+            raise ValueError(f"GPU AQL env must be one of {sorted(ENV_KINDS)}")
+        self.kind = ENV_KINDS[cfg.env_id]
+        self.host_env = envs.make(cfg.env_id)
+        torch.manual_seed(cfg.seed)
+        kw = dict(propose_sample=cfg.propose_sample, uniform_sample=cfg.uniform_sample, action_var=cfg.action_var,
+                  device=dev)
+        self.model = AQL(env=self.host_env, **kw).to(dev)
+        self.target = AQL(env=self.host_env, **kw).to(dev)
+        self.target.load_state_dict(self.model.state_dict())
+        self.actor_model = AQL(env=self.host_env, **kw).to(dev)
+        for m in (self.model, self.target, self.actor_model):
+            m.q.train()
+        self.cont = bool(self.model.env_iscontinuous)
+        self.T = int(self.model.total_sample)
+        self.obs = int(self.host_env.observation_space.shape[0])
+        self.adim = int(self.model.num_actions) if self.cont else 1
+        self.replay = AQLReplay(cfg.capacity, self.obs, self.T, self.adim, cfg.alpha, dev, seed=cfg.seed + 17)
+        self.learner = AQLLearner(self.model, self.target, self.replay, cfg)
+        self.actor_flat = flatten_module_params(self.actor_model)
+        self.actor_eps = flatten_noise(self.actor_model)
+        self.publish()
+        E = cfg.n_envs
+        self.E = E
+        self.K = cfg.learner_steps if cfg.learner_steps is not None else max(1, E // cfg.batch_size)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.obs_buf = torch.zeros(E, self.obs, **f32)
+        self.phys = torch.zeros(E, 4, **f32)
+        self.ep_len = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.ep_ret = torch.zeros(E, **f32)
+        self.ep_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.log_cap = 4096
+        self.ep_log = torch.zeros(self.log_cap, 2, **f32)
+        self.amu = torch.zeros(E, self.T, self.adim, **f32)
+        self.qbuf = torch.zeros(E, self.T, **f32)
+        self.act_idx = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.env_act = torch.zeros(E, self.adim, **f32)
+        self.slots = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.actor_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        total = cfg.total_actors or E
+        eps = actor_epsilon(np.arange(cfg.actor_offset, cfg.actor_offset + E), total, cfg.eps_base, cfg.eps_alpha)
+        self.eps = torch.as_tensor(np.atleast_1d(eps), **f32)
+        self.ws = torch.zeros(h.aql_workspace_floats(), **f32)
+        if self.cont:
+            sp = self.host_env.action_space
+            self.low = torch.as_tensor(np.asarray(sp.low, dtype=np.float32).reshape(-1), **f32)
+            self.high = torch.as_tensor(np.asarray(sp.high, dtype=np.float32).reshape(-1), **f32)
+        else:
+            self.low = self.high = torch.zeros(1, **f32)
+        self.var = self.model.proposal.action_var.to(**f32).contiguous()
+        if self.kind == 0:
+            self.dynA = torch.as_tensor(self.host_env.unwrapped._A, **f32).contiguous()
+            self.dynB = torch.as_tensor(self.host_env.unwrapped._B, **f32).contiguous()
+            self.dynw = torch.as_tensor(self.host_env.unwrapped._w, **f32).contiguous()
+        else:
+            self.dynA = self.dynB = self.dynw = torch.zeros(1, **f32)
+        self.seed = (cfg.seed * 0x2545F491 + 0xAC7) & 0xFFFFFFFFFFFF
+        self.env = h.make_aql_env(dict(
+            kind=self.kind, E=E, obs=self.obs, adim=self.adim, T=self.T,
+            max_steps=int(getattr(self.host_env, "_max_episode_steps", None) or 1_000_000),
+            obs_buf=self.obs_buf.data_ptr(), phys=self.phys.data_ptr(), ep_len=self.ep_len.data_ptr(),
+            ep_ret=self.ep_ret.data_ptr(), dynA=self.dynA.data_ptr(), dynB=self.dynB.data_ptr(),
+            dynw=self.dynw.data_ptr(), seed=self.seed, counter=self.actor_ctr.data_ptr(),
+            ep_count=self.ep_count.data_ptr(), ep_log=self.ep_log.data_ptr(), log_cap=self.log_cap))
+        self.ins = h.make_aql_insert(dict(self.replay.table_ptrs(), C=self.replay.capacity,
+                                          filled=self.replay.filled.data_ptr(), slots=self.slots.data_ptr()))
+        self.actor_net = FusedAQL(self.actor_model)._net()
+        h.aql_env_reset(self.env, self._s())
+        self.iterations = 0
+        self.learner_steps = 0
+        self._g_actor = self._g_learn = None
+        self._ep_read = 0
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    # ------------------------------------------------------------------ phases
+    def publish(self) -> None:
+        """set_worker_weights: the actors' copy of the online network (noise included)."""
+        s = self._s()
+        self.hip.copy_f32(self.actor_flat.data_ptr(), self.learner.flat.data_ptr(), self.learner.P, s)
+        self.hip.copy_f32(self.actor_eps.data_ptr(), self.learner.eps.data_ptr(), self.learner.eps.numel(), s)
+
+    def actor_step(self) -> None:
+        h, s, E, r = self.hip, self._s(), self.E, self.replay
+        h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
+                      self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s)
+        h.aql_candidate_q(self.actor_net, self.ws.data_ptr(), self.obs_buf.data_ptr(), self.amu.data_ptr(), E,
+                          self.qbuf.data_ptr(), s)
+        h.aql_select(self.qbuf.data_ptr(), self.amu.data_ptr(), E, self.T, self.adim, self.eps.data_ptr(),
+                     self.seed ^ 0xA9C1, self.actor_ctr.data_ptr(), self.act_idx.data_ptr(), self.env_act.data_ptr(), s)
+        h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(), self.ins, s)
+        h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
+                           r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
+
+    def learn_steps(self) -> None:
+        for _ in range(self.K):
+            self.learner.step()
+
+    def fill(self, threshold: int | None = None) -> None:
+        """Act until the replay holds more than ``threshold`` transitions (AQL_dis.py:120:
+        learning starts once len(buffer) > batch_size)."""
+        thr = threshold if threshold is not None else (self.cfg.threshold or self.cfg.batch_size + 1)
+        for _ in range(max(1, -(-int(thr) // self.E))):
+            self.actor_step()
+        self.publish()
+
+    def capture(self) -> None:
+        """Actor step and the K learner steps each as one hipGraph (same stream order)."""
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):  # warm the launch paths outside capture
+            torch.cuda.synchronize(self.device)
+        self._g_actor = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_actor):
+            self.actor_step()
+        self._g_learn = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_learn):
+            self.learn_steps()
+        torch.cuda.synchronize(self.device)
+
+    def _beta(self) -> float:
+        c = self.cfg  # AQL_dis.py:57 operator precedence kept
+        return min(1.0, c.beta_start + self.iterations * (1.0 - c.beta_start) / c.max_step * c.n_workers)
+
+    def iteration(self) -> None:
+        """One actor step of all envs, weight publish, K learner steps."""
+        self.learner.beta.fill_(self._beta())
+        if self._g_actor is not None:
+            self._g_actor.replay()
+        else:
+            self.actor_step()
+        if self._g_learn is not None:
+            self._g_learn.replay()
+        else:
+            self.learn_steps()
+        self.publish()
+        before = self.learner_steps
+        self.learner_steps += self.K
+        tu = self.cfg.target_update_steps
+        if tu > 0 and before // tu != self.learner_steps // tu:
+            self.learner.sync_target()
+        self.iterations += 1
+
+    def finished_episodes(self) -> list[tuple[float, int]]:
+        """(return, length) of the episodes finished since the last call (host sync)."""
+        n = int(self.ep_count.item())
+        lo = max(self._ep_read, n - self.log_cap)
+        out = []
+        if n > lo:
+            log = self.ep_log.cpu()
+            out = [(float(log[k % self.log_cap, 0]), int(log[k % self.log_cap, 1])) for k in range(lo, n)]
+        self._ep_read = n
+        return out
+
+    @property
+    def transitions_per_iteration(self) -> int:
+        return self.E

@@ -42,6 +42,7 @@ HIP_SOURCES = [
     "conv_kernels.hip",
     "conv_bwd_kernels.hip",
     "aql_kernels.hip",
+    "aql_engine_kernels.hip",
     "conv1_kernels.hip",
     "fc_kernels.hip",
     "loss_heads_kernels.hip",

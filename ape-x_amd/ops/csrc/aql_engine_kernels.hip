@@ -1,0 +1,646 @@
+// GPU AQL engine kernels for gfx950 (BASELINE config 4).
+//
+// One learner step of AQL_dis (reference AQL_dis.py:63-108, utils.py:44-61,
+// model.py:132-390) is five launches plus the shared replay / optimizer kernels:
+//
+//   per_sample -> aql_learn_fwd -> aql_learn_bwd -> per_write_leaves(mix) -> aql_grad
+//              -> adam_step(critic) -> adam_step(proposal) -> aql_post
+//
+// * aql_learn_fwd: Q over every (state, candidate) pair of the batch for the three
+//   evaluations of compute_loss_AQL -- online Q(s, .), online Q(s', .), target Q(s', .)
+//   (the candidate set a_mu sampled at s_t is re-used for s', utils.py:44-49).  The action
+//   encoder and the candidate half of advantage1 do not depend on the state, so the
+//   online encodings are computed once for s and s'; the state half of advantage1
+//   (W1[:, 64:] q_feature(s) + b1) is one 64-vector per state.  Workgroup = (net, sample,
+//   16 candidates); 4 waves split the 64 output columns; both candidate GEMMs
+//   (ao_h1[16x128] x ao_w2^T, ao_out[16x64] x W1a^T) run on v_mfma_f32_16x16x4_f32 with
+//   the weights staged in LDS at bank-conflict-free pitches (132 / 68 floats: row n,
+//   k-slot q -> bank 4n + q).  ao_h1 is generated in the A-operand registers (adim FMAs).
+// * aql_learn_bwd: per sample -- the two argmaxes, the Double-Q TD target, Huber/IS
+//   gradient, the forward recomputed for the ONE taken candidate (the critic loss only
+//   reaches Q(s, a)), its backward to every layer input, and the proposal forward +
+//   analytic log-prob/entropy gradient (MVN with fixed diagonal variance: the entropy is
+//   constant; Categorical: the reference's [B,1] vs [B] broadcast, see below).  Writes
+//   the per-sample vectors of aqlv:: -- no per-sample weight-gradient partials.
+// * aql_grad: each parameter's gradient as a length-B contraction of those vectors
+//   (NoisyLinear sigma = mu-gradient x epsilon), plus per-group sums of squares for the
+//   two clip_grad_norm_(40) calls (critic / proposal are clipped separately).
+// * aql_post: reset_noise() on the online and target critics (factorised Gaussian, Philox)
+//   and the per-step proposal hard copy online -> target, then the step counter bump
+//   (last-block ticket).
+// * aql_env_reset / aql_env_step: vectorised GPU envs (BipedalWalker-shaped, CartPole,
+//   Pendulum: envs/classic.py dynamics) that also insert the raw (s, a, r, s', d, a_mu)
+//   transition into the replay ring (batchrecoder_AQL.py:48-51: no n-step, no actor
+//   priorities; the slots go to per_write_leaves at max priority).
+//
+// Discrete proposal quirk kept from AQL_dis.py:84-86: the best candidate is reshaped to
+// [B, 1] and scored by a Categorical of batch shape [B], so log_prob broadcasts to [B, B]
+// and loss_p = mean_ij(-log pi_j(best_i)) - ent_lam * mean_j H_j.  Per sample j that is
+// -(1/B) sum_k cnt_k log p_jk - ent_lam H_j with cnt_k = #{i : best_i = k}.
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kH = 64, kCat = 128, kP132 = 132, kP68 = 68, kMaxAdim = 8;
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float noisy_w(const float* mu, const float* sg, const float* ep, int i, int noisy) {
+  const float m = mu[i];
+  return noisy ? fmaf(sg[i], ep[i], m) : m;
+}
+__device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
+
+// (value, index) argmax over a row of length T by one wave; ties -> lowest index
+__device__ __forceinline__ int wave_argmax(const float* row, int T, int lane) {
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int t = lane; t < T; t += 64) {
+    const float v = row[t];
+    if (v > bv || (v == bv && t < bi)) { bv = v; bi = t; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  return bi == 0x7fffffff ? 0 : bi;
+}
+
+// ------------------------------------------------------------------ forward over candidates
+__global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
+  __shared__ float ao2[kH * kP132];     // action_out.2 weight [n][k]
+  __shared__ float w1a[kH * kP68];      // advantage1 effective weight, candidate half [n][k]
+  __shared__ float xt[16 * kP68];       // ao_out tile [16 candidates][64]
+  __shared__ float ao1w[kCat * kMaxAdim];
+  __shared__ float ao1b[kCat], ao2b[kH], w2e[kH];
+  __shared__ float sv[2][64], hq[2][kH], qf[2][kH], stp[2][kH];
+  __shared__ float qpart[4][2][16];
+  const bool tgt = blockIdx.y != 0;
+  const AQLNet& N = tgt ? L.tg : L.on;
+  const int T = N.T, RT = (T + 15) >> 4;
+  const int b = blockIdx.x / RT, rt = blockIdx.x - b * RT;
+  const int nst = tgt ? 1 : 2;  // online: {s, s'}, target: {s'}
+  const int row = L.idx[b];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, q = lane >> 4;
+  const int obs = N.obs, adim = N.adim, cont = N.cont, noisy = N.noisy;
+  if (t < 128) {
+    const int si = t >> 6, i = t & 63;
+    if (si < nst && i < obs) sv[si][i] = ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i];
+  }
+  for (int e = t; e < kH * kCat; e += 256) {
+    const int n = e >> 7, k = e & 127;
+    if (cont) ao2[n * kP132 + k] = N.ao_w2[e];
+    if (k < kH) w1a[n * kP68 + k] = noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, e, noisy);
+  }
+  const int nao1 = cont ? kCat : kH;
+  for (int e = t; e < nao1 * adim; e += 256) ao1w[e] = N.ao_w1[e];
+  if (t < nao1) ao1b[t] = N.ao_b1[t];
+  if (t < kH) {
+    if (cont) ao2b[t] = N.ao_b2[t];
+    w2e[t] = noisy_w(N.a2_wmu, N.a2_wsig, N.a2_weps, t, noisy);
+  }
+  __syncthreads();
+  // state halves: wave si < nst handles state si (q_feature MLP, then W1[:, 64:] . qf + b1)
+  if (wave < nst) {
+    float a = N.qf_b1[lane];
+    for (int i = 0; i < obs; ++i) a = fmaf(N.qf_w1[lane * obs + i], sv[wave][i], a);
+    hq[wave][lane] = relu(a);
+  }
+  __syncthreads();
+  if (wave < nst) {
+    float a = N.qf_b2[lane];
+    for (int k = 0; k < kH; ++k) a = fmaf(N.qf_w2[lane * kH + k], hq[wave][k], a);
+    qf[wave][lane] = relu(a);
+  }
+  __syncthreads();
+  if (wave < nst) {
+    float a = noisy_w(N.a1_bmu, N.a1_bsig, N.a1_beps, lane, noisy);
+    for (int k = 0; k < kH; ++k)
+      a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, lane * kCat + kH + k, noisy), qf[wave][k], a);
+    stp[wave][lane] = a;
+  }
+  // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
+  const int n = 16 * wave + j;
+  if (cont) {
+    const int r = min(rt * 16 + j, T - 1);  // tail rows recompute a valid candidate (discarded)
+    const float* am = L.amu + ((size_t)row * T + r) * adim;
+    float av[kMaxAdim];
+#pragma unroll
+    for (int d = 0; d < kMaxAdim; ++d) av[d] = d < adim ? am[d] : 0.f;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int k0 = 0; k0 < kCat; k0 += 8) {
+      float h0 = ao1b[k0 + q], h1 = ao1b[k0 + 4 + q];
+#pragma unroll
+      for (int d = 0; d < kMaxAdim; ++d) {
+        if (d < adim) {
+          h0 = fmaf(ao1w[(k0 + q) * adim + d], av[d], h0);
+          h1 = fmaf(ao1w[(k0 + 4 + q) * adim + d], av[d], h1);
+        }
+      }
+      acc0 = mfma4(relu(h0), ao2[n * kP132 + k0 + q], acc0);
+      acc1 = mfma4(relu(h1), ao2[n * kP132 + k0 + 4 + q], acc1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xt[(4 * q + i) * kP68 + n] = relu(acc0[i] + acc1[i] + ao2b[n]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(rt * 16 + 4 * q + i, T - 1);
+      xt[(4 * q + i) * kP68 + n] = relu(fmaf(ao1w[n], L.amu[(size_t)row * T + r], ao1b[n]));
+    }
+  }
+  __syncthreads();
+  // advantage1 candidate half: pre[16][64] = ao_out . W1a^T; wave w -> columns 16w..16w+15
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+  for (int k0 = 0; k0 < kH; k0 += 8) {
+    c0 = mfma4(xt[j * kP68 + k0 + q], w1a[n * kP68 + k0 + q], c0);
+    c1 = mfma4(xt[j * kP68 + k0 + 4 + q], w1a[n * kP68 + k0 + 4 + q], c1);
+  }
+  for (int si = 0; si < nst; ++si) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v = w2e[n] * relu(c0[i] + c1[i] + stp[si][n]);
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (j == 0) qpart[wave][si][4 * q + i] = v;
+    }
+  }
+  __syncthreads();
+  if (t < 16 * nst) {
+    const int m = t & 15, si = t >> 4, tt = rt * 16 + m;
+    if (tt < T) {
+      const float b2 = noisy_w(N.a2_bmu, N.a2_bsig, N.a2_beps, 0, noisy);
+      const float qv = ((qpart[0][si][m] + qpart[1][si][m]) + (qpart[2][si][m] + qpart[3][si][m])) + b2;
+      float* out = tgt ? L.qt_s2 : (si ? L.q_s2 : L.q_s);
+      out[(size_t)b * T + tt] = qv;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ per-sample loss + backward
+__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
+  __shared__ float s_s[64], s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], hh[kH], gh[kH], gx[kCat];
+  __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
+  __shared__ int cnt[64];
+  __shared__ int s_best, s_next;
+  __shared__ float s_gq;
+  const AQLNet& N = L.on;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int T = N.T, obs = N.obs, adim = N.adim, na = N.na, B = L.B, cont = N.cont, noisy = N.noisy;
+  const int row = L.idx[b];
+  const int a_idx = L.act[row];
+  if (wave == 0) {
+    const int bi = wave_argmax(L.q_s + (size_t)b * T, T, lane);
+    if (lane == 0) s_best = bi;
+  } else if (wave == 1) {
+    const int bi = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
+    if (lane == 0) s_next = bi;
+  }
+  if (t < 64) cnt[t] = 0;
+  if (t < obs) s_s[t] = L.st[(size_t)row * obs + t];
+  if (t < adim) s_a[t] = L.amu[((size_t)row * T + a_idx) * adim + t];
+  __syncthreads();
+  if (!cont) {  // counts of every sample's best candidate (the [B, B] log-prob broadcast)
+    for (int i = wave; i < B; i += 4) {
+      const int ri = L.idx[i];
+      const int bi = wave_argmax(L.q_s + (size_t)i * T, T, lane);
+      if (lane == 0) {
+        const int k = (int)L.amu[(size_t)ri * T + bi];
+        if (k >= 0 && k < 64) atomicAdd(&cnt[k], 1);
+      }
+    }
+  }
+  if (t == 0) {  // Double-Q TD target, Huber + IS weight (utils.py:50-60)
+    const float qa = L.q_s[(size_t)b * T + a_idx], qt = L.qt_s2[(size_t)b * T + s_next];
+    const float y = L.rew[row] + L.gamma_n * qt * (1.f - L.done[row]);
+    const float diff = y - qa, dl = fabsf(diff), wb = L.w[b];
+    L.delta[b] = dl;
+    L.lw[b] = wb * (dl < 1.f ? 0.5f * dl * dl : dl - 0.5f);
+    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+    s_gq = -sg * fminf(dl, 1.f) * wb / (float)B;
+  }
+  // forward of the taken candidate (s, a_mu[a]) + the proposal trunk
+  if (t < kH) {
+    float a = N.qf_b1[t];
+    for (int i = 0; i < obs; ++i) a = fmaf(N.qf_w1[t * obs + i], s_s[i], a);
+    qfh[t] = relu(a);
+  } else if (t < kH + (cont ? kCat : kH)) {
+    const int k = t - kH;
+    float a = N.ao_b1[k];
+    for (int d = 0; d < adim; ++d) a = fmaf(N.ao_w1[k * adim + d], s_a[d], a);
+    aoh[k] = relu(a);
+  }
+  __syncthreads();
+  if (t < kH) {
+    float a = N.qf_b2[t];
+    for (int k = 0; k < kH; ++k) a = fmaf(N.qf_w2[t * kH + k], qfh[k], a);
+    x[kH + t] = relu(a);
+  } else if (t < 2 * kH) {
+    const int nn = t - kH;
+    if (cont) {
+      float a = N.ao_b2[nn];
+      for (int k = 0; k < kCat; ++k) a = fmaf(N.ao_w2[nn * kCat + k], aoh[k], a);
+      x[nn] = relu(a);
+    } else {
+      x[nn] = aoh[nn];
+    }
+  } else {
+    const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
+    float a = N.f_b[k];
+    for (int i = 0; i < obs; ++i) a = fmaf(N.f_w[k * obs + i], s_s[i], a);
+    emb[k] = relu(a);
+  }
+  __syncthreads();
+  if (t < kH) {
+    float a = noisy_w(N.a1_bmu, N.a1_bsig, N.a1_beps, t, noisy);
+    for (int k = 0; k < kCat; ++k) a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, t * kCat + k, noisy), x[k], a);
+    hh[t] = relu(a);
+    gh[t] = a > 0.f ? s_gq * noisy_w(N.a2_wmu, N.a2_wsig, N.a2_weps, t, noisy) : 0.f;
+  } else if (t >= 2 * kH) {
+    const int k = t - 2 * kH;
+    float a = N.df_b1[k];
+    for (int i = 0; i < kCat; ++i) a = fmaf(N.df_w1[k * kCat + i], emb[i], a);
+    hid[k] = relu(a);
+  }
+  __syncthreads();
+  if (t < kCat) {
+    float a = 0.f;
+    for (int nn = 0; nn < kH; ++nn) a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, nn * kCat + t, noisy), gh[nn], a);
+    gx[t] = x[t] > 0.f ? a : 0.f;
+  } else if (t - kCat < na) {
+    const int d = t - kCat;
+    float a = N.df_b2[d];
+    for (int k = 0; k < kCat; ++k) a = fmaf(N.df_w2[d * kCat + k], hid[k], a);
+    mu[d] = a;
+  }
+  __syncthreads();
+  float* V = L.vec + (size_t)b * aqlv::STRIDE;
+  if (t < kCat) {
+    if (cont) {  // action_out.0 input gradient
+      float a = 0.f;
+      for (int nn = 0; nn < kH; ++nn) a = fmaf(N.ao_w2[nn * kCat + t], gx[nn], a);
+      V[aqlv::GAOH + t] = aoh[t] > 0.f ? a : 0.f;
+      V[aqlv::AOH + t] = aoh[t];
+    }
+  } else if (t < kCat + kH) {  // q_feature.0 input gradient
+    const int k = t - kCat;
+    float a = 0.f;
+    for (int nn = 0; nn < kH; ++nn) a = fmaf(N.qf_w2[nn * kH + k], gx[kH + nn], a);
+    V[aqlv::GQFH + k] = qfh[k] > 0.f ? a : 0.f;
+    V[aqlv::QFH + k] = qfh[k];
+  } else {  // wave 3: proposal loss gradient w.r.t. mu (analytic)
+    float lp = 0.f;
+    if (cont) {
+      float d2 = 0.f, lv = 0.f;
+      if (lane < na) {
+        const float best = L.amu[((size_t)row * T + s_best) * adim + lane];
+        const float var = L.var[lane], diff = best - mu[lane];
+        gmu[lane] = -diff / var / (float)B;
+        d2 = diff * diff / var;
+        lv = logf(var);
+      }
+      d2 = wave_sum(d2);
+      lv = wave_sum(lv);
+      const float l2pi = 1.8378770664093453f;
+      const float logp = -0.5f * (d2 + lv + (float)na * l2pi);
+      const float ent = 0.5f * ((float)na * (1.f + l2pi) + lv);
+      lp = -logp - L.ent_lam * ent;
+    } else {
+      const float m = lane < na ? mu[lane] : -INFINITY;
+      const float mx = wave_max(m);
+      const float ex = lane < na ? expf(m - mx) : 0.f;
+      const float z = wave_sum(ex);
+      const float logp = lane < na ? (m - mx) - logf(z) : 0.f;
+      const float p = lane < na ? ex / z : 0.f;
+      const float ent = -wave_sum(p * logp);
+      const float c = lane < na ? (float)cnt[lane] / (float)B : 0.f;
+      if (lane < na) gmu[lane] = ((p - c) + L.ent_lam * p * (logp + ent)) / (float)B;
+      lp = -wave_sum(c * logp) - L.ent_lam * ent;
+    }
+    if (lane == 0) L.lossp[b] = lp;
+  }
+  __syncthreads();
+  if (t < kCat) {  // proposal hidden gradient
+    float a = 0.f;
+    for (int d = 0; d < na; ++d) a = fmaf(N.df_w2[d * kCat + t], gmu[d], a);
+    V[aqlv::GHID + t] = hid[t] > 0.f ? a : 0.f;
+    V[aqlv::HID + t] = hid[t];
+    V[aqlv::EMB + t] = emb[t];
+    V[aqlv::X + t] = x[t];
+    V[aqlv::GX + t] = gx[t];
+  } else if (t < kCat + kH) {
+    const int k = t - kCat;
+    V[aqlv::H + k] = hh[k];
+    V[aqlv::GH + k] = gh[k];
+    if (k < na) V[aqlv::GMU + k] = gmu[k];
+    if (k < obs) V[aqlv::S + k] = s_s[k];
+    if (k < adim) V[aqlv::A + k] = s_a[k];
+    if (k == 0) V[aqlv::GQ] = s_gq;
+  }
+}
+
+// ------------------------------------------------------------------ weight gradients
+constexpr int kGradThreads = 256;
+
+__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+  __shared__ double red[2][4];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int64_t i = (int64_t)blockIdx.x * kGradThreads + t;
+  float g = 0.f;
+  int grp = -1;
+  if (i < G.n) {
+    int jb = 0;
+    for (int k = 1; k < G.njobs; ++k)
+      if (i >= G.job[k].off) jb = k;
+    const AqlGradJob& J = G.job[jb];
+    const int e = (int)(i - J.off), r = e / J.cols, c = e - r * J.cols;
+    grp = J.group;
+    if (!J.zero) {
+      float acc = 0.f;
+      const float* V = G.vec;
+      for (int b = 0; b < G.B; ++b, V += aqlv::STRIDE)
+        acc = fmaf(V[J.goff + r], J.xoff >= 0 ? V[J.xoff + c] : 1.f, acc);
+      g = J.eps ? acc * J.eps[e] : acc;
+    }
+    G.grad[i] = g;
+  }
+  double s0 = grp == 0 ? (double)g * (double)g : 0.0, s1 = grp == 1 ? (double)g * (double)g : 0.0;
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  if (lane == 0) {
+    red[0][wave] = s0;
+    red[1][wave] = s1;
+  }
+  __syncthreads();
+  if (t == 0) {
+    G.part[blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    G.part[gridDim.x + blockIdx.x] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+  if (blockIdx.x == 0 && wave == 1 && G.lossp_out) {
+    float a = 0.f;
+    for (int b = lane; b < G.B; b += 64) a += G.lossp[b];
+    a = wave_sum(a);
+    if (lane == 0) G.lossp_out[0] = a / (float)G.B;
+  }
+}
+
+// ------------------------------------------------------------------ noise reset + proposal copy
+__device__ __forceinline__ float scaled_noise(uint64_t seed, int layer, int kind, int i, uint64_t ctr) {
+  float u[4];
+  uniform4(seed, ((uint64_t)layer << 40) | ((uint64_t)kind << 32) | (uint32_t)i, ctr, u);
+  const float x = std_normal(u[0], u[1]);
+  return copysignf(sqrtf(fabsf(x)), x);  // f(x) = sign(x) sqrt(|x|) (model.py:160-163)
+}
+
+__global__ __launch_bounds__(256) void aql_post_k(AqlPost P) {
+  const uint64_t st = (uint64_t)P.step[0];
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const AqlNoise& z = P.layer[l];
+    const int64_t nw = (int64_t)z.out * z.in;
+    if (i >= 0 && i < nw) {
+      const int o = (int)(i / z.in), c = (int)(i - (int64_t)o * z.in);
+      z.weps[i] = scaled_noise(P.seed, l, 0, o, st) * scaled_noise(P.seed, l, 1, c, st);
+    } else if (i >= nw && i < nw + z.out) {
+      z.beps[i - nw] = scaled_noise(P.seed, l, 2, (int)(i - nw), st);
+    }
+    i -= nw + z.out;
+  }
+  if (i >= 0 && i < P.n_copy) P.dst[i] = P.src[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const int tk = atomicAdd(P.ticket, 1);
+    if (tk == (int)gridDim.x - 1) {
+      P.step[0] = (int64_t)st + 1;
+      P.ticket[0] = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ vector envs
+constexpr int kBwObs = 24, kBwAct = 4;
+
+__device__ __forceinline__ float env_normal(uint64_t seed, int e, int i, int kind, uint64_t ctr) {
+  float u[4];
+  uniform4(seed, ((uint64_t)kind << 48) | ((uint64_t)(uint32_t)e << 8) | (uint32_t)i, ctr, u);
+  return std_normal(u[0], u[1]);
+}
+__device__ __forceinline__ float env_uniform(uint64_t seed, int e, int i, int kind, uint64_t ctr) {
+  float u[4];
+  uniform4(seed, ((uint64_t)kind << 48) | ((uint64_t)(uint32_t)e << 8) | (uint32_t)i, ctr, u);
+  return u[2];
+}
+
+// reset env e (one wave): new observation into obs_buf / phys
+__device__ void env_reset_one(const AqlEnv& V, int e, int lane, uint64_t ctr) {
+  float* o = V.obs_buf + (size_t)e * V.obs;
+  if (V.kind == 0) {  // s ~ N(0, 0.1)
+    if (lane < kBwObs) o[lane] = 0.1f * env_normal(V.seed, e, lane, 1, ctr);
+  } else if (V.kind == 1) {  // CartPole: U(-0.05, 0.05)^4
+    if (lane < 4) {
+      const float v = -0.05f + 0.1f * env_uniform(V.seed, e, lane, 1, ctr);
+      o[lane] = v;
+      V.phys[(size_t)e * 4 + lane] = v;
+    }
+  } else {  // Pendulum: th ~ U(-pi, pi), thdot ~ U(-1, 1)
+    const float th = -3.14159265f + 6.2831853f * env_uniform(V.seed, e, 0, 1, ctr);
+    const float thd = -1.f + 2.f * env_uniform(V.seed, e, 1, 1, ctr);
+    if (lane == 0) {
+      V.phys[(size_t)e * 4] = th;
+      V.phys[(size_t)e * 4 + 1] = thd;
+      o[0] = cosf(th);
+      o[1] = sinf(th);
+      o[2] = thd;
+    }
+  }
+  if (lane == 0) {
+    V.ep_len[e] = 0;
+    V.ep_ret[e] = 0.f;
+  }
+}
+
+__global__ __launch_bounds__(256) void aql_env_reset_k(AqlEnv V) {
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= V.E) return;
+  env_reset_one(V, e, threadIdx.x & 63, 0xFFFFFFFFull);
+}
+
+__global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __restrict__ act,
+                                                      const int* __restrict__ act_idx, const float* __restrict__ amu,
+                                                      AqlInsert I) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= V.E) return;
+  const uint64_t ctr = (uint64_t)V.counter[0];
+  const int64_t slot = (I.filled[0] + e) % I.C;
+  const int obs = V.obs;
+  const float* s = V.obs_buf + (size_t)e * obs;
+  float s2 = 0.f, r = 0.f;
+  bool term = false;
+  if (V.kind == 0) {  // BipedalWalker-shaped (envs/classic.py BipedalWalkerShapedEnv.step)
+    float a[kBwAct], pen = 0.f;
+#pragma unroll
+    for (int d = 0; d < kBwAct; ++d) {
+      a[d] = fminf(fmaxf(act[(size_t)e * kBwAct + d], -1.f), 1.f);
+      pen += fabsf(a[d]);
+    }
+    if (lane < kBwObs) {
+      float z = 0.01f * env_normal(V.seed, e, lane, 0, ctr);
+      for (int k = 0; k < kBwObs; ++k) z = fmaf(V.dynA[lane * kBwObs + k], s[k], z);
+#pragma unroll
+      for (int d = 0; d < kBwAct; ++d) z = fmaf(V.dynB[lane * kBwAct + d], a[d], z);
+      s2 = tanhf(z);
+    }
+    const float progress = 0.05f * wave_sum(lane < kBwObs ? V.dynw[lane] * s2 : 0.f);
+    r = progress - 0.00035f * 80.f * pen;
+    const float s0 = __shfl(s2, 0, 64);
+    if (fabsf(s0) > 0.995f) {  // "hull touches ground"
+      r = -100.f;
+      term = true;
+    }
+  } else if (V.kind == 1) {  // CartPole (Barto et al. 1983; envs/classic.py CartPoleEnv)
+    float* ph = V.phys + (size_t)e * 4;
+    const float x = ph[0], xd = ph[1], th = ph[2], thd = ph[3];
+    const float force = ((int)act[e] == 1) ? 10.f : -10.f;
+    const float ct = cosf(th), sn = sinf(th);
+    const float tmp = (force + 0.05f * thd * thd * sn) / 1.1f;
+    const float tha = (9.8f * sn - ct * tmp) / (0.5f * (4.f / 3.f - 0.1f * ct * ct / 1.1f));
+    const float xa = tmp - 0.05f * tha * ct / 1.1f;
+    const float nv[4] = {x + 0.02f * xd, xd + 0.02f * xa, th + 0.02f * thd, thd + 0.02f * tha};
+    if (lane < 4) s2 = nv[lane];
+    r = 1.f;
+    term = nv[0] < -2.4f || nv[0] > 2.4f || nv[2] < -0.20943951f || nv[2] > 0.20943951f;
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 4) ph[lane] = nv[lane];
+  } else {  // Pendulum (envs/classic.py PendulumEnv)
+    float* ph = V.phys + (size_t)e * 4;
+    const float th = ph[0], thd = ph[1];
+    const float u = fminf(fmaxf(act[e], -2.f), 2.f);
+    const float an = remainderf(th, 6.2831853f);  // normalised angle in [-pi, pi]
+    const float cost = an * an + 0.1f * thd * thd + 0.001f * u * u;
+    float nthd = thd + (-3.f * 10.f / 2.f * sinf(th + 3.14159265f) + 3.f * u) * 0.05f;
+    const float nth = th + nthd * 0.05f;
+    nthd = fminf(fmaxf(nthd, -8.f), 8.f);
+    const float nv[3] = {cosf(nth), sinf(nth), nthd};
+    if (lane < 3) s2 = nv[lane];
+    r = -cost;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      ph[0] = nth;
+      ph[1] = nthd;
+    }
+  }
+  const int len = V.ep_len[e] + 1;
+  const bool done = term || len >= V.max_steps;  // TimeLimit sets done (stored as terminal)
+  // raw transition into the replay ring
+  if (lane < obs) {
+    I.st[slot * obs + lane] = s[lane];
+    I.st2[slot * obs + lane] = s2;
+  }
+  const int TA = V.T * V.adim;
+  for (int k = lane; k < TA; k += 64) I.amu[slot * TA + k] = amu[(size_t)e * TA + k];
+  if (lane == 0) {
+    I.act[slot] = act_idx[e];
+    I.rew[slot] = r;
+    I.done[slot] = done ? 1.f : 0.f;
+    I.slots[e] = (int)slot;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (done) {
+    if (lane == 0) {
+      const int k = atomicAdd(V.ep_count, 1);
+      float* lg = V.ep_log + (size_t)(k % V.log_cap) * 2;
+      lg[0] = V.ep_ret[e] + r;
+      lg[1] = (float)len;
+    }
+    __builtin_amdgcn_wave_barrier();
+    env_reset_one(V, e, lane, ctr);
+  } else {
+    if (lane < obs) V.obs_buf[(size_t)e * obs + lane] = s2;
+    if (lane == 0) {
+      V.ep_len[e] = len;
+      V.ep_ret[e] += r;
+    }
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+static void check_net(const AQLNet& n) {
+  if (n.obs < 1 || n.obs > 64) throw std::invalid_argument("aql learner: 1 <= obs <= 64");
+  if (n.adim < 1 || n.adim > kMaxAdim) throw std::invalid_argument("aql learner: 1 <= action dim <= 8");
+  if (n.T < 1 || n.T > 4096) throw std::invalid_argument("aql learner: 1 <= candidates <= 4096");
+  if (n.na < 1 || n.na > 64) throw std::invalid_argument("aql learner: 1 <= proposal outputs <= 64");
+  if (!n.f_w || !n.df_w1 || !n.df_w2 || (n.cont && !n.ao_w2)) throw std::invalid_argument("aql learner: weights");
+}
+
+void aql_learn_fwd(const AqlLearn& L, hipStream_t s) {
+  check_net(L.on);
+  if (L.tg.T != L.on.T || L.tg.cont != L.on.cont || L.tg.obs != L.on.obs || L.tg.adim != L.on.adim)
+    throw std::invalid_argument("aql learner: online / target shapes differ");
+  if (L.B < 1) return;
+  const int RT = (L.on.T + 15) / 16;
+  aql_learn_fwd_k<<<dim3(L.B * RT, 2), 256, 0, s>>>(L);
+  LAUNCH_CHECK();
+}
+
+void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
+  check_net(L.on);
+  if (L.B < 1) return;
+  aql_learn_bwd_k<<<L.B, 256, 0, s>>>(L);
+  LAUNCH_CHECK();
+}
+
+int aql_grad_blocks(int64_t n) { return (int)((n + kGradThreads - 1) / kGradThreads); }
+
+void aql_grad(const AqlGrad& g, hipStream_t s) {
+  if (g.njobs < 1 || g.njobs > kAqlMaxJobs || g.job[0].off != 0) throw std::invalid_argument("aql_grad: jobs");
+  for (int k = 0; k < g.njobs; ++k) {
+    const AqlGradJob& J = g.job[k];
+    const int64_t end = k + 1 < g.njobs ? g.job[k + 1].off : g.n;
+    if (J.off + (int64_t)J.rows * J.cols != end) throw std::invalid_argument("aql_grad: jobs must tile [0, n)");
+    if (J.goff < 0 || J.goff + J.rows > aqlv::STRIDE || J.xoff + J.cols > aqlv::STRIDE)
+      throw std::invalid_argument("aql_grad: vector offsets");
+  }
+  aql_grad_k<<<aql_grad_blocks(g.n), kGradThreads, 0, s>>>(g);
+  LAUNCH_CHECK();
+}
+
+void aql_post(const AqlPost& p, hipStream_t s) {
+  int64_t n = p.n_copy;
+  for (int l = 0; l < 4; ++l) n += (int64_t)p.layer[l].out * p.layer[l].in + p.layer[l].out;
+  aql_post_k<<<(int)((n + 255) / 256), 256, 0, s>>>(p);
+  LAUNCH_CHECK();
+}
+
+void aql_env_reset(const AqlEnv& e, hipStream_t s) {
+  if (e.kind < 0 || e.kind > 2) throw std::invalid_argument("aql env: kind 0 (bipedal) / 1 (cartpole) / 2 (pendulum)");
+  if (e.E < 1) return;
+  aql_env_reset_k<<<(e.E + 3) / 4, 256, 0, s>>>(e);
+  LAUNCH_CHECK();
+}
+
+void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, const float* amu, const AqlInsert& ins,
+                  hipStream_t s) {
+  static const int obs_of[3] = {kBwObs, 4, 3}, adim_of[3] = {kBwAct, 1, 1};
+  if (e.kind < 0 || e.kind > 2) throw std::invalid_argument("aql env: kind");
+  if (e.obs != obs_of[e.kind] || e.adim != adim_of[e.kind]) throw std::invalid_argument("aql env: obs/action dims");
+  if (ins.C < e.E) throw std::invalid_argument("aql env: replay capacity < envs");
+  if (e.E < 1) return;
+  aql_env_step_k<<<(e.E + 3) / 4, 256, 0, s>>>(e, env_act, act_idx, amu, ins);
+  LAUNCH_CHECK();
+}
+
+}  // namespace apex

@@ -103,12 +103,6 @@ __global__ __launch_bounds__(256) void aql_candidate_q_k(AQLNet net, const float
   }
 }
 
-// Box-Muller standard normal from two uniforms in [0,1)
-__device__ __forceinline__ float std_normal(float u1, float u2) {
-  const float r = sqrtf(-2.f * logf(fmaxf(u1, 1e-12f)));
-  return r * cospif(2.f * u2);
-}
-
 __global__ __launch_bounds__(64) void aql_propose_k(AQLNet net, const float* __restrict__ state, int B,
                                                     const float* __restrict__ low, const float* __restrict__ high,
                                                     const float* __restrict__ var, uint64_t seed,

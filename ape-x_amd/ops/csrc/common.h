@@ -97,6 +97,12 @@ __device__ __forceinline__ void uniform4(uint64_t seed, uint64_t stream, uint64_
   out[3] = (r.w >> 8) * s;
 }
 
+// Box-Muller standard normal from two uniforms in [0,1)
+__device__ __forceinline__ float std_normal(float u1, float u2) {
+  const float r = sqrtf(-2.f * logf(fmaxf(u1, 1e-12f)));
+  return r * cospif(2.f * u2);
+}
+
 __device__ __forceinline__ double uniform_double(uint64_t seed, uint64_t stream, uint64_t counter) {
   u32x4 c{(uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
   u32x4 r = philox4x32(c, (uint32_t)seed, (uint32_t)(seed >> 32));

@@ -537,6 +537,101 @@ PYBIND11_MODULE(_apex_hip, m) {
     aql_propose(n, P<const float>(state), B, P<const float>(low), P<const float>(high), P<const float>(var), seed,
                 P<const int64_t>(counter), P<float>(a_mu), P<float>(mu_out), S(s));
   });
+  // ---- GPU AQL engine (aql_engine_kernels.hip): descriptors built once, per-step calls take a stream
+  py::class_<AqlLearn>(m, "AqlLearn");
+  m.def("make_aql_learn", [](const AQLNet& on, const AQLNet& tg, py::dict p, int B, float gamma_n, float ent_lam) {
+    auto g = [&](const char* k) { return p[k].cast<uint64_t>(); };
+    AqlLearn L{};
+    L.on = on;
+    L.tg = tg;
+    L.st = P<const float>(g("st")); L.st2 = P<const float>(g("st2")); L.rew = P<const float>(g("rew"));
+    L.done = P<const float>(g("done")); L.amu = P<const float>(g("amu")); L.act = P<const int>(g("act"));
+    L.idx = P<const int>(g("idx")); L.w = P<const float>(g("w")); L.var = P<const float>(g("var"));
+    L.q_s = P<float>(g("q_s")); L.q_s2 = P<float>(g("q_s2")); L.qt_s2 = P<float>(g("qt_s2"));
+    L.vec = P<float>(g("vec")); L.delta = P<float>(g("delta")); L.lw = P<float>(g("lw"));
+    L.lossp = P<float>(g("lossp"));
+    L.B = B;
+    L.gamma_n = gamma_n;
+    L.ent_lam = ent_lam;
+    return L;
+  });
+  m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
+  m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });
+  m.def("aql_vec_layout", []() {
+    py::dict d;
+    d["GQ"] = aqlv::GQ; d["H"] = aqlv::H; d["GH"] = aqlv::GH; d["X"] = aqlv::X; d["GX"] = aqlv::GX;
+    d["AOH"] = aqlv::AOH; d["GAOH"] = aqlv::GAOH; d["A"] = aqlv::A; d["QFH"] = aqlv::QFH; d["GQFH"] = aqlv::GQFH;
+    d["S"] = aqlv::S; d["EMB"] = aqlv::EMB; d["HID"] = aqlv::HID; d["GHID"] = aqlv::GHID; d["GMU"] = aqlv::GMU;
+    d["STRIDE"] = aqlv::STRIDE;
+    return d;
+  });
+  py::class_<AqlGrad>(m, "AqlGrad");
+  // jobs: (off, rows, cols, goff, xoff, eps_ptr, group, zero)
+  m.def("make_aql_grad", [](const std::vector<std::array<int64_t, 8>>& jobs, int64_t n, uint64_t vec, int B,
+                            uint64_t grad, uint64_t part, uint64_t lossp, uint64_t lossp_out) {
+    if (jobs.empty() || (int)jobs.size() > kAqlMaxJobs) throw std::invalid_argument("make_aql_grad: 1..24 jobs");
+    AqlGrad G{};
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      const auto& j = jobs[k];
+      G.job[k] = AqlGradJob{j[0], (int)j[1], (int)j[2], (int)j[3], (int)j[4], P<const float>((uint64_t)j[5]),
+                            (int)j[6], (int)j[7]};
+    }
+    G.njobs = (int)jobs.size();
+    G.n = n;
+    G.vec = P<const float>(vec);
+    G.B = B;
+    G.grad = P<float>(grad);
+    G.part = P<double>(part);
+    G.lossp = P<const float>(lossp);
+    G.lossp_out = P<float>(lossp_out);
+    return G;
+  });
+  m.def("aql_grad", [](const AqlGrad& G, uint64_t s) { aql_grad(G, S(s)); });
+  m.def("aql_grad_blocks", &aql_grad_blocks);
+  py::class_<AqlPost>(m, "AqlPost");
+  // layers: 4 x (weps, beps, out, in)
+  m.def("make_aql_post", [](const std::vector<std::array<uint64_t, 4>>& layers, uint64_t src, uint64_t dst,
+                            int64_t n_copy, uint64_t step, uint64_t ticket, uint64_t seed) {
+    if (layers.size() != 4) throw std::invalid_argument("make_aql_post: 4 noisy layers");
+    AqlPost p{};
+    for (int l = 0; l < 4; ++l)
+      p.layer[l] = AqlNoise{P<float>(layers[l][0]), P<float>(layers[l][1]), (int)layers[l][2], (int)layers[l][3]};
+    p.src = P<const float>(src);
+    p.dst = P<float>(dst);
+    p.n_copy = n_copy;
+    p.step = P<int64_t>(step);
+    p.ticket = P<int>(ticket);
+    p.seed = seed;
+    return p;
+  });
+  m.def("aql_post", [](const AqlPost& p, uint64_t s) { aql_post(p, S(s)); });
+  py::class_<AqlEnv>(m, "AqlEnv");
+  m.def("make_aql_env", [](py::dict d) {
+    auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+    auto gi = [&](const char* k) { return d[k].cast<int>(); };
+    AqlEnv e{};
+    e.kind = gi("kind"); e.E = gi("E"); e.obs = gi("obs"); e.adim = gi("adim"); e.T = gi("T");
+    e.max_steps = gi("max_steps");
+    e.obs_buf = P<float>(g("obs_buf")); e.phys = P<float>(g("phys")); e.ep_len = P<int>(g("ep_len"));
+    e.ep_ret = P<float>(g("ep_ret")); e.dynA = P<const float>(g("dynA")); e.dynB = P<const float>(g("dynB"));
+    e.dynw = P<const float>(g("dynw")); e.seed = g("seed"); e.counter = P<const int64_t>(g("counter"));
+    e.ep_count = P<int>(g("ep_count")); e.ep_log = P<float>(g("ep_log")); e.log_cap = gi("log_cap");
+    return e;
+  });
+  py::class_<AqlInsert>(m, "AqlInsert");
+  m.def("make_aql_insert", [](py::dict d) {
+    auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+    AqlInsert i{};
+    i.st = P<float>(g("st")); i.st2 = P<float>(g("st2")); i.rew = P<float>(g("rew")); i.done = P<float>(g("done"));
+    i.amu = P<float>(g("amu")); i.act = P<int>(g("act")); i.C = d["C"].cast<int64_t>();
+    i.filled = P<const int64_t>(g("filled")); i.slots = P<int>(g("slots"));
+    return i;
+  });
+  m.def("aql_env_reset", [](const AqlEnv& e, uint64_t s) { aql_env_reset(e, S(s)); });
+  m.def("aql_env_step", [](const AqlEnv& e, uint64_t env_act, uint64_t act_idx, uint64_t amu, const AqlInsert& ins,
+                           uint64_t s) {
+    aql_env_step(e, P<const float>(env_act), P<const int>(act_idx), P<const float>(amu), ins, S(s));
+  });
   m.def("aql_select", [](uint64_t q, uint64_t a_mu, int B, int T, int adim, uint64_t eps, uint64_t seed,
                          uint64_t counter, uint64_t act_idx, uint64_t env_act, uint64_t s) {
     aql_select(P<const float>(q), P<const float>(a_mu), B, T, adim, P<const float>(eps), seed,

@@ -393,4 +393,87 @@ void aql_propose(const AQLNet& net, const float* state, int B, const float* low,
 void aql_select(const float* q, const float* a_mu, int B, int T, int adim, const float* eps, uint64_t seed,
                 const int64_t* counter, int* act_idx, float* env_act, hipStream_t s);
 
+// ---- aql_engine_kernels.hip (GPU AQL engine: fused learner step, vector envs + replay insert)
+// Per-sample backward vectors written by aql_learn_bwd and contracted over the batch by
+// aql_grad (every weight gradient is sum_b G[b][row] * X[b][col]).  Offsets in floats.
+namespace aqlv {
+constexpr int GQ = 0, H = 8, GH = 72, X = 136, GX = 264, AOH = 392, GAOH = 520, A = 648, QFH = 656, GQFH = 720,
+              S = 784, EMB = 848, HID = 976, GHID = 1104, GMU = 1232, STRIDE = 1296;
+}
+constexpr int kAqlMaxJobs = 24;
+struct AqlLearn {
+  AQLNet on, tg;                             // online / target critic + proposal weights
+  const float *st, *st2, *rew, *done, *amu;  // replay tables [C][obs] x2, [C], [C], [C][T][adim]
+  const int* act;                            // [C] taken candidate index
+  const int* idx;                            // [B] sampled slots
+  const float* w;                            // [B] IS weights
+  int B;
+  float gamma_n, ent_lam;
+  const float* var;                          // proposal MVN diagonal [na]
+  float *q_s, *q_s2, *qt_s2;                 // [B][T] Q(s,.), Q(s',.), Q_tgt(s',.)
+  float* vec;                                // [B][aqlv::STRIDE]
+  float *delta, *lw, *lossp;                 // [B] |td|, w*Huber, per-sample proposal loss
+};
+void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
+void aql_learn_bwd(const AqlLearn& L, hipStream_t s);
+struct AqlGradJob {
+  int64_t off;         // flat offset of the parameter tensor
+  int rows, cols;      // [rows][cols]; a bias has cols = 1 and xoff < 0
+  int goff, xoff;      // aqlv offsets of the output-gradient / input vectors
+  const float* eps;    // NoisyLinear sigma: grad = grad_mu * eps (nullable)
+  int group;           // 0 = critic (optimizer_q), 1 = proposal (optimizer_proposal)
+  int zero;            // identically zero (q.features: only the proposal loss reaches it)
+};
+struct AqlGrad {
+  AqlGradJob job[kAqlMaxJobs];
+  int njobs;
+  int64_t n;           // flat parameters (jobs cover [0, n) in offset order)
+  const float* vec;
+  int B;
+  float* grad;
+  double* part;        // [2][blocks] sum of squares per group
+  const float* lossp;  // [B]
+  float* lossp_out;    // [1] proposal loss mean
+};
+int aql_grad_blocks(int64_t n);
+void aql_grad(const AqlGrad& g, hipStream_t s);
+struct AqlNoise {
+  float *weps, *beps;  // NoisyLinear epsilon buffers [out][in], [out]
+  int out, in;
+};
+struct AqlPost {
+  AqlNoise layer[4];   // online advantage1/2, target advantage1/2 (fresh factorised noise)
+  const float* src;    // online proposal parameters ...
+  float* dst;          // ... hard-copied into the target's (AQL_dis.py:92)
+  int64_t n_copy;
+  int64_t* step;       // learner step counter (+1 by the last block)
+  int* ticket;
+  uint64_t seed;
+};
+void aql_post(const AqlPost& p, hipStream_t s);
+struct AqlEnv {
+  int kind;            // 0 BipedalWalker-shaped, 1 CartPole, 2 Pendulum
+  int E, obs, adim, T, max_steps;
+  float* obs_buf;      // [E][obs]
+  float* phys;         // [E][4] internal state (CartPole, Pendulum)
+  int* ep_len;
+  float* ep_ret;
+  const float *dynA, *dynB, *dynw;  // BipedalWalker-shaped dynamics [24][24], [24][4], [24]
+  uint64_t seed;
+  const int64_t* counter;           // actor step counter (Philox)
+  int* ep_count;                    // finished episodes (monotone)
+  float* ep_log;                    // [log_cap][2] (return, length) ring
+  int log_cap;
+};
+struct AqlInsert {
+  float *st, *st2, *rew, *done, *amu;
+  int* act;
+  int64_t C;
+  const int64_t* filled;
+  int* slots;          // [E] out: ring slots written this step
+};
+void aql_env_reset(const AqlEnv& e, hipStream_t s);
+void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, const float* amu, const AqlInsert& ins,
+                  hipStream_t s);
+
 }  // namespace apex
