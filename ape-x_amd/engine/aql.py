@@ -38,6 +38,7 @@ broadcasts log_prob([B,1]) against batch [B] (see aql_engine_kernels.hip).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -52,17 +53,23 @@ from .hbm_replay import tree_level_sizes
 ENV_KINDS = {"BipedalWalker-v3": 0, "CartPole-v0": 1, "CartPole-v1": 1, "Pendulum-v0": 2, "Pendulum-v1": 2}
 
 
-def flatten_module_params(module: torch.nn.Module) -> torch.Tensor:
+def flatten_module_params(module: torch.nn.Module, align: int = 4) -> torch.Tensor:
     """Re-seat every parameter of ``module`` as a view of one contiguous fp32 buffer
-    (named_parameters order); returns the buffer."""
-    params = list(module.parameters())
-    flat = torch.empty(sum(p.numel() for p in params), dtype=torch.float32, device=params[0].device)
-    off = 0
-    for p in params:
-        n = p.numel()
-        flat[off:off + n].copy_(p.data.reshape(-1))
-        p.data = flat[off:off + n].view_as(p.data)
-        off += n
+    (named_parameters order), each starting at a multiple of ``align`` floats (16-byte rows
+    for the learner's vector loads; the zero gaps get zero gradients and stay zero).
+    Offsets are kept in ``module._flat_offsets``; returns the buffer."""
+    params = list(module.named_parameters())
+    offs, off = {}, 0
+    for name, p in params:
+        off = -(-off // align) * align
+        offs[name] = off
+        off += p.numel()
+    flat = torch.zeros(-(-off // align) * align, dtype=torch.float32, device=params[0][1].device)
+    for name, p in params:
+        o, n = offs[name], p.numel()
+        flat[o:o + n].copy_(p.data.reshape(-1))
+        p.data = flat[o:o + n].view_as(p.data)
+    module._flat_offsets = offs
     return flat
 
 
@@ -110,6 +117,11 @@ class AQLReplay:
         self.max_prio = torch.ones(1, **f32)
         self.filled = torch.zeros(1, dtype=torch.int64, device=dev)
         self.sorted_scratch = torch.zeros(1024, dtype=torch.int32, device=dev)
+        # batched tree write scratch (per_write_batch): dedup claims (-1 between writes),
+        # dirty-slot list, last-block ticket
+        self.owner = torch.full((C,), -1, dtype=torch.int32, device=dev)
+        self.wlist = torch.zeros(2048, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         self.tree = self.hip.make_tree(self.leaf_sum.data_ptr(), self.leaf_min.data_ptr(),
                                        [t.data_ptr() for t in self.node_sum], [t.data_ptr() for t in self.node_min],
                                        sizes)
@@ -173,10 +185,11 @@ class AQLLearner:
         self.eps = flatten_noise(model)
         self.teps = flatten_noise(target)
         names = [n for n, _ in model.named_parameters()]
-        self.P = self.flat.numel()
-        self.P_q = sum(p.numel() for n, p in model.named_parameters() if n.startswith("q."))
-        assert all(n.startswith("q.") for n in names[:sum(1 for n in names if n.startswith("q."))]), \
+        n_q = sum(1 for n in names if n.startswith("q."))
+        assert all(n.startswith("q.") for n in names[:n_q]) and n_q < len(names), \
             "critic parameters must precede the proposal's in the flat layout"
+        self.P = self.flat.numel()
+        self.P_q = model._flat_offsets[names[n_q]]  # first proposal parameter (aligned)
         self.P_p = self.P - self.P_q
         B, T = cfg.batch_size, model.total_sample
         self.B, self.T = B, T
@@ -209,22 +222,39 @@ class AQLLearner:
         self.hp = h.AdamParams(cfg.lr, max_norm=cfg.max_norm)
         self.fused_on = FusedAQL(model)
         self.fused_tg = FusedAQL(target)
-        p = dict(replay.table_ptrs(), idx=self.idx.data_ptr(), w=self.w.data_ptr(), var=self.var.data_ptr(),
+        nws = h.aql_workspace_floats()  # effective NoisyLinear weights: W1 [64][128] | b1 | w2 | b2
+        self.eff_on = torch.zeros(nws, **f32)
+        self.eff_tg = torch.zeros(nws, **f32)
+        self.dbg = torch.zeros(16, dtype=torch.int64, device=dev) if os.environ.get("APEX_AQL_DBG") else None
+        p = dict(replay.table_ptrs(), eff_on=self.eff_on.data_ptr(), eff_tg=self.eff_tg.data_ptr(), idx=self.idx.data_ptr(), w=self.w.data_ptr(), var=self.var.data_ptr(),
                  q_s=self.q_s.data_ptr(), q_s2=self.q_s2.data_ptr(), qt_s2=self.qt_s2.data_ptr(),
                  vec=self.vec.data_ptr(), delta=self.delta.data_ptr(), lw=self.lw.data_ptr(),
                  lossp=self.lossp.data_ptr())
+        if self.dbg is not None:  # phase timestamps of the backward kernel (diagnostics)
+            p["dbg"] = self.dbg.data_ptr()
         self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
                                   float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
         self.G = h.make_aql_grad(self._grad_jobs(), self.P, self.vec.data_ptr(), B, self.grad.data_ptr(),
                                  self.part.data_ptr(), self.lossp.data_ptr(), self.loss_p.data_ptr())
         layers = []
-        for m in (model, target):
-            for lin in (m.q.advantage1, m.q.advantage2):
-                layers.append((lin.weight_epsilon.data_ptr(), lin.bias_epsilon.data_ptr(), lin.out_features,
-                               lin.in_features))
+        for m, eff in ((model, self.eff_on), (target, self.eff_tg)):
+            n1 = 64 * 128
+            views = ((eff[:n1], eff[n1:n1 + 64]), (eff[n1 + 64:n1 + 128], eff[n1 + 128:n1 + 129]))
+            for lin, (weff, beff) in zip((m.q.advantage1, m.q.advantage2), views):
+                assert weff.numel() == lin.weight_mu.numel() and beff.numel() == lin.bias_mu.numel()
+                layers.append((lin.weight_epsilon.data_ptr(), lin.bias_epsilon.data_ptr(), lin.weight_mu.data_ptr(),
+                               lin.weight_sigma.data_ptr(), lin.bias_mu.data_ptr(), lin.bias_sigma.data_ptr(),
+                               weff.data_ptr(), beff.data_ptr(), lin.out_features, lin.in_features))
         self.post = h.make_aql_post(layers, self.flat[self.P_q:].data_ptr(), self.tflat[self.P_q:].data_ptr(),
                                     self.P_p, self.step_ctr.data_ptr(), self.ticket.data_ptr(),
                                     (cfg.seed * 0x9E3779B1 + 0x5EED) & 0xFFFFFFFFFFFF)
+        self.refresh()
+
+    def refresh(self) -> None:
+        """Recompute the effective NoisyLinear weights (mu + sigma * eps) of both networks
+        from their current parameters / noise: after init, a target sync or any direct
+        parameter edit (load_state_dict)."""
+        self.hip.aql_post(self.post, 0, self._s())
 
     def _grad_jobs(self):
         lay, m = self.lay, self.model
@@ -245,6 +275,10 @@ class AQLLearner:
         }
         jobs, off = [], 0
         for name, p in m.named_parameters():
+            o = m._flat_offsets[name]
+            if o > off:  # alignment gap: zero gradient
+                jobs.append((off, o - off, 1, 0, -1, 0, 0, 1))
+                off = o
             rows = p.shape[0]
             cols = p.numel() // rows
             group = 1 if name.startswith("proposal.") else 0
@@ -258,6 +292,8 @@ class AQLLearner:
                     rows, cols = p.numel(), 1
                 jobs.append((off, rows, cols, goff, xoff, 0 if eps is None else eps.data_ptr(), group, 0))
             off += p.numel()
+        if off < self.P:
+            jobs.append((off, self.P - off, 1, 0, -1, 0, 1, 1))
         return jobs
 
     @staticmethod
@@ -271,9 +307,11 @@ class AQLLearner:
                      self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
         h.aql_learn_fwd(self.L, s)
         h.aql_learn_bwd(self.L, s)
-        h.per_write_leaves(r.tree, self.idx.data_ptr(), 0, self.B, r.alpha, r.max_prio.data_ptr(), 1,
-                           r.sorted_scratch.data_ptr(), 0, 0, 0, 0, s, self.delta.data_ptr(), self.lw.data_ptr(),
-                           self.prio.data_ptr(), self.loss_q.data_ptr())
+        # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
+        # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
+        h.per_write_batch(r.tree, 0, 0, 0, 0, self.idx.data_ptr(), 0, self.B, self.delta.data_ptr(),
+                          self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
+                          r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), s)
         h.aql_grad(self.G, s)
         Pq = self.P_q
         h.adam_step(self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
@@ -282,13 +320,14 @@ class AQLLearner:
         h.adam_step(self.flat.data_ptr() + o, self.grad.data_ptr() + o, self.m.data_ptr() + o, self.v.data_ptr() + o,
                     self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk, self.hp, self.step_ctr.data_ptr(),
                     self.norms_p.data_ptr(), s)
-        h.aql_post(self.post, s)
+        h.aql_post(self.post, 1, s)
 
     def sync_target(self) -> None:
         """update_target (AQL_dis.py:60-61): full state_dict copy, noise buffers included."""
         s = self._s()
         self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, s)
         self.hip.copy_f32(self.teps.data_ptr(), self.eps.data_ptr(), self.eps.numel(), s)
+        self.refresh()
 
     def stats(self) -> dict:
         return {"loss_q": float(self.loss_q.item()), "loss_proposal": float(self.loss_p.item()),

@@ -54,6 +54,12 @@ __device__ __forceinline__ float noisy_w(const float* mu, const float* sg, const
   return noisy ? fmaf(sg[i], ep[i], m) : m;
 }
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
+// phase timestamp (diagnostics): block 0, thread 0, after a barrier
+#define AQL_STAMP(L, k)                                                   \
+  do {                                                                    \
+    if ((L).dbg && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) \
+      (L).dbg[k] = (long long)clock64();                                  \
+  } while (0)
 
 // (value, index) argmax over a row of length T by one wave; ties -> lowest index
 __device__ __forceinline__ int wave_argmax(const float* row, int T, int lane) {
@@ -73,56 +79,79 @@ __device__ __forceinline__ int wave_argmax(const float* row, int T, int lane) {
 }
 
 // ------------------------------------------------------------------ forward over candidates
+// Effective NoisyLinear weights come precomputed (aql_post writes mu + sigma * eps after each
+// update): the forward reads one array per layer instead of three.
+constexpr int kEffB1 = kH * kCat, kEffW2 = kEffB1 + kH, kEffB2 = kEffW2 + kH;
+
 __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
-  __shared__ float ao2[kH * kP132];     // action_out.2 weight [n][k]
-  __shared__ float w1a[kH * kP68];      // advantage1 effective weight, candidate half [n][k]
-  __shared__ float xt[16 * kP68];       // ao_out tile [16 candidates][64]
+  __shared__ __attribute__((aligned(16))) float ao2[kH * kP132];  // action_out.2 weight [n][k]
+  __shared__ __attribute__((aligned(16))) float w1[kH * kP132];   // advantage1 effective weight [n][k]
+  __shared__ float qw1[kH * 65], qw2[kH * 65];                     // q_feature.0 [n][obs], .2 [n][k]
+  __shared__ float xt[16 * kP68];                                  // ao_out tile [16 candidates][64]
   __shared__ float ao1w[kCat * kMaxAdim];
-  __shared__ float ao1b[kCat], ao2b[kH], w2e[kH];
+  __shared__ float ao1b[kCat], ao2b[kH], w2e[kH], b1e[kH], qb1[kH], qb2[kH];
   __shared__ float sv[2][64], hq[2][kH], qf[2][kH], stp[2][kH];
   __shared__ float qpart[4][2][16];
   const bool tgt = blockIdx.y != 0;
   const AQLNet& N = tgt ? L.tg : L.on;
+  const float* eff = tgt ? L.eff_tg : L.eff_on;
   const int T = N.T, RT = (T + 15) >> 4;
   const int b = blockIdx.x / RT, rt = blockIdx.x - b * RT;
   const int nst = tgt ? 1 : 2;  // online: {s, s'}, target: {s'}
   const int row = L.idx[b];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, q = lane >> 4;
-  const int obs = N.obs, adim = N.adim, cont = N.cont, noisy = N.noisy;
-  if (t < 128) {
-    const int si = t >> 6, i = t & 63;
-    if (si < nst && i < obs) sv[si][i] = ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i];
+  const int obs = N.obs, adim = N.adim, cont = N.cont, po = obs + 1;
+  {  // stage the two 64x128 matrices with 16-byte loads, all in flight before the stores
+    const f32x4* a4 = reinterpret_cast<const f32x4*>(N.ao_w2);
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(eff);
+    f32x4 va[8], vw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (cont) va[k] = a4[t + 256 * k];
+      vw[k] = w4[t + 256 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int e4 = t + 256 * k, r = e4 >> 5, c = (e4 & 31) * 4;
+      if (cont) *reinterpret_cast<f32x4*>(&ao2[r * kP132 + c]) = va[k];
+      *reinterpret_cast<f32x4*>(&w1[r * kP132 + c]) = vw[k];
+    }
   }
-  for (int e = t; e < kH * kCat; e += 256) {
-    const int n = e >> 7, k = e & 127;
-    if (cont) ao2[n * kP132 + k] = N.ao_w2[e];
-    if (k < kH) w1a[n * kP68 + k] = noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, e, noisy);
+  for (int e = t; e < kH * obs; e += 256) qw1[(e / obs) * po + e % obs] = N.qf_w1[e];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int e = t + 256 * k;
+    qw2[(e >> 6) * 65 + (e & 63)] = N.qf_w2[e];
   }
   const int nao1 = cont ? kCat : kH;
   for (int e = t; e < nao1 * adim; e += 256) ao1w[e] = N.ao_w1[e];
   if (t < nao1) ao1b[t] = N.ao_b1[t];
   if (t < kH) {
     if (cont) ao2b[t] = N.ao_b2[t];
-    w2e[t] = noisy_w(N.a2_wmu, N.a2_wsig, N.a2_weps, t, noisy);
+    w2e[t] = eff[kEffW2 + t];
+    b1e[t] = eff[kEffB1 + t];
+    qb1[t] = N.qf_b1[t];
+    qb2[t] = N.qf_b2[t];
+  }
+  if (t < 128) {
+    const int si = t >> 6, i = t & 63;
+    if (si < nst && i < obs) sv[si][i] = ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i];
   }
   __syncthreads();
-  // state halves: wave si < nst handles state si (q_feature MLP, then W1[:, 64:] . qf + b1)
+  // state halves, from LDS: wave si < nst handles state si (q_feature MLP, W1[:, 64:] . qf + b1)
   if (wave < nst) {
-    float a = N.qf_b1[lane];
-    for (int i = 0; i < obs; ++i) a = fmaf(N.qf_w1[lane * obs + i], sv[wave][i], a);
+    float a = qb1[lane];
+    for (int i = 0; i < obs; ++i) a = fmaf(qw1[lane * po + i], sv[wave][i], a);
     hq[wave][lane] = relu(a);
-  }
-  __syncthreads();
-  if (wave < nst) {
-    float a = N.qf_b2[lane];
-    for (int k = 0; k < kH; ++k) a = fmaf(N.qf_w2[lane * kH + k], hq[wave][k], a);
+    __builtin_amdgcn_wave_barrier();
+    a = qb2[lane];
+#pragma unroll 16
+    for (int k = 0; k < kH; ++k) a = fmaf(qw2[lane * 65 + k], hq[wave][k], a);
     qf[wave][lane] = relu(a);
-  }
-  __syncthreads();
-  if (wave < nst) {
-    float a = noisy_w(N.a1_bmu, N.a1_bsig, N.a1_beps, lane, noisy);
-    for (int k = 0; k < kH; ++k)
-      a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, lane * kCat + kH + k, noisy), qf[wave][k], a);
+    __builtin_amdgcn_wave_barrier();
+    a = b1e[lane];
+#pragma unroll 16
+    for (int k = 0; k < kH; ++k) a = fmaf(w1[lane * kP132 + kH + k], qf[wave][k], a);
     stp[wave][lane] = a;
   }
   // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
@@ -134,6 +163,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
 #pragma unroll
     for (int d = 0; d < kMaxAdim; ++d) av[d] = d < adim ? am[d] : 0.f;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll 4
     for (int k0 = 0; k0 < kCat; k0 += 8) {
       float h0 = ao1b[k0 + q], h1 = ao1b[k0 + 4 + q];
 #pragma unroll
@@ -160,8 +190,8 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
   for (int k0 = 0; k0 < kH; k0 += 8) {
-    c0 = mfma4(xt[j * kP68 + k0 + q], w1a[n * kP68 + k0 + q], c0);
-    c1 = mfma4(xt[j * kP68 + k0 + 4 + q], w1a[n * kP68 + k0 + 4 + q], c1);
+    c0 = mfma4(xt[j * kP68 + k0 + q], w1[n * kP132 + k0 + q], c0);
+    c1 = mfma4(xt[j * kP68 + k0 + 4 + q], w1[n * kP132 + k0 + 4 + q], c1);
   }
   for (int si = 0; si < nst; ++si) {
 #pragma unroll
@@ -178,8 +208,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   if (t < 16 * nst) {
     const int m = t & 15, si = t >> 4, tt = rt * 16 + m;
     if (tt < T) {
-      const float b2 = noisy_w(N.a2_bmu, N.a2_bsig, N.a2_beps, 0, noisy);
-      const float qv = ((qpart[0][si][m] + qpart[1][si][m]) + (qpart[2][si][m] + qpart[3][si][m])) + b2;
+      const float qv = ((qpart[0][si][m] + qpart[1][si][m]) + (qpart[2][si][m] + qpart[3][si][m])) + eff[kEffB2];
       float* out = tgt ? L.qt_s2 : (si ? L.q_s2 : L.q_s);
       out[(size_t)b * T + tt] = qv;
     }
@@ -187,17 +216,63 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
 }
 
 // ------------------------------------------------------------------ per-sample loss + backward
+// sum_r W[r][k] g[r] for column k (one thread per column, R <= RMAX rows, all loads issued
+// before the FMAs; each row is read coalesced across the threads)
+template <int RMAX>
+__device__ __forceinline__ float cols_dot(const float* __restrict__ W, int K, int R, const float* g, int k) {
+  float w[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) w[r] = r < R ? W[(size_t)r * K + k] : 0.f;
+  float a = 0.f;
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) a = r < R ? fmaf(w[r], g[r], a) : a;
+  return a;
+}
+
+// sum_i W[r][i] v[i] for one row of n = 4*N4 inputs (16-byte aligned rows): all N4 16-byte
+// loads of the row issued before the FMAs -- no cross-lane reduction (the ds_bpermute
+// butterflies of a wave-per-row scheme serialise: 33 us for this phase)
+template <int N4>
+__device__ __forceinline__ float row_dot4(const float* __restrict__ W, int r, const float* v) {
+  const f32x4* w = reinterpret_cast<const f32x4*>(W + (size_t)r * 4 * N4);
+  f32x4 x[N4];
+#pragma unroll
+  for (int k = 0; k < N4; ++k) x[k] = w[k];
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < N4; ++k) {
+    a0 = fmaf(x[k].x, v[4 * k], a0);
+    a1 = fmaf(x[k].y, v[4 * k + 1], a1);
+    a0 = fmaf(x[k].z, v[4 * k + 2], a0);
+    a1 = fmaf(x[k].w, v[4 * k + 3], a1);
+  }
+  return a0 + a1;
+}
+
+// small first-layer matrices (inputs obs / adim <= 64) from LDS: one thread per output row
+__device__ __forceinline__ float lds_row_dot(const float* Wl, int n, const float* v, float bias) {
+  float a = bias;
+  for (int i = 0; i < n; ++i) a = fmaf(Wl[i], v[i], a);
+  return a;
+}
+
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
-  __shared__ float s_s[64], s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], hh[kH], gh[kH], gx[kCat];
+  __shared__ float s_s[64], s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
   __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
   __shared__ int cnt[64];
   __shared__ int s_best, s_next;
   __shared__ float s_gq;
+  __shared__ float sw_qf1[kH * 64], sw_ao1[kCat * kMaxAdim], sw_f[kCat * 64];  // first layers [row][in]
   const AQLNet& N = L.on;
+  const float* eff = L.eff_on;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int T = N.T, obs = N.obs, adim = N.adim, na = N.na, B = L.B, cont = N.cont, noisy = N.noisy;
+  const int T = N.T, obs = N.obs, adim = N.adim, na = N.na, B = L.B, cont = N.cont;
   const int row = L.idx[b];
   const int a_idx = L.act[row];
+  AQL_STAMP(L, 0);
+  for (int e = t; e < kH * obs; e += 256) sw_qf1[e] = N.qf_w1[e];
+  for (int e = t; e < (cont ? kCat : kH) * adim; e += 256) sw_ao1[e] = N.ao_w1[e];
+  for (int e = t; e < kCat * obs; e += 256) sw_f[e] = N.f_w[e];
   if (wave == 0) {
     const int bi = wave_argmax(L.q_s + (size_t)b * T, T, lane);
     if (lane == 0) s_best = bi;
@@ -209,6 +284,7 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   if (t < obs) s_s[t] = L.st[(size_t)row * obs + t];
   if (t < adim) s_a[t] = L.amu[((size_t)row * T + a_idx) * adim + t];
   __syncthreads();
+  AQL_STAMP(L, 1);
   if (!cont) {  // counts of every sample's best candidate (the [B, B] log-prob broadcast)
     for (int i = wave; i < B; i += 4) {
       const int ri = L.idx[i];
@@ -228,76 +304,42 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
     const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
     s_gq = -sg * fminf(dl, 1.f) * wb / (float)B;
   }
-  // forward of the taken candidate (s, a_mu[a]) + the proposal trunk
+  // forward of the taken candidate (s, a_mu[a]) + the proposal trunk.  First layers from
+  // the LDS-staged matrices (thread per row), then the 64/128-wide layers wave-per-row.
   if (t < kH) {
-    float a = N.qf_b1[t];
-    for (int i = 0; i < obs; ++i) a = fmaf(N.qf_w1[t * obs + i], s_s[i], a);
-    qfh[t] = relu(a);
+    qfh[t] = relu(lds_row_dot(sw_qf1 + t * obs, obs, s_s, N.qf_b1[t]));
   } else if (t < kH + (cont ? kCat : kH)) {
     const int k = t - kH;
-    float a = N.ao_b1[k];
-    for (int d = 0; d < adim; ++d) a = fmaf(N.ao_w1[k * adim + d], s_a[d], a);
-    aoh[k] = relu(a);
+    aoh[k] = relu(lds_row_dot(sw_ao1 + k * adim, adim, s_a, N.ao_b1[k]));
   }
-  __syncthreads();
-  if (t < kH) {
-    float a = N.qf_b2[t];
-    for (int k = 0; k < kH; ++k) a = fmaf(N.qf_w2[t * kH + k], qfh[k], a);
-    x[kH + t] = relu(a);
-  } else if (t < 2 * kH) {
-    const int nn = t - kH;
-    if (cont) {
-      float a = N.ao_b2[nn];
-      for (int k = 0; k < kCat; ++k) a = fmaf(N.ao_w2[nn * kCat + k], aoh[k], a);
-      x[nn] = relu(a);
-    } else {
-      x[nn] = aoh[nn];
-    }
-  } else {
+  if (t >= 2 * kH) {
     const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
-    float a = N.f_b[k];
-    for (int i = 0; i < obs; ++i) a = fmaf(N.f_w[k * obs + i], s_s[i], a);
-    emb[k] = relu(a);
+    emb[k] = relu(lds_row_dot(sw_f + k * obs, obs, s_s, N.f_b[k]));
   }
   __syncthreads();
-  if (t < kH) {
-    float a = noisy_w(N.a1_bmu, N.a1_bsig, N.a1_beps, t, noisy);
-    for (int k = 0; k < kCat; ++k) a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, t * kCat + k, noisy), x[k], a);
-    hh[t] = relu(a);
-    gh[t] = a > 0.f ? s_gq * noisy_w(N.a2_wmu, N.a2_wsig, N.a2_weps, t, noisy) : 0.f;
-  } else if (t >= 2 * kH) {
+  AQL_STAMP(L, 2);
+  if (t < kH) {  // q_feature.2
+    x[kH + t] = relu(row_dot4<kH / 4>(N.qf_w2, t, qfh) + N.qf_b2[t]);
+  } else if (t < 2 * kH) {  // action_out.2 (continuous) / identity (discrete)
+    const int nn = t - kH;
+    x[nn] = cont ? relu(row_dot4<kCat / 4>(N.ao_w2, nn, aoh) + N.ao_b2[nn]) : aoh[nn];
+  } else {  // proposal dist_feature.0
     const int k = t - 2 * kH;
-    float a = N.df_b1[k];
-    for (int i = 0; i < kCat; ++i) a = fmaf(N.df_w1[k * kCat + i], emb[i], a);
-    hid[k] = relu(a);
+    hid[k] = relu(row_dot4<kCat / 4>(N.df_w1, k, emb) + N.df_b1[k]);
   }
   __syncthreads();
-  if (t < kCat) {
-    float a = 0.f;
-    for (int nn = 0; nn < kH; ++nn) a = fmaf(noisy_w(N.a1_wmu, N.a1_wsig, N.a1_weps, nn * kCat + t, noisy), gh[nn], a);
-    gx[t] = x[t] > 0.f ? a : 0.f;
-  } else if (t - kCat < na) {
-    const int d = t - kCat;
-    float a = N.df_b2[d];
-    for (int k = 0; k < kCat; ++k) a = fmaf(N.df_w2[d * kCat + k], hid[k], a);
-    mu[d] = a;
+  AQL_STAMP(L, 3);
+  if (t < kH) {  // advantage1 pre-activation (effective noisy weight)
+    pre[t] = row_dot4<kCat / 4>(eff, t, x) + eff[kEffB1 + t];
+  } else if (t >= 2 * kH && t - 2 * kH < na) {  // proposal mean / logits
+    const int d = t - 2 * kH;
+    mu[d] = row_dot4<kCat / 4>(N.df_w2, d, hid) + N.df_b2[d];
   }
   __syncthreads();
-  float* V = L.vec + (size_t)b * aqlv::STRIDE;
-  if (t < kCat) {
-    if (cont) {  // action_out.0 input gradient
-      float a = 0.f;
-      for (int nn = 0; nn < kH; ++nn) a = fmaf(N.ao_w2[nn * kCat + t], gx[nn], a);
-      V[aqlv::GAOH + t] = aoh[t] > 0.f ? a : 0.f;
-      V[aqlv::AOH + t] = aoh[t];
-    }
-  } else if (t < kCat + kH) {  // q_feature.0 input gradient
-    const int k = t - kCat;
-    float a = 0.f;
-    for (int nn = 0; nn < kH; ++nn) a = fmaf(N.qf_w2[nn * kH + k], gx[kH + nn], a);
-    V[aqlv::GQFH + k] = qfh[k] > 0.f ? a : 0.f;
-    V[aqlv::QFH + k] = qfh[k];
-  } else {  // wave 3: proposal loss gradient w.r.t. mu (analytic)
+  AQL_STAMP(L, 4);
+  if (t < kH) {
+    gh[t] = pre[t] > 0.f ? s_gq * eff[kEffW2 + t] : 0.f;
+  } else if (wave == 3) {  // proposal loss gradient w.r.t. mu (analytic)
     float lp = 0.f;
     if (cont) {
       float d2 = 0.f, lv = 0.f;
@@ -329,23 +371,43 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
     if (lane == 0) L.lossp[b] = lp;
   }
   __syncthreads();
-  if (t < kCat) {  // proposal hidden gradient
-    float a = 0.f;
-    for (int d = 0; d < na; ++d) a = fmaf(N.df_w2[d * kCat + t], gmu[d], a);
-    V[aqlv::GHID + t] = hid[t] > 0.f ? a : 0.f;
-    V[aqlv::HID + t] = hid[t];
-    V[aqlv::EMB + t] = emb[t];
+  AQL_STAMP(L, 5);
+  float* V = L.vec + (size_t)b * aqlv::STRIDE;
+  if (t < kCat) {  // advantage1 input gradient
+    const float a = cols_dot<kH>(eff, kCat, kH, gh, t);
+    gx[t] = x[t] > 0.f ? a : 0.f;
+  } else {  // proposal hidden gradient
+    const int k = t - kCat;
+    const float a = cols_dot<64>(N.df_w2, kCat, na, gmu, k);
+    V[aqlv::GHID + k] = hid[k] > 0.f ? a : 0.f;
+    V[aqlv::HID + k] = hid[k];
+    V[aqlv::EMB + k] = emb[k];
+  }
+  __syncthreads();
+  AQL_STAMP(L, 6);
+  if (t < kCat) {
+    if (cont) {  // action_out.0 input gradient
+      const float a = cols_dot<kH>(N.ao_w2, kCat, kH, gx, t);
+      V[aqlv::GAOH + t] = aoh[t] > 0.f ? a : 0.f;
+      V[aqlv::AOH + t] = aoh[t];
+    }
     V[aqlv::X + t] = x[t];
     V[aqlv::GX + t] = gx[t];
-  } else if (t < kCat + kH) {
+  } else if (t < kCat + kH) {  // q_feature.0 input gradient
     const int k = t - kCat;
-    V[aqlv::H + k] = hh[k];
+    const float a = cols_dot<kH>(N.qf_w2, kH, kH, gx + kH, k);
+    V[aqlv::GQFH + k] = qfh[k] > 0.f ? a : 0.f;
+    V[aqlv::QFH + k] = qfh[k];
+    V[aqlv::H + k] = relu(pre[k]);
     V[aqlv::GH + k] = gh[k];
+  } else {
+    const int k = t - kCat - kH;
     if (k < na) V[aqlv::GMU + k] = gmu[k];
     if (k < obs) V[aqlv::S + k] = s_s[k];
     if (k < adim) V[aqlv::A + k] = s_a[k];
     if (k == 0) V[aqlv::GQ] = s_gq;
   }
+  AQL_STAMP(L, 7);
 }
 
 // ------------------------------------------------------------------ weight gradients
@@ -365,10 +427,21 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
     const int e = (int)(i - J.off), r = e / J.cols, c = e - r * J.cols;
     grp = J.group;
     if (!J.zero) {
+      // the batch contraction in chunks of 16 samples, every load of a chunk in flight
       float acc = 0.f;
-      const float* V = G.vec;
-      for (int b = 0; b < G.B; ++b, V += aqlv::STRIDE)
-        acc = fmaf(V[J.goff + r], J.xoff >= 0 ? V[J.xoff + c] : 1.f, acc);
+      const float* gp = G.vec + J.goff + r;
+      const float* xp = G.vec + (J.xoff >= 0 ? J.xoff + c : 0);
+      for (int b0 = 0; b0 < G.B; b0 += 16) {
+        float gv[16], xv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const bool ok = b0 + k < G.B;
+          gv[k] = ok ? gp[(size_t)(b0 + k) * aqlv::STRIDE] : 0.f;
+          xv[k] = (ok && J.xoff >= 0) ? xp[(size_t)(b0 + k) * aqlv::STRIDE] : 1.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fmaf(gv[k], xv[k], acc);
+      }
       g = J.eps ? acc * J.eps[e] : acc;
     }
     G.grad[i] = g;
@@ -401,7 +474,7 @@ __device__ __forceinline__ float scaled_noise(uint64_t seed, int layer, int kind
   return copysignf(sqrtf(fabsf(x)), x);  // f(x) = sign(x) sqrt(|x|) (model.py:160-163)
 }
 
-__global__ __launch_bounds__(256) void aql_post_k(AqlPost P) {
+__global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
   const uint64_t st = (uint64_t)P.step[0];
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 #pragma unroll
@@ -410,12 +483,24 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P) {
     const int64_t nw = (int64_t)z.out * z.in;
     if (i >= 0 && i < nw) {
       const int o = (int)(i / z.in), c = (int)(i - (int64_t)o * z.in);
-      z.weps[i] = scaled_noise(P.seed, l, 0, o, st) * scaled_noise(P.seed, l, 1, c, st);
+      float e = z.weps[i];
+      if (regen) {
+        e = scaled_noise(P.seed, l, 0, o, st) * scaled_noise(P.seed, l, 1, c, st);
+        z.weps[i] = e;
+      }
+      z.weff[i] = fmaf(z.wsig[i], e, z.wmu[i]);
     } else if (i >= nw && i < nw + z.out) {
-      z.beps[i - nw] = scaled_noise(P.seed, l, 2, (int)(i - nw), st);
+      const int o = (int)(i - nw);
+      float e = z.beps[o];
+      if (regen) {
+        e = scaled_noise(P.seed, l, 2, o, st);
+        z.beps[o] = e;
+      }
+      z.beff[o] = fmaf(z.bsig[o], e, z.bmu[o]);
     }
     i -= nw + z.out;
   }
+  if (!regen) return;
   if (i >= 0 && i < P.n_copy) P.dst[i] = P.src[i];
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -588,6 +673,13 @@ static void check_net(const AQLNet& n) {
 
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s) {
   check_net(L.on);
+  if (!L.eff_on || !L.eff_tg) throw std::invalid_argument("aql learner: effective-weight workspaces");
+  for (const float* w : {L.on.qf_w2, L.on.ao_w2, L.on.df_w1, L.on.df_w2})
+    if (w && (reinterpret_cast<uintptr_t>(w) & 15))
+      throw std::invalid_argument("aql learner: weight matrices must be 16-byte aligned (flatten with align=4)");
+  if (((reinterpret_cast<uintptr_t>(L.eff_on) | reinterpret_cast<uintptr_t>(L.eff_tg) |
+        reinterpret_cast<uintptr_t>(L.on.ao_w2) | reinterpret_cast<uintptr_t>(L.tg.ao_w2)) & 15))
+    throw std::invalid_argument("aql learner: action_out.2 weights / workspaces must be 16-byte aligned");
   if (L.tg.T != L.on.T || L.tg.cont != L.on.cont || L.tg.obs != L.on.obs || L.tg.adim != L.on.adim)
     throw std::invalid_argument("aql learner: online / target shapes differ");
   if (L.B < 1) return;
@@ -618,10 +710,10 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
   LAUNCH_CHECK();
 }
 
-void aql_post(const AqlPost& p, hipStream_t s) {
-  int64_t n = p.n_copy;
+void aql_post(const AqlPost& p, int regen, hipStream_t s) {
+  int64_t n = regen ? p.n_copy : 0;
   for (int l = 0; l < 4; ++l) n += (int64_t)p.layer[l].out * p.layer[l].in + p.layer[l].out;
-  aql_post_k<<<(int)((n + 255) / 256), 256, 0, s>>>(p);
+  aql_post_k<<<(int)((n + 255) / 256), 256, 0, s>>>(p, regen);
   LAUNCH_CHECK();
 }
 

@@ -550,6 +550,8 @@ PYBIND11_MODULE(_apex_hip, m) {
     L.q_s = P<float>(g("q_s")); L.q_s2 = P<float>(g("q_s2")); L.qt_s2 = P<float>(g("qt_s2"));
     L.vec = P<float>(g("vec")); L.delta = P<float>(g("delta")); L.lw = P<float>(g("lw"));
     L.lossp = P<float>(g("lossp"));
+    L.eff_on = P<const float>(g("eff_on")); L.eff_tg = P<const float>(g("eff_tg"));
+    L.dbg = p.contains("dbg") ? P<long long>(g("dbg")) : nullptr;
     L.B = B;
     L.gamma_n = gamma_n;
     L.ent_lam = ent_lam;
@@ -569,7 +571,7 @@ PYBIND11_MODULE(_apex_hip, m) {
   // jobs: (off, rows, cols, goff, xoff, eps_ptr, group, zero)
   m.def("make_aql_grad", [](const std::vector<std::array<int64_t, 8>>& jobs, int64_t n, uint64_t vec, int B,
                             uint64_t grad, uint64_t part, uint64_t lossp, uint64_t lossp_out) {
-    if (jobs.empty() || (int)jobs.size() > kAqlMaxJobs) throw std::invalid_argument("make_aql_grad: 1..24 jobs");
+    if (jobs.empty() || (int)jobs.size() > kAqlMaxJobs) throw std::invalid_argument("make_aql_grad: 1..32 jobs");
     AqlGrad G{};
     for (size_t k = 0; k < jobs.size(); ++k) {
       const auto& j = jobs[k];
@@ -589,13 +591,17 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("aql_grad", [](const AqlGrad& G, uint64_t s) { aql_grad(G, S(s)); });
   m.def("aql_grad_blocks", &aql_grad_blocks);
   py::class_<AqlPost>(m, "AqlPost");
-  // layers: 4 x (weps, beps, out, in)
-  m.def("make_aql_post", [](const std::vector<std::array<uint64_t, 4>>& layers, uint64_t src, uint64_t dst,
+  // layers: 4 x (weps, beps, wmu, wsig, bmu, bsig, weff, beff, out, in)
+  m.def("make_aql_post", [](const std::vector<std::array<uint64_t, 10>>& layers, uint64_t src, uint64_t dst,
                             int64_t n_copy, uint64_t step, uint64_t ticket, uint64_t seed) {
     if (layers.size() != 4) throw std::invalid_argument("make_aql_post: 4 noisy layers");
     AqlPost p{};
-    for (int l = 0; l < 4; ++l)
-      p.layer[l] = AqlNoise{P<float>(layers[l][0]), P<float>(layers[l][1]), (int)layers[l][2], (int)layers[l][3]};
+    for (int l = 0; l < 4; ++l) {
+      const auto& y = layers[l];
+      p.layer[l] = AqlNoise{P<float>(y[0]), P<float>(y[1]), P<const float>(y[2]), P<const float>(y[3]),
+                            P<const float>(y[4]), P<const float>(y[5]), P<float>(y[6]), P<float>(y[7]), (int)y[8],
+                            (int)y[9]};
+    }
     p.src = P<const float>(src);
     p.dst = P<float>(dst);
     p.n_copy = n_copy;
@@ -604,7 +610,7 @@ PYBIND11_MODULE(_apex_hip, m) {
     p.seed = seed;
     return p;
   });
-  m.def("aql_post", [](const AqlPost& p, uint64_t s) { aql_post(p, S(s)); });
+  m.def("aql_post", [](const AqlPost& p, int regen, uint64_t s) { aql_post(p, regen, S(s)); });
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

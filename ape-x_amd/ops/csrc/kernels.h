@@ -400,9 +400,10 @@ namespace aqlv {
 constexpr int GQ = 0, H = 8, GH = 72, X = 136, GX = 264, AOH = 392, GAOH = 520, A = 648, QFH = 656, GQFH = 720,
               S = 784, EMB = 848, HID = 976, GHID = 1104, GMU = 1232, STRIDE = 1296;
 }
-constexpr int kAqlMaxJobs = 24;
+constexpr int kAqlMaxJobs = 32;
 struct AqlLearn {
   AQLNet on, tg;                             // online / target critic + proposal weights
+  const float *eff_on, *eff_tg;              // effective NoisyLinear weights (aql_workspace_floats layout)
   const float *st, *st2, *rew, *done, *amu;  // replay tables [C][obs] x2, [C], [C], [C][T][adim]
   const int* act;                            // [C] taken candidate index
   const int* idx;                            // [B] sampled slots
@@ -413,6 +414,7 @@ struct AqlLearn {
   float *q_s, *q_s2, *qt_s2;                 // [B][T] Q(s,.), Q(s',.), Q_tgt(s',.)
   float* vec;                                // [B][aqlv::STRIDE]
   float *delta, *lw, *lossp;                 // [B] |td|, w*Huber, per-sample proposal loss
+  long long* dbg;                            // optional phase timestamps (block 0, s_memtime) or null
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
 void aql_learn_bwd(const AqlLearn& L, hipStream_t s);
@@ -438,11 +440,13 @@ struct AqlGrad {
 int aql_grad_blocks(int64_t n);
 void aql_grad(const AqlGrad& g, hipStream_t s);
 struct AqlNoise {
-  float *weps, *beps;  // NoisyLinear epsilon buffers [out][in], [out]
+  float *weps, *beps;                    // NoisyLinear epsilon buffers [out][in], [out]
+  const float *wmu, *wsig, *bmu, *bsig;  // parameters (post-update)
+  float *weff, *beff;                    // effective weight mu + sigma * eps (learner workspace)
   int out, in;
 };
 struct AqlPost {
-  AqlNoise layer[4];   // online advantage1/2, target advantage1/2 (fresh factorised noise)
+  AqlNoise layer[4];   // online advantage1/2, target advantage1/2
   const float* src;    // online proposal parameters ...
   float* dst;          // ... hard-copied into the target's (AQL_dis.py:92)
   int64_t n_copy;
@@ -450,7 +454,10 @@ struct AqlPost {
   int* ticket;
   uint64_t seed;
 };
-void aql_post(const AqlPost& p, hipStream_t s);
+// regen = 1: fresh factorised noise for all four layers (reset_noise), effective weights,
+// proposal copy, step + 1.  regen = 0: effective weights from the current noise only
+// (after initialisation / a target sync).
+void aql_post(const AqlPost& p, int regen, hipStream_t s);
 struct AqlEnv {
   int kind;            // 0 BipedalWalker-shaped, 1 CartPole, 2 Pendulum
   int E, obs, adim, T, max_steps;

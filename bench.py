@@ -37,6 +37,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 REFERENCE_BATCHES_PER_S = 12.0   # upper end of the reference's 10-12 batches/s
 PAPER_BATCHES_PER_S = 19.0
 
@@ -102,6 +104,10 @@ def parse():
                          "(under torch.distributed.run --nproc-per-node 1): measures its single-GPU overhead")
     ap.add_argument("--local-sampling", action="store_true",
                     help="N>1: sample each replay shard on its own (default: global PER over shards)")
+    ap.add_argument("--algo", default="apex", choices=["apex", "aql"],
+                    help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
+                         "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
+    ap.add_argument("--aql-env", default="BipedalWalker-v3")
     return ap.parse_args()
 
 
@@ -135,6 +141,8 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
     if args.topology == "central":
         return central(args, rank, world, device)
+    if args.algo == "aql":
+        return aql(args, rank, world, device)
 
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
@@ -259,6 +267,73 @@ def main():
             "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
         }
         print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def aql(args, rank, world, device):
+    """GPU AQL engine (engine/aql.py), AQL_dis defaults: batch 32, propose 1 + uniform 50
+    candidates, Adam lr 1e-3, n-step 1; replay ratio of the reference (one SGD step per 32
+    new transitions).  ``value`` = learner SGD steps/s (whole job); actor env steps/s beside.
+    Multi-GPU: independent engines per rank (no published AQL scaling number to compare)."""
+    import torch
+    import torch.distributed as dist
+
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    cap = min(args.capacity, 1_000_000)
+    cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed + rank,
+                          actor_offset=rank * args.envs, total_actors=world * args.envs)
+    eng = AQLEngine(cfg, device)
+    t_fill = time.perf_counter()
+    eng.fill(max(1024, 4 * args.envs))
+    torch.cuda.synchronize(device)
+    t_fill = time.perf_counter() - t_fill
+    if not args.no_graphs:
+        eng.capture()
+    for _ in range(args.warmup):
+        eng.iteration()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.iteration()
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.learner.stats()
+    eps = eng.finished_episodes()
+    sgd = world * args.steps * eng.K / dt
+    env_steps = world * args.steps * eng.E / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": "AQL learner SGD steps/sec + actor env steps/sec (AQL_dis, BipedalWalker-shaped)",
+            "value": round(sgd, 1), "unit": "learner SGD steps (batch 32) per second, whole job",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (GPU BipedalWalker-shaped env, random-init weights)",
+            "config": {"model": f"AQL NoisyNet critic + proposal, {eng.obs}-d obs, {eng.adim}-d action, "
+                                f"T={eng.T} candidates", "global_batch": cfg.batch_size * world, "seq_len": 1,
+                       "parallelism": f"independent x{world}", "env": cfg.env_id, "envs_per_gpu": eng.E,
+                       "sgd_steps_per_iteration": eng.K, "replay_capacity_per_gpu": cap,
+                       "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
+            "actor_env_steps_per_sec": round(env_steps, 1),
+            "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),
+            "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
+            "replay_fill_seconds": round(t_fill, 3),
+            "last_loss_q": round(st["loss_q"], 6), "last_loss_proposal": round(st["loss_proposal"], 6),
+            "episodes_finished": len(eps),
+            "mean_episode_return": round(float(np.mean([r for r, _ in eps])), 3) if eps else None,
+        }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -1,0 +1,49 @@
+#!/usr/bin/env python
+"""AQL learner-step microbenchmark (rocprofv3 / PMC target): builds the GPU AQL engine,
+fills the replay and runs ``--iters`` learner steps (optionally as one captured graph)."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--env", default="BipedalWalker-v3")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--graph", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    eng = AQLEngine(AQLEngineConfig(env_id=a.env, capacity=1_000_000), "cuda:0")
+    eng.fill(4096)
+    L = eng.learner
+    L.step()
+    torch.cuda.synchronize()
+    if a.graph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(a.iters):
+                L.step()
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.replay()
+    else:
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            L.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"{a.iters} learner steps: {1e6 * dt / a.iters:.1f} us/step", L.stats())
+    if L.dbg is not None:  # APEX_AQL_DBG=1: backward phase timestamps (s_memtime cycles) of the last step
+        d = L.dbg.cpu().tolist()
+        print("bwd phase cycles:", [d[k + 1] - d[k] for k in range(7)], "total", d[7] - d[0])
+
+
+if __name__ == "__main__":
+    main()

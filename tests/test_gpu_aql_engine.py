@@ -111,19 +111,20 @@ def test_learner_step_matches_reference(cuda, env_id):
     pr = torch.as_tensor(prios, dtype=torch.float64)
     assert (L.prio.double().cpu() - pr).abs().max().item() <= 1e-4 * pr.abs().max().item()
     # --- gradients (pre-clip), per tensor
-    off = 0
+    offs = eng.model._flat_offsets  # parameters start at 16-byte offsets of the flat buffer
     for name, p in eng.model.named_parameters():
-        n = p.numel()
+        n, off = p.numel(), offs[name]
         g = L.grad[off:off + n].double().reshape(p.shape)
         ref = g_ref[name]
         err = (g - ref).norm().item()
         assert err <= 1e-4 * ref.norm().item() + 1e-9, (name, err, ref.norm().item())
-        off += n
     # --- parameters after both clipped Adam steps: |dp| = lr * m/(sqrt(v)+eps) is sign-like on
     # the first step, so compare the update with an lr-relative bound
+    sel = torch.cat([torch.arange(offs[n], offs[n] + p.numel()) for n, p in eng.model.named_parameters()])
+    sel = sel.to(L.flat.device)
     p_ref = torch.cat([p.detach().reshape(-1) for p in mr.parameters()])
-    diff = (L.flat.double() - p_ref).abs()
-    moved = (p_ref - p_before.double()).abs()
+    diff = (L.flat[sel].double() - p_ref).abs()
+    moved = (p_ref - p_before[sel].double()).abs()
     assert diff.max().item() <= 2.01 * cfg.lr
     assert (diff > 1e-3 * cfg.lr).float().mean().item() < 1e-3, "more than 0.1% of updates differ"
     assert moved.max().item() > 0.5 * cfg.lr
