@@ -57,6 +57,9 @@ def parse():
                     help="weak: batch per rank fixed (global batch batch*N); strong: global batch fixed (batch/N per rank)")
     ap.add_argument("--capacity", type=int, default=2_000_000)
     ap.add_argument("--threshold", type=int, default=50_000)
+    ap.add_argument("--fill", action="store_true",
+                    help="fill the whole replay (every transition slot written, frame ring wrapped to capacity) "
+                         "before timing: BASELINE config 5 with --capacity 10000000")
     ap.add_argument("--actions", type=int, default=18)
     ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
@@ -188,7 +191,7 @@ def main():
         eng.learner.copy_params_to(eng.actor_flat)
 
     t_fill = time.perf_counter()
-    eng.fill(args.threshold)
+    eng.fill(args.capacity + 8 * args.envs if args.fill else args.threshold)
     torch.cuda.synchronize(device)
     t_fill = time.perf_counter() - t_fill
     if not args.no_graphs:
@@ -261,6 +264,9 @@ def main():
             "learner_samples_per_sec": round(samples_per_s, 1),
             "vs_paper_19_batches_per_s": round(batches_per_s / PAPER_BATCHES_PER_S, 2),
             "replay_fill_seconds": round(t_fill, 3),
+            "replay_bytes_per_gpu": eng.replay.nbytes(),
+            "replay_live_transitions": int((eng.replay.leaf_sum > 0).sum().item()),
+            "replay_slots_written": int(eng.replay.filled.item()),
             "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
             "stream_probe": eng.stream_probe,
             "last_loss": round(stats["loss"], 6),

@@ -263,3 +263,44 @@ def test_sample_api_returns_the_sampled_transitions(cuda):
     assert torch.equal(s2, rp.frames[rp.s2_ids[il].long()].view(256, 4, 84, 84))
     assert torch.equal(r, rp.reward[il]) and torch.equal(d, rp.done[il])
     assert bool((w > 0).all()) and bool((w <= 1.0 + 1e-6).all())
+
+
+def test_frame_ring_outlives_transitions_across_wraps(cuda):
+    """SURVEY §5.7 / BASELINE config 5: the transition ring (slot = step*E + e mod C) and the
+    frame ring (slot = (step+1)*E + e mod F, F = C + (2n+8)E) both advance E slots per actor
+    step, so a transition is always overwritten before any of its 8 frames.  After many wraps
+    of both rings, every live transition (sampling mass > 0) must reference only frames
+    written within the n-step window of the step that emitted it (a frame overwritten later
+    would carry a much newer write step)."""
+    from apex_amd.engine.apex import ApexEngine, EngineConfig
+    from apex_amd.engine.learner import LearnerConfig
+
+    E, C = 64, 16 * 64
+    cfg = EngineConfig(n_envs=E, replay_capacity=C, threshold_size=C, use_graphs=False,
+                       learner=LearnerConfig(batch_size=32, forward="hip"))
+    eng = ApexEngine(cfg, cuda)
+    rp, act = eng.replay, eng.actor
+    F, n = rp.frame_capacity, cfg.learner.n_step
+    assert F == C + (2 * n + 8) * E
+    last_write = torch.full((F,), -10**9, dtype=torch.int64)
+    last_write[:E] = -1  # reset frames (step 0 initial observations)
+    emit_step = torch.full((C,), -1, dtype=torch.int64)
+    steps = 12 * (F // E)  # ~12 wraps of the frame ring, ~13 of the transition ring
+    for _ in range(steps):
+        t = int(act.step_counter.item())
+        eng.actor_step()
+        torch.cuda.synchronize()
+        last_write[act.new_frame.long().cpu()] = t
+        emitted = act.prio.cpu() > 0
+        slots = act.slot.long().cpu()
+        emit_step[slots[emitted]] = t
+        emit_step[slots[~emitted]] = -1  # slot reused without a transition: no mass
+    live = (rp.leaf_sum.cpu() > 0).nonzero().flatten()
+    assert live.numel() > C // 2
+    ids = torch.cat([rp.s_ids.cpu()[live], rp.s2_ids.cpu()[live]], 1).long()  # [L, 8]
+    w = last_write[ids]
+    te = emit_step[live].unsqueeze(1)
+    assert bool((te >= 0).all()), "live slot without a recorded emission"
+    # every frame of a live transition was last written in [t_emit - n - 4, t_emit]
+    assert bool((w <= te).all()), "a live transition references a frame overwritten after its emission"
+    assert bool((w >= te - n - 4).all())
