@@ -1,29 +1,44 @@
-"""Central-replay Ape-X topology across GPUs (BASELINE config 3).
+"""Central-replay Ape-X topology across GPUs, asynchronous and fault tolerant
+(BASELINE config 3).
 
 Rank 0 is the learner and holds the one HBM replay (frame ring + transition table +
 priority tree), split into one region per actor rank.  Ranks 1..W-1 are actor GPUs:
-each runs an :class:`ActorShard` (E GPU envs, batched MFMA inference with the global
-Ape-X epsilon ladder, on-device n-step) writing into a *local mirror* of its region,
-and after every actor step pushes the step's E new frames + E transition rows to rank 0
-(``parallel.experience``: 2 point-to-point messages, RCCL over xGMI).  Rank 0 scatters
-them into the region and writes their priorities into the tree; the learner samples
-the union.  Every ``publish_param_interval`` learner steps rank 0 broadcasts its flat
-parameters to all actor ranks (RCCL broadcast, ``parallel.broadcast``).
+each runs an :class:`ActorShard` (E GPU envs, batched inference with the global Ape-X
+epsilon ladder, on-device n-step) writing into a *local mirror* of its region, and pushes
+every actor step (E new frames + E transition rows) to rank 0 over its own link
+(``parallel.experience``; RCCL over xGMI with ``nccl``, host-staged with ``gloo``).
 
-The step is lock-step (``actor_steps_per_learner_step`` pushes per learner step), so the
-message order on every link is fixed and no host polling is needed.  This is the
-reference's replay-server topology (actor.py -> replay.py <- learner.py) with ZMQ +
-pickle replaced by device-to-device messages; the data-parallel *sharded* topology
-(``ApexEngine`` with ``sharded=True``) is the other multi-GPU layout.
+Nothing is lock-step (the reference decouples its roles the same way: actor.py pushes with
+3 outstanding, replay.py ingests with 16 workers, learner.py prefetches):
+
+* actor rank: act (hipGraph) -> copy the packet into a free slot of its send ring (credit
+  window of ``depth`` = 3 packets in flight, actor.py:105-115) -> isend; between steps it
+  polls its parameter subscription (conflated + versioned, actor.py:40-49) and posts a
+  heartbeat to the TCPStore;
+* rank 0: learner step (hipGraph) -> poll every live link's pre-posted receives without
+  blocking -> ONE batched scatter of all landed packets into their regions + one tree
+  write (``apply_packets``) on the learner stream -> re-post; every
+  ``publish_param_interval`` steps a new parameter version to every link whose previous
+  one was delivered.  The learner never waits for an actor: a slow actor only lowers the
+  experience rate, a dead one (receive error or a heartbeat that stopped for
+  ``dead_after`` s) is dropped and the learner keeps stepping on the rest
+  (learner.py:57-68: PUB/SUB drops slow subscribers).
+* :meth:`close` ends the run with a bounded handshake (stop on the parameter channel,
+  packet counts through the store, filler packets) so no send or receive is left posted.
+
+``APEX_FAULT=actor<r>:kill@<step>`` hard-kills actor rank r at that actor step (tests).
 """
 from __future__ import annotations
 
+import time
 import torch
 import torch.distributed as dist
 
 from ..models.dqn import DuelingDQN
 from ..models.fused import make_hip_net, make_workspace
-from ..parallel.experience import ExperienceReceiver, ExperienceSender, Region, apply_packet, pack_meta
+from ..parallel.experience import (META_COLS, STOP, ActorLink, LearnerLinks, Region, apply_packets, link_groups,
+                                   pack_meta)
+from ..roles.common import maybe_fault
 from .actor_shard import ActorShard
 from .apex import EngineConfig
 from .hbm_replay import FRAME_BYTES, HBMReplay
@@ -39,7 +54,8 @@ def region_geometry(cfg: EngineConfig, n_actor_ranks: int) -> tuple[int, int]:
 
 
 class CentralApexEngine:
-    def __init__(self, cfg: EngineConfig, device, rank: int | None = None, world: int | None = None):
+    def __init__(self, cfg: EngineConfig, device, rank: int | None = None, world: int | None = None,
+                 depth: int = 3, dead_after: float = 30.0, heartbeat_every: int = 50, paced: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.rank = dist.get_rank() if rank is None else rank
@@ -47,6 +63,7 @@ class CentralApexEngine:
         if self.world < 2:
             raise ValueError("the central topology needs >= 2 ranks (rank 0 learner, ranks 1.. actors)")
         self.R = self.world - 1
+        self.depth = int(depth)
         lc = cfg.learner
         E = cfg.n_envs
         self.E = E
@@ -54,10 +71,15 @@ class CentralApexEngine:
         torch.manual_seed(cfg.seed)
         model = DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions)
         self.is_learner = self.rank == 0
-        self.via_host = dist.get_backend() != "nccl"
         self.learn_steps = self.actor_steps = 0
-        self.rounds = 0  # lock-step rounds (identical on every rank: drives the broadcast cadence)
         self._g_actor = self._g_learn = None
+        self.groups = link_groups(self.world)  # collective: every rank creates every link group
+        self.store = dist.distributed_c10d._get_default_store()
+        self.heartbeat_every = int(heartbeat_every)
+        # paced: each learner step consumes at most actor_steps_per_learner_step packets per link,
+        # so the 3-packet credit window holds every actor at that rate (the single-GPU engine's
+        # ratio); unpaced: actors run free and rank 0 ingests everything that landed
+        self.ingest_cap = cfg.actor_steps_per_learner_step if paced else None
         if self.is_learner:
             self.replay = HBMReplay(self.C_r * self.R, E, lc.n_step, cfg.alpha, self.device,
                                     frame_capacity=self.F_r * self.R, exact_mass=cfg.exact_mass, seed=cfg.seed)
@@ -65,7 +87,6 @@ class CentralApexEngine:
             self.flat = self.learner.flat
             self.regions = {r: Region((r - 1) * self.C_r, self.C_r, (r - 1) * self.F_r, self.F_r)
                             for r in range(1, self.world)}
-            self.receiver = ExperienceReceiver(E, FRAME_BYTES, self.device, range(1, self.world))
             rp = self.replay
             self.tables = {"frames": rp.frames, "s_ids": rp.s_ids, "s2_ids": rp.s2_ids, "action": rp.action,
                            "reward": rp.reward, "done": rp.done}
@@ -82,19 +103,16 @@ class CentralApexEngine:
             self.model = model
             self.net = make_hip_net(model, cfg.learner.dtype)
             self.ws = make_workspace(E, cfg.n_actions, self.device, cfg.learner.dtype)
-            self.sender = ExperienceSender(E, FRAME_BYTES, self.device, dst=0)
-            self.pkt_frames = torch.empty(E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
-        self.broadcast_params()
-        if not self.is_learner:  # the reset frames are the first packet
-            self._stage_packet(initial=True)
-            self.sender.send(self.pkt_frames, self.sender.meta)
+        self._initial_params()
+        if self.is_learner:
+            self._setup_learner_links(dead_after)
         else:
-            self._ingest()
+            self._setup_actor_link()
 
-    # ------------------------------------------------------------------ params
-    def broadcast_params(self) -> None:
-        """Rank 0 -> all actor ranks (RCCL broadcast of the 3.5 MB flat buffer)."""
-        if self.via_host:
+    # ------------------------------------------------------------------ setup
+    def _initial_params(self) -> None:
+        """Identical weights everywhere before the links start (one collective broadcast)."""
+        if dist.get_backend() != "nccl":
             h = self.flat.cpu()
             dist.broadcast(h, src=0)
             if not self.is_learner:
@@ -104,18 +122,55 @@ class CentralApexEngine:
         if not self.is_learner:
             self.net.repack()
 
+    def _setup_learner_links(self, dead_after: float) -> None:
+        R, D, E, dev = self.R, self.depth, self.E, self.device
+        self.rx_frames = torch.empty(R, D, E, FRAME_BYTES, dtype=torch.uint8, device=dev)
+        self.rx_meta = torch.empty(R, D, E, META_COLS, dtype=torch.int32, device=dev)
+        # per receive slot (link r, ring slot k): the region's frame / transition-slot base
+        fb = [self.regions[r].frame_base for r in range(1, self.world) for _ in range(D)]
+        sb = [self.regions[r].slot_base for r in range(1, self.world) for _ in range(D)]
+        self._fbase = torch.tensor(fb, dtype=torch.int64, device=dev)
+        self._sbase = torch.tensor(sb, dtype=torch.int64, device=dev)
+        self.links = LearnerLinks(self.world, self.groups, self.store, self.flat, self.rx_frames, self.rx_meta,
+                                  self._apply, dead_after)
+
+    def _setup_actor_link(self) -> None:
+        self.link = ActorLink(self.rank, self.groups[self.rank], self.store, self.flat, self.E, FRAME_BYTES,
+                              self.depth, self.heartbeat_every)
+        self.pkt_frames = torch.empty(self.E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
+        self.pkt_meta = torch.empty(self.E, META_COLS, dtype=torch.int32, device=self.device)
+        self.param_version = 0
+        self._stage_packet(initial=True)  # the reset frames are the first packet
+        self.link.push(self.pkt_frames, self.pkt_meta)
+
+    @property
+    def stopped(self) -> bool:
+        return self.link.stopped
+
+    @property
+    def live(self) -> set:
+        return self.links.live
+
+    @property
+    def dropped(self) -> dict:
+        return self.links.dropped
+
+    @property
+    def applied(self) -> dict:
+        return self.links.applied
+
     # ------------------------------------------------------------------ actor ranks
     def _stage_packet(self, initial: bool = False) -> None:
         a, rp = self.actor, self.replay
         if initial:  # reset frames only: no transition rows (priority 0)
             z = torch.zeros(self.E, dtype=torch.float32, device=self.device)
             slot = torch.arange(self.E, dtype=torch.int32, device=self.device)
-            pack_meta(a.st["hist"], a.st["hist"], a.actions, z, z, z, slot, a.new_frame, out=self.sender.meta)
+            pack_meta(a.st["hist"], a.st["hist"], a.actions, z, z, z, slot, a.new_frame, out=self.pkt_meta)
         else:
             sl = a.slot.long()
             pack_meta(rp.s_ids.index_select(0, sl), rp.s2_ids.index_select(0, sl), rp.action.index_select(0, sl),
                       rp.reward.index_select(0, sl), rp.done.index_select(0, sl), a.prio, a.slot, a.new_frame,
-                      out=self.sender.meta)
+                      out=self.pkt_meta)
         torch.index_select(rp.frames, 0, a.new_frame.long(), out=self.pkt_frames)
 
     def _actor_body(self) -> None:
@@ -123,25 +178,45 @@ class CentralApexEngine:
         self.actor.act_and_step(q)
         self._stage_packet()
 
-    def actor_step(self) -> None:
-        self.sender.wait()  # the previous packet left the staging buffers
+    def actor_step(self) -> bool:
+        """One actor step + push; False once the learner has stopped this actor."""
+        if self.link.stopped:
+            return False
+        v = self.link.poll_params()
+        if v == STOP:
+            return False
+        if v is not None:
+            self.net.repack()
+            self.param_version = v
+        maybe_fault("actor", self.rank, self.actor_steps)
         if self._g_actor is not None:
             self._g_actor.replay()
         else:
             self._actor_body()
-        self.sender.send(self.pkt_frames, self.sender.meta)
+        self.link.push(self.pkt_frames, self.pkt_meta)  # credit window: blocks only with 3 unconsumed
         self.actor_steps += 1
+        return True
 
     # ------------------------------------------------------------------ learner rank
-    def _ingest(self) -> None:
-        self.receiver.post()
-        slots, prios = [], []
-        for r, (frames, meta) in self.receiver.take(self.device).items():
-            sl, pr = apply_packet(self.tables, self.regions[r], frames, meta)
-            slots.append(sl)
-            prios.append(pr)
-        self.replay.write_priorities(torch.cat(slots), torch.cat(prios), dedup=False,
-                                     bumps=((self.replay.filled, self.E * self.R),))
+    def _apply(self, ready: list[tuple[int, int]]) -> None:
+        """ONE batched scatter of every landed packet into its region + one tree write,
+        on the learner stream (between learner steps)."""
+        sel = torch.tensor([(r - 1) * self.depth + k for r, k in ready], dtype=torch.int64).pin_memory()
+        idx = sel.to(self.device, non_blocking=True)
+        D, E = self.depth, self.E
+        frames = self.rx_frames.view(self.R * D, E, FRAME_BYTES).index_select(0, idx)
+        meta = self.rx_meta.view(self.R * D, E, META_COLS).index_select(0, idx)
+        slots, prio = apply_packets(self.tables, frames, meta, self._fbase.index_select(0, idx),
+                                    self._sbase.index_select(0, idx))
+        self.replay.write_priorities(slots, prio, dedup=False, bumps=((self.replay.filled, len(ready) * E),))
+
+    def ingest(self, cap: int | None = None) -> int:
+        return self.links.ingest(cap)
+
+    def publish_params(self) -> None:
+        """Conflated, versioned publish to every live actor link (rank 0)."""
+        if self.is_learner:
+            self.links.publish(self.flat)
 
     def learner_step(self) -> None:
         if self._g_learn is not None:
@@ -152,66 +227,63 @@ class CentralApexEngine:
         if self.learn_steps % self.cfg.target_update_interval == 0:
             self.learner.sync_target()
 
-    # ------------------------------------------------------------------ lock-step driver
-    def fill_steps(self) -> int:
-        return max(4, -(-self.cfg.threshold_size // (self.E * self.R)))
-
-    def fill(self) -> None:
-        for _ in range(self.fill_steps()):
-            if self.is_learner:
-                self._ingest()
-            else:
-                self.actor_step()
-
-    def _round_eager(self) -> None:
-        if self.is_learner:
-            self.learner.step()
-            self.learn_steps += 1
-            for _ in range(self.cfg.actor_steps_per_learner_step):
-                self._ingest()
-        else:
-            for _ in range(self.cfg.actor_steps_per_learner_step):
-                self.actor_step()
-
-    def capture(self, warmup_rounds: int = 3) -> None:
-        """Warm up with real lock-step rounds (messages included, so every link keeps
-        its per-round message count), then capture the compute-only bodies; the
-        messages stay eager around the graph replays."""
-        s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            for _ in range(warmup_rounds):
-                self._round_eager()
-        torch.cuda.current_stream(self.device).wait_stream(s)
+    def close(self, timeout: float = 60.0) -> dict:
+        """Stop every live actor and drain its link (bounded).  Returns link stats."""
+        if not self.is_learner:
+            return {}
+        st = self.links.close(timeout)
         torch.cuda.synchronize(self.device)
+        return st
+
+    # ------------------------------------------------------------------ driver
+    def fill(self, timeout: float = 600.0) -> None:
+        """Rank 0: ingest until ``threshold_size`` transitions landed (bounded); actor
+        ranks start acting in :meth:`train_step`."""
+        if not self.is_learner:
+            return
+        need = -(-self.cfg.threshold_size // self.E)
+        deadline = time.monotonic() + timeout
+        while sum(self.applied.values()) < need + len(self.live):
+            if not self.live or time.monotonic() > deadline:
+                raise RuntimeError(f"central fill: {sum(self.applied.values())} packets after {timeout}s, "
+                                   f"live actors {sorted(self.live)}")
+            if not self.ingest():
+                time.sleep(0.0005)
+            self.links.check_heartbeats()
+
+    def capture(self) -> None:
+        """hipGraphs of the compute bodies (the links stay eager around them)."""
         pool = torch.cuda.graph_pool_handle()
         if self.is_learner:
+            self.learner.step()  # eager warm-up (a real step)
+            self.learn_steps += 1
+            torch.cuda.synchronize(self.device)
             self._g_learn = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_learn, pool=pool, capture_error_mode="thread_local"):
                 self.learner.step()
         else:
-            self.sender.wait()
+            if not self.actor_step():  # eager warm-up (a real, pushed step)
+                return
+            torch.cuda.synchronize(self.device)
             self._g_actor = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_actor, pool=pool, capture_error_mode="thread_local"):
                 self._actor_body()
         torch.cuda.synchronize(self.device)
 
-    def train_step(self) -> None:
-        """One lock-step round: rank 0 = 1 learner step + ingest of every actor rank's
-        pushes; actor ranks = ``actor_steps_per_learner_step`` actor steps + pushes."""
-        k = self.cfg.actor_steps_per_learner_step
-        if self.is_learner:
-            self.learner_step()
-            for _ in range(k):
-                self._ingest()
-        else:
-            for _ in range(k):
-                self.actor_step()
-        self.rounds += 1
-        if self.rounds % self.cfg.publish_param_interval == 0:
-            if not self.is_learner:
-                self.sender.wait()
-            self.broadcast_params()
+    def train_step(self) -> bool:
+        """Rank 0: one learner step + ingest (+ publish / heartbeat checks).  Actor ranks:
+        ``actor_steps_per_learner_step`` actor steps.  False once this rank is done."""
+        if not self.is_learner:
+            for _ in range(self.cfg.actor_steps_per_learner_step):
+                if not self.actor_step():
+                    return False
+            return True
+        self.learner_step()
+        self.ingest(self.ingest_cap)
+        if self.learn_steps % self.cfg.publish_param_interval == 0:
+            self.publish_params()
+        self.links.check_heartbeats()
+        return True
 
     @property
     def frames_per_actor_step(self) -> int:

@@ -1,28 +1,49 @@
-"""Actor -> replay experience push for the central-replay topology.
+"""Asynchronous actor -> learner experience links for the central-replay topology
+(reference actor.py:40-49,105-115, replay.py:77-146,
+learner.py:57-68).
 
-Central topology: rank 0 owns the single HBM replay and the learner; ranks 1..W-1 run
-GPU actor shards only.  Each remote rank's actor writes into a *local mirror* of its
-region of the rank-0 replay (same frame-ring and transition-slot geometry), so one
-actor step produces, at positions the shard itself reports:
+Rank 0 owns the single HBM replay and the learner; ranks 1..W-1 run GPU actor shards.
+Each actor rank writes into a *local mirror* of its region of the rank-0 replay (same
+frame-ring and transition-slot geometry), so one actor step produces, at positions the
+shard itself reports, E new frames and E transition rows (priority 0 = no row).  A
+*packet* is one actor step: frames ``[E, frame_bytes]`` u8 + metadata ``[E, 14]`` i32.
 
-* E new frames (one per env, local frame slots in ``ActorShard.new_frame``), and
-* E transition rows (local slots in ``ActorShard.slot``; priority 0 = no row emitted).
+Transport (one torch.distributed P2P group per actor link, so a slow or dead link never
+blocks another: with ``nccl`` each link has its own RCCL communicator / stream over xGMI,
+with ``gloo`` packets are staged through pinned host memory):
 
-Per actor step the remote rank gathers them on device (inside its captured actor graph)
-and sends one frame tensor ``[E, frame_bytes]`` u8 and one metadata tensor ``[E, 14]``
-int32 -- point-to-point over RCCL/xGMI with the ``nccl`` backend (a 1.8 MB message per
-256-env step), or staged through host memory with ``gloo``.  Rank 0 scatters them into
-region r (frame ids re-based by the region's frame offset) and writes the priorities
-into the tree.  Reference equivalent: actor pickles 50
-transitions and pushes them over ZeroMQ to the replay process (actor.py:105-115,
-replay.py:77-107).
+* :class:`PacketSender` (actor): a ring of ``depth`` packet slots; at most ``depth``
+  packets in flight -- the reference's credit window (actor.py:105-115 keeps 3 pushes
+  outstanding).  Acquiring a slot waits (bounded) for its previous send.
+* :class:`PacketInbox` (rank 0): ``depth`` receives always pre-posted; :meth:`poll` hands
+  back the packets that have landed, in send order, without blocking; a failed receive
+  (peer gone) marks the link dead.
+* :func:`apply_packets`: every ready packet of every link scattered into its region and
+  written into the priority tree as ONE batch of device ops between learner steps (no
+  per-round host ``take()``, no lock-step).
+* :class:`ParamLink` / :class:`ParamSubscriber`: conflated, versioned parameter publish
+  (reference PUB/SUB with CONFLATE, actor.py:40-49): rank 0 sends the newest snapshot to
+  a link only when that link's previous snapshot has been delivered; version -1 = stop.
+* :class:`Heartbeats`: actors post their packet count in the TCPStore; rank 0 drops a
+  link whose count has not moved for ``dead_after`` seconds.
+
+Shutdown handshake (bounded, see ``CentralApexEngine.close``): rank 0 sends stop on the
+param channel; the actor publishes its packet count; rank 0 publishes how many packets
+it has receives posted for; the actor pads with dummy packets (slot -1) until the two
+match, so no receive or send is left dangling.
 """
 from __future__ import annotations
+
+import queue
+import threading
+import time
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
 
 META_COLS = 14
+STOP = -1
 
 
 def pack_meta(s_ids, s2_ids, action, reward, done, prio, slot, fslot, out: torch.Tensor | None = None):
@@ -65,54 +86,497 @@ def apply_packet(tables: dict, region: Region, frames: torch.Tensor, meta: torch
     return slot.to(torch.int32), meta[:, 11].contiguous().view(torch.float32)
 
 
-class _P2P:
-    def __init__(self, device: torch.device, group=None):
-        self.group = group
-        backend = dist.get_backend(group)
-        self.via_host = device.type == "cuda" and backend != "nccl"  # gloo: stage through host memory
-        self.works: list = []
+def apply_packets(tables: dict, frames: torch.Tensor, meta: torch.Tensor, frame_base: torch.Tensor,
+                  slot_base: torch.Tensor):
+    """Batched :func:`apply_packet`: ``frames`` [n, E, FB], ``meta`` [n, E, 14] (n ready
+    packets, any links), ``frame_base`` / ``slot_base`` int64 [n] the packets' region
+    offsets.  One set of scatters for all packets; returns (slots int32, priorities)."""
+    n, E = meta.shape[0], meta.shape[1]
+    m = meta.reshape(n * E, META_COLS)
+    fb = frame_base.repeat_interleave(E)
+    sb = slot_base.repeat_interleave(E)
+    tables["frames"].index_copy_(0, m[:, 13].long() + fb, frames.reshape(n * E, -1))
+    slot = m[:, 12].long() + sb
+    ids = m[:, 0:8] + fb.to(torch.int32).unsqueeze(1)
+    tables["s_ids"].index_copy_(0, slot, ids[:, 0:4].contiguous())
+    tables["s2_ids"].index_copy_(0, slot, ids[:, 4:8].contiguous())
+    tables["action"].index_copy_(0, slot, m[:, 8].contiguous())
+    tables["reward"].index_copy_(0, slot, m[:, 9].contiguous().view(torch.float32))
+    tables["done"].index_copy_(0, slot, m[:, 10].contiguous().view(torch.float32))
+    return slot.to(torch.int32), m[:, 11].contiguous().view(torch.float32)
 
-    def wait(self):
-        for w in self.works:
-            w.wait()
-        self.works = []
+
+def _via_host(device: torch.device, group) -> bool:
+    return device.type == "cuda" and dist.get_backend(group) != "nccl"
 
 
-class ExperienceSender(_P2P):
-    def __init__(self, E: int, frame_bytes: int, device, dst: int = 0, group=None):
-        super().__init__(torch.device(device), group)
-        self.dst = dst
-        self.meta = torch.empty(E, META_COLS, dtype=torch.int32, device=device)
+class _Pending:
+    __slots__ = ("works", "event", "error")
+
+    def __init__(self, works):
+        self.works, self.event, self.error = works, threading.Event(), None
+
+
+class WorkTracker:
+    """Completion of torch.distributed P2P works without blocking the caller.  RCCL/NCCL
+    works report ``is_completed()`` (event query).  Gloo P2P works only complete inside
+    ``wait()``, so a daemon thread per channel waits on them in posting order (the GIL is
+    released while it blocks) and flags each batch; a failed wait (peer gone) is recorded
+    and re-raised by :meth:`done`."""
+
+    def __init__(self, group):
+        self.native = dist.get_backend(group) == "nccl"
+        self.q: queue.Queue | None = None
+
+    def add(self, works) -> _Pending:
+        p = _Pending(works)
+        if not self.native:
+            self._queue().put(p)
+        return p
+
+    def add_deferred(self, event, issue) -> _Pending:
+        """Gloo only: the tracker thread waits for ``event`` (e.g. the D2H copy that filled
+        the send buffer), then calls ``issue()`` for the works and waits for them."""
+        assert not self.native
+        p = _Pending((event, issue))
+        self._queue().put(p)
+        return p
+
+    def _queue(self) -> queue.Queue:
+        if self.q is None:
+            self.q = queue.Queue()
+            threading.Thread(target=self._run, args=(self.q,), daemon=True).start()
+        return self.q
+
+    @staticmethod
+    def _run(q):
+        while True:
+            p = q.get()
+            try:
+                if isinstance(p.works, tuple):  # deferred issue
+                    ev, issue = p.works
+                    ev.synchronize()
+                    p.works = issue()
+                for w in p.works:
+                    w.wait()
+            except Exception as e:  # recorded for the poller
+                p.error = e
+            finally:
+                p.event.set()
+
+    def done(self, p: _Pending | None) -> bool:
+        if p is None:
+            return True
+        if self.native:
+            return all(w.is_completed() for w in p.works)
+        if p.error is not None:
+            raise p.error
+        return p.event.is_set()
+
+    def wait(self, p: _Pending | None, timeout: float) -> bool:
+        """Bounded wait: True when completed (an error raises)."""
+        deadline = time.monotonic() + timeout
+        while not self.done(p):
+            if time.monotonic() > deadline:
+                return False
+            time.sleep(0.0002)
+        if p is not None and self.native:
+            for w in p.works:
+                w.wait()  # orders the caller's stream after the transfer (no host block)
+        return True
+
+
+def link_groups(world: int) -> dict:
+    """One P2P group per actor link {r: group([0, r])}; collective: every rank calls it."""
+    return {r: dist.new_group([0, r]) for r in range(1, world)}
+
+
+class PacketSender:
+    """Actor end of a link: ``depth`` packet slots, at most ``depth`` in flight."""
+
+    def __init__(self, E: int, frame_bytes: int, device, group, dst: int = 0, depth: int = 3):
+        self.device = torch.device(device)
+        self.group, self.dst, self.depth = group, dst, int(depth)
+        self.via_host = _via_host(self.device, group)
+        dev = "cpu" if self.via_host else self.device
+        pin = self.via_host and torch.cuda.is_available()
+        mk = lambda *s, dt: (torch.empty(*s, dtype=dt).pin_memory() if pin else  # noqa: E731
+                             torch.empty(*s, dtype=dt, device=dev))
+        self.frames = [mk(E, frame_bytes, dt=torch.uint8) for _ in range(depth)]
+        self.meta = [mk(E, META_COLS, dt=torch.int32) for _ in range(depth)]
+        self.works: list = [None] * depth
+        self.track = WorkTracker(group)
+        self.k = 0
+        self.n_sent = 0
+
+    def acquire(self, timeout: float = 60.0):
+        """(frames, meta) buffers of the next slot, once its previous send has left
+        (credit window).  Raises TimeoutError if the learner stopped draining."""
+        if not self.track.wait(self.works[self.k], timeout):
+            raise TimeoutError(f"experience link to rank {self.dst}: no credit for {timeout}s")
+        self.works[self.k] = None
+        return self.frames[self.k], self.meta[self.k]
+
+    def send(self) -> None:
+        k = self.k
+        if self.via_host and torch.cuda.is_available():
+            # host-staged (gloo): the slot was filled by a D2H copy on the caller's stream; the
+            # tracker thread waits for that copy's event before handing the slot to gloo, so
+            # the actor's host thread never blocks on its own GPU work
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self.works[k] = self.track.add_deferred(ev, lambda k=k: [
+                dist.isend(self.frames[k], self.dst, group=self.group),
+                dist.isend(self.meta[k], self.dst, group=self.group)])
+        else:
+            self.works[k] = self.track.add([dist.isend(self.frames[k], self.dst, group=self.group),
+                                            dist.isend(self.meta[k], self.dst, group=self.group)])
+        self.k = (k + 1) % self.depth
+        self.n_sent += 1
+
+    def send_dummy(self, timeout: float = 60.0) -> None:
+        """A filler packet (slot -1): matches one receive the learner has posted."""
+        _, meta = self.acquire(timeout)
+        meta.fill_(-1)
+        self.send()
+
+    def drain(self, timeout: float = 60.0) -> bool:
+        ok = True
+        for i in range(self.depth):
+            ok = self.track.wait(self.works[i], timeout) and ok
+            self.works[i] = None
+        return ok
+
+
+class PacketInbox:
+    """Learner end of a link: ``depth`` receives pre-posted into ``frames`` / ``meta``
+    ([depth, E, ...]); packets complete in send order."""
+
+    def __init__(self, src: int, frames: torch.Tensor, meta: torch.Tensor, group, device):
+        self.src, self.group = src, group
+        self.device = torch.device(device)
+        self.via_host = _via_host(self.device, group)
+        self.depth = frames.shape[0]
+        self.dev_frames, self.dev_meta = frames, meta  # device views (the batched apply reads these)
         if self.via_host:
-            self.h_frames = torch.empty(E, frame_bytes, dtype=torch.uint8).pin_memory() \
-                if torch.cuda.is_available() else torch.empty(E, frame_bytes, dtype=torch.uint8)
-            self.h_meta = torch.empty(E, META_COLS, dtype=torch.int32)
+            # 2*depth pinned host buffers, rotated per packet: a packet's H2D copy is issued
+            # non-blocking on the learner stream and its buffer is re-armed only once that copy's
+            # event has completed (two packets later), so the host never waits on the GPU
+            pin = torch.cuda.is_available()
+            nb = 2 * self.depth
+            mk = lambda t: torch.empty((nb,) + tuple(t.shape[1:]), dtype=t.dtype)  # noqa: E731
+            self.frames, self.meta = mk(frames), mk(meta)
+            if pin:
+                self.frames, self.meta = self.frames.pin_memory(), self.meta.pin_memory()
+            self.h_event = [None] * nb
+        else:
+            self.frames, self.meta = frames, meta
+        self.works: list = [None] * self.depth
+        self.hslot = [0] * self.depth  # host buffer of the receive posted into device slot k
+        self.track = WorkTracker(group)
+        self.n_posted = self.n_done = 0
+        self.dead = False
+        self.error: str | None = None
 
-    def send(self, frames: torch.Tensor, meta: torch.Tensor) -> None:
-        self.wait()  # one packet in flight: the staging buffers are reused
+    def _post(self, k: int) -> None:
         if self.via_host:
-            self.h_frames.copy_(frames)
-            self.h_meta.copy_(meta)
-            frames, meta = self.h_frames, self.h_meta
-        self.works = [dist.isend(frames.contiguous(), self.dst, group=self.group),
-                      dist.isend(meta.contiguous(), self.dst, group=self.group)]
+            hb = self.n_posted % (2 * self.depth)
+            if self.h_event[hb] is not None:
+                self.h_event[hb].synchronize()  # (normally long done) the buffer's last H2D copy
+                self.h_event[hb] = None
+            self.hslot[k] = hb
+            src_f, src_m = self.frames[hb], self.meta[hb]
+        else:
+            src_f, src_m = self.frames[k], self.meta[k]
+        self.works[k] = self.track.add([dist.irecv(src_f, self.src, group=self.group),
+                                        dist.irecv(src_m, self.src, group=self.group)])
+        self.n_posted += 1
+
+    def start(self) -> None:
+        for k in range(self.depth):
+            self._post(k)
+
+    def poll(self, limit: int | None = None) -> list[int]:
+        """Slots whose packets have landed, oldest first (non-blocking; stops at the first
+        incomplete receive, so order is preserved)."""
+        out = []
+        if self.dead:
+            return out
+        k = self.n_done % self.depth
+        while self.works[k] is not None and (limit is None or len(out) < limit):
+            try:
+                if not self.track.done(self.works[k]):
+                    break
+                if self.track.native:
+                    for w in self.works[k].works:
+                        w.wait()  # the current stream is ordered after the receive
+            except Exception as e:  # the peer is gone (connection closed / comm error)
+                self.dead, self.error = True, repr(e)
+                break
+            self.works[k] = None
+            if self.via_host:  # pinned host packet -> device slot, async on the caller's stream
+                hb = self.hslot[k]
+                self.dev_frames[k].copy_(self.frames[hb], non_blocking=True)
+                self.dev_meta[k].copy_(self.meta[hb], non_blocking=True)
+                if torch.cuda.is_available() and self.dev_frames.is_cuda:
+                    ev = torch.cuda.Event()
+                    ev.record(torch.cuda.current_stream(self.dev_frames.device))
+                    self.h_event[hb] = ev
+            out.append(k)
+            self.n_done += 1
+            k = self.n_done % self.depth
+        return out
+
+    def repost(self, k: int, limit: int | None = None) -> None:
+        """Re-arm slot ``k`` (after its packet was applied) unless ``limit`` receives
+        have been posted in total."""
+        if not self.dead and (limit is None or self.n_posted < limit):
+            self._post(k)
 
 
-class ExperienceReceiver(_P2P):
-    def __init__(self, E: int, frame_bytes: int, device, sources, group=None):
-        super().__init__(torch.device(device), group)
-        self.sources = list(sources)
-        dev = device if not self.via_host else "cpu"
-        self.frames = {r: torch.empty(E, frame_bytes, dtype=torch.uint8, device=dev) for r in self.sources}
-        self.meta = {r: torch.empty(E, META_COLS, dtype=torch.int32, device=dev) for r in self.sources}
+class ParamLink:
+    """Rank-0 end of a link's parameter channel: conflated, versioned snapshots."""
 
-    def post(self) -> None:
-        for r in self.sources:
-            self.works.append(dist.irecv(self.frames[r], r, group=self.group))
-            self.works.append(dist.irecv(self.meta[r], r, group=self.group))
+    def __init__(self, flat: torch.Tensor, dst: int, group):
+        self.dst, self.group = dst, group
+        self.via_host = _via_host(flat.device, group)
+        pin = self.via_host and torch.cuda.is_available()
+        self.snap = torch.empty(flat.numel(), dtype=flat.dtype).pin_memory() if pin else \
+            torch.empty(flat.numel(), dtype=flat.dtype, device="cpu" if self.via_host else flat.device)
+        self.ver = torch.zeros(1, dtype=torch.int64, device="cpu" if self.via_host else flat.device)
+        self.works = None
+        self.track = WorkTracker(group)
+        self.version = -2  # last version handed to the transport
+        self.skipped = 0
 
-    def take(self, device):
-        """Wait for the posted packets; returns {rank: (frames, meta)} on ``device``."""
-        self.wait()
-        return {r: (self.frames[r].to(device, non_blocking=True), self.meta[r].to(device, non_blocking=True))
-                for r in self.sources}
+    def publish(self, flat: torch.Tensor, version: int) -> bool:
+        """Send ``flat`` as ``version`` if the previous snapshot was delivered (conflation:
+        a busy link just gets a newer version later).  True if sent."""
+        if not self.track.done(self.works):
+            self.skipped += 1
+            return False
+        self.snap.copy_(flat.reshape(-1), non_blocking=True)
+        self.ver.fill_(version)
+        if self.via_host and torch.cuda.is_available():  # gloo: send once the D2H snapshot landed
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(flat.device))
+            self.works = self.track.add_deferred(ev, lambda: [dist.isend(self.ver, self.dst, group=self.group),
+                                                              dist.isend(self.snap, self.dst, group=self.group)])
+        else:
+            self.works = self.track.add([dist.isend(self.ver, self.dst, group=self.group),
+                                         dist.isend(self.snap, self.dst, group=self.group)])
+        self.version = version
+        return True
+
+    def stop(self, timeout: float) -> bool:
+        if not self.track.wait(self.works, timeout):
+            return False
+        self.ver.fill_(STOP)
+        self.works = self.track.add([dist.isend(self.ver, self.dst, group=self.group),
+                                     dist.isend(self.snap, self.dst, group=self.group)])
+        return self.track.wait(self.works, timeout)
+
+
+class ParamSubscriber:
+    """Actor end of the parameter channel: one receive always posted into a staging
+    buffer; :meth:`poll` swaps the newest version into ``flat``."""
+
+    def __init__(self, flat: torch.Tensor, src: int, group):
+        self.flat, self.src, self.group = flat, src, group
+        self.via_host = _via_host(flat.device, group)
+        dev = "cpu" if self.via_host else flat.device
+        self.stage = torch.empty(flat.numel(), dtype=flat.dtype, device=dev)
+        self.ver = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.version = 0
+        self.works = None
+        self.track = WorkTracker(group)
+        self._post()
+
+    def _post(self) -> None:
+        self.works = self.track.add([dist.irecv(self.ver, self.src, group=self.group),
+                                     dist.irecv(self.stage, self.src, group=self.group)])
+
+    def poll(self):
+        """None (nothing new), STOP, or the version just installed."""
+        if self.works is None or not self.track.done(self.works):
+            return None
+        self.track.wait(self.works, 0.0)
+        v = int(self.ver.item())
+        if v == STOP:
+            self.works = None
+            return STOP
+        self.flat.copy_(self.stage.to(self.flat.device, non_blocking=False).view_as(self.flat))
+        self.version = v
+        self._post()
+        return v
+
+
+class Heartbeats:
+    """Liveness through the rendezvous TCPStore (off the data path): actors post their
+    packet count; rank 0 marks a link dead when it stops moving for ``dead_after`` s."""
+
+    def __init__(self, store, ranks, dead_after: float = 30.0, prefix: str = "apex/hb"):
+        self.store, self.prefix, self.dead_after = store, prefix, float(dead_after)
+        now = time.monotonic()
+        self.last = {r: (None, now) for r in ranks}
+
+    def beat(self, rank: int, count: int) -> None:
+        self.store.set(f"{self.prefix}/{rank}", str(count))
+
+    def stale(self, ranks) -> list[int]:
+        out, now = [], time.monotonic()
+        for r in ranks:
+            key = f"{self.prefix}/{r}"
+            v = self.store.get(key) if self.store.check([key]) else None  # check: non-blocking
+            prev, t = self.last[r]
+            if v != prev:
+                self.last[r] = (v, now)
+            elif now - t > self.dead_after:
+                out.append(r)
+        return out
+
+
+class LearnerLinks:
+    """Rank-0 side of every actor link: pre-posted packet receives, conflated parameter
+    publish, heartbeats, dropping dead links and the bounded stop handshake.  Landed
+    packets are handed to ``apply(ready)`` as ``[(rank, ring slot)]`` with their data in
+    ``frames[rank - 1, slot]`` / ``meta[rank - 1, slot]`` (device tensors)."""
+
+    def __init__(self, world: int, groups: dict, store, flat: torch.Tensor, frames: torch.Tensor,
+                 meta: torch.Tensor, apply, dead_after: float = 30.0, log=print):
+        self.store, self.apply_fn, self.log = store, apply, log
+        self.frames, self.meta = frames, meta
+        dev = frames.device
+        self.inbox = {r: PacketInbox(r, frames[r - 1], meta[r - 1], groups[r], dev) for r in range(1, world)}
+        for ib in self.inbox.values():
+            ib.start()
+        self.params = {r: ParamLink(flat, r, groups[r]) for r in range(1, world)}
+        self.hb = Heartbeats(store, range(1, world), dead_after)
+        self.live = set(range(1, world))
+        self.dropped: dict[int, str] = {}
+        self.applied = {r: 0 for r in range(1, world)}
+        self.version = 0
+        self._hb_t = time.monotonic()
+        self.closed = False
+
+    def drop(self, r: int, why: str) -> None:
+        if r in self.live:
+            self.live.discard(r)
+            self.dropped[r] = why
+            self.inbox[r].dead = True
+            if self.log:
+                self.log(f"[central] dropping actor rank {r}: {why}")
+
+    def ingest(self, cap: int | None = None) -> int:
+        """Apply the packets that have landed on the live links (at most ``cap`` per link:
+        with the senders' credit window this paces each actor at ``cap`` packets per call,
+        the reference's flow control); non-blocking."""
+        ready = []
+        for r in sorted(self.live):
+            ib = self.inbox[r]
+            ready += [(r, k) for k in ib.poll(limit=cap)]
+            if ib.dead:
+                self.drop(r, f"receive failed: {ib.error}")
+        if ready:
+            self.apply_fn(ready)
+            for r, k in ready:
+                self.applied[r] += 1
+                self.inbox[r].repost(k)
+        return len(ready)
+
+    def check_heartbeats(self, every: float = 1.0) -> None:
+        now = time.monotonic()
+        if now - self._hb_t < every:
+            return
+        self._hb_t = now
+        for r in self.hb.stale(sorted(self.live)):
+            self.drop(r, f"no heartbeat for {self.hb.dead_after:.0f}s")
+
+    def publish(self, flat: torch.Tensor) -> None:
+        self.version += 1
+        for r in sorted(self.live):
+            try:
+                self.params[r].publish(flat, self.version)
+            except Exception as e:
+                self.drop(r, f"param publish failed: {e!r}")
+
+    def close(self, timeout: float = 60.0) -> dict:
+        """Stop handshake with every live link (see the module docstring); bounded."""
+        if self.closed:
+            return self.stats()
+        self.closed = True
+        for r in sorted(self.live):
+            try:
+                if not self.params[r].stop(timeout):
+                    self.drop(r, "stop not delivered")
+            except Exception as e:
+                self.drop(r, f"stop failed: {e!r}")
+        for r in sorted(self.live):
+            ib = self.inbox[r]
+            try:
+                self.store.wait([f"apex/sent/{r}"], timedelta(seconds=timeout))
+                sent = int(self.store.get(f"apex/sent/{r}"))
+            except Exception as e:
+                self.drop(r, f"no packet count: {e!r}")
+                continue
+            need = max(ib.n_posted, sent)
+            self.store.set(f"apex/need/{r}", str(need))
+            deadline = time.monotonic() + timeout
+            while ib.n_done < need and not ib.dead and time.monotonic() < deadline:
+                ks = ib.poll()
+                real = [(r, k) for k in ks if int(self.meta[r - 1, k, 0, 12].item()) >= 0]  # fillers: slot -1
+                if real:
+                    self.apply_fn(real)
+                    self.applied[r] += len(real)
+                for k in ks:
+                    ib.repost(k, limit=need)
+                if not ks:
+                    time.sleep(0.0005)
+            if ib.n_done < need:
+                self.drop(r, "drain timed out")
+        return self.stats()
+
+    def stats(self) -> dict:
+        return {"applied": dict(self.applied), "dropped": dict(self.dropped), "live": sorted(self.live),
+                "params_skipped": {r: p.skipped for r, p in self.params.items()}}
+
+
+class ActorLink:
+    """Actor side of one link: packet send ring (credit window), parameter subscription,
+    heartbeat and the stop handshake."""
+
+    def __init__(self, rank: int, group, store, flat: torch.Tensor, E: int, frame_bytes: int, depth: int = 3,
+                 heartbeat_every: int = 50):
+        self.rank, self.store = rank, store
+        self.sender = PacketSender(E, frame_bytes, flat.device, group, dst=0, depth=depth)
+        self.sub = ParamSubscriber(flat, 0, group)
+        self.hb = Heartbeats(store, [])
+        self.heartbeat_every = int(heartbeat_every)
+        self.stopped = False
+        self.steps = 0
+
+    def poll_params(self):
+        """None / the newly installed version / STOP (after which the handshake has run)."""
+        v = self.sub.poll()
+        if v == STOP:
+            self.finish()
+        return v
+
+    def push(self, frames: torch.Tensor, meta: torch.Tensor, timeout: float = 120.0) -> None:
+        f, m = self.sender.acquire(timeout)
+        f.copy_(frames, non_blocking=True)  # host-staged: the send waits for this copy's event
+        m.copy_(meta, non_blocking=True)
+        self.sender.send()
+        self.steps += 1
+        if self.steps % self.heartbeat_every == 0:
+            self.hb.beat(self.rank, self.sender.n_sent)
+
+    def finish(self, timeout: float = 120.0) -> None:
+        r = self.rank
+        self.store.set(f"apex/sent/{r}", str(self.sender.n_sent))
+        self.store.wait([f"apex/need/{r}"], timedelta(seconds=timeout))
+        need = int(self.store.get(f"apex/need/{r}"))
+        while self.sender.n_sent < need:
+            self.sender.send_dummy(timeout)
+        self.sender.drain(timeout)
+        self.stopped = True

@@ -153,7 +153,7 @@ def main(argv=None) -> int:
         if args.resume and rank == 0:
             counters = load_engine(learner, args.resume)
         if args.resume:
-            eng.broadcast_params()
+            eng.publish_params()  # rank 0: a new parameter version on every link
         n_actor_gpus = world - 1
     else:
         from .parallel.dp import FlatGradAllReduce
@@ -236,11 +236,12 @@ def main(argv=None) -> int:
     t_last, step_last = time.perf_counter(), step
     eval_rets, eval_lens = [], []
     while not max_step or step < max_step:
-        eng.train_step()
+        if eng.train_step() is False:  # central actor rank: the learner stopped this link
+            break
         step = eng.learn_steps
         if evaluator is not None and step % max(1, args.eval_interval) == 0:
             eval_chunk()
-        if step % bps_every == 0:
+        if learner is not None and step % bps_every == 0:
             torch.cuda.synchronize(device)
             now = time.perf_counter()
             sps = (step - step_last) / (now - t_last)
@@ -283,7 +284,11 @@ def main(argv=None) -> int:
         save_engine(learner, args.save_path, {"learn_steps": step, "actor_steps": eng.actor_steps})
     if writer is not None:
         writer.close()
-    if world > 1:
+    if topology == "central":  # async links: bounded stop handshake instead of a barrier
+        if rank == 0:
+            print(f"links: {eng.close()}", flush=True)
+        dist.destroy_process_group()
+    elif world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -111,6 +111,9 @@ def parse():
                     help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
                          "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
+    ap.add_argument("--unpaced", action="store_true",
+                    help="central topology: actors run free (default: paced at --actor-steps packets per learner "
+                         "step per actor through the credit window)")
     return ap.parse_args()
 
 
@@ -345,9 +348,10 @@ def aql(args, rank, world, device):
 
 
 def central(args, rank, world, device):
-    """Central-replay topology: rank 0 = learner + the one replay, ranks 1.. = actor GPUs
-    pushing experience over RCCL.  ``value`` = learner SGD steps/s (one learner);
-    actor frames/s summed over the actor GPUs."""
+    """Central-replay topology, asynchronous: rank 0 = learner + the one replay, ranks 1.. =
+    actor GPUs pushing experience over their own links (credit window 3, conflated
+    params).  ``value`` = learner SGD steps/s (one learner, batch 512, strong scaling);
+    actor frames/s = frames that reached the replay during the timed window."""
     import torch
     import torch.distributed as dist
 
@@ -361,7 +365,15 @@ def central(args, rank, world, device):
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
-    eng = CentralApexEngine(cfg, device, rank, world)
+    eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced)
+    if rank != 0:  # actor GPU: act and push until the learner stops this link
+        if not args.no_graphs:
+            eng.capture()
+        while eng.train_step():
+            pass
+        torch.cuda.synchronize(device)
+        dist.destroy_process_group()
+        return
     t_fill = time.perf_counter()
     eng.fill()
     torch.cuda.synchronize(device)
@@ -371,35 +383,33 @@ def central(args, rank, world, device):
     for _ in range(args.warmup):
         eng.train_step()
     torch.cuda.synchronize(device)
-    dist.barrier()
-    torch.cuda.synchronize(device)
+    a0 = sum(eng.applied.values())
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.train_step()
     torch.cuda.synchronize(device)
-    dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    if rank == 0:
-        st = eng.learner.stats()
-        steps_per_s = args.steps / dt
-        frames_per_s = (world - 1) * args.steps * args.actor_steps * eng.frames_per_actor_step / dt
-        print(json.dumps({
-            "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
-            "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": args.dtype,
-            "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
-            "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
-                       "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",
-                       "topology": "central replay on rank 0, experience pushed over " + args.backend,
-                       "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": args.envs},
-            "actor_frames_per_sec": round(frames_per_s, 1), "replay_fill_seconds": round(t_fill, 3),
-            "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
-        }), flush=True)
+    packets = sum(eng.applied.values()) - a0
+    links = eng.close()
+    st = eng.learner.stats()
+    steps_per_s = args.steps / dt
+    print(json.dumps({
+        "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
+        "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": args.dtype,
+        "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
+        "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
+                   "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",
+                   "topology": "central replay on rank 0, async experience links over " + args.backend,
+                   "actor_pacing": "free" if args.unpaced else f"{args.actor_steps} packet/learner step/actor",
+                   "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": args.envs},
+        "actor_frames_per_sec": round(packets * eng.frames_per_actor_step / dt, 1),
+        "packets_applied_per_learner_step": round(packets / args.steps, 3),
+        "replay_fill_seconds": round(t_fill, 3), "links": links,
+        "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
+    }), flush=True)
     dist.destroy_process_group()
 
 

@@ -214,43 +214,121 @@ def _packet(rank, k, E, FB, n_slots, n_frames):
     return frames, (s_ids, s2_ids, a, r, d, p, slot.int(), fslot.int())
 
 
-def _experience_body(rank, world, E, FB, steps):
-    from apex_amd.parallel.experience import ExperienceReceiver, ExperienceSender, Region, apply_packet, pack_meta
+def _links_body(rank, world, E, FB, kill_rank, kill_at, q):
+    """Async central links (parallel.experience) on CPU tensors: rank 0 = learner side,
+    ranks 1.. = actors pushing deterministic packets; ``kill_rank`` hard-exits after
+    ``kill_at`` packets.  Rank 0 keeps ingesting, drops the dead link, then runs the stop
+    handshake with the survivors."""
+    import time
+
+    from apex_amd.parallel.experience import (META_COLS, STOP, ActorLink, LearnerLinks, apply_packets, link_groups,
+                                              pack_meta)
 
     n_slots, n_frames = 4 * E, 6 * E
+    groups = link_groups(world)
+    store = dist.distributed_c10d._get_default_store()
+    flat = torch.zeros(16)
     if rank > 0:
-        snd = ExperienceSender(E, FB, "cpu", dst=0)
-        for k in range(steps):
+        link = ActorLink(rank, groups[rank], store, flat, E, FB, depth=3, heartbeat_every=2)
+        versions, k = [], 0
+        while True:
+            v = link.poll_params()
+            if v == STOP:
+                break
+            if v is not None:
+                versions.append((v, float(flat[0])))
+            if rank == kill_rank and k == kill_at:
+                q.put((rank, "killed"))
+                q.close()
+                q.join_thread()  # flush the queue's feeder thread before the hard exit
+                os._exit(17)
             frames, fields = _packet(rank, k, E, FB, n_slots, n_frames)
-            snd.send(frames, pack_meta(*fields, out=snd.meta.clone()))
-            snd.wait()
-        return "sent"
+            link.push(frames, pack_meta(*fields))
+            k += 1
+            time.sleep(0.002)
+        return {"sent": link.sender.n_sent, "real": k, "versions": versions}
     R = world - 1
     tables = {"frames": torch.zeros(R * n_frames, FB, dtype=torch.uint8),
               "s_ids": torch.zeros(R * n_slots, 4, dtype=torch.int32),
               "s2_ids": torch.zeros(R * n_slots, 4, dtype=torch.int32),
               "action": torch.zeros(R * n_slots, dtype=torch.int32), "reward": torch.zeros(R * n_slots),
               "done": torch.zeros(R * n_slots)}
-    regions = {r: Region((r - 1) * n_slots, n_slots, (r - 1) * n_frames, n_frames) for r in range(1, world)}
-    rcv = ExperienceReceiver(E, FB, "cpu", range(1, world))
+    D = 3
+    frames = torch.zeros(R, D, E, FB, dtype=torch.uint8)
+    meta = torch.zeros(R, D, E, META_COLS, dtype=torch.int32)
+    seen = {r: [] for r in range(1, world)}
+
+    def apply(ready):
+        sel = torch.tensor([(r - 1) * D + k for r, k in ready])
+        fb = torch.tensor([(r - 1) * n_frames for r, _ in ready])
+        sb = torch.tensor([(r - 1) * n_slots for r, _ in ready])
+        for r, k in ready:  # the packet index = how many this link delivered before it
+            seen[r].append((int(meta[r - 1, k, 0, 12]), meta[r - 1, k].clone(), frames[r - 1, k].clone()))
+        apply_packets(tables, frames.view(R * D, E, FB)[sel], meta.view(R * D, E, META_COLS)[sel], fb, sb)
+
+    links = LearnerLinks(world, groups, store, flat, frames, meta, apply, dead_after=5.0, log=None)
+    t0, it = time.monotonic(), 0
+    while time.monotonic() - t0 < 60:
+        links.ingest()
+        it += 1
+        if it % 50 == 0:
+            flat.fill_(float(it))
+            links.publish(flat)
+        links.check_heartbeats(0.2)
+        if kill_rank not in links.live and len(seen[1]) >= kill_at + 40:
+            break
+        time.sleep(0.0005)
+    st = links.close(timeout=30)
+    # content of every packet that reached the learner (the initial reset-frame packet aside)
     bad = 0
-    for k in range(steps):
-        rcv.post()
-        for r, (frames, meta) in rcv.take("cpu").items():
-            slots, prio = apply_packet(tables, regions[r], frames, meta)
-            ef, (s_ids, s2_ids, a, rew, d, p, slot, fslot) = _packet(r, k, E, FB, n_slots, n_frames)
-            reg = regions[r]
-            bad += int(not torch.equal(slots, (slot + reg.slot_base).int()))
-            bad += int(not torch.equal(prio, p))
-            bad += int(not torch.equal(tables["frames"][(fslot + reg.frame_base).long()], ef))
-            sl = (slot + reg.slot_base).long()
-            bad += int(not torch.equal(tables["s_ids"][sl], s_ids + reg.frame_base))
-            bad += int(not torch.equal(tables["s2_ids"][sl], s2_ids + reg.frame_base))
-            bad += int(not torch.equal(tables["action"][sl], a))
-            bad += int(not torch.equal(tables["reward"][sl], rew) or not torch.equal(tables["done"][sl], d))
-    return bad
+    for r, pk in seen.items():
+        for j, (_, m, f) in enumerate(pk):
+            ef, fields = _packet(r, j, E, FB, n_slots, n_frames)
+            bad += int(not torch.equal(m, pack_meta(*fields)) or not torch.equal(f, ef))
+    return {"stats": st, "seen": {r: len(v) for r, v in seen.items()}, "bad": bad, "version": links.version}
 
 
-def test_central_experience_push_regions():
-    out = _spawn(_experience_body, 3, 32, 112, 7)
-    assert out[0] == 0 and out[1] == "sent" and out[2] == "sent"
+def _links_entry(rank, world, port, q, args):
+    import traceback
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        res = _links_body(rank, world, *args, q)
+        q.put((rank, res))
+    except Exception:  # pragma: no cover - reported to the parent
+        q.put((rank, "ERROR " + traceback.format_exc()))
+    q.close()
+    q.join_thread()
+    os._exit(0)  # no collective teardown: a peer is dead by design
+
+
+def test_central_links_async_drop_dead_actor():
+    """actor rank 2 is killed mid-run; rank 0 never blocks on it, drops the
+    link (receive error / stale heartbeat), keeps ingesting rank 1, and the stop handshake
+    drains rank 1 exactly (every real packet applied, in order, bit-exact)."""
+    world, E, FB, kill_at = 3, 16, 96, 12
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_links_entry, args=(r, world, port, q, (E, FB, 2, kill_at))) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, res = q.get(timeout=180)
+        out[r] = res
+    for p in procs:
+        p.join(60)
+    for r, res in out.items():
+        assert not (isinstance(res, str) and res.startswith("ERROR")), f"rank {r}: {res}"
+    assert procs[2].exitcode == 17 and out[2] == "killed"
+    st = out[0]["stats"]
+    assert set(st["dropped"]) == {2} and st["live"] == [1]
+    # rank 1: every real packet (plus none of the fillers) reached the learner, in order
+    assert out[0]["seen"][1] == out[1]["real"] >= kill_at + 40
+    assert out[0]["bad"] == 0
+    assert out[0]["seen"][2] <= kill_at
+    # conflated versioned params: increasing versions, the value is the publishing step
+    vs = out[1]["versions"]
+    assert vs and all(a[0] < b[0] for a, b in zip(vs, vs[1:]))
+    assert all(v <= out[0]["version"] for v, _ in vs)
