@@ -368,13 +368,14 @@ class ParamLink:
         self.version = version
         return True
 
-    def stop(self, timeout: float) -> bool:
-        if not self.track.wait(self.works, timeout):
-            return False
+    def done(self) -> bool:
+        return self.track.done(self.works)
+
+    def send_stop(self) -> None:
+        """Issue the stop message (version -1); the previous message must be delivered."""
         self.ver.fill_(STOP)
         self.works = self.track.add([dist.isend(self.ver, self.dst, group=self.group),
                                      dist.isend(self.snap, self.dst, group=self.group)])
-        return self.track.wait(self.works, timeout)
 
 
 class ParamSubscriber:
@@ -505,12 +506,29 @@ class LearnerLinks:
         if self.closed:
             return self.stats()
         self.closed = True
-        for r in sorted(self.live):
-            try:
-                if not self.params[r].stop(timeout):
-                    self.drop(r, "stop not delivered")
-            except Exception as e:
-                self.drop(r, f"stop failed: {e!r}")
+        # deliver stop on every live link while still consuming packets: an actor blocked on
+        # its credit window only re-arms its parameter receive after its next push went out
+        stopping, sent_stop = set(self.live), set()
+        deadline = time.monotonic() + timeout
+        while stopping and time.monotonic() < deadline:
+            self.ingest()
+            for r in sorted(stopping):
+                pl = self.params[r]
+                try:
+                    if not pl.done():
+                        continue
+                    if r in sent_stop:
+                        stopping.discard(r)
+                    else:
+                        pl.send_stop()
+                        sent_stop.add(r)
+                except Exception as e:
+                    self.drop(r, f"stop failed: {e!r}")
+                    stopping.discard(r)
+            stopping &= self.live
+            time.sleep(0.0005)
+        for r in sorted(stopping):
+            self.drop(r, "stop not delivered")
         for r in sorted(self.live):
             ib = self.inbox[r]
             try:
