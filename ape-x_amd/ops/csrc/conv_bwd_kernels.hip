@@ -610,22 +610,31 @@ int wgrad_grid(int layer, int B) {
 // 3136 per workgroup, transposed through LDS so reads and writes are both coalesced
 constexpr int kWideG = 16;
 constexpr int kRowLen = 49 * 64;
+// norm-only job: 8 elements per thread (3136 -> 392 workgroups for the FC1 gradient: fewer
+// partials for every optimizer workgroup to re-reduce).  A last-workgroup (ticket) reduction
+// of the partials was measured 5x slower (50 vs 9.5 us): each workgroup's device-scope release
+// fence writes back the XCD L2.
+constexpr int kNormOnlyPer = 256 * 8;
+
 __host__ __device__ inline int finalize_blocks(const FinalizeJob& j) {
   if (j.kind == 2) return j.n_main / kRowLen;
-  if (j.kind == 3) return (j.n_main + 255) / 256;
+  if (j.kind == 3) return (j.n_main + kNormOnlyPer - 1) / kNormOnlyPer;
   const int per = j.G >= kWideG ? 64 : 256;
   return (j.n_main + j.n_bias + per - 1) / per;
 }
 
-__device__ __forceinline__ void finalize_sumsq(float v, double* sumsq, bool active) {
-  // block-wide fixed-order sum of v^2 (all 256 threads call this)
+__device__ __forceinline__ void finalize_sumsq_q(double q, const FinalizeSet& fs) {
+  // block-wide fixed-order sum of the threads' q (all 256 threads call this)
   __shared__ double red[4];
-  double q = active ? (double)v * (double)v : 0.0;
   q = wave_sum(q);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) red[wave] = q;
   __syncthreads();
-  if (threadIdx.x == 0) sumsq[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) fs.sumsq[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__device__ __forceinline__ void finalize_sumsq(float v, const FinalizeSet& fs, bool active) {
+  finalize_sumsq_q(active ? (double)v * (double)v : 0.0, fs);
 }
 
 __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
@@ -637,9 +646,14 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   const FinalizeJob& jb = fs.job[j];
   if (jb.kind == 3) {  // norm only: the gradient was written in place by its producer
     if (!fs.sumsq) return;
-    const int e = ((int)blockIdx.x - jb.block0) * 256 + threadIdx.x;
-    const bool have = e < jb.n_main;
-    finalize_sumsq(have ? jb.part[e] : 0.f, fs.sumsq, have);
+    const int e0 = ((int)blockIdx.x - jb.block0) * kNormOnlyPer + threadIdx.x;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = e0 + 256 * k < jb.n_main ? jb.part[e0 + 256 * k] : 0.f;
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q += (double)v[k] * (double)v[k];
+    finalize_sumsq_q(q, fs);
     return;
   }
   if (jb.kind == 2) {  // FC1 weight rows: natural [n][p*64 + c] -> reference [n][c*49 + p]
@@ -701,7 +715,7 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
       t = (s0 + s1) + (s2 + s3);
     }
   }
-  if (fs.sumsq) finalize_sumsq(t, fs.sumsq, have);
+  if (fs.sumsq) finalize_sumsq(t, fs, have);
   if (!have) return;
   if (jb.kind == 0) {  // conv: [N][KH*KW*C] (c fastest) -> reference [N][C][KH][KW]
     if (e < jb.n_main) {
