@@ -44,6 +44,7 @@
 // conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.  conv1 (forward
 // and weight gradient) has its own sample-resident kernels: u8 frame planes staged in LDS.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -98,7 +99,10 @@ struct HasColsum<P, decltype((void)P::A_COLSUM, void())> {
   static constexpr bool value = P::A_COLSUM;
 };
 
-template <class P>
+// PF = global -> register prefetch depth: 1 = the next k-block is loaded while the current one
+// computes (its LDS store follows the MFMA block); 2 = two register sets, loads issued a full
+// k-block earlier (they cover L2 / MALL latency), the MFMA block fenced from the LDS stores.
+template <class P, int PF = 1>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
@@ -117,38 +121,43 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     for (int j = 0; j < G::TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  f32x4 ra[G::NA], rb[G::NB];
+  f32x4 ra[PF][G::NA], rb[PF][G::NB];
   f32x4 csum = zero4();
 
-  auto gload = [&](int kb) {
+  auto gload = [&](int kb, auto S) {
+    constexpr int st = decltype(S)::value;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int q = t + 256 * j;
-      if (G::CA % 256 == 0 || q < G::CA) ra[j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
+      if (G::CA % 256 == 0 || q < G::CA) ra[st][j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
     }
 #pragma unroll
     for (int j = 0; j < G::NB; ++j) {
       const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) rb[j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
+      if (G::CB % 256 == 0 || q < G::CB) rb[st][j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, auto S) {
+    constexpr int st = decltype(S)::value;
     float* As = lds + buf * (G::SA + G::SB);
     float* Bs = As + G::SA;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int q = t + 256 * j;
       if (G::CA % 256 == 0 || q < G::CA) {
-        *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[j];
-        if constexpr (COLSUM) csum += ra[j];
+        *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[st][j];
+        if constexpr (COLSUM) csum += ra[st][j];
       }
     }
 #pragma unroll
     for (int j = 0; j < G::NB; ++j) {
       const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[j];
+      if (G::CB % 256 == 0 || q < G::CB)
+        *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[st][j];
     }
   };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, PF - 1>;
   auto compute = [&](int buf) {
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
@@ -186,20 +195,46 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   };
 
   int kb = ctx.kb0;
-  if (kb < ctx.kb1) {
-    gload(kb);
-    sstore(0);
-  }
-  __syncthreads();
   int cur = 0;
-  for (; kb < ctx.kb1; ++kb) {
-    const bool more = kb + 1 < ctx.kb1;
-    if (more) gload(kb + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cur);
-    if (more) sstore(cur ^ 1);
+  if constexpr (PF == 1) {
+    if (kb < ctx.kb1) {
+      gload(kb, S0{});
+      sstore(0, S0{});
+    }
     __syncthreads();
-    cur ^= 1;
+    for (; kb < ctx.kb1; ++kb) {
+      const bool more = kb + 1 < ctx.kb1;
+      if (more) gload(kb + 1, S0{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur);
+      if (more) sstore(cur ^ 1, S0{});
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {
+    // register set s holds k-block kb + 1 on entry of a step; the step loads kb + 2 into the
+    // other set, computes kb from LDS, then stores kb + 1 (loaded one full step earlier)
+    auto step = [&](int k, auto S) {
+      constexpr int st = decltype(S)::value;
+      using SO = std::integral_constant<int, 1 - st>;
+      if (k + 2 < ctx.kb1) gload(k + 2, SO{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur);
+      __builtin_amdgcn_sched_barrier(0);
+      if (k + 1 < ctx.kb1) sstore(cur ^ 1, S);
+      __syncthreads();
+      cur ^= 1;
+    };
+    if (kb < ctx.kb1) {
+      gload(kb, S0{});
+      if (kb + 1 < ctx.kb1) gload(kb + 1, S1{});
+      sstore(0, S0{});
+    }
+    __syncthreads();
+    for (; kb < ctx.kb1; kb += 2) {
+      step(kb, S1{});
+      if (kb + 1 < ctx.kb1) step(kb + 1, S0{});
+    }
   }
 
 #pragma unroll
@@ -227,11 +262,11 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   }
 }
 
-template <class P>
+template <class P, int PF>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
-  gemm_body<P>(args, blockIdx.x, lds, sm);
+  gemm_body<P, PF>(args, blockIdx.x, lds, sm);
 }
 
 template <int A, int B>
@@ -241,7 +276,7 @@ struct MaxI {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2>
+template <class P1, class P2, int PF>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
   __shared__ union {
@@ -249,9 +284,9 @@ __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1, PF>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2, PF>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -924,17 +959,22 @@ SplitPlan wgrad_plan(int layer, int B) {
   }
 }
 
+// GEMM-body register prefetch depth (f32_set_variant(8, 1|2)); see gemm_body
+int g_pf_depth = 1;
+
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  gemm_k<P><<<blocks, 256, 0, s>>>(a);
+  if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a);
+  else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  if (g_pf_depth == 2) gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
 
@@ -964,6 +1004,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 5 && v >= 0 && v <= 2) g_bwd_mode = v;
   else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
   else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
+  else if (layer == 8 && v >= 1 && v <= 2) g_pf_depth = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
