@@ -102,6 +102,36 @@ struct HasColsum<P, decltype((void)P::A_COLSUM, void())> {
 // PF = global -> register prefetch depth: 1 = the next k-block is loaded while the current one
 // computes (its LDS store follows the MFMA block); 2 = two register sets, loads issued a full
 // k-block earlier (they cover L2 / MALL latency), the MFMA block fenced from the LDS stores.
+// Policies may precompute a per-thread row state once (the k-invariant part of an operand
+// chunk's address: im2col divisions by the output width, sample / channel offsets) and load
+// each k-block from it with a scalar offset: row_a(args, ctx, row, ch) -> RowA and
+// load_a_row(args, ctx, RowA, kb) (same for B).  Without it the loaders re-derive the whole
+// address per chunk and k-block (~20 VALU per 16-byte load: 5-7 VALU per MFMA measured).
+template <class P, class = void>
+struct HasRowA : std::false_type {};
+template <class P>
+struct HasRowA<P, std::void_t<typename P::RowA>> : std::true_type {};
+template <class P, class = void>
+struct HasRowB : std::false_type {};
+template <class P>
+struct HasRowB<P, std::void_t<typename P::RowB>> : std::true_type {};
+template <class P, bool = HasRowA<P>::value>
+struct RowAOf {
+  using type = int;
+};
+template <class P>
+struct RowAOf<P, true> {
+  using type = typename P::RowA;
+};
+template <class P, bool = HasRowB<P>::value>
+struct RowBOf {
+  using type = int;
+};
+template <class P>
+struct RowBOf<P, true> {
+  using type = typename P::RowB;
+};
+
 template <class P, int PF = 1>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
@@ -123,18 +153,40 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   f32x4 ra[PF][G::NA], rb[PF][G::NB];
   f32x4 csum = zero4();
+  typename RowAOf<P>::type rowa[G::NA];
+  typename RowBOf<P>::type rowb[G::NB];
+  if constexpr (HasRowA<P>::value) {
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = min(t + 256 * j, G::CA - 1);
+      rowa[j] = P::row_a(args, ctx, q / G::RA, q % G::RA);
+    }
+  }
+  if constexpr (HasRowB<P>::value) {
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = min(t + 256 * j, G::CB - 1);
+      rowb[j] = P::row_b(args, ctx, q / G::RB, q % G::RB);
+    }
+  }
 
   auto gload = [&](int kb, auto S) {
     constexpr int st = decltype(S)::value;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int q = t + 256 * j;
-      if (G::CA % 256 == 0 || q < G::CA) ra[st][j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
+      if (G::CA % 256 == 0 || q < G::CA) {
+        if constexpr (HasRowA<P>::value) ra[st][j] = P::load_a_row(args, ctx, rowa[j], kb);
+        else ra[st][j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
+      }
     }
 #pragma unroll
     for (int j = 0; j < G::NB; ++j) {
       const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) rb[st][j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
+      if (G::CB % 256 == 0 || q < G::CB) {
+        if constexpr (HasRowB<P>::value) rb[st][j] = P::load_b_row(args, ctx, rowb[j], kb);
+        else rb[st][j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
+      }
     }
   };
   auto sstore = [&](int buf, auto S) {
@@ -374,6 +426,26 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
     return ld4(c.p.w + (c.n0 + n) * 512 + kb * BK + 4 * ch);
   }
+  // row states (BK = 32: a k-block is exactly one tap, 4*ch its channel chunk)
+  struct RowA {
+    const float* p;  // sample / window origin + channel chunk; nullptr past the last row
+  };
+  struct RowB {
+    const float* p;
+  };
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    static_assert(BK == 32, "one tap per k-block");
+    const int m = c.m0 + row;
+    if (m >= c.M) return {nullptr};
+    const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9;
+    return {static_cast<const float*>(c.p.in) + ((size_t)b * 400 + 2 * oy * 20 + 2 * ox) * 32 + 4 * ch};
+  }
+  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    const int ky = kb >> 2, kx = kb & 3;  // tap = kb (wave-uniform)
+    return r.p ? ld4(r.p + (ky * 20 + kx) * 32) : zero4();
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 512 + 4 * ch}; }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -414,6 +486,26 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
     return ld4(c.p.w + (c.n0 + n) * 576 + kb * BK + 4 * ch);
   }
+  // row states (BK = 32: tap = kb >> 1, channel half (kb & 1) * 32, chunk 4*ch)
+  struct RowA {
+    const float* p;
+  };
+  struct RowB {
+    const float* p;
+  };
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    static_assert(BK == 32, "two k-blocks per tap");
+    const int m = c.m0 + row;
+    if (m >= c.M) return {nullptr};
+    const int b = m / 49, p = m - b * 49, oy = p / 7, ox = p - oy * 7;
+    return {static_cast<const float*>(c.p.in) + ((size_t)b * 81 + oy * 9 + ox) * 64 + 4 * ch};
+  }
+  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
+    return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (kb & 1) * 32) : zero4();
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 576 + 4 * ch}; }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -645,6 +737,29 @@ struct ConvWgrad {
     const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
     const float* x = static_cast<const float*>(a.x);
     return ld4(x + ((size_t)b * IH * IH + (S * oy + ky) * IH + S * ox + kx) * C + ci);
+  }
+  // row states: the chunk's sample row within a 32-sample k-block and its (tap, ci) offset
+  struct RowA {
+    int row, ch4;
+  };
+  struct RowB {
+    int row, off;  // off = (ky * IH + kx) * C + ci of the chunk's column
+  };
+  static __device__ RowA row_a(const Args&, const Ctx&, int row, int ch) { return {row, 4 * ch}; }
+  static __device__ f32x4 load_a_row(const Args& a, const Ctx& c, const RowA& r, int kb) {
+    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + r.row;  // p, block base: wave-uniform
+    return b < a.B ? ld4(a.dy + ((size_t)b * P + p) * 64 + r.ch4) : zero4();
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int row, int ch) {
+    const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
+    return {row, (ky * IH + kx) * C + ci};
+  }
+  static __device__ f32x4 load_b_row(const Args& a, const Ctx& c, const RowB& r, int kb) {
+    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + r.row;
+    if (b >= a.B) return zero4();
+    const int oy = p / OH, ox = p - oy * OH;  // wave-uniform
+    const float* x = static_cast<const float*>(a.x);
+    return ld4(x + ((size_t)b * IH * IH + S * oy * IH + S * ox) * C + r.off);
   }
   static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
     a.out[((size_t)c.split * 64 + m) * N + c.n0 + nl] = v;

@@ -98,15 +98,18 @@ def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
         assert row["hip_vs_t32"] < 1e-4, row["hip_vs_t32"]
         assert row["hip_loss_err"] < 1e-4 and row["hip_prio_err"] < 1e-3
     # whole run: the HIP fp32 learner is no farther from the fp64 learner than PyTorch's
-    # own fp32 learner (same fp32 roundoff class)
-    # (the sign-like RMSprop steps amplify any roundoff difference -- e.g. a different
-    # grad-norm summation order -- chaotically: measured HIP/torch-fp32 ratios 0.8-1.9 of the
-    # fp64 distance; the bf16 learner sits ~100x farther)
+    # own fp32 learner (same fp32 roundoff class).  The sign-like RMSprop steps amplify any
+    # roundoff difference chaotically, and the torch fp32 reference is NOT run-to-run
+    # deterministic (its conv backward): measured on MI355X (scripts/det_check.py, 4 runs)
+    # the HIP trajectory is bit-identical every run while torch fp32's own distance to fp64
+    # at step 15 was 0.071 / 0.072 / 0.073 / 0.27 -- so a single reference run bounds each
+    # step only loosely and the tight comparison is on the steady tail's mean.
     for row in traj:
-        assert row["hip_vs_64"] <= 1.25 * row["t32_vs_64"] + 0.02, row
-        assert row["param_rel"] <= 2.0 * row["t32_param_rel"] + 2e-4, row
+        assert row["hip_vs_64"] <= 3.0 * row["t32_vs_64"] + 0.02, row
+        assert row["param_rel"] <= 3.0 * row["t32_param_rel"] + 2e-4, row
     tail = traj[len(traj) // 2:]
     mean = lambda k: sum(r[k] for r in tail) / len(tail)  # noqa: E731
+    assert mean("hip_vs_64") <= 1.5 * mean("t32_vs_64")
     assert mean("hip_loss_err") <= 2.0 * mean("t32_loss_err") + 0.02
     assert mean("hip_prio_err") <= 2.0 * mean("t32_prio_err") + 0.02
 
