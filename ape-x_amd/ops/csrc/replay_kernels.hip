@@ -18,7 +18,7 @@
 namespace apex {
 
 // ------------------------------------------------------------------ leaf writes
-// Learner updates (dedup = 1, B <= 1024): one workgroup bitonic-sorts the (slot, position)
+// Learner updates (dedup = 1, B <= 1024): one workgroup rank-sorts the (slot, position)
 // pairs in LDS; the last position of every run of equal slots wins (the reference applies
 // updates sequentially, memory.py:313-320), and the sorted slot list is written out so the
 // level kernels dedup parents by comparing with their predecessor (O(1)).
@@ -44,12 +44,25 @@ __device__ __forceinline__ float block_reduce_1024(float v, float* red, bool is_
   return t;
 }
 
+// Writes one leaf; returns the priority to fold into the running max (0 if none).
+__device__ __forceinline__ float write_leaf(const TreeDesc& t, int id, float p, float alpha) {
+  if (p > 0.f && isfinite(p)) {
+    const float v = powf(p, alpha);
+    t.leaf_sum[id] = v;
+    t.leaf_min[id] = v;
+    return p;
+  }
+  t.leaf_sum[id] = 0.f;
+  t.leaf_min[id] = INFINITY;
+  return 0.f;
+}
+
 __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, const int* __restrict__ idx,
                                                                   const float* __restrict__ prio, int B, float alpha,
                                                                   float* max_prio, int* __restrict__ sorted_out,
                                                                   int64_t* bump0, int64_t d0, int64_t* bump1,
                                                                   int64_t d1, PrioMix mix) {
-  __shared__ unsigned long long key[kSortMax];
+  __shared__ unsigned long long key[kSortMax], unsorted[kSortMax];
   __shared__ float pmix[kSortMax];
   __shared__ float red[16];
   if (mix.delta) {
@@ -65,27 +78,24 @@ __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, co
     if (k == 0 && mix.loss_out) mix.loss_out[0] = total / (float)B;
     prio = nullptr;
   }
-  int n = 1;
-  while (n < B) n <<= 1;
-  for (int k = threadIdx.x; k < n; k += blockDim.x)
-    key[k] = k < B ? (((unsigned long long)(unsigned)idx[k]) << 32) | (unsigned)k : ~0ull;
+  // rank sort: keys (slot << 32 | position) are unique, so key k's sorted position is the
+  // number of smaller keys -- B broadcast LDS reads per thread and no barrier, where a
+  // bitonic network paid log2(B)(log2(B)+1)/2 barrier stages (45 for B = 512: ~50 us on a
+  // CU shared with the backward's GEMM waves)
+  for (int k = threadIdx.x; k < B; k += blockDim.x)
+    unsorted[k] = (((unsigned long long)(unsigned)idx[k]) << 32) | (unsigned)k;
   __syncthreads();
-  for (int size = 2; size <= n; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const int o = k ^ stride;
-        if (o > k) {
-          const bool up = (k & size) == 0;
-          const unsigned long long a = key[k], b = key[o];
-          if ((a > b) == up) {
-            key[k] = b;
-            key[o] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  for (int k = threadIdx.x; k < B; k += blockDim.x) {
+    const unsigned long long mine = unsorted[k];
+    int rank = 0;
+#pragma unroll 8
+    for (int j = 0; j < B; ++j) rank += unsorted[j] < mine;  // same address in every lane
+    key[rank] = mine;
   }
+  __syncthreads();
+  // the running max priority: one block-reduced atomic (per-leaf atomics on one address
+  // serialise at L2; MI355X: 46 us for 512 learner priorities)
+  float pmax = 0.f;
   for (int k = threadIdx.x; k < B; k += blockDim.x) {
     const int id = (int)(key[k] >> 32);
     sorted_out[k] = id;
@@ -93,17 +103,12 @@ __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, co
     if (!last || id < 0 || id >= t.size[0]) continue;
     const int src = (int)(key[k] & 0xFFFFFFFFu);
     const float p = mix.delta ? pmix[src] : (prio ? prio[src] : *max_prio);
-    if (p > 0.f && isfinite(p)) {
-      const float v = powf(p, alpha);
-      t.leaf_sum[id] = v;
-      t.leaf_min[id] = v;
-      if (prio || mix.delta) atomic_max_pos_float(max_prio, p);
-    } else {
-      t.leaf_sum[id] = 0.f;
-      t.leaf_min[id] = INFINITY;
-    }
+    const float wp = write_leaf(t, id, p, alpha);
+    if (prio || mix.delta) pmax = fmaxf(pmax, wp);
   }
+  pmax = block_reduce_1024(pmax, red, true);
   if (threadIdx.x == 0) {
+    if (pmax > 0.f) atomic_max_pos_float(max_prio, pmax);
     if (bump0) *bump0 += d0;
     if (bump1) *bump1 += d1;
   }
@@ -171,6 +176,10 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
 // ------------------------------------------------------------------ fused small updates
 // Node recompute by one wave, reading through L2 (the children may have been written by
 // other waves of this workgroup earlier in the same kernel).
+// Scope: __HIP_MEMORY_SCOPE_AGENT when the children were written by other workgroups
+// (ordered by fences + a ticket), __HIP_MEMORY_SCOPE_WORKGROUP inside one workgroup
+// (ordered by the barrier).
+template <int Scope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int node, int lane) {
   const int child = node * kTreeFanout + lane;
   const int csize = t.size[level - 1];
@@ -178,11 +187,11 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
   float m = INFINITY;
   if (child < csize) {
     if (level == 1) {
-      s = (double)__hip_atomic_load(t.leaf_sum + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      m = __hip_atomic_load(t.leaf_min + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = (double)__hip_atomic_load(t.leaf_sum + child, __ATOMIC_RELAXED, Scope);
+      m = __hip_atomic_load(t.leaf_min + child, __ATOMIC_RELAXED, Scope);
     } else {
-      s = __hip_atomic_load(t.node_sum[level - 2] + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      m = __hip_atomic_load(t.node_min[level - 2] + child, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = __hip_atomic_load(t.node_sum[level - 2] + child, __ATOMIC_RELAXED, Scope);
+      m = __hip_atomic_load(t.node_min[level - 2] + child, __ATOMIC_RELAXED, Scope);
     }
   }
   s = wave_sum(s);
@@ -196,10 +205,12 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
 // Recompute levels lo..hi of the dirty paths of `ids` (run order, staged in LDS) inside
 // ONE workgroup: each wave checks 64 candidates at once (lane-parallel run detection,
 // ballot) and recomputes the first-of-run nodes; level-synchronous via the barrier.
+// Only this workgroup reads what it wrote, so the barrier (workgroup-scope release /
+// acquire) orders the levels for workgroup-scope loads.  A device-scope __threadfence
+// per level wrote the XCD L2 back each time.
 __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int* sids, int B, int lo, int hi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int level = lo; level <= hi; ++level) {
-    __threadfence();
     __syncthreads();
     const int shift = kTreeLog2Fanout * level;
     for (int base = wave * 64; base < B; base += nw * 64) {  // wave-uniform
@@ -216,7 +227,7 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
       while (m) {
         const int k = __ffsll((long long)m) - 1;
         m &= m - 1;
-        recompute_node(t, level, __shfl(node, k, 64), lane);
+        recompute_node<__HIP_MEMORY_SCOPE_WORKGROUP>(t, level, __shfl(node, k, 64), lane);
       }
     }
   }
@@ -229,22 +240,18 @@ __global__ __launch_bounds__(1024) void per_write_ring_fused_k(TreeDesc t, const
                                                                float* max_prio, int64_t* bump0, int64_t d0,
                                                                int64_t* bump1, int64_t d1) {
   __shared__ int sids[1024];
+  __shared__ float red[16];
+  float pmax = 0.f;
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
     const int id = idx[i];
     sids[i] = id;
     if (id < 0 || id >= t.size[0]) continue;
-    const float p = prio ? prio[i] : *max_prio;
-    if (p > 0.f && isfinite(p)) {
-      const float v = powf(p, alpha);
-      t.leaf_sum[id] = v;
-      t.leaf_min[id] = v;
-      if (prio) atomic_max_pos_float(max_prio, p);
-    } else {
-      t.leaf_sum[id] = 0.f;
-      t.leaf_min[id] = INFINITY;
-    }
+    const float wp = write_leaf(t, id, prio ? prio[i] : *max_prio, alpha);
+    if (prio) pmax = fmaxf(pmax, wp);
   }
+  pmax = block_reduce_1024(pmax, red, true);  // one atomic, not one per leaf
   if (threadIdx.x == 0) {
+    if (pmax > 0.f) atomic_max_pos_float(max_prio, pmax);
     if (bump0) *bump0 += d0;
     if (bump1) *bump1 += d1;
   }
@@ -386,19 +393,6 @@ __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
 // + per_update_top_k, ~60 us of latency per step on MI355X) this is ~3 short kernels.
 
 
-// Writes one leaf; returns the priority to fold into the running max (0 if none).
-__device__ __forceinline__ float write_leaf(const TreeDesc& t, int id, float p, float alpha) {
-  if (p > 0.f && isfinite(p)) {
-    const float v = powf(p, alpha);
-    t.leaf_sum[id] = v;
-    t.leaf_min[id] = v;
-    return p;
-  }
-  t.leaf_sum[id] = 0.f;
-  t.leaf_min[id] = INFINITY;
-  return 0.f;
-}
-
 __global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrite w, int small_levels_in_block) {
   __shared__ float red[16];
   __shared__ int sids[2048];
@@ -426,7 +420,6 @@ __global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrit
       p = w.prio ? w.prio[k] : *w.max_prio;
     }
   }
-  __threadfence();
   __syncthreads();  // actor leaves land before any learner leaf (last write wins)
   const int id = k < w.B ? w.idx[k] : -1;
   const bool ok = id >= 0 && id < t.size[0];
@@ -434,8 +427,7 @@ __global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrit
     sids[w.E + k] = id;
     w.list[w.E + k] = id;
   }
-  if (ok) atomicMax(w.owner + id, k);
-  __threadfence();
+  if (ok) atomicMax(w.owner + id, k);  // device atomics: performed at L2
   __syncthreads();
   if (ok && __hip_atomic_load(w.owner + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
     const float wp = write_leaf(t, id, p, w.alpha);
@@ -449,8 +441,6 @@ __global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrit
     if (w.bump) *w.bump += 1;
   }
   if (small_levels_in_block) {  // tiny trees: every level in this block
-    __threadfence();
-    __syncthreads();
     update_levels_block(t, sids, w.E + w.B, 1, t.levels);
   }
 }
