@@ -620,6 +620,127 @@ __global__ __launch_bounds__(256) void f32_conv1_fwd_k(F32Set set) {
   }
 }
 
+// conv1 forward at reference precision on the bf16 matrix cores (exact three-term split).
+//  * Input pixels are u8 (0..255, 8 significant bits): exactly representable in bf16.
+//  * An fp32 weight splits EXACTLY into three bf16 terms by truncation: hi = w with its low
+//    16 bits cleared, mid = (w - hi) likewise, lo = w - hi - mid (each subtraction is exact;
+//    lo has <= 8 significant bits).  A bf16 x bf16 product is exact in fp32.
+//  So x*w = x*hi + x*mid + x*lo with every product exact, accumulated in fp32 -- the hi
+//  products in one accumulator and the mid + lo products (2^-8 smaller) in another, so the
+//  extra terms add no rounding at the fp32 chain's scale (error vs fp64 measured in
+//  tests/test_gpu_f32_net.py against the fp32-MFMA kernel).  On v_mfma_f32_16x16x32_bf16
+//  (16 cycles per 16x16x32) the 3 terms cost 48 cycles where v_mfma_f32_16x16x4_f32 pays
+//  8 x 32 = 256 for the same 16x16x32 of fp32: 5.3x fewer MFMA cycles.
+//  Persistent over samples, two workgroups per CU (56 KB of LDS each: the sample's four
+//  planes as bf16, converted once while staging); the weight split is redone only when
+//  the problem changes.  Wave w: channels 16 (w >> 1) .. +15, output tiles w & 1, +2, ...
+//  of 16 pixels; lane (i = l & 15, q = l >> 4) holds A[pixel i][k = 8q + j] = plane c =
+//  kb >> 1, row 4 oy + 4 (kb & 1) + q, columns 4 ox + j: 8 consecutive bf16 of one row.
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
+  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
+
+struct W1Split {
+  bfx8 hi[8], mid[8], lo[8];
+};
+
+// this lane's B fragments for all 8 k-blocks: W1[row][32 kb + 8q + j], split into 3 terms
+__device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
+#pragma unroll
+  for (int kb = 0; kb < 8; ++kb) {
+    const f32x4 v0 = ld4(wrow + 32 * kb), v1 = ld4(wrow + 32 * kb + 4);
+    const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = x[2 * j], b = x[2 * j + 1];
+      const float ah = trunc_bf16(a), bh = trunc_bf16(b);
+      const float ar = a - ah, br = b - bh;
+      const float am = trunc_bf16(ar), bm = trunc_bf16(br);
+      h[j] = pack_bf16_hi(ah, bh);
+      m[j] = pack_bf16_hi(am, bm);
+      l[j] = pack_bf16_hi(ar - am, br - bm);  // exact: <= 8 significant bits
+    }
+    w.hi[kb] = __builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3]));
+    w.mid[kb] = __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3]));
+    w.lo[kb] = __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]));
+  }
+}
+
+constexpr int kC1xGrid = 512;  // two workgroups per CU
+__global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
+  __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
+  const int B = set.B, total = set.n * B;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i = lane & 15, q = lane >> 4, nh = wave >> 1;
+  const __bf16* xb = reinterpret_cast<const __bf16*>(xs);
+  W1Split w;
+  float bias = 0.f;
+  int cur = -1;
+  for (int smp = blockIdx.x; smp < total; smp += gridDim.x) {
+    const int prob = smp / B, b = smp - prob * B;
+    const F32Prob p = pick(set, prob);
+    if (prob != cur) {  // block-uniform
+      cur = prob;
+      split_w1(p.w + (nh * 16 + i) * 256 + 8 * q, w);
+      bias = p.bias[nh * 16 + i];
+    }
+    __syncthreads();  // the previous sample's tiles are done with xs
+    {  // stage: 4 x 441 16-byte u8 chunks -> 32-byte bf16 runs, all loads in flight first
+      const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
+      constexpr int kChunks = 4 * (kPlane / 16), kPer = (kChunks + 255) / 256;
+      const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
+      const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
+      const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
+      const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
+      uint4 v[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int e = min(t + 256 * k, kChunks - 1), c = e / 441;
+        const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
+        v[k] = sc[e - c * 441];
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int e = t + 256 * k;
+        if (e < kChunks) {  // chunk e = bf16 elements 16e .. 16e + 15 (7056 = 441 x 16)
+          const f32x4 a = u8x4(v[k].x), bq = u8x4(v[k].y), c = u8x4(v[k].z), d = u8x4(v[k].w);
+          uint4* dst = reinterpret_cast<uint4*>(xs) + 2 * e;
+          dst[0] = make_uint4(pack_bf16_hi(a[0], a[1]), pack_bf16_hi(a[2], a[3]), pack_bf16_hi(bq[0], bq[1]),
+                              pack_bf16_hi(bq[2], bq[3]));
+          dst[1] = make_uint4(pack_bf16_hi(c[0], c[1]), pack_bf16_hi(c[2], c[3]), pack_bf16_hi(d[0], d[1]),
+                              pack_bf16_hi(d[2], d[3]));
+        }
+      }
+    }
+    __syncthreads();
+    float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + i;
+    for (int tile = wave & 1; tile < 25; tile += 2) {
+      const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
+      const __bf16* a0 = xb + (4 * oy + q) * 84 + 4 * ox;
+      bfx8 a[8];
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
+        const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
+        const uint2 lo = ap[0], hi = ap[1];
+        a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+      f32x4 ah = zero4(), al = zero4();
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.hi[kb], ah, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.mid[kb], al, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.lo[kb], al, 0, 0, 0);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(size_t)(tile * 16 + 4 * q + e) * 32] = fmaxf(ah[e] + al[e] + bias, 0.f);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ backward policies
 struct BwdArgs {
   const void* x;        // layer input (u8 frames for conv1: FrameSrc fields)
@@ -1102,8 +1223,9 @@ void check_set(const F32Set& set) {
 
 // ------------------------------------------------------------------ host launchers
 // conv1 forward variant (benchmark knob, f32_set_variant): 0 = sample-resident kernel
-// (f32_conv1_fwd_k), 1 = generic GEMM body (128 x 32 x 16 tiles, windows gathered from global)
-int g_conv1_variant = 0;
+// (f32_conv1_fwd_k), 1 = generic GEMM body (128 x 32 x 16 tiles, windows gathered from global),
+// 2 = exact-split bf16 MFMA (f32_conv1_fwd_x3_k)
+int g_conv1_variant = 2;
 
 template <class P>
 void fwd_launch(const F32Set& set, hipStream_t s) {
@@ -1115,7 +1237,7 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 int g_bwd_mode = 0, g_dgrad_variant = 0;
 
 void f32_set_variant(int layer, int v) {
-  if (layer == 1 && v >= 0 && v <= 1) g_conv1_variant = v;
+  if (layer == 1 && v >= 0 && v <= 2) g_conv1_variant = v;
   else if (layer == 5 && v >= 0 && v <= 2) g_bwd_mode = v;
   else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
   else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
@@ -1132,6 +1254,9 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
     case 1:
       if (g_conv1_variant == 1) {
         fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
+      } else if (g_conv1_variant == 2) {
+        f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+        LAUNCH_CHECK();
       } else {
         f32_conv1_fwd_k<<<set.n * set.B, 256, 0, s>>>(set);
         LAUNCH_CHECK();

@@ -67,6 +67,41 @@ def test_f32_layers_match_fp64(cuda, B):
     assert float((ws.q - q32).norm() / q32.norm()) < 1e-5
 
 
+@pytest.mark.parametrize("B", [37, 300])
+def test_conv1_exact_split_is_fp32_class(cuda, B):
+    """conv1 on bf16 MFMA with the exact three-term weight split (f32_conv1_fwd_x3_k, knob
+    (1, 2)) vs the fp32-MFMA kernel (knob (1, 0)): per-element error against fp64, scaled by
+    sum_k |x_k w_k| (the fp32 dot-product error scale), stays in the fp32 class -- every
+    product is exact, only the fp32 accumulation rounds."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    m = _model(cuda, seed=3)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    f = m.features
+    d = lambda t: t.detach().double()  # noqa: E731
+    pre = F.conv2d(x.double(), d(f[0].weight), d(f[0].bias), stride=4)
+    scale = F.conv2d(x.double(), d(f[0].weight).abs(), None, stride=4) + d(f[0].bias).abs().view(1, -1, 1, 1)
+    ref = F.relu(pre)
+    errs = {}
+    try:
+        for v in (0, 2):
+            hip.f32_set_variant(1, v)
+            ws = F32Workspace(B, 18, cuda, keep_for_backward=True)
+            net(x, ws)
+            torch.cuda.synchronize()
+            g = _nchw(ws.a1, B, 32, 20)
+            errs[v] = float(((g - ref).abs() / scale).max())
+            assert bool((g >= 0).all())
+    finally:
+        hip.f32_set_variant(1, 2)  # the default
+    # fp32 unit roundoff 6e-8: a K = 256 accumulation stays within a few ulps of sum|x w|
+    assert errs[2] < 4e-7, errs
+    assert errs[2] <= 2.0 * errs[0] + 1e-7, errs
+
+
 def test_f32_frame_ring_and_multi_pass(cuda):
     """conv1 reading the HBM frame ring by id (rows picked by idx) == dense input, and the
     3-problem launch == three single launches (bit-identical)."""
