@@ -1063,6 +1063,142 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
   }
 }
 
+// conv1 weight gradient at reference precision on bf16 MFMA (the exact split of the
+// forward above, applied to dy): the u8 frame operand is exact in bf16 and each dy value
+// splits exactly into hi + mid + lo bf16, so every product is exact and only the fp32
+// accumulation rounds (hi products and mid + lo products in separate accumulators).
+// Same workgroup layout and partials as f32_conv1_wgrad_k (8 waves = 2 samples x 4 input
+// channels c; wave c owns columns kk = c*64 + (col >> 1)*8 + 4 (col & 1) + i of the 4 tiles
+// i, both co halves), but the reduction runs over PIXEL GROUPS of 8 on
+// v_mfma_f32_16x16x32_bf16: group g = (output row g / 3, columns 8 (g % 3) .. +7; the
+// third group of a row has 4 real pixels, dy = 0 on the 4 pad slots), 4 groups (lane q)
+// per k-step, 15 k-steps per sample.  Lane (col, q) reads the 8 consecutive plane dwords
+// (4oy + (col >> 1)) * 21 + ox0 + jj + (col & 1) once per k-step; tile i takes byte i of
+// each (kx & 3 == i), so the 4 B fragments share one set of LDS reads.
+__global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + 16];  // + pad: row-end groups
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int col = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
+  const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
+  {  // stage both samples' planes (u8): 2 x 4 x 441 16-byte chunks
+    const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
+    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
+    uint4 v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
+      v[i] = reinterpret_cast<const uint4*>(frame_plane(f, b0 + s2, ch, kPlane))[r - ch * 441];
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int e = t + 512 * i;
+      if (e < ns * kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
+    }
+    if (t < 16) pl[kConv1WgradS * 4 * kPlaneDw + t] = 0u;
+  }
+  __syncthreads();
+  f32x4 ah[2][4], al[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ah[h][i] = al[h][i] = zero4();
+  float bs0 = 0.f, bs1 = 0.f;  // bias partials of co = col, 16 + col
+  if (sl < ns) {
+    const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
+    const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (col >> 1) * 21 + (col & 1);
+    for (int ks = 0; ks < 15; ++ks) {
+      const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy);
+      const int nv = min(8, 20 - ox0);  // real pixels in this group (8 or 4)
+      // A: dy[pixel][co] for the group's 8 slots, both co halves, split into 3 bf16 terms
+      float d0[8], d1[8];
+      const float* dp = dy + (oy * 20 + ox0) * 32 + col;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        d0[jj] = jj < nv ? dp[jj * 32] : 0.f;
+        d1[jj] = jj < nv ? dp[jj * 32 + 16] : 0.f;
+        bs0 += d0[jj];
+        bs1 += d1[jj];
+      }
+      bfx8 A[2][3];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* d = h ? d1 : d0;
+        uint32_t hw[4], mw[4], lw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float x = d[2 * j], y = d[2 * j + 1];
+          const float xh = trunc_bf16(x), yh = trunc_bf16(y);
+          const float xr = x - xh, yr = y - yh;
+          const float xm = trunc_bf16(xr), ym = trunc_bf16(yr);
+          hw[j] = pack_bf16_hi(xh, yh);
+          mw[j] = pack_bf16_hi(xm, ym);
+          lw[j] = pack_bf16_hi(xr - xm, yr - ym);
+        }
+        A[h][0] = __builtin_bit_cast(bfx8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
+        A[h][1] = __builtin_bit_cast(bfx8, make_uint4(mw[0], mw[1], mw[2], mw[3]));
+        A[h][2] = __builtin_bit_cast(bfx8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
+      }
+      // B: 8 plane dwords (pixels ox0 + jj of row 4 oy + ky), byte i -> tile i
+      const uint32_t* px = pc + 4 * oy * 21 + ox0;
+      uint32_t wv[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) wv[jj] = px[jj];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t bw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 lo = u8x4(wv[2 * j]), hi = u8x4(wv[2 * j + 1]);
+          bw[j] = pack_bf16_hi(lo[i], hi[i]);
+        }
+        const bfx8 Bf = __builtin_bit_cast(bfx8, make_uint4(bw[0], bw[1], bw[2], bw[3]));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ah[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][0], Bf, ah[h][i], 0, 0, 0);
+          al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][1], Bf, al[h][i], 0, 0, 0);
+          al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][2], Bf, al[h][i], 0, 0, 0);
+        }
+      }
+    }
+  }
+  bs0 += __shfl_xor(bs0, 16, 64);
+  bs0 += __shfl_xor(bs0, 32, 64);
+  bs1 += __shfl_xor(bs1, 16, 64);
+  bs1 += __shfl_xor(bs1, 32, 64);
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2][32]
+  if (sl == 1) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = ah[h][i][e] + al[h][i][e];
+    if (c == 0 && q == 0) {
+      red[4 * 32 * 64 + col] = bs0;
+      red[4 * 32 * 64 + 16 + col] = bs1;
+    }
+  }
+  __syncthreads();
+  if (sl == 0) {
+    float* out = a.out + (size_t)blockIdx.x * 32 * 256;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v = (ah[h][i][e] + al[h][i][e]) + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
+          const int co = h * 16 + 4 * q + e, kk = c * 64 + (col >> 1) * 8 + 4 * (col & 1) + i;
+          out[co * 256 + kk] = v;
+        }
+    if (c == 0 && q == 0) {
+      a.out2[blockIdx.x * 32 + col] = bs0 + red[4 * 32 * 64 + col];
+      a.out2[blockIdx.x * 32 + 16 + col] = bs1 + red[4 * 32 * 64 + 16 + col];
+    }
+  }
+}
+
 // Input-gradient GEMMs with POSITION-MAJOR rows: row m = (spatial position, sample), so all
 // rows of a tile share one input position and the same set of in-range taps.  The k loop runs
 // over exactly those taps -- the sample-major forms above multiply the zero border: 40% of
@@ -1235,6 +1371,8 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // backward benchmark knobs: g_bwd_mode (0 both GEMMs of a conv backward launch, 1 weight
 // gradient only, 2 input gradient only), g_dgrad_variant (0 position-major, 1 sample-major)
 int g_bwd_mode = 0, g_dgrad_variant = 0;
+// conv1 weight gradient (knob 9): 0 = fp32 MFMA (f32_conv1_wgrad_k), 1 = exact-split bf16 MFMA
+int g_conv1_wgrad_variant = 1;
 
 void f32_set_variant(int layer, int v) {
   if (layer == 1 && v >= 0 && v <= 2) g_conv1_variant = v;
@@ -1242,6 +1380,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
   else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
   else if (layer == 8 && v >= 1 && v <= 2) g_pf_depth = v;
+  else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1341,7 +1480,8 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
         launch2<ConvWgrad<2>, Conv2DgradP>(g, nw2, d, mode == 1 ? 0 : Conv2DgradP::tiles(B), s);
       break;
     case 1:
-      f32_conv1_wgrad_k<<<p.splits, 512, 0, s>>>(g);
+      if (g_conv1_wgrad_variant == 1) f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);
+      else f32_conv1_wgrad_k<<<p.splits, 512, 0, s>>>(g);
       LAUNCH_CHECK();
       break;
     default: throw std::invalid_argument("f32_conv_bwd: layer must be 1, 2 or 3");

@@ -157,6 +157,42 @@ def test_f32_backward_matches_fp64_autograd(cuda, B):
                                    msg=lambda s, n=name: f"{n}: {s}")
 
 
+@pytest.mark.parametrize("B", [29, 256])
+def test_conv1_wgrad_exact_split_is_fp32_class(cuda, B):
+    """conv1 weight gradient on bf16 MFMA with dy split exactly into three bf16 terms
+    (f32_conv1_wgrad_x3_k, knob (9, 1)) vs the fp32-MFMA kernel (knob (9, 0)), both against
+    fp64 on the SAME conv1 output gradient, per element scaled by sum |dy x|."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    A = 18
+    m = _model(cuda, A=A, seed=5)
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+    net(x, ws)
+    dq = torch.randn(B, A, device=cuda) / B
+    errs, f = {}, m.features
+    try:
+        for v in (0, 1):
+            hip.f32_set_variant(9, v)
+            net.backward(dq, x, ws)
+            torch.cuda.synchronize()
+            dy = _nchw(ws.dy1, B, 32, 20)
+            ref = torch.nn.grad.conv2d_weight(x.double(), f[0].weight.shape, dy, stride=4)
+            scale = torch.nn.grad.conv2d_weight(x.double(), f[0].weight.shape, dy.abs(), stride=4)
+            errs[v] = float(((f[0].weight.grad.double() - ref).abs() / scale.clamp_min(1e-30)).max())
+            bref = dy.sum((0, 2, 3))
+            errs[f"b{v}"] = float(((f[0].bias.grad.double() - bref).abs() / dy.abs().sum((0, 2, 3))).max())
+    finally:
+        hip.f32_set_variant(9, 1)  # the default
+    assert errs[1] < 4e-7 and errs["b1"] < 4e-7, errs
+    assert errs[1] <= 2.0 * errs[0] + 1e-7, errs
+
+
 def test_f32_finalize_norm_partials(cuda):
     """trunk_backward's grad_finalize sum-of-squares partials cover every trunk + FC1
     weight gradient (the FC1 weights through norm-only jobs)."""
