@@ -314,6 +314,203 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   }
 }
 
+// ------------------------------------------------------------------ exact split GEMM (x9)
+// Reference-precision GEMM on the bf16 matrix cores: every fp32 operand element is split
+// EXACTLY into three bf16 terms (hi = x with the low 16 bits cleared, mid = (x - hi)
+// likewise, lo = the rest, <= 8 significant bits) while it is staged into LDS, and the 9
+// term products -- each exact in fp32 -- are accumulated in fp32: hi*hi in one
+// accumulator, the 8 smaller products (<= 2^-7 of it) in a second, added at the end.  So
+// the only rounding is fp32 accumulation, as on the fp32 MFMA (error vs fp64 pinned in
+// tests/test_gpu_f32_net.py).  v_mfma_f32_32x32x16_bf16 costs 32 cycles per 32x32x16 where
+// v_mfma_f32_32x32x2_f32 costs 8 x 64: 9 terms = 288 vs 512 cycles, 1.78x fewer.  Its C/D
+// layout is the fp32 32x32x2 layout, so the policies' store epilogues are unchanged.
+// K-major operands only (LDS planes [row][k], pitch BK + 8 bf16 = 16-byte aligned rows,
+// conflict-free ds_read_b128 fragment reads).
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
+  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
+
+__device__ __forceinline__ void split4(const f32x4& v, uint2& hi, uint2& mid, uint2& lo) {
+  uint32_t hw[2], mw[2], lw[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float x = v[2 * j], y = v[2 * j + 1];
+    const float xh = trunc_bf16(x), yh = trunc_bf16(y);
+    const float xr = x - xh, yr = y - yh;
+    const float xm = trunc_bf16(xr), ym = trunc_bf16(yr);
+    hw[j] = pack_bf16_hi(xh, yh);
+    mw[j] = pack_bf16_hi(xm, ym);
+    lw[j] = pack_bf16_hi(xr - xm, yr - ym);
+  }
+  hi = make_uint2(hw[0], hw[1]);
+  mid = make_uint2(mw[0], mw[1]);
+  lo = make_uint2(lw[0], lw[1]);
+}
+
+template <class P>
+struct GeoX9 {
+  using G = Geo<P>;
+  static constexpr int P2 = G::BK + 8;                  // bf16 pitch of a term plane row
+  static constexpr int SA2 = G::BM * P2, SB2 = G::BN * P2;
+  static constexpr int STAGE = 3 * (SA2 + SB2);         // bf16 elements per stage
+  static constexpr int LDS_HALVES = 2 * STAGE;
+};
+
+template <class P>
+__device__ __forceinline__ void gemm_body_x9(const typename P::Args& args, int block, uint16_t* lds,
+                                             typename P::Smem& sm) {
+  using G = Geo<P>;
+  using X = GeoX9<P>;
+  static_assert(P::A_KMAJ && P::B_KMAJ && !HasColsum<P>::value, "x9 body: K-major operands, no colsum");
+  static_assert(G::BK % 16 == 0, "k-steps of 16");
+  typename P::Ctx ctx;
+  P::decode(args, block, ctx, sm);
+  if constexpr (P::SMEM) __syncthreads();
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave % G::WM, wn = wave / G::WM;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 acc[G::TM][G::TN], acc2[G::TM][G::TN];
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = acc2[i][j][e] = 0.f;
+  f32x4 ra[G::NA], rb[G::NB];
+  typename RowAOf<P>::type rowa[G::NA];
+  typename RowBOf<P>::type rowb[G::NB];
+  if constexpr (HasRowA<P>::value) {
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = min(t + 256 * j, G::CA - 1);
+      rowa[j] = P::row_a(args, ctx, q / G::RA, q % G::RA);
+    }
+  }
+  if constexpr (HasRowB<P>::value) {
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = min(t + 256 * j, G::CB - 1);
+      rowb[j] = P::row_b(args, ctx, q / G::RB, q % G::RB);
+    }
+  }
+  auto gload = [&](int kb) {
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = t + 256 * j;
+      if (G::CA % 256 == 0 || q < G::CA) {
+        if constexpr (HasRowA<P>::value) ra[j] = P::load_a_row(args, ctx, rowa[j], kb);
+        else ra[j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = t + 256 * j;
+      if (G::CB % 256 == 0 || q < G::CB) {
+        if constexpr (HasRowB<P>::value) rb[j] = P::load_b_row(args, ctx, rowb[j], kb);
+        else rb[j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+    uint16_t* As = lds + buf * X::STAGE;
+    uint16_t* Bs = As + 3 * X::SA2;
+#pragma unroll
+    for (int j = 0; j < G::NA; ++j) {
+      const int q = t + 256 * j;
+      if (G::CA % 256 == 0 || q < G::CA) {
+        uint2 hi, mid, lo;
+        split4(ra[j], hi, mid, lo);
+        uint16_t* d = As + (q / G::RA) * X::P2 + 4 * (q % G::RA);
+        *reinterpret_cast<uint2*>(d) = hi;
+        *reinterpret_cast<uint2*>(d + X::SA2) = mid;
+        *reinterpret_cast<uint2*>(d + 2 * X::SA2) = lo;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < G::NB; ++j) {
+      const int q = t + 256 * j;
+      if (G::CB % 256 == 0 || q < G::CB) {
+        uint2 hi, mid, lo;
+        split4(rb[j], hi, mid, lo);
+        uint16_t* d = Bs + (q / G::RB) * X::P2 + 4 * (q % G::RB);
+        *reinterpret_cast<uint2*>(d) = hi;
+        *reinterpret_cast<uint2*>(d + X::SB2) = mid;
+        *reinterpret_cast<uint2*>(d + 2 * X::SB2) = lo;
+      }
+    }
+  };
+  auto compute = [&](int buf) {
+    const uint16_t* As = lds + buf * X::STAGE;
+    const uint16_t* Bs = As + 3 * X::SA2;
+#pragma unroll
+    for (int kc = 0; kc < G::BK / 16; ++kc) {
+      bfx8 a[G::TM][3], b[G::TN][3];
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi) {
+        const uint16_t* ap = As + (wm * G::WTM + mi * 32 + r) * X::P2 + kc * 16 + 8 * h;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) a[mi][u] = *reinterpret_cast<const bfx8*>(ap + u * X::SA2);
+      }
+#pragma unroll
+      for (int ni = 0; ni < G::TN; ++ni) {
+        const uint16_t* bp = Bs + (wn * G::WTN + ni * 32 + r) * X::P2 + kc * 16 + 8 * h;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) b[ni][u] = *reinterpret_cast<const bfx8*>(bp + u * X::SB2);
+      }
+#pragma unroll
+      for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < G::TN; ++ni) {
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][0], acc[mi][ni], 0, 0, 0);
+          f32x16 c2 = acc2[mi][ni];
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][1], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][0], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][1], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][2], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][0], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][2], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][1], c2, 0, 0, 0);
+          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][2], c2, 0, 0, 0);
+          acc2[mi][ni] = c2;
+        }
+    }
+  };
+  int kb = ctx.kb0, cur = 0;
+  if (kb < ctx.kb1) {
+    gload(kb);
+    sstore(0);
+  }
+  __syncthreads();
+  for (; kb < ctx.kb1; ++kb) {
+    const bool more = kb + 1 < ctx.kb1;
+    if (more) gload(kb + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur);
+    if (more) sstore(cur ^ 1);
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < G::TN; ++ni)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+        P::store(args, ctx, wm * G::WTM + mi * 32 + row, wn * G::WTN + ni * 32 + r, acc[mi][ni][e] + acc2[mi][ni][e]);
+      }
+}
+
+template <class P>
+__global__ __launch_bounds__(256) void gemm_x9_k(typename P::Args args) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[GeoX9<P>::LDS_HALVES];
+  __shared__ typename P::Smem sm;
+  gemm_body_x9<P>(args, blockIdx.x, lds, sm);
+}
+
 template <class P, int PF>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
@@ -636,13 +833,6 @@ __global__ __launch_bounds__(256) void f32_conv1_fwd_k(F32Set set) {
 //  the problem changes.  Wave w: channels 16 (w >> 1) .. +15, output tiles w & 1, +2, ...
 //  of 16 pixels; lane (i = l & 15, q = l >> 4) holds A[pixel i][k = 8q + j] = plane c =
 //  kb >> 1, row 4 oy + 4 (kb & 1) + q, columns 4 ox + j: 8 consecutive bf16 of one row.
-typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
-  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
-}
-__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
-
 struct W1Split {
   bfx8 hi[8], mid[8], lo[8];
 };
@@ -1334,9 +1524,19 @@ SplitPlan wgrad_plan(int layer, int B) {
 // GEMM-body register prefetch depth (f32_set_variant(8, 1|2)); see gemm_body
 int g_pf_depth = 1;
 
+// single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
+int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
+
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
+  if constexpr (P::A_KMAJ && P::B_KMAJ && !HasColsum<P>::value) {
+    if (g_x9) {
+      gemm_x9_k<P><<<blocks, 256, 0, s>>>(a);
+      LAUNCH_CHECK();
+      return;
+    }
+  }
   if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a);
   else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
@@ -1381,6 +1581,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
   else if (layer == 8 && v >= 1 && v <= 2) g_pf_depth = v;
   else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
+  else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 

@@ -102,6 +102,46 @@ def test_conv1_exact_split_is_fp32_class(cuda, B):
     assert errs[2] <= 2.0 * errs[0] + 1e-7, errs
 
 
+@pytest.mark.parametrize("B", [37, 200])
+def test_x9_gemm_forward_is_fp32_class(cuda, B):
+    """conv2 / conv3 / FC1 forward on the exact-split bf16 GEMM body (both operands split
+    into three bf16 terms, all 9 products exact, fp32 accumulation; knob (10, 1)) vs the
+    fp32-MFMA body (knob (10, 0)): per-element error against fp64 from the SAME layer input,
+    scaled by sum_k |a_k w_k|."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    m = _model(cuda, seed=7)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    f = m.features
+    d = lambda t: t.detach().double()  # noqa: E731
+    errs = {}
+    try:
+        for v in (0, 1):
+            hip.f32_set_variant(10, v)
+            ws = F32Workspace(B, 18, cuda, keep_for_backward=True)
+            net(x, ws)
+            torch.cuda.synchronize()
+            g1, g2, g3 = _nchw(ws.a1, B, 32, 20), _nchw(ws.a2, B, 64, 9), _nchw(ws.a3, B, 64, 7)
+            for name, inp, got, k, st in (("conv2", g1, g2, 2, 2), ("conv3", g2, g3, 4, 1)):
+                ref = F.relu(F.conv2d(inp, d(f[k].weight), d(f[k].bias), stride=st))
+                sc = F.conv2d(inp.abs(), d(f[k].weight).abs(), d(f[k].bias).abs(), stride=st)
+                errs[(name, v)] = float(((got - ref).abs() / sc.clamp_min(1e-30)).max())
+            hflat = g3.reshape(B, -1)
+            for name, lin, sl in (("fc1a", m.advantage[0], slice(0, 128)), ("fc1v", m.value[0], slice(128, 256))):
+                ref = F.relu(F.linear(hflat, d(lin.weight), d(lin.bias)))
+                sc = F.linear(hflat.abs(), d(lin.weight).abs(), d(lin.bias).abs())
+                errs[(name, v)] = float(((ws.h[:, sl].double() - ref).abs() / sc.clamp_min(1e-30)).max())
+    finally:
+        hip.f32_set_variant(10, 0)  # the default
+    for name in ("conv2", "conv3", "fc1a", "fc1v"):
+        e1, e0 = errs[(name, 1)], errs[(name, 0)]
+        assert e1 < 1e-6, (name, errs)
+        assert e1 <= 2.0 * e0 + 1e-7, (name, errs)
+
+
 def test_f32_frame_ring_and_multi_pass(cuda):
     """conv1 reading the HBM frame ring by id (rows picked by idx) == dense input, and the
     3-problem launch == three single launches (bit-identical)."""
