@@ -331,7 +331,10 @@ class PacketInbox:
         """Re-arm slot ``k`` (after its packet was applied) unless ``limit`` receives
         have been posted in total."""
         if not self.dead and (limit is None or self.n_posted < limit):
-            self._post(k)
+            try:
+                self._post(k)
+            except Exception as e:  # the peer died after its last packet landed: gloo's irecv
+                self.dead, self.error = True, repr(e)  # raises at post time ("Connection closed")
 
 
 class ParamLink:
@@ -483,6 +486,8 @@ class LearnerLinks:
             for r, k in ready:
                 self.applied[r] += 1
                 self.inbox[r].repost(k)
+                if self.inbox[r].dead:
+                    self.drop(r, f"re-posting a receive failed: {self.inbox[r].error}")
         return len(ready)
 
     def check_heartbeats(self, every: float = 1.0) -> None:

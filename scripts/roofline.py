@@ -31,7 +31,7 @@ def short(name):
 
 def model(name, wgs, B, E):
     """(flop, bytes) of one launch, or (None, None) if unmodelled."""
-    if "f32_conv1_fwd_k" in name or "conv1_fwd_k" in name:
+    if "conv1_fwd_k" in name or "conv1_fwd_x3_k" in name:
         return wgs * CONV1, None  # one workgroup per (problem, sample)
     if "Conv2Fwd" in name:
         return (3 * B if wgs > 1000 else E) * CONV2, None
