@@ -31,7 +31,9 @@ def short(name):
 
 def model(name, wgs, B, E):
     """(flop, bytes) of one launch, or (None, None) if unmodelled."""
-    if "conv1_fwd_k" in name or "conv1_fwd_x3_k" in name:
+    if "conv1_fwd_x3_k" in name:  # persistent: grid = min(samples, 512)
+        return (3 * B if wgs >= 512 else E) * CONV1, None
+    if "conv1_fwd_k" in name:
         return wgs * CONV1, None  # one workgroup per (problem, sample)
     if "Conv2Fwd" in name:
         return (3 * B if wgs > 1000 else E) * CONV2, None
