@@ -132,6 +132,17 @@ struct RowBOf<P, true> {
   using type = typename P::RowB;
 };
 
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs (b and b + 8 share an
+// L2), so with the identity order the N-tiles of one M-tile -- and neighbouring M-tiles,
+// whose im2col windows overlap -- land on different XCDs and each L2 fetches them again.
+// Chunked: XCD j walks the contiguous logical tiles [j G/8, (j+1) G/8) in order.  A pure
+// permutation of the tiles (bit-identical results); the tail past a multiple of 8 keeps
+// the identity.
+__device__ __forceinline__ int xcd_chunk(int b, int G) {
+  const int G8 = G & ~7;
+  return b >= G8 ? b : (b & 7) * (G8 >> 3) + (b >> 3);
+}
+
 template <class P, int PF = 1>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
@@ -505,17 +516,17 @@ __device__ __forceinline__ void gemm_body_x9(const typename P::Args& args, int b
 }
 
 template <class P>
-__global__ __launch_bounds__(256) void gemm_x9_k(typename P::Args args) {
+__global__ __launch_bounds__(256) void gemm_x9_k(typename P::Args args, int remap) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[GeoX9<P>::LDS_HALVES];
   __shared__ typename P::Smem sm;
-  gemm_body_x9<P>(args, blockIdx.x, lds, sm);
+  gemm_body_x9<P>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds, sm);
 }
 
 template <class P, int PF>
-__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
+__global__ __launch_bounds__(256) void gemm_k(typename P::Args args, int remap) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
-  gemm_body<P, PF>(args, blockIdx.x, lds, sm);
+  gemm_body<P, PF>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds, sm);
 }
 
 template <int A, int B>
@@ -1524,6 +1535,9 @@ SplitPlan wgrad_plan(int layer, int B) {
 // GEMM-body register prefetch depth (f32_set_variant(8, 1|2)); see gemm_body
 int g_pf_depth = 1;
 
+// XCD-chunked tile order for single-GEMM launches (f32_set_variant(11, 0|1)), see xcd_chunk
+int g_xcd = 1;
+
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
 
@@ -1532,13 +1546,13 @@ void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
   if constexpr (P::A_KMAJ && P::B_KMAJ && !HasColsum<P>::value) {
     if (g_x9) {
-      gemm_x9_k<P><<<blocks, 256, 0, s>>>(a);
+      gemm_x9_k<P><<<blocks, 256, 0, s>>>(a, g_xcd);
       LAUNCH_CHECK();
       return;
     }
   }
-  if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a);
-  else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a);
+  if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a, g_xcd);
+  else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a, g_xcd);
   LAUNCH_CHECK();
 }
 
@@ -1582,6 +1596,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 8 && v >= 1 && v <= 2) g_pf_depth = v;
   else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
   else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
+  else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 

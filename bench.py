@@ -117,6 +117,22 @@ def parse():
     return ap.parse_args()
 
 
+def _host_launch_cost(eng, device, n: int = 20) -> float:
+    """Median host time of one train_step enqueued into an idle GPU (extra, untimed steps)."""
+    import statistics
+
+    import torch
+
+    lat = []
+    for _ in range(n):
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        eng.train_step()
+        lat.append(time.perf_counter() - t1)
+    torch.cuda.synchronize(device)
+    return statistics.median(lat)
+
+
 def main():
     args = parse()
     import torch
@@ -213,6 +229,7 @@ def main():
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
+    host_launch = _host_launch_cost(eng, device)  # after the timed region
     dt = time.perf_counter() - t0
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
@@ -270,7 +287,10 @@ def main():
             "replay_bytes_per_gpu": eng.replay.nbytes(),
             "replay_live_transitions": int((eng.replay.leaf_sum > 0).sum().item()),
             "replay_slots_written": int(eng.replay.filled.item()),
+            # wall time of the enqueue loop: includes waiting on a full launch queue (back-pressure)
             "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
+            # one train_step's host cost with the GPU idle (no back-pressure), median of 20
+            "host_launch_ms_per_step": round(1000.0 * host_launch, 4),
             "stream_probe": eng.stream_probe,
             "last_loss": round(stats["loss"], 6),
             "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
