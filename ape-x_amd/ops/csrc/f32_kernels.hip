@@ -872,6 +872,45 @@ __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
 }
 
 constexpr int kC1xGrid = 512;  // two workgroups per CU
+constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
+
+// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on)
+__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer]) {
+  const int B = set.B, prob = smp / B, b = smp - prob * B, t = threadIdx.x;
+  const F32Prob p = pick(set, prob);
+  const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
+  const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
+  const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
+  const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
+  const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
+#pragma unroll
+  for (int k = 0; k < kC1xPer; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
+    const int e = min(t + 256 * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
+    const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
+    v[k] = sc[e - c * 441];
+  }
+}
+
+// registers -> LDS as bf16: chunk e = bf16 elements 16e .. 16e + 15 (7056 = 441 x 16)
+__device__ __forceinline__ void c1x_store(const uint4 (&v)[kC1xPer], uint32_t* xs) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kC1xPer; ++k) {
+    const int e = t + 256 * k;
+    if (e < kC1xChunks) {
+      const f32x4 a = u8x4(v[k].x), bq = u8x4(v[k].y), c = u8x4(v[k].z), d = u8x4(v[k].w);
+      uint4* dst = reinterpret_cast<uint4*>(xs) + 2 * e;
+      dst[0] = make_uint4(pack_bf16_hi(a[0], a[1]), pack_bf16_hi(a[2], a[3]), pack_bf16_hi(bq[0], bq[1]),
+                          pack_bf16_hi(bq[2], bq[3]));
+      dst[1] = make_uint4(pack_bf16_hi(c[0], c[1]), pack_bf16_hi(c[2], c[3]), pack_bf16_hi(d[0], d[1]),
+                          pack_bf16_hi(d[2], d[3]));
+    }
+  }
+}
+
+// Software-pipelined over the workgroup's samples: the next sample's frame chunks are
+// loaded into registers before this sample's MFMA loop, so the frame-ring (HBM) latency
+// hides behind compute; they are converted into LDS after the loop.
 __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
   const int B = set.B, total = set.n * B;
@@ -881,7 +920,13 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   W1Split w;
   float bias = 0.f;
   int cur = -1;
-  for (int smp = blockIdx.x; smp < total; smp += gridDim.x) {
+  uint4 v[kC1xPer];
+  // a contiguous run of samples per workgroup: the weight split is redone only at a
+  // problem boundary (a grid-strided walk crossed one at every sample: ~25 % of the VALU)
+  const int per = (total + gridDim.x - 1) / gridDim.x;
+  const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
+  if (s0 < s1) c1x_load(set, s0, v);
+  for (int smp = s0; smp < s1; ++smp) {
     const int prob = smp / B, b = smp - prob * B;
     const F32Prob p = pick(set, prob);
     if (prob != cur) {  // block-uniform
@@ -890,34 +935,9 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       bias = p.bias[nh * 16 + i];
     }
     __syncthreads();  // the previous sample's tiles are done with xs
-    {  // stage: 4 x 441 16-byte u8 chunks -> 32-byte bf16 runs, all loads in flight first
-      const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
-      constexpr int kChunks = 4 * (kPlane / 16), kPer = (kChunks + 255) / 256;
-      const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
-      const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
-      const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
-      const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
-      uint4 v[kPer];
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        const int e = min(t + 256 * k, kChunks - 1), c = e / 441;
-        const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
-        v[k] = sc[e - c * 441];
-      }
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        const int e = t + 256 * k;
-        if (e < kChunks) {  // chunk e = bf16 elements 16e .. 16e + 15 (7056 = 441 x 16)
-          const f32x4 a = u8x4(v[k].x), bq = u8x4(v[k].y), c = u8x4(v[k].z), d = u8x4(v[k].w);
-          uint4* dst = reinterpret_cast<uint4*>(xs) + 2 * e;
-          dst[0] = make_uint4(pack_bf16_hi(a[0], a[1]), pack_bf16_hi(a[2], a[3]), pack_bf16_hi(bq[0], bq[1]),
-                              pack_bf16_hi(bq[2], bq[3]));
-          dst[1] = make_uint4(pack_bf16_hi(c[0], c[1]), pack_bf16_hi(c[2], c[3]), pack_bf16_hi(d[0], d[1]),
-                              pack_bf16_hi(d[2], d[3]));
-        }
-      }
-    }
+    c1x_store(v, xs);
     __syncthreads();
+    if (smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
     float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + i;
     for (int tile = wave & 1; tile < 25; tile += 2) {
       const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
@@ -1586,6 +1606,8 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // gradient only, 2 input gradient only), g_dgrad_variant (0 position-major, 1 sample-major)
 int g_bwd_mode = 0, g_dgrad_variant = 0;
 // conv1 weight gradient (knob 9): 0 = fp32 MFMA (f32_conv1_wgrad_k), 1 = exact-split bf16 MFMA
+// (f32_conv1_wgrad_x3_k).  A variant splitting dy once per element into LDS (instead of in
+// each channel wave) measured 27.4 vs 26.0 us: the split VALU is not what bounds it.
 int g_conv1_wgrad_variant = 1;
 
 void f32_set_variant(int layer, int v) {
