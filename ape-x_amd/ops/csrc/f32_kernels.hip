@@ -720,7 +720,7 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
   }
 };
 
-constexpr int kFcSplits = 7;  // FC1 forward split-K: 3136 = 7 x 448
+constexpr int kFcSplits = 7;  // FC1 forward split-K: 3136 = 7 x 448 (14 splits: FC1 34.6 -> 30.9 us but the heads kernel reduces twice the slabs: step neutral)
 template <int BM_, int BN_, int BK_, int WM_>
 struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k' = p*64 + c
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
