@@ -162,7 +162,8 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     for (int j = 0; j < G::TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  f32x4 ra[PF][G::NA], rb[PF][G::NB];
+  constexpr int NSET = PF == 2 ? 2 : 1;
+  f32x4 ra[NSET][G::NA], rb[NSET][G::NB];
   f32x4 csum = zero4();
   typename RowAOf<P>::type rowa[G::NA];
   typename RowBOf<P>::type rowb[G::NB];
@@ -220,7 +221,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
   };
   using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, PF - 1>;
+  using S1 = std::integral_constant<int, NSET - 1>;
   auto compute = [&](int buf) {
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
@@ -259,7 +260,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 
   int kb = ctx.kb0;
   int cur = 0;
-  if constexpr (PF == 1) {
+  if constexpr (PF == 1 || PF == 3) {  // 3: depth 1 with the MFMA block fenced from the store
     if (kb < ctx.kb1) {
       gload(kb, S0{});
       sstore(0, S0{});
@@ -270,6 +271,10 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
       if (more) gload(kb + 1, S0{});
       __builtin_amdgcn_sched_barrier(0);
       compute(cur);
+      // every MFMA of the block is issued before the LDS store waits on the next block's
+      // global loads: unfenced, the scheduler sank half of them below the store + barrier,
+      // leaving only ~512 MFMA cycles to cover the L2 / MALL load latency
+      if constexpr (PF == 3) __builtin_amdgcn_sched_barrier(0);
       if (more) sstore(cur ^ 1, S0{});
       __syncthreads();
       cur ^= 1;
@@ -1572,6 +1577,7 @@ void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
     }
   }
   if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a, g_xcd);
+  else if (g_pf_depth == 3) gemm_k<P, 3><<<blocks, 256, 0, s>>>(a, g_xcd);
   else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a, g_xcd);
   LAUNCH_CHECK();
 }
@@ -1580,6 +1586,7 @@ template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
   if (g_pf_depth == 2) gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else if (g_pf_depth == 3) gemm2_k<P1, P2, 3><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   else gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
@@ -1615,7 +1622,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 5 && v >= 0 && v <= 2) g_bwd_mode = v;
   else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
   else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
-  else if (layer == 8 && v >= 1 && v <= 2) g_pf_depth = v;
+  else if (layer == 8 && v >= 1 && v <= 3) g_pf_depth = v;
   else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
   else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
