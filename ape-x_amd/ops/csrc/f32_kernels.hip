@@ -639,7 +639,8 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
     return ld4(c.p.w + (c.n0 + n) * 512 + kb * BK + 4 * ch);
   }
-  // row states (BK = 32: a k-block is exactly one tap, 4*ch its channel chunk)
+  // row states (32 % BK == 0: a k-block lies inside one tap; 4*ch is the chunk's channel
+  // offset within the block, the block's tap / channel base is wave-uniform)
   struct RowA {
     const float* p;  // sample / window origin + channel chunk; nullptr past the last row
   };
@@ -647,15 +648,15 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
     const float* p;
   };
   static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
-    static_assert(BK == 32, "one tap per k-block");
+    static_assert(32 % BK == 0, "a k-block inside one tap");
     const int m = c.m0 + row;
     if (m >= c.M) return {nullptr};
     const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9;
     return {static_cast<const float*>(c.p.in) + ((size_t)b * 400 + 2 * oy * 20 + 2 * ox) * 32 + 4 * ch};
   }
   static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    const int ky = kb >> 2, kx = kb & 3;  // tap = kb (wave-uniform)
-    return r.p ? ld4(r.p + (ky * 20 + kx) * 32) : zero4();
+    const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;  // wave-uniform
+    return r.p ? ld4(r.p + (ky * 20 + kx) * 32 + (k0 & 31)) : zero4();
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 512 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
@@ -699,7 +700,7 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
     return ld4(c.p.w + (c.n0 + n) * 576 + kb * BK + 4 * ch);
   }
-  // row states (BK = 32: tap = kb >> 1, channel half (kb & 1) * 32, chunk 4*ch)
+  // row states (64 % BK == 0: a k-block lies inside one tap of 64 channels, chunk 4*ch)
   struct RowA {
     const float* p;
   };
@@ -707,15 +708,15 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
     const float* p;
   };
   static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
-    static_assert(BK == 32, "two k-blocks per tap");
+    static_assert(64 % BK == 0, "a k-block inside one tap");
     const int m = c.m0 + row;
     if (m >= c.M) return {nullptr};
     const int b = m / 49, p = m - b * 49, oy = p / 7, ox = p - oy * 7;
     return {static_cast<const float*>(c.p.in) + ((size_t)b * 81 + oy * 9 + ox) * 64 + 4 * ch};
   }
   static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
-    return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (kb & 1) * 32) : zero4();
+    const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
+    return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (k0 & 63)) : zero4();
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 576 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
@@ -1562,6 +1563,9 @@ int g_pf_depth = 1;
 
 // XCD-chunked tile order for single-GEMM launches (f32_set_variant(11, 0|1)), see xcd_chunk
 int g_xcd = 1;
+// conv2 / conv3 forward tiles with BK = 16 (f32_set_variant(12, 0|1)): 25.6 KB of LDS per
+// workgroup -> 6 per CU instead of 3, twice the barriers per FLOP
+int g_fwd_bk16 = 0;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1626,6 +1630,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
   else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
+  else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1646,8 +1651,14 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
         LAUNCH_CHECK();
       }
       break;
-    case 2: fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s); break;
-    case 3: fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s); break;
+    case 2:
+      if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
+      else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
+      break;
+    case 3:
+      if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
+      else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
+      break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
   }
 }
