@@ -203,32 +203,26 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
 }
 
 // Recompute levels lo..hi of the dirty paths of `ids` (run order, staged in LDS) inside
-// ONE workgroup: each wave checks 64 candidates at once (lane-parallel run detection,
-// ballot) and recomputes the first-of-run nodes; level-synchronous via the barrier.
-// Only this workgroup reads what it wrote, so the barrier (workgroup-scope release /
-// acquire) orders the levels for workgroup-scope loads.  A device-scope __threadfence
-// per level wrote the XCD L2 back each time.
+// ONE workgroup: candidate w goes to wave w % nw (strided, so a small batch still spreads
+// over every wave; blocks of 64 per wave put a 32-row batch's whole walk on wave 0), which
+// recomputes its ancestor if it is the first of its run.  Level-synchronous: only this
+// workgroup reads what it wrote, so the barrier (workgroup-scope release / acquire) orders
+// the levels for workgroup-scope loads.  A device-scope __threadfence per level wrote the
+// XCD L2 back each time.
 __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int* sids, int B, int lo, int hi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int level = lo; level <= hi; ++level) {
     __syncthreads();
     const int shift = kTreeLog2Fanout * level;
-    for (int base = wave * 64; base < B; base += nw * 64) {  // wave-uniform
-      const int w = base + lane;
-      const int id = w < B ? sids[w] : -1;
-      const bool ok = id >= 0 && id < t.size[0];
-      const int node = ok ? id >> shift : -1;
-      bool first = ok;
-      if (ok && w > 0) {
+    for (int w = wave; w < B; w += nw) {  // wave-uniform
+      const int id = sids[w];
+      if (id < 0 || id >= t.size[0]) continue;
+      const int node = id >> shift;
+      if (w > 0) {
         const int prev = sids[w - 1];
-        if (prev >= 0 && prev < t.size[0] && (prev >> shift) == node) first = false;
+        if (prev >= 0 && prev < t.size[0] && (prev >> shift) == node) continue;
       }
-      unsigned long long m = __ballot(first);
-      while (m) {
-        const int k = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        recompute_node<__HIP_MEMORY_SCOPE_WORKGROUP>(t, level, __shfl(node, k, 64), lane);
-      }
+      recompute_node<__HIP_MEMORY_SCOPE_WORKGROUP>(t, level, node, lane);
     }
   }
 }
@@ -484,6 +478,9 @@ void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStr
   int last_big = 0;
   for (int lv = 1; lv <= t.levels; ++lv)
     if (t.size[lv] > 64) last_big = lv;
+  // a small batch (<= 64 dirty paths, e.g. AQL's 32-sample learner write) walks every level
+  // inside the leaves workgroup: cheaper than the wide launches + ticketed top levels
+  if (n <= 64) last_big = 0;
   per_batch_leaves_k<<<1, 1024, 0, s>>>(t, w, last_big == 0 ? 1 : 0);
   LAUNCH_CHECK();
   if (last_big == 0) return;
