@@ -22,6 +22,7 @@ namespace apex {
 constexpr int AQ_H = 64;        // hidden units of q_feature / action_out / advantage1
 constexpr int AQ_CAT = 128;     // concat width
 constexpr int AQ_PITCH = 129;   // LDS row pitch (floats) for 128-wide rows
+constexpr int kAqGroup = 8;     // candidates per work item of aql_candidate_q_k
 
 // workspace layout (floats): W1eff [64][128] | b1eff [64] | w2eff [64] | b2eff [1]
 size_t aql_workspace_floats() { return AQ_H * AQ_CAT + AQ_H + AQ_H + 1; }
@@ -59,9 +60,12 @@ __global__ __launch_bounds__(256) void aql_candidate_q_k(AQLNet net, const float
   const float* b1eff = ws + AQ_H * AQ_CAT;
   const float* w2eff = b1eff + AQ_H;
   const float b2eff = w2eff[AQ_H];
-  const int T = net.T, total = B * T;
-  for (int c = blockIdx.x * 4 + wave; c < total; c += gridDim.x * 4) {  // wave-uniform loop
-    const int b = c / T;
+  // work item = (state b, group of kAqGroup candidates): the state's q_feature and the state
+  // half of advantage1 (its input is [action_out | q_feature]) are computed once per item, not
+  // once per candidate (they do not depend on the action: ~45 % of a candidate's MACs)
+  const int T = net.T, ng = (T + kAqGroup - 1) / kAqGroup, items = B * ng;
+  for (int it = blockIdx.x * 4 + wave; it < items; it += gridDim.x * 4) {  // wave-uniform loop
+    const int b = it / ng, t0 = (it - b * ng) * kAqGroup, t1 = min(T, t0 + kAqGroup);
     const float* s = state + (size_t)b * net.obs;
     // q_feature: obs -> 64 -> 64 (ReLU both)
     float acc = net.qf_b1[lane];
@@ -72,34 +76,41 @@ __global__ __launch_bounds__(256) void aql_candidate_q_k(AQLNet net, const float
 #pragma unroll 8
     for (int j = 0; j < AQ_H; ++j) acc += qf2s[lane * (AQ_H + 1) + j] * hbuf[wave][j];
     xbuf[wave][AQ_H + lane] = fmaxf(acc, 0.f);
-    // action encoder
-    if (net.cont) {
-      const float* a = a_mu + (size_t)c * net.adim;
-      float h0 = net.ao_b1[lane], h1 = net.ao_b1[lane + 64];
-      for (int d = 0; d < net.adim; ++d) {
-        const float ad = a[d];
-        h0 += net.ao_w1[lane * net.adim + d] * ad;
-        h1 += net.ao_w1[(lane + 64) * net.adim + d] * ad;
+    __builtin_amdgcn_wave_barrier();
+    float sadv = b1eff[lane];  // advantage1 bias + its state half
+#pragma unroll 8
+    for (int j = 0; j < AQ_H; ++j) sadv += w1s[lane * AQ_PITCH + AQ_H + j] * xbuf[wave][AQ_H + j];
+    for (int t = t0; t < t1; ++t) {
+      const int c = b * T + t;
+      // action encoder
+      if (net.cont) {
+        const float* a = a_mu + (size_t)c * net.adim;
+        float h0 = net.ao_b1[lane], h1 = net.ao_b1[lane + 64];
+        for (int d = 0; d < net.adim; ++d) {
+          const float ad = a[d];
+          h0 += net.ao_w1[lane * net.adim + d] * ad;
+          h1 += net.ao_w1[(lane + 64) * net.adim + d] * ad;
+        }
+        __builtin_amdgcn_wave_barrier();
+        hbuf[wave][lane] = fmaxf(h0, 0.f);
+        hbuf[wave][lane + 64] = fmaxf(h1, 0.f);
+        __builtin_amdgcn_wave_barrier();
+        acc = net.ao_b2[lane];
+#pragma unroll 8
+        for (int j = 0; j < AQ_CAT; ++j) acc += ao2s[lane * AQ_PITCH + j] * hbuf[wave][j];
+        xbuf[wave][lane] = fmaxf(acc, 0.f);
+      } else {
+        xbuf[wave][lane] = fmaxf(net.ao_w1[lane] * a_mu[c] + net.ao_b1[lane], 0.f);
       }
       __builtin_amdgcn_wave_barrier();
-      hbuf[wave][lane] = fmaxf(h0, 0.f);
-      hbuf[wave][lane + 64] = fmaxf(h1, 0.f);
+      // advantage1 (NoisyLinear 128 -> 64): the action half on top of the state half; advantage2 (64 -> 1)
+      acc = sadv;
+#pragma unroll 8
+      for (int j = 0; j < AQ_H; ++j) acc += w1s[lane * AQ_PITCH + j] * xbuf[wave][j];
+      const float qv = wave_sum(w2eff[lane] * fmaxf(acc, 0.f)) + b2eff;
+      if (lane == 0) q[c] = qv;
       __builtin_amdgcn_wave_barrier();
-      acc = net.ao_b2[lane];
-#pragma unroll 8
-      for (int j = 0; j < AQ_CAT; ++j) acc += ao2s[lane * AQ_PITCH + j] * hbuf[wave][j];
-      xbuf[wave][lane] = fmaxf(acc, 0.f);
-    } else {
-      xbuf[wave][lane] = fmaxf(net.ao_w1[lane] * a_mu[c] + net.ao_b1[lane], 0.f);
     }
-    __builtin_amdgcn_wave_barrier();
-    // advantage1 (NoisyLinear 128 -> 64) + ReLU, advantage2 (64 -> 1)
-    acc = b1eff[lane];
-#pragma unroll 8
-    for (int j = 0; j < AQ_CAT; ++j) acc += w1s[lane * AQ_PITCH + j] * xbuf[wave][j];
-    const float qv = wave_sum(w2eff[lane] * fmaxf(acc, 0.f)) + b2eff;
-    if (lane == 0) q[c] = qv;
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -213,8 +224,8 @@ void aql_candidate_q(const AQLNet& net, float* ws, const float* state, const flo
   const int n = (int)aql_workspace_floats();
   aql_noisy_eff_k<<<(n + 255) / 256, 256, 0, s>>>(net, ws);
   LAUNCH_CHECK();
-  const int total = B * net.T;
-  const int grid = std::min((total + 3) / 4, 512);
+  const int items = B * ((net.T + kAqGroup - 1) / kAqGroup);
+  const int grid = std::min((items + 3) / 4, 512);
   aql_candidate_q_k<<<grid, 256, 0, s>>>(net, ws, state, a_mu, B, q);
   LAUNCH_CHECK();
 }
