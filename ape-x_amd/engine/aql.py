@@ -313,13 +313,14 @@ class AQLLearner:
                           self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
                           r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), s)
         h.aql_grad(self.G, s)
-        Pq = self.P_q
-        h.adam_step(self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
-                    self.part.data_ptr(), self.nblk, self.hp, self.step_ctr.data_ptr(), self.norms_q.data_ptr(), s)
-        o = 4 * Pq
-        h.adam_step(self.flat.data_ptr() + o, self.grad.data_ptr() + o, self.m.data_ptr() + o, self.v.data_ptr() + o,
-                    self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk, self.hp, self.step_ctr.data_ptr(),
-                    self.norms_p.data_ptr(), s)
+        Pq, o = self.P_q, 4 * self.P_q
+        # the two optimizers (critic, proposal; own clip norms) in one launch
+        h.adam_step2((self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
+                      self.part.data_ptr(), self.nblk, self.norms_q.data_ptr()),
+                     (self.flat.data_ptr() + o, self.grad.data_ptr() + o, self.m.data_ptr() + o,
+                      self.v.data_ptr() + o, self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk,
+                      self.norms_p.data_ptr()),
+                     self.hp, self.step_ctr.data_ptr(), s)
         h.aql_post(self.post, 1, s)
 
     def sync_target(self) -> None:

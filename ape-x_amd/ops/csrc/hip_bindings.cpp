@@ -269,6 +269,15 @@ PYBIND11_MODULE(_apex_hip, m) {
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
      py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
+  m.def("adam_step2", [](std::array<uint64_t, 8> a, std::array<uint64_t, 8> b, const AdamParams& hp, uint64_t step,
+                         uint64_t s) {
+    // (p, g, m, v, n, partials, n_partials, norms) per set
+    auto mk = [](const std::array<uint64_t, 8>& t) {
+      return OptSet{P<float>(t[0]), P<const float>(t[1]), P<float>(t[2]), P<float>(t[3]), (int64_t)t[4],
+                    P<const double>(t[5]), (int)t[6], P<float>(t[7]), 0};
+    };
+    adam_step2(mk(a), mk(b), hp, P<const int64_t>(step), S(s));
+  });
   // ---- network kernels
   m.def("conv_fwd", [](int layer, uint64_t in, uint64_t ids, uint64_t idx, uint64_t wp, uint64_t bias, uint64_t out,
                        int B, uint64_t s) {

@@ -240,6 +240,19 @@ struct AdamParams {
   int lr_step_size, lr_step_offset;
   float grad_scale = 1.f;
 };
+// one parameter set of a fused two-set optimizer launch (adam_step2)
+struct OptSet {
+  float* p;
+  const float* g;
+  float* s1;
+  float* s2;
+  int64_t n;
+  const double* partials;
+  int n_partials;
+  float* norms_out;
+  int nblk;  // set by the launcher
+};
+void adam_step2(OptSet a, OptSet b, const AdamParams& hp, const int64_t* step, hipStream_t s);
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
                const AdamParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
                const PackMap* pack = nullptr, const FcPack* fc = nullptr);

@@ -222,26 +222,26 @@ __device__ __forceinline__ AdamRule make_rule(const AdamParams& hp, int64_t st, 
   return AdamRule{hp.beta1, hp.beta2, hp.eps, hp.weight_decay, lr / bc1, 1.f / sqrtf(bc2)};
 }
 
+// The update of one parameter set by workgroup `bid` of `nblk` (opt_step_k: the whole grid;
+// opt_step2_k: two sets split at a block-uniform boundary).
 template <class Params>
-__global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p, const float* __restrict__ g,
-                                                          float* __restrict__ s1, float* __restrict__ s2, int64_t n,
-                                                          const double* __restrict__ partials, int n_partials,
-                                                          Params hp, const int64_t* __restrict__ step,
-                                                          float* __restrict__ norms_out, PackMap pk, FcPack fc,
-                                                          int n_fc_blocks) {
+__device__ __forceinline__ void opt_body(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s1,
+                                         float* __restrict__ s2, int64_t n, const double* __restrict__ partials,
+                                         int n_partials, const Params& hp, const int64_t* __restrict__ step,
+                                         float* __restrict__ norms_out, const PackMap& pk, const FcPack& fc,
+                                         int n_fc_blocks, int bid, int nblk) {
   const float max_norm = hp.max_norm;
   float lr;
   const auto rule = make_rule(hp, step ? step[0] : 0, lr);
   auto norms = [&]() {
     const NormInfo ni = reduce_norms(partials, n_partials, max_norm, hp.grad_scale);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && norms_out) {
+    if (bid == 0 && threadIdx.x == 0 && norms_out) {
       norms_out[0] = ni.l2;
       norms_out[2] = fminf(max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f, 1.f);
       norms_out[3] = lr;
     }
     return ni;
   };
-  const int bid = blockIdx.x;
   if (bid < n_fc_blocks) {
     __shared__ uint16_t tile[kFcTn][kFcTc * kFcP];
     __shared__ float tile_f[kFcTn][kFcTc * kFcP];
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
   }
   // generic part: every element outside the FC1 ranges, scalar, through the scatter maps
   const NormInfo ni = norms();
-  const int gb = bid - n_fc_blocks, ngb = gridDim.x - n_fc_blocks;
+  const int gb = bid - n_fc_blocks, ngb = nblk - n_fc_blocks;
   const int64_t stride = (int64_t)ngb * kOptThreads;
   int64_t lo[3], hi[3];
   int nr = 0;
@@ -330,6 +330,28 @@ __global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p,
   for (int k = 0; k < nr; ++k)
     for (int64_t i = lo[k] + (int64_t)gb * kOptThreads + threadIdx.x; i < hi[k]; i += stride)
       opt_elem(p, g, s1, s2, i, ni.clip, rule, pk);
+}
+
+template <class Params>
+__global__ __launch_bounds__(kOptThreads) void opt_step_k(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ s1, float* __restrict__ s2, int64_t n,
+                                                          const double* __restrict__ partials, int n_partials,
+                                                          Params hp, const int64_t* __restrict__ step,
+                                                          float* __restrict__ norms_out, PackMap pk, FcPack fc,
+                                                          int n_fc_blocks) {
+  opt_body(p, g, s1, s2, n, partials, n_partials, hp, step, norms_out, pk, fc, n_fc_blocks, blockIdx.x, gridDim.x);
+}
+
+// Two independent parameter sets (own partials, norms, clip) in ONE launch: blocks
+// [0, a.nblk) update set a, the rest set b (AQL: critic + proposal Adam, AQL_dis.py).
+template <class Params>
+__global__ __launch_bounds__(kOptThreads) void opt_step2_k(OptSet a, OptSet b, Params hp,
+                                                           const int64_t* __restrict__ step) {
+  const bool second = (int)blockIdx.x >= a.nblk;  // block-uniform
+  const OptSet& o = second ? b : a;
+  opt_body(o.p, o.g, o.s1, o.s2, o.n, o.partials, o.n_partials, hp, step, o.norms_out,
+           PackMap{nullptr, nullptr, nullptr, nullptr}, FcPack{}, 0, second ? (int)blockIdx.x - a.nblk : (int)blockIdx.x,
+           o.nblk);
 }
 
 template <class Params>
@@ -362,6 +384,17 @@ void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, c
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
                   const PackMap* pack, const FcPack* fc) {
   launch_opt(p, g, sq, gavg, n, partials, n_partials, hp, step, norms_out, pack, fc, s);
+}
+
+void adam_step2(OptSet a, OptSet b, const AdamParams& hp, const int64_t* step, hipStream_t s) {
+  auto blocks = [](int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n + 4 * kOptThreads - 1) / (4 * kOptThreads), kOptGenBlocksMax));
+  };
+  if (a.n <= 0 || b.n <= 0) throw std::invalid_argument("adam_step2: both sets must be non-empty");
+  a.nblk = blocks(a.n);
+  b.nblk = blocks(b.n);
+  opt_step2_k<AdamParams><<<a.nblk + b.nblk, kOptThreads, 0, s>>>(a, b, hp, step);
+  LAUNCH_CHECK();
 }
 
 void adam_step(float* p, const float* g, float* m, float* v, int64_t n, const double* partials, int n_partials,
