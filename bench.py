@@ -229,8 +229,9 @@ def main():
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
-    host_launch = _host_launch_cost(eng, device)  # after the timed region
+    torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
+    host_launch = _host_launch_cost(eng, device)  # extra untimed steps after the timed region
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
