@@ -1566,6 +1566,13 @@ int g_xcd = 1;
 // conv2 / conv3 forward tiles with BK = 16 (f32_set_variant(12, 0|1)): 25.6 KB of LDS per
 // workgroup -> 6 per CU instead of 3, twice the barriers per FLOP
 int g_fwd_bk16 = 0;
+// FC1 forward tile (f32_set_variant(13, 0..2)): 0 = 128 x 64 (2 x 2 waves of 64 x 32),
+// 1 = 64 x 64 (2 x 2 waves of 32 x 32), 2 = 128 x 32 (4 x 1 waves of 32 x 32); 1 and 2 give
+// twice the workgroups (672 per 3 x 512 rows) at half the LDS
+int g_fc1_tile = 1;  // measured: FC1 fwd 36.9 -> 31.6 us, bench 1885 -> 1933 steps/s
+// conv2 / conv3 forward tile (f32_set_variant(14, 0..1)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
+// every A row staged once, 2 x 2 waves of 32 x 32)
+int g_conv_tile = 0;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1631,6 +1638,8 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
   else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
+  else if (layer == 13 && v >= 0 && v <= 2) g_fc1_tile = v;
+  else if (layer == 14 && v >= 0 && v <= 1) g_conv_tile = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1653,10 +1662,12 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
       break;
     case 2:
       if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
+      else if (g_conv_tile == 1) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
       if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
+      else if (g_conv_tile == 1) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
@@ -1667,7 +1678,9 @@ int f32_fc1_splits() { return kFcSplits; }
 
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
-  fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
+  if (g_fc1_tile == 1) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
+  else if (g_fc1_tile == 2) fwd_launch<Fc1FwdT<128, 32, 32, 4>>(set, s);
+  else fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
   return kFcSplits;
 }
 
