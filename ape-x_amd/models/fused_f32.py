@@ -147,6 +147,10 @@ class F32DuelingNet:
         self._wgrad_wss = [torch.empty(h.f32_wgrad_workspace_floats(k, B), dtype=torch.float32, device=self.device)
                            for k in (1, 2, 3)]
         self._heads_ws = torch.empty(h.heads_wgrad_workspace_floats(self.A), dtype=torch.float32, device=self.device)
+        # FC1 weight gradient in batch slices (knob 15; 0 = one in-place pass without finalize)
+        self._fc1_G = h.f32_fc1_wgrad_slices(B) if h.f32_fc1_wgrad_splits() > 0 else 0
+        self._fc1_ws = (torch.empty(h.f32_fc1_wgrad_workspace_floats(), dtype=torch.float32, device=self.device)
+                        if self._fc1_G else None)
         self._ws_B = B
 
     # ------------------------------------------------------------------ forward
@@ -196,10 +200,20 @@ class F32DuelingNet:
                                            m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
                                            m.value[0].bias.grad.data_ptr())
 
-    def _fc1_bwd(self, ws: F32Workspace) -> None:
+    def _fc1_bwd(self, ws: F32Workspace) -> list:
+        """FC1 dgrad + weight gradient; returns the finalize jobs that complete the weight
+        gradient (sliced mode: sum the slices + transpose to the reference layout, with
+        their sum-of-squares partials), or [] when it was written in place."""
         m = self.model
+        ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+        if self._fc1_G:
+            self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
+                                       self._fc1_ws.data_ptr(), ws.B, self._s())
+            return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
+                    self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
         self.hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
-                             m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(), ws.B, self._s())
+                             ga.data_ptr(), gv.data_ptr(), ws.B, self._s())
+        return []
 
     def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None) -> list:
         """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch); returns the
@@ -223,9 +237,9 @@ class F32DuelingNet:
         place) + the finalize of ``extra_jobs`` (the heads), so the FC1/head all-reduce can
         start while :meth:`conv_backward` runs."""
         self.enable_backward(ws.B)
-        self._fc1_bwd(ws)
-        if extra_jobs:
-            self.hip.grad_finalize(list(extra_jobs), self._s(), 0)
+        jobs = self._fc1_bwd(ws) + list(extra_jobs)
+        if jobs:
+            self.hip.grad_finalize(jobs, self._s(), 0)
 
     def conv_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
                       idx: torch.Tensor | None = None, after_first=None) -> None:
@@ -241,13 +255,13 @@ class F32DuelingNet:
         given (the FC1 weight gradients, written in place, join through norm-only jobs);
         returns the partial count.  ``after_first()`` runs right after the first launch."""
         self.enable_backward(ws.B)
-        self._fc1_bwd(ws)
+        fc1_jobs = self._fc1_bwd(ws)
         if after_first is not None:
             after_first()
         h, m = self.hip, self.model
         ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
-        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs)
-        if sumsq is not None:
+        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs) + fc1_jobs
+        if sumsq is not None and not fc1_jobs:  # in-place FC1 grads join through norm-only jobs
             jobs += [h.norm_only_job(ga.data_ptr(), ga.numel()), h.norm_only_job(gv.data_ptr(), gv.numel())]
         return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr())
 

@@ -782,6 +782,14 @@ FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, fl
   return j;
 }
 
+FinalizeJob f32_fc1_finalize_job(int half, int G, const float* ws, float* grad) {
+  // fp32 learner: G batch slices of FC1 weight-gradient partials [G][256][p*64 + c]
+  // (f32_fc1_bwd_split) -> reference [n][c*49 + p], same row-transpose job as the bf16 slabs
+  FinalizeJob j = fc1_finalize_job(half, ws, grad);
+  j.G = G;
+  return j;
+}
+
 FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad) {
   // [G][256][7*7*64] natural (p, c) order -> reference [n][c*49 + p] (row-transpose job)
   constexpr int K = 49 * 64;

@@ -1015,19 +1015,27 @@ struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
 };
 
 struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the reference [n][c*49 + p]
+  // a.splits > 0: the batch is split into a.splits slices of a.kbps k-blocks (196 tiles per
+  // slice) and each slice writes its partial in the natural [n][p*64 + c] order to
+  // a.out[slice][256][3136]; grad_finalize's FC1 row job sums the slices in a fixed order and
+  // transposes (f32_fc1_finalize_job).  a.splits == 0: one pass, the reference-layout grads
+  // written in place (a.out = advantage rows, a.out2 = value rows).
   static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
   static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false;
   using Args = BwdArgs;
   using Smem = NoSmem;
   struct Ctx {
-    int m0, n0, kb0, kb1;
+    int m0, n0, kb0, kb1, split;
   };
   static __host__ __device__ int tiles(int) { return 4 * 49; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
-    c.n0 = (block % 49) * BN;
-    c.m0 = (block / 49) * BM;
-    c.kb0 = 0;
-    c.kb1 = (a.B + BK - 1) / BK;
+    const int t = block % (4 * 49);
+    c.split = block / (4 * 49);
+    c.n0 = (t % 49) * BN;
+    c.m0 = (t / 49) * BM;
+    const int nkb = (a.B + BK - 1) / BK;
+    c.kb0 = a.splits > 0 ? c.split * a.kbps : 0;
+    c.kb1 = a.splits > 0 ? min(nkb, c.kb0 + a.kbps) : nkb;
   }
   static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int b = kb * BK + row;
@@ -1040,8 +1048,13 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
     return ld4(static_cast<const float*>(a.x) + (size_t)b * 3136 + c.n0 + 4 * ch);
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
+    const int n = c.m0 + ml, k = c.n0 + nl;
+    if (a.splits > 0) {  // coalesced natural-order partial
+      a.out[((size_t)c.split * 256 + n) * 3136 + k] = v;
+      return;
+    }
     // scattered stores (write-combined in L2) instead of gathered operand loads
-    const int n = c.m0 + ml, k = c.n0 + nl, ref = (k & 63) * 49 + (k >> 6);
+    const int ref = (k & 63) * 49 + (k >> 6);
     if (n < 128) a.out[n * 3136 + ref] = v;
     else a.out2[(n - 128) * 3136 + ref] = v;
   }
@@ -1573,6 +1586,13 @@ int g_fc1_tile = 1;  // measured: FC1 fwd 36.9 -> 31.6 us, bench 1885 -> 1933 st
 // conv2 / conv3 forward tile (f32_set_variant(14, 0..1)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
 // every A row staged once, 2 x 2 waves of 32 x 32)
 int g_conv_tile = 0;
+// FC1 weight gradient batch slices (f32_set_variant(15, 0..4)): 0 = one pass writing the
+// reference-layout grads in place; G > 0 = G slices of natural-order partials reduced and
+// transposed by grad_finalize (4 x 49 x G workgroups instead of 4 x 49 beside the dgrad's 8 x 49).
+// Measured (bench.py, 2000 steps): 0: 1931 / 1931, 1: 1947, 2: 1929 / 1932, 4: 1892 steps/s --
+// more slices do not pay for the partial traffic; ONE slice wins by its coalesced natural-order
+// stores (the transpose moves into the finalize job that also takes the FC1 norm partials)
+int g_fc1_wg_splits = 1;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1640,6 +1660,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
   else if (layer == 13 && v >= 0 && v <= 2) g_fc1_tile = v;
   else if (layer == 14 && v >= 0 && v <= 1) g_conv_tile = v;
+  else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1699,7 +1720,40 @@ void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy
   w.out = g_adv;
   w.out2 = g_val;
   w.B = B;
+  w.splits = 0;
   launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B), d, Fc1Dgrad::tiles(B), s);
+}
+
+int f32_fc1_wgrad_splits() { return g_fc1_wg_splits; }
+
+size_t f32_fc1_wgrad_workspace_floats() { return (size_t)std::max(1, g_fc1_wg_splits) * 256 * 3136; }
+
+void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
+                       hipStream_t s) {
+  if (B <= 0) return;
+  if (g_fc1_wg_splits < 1) throw std::invalid_argument("f32_fc1_bwd_split: FC1 wgrad slices are off (knob 15 = 0)");
+  BwdArgs d{};
+  d.dy = dz;
+  d.w = wfc1p;
+  d.mask = a3;
+  d.out = dy3;
+  d.B = B;
+  BwdArgs w{};
+  w.x = a3;
+  w.dy = dz;
+  w.out = ws;
+  w.B = B;
+  const int nkb = (B + Fc1Wgrad::BK - 1) / Fc1Wgrad::BK;
+  w.splits = std::min(g_fc1_wg_splits, nkb);
+  w.kbps = (nkb + w.splits - 1) / w.splits;
+  w.splits = (nkb + w.kbps - 1) / w.kbps;  // every slice non-empty
+  launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B) * w.splits, d, Fc1Dgrad::tiles(B), s);
+}
+
+int f32_fc1_wgrad_slices(int B) {
+  const int nkb = (B + Fc1Wgrad::BK - 1) / Fc1Wgrad::BK;
+  const int g = std::min(std::max(1, g_fc1_wg_splits), nkb), kbps = (nkb + g - 1) / g;
+  return (nkb + kbps - 1) / kbps;
 }
 
 int f32_wgrad_splits(int layer, int B) { return wgrad_plan(layer, B).splits; }

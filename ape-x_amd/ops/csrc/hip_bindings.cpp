@@ -459,6 +459,17 @@ PYBIND11_MODULE(_apex_hip, m) {
     f32_fc1_bwd(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ga),
                 P<float>(gv), B, S(s));
   });
+  m.def("f32_fc1_bwd_split", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ws, int B,
+                                uint64_t s) {
+    f32_fc1_bwd_split(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ws), B,
+                      S(s));
+  });
+  m.def("f32_fc1_wgrad_splits", &f32_fc1_wgrad_splits);
+  m.def("f32_fc1_wgrad_slices", &f32_fc1_wgrad_slices);
+  m.def("f32_fc1_wgrad_workspace_floats", &f32_fc1_wgrad_workspace_floats);
+  m.def("f32_fc1_finalize_job", [](int half, int G, uint64_t ws, uint64_t grad) {
+    return f32_fc1_finalize_job(half, G, P<const float>(ws), P<float>(grad));
+  });
   m.def("f32_wgrad_splits", &f32_wgrad_splits);
   m.def("f32_wgrad_workspace_floats", &f32_wgrad_workspace_floats);
   m.def("f32_conv_bwd", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t w, uint64_t mask,

@@ -170,6 +170,7 @@ int grad_finalize_blocks(const FinalizeSet& fs);
 FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
 // FC1 weight half (0: advantage rows 0..127, 1: value rows 128..255) of fc1_bwd's slabs
 FinalizeJob fc1_finalize_job(int half, const float* ws, float* grad);
+FinalizeJob f32_fc1_finalize_job(int half, int G, const float* ws, float* grad);  // fp32 FC1 slices
 FinalizeJob heads_finalize_job(int G, int A, const float* part, float* g_wadv2, float* g_badv2, float* g_wval2,
                                float* g_bval2, float* g_badv1, float* g_bval1);
 
@@ -380,6 +381,11 @@ void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy
                  hipStream_t s);
 int f32_wgrad_splits(int layer, int B);
 size_t f32_wgrad_workspace_floats(int layer, int B);
+int f32_fc1_wgrad_splits();
+int f32_fc1_wgrad_slices(int B);
+size_t f32_fc1_wgrad_workspace_floats();
+void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
+                       hipStream_t s);
 // conv backward: layers 3/2 = wgrad partials + dgrad (w = w3t / w2t, masked by `mask`) in
 // one launch, layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
