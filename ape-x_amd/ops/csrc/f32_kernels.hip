@@ -1661,6 +1661,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 13 && v >= 0 && v <= 2) g_fc1_tile = v;
   else if (layer == 14 && v >= 0 && v <= 1) g_conv_tile = v;
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
+  else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 

@@ -194,6 +194,7 @@ struct LossHeadsArgs {
   int64_t* step_snap;              // out: its value for this step's optimizer (may be null)
 };
 int dqn_heads_bwd_blocks(int B);
+extern int g_lh_rows;  // dqn_heads_bwd rows per workgroup (4 or 8; f32_set_variant(16, ...))
 void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s);
 
 // ---- learner_kernels.hip

@@ -21,13 +21,18 @@
 namespace apex {
 
 namespace {
-constexpr int LH_ROWS = 8;   // rows per workgroup (B = 512 -> 64 workgroups)
-constexpr int LH_WAVES = 8;  // one row per wave: each row is a chain of dependent loads
-                             // (idx -> a, r, d; q rows), two rows per wave serialised them
+// rows per workgroup = waves per workgroup (one row per wave: each row is a chain of
+// dependent loads (idx -> a, r, d; q rows), two rows per wave serialised them).  8 rows:
+// B = 512 -> 64 workgroups; 4 rows (g_lh_rows = 4): 128 workgroups, twice the partials.
 constexpr int LH_MAXA = 63;
 }  // namespace
 
-__global__ __launch_bounds__(64 * LH_WAVES) void dqn_heads_bwd_k(LossHeadsArgs p) {
+int g_lh_rows = 8;
+
+template <int LH_ROWS>
+__global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p) {
+  constexpr int LH_WAVES = LH_ROWS;
+  static_assert(64 * LH_WAVES >= 256, "the partials take one column per thread of 256");
   __shared__ float colsum[128];
   __shared__ float gs[LH_ROWS];
   __shared__ int as[LH_ROWS];
@@ -127,12 +132,13 @@ __global__ __launch_bounds__(64 * LH_WAVES) void dqn_heads_bwd_k(LossHeadsArgs p
   part[(A + 1) * 129 + t] = dsum;
 }
 
-int dqn_heads_bwd_blocks(int B) { return (B + LH_ROWS - 1) / LH_ROWS; }
+int dqn_heads_bwd_blocks(int B) { return (B + g_lh_rows - 1) / g_lh_rows; }
 
 void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s) {
   if (args.A < 1 || args.A > LH_MAXA) throw std::invalid_argument("dqn_heads_bwd: 1 <= A <= 63");
   if (args.B <= 0) return;
-  dqn_heads_bwd_k<<<dqn_heads_bwd_blocks(args.B), 64 * LH_WAVES, 0, s>>>(args);
+  if (g_lh_rows == 4) dqn_heads_bwd_k<4><<<dqn_heads_bwd_blocks(args.B), 64 * 4, 0, s>>>(args);
+  else dqn_heads_bwd_k<8><<<dqn_heads_bwd_blocks(args.B), 64 * 8, 0, s>>>(args);
   LAUNCH_CHECK();
 }
 
