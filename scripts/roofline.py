@@ -40,7 +40,7 @@ def model(name, wgs, B, E):
     if "Conv3Fwd" in name:
         return (3 * B if wgs > 600 else E) * CONV3, None
     if "Fc1Fwd" in name or "fc1_fwd" in name:
-        return (3 * B if wgs > 100 else E) * FC1, None
+        return (3 * B if wgs > 300 else E) * FC1, None  # learner 336 (128x64) | 672 (64x64) wg
     if "Fc1Wgrad" in name or "fc1_bwd" in name:
         return 2 * B * FC1, None  # weight + input gradient
     if "ConvWgrad<3>" in name:
