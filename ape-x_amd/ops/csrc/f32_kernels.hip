@@ -1583,9 +1583,10 @@ int g_fwd_bk16 = 0;
 // 1 = 64 x 64 (2 x 2 waves of 32 x 32), 2 = 128 x 32 (4 x 1 waves of 32 x 32); 1 and 2 give
 // twice the workgroups (672 per 3 x 512 rows) at half the LDS
 int g_fc1_tile = 1;  // measured: FC1 fwd 36.9 -> 31.6 us, bench 1885 -> 1933 steps/s
-// conv2 / conv3 forward tile (f32_set_variant(14, 0..1)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
-// every A row staged once, 2 x 2 waves of 32 x 32)
-int g_conv_tile = 0;
+// conv2 / conv3 forward tile (f32_set_variant(14, 0..2)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
+// every A row staged once, 2 x 2 waves of 32 x 32), 2 = 64 x 64 for the learner's 3-problem
+// launches only (the actor's 1-problem launch keeps 128 x 32)
+int g_conv_tile = 2;  // measured (3000 steps x2): 0: 1936 / 1934, 1: 1925 / 1933, 2: 1947 / 1947 steps/s
 // FC1 weight gradient batch slices (f32_set_variant(15, 0..4)): 0 = one pass writing the
 // reference-layout grads in place; G > 0 = G slices of natural-order partials reduced and
 // transposed by grad_finalize (4 x 49 x G workgroups instead of 4 x 49 beside the dgrad's 8 x 49).
@@ -1659,7 +1660,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
   else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
   else if (layer == 13 && v >= 0 && v <= 2) g_fc1_tile = v;
-  else if (layer == 14 && v >= 0 && v <= 1) g_conv_tile = v;
+  else if (layer == 14 && v >= 0 && v <= 2) g_conv_tile = v;
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
@@ -1684,12 +1685,12 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
       break;
     case 2:
       if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 1) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
       if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 1) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
