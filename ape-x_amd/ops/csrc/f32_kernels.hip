@@ -1581,7 +1581,8 @@ int g_xcd = 1;
 int g_fwd_bk16 = 0;
 // FC1 forward tile (f32_set_variant(13, 0..2)): 0 = 128 x 64 (2 x 2 waves of 64 x 32),
 // 1 = 64 x 64 (2 x 2 waves of 32 x 32), 2 = 128 x 32 (4 x 1 waves of 32 x 32); 1 and 2 give
-// twice the workgroups (672 per 3 x 512 rows) at half the LDS
+// twice the workgroups (672 per 3 x 512 rows) at half the LDS; 3 = 64 x 64 for the learner's
+// 3-problem launch, 128 x 64 for the actor's
 int g_fc1_tile = 1;  // measured: FC1 fwd 36.9 -> 31.6 us, bench 1885 -> 1933 steps/s
 // conv2 / conv3 forward tile (f32_set_variant(14, 0..2)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
 // every A row staged once, 2 x 2 waves of 32 x 32), 2 = 64 x 64 for the learner's 3-problem
@@ -1659,7 +1660,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
   else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
-  else if (layer == 13 && v >= 0 && v <= 2) g_fc1_tile = v;
+  else if (layer == 13 && v >= 0 && v <= 3) g_fc1_tile = v;
   else if (layer == 14 && v >= 0 && v <= 2) g_conv_tile = v;
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
@@ -1701,7 +1702,7 @@ int f32_fc1_splits() { return kFcSplits; }
 
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
-  if (g_fc1_tile == 1) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
+  if (g_fc1_tile == 1 || (g_fc1_tile == 3 && set.n == 3)) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
   else if (g_fc1_tile == 2) fwd_launch<Fc1FwdT<128, 32, 32, 4>>(set, s);
   else fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
   return kFcSplits;
