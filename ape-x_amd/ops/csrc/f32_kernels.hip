@@ -1443,19 +1443,24 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 // rows of a tile share one input position and the same set of in-range taps.  The k loop runs
 // over exactly those taps -- the sample-major forms above multiply the zero border: 40% of
 // the conv3 dgrad MFMA work (21 of 27 (ky, iy) pairs in range per axis) and 19% of conv2's.
-struct Conv3DgradP {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b][pi - tap][co] w3t[tap][ci][co]
-  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+// BM x BN tiles of (samples at one input position) x (input channels); 128 x 32 (two n-tiles)
+// or 64 x 64 (whole N: each dy3 row staged once; f32_set_variant(17, 1))
+template <int BM_, int BN_, int WM_>
+struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b][pi - tap][co] w3t[tap][ci][co]
+  static constexpr int BM = BM_, BN = BN_, BK = 32, WM = WM_;
+  static constexpr int NT = 64 / BN;
+  static_assert(NT * BN == 64, "n-tiles cover the 64 input channels");
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
   using Args = BwdArgs;
   using Smem = NoSmem;
   struct Ctx {
     int b0, pos, iy, ix, ky0, kx0, nkx, n0, kb0, kb1;
   };
-  static __host__ __device__ int tiles(int B) { return 81 * 2 * ((B + BM - 1) / BM); }
+  static __host__ __device__ int tiles(int B) { return 81 * NT * ((B + BM - 1) / BM); }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     const int tpp = (a.B + BM - 1) / BM;
-    c.n0 = (block & 1) * BN;
-    block >>= 1;
+    c.n0 = (block % NT) * BN;
+    block /= NT;
     c.pos = block / tpp;
     c.b0 = (block - c.pos * tpp) * BM;
     c.iy = c.pos / 9;
@@ -1491,6 +1496,9 @@ struct Conv3DgradP {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b]
     a.out[o] = a.mask[o] > 0.f ? v : 0.f;
   }
 };
+
+using Conv3DgradP = Conv3DgradPT<128, 32, 4>;
+using Conv3DgradP64 = Conv3DgradPT<64, 64, 2>;
 
 // conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
 // output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
@@ -1595,6 +1603,8 @@ int g_conv_tile = 2;  // measured (3000 steps x2): 0: 1936 / 1934, 1: 1925 / 193
 // more slices do not pay for the partial traffic; ONE slice wins by its coalesced natural-order
 // stores (the transpose moves into the finalize job that also takes the FC1 norm partials)
 int g_fc1_wg_splits = 1;
+// conv3 input-gradient tile (f32_set_variant(17, 0..1)): 0 = 128 x 32, 1 = 64 x 64
+int g_dgrad3_tile = 0;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1664,6 +1674,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 14 && v >= 0 && v <= 2) g_conv_tile = v;
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
+  else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1796,6 +1807,8 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
     case 3:
       if (g_dgrad_variant)
         launch2<ConvWgrad<3>, Conv3Dgrad>(g, nw3, d, mode == 1 ? 0 : Conv3Dgrad::tiles(B), s);
+      else if (g_dgrad3_tile == 1)
+        launch2<ConvWgrad<3>, Conv3DgradP64>(g, nw3, d, mode == 1 ? 0 : Conv3DgradP64::tiles(B), s);
       else
         launch2<ConvWgrad<3>, Conv3DgradP>(g, nw3, d, mode == 1 ? 0 : Conv3DgradP::tiles(B), s);
       break;
