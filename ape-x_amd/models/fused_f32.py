@@ -26,6 +26,8 @@ state_dict; the arena only changes memory order, never a value.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -74,6 +76,7 @@ class F32DuelingNet:
         self.A = model.num_actions
         self.device = next(model.parameters()).device
         self._ws_B = None
+        self.fc1_in_place_dp = os.environ.get("APEX_FC1_DP_INPLACE", "1") == "1"  # A/B hook
         self._heads_ws = None
         self._maps = None
         sizes = [int(torch.Size(sh).numel()) for _, sh in self.LAYOUT]
@@ -200,13 +203,14 @@ class F32DuelingNet:
                                            m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
                                            m.value[0].bias.grad.data_ptr())
 
-    def _fc1_bwd(self, ws: F32Workspace) -> list:
+    def _fc1_bwd(self, ws: F32Workspace, in_place: bool = False) -> list:
         """FC1 dgrad + weight gradient; returns the finalize jobs that complete the weight
         gradient (sliced mode: sum the slices + transpose to the reference layout, with
-        their sum-of-squares partials), or [] when it was written in place."""
+        their sum-of-squares partials), or [] when it was written in place (``in_place``:
+        the data-parallel split, where the FC1 all-reduce waits on this launch)."""
         m = self.model
         ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
-        if self._fc1_G:
+        if self._fc1_G and not in_place:
             self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
                                        self._fc1_ws.data_ptr(), ws.B, self._s())
             return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
@@ -237,7 +241,7 @@ class F32DuelingNet:
         place) + the finalize of ``extra_jobs`` (the heads), so the FC1/head all-reduce can
         start while :meth:`conv_backward` runs."""
         self.enable_backward(ws.B)
-        jobs = self._fc1_bwd(ws) + list(extra_jobs)
+        jobs = self._fc1_bwd(ws, in_place=self.fc1_in_place_dp) + list(extra_jobs)
         if jobs:
             self.hip.grad_finalize(jobs, self._s(), 0)
 
