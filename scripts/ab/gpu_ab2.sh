@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two bench configurations, interleaved on one box (3 rounds each).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 for i in 1 2 3; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Back-to-back bench variants: each argument is a flag string for bench.py.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 i=0

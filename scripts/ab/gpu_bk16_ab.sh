@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv2/conv3 forward BK = 16 tiles (knob 12) vs BK = 32: tests, microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/bk16
 mkdir -p $O
 APEX_F32_KNOBS=12=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py -x -q --timeout 120 --timeout-method thread > $O/t1.log 2>&1 &&

@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv1 fwd (exact split) with the next sample's frames prefetched: tests, microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/c1pf
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

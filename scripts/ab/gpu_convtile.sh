@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv2/conv3 forward tile A/B (knob 14): fp32 numerics tests per tile, microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/convt
 mkdir -p $O
 for v in 1; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv2/conv3 forward tile A/B (knob 14 = 0 | 1 | 2), bench only, interleaved.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/convt2
 mkdir -p $O
 for v in 0 2 1 0 2 1; do

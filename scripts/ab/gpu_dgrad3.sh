@@ -1,7 +1,7 @@
 #!/bin/bash
 # conv3 input-gradient tile A/B (knob 17 = 0 | 1): fp32 tests at 1, microbench, bench interleaved.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/dg3
 mkdir -p $O
 APEX_F32_KNOBS="17=1" timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py tests/test_gpu_learner.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Forced-DP (1-rank RCCL group) A/B of two bench argument sets, interleaved (3 rounds).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 P=29531

@@ -1,7 +1,7 @@
 #!/bin/bash
 # FC1 forward tile A/B (knob 13): fp32 numerics tests per tile, microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fc1t
 mkdir -p $O
 for v in 1 2; do

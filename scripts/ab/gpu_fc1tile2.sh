@@ -1,7 +1,7 @@
 #!/bin/bash
 # FC1 forward tile A/B (knob 13 = 1 | 3), bench only, interleaved.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fc1t2
 mkdir -p $O
 for v in 1 3 1 3; do

@@ -1,7 +1,7 @@
 #!/bin/bash
 # FC1 weight-gradient batch slices A/B (knob 15): fp32 tests at the default, bench per setting.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fc1wg
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_f32_net.py tests/test_gpu_learner.py tests/test_gpu_learning.py tests/test_gpu_fused_bwd.py tests/test_gpu_overlap.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

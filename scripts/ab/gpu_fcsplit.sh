@@ -1,7 +1,7 @@
 #!/bin/bash
 # FC1 forward split-K count A/B: fp32 tests, microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fcs
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py tests/test_gpu_learner.py tests/test_gpu_fused_bwd.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GEMM body: MFMA block fenced from the LDS store (knob 8 = 3) vs the default: microbench + bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/fence
 mkdir -p $O
 APEX_F32_KNOBS=8=3 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Single-GPU measurement of the data-parallel step: real RCCL collectives in a 1-rank
 # group (--force-dp) vs the single-process step.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # dqn_heads_bwd rows-per-workgroup A/B (knob 16 = 4 | 8): learner tests at 4, bench both.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/lhrows
 mkdir -p $O
 APEX_F32_KNOBS="16=4" timeout -k 10 300 python -u -m pytest tests/test_gpu_learner.py tests/test_gpu_fused_bwd.py tests/test_gpu_learning.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # multirank sharded-DP test with the FC1 DP weight gradient sliced (0) then in place (1).
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/mr
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0

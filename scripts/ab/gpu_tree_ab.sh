@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tree-write kernels: replay / fused-write tests, 2000-step bench, kernel-trace Gantt.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 REPO=$(pwd)
 O=$REPO/gpurun_out/tree
 mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Strided in-block tree walk + small-batch routing: replay / AQL tests, AQL bench, Ape-X bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/treesmall
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_replay.py tests/test_gpu_fused_bwd.py tests/test_gpu_aql_engine.py tests/test_gpu_aql.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

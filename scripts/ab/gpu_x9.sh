@@ -1,7 +1,7 @@
 #!/bin/bash
 # Exact-split GEMM body (knob 10): numerics tests, per-kernel microbench x9 vs fp32 MFMA, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/x9
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

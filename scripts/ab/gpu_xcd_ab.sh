@@ -1,7 +1,7 @@
 #!/bin/bash
 # XCD-chunked tile order (knob 11) A/B: fp32 net tests, per-kernel microbench, bench.
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 O=gpurun_out/xcd
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_f32_net.py tests/test_gpu_learning.py -x -q --timeout 120 --timeout-method thread > $O/t.log 2>&1

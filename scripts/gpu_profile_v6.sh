@@ -8,7 +8,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
 timeout -k 10 300 python bench.py --steps 2000 --warmup 50 > gpurun_out/bench.log 2>&1 || exit 1
 grep '^{' gpurun_out/bench.log | cut -c1-300
-STEPS=2000 bash scripts/gpu_forcedp.sh 2>&1 | grep -v rc= || exit 1
+STEPS=2000 bash scripts/ab/gpu_forcedp.sh 2>&1 | grep -v rc= || exit 1
 cd /tmp && export TMPDIR=/tmp
 for mode in overlap seq; do
   OUT="$REPO/gpurun_out/prof_v6_$mode"; mkdir -p "$OUT"
