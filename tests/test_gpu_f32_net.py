@@ -234,6 +234,49 @@ def test_conv1_wgrad_exact_split_is_fp32_class(cuda, B):
         assert errs[v] <= 2.0 * errs[0] + 1e-7, errs
 
 
+@pytest.mark.parametrize("B", [29, 512])
+def test_f32_fc1_wgrad_slices_match_in_place(cuda, B):
+    """FC1 weight gradient in batch slices (knob 15: natural-order partials summed +
+    transposed by grad_finalize's FC1 row job) vs the in-place reference-layout pass: one
+    slice is bit-identical, more slices differ only by the fp32 slice-sum order."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    A = 18
+    m = _model(cuda, A=A, seed=7)
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+    net(x, ws)
+    net.backward(torch.randn(B, A, device=cuda) / B, x, ws)  # fills ws.dz
+    ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+    net._fc1_bwd(ws, in_place=True)
+    torch.cuda.synchronize()
+    ref_a, ref_v = ga.clone(), gv.clone()
+    try:
+        for G in (1, 2, 4):
+            hip.f32_set_variant(15, G)
+            net._ws_B = None
+            net.enable_backward(B)
+            ga.fill_(float("nan"))
+            gv.fill_(float("nan"))
+            jobs = net._fc1_bwd(ws)
+            assert len(jobs) == 2 and net._fc1_G == min(G, (B + 31) // 32)
+            hip.grad_finalize(jobs, net._s(), 0)
+            torch.cuda.synchronize()
+            if G == 1:
+                assert torch.equal(ga, ref_a) and torch.equal(gv, ref_v)
+            else:
+                torch.testing.assert_close(ga, ref_a, rtol=1e-5, atol=1e-6 * float(ref_a.abs().max()))
+                torch.testing.assert_close(gv, ref_v, rtol=1e-5, atol=1e-6 * float(ref_v.abs().max()))
+    finally:
+        hip.f32_set_variant(15, 1)  # the default
+        net._ws_B = None
+
+
 def test_f32_finalize_norm_partials(cuda):
     """trunk_backward's grad_finalize sum-of-squares partials cover every trunk + FC1
     weight gradient (the FC1 weights through norm-only jobs)."""
