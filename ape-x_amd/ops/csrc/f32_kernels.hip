@@ -981,6 +981,7 @@ struct BwdArgs {
   int B;
   int kbps;             // wgrad: k-blocks per split
   int splits;
+  int xcd_group;        // conv wgrad: the n-tiles of a split on one XCD (f32_set_variant(18, 1))
 };
 
 struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
@@ -1080,8 +1081,20 @@ struct ConvWgrad {
   static __host__ __device__ int kblocks(int B) { return P * ((B + BK - 1) / BK); }
   static __host__ __device__ int tiles(int, int splits) { return (N / BN) * splits; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
-    c.split = block / (N / BN);
-    c.n0 = (block % (N / BN)) * BN;
+    constexpr int NT = N / BN;
+    const int full = a.xcd_group ? (a.splits / 8) * 8 * NT : 0;
+    if (block < full) {
+      // workgroups go to XCD blockIdx % 8: XCD x takes every n-tile of splits x, x + 8, ...,
+      // so the NT workgroups that read the same dy rows and overlapping input windows of a
+      // split share one L2 (the plain order spreads them over all 8 XCDs)
+      const int x = block & 7, j = block >> 3;
+      c.split = (j / NT) * 8 + x;
+      c.n0 = (j % NT) * BN;
+    } else {
+      const int r = block - full;
+      c.split = full / NT + r / NT;
+      c.n0 = (r % NT) * BN;
+    }
     c.nbb = (a.B + BK - 1) / BK;
     c.kb0 = c.split * a.kbps;
     c.kb1 = min(c.kb0 + a.kbps, kblocks(a.B));
@@ -1605,6 +1618,8 @@ int g_conv_tile = 2;  // measured (3000 steps x2): 0: 1936 / 1934, 1: 1925 / 193
 int g_fc1_wg_splits = 1;
 // conv3 input-gradient tile (f32_set_variant(17, 0..1)): 0 = 128 x 32, 1 = 64 x 64
 int g_dgrad3_tile = 0;
+// conv2 / conv3 weight gradient: XCD-grouped split order (f32_set_variant(18, 0..1))
+int g_wgrad_xcd = 0;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1675,6 +1690,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
+  else if (layer == 18 && v >= 0 && v <= 1) g_wgrad_xcd = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1795,6 +1811,7 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   g.B = B;
   g.kbps = p.kbps;
   g.splits = p.splits;
+  g.xcd_group = g_wgrad_xcd;
   BwdArgs d{};
   d.dy = dy;
   d.w = w;
