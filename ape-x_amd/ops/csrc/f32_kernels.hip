@@ -982,7 +982,6 @@ struct BwdArgs {
   int kbps;             // wgrad: k-blocks per split
   int splits;
   int xcd_group;        // conv wgrad: the n-tiles of a split on one XCD (f32_set_variant(18, 1))
-  int off32;            // conv wgrad: 32-bit operand offsets (f32_set_variant(19, 1))
 };
 
 struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
@@ -1121,14 +1120,9 @@ struct ConvWgrad {
     int row, off;  // off = (ky * IH + kx) * C + ci of the chunk's column
   };
   static __device__ RowA row_a(const Args&, const Ctx&, int row, int ch) { return {row, 4 * ch}; }
-  // 32-bit element offsets from the uniform kernel-argument bases (knob 19): the loads can
-  // take the SGPR-base + 32-bit VGPR-offset form instead of per-load 64-bit address math
-  // (dy3 / dy2 / a1 / a2 of any batch the learner runs stay far below 2^32 elements)
   static __device__ f32x4 load_a_row(const Args& a, const Ctx& c, const RowA& r, int kb) {
     const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + r.row;  // p, block base: wave-uniform
-    if (b >= a.B) return zero4();
-    if (a.off32) return ld4(a.dy + (uint32_t)((b * P + p) * 64 + r.ch4));
-    return ld4(a.dy + ((size_t)b * P + p) * 64 + r.ch4);
+    return b < a.B ? ld4(a.dy + ((size_t)b * P + p) * 64 + r.ch4) : zero4();
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int row, int ch) {
     const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
@@ -1139,7 +1133,6 @@ struct ConvWgrad {
     if (b >= a.B) return zero4();
     const int oy = p / OH, ox = p - oy * OH;  // wave-uniform
     const float* x = static_cast<const float*>(a.x);
-    if (a.off32) return ld4(x + (uint32_t)((b * IH * IH + S * oy * IH + S * ox) * C + r.off));
     return ld4(x + ((size_t)b * IH * IH + S * oy * IH + S * ox) * C + r.off);
   }
   static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
@@ -1627,8 +1620,6 @@ int g_fc1_wg_splits = 1;
 int g_dgrad3_tile = 0;
 // conv2 / conv3 weight gradient: XCD-grouped split order (f32_set_variant(18, 0..1))
 int g_wgrad_xcd = 0;
-// conv2 / conv3 weight gradient: 32-bit operand offsets (f32_set_variant(19, 0..1))
-int g_wgrad_off32 = 0;
 
 // single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
 int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
@@ -1700,7 +1691,6 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
   else if (layer == 18 && v >= 0 && v <= 1) g_wgrad_xcd = v;
-  else if (layer == 19 && v >= 0 && v <= 1) g_wgrad_off32 = v;
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1822,8 +1812,6 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   g.kbps = p.kbps;
   g.splits = p.splits;
   g.xcd_group = g_wgrad_xcd;
-  // 32-bit offsets only while every operand index fits (input plane of the layer x B)
-  g.off32 = g_wgrad_off32 && (int64_t)B * 400 * 64 < (int64_t)1 << 31;
   BwdArgs d{};
   d.dy = dy;
   d.w = w;
