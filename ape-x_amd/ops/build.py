@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -65,11 +66,36 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.cuh")) + sorted(CSRC.glob("*.hpp"))
 
 
-def _stale(target: Path, deps: list[Path]) -> bool:
-    if not target.exists():
-        return True
-    t = target.stat().st_mtime
-    return any(d.stat().st_mtime > t for d in deps if d.exists())
+def _digest(parts: list) -> str:
+    """sha256 over the *contents* of the given files and the given strings (flags,
+    compiler path).  mtimes are never trusted: a tree unpacked on another machine, a
+    ``git checkout`` or a copy can leave an old binary newer than its edited source."""
+    h = hashlib.sha256()
+    for p in parts:
+        if isinstance(p, Path):
+            h.update(b"F" + p.name.encode() + b"\0")
+            h.update(p.read_bytes() if p.exists() else b"<missing>")
+        else:
+            h.update(b"S" + str(p).encode() + b"\0")
+    return h.hexdigest()
+
+
+def _sidecar(target: Path) -> Path:
+    return target.with_name(target.name + ".sha256")
+
+
+def build_hash(target: Path) -> str | None:
+    """The content hash recorded beside ``target`` by the build that produced it."""
+    sc = _sidecar(Path(target))
+    return sc.read_text().strip() if sc.exists() else None
+
+
+def _stale(target: Path, digest: str) -> bool:
+    return not target.exists() or build_hash(target) != digest
+
+
+def _stamp(target: Path, digest: str) -> None:
+    _sidecar(target).write_text(digest + "\n")
 
 
 def _run(cmd: list[str]) -> None:
@@ -98,13 +124,15 @@ def build_cpu(force: bool = False, out_dir: Path | None = None, sanitize: bool =
     ``out_dir`` -- load it with libasan preloaded (``sanitizer_env``)."""
     target = cpu_target() if out_dir is None else Path(out_dir) / cpu_target().name
     srcs = [CSRC / s for s in CPU_SOURCES]
-    if not force and not _stale(target, srcs + _headers()):
-        return target
     cxx = os.environ.get("CXX", "g++")
     opt = SANITIZE_FLAGS if sanitize else ["-O3"]
     cmd = [cxx, *opt, "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off", "-fvisibility=hidden",
            *_py_includes(), *map(str, srcs), "-o", str(target)]
+    digest = _digest([*srcs, *_headers(), *cmd[:-1]])
+    if not force and not _stale(target, digest):
+        return target
     _run(cmd)
+    _stamp(target, digest)
     return target
 
 
@@ -139,31 +167,45 @@ HIP_FLAGS = [
 
 
 def build_hip(force: bool = False, jobs: int | None = None) -> Path:
+    """Every object is keyed by the sha256 of its source, all headers and its full
+    compile line (sidecar ``<obj>.sha256``); the library by the hashes of its objects and
+    the link line.  ``build_hash(hip_target())`` identifies the binary that runs."""
     target = hip_target()
     BUILD.mkdir(exist_ok=True)
     srcs = [CSRC / s for s in HIP_SOURCES]
     hdrs = _headers()
     objs = []
     todo = []
+    digests = []
     for s in srcs:
         o = BUILD / (s.name + ".o")
         objs.append(o)
-        if force or _stale(o, [s] + hdrs):
-            if s.suffix == ".hip":
-                cmd = [_hipcc(), *HIP_FLAGS, "-x", "hip", *_py_includes(), "-c", str(s), "-o", str(o)]
-            else:
-                # host-only translation unit (pybind11 glue); still compiled by hipcc so
-                # hip_runtime types resolve, but with no device code of its own.
-                cmd = [_hipcc(), *HIP_FLAGS, *_py_includes(), "-c", str(s), "-o", str(o)]
-            todo.append(cmd)
+        if s.suffix == ".hip":
+            cmd = [_hipcc(), *HIP_FLAGS, "-x", "hip", *_py_includes(), "-c", str(s), "-o", str(o)]
+        else:
+            # host-only translation unit (pybind11 glue); still compiled by hipcc so
+            # hip_runtime types resolve, but with no device code of its own.
+            cmd = [_hipcc(), *HIP_FLAGS, *_py_includes(), "-c", str(s), "-o", str(o)]
+        d = _digest([s, *hdrs, *cmd])
+        digests.append(d)
+        if force or _stale(o, d):
+            todo.append((cmd, o, d))
+
+    def _compile(job):
+        cmd, o, d = job
+        _run(cmd)
+        _stamp(o, d)
+
     if todo:
         jobs = jobs or min(len(todo), max(1, (os.cpu_count() or 4) // 2))
         with cf.ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(_run, todo))
-    if force or todo or _stale(target, objs):
-        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
-               f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-o", str(target)]
+            list(ex.map(_compile, todo))
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs),
+           f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl", "-o", str(target)]
+    digest = _digest([*digests, *cmd])
+    if force or todo or _stale(target, digest):
         _run(cmd)
+        _stamp(target, digest)
     return target
 
 

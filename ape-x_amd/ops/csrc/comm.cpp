@@ -79,6 +79,12 @@ void register_comm(py::module_& m) {
     void* p = reinterpret_cast<void*>(static_cast<uintptr_t>(buf));
     nccl_ok(ncclBroadcast(p, p, (size_t)n, dtype_of(dtype), root, C(comm), St(stream)), "ncclBroadcast");
   }, py::arg("buf"), py::arg("n"), py::arg("dtype"), py::arg("root"), py::arg("comm"), py::arg("stream"));
+  m.def("rccl_comm_count", [](uint64_t comm) {
+    if (!comm) throw std::invalid_argument("rccl_comm_count: null communicator");
+    int n = 0;
+    nccl_ok(ncclCommCount(C(comm), &n), "ncclCommCount");
+    return n;
+  });
   m.def("rccl_comm_destroy", [](uint64_t comm) {
     if (comm) nccl_ok(ncclCommDestroy(C(comm)), "ncclCommDestroy");
   });

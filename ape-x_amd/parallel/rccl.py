@@ -36,6 +36,10 @@ class RcclComm:
         dist.broadcast_object_list(box, src=root, group=group, device=self.device)
         self.handle = self.hip.rccl_comm_init(box[0], self.world, self.rank, self.device.index or 0)
 
+    def count(self) -> int:
+        """Ranks RCCL itself reports for this communicator (ncclCommCount)."""
+        return int(self.hip.rccl_comm_count(self.handle))
+
     def all_reduce_sum(self, t: torch.Tensor, stream) -> None:
         assert t.is_contiguous() and t.device == self.device
         self.hip.rccl_all_reduce_sum(t.data_ptr(), t.numel(), _DT[t.dtype], self.handle, stream.cuda_stream)

@@ -111,6 +111,11 @@ def parse():
                     help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
                          "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="--gpus N>1 without torch.distributed.run: wall limit of the self-launched ranks")
+    ap.add_argument("--watchdog", type=float, default=1500.0,
+                    help="seconds after which a rank dumps every thread's stack and exits 1 (0 = off): "
+                         "a hung collective ends the run with a traceback instead of a silent stall")
     ap.add_argument("--unpaced", action="store_true",
                     help="central topology: actors run free (default: paced at --actor-steps packets per learner "
                          "step per actor through the credit window)")
@@ -135,6 +140,18 @@ def _host_launch_cost(eng, device, n: int = 20) -> float:
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # Not under torch.distributed.run: launch the N ranks here.  This process never
+        # touches the GPU; the children are fresh processes (Popen, not exec) that re-enter
+        # main() with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set; rank 0 prints the JSON line.
+        from apex_amd.parallel.spawn import run_ranks
+
+        sys.exit(run_ranks([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], args.gpus,
+                           timeout=args.launch_timeout))
+    if args.watchdog > 0:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.watchdog, exit=True)
     import torch
     import torch.distributed as dist
 
@@ -241,6 +258,7 @@ def main():
         eng.train_step()
     torch.cuda.synchronize(device)
 
+    rccl_ranks = allreduce.comm.count() if isinstance(allreduce, _Rccl) else None
     stats = eng.learner.stats()
     updates_per_s = args.steps / dt                # synchronous optimizer updates (all ranks step together)
     samples_per_s = world * rank_batch * args.steps / dt
@@ -279,6 +297,11 @@ def main():
                 "actor_learner_overlap": args.overlap,
                 "actor_stream": args.streams,
                 "dp_graph": eng._g_dp is not None,
+                # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
+                # gradient communicator, else the torch.distributed group size
+                "rccl_ranks": rccl_ranks,
+                "process_group_ranks": dist.get_world_size() if dist.is_initialized() else 1,
+                "process_group_backend": dist.get_backend() if dist.is_initialized() else None,
             },
             "optimizer_updates_per_s": round(updates_per_s, 3),
             "actor_frames_per_sec": round(frames_per_s, 1),
