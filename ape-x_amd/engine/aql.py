@@ -28,7 +28,9 @@ What runs where (all device-side, no host sync inside an iteration):
 Iteration = one actor step of all E envs + ``E // batch`` learner steps: the reference's
 replay ratio (``total_ep_len // batch_size`` SGD steps per recorded batch, AQL_dis.py:118).
 Weights are published to the actors every iteration (set_worker_weights, AQL_dis.py:115)
-and the target network is synced every ``target_update_steps`` learner steps.
+and the target network is synced after the learner steps of every iteration whose index is
+a multiple of ``target_update_interval`` -- iteration 0 included (AQL_dis.py:127-129);
+``target_update_steps > 0`` switches to a learner-step cadence instead (round-2 default).
 
 Reference behaviours kept: q.features (the state embedding feeding the proposal) receives
 gradient only from the proposal loss, which optimizer_q zeroes before its own backward, so
@@ -37,6 +39,7 @@ broadcasts log_prob([B,1]) against batch [B] (see aql_engine_kernels.hip).
 """
 from __future__ import annotations
 
+import collections
 import math
 import os
 from dataclasses import dataclass
@@ -161,7 +164,9 @@ class AQLEngineConfig:
     n_workers: int = 10            # the reference's beta-annealing factor (AQL_dis.py:57)
     max_norm: float = 40.0
     learner_steps: int | None = None   # per iteration; None = n_envs // batch_size
-    target_update_steps: int = 2000    # learner steps between target syncs
+    target_update_interval: int = 20   # iterations between target syncs, iteration 0 included (AQL_dis.py:127)
+    target_update_steps: int = 0       # > 0: sync every this many learner steps instead (not the reference's)
+    track_losses: bool = False         # accumulate loss_q / loss_proposal per step on device (train CLI logging)
     eps_base: float = 0.4
     eps_alpha: float = 7.0
     total_actors: int | None = None    # epsilon ladder width (multi-GPU: all actors)
@@ -172,6 +177,18 @@ class AQLEngineConfig:
     fork_tree: bool = False  # tree write on a forked stream: measured 9851 vs 11769 steps/s (two cross-queue
                              # hand-offs per ~85 us step cost more than the 11 us they hide)
     seed: int = 0
+
+
+def target_sync_due(cfg: AQLEngineConfig, iteration: int, steps_before: int, steps_after: int) -> bool:
+    """Whether the full online -> target copy follows the learner steps of ``iteration``.
+    Reference cadence: ``frame_idx % target_update_interval == 0`` after that iteration's
+    SGD loop (AQL_dis.py:127-129), so iteration 0 syncs.  ``target_update_steps > 0``:
+    whenever the learner-step count crosses a multiple of it."""
+    tu = int(cfg.target_update_steps)
+    if tu > 0:
+        return steps_before // tu != steps_after // tu
+    ti = int(cfg.target_update_interval)
+    return ti > 0 and iteration % ti == 0
 
 
 class AQLLearner:
@@ -212,6 +229,8 @@ class AQLLearner:
         self.prio = torch.zeros(B, **f32)
         self.loss_q = torch.zeros(1, **f32)
         self.loss_p = torch.zeros(1, **f32)
+        self.loss_acc = torch.zeros(3, dtype=torch.float64, device=dev)  # sum loss_q, sum loss_p, steps
+        self._acc_one = torch.ones(1, dtype=torch.float64, device=dev)
         self.grad = torch.zeros(self.P, **f32)
         self.m = torch.zeros(self.P, **f32)
         self.v = torch.zeros(self.P, **f32)
@@ -344,6 +363,18 @@ class AQLLearner:
                       self.norms_p.data_ptr()),
                      self.hp, self.step_ctr.data_ptr(), s)
         h.aql_post(self.post, 1, s)
+        if self.cfg.track_losses:  # device-side running sums; read (one sync) only when logging
+            self.loss_acc[0:1].add_(self.loss_q)
+            self.loss_acc[1:2].add_(self.loss_p)
+            self.loss_acc[2:3].add_(self._acc_one)
+
+    def take_loss_means(self) -> tuple[float, float, int]:
+        """(mean loss_q, mean loss_proposal, steps) since the previous call; resets the sums."""
+        self.join()
+        q, p, n = (float(x) for x in self.loss_acc.tolist())
+        self.loss_acc.zero_()
+        n = int(round(n))
+        return (q / n, p / n, n) if n else (float("nan"), float("nan"), 0)
 
     def sync_target(self) -> None:
         """update_target (AQL_dis.py:60-61): full state_dict copy, noise buffers included."""
@@ -438,6 +469,7 @@ class AQLEngine:
         self.learner_steps = 0
         self._g_actor = self._g_learn = None
         self._ep_read = 0
+        self.target_syncs = collections.deque(maxlen=4096)  # iterations after which the target was synced
 
     @staticmethod
     def _s() -> int:
@@ -508,9 +540,9 @@ class AQLEngine:
         self.publish()
         before = self.learner_steps
         self.learner_steps += self.K
-        tu = self.cfg.target_update_steps
-        if tu > 0 and before // tu != self.learner_steps // tu:
+        if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):
             self.learner.sync_target()
+            self.target_syncs.append(self.iterations)
         self.iterations += 1
 
     def finished_episodes(self) -> list[tuple[float, int]]:

@@ -3,12 +3,12 @@
 ALE / gym[atari] / OpenCV are not installed, so ``make_atari`` builds a seeded
 *synthetic Atari emulator* with the same observable contract as an ALE
 ``*NoFrameskip-v4`` env: 210x160x3 uint8 RGB frames, the ALE action-meaning lists,
-``ale.lives()``, ``np_random`` and raw (unclipped) game scores.  The wrapper classes
-reproduce origin_repo/wrapper.py:11-329 behaviour (NoopReset, FireReset, EpisodicLife,
-MaxAndSkip, ClipReward, WarpFrame, FrameStack/TorchFrameStack + LazyFrames,
-ScaledFloatFrame, ImageToPyTorch, TimeLimit, make_atari, wrap_deepmind,
-wrap_atari_dqn), with WarpFrame's grayscale + INTER_AREA resize implemented as a
-separable area-averaging matrix product (no OpenCV).
+``ale.lives()``, ``np_random`` and raw (unclipped) game scores.  Preprocessing is the
+pipeline of :mod:`apex_amd.envs.preprocess` (``AtariPreprocess``, vectorised, explicit
+flags); the reference's wrapper names (origin_repo/wrapper.py: NoopReset, FireReset,
+EpisodicLife, MaxAndSkip, ClipReward, WarpFrame, FrameStack/TorchFrameStack + LazyFrames,
+ScaledFloatFrame, ImageToPyTorch, make_atari, wrap_deepmind, wrap_atari_dqn) are kept as
+thin adapters over its stages.
 
 The GPU-resident vector env used by the high-throughput engine
 (`vec_env_step_k`, ops/csrc/actor_kernels.hip, driven by :mod:`apex_amd.engine.actor_shard`) renders the same game family straight to 84x84.
@@ -19,6 +19,7 @@ from collections import deque
 
 import numpy as np
 
+from . import preprocess as P
 from .core import Env, ObservationWrapper, RewardWrapper, TimeLimit, Wrapper, register
 from .spaces import Box, Discrete
 
@@ -170,125 +171,88 @@ for _g in GAME_ACTIONS:
 
 
 # ----------------------------------------------------------------------------------
-# DeepMind wrappers (origin_repo/wrapper.py)
+# Reference-named wrapper adapters (origin_repo/wrapper.py API).  The preprocessing itself
+# lives in :mod:`apex_amd.envs.preprocess` (one pipeline, AtariPreprocess); each class here
+# only binds one of its stages into the gym-style wrapper composition the reference's
+# callers use (make_atari / wrap_atari_dqn / wrap_deepmind).
 # ----------------------------------------------------------------------------------
 class NoopResetEnv(Wrapper):
+    """Start stage: emulator reset + random no-op frames (``fixed_noops`` pins the count)."""
+
     def __init__(self, env, noop_max=30):
         super().__init__(env)
+        if P.meaning(env, 0) != "NOOP":
+            raise ValueError("NoopResetEnv needs NOOP at action 0")
         self.noop_max = noop_max
-        self.override_num_noops = None
-        self.noop_action = 0
-        assert env.unwrapped.get_action_meanings()[0] == "NOOP"
+        self.fixed_noops = None
 
     def reset(self, **kwargs):
-        self.env.reset(**kwargs)
-        noops = self.override_num_noops if self.override_num_noops is not None else \
-            self.unwrapped.np_random.randint(1, self.noop_max + 1)
-        assert noops > 0
-        obs = None
-        for _ in range(noops):
-            obs, _, done, _ = self.env.step(self.noop_action)
-            if done:
-                obs = self.env.reset(**kwargs)
-        return obs
+        return P.noop_start(self.env, self.noop_max, self.fixed_noops, kwargs)
 
 
 class FireResetEnv(Wrapper):
+    """FIRE start stage."""
+
     def __init__(self, env):
         super().__init__(env)
-        assert env.unwrapped.get_action_meanings()[1] == "FIRE"
-        assert len(env.unwrapped.get_action_meanings()) >= 3
+        if P.meaning(env, 1) != "FIRE" or len(env.unwrapped.get_action_meanings()) < 3:
+            raise ValueError("FireResetEnv needs FIRE at action 1 and at least 3 actions")
 
     def reset(self, **kwargs):
-        self.env.reset(**kwargs)
-        obs, _, done, _ = self.env.step(1)
-        if done:
-            self.env.reset(**kwargs)
-        obs, _, done, _ = self.env.step(2)
-        if done:
-            self.env.reset(**kwargs)
-        return obs
+        return P.fire_start(lambda: self.env.reset(**kwargs), self.env.step)
 
 
 class EpisodicLifeEnv(Wrapper):
+    """Life-ledger stage: a lost life ends the agent's episode; ``ledger.game_over`` says
+    whether the next start must reset the emulator."""
+
     def __init__(self, env):
         super().__init__(env)
-        self.lives = 0
-        self.was_real_done = True
+        self.ledger = P.LifeLedger()
+
+    @property
+    def lives(self):
+        return self.ledger.lives
 
     def step(self, action):
         obs, reward, done, info = self.env.step(action)
-        self.was_real_done = done
-        lives = self.env.unwrapped.ale.lives()
-        if 0 < lives < self.lives:
-            done = True
-        self.lives = lives
-        return obs, reward, done, info
+        return obs, reward, self.ledger.observe(done, P.lives_of(self.env)), info
 
     def reset(self, **kwargs):
-        if self.was_real_done:
-            obs = self.env.reset(**kwargs)
-        else:
-            obs, _, _, _ = self.env.step(0)
-        self.lives = self.env.unwrapped.ale.lives()
-        return obs
+        return P.life_start(self.ledger, lambda: self.env.reset(**kwargs), self.env.step,
+                            lambda: P.lives_of(self.env))
 
 
 class MaxAndSkipEnv(Wrapper):
+    """Repeat stage: ``skip`` frames per action, max over the window's last two frames."""
+
     def __init__(self, env, skip=4):
         super().__init__(env)
-        self._obs_buffer = np.zeros((2,) + env.observation_space.shape, dtype=np.uint8)
-        self._skip = skip
+        self.pool = P.RepeatPool(skip)
 
     def step(self, action):
-        total_reward, done, info = 0.0, None, {}
-        for i in range(self._skip):
-            obs, reward, done, info = self.env.step(action)
-            if i == self._skip - 2:
-                self._obs_buffer[0] = obs
-            if i == self._skip - 1:
-                self._obs_buffer[1] = obs
-            total_reward += reward
-            if done:
-                break
-        return self._obs_buffer.max(axis=0), total_reward, done, info
+        return self.pool.run(self.env.step, action)
 
 
 class ClipRewardEnv(RewardWrapper):
     def reward(self, reward):
-        return np.sign(reward)
+        return P.sign_reward(reward)
 
 
 def _area_matrix(n_out: int, n_in: int) -> np.ndarray:
-    """Row-stochastic area-overlap weights (INTER_AREA downscale)."""
-    scale = n_in / n_out
-    m = np.zeros((n_out, n_in), dtype=np.float64)
-    for o in range(n_out):
-        lo, hi = o * scale, (o + 1) * scale
-        for i in range(int(np.floor(lo)), min(int(np.ceil(hi)), n_in)):
-            m[o, i] = max(0.0, min(hi, i + 1) - max(lo, i))
-        m[o] /= m[o].sum()
-    return m
+    return P.area_weights(n_out, n_in)
 
 
 class WarpFrame(ObservationWrapper):
+    """Resample stage: grey + area averaging to ``height x width`` (no OpenCV)."""
+
     def __init__(self, env, width=84, height=84, grayscale=True):
         super().__init__(env)
-        self.width, self.height, self.grayscale = width, height, grayscale
-        c = 1 if grayscale else 3
-        self.observation_space = Box(0, 255, shape=(height, width, c), dtype=np.uint8)
-        h_in, w_in = env.observation_space.shape[:2]
-        self._wy = _area_matrix(height, h_in)
-        self._wx = _area_matrix(width, w_in).T
+        self.resize = P.AreaResize(env.observation_space.shape[:2], (height, width), grayscale)
+        self.observation_space = Box(0, 255, shape=(height, width, self.resize.channels), dtype=np.uint8)
 
     def observation(self, frame):
-        f = frame.astype(np.float64)
-        if self.grayscale:
-            f = f @ np.array([0.299, 0.587, 0.114])
-            out = self._wy @ f @ self._wx
-            return np.clip(np.rint(out), 0, 255).astype(np.uint8)[..., None]
-        out = np.stack([self._wy @ f[..., k] @ self._wx for k in range(3)], -1)
-        return np.clip(np.rint(out), 0, 255).astype(np.uint8)
+        return self.resize(frame)
 
 
 class LazyFrames:
@@ -328,38 +292,31 @@ class TorchLazyFrames(LazyFrames):
 
 
 class FrameStack(Wrapper):
+    """Stack stage: the last ``k`` frames as one LazyFrames (shared, not copied)."""
+
+    lazy = LazyFrames
+
     def __init__(self, env, k):
         super().__init__(env)
         self.k = k
         self.frames = deque([], maxlen=k)
-        shp = env.observation_space.shape
-        self.observation_space = Box(0, 255, shape=(shp[:-1] + (shp[-1] * k,)), dtype=env.observation_space.dtype)
+        shp = list(env.observation_space.shape)
+        shp[self.lazy._axis] *= k
+        self.observation_space = Box(0, 255, shape=tuple(shp), dtype=env.observation_space.dtype)
 
     def reset(self):
-        ob = self.env.reset()
-        for _ in range(self.k):
-            self.frames.append(ob)
-        return self._get_ob()
+        first = self.env.reset()
+        self.frames.extend([first] * self.k)
+        return self.lazy(list(self.frames))
 
     def step(self, action):
         ob, reward, done, info = self.env.step(action)
         self.frames.append(ob)
-        return self._get_ob(), reward, done, info
-
-    def _get_ob(self):
-        assert len(self.frames) == self.k
-        return LazyFrames(list(self.frames))
+        return self.lazy(list(self.frames)), reward, done, info
 
 
 class TorchFrameStack(FrameStack):
-    def __init__(self, env, k):
-        super().__init__(env, k)
-        shp = env.observation_space.shape
-        self.observation_space = Box(0, 255, shape=((shp[0] * k,) + shp[1:]), dtype=env.observation_space.dtype)
-
-    def _get_ob(self):
-        assert len(self.frames) == self.k
-        return TorchLazyFrames(list(self.frames))
+    lazy = TorchLazyFrames
 
 
 class ScaledFloatFrame(ObservationWrapper):
@@ -368,59 +325,66 @@ class ScaledFloatFrame(ObservationWrapper):
         self.observation_space = Box(0, 1, shape=env.observation_space.shape, dtype=np.float32)
 
     def observation(self, observation):
-        return np.array(observation).astype(np.float32) / 255.0
+        return np.asarray(observation, dtype=np.float32) / 255.0
 
 
 class ImageToPyTorch(ObservationWrapper):
-    """HWC -> CWH via swapaxes(2, 0) (H and W transposed)."""
+    """Layout stage: HWC -> CWH (H and W transposed)."""
 
     def __init__(self, env):
         super().__init__(env)
-        old = self.observation_space.shape
-        self.observation_space = Box(0, 255, shape=(old[-1], old[0], old[1]), dtype=np.uint8)
+        h, w, c = self.observation_space.shape
+        self.observation_space = Box(0, 255, shape=(c, h, w), dtype=np.uint8)
 
     def observation(self, observation):
-        return np.swapaxes(observation, 2, 0)
+        return P.channels_first(observation)
 
 
 def make_atari(env_id, max_episode_steps=None):
+    """Raw emulator + start and repeat stages (NoFrameskip ids only)."""
     from .core import make
 
     env = make(env_id)
-    assert "NoFrameskip" in env.spec.id
-    env = NoopResetEnv(env, noop_max=30)
-    env = MaxAndSkipEnv(env, skip=4)
-    if max_episode_steps is not None:
-        env = TimeLimit(env, max_episode_steps=max_episode_steps)
+    if "NoFrameskip" not in env.spec.id:
+        raise ValueError(f"make_atari expects a NoFrameskip id, got {env_id}")
+    env = MaxAndSkipEnv(NoopResetEnv(env, noop_max=30), skip=4)
+    return TimeLimit(env, max_episode_steps=max_episode_steps) if max_episode_steps is not None else env
+
+
+def _wrap(env, spec: P.PreprocessSpec, torch_layout: bool):
+    """The pipeline stages of ``spec`` as a wrapper stack over a ``make_atari`` env."""
+    if spec.episode_life:
+        env = EpisodicLifeEnv(env)
+    if P.has_fire(env) if spec.fire_reset is None else spec.fire_reset:
+        env = FireResetEnv(env)
+    env = WarpFrame(env)
+    if spec.scale:
+        env = ScaledFloatFrame(env)
+    if spec.clip_rewards:
+        env = ClipRewardEnv(env)
+    if torch_layout:
+        env = ImageToPyTorch(env)
+    if spec.stack > 1:
+        env = (TorchFrameStack if torch_layout else FrameStack)(env, spec.stack)
     return env
 
 
 def wrap_deepmind(env, episode_life=True, clip_rewards=True, frame_stack=False, scale=False):
-    if episode_life:
-        env = EpisodicLifeEnv(env)
-    if "FIRE" in env.unwrapped.get_action_meanings():
-        env = FireResetEnv(env)
-    env = WarpFrame(env)
-    if scale:
-        env = ScaledFloatFrame(env)
-    if clip_rewards:
-        env = ClipRewardEnv(env)
-    if frame_stack:
-        env = FrameStack(env, 4)
-    return env
+    spec = P.PreprocessSpec(episode_life=episode_life, clip_rewards=clip_rewards, stack=4 if frame_stack else 1,
+                            scale=scale, channels_first=False)
+    return _wrap(env, spec, torch_layout=False)
 
 
 def wrap_atari_dqn(env, args):
-    if args.episode_life:
-        env = EpisodicLifeEnv(env)
-    if "FIRE" in env.unwrapped.get_action_meanings():
-        env = FireResetEnv(env)
-    env = WarpFrame(env)
-    if args.scale:
-        env = ScaledFloatFrame(env)
-    if args.clip_rewards:
-        env = ClipRewardEnv(env)
-    env = ImageToPyTorch(env)
-    if args.frame_stack:
-        env = TorchFrameStack(env, 4)
-    return env
+    """The Ape-X actor's stack (origin_repo/actor.py:56-57): the reference flags of ``args``."""
+    return _wrap(env, P.PreprocessSpec.from_args(args), torch_layout=True)
+
+
+def make_preprocessed(env_id: str, n: int, spec: P.PreprocessSpec | None = None, seed: int | None = None):
+    """N raw emulators of ``env_id`` under one :class:`~apex_amd.envs.preprocess.AtariPreprocess`."""
+    from .core import make
+
+    pipe = P.AtariPreprocess([make(env_id) for _ in range(n)], spec or P.PreprocessSpec())
+    if seed is not None:
+        pipe.seed(seed)
+    return pipe

@@ -1,0 +1,234 @@
+"""GPU AQL training CLI (BASELINE config 4): ``python -m apex_amd.train_aql [flags]``.
+
+The MI355X counterpart of the reference's multi-worker AQL trainer (AQL_dis.py:18-170 with
+batchrecoder_AQL.py): instead of 10 forked CPU workers that each play one episode per
+iteration and a learner that pickles weights to them, one :class:`AQLEngine` keeps E
+vectorised GPU envs, the HBM prioritized replay with candidate sets and the fused learner
+on one GPU (see ``apex_amd.engine.aql``).  One *iteration* = one step of all E envs + the
+reference replay ratio of ``E // batch_size`` SGD steps (AQL_dis.py:118) + a weight
+publish to the actors (AQL_dis.py:115).
+
+Reference cadences and artefacts kept:
+
+* target sync after iteration ``it`` when ``it % target_update_interval == 0`` (20;
+  iteration 0 included, AQL_dis.py:127-129);
+* ``model{it}.pth`` every ``save_interval`` (200) iterations and at the last one
+  (AQL_dis.py:131-133, 136-137) -- the reference state_dict (``q.*`` / ``proposal.*`` keys,
+  NoisyNet epsilon buffers included), loadable by the reference ``load_model`` -- plus a
+  ``.train.pt`` sidecar (Adam moments, step counter, target net, iteration counters) so
+  ``--resume IT`` continues exactly instead of weights-only;
+* tags ``learner/loss_q`` / ``learner/loss_proposal`` (means over the logging window, at
+  the learner-step index; AQL_dis.py:123-124) and ``actor/episode_reward`` /
+  ``actor/episode_length`` (batchrecoder_AQL.py:118-119), plus ``evaluator/episode_reward``
+  from greedy episodes (the reference's ``training=False`` branch: ``q.eval()``, eps 0,
+  AQL_dis.py:151-167) and ``learner/steps_per_sec`` / ``actor/env_steps_per_sec``.
+
+Losses are accumulated on the device (no host sync per learner step); the host reads
+them once per ``--log-interval`` iterations.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import envs
+from .engine.aql import AQLEngine, AQLEngineConfig
+from .models.aql import AQL
+from .utils.checkpoint import load_model, load_train_state, save_model, save_train_state
+from .utils.tb import NullWriter, SummaryWriter
+
+
+def parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="AQL_dis on MI355X (GPU-resident AQL engine)")
+    p.add_argument("--env", default="CartPole-v0", help="CartPole-v0/v1, Pendulum-v0/v1, BipedalWalker-v3")
+    p.add_argument("--max-step", type=int, default=1_000_000, help="iterations (AQL_dis max_step)")
+    p.add_argument("--n-envs", type=int, default=256, help="GPU envs (the reference's workers)")
+    p.add_argument("--batch-size", type=int, default=32)
+    p.add_argument("--gamma", type=float, default=0.99)
+    p.add_argument("--n-steps", type=int, default=1)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--ent-lam", type=float, default=0.8)
+    p.add_argument("--propose-sample", type=int, default=1)
+    p.add_argument("--uniform-sample", type=int, default=50)
+    p.add_argument("--action-var", type=float, default=0.25)
+    p.add_argument("--prior-alpha", type=float, default=0.6)
+    p.add_argument("--prior-beta-start", type=float, default=0.4)
+    p.add_argument("--capacity", type=int, default=10_000_000, help="replay capacity (AQL_dis.py:44: 1e7)")
+    p.add_argument("--target-update-interval", type=int, default=20, help="iterations (0 = off)")
+    p.add_argument("--target-update-steps", type=int, default=0,
+                   help="> 0: sync the target every this many learner steps instead (not the reference's cadence)")
+    p.add_argument("--save-interval", type=int, default=200, help="iterations")
+    p.add_argument("--save-dir", default=".")
+    p.add_argument("--resume", default=None, help="iteration index of model{IDX}.pth in --save-dir, or 'latest'")
+    p.add_argument("--log-dir", default=None, help="event-file directory (default runs/<time>-<env>-learner)")
+    p.add_argument("--no-tb", action="store_true")
+    p.add_argument("--log-interval", type=int, default=20, help="iterations between metric reads (host syncs)")
+    p.add_argument("--eval-interval", type=int, default=0, help="iterations between greedy evaluations (0 = off)")
+    p.add_argument("--eval-episodes", type=int, default=10)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--device", default="cuda:0")
+    p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--json-log", default=None, help="append one JSON record per log interval to this file")
+    return p
+
+
+def config_from_args(a) -> AQLEngineConfig:
+    return AQLEngineConfig(env_id=a.env, n_envs=a.n_envs, capacity=a.capacity, batch_size=a.batch_size,
+                           gamma=a.gamma, n_steps=a.n_steps, lr=a.lr, ent_lam=a.ent_lam,
+                           propose_sample=a.propose_sample, uniform_sample=a.uniform_sample,
+                           action_var=a.action_var, alpha=a.prior_alpha, beta_start=a.prior_beta_start,
+                           max_step=a.max_step, target_update_interval=a.target_update_interval,
+                           target_update_steps=a.target_update_steps, track_losses=True,
+                           use_graphs=not a.no_graphs, seed=a.seed)
+
+
+# ------------------------------------------------------------------ checkpoint
+def model_path(save_dir: str, idx: int) -> str:
+    return os.path.join(save_dir, f"model{idx}.pth")
+
+
+def save_engine(eng: AQLEngine, path: str) -> str:
+    """model{it}.pth (reference keys; the online net incl. its noise buffers) + sidecar."""
+    torch.cuda.synchronize(eng.device)
+    L = eng.learner
+    save_train_state(path, target=eng.target,
+                     counters={"iteration": eng.iterations, "learner_steps": eng.learner_steps},
+                     extra_tensors={"adam_m": L.m, "adam_v": L.v, "step_ctr": L.step_ctr})
+    save_model(eng.model, path)
+    return path
+
+
+def load_engine(eng: AQLEngine, path: str, idx: int) -> dict:
+    """Weights into the engine's flat buffers (parameters are views), then the sidecar if
+    present (Adam moments, step counter, target net, counters); effective NoisyNet weights
+    are recomputed and the actors get the loaded weights.  Training continues at
+    iteration ``idx + 1`` (the file was written after iteration ``idx``)."""
+    load_model(eng.model, path)
+    L = eng.learner
+    counters = {}
+    if os.path.exists(path + ".train.pt"):
+        st = load_train_state(path, target=eng.target, restore_rng=False)
+        L.m.copy_(st["extra"]["adam_m"])
+        L.v.copy_(st["extra"]["adam_v"])
+        L.step_ctr.copy_(st["extra"]["step_ctr"])
+        counters = st["counters"]
+    else:
+        eng.target.load_state_dict(eng.model.state_dict())
+    eng.iterations = int(counters.get("iteration", idx + 1))
+    eng.learner_steps = int(counters.get("learner_steps", 0))
+    L.refresh()
+    eng.publish()
+    torch.cuda.synchronize(eng.device)
+    return counters
+
+
+def latest_index(save_dir: str) -> int | None:
+    idx = []
+    for f in os.listdir(save_dir) if os.path.isdir(save_dir) else []:
+        if f.startswith("model") and f.endswith(".pth") and f[5:-4].isdigit():
+            idx.append(int(f[5:-4]))
+    return max(idx) if idx else None
+
+
+# ------------------------------------------------------------------ evaluation
+def greedy_eval(eng: AQLEngine, episodes: int, seed: int = 12345) -> list[float]:
+    """The reference's evaluation branch (AQL_dis.py:151-167): a CPU copy of the online
+    network with ``q.eval()`` (NoisyNet means), eps 0, env action ``a_mu[0][a]``."""
+    env = envs.make(eng.cfg.env_id)
+    env.seed(seed)
+    cfg = eng.cfg
+    m = AQL(env, propose_sample=cfg.propose_sample, uniform_sample=cfg.uniform_sample,
+            action_var=cfg.action_var, device="cpu")
+    torch.cuda.synchronize(eng.device)
+    m.load_state_dict({k: v.detach().cpu() for k, v in eng.model.state_dict().items()})
+    m.q.eval()
+    out = []
+    limit = int(getattr(env, "_max_episode_steps", None) or 10_000)
+    for _ in range(episodes):
+        s, er = env.reset(), 0.0
+        for _ in range(limit):
+            a, a_mu, _ = m.act(s, 0.0)
+            s, r, d, _ = env.step(a_mu[0][a])
+            er += float(r)
+            if d:
+                break
+        out.append(er)
+    env.close()
+    return out
+
+
+# ------------------------------------------------------------------ main
+def train(a) -> dict:
+    dev = torch.device(a.device)
+    torch.cuda.set_device(dev)
+    eng = AQLEngine(config_from_args(a), dev)
+    start = 0
+    if a.resume is not None:
+        idx = latest_index(a.save_dir) if a.resume == "latest" else int(a.resume)
+        if idx is None:
+            raise SystemExit(f"--resume latest: no model*.pth in {a.save_dir}")
+        counters = load_engine(eng, model_path(a.save_dir, idx), idx)
+        start = eng.iterations
+        print(f"resumed from {model_path(a.save_dir, idx)} at iteration {start} {counters}", flush=True)
+    writer = NullWriter() if a.no_tb else SummaryWriter(a.log_dir, comment=f"-{a.env}-learner")
+    eng.fill()
+    if not a.no_graphs:
+        eng.capture()
+    ep_idx, last = 0, {}
+    t_win, it_win, steps_win = time.perf_counter(), start, eng.learner_steps
+    jl = open(a.json_log, "a") if a.json_log else None
+    try:
+        for it in range(start, a.max_step):
+            eng.iteration()   # act + K SGD steps + publish + (it % 20 == 0) target sync
+            if it % a.save_interval == 0 or it == a.max_step - 1:
+                save_engine(eng, model_path(a.save_dir, it))
+            log_now = (it + 1 - start) % a.log_interval == 0 or it == a.max_step - 1
+            ev = a.eval_interval > 0 and ((it + 1) % a.eval_interval == 0 or it == a.max_step - 1)
+            if not (log_now or ev):
+                continue
+            lq, lp, n = eng.learner.take_loss_means()
+            eps = eng.finished_episodes()
+            now = time.perf_counter()
+            dt = max(now - t_win, 1e-9)
+            if n:
+                writer.add_scalar("learner/loss_q", lq, eng.learner_steps)
+                writer.add_scalar("learner/loss_proposal", lp, eng.learner_steps)
+            for r, length in eps:
+                writer.add_scalar("actor/episode_reward", r, ep_idx)
+                writer.add_scalar("actor/episode_length", length, ep_idx)
+                ep_idx += 1
+            sps = (eng.learner_steps - steps_win) / dt
+            writer.add_scalar("learner/steps_per_sec", sps, eng.learner_steps)
+            writer.add_scalar("actor/env_steps_per_sec", (it + 1 - it_win) * eng.E / dt, eng.learner_steps)
+            last = {"iteration": it, "learner_steps": eng.learner_steps, "loss_q": lq, "loss_proposal": lp,
+                    "episodes": len(eps), "actor_mean_return": float(np.mean([r for r, _ in eps])) if eps else None,
+                    "sgd_steps_per_s": round(sps, 1), "target_syncs": len(eng.target_syncs)}
+            if ev:
+                ret = greedy_eval(eng, a.eval_episodes, seed=a.seed + 7 * it)
+                for k, r in enumerate(ret):
+                    writer.add_scalar("evaluator/episode_reward", r, eng.learner_steps)
+                last["greedy_mean_return"] = float(np.mean(ret))
+            print(json.dumps(last), flush=True)
+            if jl:
+                jl.write(json.dumps(last) + "\n")
+                jl.flush()
+            t_win, it_win, steps_win = time.perf_counter(), it + 1, eng.learner_steps
+    finally:
+        writer.flush()
+        if jl:
+            jl.close()
+    return last
+
+
+def main(argv=None) -> int:
+    train(parser().parse_args(argv))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

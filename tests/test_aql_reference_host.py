@@ -127,3 +127,21 @@ def test_aql_dis_step_matches_reference(env_id):
         for m_o, m_r in ((ours, theirs), (ours_t, theirs_t)):
             for (n, a), b in zip(m_o.state_dict().items(), m_r.state_dict().values()):
                 torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-2 * lr, msg=n)
+
+
+def test_gpu_aql_engine_target_sync_cadence():
+    """engine.aql.target_sync_due: the reference syncs after the SGD loop of every iteration
+    whose index is a multiple of target_update_interval, iteration 0 included
+    (AQL_dis.py:127-129); the learner-step cadence is opt-in."""
+    from apex_amd.engine.aql import AQLEngineConfig, target_sync_due
+
+    cfg = AQLEngineConfig()
+    assert cfg.target_update_interval == 20 and cfg.target_update_steps == 0
+    K = 8
+    due = [it for it in range(101) if target_sync_due(cfg, it, it * K, (it + 1) * K)]
+    assert due == [0, 20, 40, 60, 80, 100]
+    steps = AQLEngineConfig(target_update_steps=100)
+    due = [it for it in range(60) if target_sync_due(steps, it, it * K, (it + 1) * K)]
+    assert due == [12, 24, 37, 49]   # learner-step count crosses 100, 200, 300, 400
+    off = AQLEngineConfig(target_update_interval=0)
+    assert not any(target_sync_due(off, it, 0, 0) for it in range(50))

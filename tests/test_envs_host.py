@@ -1,5 +1,7 @@
-"""CPU tests of the DeepMind Atari wrappers (origin_repo/wrapper.py) on a
-scripted emulator, and of the wrapped synthetic Atari env's observation contract."""
+"""CPU tests of the Atari preprocessing (origin_repo/wrapper.py): the stage
+adapters under the reference's wrapper names on a scripted emulator, the wrapped synthetic
+Atari env's observation contract (Q10: H/W transposed, raw 0..255), and the vectorised
+``AtariPreprocess`` pipeline reproducing the composed wrapper stack step for step."""
 import numpy as np
 import pytest
 
@@ -82,7 +84,7 @@ def test_episodic_life_ends_on_life_loss_without_reset():
     env = atari.EpisodicLifeEnv(Scripted(lives={3: 2}))
     env.reset()
     dones = [env.step(0)[2] for _ in range(3)]
-    assert dones == [False, False, True] and not env.was_real_done
+    assert dones == [False, False, True] and not env.ledger.game_over
     n = env.env.n_resets
     env.reset()  # life lost, game not over: a NOOP step, not an emulator reset
     assert env.env.n_resets == n and env.env.actions[-1] == 0 and env.lives == 2
@@ -90,7 +92,7 @@ def test_episodic_life_ends_on_life_loss_without_reset():
 
 def test_noop_and_fire_reset():
     env = atari.NoopResetEnv(Scripted(), noop_max=30)
-    env.override_num_noops = 5
+    env.fixed_noops = 5
     env.reset()
     assert env.env.actions == [0] * 5
     env = atari.FireResetEnv(Scripted())
@@ -130,3 +132,40 @@ def test_wrapped_synthetic_atari_contract(game):
         if done:
             ob = env.reset()
     assert np.asarray(ob).shape == (4, 84, 84)
+
+
+@pytest.mark.parametrize("game,episode_life,scale", [("Seaquest", 1, 0), ("Pong", 1, 0), ("Breakout", 0, 1)])
+def test_vector_pipeline_matches_wrapper_stack(game, episode_life, scale):
+    """AtariPreprocess over N emulators == N independent make_atari + wrap_atari_dqn stacks:
+    same observations, clipped rewards, life-loss dones and restarts."""
+    from types import SimpleNamespace
+
+    from apex_amd.envs.preprocess import AtariPreprocess, PreprocessSpec
+    from apex_amd.envs.core import make
+
+    args = SimpleNamespace(episode_life=episode_life, clip_rewards=1, frame_stack=1, scale=scale)
+    env_id = f"{game}NoFrameskip-v4"
+    N = 3
+    stacks = [atari.wrap_atari_dqn(atari.make_atari(env_id), args) for _ in range(N)]
+    for i, e in enumerate(stacks):
+        e.seed(11 + i)
+    pipe = AtariPreprocess([make(env_id) for _ in range(N)], PreprocessSpec.from_args(args))
+    pipe.seed(11)
+    obs_v = pipe.reset()
+    obs_w = np.stack([np.asarray(e.reset()) for e in stacks])
+    assert obs_v.shape == (N,) + pipe.obs_shape and np.array_equal(obs_v, obs_w)
+    rng = np.random.default_rng(0)
+    n_done = 0
+    for t in range(300):
+        acts = rng.integers(0, stacks[0].action_space.n, N)
+        obs_v, r_v, d_v, _ = pipe.step(acts)
+        for i, e in enumerate(stacks):
+            o, r, d, _ = e.step(int(acts[i]))
+            assert np.array_equal(obs_v[i], np.asarray(o)), (t, i)
+            assert r_v[i] == r and d_v[i] == d
+            if d:
+                n_done += 1
+                assert np.array_equal(pipe.reset_one(i), np.asarray(e.reset()))
+    assert obs_v.dtype == (np.float32 if scale else np.uint8)
+    if episode_life and game != "Pong":  # Pong has no lives (21-point games)
+        assert n_done > 0  # life losses and the restarts after them were exercised
