@@ -36,8 +36,8 @@ import torch.distributed as dist
 
 from ..models.dqn import DuelingDQN
 from ..models.fused import make_hip_net, make_workspace
-from ..parallel.experience import (META_COLS, STOP, ActorLink, LearnerLinks, Region, apply_packets, link_groups,
-                                   pack_meta)
+from ..parallel.experience import (META_COLS, STOP, ActorLink, Dropped, LearnerLinks, Region, apply_packets,
+                                   engine_nonce, link_groups, pack_meta)
 from ..roles.common import maybe_fault
 from .actor_shard import ActorShard
 from .apex import EngineConfig
@@ -55,7 +55,7 @@ def region_geometry(cfg: EngineConfig, n_actor_ranks: int) -> tuple[int, int]:
 
 class CentralApexEngine:
     def __init__(self, cfg: EngineConfig, device, rank: int | None = None, world: int | None = None,
-                 depth: int = 3, dead_after: float = 30.0, heartbeat_every: int = 50, paced: bool = True):
+                 depth: int = 3, dead_after: float = 30.0, heartbeat_every: float = 0.5, paced: bool = True):
         self.cfg = cfg
         self.device = torch.device(device)
         self.rank = dist.get_rank() if rank is None else rank
@@ -73,9 +73,10 @@ class CentralApexEngine:
         self.is_learner = self.rank == 0
         self.learn_steps = self.actor_steps = 0
         self._g_actor = self._g_learn = None
-        self.groups = link_groups(self.world)  # collective: every rank creates every link group
+        self.groups = link_groups(self.world)  # collective: every rank creates every link's two groups
         self.store = dist.distributed_c10d._get_default_store()
-        self.heartbeat_every = int(heartbeat_every)
+        self.prefix = engine_nonce(self.store)  # collective: per-engine store-key namespace
+        self.heartbeat_every = float(heartbeat_every)  # seconds between actor heartbeats
         # paced: each learner step consumes at most actor_steps_per_learner_step packets per link,
         # so the 3-packet credit window holds every actor at that rate (the single-GPU engine's
         # ratio); unpaced: actors run free and rank 0 ingests everything that landed
@@ -132,11 +133,15 @@ class CentralApexEngine:
         self._fbase = torch.tensor(fb, dtype=torch.int64, device=dev)
         self._sbase = torch.tensor(sb, dtype=torch.int64, device=dev)
         self.links = LearnerLinks(self.world, self.groups, self.store, self.flat, self.rx_frames, self.rx_meta,
-                                  self._apply, dead_after)
+                                  self._apply, dead_after, prefix=self.prefix)
+        # packet-selection index ring: pinned once, reused after its previous H2D copy completed
+        self._sel_host = [torch.empty(R * D, dtype=torch.int64).pin_memory() for _ in range(4)]
+        self._sel_ev = [None] * 4
+        self._sel_k = 0
 
     def _setup_actor_link(self) -> None:
         self.link = ActorLink(self.rank, self.groups[self.rank], self.store, self.flat, self.E, FRAME_BYTES,
-                              self.depth, self.heartbeat_every)
+                              self.depth, self.heartbeat_every, prefix=self.prefix)
         self.pkt_frames = torch.empty(self.E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
         self.pkt_meta = torch.empty(self.E, META_COLS, dtype=torch.int32, device=self.device)
         self.param_version = 0
@@ -179,8 +184,8 @@ class CentralApexEngine:
         self._stage_packet()
 
     def actor_step(self) -> bool:
-        """One actor step + push; False once the learner has stopped this actor."""
-        if self.link.stopped:
+        """One actor step + push; False once the learner has stopped or dropped this actor."""
+        if self.link.stopped or self.link.check_dropped():
             return False
         v = self.link.poll_params()
         if v == STOP:
@@ -193,7 +198,10 @@ class CentralApexEngine:
             self._g_actor.replay()
         else:
             self._actor_body()
-        self.link.push(self.pkt_frames, self.pkt_meta)  # credit window: blocks only with 3 unconsumed
+        try:
+            self.link.push(self.pkt_frames, self.pkt_meta)  # credit window: blocks only with 3 unconsumed
+        except Dropped:
+            return False
         self.actor_steps += 1
         return True
 
@@ -201,8 +209,17 @@ class CentralApexEngine:
     def _apply(self, ready: list[tuple[int, int]]) -> None:
         """ONE batched scatter of every landed packet into its region + one tree write,
         on the learner stream (between learner steps)."""
-        sel = torch.tensor([(r - 1) * self.depth + k for r, k in ready], dtype=torch.int64).pin_memory()
-        idx = sel.to(self.device, non_blocking=True)
+        j = self._sel_k
+        self._sel_k = (j + 1) % len(self._sel_host)
+        if self._sel_ev[j] is not None:
+            self._sel_ev[j].synchronize()  # (long done) this buffer's previous H2D copy
+        n = len(ready)
+        host = self._sel_host[j]
+        for i, (r, k) in enumerate(ready):
+            host[i] = (r - 1) * self.depth + k
+        idx = host[:n].to(self.device, non_blocking=True)
+        ev = self._sel_ev[j] = self._sel_ev[j] or torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
         D, E = self.depth, self.E
         frames = self.rx_frames.view(self.R * D, E, FRAME_BYTES).index_select(0, idx)
         meta = self.rx_meta.view(self.R * D, E, META_COLS).index_select(0, idx)

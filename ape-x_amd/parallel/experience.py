@@ -24,8 +24,12 @@ with ``gloo`` packets are staged through pinned host memory):
 * :class:`ParamLink` / :class:`ParamSubscriber`: conflated, versioned parameter publish
   (reference PUB/SUB with CONFLATE, actor.py:40-49): rank 0 sends the newest snapshot to
   a link only when that link's previous snapshot has been delivered; version -1 = stop.
-* :class:`Heartbeats`: actors post their packet count in the TCPStore; rank 0 drops a
-  link whose count has not moved for ``dead_after`` seconds.
+* :class:`Heartbeats`: actors bump a time-driven beat counter in the TCPStore (also while
+  blocked on credit); rank 0 drops a link whose counter has not moved for ``dead_after``
+  seconds and sets ``<prefix>/drop/<r>``, which a still-running actor sees and exits 0 on
+  (SURVEY §5.3).  Every key carries a per-engine nonce prefix (:func:`engine_nonce`).
+* Each link has two P2P groups (:class:`LinkGroups`): packets and parameters never share
+  an RCCL stream.
 
 Shutdown handshake (bounded, see ``CentralApexEngine.close``): rank 0 sends stop on the
 param channel; the actor publishes its packet count; rank 0 publishes how many packets
@@ -186,9 +190,32 @@ class WorkTracker:
         return True
 
 
+class LinkGroups:
+    """The two P2P channels of one actor link, each on its own group: with ``nccl`` every
+    group is its own RCCL communicator *and stream*, so a receive posted on one channel
+    (the actor's parameter subscription, rank 0's pre-posted packet receives) never sits
+    in front of traffic on the other.  One shared group deadlocks: the actor's first
+    packet would queue behind its posted parameter receive, which waits for a publish
+    that waits for that packet."""
+
+    __slots__ = ("packets", "params")
+
+    def __init__(self, packets, params):
+        self.packets, self.params = packets, params
+
+
 def link_groups(world: int) -> dict:
-    """One P2P group per actor link {r: group([0, r])}; collective: every rank calls it."""
-    return {r: dist.new_group([0, r]) for r in range(1, world)}
+    """{r: LinkGroups} for every actor rank r; collective: every rank calls it (same order)."""
+    return {r: LinkGroups(dist.new_group([0, r]), dist.new_group([0, r])) for r in range(1, world)}
+
+
+def engine_nonce(store) -> str:
+    """A key prefix unique to this engine instance (rank 0 draws it from the store, every
+    rank learns it through a broadcast; collective): a second engine on the same store
+    never reads the handshake / heartbeat keys of an earlier one."""
+    box = [int(store.add("apex/engine_gen", 1)) if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return f"apex/{box[0]}"
 
 
 class PacketSender:
@@ -209,11 +236,16 @@ class PacketSender:
         self.k = 0
         self.n_sent = 0
 
-    def acquire(self, timeout: float = 60.0):
+    def acquire(self, timeout: float = 60.0, on_wait=None, every: float = 0.25):
         """(frames, meta) buffers of the next slot, once its previous send has left
-        (credit window).  Raises TimeoutError if the learner stopped draining."""
-        if not self.track.wait(self.works[self.k], timeout):
-            raise TimeoutError(f"experience link to rank {self.dst}: no credit for {timeout}s")
+        (credit window).  ``on_wait()`` runs every ``every`` s while blocked (heartbeat,
+        drop check; it may raise).  Raises TimeoutError if the learner stopped draining."""
+        deadline = time.monotonic() + timeout
+        while not self.track.wait(self.works[self.k], every if on_wait else timeout):
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"experience link to rank {self.dst}: no credit for {timeout}s")
+            if on_wait is not None:
+                on_wait()
         self.works[self.k] = None
         return self.frames[self.k], self.meta[self.k]
 
@@ -416,16 +448,25 @@ class ParamSubscriber:
 
 
 class Heartbeats:
-    """Liveness through the rendezvous TCPStore (off the data path): actors post their
-    packet count; rank 0 marks a link dead when it stops moving for ``dead_after`` s."""
+    """Liveness through the rendezvous TCPStore (off the data path).  An actor bumps a beat
+    counter on a wall-clock period -- also while it waits for credit, so a rank-0 pause
+    (graph capture, a checkpoint) never makes healthy, blocked actors look dead; rank 0
+    drops a link whose counter has not moved for ``dead_after`` seconds of its own clock
+    (only changes are compared, so host clocks need not agree)."""
 
-    def __init__(self, store, ranks, dead_after: float = 30.0, prefix: str = "apex/hb"):
+    def __init__(self, store, ranks, dead_after: float = 30.0, prefix: str = "apex/hb", period: float = 0.5):
         self.store, self.prefix, self.dead_after = store, prefix, float(dead_after)
+        self.period = float(period)
         now = time.monotonic()
         self.last = {r: (None, now) for r in ranks}
+        self._count, self._t = 0, 0.0
 
-    def beat(self, rank: int, count: int) -> None:
-        self.store.set(f"{self.prefix}/{rank}", str(count))
+    def beat(self, rank: int, force: bool = False) -> None:
+        now = time.monotonic()
+        if force or now - self._t >= self.period:
+            self._t = now
+            self._count += 1
+            self.store.set(f"{self.prefix}/{rank}", str(self._count))
 
     def stale(self, ranks) -> list[int]:
         out, now = [], time.monotonic()
@@ -440,6 +481,10 @@ class Heartbeats:
         return out
 
 
+class Dropped(RuntimeError):
+    """Raised on an actor whose link rank 0 has dropped (it should exit cleanly)."""
+
+
 class LearnerLinks:
     """Rank-0 side of every actor link: pre-posted packet receives, conflated parameter
     publish, heartbeats, dropping dead links and the bounded stop handshake.  Landed
@@ -447,15 +492,15 @@ class LearnerLinks:
     ``frames[rank - 1, slot]`` / ``meta[rank - 1, slot]`` (device tensors)."""
 
     def __init__(self, world: int, groups: dict, store, flat: torch.Tensor, frames: torch.Tensor,
-                 meta: torch.Tensor, apply, dead_after: float = 30.0, log=print):
-        self.store, self.apply_fn, self.log = store, apply, log
+                 meta: torch.Tensor, apply, dead_after: float = 30.0, log=print, prefix: str = "apex"):
+        self.store, self.apply_fn, self.log, self.prefix = store, apply, log, prefix
         self.frames, self.meta = frames, meta
         dev = frames.device
-        self.inbox = {r: PacketInbox(r, frames[r - 1], meta[r - 1], groups[r], dev) for r in range(1, world)}
+        self.inbox = {r: PacketInbox(r, frames[r - 1], meta[r - 1], groups[r].packets, dev) for r in range(1, world)}
         for ib in self.inbox.values():
             ib.start()
-        self.params = {r: ParamLink(flat, r, groups[r]) for r in range(1, world)}
-        self.hb = Heartbeats(store, range(1, world), dead_after)
+        self.params = {r: ParamLink(flat, r, groups[r].params) for r in range(1, world)}
+        self.hb = Heartbeats(store, range(1, world), dead_after, prefix=f"{prefix}/hb")
         self.live = set(range(1, world))
         self.dropped: dict[int, str] = {}
         self.applied = {r: 0 for r in range(1, world)}
@@ -468,6 +513,10 @@ class LearnerLinks:
             self.live.discard(r)
             self.dropped[r] = why
             self.inbox[r].dead = True
+            try:  # tell a still-running actor to stop (it polls this key and exits 0)
+                self.store.set(f"{self.prefix}/drop/{r}", why[:200])
+            except Exception:
+                pass
             if self.log:
                 self.log(f"[central] dropping actor rank {r}: {why}")
 
@@ -537,13 +586,13 @@ class LearnerLinks:
         for r in sorted(self.live):
             ib = self.inbox[r]
             try:
-                self.store.wait([f"apex/sent/{r}"], timedelta(seconds=timeout))
-                sent = int(self.store.get(f"apex/sent/{r}"))
+                self.store.wait([f"{self.prefix}/sent/{r}"], timedelta(seconds=timeout))
+                sent = int(self.store.get(f"{self.prefix}/sent/{r}"))
             except Exception as e:
                 self.drop(r, f"no packet count: {e!r}")
                 continue
             need = max(ib.n_posted, sent)
-            self.store.set(f"apex/need/{r}", str(need))
+            self.store.set(f"{self.prefix}/need/{r}", str(need))
             deadline = time.monotonic() + timeout
             while ib.n_done < need and not ib.dead and time.monotonic() < deadline:
                 ks = ib.poll()
@@ -565,17 +614,21 @@ class LearnerLinks:
 
 
 class ActorLink:
-    """Actor side of one link: packet send ring (credit window), parameter subscription,
-    heartbeat and the stop handshake."""
+    """Actor side of one link: packet send ring (credit window) on the packet channel,
+    parameter subscription on the parameter channel, time-driven heartbeat, the drop
+    signal and the stop handshake."""
 
-    def __init__(self, rank: int, group, store, flat: torch.Tensor, E: int, frame_bytes: int, depth: int = 3,
-                 heartbeat_every: int = 50):
-        self.rank, self.store = rank, store
-        self.sender = PacketSender(E, frame_bytes, flat.device, group, dst=0, depth=depth)
-        self.sub = ParamSubscriber(flat, 0, group)
-        self.hb = Heartbeats(store, [])
-        self.heartbeat_every = int(heartbeat_every)
+    def __init__(self, rank: int, groups: LinkGroups, store, flat: torch.Tensor, E: int, frame_bytes: int,
+                 depth: int = 3, heartbeat_every: float = 0.5, prefix: str = "apex"):
+        self.rank, self.store, self.prefix = rank, store, prefix
+        self.sender = PacketSender(E, frame_bytes, flat.device, groups.packets, dst=0, depth=depth)
+        self.sub = ParamSubscriber(flat, 0, groups.params)
+        self.hb = Heartbeats(store, [], prefix=f"{prefix}/hb", period=heartbeat_every)
+        self.hb.beat(rank, force=True)
+        self._drop_key = f"{prefix}/drop/{rank}"
+        self._drop_t = 0.0
         self.stopped = False
+        self.dropped = False
         self.steps = 0
 
     def poll_params(self):
@@ -585,20 +638,34 @@ class ActorLink:
             self.finish()
         return v
 
+    def check_dropped(self, every: float = 0.5) -> bool:
+        """True once rank 0 has dropped this link (checked at most every ``every`` s)."""
+        now = time.monotonic()
+        if not self.dropped and now - self._drop_t >= every:
+            self._drop_t = now
+            self.dropped = bool(self.store.check([self._drop_key]))
+        return self.dropped
+
+    def _waiting(self) -> None:
+        self.hb.beat(self.rank)
+        if self.check_dropped(every=0.0):
+            raise Dropped(f"actor rank {self.rank}: dropped by the learner "
+                          f"({self.store.get(self._drop_key).decode(errors='replace')})")
+
     def push(self, frames: torch.Tensor, meta: torch.Tensor, timeout: float = 120.0) -> None:
-        f, m = self.sender.acquire(timeout)
+        """Send one packet; raises :class:`Dropped` if rank 0 dropped this link meanwhile."""
+        f, m = self.sender.acquire(timeout, on_wait=self._waiting)
         f.copy_(frames, non_blocking=True)  # host-staged: the send waits for this copy's event
         m.copy_(meta, non_blocking=True)
         self.sender.send()
         self.steps += 1
-        if self.steps % self.heartbeat_every == 0:
-            self.hb.beat(self.rank, self.sender.n_sent)
+        self.hb.beat(self.rank)
 
     def finish(self, timeout: float = 120.0) -> None:
         r = self.rank
-        self.store.set(f"apex/sent/{r}", str(self.sender.n_sent))
-        self.store.wait([f"apex/need/{r}"], timedelta(seconds=timeout))
-        need = int(self.store.get(f"apex/need/{r}"))
+        self.store.set(f"{self.prefix}/sent/{r}", str(self.sender.n_sent))
+        self.store.wait([f"{self.prefix}/need/{r}"], timedelta(seconds=timeout))
+        need = int(self.store.get(f"{self.prefix}/need/{r}"))
         while self.sender.n_sent < need:
             self.sender.send_dummy(timeout)
         self.sender.drain(timeout)

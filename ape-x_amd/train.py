@@ -244,8 +244,13 @@ def main(argv=None) -> int:
         if learner is not None and step % bps_every == 0:
             torch.cuda.synchronize(device)
             now = time.perf_counter()
-            sps = (step - step_last) / (now - t_last)
+            dt_log = now - t_last
+            sps = (step - step_last) / dt_log
             t_last, step_last = now, step
+            if topology == "central" and rank == 0:  # async links: frames that actually reached the replay
+                applied = sum(eng.applied.values())
+                fps_measured = (applied - getattr(eng, "_applied_last", 0)) * eng.frames_per_actor_step / dt_log
+                eng._applied_last = applied
             if learner is not None and rank == 0:
                 st = learner.stats()
                 # sharded DP: one synchronous update per step over a global batch of B * world, so
@@ -254,7 +259,8 @@ def main(argv=None) -> int:
                         "learner/grad_norm_l2": st["grad_norm_l2"], "learner/BPS": sps,
                         "learner/updates_per_sec": sps,
                         "learner/batches_per_sec": sps * (world if topology == "sharded" else 1),
-                        "actor/frames_per_sec": sps * frames_per_round}
+                        "actor/frames_per_sec": (fps_measured if topology == "central"
+                                                 else sps * frames_per_round)}
                 if evaluator is not None:
                     for r, n in evaluator.poll():
                         eval_rets.append(r)

@@ -172,7 +172,7 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
     from apex_amd.engine.central import CentralApexEngine
 
     dev = torch.device("cuda", 0)
-    eng = CentralApexEngine(_central_cfg(), dev, rank, world, dead_after=dead_after, heartbeat_every=5)
+    eng = CentralApexEngine(_central_cfg(), dev, rank, world, dead_after=dead_after, heartbeat_every=0.05)
     _progress("engine built")
     g = eng.groups
     if rank != 0:

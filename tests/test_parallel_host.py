@@ -229,7 +229,7 @@ def _links_body(rank, world, E, FB, kill_rank, kill_at, q):
     store = dist.distributed_c10d._get_default_store()
     flat = torch.zeros(16)
     if rank > 0:
-        link = ActorLink(rank, groups[rank], store, flat, E, FB, depth=3, heartbeat_every=2)
+        link = ActorLink(rank, groups[rank], store, flat, E, FB, depth=3, heartbeat_every=0.05)
         versions, k = [], 0
         while True:
             v = link.poll_params()
