@@ -160,8 +160,8 @@ class AQLEngineConfig:
     action_var: float = 0.25
     alpha: float = 0.6
     beta_start: float = 0.4
-    max_step: int = 1_000_000      # beta annealing horizon, in iterations (AQL_dis.py:57)
-    n_workers: int = 10            # the reference's beta-annealing factor (AQL_dis.py:57)
+    max_step: int = 1_000_000      # beta annealing horizon, in iterations (AQL_dis.py:59)
+    n_workers: int = 10            # the reference's beta-annealing factor (AQL_dis.py:59)
     max_norm: float = 40.0
     learner_steps: int | None = None   # per iteration; None = n_envs // batch_size
     target_update_interval: int = 20   # iterations between target syncs, iteration 0 included (AQL_dis.py:127)
@@ -523,7 +523,7 @@ class AQLEngine:
         torch.cuda.synchronize(self.device)
 
     def _beta(self) -> float:
-        c = self.cfg  # AQL_dis.py:57 operator precedence kept
+        c = self.cfg  # AQL_dis.py:59 operator precedence kept
         return min(1.0, c.beta_start + self.iterations * (1.0 - c.beta_start) / c.max_step * c.n_workers)
 
     def iteration(self) -> None:

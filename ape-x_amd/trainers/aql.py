@@ -312,7 +312,7 @@ class train_AQL_dis(_AQLBase):  # AQL_dis.py train_DQN
         self.learn_idx = 0
 
     def beta_by_frame(self, t):
-        # AQL_dis.py:57 (operator precedence kept: .../max_step*n_workers)
+        # AQL_dis.py:59 (operator precedence kept: .../max_step*n_workers)
         return min(1.0, self.prior_beta_start + t * (1.0 - self.prior_beta_start) / self.max_step * self.n_workers)
 
     def compute_td_loss(self, batch_size, beta):
