@@ -38,6 +38,7 @@ from ..models.dqn import DuelingDQN
 from ..models.fused import make_hip_net, make_workspace
 from ..parallel.experience import (META_COLS, STOP, ActorLink, Dropped, LearnerLinks, Region, apply_packets,
                                    engine_nonce, link_groups, pack_meta)
+from ..parallel.ipc import IpcActorLink, IpcLearnerLinks, packet_bytes
 from ..roles.common import maybe_fault
 from .actor_shard import ActorShard
 from .apex import EngineConfig
@@ -55,7 +56,11 @@ def region_geometry(cfg: EngineConfig, n_actor_ranks: int) -> tuple[int, int]:
 
 class CentralApexEngine:
     def __init__(self, cfg: EngineConfig, device, rank: int | None = None, world: int | None = None,
-                 depth: int = 3, dead_after: float = 30.0, heartbeat_every: float = 0.5, paced: bool = True):
+                 depth: int = 3, dead_after: float = 30.0, heartbeat_every: float = 0.5, paced: bool = True,
+                 transport: str = "auto"):
+        """``transport``: "ipc" (HIP IPC rings in rank 0's HBM, parallel/ipc.py; the default on
+        GPUs), "p2p" (torch.distributed isend/irecv links, parallel/experience.py; CPU tests and
+        the host-staged gloo rehearsal) or "auto"."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.rank = dist.get_rank() if rank is None else rank
@@ -73,7 +78,13 @@ class CentralApexEngine:
         self.is_learner = self.rank == 0
         self.learn_steps = self.actor_steps = 0
         self._g_actor = self._g_learn = None
-        self.groups = link_groups(self.world)  # collective: every rank creates every link's two groups
+        if transport == "auto":
+            transport = "ipc" if self.device.type == "cuda" else "p2p"
+        if transport not in ("ipc", "p2p"):
+            raise ValueError("transport must be ipc | p2p | auto")
+        self.transport = transport
+        # p2p: collective, every rank creates every link's two groups (ipc needs none)
+        self.groups = link_groups(self.world) if transport == "p2p" else None
         self.store = dist.distributed_c10d._get_default_store()
         self.prefix = engine_nonce(self.store)  # collective: per-engine store-key namespace
         self.heartbeat_every = float(heartbeat_every)  # seconds between actor heartbeats
@@ -125,6 +136,10 @@ class CentralApexEngine:
 
     def _setup_learner_links(self, dead_after: float) -> None:
         R, D, E, dev = self.R, self.depth, self.E, self.device
+        if self.transport == "ipc":
+            self.links = IpcLearnerLinks(R, D, E, self.flat.numel(), self.replay, self.regions, self.store,
+                                         self.prefix, dev, cap=self.ingest_cap, dead_after=dead_after)
+            return
         self.rx_frames = torch.empty(R, D, E, FRAME_BYTES, dtype=torch.uint8, device=dev)
         self.rx_meta = torch.empty(R, D, E, META_COLS, dtype=torch.int32, device=dev)
         # per receive slot (link r, ring slot k): the region's frame / transition-slot base
@@ -140,6 +155,17 @@ class CentralApexEngine:
         self._sel_k = 0
 
     def _setup_actor_link(self) -> None:
+        if self.transport == "ipc":
+            E, FB = self.E, FRAME_BYTES
+            self.pkt = torch.empty(packet_bytes(E), dtype=torch.uint8, device=self.device)
+            self.pkt_frames = self.pkt[:E * FB].view(E, FB)
+            self.pkt_meta = self.pkt[E * FB:].view(torch.int32).view(E, META_COLS)
+            self.link = IpcActorLink(self.rank, self.store, self.prefix, self.flat, self.pkt, self.device,
+                                     self.heartbeat_every)
+            self.param_version = 0
+            self._stage_packet(initial=True)  # the reset frames are the first packet
+            self.link.push()
+            return
         self.link = ActorLink(self.rank, self.groups[self.rank], self.store, self.flat, self.E, FRAME_BYTES,
                               self.depth, self.heartbeat_every, prefix=self.prefix)
         self.pkt_frames = torch.empty(self.E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
@@ -162,7 +188,8 @@ class CentralApexEngine:
 
     @property
     def applied(self) -> dict:
-        return self.links.applied
+        """Packets applied per actor rank (ipc: device counters, one host sync)."""
+        return self.links.applied() if self.transport == "ipc" else self.links.applied
 
     # ------------------------------------------------------------------ actor ranks
     def _stage_packet(self, initial: bool = False) -> None:
@@ -185,6 +212,8 @@ class CentralApexEngine:
 
     def actor_step(self) -> bool:
         """One actor step + push; False once the learner has stopped or dropped this actor."""
+        if self.transport == "ipc":
+            return self._actor_step_ipc()
         if self.link.stopped or self.link.check_dropped():
             return False
         v = self.link.poll_params()
@@ -201,6 +230,23 @@ class CentralApexEngine:
         try:
             self.link.push(self.pkt_frames, self.pkt_meta)  # credit window: blocks only with 3 unconsumed
         except Dropped:
+            return False
+        self.actor_steps += 1
+        return True
+
+    def _actor_step_ipc(self) -> bool:
+        v = self.link.poll_params()
+        if v == STOP:
+            return False
+        if v is not None:
+            self.net.repack()
+            self.param_version = v
+        maybe_fault("actor", self.rank, self.actor_steps)
+        if self._g_actor is not None:
+            self._g_actor.replay()
+        else:
+            self._actor_body()
+        if not self.link.push():  # credit window of ``depth`` packets; False: stopped / dropped
             return False
         self.actor_steps += 1
         return True
@@ -228,6 +274,9 @@ class CentralApexEngine:
         self.replay.write_priorities(slots, prio, dedup=False, bumps=((self.replay.filled, len(ready) * E),))
 
     def ingest(self, cap: int | None = None) -> int:
+        if self.transport == "ipc":  # device-side (normally captured in the learner graph)
+            self.links.ingest()
+            return 0
         return self.links.ingest(cap)
 
     def publish_params(self) -> None:
@@ -235,11 +284,16 @@ class CentralApexEngine:
         if self.is_learner:
             self.links.publish(self.flat)
 
+    def _learner_body(self) -> None:
+        self.learner.step()
+        if self.transport == "ipc":  # ingest rides in the learner graph: no host poll per step
+            self.links.ingest()
+
     def learner_step(self) -> None:
         if self._g_learn is not None:
             self._g_learn.replay()
         else:
-            self.learner.step()
+            self._learner_body()
         self.learn_steps += 1
         if self.learn_steps % self.cfg.target_update_interval == 0:
             self.learner.sync_target()
@@ -260,6 +314,16 @@ class CentralApexEngine:
             return
         need = -(-self.cfg.threshold_size // self.E)
         deadline = time.monotonic() + timeout
+        if self.transport == "ipc":
+            while sum(self.applied.values()) < need + len(self.live):
+                if not self.live or time.monotonic() > deadline:
+                    raise RuntimeError(f"central fill: {sum(self.applied.values())} packets after {timeout}s, "
+                                       f"live actors {sorted(self.live)}")
+                self.links.ingest(drain=True)
+                torch.cuda.synchronize(self.device)
+                self.links.check_heartbeats()
+                time.sleep(0.0005)
+            return
         while sum(self.applied.values()) < need + len(self.live):
             if not self.live or time.monotonic() > deadline:
                 raise RuntimeError(f"central fill: {sum(self.applied.values())} packets after {timeout}s, "
@@ -272,12 +336,12 @@ class CentralApexEngine:
         """hipGraphs of the compute bodies (the links stay eager around them)."""
         pool = torch.cuda.graph_pool_handle()
         if self.is_learner:
-            self.learner.step()  # eager warm-up (a real step)
+            self._learner_body()  # eager warm-up (a real step)
             self.learn_steps += 1
             torch.cuda.synchronize(self.device)
             self._g_learn = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self._g_learn, pool=pool, capture_error_mode="thread_local"):
-                self.learner.step()
+                self._learner_body()
         else:
             if not self.actor_step():  # eager warm-up (a real, pushed step)
                 return
@@ -296,7 +360,8 @@ class CentralApexEngine:
                     return False
             return True
         self.learner_step()
-        self.ingest(self.ingest_cap)
+        if self.transport == "p2p":
+            self.ingest(self.ingest_cap)
         if self.learn_steps % self.cfg.publish_param_interval == 0:
             self.publish_params()
         self.links.check_heartbeats()

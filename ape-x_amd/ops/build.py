@@ -48,7 +48,9 @@ HIP_SOURCES = [
     "fc_kernels.hip",
     "loss_heads_kernels.hip",
     "f32_kernels.hip",
+    "ipc_kernels.hip",
     "comm.cpp",
+    "ipc.cpp",
 ]
 
 

@@ -58,9 +58,11 @@ struct NStepHandle {
 }  // namespace
 
 void register_comm(py::module_& m);  // comm.cpp (direct RCCL)
+void register_ipc(py::module_& m);   // ipc.cpp (HIP IPC experience transport)
 
 PYBIND11_MODULE(_apex_hip, m) {
   register_comm(m);
+  register_ipc(m);
   m.doc() = "apex_amd gfx950 kernels (HBM replay, actor shard, fused learner)";
   m.attr("arch") = "gfx950";
 

@@ -1,0 +1,157 @@
+// Central-replay experience transport over HIP IPC (xGMI peer writes), device side.
+//
+// Reference: actor.py:105-115 pushes pickled 50-transition batches over ZeroMQ with a credit
+// window of 3; replay.py:77-107 unpickles them under one asyncio lock; learner.py:57-68 /
+// actor.py:40-49 publish parameters PUB/SUB with CONFLATE.  Here (parallel/ipc.py):
+//
+//   * rank 0 owns an UNCACHED device arena (hipDeviceMallocUncached: every access bypasses
+//     L2, so writes that peers DMA into it over xGMI are never shadowed by a stale L2 line):
+//       ring[R][D] packets  (packet = E frames [E][7056] u8 | E metadata rows [E][14] i32)
+//       seq[R][D]  int64    (packet number + 1 of what the slot holds; 0 = never written)
+//       params[2][P] fp32   (versioned double buffer the actors pull)
+//   * an actor DMAs its packet into ring[r][n % D] (hipMemcpyAsync to the IPC-mapped pointer),
+//     then -- same stream, so after the data has landed -- ipc_seq_k stores n + 1 into
+//     seq[r][n % D] with a system-scope release.
+//   * rank 0's learner graph, between learner steps, runs
+//       ipc_scan_k    : per link, how many packets are ready in order from consumed[r]
+//                       (system-scope acquire loads of seq; capped per link = pacing);
+//       ipc_apply_k   : scatters every ready packet's frames and rows into the link's region
+//                       of the HBM replay, and emits (global slot | -1, priority) pairs for
+//                       the tree write (per_write_* skip slot -1);
+//       ipc_release_k : consumed[r] += ready[r], published to the host control block
+//                       (system-scope store into hipHostRegister'ed /dev/shm, which the actor
+//                       processes read as their credit) and the replay's fill counter.
+//     No host polling and no host sync: the whole ingest is four captured launches.
+//   * parameters: rank 0 copies the master weights into params[v & 1] on its stream, then
+//     ipc_flag_k publishes v to the control block; actors read v there and pull the slot
+//     (seqlock check on the version around the copy).
+#include "common.h"
+#include "kernels.h"
+
+namespace apex {
+namespace {
+
+constexpr int kMetaCols = 14;
+constexpr int kFrameBytes = 84 * 84;
+constexpr int kFrameVec = kFrameBytes / 16;  // 441 x 16 B
+static_assert(kFrameBytes % 16 == 0, "frames are copied in 16-byte vectors");
+
+__device__ __forceinline__ int64_t load_acquire_sys(const int64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void store_release_sys(int64_t* p, int64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void ipc_scan_k(IpcIngest g) {
+  const int r = threadIdx.x;
+  if (r >= g.R) return;
+  int n = 0;
+  if (g.live == nullptr || g.live[r]) {
+    const int64_t c = g.consumed[r];
+    for (int j = 0; j < g.cap; ++j) {
+      const int64_t want = c + j + 1;
+      if (load_acquire_sys(g.seq + (int64_t)r * g.D + (want - 1) % g.D) != want) break;
+      ++n;
+    }
+  }
+  g.ready[r] = n;
+}
+
+// grid: R * cap * (E / kRows) blocks of 256 threads; block -> (link r, window j, env rows)
+constexpr int kRows = 4;
+
+__global__ __launch_bounds__(256) void ipc_apply_k(IpcIngest g) {
+  const int chunks = g.E / kRows;
+  const int b = blockIdx.x;
+  const int r = b / (g.cap * chunks);
+  const int j = (b / chunks) % g.cap;
+  const int e0 = (b % chunks) * kRows;
+  const int t = threadIdx.x;
+  const int64_t out0 = ((int64_t)r * g.cap + j) * g.E + e0;
+  if (j >= g.ready[r]) {  // nothing landed in this window position: mask the tree write
+    if (t < kRows) g.slots_out[out0 + t] = -1;
+    return;
+  }
+  const int k = (int)((g.consumed[r] + j) % g.D);
+  const uint8_t* pkt = g.ring + ((int64_t)r * g.D + k) * g.packet_bytes;
+  const int32_t* meta = reinterpret_cast<const int32_t*>(pkt + (int64_t)g.E * kFrameBytes);
+  const int64_t fbase = g.frame_base[r], sbase = g.slot_base[r];
+  // frames: kRows x 441 16-byte vectors, strided over the block (uncached source, HBM target)
+  for (int v = t; v < kRows * kFrameVec; v += 256) {
+    const int e = e0 + v / kFrameVec, w = v % kFrameVec;
+    const int32_t fs = meta[e * kMetaCols + 13];
+    if (fs < 0) continue;  // filler row
+    const uint4 x = reinterpret_cast<const uint4*>(pkt + (int64_t)e * kFrameBytes)[w];
+    reinterpret_cast<uint4*>(g.frames + (fbase + fs) * kFrameBytes)[w] = x;
+  }
+  if (t < kRows) {
+    const int e = e0 + t;
+    const int32_t* m = meta + e * kMetaCols;
+    const int32_t ls = m[12];
+    if (ls < 0) {
+      g.slots_out[out0 + t] = -1;
+      return;
+    }
+    const int64_t slot = sbase + ls;
+    const int32_t fb = (int32_t)fbase;
+    int4 s = make_int4(m[0] + fb, m[1] + fb, m[2] + fb, m[3] + fb);
+    int4 s2 = make_int4(m[4] + fb, m[5] + fb, m[6] + fb, m[7] + fb);
+    reinterpret_cast<int4*>(g.s_ids)[slot] = s;
+    reinterpret_cast<int4*>(g.s2_ids)[slot] = s2;
+    g.action[slot] = m[8];
+    g.reward[slot] = __int_as_float(m[9]);
+    g.done[slot] = __int_as_float(m[10]);
+    g.slots_out[out0 + t] = (int32_t)slot;
+    g.prio_out[out0 + t] = __int_as_float(m[11]);
+  }
+}
+
+__global__ void ipc_release_k(IpcIngest g) {
+  __shared__ int64_t total;
+  if (threadIdx.x == 0) total = 0;
+  __syncthreads();
+  const int r = threadIdx.x;
+  if (r < g.R) {
+    const int n = g.ready[r];
+    const int64_t c = g.consumed[r] + n;
+    g.consumed[r] = c;
+    if (g.applied) g.applied[r] += n;
+    // the ring slots are free again: the actor processes read this word as their credit
+    if (g.host_consumed) store_release_sys(g.host_consumed + r, c);
+    if (n) atomicAdd(reinterpret_cast<unsigned long long*>(&total), (unsigned long long)n);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && g.filled && total) g.filled[0] += total * g.E;
+}
+
+__global__ void ipc_flag_k(int64_t* p, int64_t v) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) store_release_sys(p, v);
+}
+
+}  // namespace
+
+void ipc_ingest(const IpcIngest& g, hipStream_t s) {
+  if (g.R < 1 || g.R > 1024 || g.D < 1 || g.cap < 1 || g.cap > g.D || g.E < kRows || g.E % kRows)
+    throw std::invalid_argument("ipc_ingest: bad geometry (R <= 1024, 1 <= cap <= D, E a multiple of 4)");
+  if (g.packet_bytes < (int64_t)g.E * (kFrameBytes + kMetaCols * 4))
+    throw std::invalid_argument("ipc_ingest: packet stride smaller than a packet");
+  if (!g.ring || !g.seq || !g.consumed || !g.ready || !g.frames || !g.s_ids || !g.s2_ids || !g.action || !g.reward ||
+      !g.done || !g.slots_out || !g.prio_out || !g.frame_base || !g.slot_base)
+    throw std::invalid_argument("ipc_ingest: null pointer");
+  const int thr = ((g.R + 63) / 64) * 64;
+  ipc_scan_k<<<1, thr, 0, s>>>(g);
+  LAUNCH_CHECK();
+  ipc_apply_k<<<g.R * g.cap * (g.E / kRows), 256, 0, s>>>(g);
+  LAUNCH_CHECK();
+  ipc_release_k<<<1, thr, 0, s>>>(g);
+  LAUNCH_CHECK();
+}
+
+void ipc_flag(int64_t* p, int64_t v, hipStream_t s) {
+  if (!p) throw std::invalid_argument("ipc_flag: null pointer");
+  ipc_flag_k<<<1, 64, 0, s>>>(p, v);
+  LAUNCH_CHECK();
+}
+
+}  // namespace apex

@@ -503,4 +503,26 @@ void aql_env_reset(const AqlEnv& e, hipStream_t s);
 void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, const float* amu, const AqlInsert& ins,
                   hipStream_t s);
 
+// ---- central-replay experience transport over HIP IPC (ipc_kernels.hip, parallel/ipc.py)
+struct IpcIngest {
+  int R, D, E, cap;                 // actor links, ring depth, envs per packet, packets per link per ingest
+  int64_t packet_bytes;             // ring slot stride (>= E * (7056 + 56))
+  const uint8_t* ring;              // [R][D] packets (uncached arena)
+  const int64_t* seq;               // [R][D] packet number + 1 held by each slot
+  int64_t* consumed;                // [R] packets applied so far (device)
+  int* ready;                       // [R] scratch: packets applied by this ingest
+  const int* live;                  // [R] 0 = link dropped (optional)
+  int64_t* host_consumed;           // [R] device view of the host control block (credit; optional)
+  int64_t* applied;                 // [R] statistics (optional)
+  int64_t* filled;                  // replay fill counter += E per packet (optional)
+  uint8_t* frames;                  // replay frame ring [F][7056]
+  int32_t *s_ids, *s2_ids, *action; // [C][4], [C][4], [C]
+  float *reward, *done;             // [C]
+  const int64_t *frame_base, *slot_base;  // [R] region offsets
+  int32_t* slots_out;               // [R * cap * E] global slot or -1 (tree write input)
+  float* prio_out;                  // [R * cap * E]
+};
+void ipc_ingest(const IpcIngest& g, hipStream_t s);
+void ipc_flag(int64_t* p, int64_t v, hipStream_t s);  // system-scope release store of v (one thread)
+
 }  // namespace apex

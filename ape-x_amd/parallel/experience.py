@@ -631,6 +631,10 @@ class ActorLink:
         self.dropped = False
         self.steps = 0
 
+    @property
+    def n_sent(self) -> int:
+        return self.sender.n_sent
+
     def poll_params(self):
         """None / the newly installed version / STOP (after which the handshake has run)."""
         v = self.sub.poll()

@@ -1,0 +1,398 @@
+"""Central-replay experience transport over HIP IPC (SURVEY §2.4 M1/M4, §5.3, §5.8;
+reference actor.py:40-49,105-115, replay.py:77-146, learner.py:57-68).
+
+MI355X-native replacement of the reference's ZeroMQ actor -> replay pushes and PUB/SUB
+parameter publish, for actor GPUs on the same node (xGMI):
+
+* **Data plane (device memory, no host on the path).**  Rank 0 allocates one *uncached*
+  arena in its HBM (``ipc_alloc(mode=2)``: loads and stores bypass L2, so bytes that peers
+  write over xGMI are never hidden behind a stale L2 line) holding, per actor link r, a
+  ring of ``D`` packet slots and their sequence words, plus a double-buffered parameter
+  block.  The arena is exported once with ``hipIpcGetMemHandle`` through the TCPStore.
+  An actor pushes a packet (one actor step: E new frames + E transition rows) with ONE
+  ``hipMemcpyAsync`` into its next ring slot over xGMI and then, stream-ordered behind the
+  copy, a one-thread system-scope release store of the packet number into the slot's
+  sequence word.  Rank 0 ingests inside its learner hipGraph (``ipc_ingest``: scan the
+  sequence words with system-scope acquires, scatter every ready packet into the link's
+  replay region, release the slots), followed by one masked tree write -- no Python
+  polling, no receive left posted, no host sync per step.
+* **Control plane (host memory).**  A small ``/dev/shm`` control block, mapped into every
+  process (rank 0 also registers it with ``hipHostRegister`` so its kernels can store
+  into it): per-link *consumed* counters written by rank 0's release kernel (the actors'
+  credit window, actor.py:105-115: at most ``D`` packets in flight), the published
+  parameter version, per-link heartbeat counters, drop flags, the stop flag and stop
+  acknowledgements.  The actors read and write it with plain CPU loads / stores.
+* **Parameters** (conflated, learner.py:57-68 PUB/SUB CONFLATE=1): rank 0 copies its master
+  weights into ``params[v & 1]`` on its stream, then stores ``v`` into the control block
+  (release), having announced ``v`` in a *begin* word before the copy (seqlock writer).  An
+  actor that sees a newer version pulls that half with one peer copy and then re-reads the
+  begin word: if version ``v + 2`` was announced meanwhile the half may have been
+  rewritten, and the pull is retried.  Slow actors simply skip versions.
+* **Liveness** (SURVEY §5.3): actors bump a heartbeat word on a wall-clock period (also
+  while waiting for credit); rank 0 drops a link whose word stopped moving for
+  ``dead_after`` s: its ingest mask goes to 0 and its drop flag tells a live-but-stuck actor
+  to exit.  Stop = flag + acknowledgement, then rank 0 ingests until it has applied every
+  packet the acknowledged actors counted as sent; nothing is ever left posted.  The control block is unlinked from /dev/shm as soon as every actor
+  has mapped it.
+
+The same code runs with every rank on ONE GPU (hipIpcOpenMemHandle in another process of
+the same device), which is how the 1-GPU box exercises it.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import mmap
+import os
+import time
+from datetime import timedelta
+
+import numpy as np
+import torch
+
+from .. import ops
+from .experience import META_COLS, STOP
+
+FRAME_BYTES = 84 * 84
+MODE_UNCACHED = 2
+
+# control block layout (int64 words)
+_HDR = 8          # magic, R, param_version, stop, param_begin, (reserved)
+_MAGIC = 0x4150455849504331  # "APEXIPC1"
+
+
+def _align(n: int, a: int = 256) -> int:
+    return -(-n // a) * a
+
+
+def packet_bytes(E: int) -> int:
+    return E * (FRAME_BYTES + META_COLS * 4)
+
+
+class ControlBlock:
+    """int64 words in /dev/shm: header | consumed[R] | heartbeat[R] | drop[R] | sent[R] | ack[R]."""
+
+    FIELDS = ("consumed", "heartbeat", "drop", "sent", "ack")
+
+    def __init__(self, name: str, R: int, create: bool):
+        self.name, self.R = name, int(R)
+        self.path = f"/dev/shm/{name}"
+        self.nbytes = _align(8 * (_HDR + len(self.FIELDS) * self.R), 4096)
+        if create:
+            fd = os.open(self.path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+            os.ftruncate(fd, self.nbytes)
+        else:
+            fd = os.open(self.path, os.O_RDWR)
+        try:
+            self.mm = mmap.mmap(fd, self.nbytes)
+        finally:
+            os.close(fd)
+        self.w = np.frombuffer(self.mm, dtype=np.int64)
+        if create:
+            self.w[:] = 0
+            self.w[1] = self.R
+            self.w[0] = _MAGIC
+        elif self.w[0] != _MAGIC or self.w[1] != self.R:
+            raise RuntimeError(f"{self.path}: not an apex control block for {R} links")
+        self.host_ptr = ctypes.addressof(ctypes.c_char.from_buffer(self.mm))
+        self.dev_ptr = None
+        self._hip = None
+
+    def off(self, field: str) -> int:
+        """Word offset of ``field[0]``."""
+        return _HDR + self.FIELDS.index(field) * self.R
+
+    def view(self, field: str) -> np.ndarray:
+        o = self.off(field)
+        return self.w[o:o + self.R]
+
+    @property
+    def param_version(self) -> int:
+        return int(self.w[2])
+
+    @property
+    def param_begin(self) -> int:
+        return int(self.w[4])
+
+    @property
+    def stop(self) -> bool:
+        return bool(self.w[3])
+
+    def set_stop(self) -> None:
+        self.w[3] = 1
+
+    def register(self, hip) -> int:
+        """Pin + map for kernels of this process; returns the device address of word 0."""
+        self._hip = hip
+        self.dev_ptr = hip.host_register(self.host_ptr, self.nbytes)
+        return self.dev_ptr
+
+    def unlink(self) -> None:
+        try:
+            os.unlink(self.path)
+        except FileNotFoundError:
+            pass
+
+    def close(self) -> None:
+        if self._hip is not None and self.dev_ptr is not None:
+            self._hip.host_unregister(self.host_ptr)
+            self.dev_ptr = None
+
+
+class IpcLearnerLinks:
+    """Rank-0 end: the arena, the control block, the captured ingest and the publisher."""
+
+    def __init__(self, R: int, D: int, E: int, P: int, replay, regions: dict, store, prefix: str, device,
+                 cap: int | None = None, dead_after: float = 30.0, mode: int = MODE_UNCACHED, log=print,
+                 open_timeout: float = 300.0):
+        self.hip = h = ops.hip()
+        self.R, self.D, self.E, self.P = int(R), int(D), int(E), int(P)
+        self.cap = self.D if cap is None else max(1, min(int(cap), self.D))
+        self.device = torch.device(device)
+        self.replay, self.store, self.prefix, self.log = replay, store, prefix, log
+        self.dead_after = float(dead_after)
+        self.pkt = _align(packet_bytes(E))
+        self.seq_off = _align(self.R * self.D * self.pkt)
+        self.par_off = _align(self.seq_off + 8 * self.R * self.D)
+        self.nbytes = self.par_off + 2 * 4 * self.P
+        self.arena = h.ipc_alloc(self.nbytes, mode)
+        self.ctrl = ControlBlock(f"apex_ipc_{prefix.replace('/', '_')}_{os.getpid()}", R, create=True)
+        self.ctrl.register(h)
+        dev = self.device
+        i64 = dict(dtype=torch.int64, device=dev)
+        self.consumed = torch.zeros(R, **i64)
+        self.applied_dev = torch.zeros(R, **i64)
+        self.ready = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.live_dev = torch.ones(R, dtype=torch.int32, device=dev)
+        n_out = R * self.D * E  # the drain ingests up to D packets per link
+        self.slots_out = torch.full((n_out,), -1, dtype=torch.int32, device=dev)
+        self.prio_out = torch.zeros(n_out, dtype=torch.float32, device=dev)
+        self.frame_base = torch.tensor([regions[r].frame_base for r in range(1, R + 1)], **i64)
+        self.slot_base = torch.tensor([regions[r].slot_base for r in range(1, R + 1)], **i64)
+        rp = replay
+        self._n_out = R * self.cap * E
+        mk = lambda cap: h.make_ipc_ingest(dict(  # noqa: E731
+            R=R, D=D, E=E, cap=cap, packet_bytes=self.pkt, ring=self.arena, seq=self.arena + self.seq_off,
+            consumed=self.consumed.data_ptr(), ready=self.ready.data_ptr(), live=self.live_dev.data_ptr(),
+            host_consumed=self.ctrl.dev_ptr + 8 * self.ctrl.off("consumed"), applied=self.applied_dev.data_ptr(),
+            filled=rp.filled.data_ptr(), frames=rp.frames.data_ptr(), s_ids=rp.s_ids.data_ptr(),
+            s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
+            done=rp.done.data_ptr(), frame_base=self.frame_base.data_ptr(), slot_base=self.slot_base.data_ptr(),
+            slots_out=self.slots_out.data_ptr(), prio_out=self.prio_out.data_ptr()))
+        self.ingest_handle = mk(self.cap)
+        self.drain_handle = mk(self.D)
+        self.version = 0
+        self.live = set(range(1, R + 1))
+        self.dropped: dict[int, str] = {}
+        self._hb = {r: (None, time.monotonic()) for r in self.live}
+        self._hb_t = time.monotonic()
+        self.closed = False
+        geo = dict(R=R, D=D, E=E, P=P, pkt=self.pkt, seq_off=self.seq_off, par_off=self.par_off, shm=self.ctrl.name,
+                   device=self.device.index or 0)
+        store.set(f"{prefix}/ipc/handle", h.ipc_handle(self.arena))
+        store.set(f"{prefix}/ipc/geometry", json.dumps(geo))
+        # every actor has mapped the control block -> remove its name (nothing lingers in /dev/shm)
+        self._open_timeout = float(open_timeout)
+        self._unlinked = False
+
+    def _maybe_unlink(self) -> None:
+        if self._unlinked:
+            return
+        keys = [f"{self.prefix}/ipc/opened/{r}" for r in range(1, self.R + 1)]
+        if all(self.store.check([k]) for k in keys):
+            self.ctrl.unlink()
+            self._unlinked = True
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    def ingest(self, drain: bool = False) -> None:
+        """Apply every ready packet (<= cap per link; ``drain``: <= D), release the slots,
+        write the tree.  Device-only, on the current stream: capture it in the learner graph."""
+        self.hip.ipc_ingest(self.drain_handle if drain else self.ingest_handle, self._s())
+        n = self.slots_out.numel() if drain else self._n_out
+        self.replay.write_priorities(self.slots_out[:n], self.prio_out[:n], dedup=False)
+
+    def publish(self, flat: torch.Tensor) -> None:
+        """Conflated versioned publish (seqlock writer, all on the current stream): announce
+        ``v`` as being written, copy into params[v & 1], then release ``v`` as published."""
+        self.version += 1
+        v, s = self.version, self._s()
+        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 4, v, s)
+        self.hip.memcpy_async(self.arena + self.par_off + (v & 1) * 4 * self.P, flat.data_ptr(), 4 * self.P, s)
+        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 2, v, s)
+
+    def drop(self, r: int, why: str) -> None:
+        if r in self.live:
+            self.live.discard(r)
+            self.dropped[r] = why
+            self.live_dev[r - 1] = 0     # stream-ordered: later ingests skip the link
+            self.ctrl.view("drop")[r - 1] = 1
+            if self.log:
+                self.log(f"[central/ipc] dropping actor rank {r}: {why}")
+
+    def check_heartbeats(self, every: float = 1.0) -> None:
+        now = time.monotonic()
+        if now - self._hb_t < every:
+            return
+        self._hb_t = now
+        self._maybe_unlink()
+        hb = self.ctrl.view("heartbeat")
+        for r in sorted(self.live):
+            v = int(hb[r - 1])
+            prev, t = self._hb[r]
+            if v != prev:
+                self._hb[r] = (v, now)
+            elif now - t > self.dead_after:
+                self.drop(r, f"no heartbeat for {self.dead_after:.0f}s")
+
+    def applied(self) -> dict:
+        """Packets applied per link (device counters; one host sync)."""
+        a = self.applied_dev.tolist()
+        return {r: int(a[r - 1]) for r in range(1, self.R + 1)}
+
+    def close(self, timeout: float = 60.0) -> dict:
+        """Stop every actor (flag + acknowledgement, bounded), drain what they pushed before
+        acknowledging (every packet of a live link reaches the replay), release the arena."""
+        if self.closed:
+            return self.stats()
+        self.closed = True
+        torch.cuda.synchronize(self.device)
+        self.ctrl.set_stop()
+        ack, sent = self.ctrl.view("ack"), self.ctrl.view("sent")
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline and not all(ack[r - 1] for r in self.live):
+            self.ingest(drain=True)  # keep consuming: an actor blocked on credit must see its push land
+            torch.cuda.synchronize(self.device)
+            time.sleep(0.001)
+        for r in sorted(self.live):
+            if not ack[r - 1]:
+                self.drop(r, "stop not acknowledged")
+        while time.monotonic() < deadline:
+            done = self.applied()
+            if all(done[r] >= int(sent[r - 1]) for r in self.live):
+                break
+            self.ingest(drain=True)
+            torch.cuda.synchronize(self.device)
+        st = self.stats()
+        self.ctrl.unlink()
+        self.ctrl.close()
+        self.hip.ipc_free(self.arena)
+        self.arena = 0
+        return st
+
+    def stats(self) -> dict:
+        sent = self.ctrl.view("sent")
+        return {"applied": self.applied(), "sent": {r: int(sent[r - 1]) for r in range(1, self.R + 1)},
+                "dropped": dict(self.dropped), "live": sorted(self.live), "params_version": self.version,
+                "transport": "hip-ipc"}
+
+
+class IpcActorLink:
+    """Actor end: peer copies into rank 0's ring with the credit window, pulls of the
+    newest parameter version, heartbeat, drop and stop."""
+
+    def __init__(self, rank: int, store, prefix: str, flat: torch.Tensor, packet: torch.Tensor, device,
+                 heartbeat_every: float = 0.5, timeout: float = 300.0):
+        self.hip = h = ops.hip()
+        self.rank, self.store, self.prefix = rank, store, prefix
+        self.device = torch.device(device)
+        self.flat, self.packet = flat, packet
+        store.wait([f"{prefix}/ipc/handle", f"{prefix}/ipc/geometry"], timedelta(seconds=timeout))
+        geo = json.loads(store.get(f"{prefix}/ipc/geometry"))
+        self.R, self.D, self.E, self.P = geo["R"], geo["D"], geo["E"], geo["P"]
+        self.pkt, self.seq_off, self.par_off = geo["pkt"], geo["seq_off"], geo["par_off"]
+        if packet.numel() != packet_bytes(self.E) or packet.dtype != torch.uint8:
+            raise ValueError("packet buffer must be u8 [E * (7056 + 56)]")
+        if flat.numel() != self.P:
+            raise ValueError(f"parameter count {flat.numel()} != the learner's {self.P}")
+        self.remote = h.ipc_open(store.get(f"{prefix}/ipc/handle"), self.device.index or 0)
+        self.ctrl = ControlBlock(geo["shm"], self.R, create=False)
+        store.set(f"{prefix}/ipc/opened/{rank}", "1")
+        self.i = rank - 1
+        self.consumed = self.ctrl.view("consumed")
+        self.hb = self.ctrl.view("heartbeat")
+        self.period = float(heartbeat_every)
+        self._hb_t = 0.0
+        self.sent = 0
+        self.version = 0
+        self.stopped = False
+        self.dropped = False
+        self._ev = torch.cuda.Event()
+        self.beat(force=True)
+
+    @staticmethod
+    def _s() -> int:
+        return torch.cuda.current_stream().cuda_stream
+
+    @property
+    def n_sent(self) -> int:
+        return self.sent
+
+    def beat(self, force: bool = False) -> None:
+        now = time.monotonic()
+        if force or now - self._hb_t >= self.period:
+            self._hb_t = now
+            self.hb[self.i] += 1
+
+    def check_stop(self) -> bool:
+        """True once rank 0 has stopped or dropped this link (acknowledges a stop)."""
+        if self.stopped:
+            return True
+        if self.ctrl.view("drop")[self.i]:
+            self.dropped = True
+            self.finish()
+        elif self.ctrl.stop:
+            self.finish()
+        return self.stopped
+
+    def push(self, timeout: float = 120.0) -> bool:
+        """Copy the packet into the next ring slot and publish its sequence number (both on
+        the current stream, behind the actor step that filled it).  Waits (bounded) while
+        ``D`` packets are unconsumed; False if the link was stopped or dropped meanwhile."""
+        n = self.sent
+        deadline = time.monotonic() + timeout
+        while n - int(self.consumed[self.i]) >= self.D:
+            self.beat()
+            if self.check_stop():
+                return False
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"actor rank {self.rank}: no credit for {timeout}s")
+            time.sleep(0.0001)
+        k, s = n % self.D, self._s()
+        slot = self.remote + (self.i * self.D + k) * self.pkt
+        self.hip.memcpy_async(slot, self.packet.data_ptr(), self.packet.numel(), s)
+        self.hip.ipc_flag(self.remote + self.seq_off + 8 * (self.i * self.D + k), n + 1, s)
+        self.sent = n + 1
+        self.ctrl.view("sent")[self.i] = self.sent
+        self.beat()
+        return True
+
+    def poll_params(self, retries: int = 8):
+        """None (nothing new), STOP, or the version just installed into ``flat``."""
+        if self.check_stop():
+            return STOP
+        v = self.ctrl.param_version
+        if v <= self.version:
+            return None
+        for _ in range(retries):
+            s = self._s()
+            self.hip.memcpy_async(self.flat.data_ptr(), self.remote + self.par_off + (v & 1) * 4 * self.P,
+                                  4 * self.P, s)
+            self._ev.record(torch.cuda.current_stream(self.device))
+            self._ev.synchronize()
+            if self.ctrl.param_begin < v + 2:  # rank 0 had not started rewriting half (v & 1): clean
+                self.version = v
+                return v
+            v = self.ctrl.param_version
+        return None
+
+    def finish(self) -> None:
+        if self.stopped:
+            return
+        torch.cuda.synchronize(self.device)  # our last peer copies have landed
+        self.stopped = True
+        self.ctrl.view("ack")[self.i] = 1
+        self.hip.ipc_close(self.remote)
+        self.remote = 0

@@ -5,10 +5,12 @@ the real engines' multi-rank code paths end to end:
 * sharded data-parallel ApexEngine, 2 ranks: replicas stay bit-identical after every
   step, and the in-kernel global-PER IS weights equal parallel/sharded.py's formula
   (global min priority, shard scale world * M_r / sum M) on the live trees;
-* central ApexEngine (async links), 2 ranks: after the stop handshake every transition
-  row and frame the actor produced is in rank 0's region of the replay;
-* central, 3 ranks, actor rank 2 hard-killed mid-run (APEX_FAULT): rank 0 drops it and
-  keeps stepping on rank 1's experience.
+* central ApexEngine, 2 ranks, over both transports -- HIP IPC (rings in rank 0's HBM,
+  ingest inside the learner graph; parallel/ipc.py) and the torch.distributed P2P links
+  (parallel/experience.py): after the stop every transition row and frame the actor
+  produced is in rank 0's region of the replay;
+* central over HIP IPC, 3 ranks, actor rank 2 hard-killed mid-run (APEX_FAULT): rank 0
+  drops it and keeps stepping on rank 1's experience.
 Children are started with the spawn method (fresh interpreters: no GPU state inherited).
 """
 import os
@@ -164,7 +166,7 @@ def _progress(msg):
             f.write(msg + "\n")
 
 
-def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
+def _central_body(rank, world, steps, dead_after, min_seconds=0.0, transport="ipc"):
     import time
 
     import torch.distributed as dist
@@ -172,9 +174,9 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
     from apex_amd.engine.central import CentralApexEngine
 
     dev = torch.device("cuda", 0)
-    eng = CentralApexEngine(_central_cfg(), dev, rank, world, dead_after=dead_after, heartbeat_every=0.05)
+    eng = CentralApexEngine(_central_cfg(), dev, rank, world, dead_after=dead_after, heartbeat_every=0.05,
+                            transport=transport)
     _progress("engine built")
-    g = eng.groups
     if rank != 0:
         eng.capture()
         _progress("captured")
@@ -185,12 +187,12 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
                 _progress(f"actor steps {n}")
         _progress(f"stopped after {n} steps")
         torch.cuda.synchronize(dev)
-        rp = eng.replay  # the local mirror of this rank's region -> rank 0 (over this link's group)
+        rp = eng.replay  # the local mirror of this rank's region -> rank 0 (world group, for the check)
         live = (eng.actor.step_counter.item(), rp.s_ids.cpu(), rp.s2_ids.cpu(), rp.action.cpu(), rp.reward.cpu(),
                 rp.done.cpu(), rp.frames.cpu())
         for t in live[1:]:
-            dist.send(t, 0, group=g[rank])
-        return {"actor_steps": eng.actor_steps, "sent": eng.link.sender.n_sent, "version": eng.param_version}
+            dist.send(t, 0)
+        return {"actor_steps": eng.actor_steps, "sent": eng.link.n_sent, "version": eng.param_version}
     eng.fill()
     _progress("filled")
     eng.capture()
@@ -221,7 +223,7 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
                 torch.empty_like(rp.action[:C].cpu()), torch.empty_like(rp.reward[:C].cpu()),
                 torch.empty_like(rp.done[:C].cpu()), torch.empty_like(rp.frames[:F].cpu())]
         for t in mine:
-            dist.recv(t, r, group=g[r])
+            dist.recv(t, r)
         s0, f0 = reg.slot_base, reg.frame_base
         bad = 0
         bad += int(not torch.equal(rp.s_ids[s0:s0 + C].cpu(), mine[0] + f0))
@@ -235,8 +237,9 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0):
     return res
 
 
-def test_central_two_ranks_every_row_reaches_the_replay(cuda):
-    out, codes = _run(_central_body, 2, (40, 30.0))
+@pytest.mark.parametrize("transport", ["ipc", "p2p"])
+def test_central_two_ranks_every_row_reaches_the_replay(cuda, transport):
+    out, codes = _run(_central_body, 2, (40, 30.0, 0.0, transport))
     assert codes == [0, 0]
     o = out[0]
     assert o["learn_steps"] >= 40 and o["links"]["dropped"] == {}
