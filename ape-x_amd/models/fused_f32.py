@@ -41,12 +41,18 @@ F32_SPLITS = 7  # FC1 forward split-K slabs (f32_kernels.hip kFcSplits)
 class F32Workspace:
     """fp32 activation buffers for one forward pass of batch ``B`` (+ backward buffers)."""
 
-    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False):
+    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False, px: bool | None = None):
         self.B, self.A = B, A
         f32 = dict(dtype=torch.float32, device=device)
         self.a1 = torch.empty(B, 400, 32, **f32)
         self.a2 = torch.empty(B, 81, 64, **f32)
         self.a3 = torch.empty(B, FEAT, **f32)
+        # pre-split exact forward (px_kernels.hip): each activation also as 3 bf16 planes
+        self.px = ops.hip().px_enabled() if px is None else bool(px)
+        bf = dict(dtype=torch.bfloat16, device=device)
+        self.a1x = torch.empty(3, B * 400 * 32, **bf) if self.px else None
+        self.a2x = torch.empty(3, B * 81 * 64, **bf) if self.px else None
+        self.a3x = torch.empty(3, B * FEAT, **bf) if self.px else None
         self.z = torch.empty(F32_SPLITS, B, 256, **f32)
         self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
         self.q = torch.empty(B, A, **f32)
@@ -88,6 +94,9 @@ class F32DuelingNet:
             self.arena_offsets[name] = off
             off += n
         self.fwd_numel = self.arena_offsets["w2t"]
+        # the forward layouts as 3 bf16 planes (hi | mid | lo, plane stride fwd_numel): the
+        # pre-split exact forward's B operands (px_kernels.hip), kept by repack / the optimizer
+        self.arena_x = torch.empty(3 * self.fwd_numel, dtype=torch.bfloat16, device=self.device)
         self.repack()
 
     def repack(self) -> None:
@@ -100,11 +109,22 @@ class F32DuelingNet:
             self.wfc1p[128:].copy_(m.value[0].weight.view(128, C3, P3).permute(0, 2, 1))
             self.w2t.copy_(f[2].weight.permute(2, 3, 1, 0))
             self.w3t.copy_(f[4].weight.permute(2, 3, 1, 0))
+        self.split_weights()
+
+    def split_weights(self) -> None:
+        """arena_x = the exact 3-term bf16 split of the forward layouts (one kernel)."""
+        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.fwd_numel, self.fwd_numel,
+                                  self._s())
+
+    def wx(self, name: str) -> int:
+        """Address of packed layout ``name``'s hi plane in arena_x."""
+        return self.arena_x.data_ptr() + 2 * self.arena_offsets[name]
 
     def copy_packed_from(self, other: "F32DuelingNet", forward_only: bool = True) -> None:
         """Device copy of another net's packed weights (same architecture)."""
         n = self.fwd_numel if forward_only else self.arena.numel()
         self.arena[:n].copy_(other.arena[:n])
+        self.arena_x.copy_(other.arena_x)
 
     def pack_maps(self) -> tuple[torch.Tensor, torch.Tensor]:
         """int32 (dst1, dst2) over the flat parameter order: arena positions of the packed
@@ -135,8 +155,12 @@ class F32DuelingNet:
 
     def opt_pack_args(self) -> dict:
         d1, d2 = self.pack_maps()
-        return {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
-                **self.fc_pack_args()}
+        out = {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
+               **self.fc_pack_args()}
+        if self.hip.px_enabled():  # the optimizer also rewrites the forward layouts' split planes
+            out.update(arena_x=self.arena_x.data_ptr(), x_plane=self.fwd_numel, fc_wp_x=self.wx("wfc1p"),
+                       fc_wp_x_plane=self.fwd_numel)
+        return out
 
     @staticmethod
     def _s() -> int:
@@ -279,6 +303,7 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
     B, A = passes[0][2].B, net0.A
     h, s = net0.hip, net0._s()
     c1, c2, c3, fc, hd = [], [], [], [], []
+    px = h.px_enabled() and all(p[2].px for p in passes)
     for net, x, ws, ids, idx in passes:
         assert ws.B == B and net.A == A, "one launch per layer needs a common batch and action count"
         m, f = net.model, net.model.features
@@ -287,6 +312,12 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
         c2.append((ws.a1.data_ptr(), 0, 0, net.w2p.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
         c3.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
         fc.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
+        if px:  # planes: conv1 writes a1x; conv2 / conv3 / FC1 read (activation, weight) planes
+            P, ps1, ps2, ps3 = net.fwd_numel, ws.a1x.shape[1], ws.a2x.shape[1], ws.a3x.shape[1]
+            c1[-1] += (0, 0, ws.a1x.data_ptr(), 0, 0, ps1)
+            c2[-1] += (ws.a1x.data_ptr(), net.wx("w2p"), ws.a2x.data_ptr(), ps1, P, ps2)
+            c3[-1] += (ws.a2x.data_ptr(), net.wx("w3p"), ws.a3x.data_ptr(), ps2, P, ps3)
+            fc[-1] += (ws.a3x.data_ptr(), net.wx("wfc1p"), 0, ps3, P, 0)
         hd.append(net._heads_tuple(ws))
     h.f32_conv_fwd_multi(1, c1, B, s)
     h.f32_conv_fwd_multi(2, c2, B, s)

@@ -963,7 +963,12 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
         al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.lo[kb], al, 0, 0, 0);
       }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) out[(size_t)(tile * 16 + 4 * q + e) * 32] = fmaxf(ah[e] + al[e] + bias, 0.f);
+      for (int e = 0; e < 4; ++e) {
+        const float y = fmaxf(ah[e] + al[e] + bias, 0.f);
+        const size_t o = (size_t)(tile * 16 + 4 * q + e) * 32;
+        out[o] = y;
+        if (p.outx) store_planes(p.outx, p.outx_ps, (size_t)b * 400 * 32 + nh * 16 + i + o, y);  // px forward
+      }
     }
   }
 }
@@ -1649,6 +1654,14 @@ void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, i
   LAUNCH_CHECK();
 }
 
+// every problem of the launch carries input + weight planes and px is enabled
+bool px_ready(const F32Set& set) {
+  if (!px_enabled()) return false;
+  for (int i = 0; i < set.n; ++i)
+    if (!set.p[i].inx || !set.p[i].wx) return false;
+  return true;
+}
+
 void check_set(const F32Set& set) {
   if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("f32: 1..3 problems");
   if (set.B <= 0) throw std::invalid_argument("f32: B must be positive");
@@ -1691,6 +1704,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
   else if (layer == 18 && v >= 0 && v <= 1) g_wgrad_xcd = v;
+  else if (layer == 19 && v >= 0 && v <= 1) px_set(v);  // pre-split exact forward GEMMs (px_kernels.hip)
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1701,6 +1715,9 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
   switch (layer) {
     case 1:
+      if (g_conv1_variant != 2)
+        for (int i = 0; i < set.n; ++i)
+          if (set.p[i].outx) throw std::invalid_argument("conv1: activation planes need the exact-split kernel (variant 2)");
       if (g_conv1_variant == 1) {
         fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
       } else if (g_conv1_variant == 2) {
@@ -1712,12 +1729,14 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
       }
       break;
     case 2:
-      if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
+      if (px_ready(set)) px_conv_fwd_multi(2, set, s);
+      else if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
       else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
-      if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
+      if (px_ready(set)) px_conv_fwd_multi(3, set, s);
+      else if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
       else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
@@ -1729,7 +1748,8 @@ int f32_fc1_splits() { return kFcSplits; }
 
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
-  if (g_fc1_tile == 1 || (g_fc1_tile == 3 && set.n == 3)) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
+  if (px_ready(set)) px_fc1_fwd_multi(set, s);
+  else if (g_fc1_tile == 1 || (g_fc1_tile == 3 && set.n == 3)) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
   else if (g_fc1_tile == 2) fwd_launch<Fc1FwdT<128, 32, 32, 4>>(set, s);
   else fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
   return kFcSplits;

@@ -239,16 +239,20 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
                            int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                            uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                           uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
+                           uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32,
+                           uint64_t arena_x, int64_t x_plane, uint64_t fc_wp_x, int64_t fc_wp_x_plane) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32),
+                     P<uint16_t>(arena_x), x_plane};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32),
+                    P<uint16_t>(fc_wp_x), fc_wp_x_plane};
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
                  n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
                  (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("gavg"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0,
+     py::arg("arena_x") = 0, py::arg("x_plane") = 0, py::arg("fc_wp_x") = 0, py::arg("fc_wp_x_plane") = 0);
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
                        int lr_step_size, int lr_step_offset) {
@@ -261,16 +265,20 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
                         int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                         uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                        uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
+                        uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32,
+                           uint64_t arena_x, int64_t x_plane, uint64_t fc_wp_x, int64_t fc_wp_x_plane) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32),
+                     P<uint16_t>(arena_x), x_plane};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32),
+                    P<uint16_t>(fc_wp_x), fc_wp_x_plane};
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
               hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
               (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("mm"), py::arg("v"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0,
+     py::arg("arena_x") = 0, py::arg("x_plane") = 0, py::arg("fc_wp_x") = 0, py::arg("fc_wp_x_plane") = 0);
   m.def("adam_step2", [](std::array<uint64_t, 8> a, std::array<uint64_t, 8> b, const AdamParams& hp, uint64_t step,
                          uint64_t s) {
     // (p, g, m, v, n, partials, n_partials, norms) per set
@@ -436,25 +444,39 @@ PYBIND11_MODULE(_apex_hip, m) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));
   });
   // ---- fp32 (reference-precision) network kernels (f32_kernels.hip)
-  auto f32set = [](const std::vector<std::array<uint64_t, 7>>& probs, int B) {
+  // a problem: (in, ids, idx, w, w2, bias, out) [+ (inx, wx, outx, inx_ps, wx_ps, outx_ps): pre-split planes]
+  auto f32set = [](const std::vector<std::vector<uint64_t>>& probs, int B) {
     if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
     F32Set set{};
     for (size_t i = 0; i < probs.size(); ++i) {
       const auto& t = probs[i];
+      if (t.size() != 7 && t.size() != 13) throw std::invalid_argument("f32 problem: 7 or 13 fields");
       set.p[i] = F32Prob{P<const void>(t[0]), P<const int>(t[1]), P<const int>(t[2]), P<const float>(t[3]),
                          P<const float>(t[4]), P<const float>(t[5]), P<float>(t[6])};
+      if (t.size() == 13) {
+        set.p[i].inx = P<const uint16_t>(t[7]);
+        set.p[i].wx = P<const uint16_t>(t[8]);
+        set.p[i].outx = P<uint16_t>(t[9]);
+        set.p[i].inx_ps = (int64_t)t[10];
+        set.p[i].wx_ps = (int64_t)t[11];
+        set.p[i].outx_ps = (int64_t)t[12];
+      }
     }
     set.n = (int)probs.size();
     set.B = B;
     return set;
   };
   // probs: (in, ids, idx, w, w2, bias, out)
-  m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::array<uint64_t, 7>>& probs, int B,
+  m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::vector<uint64_t>>& probs, int B,
                                        uint64_t s) { f32_conv_fwd_multi(layer, f32set(probs, B), S(s)); });
-  m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::array<uint64_t, 7>>& probs, int B, uint64_t s) {
+  m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::vector<uint64_t>>& probs, int B, uint64_t s) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
   m.def("f32_fc1_splits", &f32_fc1_splits);
+  m.def("px_enabled", &px_enabled);
+  m.def("f32_split_planes", [](uint64_t src, uint64_t dst, int64_t n, int64_t plane, uint64_t s) {
+    f32_split_planes(P<const float>(src), P<uint16_t>(dst), n, plane, S(s));
+  });
   m.def("f32_set_variant", &f32_set_variant);
   m.def("f32_fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ga, uint64_t gv, int B,
                           uint64_t s) {

@@ -220,6 +220,8 @@ struct PackMap {
   const int* dst2;
   uint16_t* arena;      // bf16 packed copies (bf16 network) ...
   float* arena_f32;     // ... or fp32 packed copies (reference-precision network)
+  uint16_t* arena_x;    // fp32 network: split planes of the forward layouts (dst1 < x_plane), or null
+  int64_t x_plane;
 };
 // FC1 weights (Nature-CNN dueling net): flat offsets of advantage.0.weight and
 // value.0.weight ([128][64*49] each) and the two packed bf16 layouts they refresh,
@@ -232,6 +234,8 @@ struct FcPack {
   uint16_t* wp;
   uint16_t* wt;
   float* wp_f32;
+  uint16_t* wp_x;       // fp32 network: split planes of wfc1p (plane stride wp_x_plane), or null
+  int64_t wp_x_plane;
 };
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
@@ -367,6 +371,12 @@ struct F32Prob {
   const float* w2;    // unused
   const float* bias;
   float* out;         // activations (conv) | split-K partials [7][B][256] (FC1)
+  // pre-split exact operands (px_kernels.hip): three bf16 planes hi | mid | lo of the same
+  // tensor, ``*_ps`` elements apart, hi + mid + lo = the fp32 value (RNE split)
+  const uint16_t* inx;  // input activation planes (conv2 / conv3 / FC1); null: fp32 path
+  const uint16_t* wx;   // packed weight planes (w2p / w3p / wfc1p layouts)
+  uint16_t* outx;       // output activation planes written beside ``out`` (null: none)
+  int64_t inx_ps, wx_ps, outx_ps;
 };
 struct F32Set {
   F32Prob p[kMaxProbs];
@@ -376,6 +386,16 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
 void f32_set_variant(int layer, int v);  // conv1 forward tile variant (benchmarks), 0 = default
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
+// pre-split exact forward GEMMs on bf16 MFMA (px_kernels.hip): every operand arrives as three
+// bf16 planes (written by the producer's epilogue / the optimizer), 6 term products per
+// element pair accumulated in fp32 (f32_set_variant(19, 1) enables them for conv2 / conv3 / FC1
+// whenever every problem of the launch carries planes)
+bool px_enabled();
+void px_set(int v);
+void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
+void px_fc1_fwd_multi(const F32Set& set, hipStream_t s);
+// dst[u * plane + i] = term u of src[i] (u = 0 hi, 1 mid, 2 lo), i < n
+void f32_split_planes(const float* src, uint16_t* dst, int64_t n, int64_t plane, hipStream_t s);
 // FC1 backward in one launch: dy3 = (a3 > 0) * dz . wfc1p (channels-last order) and the
 // reference-layout weight gradients written straight into g_adv / g_val
 void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,

@@ -116,6 +116,11 @@ def parse():
     ap.add_argument("--watchdog", type=float, default=1500.0,
                     help="seconds after which a rank dumps every thread's stack and exits 1 (0 = off): "
                          "a hung collective ends the run with a traceback instead of a silent stall")
+    ap.add_argument("--px", type=int, default=0, choices=[0, 1],
+                    help="fp32 forward GEMMs (conv2/conv3/FC1) on the pre-split exact bf16x6 kernels "
+                         "(px_kernels.hip: fp32-class, every operand as 3 exact bf16 terms)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
+                    help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
     ap.add_argument("--unpaced", action="store_true",
                     help="central topology: actors run free (default: paced at --actor-steps packets per learner "
                          "step per actor through the credit window)")
@@ -162,6 +167,10 @@ def main():
 
         trace.enable(True)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.px:
+        from apex_amd import ops
+
+        ops.hip().f32_set_variant(19, 1)  # before any network / workspace is built
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     if args.same_device:
@@ -293,6 +302,8 @@ def main():
                 "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
                 "forward": args.forward,
+                "fp32_forward_gemms": ("pre-split exact bf16x6 (3-term operands, fp32-class)" if args.px
+                                       else "fp32 MFMA") if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
                 "actor_learner_overlap": args.overlap,
                 "actor_stream": args.streams,
@@ -409,7 +420,7 @@ def central(args, rank, world, device):
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
-    eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced)
+    eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport)
     if rank != 0:  # actor GPU: act and push until the learner stops this link
         if not args.no_graphs:
             eng.capture()
@@ -446,7 +457,8 @@ def central(args, rank, world, device):
         "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
         "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
                    "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",
-                   "topology": "central replay on rank 0, async experience links over " + args.backend,
+                   "topology": "central replay on rank 0, async experience links over "
+                               + ("HIP IPC (xGMI peer copies)" if eng.transport == "ipc" else args.backend),
                    "actor_pacing": "free" if args.unpaced else f"{args.actor_steps} packet/learner step/actor",
                    "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": args.envs},
         "actor_frames_per_sec": round(packets * eng.frames_per_actor_step / dt, 1),
