@@ -244,7 +244,9 @@ class DQNLearner:
                  "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(),
                  ("dz" if self.fp32 else "dz_bf"): (self.ws_s.dz if self.fp32 else self.ws_s.dz_bf).data_ptr(),
                  "part": self.lh_part.data_ptr(), "step": self.step_counter.data_ptr(),
-                 "step_snap": self.step_snap.data_ptr()}, self.B, self.A, self.gamma_n, s)
+                 "step_snap": self.step_snap.data_ptr(),
+                 **({"dzx": self.ws_s.dzx.data_ptr(), "dzx_ps": self.ws_s.dzx.shape[1]}
+                    if getattr(self.ws_s, "dzx", None) is not None else {})}, self.B, self.A, self.gamma_n, s)
             heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
             if self.dp_split:
                 self.net.fc_backward(self.ws_s, extra_jobs=[heads_job])

@@ -56,6 +56,9 @@ class F32Workspace:
         self.z = torch.empty(F32_SPLITS, B, 256, **f32)
         self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
         self.q = torch.empty(B, A, **f32)
+        # pre-split exact backward (pxb_kernels.hip): the output gradients' planes as well
+        self.pxb = bool(keep_for_backward and self.px and ops.hip().pxb_enabled())
+        self.dzx = self.dy3x = self.dy2x = None
         if keep_for_backward:
             self.dA = torch.empty(B, A + 1, **f32)
             self.dz = torch.empty(B, 256, **f32)
@@ -63,6 +66,10 @@ class F32Workspace:
             self.dy3 = torch.empty(B, FEAT, **f32)
             self.dy2 = torch.empty(B, 81, 64, **f32)
             self.dy1 = torch.empty(B, 400, 32, **f32)
+            if self.pxb:
+                self.dzx = torch.empty(3, B * 256, **bf)
+                self.dy3x = torch.empty(3, B * FEAT, **bf)
+                self.dy2x = torch.empty(3, B * 81 * 64, **bf)
 
 
 class F32DuelingNet:
@@ -94,9 +101,11 @@ class F32DuelingNet:
             self.arena_offsets[name] = off
             off += n
         self.fwd_numel = self.arena_offsets["w2t"]
-        # the forward layouts as 3 bf16 planes (hi | mid | lo, plane stride fwd_numel): the
-        # pre-split exact forward's B operands (px_kernels.hip), kept by repack / the optimizer
-        self.arena_x = torch.empty(3 * self.fwd_numel, dtype=torch.bfloat16, device=self.device)
+        # every packed layout as 3 bf16 planes (hi | mid | lo, plane stride x_plane = the arena
+        # size): the pre-split exact GEMMs' weight operands (px_kernels.hip forward layouts,
+        # pxb_kernels.hip transposes + wfc1p), kept by repack / the optimizer's pack pass
+        self.x_plane = self.arena.numel()
+        self.arena_x = torch.empty(3 * self.x_plane, dtype=torch.bfloat16, device=self.device)
         self.repack()
 
     def repack(self) -> None:
@@ -112,8 +121,8 @@ class F32DuelingNet:
         self.split_weights()
 
     def split_weights(self) -> None:
-        """arena_x = the exact 3-term bf16 split of the forward layouts (one kernel)."""
-        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.fwd_numel, self.fwd_numel,
+        """arena_x = the exact 3-term bf16 split of the packed layouts (one kernel)."""
+        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.x_plane, self.x_plane,
                                   self._s())
 
     def wx(self, name: str) -> int:
@@ -124,7 +133,8 @@ class F32DuelingNet:
         """Device copy of another net's packed weights (same architecture)."""
         n = self.fwd_numel if forward_only else self.arena.numel()
         self.arena[:n].copy_(other.arena[:n])
-        self.arena_x.copy_(other.arena_x)
+        ax, ox = self.arena_x.view(3, -1), other.arena_x.view(3, -1)
+        ax[:, :n].copy_(ox[:, :n])
 
     def pack_maps(self) -> tuple[torch.Tensor, torch.Tensor]:
         """int32 (dst1, dst2) over the flat parameter order: arena positions of the packed
@@ -158,8 +168,8 @@ class F32DuelingNet:
         out = {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
                **self.fc_pack_args()}
         if self.hip.px_enabled():  # the optimizer also rewrites the forward layouts' split planes
-            out.update(arena_x=self.arena_x.data_ptr(), x_plane=self.fwd_numel, fc_wp_x=self.wx("wfc1p"),
-                       fc_wp_x_plane=self.fwd_numel)
+            out.update(arena_x=self.arena_x.data_ptr(), x_plane=self.x_plane, fc_wp_x=self.wx("wfc1p"),
+                       fc_wp_x_plane=self.x_plane)
         return out
 
     @staticmethod
@@ -218,6 +228,8 @@ class F32DuelingNet:
                       m.advantage[2].weight.grad.data_ptr(), m.advantage[2].bias.grad.data_ptr(),
                       m.value[2].weight.grad.data_ptr(), m.value[2].bias.grad.data_ptr(),
                       m.advantage[0].bias.grad.data_ptr(), m.value[0].bias.grad.data_ptr(), s)
+        if ws.pxb:  # (the learner's fused dqn_heads_bwd writes the planes itself)
+            h.f32_split_planes(ws.dz.data_ptr(), ws.dzx.data_ptr(), B * 256, ws.dzx.shape[1], s)
         self.trunk_backward(x, ws, ids, idx)
 
     def heads_finalize_job(self, part: torch.Tensor, G: int):
@@ -234,6 +246,18 @@ class F32DuelingNet:
         the data-parallel split, where the FC1 all-reduce waits on this launch)."""
         m = self.model
         ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+        if ws.pxb:  # pre-split exact FC1 backward (pxb_kernels.hip): same outputs, same finalize jobs
+            sliced = bool(self._fc1_G and not in_place)
+            d = {"dzx": ws.dzx.data_ptr(), "dz_ps": ws.dzx.shape[1], "a3x": ws.a3x.data_ptr(), "a3_ps": ws.a3x.shape[1],
+                 "wx": self.wx("wfc1p"), "w_ps": self.x_plane, "a3": ws.a3.data_ptr(), "dy3": ws.dy3.data_ptr(),
+                 "dy3x": ws.dy3x.data_ptr(), "dy3_ps": ws.dy3x.shape[1],
+                 "gw": self._fc1_ws.data_ptr() if sliced else ga.data_ptr(), "gw2": 0 if sliced else gv.data_ptr(),
+                 "slices": self._fc1_G if sliced else 0}
+            self.hip.pxb_fc1_bwd(d, ws.B, self._s())
+            if not sliced:
+                return []
+            return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
+                    self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
         if self._fc1_G and not in_place:
             self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
                                        self._fc1_ws.data_ptr(), ws.B, self._s())
@@ -250,12 +274,23 @@ class F32DuelingNet:
         h, s, f = self.hip, self._s(), self.model.features
         xp, ip, jp = self._src(x, ids, idx, B)
         w1, w2, w3 = self._wgrad_wss
-        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
-                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
-        if after_first is not None:
-            after_first()
-        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
-                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
+        if ws.pxb:  # pre-split exact conv3 / conv2 backward (pxb_kernels.hip)
+            h.pxb_conv_bwd(3, {"dyx": ws.dy3x.data_ptr(), "dy_ps": ws.dy3x.shape[1], "xx": ws.a2x.data_ptr(),
+                               "x_ps": ws.a2x.shape[1], "wtx": self.wx("w3t"), "wt_ps": self.x_plane,
+                               "mask": ws.a2.data_ptr(), "dx": ws.dy2.data_ptr(), "dxx": ws.dy2x.data_ptr(),
+                               "dx_ps": ws.dy2x.shape[1], "ws": w3.data_ptr()}, B, s)
+            if after_first is not None:
+                after_first()
+            h.pxb_conv_bwd(2, {"dyx": ws.dy2x.data_ptr(), "dy_ps": ws.dy2x.shape[1], "xx": ws.a1x.data_ptr(),
+                               "x_ps": ws.a1x.shape[1], "wtx": self.wx("w2t"), "wt_ps": self.x_plane,
+                               "mask": ws.a1.data_ptr(), "dx": ws.dy1.data_ptr(), "ws": w2.data_ptr()}, B, s)
+        else:
+            h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
+                           ws.dy2.data_ptr(), w3.data_ptr(), B, s)
+            if after_first is not None:
+                after_first()
+            h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
+                           ws.dy1.data_ptr(), w2.data_ptr(), B, s)
         h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
         return [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
                                         f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
@@ -313,7 +348,7 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
         c3.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
         fc.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
         if px:  # planes: conv1 writes a1x; conv2 / conv3 / FC1 read (activation, weight) planes
-            P, ps1, ps2, ps3 = net.fwd_numel, ws.a1x.shape[1], ws.a2x.shape[1], ws.a3x.shape[1]
+            P, ps1, ps2, ps3 = net.x_plane, ws.a1x.shape[1], ws.a2x.shape[1], ws.a3x.shape[1]
             c1[-1] += (0, 0, ws.a1x.data_ptr(), 0, 0, ps1)
             c2[-1] += (ws.a1x.data_ptr(), net.wx("w2p"), ws.a2x.data_ptr(), ps1, P, ps2)
             c3[-1] += (ws.a2x.data_ptr(), net.wx("w3p"), ws.a3x.data_ptr(), ps2, P, ps3)

@@ -50,6 +50,7 @@ HIP_SOURCES = [
     "f32_kernels.hip",
     "ipc_kernels.hip",
     "px_kernels.hip",
+    "pxb_kernels.hip",
     "comm.cpp",
     "ipc.cpp",
 ]

@@ -1704,7 +1704,8 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
   else if (layer == 18 && v >= 0 && v <= 1) g_wgrad_xcd = v;
-  else if (layer == 19 && v >= 0 && v <= 1) px_set(v);  // pre-split exact forward GEMMs (px_kernels.hip)
+  else if (layer == 19 && v >= 0 && v <= 2) px_set(v);  // pre-split exact forward GEMMs (px_kernels.hip)
+  else if (layer == 20 && v >= 0 && v <= 1) pxb_set(v);  // pre-split exact backward GEMMs (pxb_kernels.hip)
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1807,6 +1808,8 @@ int f32_fc1_wgrad_slices(int B) {
 }
 
 int f32_wgrad_splits(int layer, int B) { return wgrad_plan(layer, B).splits; }
+
+int f32_wgrad_kbps(int layer, int B) { return wgrad_plan(layer, B).kbps; }
 
 size_t f32_wgrad_workspace_floats(int layer, int B) {
   const SplitPlan p = wgrad_plan(layer, B);

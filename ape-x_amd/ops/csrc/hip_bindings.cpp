@@ -427,6 +427,9 @@ PYBIND11_MODULE(_apex_hip, m) {
     a.lw = P<float>(g("lw"));
     a.dz_bf = P<uint16_t>(g("dz_bf"));
     a.dz = P<float>(g("dz"));
+    a.dzx = P<uint16_t>(g("dzx"));
+    a.dzx_ps = d.contains("dzx_ps") ? d["dzx_ps"].cast<int64_t>() : 0;
+    if (a.dzx && (!a.dz || a.dzx_ps < (int64_t)B * 256)) throw std::invalid_argument("dqn_heads_bwd: dz planes need dz and dzx_ps >= B*256");
     a.part = P<float>(g("part"));
     a.step = P<const int64_t>(g("step"));
     a.step_snap = P<int64_t>(g("step_snap"));
@@ -474,6 +477,50 @@ PYBIND11_MODULE(_apex_hip, m) {
   });
   m.def("f32_fc1_splits", &f32_fc1_splits);
   m.def("px_enabled", &px_enabled);
+  m.def("pxb_enabled", &pxb_enabled);
+  m.def("px_terms", &px_terms);
+  // pre-split backward: FC1 (dz planes, a3 planes, wfc1p planes) and conv3 / conv2 launches
+  m.def("pxb_fc1_bwd", [](py::dict d, int B, uint64_t s) {
+    auto g = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
+    auto i = [&](const char* k) -> int64_t { return d.contains(k) ? d[k].cast<int64_t>() : 0; };
+    PxbFc1 f{};
+    f.dzx = P<const uint16_t>(g("dzx"));
+    f.dz_ps = i("dz_ps");
+    f.a3x = P<const uint16_t>(g("a3x"));
+    f.a3_ps = i("a3_ps");
+    f.wx = P<const uint16_t>(g("wx"));
+    f.w_ps = i("w_ps");
+    f.a3 = P<const float>(g("a3"));
+    f.dy3 = P<float>(g("dy3"));
+    f.dy3x = P<uint16_t>(g("dy3x"));
+    f.dy3_ps = i("dy3_ps");
+    f.gw = P<float>(g("gw"));
+    f.gw2 = P<float>(g("gw2"));
+    f.slices = (int)i("slices");
+    if (!f.a3 || !f.dy3 || !f.gw || (f.slices == 0 && !f.gw2)) throw std::invalid_argument("pxb_fc1_bwd: missing pointer");
+    pxb_fc1_bwd(f, B, S(s));
+  });
+  m.def("pxb_conv_bwd", [](int layer, py::dict d, int B, uint64_t s) {
+    auto g = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
+    auto i = [&](const char* k) -> int64_t { return d.contains(k) ? d[k].cast<int64_t>() : 0; };
+    PxbConv c{};
+    c.dyx = P<const uint16_t>(g("dyx"));
+    c.dy_ps = i("dy_ps");
+    c.xx = P<const uint16_t>(g("xx"));
+    c.x_ps = i("x_ps");
+    c.wtx = P<const uint16_t>(g("wtx"));
+    c.wt_ps = i("wt_ps");
+    c.mask = P<const float>(g("mask"));
+    c.dx = P<float>(g("dx"));
+    c.dxx = P<uint16_t>(g("dxx"));
+    c.dx_ps = i("dx_ps");
+    c.ws = P<float>(g("ws"));
+    if (layer != 2 && layer != 3) throw std::invalid_argument("pxb_conv_bwd: layer 2 or 3");
+    if (!c.mask || !c.dx || !c.ws) throw std::invalid_argument("pxb_conv_bwd: missing pointer");
+    const int splits = f32_wgrad_splits(layer, B);
+    c.ws_bias = c.ws + (size_t)splits * 64 * (layer == 2 ? 512 : 576);
+    pxb_conv_bwd(layer, c, B, splits, f32_wgrad_kbps(layer, B), S(s));
+  });
   m.def("f32_split_planes", [](uint64_t src, uint64_t dst, int64_t n, int64_t plane, uint64_t s) {
     f32_split_planes(P<const float>(src), P<uint16_t>(dst), n, plane, S(s));
   });

@@ -190,6 +190,8 @@ struct LossHeadsArgs {
   uint16_t* dz_bf;                 // [B][256] out: dL/dz (FC1 pre-activation), bf16
   float* part;                     // [blocks][(A+1)*128 + (A+1) + 256] out: gradient partials
   float* dz;                       // [B][256] out (optional, replaces dz_bf): dL/dz in fp32
+  uint16_t* dzx;                   // with dz: its three bf16 planes (pre-split backward), or null
+  int64_t dzx_ps;
   const int64_t* step;             // learner step counter (read)
   int64_t* step_snap;              // out: its value for this step's optimizer (may be null)
 };
@@ -220,7 +222,7 @@ struct PackMap {
   const int* dst2;
   uint16_t* arena;      // bf16 packed copies (bf16 network) ...
   float* arena_f32;     // ... or fp32 packed copies (reference-precision network)
-  uint16_t* arena_x;    // fp32 network: split planes of the forward layouts (dst1 < x_plane), or null
+  uint16_t* arena_x;    // fp32 network: split planes of every packed layout (plane stride x_plane), or null
   int64_t x_plane;
 };
 // FC1 weights (Nature-CNN dueling net): flat offsets of advantage.0.weight and
@@ -392,8 +394,37 @@ int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab co
 // whenever every problem of the launch carries planes)
 bool px_enabled();
 void px_set(int v);
+int px_terms();  // 6 or 8 term products (knob 19 = 1 | 2)
 void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
 void px_fc1_fwd_multi(const F32Set& set, hipStream_t s);
+// pre-split exact BACKWARD GEMMs (pxb_kernels.hip, f32_set_variant(20, 1) with knob 19 on):
+// FC1 input gradient + weight gradient in one launch, conv3 / conv2 weight gradient + input
+// gradient in one launch each, every operand as three bf16 planes
+bool pxb_enabled();
+void pxb_set(int v);
+struct PxbFc1 {
+  const uint16_t* dzx;  int64_t dz_ps;   // dL/dz planes [B][256] (dqn_heads_bwd)
+  const uint16_t* a3x;  int64_t a3_ps;   // a3 planes [B][3136] (conv3 forward epilogue)
+  const uint16_t* wx;   int64_t w_ps;    // wfc1p planes [256][3136] (optimizer)
+  const float* a3;                       // ReLU mask of dy3
+  float* dy3;                            // [B][3136] out
+  uint16_t* dy3x;       int64_t dy3_ps;  // dy3 planes out (null: none)
+  float* gw;            // slices > 0: natural-order partials [slices][256][3136]; 0: advantage rows in place
+  float* gw2;           // slices == 0: value rows in place
+  int slices;
+};
+void pxb_fc1_bwd(const PxbFc1& f, int B, hipStream_t s);
+struct PxbConv {
+  const uint16_t* dyx;  int64_t dy_ps;   // output-gradient planes [B][P][64]
+  const uint16_t* xx;   int64_t x_ps;    // layer-input planes (a2 for conv3, a1 for conv2)
+  const uint16_t* wtx;  int64_t wt_ps;   // transposed weight planes (w3t / w2t)
+  const float* mask;                     // ReLU mask of dx (the layer input)
+  float* dx;                             // input gradient out
+  uint16_t* dxx;        int64_t dx_ps;   // its planes (null: none)
+  float* ws;            // weight-gradient partials [splits][64][N]
+  float* ws_bias;       // bias partials [splits][64]
+};
+void pxb_conv_bwd(int layer, const PxbConv& c, int B, int splits, int kbps, hipStream_t s);
 // dst[u * plane + i] = term u of src[i] (u = 0 hi, 1 mid, 2 lo), i < n
 void f32_split_planes(const float* src, uint16_t* dst, int64_t n, int64_t plane, hipStream_t s);
 // FC1 backward in one launch: dy3 = (a3 > 0) * dz . wfc1p (channels-last order) and the
@@ -401,6 +432,7 @@ void f32_split_planes(const float* src, uint16_t* dst, int64_t n, int64_t plane,
 void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,
                  hipStream_t s);
 int f32_wgrad_splits(int layer, int B);
+int f32_wgrad_kbps(int layer, int B);  // k-blocks (32 rows) per split
 size_t f32_wgrad_workspace_floats(int layer, int B);
 int f32_fc1_wgrad_splits();
 int f32_fc1_wgrad_slices(int B);

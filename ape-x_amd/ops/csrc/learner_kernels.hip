@@ -143,12 +143,19 @@ __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v
     const int d1 = pk.dst1[i], d2 = pk.dst2[i];
     if (d1 >= 0) pk.arena_f32[d1] = v;
     if (d2 >= 0) pk.arena_f32[d2] = v;
-    if (pk.arena_x && d1 >= 0 && d1 < pk.x_plane) {  // pre-split planes of the forward layout
+    if (pk.arena_x) {  // pre-split planes of every packed layout (plane stride = the arena size)
       uint16_t h, m, l;
       split3_rne(v, h, m, l);
-      pk.arena_x[d1] = h;
-      pk.arena_x[pk.x_plane + d1] = m;
-      pk.arena_x[2 * pk.x_plane + d1] = l;
+      if (d1 >= 0) {
+        pk.arena_x[d1] = h;
+        pk.arena_x[pk.x_plane + d1] = m;
+        pk.arena_x[2 * pk.x_plane + d1] = l;
+      }
+      if (d2 >= 0) {
+        pk.arena_x[d2] = h;
+        pk.arena_x[pk.x_plane + d2] = m;
+        pk.arena_x[2 * pk.x_plane + d2] = l;
+      }
     }
     return;
   }

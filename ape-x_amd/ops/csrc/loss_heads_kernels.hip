@@ -99,8 +99,12 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
       float d = j < 128 ? g * p.w_adv2[a * 128 + j] - ga * colsum[j] : g * p.w_val2[j - 128];
       d = hr[j] > 0.f ? d : 0.f;
       dzs[rr][j] = d;
-      if (p.dz) p.dz[(size_t)b * 256 + j] = d;
-      else p.dz_bf[(size_t)b * 256 + j] = f2bf(d);
+      if (p.dz) {
+        p.dz[(size_t)b * 256 + j] = d;
+        if (p.dzx) store_planes(p.dzx, p.dzx_ps, (size_t)b * 256 + j, d);  // pxb_kernels.hip operand
+      } else {
+        p.dz_bf[(size_t)b * 256 + j] = f2bf(d);
+      }
     }
   }
   __syncthreads();

@@ -13,7 +13,10 @@
 // exact in fp32 -- carry fp32 accuracy.  They cost 6 x 32 = 192 MFMA cycles per 32x32x16
 // (v_mfma_f32_32x32x16_bf16) instead of 512: 2.7x fewer.  The hh' term is accumulated
 // alone and the five smaller ones in a second accumulator (added once at the end), so the
-// small terms never round against the large running sum.
+// small terms never round against the large running sum.  Knob (19, 2) adds ml' + lm' (8
+// products, 256 cycles): only ll' (<= 2^-32 |x y|) is dropped, so the per-product
+// representation error falls far below one fp32 rounding (MI355X, 6 terms: layer errors
+// 2-3.5x the fp32-MFMA body's; learner step-0 parity 2.0e-4 vs 7.8e-5 of the update length).
 //
 // The round-2 attempt split both operands while staging them into LDS (gemm_x9_k in
 // f32_kernels.hip): ~5.5 VALU per element ate the MFMA savings.  Here nothing is split in
@@ -63,8 +66,9 @@ struct GeoPx {
   static_assert(BK % 16 == 0, "k-steps of 16");
 };
 
-template <class P>
+template <class P, int NTERM>
 __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint16_t* lds) {
+  static_assert(NTERM == 6 || NTERM == 8, "6 or 8 term products");
   using G = GeoPx<P>;
   typename P::Ctx ctx;
   P::decode(args, block, ctx);
@@ -161,6 +165,10 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
           c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][1], c2, 0, 0, 0);
           c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][2], c2, 0, 0, 0);
           c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][0], c2, 0, 0, 0);
+          if constexpr (NTERM == 8) {  // the 2^-24 terms too: only ll' (2^-32) is dropped
+            c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][2], c2, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][1], c2, 0, 0, 0);
+          }
           acc2[mi][ni] = c2;
         }
     }
@@ -191,10 +199,10 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
       }
 }
 
-template <class P>
+template <class P, int NTERM>
 __global__ __launch_bounds__(256, 2) void gemm_px_k(F32Set args, int remap) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[GeoPx<P>::LDS_HALVES];
-  gemm_body_px<P>(args, remap ? xcd_chunk_px(blockIdx.x, gridDim.x) : blockIdx.x, lds);
+  gemm_body_px<P, NTERM>(args, remap ? xcd_chunk_px(blockIdx.x, gridDim.x) : blockIdx.x, lds);
 }
 
 // ------------------------------------------------------------------ policies
@@ -331,14 +339,15 @@ __global__ void split_planes_k(const float* __restrict__ src, uint16_t* __restri
     store_planes(dst, ps, i, src[i]);
 }
 
-int g_px = 0;     // f32_set_variant(19, 0|1)
+int g_px = 0;     // f32_set_variant(19, 0|1|2): off | 6 term products | 8 term products
 int g_px_xcd = 1;
 
 template <class P>
 void px_launch(const F32Set& set, hipStream_t s) {
   const int blocks = set.n * P::tiles(set.B);
   if (blocks <= 0) return;
-  gemm_px_k<P><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+  if (g_px == 2) gemm_px_k<P, 8><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+  else gemm_px_k<P, 6><<<blocks, 256, 0, s>>>(set, g_px_xcd);
   LAUNCH_CHECK();
 }
 
@@ -356,6 +365,8 @@ void check_px(const F32Set& set) {
 }  // namespace
 
 bool px_enabled() { return g_px != 0; }
+
+int px_terms() { return g_px == 2 ? 8 : 6; }
 
 void px_set(int v) { g_px = v; }
 

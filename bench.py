@@ -116,9 +116,10 @@ def parse():
     ap.add_argument("--watchdog", type=float, default=1500.0,
                     help="seconds after which a rank dumps every thread's stack and exits 1 (0 = off): "
                          "a hung collective ends the run with a traceback instead of a silent stall")
-    ap.add_argument("--px", type=int, default=0, choices=[0, 1],
-                    help="fp32 forward GEMMs (conv2/conv3/FC1) on the pre-split exact bf16x6 kernels "
-                         "(px_kernels.hip: fp32-class, every operand as 3 exact bf16 terms)")
+    ap.add_argument("--px", type=int, default=0, choices=[0, 1, 2],
+                    help="fp32 forward GEMMs (conv2/conv3/FC1) on the pre-split exact bf16 kernels "
+                         "(px_kernels.hip: every operand as 3 exact bf16 terms; 1 = 6 term products, "
+                         "2 = 8 term products)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
     ap.add_argument("--unpaced", action="store_true",
@@ -170,7 +171,7 @@ def main():
     if args.px:
         from apex_amd import ops
 
-        ops.hip().f32_set_variant(19, 1)  # before any network / workspace is built
+        ops.hip().f32_set_variant(19, args.px)  # before any network / workspace is built
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     if args.same_device:
@@ -302,7 +303,7 @@ def main():
                 "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
                 "forward": args.forward,
-                "fp32_forward_gemms": ("pre-split exact bf16x6 (3-term operands, fp32-class)" if args.px
+                "fp32_forward_gemms": (f"pre-split exact bf16x{4 + 2 * args.px} (3-term operands, fp32-class)" if args.px
                                        else "fp32 MFMA") if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
                 "actor_learner_overlap": args.overlap,

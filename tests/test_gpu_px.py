@@ -68,7 +68,7 @@ def test_px_forward_is_fp32_class(cuda, B):
             if v:  # the activation planes are exact splits of the fp32 activations
                 for full, planes in ((ws.a1, ws.a1x), (ws.a2, ws.a2x), (ws.a3, ws.a3x)):
                     assert torch.equal(_sum_planes(planes), full.reshape(-1).double())
-                assert torch.equal(_sum_planes(net.arena_x.view(3, -1)), net.arena[:net.fwd_numel].double())
+                assert torch.equal(_sum_planes(net.arena_x.view(3, -1)), net.arena.double())
             g1, g2, g3 = _nchw(ws.a1, B, 32, 20), _nchw(ws.a2, B, 64, 9), _nchw(ws.a3, B, 64, 7)
             for name, inp, got, k, st in (("conv2", g1, g2, 2, 2), ("conv3", g2, g3, 4, 1)):
                 ref = F.relu(F.conv2d(inp, d(f[k].weight), d(f[k].bias), stride=st))
@@ -122,9 +122,55 @@ def test_px_optimizer_keeps_weight_planes(cuda, px):
     torch.cuda.synchronize()
     assert not torch.equal(before, net.arena_x)  # the weights moved
     fresh = torch.empty_like(net.arena_x)
-    eng.learner.net.hip.f32_split_planes(net.arena.data_ptr(), fresh.data_ptr(), net.fwd_numel, net.fwd_numel,
+    eng.learner.net.hip.f32_split_planes(net.arena.data_ptr(), fresh.data_ptr(), net.x_plane, net.x_plane,
                                           torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert torch.equal(fresh, net.arena_x)
     st = eng.learner.stats()
     assert st["loss"] == st["loss"]
+
+
+@pytest.mark.parametrize("B,terms,fc1_slices", [(29, 1, 1), (128, 2, 1), (128, 1, 0)])
+def test_pxb_backward_matches_fp64_autograd(cuda, B, terms, fc1_slices):
+    """Pre-split exact backward (pxb_kernels.hip, knobs (19, terms) + (20, 1)): every parameter
+    gradient against fp64 autograd, next to the fp32-MFMA backward's own error; the output
+    gradients' planes the FC1 / conv3 input-gradient epilogues write are exact splits."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    A = 18
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    dq = torch.randn(B, A, device=cuda) / B
+    m64 = _model(cuda, A=A, seed=3).double()
+    (m64(x.double()) * dq.double()).sum().backward()
+    errs = {}
+    try:
+        hip.f32_set_variant(15, fc1_slices)
+        for v in (0, terms):
+            hip.f32_set_variant(19, v)
+            hip.f32_set_variant(20, 1 if v else 0)
+            m = _model(cuda, A=A, seed=3)
+            for p in m.parameters():
+                p.grad = torch.full_like(p, float("nan"))  # every gradient must be written
+            net = F32DuelingNet(m)
+            ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+            assert ws.pxb == bool(v)
+            net(x, ws)
+            net.backward(dq, x, ws)
+            torch.cuda.synchronize()
+            if v:
+                for full, planes in ((ws.dz, ws.dzx), (ws.dy3, ws.dy3x), (ws.dy2, ws.dy2x)):
+                    assert torch.equal(_sum_planes(planes)[:full.numel()], full.reshape(-1).double())
+            for (name, p), p64 in zip(m.named_parameters(), m64.parameters()):
+                ref = p64.grad
+                errs[(name, v)] = float((p.grad.double() - ref).norm() / ref.norm().clamp_min(1e-30))
+    finally:
+        hip.f32_set_variant(19, 0)
+        hip.f32_set_variant(20, 0)
+        hip.f32_set_variant(15, 1)
+    print("pxb grad errors (rel, vs fp64):", {k: f"{e:.2e}" for k, e in errs.items()})
+    for (name, v), e in errs.items():
+        if v:
+            assert e < 1e-4, (name, e)
+            assert e <= 3.0 * errs[(name, 0)] + 1e-6, (name, e, errs[(name, 0)])
