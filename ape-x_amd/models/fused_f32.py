@@ -36,6 +36,14 @@ from .dqn import DuelingDQN
 P3, C3 = 49, 64
 FEAT = P3 * C3  # 3136
 F32_SPLITS = 7  # FC1 forward split-K slabs (f32_kernels.hip kFcSplits)
+# extra elements between the three bf16 planes of a split tensor (A/B knob: plane strides that
+# are large powers-of-two multiples put the three loads of one chunk on the same HBM channel)
+PX_PAD = int(os.environ.get("APEX_PX_PAD", "0"))
+
+
+def _planes(n: int, device) -> torch.Tensor:
+    """[3, n + PX_PAD] bf16: hi | mid | lo planes of an n-element tensor (plane stride = shape[1])."""
+    return torch.empty(3, n + PX_PAD, dtype=torch.bfloat16, device=device)
 
 
 class F32Workspace:
@@ -50,9 +58,9 @@ class F32Workspace:
         # pre-split exact forward (px_kernels.hip): each activation also as 3 bf16 planes
         self.px = ops.hip().px_enabled() if px is None else bool(px)
         bf = dict(dtype=torch.bfloat16, device=device)
-        self.a1x = torch.empty(3, B * 400 * 32, **bf) if self.px else None
-        self.a2x = torch.empty(3, B * 81 * 64, **bf) if self.px else None
-        self.a3x = torch.empty(3, B * FEAT, **bf) if self.px else None
+        self.a1x = _planes(B * 400 * 32, device) if self.px else None
+        self.a2x = _planes(B * 81 * 64, device) if self.px else None
+        self.a3x = _planes(B * FEAT, device) if self.px else None
         self.z = torch.empty(F32_SPLITS, B, 256, **f32)
         self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
         self.q = torch.empty(B, A, **f32)
@@ -67,9 +75,9 @@ class F32Workspace:
             self.dy2 = torch.empty(B, 81, 64, **f32)
             self.dy1 = torch.empty(B, 400, 32, **f32)
             if self.pxb:
-                self.dzx = torch.empty(3, B * 256, **bf)
-                self.dy3x = torch.empty(3, B * FEAT, **bf)
-                self.dy2x = torch.empty(3, B * 81 * 64, **bf)
+                self.dzx = _planes(B * 256, device)
+                self.dy3x = _planes(B * FEAT, device)
+                self.dy2x = _planes(B * 81 * 64, device)
 
 
 class F32DuelingNet:
@@ -104,7 +112,7 @@ class F32DuelingNet:
         # every packed layout as 3 bf16 planes (hi | mid | lo, plane stride x_plane = the arena
         # size): the pre-split exact GEMMs' weight operands (px_kernels.hip forward layouts,
         # pxb_kernels.hip transposes + wfc1p), kept by repack / the optimizer's pack pass
-        self.x_plane = self.arena.numel()
+        self.x_plane = self.arena.numel() + PX_PAD
         self.arena_x = torch.empty(3 * self.x_plane, dtype=torch.bfloat16, device=self.device)
         self.repack()
 
@@ -122,7 +130,7 @@ class F32DuelingNet:
 
     def split_weights(self) -> None:
         """arena_x = the exact 3-term bf16 split of the packed layouts (one kernel)."""
-        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.x_plane, self.x_plane,
+        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.arena.numel(), self.x_plane,
                                   self._s())
 
     def wx(self, name: str) -> int:

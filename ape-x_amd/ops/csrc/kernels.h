@@ -395,6 +395,8 @@ int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab co
 bool px_enabled();
 void px_set(int v);
 int px_terms();  // 6 or 8 term products (knob 19 = 1 | 2)
+int px_pipe();   // knob 21: 0 = two LDS stages + 1 register prefetch, 1 = one LDS stage + 2-deep register ring
+void px_set_pipe(int v);
 void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
 void px_fc1_fwd_multi(const F32Set& set, hipStream_t s);
 // pre-split exact BACKWARD GEMMs (pxb_kernels.hip, f32_set_variant(20, 1) with knob 19 on):

@@ -66,7 +66,7 @@ struct GeoPx {
   static_assert(BK % 16 == 0, "k-steps of 16");
 };
 
-template <class P, int NTERM>
+template <class P, int NTERM, int PIPE>
 __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint16_t* lds) {
   static_assert(NTERM == 6 || NTERM == 8, "6 or 8 term products");
   using G = GeoPx<P>;
@@ -95,8 +95,8 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
     const int q = min(t + 256 * j, G::CB - 1);
     rowb[j] = P::row_b(ctx, q / G::RA, q % G::RA);
   }
-  uint4 ra[G::NA][3], rb[G::NB][3];
-  auto gload = [&](int kb) {
+  uint4 ra0[G::NA][3], rb0[G::NB][3], ra1[G::NA][3], rb1[G::NB][3];
+  auto gload = [&](int kb, uint4 (&ra)[G::NA][3], uint4 (&rb)[G::NB][3]) {
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       if (G::CA % 256 == 0 || t + 256 * j < G::CA) {
@@ -114,7 +114,7 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
       }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const uint4 (&ra)[G::NA][3], const uint4 (&rb)[G::NB][3]) {
     uint16_t* As = lds + buf * G::STAGE;
     uint16_t* Bs = As + 3 * G::SA;
 #pragma unroll
@@ -173,20 +173,39 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
         }
     }
   };
-  int kb = ctx.kb0, cur = 0;
-  if (kb < ctx.kb1) {
-    gload(kb);
-    sstore(0);
-  }
-  __syncthreads();
-  for (; kb < ctx.kb1; ++kb) {
-    const bool more = kb + 1 < ctx.kb1;
-    if (more) gload(kb + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cur);
-    if (more) sstore(cur ^ 1);
+  if constexpr (PIPE == 0) {  // two LDS stages, the next k-block prefetched in registers
+    int kb = ctx.kb0, cur = 0;
+    if (kb < ctx.kb1) {
+      gload(kb, ra0, rb0);
+      sstore(0, ra0, rb0);
+    }
     __syncthreads();
-    cur ^= 1;
+    for (; kb < ctx.kb1; ++kb) {
+      const bool more = kb + 1 < ctx.kb1;
+      if (more) gload(kb + 1, ra0, rb0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur);
+      if (more) sstore(cur ^ 1, ra0, rb0);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {  // one LDS stage (4 workgroups per CU), k-blocks kb+1 and kb+2 in flight in registers
+    int kb = ctx.kb0;
+    if (kb < ctx.kb1) gload(kb, ra0, rb0);
+    if (kb + 1 < ctx.kb1) gload(kb + 1, ra1, rb1);
+    for (; kb < ctx.kb1; kb += 2) {
+      __syncthreads();  // every wave is done reading the stage
+      sstore(0, ra0, rb0);
+      __syncthreads();
+      if (kb + 2 < ctx.kb1) gload(kb + 2, ra0, rb0);
+      compute(0);
+      if (kb + 1 >= ctx.kb1) break;
+      __syncthreads();
+      sstore(0, ra1, rb1);
+      __syncthreads();
+      if (kb + 3 < ctx.kb1) gload(kb + 3, ra1, rb1);
+      compute(0);
+    }
   }
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi)
@@ -202,7 +221,15 @@ __device__ __forceinline__ void gemm_body_px(const F32Set& args, int block, uint
 template <class P, int NTERM>
 __global__ __launch_bounds__(256, 2) void gemm_px_k(F32Set args, int remap) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[GeoPx<P>::LDS_HALVES];
-  gemm_body_px<P, NTERM>(args, remap ? xcd_chunk_px(blockIdx.x, gridDim.x) : blockIdx.x, lds);
+  gemm_body_px<P, NTERM, 0>(args, remap ? xcd_chunk_px(blockIdx.x, gridDim.x) : blockIdx.x, lds);
+}
+// PIPE 1: one LDS stage + a 2-deep register ring (MI355X, conv2 forward: the 2-stage form ran
+// at 19 % MFMA busy with 2 workgroups per CU -- each k-block's loads waited ~1 us of memory
+// latency behind ~450 MFMA cycles; 4 resident workgroups x 2 k-blocks in flight hide it)
+template <class P, int NTERM>
+__global__ __launch_bounds__(256, 3) void gemm_px1_k(F32Set args, int remap) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[GeoPx<P>::STAGE];
+  gemm_body_px<P, NTERM, 1>(args, remap ? xcd_chunk_px(blockIdx.x, gridDim.x) : blockIdx.x, lds);
 }
 
 // ------------------------------------------------------------------ policies
@@ -341,13 +368,19 @@ __global__ void split_planes_k(const float* __restrict__ src, uint16_t* __restri
 
 int g_px = 0;     // f32_set_variant(19, 0|1|2): off | 6 term products | 8 term products
 int g_px_xcd = 1;
+int g_px_pipe = 1;  // f32_set_variant(21, 0|1): pipeline form of the px / pxb bodies (see gemm_px1_k)
 
 template <class P>
 void px_launch(const F32Set& set, hipStream_t s) {
   const int blocks = set.n * P::tiles(set.B);
   if (blocks <= 0) return;
-  if (g_px == 2) gemm_px_k<P, 8><<<blocks, 256, 0, s>>>(set, g_px_xcd);
-  else gemm_px_k<P, 6><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+  if (g_px_pipe == 1) {
+    if (g_px == 2) gemm_px1_k<P, 8><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+    else gemm_px1_k<P, 6><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+  } else {
+    if (g_px == 2) gemm_px_k<P, 8><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+    else gemm_px_k<P, 6><<<blocks, 256, 0, s>>>(set, g_px_xcd);
+  }
   LAUNCH_CHECK();
 }
 
@@ -367,6 +400,10 @@ void check_px(const F32Set& set) {
 bool px_enabled() { return g_px != 0; }
 
 int px_terms() { return g_px == 2 ? 8 : 6; }
+
+int px_pipe() { return g_px_pipe; }
+
+void px_set_pipe(int v) { g_px_pipe = v; }
 
 void px_set(int v) { g_px = v; }
 

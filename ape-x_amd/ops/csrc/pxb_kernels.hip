@@ -90,7 +90,7 @@ __device__ __forceinline__ bfx8 frag_row(const uint16_t* img, int kc, int r0, in
   return *reinterpret_cast<const bfx8*>(img + (r0 + (lane & 31)) * RP + kc * 16 + 8 * (lane >> 5));
 }
 
-template <class P, int NTERM>
+template <class P, int NTERM, int PIPE>
 __device__ __forceinline__ void pxb_body(const PxbArgs& args, int block, uint16_t* lds) {
   using G = GeoB<P>;
   static_assert(NTERM == 6 || NTERM == 8, "6 or 8 term products");
@@ -121,8 +121,8 @@ __device__ __forceinline__ void pxb_body(const PxbArgs& args, int block, uint16_
   for (int j = 0; j < G::NA; ++j) la[j] = P::init_a(args, ctx, min(t + 256 * j, G::CA - 1));
 #pragma unroll
   for (int j = 0; j < G::NB; ++j) lb[j] = P::init_b(args, ctx, min(t + 256 * j, G::CB - 1));
-  uint4 ra[G::NA][3], rb[G::NB][3];
-  auto gload = [&](int kb) {
+  uint4 ra0[G::NA][3], rb0[G::NB][3], ra1[G::NA][3], rb1[G::NB][3];
+  auto gload = [&](int kb, uint4 (&ra)[G::NA][3], uint4 (&rb)[G::NB][3]) {
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       if (G::CA % 256 != 0 && t + 256 * j >= G::CA) continue;
@@ -138,7 +138,7 @@ __device__ __forceinline__ void pxb_body(const PxbArgs& args, int block, uint16_
       for (int u = 0; u < 3; ++u) rb[j][u] = b ? *reinterpret_cast<const uint4*>(b + u * psb) : make_uint4(0, 0, 0, 0);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const uint4 (&ra)[G::NA][3], const uint4 (&rb)[G::NB][3]) {
     uint16_t* As = lds + buf * G::STAGE;
     uint16_t* Bs = As + 3 * G::SA;
 #pragma unroll
@@ -212,20 +212,39 @@ __device__ __forceinline__ void pxb_body(const PxbArgs& args, int block, uint16_
       }
     }
   };
-  int kb = ctx.kb0, cur = 0;
-  if (kb < ctx.kb1) {
-    gload(kb);
-    sstore(0);
-  }
-  __syncthreads();
-  for (; kb < ctx.kb1; ++kb) {
-    const bool more = kb + 1 < ctx.kb1;
-    if (more) gload(kb + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cur);
-    if (more) sstore(cur ^ 1);
+  if constexpr (PIPE == 0) {  // two LDS stages, the next k-block prefetched in registers
+    int kb = ctx.kb0, cur = 0;
+    if (kb < ctx.kb1) {
+      gload(kb, ra0, rb0);
+      sstore(0, ra0, rb0);
+    }
     __syncthreads();
-    cur ^= 1;
+    for (; kb < ctx.kb1; ++kb) {
+      const bool more = kb + 1 < ctx.kb1;
+      if (more) gload(kb + 1, ra0, rb0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur);
+      if (more) sstore(cur ^ 1, ra0, rb0);
+      __syncthreads();
+      cur ^= 1;
+    }
+  } else {  // one LDS stage, k-blocks kb+1 and kb+2 in flight in registers (px_kernels.hip gemm_px1_k)
+    int kb = ctx.kb0;
+    if (kb < ctx.kb1) gload(kb, ra0, rb0);
+    if (kb + 1 < ctx.kb1) gload(kb + 1, ra1, rb1);
+    for (; kb < ctx.kb1; kb += 2) {
+      __syncthreads();
+      sstore(0, ra0, rb0);
+      __syncthreads();
+      if (kb + 2 < ctx.kb1) gload(kb + 2, ra0, rb0);
+      compute(0);
+      if (kb + 1 >= ctx.kb1) break;
+      __syncthreads();
+      sstore(0, ra1, rb1);
+      __syncthreads();
+      if (kb + 3 < ctx.kb1) gload(kb + 3, ra1, rb1);
+      compute(0);
+    }
   }
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -255,8 +274,14 @@ struct MaxOf {
 template <class P1, class P2, int NTERM>
 __global__ __launch_bounds__(256, 2) void pxb2_k(PxbArgs a1, PxbArgs a2, int n1) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[MaxOf<GeoB<P1>::LDS, GeoB<P2>::LDS>::v];
-  if ((int)blockIdx.x < n1) pxb_body<P1, NTERM>(a1, blockIdx.x, lds);
-  else pxb_body<P2, NTERM>(a2, blockIdx.x - n1, lds);
+  if ((int)blockIdx.x < n1) pxb_body<P1, NTERM, 0>(a1, blockIdx.x, lds);
+  else pxb_body<P2, NTERM, 0>(a2, blockIdx.x - n1, lds);
+}
+template <class P1, class P2, int NTERM>
+__global__ __launch_bounds__(256, 2) void pxb2p1_k(PxbArgs a1, PxbArgs a2, int n1) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[MaxOf<GeoB<P1>::STAGE, GeoB<P2>::STAGE>::v];
+  if ((int)blockIdx.x < n1) pxb_body<P1, NTERM, 1>(a1, blockIdx.x, lds);
+  else pxb_body<P2, NTERM, 1>(a2, blockIdx.x - n1, lds);
 }
 
 // ------------------------------------------------------------------ policies
@@ -528,8 +553,13 @@ int g_pxb = 0;  // f32_set_variant(20, 0|1): the backward GEMMs on the pre-split
 template <class P1, class P2>
 void launch_pair(const PxbArgs& a1, int n1, const PxbArgs& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  if (px_terms() == 8) pxb2_k<P1, P2, 8><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else pxb2_k<P1, P2, 6><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  if (px_pipe() == 1) {
+    if (px_terms() == 8) pxb2p1_k<P1, P2, 8><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+    else pxb2p1_k<P1, P2, 6><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  } else {
+    if (px_terms() == 8) pxb2_k<P1, P2, 8><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+    else pxb2_k<P1, P2, 6><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  }
   LAUNCH_CHECK();
 }
 

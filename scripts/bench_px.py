@@ -19,6 +19,8 @@ ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--terms", default="0,6,8", help="0 = fp32 MFMA body, 6 / 8 = px term products")
 ap.add_argument("--only", default=None)
+ap.add_argument("--pipes", default="1", help="px pipeline forms to sweep (knob 21)")
+ap.add_argument("--bwd", type=int, default=1, help="also time the backward (pxb with px on)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -63,8 +65,10 @@ P = 3 * B
 FLOP = {1: 2 * P * 400 * 32 * 256, 2: 2 * P * 81 * 64 * 512, 3: 2 * P * 49 * 64 * 576, 4: 2 * P * 256 * 3136}
 NAME = {1: "conv1_fwd", 2: "conv2_fwd", 3: "conv3_fwd", 4: "fc1_fwd"}
 outs = {}
-for terms in map(int, a.terms.split(",")):
+combos = [(t, p) for t in map(int, a.terms.split(",")) for p in (map(int, a.pipes.split(",")) if t else [0])]
+for terms, pipe in combos:
     hip.f32_set_variant(19, {0: 0, 6: 1, 8: 2}[terms])
+    hip.f32_set_variant(21, pipe)
     net = F32DuelingNet(m)
     wss = [F32Workspace(B, A, dev, keep_for_backward=(i == 0)) for i in range(3)]
     forward_multi_f32([(net, frames, w, ids, idx) for w in wss])
@@ -100,10 +104,28 @@ for terms in map(int, a.terms.split(",")):
               else (lambda s=sets: hip.f32_fc1_fwd_multi(s, B, S())))
         us = time_fn(fn)
         tf = FLOP[layer] / us / 1e6
-        print(f"terms={terms} {NAME[layer]:10s} {us:8.2f} us  {tf:6.1f} fp32-equivalent TFLOP/s")
-    outs[terms] = wss[0].z.clone()
+        print(f"terms={terms} pipe={pipe} {NAME[layer]:10s} {us:8.2f} us  {tf:6.1f} fp32-equivalent TFLOP/s")
+    outs[(terms, pipe)] = wss[0].z.clone()
+    if a.bwd:  # backward: FC1 (dgrad + wgrad) and the conv chain (conv3 / conv2 pairs + conv1 wgrad)
+        hip.f32_set_variant(20, 1 if px else 0)
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        netb = F32DuelingNet(m)
+        netb.enable_backward(B)
+        wb = F32Workspace(B, A, dev, keep_for_backward=True)
+        forward_multi_f32([(netb, frames, wb, ids, idx)])
+        wb.dz.normal_()
+        wb.dz.mul_((wb.h > 0).float())
+        if wb.pxb:
+            hip.f32_split_planes(wb.dz.data_ptr(), wb.dzx.data_ptr(), B * 256, wb.dzx.shape[1], S())
+        for nm, fn, flop in (("fc1_bwd", lambda: netb._fc1_bwd(wb), 2 * 2 * B * 256 * 3136),
+                             ("conv_bwd", lambda: netb._conv_chain(frames, wb, ids, idx),
+                              2 * 2 * B * (49 * 64 * 576 + 81 * 64 * 512) + 2 * B * 400 * 32 * 256)):
+            us = time_fn(fn)
+            print(f"terms={terms} pipe={pipe} pxb={int(wb.pxb)} {nm:10s} {us:8.2f} us  {flop / us / 1e6:6.1f} fp32-equivalent TFLOP/s")
+        hip.f32_set_variant(20, 0)
 hip.f32_set_variant(19, 0)
-base = outs.get(0)
-for t, z in outs.items():
+base = outs.get((0, 0))
+for (t, p), z in outs.items():
     if base is not None and t:
-        print(f"terms={t}: max |z - z_fp32| / max|z| = {float((z - base).abs().max() / base.abs().max()):.3e}")
+        print(f"terms={t} pipe={p}: max |z - z_fp32| / max|z| = {float((z - base).abs().max() / base.abs().max()):.3e}")

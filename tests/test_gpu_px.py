@@ -31,8 +31,9 @@ def _nchw(t, B, C, H):
     return t.view(B, H, H, C).permute(0, 3, 1, 2).double()
 
 
-def _sum_planes(x):
-    """fp64 sum of the three bf16 planes [3, N] (each term exact in fp64)."""
+def _sum_planes(x, n=None):
+    """fp64 sum of the three bf16 planes [3, N] (each term exact in fp64), first n elements."""
+    x = x[:, :n] if n is not None else x
     return x[0].double() + x[1].double() + x[2].double()
 
 
@@ -67,8 +68,8 @@ def test_px_forward_is_fp32_class(cuda, B):
             torch.cuda.synchronize()
             if v:  # the activation planes are exact splits of the fp32 activations
                 for full, planes in ((ws.a1, ws.a1x), (ws.a2, ws.a2x), (ws.a3, ws.a3x)):
-                    assert torch.equal(_sum_planes(planes), full.reshape(-1).double())
-                assert torch.equal(_sum_planes(net.arena_x.view(3, -1)), net.arena.double())
+                    assert torch.equal(_sum_planes(planes, full.numel()), full.reshape(-1).double())
+                assert torch.equal(_sum_planes(net.arena_x.view(3, -1), net.arena.numel()), net.arena.double())
             g1, g2, g3 = _nchw(ws.a1, B, 32, 20), _nchw(ws.a2, B, 64, 9), _nchw(ws.a3, B, 64, 7)
             for name, inp, got, k, st in (("conv2", g1, g2, 2, 2), ("conv3", g2, g3, 4, 1)):
                 ref = F.relu(F.conv2d(inp, d(f[k].weight), d(f[k].bias), stride=st))
@@ -122,10 +123,11 @@ def test_px_optimizer_keeps_weight_planes(cuda, px):
     torch.cuda.synchronize()
     assert not torch.equal(before, net.arena_x)  # the weights moved
     fresh = torch.empty_like(net.arena_x)
-    eng.learner.net.hip.f32_split_planes(net.arena.data_ptr(), fresh.data_ptr(), net.x_plane, net.x_plane,
+    n = net.arena.numel()
+    eng.learner.net.hip.f32_split_planes(net.arena.data_ptr(), fresh.data_ptr(), n, net.x_plane,
                                           torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    assert torch.equal(fresh, net.arena_x)
+    assert torch.equal(fresh.view(3, -1)[:, :n], net.arena_x.view(3, -1)[:, :n])
     st = eng.learner.stats()
     assert st["loss"] == st["loss"]
 
@@ -161,7 +163,7 @@ def test_pxb_backward_matches_fp64_autograd(cuda, B, terms, fc1_slices):
             torch.cuda.synchronize()
             if v:
                 for full, planes in ((ws.dz, ws.dzx), (ws.dy3, ws.dy3x), (ws.dy2, ws.dy2x)):
-                    assert torch.equal(_sum_planes(planes)[:full.numel()], full.reshape(-1).double())
+                    assert torch.equal(_sum_planes(planes, full.numel()), full.reshape(-1).double())
             for (name, p), p64 in zip(m.named_parameters(), m64.parameters()):
                 ref = p64.grad
                 errs[(name, v)] = float((p.grad.double() - ref).norm() / ref.norm().clamp_min(1e-30))
