@@ -176,6 +176,16 @@ class AQLEngineConfig:
     use_graphs: bool = True
     fork_tree: bool = False  # tree write on a forked stream: measured 9851 vs 11769 steps/s (two cross-queue
                              # hand-offs per ~85 us step cost more than the 11 us they hide)
+    # acting on its own HIP stream beside the learner steps (staged transitions); MI355X, B 32:
+    # 12978-13005 vs 13161 SGD steps/s serial -- the learner's chain of small kernels slows by
+    # about what the hidden acting step saves, so serial stays the default
+    overlap: bool = False
+    fused_sample: bool = os.environ.get("APEX_AQL_FUSED_SAMPLE", "1") == "1"  # PER draw inside aql_learn_fwd
+    # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
+    # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
+    act_blocks: int = int(os.environ.get("APEX_AQL_ACT_BLOCKS", "0"))
+    act_q: str = os.environ.get("APEX_AQL_ACTQ", "mfma")  # acting Q: "mfma" = the learner's fp32-MFMA candidate forward (aql_act_q),
+                             # "scalar" = one wave per candidate item (aql_candidate_q)
     seed: int = 0
 
 
@@ -257,6 +267,10 @@ class AQLLearner:
             p["dbg"] = self.dbg.data_ptr()
         self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
                                   float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
+        # fused sampling: the same stratified draw (seed, counter, mass) as per_sample inside the forward
+        self.Ls = (h.aql_learn_set_sample(self.L, replay.tree, replay.filled.data_ptr(), self.beta.data_ptr(),
+                                          self.step_ctr.data_ptr(), replay.seed ^ 0x51A7,
+                                          0 if cfg.exact_mass else 1) if cfg.fused_sample else None)
         self.G = h.make_aql_grad(self._grad_jobs(), self.P, self.vec.data_ptr(), B, self.grad.data_ptr(),
                                  self.part.data_ptr(), self.lossp.data_ptr(), self.loss_p.data_ptr())
         layers = []
@@ -332,10 +346,13 @@ class AQLLearner:
     def step(self) -> None:
         self.join()  # the sampler reads the tree the previous step's forked write updated
         h, r, s = self.hip, self.replay, self._s()
-        excl = 0 if self.cfg.exact_mass else 1
-        h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
-                     self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
-        h.aql_learn_fwd(self.L, s)
+        if self.Ls is not None:  # the forward samples its own rows (one launch fewer)
+            h.aql_learn_fwd(self.Ls, s)
+        else:
+            excl = 0 if self.cfg.exact_mass else 1
+            h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
+                         self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
+            h.aql_learn_fwd(self.L, s)
         h.aql_learn_bwd(self.L, s)
         # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
         # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
@@ -463,7 +480,33 @@ class AQLEngine:
             ep_count=self.ep_count.data_ptr(), ep_log=self.ep_log.data_ptr(), log_cap=self.log_cap))
         self.ins = h.make_aql_insert(dict(self.replay.table_ptrs(), C=self.replay.capacity,
                                           filled=self.replay.filled.data_ptr(), slots=self.slots.data_ptr()))
+        # overlap: the acting step writes its transitions into staging half h (rows 0..E-1);
+        # the learner's graph applies the other half (the previous acting step's) to the ring
+        # before its first sample, so acting never touches a table or tree the learner reads
+        self.overlap = bool(cfg.overlap)
+        self._half = 0
+        if self.overlap:
+            assert not cfg.fork_tree, "overlap and fork_tree are exclusive"
+            self._zero64 = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._stage_slots = torch.zeros(E, dtype=torch.int32, device=dev)
+            self._stage = []
+            self._stage_ins = []
+            for _ in (0, 1):
+                t = {"st": torch.zeros(E, self.obs, **f32), "st2": torch.zeros(E, self.obs, **f32),
+                     "rew": torch.zeros(E, **f32), "done": torch.zeros(E, **f32),
+                     "amu": torch.zeros(E, self.T, self.adim, **f32),
+                     "act": torch.zeros(E, dtype=torch.int32, device=dev)}
+                self._stage.append(t)
+                self._stage_ins.append(h.make_aql_insert(dict({k: v.data_ptr() for k, v in t.items()}, C=E,
+                                                              filled=self._zero64.data_ptr(),
+                                                              slots=self._stage_slots.data_ptr())))
+            self._astream = torch.cuda.Stream(device=dev)
+            self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()]
+            self._ev_learn = torch.cuda.Event()
         self.actor_net = FusedAQL(self.actor_model)._net()
+        # acting on the learner's MFMA candidate forward (online net, s only, row = env index)
+        self.actL = h.make_aql_act(self.actor_net, self.obs_buf.data_ptr(), self.amu.data_ptr(), self.ws.data_ptr(),
+                                   self.qbuf.data_ptr(), E, int(cfg.act_blocks) or (64 if cfg.overlap else 0))
         h.aql_env_reset(self.env, self._s())
         self.iterations = 0
         self.learner_steps = 0
@@ -482,18 +525,36 @@ class AQLEngine:
         self.hip.copy_f32(self.actor_flat.data_ptr(), self.learner.flat.data_ptr(), self.learner.P, s)
         self.hip.copy_f32(self.actor_eps.data_ptr(), self.learner.eps.data_ptr(), self.learner.eps.numel(), s)
 
-    def actor_step(self) -> None:
+    def actor_step(self, half: int | None = None) -> None:
+        """One acting step of all E envs.  ``half`` (overlap mode): write the transitions into
+        staging half ``half`` instead of the ring (see :meth:`apply_staged`)."""
         self.learner.join()  # the actor's tree writes follow the learner's forked one
         h, s, E, r = self.hip, self._s(), self.E, self.replay
         h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
                       self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s)
-        h.aql_candidate_q(self.actor_net, self.ws.data_ptr(), self.obs_buf.data_ptr(), self.amu.data_ptr(), E,
-                          self.qbuf.data_ptr(), s)
+        if self.cfg.act_q == "mfma":
+            h.aql_noisy_eff(self.actor_net, self.ws.data_ptr(), s)
+            h.aql_act_q(self.actL, s)
+        else:
+            h.aql_candidate_q(self.actor_net, self.ws.data_ptr(), self.obs_buf.data_ptr(), self.amu.data_ptr(), E,
+                              self.qbuf.data_ptr(), s)
         h.aql_select(self.qbuf.data_ptr(), self.amu.data_ptr(), E, self.T, self.adim, self.eps.data_ptr(),
                      self.seed ^ 0xA9C1, self.actor_ctr.data_ptr(), self.act_idx.data_ptr(), self.env_act.data_ptr(), s)
+        if half is not None:
+            h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(),
+                           self._stage_ins[half], s)
+            self.actor_ctr.add_(1)  # the acting RNG counter (per_write_leaves bumps it otherwise)
+            return
         h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(), self.ins, s)
         h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
+
+    def apply_staged(self, half: int) -> None:
+        """Overlap mode, learner stream: staging half ``half`` -> the ring at max priority."""
+        h, s, E, r = self.hip, self._s(), self.E, self.replay
+        h.aql_apply_staged(self._stage_ins[half], self.ins, E, self.obs, self.T * self.adim, s)
+        h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
+                           r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, 0, 0, s)
 
     def learn_steps(self) -> None:
         for _ in range(self.K):
@@ -504,16 +565,40 @@ class AQLEngine:
         """Act until the replay holds more than ``threshold`` transitions (AQL_dis.py:120:
         learning starts once len(buffer) > batch_size)."""
         thr = threshold if threshold is not None else (self.cfg.threshold or self.cfg.batch_size + 1)
-        for _ in range(max(1, -(-int(thr) // self.E))):
+        n = max(1, -(-int(thr) // self.E))
+        if self.overlap:  # staged halves applied right away, plus one more left staged for the first iteration
+            for i in range(n + 1):
+                self.actor_step(self._half)
+                if i < n:
+                    self.apply_staged(self._half)
+                self._half ^= 1
+            self.publish()
+            return
+        for _ in range(n):
             self.actor_step()
         self.publish()
 
     def capture(self) -> None:
-        """Actor step and the K learner steps each as one hipGraph (same stream order)."""
+        """Actor step and the K learner steps each as one hipGraph (same stream order); overlap
+        mode: one actor graph and one learner graph (apply + K steps) per staging half."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):  # warm the launch paths outside capture
             torch.cuda.synchronize(self.device)
+        if self.overlap:
+            self._g_actor, self._g_learn = [], []
+            for hh in (0, 1):
+                ga, gl = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    self.actor_step(hh)
+                with torch.cuda.graph(gl):
+                    self.apply_staged(1 - hh)
+                    self.learn_steps()
+                self._g_actor.append(ga)
+                self._g_learn.append(gl)
+            torch.cuda.synchronize(self.device)
+            self._ev_learn.record(torch.cuda.current_stream(self.device))
+            return
         self._g_actor = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_actor):
             self.actor_step()
@@ -528,6 +613,8 @@ class AQLEngine:
 
     def iteration(self) -> None:
         """One actor step of all envs, weight publish, K learner steps."""
+        if self.overlap:
+            return self._iteration_overlap()
         self.learner.beta.fill_(self._beta())
         if self._g_actor is not None:
             self._g_actor.replay()
@@ -544,6 +631,38 @@ class AQLEngine:
             self.learner.sync_target()
             self.target_syncs.append(self.iterations)
         self.iterations += 1
+
+    def _iteration_overlap(self) -> None:
+        """Acting step t (staging half h) on the acting stream || the learner (apply half 1-h,
+        the acting step t-1's, then K SGD steps) on the caller's stream.  Events: acting t
+        waits for the learner t-1 (its publish); the learner t waits for acting t-1 (the half
+        it applies) and, before publishing into the acting weights, for acting t."""
+        hh = self._half
+        L, A = torch.cuda.current_stream(self.device), self._astream
+        A.wait_event(self._ev_learn)
+        with torch.cuda.stream(A):
+            if self._g_actor is not None:
+                self._g_actor[hh].replay()
+            else:
+                self.actor_step(hh)
+        self._ev_actor[hh].record(A)
+        L.wait_event(self._ev_actor[1 - hh])
+        self.learner.beta.fill_(self._beta())
+        if self._g_learn is not None:
+            self._g_learn[hh].replay()
+        else:
+            self.apply_staged(1 - hh)
+            self.learn_steps()
+        L.wait_event(self._ev_actor[hh])
+        self.publish()
+        before = self.learner_steps
+        self.learner_steps += self.K
+        if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):
+            self.learner.sync_target()
+            self.target_syncs.append(self.iterations)
+        self.iterations += 1
+        self._ev_learn.record(L)
+        self._half ^= 1
 
     def finished_episodes(self) -> list[tuple[float, int]]:
         """(return, length) of the episodes finished since the last call (host sync)."""

@@ -37,6 +37,8 @@
 // [B, 1] and scored by a Categorical of batch shape [B], so log_prob broadcasts to [B, B]
 // and loss_p = mean_ij(-log pi_j(best_i)) - ent_lam * mean_j H_j.  Per sample j that is
 // -(1/B) sum_k cnt_k log p_jk - ent_lam H_j with cnt_k = #{i : best_i = k}.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -92,13 +94,12 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   __shared__ float ao1b[kCat], ao2b[kH], w2e[kH], b1e[kH], qb1[kH], qb2[kH];
   __shared__ float sv[2][64], hq[2][kH], qf[2][kH], stp[2][kH];
   __shared__ float qpart[4][2][16];
+  __shared__ int srow;
   const bool tgt = blockIdx.y != 0;
   const AQLNet& N = tgt ? L.tg : L.on;
   const float* eff = tgt ? L.eff_tg : L.eff_on;
   const int T = N.T, RT = (T + 15) >> 4;
-  const int b = blockIdx.x / RT, rt = blockIdx.x - b * RT;
-  const int nst = tgt ? 1 : 2;  // online: {s, s'}, target: {s'}
-  const int row = L.idx[b];
+  const int nst = (tgt || L.act_mode) ? 1 : 2;  // online: {s, s'} (acting: {s}), target: {s'}
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, q = lane >> 4;
   const int obs = N.obs, adim = N.adim, cont = N.cont, po = obs + 1;
   {  // stage the two 64x128 matrices with 16-byte loads, all in flight before the stores
@@ -133,6 +134,30 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
     qb1[t] = N.qf_b1[t];
     qb2[t] = N.qf_b2[t];
   }
+  // work items (sample b, candidate tile rt): one per workgroup for the learner; the acting
+  // launch (act_mode) runs a small grid that loops, so the weights staged above (~110 KB of
+  // LDS, one workgroup per CU) are loaded once per workgroup and most CUs stay free for the
+  // learner's kernels running beside it
+  for (int item = blockIdx.x; item < L.B * RT; item += gridDim.x) {
+  const int b = item / RT, rt = item - b * RT;
+  __syncthreads();  // the previous item is done with sv / xt / stp / qpart / srow
+  if (L.fused_sample) {  // wave 0 draws sample b (identical in every workgroup of b: same Philox stream)
+    if (wave == 0) {
+      const int64_t f = L.filled[0];
+      const int length = (int)(f < (int64_t)L.tree.size[0] ? f : (int64_t)L.tree.size[0]);
+      const int node = tree_sample_leaf(L.tree, b, L.B, length, L.exclude_last, L.seed, (uint64_t)L.ctr[0], lane);
+      if (lane == 0) {
+        srow = node;
+        if (rt == 0 && !tgt) {
+          const float p = L.tree.leaf_sum[node], pmin = L.tree.node_min[L.tree.levels - 1][0], beta = L.beta[0];
+          L.idx_out[b] = node;
+          L.w_out[b] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const int row = L.fused_sample ? srow : (L.idx ? L.idx[b] : b);
   if (t < 128) {
     const int si = t >> 6, i = t & 63;
     if (si < nst && i < obs) sv[si][i] = ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i];
@@ -213,6 +238,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       out[(size_t)b * T + tt] = qv;
     }
   }
+  }  // work items
 }
 
 // ------------------------------------------------------------------ per-sample loss + backward
@@ -660,6 +686,26 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
   }
 }
 
+// staged transitions (rows 0..E-1 of src, written by the acting stream) -> replay ring slots
+// (dst.filled + e) % dst.C, slot list into dst.slots; the learner's stream applies them before
+// its priority-tree write, so the acting step never touches a table the learner reads
+__global__ __launch_bounds__(256) void aql_apply_staged_k(AqlInsert src, AqlInsert dst, int E, int obs, int TA) {
+  const int lane = threadIdx.x & 63, e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= E) return;
+  const int64_t slot = (dst.filled[0] + e) % dst.C;
+  if (lane < obs) {
+    dst.st[slot * obs + lane] = src.st[(size_t)e * obs + lane];
+    dst.st2[slot * obs + lane] = src.st2[(size_t)e * obs + lane];
+  }
+  for (int k = lane; k < TA; k += 64) dst.amu[slot * TA + k] = src.amu[(size_t)e * TA + k];
+  if (lane == 0) {
+    dst.act[slot] = src.act[e];
+    dst.rew[slot] = src.rew[e];
+    dst.done[slot] = src.done[e];
+    dst.slots[e] = (int)slot;
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -685,6 +731,19 @@ void aql_learn_fwd(const AqlLearn& L, hipStream_t s) {
   if (L.B < 1) return;
   const int RT = (L.on.T + 15) / 16;
   aql_learn_fwd_k<<<dim3(L.B * RT, 2), 256, 0, s>>>(L);
+  LAUNCH_CHECK();
+}
+
+void aql_act_q(const AqlLearn& L, hipStream_t s) {
+  check_net(L.on);
+  if (!L.act_mode || !L.eff_on || !L.st || !L.amu || !L.q_s) throw std::invalid_argument("aql_act_q: acting config");
+  if (((reinterpret_cast<uintptr_t>(L.eff_on) | reinterpret_cast<uintptr_t>(L.on.ao_w2) |
+        reinterpret_cast<uintptr_t>(L.on.qf_w2)) & 15))
+    throw std::invalid_argument("aql_act_q: weights / workspace must be 16-byte aligned");
+  if (L.B < 1) return;
+  const int RT = (L.on.T + 15) / 16;
+  const int blocks = std::max(1, std::min(L.B * RT, L.act_blocks > 0 ? L.act_blocks : L.B * RT));
+  aql_learn_fwd_k<<<dim3(blocks, 1), 256, 0, s>>>(L);  // grid.y = 1: the online net only
   LAUNCH_CHECK();
 }
 
@@ -732,6 +791,16 @@ void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, con
   if (ins.C < e.E) throw std::invalid_argument("aql env: replay capacity < envs");
   if (e.E < 1) return;
   aql_env_step_k<<<(e.E + 3) / 4, 256, 0, s>>>(e, env_act, act_idx, amu, ins);
+  LAUNCH_CHECK();
+}
+
+void aql_apply_staged(const AqlInsert& src, const AqlInsert& dst, int E, int obs, int TA, hipStream_t s) {
+  if (E <= 0) return;
+  if (obs < 1 || obs > 64 || TA < 1) throw std::invalid_argument("aql_apply_staged: 1 <= obs <= 64, T * adim >= 1");
+  if (!src.st || !src.st2 || !src.amu || !src.act || !src.rew || !src.done || !dst.st || !dst.st2 || !dst.amu ||
+      !dst.act || !dst.rew || !dst.done || !dst.filled || !dst.slots || dst.C < E)
+    throw std::invalid_argument("aql_apply_staged: tables");
+  aql_apply_staged_k<<<(E + 3) / 4, 256, 0, s>>>(src, dst, E, obs, TA);
   LAUNCH_CHECK();
 }
 

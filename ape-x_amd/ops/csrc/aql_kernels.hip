@@ -230,6 +230,12 @@ void aql_candidate_q(const AQLNet& net, float* ws, const float* state, const flo
   LAUNCH_CHECK();
 }
 
+void aql_noisy_eff(const AQLNet& net, float* ws, hipStream_t s) {
+  const int n = (int)aql_workspace_floats();
+  aql_noisy_eff_k<<<(n + 255) / 256, 256, 0, s>>>(net, ws);
+  LAUNCH_CHECK();
+}
+
 void aql_propose(const AQLNet& net, const float* state, int B, const float* low, const float* high, const float* var,
                  uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s) {
   if (B <= 0) return;

@@ -110,6 +110,44 @@ __device__ __forceinline__ double uniform_double(uint64_t seed, uint64_t stream,
   return (double)(bits & ((1ull << 53) - 1)) * (1.0 / 9007199254740992.0);
 }
 
+// One wave draws stratified proportional sample i of B from a fanout-64 sum tree (TreeDesc of
+// kernels.h): mass (u_i + i) * total / B with u_i from Philox (seed, i, counter), descended with
+// a wave-wide inclusive scan of the 64 child sums per level; returns the leaf.  ``length``
+// live slots; ``exclude_last``: the newest slot's leaf is left out of the mass (reference Q5).
+// Shared by per_sample_k (replay_kernels.hip) and the AQL learner forward, which samples its
+// own row (aql_engine_kernels.hip).
+template <class TD>
+__device__ __forceinline__ int tree_sample_leaf(const TD& t, int i, int B, int length, int exclude_last,
+                                                uint64_t seed, uint64_t ctr, int lane) {
+  const int L = t.levels;
+  double total = t.node_sum[L - 1][0];
+  if (exclude_last && length > 0 && length <= t.size[0]) total -= (double)t.leaf_sum[length - 1];
+  const double u = uniform_double(seed, (uint64_t)i, ctr);
+  double mass = (u + (double)i) * total / (double)B;
+  int node = 0;
+  for (int level = L; level >= 1; --level) {
+    const int child = node * 64 + lane;
+    const int csize = t.size[level - 1];
+    double v = 0.0;
+    if (child < csize) v = (level == 1) ? (double)t.leaf_sum[child] : t.node_sum[level - 2][child];
+    if (exclude_last && level == 1 && child == length - 1) v = 0.0;
+    const double incl = wave_inclusive_scan(v, lane);
+    unsigned long long hit = __ballot(incl > mass);
+    int k;
+    if (hit) {
+      k = __ffsll((long long)hit) - 1;
+    } else {  // rounding at the top end: take the last child with mass
+      unsigned long long nz = __ballot(v > 0.0);
+      k = nz ? 63 - __clzll((long long)nz) : 0;
+    }
+    const double before = __shfl(incl - v, k, 64);
+    mass -= before;
+    if (mass < 0.0) mass = 0.0;
+    node = node * 64 + k;
+  }
+  return node;
+}
+
 // ---------------------------------------------------------------- bf16
 __device__ __forceinline__ uint16_t f2bf(float f) {
   return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)

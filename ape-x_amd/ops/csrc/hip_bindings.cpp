@@ -648,6 +648,39 @@ PYBIND11_MODULE(_apex_hip, m) {
     L.ent_lam = ent_lam;
     return L;
   });
+  m.def("make_aql_act", [](const AQLNet& on, uint64_t state, uint64_t amu, uint64_t eff, uint64_t q, int B,
+                           int blocks) {
+    AqlLearn L{};
+    L.on = on;
+    L.tg = on;
+    L.st = P<const float>(state);
+    L.st2 = L.st;
+    L.amu = P<const float>(amu);
+    L.eff_on = L.eff_tg = P<const float>(eff);
+    L.q_s = P<float>(q);
+    L.B = B;
+    L.act_mode = 1;
+    L.act_blocks = blocks;
+    return L;
+  });
+  m.def("aql_act_q", [](const AqlLearn& L, uint64_t s) { aql_act_q(L, S(s)); });
+  // the learner forward samples its own rows (replaces per_sample before aql_learn_fwd)
+  m.def("aql_learn_set_sample", [](const AqlLearn& L0, const TreeHandle& t, uint64_t filled, uint64_t beta,
+                                   uint64_t ctr, uint64_t seed, int exclude_last) {
+    AqlLearn L = L0;
+    L.fused_sample = 1;
+    L.tree = t.d;
+    L.filled = P<const int64_t>(filled);
+    L.beta = P<const float>(beta);
+    L.ctr = P<const int64_t>(ctr);
+    L.seed = seed;
+    L.exclude_last = exclude_last;
+    L.idx_out = const_cast<int*>(L.idx);
+    L.w_out = const_cast<float*>(L.w);
+    if (!L.filled || !L.beta || !L.ctr || !L.idx_out || !L.w_out) throw std::invalid_argument("aql_learn_set_sample");
+    return L;
+  });
+  m.def("aql_noisy_eff", [](const AQLNet& net, uint64_t ws, uint64_t s) { aql_noisy_eff(net, P<float>(ws), S(s)); });
   m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
   m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });
   m.def("aql_vec_layout", []() {
@@ -725,6 +758,9 @@ PYBIND11_MODULE(_apex_hip, m) {
     return i;
   });
   m.def("aql_env_reset", [](const AqlEnv& e, uint64_t s) { aql_env_reset(e, S(s)); });
+  m.def("aql_apply_staged", [](const AqlInsert& src, const AqlInsert& dst, int E, int obs, int TA, uint64_t s) {
+    aql_apply_staged(src, dst, E, obs, TA, S(s));
+  });
   m.def("aql_env_step", [](const AqlEnv& e, uint64_t env_act, uint64_t act_idx, uint64_t amu, const AqlInsert& ins,
                            uint64_t s) {
     aql_env_step(e, P<const float>(env_act), P<const int>(act_idx), P<const float>(amu), ins, S(s));

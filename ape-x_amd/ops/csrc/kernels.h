@@ -460,6 +460,7 @@ struct AQLNet {
   const float *df_w1, *df_b1, *df_w2, *df_b2;        // proposal.dist_feature: 128->128->na
 };
 size_t aql_workspace_floats();
+void aql_noisy_eff(const AQLNet& net, float* ws, hipStream_t s);  // W_eff = mu + sigma eps into ws
 void aql_candidate_q(const AQLNet& net, float* ws, const float* state, const float* a_mu, int B, float* q,
                      hipStream_t s);
 void aql_propose(const AQLNet& net, const float* state, int B, const float* low, const float* high, const float* var,
@@ -489,8 +490,23 @@ struct AqlLearn {
   float* vec;                                // [B][aqlv::STRIDE]
   float *delta, *lw, *lossp;                 // [B] |td|, w*Huber, per-sample proposal loss
   long long* dbg;                            // optional phase timestamps (block 0, s_memtime) or null
+  int act_mode;                              // 1: acting -- online Q(st[row], .) only, row = idx ? idx[b] : b
+  int act_blocks;                            // acting: workgroups (each loops over its items); 0 = one per item
+  // fused sampling (aql_learn_set_sample): every forward workgroup draws its sample's row from
+  // the PER tree itself (tree_sample_leaf, as per_sample_k) and the (tile 0, online) workgroup
+  // writes idx / IS weight for the backward -- no per_sample launch
+  int fused_sample, exclude_last;
+  TreeDesc tree;
+  const int64_t* filled;                     // live slots (min with the capacity)
+  const float* beta;
+  const int64_t* ctr;                        // Philox counter (the learner step)
+  uint64_t seed;
+  int* idx_out;
+  float* w_out;
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
+// acting on the learner's MFMA forward: q_s[b][t] = Q_on(st[b], amu[b][t]) for B states
+void aql_act_q(const AqlLearn& L, hipStream_t s);
 void aql_learn_bwd(const AqlLearn& L, hipStream_t s);
 struct AqlGradJob {
   int64_t off;         // flat offset of the parameter tensor
@@ -556,6 +572,8 @@ struct AqlInsert {
 void aql_env_reset(const AqlEnv& e, hipStream_t s);
 void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, const float* amu, const AqlInsert& ins,
                   hipStream_t s);
+// rows 0..E-1 of the staging tables ``src`` -> ring slots (dst.filled + e) % dst.C (slot list in dst.slots)
+void aql_apply_staged(const AqlInsert& src, const AqlInsert& dst, int E, int obs, int TA, hipStream_t s);
 
 // ---- central-replay experience transport over HIP IPC (ipc_kernels.hip, parallel/ipc.py)
 struct IpcIngest {

@@ -368,7 +368,7 @@ __global__ void split_planes_k(const float* __restrict__ src, uint16_t* __restri
 
 int g_px = 0;     // f32_set_variant(19, 0|1|2): off | 6 term products | 8 term products
 int g_px_xcd = 1;
-int g_px_pipe = 1;  // f32_set_variant(21, 0|1): pipeline form of the px / pxb bodies (see gemm_px1_k)
+int g_px_pipe = 0;  // f32_set_variant(21, 0|1): pipeline form of the px / pxb bodies (see gemm_px1_k; 1 measured slower)
 
 template <class P>
 void px_launch(const F32Set& set, hipStream_t s) {

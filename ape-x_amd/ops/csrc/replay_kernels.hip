@@ -286,32 +286,8 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
   const int length = (int)(len64 < (int64_t)t.size[0] ? len64 : (int64_t)t.size[0]);
   const float beta = beta_ptr ? beta_ptr[0] : beta_const;
   const int L = t.levels;
-  double total = t.node_sum[L - 1][0];
-  if (exclude_last && length > 0 && length <= t.size[0]) total -= (double)t.leaf_sum[length - 1];
   const uint64_t ctr = counter ? (uint64_t)counter[0] : 0ull;
-  const double u = uniform_double(seed, (uint64_t)i, ctr);
-  double mass = (u + (double)i) * total / (double)B;
-  int node = 0;
-  for (int level = L; level >= 1; --level) {
-    const int child = node * kTreeFanout + lane;
-    const int csize = t.size[level - 1];
-    double v = 0.0;
-    if (child < csize) v = (level == 1) ? (double)t.leaf_sum[child] : t.node_sum[level - 2][child];
-    if (exclude_last && level == 1 && child == length - 1) v = 0.0;
-    const double incl = wave_inclusive_scan(v, lane);
-    unsigned long long hit = __ballot(incl > mass);
-    int k;
-    if (hit) {
-      k = __ffsll((long long)hit) - 1;
-    } else {  // rounding at the top end: take the last child with mass
-      unsigned long long nz = __ballot(v > 0.0);
-      k = nz ? 63 - __clzll((long long)nz) : 0;
-    }
-    const double before = __shfl(incl - v, k, 64);
-    mass -= before;
-    if (mass < 0.0) mass = 0.0;
-    node = node * kTreeFanout + k;
-  }
+  const int node = tree_sample_leaf(t, i, B, length, exclude_last, seed, ctr, lane);
   float pmin = glob ? glob[0] : t.node_min[L - 1][0];
   float wscale = glob ? glob[1] : 1.f;
   if (sg.slots) {  // global min priority + k M_rank / sum M over the shards (world <= 64)

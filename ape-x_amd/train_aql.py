@@ -73,6 +73,9 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", default="cuda:0")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--overlap", action="store_true",
+                   help="acting on its own HIP stream beside the learner steps (the learner sees each acting "
+                        "step's transitions one iteration later; a checkpoint does not hold the staged half)")
     p.add_argument("--json-log", default=None, help="append one JSON record per log interval to this file")
     return p
 
@@ -84,7 +87,7 @@ def config_from_args(a) -> AQLEngineConfig:
                            action_var=a.action_var, alpha=a.prior_alpha, beta_start=a.prior_beta_start,
                            max_step=a.max_step, target_update_interval=a.target_update_interval,
                            target_update_steps=a.target_update_steps, track_losses=True,
-                           use_graphs=not a.no_graphs, seed=a.seed)
+                           use_graphs=not a.no_graphs, seed=a.seed, overlap=a.overlap)
 
 
 # ------------------------------------------------------------------ checkpoint

@@ -111,6 +111,8 @@ def parse():
                     help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
                          "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
+    ap.add_argument("--aql-overlap", action="store_true",
+                    help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=3000.0,
                     help="--gpus N>1 without torch.distributed.run: wall limit of the self-launched ranks")
     ap.add_argument("--watchdog", type=float, default=1500.0,
@@ -348,7 +350,7 @@ def aql(args, rank, world, device):
 
     cap = min(args.capacity, 1_000_000)
     cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed + rank,
-                          actor_offset=rank * args.envs, total_actors=world * args.envs)
+                          actor_offset=rank * args.envs, total_actors=world * args.envs, overlap=args.aql_overlap)
     eng = AQLEngine(cfg, device)
     t_fill = time.perf_counter()
     eng.fill(max(1024, 4 * args.envs))
@@ -390,6 +392,8 @@ def aql(args, rank, world, device):
                                 f"T={eng.T} candidates", "global_batch": cfg.batch_size * world, "seq_len": 1,
                        "parallelism": f"independent x{world}", "env": cfg.env_id, "envs_per_gpu": eng.E,
                        "sgd_steps_per_iteration": eng.K, "replay_capacity_per_gpu": cap,
+                       "acting": ("own HIP stream beside the learner (staged transitions)" if eng.overlap
+                                  else "serial before the learner steps") + f", Q on {cfg.act_q}",
                        "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
             "actor_env_steps_per_sec": round(env_steps, 1),
             "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),

@@ -214,3 +214,77 @@ def test_engine_iterations_graph_replay(cuda):
     assert len(eps) > 0 and all(1 <= ln <= 200 for _, ln in eps)
     # actors hold the published online weights
     assert torch.equal(eng.actor_flat, eng.learner.flat)
+
+
+@pytest.mark.parametrize("env_id", ["BipedalWalker-v3", "CartPole-v0"])
+def test_acting_q_mfma_matches_fp64(cuda, env_id):
+    """Acting Q on the learner's MFMA candidate forward (aql_act_q, the engine default) and the
+    one-wave-per-item kernel (aql_candidate_q) against the fp64 reference Q_Network over the
+    engine's own candidate sets."""
+    eng = _engine(cuda, env_id, fill=256)
+    h, s = eng.hip, torch.cuda.current_stream().cuda_stream
+    E, T = eng.E, eng.T
+    h.aql_propose(eng.actor_net, eng.obs_buf.data_ptr(), E, eng.low.data_ptr(), eng.high.data_ptr(),
+                  eng.var.data_ptr(), 77, eng.actor_ctr.data_ptr(), eng.amu.data_ptr(), 0, s)
+    h.aql_noisy_eff(eng.actor_net, eng.ws.data_ptr(), s)
+    h.aql_act_q(eng.actL, s)
+    torch.cuda.synchronize()
+    q_mfma = eng.qbuf.clone()
+    h.aql_candidate_q(eng.actor_net, eng.ws.data_ptr(), eng.obs_buf.data_ptr(), eng.amu.data_ptr(), E,
+                      eng.qbuf.data_ptr(), s)
+    torch.cuda.synchronize()
+    q_scalar = eng.qbuf.clone()
+    ref = copy.deepcopy(eng.actor_model).double()
+    with torch.no_grad():  # Q_Network.candidate_q in fp64 (its discrete branch casts to fp32)
+        qn = ref.q
+        a_out = qn.action_out(eng.amu.double().reshape(E * T, eng.adim)).reshape(E, T, qn.A_OUT)
+        q_f = qn.q_feature(eng.obs_buf.double()).repeat(1, T).reshape(E, T, qn.F_OUT)
+        q64 = qn.forward(torch.relu(torch.cat([a_out, q_f], dim=2))).reshape(E, T)
+    for q in (q_mfma, q_scalar):
+        err = float((q.double() - q64).abs().max() / q64.abs().max().clamp_min(1e-30))
+        assert err < 1e-5, err
+
+
+def test_overlapped_acting_graphs_equal_eager(cuda):
+    """Overlap mode (acting on its own stream, transitions staged and applied by the learner's
+    graph): captured graphs == the same schedule run eagerly on one stream, bit for bit, and
+    the ring advances E transitions per iteration."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    def run(graphs: bool):
+        cfg = AQLEngineConfig(env_id="CartPole-v0", n_envs=128, capacity=16384, batch_size=32, overlap=True, seed=5)
+        eng = AQLEngine(cfg, cuda)
+        eng.fill(1024)
+        if graphs:
+            eng.capture()
+        f0 = int(eng.replay.filled.item())
+        for _ in range(12):
+            eng.iteration()
+        torch.cuda.synchronize()
+        assert int(eng.replay.filled.item()) == f0 + 12 * cfg.n_envs
+        assert eng.learner.stats()["steps"] == 12 * eng.K
+        return eng.learner.flat.clone(), eng.replay.leaf_sum.clone(), eng.obs_buf.clone()
+
+    a, b = run(False), run(True)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_fused_sampling_equals_per_sample(cuda):
+    """The learner forward's own PER draw (fused_sample) == per_sample + forward: same rows,
+    IS weights and parameters after several iterations, bit for bit."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    out = []
+    for fused in (False, True):
+        cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
+                              fused_sample=fused)
+        eng = AQLEngine(cfg, cuda)
+        assert (eng.learner.Ls is not None) == fused
+        eng.fill(1024)
+        for _ in range(5):
+            eng.iteration()
+        torch.cuda.synchronize()
+        out.append((eng.learner.idx.clone(), eng.learner.w.clone(), eng.learner.flat.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
