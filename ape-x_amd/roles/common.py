@@ -146,8 +146,13 @@ class Heartbeat:
                 return
             self._stop.wait(self.interval)
 
-    def stop(self):
+    def stop(self, join_timeout: float = 10.0):
+        """Stop and JOIN the beat thread: a daemon thread still inside a TCPStore call when the
+        interpreter exits (the store's server -- the learner -- may already be gone) aborts the
+        process ('terminate called without an active exception')."""
         self._stop.set()
+        if self._t.is_alive() and threading.current_thread() is not self._t:
+            self._t.join(join_timeout)
 
 
 def dead_ranks(ranks, timeout: float = 10.0, st=None) -> list[int]:

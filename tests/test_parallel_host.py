@@ -346,5 +346,6 @@ def test_central_links_async_drop_dead_actor(world):
         vs = out[r]["versions"]
         assert vs and all(a[0] < b[0] for a, b in zip(vs, vs[1:]))
         assert all(v <= out[0]["version"] for v, _ in vs)
+    idle = out[0]["idle_poll_us"]  # None when every poll of the run found a packet waiting
     print(f"\nworld {world}: rank-0 link layer {out[0]['links_us_per_iter']:.1f} us/iteration "
-          f"(idle poll of {world - 1} links: {out[0]['idle_poll_us']:.1f} us median)")
+          f"(idle poll of {world - 1} links: {'n/a' if idle is None else f'{idle:.1f} us'} median)")
