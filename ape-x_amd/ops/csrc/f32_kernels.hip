@@ -1707,6 +1707,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 19 && v >= 0 && v <= 2) px_set(v);  // pre-split exact forward GEMMs (px_kernels.hip)
   else if (layer == 20 && v >= 0 && v <= 1) pxb_set(v);  // pre-split exact backward GEMMs (pxb_kernels.hip)
   else if (layer == 21 && v >= 0 && v <= 1) px_set_pipe(v);  // px / pxb pipeline form
+  else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 

@@ -397,6 +397,7 @@ void px_set(int v);
 int px_terms();  // 6 or 8 term products (knob 19 = 1 | 2)
 int px_pipe();   // knob 21: 0 = two LDS stages + 1 register prefetch, 1 = one LDS stage + 2-deep register ring
 void px_set_pipe(int v);
+void px_set_bk(int v);   // knob 22: px forward k-block depth 32 | 64
 void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
 void px_fc1_fwd_multi(const F32Set& set, hipStream_t s);
 // pre-split exact BACKWARD GEMMs (pxb_kernels.hip, f32_set_variant(20, 1) with knob 19 on):

@@ -238,7 +238,9 @@ __global__ __launch_bounds__(256, 3) void gemm_px1_k(F32Set args, int remap) {
 template <int BM_, int BN_, int BK_, int WM_>
 struct Conv2FwdX {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
-  static_assert(32 % BK == 0 && BN <= 64, "a k-block lies inside one tap");
+  // a k-block lies inside one tap, or (BK = 64) covers taps (ky, 2j) and (ky, 2j + 1): adjacent
+  // pixels, so one k-block row is 64 contiguous channels -- a full 128-byte line per plane
+  static_assert((32 % BK == 0 || BK == 64) && BN <= 64, "k-block within one tap or one even tap pair");
   static constexpr int NT = 64 / BN;
   struct Ctx {
     F32Prob p;
@@ -368,6 +370,7 @@ __global__ void split_planes_k(const float* __restrict__ src, uint16_t* __restri
 
 int g_px = 0;     // f32_set_variant(19, 0|1|2): off | 6 term products | 8 term products
 int g_px_xcd = 1;
+int g_px_bk = 32;   // f32_set_variant(22, 32|64): k-block depth (64: 128-byte plane rows = full lines)
 int g_px_pipe = 0;  // f32_set_variant(21, 0|1): pipeline form of the px / pxb bodies (see gemm_px1_k; 1 measured slower)
 
 template <class P>
@@ -405,10 +408,18 @@ int px_pipe() { return g_px_pipe; }
 
 void px_set_pipe(int v) { g_px_pipe = v; }
 
+void px_set_bk(int v) { g_px_bk = v; }
+
 void px_set(int v) { g_px = v; }
 
 void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_px(set);
+  if (g_px_bk == 64) {
+    if (layer == 2) px_launch<Conv2FwdX<64, 64, 64, 2>>(set, s);
+    else if (layer == 3) px_launch<Conv3FwdX<64, 64, 64, 2>>(set, s);
+    else throw std::invalid_argument("px_conv_fwd_multi: layer 2 or 3");
+    return;
+  }
   if (layer == 2) px_launch<Conv2FwdX<64, 64, 32, 2>>(set, s);
   else if (layer == 3) px_launch<Conv3FwdX<64, 64, 32, 2>>(set, s);
   else throw std::invalid_argument("px_conv_fwd_multi: layer 2 or 3");
@@ -416,7 +427,8 @@ void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
 
 void px_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_px(set);
-  px_launch<Fc1FwdX<64, 64, 32, 2>>(set, s);
+  if (g_px_bk == 64) px_launch<Fc1FwdX<64, 64, 64, 2>>(set, s);
+  else px_launch<Fc1FwdX<64, 64, 32, 2>>(set, s);
 }
 
 void f32_split_planes(const float* src, uint16_t* dst, int64_t n, int64_t plane, hipStream_t s) {
