@@ -181,6 +181,9 @@ class AQLEngineConfig:
     # about what the hidden acting step saves, so serial stays the default
     overlap: bool = False
     fused_sample: bool = os.environ.get("APEX_AQL_FUSED_SAMPLE", "1") == "1"  # PER draw inside aql_learn_fwd
+    # priority write as an extra workgroup of the noise-reset launch: measured 12936-12958 vs 13117
+    # SGD steps/s (the one-workgroup tree write, ~15 us in a 256-thread block, then bounds that launch)
+    fused_tree: bool = os.environ.get("APEX_AQL_FUSED_TREE", "0") == "1"
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
     act_blocks: int = int(os.environ.get("APEX_AQL_ACT_BLOCKS", "0"))
@@ -285,6 +288,14 @@ class AQLLearner:
         self.post = h.make_aql_post(layers, self.flat[self.P_q:].data_ptr(), self.tflat[self.P_q:].data_ptr(),
                                     self.P_p, self.step_ctr.data_ptr(), self.ticket.data_ptr(),
                                     (cfg.seed * 0x9E3779B1 + 0x5EED) & 0xFFFFFFFFFFFF)
+        # the priority write (0.9 max + 0.1 |td| + 1e-6, loss mean) as one extra workgroup of the
+        # noise-reset launch: it only feeds the NEXT step's sampling, and the gradient contraction,
+        # the optimizers and the noise reset read none of the tree
+        r = replay
+        self.post_tree = (h.aql_post_set_tree(self.post, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
+                                              self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
+                                              r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
+                          if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
         self.refresh()
 
     def refresh(self) -> None:
@@ -363,7 +374,9 @@ class AQLLearner:
                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
                               r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), ts)
 
-        if self.cfg.fork_tree:
+        if self.post_tree is not None:
+            pass  # folded into the noise-reset launch below (aql_post_set_tree)
+        elif self.cfg.fork_tree:
             self.tree_stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.tree_stream):
                 tree_write(self._s())
@@ -379,7 +392,7 @@ class AQLLearner:
                       self.v.data_ptr() + o, self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk,
                       self.norms_p.data_ptr()),
                      self.hp, self.step_ctr.data_ptr(), s)
-        h.aql_post(self.post, 1, s)
+        h.aql_post(self.post if self.post_tree is None else self.post_tree, 1, s)
         if self.cfg.track_losses:  # device-side running sums; read (one sync) only when logging
             self.loss_acc[0:1].add_(self.loss_q)
             self.loss_acc[1:2].add_(self.loss_p)

@@ -41,6 +41,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "tree_dev.h"
 
 namespace apex {
 namespace {
@@ -500,8 +501,8 @@ __device__ __forceinline__ float scaled_noise(uint64_t seed, int layer, int kind
   return copysignf(sqrtf(fabsf(x)), x);  // f(x) = sign(x) sqrt(|x|) (model.py:160-163)
 }
 
-__global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
-  const uint64_t st = (uint64_t)P.step[0];
+// noise reset / effective weights / proposal copy for the elements of this block
+__device__ __forceinline__ void aql_post_block(const AqlPost& P, int regen, uint64_t st) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 #pragma unroll
   for (int l = 0; l < 4; ++l) {
@@ -528,6 +529,18 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
   }
   if (!regen) return;
   if (i >= 0 && i < P.n_copy) P.dst[i] = P.src[i];
+}
+
+__global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
+  const uint64_t st = (uint64_t)P.step[0];
+  if (regen && P.tree_write && blockIdx.x == gridDim.x - 1) {  // block-uniform: the fused tree write
+    __shared__ float red[16];
+    __shared__ int sids[64];
+    batch_leaves_block(P.tree, P.bw, 1, red, sids);
+  } else {
+    aql_post_block(P, regen, st);
+  }
+  if (!regen) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -772,7 +785,10 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
 void aql_post(const AqlPost& p, int regen, hipStream_t s) {
   int64_t n = regen ? p.n_copy : 0;
   for (int l = 0; l < 4; ++l) n += (int64_t)p.layer[l].out * p.layer[l].in + p.layer[l].out;
-  aql_post_k<<<(int)((n + 255) / 256), 256, 0, s>>>(p, regen);
+  const int extra = (regen && p.tree_write) ? 1 : 0;  // the fused tree-write workgroup
+  if (extra && (p.bw.B > 64 || p.bw.E != 0 || !p.bw.idx))
+    throw std::invalid_argument("aql_post: the fused tree write takes <= 64 learner rows and no actor rows");
+  aql_post_k<<<(int)((n + 255) / 256) + extra, 256, 0, s>>>(p, regen);
   LAUNCH_CHECK();
 }
 

@@ -544,6 +544,12 @@ struct AqlPost {
   int64_t* step;       // learner step counter (+1 by the last block)
   int* ticket;
   uint64_t seed;
+  // fused priority write (aql_post_set_tree): one extra workgroup of the regen launch runs
+  // this step's batched tree write (per_write_batch's leaves + all levels, B <= 64) beside
+  // the noise reset -- neither reads what the other writes; the next step's sampling follows
+  int tree_write;
+  TreeDesc tree;
+  BatchWrite bw;
 };
 // regen = 1: fresh factorised noise for all four layers (reset_noise), effective weights,
 // proposal copy, step + 1.  regen = 0: effective weights from the current noise only

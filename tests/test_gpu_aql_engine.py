@@ -271,20 +271,25 @@ def test_overlapped_acting_graphs_equal_eager(cuda):
 
 
 def test_fused_sampling_equals_per_sample(cuda):
-    """The learner forward's own PER draw (fused_sample) == per_sample + forward: same rows,
-    IS weights and parameters after several iterations, bit for bit."""
+    """The learner forward's own PER draw (fused_sample) == per_sample + forward, and the
+    priority write folded into the noise-reset launch (fused_tree) == its own launch: same
+    rows, IS weights, tree, loss and parameters after several iterations, bit for bit."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    for fused in (False, True):
+    for fused_sample, fused_tree in ((False, False), (True, False), (True, True)):
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
-                              fused_sample=fused)
+                              fused_sample=fused_sample, fused_tree=fused_tree)
         eng = AQLEngine(cfg, cuda)
-        assert (eng.learner.Ls is not None) == fused
+        assert (eng.learner.Ls is not None) == fused_sample
+        assert (eng.learner.post_tree is not None) == fused_tree
         eng.fill(1024)
         for _ in range(5):
             eng.iteration()
         torch.cuda.synchronize()
-        out.append((eng.learner.idx.clone(), eng.learner.w.clone(), eng.learner.flat.clone()))
-    for x, y in zip(*out):
-        assert torch.equal(x, y)
+        L, r = eng.learner, eng.replay
+        out.append((L.idx.clone(), L.w.clone(), L.flat.clone(), L.loss_q.clone(), r.leaf_sum.clone(),
+                    r.node_sum[-1].clone(), r.max_prio.clone()))
+    for other in out[1:]:
+        for x, y in zip(out[0], other):
+            assert torch.equal(x, y)
