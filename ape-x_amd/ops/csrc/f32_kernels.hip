@@ -554,6 +554,103 @@ __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2
     gemm_body<P2, PF>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
+// ------------------------------------------------------------------ LDS-DMA ring body (knob 23)
+// The register-staged body keeps ONE k-block in flight per workgroup (global -> registers ->
+// ds_write), and every body measured moves its k-blocks at ~5 TB/s chip-wide: one k-block per
+// ~2 us of loaded-memory latency (profiles/r3_px_findings.md).  Here the operands go straight
+// from global memory into LDS with global_load_lds_dwordx4 (LDS-DMA: no registers, no ds_write)
+// into an S-stage ring, so S - 1 k-blocks are in flight while one is computed; a counted
+// s_waitcnt vmcnt + raw s_barrier retires exactly the stage about to be read (a __syncthreads
+// would drain every DMA, vmcnt(0)).  K-major A and B only (the forward GEMMs): BK = 32 fp32 =
+// 128-byte rows, each wave-instruction fills 8 rows x 128 B (lane-linear destination), the
+// 16-byte chunk a lane fetches is XOR-swizzled on the SOURCE side (chunk c of row r lands in
+// slot c ^ ((r >> 1) & 7)) so the ds_read_b128 fragment reads are bank-conflict-free.  Rows past
+// the tile's end read a zero page.  The MFMA chain runs in the register body's k order, so the
+// results are bit-identical to it.
+__device__ __attribute__((aligned(16))) float g_zero_page[64];
+
+// all but the newest S - 2 stages (4 DMAs each) landed, and this wave's LDS reads of the stage
+// the next DMA overwrites are complete (the compiler hoists the next iteration's raw barrier
+// above the last fragment reads' lgkmcnt wait)
+template <int S>
+__device__ __forceinline__ void wait_stage_dma() {
+  if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+}
+
+template <class P, int S>
+__device__ __forceinline__ void gemm_body_g(const typename P::Args& args, int block, float* lds) {
+  static_assert(P::A_KMAJ && P::B_KMAJ && P::BK == 32 && P::BM == 64 && P::BN == 64 && P::WM == 2,
+                "LDS-DMA body: K-major 64 x 64 x 32 tiles, 2 x 2 waves");
+  static_assert(S >= 2 && S <= 4, "2..4 stages");
+  constexpr int ST = 2 * 64 * 32;  // floats per stage: A then B, [64 rows][32] each, swizzled
+  typename P::Ctx ctx;
+  typename P::Smem sm;
+  P::decode(args, block, ctx, sm);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave & 1, wn = wave >> 1, r = lane & 31, h = lane >> 5;
+  // this lane's DMA rows: (2 wave + i) * 8 + lane / 8, i = 0, 1; the slot it fills is lane & 7,
+  // the chunk it fetches is slot ^ swizzle(row)
+  typename P::RowA ra[2];
+  typename P::RowB rb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (2 * wave + i) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    ra[i] = P::row_a(args, ctx, row, ch);
+    rb[i] = P::row_b(args, ctx, row, ch);
+  }
+  auto issue = [&](int kb, int slot) {
+    float* st = lds + slot * ST;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float* ga = P::ptr_a_row(args, ctx, ra[i], kb);
+      const float* gb = P::ptr_b_row(args, ctx, rb[i], kb);
+      __builtin_amdgcn_global_load_lds(ga ? ga : g_zero_page,
+                                       (__attribute__((address_space(3))) void*)(st + (2 * wave + i) * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gb ? gb : g_zero_page,
+                                       (__attribute__((address_space(3))) void*)(st + 64 * 32 + (2 * wave + i) * 256),
+                                       16, 0, 0);
+    }
+  };
+  f32x16 acc = {};
+  const int kb0 = ctx.kb0, kb1 = ctx.kb1;
+  // prologue: stages kb0 .. kb0 + S - 2 (clamped: a redundant refetch of the last k-block
+  // keeps the DMA count per iteration constant, so the vmcnt immediates stay exact)
+#pragma unroll
+  for (int j = 0; j < S - 1; ++j) issue(min(kb0 + j, kb1 - 1), j);
+  const int ar = wm * 32 + r, br = wn * 32 + r, sa = (ar >> 1) & 7, sb = (br >> 1) & 7;
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int it = kb - kb0;
+    wait_stage_dma<S>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of stage it landed; stage it - 1 is free
+    issue(min(kb + S - 1, kb1 - 1), (it + S - 1) % S);
+    const float* As = lds + (it % S) * ST;
+    const float* Bs = As + 64 * 32;
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const int c = 2 * kc + h;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(As + ar * 32 + 4 * (c ^ sa));
+      const f32x4 b = *reinterpret_cast<const f32x4*>(Bs + br * 32 + 4 * (c ^ sb));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[i], acc, 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing refetches land before exit
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+    P::store(args, ctx, wm * 32 + row, wn * 32 + r, acc[e]);
+  }
+}
+
+template <class P, int S>
+__global__ __launch_bounds__(256) void gemm_g_k(typename P::Args args, int remap) {
+  __shared__ __attribute__((aligned(16))) float lds[S * 2 * 64 * 32];
+  gemm_body_g<P, S>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds);
+}
+
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
   return i == 0 ? s.p[0] : (i == 1 ? s.p[1] : s.p[2]);
 }
@@ -658,8 +755,13 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
     const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;  // wave-uniform
     return r.p ? ld4(r.p + (ky * 20 + kx) * 32 + (k0 & 31)) : zero4();
   }
+  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;
+    return r.p ? r.p + (ky * 20 + kx) * 32 + (k0 & 31) : nullptr;
+  }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 512 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -718,8 +820,13 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
     const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
     return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (k0 & 63)) : zero4();
   }
+  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;
+    return r.p ? r.p + (ky * 9 + kx) * 64 + (k0 & 63) : nullptr;
+  }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 576 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -765,6 +872,28 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
     const int b = c.m0 + ml;
     if (b < c.B) c.p.out[((size_t)c.split * c.B + b) * 256 + c.n0 + nl] = v;
   }
+  // row states for the LDS-DMA body (gemm_g_k)
+  struct RowA {
+    const float* p;
+  };
+  struct RowB {
+    const float* p;
+  };
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    const int b = c.m0 + row;
+    return {b < c.B ? static_cast<const float*>(c.p.in) + (size_t)b * 3136 + 4 * ch : nullptr};
+  }
+  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    return r.p ? ld4(r.p + kb * BK) : zero4();
+  }
+  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+    return r.p ? r.p + kb * BK : nullptr;
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int nl, int ch) {
+    return {c.p.w + (size_t)(c.n0 + nl) * 3136 + 4 * ch};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
 };
 
 // conv1 forward, sample-resident: one workgroup per (problem, sample).  The sample's four
@@ -1675,9 +1804,23 @@ void check_set(const F32Set& set) {
 // 2 = exact-split bf16 MFMA (f32_conv1_fwd_x3_k)
 int g_conv1_variant = 2;
 
+// forward GEMMs on the LDS-DMA ring body (f32_set_variant(23, S)): 0 = off (register-staged
+// gemm_k), S = 2..4 ring stages; 64 x 64 K-major tiles only (the learner's 3-problem launches)
+int g_fwd_dma = 0;
+
 template <class P>
 void fwd_launch(const F32Set& set, hipStream_t s) {
-  launch1<P>(set, set.n * P::tiles(set.B), s);
+  const int blocks = set.n * P::tiles(set.B);
+  if constexpr (P::BM == 64 && P::BN == 64 && P::BK == 32 && P::WM == 2) {
+    if (g_fwd_dma >= 2 && blocks > 0) {
+      if (g_fwd_dma == 2) gemm_g_k<P, 2><<<blocks, 256, 0, s>>>(set, g_xcd);
+      else if (g_fwd_dma == 3) gemm_g_k<P, 3><<<blocks, 256, 0, s>>>(set, g_xcd);
+      else gemm_g_k<P, 4><<<blocks, 256, 0, s>>>(set, g_xcd);
+      LAUNCH_CHECK();
+      return;
+    }
+  }
+  launch1<P>(set, blocks, s);
 }
 
 // backward benchmark knobs: g_bwd_mode (0 both GEMMs of a conv backward launch, 1 weight
@@ -1708,6 +1851,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 20 && v >= 0 && v <= 1) pxb_set(v);  // pre-split exact backward GEMMs (pxb_kernels.hip)
   else if (layer == 21 && v >= 0 && v <= 1) px_set_pipe(v);  // px / pxb pipeline form
   else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
+  else if (layer == 23 && (v == 0 || (v >= 2 && v <= 4))) g_fwd_dma = v;  // LDS-DMA ring forward GEMMs
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
