@@ -89,5 +89,8 @@ def run_ranks(cmd: list[str], world: int, timeout: float = 3600.0, poll: float =
     finally:
         _stop(procs, grace)
         for s, h in old.items():
-            signal.signal(s, h)
+            # a handler installed outside Python (e.g. a profiler's preloaded library) reads
+            # back as None and cannot be re-installed from here: leave ours in place then
+            if h is not None:
+                signal.signal(s, h)
     return code if code != 0 else 1
