@@ -1842,7 +1842,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
   else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
   else if (layer == 13 && v >= 0 && v <= 3) g_fc1_tile = v;
-  else if (layer == 14 && v >= 0 && v <= 2) g_conv_tile = v;
+  else if (layer == 14 && v >= 0 && v <= 3) g_conv_tile = v;  // 3: 128 x 64 (2 x 2 waves of 64 x 32) learner tiles
   else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
   else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
   else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
@@ -1878,13 +1878,15 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
     case 2:
       if (px_ready(set)) px_conv_fwd_multi(2, set, s);
       else if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 3 && set.n == 3) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && set.n == 3)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
       if (px_ready(set)) px_conv_fwd_multi(3, set, s);
       else if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile == 2 && set.n == 3)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 3 && set.n == 3) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && set.n == 3)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
