@@ -23,6 +23,7 @@ phase graphs so the FC1/head gradient all-reduce overlaps the conv backward
 from __future__ import annotations
 
 import copy
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -35,6 +36,10 @@ from ..models.fused import make_hip_net, make_workspace
 from .actor_shard import ActorShard
 from .hbm_replay import HBMReplay
 from .learner import DQNLearner, LearnerConfig, forward_q
+
+# diagnostic only (scripts/ab/actor_share.sh): capture the step without the actor's kernels, to
+# price how much the concurrent actor slows the learner chain; never a valid bench config
+_DIAG_NO_ACTOR = os.environ.get("APEX_DIAG_NO_ACTOR") == "1"
 
 
 @dataclass
@@ -153,6 +158,9 @@ class ApexEngine:
 
             self._sharded = ShardedSampling(self.replay, force=force_collectives, comm=allreduce)
         self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce, sharded=self._sharded)
+        # sampled-ahead batches: their target passes ride the actor's graph (its queue is busy
+        # ~1/3 of a step) when actor and learner overlap
+        self.learner.target_in_actor = self.overlap and self.learner.ahead is not None and lc.target_pass == "actor"
         self.actor_model = copy.deepcopy(self.learner.model)
         self.actor_model._flat = None
         self.actor_flat = self.actor_model.flatten_parameters()
@@ -168,6 +176,7 @@ class ApexEngine:
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
+        self._diag_skip_actor = False
         self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = self._g_step = None
         self._pool = None
         self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
@@ -202,10 +211,15 @@ class ApexEngine:
                 q = forward_q(self.actor_model, obs, self.cfg.learner.dtype == "bf16")
         self.actor.act_and_step(q, stage)
 
-    def _actor_half(self, half: int):
+    def _actor_half(self, half: int, train: bool = False):
+        """Actor steps into staging half ``half``; ``train`` (a train step, not a fill): then
+        the target pass of the learner's next batch (LearnerConfig.target_ahead)."""
         k = self.cfg.actor_steps_per_learner_step
-        for i in range(k):
-            self._actor_body(half * k + i)
+        if not self._diag_skip_actor:
+            for i in range(k):
+                self._actor_body(half * k + i)
+        if train and self.learner.target_in_actor:
+            self.learner.target_pass_next()
 
     def _apply_half(self, half: int):
         k = self.cfg.actor_steps_per_learner_step
@@ -252,6 +266,7 @@ class ApexEngine:
         Single-process: ``a1`` is the whole step and ``a2``/``b`` are None."""
         with trace.range("apex.learner"):
             self._learn_phases(a1, a2, b, pipelined_mass)
+        self.learner.advance()
 
     def _learn_phases(self, a1, a2, b, pipelined_mass: bool) -> None:
         R = trace.range
@@ -318,12 +333,26 @@ class ApexEngine:
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
         self._g_actor = self._graph(self._actor_body, self._pool)
-        if self._dp:
-            self._g_learn_a = self._graph(self.learner.forward_phase, self._pool)
-            self._g_learn_a2 = self._graph(self.learner.backward_phase, self._pool)
-            self._g_learn_b = self._graph(self._learn_b, self._pool)
-        else:  # no host collective in between: one graph per step
-            self._g_learn_a = self._graph(lambda: (self.learner.forward_phase(), self._learn_b()), self._pool)
+        L = self.learner
+        c0 = L.cur
+        # sampled-ahead batches alternate between two buffers: one learner graph per buffer
+        # (indexed by learner.cur at replay); otherwise a single graph
+        ga, ga2, gb = [], [], []
+        b_per_buf = self._dp and L.ahead is not None and self._sharded is not None
+        for c in ((0, 1) if L.ahead is not None else (c0,)):
+            L.cur = c
+            if self._dp:
+                ga.append(self._graph(L.forward_phase, self._pool))
+                ga2.append(self._graph(L.backward_phase, self._pool))
+                if b_per_buf or not gb:  # sharded + sampled ahead: the optimizer graph draws a batch
+                    gb.append(self._graph(self._learn_b, self._pool))
+            else:  # no host collective in between: one graph per step
+                ga.append(self._graph(lambda: (L.forward_phase(), self._learn_b()), self._pool))
+        if L.ahead is not None:
+            L.set_cur(c0)
+        self._g_learn_a = ga if L.ahead is not None else ga[0]
+        self._g_learn_a2 = (ga2 if L.ahead is not None else ga2[0]) if self._dp else None
+        self._g_learn_b = (gb if len(gb) == 2 else gb[0]) if self._dp else None
         self._captured = True
         torch.cuda.synchronize(self.device)
 
@@ -341,6 +370,24 @@ class ApexEngine:
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
         apool = torch.cuda.graph_pool_handle()  # actor graphs run concurrently: never share memory
+        L = self.learner
+        c0, half0 = L.cur, self._half
+
+        def at_half(h: int, fn):
+            # the learner graph of staging half h runs when learner.cur = c0 ^ h ^ half0 (both
+            # flip once per step): capture it with that sampled-ahead buffer
+            def body():
+                L.cur = c0 ^ h ^ half0 if L.ahead is not None else c0
+                fn()
+            return body
+
+        try:
+            self._capture_overlap_graphs(apool, at_half)
+        finally:
+            if L.ahead is not None:
+                L.set_cur(c0)
+
+    def _capture_overlap_graphs(self, apool, at_half) -> None:
         self._g_actor, self._g_learn_a, self._g_learn_a2 = [], [], []
         self._g_dp = None
         if self._dp and self.cfg.dp_graph and self._mass_pending_ok():
@@ -349,8 +396,8 @@ class ApexEngine:
             try:
                 g_actor, g_dp = [], []
                 for h in (0, 1):
-                    g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
-                    g_dp.append(self._graph(lambda h=h: self._dp_step_body(1 - h), self._pool))
+                    g_actor.append(self._graph(at_half(h, lambda h=h: self._actor_half(h, True)), apool))
+                    g_dp.append(self._graph(at_half(h, lambda h=h: self._dp_step_body(1 - h)), self._pool))
                 self._g_actor, self._g_dp = g_actor, g_dp
                 self._captured = True
                 torch.cuda.synchronize(self.device)
@@ -364,19 +411,29 @@ class ApexEngine:
                 torch.cuda.synchronize(self.device)
                 apool = torch.cuda.graph_pool_handle()
         if self.cfg.step_graph and not self._dp:
-            self._g_step = [self._graph(lambda h=h: self._fused_step_body(h), self._pool) for h in (0, 1)]
+            self._g_step = [self._graph(at_half(h, lambda h=h: self._fused_step_body(h)), self._pool) for h in (0, 1)]
             self._captured = True
             torch.cuda.synchronize(self.device)
             self._ev_learn.record(torch.cuda.current_stream(self.device))
             return
+        # sharded + sampled ahead: the optimizer graph draws the batch after next (per half,
+        # captured right after its half's phases: they hand it the staged rows to scatter)
+        b_per_half = self._dp and self.learner.ahead is not None and self._sharded is not None
+        gb = []
         for h in (0, 1):
-            self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+            self._g_actor.append(self._graph(at_half(h, lambda h=h: self._actor_half(h, True)), apool))
             if self._dp:
-                self._g_learn_a.append(self._graph(lambda h=h: self._learn_a(1 - h), self._pool))
-                self._g_learn_a2.append(self._graph(self.learner.backward_phase, self._pool))
+                self._g_learn_a.append(self._graph(at_half(h, lambda h=h: self._learn_a(1 - h)), self._pool))
+                self._g_learn_a2.append(self._graph(at_half(h, self.learner.backward_phase), self._pool))
+                if b_per_half:
+                    gb.append(self._graph(at_half(h, self._learn_b), self._pool))
             else:
-                self._g_learn_a.append(self._graph(lambda h=h: (self._learn_a(1 - h), self._learn_b()), self._pool))
-        self._g_learn_b = self._graph(self._learn_b, self._pool) if self._dp else None
+                self._g_learn_a.append(self._graph(at_half(h, lambda h=h: (self._learn_a(1 - h), self._learn_b())),
+                                                   self._pool))
+        if b_per_half:
+            self._g_learn_b = gb
+        else:
+            self._g_learn_b = self._graph(self._learn_b, self._pool) if self._dp else None
         self._captured = True
         torch.cuda.synchronize(self.device)
         self._ev_learn.record(torch.cuda.current_stream(self.device))
@@ -399,7 +456,7 @@ class ApexEngine:
         self._learn_b()
         A.wait_event(start)
         with torch.cuda.stream(A):
-            self._actor_half(h)
+            self._actor_half(h, True)
         L.wait_stream(A)
         self._step_events = start
 
@@ -430,7 +487,7 @@ class ApexEngine:
     def _train_step_eager(self) -> None:
         """Overlap-mode semantics, run sequentially on the current stream."""
         h = self._half
-        self._actor_half(h)
+        self._actor_half(h, True)
         self._learner_eager(1 - h)
         self._half ^= 1
 
@@ -448,12 +505,13 @@ class ApexEngine:
         if self._g_step is not None:
             with trace.range("apex.step_graph"):
                 self._g_step[h].replay()
+            self.learner.advance()
             self.learn_steps += 1
             self.actor_steps += self.cfg.actor_steps_per_learner_step
             if self.learn_steps % self.cfg.publish_param_interval == 0:
                 self.publish_params()  # the graph joined its actor branch
             if self.learn_steps % self.cfg.target_update_interval == 0:
-                self.learner.sync_target()
+                self.learner.sync_target()  # (the step graph joined its actor branch)
             self._half ^= 1
             return
         with trace.range("actor.launch"):
@@ -467,9 +525,11 @@ class ApexEngine:
                 self._sharded.exchange()
             with trace.range("apex.learner"):
                 self._g_dp[h].replay()
+            self.learner.advance()
             self._mass_pending = self._sharded is not None  # the graph's conv all-reduce carried them
         elif self._dp:
-            self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, self._g_learn_b.replay, True)
+            gb = self._g_learn_b[h] if isinstance(self._g_learn_b, list) else self._g_learn_b
+            self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, gb.replay, True)
         else:
             self._learn(self._g_learn_a[h].replay, None, None, False)
         self.learn_steps += 1
@@ -478,6 +538,8 @@ class ApexEngine:
             self._ev_actor[h].block(L)  # the actor is not reading its weights
             self.publish_params()
         if self.learn_steps % self.cfg.target_update_interval == 0:
+            if self.learner.target_in_actor:
+                self._ev_actor[h].block(L)  # its target pass of the next batch is redone
             self.learner.sync_target()
         self._ev_learn.record(L)
         self._half ^= 1
@@ -492,12 +554,14 @@ class ApexEngine:
         self.actor_steps += 1
 
     def learner_step(self) -> None:
+        pick = lambda g: g[self.learner.cur] if isinstance(g, list) else g  # noqa: E731
         if self._g_learn_a is None:
             self._learner_eager()
         elif self._dp:
-            self._learn(self._g_learn_a.replay, self._g_learn_a2.replay, self._g_learn_b.replay, False)
+            self._learn(pick(self._g_learn_a).replay, pick(self._g_learn_a2).replay, pick(self._g_learn_b).replay,
+                        False)
         else:
-            self._learn(self._g_learn_a.replay, None, None, False)
+            self._learn(pick(self._g_learn_a).replay, None, None, False)
         self.learn_steps += 1
         if self.learn_steps % self.cfg.publish_param_interval == 0:
             self.publish_params()
@@ -521,9 +585,10 @@ class ApexEngine:
                     self._apply_half(self._half)
                 self._half ^= 1
                 self.actor_steps += k
-            return
-        for _ in range(steps):
-            self.actor_step()
+        else:
+            for _ in range(steps):
+                self.actor_step()
+        self._diag_skip_actor = _DIAG_NO_ACTOR
 
     def _make_streams(self, mode: str):
         """(actor stream, learner stream or None = the caller's stream), see
@@ -607,6 +672,8 @@ class ApexEngine:
         return self._train_step()
 
     def _train_step(self) -> None:
+        if not self.learner.primed:  # the first two sampled-ahead batches (eager)
+            self.learner.prime()
         if self.overlap:
             if self._captured:
                 self._train_step_overlap()

@@ -130,21 +130,38 @@ class HBMReplay:
 
     def sample_indices(self, B: int, out_idx: torch.Tensor, out_w: torch.Tensor, counter: torch.Tensor,
                        beta: float | torch.Tensor = 0.4, exclude_last: bool | None = None,
-                       glob: torch.Tensor | None = None, shard: tuple | None = None, rows: tuple | None = None) -> None:
+                       glob: torch.Tensor | None = None, shard: tuple | None = None, rows: tuple | None = None,
+                       out_rows: dict | None = None, seed: int | None = None) -> None:
         """``glob`` (sharded replay): f32 [2] device tensor = (global min priority, this
         shard's IS-weight scale), see :mod:`apex_amd.parallel.sharded`; or ``shard`` =
         (exchanged fp32 slots [world, 2] = (mass, min priority) per shard, world, rank):
         the sampler derives both in-kernel.  ``rows`` = (staged table ptr dict, slot [E],
-        prio [E]): an actor step's staged rows scattered into the tables by the same launch."""
+        prio [E]): an actor step's staged rows scattered into the tables by the same launch.
+        ``out_rows`` (:meth:`row_buffers`): a private copy of every sampled row (frame ids,
+        action, return, done) taken by the same launch -- the learner's sampled-ahead batch
+        stays valid when the actor overwrites its slots before the batch is used."""
         excl = (not self.exact_mass) if exclude_last is None else exclude_last
         beta_ptr = beta.data_ptr() if isinstance(beta, torch.Tensor) else 0
         beta_c = 0.0 if isinstance(beta, torch.Tensor) else float(beta)
-        self.hip.per_sample(self.tree, B, self.filled.data_ptr(), 0, beta_ptr, beta_c, self.seed, counter.data_ptr(),
+        sd = self.seed if seed is None else int(seed)
+        self.hip.per_sample(self.tree, B, self.filled.data_ptr(), 0, beta_ptr, beta_c, sd, counter.data_ptr(),
                             out_idx.data_ptr(), out_w.data_ptr(), int(excl), self._stream(),
                             0 if glob is None else glob.data_ptr(),
                             *((0, 0, 0) if shard is None else (shard[0].data_ptr(), int(shard[1]), int(shard[2]))),
                             *((None, None, 0, 0, 0) if rows is None else
-                              (rows[0], self.trans_ptrs(), rows[1].data_ptr(), rows[2].data_ptr(), rows[1].numel())))
+                              (rows[0], self.trans_ptrs(), rows[1].data_ptr(), rows[2].data_ptr(), rows[1].numel())),
+                            *((None, None) if out_rows is None else
+                              (self.trans_ptrs(), {k: t.data_ptr() for k, t in out_rows.items()})))
+
+    def row_buffers(self, B: int) -> dict:
+        """Private transition rows for ``B`` samples (``sample_indices(out_rows=)``), same
+        dtypes and layout as the replay tables."""
+        dev = self.device
+        return {"s_ids": torch.zeros(B, 4, dtype=torch.int32, device=dev),
+                "s2_ids": torch.zeros(B, 4, dtype=torch.int32, device=dev),
+                "action": torch.zeros(B, dtype=torch.int32, device=dev),
+                "reward": torch.zeros(B, dtype=torch.float32, device=dev),
+                "done": torch.zeros(B, dtype=torch.float32, device=dev)}
 
     def pack_shard_slots(self, slots: torch.Tensor, world: int, rank: int) -> None:
         """slots[:] = 0 except slot ``rank`` = (root mass, root min priority) (fp32)."""

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import copy
 from dataclasses import dataclass
+from types import SimpleNamespace
 
 import torch
 
@@ -54,6 +55,12 @@ class LearnerConfig:
     tree_write: str = "legacy"     # "legacy": single-workgroup walks on the tree fork (few CUs beside the
                                    # backward: 3315 vs 3195 steps/s) | "batch": HBMReplay.write_batch (wide
                                    # kernels; lower latency, better when the tree write is inline)
+    target_ahead: bool = False     # hip path: batches sampled two steps ahead (private row copies), their
+                                   # target pass Q_target(s') run beside the previous learner step (in the
+                                   # actor's graph when the engine overlaps them); see DQNLearner.sample_next
+    target_pass: str = "actor"     # target_ahead: where the next batch's target pass runs -- "actor" (the
+                                   # engine's actor graph, overlap mode) | "fork" (the tree branch, after the
+                                   # priority write, beside the backward) | "inline" (right after the draw)
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -168,6 +175,23 @@ class DQNLearner:
             # all-reduce the norm must be taken after it (grad_sumsq)
             self.fin_partials = torch.zeros(8192, dtype=torch.float64, device=dev)
             self.n_fin_partials = 0
+        # sampled-ahead batches (LearnerConfig.target_ahead): two buffers, ``cur`` holds the
+        # batch this step trains on (sampled one step earlier, its target pass done beside
+        # that step); the engine flips ``cur`` after every learner step (:meth:`advance`)
+        self.ahead = None
+        self.cur = 0
+        self._primed = False
+        if self.hip_net and cfg.target_ahead:
+            self.ahead = [SimpleNamespace(idx=torch.zeros(B, dtype=torch.int32, device=dev),
+                                          w=torch.zeros(B, dtype=torch.float32, device=dev),
+                                          rows=replay.row_buffers(B), ws_t=make_workspace(B, A, dev, cfg.dtype))
+                          for _ in range(2)]
+        # the engine runs target_pass_next() in its actor graph (overlap mode); otherwise the
+        # learner runs each target pass right after the draw
+        self.target_in_actor = False
+        self.target_on_fork = self.ahead is not None and cfg.target_pass == "fork" and cfg.tree_fork
+        self._src = None  # (s ids, s' ids, idx, transition table) of the batch in flight
+        self._pending_rows = None
         # one-shot callables run on the tree stream before this step's priority write
         # (the overlapped engine's deferred actor-row priorities)
         self.tree_hooks = []
@@ -215,7 +239,7 @@ class DQNLearner:
         too; data-parallel split: up to the FC1 backward and its finalize."""
         s = self._stream()
         glob = shard = None
-        if self.sharded is not None:  # gathered shard masses -> global pmin + shard weight scale
+        if self.sharded is not None and self.ahead is None:  # gathered shard masses -> global pmin + weight scale
             if self.sharded.in_kernel:
                 shard = self.sharded.sample_args()
             else:
@@ -225,21 +249,32 @@ class DQNLearner:
         for extra in rows[:-1]:  # more than one staged actor step per learner step
             self.hip.apply_staged_rows(extra[0], self.replay.trans_ptrs(), extra[1].data_ptr(), extra[2].data_ptr(),
                                        extra[1].numel(), s)
-        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
-                                   rows=rows[-1] if rows else None)
+        rp = self.replay
+        if self.ahead is not None:  # this step's batch was drawn two steps ago (sample_next)
+            cur = self.ahead[self.cur]
+            self.idx, self.w = cur.idx, cur.w
+            self._src = (cur.rows["s_ids"], cur.rows["s2_ids"], None, SimpleNamespace(**cur.rows))
+            self._pending_rows = rows[-1] if rows else None  # scattered by sample_next's launch
+            q2t = cur.ws_t.q
+        else:
+            self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
+                                       rows=rows[-1] if rows else None)
+            self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
-            # the loss reads (a, r, d) straight out of the transition table.
-            # The three passes share each layer's launch (5 kernels, not 15).
-            rp = self.replay
-            forward_multi([(self.net, rp.frames, self.ws_s, rp.s_ids, self.idx),
-                           (self.net, rp.frames, self.ws_s2, rp.s2_ids, self.idx),
-                           (self.tnet, rp.frames, self.ws_t, rp.s2_ids, self.idx)])
+            # the loss reads (a, r, d) straight out of the transition table (or the batch's
+            # private rows).  The passes share each layer's launch (5 kernels, not 15).
+            ids_s, ids_s2, jdx, tab = self._src
+            passes = [(self.net, rp.frames, self.ws_s, ids_s, jdx), (self.net, rp.frames, self.ws_s2, ids_s2, jdx)]
+            if self.ahead is None:
+                passes.append((self.tnet, rp.frames, self.ws_t, ids_s2, jdx))
+                q2t = self.ws_t.q
+            forward_multi(passes)
             m = self.model
             self.hip.dqn_heads_bwd(
-                {"q": self.ws_s.q.data_ptr(), "q2": self.ws_s2.q.data_ptr(), "q2t": self.ws_t.q.data_ptr(),
-                 "act": rp.action.data_ptr(), "rew": rp.reward.data_ptr(), "done": rp.done.data_ptr(),
-                 "idx": self.idx.data_ptr(), "w": self.w.data_ptr(), "h": self.ws_s.h.data_ptr(),
+                {"q": self.ws_s.q.data_ptr(), "q2": self.ws_s2.q.data_ptr(), "q2t": q2t.data_ptr(),
+                 "act": tab.action.data_ptr(), "rew": tab.reward.data_ptr(), "done": tab.done.data_ptr(),
+                 "idx": 0 if jdx is None else jdx.data_ptr(), "w": self.w.data_ptr(), "h": self.ws_s.h.data_ptr(),
                  "w_adv2": m.advantage[2].weight.data_ptr(), "w_val2": m.value[2].weight.data_ptr(),
                  "delta": self.delta.data_ptr(), "lw": self.lw.data_ptr(),
                  ("dz" if self.fp32 else "dz_bf"): (self.ws_s.dz if self.fp32 else self.ws_s.dz_bf).data_ptr(),
@@ -252,7 +287,7 @@ class DQNLearner:
                 self.net.fc_backward(self.ws_s, extra_jobs=[heads_job])
                 return
             after = self._fork_point()
-            n = self.net.trunk_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, extra_jobs=[heads_job],
+            n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
                                         sumsq=self.fin_partials if self.allreduce is None else None,
                                         after_first=after)
             if self.allreduce is None:
@@ -262,6 +297,7 @@ class DQNLearner:
                 self._join_pending = True  # joined after the optimizer (it reads nothing the branch writes)
             else:
                 self._tree_fork_end()
+                self.sample_next()
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
@@ -288,12 +324,91 @@ class DQNLearner:
         rp = self.replay
         tree = self._fork_point()
         after = tree if after_first is None else (after_first if tree is None else (lambda: (tree(), after_first())))
-        self.net.conv_backward(rp.frames, self.ws_s, rp.s_ids, self.idx, after_first=after)
+        ids_s, _, jdx, _ = self._src
+        self.net.conv_backward(rp.frames, self.ws_s, ids_s, jdx, after_first=after)
         self._tree_fork_end()
         if self.sharded is not None and self.grad_prefix:
             # the tree is final for the next sample: pack this shard's slot, which the
             # conv-gradient all-reduce then exchanges (the next step's shard masses)
             self.sharded.pack()
+        if self.sharded is None:
+            self.sample_next()  # (sharded: after the all-reduce brought the masses, in optimize)
+
+    # ------------------------------------------------------------------ sampled-ahead batches
+    def sample_next(self) -> None:
+        """Target pass off the critical chain (``LearnerConfig.target_ahead``).
+
+        Q_target(s') depends only on the sampled batch and the target weights (fixed between
+        syncs).  So at the end of step t -- right after its priority write joined -- the
+        learner draws batch t+2 into the buffer batch t just freed, and the target pass of
+        batch t+1 (drawn at the end of step t-1) runs beside step t: in the actor's graph
+        (``target_pass_next``, engine overlap mode; the actor queue is busy ~1/3 of a step),
+        else inline.  A batch misses the one priority update of the step between its draw and
+        its use, as the reference learner's prefetched batches do (the replay server answers
+        the next ``sample`` while the learner trains).  The sampling launch also scatters the
+        staged actor rows and copies every sampled row (frame ids, action, return, done) into
+        the buffer, so the actor overwriting a slot before the batch is used cannot mix two
+        transitions in one TD target; the frames outlive an overwritten slot by >= n + 7 actor
+        steps (the frame ring's margin, HBMReplay)."""
+        if self.ahead is None:
+            return
+        glob = shard = None
+        if self.sharded is not None:
+            if self.sharded.in_kernel:
+                shard = self.sharded.sample_args()
+            else:
+                self.sharded.finalize()
+                glob = self.sharded.glob
+        buf = self.ahead[self.cur]
+        self.replay.sample_indices(self.B, buf.idx, buf.w, self.step_counter, self.beta, glob=glob, shard=shard,
+                                   rows=self._pending_rows, out_rows=buf.rows)
+        self._pending_rows = None
+        if not self._deferred:
+            self._target_pass(buf)
+
+    @property
+    def _deferred(self) -> bool:
+        """The next batch's target pass runs during the following step (actor graph / fork)."""
+        return self.target_in_actor or self.target_on_fork
+
+    def target_pass_next(self) -> None:
+        """Q_target(s') of the next step's batch (drawn at the end of the previous step),
+        for the engine's actor graph: run it after that step and before the next one."""
+        self._target_pass(self.ahead[1 - self.cur])
+
+    def _target_pass(self, buf) -> None:
+        forward_multi([(self.tnet, self.replay.frames, buf.ws_t, buf.rows["s2_ids"], None)])
+
+    @property
+    def primed(self) -> bool:
+        return self.ahead is None or self._primed
+
+    def prime(self) -> None:
+        """The first two sampled-ahead batches (eager, before any capture), each drawn with
+        its own Philox stream, and the current one's target pass (the next one's too when
+        the learner runs them itself)."""
+        for k, c in ((1, self.cur), (2, 1 - self.cur)):
+            buf = self.ahead[c]
+            self.replay.sample_indices(self.B, buf.idx, buf.w, self.step_counter, self.beta, out_rows=buf.rows,
+                                       seed=self.replay.seed + k * 0x9E3779B9)
+        self._target_pass(self.ahead[self.cur])
+        if not self._deferred:
+            self._target_pass(self.ahead[1 - self.cur])
+        self._primed = True
+
+    def advance(self) -> None:
+        """One learner step done (eager or replayed): the sampled-ahead batch becomes current."""
+        if self.ahead is not None:
+            self.set_cur(self.cur ^ 1)
+
+    def set_cur(self, c: int) -> None:
+        """Host view of the buffer state: buffer ``c`` holds the next step's batch (a replayed
+        graph runs no Python, so the engine keeps this).  ``idx`` / ``w`` name the other
+        buffer: the last step's batch until its end, then the batch drawn for the step after
+        the next one."""
+        self.cur = c
+        other = self.ahead[1 - c]
+        self.idx, self.w = other.idx, other.w
 
     def _fork_point(self):
         """Fork the tree branch HERE (it depends on everything launched so far) but capture
@@ -329,11 +444,13 @@ class DQNLearner:
                     self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
                 self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
                                              mix=(self.delta, self.lw, self.prio, self.loss))
-                return
-            for extra in pre[:-1]:  # more than one staged actor step per learner step
-                self.replay.write_batch(pre=extra)
-            self.replay.write_batch(pre=pre[-1] if pre else None, idx=self.idx, bump=self.step_counter,
-                                    mix=(self.delta, self.lw, self.prio, self.loss))
+            else:
+                for extra in pre[:-1]:  # more than one staged actor step per learner step
+                    self.replay.write_batch(pre=extra)
+                self.replay.write_batch(pre=pre[-1] if pre else None, idx=self.idx, bump=self.step_counter,
+                                        mix=(self.delta, self.lw, self.prio, self.loss))
+            if self.target_on_fork:  # the next batch's target pass, beside the rest of the backward
+                self.target_pass_next()
 
     def _tree_fork_end(self) -> None:
         if self.cfg.tree_fork:
@@ -342,6 +459,8 @@ class DQNLearner:
     def optimize(self) -> None:
         s = self._stream()
         h = self.hip
+        if self.dp_split and self.sharded is not None:
+            self.sample_next()  # the all-reduce brought this step's shard masses
         if self.hip_net and self.n_fin_partials:
             parts, nparts = self.fin_partials, self.n_fin_partials  # from grad_finalize
         else:
@@ -365,9 +484,12 @@ class DQNLearner:
         if self._join_pending:
             self._join_pending = False
             self._tree_fork_end()
+            self.sample_next()
 
     def step(self) -> None:
         """One eager learner step (the engine runs the same phases as hipGraphs)."""
+        if not self.primed:
+            self.prime()
         if self.sharded is not None:
             self.sharded.exchange()
         self.forward_phase()
@@ -382,6 +504,7 @@ class DQNLearner:
         else:
             self.allreduce.wait(self.allreduce.start(self.flat_grad))
         self.optimize()
+        self.advance()
         self.host_steps += 1
 
     # ------------------------------------------------------------------ target / params
@@ -395,6 +518,14 @@ class DQNLearner:
         self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
         if self.hip_net:
             self.tnet.copy_packed_from(self.net)
+        if self.ahead is not None and self._primed:
+            # the sampled-ahead batches' target passes ran on the old weights: redo them, so
+            # every step after a sync sees the synced target (as without target_ahead).  With
+            # the pass in the actor graph the engine first waits for it; the batch after is
+            # then still to be drawn or to get its pass
+            self._target_pass(self.ahead[self.cur])
+            if not self._deferred:
+                self._target_pass(self.ahead[1 - self.cur])
 
     def copy_params_to(self, dst_flat: torch.Tensor) -> None:
         self.hip.copy_f32(dst_flat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())

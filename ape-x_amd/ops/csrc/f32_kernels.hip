@@ -1858,6 +1858,10 @@ void f32_set_variant(int layer, int v) {
 // Tiles (MI355X, 3 x 512-sample launches): 128 x 32 blocks, one 32x32 accumulator per wave,
 // beat 128 x 64 / 256-row blocks: 46-55 KB of LDS per workgroup gave 2-3 per CU, too few
 // waves to cover the operand-load latency.
+// the learner's launches (2-3 passes of its batch: >= 1024 rows) vs the actor's (one pass of
+// 256 envs) and the sampled-ahead target pass (one pass of 512)
+static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
+
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
   switch (layer) {
@@ -1878,15 +1882,15 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
     case 2:
       if (px_ready(set)) px_conv_fwd_multi(2, set, s);
       else if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 3 && set.n == 3) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && set.n == 3)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
       if (px_ready(set)) px_conv_fwd_multi(3, set, s);
       else if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 3 && set.n == 3) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && set.n == 3)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
+      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
@@ -1898,7 +1902,7 @@ int f32_fc1_splits() { return kFcSplits; }
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
   if (px_ready(set)) px_fc1_fwd_multi(set, s);
-  else if (g_fc1_tile == 1 || (g_fc1_tile == 3 && set.n == 3)) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
+  else if (g_fc1_tile == 1 || (g_fc1_tile == 3 && learner_sized(set))) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
   else if (g_fc1_tile == 2) fwd_launch<Fc1FwdT<128, 32, 32, 4>>(set, s);
   else fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
   return kFcSplits;

@@ -110,25 +110,27 @@ PYBIND11_MODULE(_apex_hip, m) {
                          float beta, uint64_t seed, uint64_t counter, uint64_t out_idx, uint64_t out_w,
                          int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank,
                          py::object rows_stage, py::object rows_dst, uint64_t rows_slot, uint64_t rows_prio,
-                         int rows_E) {
+                         int rows_E, py::object src, py::object out) {
+    auto tab = [](py::dict d) {
+      auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+      return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
+                        P<float>(g("done"))};
+    };
     StagedRows rows{};
-    if (rows_E > 0) {
-      auto tab = [](py::dict d) {
-        auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
-        return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
-                          P<float>(g("done"))};
-      };
+    if (rows_E > 0)
       rows = StagedRows{tab(rows_stage.cast<py::dict>()), tab(rows_dst.cast<py::dict>()), P<const int>(rows_slot),
                         P<const float>(rows_prio), rows_E};
-    }
+    SampleRowsOut ro{};
+    if (!out.is_none()) ro = SampleRowsOut{tab(src.cast<py::dict>()), tab(out.cast<py::dict>())};
     per_sample(t.d, B, P<const int64_t>(length_ptr), length, P<const float>(beta_ptr), beta, seed,
                P<const int64_t>(counter), P<int>(out_idx), P<float>(out_w), exclude_last, P<const float>(glob), S(s),
-               ShardGlob{P<const float>(gathered), world, rank}, rows_E > 0 ? &rows : nullptr);
+               ShardGlob{P<const float>(gathered), world, rank}, rows_E > 0 ? &rows : nullptr,
+               out.is_none() ? nullptr : &ro);
   }, py::arg("t"), py::arg("B"), py::arg("length_ptr"), py::arg("length"), py::arg("beta_ptr"), py::arg("beta"),
      py::arg("seed"), py::arg("counter"), py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"),
      py::arg("s"), py::arg("glob") = 0, py::arg("slots") = 0, py::arg("world") = 0, py::arg("rank") = 0,
      py::arg("rows_stage") = py::none(), py::arg("rows_dst") = py::none(), py::arg("rows_slot") = 0,
-     py::arg("rows_prio") = 0, py::arg("rows_E") = 0);
+     py::arg("rows_prio") = 0, py::arg("rows_E") = 0, py::arg("src") = py::none(), py::arg("out") = py::none());
   m.def("gather_transitions", [](uint64_t frames, int frame_bytes, uint64_t s_ids, uint64_t s2_ids, uint64_t act,
                                  uint64_t rew, uint64_t done, uint64_t idx, int B, uint64_t out_s, uint64_t out_s2,
                                  uint64_t out_a, uint64_t out_r, uint64_t out_d, uint64_t s) {

@@ -79,7 +79,7 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s);
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
                 int exclude_last, const float* glob, hipStream_t s, ShardGlob sg = ShardGlob{nullptr, 0, 0},
-                const struct StagedRows* rows = nullptr);
+                const struct StagedRows* rows = nullptr, const struct SampleRowsOut* rows_out = nullptr);
 void gather_transitions(const uint8_t* frames, int frame_bytes, const int* s_ids, const int* s2_ids,
                         const int* act, const float* rew, const float* done, const int* idx, int B, uint8_t* out_s,
                         uint8_t* out_s2, int* out_a, float* out_r, float* out_d, hipStream_t s);
@@ -147,6 +147,12 @@ struct StagedRows {
   int E;
 };
 void apply_staged_rows(TransTable stage, TransTable dst, const int* slot, const float* prio, int E, hipStream_t s);
+// per_sample's private copy of every sampled row (the learner's sampled-ahead batch):
+// out.*[i] = the row of slot out_idx[i] -- from the staged rows when this very launch
+// scatters that slot, else from ``src`` (the replay tables)
+struct SampleRowsOut {
+  TransTable src, out;
+};
 
 // ---- conv_bwd_kernels.hip: one launch for all batch-sliced gradient reductions
 constexpr int kMaxFinalizeJobs = 6;

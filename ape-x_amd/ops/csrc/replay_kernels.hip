@@ -192,7 +192,7 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
                              const float* beta_ptr, float beta_const, uint64_t seed,
                              const int64_t* __restrict__ counter, int* __restrict__ out_idx,
                              float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob,
-                             ShardGlob sg, StagedRows rows, int sample_blocks) {
+                             ShardGlob sg, StagedRows rows, SampleRowsOut ro, int sample_blocks) {
   if ((int)blockIdx.x >= sample_blocks) {  // fused staged-row scatter (apply_staged_rows)
     const int e = (blockIdx.x - sample_blocks) * blockDim.x + threadIdx.x;
     if (e >= rows.E || !(rows.prio[e] > 0.f)) return;
@@ -225,6 +225,20 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
     const float p = t.leaf_sum[node];
     out_idx[i] = node;
     out_w[i] = wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
+  }
+  if (ro.out.s_ids) {  // private row copy: the staged row if this launch scatters the slot (no race with
+                       // the scatter blocks), else the table row (a slot nobody writes in this launch)
+    int se = -1;
+    for (int e = lane; e < rows.E; e += 64)
+      if (rows.slot[e] == node && rows.prio[e] > 0.f) se = e;
+    se = wave_max(se);
+    const TransTable& src = se >= 0 ? rows.st : ro.src;
+    const int r = se >= 0 ? se : node;
+    if (lane < 4) ro.out.s_ids[4 * i + lane] = src.s_ids[4 * r + lane];
+    else if (lane < 8) ro.out.s2_ids[4 * i + lane - 4] = src.s2_ids[4 * r + lane - 4];
+    else if (lane == 8) ro.out.action[i] = src.action[r];
+    else if (lane == 9) ro.out.reward[i] = src.reward[r];
+    else if (lane == 10) ro.out.done[i] = src.done[r];
   }
 }
 
@@ -393,17 +407,19 @@ void per_update_levels(const TreeDesc& t, const int* idx, int B, hipStream_t s) 
 
 void per_sample(const TreeDesc& t, int B, const int64_t* length_ptr, int64_t length_const, const float* beta_ptr,
                 float beta_const, uint64_t seed, const int64_t* counter, int* out_idx, float* out_w,
-                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg, const StagedRows* rows) {
+                int exclude_last, const float* glob, hipStream_t s, ShardGlob sg, const StagedRows* rows,
+                const SampleRowsOut* rows_out) {
   if (B <= 0) return;
   if (sg.slots && (sg.world < 1 || sg.world > 64 || sg.rank < 0 || sg.rank >= sg.world))
     throw std::invalid_argument("per_sample: sharded world must be in [1, 64] with 0 <= rank < world");
   const int waves_per_block = 4;
   const int sblocks = (B + waves_per_block - 1) / waves_per_block;
   const StagedRows r = rows ? *rows : StagedRows{};
+  const SampleRowsOut ro = rows_out ? *rows_out : SampleRowsOut{};
   const int rblocks = r.E > 0 ? (r.E + 64 * waves_per_block - 1) / (64 * waves_per_block) : 0;
   per_sample_k<<<sblocks + rblocks, 64 * waves_per_block, 0, s>>>(
       t, B, length_ptr, length_const, beta_ptr, beta_const, seed, counter, out_idx, out_w, exclude_last, glob, sg, r,
-      sblocks);
+      ro, sblocks);
   LAUNCH_CHECK();
 }
 

@@ -118,6 +118,10 @@ def parse():
     ap.add_argument("--watchdog", type=float, default=1500.0,
                     help="seconds after which a rank dumps every thread's stack and exits 1 (0 = off): "
                          "a hung collective ends the run with a traceback instead of a silent stall")
+    ap.add_argument("--target-ahead", type=int, default=0, choices=[0, 1],
+                    help="1: sample batch t+1 at the start of step t and run its target pass beside step t")
+    ap.add_argument("--target-pass", default="actor", choices=["actor", "fork", "inline"],
+                    help="--target-ahead 1: where the next batch's target pass runs")
     ap.add_argument("--px", type=int, default=0, choices=[0, 1, 2],
                     help="fp32 forward GEMMs (conv2/conv3/FC1) on the pre-split exact bf16 kernels "
                          "(px_kernels.hip: every operand as 3 exact bf16 terms; 1 = 6 term products, "
@@ -205,7 +209,8 @@ def main():
     lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
                        tree_fork=args.tree_fork,
                        fork_late=args.fork_late, late_join=args.late_join,
-                       bwd_fork=args.bwd_fork, tree_write=args.tree_write)
+                       bwd_fork=args.bwd_fork, tree_write=args.tree_write, target_ahead=bool(args.target_ahead),
+                       target_pass=args.target_pass)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
@@ -304,6 +309,8 @@ def main():
                 "actor_steps_per_learner_step": args.actor_steps,
                 "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
+                "batch_pipeline": (f"sampled two steps ahead, target pass beside the previous step ({args.target_pass})"
+                                   if args.target_ahead else "sampled at the step start, 3-pass forward"),
                 "forward": args.forward,
                 "fp32_forward_gemms": (f"pre-split exact bf16x{4 + 2 * args.px} (3-term operands, fp32-class)" if args.px
                                        else "fp32 MFMA") if args.dtype == "fp32" else None,

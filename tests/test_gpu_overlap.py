@@ -52,11 +52,12 @@ def _engine(dev, overlap, graphs, dp=False, sharded=False, light_events=False, *
     return ApexEngine(cfg, dev, allreduce=FlatGradAllReduce(1) if dp else None, sharded=sharded)
 
 
-@pytest.mark.parametrize("step_graph,light", [(False, False), (True, False), (False, True)])
-def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph, light):
-    eng_g = _engine(cuda, True, True, light_events=light)
+@pytest.mark.parametrize("step_graph,light,ahead", [(False, False, False), (True, False, False), (False, True, False),
+                                                    (False, False, True), (True, False, True)])
+def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph, light, ahead):
+    eng_g = _engine(cuda, True, True, light_events=light, target_ahead=ahead)
     eng_g.cfg.step_graph = step_graph
-    eng_e = _engine(cuda, True, False)
+    eng_e = _engine(cuda, True, False, target_ahead=ahead)
     for eng in (eng_g, eng_e):
         eng.fill()
     eng_g.capture()                  # 3 counted warm-up steps, run sequentially
@@ -94,15 +95,16 @@ def test_graph_fork_layouts_equal_default(cuda, lkw):
     assert torch.isfinite(eng_a.learner.flat).all()
 
 
-@pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("sharded", [False, True])
-def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded):
+@pytest.mark.parametrize("overlap,sharded,ahead", [(True, False, False), (False, False, False), (True, True, False),
+                                                   (False, True, False), (True, True, True), (False, False, True)])
+def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded, ahead):
     """The data-parallel step (three phase graphs, async all-reduce slices, pipelined
     shard-mass exchange) replays exactly like its eager schedule, and its first step
-    matches the single-process fused step (different grad-norm summation order only)."""
-    eng_g = _engine(cuda, overlap, True, dp=True, sharded=sharded)
-    eng_e = _engine(cuda, overlap, False, dp=True, sharded=sharded)
-    eng_1 = _engine(cuda, overlap, False)
+    matches the single-process fused step (different grad-norm summation order only);
+    ``ahead``: with sampled-ahead batches (one graph per batch buffer)."""
+    eng_g = _engine(cuda, overlap, True, dp=True, sharded=sharded, target_ahead=ahead)
+    eng_e = _engine(cuda, overlap, False, dp=True, sharded=sharded, target_ahead=ahead)
+    eng_1 = _engine(cuda, overlap, False, target_ahead=ahead)
     assert eng_g.learner.dp_split and eng_g._dp and not eng_1._dp
     for eng in (eng_g, eng_e, eng_1):
         eng.fill()
@@ -123,4 +125,25 @@ def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded):
     assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
     assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
+    assert torch.isfinite(eng_g.learner.flat).all()
+
+
+def test_target_ahead_single_graph_mode_equals_eager(cuda):
+    """No overlap: the learner step is captured once per sampled-ahead buffer and the
+    replays (picked by learner.cur) match the eager engine bit for bit, target syncs included."""
+    eng_g = _engine(cuda, False, True, target_ahead=True)
+    eng_e = _engine(cuda, False, False, target_ahead=True)
+    for eng in (eng_g, eng_e):
+        eng.fill()
+    eng_g.capture()
+    for _ in range(3):
+        eng_e.train_step()
+    for _ in range(20):
+        eng_g.train_step()
+        eng_e.train_step()
+    torch.cuda.synchronize()
+    assert isinstance(eng_g._g_learn_a, list) and len(eng_g._g_learn_a) == 2
+    assert eng_g.learner.cur == eng_e.learner.cur
+    assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
+    assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.isfinite(eng_g.learner.flat).all()
