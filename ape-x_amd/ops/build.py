@@ -163,7 +163,7 @@ HIP_FLAGS = [
     "-std=c++17",
     "-fPIC",
     "-fvisibility=hidden",
-    "-ffp-contract=fast",
+    "-ffp-contract=fast-honor-pragmas",  # fast, except where a kernel pins its rounding (prio_mix)
     "-munsafe-fp-atomics",
     "-mcode-object-version=5",
     "-Wno-unused-result",

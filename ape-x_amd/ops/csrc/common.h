@@ -23,6 +23,15 @@
 
 namespace apex {
 
+// Ape-X priority mix (utils.py:77, learner.py): 0.9 max|delta| + 0.1 |delta| + 1e-6, rounded
+// step by step in torch's fp32 order -- no fma contraction, so every kernel that forms it
+// (sequential and batched tree writes, the loss kernel) agrees bit for bit whatever the
+// compiler does around it
+__device__ __forceinline__ float prio_mix(float dmax, float d) {
+#pragma clang fp contract(off)
+  return (0.9f * dmax + 0.1f * d) + 1e-6f;
+}
+
 // ---------------------------------------------------------------- wave reductions
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

@@ -1200,12 +1200,15 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
 // im2col address of a row is (sample) * plane + (position, tap) offset -- the position is
 // uniform per k-block (scalar), where sample-major rows paid ~30 VALU per 16-byte load
 // dividing the row index by P and OH (MI355X: conv3 wgrad 45 -> see profiles).
-template <int L>
+// BN_ (knob 24): the (tap, ci) width of a workgroup's tile -- each dy k-block it stages is
+// re-read by N / BN_ workgroups, so wider tiles move fewer L2 bytes per FLOP
+template <int L, int BN_ = 64>
 struct ConvWgrad {
   static constexpr int C = L == 3 ? 64 : 32, K = L == 3 ? 3 : 4, S = L == 3 ? 1 : 2;
   static constexpr int IH = L == 3 ? 9 : 20, OH = L == 3 ? 7 : 9, P = OH * OH;
   static constexpr int N = K * K * C;
-  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
+  static constexpr int BM = 64, BN = BN_, BK = 32, WM = 2;
+  static_assert(N % BN == 0, "whole tiles");
   static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false, A_COLSUM = true;
   using Args = BwdArgs;
   using Smem = NoSmem;
@@ -1717,11 +1720,20 @@ SplitPlan plan_splits(int kbt, int ntiles, int target_blocks, int max_kbps) {
   return {s, kbps};
 }
 
+// conv2 / conv3 weight-gradient tile width (f32_set_variant(24, 0..2)): 0 = 64 (2 x 2 waves of
+// 32 x 32), 1 = conv2 128 / conv3 192, 2 = conv2 256 / conv3 192; same workgroup count (more
+// batch splits, shorter k ranges)
+int g_wgrad_wide = 0;
+static int wgrad_bn(int layer) {
+  if (!g_wgrad_wide) return 64;
+  return layer == 2 ? (g_wgrad_wide == 2 ? 256 : 128) : 192;
+}
+
 SplitPlan wgrad_plan(int layer, int B) {
   switch (layer) {
     case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_k workgroups
-    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 8, 256 * g_wgrad_occ, 1 << 20);
-    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 9, 252 * g_wgrad_occ, 1 << 20);
+    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / wgrad_bn(2), 256 * g_wgrad_occ, 1 << 20);
+    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / wgrad_bn(3), 252 * g_wgrad_occ, 1 << 20);
     default: throw std::invalid_argument("f32 wgrad layer");
   }
 }
@@ -1852,6 +1864,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 21 && v >= 0 && v <= 1) px_set_pipe(v);  // px / pxb pipeline form
   else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
   else if (layer == 23 && (v == 0 || (v >= 2 && v <= 4))) g_fwd_dma = v;  // LDS-DMA ring forward GEMMs
+  else if (layer == 24 && v >= 0 && v <= 2) g_wgrad_wide = v;  // conv2 / conv3 weight-gradient tile width
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1994,7 +2007,17 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.out = dx;
   d.B = B;
   const int mode = g_bwd_mode;  // benchmark knob: 0 both, 1 weight gradient only, 2 input gradient only
-  const int nw3 = mode == 2 ? 0 : ConvWgrad<3>::tiles(B, p.splits), nw2 = mode == 2 ? 0 : ConvWgrad<2>::tiles(B, p.splits);
+  const int nw3 = mode == 2 ? 0 : (576 / wgrad_bn(3)) * p.splits, nw2 = mode == 2 ? 0 : (512 / wgrad_bn(2)) * p.splits;
+  const int nd3 = mode == 1 ? 0 : Conv3DgradP::tiles(B), nd2 = mode == 1 ? 0 : Conv2DgradP::tiles(B);
+  if (layer == 3 && wgrad_bn(3) == 192 && !g_dgrad_variant && g_dgrad3_tile != 1) {
+    launch2<ConvWgrad<3, 192>, Conv3DgradP>(g, nw3, d, nd3, s);
+    return;
+  }
+  if (layer == 2 && wgrad_bn(2) != 64 && !g_dgrad_variant) {
+    if (wgrad_bn(2) == 256) launch2<ConvWgrad<2, 256>, Conv2DgradP>(g, nw2, d, nd2, s);
+    else launch2<ConvWgrad<2, 128>, Conv2DgradP>(g, nw2, d, nd2, s);
+    return;
+  }
   switch (layer) {
     case 3:
       if (g_dgrad_variant)

@@ -65,7 +65,7 @@ __global__ void dqn_loss_k(const float* __restrict__ q, const float* __restrict_
   const float total = block_sum_f(lw, red);
   const float dmax = block_max_f(b < B ? delta : -INFINITY, red);
   if (b < B) {
-    prio[b] = 0.9f * dmax + 0.1f * delta + 1e-6f;
+    prio[b] = prio_mix(dmax, delta);
     float* dr = dq + (size_t)b * ldq;
     for (int k = 0; k < A; ++k) dr[k] = (k == a) ? g : 0.f;
   }

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(1024) void per_write_leaves_sorted_k(TreeDesc t, co
     const float total = block_reduce_1024(k < B ? mix.lw[k] : 0.f, red, false);
     const float dmax = block_reduce_1024(k < B ? dl : -INFINITY, red, true);
     if (k < B) {
-      const float p = 0.9f * dmax + 0.1f * dl + 1e-6f;
+      const float p = prio_mix(dmax, dl);
       pmix[k] = p;
       if (mix.prio_out) mix.prio_out[k] = p;
     }

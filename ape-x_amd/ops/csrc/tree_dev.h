@@ -109,7 +109,7 @@ __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const Batc
       const float dl = k < w.B ? w.mix.delta[k] : 0.f;
       const float total = block_reduce_1024(k < w.B ? w.mix.lw[k] : 0.f, red, false);
       const float dmax = block_reduce_1024(k < w.B ? dl : -INFINITY, red, true);
-      p = 0.9f * dmax + 0.1f * dl + 1e-6f;
+      p = prio_mix(dmax, dl);
       if (k < w.B && w.mix.prio_out) w.mix.prio_out[k] = p;
       if (k == 0 && w.mix.loss_out) w.mix.loss_out[0] = total / (float)w.B;
     } else if (k < w.B) {
