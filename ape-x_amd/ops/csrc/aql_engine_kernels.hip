@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   __shared__ __attribute__((aligned(16))) float w1[kH * kP132];   // advantage1 effective weight [n][k]
   __shared__ float qw1[kH * 65], qw2[kH * 65];                     // q_feature.0 [n][obs], .2 [n][k]
   __shared__ float xt[16 * kP68];                                  // ao_out tile [16 candidates][64]
-  __shared__ float ao1w[kCat * kMaxAdim];
+  __shared__ __attribute__((aligned(16))) float ao1w[kCat * kMaxAdim];  // [k][8], zero-padded past adim
   __shared__ float ao1b[kCat], ao2b[kH], w2e[kH], b1e[kH], qb1[kH], qb2[kH];
   __shared__ float sv[2][64], hq[2][kH], qf[2][kH], stp[2][kH];
   __shared__ float qpart[4][2][16];
@@ -102,7 +102,26 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   const int T = N.T, RT = (T + 15) >> 4;
   const int nst = (tgt || L.act_mode) ? 1 : 2;  // online: {s, s'} (acting: {s}), target: {s'}
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, q = lane >> 4;
-  const int obs = N.obs, adim = N.adim, cont = N.cont, po = obs + 1;
+  const int obs = N.obs, adim = N.adim, cont = N.cont;
+  AQL_STAMP(L, 8);
+  // the PER draw of sample b (fused sampling) by wave 0: identical in every workgroup of b (same
+  // Philox stream); the (tile 0, online) workgroup also writes the slot and its IS weight
+  auto draw = [&](int b, int rt) {
+    const int64_t f = L.filled[0];
+    const int length = (int)(f < (int64_t)L.tree.size[0] ? f : (int64_t)L.tree.size[0]);
+    const int node = tree_sample_leaf(L.tree, b, L.B, length, L.exclude_last, L.seed, (uint64_t)L.ctr[0], lane);
+    if (lane == 0) {
+      srow = node;
+      if (rt == 0 && !tgt) {
+        const float p = L.tree.leaf_sum[node], pmin = L.tree.node_min[L.tree.levels - 1][0], beta = L.beta[0];
+        L.idx_out[b] = node;
+        L.w_out[b] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
+      }
+    }
+  };
+  // (measured: drawing on wave 0 WHILE waves 1-3 stage the weights was slower than the two in
+  // sequence -- 25.4k vs 18.0k cycles: the descent's dependent loads queue behind the staging
+  // traffic in the CU's memory pipeline)
   {  // stage the two 64x128 matrices with 16-byte loads, all in flight before the stores
     const f32x4* a4 = reinterpret_cast<const f32x4*>(N.ao_w2);
     const f32x4* w4 = reinterpret_cast<const f32x4*>(eff);
@@ -119,55 +138,63 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       *reinterpret_cast<f32x4*>(&w1[r * kP132 + c]) = vw[k];
     }
   }
-  for (int e = t; e < kH * obs; e += 256) qw1[(e / obs) * po + e % obs] = N.qf_w1[e];
+  {
+    // first-layer rows zero-padded to whole 8-column blocks (branch-free, unrolled dot
+    // products: a runtime-length loop of LDS loads serialised one LDS latency per term)
+    const int obs8 = (obs + 7) & ~7, po = obs8 + 1;
+    for (int e = t; e < kH * obs; e += 256) qw1[(e / obs) * po + e % obs] = N.qf_w1[e];  // coalesced copy
+    for (int e = t; e < kH * (obs8 - obs); e += 256) {                                  // then the pads
+      const int r = e / (obs8 - obs);
+      qw1[r * po + obs + (e - r * (obs8 - obs))] = 0.f;
+    }
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int e = t + 256 * k;
-    qw2[(e >> 6) * 65 + (e & 63)] = N.qf_w2[e];
+    for (int k = 0; k < 16; ++k) {
+      const int e = t + 256 * k;
+      qw2[(e >> 6) * 65 + (e & 63)] = N.qf_w2[e];
+    }
+    const int nao1 = cont ? kCat : kH;
+    for (int e = t; e < nao1 * adim; e += 256) ao1w[(e / adim) * kMaxAdim + e % adim] = N.ao_w1[e];
+    for (int e = t; e < nao1 * (kMaxAdim - adim); e += 256) {
+      const int r = e / (kMaxAdim - adim);
+      ao1w[r * kMaxAdim + adim + (e - r * (kMaxAdim - adim))] = 0.f;
+    }
+    if (t < nao1) ao1b[t] = N.ao_b1[t];
+    if (t < kH) {
+      if (cont) ao2b[t] = N.ao_b2[t];
+      w2e[t] = eff[kEffW2 + t];
+      b1e[t] = eff[kEffB1 + t];
+      qb1[t] = N.qf_b1[t];
+      qb2[t] = N.qf_b2[t];
+    }
   }
-  const int nao1 = cont ? kCat : kH;
-  for (int e = t; e < nao1 * adim; e += 256) ao1w[e] = N.ao_w1[e];
-  if (t < nao1) ao1b[t] = N.ao_b1[t];
-  if (t < kH) {
-    if (cont) ao2b[t] = N.ao_b2[t];
-    w2e[t] = eff[kEffW2 + t];
-    b1e[t] = eff[kEffB1 + t];
-    qb1[t] = N.qf_b1[t];
-    qb2[t] = N.qf_b2[t];
-  }
+  const int obs8 = (obs + 7) & ~7, po = obs8 + 1;
   // work items (sample b, candidate tile rt): one per workgroup for the learner; the acting
   // launch (act_mode) runs a small grid that loops, so the weights staged above (~110 KB of
   // LDS, one workgroup per CU) are loaded once per workgroup and most CUs stay free for the
   // learner's kernels running beside it
   for (int item = blockIdx.x; item < L.B * RT; item += gridDim.x) {
   const int b = item / RT, rt = item - b * RT;
-  __syncthreads();  // the previous item is done with sv / xt / stp / qpart / srow
-  if (L.fused_sample) {  // wave 0 draws sample b (identical in every workgroup of b: same Philox stream)
-    if (wave == 0) {
-      const int64_t f = L.filled[0];
-      const int length = (int)(f < (int64_t)L.tree.size[0] ? f : (int64_t)L.tree.size[0]);
-      const int node = tree_sample_leaf(L.tree, b, L.B, length, L.exclude_last, L.seed, (uint64_t)L.ctr[0], lane);
-      if (lane == 0) {
-        srow = node;
-        if (rt == 0 && !tgt) {
-          const float p = L.tree.leaf_sum[node], pmin = L.tree.node_min[L.tree.levels - 1][0], beta = L.beta[0];
-          L.idx_out[b] = node;
-          L.w_out[b] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
-        }
-      }
-    }
+  __syncthreads();  // the staging / the previous item is done with sv / xt / stp / qpart / srow
+  if (item == blockIdx.x) AQL_STAMP(L, 9);
+  if (L.fused_sample) {
+    if (wave == 0) draw(b, rt);
     __syncthreads();
   }
+  if (item == blockIdx.x) AQL_STAMP(L, 10);
   const int row = L.fused_sample ? srow : (L.idx ? L.idx[b] : b);
   if (t < 128) {
     const int si = t >> 6, i = t & 63;
-    if (si < nst && i < obs) sv[si][i] = ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i];
+    if (si < nst) sv[si][i] = i < obs ? ((tgt || si) ? L.st2 : L.st)[(size_t)row * obs + i] : 0.f;
   }
   __syncthreads();
+  if (item == blockIdx.x) AQL_STAMP(L, 11);
   // state halves, from LDS: wave si < nst handles state si (q_feature MLP, W1[:, 64:] . qf + b1)
   if (wave < nst) {
     float a = qb1[lane];
-    for (int i = 0; i < obs; ++i) a = fmaf(qw1[lane * po + i], sv[wave][i], a);
+    for (int i0 = 0; i0 < obs8; i0 += 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a = fmaf(qw1[lane * po + i0 + i], sv[wave][i0 + i], a);
+    }
     hq[wave][lane] = relu(a);
     __builtin_amdgcn_wave_barrier();
     a = qb2[lane];
@@ -192,12 +219,18 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
 #pragma unroll 4
     for (int k0 = 0; k0 < kCat; k0 += 8) {
       float h0 = ao1b[k0 + q], h1 = ao1b[k0 + 4 + q];
+      const f32x4* w0 = reinterpret_cast<const f32x4*>(&ao1w[(k0 + q) * kMaxAdim]);
+      const f32x4* w1r = reinterpret_cast<const f32x4*>(&ao1w[(k0 + 4 + q) * kMaxAdim]);
+      const f32x4 x0 = w0[0], x1 = w0[1], y0 = w1r[0], y1 = w1r[1];  // zero past adim (av too)
 #pragma unroll
-      for (int d = 0; d < kMaxAdim; ++d) {
-        if (d < adim) {
-          h0 = fmaf(ao1w[(k0 + q) * adim + d], av[d], h0);
-          h1 = fmaf(ao1w[(k0 + 4 + q) * adim + d], av[d], h1);
-        }
+      for (int d = 0; d < 4; ++d) {
+        h0 = fmaf(x0[d], av[d], h0);
+        h1 = fmaf(y0[d], av[d], h1);
+      }
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        h0 = fmaf(x1[d], av[4 + d], h0);
+        h1 = fmaf(y1[d], av[4 + d], h1);
       }
       acc0 = mfma4(relu(h0), ao2[n * kP132 + k0 + q], acc0);
       acc1 = mfma4(relu(h1), ao2[n * kP132 + k0 + 4 + q], acc1);
@@ -208,10 +241,11 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = min(rt * 16 + 4 * q + i, T - 1);
-      xt[(4 * q + i) * kP68 + n] = relu(fmaf(ao1w[n], L.amu[(size_t)row * T + r], ao1b[n]));
+      xt[(4 * q + i) * kP68 + n] = relu(fmaf(ao1w[n * kMaxAdim], L.amu[(size_t)row * T + r], ao1b[n]));
     }
   }
   __syncthreads();
+  if (item == blockIdx.x) AQL_STAMP(L, 12);
   // advantage1 candidate half: pre[16][64] = ao_out . W1a^T; wave w -> columns 16w..16w+15
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
@@ -231,6 +265,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
     }
   }
   __syncthreads();
+  if (item == blockIdx.x) AQL_STAMP(L, 13);
   if (t < 16 * nst) {
     const int m = t & 15, si = t >> 4, tt = rt * 16 + m;
     if (tt < T) {
@@ -240,6 +275,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
     }
   }
   }  // work items
+  AQL_STAMP(L, 14);
 }
 
 // ------------------------------------------------------------------ per-sample loss + backward
@@ -276,20 +312,25 @@ __device__ __forceinline__ float row_dot4(const float* __restrict__ W, int r, co
   return a0 + a1;
 }
 
-// small first-layer matrices (inputs obs / adim <= 64) from LDS: one thread per output row
-__device__ __forceinline__ float lds_row_dot(const float* Wl, int n, const float* v, float bias) {
+// small first-layer matrices (inputs obs / adim <= 64) from LDS: one thread per output row,
+// rows zero-padded to n8 (a multiple of 8) so the dot product is branch-free and unrolled
+__device__ __forceinline__ float lds_row_dot(const float* Wl, int n8, const float* v, float bias) {
   float a = bias;
-  for (int i = 0; i < n; ++i) a = fmaf(Wl[i], v[i], a);
+  for (int i0 = 0; i0 < n8; i0 += 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a = fmaf(Wl[i0 + i], v[i0 + i], a);
+  }
   return a;
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   __shared__ float s_s[64], s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
+  // first-layer rows [row][in] at odd pitches (obs8 + 1, adim -> 8 + 1), zero-padded
   __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
   __shared__ int cnt[64];
   __shared__ int s_best, s_next;
   __shared__ float s_gq;
-  __shared__ float sw_qf1[kH * 64], sw_ao1[kCat * kMaxAdim], sw_f[kCat * 64];  // first layers [row][in]
+  __shared__ float sw_qf1[kH * 65], sw_ao1[kCat * (kMaxAdim + 1)], sw_f[kCat * 65];
   const AQLNet& N = L.on;
   const float* eff = L.eff_on;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -297,9 +338,19 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   const int row = L.idx[b];
   const int a_idx = L.act[row];
   AQL_STAMP(L, 0);
-  for (int e = t; e < kH * obs; e += 256) sw_qf1[e] = N.qf_w1[e];
-  for (int e = t; e < (cont ? kCat : kH) * adim; e += 256) sw_ao1[e] = N.ao_w1[e];
-  for (int e = t; e < kCat * obs; e += 256) sw_f[e] = N.f_w[e];
+  const int obs8 = (obs + 7) & ~7, po = obs8 + 1, pa = kMaxAdim + 1, nao1 = cont ? kCat : kH;
+  for (int e = t; e < kH * obs; e += 256) sw_qf1[(e / obs) * po + e % obs] = N.qf_w1[e];  // coalesced copies
+  for (int e = t; e < nao1 * adim; e += 256) sw_ao1[(e / adim) * pa + e % adim] = N.ao_w1[e];
+  for (int e = t; e < kCat * obs; e += 256) sw_f[(e / obs) * po + e % obs] = N.f_w[e];
+  for (int e = t; e < kCat * (obs8 - obs); e += 256) {  // then the pads
+    const int r = e / (obs8 - obs), i = obs + e - r * (obs8 - obs);
+    if (r < kH) sw_qf1[r * po + i] = 0.f;
+    sw_f[r * po + i] = 0.f;
+  }
+  for (int e = t; e < nao1 * (kMaxAdim - adim); e += 256) {
+    const int r = e / (kMaxAdim - adim);
+    sw_ao1[r * pa + adim + e - r * (kMaxAdim - adim)] = 0.f;
+  }
   if (wave == 0) {
     const int bi = wave_argmax(L.q_s + (size_t)b * T, T, lane);
     if (lane == 0) s_best = bi;
@@ -308,8 +359,8 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
     if (lane == 0) s_next = bi;
   }
   if (t < 64) cnt[t] = 0;
-  if (t < obs) s_s[t] = L.st[(size_t)row * obs + t];
-  if (t < adim) s_a[t] = L.amu[((size_t)row * T + a_idx) * adim + t];
+  if (t < 64) s_s[t] = t < obs ? L.st[(size_t)row * obs + t] : 0.f;
+  if (t < kMaxAdim) s_a[t] = t < adim ? L.amu[((size_t)row * T + a_idx) * adim + t] : 0.f;
   __syncthreads();
   AQL_STAMP(L, 1);
   if (!cont) {  // counts of every sample's best candidate (the [B, B] log-prob broadcast)
@@ -334,14 +385,14 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   // forward of the taken candidate (s, a_mu[a]) + the proposal trunk.  First layers from
   // the LDS-staged matrices (thread per row), then the 64/128-wide layers wave-per-row.
   if (t < kH) {
-    qfh[t] = relu(lds_row_dot(sw_qf1 + t * obs, obs, s_s, N.qf_b1[t]));
+    qfh[t] = relu(lds_row_dot(sw_qf1 + t * po, obs8, s_s, N.qf_b1[t]));
   } else if (t < kH + (cont ? kCat : kH)) {
     const int k = t - kH;
-    aoh[k] = relu(lds_row_dot(sw_ao1 + k * adim, adim, s_a, N.ao_b1[k]));
+    aoh[k] = relu(lds_row_dot(sw_ao1 + k * pa, kMaxAdim, s_a, N.ao_b1[k]));
   }
   if (t >= 2 * kH) {
     const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
-    emb[k] = relu(lds_row_dot(sw_f + k * obs, obs, s_s, N.f_b[k]));
+    emb[k] = relu(lds_row_dot(sw_f + k * po, obs8, s_s, N.f_b[k]));
   }
   __syncthreads();
   AQL_STAMP(L, 2);

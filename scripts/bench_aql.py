@@ -43,6 +43,8 @@ def main():
     if L.dbg is not None:  # APEX_AQL_DBG=1: backward phase timestamps (s_memtime cycles) of the last step
         d = L.dbg.cpu().tolist()
         print("bwd phase cycles:", [d[k + 1] - d[k] for k in range(7)], "total", d[7] - d[0])
+        print("fwd phase cycles (staging, sampling, state load, encodings, adv1, out):",
+              [d[k + 1] - d[k] for k in range(8, 14)], "total", d[14] - d[8])
 
 
 if __name__ == "__main__":
