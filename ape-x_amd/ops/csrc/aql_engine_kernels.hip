@@ -57,6 +57,29 @@ __device__ __forceinline__ float noisy_w(const float* mu, const float* sg, const
   return noisy ? fmaf(sg[i], ep[i], m) : m;
 }
 __device__ __forceinline__ float relu(float x) { return fmaxf(x, 0.f); }
+// a + sum_k w[k] v[k] over 64 columns, sequential fma order; w: one LDS row, v: a broadcast LDS
+// vector, both 16-byte aligned.  Eight 16-byte loads of each are issued before their FMAs: with
+// scalar loads the compiler re-used one register quad and waited out an LDS latency every
+// 2-4 FMAs (~3k cycles per 64-term row)
+__device__ __forceinline__ float lds_dot64(const float* w, const float* v, float a) {
+#pragma unroll
+  for (int c = 0; c < 64; c += 32) {
+    f32x4 x[8], y[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      x[i] = *reinterpret_cast<const f32x4*>(w + c + 4 * i);
+      y[i] = *reinterpret_cast<const f32x4*>(v + c + 4 * i);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a = fmaf(x[i].x, y[i].x, a);
+      a = fmaf(x[i].y, y[i].y, a);
+      a = fmaf(x[i].z, y[i].z, a);
+      a = fmaf(x[i].w, y[i].w, a);
+    }
+  }
+  return a;
+}
 // phase timestamp (diagnostics): block 0, thread 0, after a barrier
 #define AQL_STAMP(L, k)                                                   \
   do {                                                                    \
@@ -89,11 +112,14 @@ constexpr int kEffB1 = kH * kCat, kEffW2 = kEffB1 + kH, kEffB2 = kEffW2 + kH;
 __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   __shared__ __attribute__((aligned(16))) float ao2[kH * kP132];  // action_out.2 weight [n][k]
   __shared__ __attribute__((aligned(16))) float w1[kH * kP132];   // advantage1 effective weight [n][k]
-  __shared__ float qw1[kH * 65], qw2[kH * 65];                     // q_feature.0 [n][obs], .2 [n][k]
+  // q_feature.0 [n][obs -> 64, zero-padded], .2 [n][k]: pitch 68 = 4 x odd, so the 16-byte row
+  // reads of 16 lanes (one row each) cover all 64 banks
+  __shared__ __attribute__((aligned(16))) float qw1[kH * kP68], qw2[kH * kP68];
   __shared__ float xt[16 * kP68];                                  // ao_out tile [16 candidates][64]
   __shared__ __attribute__((aligned(16))) float ao1w[kCat * kMaxAdim];  // [k][8], zero-padded past adim
   __shared__ float ao1b[kCat], ao2b[kH], w2e[kH], b1e[kH], qb1[kH], qb2[kH];
-  __shared__ float sv[2][64], hq[2][kH], qf[2][kH], stp[2][kH];
+  __shared__ __attribute__((aligned(16))) float sv[2][64], hq[2][kH], qf[2][kH];
+  __shared__ float stp[2][kH];
   __shared__ float qpart[4][2][16];
   __shared__ int srow;
   const bool tgt = blockIdx.y != 0;
@@ -141,16 +167,21 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   {
     // first-layer rows zero-padded to whole 8-column blocks (branch-free, unrolled dot
     // products: a runtime-length loop of LDS loads serialised one LDS latency per term)
-    const int obs8 = (obs + 7) & ~7, po = obs8 + 1;
-    for (int e = t; e < kH * obs; e += 256) qw1[(e / obs) * po + e % obs] = N.qf_w1[e];  // coalesced copy
-    for (int e = t; e < kH * (obs8 - obs); e += 256) {                                  // then the pads
-      const int r = e / (obs8 - obs);
-      qw1[r * po + obs + (e - r * (obs8 - obs))] = 0.f;
-    }
+    {  // both 64-row matrices, every load in flight before the stores (clamped column index:
+       // unconditional loads; q_feature.0's columns past obs stored as zeros)
+      float x1[16], x2[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = t + 256 * k;
-      qw2[(e >> 6) * 65 + (e & 63)] = N.qf_w2[e];
+      for (int k = 0; k < 16; ++k) {
+        const int e = t + 256 * k, r = e >> 6, i = e & 63;
+        x1[k] = N.qf_w1[r * obs + min(i, obs - 1)];
+        x2[k] = N.qf_w2[e];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = t + 256 * k, r = e >> 6, i = e & 63;
+        qw1[r * kP68 + i] = i < obs ? x1[k] : 0.f;
+        qw2[r * kP68 + i] = x2[k];
+      }
     }
     const int nao1 = cont ? kCat : kH;
     for (int e = t; e < nao1 * adim; e += 256) ao1w[(e / adim) * kMaxAdim + e % adim] = N.ao_w1[e];
@@ -167,7 +198,6 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       qb2[t] = N.qf_b2[t];
     }
   }
-  const int obs8 = (obs + 7) & ~7, po = obs8 + 1;
   // work items (sample b, candidate tile rt): one per workgroup for the learner; the acting
   // launch (act_mode) runs a small grid that loops, so the weights staged above (~110 KB of
   // LDS, one workgroup per CU) are loaded once per workgroup and most CUs stay free for the
@@ -190,22 +220,11 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   if (item == blockIdx.x) AQL_STAMP(L, 11);
   // state halves, from LDS: wave si < nst handles state si (q_feature MLP, W1[:, 64:] . qf + b1)
   if (wave < nst) {
-    float a = qb1[lane];
-    for (int i0 = 0; i0 < obs8; i0 += 8) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) a = fmaf(qw1[lane * po + i0 + i], sv[wave][i0 + i], a);
-    }
-    hq[wave][lane] = relu(a);
+    hq[wave][lane] = relu(lds_dot64(qw1 + lane * kP68, sv[wave], qb1[lane]));  // (zero past obs)
     __builtin_amdgcn_wave_barrier();
-    a = qb2[lane];
-#pragma unroll 16
-    for (int k = 0; k < kH; ++k) a = fmaf(qw2[lane * 65 + k], hq[wave][k], a);
-    qf[wave][lane] = relu(a);
+    qf[wave][lane] = relu(lds_dot64(qw2 + lane * kP68, hq[wave], qb2[lane]));
     __builtin_amdgcn_wave_barrier();
-    a = b1e[lane];
-#pragma unroll 16
-    for (int k = 0; k < kH; ++k) a = fmaf(w1[lane * kP132 + kH + k], qf[wave][k], a);
-    stp[wave][lane] = a;
+    stp[wave][lane] = lds_dot64(w1 + lane * kP132 + kH, qf[wave], b1e[lane]);
   }
   // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
   const int n = 16 * wave + j;
