@@ -331,6 +331,20 @@ __device__ __forceinline__ float row_dot4(const float* __restrict__ W, int r, co
   return a0 + a1;
 }
 
+// row_dot4 on a row already in registers (same fma order)
+template <int N4>
+__device__ __forceinline__ float regs_dot4(const f32x4* x, const float* v) {
+  float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < N4; ++k) {
+    a0 = fmaf(x[k].x, v[4 * k], a0);
+    a1 = fmaf(x[k].y, v[4 * k + 1], a1);
+    a0 = fmaf(x[k].z, v[4 * k + 2], a0);
+    a1 = fmaf(x[k].w, v[4 * k + 3], a1);
+  }
+  return a0 + a1;
+}
+
 // small first-layer matrices (inputs obs / adim <= 64) from LDS: one thread per output row,
 // rows zero-padded to n8 (a multiple of 8) so the dot product is branch-free and unrolled
 __device__ __forceinline__ float lds_row_dot(const float* Wl, int n8, const float* v, float bias) {
@@ -343,13 +357,16 @@ __device__ __forceinline__ float lds_row_dot(const float* Wl, int n8, const floa
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
-  __shared__ float s_s[64], s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
-  // first-layer rows [row][in] at odd pitches (obs8 + 1, adim -> 8 + 1), zero-padded
+  __shared__ __attribute__((aligned(16))) float s_s[64];
+  __shared__ float s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
   __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
   __shared__ int cnt[64];
   __shared__ int s_best, s_next;
   __shared__ float s_gq;
-  __shared__ float sw_qf1[kH * 65], sw_ao1[kCat * (kMaxAdim + 1)], sw_f[kCat * 65];
+  // first layers [row][in]: q_feature.0 / features.0 zero-padded to 64 columns at pitch 68 (16-byte
+  // row reads, conflict-free), action_out.0 zero-padded to 8 at pitch 9
+  __shared__ __attribute__((aligned(16))) float sw_qf1[kH * kP68], sw_f[kCat * kP68];
+  __shared__ float sw_ao1[kCat * (kMaxAdim + 1)];
   const AQLNet& N = L.on;
   const float* eff = L.eff_on;
   const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -357,18 +374,52 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   const int row = L.idx[b];
   const int a_idx = L.act[row];
   AQL_STAMP(L, 0);
-  const int obs8 = (obs + 7) & ~7, po = obs8 + 1, pa = kMaxAdim + 1, nao1 = cont ? kCat : kH;
-  for (int e = t; e < kH * obs; e += 256) sw_qf1[(e / obs) * po + e % obs] = N.qf_w1[e];  // coalesced copies
-  for (int e = t; e < nao1 * adim; e += 256) sw_ao1[(e / adim) * pa + e % adim] = N.ao_w1[e];
-  for (int e = t; e < kCat * obs; e += 256) sw_f[(e / obs) * po + e % obs] = N.f_w[e];
-  for (int e = t; e < kCat * (obs8 - obs); e += 256) {  // then the pads
-    const int r = e / (obs8 - obs), i = obs + e - r * (obs8 - obs);
-    if (r < kH) sw_qf1[r * po + i] = 0.f;
-    sw_f[r * po + i] = 0.f;
+  // the second-layer row this thread contracts later (q_feature.2 / action_out.2 /
+  // dist_feature.0), prefetched now: its loads fly under the staging and the first layers
+  // instead of opening a phase of their own
+  const float* w2row = t < kH ? N.qf_w2 + (size_t)t * kH
+                              : (t < 2 * kH ? (cont ? N.ao_w2 + (size_t)(t - kH) * kCat : nullptr)
+                                            : N.df_w1 + (size_t)(t - 2 * kH) * kCat);
+  f32x4 xr[kCat / 4];
+  if (w2row) {
+#pragma unroll
+    for (int k = 0; k < kCat / 4; ++k)
+      if (t >= kH || k < kH / 4) xr[k] = reinterpret_cast<const f32x4*>(w2row)[k];
   }
-  for (int e = t; e < nao1 * (kMaxAdim - adim); e += 256) {
-    const int r = e / (kMaxAdim - adim);
-    sw_ao1[r * pa + adim + e - r * (kMaxAdim - adim)] = 0.f;
+  const int pa = kMaxAdim + 1, nao1 = cont ? kCat : kH;
+  {  // first layers, every load in flight before the stores (clamped column index:
+     // unconditional loads; columns past obs / adim stored as zeros)
+    float y1[16], y2[32], y3[4];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      y1[k] = N.qf_w1[r * obs + min(i, obs - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      y2[k] = N.f_w[r * obs + min(i, obs - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = t + 256 * k, r = e >> 3, i = e & 7;
+      y3[k] = N.ao_w1[min(r, nao1 - 1) * adim + min(i, adim - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      sw_qf1[r * kP68 + i] = i < obs ? y1[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      sw_f[r * kP68 + i] = i < obs ? y2[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = t + 256 * k, r = e >> 3, i = e & 7;
+      if (r < nao1) sw_ao1[r * pa + i] = i < adim ? y3[k] : 0.f;
+    }
   }
   if (wave == 0) {
     const int bi = wave_argmax(L.q_s + (size_t)b * T, T, lane);
@@ -404,25 +455,25 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   // forward of the taken candidate (s, a_mu[a]) + the proposal trunk.  First layers from
   // the LDS-staged matrices (thread per row), then the 64/128-wide layers wave-per-row.
   if (t < kH) {
-    qfh[t] = relu(lds_row_dot(sw_qf1 + t * po, obs8, s_s, N.qf_b1[t]));
+    qfh[t] = relu(lds_dot64(sw_qf1 + t * kP68, s_s, N.qf_b1[t]));  // (zero past obs)
   } else if (t < kH + (cont ? kCat : kH)) {
     const int k = t - kH;
     aoh[k] = relu(lds_row_dot(sw_ao1 + k * pa, kMaxAdim, s_a, N.ao_b1[k]));
   }
   if (t >= 2 * kH) {
     const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
-    emb[k] = relu(lds_row_dot(sw_f + k * po, obs8, s_s, N.f_b[k]));
+    emb[k] = relu(lds_dot64(sw_f + k * kP68, s_s, N.f_b[k]));
   }
   __syncthreads();
   AQL_STAMP(L, 2);
-  if (t < kH) {  // q_feature.2
-    x[kH + t] = relu(row_dot4<kH / 4>(N.qf_w2, t, qfh) + N.qf_b2[t]);
+  if (t < kH) {  // q_feature.2 (from the prefetched row)
+    x[kH + t] = relu(regs_dot4<kH / 4>(xr, qfh) + N.qf_b2[t]);
   } else if (t < 2 * kH) {  // action_out.2 (continuous) / identity (discrete)
     const int nn = t - kH;
-    x[nn] = cont ? relu(row_dot4<kCat / 4>(N.ao_w2, nn, aoh) + N.ao_b2[nn]) : aoh[nn];
+    x[nn] = cont ? relu(regs_dot4<kCat / 4>(xr, aoh) + N.ao_b2[nn]) : aoh[nn];
   } else {  // proposal dist_feature.0
     const int k = t - 2 * kH;
-    hid[k] = relu(row_dot4<kCat / 4>(N.df_w1, k, emb) + N.df_b1[k]);
+    hid[k] = relu(regs_dot4<kCat / 4>(xr, emb) + N.df_b1[k]);
   }
   __syncthreads();
   AQL_STAMP(L, 3);
