@@ -575,20 +575,26 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
     const int e = (int)(i - J.off), r = e / J.cols, c = e - r * J.cols;
     grp = J.group;
     if (!J.zero) {
-      // the batch contraction in chunks of 16 samples, every load of a chunk in flight
+      // the batch contraction in chunks of 32 samples, every load of a chunk in flight: the
+      // loads are unconditional (clamped sample index, results selected after), a guarded
+      // load compiled to a branch + wait each
       float acc = 0.f;
       const float* gp = G.vec + J.goff + r;
       const float* xp = G.vec + (J.xoff >= 0 ? J.xoff + c : 0);
-      for (int b0 = 0; b0 < G.B; b0 += 16) {
-        float gv[16], xv[16];
+      const bool hasx = J.xoff >= 0;
+      for (int b0 = 0; b0 < G.B; b0 += 32) {
+        float gv[32], xv[32];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const bool ok = b0 + k < G.B;
-          gv[k] = ok ? gp[(size_t)(b0 + k) * aqlv::STRIDE] : 0.f;
-          xv[k] = (ok && J.xoff >= 0) ? xp[(size_t)(b0 + k) * aqlv::STRIDE] : 1.f;
+        for (int k = 0; k < 32; ++k) {
+          const size_t bb = (size_t)min(b0 + k, G.B - 1) * aqlv::STRIDE;
+          gv[k] = gp[bb];
+          xv[k] = xp[bb];
         }
 #pragma unroll
-        for (int k = 0; k < 16; ++k) acc = fmaf(gv[k], xv[k], acc);
+        for (int k = 0; k < 32; ++k) {
+          const bool ok = b0 + k < G.B;
+          acc = fmaf(ok ? gv[k] : 0.f, (ok && hasx) ? xv[k] : 1.f, acc);
+        }
       }
       g = J.eps ? acc * J.eps[e] : acc;
     }
