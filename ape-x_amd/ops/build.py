@@ -209,8 +209,24 @@ def build_hip(force: bool = False, jobs: int | None = None) -> Path:
     digest = _digest([*digests, *cmd])
     if force or todo or _stale(target, digest):
         _run(cmd)
+        _check_kernel_stubs(target)
         _stamp(target, digest)
     return target
+
+
+def _check_kernel_stubs(lib: Path) -> None:
+    """A kernel the host pass did not emit leaves its launch stub undefined in the shared
+    object (seen with hipcc for a template kernel whose body holds a lambda over a
+    ``__shared__`` array); the library links, and only the GPU box's dlopen fails.  Refuse it
+    here instead."""
+    nm = shutil.which("nm")
+    if not nm:
+        return
+    out = subprocess.run([nm, "-D", "--undefined-only", str(lib)], capture_output=True, text=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "__device_stub__" in ln]
+    if bad:
+        lib.unlink()
+        raise RuntimeError(f"{lib.name}: undefined kernel launch stubs {bad}")
 
 
 def build_all(force: bool = False, only: str | None = None, jobs: int | None = None) -> list[Path]:

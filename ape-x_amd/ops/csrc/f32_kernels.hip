@@ -963,6 +963,186 @@ __global__ __launch_bounds__(256) void f32_conv1_fwd_k(F32Set set) {
   }
 }
 
+// conv2 / conv3 forward, sample-resident (knob 25).  Every GEMM-body form of these layers
+// landed at ~90 TF/s: a 64 x 64 tile streams its im2col A rows from L2 (conv2: each input
+// pixel gathered 3.2x, conv3 2.9x) and at N = 64 each A float feeds only 64 MACs, so the
+// chip-wide k-block rate (~5 TB/s, profiles/r3_px_findings.md) caps them below the fp32
+// MFMA peak whatever the pipeline depth.  Here the im2col never leaves the CU:
+//   * a persistent workgroup (one per CU, 4 waves) owns a contiguous range of 16-row output
+//     tiles of ONE problem; the input samples its tiles touch stream whole into a 3-slot LDS
+//     ring with global_load_lds_dwordx4 (LDS-DMA, no registers), one sample ahead of use, so
+//     each input byte crosses L2 -> CU once;
+//   * wave w keeps output channels 16w .. 16w+15 of the weights in registers for the whole
+//     kernel (B operand, K/4 f32x4), so the only per-MFMA operand traffic is the A fragment:
+//     one ds_read_b128 (4 k of one im2col row) per 4 v_mfma_f32_16x16x4_f32;
+//   * k order: 16-k steps st (tap = 16 st / C, channels c16 = 16 st % C); lane (i = l & 15,
+//     g = l >> 4) holds k = 16 st + 4 g .. +3, MFMA s of the step takes element s (A and B
+//     share the map, so the sum is the same up to fp32 rounding order);
+//   * LDS image of a sample: its [pixel][C] fp32 block as 256-byte rows (row q = input row
+//     iy = q / W, column block x = q % W), 16-byte chunk col of row q stored at slot
+//     col ^ h(q), h = (2 x + HB iy) & 15: the 16 rows of a tile span 2-3 output rows, and a plain
+//     q & 15 swizzle put rows of different output rows on one slot (3-way ds_read_b128 bank
+//     conflicts, SQ_LDS_BANK_CONFLICT 7.7x the LDS cycles); the even x coefficient keeps the
+//     lane groups' k-chunks (col ^ 1) apart and HB staggers the input rows -- 4.7 / 5.2 LDS
+//     cycles per read for conv2 / conv3 (4 = conflict-free) in a bank model of every tile;
+//   * G tiles per group (64 / 48 rows < one sample) keep G independent accumulator chains
+//     (covers the 40-cycle dependent MFMA latency) and let a group touch at most 2 samples:
+//     the ring's third slot fills while they are read.
+template <int L>
+struct DConv;
+// W = 256-byte image rows per input row, HB = the swizzle's input-row coefficient
+template <>
+struct DConv<2> {
+  static constexpr int IH = 20, C = 32, OH = 9, K = 4, S = 2, W = 10, HB = 1;
+  static constexpr int G1 = 4, G2 = 4;  // tiles per group at 4 / 8 waves
+};
+template <>
+struct DConv<3> {
+  static constexpr int IH = 9, C = 64, OH = 7, K = 3, S = 1, W = 9, HB = 14;
+  static constexpr int G1 = 3, G2 = 2;
+};
+template <int L>
+struct DGeo {
+  using D = DConv<L>;
+  static constexpr int P = D::OH * D::OH, PIX = D::IH * D::IH, KK = D::K * D::K * D::C, NST = KK / 16;
+  static constexpr int ROWS = PIX * D::C / 64;           // 256-byte rows of a sample image
+  static constexpr int NI = (ROWS + 3) / 4;              // 1 KB DMA wave-instructions per sample
+  static constexpr int SLOT = NI * 256;                  // floats per ring slot
+  static_assert(D::C % 16 == 0 && (PIX * D::C) % 64 == 0, "whole 16-k steps, whole rows");
+  static_assert(32 * D::G1 < 2 * P + 2 && 32 * D::G2 < 2 * P + 2, "a group and the next stay within 3 ring slots");
+  static_assert(3 * SLOT * 4 <= 160 * 1024, "3-slot ring fits the 160 KB LDS");
+};
+constexpr int kDconvTile = 16;
+
+template <int L>
+__device__ __forceinline__ int dconv_swz(int q) {
+  using D = DConv<L>;
+  return (2 * (q % D::W) + D::HB * (q / D::W)) & 15;
+}
+
+// MH = 1: 4 waves, each every tile of a group; MH = 2: 8 waves (two per SIMD, one's MFMAs
+// cover the other's LDS waits), waves 4 mh .. 4 mh + 3 take the group's mh-th half
+template <int L, int MH>
+__device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw, int wgpp, float* ring) {
+  using D = DConv<L>;
+  using Q = DGeo<L>;
+  constexpr int G = MH == 1 ? D::G1 : D::G2, GW = G / MH, P = Q::P, C4 = D::C / 4;
+  static_assert(G % MH == 0, "whole tiles per wave");
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nq = wave & 3, mh = wave >> 2;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int prob = blockIdx.x / wgpp;
+  const F32Prob p = pick(set, prob);
+  const int M = set.B * P, Tp = (M + kDconvTile - 1) / kDconvTile;
+  const int t0 = (blockIdx.x - prob * wgpp) * tpw, t1 = min(Tp, t0 + tpw);
+  if (t0 >= t1) return;  // whole workgroup, before any barrier
+  const int rend = min(kDconvTile * t1, M);
+  const int sf = kDconvTile * t0 / P;  // first sample of the range (local sample 0)
+  const float* in = static_cast<const float*>(p.in) + (size_t)sf * Q::PIX * D::C;
+  // local sample j -> ring slot j % 3; wave-instruction i fills rows 4i .. 4i+3 lane-linearly,
+  // so lane l fetches the logical chunk stored at slot (l & 15) of row 4i + (l >> 4)
+  auto issue = [&](int j) {
+    const float* src = in + (size_t)j * Q::PIX * D::C;
+    float* dst = ring + (j % 3) * Q::SLOT;
+    for (int i = wave; i < Q::NI; i += 4 * MH) {
+      const int q = 4 * i + g, u = q * 16 + (i16 ^ dconv_swz<L>(q));
+      __builtin_amdgcn_global_load_lds(q < Q::ROWS ? src + 4 * u : src,
+                                       (__attribute__((address_space(3))) void*)(dst + i * 256), 16, 0, 0);
+    }
+  };
+  auto last_sample = [&](int tg) { return (min(kDconvTile * (tg + G), rend) - 1) / P - sf; };
+  int loaded = 0;
+  for (const int hi = last_sample(t0); loaded <= hi; ++loaded) issue(loaded);
+  // this wave's 16 output channels of W (w2p / w3p rows, k-contiguous)
+  const int n = 16 * nq + i16;
+  f32x4 bw[Q::NST];
+  const float* wrow = p.w + (size_t)n * Q::KK + 4 * g;
+#pragma unroll
+  for (int st = 0; st < Q::NST; ++st) bw[st] = ld4(wrow + 16 * st);
+  const float bias = p.bias[n];
+  float* out = p.out + n;
+  // a group's results are stored after the NEXT group's DMA wait (stores count in vmcnt: stored
+  // at the group's end, the wait at the next group's start would drain their round trip)
+  f32x4 pacc[GW];
+  int ptg = -1;
+  auto store = [&](int tq) {
+#pragma unroll
+    for (int k = 0; k < GW; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // D[row 4g + e][col i16] of tile tq + mh GW + k -> a2/a3 row, channel n
+        const int r = kDconvTile * (tq + mh * GW + k) + 4 * g + e;
+        if (r < rend) out[(size_t)r * 64] = fmaxf(pacc[k][e] + bias, 0.f);
+      }
+  };
+  for (int tg = t0; tg < t1; tg += G) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs (and stores) landed
+    __syncthreads();                                  // every wave's; the previous group is read
+    if (tg + G < t1)
+      for (const int hi = last_sample(tg + G); loaded <= hi; ++loaded) issue(loaded);
+    if (ptg >= 0) store(ptg);
+    // per tile: this lane's im2col row -> (ring slot base, window origin pixel)
+    // (its image row at tap (0, 0) + slot base, and the swizzle there).  A tap (ky, kx) moves
+    // the row by dq = ky W + kx C / 64 (x stays inside the input row: no carry into iy) and the
+    // swizzle by dh = 2 kx C / 64 + HB ky; the chunk within the row is col + g with col =
+    // (kx C / 4) % 16 + k-chunk a multiple of 4, so the slot is col ^ (g ^ h): per tile and
+    // distinct dh (conv2 6, conv3 5) the byte offset of chunk g ^ h is kept, and a read costs
+    // one XOR with 16 col, its dq lands in the ds_read offset field
+    int ad[GW][16];
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      const int r = min(kDconvTile * (tg + mh * GW + k) + i16, rend - 1);
+      const int s = r / P, pos = r - s * P, oy = pos / D::OH, ox = pos - oy * D::OH;
+      const int q = D::S * (oy * D::IH + ox) * C4 / 16;  // window origin (x, iy) = (S ox C / 64, S oy)
+      const int qb = ((s - sf) % 3) * (Q::SLOT / 4) + q * 16;
+      const int hb = 2 * (q % D::W) + D::HB * (q / D::W);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) ad[k][d] = 16 * (qb + (g ^ ((hb + d) & 15)));  // unused d: dead code
+    }
+    const char* lds_b = reinterpret_cast<const char*>(ring);
+    auto read = [&](int st, int k) {
+      const int k0 = 16 * st, tap = k0 / D::C, ky = tap / D::K, kx = tap - ky * D::K;
+      const int dq = ky * D::W + kx * D::C / 64, col = (kx * C4) % 16 + (k0 % D::C) / 4;
+      const int dh = (2 * (kx * D::C / 64) + D::HB * ky) & 15;
+      return *reinterpret_cast<const f32x4*>(lds_b + ((ad[k][dh] ^ (16 * col)) + 256 * dq));
+    };
+    f32x4 acc[GW], a[GW], an[GW];
+#pragma unroll
+    for (int k = 0; k < GW; ++k) {
+      acc[k] = zero4();
+      a[k] = read(0, k);
+    }
+#pragma unroll
+    for (int st = 0; st < Q::NST; ++st) {
+#pragma unroll
+      for (int k = 0; k < GW; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k][0], bw[st][0], acc[k], 0, 0, 0);
+      // the next step's reads go out after this step's first G MFMAs: the compiler waits for
+      // LDS with lgkmcnt(0), so reads issued any later would stall the next step's first MFMA
+      // and reads issued earlier (the default schedule) would be waited on with this step's
+      __builtin_amdgcn_sched_barrier(0);
+      if (st + 1 < Q::NST) {
+#pragma unroll
+        for (int k = 0; k < GW; ++k) an[k] = read(st + 1, k);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 1; s < 4; ++s)
+#pragma unroll
+        for (int k = 0; k < GW; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k][s], bw[st][s], acc[k], 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < GW; ++k) a[k] = an[k];
+    }
+#pragma unroll
+    for (int k = 0; k < GW; ++k) pacc[k] = acc[k];
+    ptg = tg;
+  }
+  store(ptg);
+}
+
+template <int L, int MH>
+__global__ __launch_bounds__(256 * MH) void f32_conv_fwd_direct_k(F32Set set, int tpw, int wgpp) {
+  __shared__ __attribute__((aligned(16))) float ring[3 * DGeo<L>::SLOT];
+  conv_fwd_direct_body<L, MH>(set, tpw, wgpp, ring);
+}
+
 // conv1 forward at reference precision on the bf16 matrix cores (exact three-term split).
 //  * Input pixels are u8 (0..255, 8 significant bits): exactly representable in bf16.
 //  * An fp32 weight splits EXACTLY into three bf16 terms by truncation: hi = w with its low
@@ -1820,6 +2000,41 @@ int g_conv1_variant = 2;
 // gemm_k), S = 2..4 ring stages; 64 x 64 K-major tiles only (the learner's 3-problem launches)
 int g_fwd_dma = 0;
 
+// conv2 / conv3 forward on the sample-resident kernel (f32_set_variant(25, 0..2)), see
+// f32_conv_fwd_direct_k: 0 = the GEMM bodies below, 1 = one 4-wave workgroup per CU, 2 = one
+// 8-wave workgroup per CU (two waves per SIMD), 3 = conv3 at two 4-wave workgroups per CU (its
+// 3-slot ring is 63 KB)
+int g_fwd_direct = 0;
+
+static int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// one persistent workgroup per CU: the CUs are dealt to the problems evenly, each problem's
+// 16-row tiles split into equal contiguous ranges (tpw tiles per workgroup)
+static bool any_outx(const F32Set& set) {
+  for (int i = 0; i < set.n; ++i)
+    if (set.p[i].outx) return true;
+  return false;
+}
+
+template <int L>
+void direct_launch(const F32Set& set, hipStream_t s) {
+  const int M = set.B * DGeo<L>::P, Tp = (M + kDconvTile - 1) / kDconvTile;
+  const int per = std::max(1, device_cus() * (L == 3 && g_fwd_direct == 3 ? 2 : 1) / set.n);
+  const int tpw = (Tp + per - 1) / per, wgpp = (Tp + tpw - 1) / tpw;
+  if (g_fwd_direct == 2) f32_conv_fwd_direct_k<L, 2><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
+  else f32_conv_fwd_direct_k<L, 1><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
+  LAUNCH_CHECK();
+}
+
 template <class P>
 void fwd_launch(const F32Set& set, hipStream_t s) {
   const int blocks = set.n * P::tiles(set.B);
@@ -1865,6 +2080,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
   else if (layer == 23 && (v == 0 || (v >= 2 && v <= 4))) g_fwd_dma = v;  // LDS-DMA ring forward GEMMs
   else if (layer == 24 && v >= 0 && v <= 2) g_wgrad_wide = v;  // conv2 / conv3 weight-gradient tile width
+  else if (layer == 25 && v >= 0 && v <= 3) g_fwd_direct = v;  // sample-resident conv2 / conv3 forward
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
@@ -1894,6 +2110,7 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
       break;
     case 2:
       if (px_ready(set)) px_conv_fwd_multi(2, set, s);
+      else if (g_fwd_direct && !any_outx(set)) direct_launch<2>(set, s);
       else if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
       else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
       else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
@@ -1901,6 +2118,7 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
       break;
     case 3:
       if (px_ready(set)) px_conv_fwd_multi(3, set, s);
+      else if (g_fwd_direct && !any_outx(set)) direct_launch<3>(set, s);
       else if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
       else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
       else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);

@@ -26,6 +26,7 @@ ap.add_argument("--json", action="store_true")
 ap.add_argument("--wgrad-occ", type=int, default=0, help="conv2/3 wgrad workgroups per CU (knob 7; 0 = default)")
 ap.add_argument("--bwd-sweep", action="store_true", help="conv backward: wgrad / dgrad split and dgrad variants")
 ap.add_argument("--variants", default=None, help="forward tile variants to sweep, e.g. 0,1,2,3 (f32_set_variant)")
+ap.add_argument("--knobs", default="", help="f32_set_variant settings for the whole run, e.g. 25=1,14=2")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -36,6 +37,8 @@ for p in m.parameters():
     p.grad = torch.zeros_like(p)
 if a.wgrad_occ:
     hip.f32_set_variant(7, a.wgrad_occ)
+for kv in filter(None, a.knobs.split(",")):
+    hip.f32_set_variant(*map(int, kv.split("=")))
 net = F32DuelingNet(m)
 net.enable_backward(B)
 F = 4 * B

@@ -142,6 +142,53 @@ def test_x9_gemm_forward_is_fp32_class(cuda, B):
         assert e1 <= 2.0 * e0 + 1e-7, (name, errs)
 
 
+@pytest.mark.parametrize("B", [37, 300])
+def test_direct_conv_forward_is_fp32_class(cuda, B):
+    """conv2 / conv3 forward on the sample-resident kernel (f32_conv_fwd_direct_k, knob
+    (25, 1): input samples in an LDS ring, weights in registers, v_mfma_f32_16x16x4_f32) vs
+    the GEMM body (knob (25, 0)), per problem of a 3-problem launch (online / online on other
+    frames / target net: the persistent workgroups split each problem's tiles, ranges start
+    mid-sample): error against fp64 from the SAME layer input, scaled by sum_k |a_k w_k|;
+    the single-problem launch is bit-identical to the 3-problem one."""
+    from apex_amd import ops
+    from apex_amd.models.fused import forward_multi
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    m, mt = _model(cuda, seed=11), _model(cuda, seed=12)
+    net, tnet = F32DuelingNet(m), F32DuelingNet(mt)
+    xs = [torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda) for _ in range(2)]
+    d = lambda t: t.detach().double()  # noqa: E731
+    errs, q = {}, {}
+    try:
+        for v in (0, 1, 2, 3):
+            hip.f32_set_variant(25, v)
+            wss = [F32Workspace(B, 18, cuda, keep_for_backward=True) for _ in range(3)]
+            forward_multi([(net, xs[0], wss[0], None, None), (net, xs[1], wss[1], None, None),
+                           (tnet, xs[0], wss[2], None, None)])
+            single = F32Workspace(B, 18, cuda, keep_for_backward=True)
+            tnet(xs[0], single)
+            torch.cuda.synchronize()
+            assert torch.equal(single.a2, wss[2].a2) and torch.equal(single.a3, wss[2].a3), v
+            for i, (mod, ws) in enumerate(zip((m, m, mt), wss)):
+                f = mod.features
+                g1, g2, g3 = _nchw(ws.a1, B, 32, 20), _nchw(ws.a2, B, 64, 9), _nchw(ws.a3, B, 64, 7)
+                for name, inp, got, k, st in (("conv2", g1, g2, 2, 2), ("conv3", g2, g3, 4, 1)):
+                    ref = F.relu(F.conv2d(inp, d(f[k].weight), d(f[k].bias), stride=st))
+                    sc = F.conv2d(inp.abs(), d(f[k].weight).abs(), d(f[k].bias).abs(), stride=st)
+                    errs[(name, i, v)] = float(((got - ref).abs() / sc.clamp_min(1e-30)).max())
+                q[(i, v)] = ws.q.clone()
+    finally:
+        hip.f32_set_variant(25, 0)
+    for key in [k for k in errs if k[2] > 0]:
+        e1, e0 = errs[key], errs[key[:2] + (0,)]
+        assert e1 < 1e-6, (key, errs)
+        assert e1 <= 2.0 * e0 + 1e-7, (key, errs)
+    for i in range(3):
+        assert torch.equal(q[(i, 1)], q[(i, 2)]) and torch.equal(q[(i, 1)], q[(i, 3)])  # same per-row k order
+        assert float((q[(i, 1)] - q[(i, 0)]).norm() / q[(i, 0)].norm()) < 1e-5
+
+
 def test_f32_frame_ring_and_multi_pass(cuda):
     """conv1 reading the HBM frame ring by id (rows picked by idx) == dense input, and the
     3-problem launch == three single launches (bit-identical)."""
