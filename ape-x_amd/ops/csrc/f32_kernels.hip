@@ -1022,7 +1022,10 @@ __device__ __forceinline__ int dconv_swz(int q) {
 
 // MH = 1: 4 waves, each every tile of a group; MH = 2: 8 waves (two per SIMD, one's MFMAs
 // cover the other's LDS waits), waves 4 mh .. 4 mh + 3 take the group's mh-th half
-template <int L, int MH>
+// DBG (knob 25 = 4 | 5: MH 1 | 2): every wave adds its cycles per phase (s_memtime) and writes
+// them to the int64 buffer passed as the problem's w2 pointer: [wg][wave][wait, issue, setup,
+// steps, total]
+template <int L, int MH, bool DBG = false>
 __device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw, int wgpp, float* ring) {
   using D = DConv<L>;
   using Q = DGeo<L>;
@@ -1035,19 +1038,28 @@ __device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw,
   const int M = set.B * P, Tp = (M + kDconvTile - 1) / kDconvTile;
   const int t0 = (blockIdx.x - prob * wgpp) * tpw, t1 = min(Tp, t0 + tpw);
   if (t0 >= t1) return;  // whole workgroup, before any barrier
+  long long ph[5] = {0, 0, 0, 0, 0}, tq0 = DBG ? clock64() : 0, tq;
+  auto stamp = [&](int i) {
+    if constexpr (DBG) {
+      const long long now = clock64();
+      ph[i] += now - tq;
+      tq = now;
+    }
+  };
   const int rend = min(kDconvTile * t1, M);
   const int sf = kDconvTile * t0 / P;  // first sample of the range (local sample 0)
   const float* in = static_cast<const float*>(p.in) + (size_t)sf * Q::PIX * D::C;
   // local sample j -> ring slot j % 3; wave-instruction i fills rows 4i .. 4i+3 lane-linearly,
   // so lane l fetches the logical chunk stored at slot (l & 15) of row 4i + (l >> 4)
-  auto issue = [&](int j) {
+  auto issue_one = [&](int j, int i) {
     const float* src = in + (size_t)j * Q::PIX * D::C;
-    float* dst = ring + (j % 3) * Q::SLOT;
-    for (int i = wave; i < Q::NI; i += 4 * MH) {
-      const int q = 4 * i + g, u = q * 16 + (i16 ^ dconv_swz<L>(q));
-      __builtin_amdgcn_global_load_lds(q < Q::ROWS ? src + 4 * u : src,
-                                       (__attribute__((address_space(3))) void*)(dst + i * 256), 16, 0, 0);
-    }
+    const int q = 4 * i + g, u = q * 16 + (i16 ^ dconv_swz<L>(q));
+    __builtin_amdgcn_global_load_lds(q < Q::ROWS ? src + 4 * u : src,
+                                     (__attribute__((address_space(3))) void*)(ring + (j % 3) * Q::SLOT + i * 256),
+                                     16, 0, 0);
+  };
+  auto issue = [&](int j) {
+    for (int i = wave; i < Q::NI; i += 4 * MH) issue_one(j, i);
   };
   auto last_sample = [&](int tg) { return (min(kDconvTile * (tg + G), rend) - 1) / P - sf; };
   int loaded = 0;
@@ -1064,21 +1076,31 @@ __device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw,
   // at the group's end, the wait at the next group's start would drain their round trip)
   f32x4 pacc[GW];
   int ptg = -1;
+  auto store_one = [&](int tq, int k, int e) {  // D[row 4g + e][col i16] of tile tq + mh GW + k -> a2/a3 row n
+    const int r = kDconvTile * (tq + mh * GW + k) + 4 * g + e;
+    if (r < rend) out[(size_t)r * 64] = fmaxf(pacc[k][e] + bias, 0.f);
+  };
   auto store = [&](int tq) {
 #pragma unroll
     for (int k = 0; k < GW; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {  // D[row 4g + e][col i16] of tile tq + mh GW + k -> a2/a3 row, channel n
-        const int r = kDconvTile * (tq + mh * GW + k) + 4 * g + e;
-        if (r < rend) out[(size_t)r * 64] = fmaxf(pacc[k][e] + bias, 0.f);
-      }
+      for (int e = 0; e < 4; ++e) store_one(tq, k, e);
   };
+  if constexpr (DBG) tq = clock64();
   for (int tg = t0; tg < t1; tg += G) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs (and stores) landed
     __syncthreads();                                  // every wave's; the previous group is read
-    if (tg + G < t1)
-      for (const int hi = last_sample(tg + G); loaded <= hi; ++loaded) issue(loaded);
-    if (ptg >= 0) store(ptg);
+    stamp(0);
+    // the next group's new sample (at most one: a group is < one sample of rows) goes out one
+    // DMA wave-instruction per MFMA step, and the previous group's results one store per step:
+    // issued back to back they filled the memory queue and stalled the wave ~2.9k cycles a group
+    int pend = -1;
+    if (tg + G < t1) {
+      const int hi = last_sample(tg + G);
+      for (; loaded < hi; ++loaded) issue(loaded);
+      if (loaded == hi) pend = loaded++;
+    }
+    stamp(1);
     // per tile: this lane's im2col row -> (ring slot base, window origin pixel)
     // (its image row at tap (0, 0) + slot base, and the swizzle there).  A tap (ky, kx) moves
     // the row by dq = ky W + kx C / 64 (x stays inside the input row: no carry into iy) and the
@@ -1110,37 +1132,63 @@ __device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw,
       acc[k] = zero4();
       a[k] = read(0, k);
     }
+    stamp(2);
 #pragma unroll
     for (int st = 0; st < Q::NST; ++st) {
-#pragma unroll
-      for (int k = 0; k < GW; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k][0], bw[st][0], acc[k], 0, 0, 0);
-      // the next step's reads go out after this step's first G MFMAs: the compiler waits for
-      // LDS with lgkmcnt(0), so reads issued any later would stall the next step's first MFMA
-      // and reads issued earlier (the default schedule) would be waited on with this step's
-      __builtin_amdgcn_sched_barrier(0);
+      // the next step's reads go out between this step's first MFMAs, one (XOR + ds_read) per
+      // MFMA gap (one wave per SIMD: a cluster of them longer than a 32-cycle gap idles the
+      // MFMA pipe); the compiler waits for LDS with lgkmcnt(0) at the next step's first MFMA,
+      // a whole step later.  The DMA / store of the step follow in later gaps.
       if (st + 1 < Q::NST) {
 #pragma unroll
         for (int k = 0; k < GW; ++k) an[k] = read(st + 1, k);
       }
-      __builtin_amdgcn_sched_barrier(0);
+      if (pend >= 0 && wave + 4 * MH * st < Q::NI) issue_one(pend, wave + 4 * MH * st);
+      if (st < 4 * GW && ptg >= 0) store_one(ptg, st / 4, st % 4);
 #pragma unroll
-      for (int s = 1; s < 4; ++s)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int k = 0; k < GW; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k][s], bw[st][s], acc[k], 0, 0, 0);
+      if (st + 1 < Q::NST) {
+#pragma unroll
+        for (int k = 0; k < GW; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (the XOR)
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        }
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (DMA or store)
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * GW, 0);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < GW; ++k) a[k] = an[k];
     }
 #pragma unroll
     for (int k = 0; k < GW; ++k) pacc[k] = acc[k];
     ptg = tg;
+    if constexpr (DBG) {  // the MFMA results are in flight until their first use
+      asm volatile("s_nop 0" ::: "memory");
+    }
+    stamp(3);
   }
   store(ptg);
+  if constexpr (DBG) {
+    ph[4] = clock64() - tq0;
+    if (lane == 0) {
+      long long* o = const_cast<long long*>(reinterpret_cast<const long long*>(p.w2)) + ((size_t)blockIdx.x * 4 * MH + wave) * 5;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = ph[i];
+    }
+  }
 }
 
-template <int L, int MH>
+template <int L, int MH, bool DBG = false>
 __global__ __launch_bounds__(256 * MH) void f32_conv_fwd_direct_k(F32Set set, int tpw, int wgpp) {
   __shared__ __attribute__((aligned(16))) float ring[3 * DGeo<L>::SLOT];
-  conv_fwd_direct_body<L, MH>(set, tpw, wgpp, ring);
+  conv_fwd_direct_body<L, MH, DBG>(set, tpw, wgpp, ring);
 }
 
 // conv1 forward at reference precision on the bf16 matrix cores (exact three-term split).
@@ -2030,8 +2078,16 @@ void direct_launch(const F32Set& set, hipStream_t s) {
   const int M = set.B * DGeo<L>::P, Tp = (M + kDconvTile - 1) / kDconvTile;
   const int per = std::max(1, device_cus() * (L == 3 && g_fwd_direct == 3 ? 2 : 1) / set.n);
   const int tpw = (Tp + per - 1) / per, wgpp = (Tp + tpw - 1) / tpw;
-  if (g_fwd_direct == 2) f32_conv_fwd_direct_k<L, 2><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
-  else f32_conv_fwd_direct_k<L, 1><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
+  if (g_fwd_direct == 4 || g_fwd_direct == 5) {  // phase-stamp diagnostics into each problem's w2
+    for (int i = 0; i < set.n; ++i)
+      if (!set.p[i].w2) throw std::invalid_argument("direct conv diagnostics: pass an int64 stamp buffer as w2");
+    if (g_fwd_direct == 5) f32_conv_fwd_direct_k<L, 2, true><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
+    else f32_conv_fwd_direct_k<L, 1, true><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
+  } else if (g_fwd_direct == 2) {
+    f32_conv_fwd_direct_k<L, 2><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
+  } else {
+    f32_conv_fwd_direct_k<L, 1><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
+  }
   LAUNCH_CHECK();
 }
 
@@ -2080,7 +2136,7 @@ void f32_set_variant(int layer, int v) {
   else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
   else if (layer == 23 && (v == 0 || (v >= 2 && v <= 4))) g_fwd_dma = v;  // LDS-DMA ring forward GEMMs
   else if (layer == 24 && v >= 0 && v <= 2) g_wgrad_wide = v;  // conv2 / conv3 weight-gradient tile width
-  else if (layer == 25 && v >= 0 && v <= 3) g_fwd_direct = v;  // sample-resident conv2 / conv3 forward
+  else if (layer == 25 && v >= 0 && v <= 5) g_fwd_direct = v;  // sample-resident conv2 / conv3 forward
   else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
 }
 
