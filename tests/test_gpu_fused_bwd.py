@@ -105,14 +105,15 @@ def test_tree_write_priority_mix(cuda):
     torch.testing.assert_close(out_p, prio, rtol=1e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("C", [4096, 8192, 1 << 21])
-def test_batched_tree_write_equals_sequential_writes(cuda, C):
+@pytest.mark.parametrize("C,B,E", [(4096, 512, 256), (8192, 512, 256), (1 << 21, 512, 256), (8192, 32, 16),
+                                   (1 << 21, 64, 32)])
+def test_batched_tree_write_equals_sequential_writes(cuda, C, B, E):
     """write_batch (actor rows + mixed learner priorities, dedup by claims, wide level
-    kernels + last-block top levels) leaves the tree bit-identical to the old sequential
-    path (ring write, then the sorted dedup write), repeatedly (claims released)."""
+    kernels + last-block top levels -- or, at <= 64 rows, every level inside the leaves
+    workgroup) leaves the tree bit-identical to the old sequential path (ring write, then the
+    sorted dedup write), repeatedly (claims released)."""
     from apex_amd.engine.hbm_replay import HBMReplay
 
-    B, E = 512, 256
     g = torch.Generator(device=cuda).manual_seed(11)
     rp1 = HBMReplay(C, E, 3, 0.6, cuda)
     rp2 = HBMReplay(C, E, 3, 0.6, cuda)
