@@ -184,6 +184,12 @@ class AQLEngineConfig:
     # priority write as an extra workgroup of the noise-reset launch: measured 12936-12958 vs 13117
     # SGD steps/s (the one-workgroup tree write, ~15 us in a 256-thread block, then bounds that launch)
     fused_tree: bool = os.environ.get("APEX_AQL_FUSED_TREE", "0") == "1"
+    # priority write split over the two launches that follow the backward: the leaves (claims,
+    # mix, loss mean, dirty list) as an extra workgroup of the gradient contraction, the level
+    # walk as an extra workgroup of the noise reset -- no launch of its own on the chain
+    # (MI355X, batch 32: 14758-14771 vs 13882-13899 SGD steps/s with the write as its own launch,
+    # one box, interleaved; scripts/ab/aql_split_tree.sh)
+    split_tree: bool = os.environ.get("APEX_AQL_SPLIT_TREE", "1") == "1"
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
     act_blocks: int = int(os.environ.get("APEX_AQL_ACT_BLOCKS", "0"))
@@ -296,6 +302,12 @@ class AQLLearner:
                                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
                                               r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                           if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
+        split = cfg.split_tree and self.post_tree is None and not cfg.fork_tree and B <= 64
+        self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
+                                           self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
+                                           r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
+                       if split else None)
+        self.post_levels = h.aql_post_set_levels(self.post, r.tree, r.wlist.data_ptr(), B) if split else None
         self.refresh()
 
     def refresh(self) -> None:
@@ -374,8 +386,8 @@ class AQLLearner:
                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
                               r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), ts)
 
-        if self.post_tree is not None:
-            pass  # folded into the noise-reset launch below (aql_post_set_tree)
+        if self.post_tree is not None or self.G_tree is not None:
+            pass  # folded into the launches below (aql_post_set_tree | aql_grad_set_tree + aql_post_set_levels)
         elif self.cfg.fork_tree:
             self.tree_stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.tree_stream):
@@ -383,7 +395,7 @@ class AQLLearner:
             self._tree_pending = True
         else:
             tree_write(s)
-        h.aql_grad(self.G, s)
+        h.aql_grad(self.G if self.G_tree is None else self.G_tree, s)
         Pq, o = self.P_q, 4 * self.P_q
         # the two optimizers (critic, proposal; own clip norms) in one launch
         h.adam_step2((self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
@@ -392,7 +404,8 @@ class AQLLearner:
                       self.v.data_ptr() + o, self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk,
                       self.norms_p.data_ptr()),
                      self.hp, self.step_ctr.data_ptr(), s)
-        h.aql_post(self.post if self.post_tree is None else self.post_tree, 1, s)
+        h.aql_post(self.post_tree if self.post_tree is not None else
+                   (self.post_levels if self.post_levels is not None else self.post), 1, s)
         if self.cfg.track_losses:  # device-side running sums; read (one sync) only when logging
             self.loss_acc[0:1].add_(self.loss_q)
             self.loss_acc[1:2].add_(self.loss_p)

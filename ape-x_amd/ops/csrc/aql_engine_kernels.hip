@@ -563,6 +563,13 @@ constexpr int kGradThreads = 256;
 
 __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   __shared__ double red[2][4];
+  if (G.tree_leaves && blockIdx.x == gridDim.x - 1) {  // block-uniform: the split tree write's leaves
+    __shared__ float tred[16];
+    __shared__ int sids[64];
+    batch_leaves_block(G.tree, G.bw, 0, tred, sids);
+    return;
+  }
+  const int nblk = (int)gridDim.x - G.tree_leaves;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int64_t i = (int64_t)blockIdx.x * kGradThreads + t;
   float g = 0.f;
@@ -610,7 +617,7 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   __syncthreads();
   if (t == 0) {
     G.part[blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    G.part[gridDim.x + blockIdx.x] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    G.part[nblk + blockIdx.x] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
   if (blockIdx.x == 0 && wave == 1 && G.lossp_out) {
     float a = 0.f;
@@ -663,7 +670,12 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
   if (regen && P.tree_write && blockIdx.x == gridDim.x - 1) {  // block-uniform: the fused tree write
     __shared__ float red[16];
     __shared__ int sids[64];
-    batch_leaves_block(P.tree, P.bw, 1, red, sids);
+    if (P.tree_write == 2) {  // levels only: aql_grad_k wrote the leaves and the dirty list
+      for (int i = threadIdx.x; i < P.bw.B; i += blockDim.x) sids[i] = P.bw.list[i];
+      update_levels_block(P.tree, sids, P.bw.B, 1, P.tree.levels);
+    } else {
+      batch_leaves_block(P.tree, P.bw, 1, red, sids);
+    }
   } else {
     aql_post_block(P, regen, st);
   }
@@ -905,7 +917,9 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
     if (J.goff < 0 || J.goff + J.rows > aqlv::STRIDE || J.xoff + J.cols > aqlv::STRIDE)
       throw std::invalid_argument("aql_grad: vector offsets");
   }
-  aql_grad_k<<<aql_grad_blocks(g.n), kGradThreads, 0, s>>>(g);
+  if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || g.bw.E != 0 || !g.bw.idx || !g.bw.list))
+    throw std::invalid_argument("aql_grad: the split tree write takes 1..64 learner rows and no actor rows");
+  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), kGradThreads, 0, s>>>(g);
   LAUNCH_CHECK();
 }
 
@@ -913,7 +927,7 @@ void aql_post(const AqlPost& p, int regen, hipStream_t s) {
   int64_t n = regen ? p.n_copy : 0;
   for (int l = 0; l < 4; ++l) n += (int64_t)p.layer[l].out * p.layer[l].in + p.layer[l].out;
   const int extra = (regen && p.tree_write) ? 1 : 0;  // the fused tree-write workgroup
-  if (extra && (p.bw.B > 64 || p.bw.E != 0 || !p.bw.idx))
+  if (extra && (p.bw.B < 1 || p.bw.B > 64 || p.bw.E != 0 || (p.tree_write == 1 && !p.bw.idx) || !p.bw.list))
     throw std::invalid_argument("aql_post: the fused tree write takes <= 64 learner rows and no actor rows");
   aql_post_k<<<(int)((n + 255) / 256) + extra, 256, 0, s>>>(p, regen);
   LAUNCH_CHECK();

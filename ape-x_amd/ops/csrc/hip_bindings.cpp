@@ -757,6 +757,36 @@ PYBIND11_MODULE(_apex_hip, m) {
     p.bw = w;
     return p;
   });
+  m.def("aql_grad_set_tree", [](const AqlGrad& g0, const TreeHandle& t, uint64_t idx, int B, uint64_t delta,
+                                uint64_t lw, uint64_t prio_out, uint64_t loss_out, uint64_t owner, uint64_t list,
+                                uint64_t max_prio, float alpha) {
+    AqlGrad g = g0;
+    BatchWrite w{};
+    w.idx = P<const int>(idx);
+    w.B = B;
+    w.mix = PrioMix{P<const float>(delta), P<const float>(lw), P<float>(prio_out), P<float>(loss_out)};
+    w.owner = P<int>(owner);
+    w.list = P<int>(list);
+    w.max_prio = P<float>(max_prio);
+    w.alpha = alpha;
+    if (!w.idx || !w.mix.delta || !w.mix.lw || !w.owner || !w.list || !w.max_prio || B < 1 || B > 64)
+      throw std::invalid_argument("aql_grad_set_tree: 1 <= B <= 64 and every pointer");
+    g.tree_leaves = 1;
+    g.tree = t.d;
+    g.bw = w;
+    return g;
+  });
+  m.def("aql_post_set_levels", [](const AqlPost& p0, const TreeHandle& t, uint64_t list, int B) {
+    AqlPost p = p0;
+    BatchWrite w{};
+    w.list = P<int>(list);
+    w.B = B;
+    if (!w.list || B < 1 || B > 64) throw std::invalid_argument("aql_post_set_levels: 1 <= B <= 64 and a list");
+    p.tree_write = 2;
+    p.tree = t.d;
+    p.bw = w;
+    return p;
+  });
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

@@ -533,6 +533,12 @@ struct AqlGrad {
   double* part;        // [2][blocks] sum of squares per group
   const float* lossp;  // [B]
   float* lossp_out;    // [1] proposal loss mean
+  // split priority write (aql_grad_set_tree): one extra workgroup writes this step's leaves
+  // (per_write_batch's leaves part, B <= 64) and the dirty list; the noise-reset launch's
+  // extra workgroup then walks the levels (AqlPost::tree_write = 2)
+  int tree_leaves;
+  TreeDesc tree;
+  BatchWrite bw;
 };
 int aql_grad_blocks(int64_t n);
 void aql_grad(const AqlGrad& g, hipStream_t s);
@@ -552,7 +558,8 @@ struct AqlPost {
   uint64_t seed;
   // fused priority write (aql_post_set_tree): one extra workgroup of the regen launch runs
   // this step's batched tree write (per_write_batch's leaves + all levels, B <= 64) beside
-  // the noise reset -- neither reads what the other writes; the next step's sampling follows
+  // the noise reset -- neither reads what the other writes; the next step's sampling follows.
+  // tree_write = 2 (aql_post_set_levels): the levels only, the leaves ran in aql_grad_k
   int tree_write;
   TreeDesc tree;
   BatchWrite bw;

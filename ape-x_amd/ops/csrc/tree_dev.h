@@ -67,8 +67,78 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
 // workgroup reads what it wrote, so the barrier (workgroup-scope release / acquire) orders
 // the levels for workgroup-scope loads.  A device-scope __threadfence per level wrote the
 // XCD L2 back each time.
+// K candidates per wave (B <= K x waves, e.g. AQL's 32 rows: K = 8 on 4 waves, 2 on 16): a
+// wave's candidates load their 64 children together -- unconditional loads from clamped
+// addresses, selected after, so nothing serialises on a per-candidate wait -- then reduce:
+// one L2 round trip per level instead of one per candidate.  Same per-node arithmetic, so the
+// sums are bit-identical to the one-at-a-time loop.
+template <int K>
+__device__ __forceinline__ void update_levels_ilp(const TreeDesc& t, const int* sids, int B, int lo, int hi) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int level = lo; level <= hi; ++level) {
+    __syncthreads();
+    const int shift = kTreeLog2Fanout * level, csize = t.size[level - 1], n0 = t.size[0];
+    int node[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int w = wave + j * nw;
+      const int id = sids[min(w, B - 1)], prev = sids[max(min(w, B - 1) - 1, 0)];
+      const int nd = id >> shift;
+      const bool first = w == 0 || !(prev >= 0 && prev < n0 && (prev >> shift) == nd);
+      node[j] = (w < B && id >= 0 && id < n0 && first) ? nd : -1;
+    }
+    double s[K];
+    float m[K];
+    if (level == 1) {
+      float fs[K], fm[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int c = min(max(node[j], 0) * kTreeFanout + lane, csize - 1);
+        fs[j] = __hip_atomic_load(t.leaf_sum + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        fm[j] = __hip_atomic_load(t.leaf_min + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const bool ok = node[j] >= 0 && node[j] * kTreeFanout + lane < csize;
+        s[j] = ok ? (double)fs[j] : 0.0;
+        m[j] = ok ? fm[j] : INFINITY;
+      }
+    } else {
+      double ds[K];
+      float dm[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int c = min(max(node[j], 0) * kTreeFanout + lane, csize - 1);
+        ds[j] = __hip_atomic_load(t.node_sum[level - 2] + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        dm[j] = __hip_atomic_load(t.node_min[level - 2] + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const bool ok = node[j] >= 0 && node[j] * kTreeFanout + lane < csize;
+        s[j] = ok ? ds[j] : 0.0;
+        m[j] = ok ? dm[j] : INFINITY;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const double sj = wave_sum(s[j]);
+      const float mj = wave_min(m[j]);
+      if (node[j] >= 0 && lane == 0) {
+        t.node_sum[level - 1][node[j]] = sj;
+        t.node_min[level - 1][node[j]] = mj;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int* sids, int B, int lo, int hi) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // block-uniform dispatch on candidates per wave: the grouped loads pay from 3 per wave (the
+  // 256-thread AQL launches: 8); at 1-2 (per_batch_leaves_k's 16 waves) the loop below measured
+  // as fast
+  const int k = (B + nw - 1) / nw;
+  if (k >= 3 && k <= 4) return update_levels_ilp<4>(t, sids, B, lo, hi);
+  if (k >= 5 && k <= 8) return update_levels_ilp<8>(t, sids, B, lo, hi);
   for (int level = lo; level <= hi; ++level) {
     __syncthreads();
     const int shift = kTreeLog2Fanout * level;

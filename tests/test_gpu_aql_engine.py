@@ -272,17 +272,20 @@ def test_overlapped_acting_graphs_equal_eager(cuda):
 
 def test_fused_sampling_equals_per_sample(cuda):
     """The learner forward's own PER draw (fused_sample) == per_sample + forward, and the
-    priority write folded into the noise-reset launch (fused_tree) == its own launch: same
-    rows, IS weights, tree, loss and parameters after several iterations, bit for bit."""
+    priority write folded into the noise-reset launch (fused_tree) or split over the gradient
+    and noise-reset launches (split_tree) == its own launch: same rows, IS weights, tree, loss
+    and parameters after several iterations, bit for bit."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    for fused_sample, fused_tree in ((False, False), (True, False), (True, True)):
+    for fused_sample, fused_tree, split_tree in ((False, False, False), (True, False, False), (True, True, False),
+                                                 (True, False, True)):
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
-                              fused_sample=fused_sample, fused_tree=fused_tree)
+                              fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree)
         eng = AQLEngine(cfg, cuda)
         assert (eng.learner.Ls is not None) == fused_sample
         assert (eng.learner.post_tree is not None) == fused_tree
+        assert (eng.learner.G_tree is not None) == split_tree
         eng.fill(1024)
         for _ in range(5):
             eng.iteration()
