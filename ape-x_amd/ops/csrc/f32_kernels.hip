@@ -1597,24 +1597,36 @@ struct Conv2Dgrad {
 // added through LDS (fixed order) into partial g: ws[g][co][kk] + bias partials ws_b[g][co]
 // (sum of dy1 over the pixels), reduced over g by grad_finalize like the other layers.
 constexpr int kConv1WgradS = 2;  // samples per workgroup (partials = ceil(B / 2))
+// staging dump (dwords): the 512-thread chunk loop's tail past 2 samples' 3528 chunks
+constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) / 512) * 512 - kConv1WgradS * 4 * (kPlane / 16));
 __global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw];
+  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + kConv1WgradDump];
+  __shared__ int64_t wplanes[kConv1WgradS * 4];  // plane byte offsets from the frames base
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int j = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
   const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
   {  // stage both samples' planes: 2 x 4 x 441 16-byte chunks
     const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
     constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
+    // the 8 plane addresses once (frame_plane reads idx then ids: two dependent round trips,
+    // paid per chunk when resolved inside the loop below)
+    // (kept as offsets from the kernel-argument base: a pointer read back from LDS is a flat
+    // pointer, and flat loads may alias the LDS stores below -- each waited out before its store)
+    const uint8_t* fb = static_cast<const uint8_t*>(a.x);
+    if (t < kConv1WgradS * 4) wplanes[t] = frame_plane(f, b0 + min(t >> 2, ns - 1), t & 3, kPlane) - fb;
+    __syncthreads();
     uint4 v[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
-      v[i] = reinterpret_cast<const uint4*>(frame_plane(f, b0 + s2, ch, kPlane))[r - ch * 441];
+      v[i] = reinterpret_cast<const uint4*>(fb + wplanes[s2 * 4 + ch])[r - ch * 441];
     }
+    // unconditional stores (a guarded store sank its load into the branch: one round trip per
+    // chunk); the tail chunks past both samples land in the dump past the planes (and pad)
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = t + 512 * i;
-      if (e < ns * kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
+      reinterpret_cast<uint4*>(pl)[e < kConv1WgradS * kChunks ? e : e + 0] = v[i];
     }
   }
   __syncthreads();
@@ -1694,23 +1706,33 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
 // (4oy + (col >> 1)) * 21 + ox0 + jj + (col & 1) once per k-step; tile i takes byte i of
 // each (kx & 3 == i), so the 4 B fragments share one set of LDS reads.
 __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + 16];  // + pad: row-end groups
+  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + 16 + kConv1WgradDump];  // + pad: row-end groups
+  __shared__ int64_t wplanes[kConv1WgradS * 4];  // plane byte offsets from the frames base
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int col = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
   const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
   {  // stage both samples' planes (u8): 2 x 4 x 441 16-byte chunks
     const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
     constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
+    // the 8 plane addresses once (frame_plane reads idx then ids: two dependent round trips,
+    // paid per chunk when resolved inside the loop below)
+    // (kept as offsets from the kernel-argument base: a pointer read back from LDS is a flat
+    // pointer, and flat loads may alias the LDS stores below -- each waited out before its store)
+    const uint8_t* fb = static_cast<const uint8_t*>(a.x);
+    if (t < kConv1WgradS * 4) wplanes[t] = frame_plane(f, b0 + min(t >> 2, ns - 1), t & 3, kPlane) - fb;
+    __syncthreads();
     uint4 v[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
-      v[i] = reinterpret_cast<const uint4*>(frame_plane(f, b0 + s2, ch, kPlane))[r - ch * 441];
+      v[i] = reinterpret_cast<const uint4*>(fb + wplanes[s2 * 4 + ch])[r - ch * 441];
     }
+    // unconditional stores (a guarded store sank its load into the branch: one round trip per
+    // chunk); the tail chunks past both samples land in the dump past the planes (and pad)
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
       const int e = t + 512 * i;
-      if (e < ns * kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
+      reinterpret_cast<uint4*>(pl)[e < kConv1WgradS * kChunks ? e : e + 4] = v[i];
     }
     if (t < 16) pl[kConv1WgradS * 4 * kPlaneDw + t] = 0u;
   }
@@ -1724,19 +1746,34 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
   if (sl < ns) {
     const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
     const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (col >> 1) * 21 + (col & 1);
+    // dy of k-step ks + 1 is loaded while ks computes (unconditional loads from clamped pixel
+    // slots, zeroed after): loaded at their use, guarded, each k-step waited out one global
+    // round trip -- 15 per sample
+    float n0[8], n1[8];
+    auto load_dy = [&](int ks) {
+      const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
+      const float* dp = dy + (oy * 20 + ox0) * 32 + col;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int jc = min(jj, nv - 1);
+        n0[jj] = dp[jc * 32];
+        n1[jj] = dp[jc * 32 + 16];
+      }
+    };
+    load_dy(0);
     for (int ks = 0; ks < 15; ++ks) {
       const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy);
       const int nv = min(8, 20 - ox0);  // real pixels in this group (8 or 4)
       // A: dy[pixel][co] for the group's 8 slots, both co halves, split into 3 bf16 terms
       float d0[8], d1[8];
-      const float* dp = dy + (oy * 20 + ox0) * 32 + col;
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        d0[jj] = jj < nv ? dp[jj * 32] : 0.f;
-        d1[jj] = jj < nv ? dp[jj * 32 + 16] : 0.f;
+        d0[jj] = jj < nv ? n0[jj] : 0.f;
+        d1[jj] = jj < nv ? n1[jj] : 0.f;
         bs0 += d0[jj];
         bs1 += d1[jj];
       }
+      if (ks + 1 < 15) load_dy(ks + 1);
       bfx8 A[2][3];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
