@@ -135,11 +135,13 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   auto draw = [&](int b, int rt) {
     const int64_t f = L.filled[0];
     const int length = (int)(f < (int64_t)L.tree.size[0] ? f : (int64_t)L.tree.size[0]);
-    const int node = tree_sample_leaf(L.tree, b, L.B, length, L.exclude_last, L.seed, (uint64_t)L.ctr[0], lane);
+    const bool wr = rt == 0 && !tgt;
+    const float pmin = wr ? L.tree.node_min[L.tree.levels - 1][0] : 0.f, beta = wr ? L.beta[0] : 0.f;
+    float p;
+    const int node = tree_sample_leaf(L.tree, b, L.B, length, L.exclude_last, L.seed, (uint64_t)L.ctr[0], lane, &p);
     if (lane == 0) {
       srow = node;
-      if (rt == 0 && !tgt) {
-        const float p = L.tree.leaf_sum[node], pmin = L.tree.node_min[L.tree.levels - 1][0], beta = L.beta[0];
+      if (wr) {
         L.idx_out[b] = node;
         L.w_out[b] = (p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f;
       }

@@ -127,7 +127,9 @@ __device__ __forceinline__ double uniform_double(uint64_t seed, uint64_t stream,
 // own row (aql_engine_kernels.hip).
 template <class TD>
 __device__ __forceinline__ int tree_sample_leaf(const TD& t, int i, int B, int length, int exclude_last,
-                                                uint64_t seed, uint64_t ctr, int lane) {
+                                                uint64_t seed, uint64_t ctr, int lane, float* leaf_p = nullptr) {
+  // leaf_p: the drawn leaf's stored value (leaf_sum[node]), taken from the last level's
+  // children instead of a dependent re-read after the descent
   const int L = t.levels;
   double total = t.node_sum[L - 1][0];
   if (exclude_last && length > 0 && length <= t.size[0]) total -= (double)t.leaf_sum[length - 1];
@@ -138,7 +140,15 @@ __device__ __forceinline__ int tree_sample_leaf(const TD& t, int i, int B, int l
     const int child = node * 64 + lane;
     const int csize = t.size[level - 1];
     double v = 0.0;
-    if (child < csize) v = (level == 1) ? (double)t.leaf_sum[child] : t.node_sum[level - 2][child];
+    float raw = 0.f;
+    if (child < csize) {
+      if (level == 1) {
+        raw = t.leaf_sum[child];
+        v = (double)raw;
+      } else {
+        v = t.node_sum[level - 2][child];
+      }
+    }
     if (exclude_last && level == 1 && child == length - 1) v = 0.0;
     const double incl = wave_inclusive_scan(v, lane);
     unsigned long long hit = __ballot(incl > mass);
@@ -150,6 +160,7 @@ __device__ __forceinline__ int tree_sample_leaf(const TD& t, int i, int B, int l
       k = nz ? 63 - __clzll((long long)nz) : 0;
     }
     const double before = __shfl(incl - v, k, 64);
+    if (level == 1 && leaf_p) *leaf_p = __shfl(raw, k, 64);
     mass -= before;
     if (mass < 0.0) mass = 0.0;
     node = node * 64 + k;

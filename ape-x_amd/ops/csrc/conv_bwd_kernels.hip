@@ -648,8 +648,12 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
     if (!fs.sumsq) return;
     const int e0 = ((int)blockIdx.x - jb.block0) * kNormOnlyPer + threadIdx.x;
     float v[8];
+    // unconditional loads from clamped indices, zeroed after: guarded, each load compiled to a
+    // branch + wait (8 serial round trips per workgroup)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = e0 + 256 * k < jb.n_main ? jb.part[e0 + 256 * k] : 0.f;
+    for (int k = 0; k < 8; ++k) v[k] = jb.part[min(e0 + 256 * k, max(jb.n_main - 1, 0))];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = e0 + 256 * k < jb.n_main ? v[k] : 0.f;
     double q = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) q += (double)v[k] * (double)v[k];
@@ -686,11 +690,13 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   if (jb.G >= kWideG) {
     e = ((int)blockIdx.x - jb.block0) * 64 + lane;
     float s = 0.f;
+    // (16 slices per unrolled batch: the loads of a batch are in flight together, the adds
+    // stay in slice order)
     if (e < jb.n_main) {
-#pragma unroll 4
+#pragma unroll 16
       for (int g = wave; g < jb.G; g += 4) s += jb.part[(size_t)g * jb.pstride + e];
     } else if (e < total) {
-#pragma unroll 4
+#pragma unroll 16
       for (int g = wave; g < jb.G; g += 4) s += jb.bpart[(size_t)g * jb.bstride + (e - jb.n_main)];
     }
     red[wave][lane] = s;

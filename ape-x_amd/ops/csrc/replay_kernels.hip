@@ -212,9 +212,11 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
   const float beta = beta_ptr ? beta_ptr[0] : beta_const;
   const int L = t.levels;
   const uint64_t ctr = counter ? (uint64_t)counter[0] : 0ull;
-  const int node = tree_sample_leaf(t, i, B, length, exclude_last, seed, ctr, lane);
+  // the root min / global pair read before the descent (independent of it)
   float pmin = glob ? glob[0] : t.node_min[L - 1][0];
   float wscale = glob ? glob[1] : 1.f;
+  float p;
+  const int node = tree_sample_leaf(t, i, B, length, exclude_last, seed, ctr, lane, &p);
   if (sg.slots) {  // global min priority + k M_rank / sum M over the shards (world <= 64)
     const bool ok = lane < sg.world;
     const double m = wave_sum(ok ? (double)sg.slots[2 * lane] : 0.0);
@@ -222,7 +224,6 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
     wscale = (float)((double)sg.world * (double)sg.slots[2 * sg.rank] / fmax(m, 1e-300));
   }
   if (lane == 0) {
-    const float p = t.leaf_sum[node];
     out_idx[i] = node;
     out_w[i] = wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
   }
