@@ -1169,9 +1169,6 @@ __device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw,
 #pragma unroll
     for (int k = 0; k < GW; ++k) pacc[k] = acc[k];
     ptg = tg;
-    if constexpr (DBG) {  // the MFMA results are in flight until their first use
-      asm volatile("s_nop 0" ::: "memory");
-    }
     stamp(3);
   }
   store(ptg);
