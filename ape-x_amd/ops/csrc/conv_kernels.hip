@@ -248,9 +248,22 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
   }
   const HeadsProb& pr = set.p[pb];
   const float* __restrict__ z = pr.z;
-  for (int e = threadIdx.x; e < (A + 1) * 128; e += 256) {
-    const int a = e / 128, j = e % 128;
-    ws[a * 129 + j] = a < A ? pr.w_adv2[a * 128 + j] : pr.w_val2[j];
+  // head weights staged 8 loads at a time (a rolled load -> LDS store loop waits out one L2
+  // round trip per element: ~10 per thread before the first row)
+  const float* __restrict__ wa2 = pr.w_adv2;
+  const float* __restrict__ wv2 = pr.w_val2;
+  for (int e0 = threadIdx.x; e0 < (A + 1) * 128; e0 += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = min(e0 + 256 * u, (A + 1) * 128 - 1), a = e / 128, j = e % 128;
+      v[u] = a < A ? wa2[a * 128 + j] : wv2[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + 256 * u;
+      if (e < (A + 1) * 128) ws[(e / 128) * 129 + e % 128] = v[u];
+    }
   }
   const float bo = lane < A ? pr.b_adv2[lane] : (lane == A ? pr.b_val2[0] : 0.f);
   for (int rr = 0; rr < kHeadRows / 4; ++rr) {

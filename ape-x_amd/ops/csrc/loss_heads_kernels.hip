@@ -43,8 +43,17 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
   const int r0 = blockIdx.x * LH_ROWS, nr = min(LH_ROWS, B - r0);
   if (blockIdx.x == 0 && t == 0 && p.step_snap) p.step_snap[0] = p.step[0];
   if (t < 128) {
+    // 16 loads in flight per batch (the rolled loop waited out one L2 round trip per action:
+    // ~18 of them before the first row could start), summed in action order
     float c = 0.f;
-    for (int a = 0; a < A; ++a) c += p.w_adv2[a * 128 + t];
+    for (int a0 = 0; a0 < A; a0 += 16) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p.w_adv2[min(a0 + u, A - 1) * 128 + t];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (a0 + u < A) c += v[u];
+    }
     colsum[t] = c;
   }
   for (int e = t; e < A * 128; e += 64 * LH_WAVES) adv[e / 128][e % 128] = 0.f;
@@ -113,8 +122,13 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
   const int stride = (A + 1) * 128 + (A + 1) + 256;
   float* part = p.part + (size_t)blockIdx.x * stride;
   float S = 0.f, dsum = 0.f;
-  for (int r = 0; r < nr; ++r) {
-    const float hv = p.h[(size_t)(r0 + r) * 256 + t];
+  float hvs[LH_ROWS];  // every row's h loaded before the (row-ordered) accumulation
+#pragma unroll
+  for (int r = 0; r < LH_ROWS; ++r) hvs[r] = p.h[(size_t)(r0 + min(r, nr - 1)) * 256 + t];
+#pragma unroll
+  for (int r = 0; r < LH_ROWS; ++r) {
+    if (r >= nr) break;
+    const float hv = hvs[r];
     S += gs[r] * hv;
     if (t < 128) adv[as[r]][t] += gs[r] * hv;  // column t is this thread's alone
     dsum += dzs[r][t];
