@@ -121,7 +121,17 @@ struct NormInfo {
 __device__ NormInfo reduce_norms(const double* partials, int n_partials, float max_norm, float grad_scale) {
   __shared__ double red[4];
   double t = 0.0;
-  for (int k = threadIdx.x; k < n_partials; k += blockDim.x) t += partials[k];
+  // 4 loads in flight per round, added in the same (k-ascending) order as one at a time
+  const int bd = blockDim.x;
+  int k = threadIdx.x;
+  for (; k + 3 * bd < n_partials; k += 4 * bd) {
+    const double a0 = partials[k], a1 = partials[k + bd], a2 = partials[k + 2 * bd], a3 = partials[k + 3 * bd];
+    t += a0;
+    t += a1;
+    t += a2;
+    t += a3;
+  }
+  for (; k < n_partials; k += bd) t += partials[k];
   t = wave_sum(t);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
