@@ -47,6 +47,17 @@ void register_ipc(py::module_& m) {
     hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize");
     return U(p);
   }, py::arg("bytes"), py::arg("mode") = 2);
+  // multi-GPU preflight (parallel/preflight.py): can ``device`` map ``peer``'s memory (xGMI)?
+  m.def("device_can_access_peer", [](int device, int peer) {
+    int can = 0;
+    hip_ok(hipDeviceCanAccessPeer(&can, device, peer), "hipDeviceCanAccessPeer");
+    return can;
+  });
+  m.def("device_count", []() {
+    int n = 0;
+    hip_ok(hipGetDeviceCount(&n), "hipGetDeviceCount");
+    return n;
+  });
   m.def("ipc_free", [](uint64_t p) {
     if (p) hip_ok(hipFree(P<void>(p)), "hipFree");
   });

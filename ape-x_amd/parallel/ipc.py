@@ -269,9 +269,17 @@ class IpcLearnerLinks:
         for r in sorted(self.live):
             if not ack[r - 1]:
                 self.drop(r, "stop not acknowledged")
-        while time.monotonic() < deadline:
+        # every live actor acknowledged after its last push landed (finish() synchronises
+        # first): its ``sent`` is final -- apply up to it, on a deadline of its own
+        deadline = time.monotonic() + timeout
+        while True:
             done = self.applied()
-            if all(done[r] >= int(sent[r - 1]) for r in self.live):
+            short = {r: int(sent[r - 1]) - done[r] for r in sorted(self.live) if done[r] < int(sent[r - 1])}
+            if not short:
+                break
+            if time.monotonic() > deadline:
+                for r, k in short.items():  # never silent: the shortfall shows in stats()["dropped"]
+                    self.drop(r, f"drain timed out with {k} pushed packets unapplied")
                 break
             self.ingest(drain=True)
             torch.cuda.synchronize(self.device)
@@ -294,8 +302,9 @@ class IpcActorLink:
     newest parameter version, heartbeat, drop and stop."""
 
     def __init__(self, rank: int, store, prefix: str, flat: torch.Tensor, packet: torch.Tensor, device,
-                 heartbeat_every: float = 0.5, timeout: float = 300.0):
+                 heartbeat_every: float = 0.5, timeout: float = 300.0, credit_timeout: float = 120.0):
         self.hip = h = ops.hip()
+        self.credit_timeout = float(credit_timeout)
         self.rank, self.store, self.prefix = rank, store, prefix
         self.device = torch.device(device)
         self.flat, self.packet = flat, packet
@@ -347,18 +356,28 @@ class IpcActorLink:
             self.finish()
         return self.stopped
 
-    def push(self, timeout: float = 120.0) -> bool:
+    def push(self, timeout: float | None = None) -> bool:
         """Copy the packet into the next ring slot and publish its sequence number (both on
         the current stream, behind the actor step that filled it).  Waits (bounded) while
-        ``D`` packets are unconsumed; False if the link was stopped or dropped meanwhile."""
+        ``D`` packets are unconsumed.
+
+        The packet is already staged and the actor's local mirror already holds its rows, so
+        a *stop* seen while waiting does not abandon it: rank 0 keeps draining until every
+        live actor has acknowledged (IpcLearnerLinks.close), credit arrives, the packet is
+        pushed and the next :meth:`check_stop` acknowledges (the reference acks every push,
+        actor.py:105-115 / replay.py:94, so an accepted batch is never lost).  Only a *drop*
+        abandons it (rank 0 no longer ingests this link): then False."""
         n = self.sent
+        timeout = self.credit_timeout if timeout is None else float(timeout)
         deadline = time.monotonic() + timeout
         while n - int(self.consumed[self.i]) >= self.D:
             self.beat()
-            if self.check_stop():
+            if self.stopped or self.ctrl.view("drop")[self.i]:
+                self.check_stop()  # a drop: acknowledge and abandon the staged packet
                 return False
             if time.monotonic() > deadline:
-                raise TimeoutError(f"actor rank {self.rank}: no credit for {timeout}s")
+                raise TimeoutError(f"actor rank {self.rank}: no credit for {timeout:.0f}s "
+                                   f"(sent {n}, consumed {int(self.consumed[self.i])}, stop {self.ctrl.stop})")
             time.sleep(0.0001)
         k, s = n % self.D, self._s()
         slot = self.remote + (self.i * self.D + k) * self.pkt

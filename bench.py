@@ -85,8 +85,11 @@ def parse():
                     choices=["none", "pool", "probe", "dedicated", "priority-actor", "priority-learner"],
                     help="overlap mode: how the actor and learner streams get separate HW queues")
     ap.add_argument("--roctx", action="store_true", help="roctx ranges around engine phases (rocprofv3 --marker-trace)")
-    ap.add_argument("--topology", default="sharded", choices=["sharded", "central"],
-                    help="sharded: DP learner per GPU (default); central: rank 0 learner+replay, ranks 1.. actors")
+    ap.add_argument("--topology", default="auto", choices=["auto", "central", "sharded"],
+                    help="auto (default): one GPU = the single-GPU engine, N>1 = central (BASELINE config 3, the "
+                         "reference's design: rank 0 = the one learner at batch 512 + the replay, ranks 1.. = actor "
+                         "GPUs pushing experience over HIP IPC); sharded: a data-parallel learner per GPU sampling "
+                         "the shards as one global PER (global batch 512*N; value = sample throughput / 512)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"], help="gloo: host-staged (tests)")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (1-GPU rehearsal, gloo)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"],
@@ -113,11 +116,15 @@ def parse():
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
-    ap.add_argument("--launch-timeout", type=float, default=3000.0,
-                    help="--gpus N>1 without torch.distributed.run: wall limit of the self-launched ranks")
-    ap.add_argument("--watchdog", type=float, default=1500.0,
-                    help="seconds after which a rank dumps every thread's stack and exits 1 (0 = off): "
-                         "a hung collective ends the run with a traceback instead of a silent stall")
+    ap.add_argument("--launch-timeout", type=float, default=560.0,
+                    help="--gpus N>1 without torch.distributed.run: wall limit of the self-launched ranks "
+                         "(inside the driver's 600 s)")
+    ap.add_argument("--watchdog", type=float, default=240.0,
+                    help="no-progress limit in seconds (0 = off): re-armed at every phase and every few hundred "
+                         "steps; a rank that makes no progress for this long (a hung collective, IPC credit wait "
+                         "or peer copy) dumps every thread's stack and exits 1, inside the driver's 600 s")
+    ap.add_argument("--no-preflight", dest="preflight", action="store_false",
+                    help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
     ap.add_argument("--target-ahead", type=int, default=0, choices=[0, 1],
                     help="1: sample batch t+1 at the start of step t and run its target pass beside step t")
     ap.add_argument("--target-pass", default="actor", choices=["actor", "fork", "inline"],
@@ -150,6 +157,54 @@ def _host_launch_cost(eng, device, n: int = 20) -> float:
     return statistics.median(lat)
 
 
+class Watchdog:
+    """No-progress watchdog: ``kick()`` re-arms faulthandler's timer (stack dump of every
+    thread, then exit 1) -- a long healthy run is never killed, a stall is."""
+
+    def __init__(self, seconds: float):
+        self.s = float(seconds)
+        self._t = 0.0
+        self.kick()
+
+    def kick(self, every: float = 0.0) -> None:
+        if self.s <= 0:
+            return
+        now = time.monotonic()
+        if every and now - self._t < every:
+            return
+        self._t = now
+        import faulthandler
+
+        faulthandler.dump_traceback_later(self.s, exit=True)
+
+    def off(self) -> None:
+        if self.s > 0:
+            import faulthandler
+
+            faulthandler.cancel_dump_traceback_later()
+
+
+def select_topology(topology: str, world: int) -> str:
+    """auto: "single" for one rank, "central" (BASELINE config 3) for more."""
+    if topology == "auto":
+        return "central" if world > 1 else "single"
+    if topology == "central" and world < 2:
+        raise SystemExit("--topology central needs >= 2 ranks")
+    return topology if world > 1 else "single"
+
+
+def run_preflight(args, topo: str, device, wd: "Watchdog") -> dict | None:
+    """N>1: prove peer access, the IPC round trip and the collective before timing."""
+    if not args.preflight:
+        return None
+    from apex_amd.parallel import preflight
+
+    ipc = topo == "central" and args.transport in ("auto", "ipc")
+    rep = preflight.run(device, ipc=ipc, timeout=90.0)
+    wd.kick()
+    return rep
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -160,10 +215,7 @@ def main():
 
         sys.exit(run_ranks([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], args.gpus,
                            timeout=args.launch_timeout))
-    if args.watchdog > 0:
-        import faulthandler
-
-        faulthandler.dump_traceback_later(args.watchdog, exit=True)
+    wd = Watchdog(args.watchdog)
     import torch
     import torch.distributed as dist
 
@@ -184,7 +236,8 @@ def main():
         local_rank = 0
     torch.cuda.set_device(local_rank)
     device = torch.device("cuda", local_rank)
-    if args.reserve and args.topology == "sharded":
+    topo = select_topology(args.topology, world)
+    if args.reserve and topo != "central":
         from apex_amd.engine.apex import reserve_actor_stream
 
         reserve_actor_stream(device)  # before the process group draws its pool streams
@@ -194,10 +247,12 @@ def main():
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
-    if args.topology == "central":
-        return central(args, rank, world, device)
+    wd.kick()
+    pre = run_preflight(args, topo, device, wd) if world > 1 else None
     if args.algo == "aql":
         return aql(args, rank, world, device)
+    if topo == "central":
+        return central(args, rank, world, device, wd, pre)
 
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
@@ -247,11 +302,14 @@ def main():
     eng.fill(args.capacity + 8 * args.envs if args.fill else args.threshold)
     torch.cuda.synchronize(device)
     t_fill = time.perf_counter() - t_fill
+    wd.kick()
     if not args.no_graphs:
         eng.capture()
+    wd.kick()
     for _ in range(args.warmup):
         eng.train_step()
     torch.cuda.synchronize(device)
+    wd.kick()
 
     if world > 1:
         dist.barrier()
@@ -271,9 +329,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    wd.kick()
     for _ in range(args.profile_steps):
         eng.train_step()
     torch.cuda.synchronize(device)
+    wd.off()
 
     rccl_ranks = allreduce.comm.count() if isinstance(allreduce, _Rccl) else None
     stats = eng.learner.stats()
@@ -285,7 +345,10 @@ def main():
         out = {
             "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
             "value": round(batches_per_s, 3),
-            "unit": "learner batches of 512 sampled transitions per second, whole job (= SGD steps/s at N=1)",
+            "unit": ("learner batches of 512 sampled transitions per second, whole job (= SGD steps/s at N=1)"
+                     if world == 1 else
+                     f"sampled transitions/s / 512 of {world} data-parallel learners at global batch {512 * world} "
+                     f"(sample throughput, NOT single-learner SGD steps/s: see optimizer_updates_per_s)"),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -414,11 +477,14 @@ def aql(args, rank, world, device):
         dist.destroy_process_group()
 
 
-def central(args, rank, world, device):
-    """Central-replay topology, asynchronous: rank 0 = learner + the one replay, ranks 1.. =
-    actor GPUs pushing experience over their own links (credit window 3, conflated
-    params).  ``value`` = learner SGD steps/s (one learner, batch 512, strong scaling);
-    actor frames/s = frames that reached the replay during the timed window."""
+def central(args, rank, world, device, wd, pre=None):
+    """Central-replay topology (BASELINE config 3; the default for N>1), asynchronous:
+    rank 0 = THE learner (batch 512, the reference's single learner, origin_repo/learner.py:
+    134-175) + the one replay, ranks 1.. = actor GPUs pushing experience over their own
+    HIP IPC links (credit window 3, conflated params; origin_repo/actor.py:105-115).
+    ``value`` = learner SGD steps/s (one learner, batch 512: global work per step fixed ->
+    "strong"); actor frames/s = frames that reached the replay during the timed window.
+    Only rank 0 takes timed steps; the actor ranks act continuously until it stops them."""
     import torch
     import torch.distributed as dist
 
@@ -433,23 +499,27 @@ def central(args, rank, world, device):
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
     eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport)
+    wd.kick()
     if rank != 0:  # actor GPU: act and push until the learner stops this link
         if not args.no_graphs:
             eng.capture()
         while eng.train_step():
-            pass
+            wd.kick(every=5.0)
         torch.cuda.synchronize(device)
+        wd.off()
         dist.destroy_process_group()
         return
     t_fill = time.perf_counter()
-    eng.fill()
+    eng.fill(timeout=300.0)
     torch.cuda.synchronize(device)
     t_fill = time.perf_counter() - t_fill
+    wd.kick()
     if not args.no_graphs:
         eng.capture()
     for _ in range(args.warmup):
         eng.train_step()
     torch.cuda.synchronize(device)
+    wd.kick()
     a0 = sum(eng.applied.values())
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -457,7 +527,9 @@ def central(args, rank, world, device):
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     packets = sum(eng.applied.values()) - a0
+    wd.kick()
     links = eng.close()
+    wd.off()
     st = eng.learner.stats()
     steps_per_s = args.steps / dt
     print(json.dumps({
@@ -476,6 +548,9 @@ def central(args, rank, world, device):
         "actor_frames_per_sec": round(packets * eng.frames_per_actor_step / dt, 1),
         "packets_applied_per_learner_step": round(packets / args.steps, 3),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
+        "links_complete": all(links["applied"][r] == links.get("sent", {}).get(r, links["applied"][r]) for r in links["live"]),
+        "preflight": pre,
+        "timing": "rank 0 (the one learner) between two device syncs; actor ranks act continuously",
         "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
     }), flush=True)
     dist.destroy_process_group()

@@ -237,6 +237,89 @@ def _central_body(rank, world, steps, dead_after, min_seconds=0.0, transport="ip
     return res
 
 
+def _stop_while_credit_blocked_body(rank, world, killed):
+    """Rank 0 never ingests until the stop, so every live actor fills its D-packet window,
+    stages one more step (its local mirror already holds it) and blocks on credit.  Rank 0
+    waits until that is so -- ``sent == D`` and the heartbeat, bumped only inside the
+    credit wait from then on, has moved twice -- optionally drops the killed peer, and
+    stops.  The staged packet must still reach the replay."""
+    import time
+
+    import torch.distributed as dist
+
+    from apex_amd.engine.central import CentralApexEngine
+
+    dev = torch.device("cuda", 0)
+    eng = CentralApexEngine(_central_cfg(), dev, rank, world, dead_after=1.0, heartbeat_every=0.02,
+                            transport="ipc")
+    if rank != 0:
+        eng.capture()
+        while eng.train_step():
+            pass
+        torch.cuda.synchronize(dev)
+        rp = eng.replay
+        for t in (rp.s_ids.cpu(), rp.s2_ids.cpu(), rp.action.cpu(), rp.reward.cpu(), rp.done.cpu(), rp.frames.cpu()):
+            dist.send(t, 0)
+        return {"actor_steps": eng.actor_steps, "sent": eng.link.n_sent}
+    L = eng.links
+    sent, hb = L.ctrl.view("sent"), L.ctrl.view("heartbeat")
+    deadline = time.monotonic() + 120
+    blocked = set()
+    for r in range(1, world):
+        if r in killed:
+            continue
+        while int(sent[r - 1]) < L.D:
+            assert time.monotonic() < deadline, f"actor {r} never filled its window"
+            time.sleep(0.005)
+        h0 = int(hb[r - 1])
+        while int(hb[r - 1]) < h0 + 2:
+            assert time.monotonic() < deadline, f"actor {r} not waiting for credit"
+            time.sleep(0.005)
+        blocked.add(r)
+    for r in killed:  # its heartbeat stops: dropped before the stop
+        while r in L.live:
+            assert time.monotonic() < deadline, f"dead actor {r} never dropped"
+            L.check_heartbeats(every=0.0)
+            time.sleep(0.05)
+    consumed_before = {r: int(L.ctrl.view("consumed")[r - 1]) for r in blocked}
+    links = eng.close()
+    rp = eng.replay
+    mism = {}
+    for r in sorted(links["live"]):
+        reg = eng.regions[r]
+        C, F = reg.n_slots, reg.n_frames
+        mine = [torch.empty_like(rp.s_ids[:C].cpu()), torch.empty_like(rp.s2_ids[:C].cpu()),
+                torch.empty_like(rp.action[:C].cpu()), torch.empty_like(rp.reward[:C].cpu()),
+                torch.empty_like(rp.done[:C].cpu()), torch.empty_like(rp.frames[:F].cpu())]
+        for t in mine:
+            dist.recv(t, r)
+        s0, f0 = reg.slot_base, reg.frame_base
+        bad = [n for n, a, b in (("s_ids", rp.s_ids[s0:s0 + C].cpu(), mine[0] + f0),
+                                 ("s2_ids", rp.s2_ids[s0:s0 + C].cpu(), mine[1] + f0),
+                                 ("action", rp.action[s0:s0 + C].cpu(), mine[2]),
+                                 ("reward", rp.reward[s0:s0 + C].cpu(), mine[3]),
+                                 ("done", rp.done[s0:s0 + C].cpu(), mine[4]),
+                                 ("frames", rp.frames[f0:f0 + F].cpu(), mine[5])) if not torch.equal(a, b)]
+        mism[r] = bad
+    return {"links": links, "mismatch": mism, "blocked": sorted(blocked), "consumed_before": consumed_before}
+
+
+@pytest.mark.parametrize("killed", [(), (2,)], ids=["no-drop", "dropped-peer"])
+def test_central_stop_while_actor_credit_blocked_loses_nothing(cuda, killed):
+    world = 3 if killed else 2
+    env = {"APEX_FAULT": "actor2:kill@1"} if killed else {}
+    out, codes = _run(_stop_while_credit_blocked_body, world, (killed,), env=env, timeout=200)
+    o = out[0]
+    assert o["blocked"] == [1] and o["consumed_before"] == {1: 0}
+    assert o["links"]["live"] == [1] and set(o["links"]["dropped"]) == set(killed)
+    # the reset packet + every actor step, INCLUDING the one staged while credit-blocked
+    assert o["links"]["applied"][1] == o["links"]["sent"][1] == out[1]["actor_steps"] + 1 == out[1]["sent"]
+    assert out[1]["actor_steps"] >= o["links"]["sent"][1] - 1 >= 3
+    assert o["mismatch"] == {1: []}, o["mismatch"]
+    if killed:
+        assert codes[2] == 17
+
+
 @pytest.mark.parametrize("transport", ["ipc", "p2p"])
 def test_central_two_ranks_every_row_reaches_the_replay(cuda, transport):
     out, codes = _run(_central_body, 2, (40, 30.0, 0.0, transport))

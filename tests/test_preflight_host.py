@@ -1,0 +1,149 @@
+"""Multi-GPU preflight (parallel/preflight.py) on CPU: every check and every failure
+message, driven with fakes of the HIP calls (peer-access query, IPC export / open, peer
+write, readback) and of the collective; ranks run as threads over an in-memory store.
+The real path runs on the GPU box (bench.py --same-device, tests/test_gpu_multirank.py)."""
+import ctypes
+import threading
+import time
+
+import pytest
+
+from apex_amd.parallel import preflight as pf
+
+
+class FakeStore:
+    def __init__(self):
+        self.d, self.cv = {}, threading.Condition()
+
+    def set(self, k, v):
+        with self.cv:
+            self.d[k] = v.encode() if isinstance(v, str) else bytes(v)
+            self.cv.notify_all()
+
+    def get(self, k):
+        with self.cv:
+            return self.d[k]
+
+    def check(self, keys):
+        with self.cv:
+            return all(k in self.d for k in keys)
+
+    def wait(self, keys, timeout):
+        end = time.monotonic() + timeout.total_seconds()
+        with self.cv:
+            while not all(k in self.d for k in keys):
+                left = end - time.monotonic()
+                if left <= 0:
+                    raise RuntimeError("Socket Timeout")
+                self.cv.wait(left)
+
+
+class FakeHip:
+    """'Device' memory is host memory (ctypes buffers): hipMemcpy = memmove, and an IPC
+    handle is the arena's address (all ranks share this process)."""
+
+    def __init__(self, peer=1, open_error=None, corrupt_rank=None, count=None):
+        self.peer, self.open_error, self.corrupt_rank = peer, open_error, corrupt_rank
+        self.bufs, self.opened, self.freed = {}, [], []
+
+    def device_can_access_peer(self, a, b):
+        return self.peer
+
+    def ipc_alloc(self, n, mode):
+        assert mode == pf.MODE_UNCACHED
+        b = ctypes.create_string_buffer(n)
+        self.bufs[ctypes.addressof(b)] = b
+        return ctypes.addressof(b)
+
+    def ipc_handle(self, p):
+        return str(p).encode()
+
+    def ipc_open(self, h, device):
+        if self.open_error:
+            raise RuntimeError(self.open_error)
+        p = int(h)
+        self.opened.append((p, device))
+        return p
+
+    def ipc_close(self, p):
+        pass
+
+    def ipc_free(self, p):
+        self.freed.append(p)
+
+    def memcpy_sync(self, dst, src, n):
+        ctypes.memmove(dst, src, n)
+        if self.corrupt_rank is not None and dst in {a + self.corrupt_rank * pf.BLOCK for a in self.bufs}:
+            ctypes.memset(dst + 7, 0, 3)  # a peer write that lands wrong
+
+
+def _ranks(world, fn):
+    out, errs = {}, {}
+
+    def run(r):
+        try:
+            out[r] = fn(r)
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(30)
+    return out, errs
+
+
+def test_ipc_round_trip_ok_and_arena_freed():
+    hip, st = FakeHip(), FakeStore()
+    out, errs = _ranks(4, lambda r: pf.check_ipc(hip, st, r, 4, r, "t", 5.0))
+    assert not errs and out[0] == {"ipc": "ok", "blocks": 3}
+    assert sorted(d for _, d in hip.opened) == [1, 2, 3]  # each actor opened on its own device
+    assert len(hip.freed) == 1
+
+
+def test_ipc_bad_peer_write_is_named_on_every_rank():
+    hip, st = FakeHip(corrupt_rank=2), FakeStore()
+    out, errs = _ranks(3, lambda r: pf.check_ipc(hip, st, r, 3, r, "t", 5.0))
+    assert set(errs) == {0, 1, 2}  # every rank fails alike (no rank goes on to time a broken job)
+    assert "read back 3 of 4096 bytes wrong from rank 2" in str(errs[0])
+    assert "for this rank" in str(errs[2]) and "on rank(s) [2]" in str(errs[1])
+
+
+def test_ipc_open_failure_is_reported_by_rank_zero():
+    hip, st = FakeHip(open_error="hipIpcOpenMemHandle: invalid argument"), FakeStore()
+    out, errs = _ranks(2, lambda r: pf.check_ipc(hip, st, r, 2, r, "t", 5.0))
+    assert set(errs) == {0, 1}
+    assert "rank 1 on GPU 1: RuntimeError: hipIpcOpenMemHandle: invalid argument" in str(errs[0])
+
+
+def test_ipc_missing_rank_times_out_with_its_key():
+    hip, st = FakeHip(), FakeStore()
+    with pytest.raises(pf.PreflightError, match=r"IPC peer writes: timed out after 0s.*wrote/2"):
+        pf.check_ipc(hip, st, 0, 3, 0, "t", 0.3)  # no rank 1 / 2 ever writes
+
+
+def test_peer_access():
+    assert pf.check_peer_access(FakeHip(), 1, 0, 0)["peer_access"] == "same device"
+    assert pf.check_peer_access(FakeHip(), 3, 3, 0)["peer_access"] is True
+    with pytest.raises(pf.PreflightError, match=r"rank 2: GPU 2 cannot access peer GPU 0 \(hipDeviceCanAccessPeer = 0\)"):
+        pf.check_peer_access(FakeHip(peer=0), 2, 2, 0)
+
+
+def test_collective_checks():
+    world = 4
+
+    def summed(vec):
+        return [1] * len(vec)
+
+    assert pf.check_collective(1, world, summed, lambda: 4) == {"allreduce": "ok", "rccl_comm_count": 4}
+    with pytest.raises(pf.PreflightError, match=r"gave \[1, 0, 1, 1\] \(ranks \[1\] missing"):
+        pf.check_collective(0, world, lambda v: [1, 0, 1, 1])
+    with pytest.raises(pf.PreflightError, match="ncclCommCount = 2, world size = 4"):
+        pf.check_collective(0, world, summed, lambda: 2)
+    with pytest.raises(pf.PreflightError, match="all-reduce failed: RuntimeError: boom"):
+        pf.check_collective(0, world, lambda v: (_ for _ in ()).throw(RuntimeError("boom")))
+
+
+def test_pattern_is_rank_tagged():
+    assert pf.pattern(1) != pf.pattern(2) and len(pf.pattern(5)) == pf.BLOCK and any(pf.pattern(0))
