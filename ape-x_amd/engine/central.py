@@ -194,9 +194,9 @@ class CentralApexEngine:
     # ------------------------------------------------------------------ actor ranks
     def _stage_packet(self, initial: bool = False) -> None:
         a, rp = self.actor, self.replay
-        if initial:  # reset frames only: no transition rows (priority 0)
+        if initial:  # reset frames only: every row is a filler (slot -1: no transition row is written)
             z = torch.zeros(self.E, dtype=torch.float32, device=self.device)
-            slot = torch.arange(self.E, dtype=torch.int32, device=self.device)
+            slot = torch.full((self.E,), -1, dtype=torch.int32, device=self.device)
             pack_meta(a.st["hist"], a.st["hist"], a.actions, z, z, z, slot, a.new_frame, out=self.pkt_meta)
         else:
             sl = a.slot.long()

@@ -16,11 +16,12 @@
 //       ipc_scan_k    : per link, how many packets are ready in order from consumed[r]
 //                       (system-scope acquire loads of seq; capped per link = pacing);
 //       ipc_apply_k   : scatters every ready packet's frames and rows into the link's region
-//                       of the HBM replay, and emits (global slot | -1, priority) pairs for
-//                       the tree write (per_write_* skip slot -1);
+//                       of the HBM replay, emits (global slot | -1, priority) pairs for
+//                       the tree write (per_write_* skip slot -1) and advances the replay's
+//                       fill counter by the real rows (filler rows, slot -1, carry frames only);
 //       ipc_release_k : consumed[r] += ready[r], published to the host control block
 //                       (system-scope store into hipHostRegister'ed /dev/shm, which the actor
-//                       processes read as their credit) and the replay's fill counter.
+//                       processes read as their credit).
 //     No host polling and no host sync: the whole ingest is four captured launches.
 //   * parameters: rank 0 copies the master weights into params[v & 1] on its stream, then
 //     ipc_flag_k publishes v to the control block; actors read v there and pull the slot
@@ -89,6 +90,11 @@ __global__ __launch_bounds__(256) void ipc_apply_k(IpcIngest g) {
     const int e = e0 + t;
     const int32_t* m = meta + e * kMetaCols;
     const int32_t ls = m[12];
+    // replay fill counter: transition rows written (filler rows, e.g. the reset-frame
+    // packet's, carry frames only); one atomic per block from the first lane
+    const unsigned long long real = __ballot(ls >= 0) & ((1ull << kRows) - 1);
+    if (t == 0 && g.filled && real)
+      atomicAdd(reinterpret_cast<unsigned long long*>(g.filled), (unsigned long long)__popcll(real));
     if (ls < 0) {
       g.slots_out[out0 + t] = -1;
       return;
@@ -108,9 +114,7 @@ __global__ __launch_bounds__(256) void ipc_apply_k(IpcIngest g) {
 }
 
 __global__ void ipc_release_k(IpcIngest g) {
-  __shared__ int64_t total;
-  if (threadIdx.x == 0) total = 0;
-  __syncthreads();
+  // (the replay's fill counter is advanced per real transition row by ipc_apply_k)
   const int r = threadIdx.x;
   if (r < g.R) {
     const int n = g.ready[r];
@@ -119,10 +123,7 @@ __global__ void ipc_release_k(IpcIngest g) {
     if (g.applied) g.applied[r] += n;
     // the ring slots are free again: the actor processes read this word as their credit
     if (g.host_consumed) store_release_sys(g.host_consumed + r, c);
-    if (n) atomicAdd(reinterpret_cast<unsigned long long*>(&total), (unsigned long long)n);
   }
-  __syncthreads();
-  if (threadIdx.x == 0 && g.filled && total) g.filled[0] += total * g.E;
 }
 
 __global__ void ipc_flag_k(int64_t* p, int64_t v) {

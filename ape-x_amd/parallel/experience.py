@@ -100,14 +100,21 @@ def apply_packets(tables: dict, frames: torch.Tensor, meta: torch.Tensor, frame_
     fb = frame_base.repeat_interleave(E)
     sb = slot_base.repeat_interleave(E)
     tables["frames"].index_copy_(0, m[:, 13].long() + fb, frames.reshape(n * E, -1))
-    slot = m[:, 12].long() + sb
+    local = m[:, 12].long()
+    slot = local + sb
+    real = local >= 0  # filler rows (slot -1, e.g. the reset-frame packet) carry frames only
     ids = m[:, 0:8] + fb.to(torch.int32).unsqueeze(1)
-    tables["s_ids"].index_copy_(0, slot, ids[:, 0:4].contiguous())
-    tables["s2_ids"].index_copy_(0, slot, ids[:, 4:8].contiguous())
-    tables["action"].index_copy_(0, slot, m[:, 8].contiguous())
-    tables["reward"].index_copy_(0, slot, m[:, 9].contiguous().view(torch.float32))
-    tables["done"].index_copy_(0, slot, m[:, 10].contiguous().view(torch.float32))
-    return slot.to(torch.int32), m[:, 11].contiguous().view(torch.float32)
+    rows = (ids[:, 0:4], ids[:, 4:8], m[:, 8], m[:, 9].contiguous().view(torch.float32),
+            m[:, 10].contiguous().view(torch.float32))
+    if not bool(real.all()):  # eager path only (host-staged links): a data-dependent subset
+        keep = real.nonzero().squeeze(1)
+        rows = tuple(t.index_select(0, keep) for t in rows)
+        dst = slot.index_select(0, keep)
+    else:
+        dst = slot
+    for name, t in zip(("s_ids", "s2_ids", "action", "reward", "done"), rows):
+        tables[name].index_copy_(0, dst, t.contiguous())
+    return torch.where(real, slot, -1).to(torch.int32), m[:, 11].contiguous().view(torch.float32)
 
 
 def _via_host(device: torch.device, group) -> bool:
@@ -596,7 +603,8 @@ class LearnerLinks:
             deadline = time.monotonic() + timeout
             while ib.n_done < need and not ib.dead and time.monotonic() < deadline:
                 ks = ib.poll()
-                real = [(r, k) for k in ks if int(self.meta[r - 1, k, 0, 12].item()) >= 0]  # fillers: slot -1
+                # filler packets are all -1 (no frame slot either; the reset-frame packet has frames)
+                real = [(r, k) for k in ks if int(self.meta[r - 1, k, 0, 13].item()) >= 0]
                 if real:
                     self.apply_fn(real)
                     self.applied[r] += len(real)

@@ -349,3 +349,29 @@ def test_central_links_async_drop_dead_actor(world):
     idle = out[0]["idle_poll_us"]  # None when every poll of the run found a packet waiting
     print(f"\nworld {world}: rank-0 link layer {out[0]['links_us_per_iter']:.1f} us/iteration "
           f"(idle poll of {world - 1} links: {'n/a' if idle is None else f'{idle:.1f} us'} median)")
+
+
+def test_apply_packets_filler_rows_write_frames_only():
+    """A reset-frame packet (slot -1 rows) lands its frames but no transition row, and its
+    tree-write slots come back as -1 (skipped)."""
+    import torch
+
+    from apex_amd.parallel.experience import META_COLS, apply_packets, pack_meta
+
+    E, FB = 4, 16
+    tables = {"frames": torch.zeros(32, FB, dtype=torch.uint8), "s_ids": torch.full((8, 4), 7, dtype=torch.int32),
+              "s2_ids": torch.full((8, 4), 7, dtype=torch.int32), "action": torch.full((8,), 7, dtype=torch.int32),
+              "reward": torch.full((8,), 7.0), "done": torch.full((8,), 7.0)}
+    z = torch.zeros(E)
+    ids = torch.arange(4 * E, dtype=torch.int32).view(E, 4)
+    fill = pack_meta(ids, ids, torch.ones(E, dtype=torch.int32), z, z, z, torch.full((E,), -1, dtype=torch.int32),
+                     torch.arange(E, dtype=torch.int32))
+    real = pack_meta(ids, ids, torch.ones(E, dtype=torch.int32), z + 1, z, z + 0.5, torch.arange(E, dtype=torch.int32),
+                     torch.arange(E, 2 * E, dtype=torch.int32))
+    frames = torch.arange(2 * E * FB, dtype=torch.int64).remainder(251).to(torch.uint8).view(2, E, FB)
+    meta = torch.stack([fill, real]).view(2, E, META_COLS)
+    slots, prio = apply_packets(tables, frames, meta, torch.tensor([8, 8]), torch.tensor([4, 0]))
+    assert slots[:E].tolist() == [-1] * E and slots[E:].tolist() == [0, 1, 2, 3]
+    assert torch.equal(tables["frames"][8:16], frames.view(2 * E, FB))  # both packets' frames landed
+    assert (tables["action"][4:] == 7).all() and (tables["action"][:4] == 1).all()  # filler rows untouched
+    assert torch.equal(tables["s_ids"][:4], ids + 8) and (tables["s_ids"][4:] == 7).all()
