@@ -551,11 +551,25 @@ class AQLEngine:
         self.hip.copy_f32(self.actor_flat.data_ptr(), self.learner.flat.data_ptr(), self.learner.P, s)
         self.hip.copy_f32(self.actor_eps.data_ptr(), self.learner.eps.data_ptr(), self.learner.eps.numel(), s)
 
-    def actor_step(self, half: int | None = None) -> None:
+    def actor_step(self, half: int | None = None, into=None) -> None:
         """One acting step of all E envs.  ``half`` (overlap mode): write the transitions into
-        staging half ``half`` instead of the ring (see :meth:`apply_staged`)."""
+        staging half ``half`` instead of the ring (see :meth:`apply_staged`); ``into``: an
+        ``AqlInsert`` of E rows (C = E) to write them to instead -- e.g. a central-topology
+        actor rank's packet buffer (engine.central_aql); no tree write then."""
         self.learner.join()  # the actor's tree writes follow the learner's forked one
         h, s, E, r = self.hip, self._s(), self.E, self.replay
+        self._act(h, s, E)
+        if into is not None or half is not None:
+            dst = into if into is not None else self._stage_ins[half]
+            h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(), dst, s)
+            self.actor_ctr.add_(1)  # the acting RNG counter (per_write_leaves bumps it otherwise)
+            return
+        h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(), self.ins, s)
+        h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
+                           r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
+
+    def _act(self, h, s, E) -> None:
+        """Proposal, candidate Q and epsilon-greedy selection for all E envs."""
         h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
                       self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s)
         if self.cfg.act_q == "mfma":
@@ -566,14 +580,6 @@ class AQLEngine:
                               self.qbuf.data_ptr(), s)
         h.aql_select(self.qbuf.data_ptr(), self.amu.data_ptr(), E, self.T, self.adim, self.eps.data_ptr(),
                      self.seed ^ 0xA9C1, self.actor_ctr.data_ptr(), self.act_idx.data_ptr(), self.env_act.data_ptr(), s)
-        if half is not None:
-            h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(),
-                           self._stage_ins[half], s)
-            self.actor_ctr.add_(1)  # the acting RNG counter (per_write_leaves bumps it otherwise)
-            return
-        h.aql_env_step(self.env, self.env_act.data_ptr(), self.act_idx.data_ptr(), self.amu.data_ptr(), self.ins, s)
-        h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
-                           r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
 
     def apply_staged(self, half: int) -> None:
         """Overlap mode, learner stream: staging half ``half`` -> the ring at max priority."""

@@ -137,8 +137,8 @@ class CentralApexEngine:
     def _setup_learner_links(self, dead_after: float) -> None:
         R, D, E, dev = self.R, self.depth, self.E, self.device
         if self.transport == "ipc":
-            self.links = IpcLearnerLinks(R, D, E, self.flat.numel(), self.replay, self.regions, self.store,
-                                         self.prefix, dev, cap=self.ingest_cap, dead_after=dead_after)
+            self.links = IpcLearnerLinks.for_dqn(R, D, E, self.flat.numel(), self.replay, self.regions, self.store,
+                                                 self.prefix, dev, cap=self.ingest_cap, dead_after=dead_after)
             return
         self.rx_frames = torch.empty(R, D, E, FRAME_BYTES, dtype=torch.uint8, device=dev)
         self.rx_meta = torch.empty(R, D, E, META_COLS, dtype=torch.int32, device=dev)

@@ -105,6 +105,20 @@ void register_ipc(py::module_& m) {
     auto& g = h.g;
     auto i = [&](const char* k) { return d[k].cast<int64_t>(); };
     auto p = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
+    g.kind = d.contains("kind") ? (int)i("kind") : 0;
+    g.prefix = P<int>(p("prefix"));
+    if (g.kind == 1) {
+      g.obs = (int)i("obs");
+      g.TA = (int)i("TA");
+      g.aql.st = P<float>(p("aql_st"));
+      g.aql.st2 = P<float>(p("aql_st2"));
+      g.aql.amu = P<float>(p("aql_amu"));
+      g.aql.act = P<int>(p("aql_act"));
+      g.aql.rew = P<float>(p("aql_rew"));
+      g.aql.done = P<float>(p("aql_done"));
+      g.aql.C = i("aql_C");
+      g.aql.filled = P<const int64_t>(p("filled"));
+    }
     g.R = (int)i("R");
     g.D = (int)i("D");
     g.E = (int)i("E");

@@ -23,6 +23,8 @@
 //                       (system-scope store into hipHostRegister'ed /dev/shm, which the actor
 //                       processes read as their credit).
 //     No host polling and no host sync: the whole ingest is four captured launches.
+//   * AQL packets (kind 1, parallel/ipc.py AQL_PACKET): rows appended in (link, packet) order to
+//     the ONE replay ring at its cursor, then a max-priority leaf write (AQL_dis.py:120-123).
 //   * parameters: rank 0 copies the master weights into params[v & 1] on its stream, then
 //     ipc_flag_k publishes v to the control block; actors read v there and pull the slot
 //     (seqlock check on the version around the copy).
@@ -45,10 +47,10 @@ __device__ __forceinline__ void store_release_sys(int64_t* p, int64_t v) {
 }
 
 __global__ void ipc_scan_k(IpcIngest g) {
+  __shared__ int nready[1024];
   const int r = threadIdx.x;
-  if (r >= g.R) return;
   int n = 0;
-  if (g.live == nullptr || g.live[r]) {
+  if (r < g.R && (g.live == nullptr || g.live[r])) {
     const int64_t c = g.consumed[r];
     for (int j = 0; j < g.cap; ++j) {
       const int64_t want = c + j + 1;
@@ -56,7 +58,59 @@ __global__ void ipc_scan_k(IpcIngest g) {
       ++n;
     }
   }
-  g.ready[r] = n;
+  if (r < g.R) {
+    g.ready[r] = n;
+    nready[r] = n;
+  }
+  if (!g.prefix) return;  // (uniform branch)
+  __syncthreads();
+  if (r < g.R) {  // exclusive prefix over the links: where this link's packets go in ring order
+    int p = 0;
+    for (int q = 0; q < r; ++q) p += nready[q];
+    g.prefix[r] = p;
+  }
+}
+
+// AQL packets (structure of arrays, E rows): st [E][obs] | st2 [E][obs] | amu [E][TA] | act [E]
+// (i32) | rew [E] | done [E].  Every ready packet's rows are appended to the ONE replay ring at
+// (aql.filled + row) % aql.C in (link, packet) order; slots_out gets the slot (the max-priority
+// leaf write that follows) or -1 for an empty window position.
+// grid: R * cap * (E / kAqlRows) blocks of 256 threads = 4 waves, one row per wave.
+constexpr int kAqlRows = 4;
+
+__global__ __launch_bounds__(256) void ipc_apply_aql_k(IpcIngest g) {
+  const int chunks = g.E / kAqlRows;
+  const int b = blockIdx.x;
+  const int r = b / (g.cap * chunks);
+  const int j = (b / chunks) % g.cap;
+  const int lane = threadIdx.x & 63, e = (b % chunks) * kAqlRows + (threadIdx.x >> 6);
+  const int64_t out = ((int64_t)r * g.cap + j) * g.E + e;
+  if (j >= g.ready[r]) {
+    if (lane == 0) g.slots_out[out] = -1;
+    return;
+  }
+  const int k = (int)((g.consumed[r] + j) % g.D);
+  const float* pk = reinterpret_cast<const float*>(g.ring + ((int64_t)r * g.D + k) * g.packet_bytes);
+  const int E = g.E, obs = g.obs, TA = g.TA;
+  const float* st = pk;
+  const float* st2 = st + (size_t)E * obs;
+  const float* amu = st2 + (size_t)E * obs;
+  const int* act = reinterpret_cast<const int*>(amu + (size_t)E * TA);
+  const float* rew = reinterpret_cast<const float*>(act + E);
+  const float* done = rew + E;
+  const int64_t row = (int64_t)(g.prefix[r] + j) * E + e;
+  const int64_t slot = (g.aql.filled[0] + row) % g.aql.C;
+  for (int c = lane; c < obs; c += 64) {
+    g.aql.st[slot * obs + c] = st[(size_t)e * obs + c];
+    g.aql.st2[slot * obs + c] = st2[(size_t)e * obs + c];
+  }
+  for (int c = lane; c < TA; c += 64) g.aql.amu[slot * TA + c] = amu[(size_t)e * TA + c];
+  if (lane == 0) {
+    g.aql.act[slot] = act[e];
+    g.aql.rew[slot] = rew[e];
+    g.aql.done[slot] = done[e];
+    g.slots_out[out] = (int32_t)slot;
+  }
 }
 
 // grid: R * cap * (E / kRows) blocks of 256 threads; block -> (link r, window j, env rows)
@@ -114,7 +168,11 @@ __global__ __launch_bounds__(256) void ipc_apply_k(IpcIngest g) {
 }
 
 __global__ void ipc_release_k(IpcIngest g) {
-  // (the replay's fill counter is advanced per real transition row by ipc_apply_k)
+  // DQN: the replay's fill counter was advanced per real transition row by ipc_apply_k;
+  // AQL: it is the ring cursor the apply read, advanced here by every applied row
+  __shared__ unsigned long long total;
+  if (threadIdx.x == 0) total = 0;
+  __syncthreads();
   const int r = threadIdx.x;
   if (r < g.R) {
     const int n = g.ready[r];
@@ -123,7 +181,10 @@ __global__ void ipc_release_k(IpcIngest g) {
     if (g.applied) g.applied[r] += n;
     // the ring slots are free again: the actor processes read this word as their credit
     if (g.host_consumed) store_release_sys(g.host_consumed + r, c);
+    if (g.kind == 1 && n) atomicAdd(&total, (unsigned long long)n);
   }
+  __syncthreads();
+  if (threadIdx.x == 0 && g.kind == 1 && g.filled && total) g.filled[0] += (int64_t)total * g.E;
 }
 
 __global__ void ipc_flag_k(int64_t* p, int64_t v) {
@@ -135,15 +196,30 @@ __global__ void ipc_flag_k(int64_t* p, int64_t v) {
 void ipc_ingest(const IpcIngest& g, hipStream_t s) {
   if (g.R < 1 || g.R > 1024 || g.D < 1 || g.cap < 1 || g.cap > g.D || g.E < kRows || g.E % kRows)
     throw std::invalid_argument("ipc_ingest: bad geometry (R <= 1024, 1 <= cap <= D, E a multiple of 4)");
-  if (g.packet_bytes < (int64_t)g.E * (kFrameBytes + kMetaCols * 4))
-    throw std::invalid_argument("ipc_ingest: packet stride smaller than a packet");
-  if (!g.ring || !g.seq || !g.consumed || !g.ready || !g.frames || !g.s_ids || !g.s2_ids || !g.action || !g.reward ||
-      !g.done || !g.slots_out || !g.prio_out || !g.frame_base || !g.slot_base)
+  if (!g.ring || !g.seq || !g.consumed || !g.ready || !g.slots_out)
     throw std::invalid_argument("ipc_ingest: null pointer");
+  if (g.kind == 0) {
+    if (g.packet_bytes < (int64_t)g.E * (kFrameBytes + kMetaCols * 4))
+      throw std::invalid_argument("ipc_ingest: packet stride smaller than a packet");
+    if (!g.frames || !g.s_ids || !g.s2_ids || !g.action || !g.reward || !g.done || !g.prio_out || !g.frame_base ||
+        !g.slot_base)
+      throw std::invalid_argument("ipc_ingest: null DQN table pointer");
+  } else if (g.kind == 1) {
+    if (g.obs < 1 || g.TA < 1 || g.packet_bytes < (int64_t)g.E * (2 * g.obs + g.TA + 3) * 4)
+      throw std::invalid_argument("ipc_ingest: AQL packet stride smaller than a packet");
+    if (g.packet_bytes % 4) throw std::invalid_argument("ipc_ingest: AQL packet stride must be a multiple of 4");
+    const AqlInsert& a = g.aql;
+    if (!g.prefix || !a.st || !a.st2 || !a.amu || !a.act || !a.rew || !a.done || !a.filled || !g.filled ||
+        a.C < (int64_t)g.R * g.cap * g.E)
+      throw std::invalid_argument("ipc_ingest: AQL tables (capacity >= R * cap * E)");
+  } else {
+    throw std::invalid_argument("ipc_ingest: kind must be 0 (DQN) or 1 (AQL)");
+  }
   const int thr = ((g.R + 63) / 64) * 64;
   ipc_scan_k<<<1, thr, 0, s>>>(g);
   LAUNCH_CHECK();
-  ipc_apply_k<<<g.R * g.cap * (g.E / kRows), 256, 0, s>>>(g);
+  if (g.kind == 0) ipc_apply_k<<<g.R * g.cap * (g.E / kRows), 256, 0, s>>>(g);
+  else ipc_apply_aql_k<<<g.R * g.cap * (g.E / kAqlRows), 256, 0, s>>>(g);
   LAUNCH_CHECK();
   ipc_release_k<<<1, thr, 0, s>>>(g);
   LAUNCH_CHECK();

@@ -597,8 +597,13 @@ void aql_apply_staged(const AqlInsert& src, const AqlInsert& dst, int E, int obs
 
 // ---- central-replay experience transport over HIP IPC (ipc_kernels.hip, parallel/ipc.py)
 struct IpcIngest {
+  int kind;                         // 0: Ape-X DQN packets (frames + rows into per-link regions)
+                                    // 1: AQL packets (SoA rows appended to one global replay ring)
   int R, D, E, cap;                 // actor links, ring depth, envs per packet, packets per link per ingest
-  int64_t packet_bytes;             // ring slot stride (>= E * (7056 + 56))
+  int64_t packet_bytes;             // ring slot stride (DQN: >= E * (7056 + 56); AQL: >= E * (2 obs + TA + 3) * 4)
+  int* prefix;                      // [R] scratch: ready packets of the links before r (AQL ring order)
+  int obs, TA;                      // AQL: state width, candidates x action dims
+  AqlInsert aql;                    // AQL: destination tables; ring slot (aql.filled + row) % aql.C
   const uint8_t* ring;              // [R][D] packets (uncached arena)
   const int64_t* seq;               // [R][D] packet number + 1 held by each slot
   int64_t* consumed;                // [R] packets applied so far (device)
@@ -606,7 +611,7 @@ struct IpcIngest {
   const int* live;                  // [R] 0 = link dropped (optional)
   int64_t* host_consumed;           // [R] device view of the host control block (credit; optional)
   int64_t* applied;                 // [R] statistics (optional)
-  int64_t* filled;                  // replay fill counter += E per packet (optional)
+  int64_t* filled;                  // replay fill counter (DQN: += real rows; AQL: += E per packet)
   uint8_t* frames;                  // replay frame ring [F][7056]
   int32_t *s_ids, *s2_ids, *action; // [C][4], [C][4], [C]
   float *reward, *done;             // [C]

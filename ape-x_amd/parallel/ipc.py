@@ -139,19 +139,46 @@ class ControlBlock:
             self.dev_ptr = None
 
 
-class IpcLearnerLinks:
-    """Rank-0 end: the arena, the control block, the captured ingest and the publisher."""
+def aql_packet_floats(E: int, obs: int, TA: int) -> int:
+    """AQL packet (structure of arrays, 4-byte words): st [E][obs] | st2 [E][obs] |
+    amu [E][TA] | act [E] (i32) | rew [E] | done [E]  (ipc_kernels.hip ipc_apply_aql_k)."""
+    return E * (2 * obs + TA + 3)
 
-    def __init__(self, R: int, D: int, E: int, P: int, replay, regions: dict, store, prefix: str, device,
-                 cap: int | None = None, dead_after: float = 30.0, mode: int = MODE_UNCACHED, log=print,
-                 open_timeout: float = 300.0):
+
+def aql_packet_views(buf: torch.Tensor, E: int, obs: int, TA: int) -> dict:
+    """Named views of one AQL packet buffer (f32 [aql_packet_floats]): an ``AqlInsert``
+    over them (C = E, cursor 0) makes the acting kernels write the packet in place."""
+    o, out = 0, {}
+    for name, n in (("st", E * obs), ("st2", E * obs), ("amu", E * TA), ("act", E), ("rew", E), ("done", E)):
+        out[name] = buf[o:o + n]
+        o += n
+    out["act"] = out["act"].view(torch.int32)
+    out["st"], out["st2"] = out["st"].view(E, obs), out["st2"].view(E, obs)
+    out["amu"] = out["amu"].view(E, TA)
+    return out
+
+
+class IpcLearnerLinks:
+    """Rank-0 end: the arena, the control block, the captured ingest and the publisher.
+
+    The transport is payload-agnostic: ``tables`` holds the ingest kernel's kind-specific
+    fields (``kind`` 0 = Ape-X DQN packets into per-link replay regions, 1 = AQL rows
+    appended to one replay ring; see :func:`dqn_tables` / :func:`aql_tables`) and
+    ``tree_write(slots, prios)`` the priority write of the rows an ingest applied (slot -1
+    = nothing there)."""
+
+    def __init__(self, R: int, D: int, E: int, P: int, store, prefix: str, device, *, packet_nbytes: int,
+                 tables: dict, tree_write, cap: int | None = None, dead_after: float = 30.0,
+                 mode: int = MODE_UNCACHED, log=print, open_timeout: float = 300.0):
         self.hip = h = ops.hip()
         self.R, self.D, self.E, self.P = int(R), int(D), int(E), int(P)
         self.cap = self.D if cap is None else max(1, min(int(cap), self.D))
         self.device = torch.device(device)
-        self.replay, self.store, self.prefix, self.log = replay, store, prefix, log
+        self.store, self.prefix, self.log = store, prefix, log
+        self.tree_write = tree_write
         self.dead_after = float(dead_after)
-        self.pkt = _align(packet_bytes(E))
+        self.packet_nbytes = int(packet_nbytes)
+        self.pkt = _align(self.packet_nbytes)
         self.seq_off = _align(self.R * self.D * self.pkt)
         self.par_off = _align(self.seq_off + 8 * self.R * self.D)
         self.nbytes = self.par_off + 2 * 4 * self.P
@@ -163,22 +190,18 @@ class IpcLearnerLinks:
         self.consumed = torch.zeros(R, **i64)
         self.applied_dev = torch.zeros(R, **i64)
         self.ready = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.prefix_dev = torch.zeros(R, dtype=torch.int32, device=dev)
         self.live_dev = torch.ones(R, dtype=torch.int32, device=dev)
         n_out = R * self.D * E  # the drain ingests up to D packets per link
         self.slots_out = torch.full((n_out,), -1, dtype=torch.int32, device=dev)
         self.prio_out = torch.zeros(n_out, dtype=torch.float32, device=dev)
-        self.frame_base = torch.tensor([regions[r].frame_base for r in range(1, R + 1)], **i64)
-        self.slot_base = torch.tensor([regions[r].slot_base for r in range(1, R + 1)], **i64)
-        rp = replay
         self._n_out = R * self.cap * E
         mk = lambda cap: h.make_ipc_ingest(dict(  # noqa: E731
-            R=R, D=D, E=E, cap=cap, packet_bytes=self.pkt, ring=self.arena, seq=self.arena + self.seq_off,
+            tables, R=R, D=D, E=E, cap=cap, packet_bytes=self.pkt, ring=self.arena, seq=self.arena + self.seq_off,
             consumed=self.consumed.data_ptr(), ready=self.ready.data_ptr(), live=self.live_dev.data_ptr(),
-            host_consumed=self.ctrl.dev_ptr + 8 * self.ctrl.off("consumed"), applied=self.applied_dev.data_ptr(),
-            filled=rp.filled.data_ptr(), frames=rp.frames.data_ptr(), s_ids=rp.s_ids.data_ptr(),
-            s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
-            done=rp.done.data_ptr(), frame_base=self.frame_base.data_ptr(), slot_base=self.slot_base.data_ptr(),
-            slots_out=self.slots_out.data_ptr(), prio_out=self.prio_out.data_ptr()))
+            prefix=self.prefix_dev.data_ptr(), host_consumed=self.ctrl.dev_ptr + 8 * self.ctrl.off("consumed"),
+            applied=self.applied_dev.data_ptr(), slots_out=self.slots_out.data_ptr(),
+            prio_out=self.prio_out.data_ptr()))
         self.ingest_handle = mk(self.cap)
         self.drain_handle = mk(self.D)
         self.version = 0
@@ -187,13 +210,51 @@ class IpcLearnerLinks:
         self._hb = {r: (None, time.monotonic()) for r in self.live}
         self._hb_t = time.monotonic()
         self.closed = False
-        geo = dict(R=R, D=D, E=E, P=P, pkt=self.pkt, seq_off=self.seq_off, par_off=self.par_off, shm=self.ctrl.name,
-                   device=self.device.index or 0)
+        geo = dict(R=R, D=D, E=E, P=P, pkt=self.pkt, packet_nbytes=self.packet_nbytes, seq_off=self.seq_off,
+                   par_off=self.par_off, shm=self.ctrl.name, device=self.device.index or 0)
         store.set(f"{prefix}/ipc/handle", h.ipc_handle(self.arena))
         store.set(f"{prefix}/ipc/geometry", json.dumps(geo))
         # every actor has mapped the control block -> remove its name (nothing lingers in /dev/shm)
         self._open_timeout = float(open_timeout)
         self._unlinked = False
+
+    @classmethod
+    def for_dqn(cls, R: int, D: int, E: int, P: int, replay, regions: dict, store, prefix: str, device, **kw):
+        """Ape-X DQN links: packets of E new frames + E transition rows (parallel.experience
+        META_COLS layout) scattered into link r's region of ``replay`` (engine.hbm_replay)."""
+        dev = torch.device(device)
+        i64 = dict(dtype=torch.int64, device=dev)
+        fb = torch.tensor([regions[r].frame_base for r in range(1, R + 1)], **i64)
+        sb = torch.tensor([regions[r].slot_base for r in range(1, R + 1)], **i64)
+        rp = replay
+        tables = dict(kind=0, filled=rp.filled.data_ptr(), frames=rp.frames.data_ptr(), s_ids=rp.s_ids.data_ptr(),
+                      s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
+                      done=rp.done.data_ptr(), frame_base=fb.data_ptr(), slot_base=sb.data_ptr())
+        links = cls(R, D, E, P, store, prefix, device, packet_nbytes=packet_bytes(E), tables=tables,
+                    tree_write=lambda slots, prios: rp.write_priorities(slots, prios, dedup=False), **kw)
+        links.replay, links.frame_base, links.slot_base = rp, fb, sb  # (kept alive: the kernel reads them)
+        return links
+
+    @classmethod
+    def for_aql(cls, R: int, D: int, E: int, P: int, replay, store, prefix: str, device, **kw):
+        """AQL links (AQL_dis.py:109-126 over xGMI): packets of E raw (s, s', a_mu, a, r, d)
+        rows appended to ``replay``'s ring (engine.aql.AQLReplay) at max priority
+        (CustomPrioritizedReplayBuffer_AQL.add, memory.py:368-378)."""
+        rp = replay
+        TA = rp.T * rp.adim
+        tables = dict(kind=1, obs=rp.obs, TA=TA, aql_st=rp.st.data_ptr(), aql_st2=rp.st2.data_ptr(),
+                      aql_amu=rp.a_mu.data_ptr(), aql_act=rp.action.data_ptr(), aql_rew=rp.reward.data_ptr(),
+                      aql_done=rp.done.data_ptr(), aql_C=rp.capacity, filled=rp.filled.data_ptr())
+        h = ops.hip()
+
+        def tree_write(slots, _prios):  # every new row at the running max priority (ring order, -1 skipped)
+            h.per_write_leaves(rp.tree, slots.data_ptr(), 0, slots.numel(), rp.alpha, rp.max_prio.data_ptr(), 0, 0,
+                               0, 0, 0, 0, torch.cuda.current_stream().cuda_stream)
+
+        links = cls(R, D, E, P, store, prefix, device, packet_nbytes=4 * aql_packet_floats(E, rp.obs, TA),
+                    tables=tables, tree_write=tree_write, **kw)
+        links.replay = rp
+        return links
 
     def _maybe_unlink(self) -> None:
         if self._unlinked:
@@ -212,7 +273,7 @@ class IpcLearnerLinks:
         write the tree.  Device-only, on the current stream: capture it in the learner graph."""
         self.hip.ipc_ingest(self.drain_handle if drain else self.ingest_handle, self._s())
         n = self.slots_out.numel() if drain else self._n_out
-        self.replay.write_priorities(self.slots_out[:n], self.prio_out[:n], dedup=False)
+        self.tree_write(self.slots_out[:n], self.prio_out[:n])
 
     def publish(self, flat: torch.Tensor) -> None:
         """Conflated versioned publish (seqlock writer, all on the current stream): announce
@@ -312,8 +373,9 @@ class IpcActorLink:
         geo = json.loads(store.get(f"{prefix}/ipc/geometry"))
         self.R, self.D, self.E, self.P = geo["R"], geo["D"], geo["E"], geo["P"]
         self.pkt, self.seq_off, self.par_off = geo["pkt"], geo["seq_off"], geo["par_off"]
-        if packet.numel() != packet_bytes(self.E) or packet.dtype != torch.uint8:
-            raise ValueError("packet buffer must be u8 [E * (7056 + 56)]")
+        want = geo.get("packet_nbytes", packet_bytes(self.E))
+        if packet.numel() * packet.element_size() != want or not packet.is_contiguous():
+            raise ValueError(f"packet buffer must be {want} contiguous bytes (the learner's packet layout)")
         if flat.numel() != self.P:
             raise ValueError(f"parameter count {flat.numel()} != the learner's {self.P}")
         self.remote = h.ipc_open(store.get(f"{prefix}/ipc/handle"), self.device.index or 0)
@@ -381,7 +443,7 @@ class IpcActorLink:
             time.sleep(0.0001)
         k, s = n % self.D, self._s()
         slot = self.remote + (self.i * self.D + k) * self.pkt
-        self.hip.memcpy_async(slot, self.packet.data_ptr(), self.packet.numel(), s)
+        self.hip.memcpy_async(slot, self.packet.data_ptr(), self.packet.numel() * self.packet.element_size(), s)
         self.hip.ipc_flag(self.remote + self.seq_off + 8 * (self.i * self.D + k), n + 1, s)
         self.sent = n + 1
         self.ctrl.view("sent")[self.i] = self.sent

@@ -15,8 +15,10 @@ Reference cadences and artefacts kept:
 * ``model{it}.pth`` every ``save_interval`` (200) iterations and at the last one
   (AQL_dis.py:131-133, 136-137) -- the reference state_dict (``q.*`` / ``proposal.*`` keys,
   NoisyNet epsilon buffers included), loadable by the reference ``load_model`` -- plus a
-  ``.train.pt`` sidecar (Adam moments, step counter, target net, iteration counters) so
-  ``--resume IT`` continues exactly instead of weights-only;
+  ``.train.pt`` sidecar (Adam moments, step counter, target net, iteration counters):
+  ``--resume IT`` restores the optimizer state and counters, not weights only; the replay,
+  the env states and the acting RNG counters are not saved, so training continues on a
+  freshly filled replay (it does not replay the uninterrupted run bit for bit);
 * tags ``learner/loss_q`` / ``learner/loss_proposal`` (means over the logging window, at
   the learner-step index; AQL_dis.py:123-124) and ``actor/episode_reward`` /
   ``actor/episode_length`` (batchrecoder_AQL.py:118-119), plus ``evaluator/episode_reward``
@@ -25,6 +27,12 @@ Reference cadences and artefacts kept:
 
 Losses are accumulated on the device (no host sync per learner step); the host reads
 them once per ``--log-interval`` iterations.
+
+``--gpus N`` (N > 1; or any launch with WORLD_SIZE > 1): the distributed form of AQL_dis
+across GPUs (``apex_amd.engine.central_aql``): rank 0 trains and checkpoints, ranks 1..N-1
+are actor GPUs pushing transitions over HIP IPC; one iteration = one packet per actor +
+``(N-1) * n_envs // batch_size`` SGD steps.  ``--same-device`` puts every rank on cuda:0
+(rehearsal on one GPU).
 """
 from __future__ import annotations
 
@@ -77,6 +85,11 @@ def parser() -> argparse.ArgumentParser:
                    help="acting on its own HIP stream beside the learner steps (the learner sees each acting "
                         "step's transitions one iteration later; a checkpoint does not hold the staged half)")
     p.add_argument("--json-log", default=None, help="append one JSON record per log interval to this file")
+    p.add_argument("--gpus", type=int, default=1, help="N > 1: rank 0 learner + N-1 actor GPUs over HIP IPC")
+    p.add_argument("--same-device", action="store_true", help="--gpus N on one GPU (every rank on cuda:0)")
+    p.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
+                   help="control-plane backend of the multi-rank form (the data plane is HIP IPC)")
+    p.add_argument("--launch-timeout", type=float, default=3600.0, help="--gpus N self-launch wall limit")
     return p
 
 
@@ -167,6 +180,18 @@ def greedy_eval(eng: AQLEngine, episodes: int, seed: int = 12345) -> list[float]
 
 # ------------------------------------------------------------------ main
 def train(a) -> dict:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and world == 1:  # self-launch one process per rank (never exec from a GPU process)
+        import sys
+
+        from .parallel.spawn import run_ranks
+
+        code = run_ranks([sys.executable, "-m", "apex_amd.train_aql", *sys.argv[1:]], a.gpus, timeout=a.launch_timeout)
+        if code:
+            raise SystemExit(code)
+        return {}
+    if world > 1:
+        return train_central(a, int(os.environ["RANK"]), world)
     dev = torch.device(a.device)
     torch.cuda.set_device(dev)
     eng = AQLEngine(config_from_args(a), dev)
@@ -182,12 +207,66 @@ def train(a) -> dict:
     eng.fill()
     if not a.no_graphs:
         eng.capture()
+    return _loop(a, eng, eng.iteration, eng.E, eng.finished_episodes, start, writer)
+
+
+def train_central(a, rank: int, world: int) -> dict:
+    """Rank 0: the AQL learner loop (logging, evaluation, checkpoints) over a
+    :class:`CentralAQLEngine`; ranks 1..: act and push until rank 0 stops them."""
+    import torch.distributed as dist
+
+    from .engine.central_aql import CentralAQLEngine
+
+    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", rank))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if a.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    ceng = CentralAQLEngine(config_from_args(a), dev, rank, world)
+    last = {}
+    try:
+        if rank != 0:
+            if not a.no_graphs:
+                ceng.capture()
+            while ceng.iteration():
+                pass
+            torch.cuda.synchronize(dev)
+            return {}
+        if a.resume is not None:
+            idx = latest_index(a.save_dir) if a.resume == "latest" else int(a.resume)
+            if idx is None:
+                raise SystemExit(f"--resume latest: no model*.pth in {a.save_dir}")
+            load_engine(ceng.eng, model_path(a.save_dir, idx), idx)
+            ceng.iterations, ceng.learner_steps = ceng.eng.iterations, ceng.eng.learner_steps
+        writer = NullWriter() if a.no_tb else SummaryWriter(a.log_dir, comment=f"-{a.env}-learner-central")
+        ceng.fill()
+        if not a.no_graphs:
+            ceng.capture()
+        last = _loop(a, ceng.eng, ceng.iteration, ceng.R * ceng.E, lambda: [], ceng.iterations, writer,
+                     central=ceng)
+        last["links"] = ceng.close()
+        print(json.dumps({"links": last["links"]}), flush=True)
+    finally:
+        if rank == 0:
+            ceng.close()
+        dist.destroy_process_group()
+    return last
+
+
+def _loop(a, eng: AQLEngine, iterate, envs_per_iter: int, episodes, start: int, writer, central=None) -> dict:
+    """The training loop: ``iterate()`` per iteration (act + K SGD steps + publish + target
+    cadence, or its central form), checkpoints, metrics and greedy evaluations."""
     ep_idx, last = 0, {}
     t_win, it_win, steps_win = time.perf_counter(), start, eng.learner_steps
     jl = open(a.json_log, "a") if a.json_log else None
     try:
         for it in range(start, a.max_step):
-            eng.iteration()   # act + K SGD steps + publish + (it % 20 == 0) target sync
+            iterate()   # act + K SGD steps + publish + (it % 20 == 0) target sync
+            if central is not None:
+                eng.iterations, eng.learner_steps = central.iterations, central.learner_steps
             if it % a.save_interval == 0 or it == a.max_step - 1:
                 save_engine(eng, model_path(a.save_dir, it))
             log_now = (it + 1 - start) % a.log_interval == 0 or it == a.max_step - 1
@@ -195,7 +274,7 @@ def train(a) -> dict:
             if not (log_now or ev):
                 continue
             lq, lp, n = eng.learner.take_loss_means()
-            eps = eng.finished_episodes()
+            eps = episodes()
             now = time.perf_counter()
             dt = max(now - t_win, 1e-9)
             if n:
@@ -207,10 +286,12 @@ def train(a) -> dict:
                 ep_idx += 1
             sps = (eng.learner_steps - steps_win) / dt
             writer.add_scalar("learner/steps_per_sec", sps, eng.learner_steps)
-            writer.add_scalar("actor/env_steps_per_sec", (it + 1 - it_win) * eng.E / dt, eng.learner_steps)
+            writer.add_scalar("actor/env_steps_per_sec", (it + 1 - it_win) * envs_per_iter / dt, eng.learner_steps)
             last = {"iteration": it, "learner_steps": eng.learner_steps, "loss_q": lq, "loss_proposal": lp,
                     "episodes": len(eps), "actor_mean_return": float(np.mean([r for r, _ in eps])) if eps else None,
                     "sgd_steps_per_s": round(sps, 1), "target_syncs": len(eng.target_syncs)}
+            if central is not None:
+                last["packets_applied"] = sum(central.applied.values())
             if ev:
                 ret = greedy_eval(eng, a.eval_episodes, seed=a.seed + 7 * it)
                 for k, r in enumerate(ret):

@@ -250,6 +250,8 @@ def main():
     wd.kick()
     pre = run_preflight(args, topo, device, wd) if world > 1 else None
     if args.algo == "aql":
+        if topo == "central":
+            return aql_central(args, rank, world, device, wd, pre)
         return aql(args, rank, world, device)
     if topo == "central":
         return central(args, rank, world, device, wd, pre)
@@ -475,6 +477,82 @@ def aql(args, rank, world, device):
         }), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def aql_central(args, rank, world, device, wd, pre=None):
+    """Distributed AQL_dis (BASELINE config 4; the default for --algo aql with N>1): rank 0 =
+    THE AQL learner (batch 32, AQL_dis.py:31-47) + the one replay, ranks 1.. = actor GPUs
+    with ``--envs`` envs each pushing raw (s, a, r, s', d, a_mu) rows over HIP IPC
+    (engine/central_aql.py; AQL_dis.py:50-53,109-126).  One rank-0 iteration = ingest (<= one
+    packet per actor) + K = (N-1) * envs / 32 SGD steps (the reference replay ratio) + a
+    weight publish.  ``value`` = learner SGD steps/s; actor env steps/s = rows that reached
+    the replay during the timed window."""
+    import torch
+    import torch.distributed as dist
+
+    from apex_amd.engine.aql import AQLEngineConfig
+    from apex_amd.engine.central_aql import CentralAQLEngine
+
+    cap = min(args.capacity, 1_000_000)
+    cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed)
+    eng = CentralAQLEngine(cfg, device, rank, world, paced=not args.unpaced)
+    wd.kick()
+    if rank != 0:
+        if not args.no_graphs:
+            eng.capture()
+        while eng.iteration():
+            wd.kick(every=5.0)
+        torch.cuda.synchronize(device)
+        wd.off()
+        dist.destroy_process_group()
+        return
+    t_fill = time.perf_counter()
+    eng.fill()
+    torch.cuda.synchronize(device)
+    t_fill = time.perf_counter() - t_fill
+    wd.kick()
+    if not args.no_graphs:
+        eng.capture()
+    for _ in range(args.warmup):
+        eng.iteration()
+    torch.cuda.synchronize(device)
+    wd.kick()
+    a0 = sum(eng.applied.values())
+    s0 = eng.learner_steps
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.iteration()
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    packets = sum(eng.applied.values()) - a0
+    sgd = (eng.learner_steps - s0) / dt
+    wd.kick()
+    st = eng.eng.learner.stats()
+    links = eng.close()
+    wd.off()
+    e = eng.eng
+    print(json.dumps({
+        "metric": "AQL learner SGD steps/sec + actor env steps/sec (AQL_dis, BipedalWalker-shaped)",
+        "value": round(sgd, 1), "unit": "learner SGD steps (batch 32) per second, one central learner",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (GPU BipedalWalker-shaped env, random-init weights)",
+        "config": {"model": f"AQL NoisyNet critic + proposal, {e.obs}-d obs, {e.adim}-d action, T={e.T} candidates",
+                   "global_batch": cfg.batch_size, "seq_len": 1, "parallelism": f"central1+actors{world - 1}",
+                   "topology": "AQL learner + replay on rank 0, actor GPUs push rows over HIP IPC",
+                   "env": cfg.env_id, "envs_per_actor_gpu": args.envs, "sgd_steps_per_iteration": eng.K,
+                   "replay_capacity": cap, "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
+        "actor_env_steps_per_sec": round(packets * eng.E / dt, 1),
+        "packets_applied_per_iteration": round(packets / args.steps, 3),
+        "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),
+        "replay_fill_seconds": round(t_fill, 3), "links": links,
+        "links_complete": all(links["applied"][r] == links["sent"][r] for r in links["live"]),
+        "preflight": pre,
+        "timing": "rank 0 (the one learner) between two device syncs; actor ranks act continuously",
+        "last_loss_q": round(st["loss_q"], 6), "last_loss_proposal": round(st["loss_proposal"], 6),
+    }), flush=True)
+    dist.destroy_process_group()
 
 
 def central(args, rank, world, device, wd, pre=None):
