@@ -60,63 +60,12 @@ class EngineConfig:
     use_graphs: bool = True
     overlap: bool = False                # actor graph on its own stream, concurrent with the learner
     exact_mass: bool = False             # SURVEY Q5 parity: the newest slot is excluded from the sampled mass
-    # overlap mode: how the actor and learner streams reach separate hardware queues.
-    # HIP spreads the streams of one priority over GPU_MAX_HW_QUEUES (4) shared queues,
-    # so with enough streams in the process (RCCL/PG streams, torch's stream pools) the
-    # actor and learner streams can share one queue and serialise.
-    #   "none": the next torch pool stream, or the one ``reserve_actor_stream`` took
-    #           before the process group existed (default)
-    #   "pool": both on torch pool streams (the learner off the null stream)
-    #   "probe": the first pool stream that a measured concurrency probe shows running
-    #            beside the learner's stream (experimental)
-    #   "dedicated": CU-masked streams (own HSA queues; measured 2x slower: queue
-    #                oversubscription)
-    #   "priority-actor" / "priority-learner": a high-priority stream (measured slower in
-    #                the single-process step: preemption of the other queue's waves)
-    streams: str = "none"
     # data-parallel overlap mode: capture the whole learner step INCLUDING the two RCCL
     # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
     # staging half, instead of three phase graphs with eager collectives in between
     dp_graph: bool = False
-    # overlap mode, single process: actor half and learner step as ONE graph per half (two
-    # branches: the learner captured first keeps the launch queue, the actor forks beside it)
-    # overlap: actor/learner hand-off events without the system-scope fence (StreamEvent)
-    light_events: bool = False  # A/B 3602 vs 3576 steps/s (noise level): off
-    step_graph: bool = False  # A/B 3320 vs 3647 steps/s: off
-    dp_comm_late: bool = True  # one-graph DP: capture the FC1 all-reduce branch after the backward's first launch
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
-
-
-class StreamEvent:
-    """Actor/learner stream hand-off event.  ``light``: a raw HIP event created with
-    hipEventDisableSystemFence (record/wait order the two device queues without the
-    system-scope cache writeback/invalidate of a default event); otherwise a torch event."""
-
-    def __init__(self, light: bool):
-        self._hip = ops.hip() if light else None
-        self._h = self._hip.event_create(True) if light else None
-        self._t = None if light else torch.cuda.Event()
-
-    def record(self, stream: torch.cuda.Stream) -> None:
-        if self._hip is None:
-            self._t.record(stream)
-        else:
-            self._hip.event_record(self._h, stream.cuda_stream)
-
-    def block(self, stream: torch.cuda.Stream) -> None:
-        """Make ``stream`` wait for the last record."""
-        if self._hip is None:
-            stream.wait_event(self._t)
-        else:
-            self._hip.stream_wait_event(stream.cuda_stream, self._h)
-
-    def __del__(self):
-        if self._hip is not None and self._h:
-            try:
-                self._hip.event_destroy(self._h)
-            except Exception:  # interpreter shutdown
-                pass
 
 
 _RESERVED: dict = {}
@@ -158,9 +107,6 @@ class ApexEngine:
 
             self._sharded = ShardedSampling(self.replay, force=force_collectives, comm=allreduce)
         self.learner = DQNLearner(model, self.replay, lc, allreduce=allreduce, sharded=self._sharded)
-        # sampled-ahead batches: their target passes ride the actor's graph (its queue is busy
-        # ~1/3 of a step) when actor and learner overlap
-        self.learner.target_in_actor = self.overlap and self.learner.ahead is not None and lc.target_pass == "actor"
         self.actor_model = copy.deepcopy(self.learner.model)
         self.actor_model._flat = None
         self.actor_flat = self.actor_model.flatten_parameters()
@@ -177,7 +123,7 @@ class ApexEngine:
         self.learn_steps = 0
         self.actor_steps = 0
         self._diag_skip_actor = False
-        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = self._g_step = None
+        self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = None
         self._pool = None
         self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
         self._captured = False
@@ -185,11 +131,12 @@ class ApexEngine:
         # overlap: staging half h (sets h*k .. h*k+k-1) is filled by the actor steps of one
         # train step while the learner applies the other half (the previous step's)
         self._half = 0
-        self.stream_probe = None
-        self._astream, self._lstream = self._make_streams(cfg.streams) if self.overlap else (None, None)
-        light = bool(cfg.light_events)
-        self._ev_actor = [StreamEvent(light), StreamEvent(light)] if self.overlap else None
-        self._ev_learn = StreamEvent(light) if self.overlap else None
+        # the actor stream: the one reserve_actor_stream took before the process group drew
+        # its pool streams, else the next pool stream
+        self._astream = (_RESERVED.pop(self.device, None) or torch.cuda.Stream(device=self.device)) if self.overlap \
+            else None
+        self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()] if self.overlap else None
+        self._ev_learn = torch.cuda.Event() if self.overlap else None
 
     # ------------------------------------------------------------------ eager bodies
     def publish_params(self) -> None:
@@ -211,15 +158,12 @@ class ApexEngine:
                 q = forward_q(self.actor_model, obs, self.cfg.learner.dtype == "bf16")
         self.actor.act_and_step(q, stage)
 
-    def _actor_half(self, half: int, train: bool = False):
-        """Actor steps into staging half ``half``; ``train`` (a train step, not a fill): then
-        the target pass of the learner's next batch (LearnerConfig.target_ahead)."""
+    def _actor_half(self, half: int):
+        """Actor steps into staging half ``half``."""
         k = self.cfg.actor_steps_per_learner_step
         if not self._diag_skip_actor:
             for i in range(k):
                 self._actor_body(half * k + i)
-        if train and self.learner.target_in_actor:
-            self.learner.target_pass_next()
 
     def _apply_half(self, half: int):
         k = self.cfg.actor_steps_per_learner_step
@@ -266,7 +210,6 @@ class ApexEngine:
         Single-process: ``a1`` is the whole step and ``a2``/``b`` are None."""
         with trace.range("apex.learner"):
             self._learn_phases(a1, a2, b, pipelined_mass)
-        self.learner.advance()
 
     def _learn_phases(self, a1, a2, b, pipelined_mass: bool) -> None:
         R = trace.range
@@ -312,18 +255,10 @@ class ApexEngine:
         return g
 
     def capture(self, warmup_iters: int = 3) -> None:
-        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
-            with self._on_lstream():
-                return self.capture(warmup_iters)
-        return self._capture(warmup_iters)
-
-    def _capture(self, warmup_iters: int) -> None:
         """Warm up on a side stream, then capture actor and learner steps as hipGraphs.
         The warm-up iterations are real train steps and are counted as such.  Collectives
-        stay eager, between the learner's phase graphs."""
+        stay eager, between the learner's phase graphs (unless ``dp_graph``)."""
         self._drain_mass()
-        if self.overlap:
-            return self._capture_overlap(warmup_iters)
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -332,62 +267,26 @@ class ApexEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self._pool = torch.cuda.graph_pool_handle()
-        self._g_actor = self._graph(self._actor_body, self._pool)
-        L = self.learner
-        c0 = L.cur
-        # sampled-ahead batches alternate between two buffers: one learner graph per buffer
-        # (indexed by learner.cur at replay); otherwise a single graph
-        ga, ga2, gb = [], [], []
-        b_per_buf = self._dp and L.ahead is not None and self._sharded is not None
-        for c in ((0, 1) if L.ahead is not None else (c0,)):
-            L.cur = c
+        if self.overlap:
+            self._capture_overlap_graphs(torch.cuda.graph_pool_handle())  # actor graphs run concurrently:
+        else:                                                           # never share their memory
+            L = self.learner
+            self._g_actor = self._graph(self._actor_body, self._pool)
             if self._dp:
-                ga.append(self._graph(L.forward_phase, self._pool))
-                ga2.append(self._graph(L.backward_phase, self._pool))
-                if b_per_buf or not gb:  # sharded + sampled ahead: the optimizer graph draws a batch
-                    gb.append(self._graph(self._learn_b, self._pool))
+                self._g_learn_a = self._graph(L.forward_phase, self._pool)
+                self._g_learn_a2 = self._graph(L.backward_phase, self._pool)
+                self._g_learn_b = self._graph(self._learn_b, self._pool)
             else:  # no host collective in between: one graph per step
-                ga.append(self._graph(lambda: (L.forward_phase(), self._learn_b()), self._pool))
-        if L.ahead is not None:
-            L.set_cur(c0)
-        self._g_learn_a = ga if L.ahead is not None else ga[0]
-        self._g_learn_a2 = (ga2 if L.ahead is not None else ga2[0]) if self._dp else None
-        self._g_learn_b = (gb if len(gb) == 2 else gb[0]) if self._dp else None
+                self._g_learn_a = self._graph(lambda: (L.forward_phase(), self._learn_b()), self._pool)
         self._captured = True
         torch.cuda.synchronize(self.device)
+        if self.overlap:
+            self._ev_learn.record(torch.cuda.current_stream(self.device))
 
-    def _capture_overlap(self, warmup_iters: int) -> None:
+    def _capture_overlap_graphs(self, apool) -> None:
         """Overlap mode: graphs per staging half (actor: fill half h; learner: apply half
         1-h, sample, forward, backward [, optimizer]); data-parallel: the learner's three
-        phase graphs per half.  Warm-up runs real sequential train steps, keeping the
-        one-step-behind staging invariant."""
-        s = torch.cuda.Stream(device=self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            for _ in range(warmup_iters):  # full eager train steps (counters, publish/target cadence)
-                self.train_step()
-        torch.cuda.current_stream(self.device).wait_stream(s)
-        torch.cuda.synchronize(self.device)
-        self._pool = torch.cuda.graph_pool_handle()
-        apool = torch.cuda.graph_pool_handle()  # actor graphs run concurrently: never share memory
-        L = self.learner
-        c0, half0 = L.cur, self._half
-
-        def at_half(h: int, fn):
-            # the learner graph of staging half h runs when learner.cur = c0 ^ h ^ half0 (both
-            # flip once per step): capture it with that sampled-ahead buffer
-            def body():
-                L.cur = c0 ^ h ^ half0 if L.ahead is not None else c0
-                fn()
-            return body
-
-        try:
-            self._capture_overlap_graphs(apool, at_half)
-        finally:
-            if L.ahead is not None:
-                L.set_cur(c0)
-
-    def _capture_overlap_graphs(self, apool, at_half) -> None:
+        phase graphs per half, or ONE graph per half with the all-reduces inside."""
         self._g_actor, self._g_learn_a, self._g_learn_a2 = [], [], []
         self._g_dp = None
         if self._dp and self.cfg.dp_graph and self._mass_pending_ok():
@@ -396,12 +295,9 @@ class ApexEngine:
             try:
                 g_actor, g_dp = [], []
                 for h in (0, 1):
-                    g_actor.append(self._graph(at_half(h, lambda h=h: self._actor_half(h, True)), apool))
-                    g_dp.append(self._graph(at_half(h, lambda h=h: self._dp_step_body(1 - h)), self._pool))
+                    g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+                    g_dp.append(self._graph(lambda h=h: self._dp_step_body(1 - h), self._pool))
                 self._g_actor, self._g_dp = g_actor, g_dp
-                self._captured = True
-                torch.cuda.synchronize(self.device)
-                self._ev_learn.record(torch.cuda.current_stream(self.device))
                 return
             except RuntimeError as e:  # RCCL capture unsupported here: the phase graphs instead
                 import warnings
@@ -410,70 +306,30 @@ class ApexEngine:
                 self._g_dp = None
                 torch.cuda.synchronize(self.device)
                 apool = torch.cuda.graph_pool_handle()
-        if self.cfg.step_graph and not self._dp:
-            self._g_step = [self._graph(at_half(h, lambda h=h: self._fused_step_body(h)), self._pool) for h in (0, 1)]
-            self._captured = True
-            torch.cuda.synchronize(self.device)
-            self._ev_learn.record(torch.cuda.current_stream(self.device))
-            return
-        # sharded + sampled ahead: the optimizer graph draws the batch after next (per half,
-        # captured right after its half's phases: they hand it the staged rows to scatter)
-        b_per_half = self._dp and self.learner.ahead is not None and self._sharded is not None
-        gb = []
         for h in (0, 1):
-            self._g_actor.append(self._graph(at_half(h, lambda h=h: self._actor_half(h, True)), apool))
+            self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
             if self._dp:
-                self._g_learn_a.append(self._graph(at_half(h, lambda h=h: self._learn_a(1 - h)), self._pool))
-                self._g_learn_a2.append(self._graph(at_half(h, self.learner.backward_phase), self._pool))
-                if b_per_half:
-                    gb.append(self._graph(at_half(h, self._learn_b), self._pool))
+                self._g_learn_a.append(self._graph(lambda h=h: self._learn_a(1 - h), self._pool))
+                self._g_learn_a2.append(self._graph(self.learner.backward_phase, self._pool))
             else:
-                self._g_learn_a.append(self._graph(at_half(h, lambda h=h: (self._learn_a(1 - h), self._learn_b())),
-                                                   self._pool))
-        if b_per_half:
-            self._g_learn_b = gb
-        else:
-            self._g_learn_b = self._graph(self._learn_b, self._pool) if self._dp else None
-        self._captured = True
-        torch.cuda.synchronize(self.device)
-        self._ev_learn.record(torch.cuda.current_stream(self.device))
+                self._g_learn_a.append(self._graph(lambda h=h: (self._learn_a(1 - h), self._learn_b()), self._pool))
+        self._g_learn_b = self._graph(self._learn_b, self._pool) if self._dp else None
 
     def _mass_pending_ok(self) -> bool:
         """One-graph DP step: the shard masses must always arrive with the previous step's
         conv-gradient all-reduce (overlap mode, slots in the gradient prefix)."""
         return self._sharded is None or (self.overlap and self.learner.grad_prefix > 0)
 
-    def _fused_step_body(self, h: int) -> None:
-        """Captured body of one overlapped train step (EngineConfig.step_graph): the learner
-        step (applying staging half 1-h) on the capture stream, and -- forked from the same
-        start point, captured second -- the actor half h on the actor stream, joined at the
-        end.  Replays serialise on the stream, which is the event protocol of
-        :meth:`_train_step_overlap` (actor t after learner t-1, learner t after actor t-1)."""
-        L, A = torch.cuda.current_stream(self.device), self._astream
-        start = torch.cuda.Event()
-        start.record(L)
-        self._learn_a(1 - h)
-        self._learn_b()
-        A.wait_event(start)
-        with torch.cuda.stream(A):
-            self._actor_half(h, True)
-        L.wait_stream(A)
-        self._step_events = start
-
     def _dp_step_body(self, apply_half: int) -> None:
         """Captured body of the one-graph DP step (EngineConfig.dp_graph)."""
         ar = self._allreduce
         self._learn_a(apply_half)
         fc, conv = self.learner.grad_slices()
-        if self.cfg.dp_comm_late and hasattr(ar, "mark"):
-            # the FC1/head all-reduce depends on this point but is captured after the conv
-            # backward's first launch, so the backward chain keeps the graph's queue
-            ready, w = ar.mark(), []
-            self.learner.backward_phase(after_first=lambda: w.append(ar.start(fc, ready=ready)))
-            w1 = w[0]
-        else:
-            w1 = ar.start(fc)
-            self.learner.backward_phase()
+        # the FC1/head all-reduce depends on this point but is captured after the conv
+        # backward's first launch, so the backward chain keeps the graph's queue
+        ready, w = ar.mark(), []
+        self.learner.backward_phase(after_first=lambda: w.append(ar.start(fc, ready=ready)))
+        w1 = w[0]
         w2 = ar.start(conv)
         ar.wait(w1, w2)
         self._learn_b()
@@ -487,7 +343,7 @@ class ApexEngine:
     def _train_step_eager(self) -> None:
         """Overlap-mode semantics, run sequentially on the current stream."""
         h = self._half
-        self._actor_half(h, True)
+        self._actor_half(h)
         self._learner_eager(1 - h)
         self._half ^= 1
 
@@ -502,44 +358,28 @@ class ApexEngine:
         h = self._half
         L = torch.cuda.current_stream(self.device)
         A = self._astream
-        if self._g_step is not None:
-            with trace.range("apex.step_graph"):
-                self._g_step[h].replay()
-            self.learner.advance()
-            self.learn_steps += 1
-            self.actor_steps += self.cfg.actor_steps_per_learner_step
-            if self.learn_steps % self.cfg.publish_param_interval == 0:
-                self.publish_params()  # the graph joined its actor branch
-            if self.learn_steps % self.cfg.target_update_interval == 0:
-                self.learner.sync_target()  # (the step graph joined its actor branch)
-            self._half ^= 1
-            return
         with trace.range("actor.launch"):
-            self._ev_learn.block(A)
+            A.wait_event(self._ev_learn)
             with torch.cuda.stream(A):
                 self._g_actor[h].replay()
             self._ev_actor[h].record(A)
-            self._ev_actor[1 - h].block(L)
+            L.wait_event(self._ev_actor[1 - h])
         if self._g_dp is not None:
             if self._sharded is not None and not self._mass_pending:  # e.g. after fill(): re-exchange
                 self._sharded.exchange()
             with trace.range("apex.learner"):
                 self._g_dp[h].replay()
-            self.learner.advance()
             self._mass_pending = self._sharded is not None  # the graph's conv all-reduce carried them
         elif self._dp:
-            gb = self._g_learn_b[h] if isinstance(self._g_learn_b, list) else self._g_learn_b
-            self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, gb.replay, True)
+            self._learn(self._g_learn_a[h].replay, self._g_learn_a2[h].replay, self._g_learn_b.replay, True)
         else:
             self._learn(self._g_learn_a[h].replay, None, None, False)
         self.learn_steps += 1
         self.actor_steps += self.cfg.actor_steps_per_learner_step
         if self.learn_steps % self.cfg.publish_param_interval == 0:
-            self._ev_actor[h].block(L)  # the actor is not reading its weights
+            L.wait_event(self._ev_actor[h])  # the actor is not reading its weights
             self.publish_params()
         if self.learn_steps % self.cfg.target_update_interval == 0:
-            if self.learner.target_in_actor:
-                self._ev_actor[h].block(L)  # its target pass of the next batch is redone
             self.learner.sync_target()
         self._ev_learn.record(L)
         self._half ^= 1
@@ -554,14 +394,12 @@ class ApexEngine:
         self.actor_steps += 1
 
     def learner_step(self) -> None:
-        pick = lambda g: g[self.learner.cur] if isinstance(g, list) else g  # noqa: E731
         if self._g_learn_a is None:
             self._learner_eager()
         elif self._dp:
-            self._learn(pick(self._g_learn_a).replay, pick(self._g_learn_a2).replay, pick(self._g_learn_b).replay,
-                        False)
+            self._learn(self._g_learn_a.replay, self._g_learn_a2.replay, self._g_learn_b.replay, False)
         else:
-            self._learn(pick(self._g_learn_a).replay, None, None, False)
+            self._learn(self._g_learn_a.replay, None, None, False)
         self.learn_steps += 1
         if self.learn_steps % self.cfg.publish_param_interval == 0:
             self.publish_params()
@@ -570,9 +408,6 @@ class ApexEngine:
 
     def fill(self, min_transitions: int | None = None) -> None:
         """Run actor steps until the replay holds ``threshold_size`` slots."""
-        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
-            with self._on_lstream():
-                return self.fill(min_transitions)
         self._drain_mass()
         need = self.cfg.threshold_size if min_transitions is None else min_transitions
         steps = max(-(-need // self.cfg.n_envs), 4)
@@ -590,90 +425,14 @@ class ApexEngine:
                 self.actor_step()
         self._diag_skip_actor = _DIAG_NO_ACTOR
 
-    def _make_streams(self, mode: str):
-        """(actor stream, learner stream or None = the caller's stream), see
-        EngineConfig.streams."""
-        dev = self.device
-        if mode == "probe":
-            return self._probe_actor_stream(), None
-        if mode == "dedicated":
-            from .. import ops
-
-            h = ops.hip()
-            mk = lambda: torch.cuda.ExternalStream(h.create_dedicated_stream(dev.index or 0), device=dev)  # noqa: E731
-            return mk(), mk()
-        if mode == "pool":  # learner off the null stream too (no legacy null-stream syncs)
-            return _RESERVED.pop(dev, None) or torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
-        if mode == "priority-actor":
-            return torch.cuda.Stream(device=dev, priority=-1), None
-        if mode == "priority-learner":
-            return torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev, priority=-1)
-        if mode == "none":
-            return _RESERVED.pop(dev, None) or torch.cuda.Stream(device=dev), None
-        raise ValueError(f"streams={mode!r}")
-
-    def _probe_actor_stream(self, tries: int = 8):
-        """Pick an actor stream that really runs concurrently with the learner's stream
-        (the caller's current stream): a 300 us one-wave spin on the learner stream, a
-        tiny one on the candidate; concurrent iff the candidate's finishes first.  Pool
-        streams cycle over the hardware queues, so a few candidates cover them all."""
-        from .. import ops
-
-        h = ops.hip()
-        L = torch.cuda.current_stream(self.device)
-        first = None
-        for _ in range(tries):
-            A = torch.cuda.Stream(device=self.device)
-            first = first or A
-            torch.cuda.synchronize(self.device)
-            e0, e1, ea = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-            e0.record(L)
-            h.spin_us(300, L.cuda_stream)
-            e1.record(L)
-            h.spin_us(1, A.cuda_stream)
-            ea.record(A)
-            torch.cuda.synchronize(self.device)
-            if e0.elapsed_time(ea) < 0.5 * e0.elapsed_time(e1):
-                self.stream_probe = {"tries": _ + 1, "concurrent": True}
-                return A
-        self.stream_probe = {"tries": tries, "concurrent": False}
-        import warnings
-
-        warnings.warn("no pool stream ran concurrently with the learner stream; actor/learner overlap may serialise")
-        return first
-
-    def _on_lstream(self):
-        """Context: the learner's stream (high priority) when configured, else a no-op.
-        Entering it makes that stream wait for the caller's stream (ordering with work
-        the caller enqueued, e.g. a weight broadcast)."""
-        import contextlib
-
-        if self._lstream is None:
-            return contextlib.nullcontext()
-
-        @contextlib.contextmanager
-        def ctx():
-            cur = torch.cuda.current_stream(self.device)
-            self._lstream.wait_stream(cur)
-            with torch.cuda.stream(self._lstream):
-                yield
-            cur.wait_stream(self._lstream)  # results visible to the caller's stream
-
-        return ctx()
-
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""
-        if self._lstream is not None and torch.cuda.current_stream(self.device) != self._lstream:
-            with self._on_lstream():
-                return self.train_step()
         if trace.enabled():
             with trace.range("apex.train_step"):
                 return self._train_step()
         return self._train_step()
 
     def _train_step(self) -> None:
-        if not self.learner.primed:  # the first two sampled-ahead batches (eager)
-            self.learner.prime()
         if self.overlap:
             if self._captured:
                 self._train_step_overlap()

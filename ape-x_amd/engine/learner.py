@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import copy
 from dataclasses import dataclass
-from types import SimpleNamespace
 
 import torch
 
@@ -48,19 +47,6 @@ class LearnerConfig:
     dtype: str = "fp32"            # compute precision: "fp32" (reference, learner.py:139-145: fp32 MFMA on the
                                    # hip path, no autocast on the torch path) | "bf16" (opt-in fast mode)
     seed: int = 0
-    tree_fork: bool = True         # hip path: priority-tree writes on a forked stream
-    bwd_fork: bool = False         # hip path: wgrad3/wgrad2 on a forked stream (measured slower: off)
-    late_join: bool = False        # single-process: join the tree branch after the optimizer (A/B 3555 vs 3633: off)
-    fork_late: bool = True         # capture the tree branch after the backward's first launch (see _fork_point)
-    tree_write: str = "legacy"     # "legacy": single-workgroup walks on the tree fork (few CUs beside the
-                                   # backward: 3315 vs 3195 steps/s) | "batch": HBMReplay.write_batch (wide
-                                   # kernels; lower latency, better when the tree write is inline)
-    target_ahead: bool = False     # hip path: batches sampled two steps ahead (private row copies), their
-                                   # target pass Q_target(s') run beside the previous learner step (in the
-                                   # actor's graph when the engine overlaps them); see DQNLearner.sample_next
-    target_pass: str = "actor"     # target_ahead: where the next batch's target pass runs -- "actor" (the
-                                   # engine's actor graph, overlap mode) | "fork" (the tree branch, after the
-                                   # priority write, beside the backward) | "inline" (right after the draw)
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -90,7 +76,6 @@ class DQNLearner:
         self.device = replay.device
         self.model = model.to(self.device)
         self.flat = self.model.flatten_parameters()
-        self._join_pending = False
         self.target = copy.deepcopy(self.model)
         self.target._flat = None
         self.tflat = self.target.flatten_parameters()
@@ -152,7 +137,6 @@ class DQNLearner:
         self.n_fin_partials = 0
         if self.hip_net:
             self.net = make_hip_net(self.model, cfg.dtype)
-            self.net.bwd_fork = cfg.bwd_fork
             self.net.enable_backward(B)
             self.tnet = make_hip_net(self.target, cfg.dtype)
             # the optimizer refreshes the packed weight copies (bf16 or exact fp32) in its pass
@@ -175,23 +159,7 @@ class DQNLearner:
             # all-reduce the norm must be taken after it (grad_sumsq)
             self.fin_partials = torch.zeros(8192, dtype=torch.float64, device=dev)
             self.n_fin_partials = 0
-        # sampled-ahead batches (LearnerConfig.target_ahead): two buffers, ``cur`` holds the
-        # batch this step trains on (sampled one step earlier, its target pass done beside
-        # that step); the engine flips ``cur`` after every learner step (:meth:`advance`)
-        self.ahead = None
-        self.cur = 0
-        self._primed = False
-        if self.hip_net and cfg.target_ahead:
-            self.ahead = [SimpleNamespace(idx=torch.zeros(B, dtype=torch.int32, device=dev),
-                                          w=torch.zeros(B, dtype=torch.float32, device=dev),
-                                          rows=replay.row_buffers(B), ws_t=make_workspace(B, A, dev, cfg.dtype))
-                          for _ in range(2)]
-        # the engine runs target_pass_next() in its actor graph (overlap mode); otherwise the
-        # learner runs each target pass right after the draw
-        self.target_in_actor = False
-        self.target_on_fork = self.ahead is not None and cfg.target_pass == "fork" and cfg.tree_fork
         self._src = None  # (s ids, s' ids, idx, transition table) of the batch in flight
-        self._pending_rows = None
         # one-shot callables run on the tree stream before this step's priority write
         # (the overlapped engine's deferred actor-row priorities)
         self.tree_hooks = []
@@ -239,7 +207,7 @@ class DQNLearner:
         too; data-parallel split: up to the FC1 backward and its finalize."""
         s = self._stream()
         glob = shard = None
-        if self.sharded is not None and self.ahead is None:  # gathered shard masses -> global pmin + weight scale
+        if self.sharded is not None:  # gathered shard masses -> global pmin + weight scale
             if self.sharded.in_kernel:
                 shard = self.sharded.sample_args()
             else:
@@ -250,26 +218,17 @@ class DQNLearner:
             self.hip.apply_staged_rows(extra[0], self.replay.trans_ptrs(), extra[1].data_ptr(), extra[2].data_ptr(),
                                        extra[1].numel(), s)
         rp = self.replay
-        if self.ahead is not None:  # this step's batch was drawn two steps ago (sample_next)
-            cur = self.ahead[self.cur]
-            self.idx, self.w = cur.idx, cur.w
-            self._src = (cur.rows["s_ids"], cur.rows["s2_ids"], None, SimpleNamespace(**cur.rows))
-            self._pending_rows = rows[-1] if rows else None  # scattered by sample_next's launch
-            q2t = cur.ws_t.q
-        else:
-            self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
-                                       rows=rows[-1] if rows else None)
-            self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
+        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
+                                   rows=rows[-1] if rows else None)
+        self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
-            # the loss reads (a, r, d) straight out of the transition table (or the batch's
-            # private rows).  The passes share each layer's launch (5 kernels, not 15).
+            # the loss reads (a, r, d) straight out of the transition table.  The three passes
+            # share each layer's launch (5 kernels, not 15).
             ids_s, ids_s2, jdx, tab = self._src
-            passes = [(self.net, rp.frames, self.ws_s, ids_s, jdx), (self.net, rp.frames, self.ws_s2, ids_s2, jdx)]
-            if self.ahead is None:
-                passes.append((self.tnet, rp.frames, self.ws_t, ids_s2, jdx))
-                q2t = self.ws_t.q
-            forward_multi(passes)
+            forward_multi([(self.net, rp.frames, self.ws_s, ids_s, jdx), (self.net, rp.frames, self.ws_s2, ids_s2, jdx),
+                           (self.tnet, rp.frames, self.ws_t, ids_s2, jdx)])
+            q2t = self.ws_t.q
             m = self.model
             self.hip.dqn_heads_bwd(
                 {"q": self.ws_s.q.data_ptr(), "q2": self.ws_s2.q.data_ptr(), "q2t": q2t.data_ptr(),
@@ -293,11 +252,7 @@ class DQNLearner:
             if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n
-            if self.cfg.late_join and self.allreduce is None:
-                self._join_pending = True  # joined after the optimizer (it reads nothing the branch writes)
-            else:
-                self._tree_fork_end()
-                self.sample_next()
+            self._tree_fork_end()
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
@@ -323,7 +278,7 @@ class DQNLearner:
         assert self.dp_split
         rp = self.replay
         tree = self._fork_point()
-        after = tree if after_first is None else (after_first if tree is None else (lambda: (tree(), after_first())))
+        after = tree if after_first is None else (lambda: (tree(), after_first()))
         ids_s, _, jdx, _ = self._src
         self.net.conv_backward(rp.frames, self.ws_s, ids_s, jdx, after_first=after)
         self._tree_fork_end()
@@ -331,136 +286,38 @@ class DQNLearner:
             # the tree is final for the next sample: pack this shard's slot, which the
             # conv-gradient all-reduce then exchanges (the next step's shard masses)
             self.sharded.pack()
-        if self.sharded is None:
-            self.sample_next()  # (sharded: after the all-reduce brought the masses, in optimize)
-
-    # ------------------------------------------------------------------ sampled-ahead batches
-    def sample_next(self) -> None:
-        """Target pass off the critical chain (``LearnerConfig.target_ahead``).
-
-        Q_target(s') depends only on the sampled batch and the target weights (fixed between
-        syncs).  So at the end of step t -- right after its priority write joined -- the
-        learner draws batch t+2 into the buffer batch t just freed, and the target pass of
-        batch t+1 (drawn at the end of step t-1) runs beside step t: in the actor's graph
-        (``target_pass_next``, engine overlap mode; the actor queue is busy ~1/3 of a step),
-        else inline.  A batch misses the one priority update of the step between its draw and
-        its use, as the reference learner's prefetched batches do (the replay server answers
-        the next ``sample`` while the learner trains).  The sampling launch also scatters the
-        staged actor rows and copies every sampled row (frame ids, action, return, done) into
-        the buffer, so the actor overwriting a slot before the batch is used cannot mix two
-        transitions in one TD target; the frames outlive an overwritten slot by >= n + 7 actor
-        steps (the frame ring's margin, HBMReplay)."""
-        if self.ahead is None:
-            return
-        glob = shard = None
-        if self.sharded is not None:
-            if self.sharded.in_kernel:
-                shard = self.sharded.sample_args()
-            else:
-                self.sharded.finalize()
-                glob = self.sharded.glob
-        buf = self.ahead[self.cur]
-        self.replay.sample_indices(self.B, buf.idx, buf.w, self.step_counter, self.beta, glob=glob, shard=shard,
-                                   rows=self._pending_rows, out_rows=buf.rows)
-        self._pending_rows = None
-        if not self._deferred:
-            self._target_pass(buf)
-
-    @property
-    def _deferred(self) -> bool:
-        """The next batch's target pass runs during the following step (actor graph / fork)."""
-        return self.target_in_actor or self.target_on_fork
-
-    def target_pass_next(self) -> None:
-        """Q_target(s') of the next step's batch (drawn at the end of the previous step),
-        for the engine's actor graph: run it after that step and before the next one."""
-        self._target_pass(self.ahead[1 - self.cur])
-
-    def _target_pass(self, buf) -> None:
-        forward_multi([(self.tnet, self.replay.frames, buf.ws_t, buf.rows["s2_ids"], None)])
-
-    @property
-    def primed(self) -> bool:
-        return self.ahead is None or self._primed
-
-    def prime(self) -> None:
-        """The first two sampled-ahead batches (eager, before any capture), each drawn with
-        its own Philox stream, and the current one's target pass (the next one's too when
-        the learner runs them itself)."""
-        for k, c in ((1, self.cur), (2, 1 - self.cur)):
-            buf = self.ahead[c]
-            self.replay.sample_indices(self.B, buf.idx, buf.w, self.step_counter, self.beta, out_rows=buf.rows,
-                                       seed=self.replay.seed + k * 0x9E3779B9)
-        self._target_pass(self.ahead[self.cur])
-        if not self._deferred:
-            self._target_pass(self.ahead[1 - self.cur])
-        self._primed = True
-
-    def advance(self) -> None:
-        """One learner step done (eager or replayed): the sampled-ahead batch becomes current."""
-        if self.ahead is not None:
-            self.set_cur(self.cur ^ 1)
-
-    def set_cur(self, c: int) -> None:
-        """Host view of the buffer state: buffer ``c`` holds the next step's batch (a replayed
-        graph runs no Python, so the engine keeps this).  ``idx`` / ``w`` name the other
-        buffer: the last step's batch until its end, then the batch drawn for the step after
-        the next one."""
-        self.cur = c
-        other = self.ahead[1 - c]
-        self.idx, self.w = other.idx, other.w
 
     def _fork_point(self):
         """Fork the tree branch HERE (it depends on everything launched so far) but capture
-        it after the backward's first launch (``fork_late``): in the captured graph the
-        backward chain is then the first child of the fork and keeps the launch queue,
-        and only the tree branch pays the cross-queue hand-off.  Returns the callback for
-        ``after_first`` (None: the branch was forked right away)."""
-        if not (self.cfg.tree_fork and self.cfg.fork_late):
-            self._tree_fork_begin()
-            return None
+        it after the backward's first launch: in the captured graph the backward chain is
+        then the first child of the fork and keeps the launch queue, and only the tree
+        branch pays the cross-queue hand-off.  Returns the callback for ``after_first``."""
         self._ev_fork = ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
         return lambda: self._tree_fork_begin(ev)
 
-    def _tree_fork_begin(self, ev: torch.cuda.Event | None = None) -> None:
+    def _tree_fork_begin(self, ev: torch.cuda.Event) -> None:
         """Fork: deferred actor-row priorities, then the priority mix + loss mean + tree
-        write (+ step bump) of this step's samples, beside the backward (``ev``: the fork
-        point, recorded earlier on the main stream)."""
-        main = torch.cuda.current_stream()
-        fork = self.cfg.tree_fork
-        if fork:
-            if ev is None:
-                self.tree_stream.wait_stream(main)
-            else:
-                self.tree_stream.wait_event(ev)
-        with torch.cuda.stream(self.tree_stream if fork else main):
+        write (+ step bump) of this step's samples, on the tree stream beside the backward
+        (``ev``: the fork point, recorded earlier on the main stream).  The tree write is
+        the single-workgroup level walk: it occupies few CUs beside the backward GEMMs."""
+        self.tree_stream.wait_event(ev)
+        with torch.cuda.stream(self.tree_stream):
             hooks, self.tree_hooks = self.tree_hooks, []
             for fn in hooks:
                 fn()
             pre, self.pre_writes = self.pre_writes, []
-            if self.cfg.tree_write == "legacy":  # single-workgroup level walks (A/B reference)
-                for slots, prios, filled in pre:
-                    self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
-                self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
-                                             mix=(self.delta, self.lw, self.prio, self.loss))
-            else:
-                for extra in pre[:-1]:  # more than one staged actor step per learner step
-                    self.replay.write_batch(pre=extra)
-                self.replay.write_batch(pre=pre[-1] if pre else None, idx=self.idx, bump=self.step_counter,
-                                        mix=(self.delta, self.lw, self.prio, self.loss))
-            if self.target_on_fork:  # the next batch's target pass, beside the rest of the backward
-                self.target_pass_next()
+            for slots, prios, filled in pre:
+                self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
+            self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
+                                         mix=(self.delta, self.lw, self.prio, self.loss))
 
     def _tree_fork_end(self) -> None:
-        if self.cfg.tree_fork:
-            torch.cuda.current_stream().wait_stream(self.tree_stream)  # join: the next sample reads the tree
+        torch.cuda.current_stream().wait_stream(self.tree_stream)  # join: the next sample reads the tree
 
     def optimize(self) -> None:
         s = self._stream()
         h = self.hip
-        if self.dp_split and self.sharded is not None:
-            self.sample_next()  # the all-reduce brought this step's shard masses
         if self.hip_net and self.n_fin_partials:
             parts, nparts = self.fin_partials, self.n_fin_partials  # from grad_finalize
         else:
@@ -481,15 +338,9 @@ class DQNLearner:
              parts.data_ptr(), nparts, self.hp, stp.data_ptr(), self.norms.data_ptr(), s, **pk)
         if not self.hip_net:
             self.replay.write_priorities(self.idx, self.prio, dedup=True, bumps=((self.step_counter, 1),))
-        if self._join_pending:
-            self._join_pending = False
-            self._tree_fork_end()
-            self.sample_next()
 
     def step(self) -> None:
         """One eager learner step (the engine runs the same phases as hipGraphs)."""
-        if not self.primed:
-            self.prime()
         if self.sharded is not None:
             self.sharded.exchange()
         self.forward_phase()
@@ -504,7 +355,6 @@ class DQNLearner:
         else:
             self.allreduce.wait(self.allreduce.start(self.flat_grad))
         self.optimize()
-        self.advance()
         self.host_steps += 1
 
     # ------------------------------------------------------------------ target / params
@@ -518,14 +368,6 @@ class DQNLearner:
         self.hip.copy_f32(self.tflat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())
         if self.hip_net:
             self.tnet.copy_packed_from(self.net)
-        if self.ahead is not None and self._primed:
-            # the sampled-ahead batches' target passes ran on the old weights: redo them, so
-            # every step after a sync sees the synced target (as without target_ahead).  With
-            # the pass in the actor graph the engine first waits for it; the batch after is
-            # then still to be drawn or to get its pass
-            self._target_pass(self.ahead[self.cur])
-            if not self._deferred:
-                self._target_pass(self.ahead[1 - self.cur])
 
     def copy_params_to(self, dst_flat: torch.Tensor) -> None:
         self.hip.copy_f32(dst_flat.data_ptr(), self.flat.data_ptr(), self.P, self._stream())

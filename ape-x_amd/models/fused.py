@@ -95,7 +95,6 @@ class HipDuelingNet:
         self.fwd_numel = self.arena_offsets["w2t"]   # forward-only part of the arena
         self._wgrad_ws = None
         self._maps = None
-        self.bwd_fork = False  # wgrad3 / wgrad2 on a forked stream (A/B: 3095 vs 3236 steps/s, off)
         f = model.features
         self.b1, self.b2, self.b3 = f[0].bias, f[2].bias, f[4].bias
         self.repack()
@@ -178,7 +177,6 @@ class HipDuelingNet:
         self._heads_ws = torch.empty(self.hip.heads_wgrad_workspace_floats(self.A), dtype=torch.float32,
                                      device=self.device)
         self._fc1_ws = torch.empty(self.hip.fc1_bwd_workspace_floats(), dtype=torch.float32, device=self.device)
-        self._bwd_stream = torch.cuda.Stream(device=self.device)
         self.repack()
 
     # ------------------------------------------------------------------ forward
@@ -283,39 +281,13 @@ class HipDuelingNet:
         xp, ip, jp = self._src(x, ids, idx, B)
         h, s, f = self.hip, self._s(), self.model.features
         w1, w2, w3 = (t.data_ptr() for t in self._wgrad_wss)
-        fork = self.bwd_fork
-        main = torch.cuda.current_stream()
-        if not fork:
-            h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, s)
-            if after_first is not None:
-                after_first()
-            h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
-            h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, s)
-            h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
-            h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
-        else:
-            # the dgrad chain (dy3 -> dy2 -> dy1 -> wgrad1) is the critical path; wgrad3 and
-            # wgrad2 hang off it on a side stream.  Each fork is captured main-chain-first so
-            # the chain stays the first child (keeps the graph's queue); the side branch
-            # takes the cross-queue hand-offs.
-            side = self._bwd_stream
-            ev3 = torch.cuda.Event()
-            ev3.record(main)  # dy3 ready
-            h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
-            if after_first is not None:
-                after_first()
-            ev2 = torch.cuda.Event()
-            ev2.record(main)  # dy2 ready
-            h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
-            side.wait_event(ev3)
-            with torch.cuda.stream(side):
-                h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, side.cuda_stream)
-            side.wait_event(ev2)
-            with torch.cuda.stream(side):
-                h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, side.cuda_stream)
-            h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
-            main.wait_stream(side)
-            self._bwd_events = (ev3, ev2)
+        h.conv_wgrad(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), 0, B, w3, 0, 0, s)
+        if after_first is not None:
+            after_first()
+        h.conv_dgrad(3, ws.dy3.data_ptr(), 0, self.w3t.data_ptr(), ws.dy2.data_ptr(), ws.a2.data_ptr(), B, s)
+        h.conv_wgrad(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), 0, B, w2, 0, 0, s)
+        h.conv_dgrad(2, ws.dy2.data_ptr(), 0, self.w2t.data_ptr(), ws.dy1.data_ptr(), ws.a1.data_ptr(), B, s)
+        h.conv_wgrad(1, xp, ip, jp, ws.dy1.data_ptr(), 0, B, w1, 0, 0, s)
         return [h.conv_finalize_job(k, B, wsp, f[2 * k - 2].weight.grad.data_ptr(), f[2 * k - 2].bias.grad.data_ptr())
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
 

@@ -26,8 +26,6 @@ state_dict; the arena only changes memory order, never a value.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import ops
@@ -36,37 +34,20 @@ from .dqn import DuelingDQN
 P3, C3 = 49, 64
 FEAT = P3 * C3  # 3136
 F32_SPLITS = 7  # FC1 forward split-K slabs (f32_kernels.hip kFcSplits)
-# extra elements between the three bf16 planes of a split tensor (A/B knob: plane strides that
-# are large powers-of-two multiples put the three loads of one chunk on the same HBM channel)
-PX_PAD = int(os.environ.get("APEX_PX_PAD", "0"))
-
-
-def _planes(n: int, device) -> torch.Tensor:
-    """[3, n + PX_PAD] bf16: hi | mid | lo planes of an n-element tensor (plane stride = shape[1])."""
-    return torch.empty(3, n + PX_PAD, dtype=torch.bfloat16, device=device)
 
 
 class F32Workspace:
     """fp32 activation buffers for one forward pass of batch ``B`` (+ backward buffers)."""
 
-    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False, px: bool | None = None):
+    def __init__(self, B: int, A: int, device, keep_for_backward: bool = False):
         self.B, self.A = B, A
         f32 = dict(dtype=torch.float32, device=device)
         self.a1 = torch.empty(B, 400, 32, **f32)
         self.a2 = torch.empty(B, 81, 64, **f32)
         self.a3 = torch.empty(B, FEAT, **f32)
-        # pre-split exact forward (px_kernels.hip): each activation also as 3 bf16 planes
-        self.px = ops.hip().px_enabled() if px is None else bool(px)
-        bf = dict(dtype=torch.bfloat16, device=device)
-        self.a1x = _planes(B * 400 * 32, device) if self.px else None
-        self.a2x = _planes(B * 81 * 64, device) if self.px else None
-        self.a3x = _planes(B * FEAT, device) if self.px else None
         self.z = torch.empty(F32_SPLITS, B, 256, **f32)
         self.h = torch.empty(B, 256, **f32) if keep_for_backward else None
         self.q = torch.empty(B, A, **f32)
-        # pre-split exact backward (pxb_kernels.hip): the output gradients' planes as well
-        self.pxb = bool(keep_for_backward and self.px and ops.hip().pxb_enabled())
-        self.dzx = self.dy3x = self.dy2x = None
         if keep_for_backward:
             self.dA = torch.empty(B, A + 1, **f32)
             self.dz = torch.empty(B, 256, **f32)
@@ -74,17 +55,12 @@ class F32Workspace:
             self.dy3 = torch.empty(B, FEAT, **f32)
             self.dy2 = torch.empty(B, 81, 64, **f32)
             self.dy1 = torch.empty(B, 400, 32, **f32)
-            if self.pxb:
-                self.dzx = _planes(B * 256, device)
-                self.dy3x = _planes(B * FEAT, device)
-                self.dy2x = _planes(B * 81 * 64, device)
 
 
 class F32DuelingNet:
     """fp32 MFMA kernels over a :class:`DuelingDQN` (fp32 master params, reference layout)."""
 
     fp32 = True
-    bwd_fork = False  # the bf16 net's side-stream wgrad option; the fp32 backward pairs wgrad+dgrad per launch
     # fp32 arena: forward layouts first (all an actor / target net needs), then the transposes
     LAYOUT = (("w2p", (64, 4, 4, 32)), ("w3p", (64, 3, 3, 64)), ("wfc1p", (256, P3, C3)),
               ("w2t", (4, 4, 32, 64)), ("w3t", (3, 3, 64, 64)))
@@ -97,7 +73,6 @@ class F32DuelingNet:
         self.A = model.num_actions
         self.device = next(model.parameters()).device
         self._ws_B = None
-        self.fc1_in_place_dp = os.environ.get("APEX_FC1_DP_INPLACE", "1") == "1"  # A/B hook
         self._heads_ws = None
         self._maps = None
         sizes = [int(torch.Size(sh).numel()) for _, sh in self.LAYOUT]
@@ -109,11 +84,6 @@ class F32DuelingNet:
             self.arena_offsets[name] = off
             off += n
         self.fwd_numel = self.arena_offsets["w2t"]
-        # every packed layout as 3 bf16 planes (hi | mid | lo, plane stride x_plane = the arena
-        # size): the pre-split exact GEMMs' weight operands (px_kernels.hip forward layouts,
-        # pxb_kernels.hip transposes + wfc1p), kept by repack / the optimizer's pack pass
-        self.x_plane = self.arena.numel() + PX_PAD
-        self.arena_x = torch.empty(3 * self.x_plane, dtype=torch.bfloat16, device=self.device)
         self.repack()
 
     def repack(self) -> None:
@@ -126,23 +96,11 @@ class F32DuelingNet:
             self.wfc1p[128:].copy_(m.value[0].weight.view(128, C3, P3).permute(0, 2, 1))
             self.w2t.copy_(f[2].weight.permute(2, 3, 1, 0))
             self.w3t.copy_(f[4].weight.permute(2, 3, 1, 0))
-        self.split_weights()
-
-    def split_weights(self) -> None:
-        """arena_x = the exact 3-term bf16 split of the packed layouts (one kernel)."""
-        self.hip.f32_split_planes(self.arena.data_ptr(), self.arena_x.data_ptr(), self.arena.numel(), self.x_plane,
-                                  self._s())
-
-    def wx(self, name: str) -> int:
-        """Address of packed layout ``name``'s hi plane in arena_x."""
-        return self.arena_x.data_ptr() + 2 * self.arena_offsets[name]
 
     def copy_packed_from(self, other: "F32DuelingNet", forward_only: bool = True) -> None:
         """Device copy of another net's packed weights (same architecture)."""
         n = self.fwd_numel if forward_only else self.arena.numel()
         self.arena[:n].copy_(other.arena[:n])
-        ax, ox = self.arena_x.view(3, -1), other.arena_x.view(3, -1)
-        ax[:, :n].copy_(ox[:, :n])
 
     def pack_maps(self) -> tuple[torch.Tensor, torch.Tensor]:
         """int32 (dst1, dst2) over the flat parameter order: arena positions of the packed
@@ -173,12 +131,8 @@ class F32DuelingNet:
 
     def opt_pack_args(self) -> dict:
         d1, d2 = self.pack_maps()
-        out = {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
-               **self.fc_pack_args()}
-        if self.hip.px_enabled():  # the optimizer also rewrites the forward layouts' split planes
-            out.update(arena_x=self.arena_x.data_ptr(), x_plane=self.x_plane, fc_wp_x=self.wx("wfc1p"),
-                       fc_wp_x_plane=self.x_plane)
-        return out
+        return {"dst1": d1.data_ptr(), "dst2": d2.data_ptr(), "arena_f32": self.arena.data_ptr(),
+                **self.fc_pack_args()}
 
     @staticmethod
     def _s() -> int:
@@ -192,10 +146,9 @@ class F32DuelingNet:
         self._wgrad_wss = [torch.empty(h.f32_wgrad_workspace_floats(k, B), dtype=torch.float32, device=self.device)
                            for k in (1, 2, 3)]
         self._heads_ws = torch.empty(h.heads_wgrad_workspace_floats(self.A), dtype=torch.float32, device=self.device)
-        # FC1 weight gradient in batch slices (knob 15; 0 = one in-place pass without finalize)
-        self._fc1_G = h.f32_fc1_wgrad_slices(B) if h.f32_fc1_wgrad_splits() > 0 else 0
-        self._fc1_ws = (torch.empty(h.f32_fc1_wgrad_workspace_floats(), dtype=torch.float32, device=self.device)
-                        if self._fc1_G else None)
+        # FC1 weight gradient: natural-order batch-slice partials, transposed by grad_finalize
+        self._fc1_G = h.f32_fc1_wgrad_slices(B)
+        self._fc1_ws = torch.empty(h.f32_fc1_wgrad_workspace_floats(), dtype=torch.float32, device=self.device)
         self._ws_B = B
 
     # ------------------------------------------------------------------ forward
@@ -236,8 +189,6 @@ class F32DuelingNet:
                       m.advantage[2].weight.grad.data_ptr(), m.advantage[2].bias.grad.data_ptr(),
                       m.value[2].weight.grad.data_ptr(), m.value[2].bias.grad.data_ptr(),
                       m.advantage[0].bias.grad.data_ptr(), m.value[0].bias.grad.data_ptr(), s)
-        if ws.pxb:  # (the learner's fused dqn_heads_bwd writes the planes itself)
-            h.f32_split_planes(ws.dz.data_ptr(), ws.dzx.data_ptr(), B * 256, ws.dzx.shape[1], s)
         self.trunk_backward(x, ws, ids, idx)
 
     def heads_finalize_job(self, part: torch.Tensor, G: int):
@@ -247,33 +198,16 @@ class F32DuelingNet:
                                            m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
                                            m.value[0].bias.grad.data_ptr())
 
-    def _fc1_bwd(self, ws: F32Workspace, in_place: bool = False) -> list:
-        """FC1 dgrad + weight gradient; returns the finalize jobs that complete the weight
-        gradient (sliced mode: sum the slices + transpose to the reference layout, with
-        their sum-of-squares partials), or [] when it was written in place (``in_place``:
-        the data-parallel split, where the FC1 all-reduce waits on this launch)."""
+    def _fc1_bwd(self, ws: F32Workspace) -> list:
+        """FC1 dgrad + weight gradient (one launch); returns the finalize jobs that complete
+        the weight gradient (sum the slices + transpose to the reference layout, with their
+        sum-of-squares partials)."""
         m = self.model
         ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
-        if ws.pxb:  # pre-split exact FC1 backward (pxb_kernels.hip): same outputs, same finalize jobs
-            sliced = bool(self._fc1_G and not in_place)
-            d = {"dzx": ws.dzx.data_ptr(), "dz_ps": ws.dzx.shape[1], "a3x": ws.a3x.data_ptr(), "a3_ps": ws.a3x.shape[1],
-                 "wx": self.wx("wfc1p"), "w_ps": self.x_plane, "a3": ws.a3.data_ptr(), "dy3": ws.dy3.data_ptr(),
-                 "dy3x": ws.dy3x.data_ptr(), "dy3_ps": ws.dy3x.shape[1],
-                 "gw": self._fc1_ws.data_ptr() if sliced else ga.data_ptr(), "gw2": 0 if sliced else gv.data_ptr(),
-                 "slices": self._fc1_G if sliced else 0}
-            self.hip.pxb_fc1_bwd(d, ws.B, self._s())
-            if not sliced:
-                return []
-            return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
-                    self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
-        if self._fc1_G and not in_place:
-            self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
-                                       self._fc1_ws.data_ptr(), ws.B, self._s())
-            return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
-                    self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
-        self.hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
-                             ga.data_ptr(), gv.data_ptr(), ws.B, self._s())
-        return []
+        self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
+                                   self._fc1_ws.data_ptr(), ws.B, self._s())
+        return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
+                self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
 
     def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None) -> list:
         """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch); returns the
@@ -282,35 +216,22 @@ class F32DuelingNet:
         h, s, f = self.hip, self._s(), self.model.features
         xp, ip, jp = self._src(x, ids, idx, B)
         w1, w2, w3 = self._wgrad_wss
-        if ws.pxb:  # pre-split exact conv3 / conv2 backward (pxb_kernels.hip)
-            h.pxb_conv_bwd(3, {"dyx": ws.dy3x.data_ptr(), "dy_ps": ws.dy3x.shape[1], "xx": ws.a2x.data_ptr(),
-                               "x_ps": ws.a2x.shape[1], "wtx": self.wx("w3t"), "wt_ps": self.x_plane,
-                               "mask": ws.a2.data_ptr(), "dx": ws.dy2.data_ptr(), "dxx": ws.dy2x.data_ptr(),
-                               "dx_ps": ws.dy2x.shape[1], "ws": w3.data_ptr()}, B, s)
-            if after_first is not None:
-                after_first()
-            h.pxb_conv_bwd(2, {"dyx": ws.dy2x.data_ptr(), "dy_ps": ws.dy2x.shape[1], "xx": ws.a1x.data_ptr(),
-                               "x_ps": ws.a1x.shape[1], "wtx": self.wx("w2t"), "wt_ps": self.x_plane,
-                               "mask": ws.a1.data_ptr(), "dx": ws.dy1.data_ptr(), "ws": w2.data_ptr()}, B, s)
-        else:
-            h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
-                           ws.dy2.data_ptr(), w3.data_ptr(), B, s)
-            if after_first is not None:
-                after_first()
-            h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
-                           ws.dy1.data_ptr(), w2.data_ptr(), B, s)
+        h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
+                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
+        if after_first is not None:
+            after_first()
+        h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
+                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
         h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
         return [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
                                         f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
 
     def fc_backward(self, ws: F32Workspace, extra_jobs=()) -> None:
-        """Data-parallel split, part 1: the FC1 backward (its weight gradients are written in
-        place) + the finalize of ``extra_jobs`` (the heads), so the FC1/head all-reduce can
-        start while :meth:`conv_backward` runs."""
+        """Data-parallel split, part 1: the FC1 backward + the finalize of its slices and of
+        ``extra_jobs`` (the heads), so the FC1/head all-reduce can start while
+        :meth:`conv_backward` runs."""
         self.enable_backward(ws.B)
-        jobs = self._fc1_bwd(ws, in_place=self.fc1_in_place_dp) + list(extra_jobs)
-        if jobs:
-            self.hip.grad_finalize(jobs, self._s(), 0)
+        self.hip.grad_finalize(self._fc1_bwd(ws) + list(extra_jobs), self._s(), 0)
 
     def conv_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
                       idx: torch.Tensor | None = None, after_first=None) -> None:
@@ -323,17 +244,13 @@ class F32DuelingNet:
         """FC1 + conv backward from ``ws.dz`` (fp32 dL/dz).  The conv weight-gradient
         partials (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes the
         per-workgroup sum-of-squares partials of EVERY gradient into ``sumsq`` (fp64) when
-        given (the FC1 weight gradients, written in place, join through norm-only jobs);
-        returns the partial count.  ``after_first()`` runs right after the first launch."""
+        given; returns the partial count.  ``after_first()`` runs right after the first launch."""
         self.enable_backward(ws.B)
         fc1_jobs = self._fc1_bwd(ws)
         if after_first is not None:
             after_first()
-        h, m = self.hip, self.model
-        ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
+        h = self.hip
         jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs) + fc1_jobs
-        if sumsq is not None and not fc1_jobs:  # in-place FC1 grads join through norm-only jobs
-            jobs += [h.norm_only_job(ga.data_ptr(), ga.numel()), h.norm_only_job(gv.data_ptr(), gv.numel())]
         return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr())
 
 
@@ -346,7 +263,6 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
     B, A = passes[0][2].B, net0.A
     h, s = net0.hip, net0._s()
     c1, c2, c3, fc, hd = [], [], [], [], []
-    px = h.px_enabled() and all(p[2].px for p in passes)
     for net, x, ws, ids, idx in passes:
         assert ws.B == B and net.A == A, "one launch per layer needs a common batch and action count"
         m, f = net.model, net.model.features
@@ -355,12 +271,6 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
         c2.append((ws.a1.data_ptr(), 0, 0, net.w2p.data_ptr(), 0, f[2].bias.data_ptr(), ws.a2.data_ptr()))
         c3.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
         fc.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
-        if px:  # planes: conv1 writes a1x; conv2 / conv3 / FC1 read (activation, weight) planes
-            P, ps1, ps2, ps3 = net.x_plane, ws.a1x.shape[1], ws.a2x.shape[1], ws.a3x.shape[1]
-            c1[-1] += (0, 0, ws.a1x.data_ptr(), 0, 0, ps1)
-            c2[-1] += (ws.a1x.data_ptr(), net.wx("w2p"), ws.a2x.data_ptr(), ps1, P, ps2)
-            c3[-1] += (ws.a2x.data_ptr(), net.wx("w3p"), ws.a3x.data_ptr(), ps2, P, ps3)
-            fc[-1] += (ws.a3x.data_ptr(), net.wx("wfc1p"), 0, ps3, P, 0)
         hd.append(net._heads_tuple(ws))
     h.f32_conv_fwd_multi(1, c1, B, s)
     h.f32_conv_fwd_multi(2, c2, B, s)

@@ -58,13 +58,7 @@ def hip():
     import torch  # noqa: F401  -- binds libamdhip64.so.7 to torch's copy before our dlopen
     from . import build
 
-    first = "_apex_hip" not in _mods
-    m = _load("_apex_hip", lambda: build.build_hip())
-    if first:  # kernel-variant knobs for A/B runs: APEX_F32_KNOBS="8=2,7=2" -> f32_set_variant(8, 2) ...
-        for item in filter(None, os.environ.get("APEX_F32_KNOBS", "").split(",")):
-            k, _, v = item.partition("=")
-            m.f32_set_variant(int(k), int(v))
-    return m
+    return _load("_apex_hip", lambda: build.build_hip())
 
 
 def hip_available() -> bool:

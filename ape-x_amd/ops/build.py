@@ -49,8 +49,6 @@ HIP_SOURCES = [
     "loss_heads_kernels.hip",
     "f32_kernels.hip",
     "ipc_kernels.hip",
-    "px_kernels.hip",
-    "pxb_kernels.hip",
     "comm.cpp",
     "ipc.cpp",
 ]

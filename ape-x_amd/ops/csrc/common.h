@@ -173,25 +173,6 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __bfloat16_as_ushort(__float2bfloat16(f));  // RNE, NaN-preserving (v_cvt_pk_bf16_f32)
 }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
-// Three-term bf16 split, round-to-nearest-even at each step: h = bf16(x), m = bf16(x - h),
-// l = bf16(x - h - m).  Both remainders are exact in fp32 (Sterbenz) and the last term carries
-// the remaining <= 8 significant bits, so h + m + l == x for normal fp32 x, |m| <= 2^-8 |x|,
-// |l| <= 2^-16 |x| (the pre-split GEMM operands of px_kernels.hip).
-__device__ __forceinline__ void split3_rne(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
-  h = f2bf(x);
-  const float r1 = x - bf2f(h);
-  m = f2bf(r1);
-  l = f2bf(r1 - bf2f(m));
-}
-// the three terms of v into planes base[0 | ps | 2 ps] at element i
-__device__ __forceinline__ void store_planes(uint16_t* base, int64_t ps, size_t i, float v) {
-  uint16_t h, m, l;
-  split3_rne(v, h, m, l);
-  base[i] = h;
-  base[ps + i] = m;
-  base[2 * ps + i] = l;
-}
-
 __device__ __forceinline__ void atomic_max_pos_float(float* addr, float v) {
   // valid for non-negative floats: IEEE order == signed-int order
   atomicMax(reinterpret_cast<int*>(addr), __float_as_int(v));

@@ -99,10 +99,8 @@ struct HasColsum<P, decltype((void)P::A_COLSUM, void())> {
   static constexpr bool value = P::A_COLSUM;
 };
 
-// PF = global -> register prefetch depth: 1 = the next k-block is loaded while the current one
-// computes (its LDS store follows the MFMA block); 2 = two register sets, loads issued a full
-// k-block earlier (they cover L2 / MALL latency), the MFMA block fenced from the LDS stores.
-// Policies may precompute a per-thread row state once (the k-invariant part of an operand
+// The next k-block is loaded into registers while the current one computes (its LDS store
+// follows the MFMA block).  Policies may precompute a per-thread row state once (the k-invariant part of an operand
 // chunk's address: im2col divisions by the output width, sample / channel offsets) and load
 // each k-block from it with a scalar offset: row_a(args, ctx, row, ch) -> RowA and
 // load_a_row(args, ctx, RowA, kb) (same for B).  Without it the loaders re-derive the whole
@@ -143,7 +141,7 @@ __device__ __forceinline__ int xcd_chunk(int b, int G) {
   return b >= G8 ? b : (b & 7) * (G8 >> 3) + (b >> 3);
 }
 
-template <class P, int PF = 1>
+template <class P>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
@@ -162,7 +160,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     for (int j = 0; j < G::TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  constexpr int NSET = PF == 2 ? 2 : 1;
+  constexpr int NSET = 1;
   f32x4 ra[NSET][G::NA], rb[NSET][G::NB];
   f32x4 csum = zero4();
   typename RowAOf<P>::type rowa[G::NA];
@@ -221,7 +219,6 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
   };
   using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, NSET - 1>;
   auto compute = [&](int buf) {
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
@@ -260,49 +257,22 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 
   int kb = ctx.kb0;
   int cur = 0;
-  if constexpr (PF == 1 || PF == 3) {  // 3: depth 1 with the MFMA block fenced from the store
-    if (kb < ctx.kb1) {
-      gload(kb, S0{});
-      sstore(0, S0{});
-    }
+  if (kb < ctx.kb1) {
+    gload(kb, S0{});
+    sstore(0, S0{});
+  }
+  __syncthreads();
+  for (; kb < ctx.kb1; ++kb) {
+    const bool more = kb + 1 < ctx.kb1;
+    if (more) gload(kb + 1, S0{});
+    // every MFMA of the block is issued before the LDS store waits on the next block's
+    // global loads: unfenced, the scheduler sinks late-needed loads next to their store and
+    // exposes their latency
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur);
+    if (more) sstore(cur ^ 1, S0{});
     __syncthreads();
-    for (; kb < ctx.kb1; ++kb) {
-      const bool more = kb + 1 < ctx.kb1;
-      if (more) gload(kb + 1, S0{});
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur);
-      // every MFMA of the block is issued before the LDS store waits on the next block's
-      // global loads: unfenced, the scheduler sank half of them below the store + barrier,
-      // leaving only ~512 MFMA cycles to cover the L2 / MALL load latency
-      if constexpr (PF == 3) __builtin_amdgcn_sched_barrier(0);
-      if (more) sstore(cur ^ 1, S0{});
-      __syncthreads();
-      cur ^= 1;
-    }
-  } else {
-    // register set s holds k-block kb + 1 on entry of a step; the step loads kb + 2 into the
-    // other set, computes kb from LDS, then stores kb + 1 (loaded one full step earlier)
-    auto step = [&](int k, auto S) {
-      constexpr int st = decltype(S)::value;
-      using SO = std::integral_constant<int, 1 - st>;
-      if (k + 2 < ctx.kb1) gload(k + 2, SO{});
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur);
-      __builtin_amdgcn_sched_barrier(0);
-      if (k + 1 < ctx.kb1) sstore(cur ^ 1, S);
-      __syncthreads();
-      cur ^= 1;
-    };
-    if (kb < ctx.kb1) {
-      gload(kb, S0{});
-      if (kb + 1 < ctx.kb1) gload(kb + 1, S1{});
-      sstore(0, S0{});
-    }
-    __syncthreads();
-    for (; kb < ctx.kb1; kb += 2) {
-      step(kb, S1{});
-      if (kb + 1 < ctx.kb1) step(kb + 1, S0{});
-    }
+    cur ^= 1;
   }
 
 #pragma unroll
@@ -330,18 +300,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   }
 }
 
-// ------------------------------------------------------------------ exact split GEMM (x9)
-// Reference-precision GEMM on the bf16 matrix cores: every fp32 operand element is split
-// EXACTLY into three bf16 terms (hi = x with the low 16 bits cleared, mid = (x - hi)
-// likewise, lo = the rest, <= 8 significant bits) while it is staged into LDS, and the 9
-// term products -- each exact in fp32 -- are accumulated in fp32: hi*hi in one
-// accumulator, the 8 smaller products (<= 2^-7 of it) in a second, added at the end.  So
-// the only rounding is fp32 accumulation, as on the fp32 MFMA (error vs fp64 pinned in
-// tests/test_gpu_f32_net.py).  v_mfma_f32_32x32x16_bf16 costs 32 cycles per 32x32x16 where
-// v_mfma_f32_32x32x2_f32 costs 8 x 64: 9 terms = 288 vs 512 cycles, 1.78x fewer.  Its C/D
-// layout is the fp32 32x32x2 layout, so the policies' store epilogues are unchanged.
-// K-major operands only (LDS planes [row][k], pitch BK + 8 bf16 = 16-byte aligned rows,
-// conflict-free ds_read_b128 fragment reads).
+// bf16 helpers of the exact-split conv1 kernels below (every fp32 term split by truncation)
 typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
@@ -349,189 +308,11 @@ __device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two e
 }
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
 
-__device__ __forceinline__ void split4(const f32x4& v, uint2& hi, uint2& mid, uint2& lo) {
-  uint32_t hw[2], mw[2], lw[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float x = v[2 * j], y = v[2 * j + 1];
-    const float xh = trunc_bf16(x), yh = trunc_bf16(y);
-    const float xr = x - xh, yr = y - yh;
-    const float xm = trunc_bf16(xr), ym = trunc_bf16(yr);
-    hw[j] = pack_bf16_hi(xh, yh);
-    mw[j] = pack_bf16_hi(xm, ym);
-    lw[j] = pack_bf16_hi(xr - xm, yr - ym);
-  }
-  hi = make_uint2(hw[0], hw[1]);
-  mid = make_uint2(mw[0], mw[1]);
-  lo = make_uint2(lw[0], lw[1]);
-}
-
 template <class P>
-struct GeoX9 {
-  using G = Geo<P>;
-  static constexpr int P2 = G::BK + 8;                  // bf16 pitch of a term plane row
-  static constexpr int SA2 = G::BM * P2, SB2 = G::BN * P2;
-  static constexpr int STAGE = 3 * (SA2 + SB2);         // bf16 elements per stage
-  static constexpr int LDS_HALVES = 2 * STAGE;
-};
-
-template <class P>
-__device__ __forceinline__ void gemm_body_x9(const typename P::Args& args, int block, uint16_t* lds,
-                                             typename P::Smem& sm) {
-  using G = Geo<P>;
-  using X = GeoX9<P>;
-  static_assert(P::A_KMAJ && P::B_KMAJ && !HasColsum<P>::value, "x9 body: K-major operands, no colsum");
-  static_assert(G::BK % 16 == 0, "k-steps of 16");
-  typename P::Ctx ctx;
-  P::decode(args, block, ctx, sm);
-  if constexpr (P::SMEM) __syncthreads();
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave % G::WM, wn = wave / G::WM;
-  const int r = lane & 31, h = lane >> 5;
-  f32x16 acc[G::TM][G::TN], acc2[G::TM][G::TN];
-#pragma unroll
-  for (int i = 0; i < G::TM; ++i)
-#pragma unroll
-    for (int j = 0; j < G::TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = acc2[i][j][e] = 0.f;
-  f32x4 ra[G::NA], rb[G::NB];
-  typename RowAOf<P>::type rowa[G::NA];
-  typename RowBOf<P>::type rowb[G::NB];
-  if constexpr (HasRowA<P>::value) {
-#pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int q = min(t + 256 * j, G::CA - 1);
-      rowa[j] = P::row_a(args, ctx, q / G::RA, q % G::RA);
-    }
-  }
-  if constexpr (HasRowB<P>::value) {
-#pragma unroll
-    for (int j = 0; j < G::NB; ++j) {
-      const int q = min(t + 256 * j, G::CB - 1);
-      rowb[j] = P::row_b(args, ctx, q / G::RB, q % G::RB);
-    }
-  }
-  auto gload = [&](int kb) {
-#pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int q = t + 256 * j;
-      if (G::CA % 256 == 0 || q < G::CA) {
-        if constexpr (HasRowA<P>::value) ra[j] = P::load_a_row(args, ctx, rowa[j], kb);
-        else ra[j] = P::load_a(args, ctx, sm, kb, q / G::RA, q % G::RA);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < G::NB; ++j) {
-      const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) {
-        if constexpr (HasRowB<P>::value) rb[j] = P::load_b_row(args, ctx, rowb[j], kb);
-        else rb[j] = P::load_b(args, ctx, sm, kb, q / G::RB, q % G::RB);
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-    uint16_t* As = lds + buf * X::STAGE;
-    uint16_t* Bs = As + 3 * X::SA2;
-#pragma unroll
-    for (int j = 0; j < G::NA; ++j) {
-      const int q = t + 256 * j;
-      if (G::CA % 256 == 0 || q < G::CA) {
-        uint2 hi, mid, lo;
-        split4(ra[j], hi, mid, lo);
-        uint16_t* d = As + (q / G::RA) * X::P2 + 4 * (q % G::RA);
-        *reinterpret_cast<uint2*>(d) = hi;
-        *reinterpret_cast<uint2*>(d + X::SA2) = mid;
-        *reinterpret_cast<uint2*>(d + 2 * X::SA2) = lo;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < G::NB; ++j) {
-      const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) {
-        uint2 hi, mid, lo;
-        split4(rb[j], hi, mid, lo);
-        uint16_t* d = Bs + (q / G::RB) * X::P2 + 4 * (q % G::RB);
-        *reinterpret_cast<uint2*>(d) = hi;
-        *reinterpret_cast<uint2*>(d + X::SB2) = mid;
-        *reinterpret_cast<uint2*>(d + 2 * X::SB2) = lo;
-      }
-    }
-  };
-  auto compute = [&](int buf) {
-    const uint16_t* As = lds + buf * X::STAGE;
-    const uint16_t* Bs = As + 3 * X::SA2;
-#pragma unroll
-    for (int kc = 0; kc < G::BK / 16; ++kc) {
-      bfx8 a[G::TM][3], b[G::TN][3];
-#pragma unroll
-      for (int mi = 0; mi < G::TM; ++mi) {
-        const uint16_t* ap = As + (wm * G::WTM + mi * 32 + r) * X::P2 + kc * 16 + 8 * h;
-#pragma unroll
-        for (int u = 0; u < 3; ++u) a[mi][u] = *reinterpret_cast<const bfx8*>(ap + u * X::SA2);
-      }
-#pragma unroll
-      for (int ni = 0; ni < G::TN; ++ni) {
-        const uint16_t* bp = Bs + (wn * G::WTN + ni * 32 + r) * X::P2 + kc * 16 + 8 * h;
-#pragma unroll
-        for (int u = 0; u < 3; ++u) b[ni][u] = *reinterpret_cast<const bfx8*>(bp + u * X::SB2);
-      }
-#pragma unroll
-      for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < G::TN; ++ni) {
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][0], acc[mi][ni], 0, 0, 0);
-          f32x16 c2 = acc2[mi][ni];
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][1], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][0], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][1], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][2], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][0], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][2], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][1], c2, 0, 0, 0);
-          c2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][2], c2, 0, 0, 0);
-          acc2[mi][ni] = c2;
-        }
-    }
-  };
-  int kb = ctx.kb0, cur = 0;
-  if (kb < ctx.kb1) {
-    gload(kb);
-    sstore(0);
-  }
-  __syncthreads();
-  for (; kb < ctx.kb1; ++kb) {
-    const bool more = kb + 1 < ctx.kb1;
-    if (more) gload(kb + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cur);
-    if (more) sstore(cur ^ 1);
-    __syncthreads();
-    cur ^= 1;
-  }
-#pragma unroll
-  for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < G::TN; ++ni)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-        P::store(args, ctx, wm * G::WTM + mi * 32 + row, wn * G::WTN + ni * 32 + r, acc[mi][ni][e] + acc2[mi][ni][e]);
-      }
-}
-
-template <class P>
-__global__ __launch_bounds__(256) void gemm_x9_k(typename P::Args args, int remap) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[GeoX9<P>::LDS_HALVES];
-  __shared__ typename P::Smem sm;
-  gemm_body_x9<P>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds, sm);
-}
-
-template <class P, int PF>
-__global__ __launch_bounds__(256) void gemm_k(typename P::Args args, int remap) {
+__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
-  gemm_body<P, PF>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds, sm);
+  gemm_body<P>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
 
 template <int A, int B>
@@ -541,7 +322,7 @@ struct MaxI {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2, int PF>
+template <class P1, class P2>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
   __shared__ union {
@@ -549,106 +330,9 @@ __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1, PF>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2, PF>(a2, (int)blockIdx.x - n1, lds, sm.s2);
-}
-
-// ------------------------------------------------------------------ LDS-DMA ring body (knob 23)
-// The register-staged body keeps ONE k-block in flight per workgroup (global -> registers ->
-// ds_write), and every body measured moves its k-blocks at ~5 TB/s chip-wide: one k-block per
-// ~2 us of loaded-memory latency (profiles/r3_px_findings.md).  Here the operands go straight
-// from global memory into LDS with global_load_lds_dwordx4 (LDS-DMA: no registers, no ds_write)
-// into an S-stage ring, so S - 1 k-blocks are in flight while one is computed; a counted
-// s_waitcnt vmcnt + raw s_barrier retires exactly the stage about to be read (a __syncthreads
-// would drain every DMA, vmcnt(0)).  K-major A and B only (the forward GEMMs): BK = 32 fp32 =
-// 128-byte rows, each wave-instruction fills 8 rows x 128 B (lane-linear destination), the
-// 16-byte chunk a lane fetches is XOR-swizzled on the SOURCE side (chunk c of row r lands in
-// slot c ^ ((r >> 1) & 7)) so the ds_read_b128 fragment reads are bank-conflict-free.  Rows past
-// the tile's end read a zero page.  The MFMA chain runs in the register body's k order, so the
-// results are bit-identical to it.
-__device__ __attribute__((aligned(16))) float g_zero_page[64];
-
-// all but the newest S - 2 stages (4 DMAs each) landed, and this wave's LDS reads of the stage
-// the next DMA overwrites are complete (the compiler hoists the next iteration's raw barrier
-// above the last fragment reads' lgkmcnt wait)
-template <int S>
-__device__ __forceinline__ void wait_stage_dma() {
-  if constexpr (S == 2) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  else if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-}
-
-template <class P, int S>
-__device__ __forceinline__ void gemm_body_g(const typename P::Args& args, int block, float* lds) {
-  static_assert(P::A_KMAJ && P::B_KMAJ && P::BK == 32 && P::BM == 64 && P::BN == 64 && P::WM == 2,
-                "LDS-DMA body: K-major 64 x 64 x 32 tiles, 2 x 2 waves");
-  static_assert(S >= 2 && S <= 4, "2..4 stages");
-  constexpr int ST = 2 * 64 * 32;  // floats per stage: A then B, [64 rows][32] each, swizzled
-  typename P::Ctx ctx;
-  typename P::Smem sm;
-  P::decode(args, block, ctx, sm);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int wm = wave & 1, wn = wave >> 1, r = lane & 31, h = lane >> 5;
-  // this lane's DMA rows: (2 wave + i) * 8 + lane / 8, i = 0, 1; the slot it fills is lane & 7,
-  // the chunk it fetches is slot ^ swizzle(row)
-  typename P::RowA ra[2];
-  typename P::RowB rb[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = (2 * wave + i) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    ra[i] = P::row_a(args, ctx, row, ch);
-    rb[i] = P::row_b(args, ctx, row, ch);
-  }
-  auto issue = [&](int kb, int slot) {
-    float* st = lds + slot * ST;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float* ga = P::ptr_a_row(args, ctx, ra[i], kb);
-      const float* gb = P::ptr_b_row(args, ctx, rb[i], kb);
-      __builtin_amdgcn_global_load_lds(ga ? ga : g_zero_page,
-                                       (__attribute__((address_space(3))) void*)(st + (2 * wave + i) * 256), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(gb ? gb : g_zero_page,
-                                       (__attribute__((address_space(3))) void*)(st + 64 * 32 + (2 * wave + i) * 256),
-                                       16, 0, 0);
-    }
-  };
-  f32x16 acc = {};
-  const int kb0 = ctx.kb0, kb1 = ctx.kb1;
-  // prologue: stages kb0 .. kb0 + S - 2 (clamped: a redundant refetch of the last k-block
-  // keeps the DMA count per iteration constant, so the vmcnt immediates stay exact)
-#pragma unroll
-  for (int j = 0; j < S - 1; ++j) issue(min(kb0 + j, kb1 - 1), j);
-  const int ar = wm * 32 + r, br = wn * 32 + r, sa = (ar >> 1) & 7, sb = (br >> 1) & 7;
-  for (int kb = kb0; kb < kb1; ++kb) {
-    const int it = kb - kb0;
-    wait_stage_dma<S>();
-    __builtin_amdgcn_s_barrier();  // every wave's DMAs of stage it landed; stage it - 1 is free
-    issue(min(kb + S - 1, kb1 - 1), (it + S - 1) % S);
-    const float* As = lds + (it % S) * ST;
-    const float* Bs = As + 64 * 32;
-#pragma unroll
-    for (int kc = 0; kc < 4; ++kc) {
-      const int c = 2 * kc + h;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(As + ar * 32 + 4 * (c ^ sa));
-      const f32x4 b = *reinterpret_cast<const f32x4*>(Bs + br * 32 + 4 * (c ^ sb));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[i], acc, 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing refetches land before exit
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-    P::store(args, ctx, wm * 32 + row, wn * 32 + r, acc[e]);
-  }
-}
-
-template <class P, int S>
-__global__ __launch_bounds__(256) void gemm_g_k(typename P::Args args, int remap) {
-  __shared__ __attribute__((aligned(16))) float lds[S * 2 * 64 * 32];
-  gemm_body_g<P, S>(args, remap ? xcd_chunk(blockIdx.x, gridDim.x) : blockIdx.x, lds);
+    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -656,52 +340,6 @@ __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
 }
 
 // ------------------------------------------------------------------ forward policies
-template <int BM_, int BN_, int BK_, int WM_>
-struct Conv1FwdT {  // a1[m][n] = relu(sum_k frame(m, k) W1[n][k] + b1[n]), k = (c, ky, kx)
-  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
-  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = true;
-  static_assert(BM <= 400 && 256 % BK == 0, "a tile touches <= 2 samples");
-  using Args = F32Set;
-  struct Smem {
-    const uint8_t* pl[2][4];  // frame planes of the (<= 2) samples the tile touches
-  };
-  struct Ctx {
-    F32Prob p;
-    int M, m0, s0, kb0, kb1;
-  };
-  static __host__ __device__ int tiles(int B) { return (B * 400 + BM - 1) / BM; }
-  static __device__ void decode(const Args& a, int block, Ctx& c, Smem& sm) {
-    const int tp = tiles(a.B);
-    c.p = pick(a, block / tp);
-    c.M = a.B * 400;
-    c.m0 = (block % tp) * BM;
-    c.s0 = c.m0 / 400;
-    c.kb0 = 0;
-    c.kb1 = 256 / BK;
-    const int t = threadIdx.x;
-    if (t < 8) {
-      const int b = c.s0 + (t >> 2), ch = t & 3;
-      const FrameSrc f{static_cast<const uint8_t*>(c.p.in), c.p.ids, c.p.idx};
-      sm.pl[t >> 2][ch] = b < a.B ? frame_plane(f, b, ch, kPlane) : nullptr;
-    }
-  }
-  static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem& sm, int kb, int row, int ch) {
-    const int m = c.m0 + row;
-    if (m >= c.M) return zero4();
-    const int b = m / 400, p = m - b * 400, oy = p / 20, ox = p - oy * 20;
-    const int k = kb * BK + 4 * ch, cc = k >> 6, ky = (k >> 3) & 7, kx = k & 7;
-    const uint8_t* pl = sm.pl[b - c.s0][cc];
-    return u8x4(*reinterpret_cast<const uint32_t*>(pl + (4 * oy + ky) * 84 + 4 * ox + kx));
-  }
-  static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
-    return ld4(c.p.w + n * 256 + kb * BK + 4 * ch);
-  }
-  static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
-    const int m = c.m0 + ml;
-    if (m < c.M) c.p.out[(size_t)m * 32 + n] = fmaxf(v + c.p.bias[n], 0.f);
-  }
-};
-
 template <int BM_, int BN_, int BK_, int WM_>
 struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32 + ci; w = w2p
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
@@ -755,13 +393,8 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
     const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;  // wave-uniform
     return r.p ? ld4(r.p + (ky * 20 + kx) * 32 + (k0 & 31)) : zero4();
   }
-  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;
-    return r.p ? r.p + (ky * 20 + kx) * 32 + (k0 & 31) : nullptr;
-  }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 512 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
-  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -820,13 +453,8 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
     const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
     return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (k0 & 63)) : zero4();
   }
-  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;
-    return r.p ? r.p + (ky * 9 + kx) * 64 + (k0 & 63) : nullptr;
-  }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 576 + 4 * ch}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
-  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -872,7 +500,7 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
     const int b = c.m0 + ml;
     if (b < c.B) c.p.out[((size_t)c.split * c.B + b) * 256 + c.n0 + nl] = v;
   }
-  // row states for the LDS-DMA body (gemm_g_k)
+  // row states: the chunk's row base pointers (k-invariant)
   struct RowA {
     const float* p;
   };
@@ -886,307 +514,13 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
   static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
     return r.p ? ld4(r.p + kb * BK) : zero4();
   }
-  static __device__ const float* ptr_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    return r.p ? r.p + kb * BK : nullptr;
-  }
   static __device__ RowB row_b(const Args&, const Ctx& c, int nl, int ch) {
     return {c.p.w + (size_t)(c.n0 + nl) * 3136 + 4 * ch};
   }
   static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
-  static __device__ const float* ptr_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return r.p + kb * BK; }
 };
 
-// conv1 forward, sample-resident: one workgroup per (problem, sample).  The sample's four
-// 84x84 u8 planes (28 KB) are staged once into LDS with 16-byte loads (the GEMM-body
-// version gathered every 8x8 window from global memory, 4 bytes per load, each pixel four
-// times over); each wave keeps its half of W1 (16 output channels x K = 256) in registers
-// for the whole sample and sweeps output pixels in 16-row tiles on v_mfma_f32_16x16x4_f32:
-// 400 = 25 tiles exactly, waves {0,1} take channels 0-15 and {2,3} channels 16-31, each
-// pair splitting the 25 tiles 13/12.  A operand: lane (i = l & 15, q = l >> 4) reads ONE
-// dword of the plane row = 4 u8 pixels = k-slots 4q..4q+3 of a 16-k block (two ky rows x
-// 8 kx), converted with v_cvt_f32_ubyte*; MFMA i' of the block consumes element i', so its
-// k-slot q is k = 16 kb + 4q + i' and B (W1 row, reference k order) uses the same map.
-// Two accumulators (even / odd k-blocks) cover the 40-cycle dependent-MFMA latency.
 constexpr int kPlaneDw = kPlane / 4;  // 1764 dwords per plane
-__global__ __launch_bounds__(256) void f32_conv1_fwd_k(F32Set set) {
-  __shared__ __attribute__((aligned(16))) uint32_t pl[4 * kPlaneDw];
-  const int B = set.B, prob = blockIdx.x / B, b = blockIdx.x - prob * B;
-  const F32Prob p = pick(set, prob);
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int j = lane & 15, q = lane >> 4, nh = wave >> 1;
-  // stage the planes: 4 x 441 16-byte chunks, all loads in flight before the first store
-  {
-    const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
-    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kChunks + 255) / 256;
-    const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
-    const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
-    const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
-    const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
-    uint4 v[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {  // (no dynamically indexed pointer array: it would live in scratch)
-      const int e = min(t + 256 * i, kChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
-      const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
-      v[i] = sc[e - c * 441];
-    }
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = t + 256 * i;
-      if (e < kChunks) reinterpret_cast<uint4*>(pl)[e] = v[i];
-    }
-  }
-  // W1 fragments of this wave's 16 channels: breg[kb] = W1[nh*16 + j][16 kb + 4q .. +3]
-  f32x4 breg[16];
-  const float* wrow = p.w + (nh * 16 + j) * 256 + 4 * q;
-#pragma unroll
-  for (int kb = 0; kb < 16; ++kb) breg[kb] = ld4(wrow + 16 * kb);
-  __syncthreads();
-  const float bias = p.bias[nh * 16 + j];
-  float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + j;
-  for (int tile = wave & 1; tile < 25; tile += 2) {
-    const int m = tile * 16 + j, oy = m / 20, ox = m - oy * 20;
-    const uint32_t* a0 = pl + (4 * oy + (q >> 1)) * 21 + ox + (q & 1);
-    f32x4 acc0 = zero4(), acc1 = zero4();
-#pragma unroll
-    for (int kb = 0; kb < 16; kb += 2) {
-      // k-block kb: channel kb >> 2, rows ky = 2 (kb & 3) + (q >> 1)
-      const f32x4 x0 = u8x4(a0[(kb >> 2) * kPlaneDw + 2 * (kb & 3) * 21]);
-      const f32x4 x1 = u8x4(a0[((kb + 1) >> 2) * kPlaneDw + 2 * ((kb + 1) & 3) * 21]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[i], breg[kb][i], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[i], breg[kb + 1][i], acc1, 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) out[(size_t)(tile * 16 + 4 * q + e) * 32] = fmaxf(acc0[e] + acc1[e] + bias, 0.f);
-  }
-}
-
-// conv2 / conv3 forward, sample-resident (knob 25).  Every GEMM-body form of these layers
-// landed at ~90 TF/s: a 64 x 64 tile streams its im2col A rows from L2 (conv2: each input
-// pixel gathered 3.2x, conv3 2.9x) and at N = 64 each A float feeds only 64 MACs, so the
-// chip-wide k-block rate (~5 TB/s, profiles/r3_px_findings.md) caps them below the fp32
-// MFMA peak whatever the pipeline depth.  Here the im2col never leaves the CU:
-//   * a persistent workgroup (one per CU, 4 waves) owns a contiguous range of 16-row output
-//     tiles of ONE problem; the input samples its tiles touch stream whole into a 3-slot LDS
-//     ring with global_load_lds_dwordx4 (LDS-DMA, no registers), one sample ahead of use, so
-//     each input byte crosses L2 -> CU once;
-//   * wave w keeps output channels 16w .. 16w+15 of the weights in registers for the whole
-//     kernel (B operand, K/4 f32x4), so the only per-MFMA operand traffic is the A fragment:
-//     one ds_read_b128 (4 k of one im2col row) per 4 v_mfma_f32_16x16x4_f32;
-//   * k order: 16-k steps st (tap = 16 st / C, channels c16 = 16 st % C); lane (i = l & 15,
-//     g = l >> 4) holds k = 16 st + 4 g .. +3, MFMA s of the step takes element s (A and B
-//     share the map, so the sum is the same up to fp32 rounding order);
-//   * LDS image of a sample: its [pixel][C] fp32 block as 256-byte rows (row q = input row
-//     iy = q / W, column block x = q % W), 16-byte chunk col of row q stored at slot
-//     col ^ h(q), h = (2 x + HB iy) & 15: the 16 rows of a tile span 2-3 output rows, and a plain
-//     q & 15 swizzle put rows of different output rows on one slot (3-way ds_read_b128 bank
-//     conflicts, SQ_LDS_BANK_CONFLICT 7.7x the LDS cycles); the even x coefficient keeps the
-//     lane groups' k-chunks (col ^ 1) apart and HB staggers the input rows -- 4.7 / 5.2 LDS
-//     cycles per read for conv2 / conv3 (4 = conflict-free) in a bank model of every tile;
-//   * G tiles per group (64 / 48 rows < one sample) keep G independent accumulator chains
-//     (covers the 40-cycle dependent MFMA latency) and let a group touch at most 2 samples:
-//     the ring's third slot fills while they are read.
-template <int L>
-struct DConv;
-// W = 256-byte image rows per input row, HB = the swizzle's input-row coefficient
-template <>
-struct DConv<2> {
-  static constexpr int IH = 20, C = 32, OH = 9, K = 4, S = 2, W = 10, HB = 1;
-  static constexpr int G1 = 4, G2 = 4;  // tiles per group at 4 / 8 waves
-};
-template <>
-struct DConv<3> {
-  static constexpr int IH = 9, C = 64, OH = 7, K = 3, S = 1, W = 9, HB = 14;
-  static constexpr int G1 = 3, G2 = 2;
-};
-template <int L>
-struct DGeo {
-  using D = DConv<L>;
-  static constexpr int P = D::OH * D::OH, PIX = D::IH * D::IH, KK = D::K * D::K * D::C, NST = KK / 16;
-  static constexpr int ROWS = PIX * D::C / 64;           // 256-byte rows of a sample image
-  static constexpr int NI = (ROWS + 3) / 4;              // 1 KB DMA wave-instructions per sample
-  static constexpr int SLOT = NI * 256;                  // floats per ring slot
-  static_assert(D::C % 16 == 0 && (PIX * D::C) % 64 == 0, "whole 16-k steps, whole rows");
-  static_assert(32 * D::G1 < 2 * P + 2 && 32 * D::G2 < 2 * P + 2, "a group and the next stay within 3 ring slots");
-  static_assert(3 * SLOT * 4 <= 160 * 1024, "3-slot ring fits the 160 KB LDS");
-};
-constexpr int kDconvTile = 16;
-
-template <int L>
-__device__ __forceinline__ int dconv_swz(int q) {
-  using D = DConv<L>;
-  return (2 * (q % D::W) + D::HB * (q / D::W)) & 15;
-}
-
-// MH = 1: 4 waves, each every tile of a group; MH = 2: 8 waves (two per SIMD, one's MFMAs
-// cover the other's LDS waits), waves 4 mh .. 4 mh + 3 take the group's mh-th half
-// DBG (knob 25 = 4 | 5: MH 1 | 2): every wave adds its cycles per phase (s_memtime) and writes
-// them to the int64 buffer passed as the problem's w2 pointer: [wg][wave][wait, issue, setup,
-// steps, total]
-template <int L, int MH, bool DBG = false>
-__device__ __forceinline__ void conv_fwd_direct_body(const F32Set& set, int tpw, int wgpp, float* ring) {
-  using D = DConv<L>;
-  using Q = DGeo<L>;
-  constexpr int G = MH == 1 ? D::G1 : D::G2, GW = G / MH, P = Q::P, C4 = D::C / 4;
-  static_assert(G % MH == 0, "whole tiles per wave");
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nq = wave & 3, mh = wave >> 2;
-  const int i16 = lane & 15, g = lane >> 4;
-  const int prob = blockIdx.x / wgpp;
-  const F32Prob p = pick(set, prob);
-  const int M = set.B * P, Tp = (M + kDconvTile - 1) / kDconvTile;
-  const int t0 = (blockIdx.x - prob * wgpp) * tpw, t1 = min(Tp, t0 + tpw);
-  if (t0 >= t1) return;  // whole workgroup, before any barrier
-  long long ph[5] = {0, 0, 0, 0, 0}, tq0 = DBG ? clock64() : 0, tq;
-  auto stamp = [&](int i) {
-    if constexpr (DBG) {
-      const long long now = clock64();
-      ph[i] += now - tq;
-      tq = now;
-    }
-  };
-  const int rend = min(kDconvTile * t1, M);
-  const int sf = kDconvTile * t0 / P;  // first sample of the range (local sample 0)
-  const float* in = static_cast<const float*>(p.in) + (size_t)sf * Q::PIX * D::C;
-  // local sample j -> ring slot j % 3; wave-instruction i fills rows 4i .. 4i+3 lane-linearly,
-  // so lane l fetches the logical chunk stored at slot (l & 15) of row 4i + (l >> 4)
-  auto issue_one = [&](int j, int i) {
-    const float* src = in + (size_t)j * Q::PIX * D::C;
-    const int q = 4 * i + g, u = q * 16 + (i16 ^ dconv_swz<L>(q));
-    __builtin_amdgcn_global_load_lds(q < Q::ROWS ? src + 4 * u : src,
-                                     (__attribute__((address_space(3))) void*)(ring + (j % 3) * Q::SLOT + i * 256),
-                                     16, 0, 0);
-  };
-  auto issue = [&](int j) {
-    for (int i = wave; i < Q::NI; i += 4 * MH) issue_one(j, i);
-  };
-  auto last_sample = [&](int tg) { return (min(kDconvTile * (tg + G), rend) - 1) / P - sf; };
-  int loaded = 0;
-  for (const int hi = last_sample(t0); loaded <= hi; ++loaded) issue(loaded);
-  // this wave's 16 output channels of W (w2p / w3p rows, k-contiguous)
-  const int n = 16 * nq + i16;
-  f32x4 bw[Q::NST];
-  const float* wrow = p.w + (size_t)n * Q::KK + 4 * g;
-#pragma unroll
-  for (int st = 0; st < Q::NST; ++st) bw[st] = ld4(wrow + 16 * st);
-  const float bias = p.bias[n];
-  float* out = p.out + n;
-  // a group's results are stored after the NEXT group's DMA wait (stores count in vmcnt: stored
-  // at the group's end, the wait at the next group's start would drain their round trip)
-  f32x4 pacc[GW];
-  int ptg = -1;
-  auto store_one = [&](int tq, int k, int e) {  // D[row 4g + e][col i16] of tile tq + mh GW + k -> a2/a3 row n
-    const int r = kDconvTile * (tq + mh * GW + k) + 4 * g + e;
-    if (r < rend) out[(size_t)r * 64] = fmaxf(pacc[k][e] + bias, 0.f);
-  };
-  auto store = [&](int tq) {
-#pragma unroll
-    for (int k = 0; k < GW; ++k)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) store_one(tq, k, e);
-  };
-  if constexpr (DBG) tq = clock64();
-  for (int tg = t0; tg < t1; tg += G) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs (and stores) landed
-    __syncthreads();                                  // every wave's; the previous group is read
-    stamp(0);
-    // the next group's new sample (at most one: a group is < one sample of rows) goes out one
-    // DMA wave-instruction per MFMA step, and the previous group's results one store per step:
-    // issued back to back they filled the memory queue and stalled the wave ~2.9k cycles a group
-    int pend = -1;
-    if (tg + G < t1) {
-      const int hi = last_sample(tg + G);
-      for (; loaded < hi; ++loaded) issue(loaded);
-      if (loaded == hi) pend = loaded++;
-    }
-    stamp(1);
-    // per tile: this lane's im2col row -> (ring slot base, window origin pixel)
-    // (its image row at tap (0, 0) + slot base, and the swizzle there).  A tap (ky, kx) moves
-    // the row by dq = ky W + kx C / 64 (x stays inside the input row: no carry into iy) and the
-    // swizzle by dh = 2 kx C / 64 + HB ky; the chunk within the row is col + g with col =
-    // (kx C / 4) % 16 + k-chunk a multiple of 4, so the slot is col ^ (g ^ h): per tile and
-    // distinct dh (conv2 6, conv3 5) the byte offset of chunk g ^ h is kept, and a read costs
-    // one XOR with 16 col, its dq lands in the ds_read offset field
-    int ad[GW][16];
-#pragma unroll
-    for (int k = 0; k < GW; ++k) {
-      const int r = min(kDconvTile * (tg + mh * GW + k) + i16, rend - 1);
-      const int s = r / P, pos = r - s * P, oy = pos / D::OH, ox = pos - oy * D::OH;
-      const int q = D::S * (oy * D::IH + ox) * C4 / 16;  // window origin (x, iy) = (S ox C / 64, S oy)
-      const int qb = ((s - sf) % 3) * (Q::SLOT / 4) + q * 16;
-      const int hb = 2 * (q % D::W) + D::HB * (q / D::W);
-#pragma unroll
-      for (int d = 0; d < 16; ++d) ad[k][d] = 16 * (qb + (g ^ ((hb + d) & 15)));  // unused d: dead code
-    }
-    const char* lds_b = reinterpret_cast<const char*>(ring);
-    auto read = [&](int st, int k) {
-      const int k0 = 16 * st, tap = k0 / D::C, ky = tap / D::K, kx = tap - ky * D::K;
-      const int dq = ky * D::W + kx * D::C / 64, col = (kx * C4) % 16 + (k0 % D::C) / 4;
-      const int dh = (2 * (kx * D::C / 64) + D::HB * ky) & 15;
-      return *reinterpret_cast<const f32x4*>(lds_b + ((ad[k][dh] ^ (16 * col)) + 256 * dq));
-    };
-    f32x4 acc[GW], a[GW], an[GW];
-#pragma unroll
-    for (int k = 0; k < GW; ++k) {
-      acc[k] = zero4();
-      a[k] = read(0, k);
-    }
-    stamp(2);
-#pragma unroll
-    for (int st = 0; st < Q::NST; ++st) {
-      // the next step's reads go out between this step's first MFMAs, one (XOR + ds_read) per
-      // MFMA gap (one wave per SIMD: a cluster of them longer than a 32-cycle gap idles the
-      // MFMA pipe); the compiler waits for LDS with lgkmcnt(0) at the next step's first MFMA,
-      // a whole step later.  The DMA / store of the step follow in later gaps.
-      if (st + 1 < Q::NST) {
-#pragma unroll
-        for (int k = 0; k < GW; ++k) an[k] = read(st + 1, k);
-      }
-      if (pend >= 0 && wave + 4 * MH * st < Q::NI) issue_one(pend, wave + 4 * MH * st);
-      if (st < 4 * GW && ptg >= 0) store_one(ptg, st / 4, st % 4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int k = 0; k < GW; ++k) acc[k] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k][s], bw[st][s], acc[k], 0, 0, 0);
-      if (st + 1 < Q::NST) {
-#pragma unroll
-        for (int k = 0; k < GW; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // VALU (the XOR)
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-        }
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // VMEM (DMA or store)
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 4 * GW, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k = 0; k < GW; ++k) a[k] = an[k];
-    }
-#pragma unroll
-    for (int k = 0; k < GW; ++k) pacc[k] = acc[k];
-    ptg = tg;
-    stamp(3);
-  }
-  store(ptg);
-  if constexpr (DBG) {
-    ph[4] = clock64() - tq0;
-    if (lane == 0) {
-      long long* o = const_cast<long long*>(reinterpret_cast<const long long*>(p.w2)) + ((size_t)blockIdx.x * 4 * MH + wave) * 5;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) o[i] = ph[i];
-    }
-  }
-}
-
-template <int L, int MH, bool DBG = false>
-__global__ __launch_bounds__(256 * MH) void f32_conv_fwd_direct_k(F32Set set, int tpw, int wgpp) {
-  __shared__ __attribute__((aligned(16))) float ring[3 * DGeo<L>::SLOT];
-  conv_fwd_direct_body<L, MH, DBG>(set, tpw, wgpp, ring);
-}
 
 // conv1 forward at reference precision on the bf16 matrix cores (exact three-term split).
 //  * Input pixels are u8 (0..255, 8 significant bits): exactly representable in bf16.
@@ -1321,7 +655,6 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
         const float y = fmaxf(ah[e] + al[e] + bias, 0.f);
         const size_t o = (size_t)(tile * 16 + 4 * q + e) * 32;
         out[o] = y;
-        if (p.outx) store_planes(p.outx, p.outx_ps, (size_t)b * 400 * 32 + nh * 16 + i + o, y);  // px forward
       }
     }
   }
@@ -1340,7 +673,6 @@ struct BwdArgs {
   int B;
   int kbps;             // wgrad: k-blocks per split
   int splits;
-  int xcd_group;        // conv wgrad: the n-tiles of a split on one XCD (f32_set_variant(18, 1))
 };
 
 struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
@@ -1425,14 +757,12 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
 // im2col address of a row is (sample) * plane + (position, tap) offset -- the position is
 // uniform per k-block (scalar), where sample-major rows paid ~30 VALU per 16-byte load
 // dividing the row index by P and OH (MI355X: conv3 wgrad 45 -> see profiles).
-// BN_ (knob 24): the (tap, ci) width of a workgroup's tile -- each dy k-block it stages is
-// re-read by N / BN_ workgroups, so wider tiles move fewer L2 bytes per FLOP
-template <int L, int BN_ = 64>
+template <int L>
 struct ConvWgrad {
   static constexpr int C = L == 3 ? 64 : 32, K = L == 3 ? 3 : 4, S = L == 3 ? 1 : 2;
   static constexpr int IH = L == 3 ? 9 : 20, OH = L == 3 ? 7 : 9, P = OH * OH;
   static constexpr int N = K * K * C;
-  static constexpr int BM = 64, BN = BN_, BK = 32, WM = 2;
+  static constexpr int BM = 64, BN = 64, BK = 32, WM = 2;
   static_assert(N % BN == 0, "whole tiles");
   static constexpr bool A_KMAJ = false, B_KMAJ = false, SMEM = false, A_COLSUM = true;
   using Args = BwdArgs;
@@ -1444,19 +774,8 @@ struct ConvWgrad {
   static __host__ __device__ int tiles(int, int splits) { return (N / BN) * splits; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     constexpr int NT = N / BN;
-    const int full = a.xcd_group ? (a.splits / 8) * 8 * NT : 0;
-    if (block < full) {
-      // workgroups go to XCD blockIdx % 8: XCD x takes every n-tile of splits x, x + 8, ...,
-      // so the NT workgroups that read the same dy rows and overlapping input windows of a
-      // split share one L2 (the plain order spreads them over all 8 XCDs)
-      const int x = block & 7, j = block >> 3;
-      c.split = (j / NT) * 8 + x;
-      c.n0 = (j % NT) * BN;
-    } else {
-      const int r = block - full;
-      c.split = full / NT + r / NT;
-      c.n0 = (r % NT) * BN;
-    }
+    c.split = block / NT;
+    c.n0 = (block % NT) * BN;
     c.nbb = (a.B + BK - 1) / BK;
     c.kb0 = c.split * a.kbps;
     c.kb1 = min(c.kb0 + a.kbps, kblocks(a.B));
@@ -1506,83 +825,6 @@ struct ConvWgrad {
   }
 };
 
-struct Conv3Dgrad {  // dy2[b][pi][ci] = (a2 > 0) * sum_{tap, co} dy3[b][pi - tap][co] W3[co][ci][tap]
-  static constexpr int BM = 128, BN = 64, BK = 32, WM = 2;
-  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
-  using Args = BwdArgs;
-  using Smem = NoSmem;
-  struct Ctx {
-    int M, m0, kb0, kb1;
-  };
-  static __host__ __device__ int tiles(int B) { return (B * 81 + BM - 1) / BM; }
-  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
-    c.M = a.B * 81;
-    c.m0 = block * BM;
-    c.kb0 = 0;
-    c.kb1 = 18;
-  }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int m = c.m0 + row;
-    if (m >= c.M) return zero4();
-    const int b = m / 81, pi = m - b * 81, iy = pi / 9, ix = pi - iy * 9;
-    const int tap = kb >> 1, ky = tap / 3, kx = tap - ky * 3, oy = iy - ky, ox = ix - kx;
-    if (oy < 0 || oy >= 7 || ox < 0 || ox >= 7) return zero4();
-    return ld4(a.dy + ((size_t)b * 49 + oy * 7 + ox) * 64 + (kb & 1) * 32 + 4 * ch);
-  }
-  static __device__ f32x4 load_b(const Args& a, const Ctx&, const Smem&, int kb, int n, int ch) {
-    const int tap = kb >> 1, co = (kb & 1) * 32 + 4 * ch;
-    return ld4(a.w + (tap * 64 + n) * 64 + co);  // w3t [tap][ci][co]
-  }
-  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
-    const int m = c.m0 + ml;
-    if (m >= c.M) return;
-    const size_t o = (size_t)m * 64 + n;
-    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
-  }
-};
-
-// conv2 dgrad as 4 stride-1 sub-pixel problems: input pixel (iy, ix) = (2jy + py, 2jx + px)
-// receives taps ky = py + 2ty, kx = px + 2tx from output pixel (jy - ty, jx - tx)
-struct Conv2Dgrad {
-  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
-  static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
-  using Args = BwdArgs;
-  using Smem = NoSmem;
-  struct Ctx {
-    int M, m0, cls, kb0, kb1;
-  };
-  static __host__ __device__ int tiles(int B) { return 4 * ((B * 100 + BM - 1) / BM); }
-  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
-    const int tc = (a.B * 100 + BM - 1) / BM;
-    c.cls = block / tc;
-    c.m0 = (block % tc) * BM;
-    c.M = a.B * 100;
-    c.kb0 = 0;
-    c.kb1 = 8;
-  }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int m = c.m0 + row;
-    if (m >= c.M) return zero4();
-    const int b = m / 100, j = m - b * 100, jy = j / 10, jx = j - jy * 10;
-    const int t = kb >> 1, oy = jy - (t >> 1), ox = jx - (t & 1);
-    if (oy < 0 || oy >= 9 || ox < 0 || ox >= 9) return zero4();
-    return ld4(a.dy + ((size_t)b * 81 + oy * 9 + ox) * 64 + (kb & 1) * 32 + 4 * ch);
-  }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
-    const int t = kb >> 1, ky = (c.cls >> 1) + 2 * (t >> 1), kx = (c.cls & 1) + 2 * (t & 1);
-    const int co = (kb & 1) * 32 + 4 * ch;
-    return ld4(a.w + ((ky * 4 + kx) * 32 + n) * 64 + co);  // w2t [ky][kx][ci][co]
-  }
-  static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
-    const int m = c.m0 + ml;
-    if (m >= c.M) return;
-    const int b = m / 100, j = m - b * 100, jy = j / 10, jx = j - jy * 10;
-    const int iy = 2 * jy + (c.cls >> 1), ix = 2 * jx + (c.cls & 1);
-    const size_t o = ((size_t)b * 400 + iy * 20 + ix) * 32 + n;
-    a.out[o] = a.mask[o] > 0.f ? v : 0.f;
-  }
-};
-
 // conv1 weight gradient, sample-resident: workgroup g (8 waves) holds samples 2g, 2g+1
 // (their frame planes staged in LDS once), wave w takes sample w >> 2 and input channel
 // c = w & 3, i.e. the 64 columns kk = c*64 + ky*8 + kx of dW1[32][256], as 2 (co halves) x 4
@@ -1596,100 +838,6 @@ struct Conv2Dgrad {
 constexpr int kConv1WgradS = 2;  // samples per workgroup (partials = ceil(B / 2))
 // staging dump (dwords): the 512-thread chunk loop's tail past 2 samples' 3528 chunks
 constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) / 512) * 512 - kConv1WgradS * 4 * (kPlane / 16));
-__global__ __launch_bounds__(512) void f32_conv1_wgrad_k(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + kConv1WgradDump];
-  __shared__ int64_t wplanes[kConv1WgradS * 4];  // plane byte offsets from the frames base
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int j = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
-  const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
-  {  // stage both samples' planes: 2 x 4 x 441 16-byte chunks
-    const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
-    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
-    // the 8 plane addresses once (frame_plane reads idx then ids: two dependent round trips,
-    // paid per chunk when resolved inside the loop below)
-    // (kept as offsets from the kernel-argument base: a pointer read back from LDS is a flat
-    // pointer, and flat loads may alias the LDS stores below -- each waited out before its store)
-    const uint8_t* fb = static_cast<const uint8_t*>(a.x);
-    if (t < kConv1WgradS * 4) wplanes[t] = frame_plane(f, b0 + min(t >> 2, ns - 1), t & 3, kPlane) - fb;
-    __syncthreads();
-    uint4 v[kPer];
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
-      v[i] = reinterpret_cast<const uint4*>(fb + wplanes[s2 * 4 + ch])[r - ch * 441];
-    }
-    // unconditional stores (a guarded store sank its load into the branch: one round trip per
-    // chunk); the tail chunks past both samples land in the dump past the planes (and pad)
-#pragma unroll
-    for (int i = 0; i < kPer; ++i) {
-      const int e = t + 512 * i;
-      reinterpret_cast<uint4*>(pl)[e < kConv1WgradS * kChunks ? e : e + 0] = v[i];
-    }
-  }
-  __syncthreads();
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[h][i] = zero4();
-  float bs0 = 0.f, bs1 = 0.f;  // bias partials of co = j, 16 + j (wave c == 0)
-  if (sl < ns) {
-    const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
-    const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (j >> 1) * 21 + (j & 1);
-#pragma unroll 4
-    for (int p0 = 0; p0 < 400; p0 += 4) {
-      const int pix = p0 + q, oy = pix / 20, ox = pix - oy * 20;
-      const float x0 = dy[pix * 32 + j], x1 = dy[pix * 32 + 16 + j];
-      const f32x4 xb = u8x4(pc[4 * oy * 21 + ox]);
-      bs0 += x0;
-      bs1 += x1;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[0][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x0, xb[i], acc[0][i], 0, 0, 0);
-        acc[1][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(x1, xb[i], acc[1][i], 0, 0, 0);
-      }
-    }
-  }
-  // bias: sum the 4 pixel slots (lanes j, j+16, j+32, j+48)
-  bs0 += __shfl_xor(bs0, 16, 64);
-  bs0 += __shfl_xor(bs0, 32, 64);
-  bs1 += __shfl_xor(bs1, 16, 64);
-  bs1 += __shfl_xor(bs1, 32, 64);
-  // second sample's waves hand their tiles to the first's through LDS (planes are dead)
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2][32]
-  if (sl == 1) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = acc[h][i][e];
-    if (c == 0 && q == 0) {
-      red[4 * 32 * 64 + j] = bs0;
-      red[4 * 32 * 64 + 16 + j] = bs1;
-    }
-  }
-  __syncthreads();
-  if (sl == 0) {
-    float* out = a.out + (size_t)blockIdx.x * 32 * 256;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float v = acc[h][i][e] + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
-          const int co = h * 16 + 4 * q + e, kk = c * 64 + (j >> 1) * 8 + 4 * (j & 1) + i;
-          out[co * 256 + kk] = v;
-        }
-    if (c == 0 && q == 0) {
-      a.out2[blockIdx.x * 32 + j] = bs0 + red[4 * 32 * 64 + j];
-      a.out2[blockIdx.x * 32 + 16 + j] = bs1 + red[4 * 32 * 64 + 16 + j];
-    }
-  }
-}
-
 // conv1 weight gradient at reference precision on bf16 MFMA (the exact split of the
 // forward above, applied to dy): the u8 frame operand is exact in bf16 and each dy value
 // splits exactly into hi + mid + lo bf16, so every product is exact and only the fp32
@@ -1910,7 +1058,6 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
 };
 
 using Conv3DgradP = Conv3DgradPT<128, 32, 4>;
-using Conv3DgradP64 = Conv3DgradPT<64, 64, 2>;
 
 // conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
 // output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
@@ -1969,100 +1116,36 @@ struct Conv2DgradP {
 struct SplitPlan {
   int splits, kbps;
 };
-// conv2/conv3 weight-gradient workgroups per CU (256 CUs): more splits = more waves to hide
-// latency, but more partials for grad_finalize to reduce
-int g_wgrad_occ = 1;
 
-SplitPlan plan_splits(int kbt, int ntiles, int target_blocks, int max_kbps) {
+SplitPlan plan_splits(int kbt, int ntiles, int target_blocks) {
   int s = std::max(1, target_blocks / ntiles);
-  int kbps = (kbt + s - 1) / s;
-  if (kbps > max_kbps) kbps = max_kbps;
-  if (kbps < 1) kbps = 1;
+  int kbps = std::max(1, (kbt + s - 1) / s);
   s = (kbt + kbps - 1) / kbps;
   return {s, kbps};
 }
 
-// conv2 / conv3 weight-gradient tile width (f32_set_variant(24, 0..2)): 0 = 64 (2 x 2 waves of
-// 32 x 32), 1 = conv2 128 / conv3 192, 2 = conv2 256 / conv3 192; same workgroup count (more
-// batch splits, shorter k ranges)
-int g_wgrad_wide = 0;
-static int wgrad_bn(int layer) {
-  if (!g_wgrad_wide) return 64;
-  return layer == 2 ? (g_wgrad_wide == 2 ? 256 : 128) : 192;
-}
-
+// conv2 / conv3 weight gradient: ~one workgroup per CU over (64-wide n-tiles x batch splits)
 SplitPlan wgrad_plan(int layer, int B) {
   switch (layer) {
-    case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_k workgroups
-    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / wgrad_bn(2), 256 * g_wgrad_occ, 1 << 20);
-    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / wgrad_bn(3), 252 * g_wgrad_occ, 1 << 20);
+    case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_x3_k workgroups
+    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / 64, 256);
+    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / 64, 252);
     default: throw std::invalid_argument("f32 wgrad layer");
   }
 }
 
-// GEMM-body register prefetch depth (f32_set_variant(8, 1|2)); see gemm_body
-int g_pf_depth = 1;
-
-// XCD-chunked tile order for single-GEMM launches (f32_set_variant(11, 0|1)), see xcd_chunk
-int g_xcd = 1;
-// conv2 / conv3 forward tiles with BK = 16 (f32_set_variant(12, 0|1)): 25.6 KB of LDS per
-// workgroup -> 6 per CU instead of 3, twice the barriers per FLOP
-int g_fwd_bk16 = 0;
-// FC1 forward tile (f32_set_variant(13, 0..2)): 0 = 128 x 64 (2 x 2 waves of 64 x 32),
-// 1 = 64 x 64 (2 x 2 waves of 32 x 32), 2 = 128 x 32 (4 x 1 waves of 32 x 32); 1 and 2 give
-// twice the workgroups (672 per 3 x 512 rows) at half the LDS; 3 = 64 x 64 for the learner's
-// 3-problem launch, 128 x 64 for the actor's
-int g_fc1_tile = 1;  // measured: FC1 fwd 36.9 -> 31.6 us, bench 1885 -> 1933 steps/s
-// conv2 / conv3 forward tile (f32_set_variant(14, 0..2)): 0 = 128 x 32, 1 = 64 x 64 (whole N:
-// every A row staged once, 2 x 2 waves of 32 x 32), 2 = 64 x 64 for the learner's 3-problem
-// launches only (the actor's 1-problem launch keeps 128 x 32)
-int g_conv_tile = 2;  // measured (3000 steps x2): 0: 1936 / 1934, 1: 1925 / 1933, 2: 1947 / 1947 steps/s
-// FC1 weight gradient batch slices (f32_set_variant(15, 0..4)): 0 = one pass writing the
-// reference-layout grads in place; G > 0 = G slices of natural-order partials reduced and
-// transposed by grad_finalize (4 x 49 x G workgroups instead of 4 x 49 beside the dgrad's 8 x 49).
-// Measured (bench.py, 2000 steps): 0: 1931 / 1931, 1: 1947, 2: 1929 / 1932, 4: 1892 steps/s --
-// more slices do not pay for the partial traffic; ONE slice wins by its coalesced natural-order
-// stores (the transpose moves into the finalize job that also takes the FC1 norm partials)
-int g_fc1_wg_splits = 1;
-// conv3 input-gradient tile (f32_set_variant(17, 0..1)): 0 = 128 x 32, 1 = 64 x 64
-int g_dgrad3_tile = 0;
-// conv2 / conv3 weight gradient: XCD-grouped split order (f32_set_variant(18, 0..1))
-int g_wgrad_xcd = 0;
-
-// single-GEMM launches on the exact-split bf16 body (f32_set_variant(10, 0|1))
-int g_x9 = 0;  // measured slower on MI355X (split VALU + 3 LDS planes): opt-in
-
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  if constexpr (P::A_KMAJ && P::B_KMAJ && !HasColsum<P>::value) {
-    if (g_x9) {
-      gemm_x9_k<P><<<blocks, 256, 0, s>>>(a, g_xcd);
-      LAUNCH_CHECK();
-      return;
-    }
-  }
-  if (g_pf_depth == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a, g_xcd);
-  else if (g_pf_depth == 3) gemm_k<P, 3><<<blocks, 256, 0, s>>>(a, g_xcd);
-  else gemm_k<P, 1><<<blocks, 256, 0, s>>>(a, g_xcd);
+  gemm_k<P><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  if (g_pf_depth == 2) gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else if (g_pf_depth == 3) gemm2_k<P1, P2, 3><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
-}
-
-// every problem of the launch carries input + weight planes and px is enabled
-bool px_ready(const F32Set& set) {
-  if (!px_enabled()) return false;
-  for (int i = 0; i < set.n; ++i)
-    if (!set.p[i].inx || !set.p[i].wx) return false;
-  return true;
 }
 
 void check_set(const F32Set& set) {
@@ -2070,148 +1153,34 @@ void check_set(const F32Set& set) {
   if (set.B <= 0) throw std::invalid_argument("f32: B must be positive");
 }
 
+template <class P>
+void fwd_launch(const F32Set& set, hipStream_t s) {
+  launch1<P>(set, set.n * P::tiles(set.B), s);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ host launchers
-// conv1 forward variant (benchmark knob, f32_set_variant): 0 = sample-resident kernel
-// (f32_conv1_fwd_k), 1 = generic GEMM body (128 x 32 x 16 tiles, windows gathered from global),
-// 2 = exact-split bf16 MFMA (f32_conv1_fwd_x3_k)
-int g_conv1_variant = 2;
-
-// forward GEMMs on the LDS-DMA ring body (f32_set_variant(23, S)): 0 = off (register-staged
-// gemm_k), S = 2..4 ring stages; 64 x 64 K-major tiles only (the learner's 3-problem launches)
-int g_fwd_dma = 0;
-
-// conv2 / conv3 forward on the sample-resident kernel (f32_set_variant(25, 0..2)), see
-// f32_conv_fwd_direct_k: 0 = the GEMM bodies below, 1 = one 4-wave workgroup per CU, 2 = one
-// 8-wave workgroup per CU (two waves per SIMD), 3 = conv3 at two 4-wave workgroups per CU (its
-// 3-slot ring is 63 KB)
-int g_fwd_direct = 0;
-
-static int device_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    if (cus <= 0) cus = 256;
-  }
-  return cus;
-}
-
-// one persistent workgroup per CU: the CUs are dealt to the problems evenly, each problem's
-// 16-row tiles split into equal contiguous ranges (tpw tiles per workgroup)
-static bool any_outx(const F32Set& set) {
-  for (int i = 0; i < set.n; ++i)
-    if (set.p[i].outx) return true;
-  return false;
-}
-
-template <int L>
-void direct_launch(const F32Set& set, hipStream_t s) {
-  const int M = set.B * DGeo<L>::P, Tp = (M + kDconvTile - 1) / kDconvTile;
-  const int per = std::max(1, device_cus() * (L == 3 && g_fwd_direct == 3 ? 2 : 1) / set.n);
-  const int tpw = (Tp + per - 1) / per, wgpp = (Tp + tpw - 1) / tpw;
-  if (g_fwd_direct == 4 || g_fwd_direct == 5) {  // phase-stamp diagnostics into each problem's w2
-    for (int i = 0; i < set.n; ++i)
-      if (!set.p[i].w2) throw std::invalid_argument("direct conv diagnostics: pass an int64 stamp buffer as w2");
-    if (g_fwd_direct == 5) f32_conv_fwd_direct_k<L, 2, true><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
-    else f32_conv_fwd_direct_k<L, 1, true><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
-  } else if (g_fwd_direct == 2) {
-    f32_conv_fwd_direct_k<L, 2><<<set.n * wgpp, 512, 0, s>>>(set, tpw, wgpp);
-  } else {
-    f32_conv_fwd_direct_k<L, 1><<<set.n * wgpp, 256, 0, s>>>(set, tpw, wgpp);
-  }
-  LAUNCH_CHECK();
-}
-
-template <class P>
-void fwd_launch(const F32Set& set, hipStream_t s) {
-  const int blocks = set.n * P::tiles(set.B);
-  if constexpr (P::BM == 64 && P::BN == 64 && P::BK == 32 && P::WM == 2) {
-    if (g_fwd_dma >= 2 && blocks > 0) {
-      if (g_fwd_dma == 2) gemm_g_k<P, 2><<<blocks, 256, 0, s>>>(set, g_xcd);
-      else if (g_fwd_dma == 3) gemm_g_k<P, 3><<<blocks, 256, 0, s>>>(set, g_xcd);
-      else gemm_g_k<P, 4><<<blocks, 256, 0, s>>>(set, g_xcd);
-      LAUNCH_CHECK();
-      return;
-    }
-  }
-  launch1<P>(set, blocks, s);
-}
-
-// backward benchmark knobs: g_bwd_mode (0 both GEMMs of a conv backward launch, 1 weight
-// gradient only, 2 input gradient only), g_dgrad_variant (0 position-major, 1 sample-major)
-int g_bwd_mode = 0, g_dgrad_variant = 0;
-// conv1 weight gradient (knob 9): 0 = fp32 MFMA (f32_conv1_wgrad_k), 1 = exact-split bf16 MFMA
-// (f32_conv1_wgrad_x3_k).  A variant splitting dy once per element into LDS (instead of in
-// each channel wave) measured 27.4 vs 26.0 us: the split VALU is not what bounds it.
-int g_conv1_wgrad_variant = 1;
-
-void f32_set_variant(int layer, int v) {
-  if (layer == 1 && v >= 0 && v <= 2) g_conv1_variant = v;
-  else if (layer == 5 && v >= 0 && v <= 2) g_bwd_mode = v;
-  else if (layer == 6 && v >= 0 && v <= 1) g_dgrad_variant = v;
-  else if (layer == 7 && v >= 1 && v <= 8) g_wgrad_occ = v;  // set BEFORE sizing the workspaces
-  else if (layer == 8 && v >= 1 && v <= 3) g_pf_depth = v;
-  else if (layer == 9 && v >= 0 && v <= 1) g_conv1_wgrad_variant = v;
-  else if (layer == 10 && v >= 0 && v <= 1) g_x9 = v;
-  else if (layer == 11 && v >= 0 && v <= 1) g_xcd = v;
-  else if (layer == 12 && v >= 0 && v <= 1) g_fwd_bk16 = v;
-  else if (layer == 13 && v >= 0 && v <= 3) g_fc1_tile = v;
-  else if (layer == 14 && v >= 0 && v <= 3) g_conv_tile = v;  // 3: 128 x 64 (2 x 2 waves of 64 x 32) learner tiles
-  else if (layer == 15 && v >= 0 && v <= 4) g_fc1_wg_splits = v;
-  else if (layer == 16 && (v == 4 || v == 8)) g_lh_rows = v;
-  else if (layer == 17 && v >= 0 && v <= 1) g_dgrad3_tile = v;
-  else if (layer == 18 && v >= 0 && v <= 1) g_wgrad_xcd = v;
-  else if (layer == 19 && v >= 0 && v <= 2) px_set(v);  // pre-split exact forward GEMMs (px_kernels.hip)
-  else if (layer == 20 && v >= 0 && v <= 1) pxb_set(v);  // pre-split exact backward GEMMs (pxb_kernels.hip)
-  else if (layer == 21 && v >= 0 && v <= 1) px_set_pipe(v);  // px / pxb pipeline form
-  else if (layer == 22 && (v == 32 || v == 64)) px_set_bk(v);  // px forward k-block depth
-  else if (layer == 23 && (v == 0 || (v >= 2 && v <= 4))) g_fwd_dma = v;  // LDS-DMA ring forward GEMMs
-  else if (layer == 24 && v >= 0 && v <= 2) g_wgrad_wide = v;  // conv2 / conv3 weight-gradient tile width
-  else if (layer == 25 && v >= 0 && v <= 5) g_fwd_direct = v;  // sample-resident conv2 / conv3 forward
-  else throw std::invalid_argument("f32_set_variant: (1, 0..1) conv1 | (5, 0..2) bwd mode | (6, 0..1) dgrad");
-}
-
-// Tiles (MI355X, 3 x 512-sample launches): 128 x 32 blocks, one 32x32 accumulator per wave,
-// beat 128 x 64 / 256-row blocks: 46-55 KB of LDS per workgroup gave 2-3 per CU, too few
-// waves to cover the operand-load latency.
-// the learner's launches (2-3 passes of its batch: >= 1024 rows) vs the actor's (one pass of
-// 256 envs) and the sampled-ahead target pass (one pass of 512)
+// Tiles (MI355X, measured): the learner's launches (2-3 passes of its batch: >= 1024 rows) on
+// 64 x 64 tiles (every A row staged once, 2 x 2 waves of 32 x 32: conv2 / conv3 1947 vs 1934
+// steps/s for 128 x 32), the actor's single 256-env pass on 128 x 32 (4 x 1 waves: twice the
+// workgroups); FC1 on 64 x 64 (31.6 vs 36.9 us for 128 x 64); the tuning log is
+// profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
   switch (layer) {
     case 1:
-      if (g_conv1_variant != 2)
-        for (int i = 0; i < set.n; ++i)
-          if (set.p[i].outx) throw std::invalid_argument("conv1: activation planes need the exact-split kernel (variant 2)");
-      if (g_conv1_variant == 1) {
-        fwd_launch<Conv1FwdT<128, 32, 16, 4>>(set, s);
-      } else if (g_conv1_variant == 2) {
-        f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
-        LAUNCH_CHECK();
-      } else {
-        f32_conv1_fwd_k<<<set.n * set.B, 256, 0, s>>>(set);
-        LAUNCH_CHECK();
-      }
+      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+      LAUNCH_CHECK();
       break;
     case 2:
-      if (px_ready(set)) px_conv_fwd_multi(2, set, s);
-      else if (g_fwd_direct && !any_outx(set)) direct_launch<2>(set, s);
-      else if (g_fwd_bk16) fwd_launch<Conv2FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
-      if (px_ready(set)) px_conv_fwd_multi(3, set, s);
-      else if (g_fwd_direct && !any_outx(set)) direct_launch<3>(set, s);
-      else if (g_fwd_bk16) fwd_launch<Conv3FwdT<128, 32, 16, 4>>(set, s);
-      else if (g_conv_tile == 3 && learner_sized(set)) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
-      else if (g_conv_tile == 1 || (g_conv_tile >= 2 && learner_sized(set))) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
@@ -2222,40 +1191,22 @@ int f32_fc1_splits() { return kFcSplits; }
 
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s) {
   check_set(set);
-  if (px_ready(set)) px_fc1_fwd_multi(set, s);
-  else if (g_fc1_tile == 1 || (g_fc1_tile == 3 && learner_sized(set))) fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
-  else if (g_fc1_tile == 2) fwd_launch<Fc1FwdT<128, 32, 32, 4>>(set, s);
-  else fwd_launch<Fc1FwdT<128, 64, 32, 2>>(set, s);
+  fwd_launch<Fc1FwdT<64, 64, 32, 2>>(set, s);
   return kFcSplits;
 }
 
-void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,
-                 hipStream_t s) {
-  if (B <= 0) return;
-  BwdArgs d{};
-  d.dy = dz;
-  d.w = wfc1p;
-  d.mask = a3;
-  d.out = dy3;
-  d.B = B;
-  BwdArgs w{};
-  w.x = a3;
-  w.dy = dz;
-  w.out = g_adv;
-  w.out2 = g_val;
-  w.B = B;
-  w.splits = 0;
-  launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B), d, Fc1Dgrad::tiles(B), s);
-}
+// FC1 weight gradient: ONE batch slice of natural-order partials, reduced and transposed by
+// grad_finalize (coalesced stores; more slices did not pay for their partial traffic:
+// 1947 vs 1929 / 1892 steps/s for 2 / 4)
+constexpr int kFc1WgSlices = 1;
 
-int f32_fc1_wgrad_splits() { return g_fc1_wg_splits; }
+int f32_fc1_wgrad_splits() { return kFc1WgSlices; }
 
-size_t f32_fc1_wgrad_workspace_floats() { return (size_t)std::max(1, g_fc1_wg_splits) * 256 * 3136; }
+size_t f32_fc1_wgrad_workspace_floats() { return (size_t)kFc1WgSlices * 256 * 3136; }
 
 void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
                        hipStream_t s) {
   if (B <= 0) return;
-  if (g_fc1_wg_splits < 1) throw std::invalid_argument("f32_fc1_bwd_split: FC1 wgrad slices are off (knob 15 = 0)");
   BwdArgs d{};
   d.dy = dz;
   d.w = wfc1p;
@@ -2268,7 +1219,7 @@ void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, flo
   w.out = ws;
   w.B = B;
   const int nkb = (B + Fc1Wgrad::BK - 1) / Fc1Wgrad::BK;
-  w.splits = std::min(g_fc1_wg_splits, nkb);
+  w.splits = std::min(kFc1WgSlices, nkb);
   w.kbps = (nkb + w.splits - 1) / w.splits;
   w.splits = (nkb + w.kbps - 1) / w.kbps;  // every slice non-empty
   launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B) * w.splits, d, Fc1Dgrad::tiles(B), s);
@@ -2276,7 +1227,7 @@ void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, flo
 
 int f32_fc1_wgrad_slices(int B) {
   const int nkb = (B + Fc1Wgrad::BK - 1) / Fc1Wgrad::BK;
-  const int g = std::min(std::max(1, g_fc1_wg_splits), nkb), kbps = (nkb + g - 1) / g;
+  const int g = std::min(kFc1WgSlices, nkb), kbps = (nkb + g - 1) / g;
   return (nkb + kbps - 1) / kbps;
 }
 
@@ -2307,43 +1258,21 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   g.B = B;
   g.kbps = p.kbps;
   g.splits = p.splits;
-  g.xcd_group = g_wgrad_xcd;
   BwdArgs d{};
   d.dy = dy;
   d.w = w;
   d.mask = mask;
   d.out = dx;
   d.B = B;
-  const int mode = g_bwd_mode;  // benchmark knob: 0 both, 1 weight gradient only, 2 input gradient only
-  const int nw3 = mode == 2 ? 0 : (576 / wgrad_bn(3)) * p.splits, nw2 = mode == 2 ? 0 : (512 / wgrad_bn(2)) * p.splits;
-  const int nd3 = mode == 1 ? 0 : Conv3DgradP::tiles(B), nd2 = mode == 1 ? 0 : Conv2DgradP::tiles(B);
-  if (layer == 3 && wgrad_bn(3) == 192 && !g_dgrad_variant && g_dgrad3_tile != 1) {
-    launch2<ConvWgrad<3, 192>, Conv3DgradP>(g, nw3, d, nd3, s);
-    return;
-  }
-  if (layer == 2 && wgrad_bn(2) != 64 && !g_dgrad_variant) {
-    if (wgrad_bn(2) == 256) launch2<ConvWgrad<2, 256>, Conv2DgradP>(g, nw2, d, nd2, s);
-    else launch2<ConvWgrad<2, 128>, Conv2DgradP>(g, nw2, d, nd2, s);
-    return;
-  }
   switch (layer) {
     case 3:
-      if (g_dgrad_variant)
-        launch2<ConvWgrad<3>, Conv3Dgrad>(g, nw3, d, mode == 1 ? 0 : Conv3Dgrad::tiles(B), s);
-      else if (g_dgrad3_tile == 1)
-        launch2<ConvWgrad<3>, Conv3DgradP64>(g, nw3, d, mode == 1 ? 0 : Conv3DgradP64::tiles(B), s);
-      else
-        launch2<ConvWgrad<3>, Conv3DgradP>(g, nw3, d, mode == 1 ? 0 : Conv3DgradP::tiles(B), s);
+      launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
       break;
     case 2:
-      if (g_dgrad_variant)
-        launch2<ConvWgrad<2>, Conv2Dgrad>(g, nw2, d, mode == 1 ? 0 : Conv2Dgrad::tiles(B), s);
-      else
-        launch2<ConvWgrad<2>, Conv2DgradP>(g, nw2, d, mode == 1 ? 0 : Conv2DgradP::tiles(B), s);
+      launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
       break;
     case 1:
-      if (g_conv1_wgrad_variant == 1) f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);
-      else f32_conv1_wgrad_k<<<p.splits, 512, 0, s>>>(g);
+      f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);
       LAUNCH_CHECK();
       break;
     default: throw std::invalid_argument("f32_conv_bwd: layer must be 1, 2 or 3");

@@ -241,20 +241,16 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("rmsprop_step", [](uint64_t p, uint64_t g, uint64_t sq, uint64_t gavg, int64_t n, uint64_t partials,
                            int n_partials, const RMSpropParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                            uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                           uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32,
-                           uint64_t arena_x, int64_t x_plane, uint64_t fc_wp_x, int64_t fc_wp_x_plane) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32),
-                     P<uint16_t>(arena_x), x_plane};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32),
-                    P<uint16_t>(fc_wp_x), fc_wp_x_plane};
+                           uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
     rmsprop_step(P<float>(p), P<const float>(g), P<float>(sq), P<float>(gavg), n, P<const double>(partials),
                  n_partials, hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
                  (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("sq"), py::arg("gavg"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0,
-     py::arg("arena_x") = 0, py::arg("x_plane") = 0, py::arg("fc_wp_x") = 0, py::arg("fc_wp_x_plane") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
   py::class_<AdamParams>(m, "AdamParams")
       .def(py::init([](float lr, float b1, float b2, float eps, float wd, float max_norm, float lr_gamma,
                        int lr_step_size, int lr_step_offset) {
@@ -267,20 +263,16 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("adam_step", [](uint64_t p, uint64_t g, uint64_t mm, uint64_t v, int64_t n, uint64_t partials,
                         int n_partials, const AdamParams& hp, uint64_t step, uint64_t norms, uint64_t s,
                         uint64_t dst1, uint64_t dst2, uint64_t arena, int64_t fc_off0, int64_t fc_off1,
-                        uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32,
-                           uint64_t arena_x, int64_t x_plane, uint64_t fc_wp_x, int64_t fc_wp_x_plane) {
-    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32),
-                     P<uint16_t>(arena_x), x_plane};
-    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32),
-                    P<uint16_t>(fc_wp_x), fc_wp_x_plane};
+                        uint64_t fc_wp, uint64_t fc_wt, uint64_t arena_f32, uint64_t fc_wp_f32) {
+    const PackMap pk{P<const int>(dst1), P<const int>(dst2), P<uint16_t>(arena), P<float>(arena_f32)};
+    const FcPack fc{{fc_off0, fc_off1}, P<uint16_t>(fc_wp), P<uint16_t>(fc_wt), P<float>(fc_wp_f32)};
     adam_step(P<float>(p), P<const float>(g), P<float>(mm), P<float>(v), n, P<const double>(partials), n_partials,
               hp, P<const int64_t>(step), P<float>(norms), S(s), (arena || arena_f32) ? &pk : nullptr,
               (fc_wp || fc_wp_f32) ? &fc : nullptr);
   }, py::arg("p"), py::arg("g"), py::arg("mm"), py::arg("v"), py::arg("n"), py::arg("partials"),
      py::arg("n_partials"), py::arg("hp"), py::arg("step"), py::arg("norms"), py::arg("s"), py::arg("dst1") = 0,
      py::arg("dst2") = 0, py::arg("arena") = 0, py::arg("fc_off0") = -1, py::arg("fc_off1") = -1,
-     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0,
-     py::arg("arena_x") = 0, py::arg("x_plane") = 0, py::arg("fc_wp_x") = 0, py::arg("fc_wp_x_plane") = 0);
+     py::arg("fc_wp") = 0, py::arg("fc_wt") = 0, py::arg("arena_f32") = 0, py::arg("fc_wp_f32") = 0);
   m.def("adam_step2", [](std::array<uint64_t, 8> a, std::array<uint64_t, 8> b, const AdamParams& hp, uint64_t step,
                          uint64_t s) {
     // (p, g, m, v, n, partials, n_partials, norms) per set
@@ -429,9 +421,6 @@ PYBIND11_MODULE(_apex_hip, m) {
     a.lw = P<float>(g("lw"));
     a.dz_bf = P<uint16_t>(g("dz_bf"));
     a.dz = P<float>(g("dz"));
-    a.dzx = P<uint16_t>(g("dzx"));
-    a.dzx_ps = d.contains("dzx_ps") ? d["dzx_ps"].cast<int64_t>() : 0;
-    if (a.dzx && (!a.dz || a.dzx_ps < (int64_t)B * 256)) throw std::invalid_argument("dqn_heads_bwd: dz planes need dz and dzx_ps >= B*256");
     a.part = P<float>(g("part"));
     a.step = P<const int64_t>(g("step"));
     a.step_snap = P<int64_t>(g("step_snap"));
@@ -449,23 +438,15 @@ PYBIND11_MODULE(_apex_hip, m) {
     pack_conv_wt(P<const float>(src), P<uint16_t>(dst), N, C, KH, KW, S(s));
   });
   // ---- fp32 (reference-precision) network kernels (f32_kernels.hip)
-  // a problem: (in, ids, idx, w, w2, bias, out) [+ (inx, wx, outx, inx_ps, wx_ps, outx_ps): pre-split planes]
+  // a problem: (in, ids, idx, w, w2, bias, out)
   auto f32set = [](const std::vector<std::vector<uint64_t>>& probs, int B) {
     if (probs.empty() || probs.size() > (size_t)kMaxProbs) throw std::invalid_argument("1..3 problems");
     F32Set set{};
     for (size_t i = 0; i < probs.size(); ++i) {
       const auto& t = probs[i];
-      if (t.size() != 7 && t.size() != 13) throw std::invalid_argument("f32 problem: 7 or 13 fields");
+      if (t.size() != 7) throw std::invalid_argument("f32 problem: 7 fields");
       set.p[i] = F32Prob{P<const void>(t[0]), P<const int>(t[1]), P<const int>(t[2]), P<const float>(t[3]),
                          P<const float>(t[4]), P<const float>(t[5]), P<float>(t[6])};
-      if (t.size() == 13) {
-        set.p[i].inx = P<const uint16_t>(t[7]);
-        set.p[i].wx = P<const uint16_t>(t[8]);
-        set.p[i].outx = P<uint16_t>(t[9]);
-        set.p[i].inx_ps = (int64_t)t[10];
-        set.p[i].wx_ps = (int64_t)t[11];
-        set.p[i].outx_ps = (int64_t)t[12];
-      }
     }
     set.n = (int)probs.size();
     set.B = B;
@@ -478,60 +459,6 @@ PYBIND11_MODULE(_apex_hip, m) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
   m.def("f32_fc1_splits", &f32_fc1_splits);
-  m.def("px_enabled", &px_enabled);
-  m.def("pxb_enabled", &pxb_enabled);
-  m.def("px_terms", &px_terms);
-  // pre-split backward: FC1 (dz planes, a3 planes, wfc1p planes) and conv3 / conv2 launches
-  m.def("pxb_fc1_bwd", [](py::dict d, int B, uint64_t s) {
-    auto g = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
-    auto i = [&](const char* k) -> int64_t { return d.contains(k) ? d[k].cast<int64_t>() : 0; };
-    PxbFc1 f{};
-    f.dzx = P<const uint16_t>(g("dzx"));
-    f.dz_ps = i("dz_ps");
-    f.a3x = P<const uint16_t>(g("a3x"));
-    f.a3_ps = i("a3_ps");
-    f.wx = P<const uint16_t>(g("wx"));
-    f.w_ps = i("w_ps");
-    f.a3 = P<const float>(g("a3"));
-    f.dy3 = P<float>(g("dy3"));
-    f.dy3x = P<uint16_t>(g("dy3x"));
-    f.dy3_ps = i("dy3_ps");
-    f.gw = P<float>(g("gw"));
-    f.gw2 = P<float>(g("gw2"));
-    f.slices = (int)i("slices");
-    if (!f.a3 || !f.dy3 || !f.gw || (f.slices == 0 && !f.gw2)) throw std::invalid_argument("pxb_fc1_bwd: missing pointer");
-    pxb_fc1_bwd(f, B, S(s));
-  });
-  m.def("pxb_conv_bwd", [](int layer, py::dict d, int B, uint64_t s) {
-    auto g = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
-    auto i = [&](const char* k) -> int64_t { return d.contains(k) ? d[k].cast<int64_t>() : 0; };
-    PxbConv c{};
-    c.dyx = P<const uint16_t>(g("dyx"));
-    c.dy_ps = i("dy_ps");
-    c.xx = P<const uint16_t>(g("xx"));
-    c.x_ps = i("x_ps");
-    c.wtx = P<const uint16_t>(g("wtx"));
-    c.wt_ps = i("wt_ps");
-    c.mask = P<const float>(g("mask"));
-    c.dx = P<float>(g("dx"));
-    c.dxx = P<uint16_t>(g("dxx"));
-    c.dx_ps = i("dx_ps");
-    c.ws = P<float>(g("ws"));
-    if (layer != 2 && layer != 3) throw std::invalid_argument("pxb_conv_bwd: layer 2 or 3");
-    if (!c.mask || !c.dx || !c.ws) throw std::invalid_argument("pxb_conv_bwd: missing pointer");
-    const int splits = f32_wgrad_splits(layer, B);
-    c.ws_bias = c.ws + (size_t)splits * 64 * (layer == 2 ? 512 : 576);
-    pxb_conv_bwd(layer, c, B, splits, f32_wgrad_kbps(layer, B), S(s));
-  });
-  m.def("f32_split_planes", [](uint64_t src, uint64_t dst, int64_t n, int64_t plane, uint64_t s) {
-    f32_split_planes(P<const float>(src), P<uint16_t>(dst), n, plane, S(s));
-  });
-  m.def("f32_set_variant", &f32_set_variant);
-  m.def("f32_fc1_bwd", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ga, uint64_t gv, int B,
-                          uint64_t s) {
-    f32_fc1_bwd(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ga),
-                P<float>(gv), B, S(s));
-  });
   m.def("f32_fc1_bwd_split", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ws, int B,
                                 uint64_t s) {
     f32_fc1_bwd_split(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ws), B,

@@ -196,13 +196,10 @@ struct LossHeadsArgs {
   uint16_t* dz_bf;                 // [B][256] out: dL/dz (FC1 pre-activation), bf16
   float* part;                     // [blocks][(A+1)*128 + (A+1) + 256] out: gradient partials
   float* dz;                       // [B][256] out (optional, replaces dz_bf): dL/dz in fp32
-  uint16_t* dzx;                   // with dz: its three bf16 planes (pre-split backward), or null
-  int64_t dzx_ps;
   const int64_t* step;             // learner step counter (read)
   int64_t* step_snap;              // out: its value for this step's optimizer (may be null)
 };
 int dqn_heads_bwd_blocks(int B);
-extern int g_lh_rows;  // dqn_heads_bwd rows per workgroup (4 or 8; f32_set_variant(16, ...))
 void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s);
 
 // ---- learner_kernels.hip
@@ -228,8 +225,6 @@ struct PackMap {
   const int* dst2;
   uint16_t* arena;      // bf16 packed copies (bf16 network) ...
   float* arena_f32;     // ... or fp32 packed copies (reference-precision network)
-  uint16_t* arena_x;    // fp32 network: split planes of every packed layout (plane stride x_plane), or null
-  int64_t x_plane;
 };
 // FC1 weights (Nature-CNN dueling net): flat offsets of advantage.0.weight and
 // value.0.weight ([128][64*49] each) and the two packed bf16 layouts they refresh,
@@ -242,8 +237,6 @@ struct FcPack {
   uint16_t* wp;
   uint16_t* wt;
   float* wp_f32;
-  uint16_t* wp_x;       // fp32 network: split planes of wfc1p (plane stride wp_x_plane), or null
-  int64_t wp_x_plane;
 };
 void rmsprop_step(float* p, const float* g, float* sq, float* gavg, int64_t n, const double* partials,
                   int n_partials, const RMSpropParams& hp, const int64_t* step, float* norms_out, hipStream_t s,
@@ -379,67 +372,14 @@ struct F32Prob {
   const float* w2;    // unused
   const float* bias;
   float* out;         // activations (conv) | split-K partials [7][B][256] (FC1)
-  // pre-split exact operands (px_kernels.hip): three bf16 planes hi | mid | lo of the same
-  // tensor, ``*_ps`` elements apart, hi + mid + lo = the fp32 value (RNE split)
-  const uint16_t* inx;  // input activation planes (conv2 / conv3 / FC1); null: fp32 path
-  const uint16_t* wx;   // packed weight planes (w2p / w3p / wfc1p layouts)
-  uint16_t* outx;       // output activation planes written beside ``out`` (null: none)
-  int64_t inx_ps, wx_ps, outx_ps;
 };
 struct F32Set {
   F32Prob p[kMaxProbs];
   int n, B;
 };
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
-void f32_set_variant(int layer, int v);  // conv1 forward tile variant (benchmarks), 0 = default
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
-// pre-split exact forward GEMMs on bf16 MFMA (px_kernels.hip): every operand arrives as three
-// bf16 planes (written by the producer's epilogue / the optimizer), 6 term products per
-// element pair accumulated in fp32 (f32_set_variant(19, 1) enables them for conv2 / conv3 / FC1
-// whenever every problem of the launch carries planes)
-bool px_enabled();
-void px_set(int v);
-int px_terms();  // 6 or 8 term products (knob 19 = 1 | 2)
-int px_pipe();   // knob 21: 0 = two LDS stages + 1 register prefetch, 1 = one LDS stage + 2-deep register ring
-void px_set_pipe(int v);
-void px_set_bk(int v);   // knob 22: px forward k-block depth 32 | 64
-void px_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
-void px_fc1_fwd_multi(const F32Set& set, hipStream_t s);
-// pre-split exact BACKWARD GEMMs (pxb_kernels.hip, f32_set_variant(20, 1) with knob 19 on):
-// FC1 input gradient + weight gradient in one launch, conv3 / conv2 weight gradient + input
-// gradient in one launch each, every operand as three bf16 planes
-bool pxb_enabled();
-void pxb_set(int v);
-struct PxbFc1 {
-  const uint16_t* dzx;  int64_t dz_ps;   // dL/dz planes [B][256] (dqn_heads_bwd)
-  const uint16_t* a3x;  int64_t a3_ps;   // a3 planes [B][3136] (conv3 forward epilogue)
-  const uint16_t* wx;   int64_t w_ps;    // wfc1p planes [256][3136] (optimizer)
-  const float* a3;                       // ReLU mask of dy3
-  float* dy3;                            // [B][3136] out
-  uint16_t* dy3x;       int64_t dy3_ps;  // dy3 planes out (null: none)
-  float* gw;            // slices > 0: natural-order partials [slices][256][3136]; 0: advantage rows in place
-  float* gw2;           // slices == 0: value rows in place
-  int slices;
-};
-void pxb_fc1_bwd(const PxbFc1& f, int B, hipStream_t s);
-struct PxbConv {
-  const uint16_t* dyx;  int64_t dy_ps;   // output-gradient planes [B][P][64]
-  const uint16_t* xx;   int64_t x_ps;    // layer-input planes (a2 for conv3, a1 for conv2)
-  const uint16_t* wtx;  int64_t wt_ps;   // transposed weight planes (w3t / w2t)
-  const float* mask;                     // ReLU mask of dx (the layer input)
-  float* dx;                             // input gradient out
-  uint16_t* dxx;        int64_t dx_ps;   // its planes (null: none)
-  float* ws;            // weight-gradient partials [splits][64][N]
-  float* ws_bias;       // bias partials [splits][64]
-};
-void pxb_conv_bwd(int layer, const PxbConv& c, int B, int splits, int kbps, hipStream_t s);
-// dst[u * plane + i] = term u of src[i] (u = 0 hi, 1 mid, 2 lo), i < n
-void f32_split_planes(const float* src, uint16_t* dst, int64_t n, int64_t plane, hipStream_t s);
-// FC1 backward in one launch: dy3 = (a3 > 0) * dz . wfc1p (channels-last order) and the
-// reference-layout weight gradients written straight into g_adv / g_val
-void f32_fc1_bwd(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* g_adv, float* g_val, int B,
-                 hipStream_t s);
 int f32_wgrad_splits(int layer, int B);
 int f32_wgrad_kbps(int layer, int B);  // k-blocks (32 rows) per split
 size_t f32_wgrad_workspace_floats(int layer, int B);

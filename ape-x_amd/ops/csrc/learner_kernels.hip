@@ -153,20 +153,6 @@ __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v
     const int d1 = pk.dst1[i], d2 = pk.dst2[i];
     if (d1 >= 0) pk.arena_f32[d1] = v;
     if (d2 >= 0) pk.arena_f32[d2] = v;
-    if (pk.arena_x) {  // pre-split planes of every packed layout (plane stride = the arena size)
-      uint16_t h, m, l;
-      split3_rne(v, h, m, l);
-      if (d1 >= 0) {
-        pk.arena_x[d1] = h;
-        pk.arena_x[pk.x_plane + d1] = m;
-        pk.arena_x[2 * pk.x_plane + d1] = l;
-      }
-      if (d2 >= 0) {
-        pk.arena_x[d2] = h;
-        pk.arena_x[pk.x_plane + d2] = m;
-        pk.arena_x[2 * pk.x_plane + d2] = l;
-      }
-    }
     return;
   }
   if (!pk.arena) return;
@@ -316,15 +302,6 @@ __device__ __forceinline__ void opt_body(float* __restrict__ p, const float* __r
         v.w = tile_f[r][(4 * half + 3) * kFcP + pp];
         const size_t o = (size_t)(nrow + r) * (kFcC * kFcP) + pp * kFcC + c0 + 4 * half;
         *reinterpret_cast<float4*>(fc.wp_f32 + o) = v;
-        if (fc.wp_x) {  // pre-split planes of wfc1p: 4 values -> one 8-byte run per plane
-          union { uint16_t h[4]; uint2 u; } ph, pm, pl;
-          const float x4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int k = 0; k < 4; ++k) split3_rne(x4[k], ph.h[k], pm.h[k], pl.h[k]);
-          *reinterpret_cast<uint2*>(fc.wp_x + o) = ph.u;
-          *reinterpret_cast<uint2*>(fc.wp_x + fc.wp_x_plane + o) = pm.u;
-          *reinterpret_cast<uint2*>(fc.wp_x + 2 * fc.wp_x_plane + o) = pl.u;
-        }
       }
       return;
     }

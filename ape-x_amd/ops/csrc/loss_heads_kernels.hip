@@ -23,11 +23,10 @@ namespace apex {
 namespace {
 // rows per workgroup = waves per workgroup (one row per wave: each row is a chain of
 // dependent loads (idx -> a, r, d; q rows), two rows per wave serialised them).  8 rows:
-// B = 512 -> 64 workgroups; 4 rows (g_lh_rows = 4): 128 workgroups, twice the partials.
+// B = 512 -> 64 workgroups (4 rows: 128 workgroups and twice the partials, measured slower).
 constexpr int LH_MAXA = 63;
+constexpr int kLhRows = 8;
 }  // namespace
-
-int g_lh_rows = 8;
 
 template <int LH_ROWS>
 __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p) {
@@ -110,7 +109,6 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
       dzs[rr][j] = d;
       if (p.dz) {
         p.dz[(size_t)b * 256 + j] = d;
-        if (p.dzx) store_planes(p.dzx, p.dzx_ps, (size_t)b * 256 + j, d);  // pxb_kernels.hip operand
       } else {
         p.dz_bf[(size_t)b * 256 + j] = f2bf(d);
       }
@@ -150,13 +148,12 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
   part[(A + 1) * 129 + t] = dsum;
 }
 
-int dqn_heads_bwd_blocks(int B) { return (B + g_lh_rows - 1) / g_lh_rows; }
+int dqn_heads_bwd_blocks(int B) { return (B + kLhRows - 1) / kLhRows; }
 
 void dqn_heads_bwd(const LossHeadsArgs& args, hipStream_t s) {
   if (args.A < 1 || args.A > LH_MAXA) throw std::invalid_argument("dqn_heads_bwd: 1 <= A <= 63");
   if (args.B <= 0) return;
-  if (g_lh_rows == 4) dqn_heads_bwd_k<4><<<dqn_heads_bwd_blocks(args.B), 64 * 4, 0, s>>>(args);
-  else dqn_heads_bwd_k<8><<<dqn_heads_bwd_blocks(args.B), 64 * 8, 0, s>>>(args);
+  dqn_heads_bwd_k<kLhRows><<<dqn_heads_bwd_blocks(args.B), 64 * kLhRows, 0, s>>>(args);
   LAUNCH_CHECK();
 }
 

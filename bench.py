@@ -67,23 +67,9 @@ def parse():
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
     ap.add_argument("--seed", type=int, default=1122)
-    ap.add_argument("--bwd-fork", action="store_true",
-                    help="wgrad3/wgrad2 on a forked stream beside the dgrad chain (measured slower)")
-    ap.add_argument("--late-join", action="store_true",
-                    help="join the priority-tree branch after the optimizer instead of before it (measured slower)")
-    ap.add_argument("--no-fork-late", dest="fork_late", action="store_false",
-                    help="capture the priority-tree branch at its fork point, before the backward chain "
-                         "(default: after the backward's first launch, so the chain keeps the graph's queue)")
-    ap.add_argument("--no-tree-fork", dest="tree_fork", action="store_false",
-                    help="priority-tree writes on the learner stream instead of a forked stream")
-    ap.add_argument("--tree-write", default="legacy", choices=["batch", "legacy"],
-                    help="learner priority-tree update: batched wide kernels or the single-workgroup walks")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--no-reserve", dest="reserve", action="store_false",
                     help="do not take the actor stream from the pool before the process group")
-    ap.add_argument("--streams", default="none",
-                    choices=["none", "pool", "probe", "dedicated", "priority-actor", "priority-learner"],
-                    help="overlap mode: how the actor and learner streams get separate HW queues")
     ap.add_argument("--roctx", action="store_true", help="roctx ranges around engine phases (rocprofv3 --marker-trace)")
     ap.add_argument("--topology", default="auto", choices=["auto", "central", "sharded"],
                     help="auto (default): one GPU = the single-GPU engine, N>1 = central (BASELINE config 3, the "
@@ -98,13 +84,6 @@ def parse():
                     help="data-parallel: three phase graphs with eager RCCL all-reduces in between (default: the "
                          "all-reduces are captured inside ONE learner hipGraph per step; forced-DP 1-rank A/B 2615 -> "
                          "3050 steps/s)")
-    ap.add_argument("--light-events", action="store_true",
-                    help="overlap: actor/learner hand-off events created with hipEventDisableSystemFence")
-    ap.add_argument("--step-graph", action="store_true",
-                    help="single process, overlap: actor half + learner step as one hipGraph per step")
-    ap.add_argument("--dp-comm-early", dest="dp_comm_late", action="store_false",
-                    help="one-graph DP: capture the FC1 all-reduce at its fork point (default: after the conv "
-                         "backward's first launch)")
     ap.add_argument("--force-dp", action="store_true",
                     help="run the data-parallel step (RCCL collectives, sharded sampling) even with 1 rank "
                          "(under torch.distributed.run --nproc-per-node 1): measures its single-GPU overhead")
@@ -125,14 +104,6 @@ def parse():
                          "or peer copy) dumps every thread's stack and exits 1, inside the driver's 600 s")
     ap.add_argument("--no-preflight", dest="preflight", action="store_false",
                     help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
-    ap.add_argument("--target-ahead", type=int, default=0, choices=[0, 1],
-                    help="1: sample batch t+1 at the start of step t and run its target pass beside step t")
-    ap.add_argument("--target-pass", default="actor", choices=["actor", "fork", "inline"],
-                    help="--target-ahead 1: where the next batch's target pass runs")
-    ap.add_argument("--px", type=int, default=0, choices=[0, 1, 2],
-                    help="fp32 forward GEMMs (conv2/conv3/FC1) on the pre-split exact bf16 kernels "
-                         "(px_kernels.hip: every operand as 3 exact bf16 terms; 1 = 6 term products, "
-                         "2 = 8 term products)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
     ap.add_argument("--unpaced", action="store_true",
@@ -226,10 +197,6 @@ def main():
 
         trace.enable(True)
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.px:
-        from apex_amd import ops
-
-        ops.hip().f32_set_variant(19, args.px)  # before any network / workspace is built
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     if args.same_device:
@@ -263,16 +230,12 @@ def main():
     if args.scaling == "strong" and args.batch % world:
         raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
     rank_batch = args.batch // world if args.scaling == "strong" else args.batch
-    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
-                       tree_fork=args.tree_fork,
-                       fork_late=args.fork_late, late_join=args.late_join,
-                       bwd_fork=args.bwd_fork, tree_write=args.tree_write, target_ahead=bool(args.target_ahead),
-                       target_pass=args.target_pass)
+    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
                        use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
-                       streams=args.streams, learner=lc)
+                       learner=lc)
     dp = world > 1 or args.force_dp
     allreduce = None
     if dp and args.comm == "rccl" and args.backend == "nccl":
@@ -287,9 +250,6 @@ def main():
     sharded = dp and not args.local_sampling
     from apex_amd.parallel.rccl import RcclGradAllReduce as _Rccl
 
-    cfg.dp_comm_late = args.dp_comm_late
-    cfg.step_graph = args.step_graph
-    cfg.light_events = args.light_events
     cfg.dp_graph = bool(args.dp_graph and isinstance(allreduce, _Rccl))  # capture needs the direct communicator
     eng = ApexEngine(cfg, device, allreduce=allreduce, sharded=sharded, force_collectives=args.force_dp)
     if world > 1:  # identical initial weights on every replica (RCCL broadcast from rank 0)
@@ -374,14 +334,11 @@ def main():
                 "actor_steps_per_learner_step": args.actor_steps,
                 "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
-                "batch_pipeline": (f"sampled two steps ahead, target pass beside the previous step ({args.target_pass})"
-                                   if args.target_ahead else "sampled at the step start, 3-pass forward"),
+                "batch_pipeline": "sampled at the step start, 3-pass forward",
                 "forward": args.forward,
-                "fp32_forward_gemms": (f"pre-split exact bf16x{4 + 2 * args.px} (3-term operands, fp32-class)" if args.px
-                                       else "fp32 MFMA") if args.dtype == "fp32" else None,
+                "fp32_forward_gemms": "fp32 MFMA" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
                 "actor_learner_overlap": args.overlap,
-                "actor_stream": args.streams,
                 "dp_graph": eng._g_dp is not None,
                 # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
                 # gradient communicator, else the torch.distributed group size
@@ -401,7 +358,6 @@ def main():
             "host_enqueue_ms_per_step": round(1000.0 * t_host / args.steps, 4),
             # one train_step's host cost with the GPU idle (no back-pressure), median of 20
             "host_launch_ms_per_step": round(1000.0 * host_launch, 4),
-            "stream_probe": eng.stream_probe,
             "last_loss": round(stats["loss"], 6),
             "last_grad_norm_l2": round(stats["grad_norm_l2"], 6),
         }

@@ -23,10 +23,6 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
-ap.add_argument("--wgrad-occ", type=int, default=0, help="conv2/3 wgrad workgroups per CU (knob 7; 0 = default)")
-ap.add_argument("--bwd-sweep", action="store_true", help="conv backward: wgrad / dgrad split and dgrad variants")
-ap.add_argument("--variants", default=None, help="forward tile variants to sweep, e.g. 0,1,2,3 (f32_set_variant)")
-ap.add_argument("--knobs", default="", help="f32_set_variant settings for the whole run, e.g. 25=1,14=2")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -35,10 +31,6 @@ m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
 m.flatten_parameters()
 for p in m.parameters():
     p.grad = torch.zeros_like(p)
-if a.wgrad_occ:
-    hip.f32_set_variant(7, a.wgrad_occ)
-for kv in filter(None, a.knobs.split(",")):
-    hip.f32_set_variant(*map(int, kv.split("=")))
 net = F32DuelingNet(m)
 net.enable_backward(B)
 F = 4 * B
@@ -81,8 +73,8 @@ cases = {
     "conv2_fwd": (lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S()), 2 * P * 81 * 64 * 512),
     "conv3_fwd": (lambda: hip.f32_conv_fwd_multi(3, set3(3), B, S()), 2 * P * 49 * 64 * 576),
     "fc1_fwd": (lambda: hip.f32_fc1_fwd_multi(set3(4), B, S()), 2 * P * 256 * 3136),
-    "fc1_bwd": (lambda: hip.f32_fc1_bwd(ws.dz.data_ptr(), ws.a3.data_ptr(), net.wfc1p.data_ptr(), ws.dy3.data_ptr(),
-                                        m.advantage[0].weight.grad.data_ptr(), m.value[0].weight.grad.data_ptr(), B, S()),
+    "fc1_bwd": (lambda: hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), net.wfc1p.data_ptr(),
+                                              ws.dy3.data_ptr(), net._fc1_ws.data_ptr(), B, S()),
                 2 * 2 * B * 256 * 3136),
     "conv3_bwd": (lambda: hip.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), net.w3t.data_ptr(),
                                            ws.a2.data_ptr(), ws.dy2.data_ptr(), w3.data_ptr(), B, S()),
@@ -98,29 +90,8 @@ cases = {
                                              0, 0, 0, w1.data_ptr(), B, S()), 2 * B * 400 * 32 * 256),
 }
 res = {}
-FWD_LAYER = {"conv1_fwd": 1}
-runs, refs = [], {}
-for name, (fn, flop) in cases.items():
-    if a.only and a.only not in name:
-        continue
-    if a.variants and name in FWD_LAYER:
-        for v in map(int, a.variants.split(",")):
-            runs.append((f"{name}@v{v}", fn, flop, (FWD_LAYER[name], v)))
-    else:
-        runs.append((name, fn, flop, None))
-if a.bwd_sweep:  # (label, knob settings, flop scale); dgrad outputs checked against the sample-major form
-    for nm in ("conv3_bwd", "conv2_bwd"):
-        fn, flop = cases[nm]
-        for lab, knobs, fr in (("wgrad", ((5, 1),), 0.5), ("dgrad_pos", ((5, 2), (6, 0)), 0.5),
-                               ("both_pos", ((5, 0), (6, 0)), 1.0)):
-            runs.append((f"{nm}:{lab}", fn, flop * fr, knobs))
-for name, fn, flop, var in runs:
-    if var is not None and isinstance(var[0], tuple):
-        for k in var:
-            hip.f32_set_variant(*k)
-        var = ("knobs", var)
-    elif var is not None:
-        hip.f32_set_variant(*var)
+runs = [(name, fn, flop) for name, (fn, flop) in cases.items() if not a.only or a.only in name]
+for name, fn, flop in runs:
     fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -142,20 +113,6 @@ for name, fn, flop, var in runs:
     torch.cuda.synchronize()
     us = 1000.0 * e0.elapsed_time(e1) / a.iters
     res[name] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1), "pct_peak": round(flop / us / 1e6 / 1.573, 1)}
-    if var is not None and var[0] == "knobs":
-        if "dgrad" in name or "both" in name:
-            dx = (ws.dy2 if name.startswith("conv3") else ws.dy1).clone()
-            key = name.split(":")[0]
-            ref0 = refs.setdefault(key, dx)
-            name += "" if torch.equal(dx, ref0) else " MISMATCH"
-        hip.f32_set_variant(5, 0)
-        hip.f32_set_variant(6, 0)
-    elif var is not None:
-        out = [getattr(w, ("a1", "a2", "a3", "z")[var[0] - 1]).clone() for w in wss]
-        ref0 = refs.setdefault(var[0], out)
-        same = all(torch.equal(x, y) for x, y in zip(out, ref0))
-        name += "" if same else " MISMATCH"
-        hip.f32_set_variant(var[0], 0)
     if not a.json:
         print(f"{name:12s} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)")
 if a.json:

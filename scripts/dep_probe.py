@@ -26,7 +26,7 @@ class NoWait:
 
 def run(nowait: bool, steps: int = 2000) -> float:
     dev = torch.device("cuda", 0)
-    cfg = EngineConfig(n_envs=256, replay_capacity=2_000_000, threshold_size=50_000, overlap=True, streams="none",
+    cfg = EngineConfig(n_envs=256, replay_capacity=2_000_000, threshold_size=50_000, overlap=True,
                        learner=LearnerConfig(batch_size=512, forward="hip", dtype="fp32"))
     eng = ApexEngine(cfg, dev)
     eng.fill()

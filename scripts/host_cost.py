@@ -16,7 +16,7 @@ from apex_amd.engine.learner import LearnerConfig  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
 dev = torch.device("cuda", 0)
 reserve_actor_stream(dev)
-cfg = EngineConfig(n_envs=256, replay_capacity=2_000_000, threshold_size=50_000, overlap=True, streams="none",
+cfg = EngineConfig(n_envs=256, replay_capacity=2_000_000, threshold_size=50_000, overlap=True,
                    learner=LearnerConfig(batch_size=512, forward="hip", dtype="fp32"))
 eng = ApexEngine(cfg, dev)
 eng.fill()

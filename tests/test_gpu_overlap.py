@@ -38,26 +38,26 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False, light_events=False, **lkw):
+def _engine(dev, overlap, graphs, dp=False, sharded=False):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=4096, threshold_size=2048, overlap=overlap, use_graphs=graphs,
-                       publish_param_interval=4, target_update_interval=6, light_events=light_events,
-                       learner=LearnerConfig(batch_size=256, forward="hip", **lkw))
+                       publish_param_interval=4, target_update_interval=6,
+                       learner=LearnerConfig(batch_size=256, forward="hip"))
     torch.manual_seed(0)
     # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
     # pipelined shard-mass exchange) with a world-1 all-reduce -- same code path, 1 GPU
     return ApexEngine(cfg, dev, allreduce=FlatGradAllReduce(1) if dp else None, sharded=sharded)
 
 
-@pytest.mark.parametrize("step_graph,light,ahead", [(False, False, False), (True, False, False), (False, True, False),
-                                                    (False, False, True), (True, False, True)])
-def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph, light, ahead):
-    eng_g = _engine(cuda, True, True, light_events=light, target_ahead=ahead)
-    eng_g.cfg.step_graph = step_graph
-    eng_e = _engine(cuda, True, False, target_ahead=ahead)
+@pytest.mark.parametrize("overlap", [True, False])
+def test_graphs_equal_sequential_schedule(cuda, overlap):
+    """The captured engine (overlap: actor graph on its own stream beside the learner graph)
+    replays exactly like the same schedule run eagerly on one stream."""
+    eng_g = _engine(cuda, overlap, True)
+    eng_e = _engine(cuda, overlap, False)
     for eng in (eng_g, eng_e):
         eng.fill()
     eng_g.capture()                  # 3 counted warm-up steps, run sequentially
@@ -76,35 +76,14 @@ def test_overlapped_graphs_equal_sequential_schedule(cuda, step_graph, light, ah
     assert torch.isfinite(eng_g.learner.flat).all()
 
 
-@pytest.mark.parametrize("lkw", [dict(bwd_fork=True), dict(fork_late=False), dict(tree_fork=False),
-                                 dict(late_join=True)])
-def test_graph_fork_layouts_equal_default(cuda, lkw):
-    """Where the captured graph forks (wgrad side stream, tree branch order, no tree
-    fork) changes the schedule only: the replayed steps are bit-identical to the default."""
-    eng_a = _engine(cuda, True, True)
-    eng_b = _engine(cuda, True, True, **lkw)
-    for eng in (eng_a, eng_b):
-        eng.fill()
-        eng.capture()
-    for _ in range(12):
-        eng_a.train_step()
-        eng_b.train_step()
-    torch.cuda.synchronize()
-    assert torch.equal(eng_a.learner.flat, eng_b.learner.flat)
-    assert torch.equal(eng_a.replay.leaf_sum, eng_b.replay.leaf_sum)
-    assert torch.isfinite(eng_a.learner.flat).all()
-
-
-@pytest.mark.parametrize("overlap,sharded,ahead", [(True, False, False), (False, False, False), (True, True, False),
-                                                   (False, True, False), (True, True, True), (False, False, True)])
-def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded, ahead):
+@pytest.mark.parametrize("overlap,sharded", [(True, False), (False, False), (True, True), (False, True)])
+def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded):
     """The data-parallel step (three phase graphs, async all-reduce slices, pipelined
     shard-mass exchange) replays exactly like its eager schedule, and its first step
-    matches the single-process fused step (different grad-norm summation order only);
-    ``ahead``: with sampled-ahead batches (one graph per batch buffer)."""
-    eng_g = _engine(cuda, overlap, True, dp=True, sharded=sharded, target_ahead=ahead)
-    eng_e = _engine(cuda, overlap, False, dp=True, sharded=sharded, target_ahead=ahead)
-    eng_1 = _engine(cuda, overlap, False, target_ahead=ahead)
+    matches the single-process fused step (different grad-norm summation order only)."""
+    eng_g = _engine(cuda, overlap, True, dp=True, sharded=sharded)
+    eng_e = _engine(cuda, overlap, False, dp=True, sharded=sharded)
+    eng_1 = _engine(cuda, overlap, False)
     assert eng_g.learner.dp_split and eng_g._dp and not eng_1._dp
     for eng in (eng_g, eng_e, eng_1):
         eng.fill()
@@ -125,25 +104,4 @@ def test_dp_phase_graphs_equal_eager_and_single_process(cuda, overlap, sharded, 
     assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
     assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
-    assert torch.isfinite(eng_g.learner.flat).all()
-
-
-def test_target_ahead_single_graph_mode_equals_eager(cuda):
-    """No overlap: the learner step is captured once per sampled-ahead buffer and the
-    replays (picked by learner.cur) match the eager engine bit for bit, target syncs included."""
-    eng_g = _engine(cuda, False, True, target_ahead=True)
-    eng_e = _engine(cuda, False, False, target_ahead=True)
-    for eng in (eng_g, eng_e):
-        eng.fill()
-    eng_g.capture()
-    for _ in range(3):
-        eng_e.train_step()
-    for _ in range(20):
-        eng_g.train_step()
-        eng_e.train_step()
-    torch.cuda.synchronize()
-    assert isinstance(eng_g._g_learn_a, list) and len(eng_g._g_learn_a) == 2
-    assert eng_g.learner.cur == eng_e.learner.cur
-    assert torch.equal(eng_g.replay.leaf_sum, eng_e.replay.leaf_sum)
-    assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.isfinite(eng_g.learner.flat).all()
