@@ -23,7 +23,6 @@ phase graphs so the FC1/head gradient all-reduce overlaps the conv backward
 from __future__ import annotations
 
 import copy
-import os
 import time
 from dataclasses import dataclass, field
 
@@ -37,9 +36,6 @@ from .actor_shard import ActorShard
 from .hbm_replay import HBMReplay
 from .learner import DQNLearner, LearnerConfig, forward_q
 
-# diagnostic only (scripts/ab/actor_share.sh): capture the step without the actor's kernels, to
-# price how much the concurrent actor slows the learner chain; never a valid bench config
-_DIAG_NO_ACTOR = os.environ.get("APEX_DIAG_NO_ACTOR") == "1"
 
 
 @dataclass
@@ -122,7 +118,6 @@ class ApexEngine:
         self.publish_params()
         self.learn_steps = 0
         self.actor_steps = 0
-        self._diag_skip_actor = False
         self._g_actor = self._g_learn_a = self._g_learn_a2 = self._g_learn_b = self._g_dp = None
         self._pool = None
         self._mass_pending = False  # next step's shard masses already exchanged (with the conv grads)
@@ -161,9 +156,8 @@ class ApexEngine:
     def _actor_half(self, half: int):
         """Actor steps into staging half ``half``."""
         k = self.cfg.actor_steps_per_learner_step
-        if not self._diag_skip_actor:
-            for i in range(k):
-                self._actor_body(half * k + i)
+        for i in range(k):
+            self._actor_body(half * k + i)
 
     def _apply_half(self, half: int):
         k = self.cfg.actor_steps_per_learner_step
@@ -423,7 +417,6 @@ class ApexEngine:
         else:
             for _ in range(steps):
                 self.actor_step()
-        self._diag_skip_actor = _DIAG_NO_ACTOR
 
     def train_step(self) -> None:
         """One Ape-X step of this rank: one learner SGD step + its actor steps."""

@@ -180,20 +180,20 @@ class AQLEngineConfig:
     # 12978-13005 vs 13161 SGD steps/s serial -- the learner's chain of small kernels slows by
     # about what the hidden acting step saves, so serial stays the default
     overlap: bool = False
-    fused_sample: bool = os.environ.get("APEX_AQL_FUSED_SAMPLE", "1") == "1"  # PER draw inside aql_learn_fwd
+    fused_sample: bool = True  # PER draw inside aql_learn_fwd
     # priority write as an extra workgroup of the noise-reset launch: measured 12936-12958 vs 13117
     # SGD steps/s (the one-workgroup tree write, ~15 us in a 256-thread block, then bounds that launch)
-    fused_tree: bool = os.environ.get("APEX_AQL_FUSED_TREE", "0") == "1"
+    fused_tree: bool = False
     # priority write split over the two launches that follow the backward: the leaves (claims,
     # mix, loss mean, dirty list) as an extra workgroup of the gradient contraction, the level
     # walk as an extra workgroup of the noise reset -- no launch of its own on the chain
     # (MI355X, batch 32: 14758-14771 vs 13882-13899 SGD steps/s with the write as its own launch,
     # one box, interleaved; scripts/ab/aql_split_tree.sh)
-    split_tree: bool = os.environ.get("APEX_AQL_SPLIT_TREE", "1") == "1"
+    split_tree: bool = True
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
-    act_blocks: int = int(os.environ.get("APEX_AQL_ACT_BLOCKS", "0"))
-    act_q: str = os.environ.get("APEX_AQL_ACTQ", "mfma")  # acting Q: "mfma" = the learner's fp32-MFMA candidate forward (aql_act_q),
+    act_blocks: int = 0
+    act_q: str = "mfma"  # acting Q: "mfma" = the learner's fp32-MFMA candidate forward (aql_act_q),
                              # "scalar" = one wave per candidate item (aql_candidate_q)
     seed: int = 0
 

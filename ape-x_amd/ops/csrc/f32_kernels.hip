@@ -1003,8 +1003,8 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 // rows of a tile share one input position and the same set of in-range taps.  The k loop runs
 // over exactly those taps -- the sample-major forms above multiply the zero border: 40% of
 // the conv3 dgrad MFMA work (21 of 27 (ky, iy) pairs in range per axis) and 19% of conv2's.
-// BM x BN tiles of (samples at one input position) x (input channels); 128 x 32 (two n-tiles)
-// or 64 x 64 (whole N: each dy3 row staged once; f32_set_variant(17, 1))
+// BM x BN tiles of (samples at one input position) x (input channels): 128 x 32 (two n-tiles;
+// 64 x 64 with each dy3 row staged once measured no better)
 template <int BM_, int BN_, int WM_>
 struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b][pi - tap][co] w3t[tap][ci][co]
   static constexpr int BM = BM_, BN = BN_, BK = 32, WM = WM_;
