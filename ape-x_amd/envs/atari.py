@@ -224,7 +224,8 @@ class EpisodicLifeEnv(Wrapper):
 
 
 class MaxAndSkipEnv(Wrapper):
-    """Repeat stage: ``skip`` frames per action, max over the window's last two frames."""
+    """Repeat stage: ``skip`` frames per action, max-pooled over the persistent two-slot
+    buffer of the reference (see ``preprocess.RepeatPool``)."""
 
     def __init__(self, env, skip=4):
         super().__init__(env)

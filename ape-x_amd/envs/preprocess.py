@@ -53,19 +53,42 @@ def lives_of(env) -> int:
 
 
 class RepeatPool:
-    """Action repeat with a max-pool over the last two emulator frames of the window."""
+    """Action repeat with a max-pool over two emulator frames.
 
-    def __init__(self, repeat: int = 4):
+    ``reference=True`` (default; origin_repo/wrapper.py:99-124 MaxAndSkipEnv): a PERSISTENT
+    two-slot buffer written only at repeat steps ``repeat - 2`` and ``repeat - 1``, so when
+    the episode ends earlier in the window the pooled frame still holds frames of an earlier
+    window (the reference notes the done-frame observation "doesn't matter"; it is kept
+    bit-exact here).  ``reference=False``: the max of the last two frames of THIS window
+    (the done frame itself when the window ends after one step)."""
+
+    def __init__(self, repeat: int = 4, reference: bool = True):
         self.repeat = int(repeat)
+        self.reference = bool(reference)
+        self._slots = None
+
+    def reset(self) -> None:
+        """Forget the persistent slots (a fresh emulator)."""
+        self._slots = None
 
     def run(self, step_fn, action):
         total, prev, last, done, info = 0.0, None, None, False, {}
-        for _ in range(self.repeat):
+        for i in range(self.repeat):
             frame, r, done, info = step_fn(action)
+            if self.reference:
+                if self._slots is None:
+                    f = np.asarray(frame)
+                    self._slots = np.zeros((2,) + f.shape, dtype=f.dtype)
+                if i == self.repeat - 2:
+                    self._slots[0] = frame
+                if i == self.repeat - 1:
+                    self._slots[1] = frame
             prev, last = last, frame
             total += r
             if done:
                 break
+        if self.reference:
+            return self._slots.max(axis=0), total, done, info
         pooled = last if prev is None else np.maximum(prev, last)
         return pooled, total, done, info
 
@@ -174,6 +197,7 @@ class PreprocessSpec:
     stack: int = 4                     # 0 / 1: no stacking
     scale: bool = False
     channels_first: bool = True        # ImageToPyTorch layout (the Ape-X actor's)
+    reference_pool: bool = True        # MaxAndSkipEnv's persistent two-slot buffer (RepeatPool)
 
     @classmethod
     def from_args(cls, args) -> "PreprocessSpec":
@@ -192,6 +216,8 @@ class AtariPreprocess:
     agent-level done (life loss included when ``episode_life``).  Observations are
     ``[k, h, w]`` (channels-first, H/W transposed) or ``[h, w, k]``, uint8 0..255, or
     float32 /255 with ``scale``.  Envs are not auto-reset: restart them with ``reset_one``.
+    The envs are stepped one after another (a Python loop over emulators: each step is an
+    emulator call plus numpy resize / stack work); only the frame stacks are one array.
     """
 
     def __init__(self, raw_envs, spec: PreprocessSpec = PreprocessSpec()):
@@ -205,7 +231,7 @@ class AtariPreprocess:
         if fire and (meaning(e0, 1) != "FIRE" or len(e0.unwrapped.get_action_meanings()) < 3):
             raise ValueError("the FIRE start needs FIRE at action 1 and at least 3 actions")
         self.fire = fire
-        self.pool = RepeatPool(spec.skip)
+        self.pools = [RepeatPool(spec.skip, spec.reference_pool) for _ in self.envs]  # per-env slots
         self.ledgers = [LifeLedger() for _ in self.envs]
         self.resize = AreaResize(e0.observation_space.shape[:2], spec.size, spec.grayscale)
         h, w = spec.size
@@ -226,7 +252,7 @@ class AtariPreprocess:
 
     # -- per-env stages composed in the reference order
     def _repeat(self, i, a):
-        return self.pool.run(self.envs[i].step, a)
+        return self.pools[i].run(self.envs[i].step, a)
 
     def _agent_step(self, i, a):
         frame, r, done, info = self._repeat(i, a)

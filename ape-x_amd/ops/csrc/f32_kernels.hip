@@ -528,9 +528,9 @@ constexpr int kPlaneDw = kPlane / 4;  // 1764 dwords per plane
 //    16 bits cleared, mid = (w - hi) likewise, lo = w - hi - mid (each subtraction is exact;
 //    lo has <= 8 significant bits).  A bf16 x bf16 product is exact in fp32.
 //  So x*w = x*hi + x*mid + x*lo with every product exact, accumulated in fp32 -- the hi
-//  products in one accumulator and the mid + lo products (2^-8 smaller) in another, so the
-//  extra terms add no rounding at the fp32 chain's scale (error vs fp64 measured in
-//  tests/test_gpu_f32_net.py against the fp32-MFMA kernel).  On v_mfma_f32_16x16x32_bf16
+//  products, the mid products and the lo products (2^-8 and 2^-16 smaller) in three
+//  accumulators, summed small-to-large at the end, so the extra terms add no rounding at the
+//  fp32 chain's scale (error vs fp64: tests/test_gpu_f32_net.py).  On v_mfma_f32_16x16x32_bf16
 //  (16 cycles per 16x16x32) the 3 terms cost 48 cycles where v_mfma_f32_16x16x4_f32 pays
 //  8 x 32 = 256 for the same 16x16x32 of fp32: 5.3x fewer MFMA cycles.
 //  Persistent over samples, two workgroups per CU (56 KB of LDS each: the sample's four
@@ -612,7 +612,6 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   const int i = lane & 15, q = lane >> 4, nh = wave >> 1;
   const __bf16* xb = reinterpret_cast<const __bf16*>(xs);
   W1Split w;
-  float bias = 0.f;
   int cur = -1;
   uint4 v[kC1xPer];
   // a contiguous run of samples per workgroup: the weight split is redone only at a
@@ -626,36 +625,55 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
     if (prob != cur) {  // block-uniform
       cur = prob;
       split_w1(p.w + (nh * 16 + i) * 256 + 8 * q, w);
-      bias = p.bias[nh * 16 + i];
     }
     __syncthreads();  // the previous sample's tiles are done with xs
     c1x_store(v, xs);
     __syncthreads();
     if (smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
-    float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + i;
-    for (int tile = wave & 1; tile < 25; tile += 2) {
+    // roles swapped on the MFMA (A = the weight slice, B = the pixels: identical lane maps),
+    // so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte store
+    float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
+    float4 bias4;
+    bias4.x = p.bias[nh * 16 + 4 * q];
+    bias4.y = p.bias[nh * 16 + 4 * q + 1];
+    bias4.z = p.bias[nh * 16 + 4 * q + 2];
+    bias4.w = p.bias[nh * 16 + 4 * q + 3];
+    auto frags = [&](int tile, bfx8 (&a)[8]) {
       const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
       const __bf16* a0 = xb + (4 * oy + q) * 84 + 4 * ox;
-      bfx8 a[8];
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
         const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
         const uint2 lo = ap[0], hi = ap[1];
         a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
-      f32x4 ah = zero4(), al = zero4();
+    };
+    auto tile_mfma = [&](int tile, const bfx8 (&a)[8]) {
+      // three accumulators (hi / mid / lo products): no MFMA waits on its predecessor's result
+      f32x4 ah = zero4(), am = zero4(), al = zero4();
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
-        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.hi[kb], ah, 0, 0, 0);
-        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.mid[kb], al, 0, 0, 0);
-        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb], w.lo[kb], al, 0, 0, 0);
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.hi[kb], a[kb], ah, 0, 0, 0);
+        am = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.mid[kb], a[kb], am, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.lo[kb], a[kb], al, 0, 0, 0);
       }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float y = fmaxf(ah[e] + al[e] + bias, 0.f);
-        const size_t o = (size_t)(tile * 16 + 4 * q + e) * 32;
-        out[o] = y;
-      }
+      float4 y;
+      y.x = fmaxf(ah[0] + (am[0] + al[0]) + bias4.x, 0.f);
+      y.y = fmaxf(ah[1] + (am[1] + al[1]) + bias4.y, 0.f);
+      y.z = fmaxf(ah[2] + (am[2] + al[2]) + bias4.z, 0.f);
+      y.w = fmaxf(ah[3] + (am[3] + al[3]) + bias4.w, 0.f);
+      *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
+    };
+    // ping-pong fragment buffers: the next tile's LDS reads are in flight during this tile's MFMAs
+    bfx8 fa[8], fb[8];
+    int tile = wave & 1;
+    frags(tile, fa);
+    for (; tile < 25; tile += 4) {
+      if (tile + 2 < 25) frags(tile + 2, fb);
+      tile_mfma(tile, fa);
+      if (tile + 2 >= 25) break;
+      if (tile + 4 < 25) frags(tile + 4, fa);
+      tile_mfma(tile + 2, fb);
     }
   }
 }
@@ -841,7 +859,7 @@ constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) /
 // conv1 weight gradient at reference precision on bf16 MFMA (the exact split of the
 // forward above, applied to dy): the u8 frame operand is exact in bf16 and each dy value
 // splits exactly into hi + mid + lo bf16, so every product is exact and only the fp32
-// accumulation rounds (hi products and mid + lo products in separate accumulators).
+// accumulation rounds (hi, mid and lo products in separate accumulators).
 // Same workgroup layout and partials as f32_conv1_wgrad_k (8 waves = 2 samples x 4 input
 // channels c; wave c owns columns kk = c*64 + (col >> 1)*8 + 4 (col & 1) + i of the 4 tiles
 // i, both co halves), but the reduction runs over PIXEL GROUPS of 8 on
@@ -882,11 +900,12 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
     if (t < 16) pl[kConv1WgradS * 4 * kPlaneDw + t] = 0u;
   }
   __syncthreads();
-  f32x4 ah[2][4], al[2][4];
+  // hi / mid / lo products in three accumulators: no MFMA waits on its predecessor's result
+  f32x4 ah[2][4], am[2][4], al[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ah[h][i] = al[h][i] = zero4();
+    for (int i = 0; i < 4; ++i) ah[h][i] = am[h][i] = al[h][i] = zero4();
   float bs0 = 0.f, bs1 = 0.f;  // bias partials of co = col, 16 + col
   if (sl < ns) {
     const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
@@ -955,7 +974,7 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           ah[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][0], Bf, ah[h][i], 0, 0, 0);
-          al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][1], Bf, al[h][i], 0, 0, 0);
+          am[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][1], Bf, am[h][i], 0, 0, 0);
           al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][2], Bf, al[h][i], 0, 0, 0);
         }
       }
@@ -973,7 +992,8 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = ah[h][i][e] + al[h][i][e];
+        for (int e = 0; e < 4; ++e)
+          red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = ah[h][i][e] + (am[h][i][e] + al[h][i][e]);
     if (c == 0 && q == 0) {
       red[4 * 32 * 64 + col] = bs0;
       red[4 * 32 * 64 + 16 + col] = bs1;
@@ -988,7 +1008,7 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float v = (ah[h][i][e] + al[h][i][e]) + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
+          const float v = (ah[h][i][e] + (am[h][i][e] + al[h][i][e])) + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
           const int co = h * 16 + 4 * q + e, kk = c * 64 + (col >> 1) * 8 + 4 * (col & 1) + i;
           out[co * 256 + kk] = v;
         }

@@ -169,3 +169,44 @@ def test_vector_pipeline_matches_wrapper_stack(game, episode_life, scale):
     assert obs_v.dtype == (np.float32 if scale else np.uint8)
     if episode_life and game != "Pong":  # Pong has no lives (21-point games)
         assert n_done > 0  # life losses and the restarts after them were exercised
+
+
+def test_repeat_pool_terminal_frames_match_the_reference_buffer():
+    """origin_repo/wrapper.py:99-124 keeps a persistent two-slot buffer written only at
+    repeat steps skip-2 and skip-1: a window that ends early returns the max of frames from
+    EARLIER windows.  RepeatPool(reference=True) pins that; reference=False is the
+    this-window max."""
+    import numpy as np
+
+    from apex_amd.envs.preprocess import RepeatPool
+
+    def stepper(dones):
+        it = iter(dones)
+        k = [0]
+
+        def step(_a):
+            k[0] += 1
+            return np.full((2, 2), k[0], dtype=np.uint8), 1.0, next(it), {}
+        return step
+
+    ref, win = RepeatPool(4), RepeatPool(4, reference=False)
+    # window 1: frames 1..4, slots <- (3, 4); window 2 ends at its first step (frame 5)
+    dones = [False] * 4 + [True]
+    s_ref, s_win = stepper(dones), stepper(dones)
+    assert int(ref.run(s_ref, 0)[0].max()) == 4 and int(win.run(s_win, 0)[0].max()) == 4
+    f_ref, r_ref, d_ref, _ = ref.run(s_ref, 0)
+    f_win, _, _, _ = win.run(s_win, 0)
+    assert d_ref and r_ref == 1.0
+    assert int(f_ref.max()) == 4   # stale slots of window 1 (the reference's behaviour)
+    assert int(f_win.max()) == 5   # this window's only frame
+    # a window ending at step skip-2 (third frame) overwrites slot 0 only: max(slot0 new, slot1 old)
+    p = RepeatPool(4)
+    s = stepper([False] * 4 + [False, False, True])
+    p.run(s, 0)                       # slots (3, 4)
+    f, _, d, _ = p.run(s, 0)          # frames 5, 6, 7(done at i=2): slot0 <- 7, slot1 stays 4
+    assert d and int(f.max()) == 7 and int(f.min()) == 7
+    p2 = RepeatPool(4)
+    s2 = stepper([False] * 4 + [False, True])
+    p2.run(s2, 0)
+    f2, _, _, _ = p2.run(s2, 0)       # frames 5, 6(done at i=1): slots untouched -> max(3, 4)
+    assert int(f2.max()) == 4
