@@ -30,6 +30,7 @@ Nothing is lock-step (the reference decouples its roles the same way: actor.py p
 """
 from __future__ import annotations
 
+import dataclasses
 import time
 import torch
 import torch.distributed as dist
@@ -95,6 +96,10 @@ class CentralApexEngine:
         if self.is_learner:
             self.replay = HBMReplay(self.C_r * self.R, E, lc.n_step, cfg.alpha, self.device,
                                     frame_capacity=self.F_r * self.R, exact_mass=cfg.exact_mass, seed=cfg.seed)
+            if transport in ("ipc", "auto") and self.device.type == "cuda" and lc.forward == "hip":
+                # the IPC ingest runs on the learner's tree stream beside the backward: the step
+                # reads private copies of its sampled rows (the ingest may rewrite their slots)
+                lc = dataclasses.replace(lc, private_rows=True)
             self.learner = DQNLearner(model, self.replay, lc)
             self.flat = self.learner.flat
             self.regions = {r: Region((r - 1) * self.C_r, self.C_r, (r - 1) * self.F_r, self.F_r)
@@ -285,8 +290,14 @@ class CentralApexEngine:
             self.links.publish(self.flat)
 
     def _learner_body(self) -> None:
+        if self.transport == "ipc" and self.learner.rows is not None:
+            # ingest rides in the learner graph (no host poll per step), on the tree stream
+            # after the step's priority write: beside the conv backward, off the critical chain
+            self.learner.tree_tail.append(self.links.ingest)
+            self.learner.step()
+            return
         self.learner.step()
-        if self.transport == "ipc":  # ingest rides in the learner graph: no host poll per step
+        if self.transport == "ipc":
             self.links.ingest()
 
     def learner_step(self) -> None:

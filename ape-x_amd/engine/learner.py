@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import copy
 from dataclasses import dataclass
+from types import SimpleNamespace
 
 import torch
 
@@ -47,6 +48,10 @@ class LearnerConfig:
     dtype: str = "fp32"            # compute precision: "fp32" (reference, learner.py:139-145: fp32 MFMA on the
                                    # hip path, no autocast on the torch path) | "bf16" (opt-in fast mode)
     seed: int = 0
+    # the sampling launch copies every sampled row (frame ids, action, return, done) into
+    # private buffers that the forward, loss and backward read: writers of the replay tables
+    # may then run beside the step (the central topology's ingest, engine/central.py)
+    private_rows: bool = False
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -160,6 +165,10 @@ class DQNLearner:
             self.fin_partials = torch.zeros(8192, dtype=torch.float64, device=dev)
             self.n_fin_partials = 0
         self._src = None  # (s ids, s' ids, idx, transition table) of the batch in flight
+        self.rows = replay.row_buffers(B) if cfg.private_rows else None
+        # one-shot callables run on the tree stream AFTER this step's priority write (the
+        # central engine's ingest: its leaf writes must follow the learner's for a shared slot)
+        self.tree_tail = []
         # one-shot callables run on the tree stream before this step's priority write
         # (the overlapped engine's deferred actor-row priorities)
         self.tree_hooks = []
@@ -219,8 +228,11 @@ class DQNLearner:
                                        extra[1].numel(), s)
         rp = self.replay
         self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
-                                   rows=rows[-1] if rows else None)
-        self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
+                                   rows=rows[-1] if rows else None, out_rows=self.rows)
+        if self.rows is not None:  # the batch reads its private rows (no idx indirection)
+            self._src = (self.rows["s_ids"], self.rows["s2_ids"], None, SimpleNamespace(**self.rows))
+        else:
+            self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.  The three passes
@@ -311,6 +323,9 @@ class DQNLearner:
                 self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
             self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
                                          mix=(self.delta, self.lw, self.prio, self.loss))
+            tail, self.tree_tail = self.tree_tail, []
+            for fn in tail:
+                fn()
 
     def _tree_fork_end(self) -> None:
         torch.cuda.current_stream().wait_stream(self.tree_stream)  # join: the next sample reads the tree
