@@ -195,6 +195,10 @@ class AQLEngineConfig:
     act_blocks: int = 0
     act_q: str = "mfma"  # acting Q: "mfma" = the learner's fp32-MFMA candidate forward (aql_act_q),
                              # "scalar" = one wave per candidate item (aql_candidate_q)
+    # everything after the forward in ONE launch (aql_step_tail_k: backward + priority write +
+    # target noise | gradients | Adam x2 + online noise + proposal copy, grid barriers between
+    # the phases) instead of four; batch <= 64, not with fork_tree
+    fused_step: bool = True
     seed: int = 0
 
 
@@ -308,6 +312,18 @@ class AQLLearner:
                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                        if split else None)
         self.post_levels = h.aql_post_set_levels(self.post, r.tree, r.wlist.data_ptr(), B) if split else None
+        self.S = None
+        if cfg.fused_step and not cfg.fork_tree and B <= 64:
+            self.bar = torch.zeros(4, dtype=torch.int32, device=dev)  # arrivals, generation, error flag
+            self.step_desc = torch.zeros(h.aql_step_nbytes(), dtype=torch.uint8, device=dev)
+            self.S = h.make_aql_step(
+                self.L, self.G, self.post, r.tree, self.hp,
+                dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
+                     norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
+                     bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
+                     loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
+                     max_prio=r.max_prio.data_ptr(), alpha=r.alpha),
+                self.step_desc.data_ptr())
         self.refresh()
 
     def refresh(self) -> None:
@@ -376,6 +392,10 @@ class AQLLearner:
             h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
                          self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
             h.aql_learn_fwd(self.L, s)
+        if self.S is not None:  # backward, priority write, gradients, optimizers, noise: one launch
+            h.aql_step_tail(self.S, s)
+            self._track_losses()
+            return
         h.aql_learn_bwd(self.L, s)
         # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
         # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
@@ -406,6 +426,9 @@ class AQLLearner:
                      self.hp, self.step_ctr.data_ptr(), s)
         h.aql_post(self.post_tree if self.post_tree is not None else
                    (self.post_levels if self.post_levels is not None else self.post), 1, s)
+        self._track_losses()
+
+    def _track_losses(self) -> None:
         if self.cfg.track_losses:  # device-side running sums; read (one sync) only when logging
             self.loss_acc[0:1].add_(self.loss_q)
             self.loss_acc[1:2].add_(self.loss_p)
@@ -426,8 +449,15 @@ class AQLLearner:
         self.hip.copy_f32(self.teps.data_ptr(), self.eps.data_ptr(), self.eps.numel(), s)
         self.refresh()
 
+    def check_fused(self) -> None:
+        """Raise if a grid barrier of the fused step tail ever timed out (host sync)."""
+        if self.S is not None and int(self.bar[2].item()) != 0:
+            raise RuntimeError("aql_step_tail: a grid barrier timed out (the grid was not co-resident); "
+                               "results since then are invalid")
+
     def stats(self) -> dict:
         self.join()
+        self.check_fused()
         return {"loss_q": float(self.loss_q.item()), "loss_proposal": float(self.loss_p.item()),
                 "grad_norm_q": float(self.norms_q[0].item()), "grad_norm_proposal": float(self.norms_p[0].item()),
                 "steps": int(self.step_ctr.item())}

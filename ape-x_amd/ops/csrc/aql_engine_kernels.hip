@@ -40,7 +40,9 @@
 #include <algorithm>
 
 #include "common.h"
+#include "grid_sync.h"
 #include "kernels.h"
+#include "opt_dev.h"
 #include "tree_dev.h"
 
 namespace apex {
@@ -358,7 +360,22 @@ __device__ __forceinline__ float lds_row_dot(const float* Wl, int n8, const floa
   return a;
 }
 
-__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
+// Double-Q TD target, Huber + IS weight (utils.py:50-60) of sample b: |td|, w * Huber and the
+// loss gradient w.r.t. Q(s, a).  Shared by the backward and the fused step's tree workgroup.
+struct AqlTd {
+  float dl, lw, gq;
+};
+__device__ __forceinline__ AqlTd aql_td(const AqlLearn& L, int b, int row, int a_idx, int s_next) {
+  const int T = L.on.T;
+  const float qa = L.q_s[(size_t)b * T + a_idx], qt = L.qt_s2[(size_t)b * T + s_next];
+  const float y = L.rew[row] + L.gamma_n * qt * (1.f - L.done[row]);
+  const float diff = y - qa, dl = fabsf(diff), wb = L.w[b];
+  const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+  return AqlTd{dl, wb * (dl < 1.f ? 0.5f * dl * dl : dl - 0.5f), -sg * fminf(dl, 1.f) * wb / (float)L.B};
+}
+
+// the backward of sample b by one workgroup (aql_learn_bwd_k, or phase A of aql_step_tail_k)
+__device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   __shared__ __attribute__((aligned(16))) float s_s[64];
   __shared__ float s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
   __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
@@ -371,7 +388,7 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   __shared__ float sw_ao1[kCat * (kMaxAdim + 1)];
   const AQLNet& N = L.on;
   const float* eff = L.eff_on;
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int T = N.T, obs = N.obs, adim = N.adim, na = N.na, B = L.B, cont = N.cont;
   const int row = L.idx[b];
   const int a_idx = L.act[row];
@@ -445,14 +462,11 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
       }
     }
   }
-  if (t == 0) {  // Double-Q TD target, Huber + IS weight (utils.py:50-60)
-    const float qa = L.q_s[(size_t)b * T + a_idx], qt = L.qt_s2[(size_t)b * T + s_next];
-    const float y = L.rew[row] + L.gamma_n * qt * (1.f - L.done[row]);
-    const float diff = y - qa, dl = fabsf(diff), wb = L.w[b];
-    L.delta[b] = dl;
-    L.lw[b] = wb * (dl < 1.f ? 0.5f * dl * dl : dl - 0.5f);
-    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-    s_gq = -sg * fminf(dl, 1.f) * wb / (float)B;
+  if (t == 0) {
+    const AqlTd td = aql_td(L, b, row, a_idx, s_next);
+    L.delta[b] = td.dl;
+    L.lw[b] = td.lw;
+    s_gq = td.gq;
   }
   // forward of the taken candidate (s, a_mu[a]) + the proposal trunk.  First layers from
   // the LDS-staged matrices (thread per row), then the 64/128-wide layers wave-per-row.
@@ -560,20 +574,17 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   AQL_STAMP(L, 7);
 }
 
+__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) { aql_bwd_block(L, blockIdx.x); }
+
 // ------------------------------------------------------------------ weight gradients
 constexpr int kGradThreads = 256;
 
-__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+// the weight gradients of flat elements [bid * 256, +256) and the block's per-group sums of
+// squares (aql_grad_k, or phase B of aql_step_tail_k); returns the thread's gradient
+__device__ __forceinline__ float aql_grad_block(const AqlGrad& G, int bid, int nblk) {
   __shared__ double red[2][4];
-  if (G.tree_leaves && blockIdx.x == gridDim.x - 1) {  // block-uniform: the split tree write's leaves
-    __shared__ float tred[16];
-    __shared__ int sids[64];
-    batch_leaves_block(G.tree, G.bw, 0, tred, sids);
-    return;
-  }
-  const int nblk = (int)gridDim.x - G.tree_leaves;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t i = (int64_t)blockIdx.x * kGradThreads + t;
+  const int64_t i = (int64_t)bid * kGradThreads + t;
   float g = 0.f;
   int grp = -1;
   if (i < G.n) {
@@ -618,15 +629,26 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   }
   __syncthreads();
   if (t == 0) {
-    G.part[blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    G.part[nblk + blockIdx.x] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    G.part[bid] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    G.part[nblk + bid] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   }
-  if (blockIdx.x == 0 && wave == 1 && G.lossp_out) {
+  if (bid == 0 && wave == 1 && G.lossp_out) {
     float a = 0.f;
     for (int b = lane; b < G.B; b += 64) a += G.lossp[b];
     a = wave_sum(a);
     if (lane == 0) G.lossp_out[0] = a / (float)G.B;
   }
+  return g;
+}
+
+__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+  if (G.tree_leaves && blockIdx.x == gridDim.x - 1) {  // block-uniform: the split tree write's leaves
+    __shared__ float tred[16];
+    __shared__ int sids[64];
+    batch_leaves_block(G.tree, G.bw, 0, tred, sids);
+    return;
+  }
+  aql_grad_block(G, blockIdx.x, (int)gridDim.x - G.tree_leaves);
 }
 
 // ------------------------------------------------------------------ noise reset + proposal copy
@@ -689,6 +711,159 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
     if (tk == (int)gridDim.x - 1) {
       P.step[0] = (int64_t)st + 1;
       P.ticket[0] = 0;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ fused step tail
+// aql_step_tail_k: everything of one learner step after the candidate forward, in ONE launch
+// of grid = max(gradient blocks, B + 1) + 1 workgroups, all co-resident (the launcher checks
+// the occupancy), in three phases separated by grid barriers (grid_sync.h):
+//
+//   A  blocks [0, B): the per-sample backward (aql_bwd_block)
+//      last block:    this step's priority write -- it recomputes the B TD terms itself
+//                     (aql_td: the same formula the backward uses) from the forward's Q
+//                     rows, so the leaves AND every level run here, beside the backward,
+//                     instead of after it (the next step's sampler is the only reader)
+//      other blocks:  the TARGET critic's noise reset (reads target parameters only)
+//   B  blocks [0, nblk): the weight-gradient contraction (aql_grad_block) + norm partials
+//   C  every block:   both clipped Adam steps over the flat parameters, the ONLINE noise
+//                     reset (the thread owning a sigma element also updates its mu partner,
+//                     then draws the new epsilon and writes mu + sigma eps), the proposal
+//                     hard copy online -> target; the last block bumps the step counter
+//
+// Same arithmetic as the separate launches (aql_learn_bwd_k, aql_grad_k, opt_step2_k,
+// aql_post_k): the gradient partials keep aql_grad_k's block layout, so the clip norms and
+// every update are bit-identical (tests/test_gpu_aql_engine.py).
+__device__ __forceinline__ float noise_w(uint64_t seed, int l, int o, int c, uint64_t st) {
+  return scaled_noise(seed, l, 0, o, st) * scaled_noise(seed, l, 1, c, st);
+}
+
+// element i of noisy layer l's [weights | biases]: fresh epsilon, effective weight from the
+// layer's parameters as they are in memory (the target critic: not updated by this step)
+__device__ __forceinline__ void noise_elem(const AqlNoise& z, int l, int64_t i, uint64_t seed, uint64_t st) {
+  const int64_t nw = (int64_t)z.out * z.in;
+  if (i < nw) {
+    const int o = (int)(i / z.in), c = (int)(i - (int64_t)o * z.in);
+    const float e = noise_w(seed, l, o, c, st);
+    z.weps[i] = e;
+    z.weff[i] = fmaf(z.wsig[i], e, z.wmu[i]);
+  } else if (i < nw + z.out) {
+    const int o = (int)(i - nw);
+    const float e = scaled_noise(seed, l, 2, o, st);
+    z.beps[o] = e;
+    z.beff[o] = fmaf(z.bsig[o], e, z.bmu[o]);
+  }
+}
+
+__device__ __forceinline__ void step_tree_block(const AqlStep& D) {
+  __shared__ float s_dl[64], s_lw[64], tred[16];
+  __shared__ int sids[64];
+  const AqlLearn& L = D.L;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, T = L.on.T;
+  for (int b = wave; b < L.B; b += (int)(blockDim.x >> 6)) {  // wave-uniform
+    const int s_next = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
+    if (lane == 0) {
+      const int row = L.idx[b];
+      const AqlTd td = aql_td(L, b, row, L.act[row], s_next);
+      s_dl[b] = td.dl;
+      s_lw[b] = td.lw;
+    }
+  }
+  __syncthreads();
+  BatchWrite w = D.bw;
+  w.mix.delta = s_dl;
+  w.mix.lw = s_lw;
+  batch_leaves_block(D.tree, w, 1, tred, sids);
+}
+
+__global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
+  const AqlStep& D = *Dp;
+  const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  const int B = D.L.B;
+  const uint64_t st = (uint64_t)D.P.step[0];
+  // ---- phase A
+  if (bid < B) {
+    aql_bwd_block(D.L, bid);
+  } else if (bid == G - 1) {
+    step_tree_block(D);
+  } else {
+    const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
+    const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
+    for (int64_t i = (int64_t)(bid - B) * 256 + t; i < n2 + n3; i += (int64_t)(G - 1 - B) * 256) {
+      if (i < n2) noise_elem(D.P.layer[2], 2, i, D.P.seed, st);
+      else noise_elem(D.P.layer[3], 3, i - n2, D.P.seed, st);
+    }
+  }
+  grid_sync(D.bar, (unsigned)G, D.err);
+  // ---- phase B
+  float g = 0.f;
+  if (bid < D.nblk) g = aql_grad_block(D.G, bid, D.nblk);
+  grid_sync(D.bar, (unsigned)G, D.err);
+  // ---- phase C
+  float lr;
+  const AdamRule rule = make_rule(D.hp, (int64_t)st, lr);
+  const NormInfo nq = reduce_norms(D.G.part, D.nblk, D.hp.max_norm, D.hp.grad_scale);
+  __syncthreads();  // reduce_norms' LDS is reused
+  const NormInfo np = reduce_norms(D.G.part + D.nblk, D.nblk, D.hp.max_norm, D.hp.grad_scale);
+  if (bid == 0 && t == 0) {
+    const float mn = D.hp.max_norm;
+    D.norms_q[0] = nq.l2;
+    D.norms_q[2] = fminf(mn > 0.f ? mn / (nq.l2 + 1e-6f) : 1.f, 1.f);
+    D.norms_q[3] = lr;
+    D.norms_p[0] = np.l2;
+    D.norms_p[2] = fminf(mn > 0.f ? mn / (np.l2 + 1e-6f) : 1.f, 1.f);
+    D.norms_p[3] = lr;
+  }
+  const int64_t i = (int64_t)bid * 256 + t;
+  if (bid < D.nblk && i < D.n) {
+    // online noisy tensors: mu elements are updated by their sigma partner's thread
+    int kind = 0, l = 0;
+    int64_t e = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int64_t nw = (int64_t)D.P.layer[k].out * D.P.layer[k].in, nb = D.P.layer[k].out;
+      if ((i >= D.mu_w[k] && i < D.mu_w[k] + nw) || (i >= D.mu_b[k] && i < D.mu_b[k] + nb)) kind = 1;
+      if (i >= D.sig_w[k] && i < D.sig_w[k] + nw) { kind = 2; l = k; e = i - D.sig_w[k]; }
+      if (i >= D.sig_b[k] && i < D.sig_b[k] + nb) { kind = 3; l = k; e = i - D.sig_b[k]; }
+    }
+    if (kind != 1) {
+      const bool prop = i >= D.P_q;
+      float a = D.m[i], b = D.v[i];
+      const float pn = rule(D.p[i], opaque(g * (prop ? np.clip : nq.clip)), a, b);
+      D.m[i] = a;
+      D.v[i] = b;
+      D.p[i] = pn;
+      if (prop) D.P.dst[i - D.P_q] = pn;
+      if (kind >= 2) {
+        const AqlNoise& z = D.P.layer[l];
+        const int64_t im = (kind == 2 ? D.mu_w[l] : D.mu_b[l]) + e;
+        float a2 = D.m[im], b2 = D.v[im];
+        const float mun = rule(D.p[im], opaque(D.G.grad[im] * nq.clip), a2, b2);
+        D.m[im] = a2;
+        D.v[im] = b2;
+        D.p[im] = mun;
+        if (kind == 2) {
+          const int o = (int)(e / z.in), c = (int)(e - (int64_t)o * z.in);
+          const float ep = noise_w(D.P.seed, l, o, c, st);
+          z.weps[e] = ep;
+          z.weff[e] = fmaf(pn, ep, mun);
+        } else {
+          const float ep = scaled_noise(D.P.seed, l, 2, (int)e, st);
+          z.beps[e] = ep;
+          z.beff[e] = fmaf(pn, ep, mun);
+        }
+      }
+    }
+  }
+  // the step counter (Adam's bias correction, the noise stream) advances once every block is done
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const int tk = atomicAdd(D.P.ticket, 1);
+    if (tk == G - 1) {
+      D.P.step[0] = (int64_t)st + 1;
+      D.P.ticket[0] = 0;
     }
   }
 }
@@ -932,6 +1107,41 @@ void aql_post(const AqlPost& p, int regen, hipStream_t s) {
   if (extra && (p.bw.B < 1 || p.bw.B > 64 || p.bw.E != 0 || (p.tree_write == 1 && !p.bw.idx) || !p.bw.list))
     throw std::invalid_argument("aql_post: the fused tree write takes <= 64 learner rows and no actor rows");
   aql_post_k<<<(int)((n + 255) / 256) + extra, 256, 0, s>>>(p, regen);
+  LAUNCH_CHECK();
+}
+
+int aql_step_grid(const AqlStep& d) { return std::max(d.nblk, d.L.B + 1) + 1; }
+
+void aql_step_check(const AqlStep& d) {
+  check_net(d.L.on);
+  const AqlGrad& G = d.G;
+  if (d.nblk != aql_grad_blocks(G.n) || d.n != G.n || G.tree_leaves)
+    throw std::invalid_argument("aql_step: gradient blocks / parameter count / split tree write");
+  if (d.L.B < 1 || d.L.B > 64) throw std::invalid_argument("aql_step: 1 <= batch <= 64 (one-workgroup tree write)");
+  if (d.P_q <= 0 || d.P_q > d.n || !d.p || !d.m || !d.v || !d.norms_q || !d.norms_p || !G.grad || !G.part)
+    throw std::invalid_argument("aql_step: optimizer tensors");
+  if (!d.bar || !d.err || !d.P.step || !d.P.ticket || !d.P.dst || d.P.n_copy != d.n - d.P_q)
+    throw std::invalid_argument("aql_step: barrier / counter / proposal copy");
+  if (!d.bw.idx || d.bw.B != d.L.B || d.bw.E != 0 || !d.bw.owner || !d.bw.list || !d.bw.max_prio)
+    throw std::invalid_argument("aql_step: priority write");
+  for (int k = 0; k < 2; ++k) {
+    const int64_t nw = (int64_t)d.P.layer[k].out * d.P.layer[k].in, nb = d.P.layer[k].out;
+    for (int64_t o : {d.mu_w[k], d.sig_w[k]})
+      if (o < 0 || o + nw > d.P_q) throw std::invalid_argument("aql_step: online noisy weights outside the critic");
+    for (int64_t o : {d.mu_b[k], d.sig_b[k]})
+      if (o < 0 || o + nb > d.P_q) throw std::invalid_argument("aql_step: online noisy biases outside the critic");
+  }
+  int dev = 0, cus = 0, per_cu = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, aql_step_tail_k, 256, 0));
+  if ((int64_t)cus * per_cu < aql_step_grid(d))
+    throw std::runtime_error("aql_step: the grid does not fit co-resident (" + std::to_string(cus) + " CUs x " +
+                             std::to_string(per_cu) + " workgroups < " + std::to_string(aql_step_grid(d)) + ")");
+}
+
+void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s) {
+  aql_step_tail_k<<<grid, 256, 0, s>>>(dev);
   LAUNCH_CHECK();
 }
 

@@ -714,6 +714,47 @@ PYBIND11_MODULE(_apex_hip, m) {
     p.bw = w;
     return p;
   });
+  // fused step tail: the descriptor is validated, copied into `desc` (device memory of
+  // aql_step_nbytes() bytes, owned by the caller) and launched from there
+  struct AqlStepHandle {
+    const AqlStep* dev;
+    int grid;
+  };
+  py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid);
+  m.def("aql_step_nbytes", []() { return sizeof(AqlStep); });
+  m.def("make_aql_step", [](const AqlLearn& L, const AqlGrad& G, const AqlPost& Pst, const TreeHandle& t,
+                            const AdamParams& hp, py::dict p, uint64_t desc) {
+    auto g = [&](const char* k) { return p[k].cast<uint64_t>(); };
+    auto gi = [&](const char* k) { return p[k].cast<int64_t>(); };
+    AqlStep d{};
+    d.L = L;
+    d.G = G;
+    d.P = Pst;
+    d.tree = t.d;
+    d.hp = hp;
+    d.p = P<float>(g("p")); d.m = P<float>(g("m")); d.v = P<float>(g("v"));
+    d.n = gi("n"); d.P_q = gi("P_q");
+    d.norms_q = P<float>(g("norms_q")); d.norms_p = P<float>(g("norms_p"));
+    d.bar = P<unsigned>(g("bar")); d.err = P<int>(g("err"));
+    d.nblk = aql_grad_blocks(d.n);
+    for (int k = 0; k < 2; ++k) {  // offsets of the online noisy tensors in the flat buffer
+      const AqlNoise& z = Pst.layer[k];
+      d.mu_w[k] = z.wmu - d.p; d.sig_w[k] = z.wsig - d.p; d.mu_b[k] = z.bmu - d.p; d.sig_b[k] = z.bsig - d.p;
+    }
+    BatchWrite w{};
+    w.idx = L.idx;
+    w.B = L.B;
+    w.mix = PrioMix{L.delta, L.lw, P<float>(g("prio")), P<float>(g("loss_q"))};  // delta / lw: LDS at run time
+    w.owner = P<int>(g("owner"));
+    w.list = P<int>(g("list"));
+    w.max_prio = P<float>(g("max_prio"));
+    w.alpha = p["alpha"].cast<float>();
+    d.bw = w;
+    aql_step_check(d);
+    HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));
+    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), aql_step_grid(d)};
+  });
+  m.def("aql_step_tail", [](const AqlStepHandle& h, uint64_t s) { aql_step_tail(h.dev, h.grid, S(s)); });
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

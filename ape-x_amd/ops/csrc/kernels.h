@@ -508,6 +508,29 @@ struct AqlPost {
 // proposal copy, step + 1.  regen = 0: effective weights from the current noise only
 // (after initialisation / a target sync).
 void aql_post(const AqlPost& p, int regen, hipStream_t s);
+// Fused learner-step tail (aql_engine_kernels.hip: aql_step_tail_k): backward + priority
+// write + target noise reset | weight gradients | both clipped Adam steps + online noise reset
+// + proposal copy + step bump -- three phases of ONE launch separated by grid barriers
+// (grid_sync.h), replacing aql_learn_bwd + aql_grad + adam_step2 + aql_post.  The descriptor
+// lives in device memory (too large for kernel arguments).
+struct AqlStep {
+  AqlLearn L;              // the backward's view (online net, replay tables, per-sample outputs)
+  AqlGrad G;               // gradient jobs, grad, partials [2][nblk], proposal loss mean
+  AqlPost P;               // noisy layers (online 0-1, target 2-3), proposal copy, step, ticket
+  BatchWrite bw;           // this step's priority write (learner rows; the mix inputs come from LDS)
+  TreeDesc tree;
+  AdamParams hp;
+  float *p, *m, *v;        // flat parameters and Adam moments
+  int64_t n, P_q;          // critic [0, P_q), proposal [P_q, n)
+  float *norms_q, *norms_p;
+  int64_t mu_w[2], sig_w[2], mu_b[2], sig_b[2];  // flat offsets of the online noisy layers' tensors
+  unsigned* bar;           // [2] grid barrier (arrivals, generation), zero-initialised
+  int* err;                // set if a barrier wait timed out (grid not co-resident)
+  int nblk;                // gradient workgroups (aql_grad_blocks(n))
+};
+int aql_step_grid(const AqlStep& d);
+void aql_step_check(const AqlStep& d);  // shapes, pointers, and that the grid fits co-resident
+void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s);
 struct AqlEnv {
   int kind;            // 0 BipedalWalker-shaped, 1 CartPole, 2 Pendulum
   int E, obs, adim, T, max_steps;

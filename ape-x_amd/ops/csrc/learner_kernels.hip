@@ -10,6 +10,7 @@
 //   The same partials give the reference's logged 'grad_norm' formula.
 #include "common.h"
 #include "kernels.h"
+#include "opt_dev.h"
 
 namespace apex {
 
@@ -109,45 +110,6 @@ void grad_sumsq(const float* g, int64_t n, double* partials, hipStream_t s) {
 
 int grad_norm_partials() { return kNormBlocks; }
 
-// Every update block re-reduces the partials in the same fixed order (deterministic,
-// identical in all blocks): strided per-thread sums, a wave64 butterfly, then the 4 wave
-// sums in order -- one __syncthreads instead of a 256-wide LDS tree.  The reference's
-// per-tensor 'grad_norm' log value is computed on demand on the host side
-// (DQNLearner.stats), not on every step.  ``grad_scale`` (1/world for data-parallel
-// replicas) turns the all-reduced SUM into the mean inside this pass (no scaling kernel).
-struct NormInfo {
-  float clip, l2;
-};
-__device__ NormInfo reduce_norms(const double* partials, int n_partials, float max_norm, float grad_scale) {
-  __shared__ double red[4];
-  double t = 0.0;
-  // 4 loads in flight per round, added in the same (k-ascending) order as one at a time
-  const int bd = blockDim.x;
-  int k = threadIdx.x;
-  for (; k + 3 * bd < n_partials; k += 4 * bd) {
-    const double a0 = partials[k], a1 = partials[k + bd], a2 = partials[k + 2 * bd], a3 = partials[k + 3 * bd];
-    t += a0;
-    t += a1;
-    t += a2;
-    t += a3;
-  }
-  for (; k < n_partials; k += bd) t += partials[k];
-  t = wave_sum(t);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
-  __syncthreads();
-  NormInfo ni;
-  ni.l2 = (float)(sqrt((red[0] + red[1]) + (red[2] + red[3])) * (double)grad_scale);
-  const float coef = max_norm > 0.f ? max_norm / (ni.l2 + 1e-6f) : 1.f;
-  ni.clip = fminf(coef, 1.f) * grad_scale;  // applied to the raw (summed) gradient
-  return ni;
-}
-
-__device__ __forceinline__ float step_lr(float lr0, float gamma, int step_size, int offset, int64_t step) {
-  if (gamma == 1.f || step_size <= 0) return lr0;
-  const int64_t k = (step + offset) / step_size;
-  return lr0 * powf(gamma, (float)k);
-}
-
 __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v) {
   if (pk.arena_f32) {  // fp32 network: exact copies in the GEMM layouts
     const int d1 = pk.dst1[i], d2 = pk.dst2[i];
@@ -161,43 +123,6 @@ __device__ __forceinline__ void pack_store(const PackMap& pk, int64_t i, float v
   if (d1 >= 0) pk.arena[d1] = b;
   if (d2 >= 0) pk.arena[d2] = b;
 }
-
-// Per-element update rules: (param, clipped grad, state1, state2) -> new param, written
-// with explicit fmaf so every call site -- the FC1 tile path and the generic path --
-// rounds identically.  The build uses -ffp-contract=fast, under which the backend may
-// fuse a multiply into a later add differently per call site (the source pragma does
-// not stop that): the clipped gradient is therefore passed through ``opaque`` (an
-// empty asm that hides the multiply from the combiner, no instruction emitted).
-__device__ __forceinline__ float opaque(float x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-struct RmsRule {
-  float lr, a, oma, eps;
-  int centered;
-  __device__ __forceinline__ float operator()(float p, float gi, float& s1, float& s2) const {
-#pragma clang fp contract(off)
-    s1 = fmaf(s1, a, oma * gi * gi);  // square average
-    float avg;
-    if (centered) {
-      s2 = fmaf(oma, gi - s2, s2);  // grad average
-      avg = sqrtf(fmaxf(fmaf(-s2, s2, s1), 0.f)) + eps;
-    } else {
-      avg = sqrtf(s1) + eps;
-    }
-    return fmaf(-lr, gi / avg, p);
-  }
-};
-struct AdamRule {
-  float b1, b2, eps, wd, step_size, rbc2;
-  __device__ __forceinline__ float operator()(float p, float gi, float& m, float& v) const {
-#pragma clang fp contract(off)
-    if (wd != 0.f) gi = fmaf(wd, p, gi);
-    m = fmaf(1.f - b1, gi - m, m);
-    v = fmaf(v, b2, (1.f - b2) * gi * gi);
-    return fmaf(-step_size, m / fmaf(sqrtf(v), rbc2, eps), p);
-  }
-};
 
 // FC1 weights (advantage.0 / value.0, reference [128][C3*P3] with column c*P3 + p) are
 // updated in tiles of 8 rows x 8 channels x all 49 positions: fp32 reads/writes stay
@@ -219,17 +144,6 @@ __device__ __forceinline__ void opt_elem(float* p, const float* g, float* s1, fl
   s2[i] = b;
   p[i] = np;
   pack_store(pk, i, np);
-}
-
-__device__ __forceinline__ RmsRule make_rule(const RMSpropParams& hp, int64_t st, float& lr) {
-  lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
-  return RmsRule{lr, hp.alpha, 1.f - hp.alpha, hp.eps, hp.centered};
-}
-__device__ __forceinline__ AdamRule make_rule(const AdamParams& hp, int64_t st, float& lr) {
-  lr = step_lr(hp.lr0, hp.lr_gamma, hp.lr_step_size, hp.lr_step_offset, st);
-  const float t = (float)(st + 1);
-  const float bc1 = 1.f - powf(hp.beta1, t), bc2 = 1.f - powf(hp.beta2, t);
-  return AdamRule{hp.beta1, hp.beta2, hp.eps, hp.weight_decay, lr / bc1, 1.f / sqrtf(bc2)};
 }
 
 // The update of one parameter set by workgroup `bid` of `nblk` (opt_step_k: the whole grid;

@@ -14,12 +14,13 @@ def main():
     ap.add_argument("--env", default="BipedalWalker-v3")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--fused-step", type=int, default=1, help="one-launch step tail (aql_step_tail_k) or four")
     a = ap.parse_args()
     import torch
 
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
-    eng = AQLEngine(AQLEngineConfig(env_id=a.env, capacity=1_000_000), "cuda:0")
+    eng = AQLEngine(AQLEngineConfig(env_id=a.env, capacity=1_000_000, fused_step=bool(a.fused_step)), "cuda:0")
     eng.fill(4096)
     L = eng.learner
     L.step()
@@ -39,7 +40,7 @@ def main():
             L.step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"{a.iters} learner steps: {1e6 * dt / a.iters:.1f} us/step", L.stats())
+    print(f"fused_step={a.fused_step} {a.iters} learner steps: {1e6 * dt / a.iters:.1f} us/step", L.stats())
     if L.dbg is not None:  # APEX_AQL_DBG=1: backward phase timestamps (s_memtime cycles) of the last step
         d = L.dbg.cpu().tolist()
         print("bwd phase cycles:", [d[k + 1] - d[k] for k in range(7)], "total", d[7] - d[0])

@@ -271,28 +271,45 @@ def test_overlapped_acting_graphs_equal_eager(cuda):
 
 
 def test_fused_sampling_equals_per_sample(cuda):
-    """The learner forward's own PER draw (fused_sample) == per_sample + forward, and the
-    priority write folded into the noise-reset launch (fused_tree) or split over the gradient
-    and noise-reset launches (split_tree) == its own launch: same rows, IS weights, tree, loss
-    and parameters after several iterations, bit for bit."""
+    """The learner forward's own PER draw (fused_sample) == per_sample + forward, the priority
+    write folded into the noise-reset launch (fused_tree) or split over the gradient and
+    noise-reset launches (split_tree) == its own launch, and the whole step tail in one
+    grid-synchronised launch (fused_step: backward, tree write, gradients, both Adam steps,
+    noise reset, proposal copy) == the separate launches: same rows, IS weights, tree, loss,
+    parameters, moments, noise and target after several iterations, bit for bit."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    for fused_sample, fused_tree, split_tree in ((False, False, False), (True, False, False), (True, True, False),
-                                                 (True, False, True)):
+    variants = ((False, False, False, False), (True, False, False, False), (True, True, False, False),
+                (True, False, True, False), (True, False, False, True), (False, False, False, True))
+    for fused_sample, fused_tree, split_tree, fused_step in variants:
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
-                              fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree)
+                              fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree,
+                              fused_step=fused_step)
         eng = AQLEngine(cfg, cuda)
-        assert (eng.learner.Ls is not None) == fused_sample
-        assert (eng.learner.post_tree is not None) == fused_tree
-        assert (eng.learner.G_tree is not None) == split_tree
+        L = eng.learner
+        assert (L.Ls is not None) == fused_sample
+        assert (L.S is not None) == fused_step
+        if not fused_step:
+            assert (L.post_tree is not None) == fused_tree
+            assert (L.G_tree is not None) == split_tree
+        else:
+            assert L.S.grid >= max(L.nblk, L.B + 1) + 1
         eng.fill(1024)
         for _ in range(5):
             eng.iteration()
+        eng.capture()  # and graph-captured
+        for _ in range(3):
+            eng.iteration()
         torch.cuda.synchronize()
-        L, r = eng.learner, eng.replay
-        out.append((L.idx.clone(), L.w.clone(), L.flat.clone(), L.loss_q.clone(), r.leaf_sum.clone(),
-                    r.node_sum[-1].clone(), r.max_prio.clone()))
-    for other in out[1:]:
-        for x, y in zip(out[0], other):
-            assert torch.equal(x, y)
+        L.check_fused()
+        r = eng.replay
+        out.append((L.idx.clone(), L.w.clone(), L.flat.clone(), L.m.clone(), L.v.clone(), L.eps.clone(),
+                    L.teps.clone(), L.tflat.clone(), L.eff_on.clone(), L.eff_tg.clone(), L.loss_q.clone(),
+                    L.loss_p.clone(), L.prio.clone(), L.norms_q.clone(), L.norms_p.clone(), L.step_ctr.clone(),
+                    r.leaf_sum.clone(), r.node_sum[-1].clone(), r.max_prio.clone()))
+    names = ("idx", "w", "flat", "m", "v", "eps", "teps", "tflat", "eff_on", "eff_tg", "loss_q", "loss_p", "prio",
+             "norms_q", "norms_p", "step", "leaf_sum", "root", "max_prio")
+    for k, other in enumerate(out[1:], 1):
+        for name, x, y in zip(names, out[0], other):
+            assert torch.equal(x, y), (variants[k], name, (x.double() - y.double()).abs().max().item())
