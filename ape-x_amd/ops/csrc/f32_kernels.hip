@@ -64,6 +64,24 @@ __device__ __forceinline__ f32x4 u8x4(uint32_t w) {
 
 constexpr int kPlane = 84 * 84;
 
+// Raw buffer resources for the backward GEMM operands: a load at a byte offset past the
+// operand's range returns zeros (the range check of a raw buffer), and the rows of every
+// backward operand are sample-major, so the rows of a tile past the batch lie past the range.
+// The loaders then keep ONE 32-bit byte offset per chunk (k-invariant, computed once) plus
+// the k-block's wave-uniform offset: a single VALU add per 16-byte load, no 64-bit address
+// math and no "sample < B" select (operands below 2 GiB: host check).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void* p, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bld4(Rsrc r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+struct BufRow {
+  uint32_t off;  // byte offset of the chunk at k-block 0
+};
+
+
 struct NoSmem {
   int unused;
 };
@@ -700,21 +718,30 @@ struct Fc1Dgrad {  // dy3[b][k'] = (a3 > 0) * sum_n dz[b][n] wfc1p[n][k']
   using Smem = NoSmem;
   struct Ctx {
     int m0, n0, kb0, kb1;
+    Rsrc dy, w;
   };
   static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * 49; }
-  static __device__ void decode(const Args&, int block, Ctx& c, Smem&) {
+  static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
     c.n0 = (block % 49) * BN;
     c.m0 = (block / 49) * BM;
     c.kb0 = 0;
     c.kb1 = 256 / BK;
+    c.dy = make_rsrc(a.dy, (uint32_t)a.B * 256 * 4);
+    c.w = make_rsrc(a.w, 256 * 3136 * 4);
   }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int b = c.m0 + row;
-    if (b >= a.B) return zero4();
-    return ld4(a.dy + (size_t)b * 256 + kb * BK + 4 * ch);
+  using RowA = BufRow;
+  using RowB = BufRow;
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)((c.m0 + row) * 256 + 4 * ch) * 4};
   }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    return ld4(a.w + (size_t)(kb * BK + row) * 3136 + c.n0 + 4 * ch);
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
+    return bld4(c.dy, r.off + (uint32_t)(kb * BK * 4));
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)(row * 3136 + c.n0 + 4 * ch) * 4};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    return bld4(c.w, r.off + (uint32_t)(kb * BK * 3136 * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
     const int b = c.m0 + ml;
@@ -736,6 +763,7 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
   using Smem = NoSmem;
   struct Ctx {
     int m0, n0, kb0, kb1, split;
+    Rsrc dy, x;
   };
   static __host__ __device__ int tiles(int) { return 4 * 49; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
@@ -746,16 +774,23 @@ struct Fc1Wgrad {  // dW[n][k'] = sum_b dz[b][n] a3[b][k'], stored to the refere
     const int nkb = (a.B + BK - 1) / BK;
     c.kb0 = a.splits > 0 ? c.split * a.kbps : 0;
     c.kb1 = a.splits > 0 ? min(nkb, c.kb0 + a.kbps) : nkb;
+    c.dy = make_rsrc(a.dy, (uint32_t)a.B * 256 * 4);
+    c.x = make_rsrc(a.x, (uint32_t)a.B * 3136 * 4);
   }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int b = kb * BK + row;
-    if (b >= a.B) return zero4();
-    return ld4(a.dy + (size_t)b * 256 + c.m0 + 4 * ch);
+  // k = sample: chunk rows are samples kb * BK + row (past the batch: past the range)
+  using RowA = BufRow;
+  using RowB = BufRow;
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)(row * 256 + c.m0 + 4 * ch) * 4};
   }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int b = kb * BK + row;
-    if (b >= a.B) return zero4();
-    return ld4(static_cast<const float*>(a.x) + (size_t)b * 3136 + c.n0 + 4 * ch);
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
+    return bld4(c.dy, r.off + (uint32_t)(kb * BK * 256 * 4));
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)(row * 3136 + c.n0 + 4 * ch) * 4};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    return bld4(c.x, r.off + (uint32_t)(kb * BK * 3136 * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int nl, float v) {
     const int n = c.m0 + ml, k = c.n0 + nl;
@@ -786,7 +821,8 @@ struct ConvWgrad {
   using Args = BwdArgs;
   using Smem = NoSmem;
   struct Ctx {
-    int n0, split, kb0, kb1, nbb, xoff;  // xoff: (tap, ci) offset of this thread's B chunk column
+    int n0, split, kb0, kb1, nbb;
+    Rsrc dy, x;
   };
   static __host__ __device__ int kblocks(int B) { return P * ((B + BK - 1) / BK); }
   static __host__ __device__ int tiles(int, int splits) { return (N / BN) * splits; }
@@ -797,42 +833,27 @@ struct ConvWgrad {
     c.nbb = (a.B + BK - 1) / BK;
     c.kb0 = c.split * a.kbps;
     c.kb1 = min(c.kb0 + a.kbps, kblocks(a.B));
+    c.dy = make_rsrc(a.dy, (uint32_t)a.B * P * 64 * 4);
+    c.x = make_rsrc(a.x, (uint32_t)a.B * IH * IH * C * 4);
   }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + row;
-    if (b >= a.B) return zero4();
-    return ld4(a.dy + ((size_t)b * P + p) * 64 + 4 * ch);
+  // row states: the chunk's sample row within a 32-sample k-block (+ its channel chunk / its
+  // (tap, ci) column offset) as a byte offset; the k-block adds (sample block, position)
+  using RowA = BufRow;
+  using RowB = BufRow;
+  static __device__ RowA row_a(const Args&, const Ctx&, int row, int ch) {
+    return {(uint32_t)(row * P * 64 + 4 * ch) * 4};
   }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + row;
-    if (b >= a.B) return zero4();
-    const int oy = p / OH, ox = p - oy * OH;
-    const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
-    const float* x = static_cast<const float*>(a.x);
-    return ld4(x + ((size_t)b * IH * IH + (S * oy + ky) * IH + S * ox + kx) * C + ci);
-  }
-  // row states: the chunk's sample row within a 32-sample k-block and its (tap, ci) offset
-  struct RowA {
-    int row, ch4;
-  };
-  struct RowB {
-    int row, off;  // off = (ky * IH + kx) * C + ci of the chunk's column
-  };
-  static __device__ RowA row_a(const Args&, const Ctx&, int row, int ch) { return {row, 4 * ch}; }
-  static __device__ f32x4 load_a_row(const Args& a, const Ctx& c, const RowA& r, int kb) {
-    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + r.row;  // p, block base: wave-uniform
-    return b < a.B ? ld4(a.dy + ((size_t)b * P + p) * 64 + r.ch4) : zero4();
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
+    const int p = kb / c.nbb, bb = kb - p * c.nbb;  // wave-uniform
+    return bld4(c.dy, r.off + (uint32_t)((bb * BK * P + p) * 64 * 4));
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int row, int ch) {
     const int n = c.n0 + 4 * ch, tap = n / C, ci = n - tap * C, ky = tap / K, kx = tap - ky * K;
-    return {row, (ky * IH + kx) * C + ci};
+    return {(uint32_t)(row * IH * IH * C + (ky * IH + kx) * C + ci) * 4};
   }
-  static __device__ f32x4 load_b_row(const Args& a, const Ctx& c, const RowB& r, int kb) {
-    const int p = kb / c.nbb, b = (kb - p * c.nbb) * BK + r.row;
-    if (b >= a.B) return zero4();
-    const int oy = p / OH, ox = p - oy * OH;  // wave-uniform
-    const float* x = static_cast<const float*>(a.x);
-    return ld4(x + ((size_t)b * IH * IH + S * oy * IH + S * ox) * C + r.off);
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    const int p = kb / c.nbb, bb = kb - p * c.nbb, oy = p / OH, ox = p - oy * OH;  // wave-uniform
+    return bld4(c.x, r.off + (uint32_t)((bb * BK * IH * IH + S * oy * IH + S * ox) * C * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int m, int nl, float v) {
     a.out[((size_t)c.split * 64 + m) * N + c.n0 + nl] = v;
@@ -1035,6 +1056,7 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
   using Smem = NoSmem;
   struct Ctx {
     int b0, pos, iy, ix, ky0, kx0, nkx, n0, kb0, kb1;
+    Rsrc dy, w;
   };
   static __host__ __device__ int tiles(int B) { return 81 * NT * ((B + BM - 1) / BM); }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
@@ -1051,23 +1073,33 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
     c.nkx = min(2, c.ix) - c.kx0 + 1;
     c.kb0 = 0;
     c.kb1 = 2 * nky * c.nkx;
+    c.dy = make_rsrc(a.dy, (uint32_t)a.B * 49 * 64 * 4);
+    c.w = make_rsrc(a.w, 9 * 64 * 64 * 4);
   }
   static __device__ void tap_of(const Ctx& c, int kb, int& ky, int& kx) {
     const int ti = kb >> 1, r = ti / c.nkx;
     ky = c.ky0 + r;
     kx = c.kx0 + ti - r * c.nkx;
   }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int b = c.b0 + row;
-    if (b >= a.B) return zero4();
-    int ky, kx;
-    tap_of(c, kb, ky, kx);
-    return ld4(a.dy + ((size_t)b * 49 + (c.iy - ky) * 7 + c.ix - kx) * 64 + (kb & 1) * 32 + 4 * ch);
+  // row states: sample row b0 + row (past the batch: past the range) / weight row n; the
+  // k-block adds the tap's (wave-uniform) offset
+  using RowA = BufRow;
+  using RowB = BufRow;
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)((c.b0 + row) * 49 * 64 + 4 * ch) * 4};
   }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     int ky, kx;
     tap_of(c, kb, ky, kx);
-    return ld4(a.w + ((ky * 3 + kx) * 64 + c.n0 + n) * 64 + (kb & 1) * 32 + 4 * ch);
+    return bld4(c.dy, r.off + (uint32_t)((((c.iy - ky) * 7 + c.ix - kx) * 64 + (kb & 1) * 32) * 4));
+  }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) {
+    return {(uint32_t)((c.n0 + n) * 64 + 4 * ch) * 4};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    int ky, kx;
+    tap_of(c, kb, ky, kx);
+    return bld4(c.w, r.off + (uint32_t)(((ky * 3 + kx) * 64 * 64 + (kb & 1) * 32) * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int b = c.b0 + ml;
@@ -1088,6 +1120,7 @@ struct Conv2DgradP {
   using Smem = NoSmem;
   struct Ctx {
     int b0, cls, jy, jx, ty0, tx0, ntx, kb0, kb1;
+    Rsrc dy, w;
   };
   static __host__ __device__ int tiles(int B) { return 400 * ((B + BM - 1) / BM); }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
@@ -1104,24 +1137,30 @@ struct Conv2DgradP {
     c.ntx = (c.jx == 0 ? 0 : 1) - c.tx0 + 1;
     c.kb0 = 0;
     c.kb1 = 2 * nty * c.ntx;
+    c.dy = make_rsrc(a.dy, (uint32_t)a.B * 81 * 64 * 4);
+    c.w = make_rsrc(a.w, 16 * 32 * 64 * 4);
   }
   static __device__ void tap_of(const Ctx& c, int kb, int& ty, int& tx) {
     const int ti = kb >> 1, r = c.ntx == 2 ? ti >> 1 : ti;
     ty = c.ty0 + r;
     tx = c.tx0 + ti - r * c.ntx;
   }
-  static __device__ f32x4 load_a(const Args& a, const Ctx& c, const Smem&, int kb, int row, int ch) {
-    const int b = c.b0 + row;
-    if (b >= a.B) return zero4();
+  using RowA = BufRow;
+  using RowB = BufRow;
+  static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
+    return {(uint32_t)((c.b0 + row) * 81 * 64 + 4 * ch) * 4};
+  }
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     int ty, tx;
     tap_of(c, kb, ty, tx);
-    return ld4(a.dy + ((size_t)b * 81 + (c.jy - ty) * 9 + c.jx - tx) * 64 + (kb & 1) * 32 + 4 * ch);
+    return bld4(c.dy, r.off + (uint32_t)((((c.jy - ty) * 9 + c.jx - tx) * 64 + (kb & 1) * 32) * 4));
   }
-  static __device__ f32x4 load_b(const Args& a, const Ctx& c, const Smem&, int kb, int n, int ch) {
+  static __device__ RowB row_b(const Args&, const Ctx&, int n, int ch) { return {(uint32_t)(n * 64 + 4 * ch) * 4}; }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
     int ty, tx;
     tap_of(c, kb, ty, tx);
     const int ky = (c.cls >> 1) + 2 * ty, kx = (c.cls & 1) + 2 * tx;
-    return ld4(a.w + ((ky * 4 + kx) * 32 + n) * 64 + (kb & 1) * 32 + 4 * ch);
+    return bld4(c.w, r.off + (uint32_t)(((ky * 4 + kx) * 32 * 64 + (kb & 1) * 32) * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int b = c.b0 + ml;
@@ -1224,9 +1263,16 @@ int f32_fc1_wgrad_splits() { return kFc1WgSlices; }
 
 size_t f32_fc1_wgrad_workspace_floats() { return (size_t)kFc1WgSlices * 256 * 3136; }
 
+// the backward loaders address operands by 32-bit byte offsets (raw buffer resources)
+static void check_bwd_batch(int B) {
+  if ((int64_t)B * 400 * 32 * 4 + (int64_t)64 * 400 * 32 * 4 >= (int64_t)1 << 31)
+    throw std::invalid_argument("f32 backward: batch too large for 32-bit operand offsets");
+}
+
 void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
                        hipStream_t s) {
   if (B <= 0) return;
+  check_bwd_batch(B);
   BwdArgs d{};
   d.dy = dz;
   d.w = wfc1p;
@@ -1266,6 +1312,7 @@ size_t f32_wgrad_workspace_floats(int layer, int B) {
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
                   const float* mask, float* dx, float* ws, int B, hipStream_t s) {
   if (B <= 0) return;
+  check_bwd_batch(B);
   const SplitPlan p = wgrad_plan(layer, B);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
   BwdArgs g{};
