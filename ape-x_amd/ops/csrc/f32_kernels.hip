@@ -881,16 +881,23 @@ constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) /
 // forward above, applied to dy): the u8 frame operand is exact in bf16 and each dy value
 // splits exactly into hi + mid + lo bf16, so every product is exact and only the fp32
 // accumulation rounds (hi, mid and lo products in separate accumulators).
-// Same workgroup layout and partials as f32_conv1_wgrad_k (8 waves = 2 samples x 4 input
-// channels c; wave c owns columns kk = c*64 + (col >> 1)*8 + 4 (col & 1) + i of the 4 tiles
-// i, both co halves), but the reduction runs over PIXEL GROUPS of 8 on
-// v_mfma_f32_16x16x32_bf16: group g = (output row g / 3, columns 8 (g % 3) .. +7; the
-// third group of a row has 4 real pixels, dy = 0 on the 4 pad slots), 4 groups (lane q)
-// per k-step, 15 k-steps per sample.  Lane (col, q) reads the 8 consecutive plane dwords
-// (4oy + (col >> 1)) * 21 + ox0 + jj + (col & 1) once per k-step; tile i takes byte i of
-// each (kx & 3 == i), so the 4 B fragments share one set of LDS reads.
+// Workgroup = 8 waves = 2 samples x 4 input channels c; wave c owns columns
+// kk = c*64 + (col >> 1)*8 + 4 (col & 1) + i of the 4 tiles i, both co halves, and the
+// reduction runs over PIXEL GROUPS of 8 on v_mfma_f32_16x16x32_bf16: group g = (output row
+// g / 3, columns 8 (g % 3) .. +7; the third group of a row has 4 real pixels, dy = 0 on the 4
+// pad slots), 4 groups (lane q) per k-step, 15 k-steps per sample.  Lane (col, q) reads the
+// 8 consecutive plane dwords (4oy + (col >> 1)) * 21 + ox0 + jj + (col & 1) once per k-step;
+// tile i takes byte i of each (kx & 3 == i), so the 4 B fragments share one set of LDS reads.
+// The A fragments (dy of the k-step's 4 groups, both co halves, as hi / mid / lo bf16) are the
+// same for the sample's 4 channel waves: each wave splits ONE quarter (co half c >> 1, slots
+// 4 (c & 1) .. +3) into an LDS double buffer and all four read the whole set back (6 x 16 B
+// per lane), one workgroup barrier per k-step -- the split (~5 VALU per value) was 4x redundant
+// and bounded the kernel (9.7 VALU per MFMA, 15 % MFMA busy, round 3).  One workgroup per CU
+// either way (~180 VGPRs: 2 waves per SIMD), so the 82 KB of LDS cost no occupancy.
+constexpr int kC1wAf = 2 * 3 * 64;  // uint4 per (buffer, sample): [half][term][lane]
 __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + 16 + kConv1WgradDump];  // + pad: row-end groups
+  __shared__ uint4 af[2][kConv1WgradS][kC1wAf];  // split dy fragments, double-buffered over k-steps
   __shared__ int64_t wplanes[kConv1WgradS * 4];  // plane byte offsets from the frames base
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int col = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
@@ -920,93 +927,92 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
     }
     if (t < 16) pl[kConv1WgradS * 4 * kPlaneDw + t] = 0u;
   }
-  __syncthreads();
   // hi / mid / lo products in three accumulators: no MFMA waits on its predecessor's result
   f32x4 ah[2][4], am[2][4], al[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[h][i] = am[h][i] = al[h][i] = zero4();
-  float bs0 = 0.f, bs1 = 0.f;  // bias partials of co = col, 16 + col
-  if (sl < ns) {
-    const float* dy = a.dy + (size_t)(b0 + sl) * 400 * 32;
-    const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (col >> 1) * 21 + (col & 1);
-    // dy of k-step ks + 1 is loaded while ks computes (unconditional loads from clamped pixel
-    // slots, zeroed after): loaded at their use, guarded, each k-step waited out one global
-    // round trip -- 15 per sample
-    float n0[8], n1[8];
-    auto load_dy = [&](int ks) {
-      const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
-      const float* dp = dy + (oy * 20 + ox0) * 32 + col;
+  // this wave's quarter of every k-step's dy: co = 16 hq + col, slots j0 .. j0 + 3 of group g
+  const int hq = c >> 1, j0 = 4 * (c & 1);
+  const bool live = sl < ns;  // a missing second sample (odd batch tail): zero dy, barriers kept
+  const float* dy = a.dy + (size_t)(b0 + (live ? sl : 0)) * 400 * 32 + 16 * hq + col;
+  float bs = 0.f;  // bias partial of co = 16 hq + col over this wave's slots
+  float nv4[4];
+  auto load_dy = [&](int ks) {  // unconditional loads from clamped pixel slots, zeroed at use
+    const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
+    const float* dp = dy + (oy * 20 + ox0) * 32;
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int jc = min(jj, nv - 1);
-        n0[jj] = dp[jc * 32];
-        n1[jj] = dp[jc * 32 + 16];
-      }
-    };
-    load_dy(0);
-    for (int ks = 0; ks < 15; ++ks) {
-      const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy);
-      const int nv = min(8, 20 - ox0);  // real pixels in this group (8 or 4)
-      // A: dy[pixel][co] for the group's 8 slots, both co halves, split into 3 bf16 terms
-      float d0[8], d1[8];
+    for (int j = 0; j < 4; ++j) nv4[j] = dp[min(j0 + j, nv - 1) * 32];
+  };
+  auto split_store = [&](int ks, int buf) {
+    const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
+    float d[4];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        d0[jj] = jj < nv ? n0[jj] : 0.f;
-        d1[jj] = jj < nv ? n1[jj] : 0.f;
-        bs0 += d0[jj];
-        bs1 += d1[jj];
+    for (int j = 0; j < 4; ++j) {
+      d[j] = (live && j0 + j < nv) ? nv4[j] : 0.f;
+      bs += d[j];
+    }
+    uint32_t hw[2], mw[2], lw[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float x = d[2 * j], y = d[2 * j + 1];
+      const float xh = trunc_bf16(x), yh = trunc_bf16(y);
+      const float xr = x - xh, yr = y - yh;
+      const float xm = trunc_bf16(xr), ym = trunc_bf16(yr);
+      hw[j] = pack_bf16_hi(xh, yh);
+      mw[j] = pack_bf16_hi(xm, ym);
+      lw[j] = pack_bf16_hi(xr - xm, yr - ym);
+    }
+    uint32_t* base = reinterpret_cast<uint32_t*>(&af[buf][sl][hq * 3 * 64 + lane]) + (c & 1) * 2;
+    *reinterpret_cast<uint2*>(base) = make_uint2(hw[0], hw[1]);
+    *reinterpret_cast<uint2*>(base + 64 * 4) = make_uint2(mw[0], mw[1]);
+    *reinterpret_cast<uint2*>(base + 2 * 64 * 4) = make_uint2(lw[0], lw[1]);
+  };
+  const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (col >> 1) * 21 + (col & 1);
+  load_dy(0);
+  split_store(0, 0);
+  __syncthreads();  // the planes and the first k-step's fragments are staged
+  for (int ks = 0; ks < 15; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < 15) load_dy(ks + 1);  // in flight under this k-step's MFMAs
+    const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy);
+    bfx8 A[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) A[h][k] = __builtin_bit_cast(bfx8, af[cur][sl][(h * 3 + k) * 64 + lane]);
+    // B: 8 plane dwords (pixels ox0 + jj of row 4 oy + ky), byte i -> tile i
+    const uint32_t* px = pc + 4 * oy * 21 + ox0;
+    uint32_t wv[8];
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) wv[jj] = px[jj];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      uint32_t bw[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 lo = u8x4(wv[2 * j]), hi = u8x4(wv[2 * j + 1]);
+        bw[j] = pack_bf16_hi(lo[i], hi[i]);
       }
-      if (ks + 1 < 15) load_dy(ks + 1);
-      bfx8 A[2][3];
+      const bfx8 Bf = __builtin_bit_cast(bfx8, make_uint4(bw[0], bw[1], bw[2], bw[3]));
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float* d = h ? d1 : d0;
-        uint32_t hw[4], mw[4], lw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float x = d[2 * j], y = d[2 * j + 1];
-          const float xh = trunc_bf16(x), yh = trunc_bf16(y);
-          const float xr = x - xh, yr = y - yh;
-          const float xm = trunc_bf16(xr), ym = trunc_bf16(yr);
-          hw[j] = pack_bf16_hi(xh, yh);
-          mw[j] = pack_bf16_hi(xm, ym);
-          lw[j] = pack_bf16_hi(xr - xm, yr - ym);
-        }
-        A[h][0] = __builtin_bit_cast(bfx8, make_uint4(hw[0], hw[1], hw[2], hw[3]));
-        A[h][1] = __builtin_bit_cast(bfx8, make_uint4(mw[0], mw[1], mw[2], mw[3]));
-        A[h][2] = __builtin_bit_cast(bfx8, make_uint4(lw[0], lw[1], lw[2], lw[3]));
-      }
-      // B: 8 plane dwords (pixels ox0 + jj of row 4 oy + ky), byte i -> tile i
-      const uint32_t* px = pc + 4 * oy * 21 + ox0;
-      uint32_t wv[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) wv[jj] = px[jj];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint32_t bw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 lo = u8x4(wv[2 * j]), hi = u8x4(wv[2 * j + 1]);
-          bw[j] = pack_bf16_hi(lo[i], hi[i]);
-        }
-        const bfx8 Bf = __builtin_bit_cast(bfx8, make_uint4(bw[0], bw[1], bw[2], bw[3]));
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          ah[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][0], Bf, ah[h][i], 0, 0, 0);
-          am[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][1], Bf, am[h][i], 0, 0, 0);
-          al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][2], Bf, al[h][i], 0, 0, 0);
-        }
+        ah[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][0], Bf, ah[h][i], 0, 0, 0);
+        am[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][1], Bf, am[h][i], 0, 0, 0);
+        al[h][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[h][2], Bf, al[h][i], 0, 0, 0);
       }
     }
+    if (ks + 1 < 15) split_store(ks + 1, cur ^ 1);  // the buffer read at ks - 1 (barrier below)
+    __syncthreads();
   }
-  bs0 += __shfl_xor(bs0, 16, 64);
-  bs0 += __shfl_xor(bs0, 32, 64);
-  bs1 += __shfl_xor(bs1, 16, 64);
-  bs1 += __shfl_xor(bs1, 32, 64);
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2][32]
+  // bias partials: co = 16 hq + col summed over the wave's 4 groups q, then the two waves
+  // (c & 1) of the half and the two samples through LDS (fixed order)
+  bs += __shfl_xor(bs, 16, 64);
+  bs += __shfl_xor(bs, 32, 64);
+  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2 samples][4 waves][16]
+  float* bred = red + 4 * 32 * 64;
+  if (q == 0) bred[(sl * 4 + c) * 16 + col] = bs;
   if (sl == 1) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
@@ -1015,10 +1021,6 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] = ah[h][i][e] + (am[h][i][e] + al[h][i][e]);
-    if (c == 0 && q == 0) {
-      red[4 * 32 * 64 + col] = bs0;
-      red[4 * 32 * 64 + 16 + col] = bs1;
-    }
   }
   __syncthreads();
   if (sl == 0) {
@@ -1033,9 +1035,12 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
           const int co = h * 16 + 4 * q + e, kk = c * 64 + (col >> 1) * 8 + 4 * (col & 1) + i;
           out[co * 256 + kk] = v;
         }
-    if (c == 0 && q == 0) {
-      a.out2[blockIdx.x * 32 + col] = bs0 + red[4 * 32 * 64 + col];
-      a.out2[blockIdx.x * 32 + 16 + col] = bs1 + red[4 * 32 * 64 + 16 + col];
+    if (t < 32) {  // co = t: half t >> 4, waves 2 (t >> 4) and +1 of both samples
+      const int h = t >> 4, cc = t & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) v += bred[(s2 * 4 + 2 * h) * 16 + cc] + bred[(s2 * 4 + 2 * h + 1) * 16 + cc];
+      a.out2[blockIdx.x * 32 + t] = v;
     }
   }
 }
