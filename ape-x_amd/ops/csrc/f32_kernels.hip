@@ -1188,12 +1188,13 @@ SplitPlan plan_splits(int kbt, int ntiles, int target_blocks) {
   return {s, kbps};
 }
 
-// conv2 / conv3 weight gradient: ~one workgroup per CU over (64-wide n-tiles x batch splits)
-SplitPlan wgrad_plan(int layer, int B) {
+// conv2 / conv3 weight gradient: ~`target` workgroups over (64-wide n-tiles x batch splits);
+// target <= 0: the default (~one per CU)
+SplitPlan wgrad_plan(int layer, int B, int target) {
   switch (layer) {
     case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_x3_k workgroups
-    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / 64, 256);
-    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / 64, 252);
+    case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / 64, target > 0 ? target : 256);
+    case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / 64, target > 0 ? target : 252);
     default: throw std::invalid_argument("f32 wgrad layer");
   }
 }
@@ -1302,12 +1303,12 @@ int f32_fc1_wgrad_slices(int B) {
   return (nkb + kbps - 1) / kbps;
 }
 
-int f32_wgrad_splits(int layer, int B) { return wgrad_plan(layer, B).splits; }
+int f32_wgrad_splits(int layer, int B, int target) { return wgrad_plan(layer, B, target).splits; }
 
-int f32_wgrad_kbps(int layer, int B) { return wgrad_plan(layer, B).kbps; }
+int f32_wgrad_kbps(int layer, int B, int target) { return wgrad_plan(layer, B, target).kbps; }
 
-size_t f32_wgrad_workspace_floats(int layer, int B) {
-  const SplitPlan p = wgrad_plan(layer, B);
+size_t f32_wgrad_workspace_floats(int layer, int B, int target) {
+  const SplitPlan p = wgrad_plan(layer, B, target);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
   const size_t cout = layer == 1 ? 32 : 64;
   return (size_t)p.splits * (per + cout);
@@ -1315,10 +1316,10 @@ size_t f32_wgrad_workspace_floats(int layer, int B) {
 
 // wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s) {
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target) {
   if (B <= 0) return;
   check_bwd_batch(B);
-  const SplitPlan p = wgrad_plan(layer, B);
+  const SplitPlan p = wgrad_plan(layer, B, target);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
   BwdArgs g{};
   g.x = x;
@@ -1351,8 +1352,8 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   }
 }
 
-FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad) {
-  const SplitPlan p = wgrad_plan(layer, B);
+FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad, int target) {
+  const SplitPlan p = wgrad_plan(layer, B, target);
   FinalizeJob j{};
   j.kind = 0;
   j.G = p.splits;

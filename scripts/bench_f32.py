@@ -23,6 +23,8 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
+                                                    "targets, e.g. 512,1024 (default plan: the plain cases)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -89,6 +91,14 @@ cases = {
     "conv1_wgrad": (lambda: hip.f32_conv_bwd(1, frames.data_ptr(), ids.data_ptr(), idx.data_ptr(), ws.dy1.data_ptr(),
                                              0, 0, 0, w1.data_ptr(), B, S()), 2 * B * 400 * 32 * 256),
 }
+for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
+    for L, xin, dyin, wt, dx in ((3, "a2", "dy3", net.w3t, "dy2"), (2, "a1", "dy2", net.w2t, "dy1")):
+        wsx = torch.empty(hip.f32_wgrad_workspace_floats(L, B, tg), dtype=torch.float32, device=dev)
+        flop = 2 * 2 * B * (49 * 64 * 576 if L == 3 else 81 * 64 * 512)
+        cases[f"conv{L}_bwd@{tg}"] = (
+            (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tg=tg: hip.f32_conv_bwd(
+                L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
+                getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), target=tg)), flop)
 res = {}
 runs = [(name, fn, flop) for name, (fn, flop) in cases.items() if not a.only or a.only in name]
 for name, fn, flop in runs:
