@@ -368,6 +368,7 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
   struct Ctx {
     F32Prob p;
     int M, m0, n0, kb0, kb1;
+    Rsrc in, w;
   };
   static constexpr int NT = 64 / BN;
   static __host__ __device__ int tiles(int B) { return NT * ((B * 81 + BM - 1) / BM); }
@@ -380,6 +381,8 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
     c.n0 = (t % NT) * BN;
     c.kb0 = 0;
     c.kb1 = 512 / BK;
+    c.in = make_rsrc(c.p.in, (uint32_t)a.B * 400 * 32 * 4);
+    c.w = make_rsrc(c.p.w, 64 * 512 * 4);
   }
   static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int m = c.m0 + row;
@@ -393,26 +396,26 @@ struct Conv2FwdT {  // a2 = relu(conv(a1, W2) + b2); k = (ky, kx, ci) = tap * 32
     return ld4(c.p.w + (c.n0 + n) * 512 + kb * BK + 4 * ch);
   }
   // row states (32 % BK == 0: a k-block lies inside one tap; 4*ch is the chunk's channel
-  // offset within the block, the block's tap / channel base is wave-uniform)
-  struct RowA {
-    const float* p;  // sample / window origin + channel chunk; nullptr past the last row
-  };
-  struct RowB {
-    const float* p;
-  };
+  // offset within the block, the block's tap / channel base is wave-uniform): byte offsets into
+  // raw buffers -- rows past the last sample lie past the range and load zeros
+  using RowA = BufRow;
+  using RowB = BufRow;
   static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
     static_assert(32 % BK == 0, "a k-block inside one tap");
     const int m = c.m0 + row;
-    if (m >= c.M) return {nullptr};
     const int b = m / 81, p = m - b * 81, oy = p / 9, ox = p - oy * 9;
-    return {static_cast<const float*>(c.p.in) + ((size_t)b * 400 + 2 * oy * 20 + 2 * ox) * 32 + 4 * ch};
+    return {(uint32_t)(((b * 400 + 2 * oy * 20 + 2 * ox) * 32 + 4 * ch) * 4)};
   }
-  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     const int k0 = kb * BK, tap = k0 >> 5, ky = tap >> 2, kx = tap & 3;  // wave-uniform
-    return r.p ? ld4(r.p + (ky * 20 + kx) * 32 + (k0 & 31)) : zero4();
+    return bld4(c.in, r.off + (uint32_t)(((ky * 20 + kx) * 32 + (k0 & 31)) * 4));
   }
-  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 512 + 4 * ch}; }
-  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) {
+    return {(uint32_t)(((c.n0 + n) * 512 + 4 * ch) * 4)};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    return bld4(c.w, r.off + (uint32_t)(kb * BK * 4));
+  }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -429,6 +432,7 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
   struct Ctx {
     F32Prob p;
     int M, m0, n0, kb0, kb1;
+    Rsrc in, w;
   };
   static constexpr int NT = 64 / BN;
   static __host__ __device__ int tiles(int B) { return NT * ((B * 49 + BM - 1) / BM); }
@@ -441,6 +445,8 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
     c.n0 = (t % NT) * BN;
     c.kb0 = 0;
     c.kb1 = 576 / BK;
+    c.in = make_rsrc(c.p.in, (uint32_t)a.B * 81 * 64 * 4);
+    c.w = make_rsrc(c.p.w, 64 * 576 * 4);
   }
   static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int m = c.m0 + row;
@@ -453,26 +459,26 @@ struct Conv3FwdT {  // a3 = relu(conv(a2, W3) + b3); k = tap * 64 + ci; w = w3p
   static __device__ f32x4 load_b(const Args&, const Ctx& c, const Smem&, int kb, int n, int ch) {
     return ld4(c.p.w + (c.n0 + n) * 576 + kb * BK + 4 * ch);
   }
-  // row states (64 % BK == 0: a k-block lies inside one tap of 64 channels, chunk 4*ch)
-  struct RowA {
-    const float* p;
-  };
-  struct RowB {
-    const float* p;
-  };
+  // row states (64 % BK == 0: a k-block lies inside one tap of 64 channels, chunk 4*ch): byte
+  // offsets into raw buffers (rows past the last sample: past the range, zeros)
+  using RowA = BufRow;
+  using RowB = BufRow;
   static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
     static_assert(64 % BK == 0, "a k-block inside one tap");
     const int m = c.m0 + row;
-    if (m >= c.M) return {nullptr};
     const int b = m / 49, p = m - b * 49, oy = p / 7, ox = p - oy * 7;
-    return {static_cast<const float*>(c.p.in) + ((size_t)b * 81 + oy * 9 + ox) * 64 + 4 * ch};
+    return {(uint32_t)(((b * 81 + oy * 9 + ox) * 64 + 4 * ch) * 4)};
   }
-  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     const int k0 = kb * BK, tap = k0 >> 6, ky = tap / 3, kx = tap - ky * 3;  // wave-uniform
-    return r.p ? ld4(r.p + (ky * 9 + kx) * 64 + (k0 & 63)) : zero4();
+    return bld4(c.in, r.off + (uint32_t)(((ky * 9 + kx) * 64 + (k0 & 63)) * 4));
   }
-  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) { return {c.p.w + (c.n0 + n) * 576 + 4 * ch}; }
-  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) {
+    return {(uint32_t)(((c.n0 + n) * 576 + 4 * ch) * 4)};
+  }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    return bld4(c.w, r.off + (uint32_t)(kb * BK * 4));
+  }
   static __device__ void store(const Args&, const Ctx& c, int ml, int n, float v) {
     const int m = c.m0 + ml;
     if (m < c.M) c.p.out[(size_t)m * 64 + c.n0 + n] = fmaxf(v + c.p.bias[c.n0 + n], 0.f);
@@ -492,6 +498,7 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
   struct Ctx {
     F32Prob p;
     int B, m0, n0, split, kb0, kb1;
+    Rsrc in, w;
   };
   static __host__ __device__ int tiles(int B) { return ((B + BM - 1) / BM) * NT * kFcSplits; }
   static __device__ void decode(const Args& a, int block, Ctx& c, Smem&) {
@@ -505,6 +512,8 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
     c.m0 = (t / kFcSplits) * BM;
     c.kb0 = c.split * KBS;
     c.kb1 = c.kb0 + KBS;
+    c.in = make_rsrc(c.p.in, (uint32_t)a.B * 3136 * 4);
+    c.w = make_rsrc(c.p.w, 256 * 3136 * 4);
   }
   static __device__ f32x4 load_a(const Args&, const Ctx& c, const Smem&, int kb, int row, int ch) {
     const int b = c.m0 + row;
@@ -518,24 +527,21 @@ struct Fc1FwdT {  // z[s][b][n] = sum_{k' in split s} a3[b][k'] wfc1p[n][k'], k'
     const int b = c.m0 + ml;
     if (b < c.B) c.p.out[((size_t)c.split * c.B + b) * 256 + c.n0 + nl] = v;
   }
-  // row states: the chunk's row base pointers (k-invariant)
-  struct RowA {
-    const float* p;
-  };
-  struct RowB {
-    const float* p;
-  };
+  // row states: the chunk's k-invariant byte offsets (rows past the batch: past the range, zeros)
+  using RowA = BufRow;
+  using RowB = BufRow;
   static __device__ RowA row_a(const Args&, const Ctx& c, int row, int ch) {
-    const int b = c.m0 + row;
-    return {b < c.B ? static_cast<const float*>(c.p.in) + (size_t)b * 3136 + 4 * ch : nullptr};
+    return {(uint32_t)(((c.m0 + row) * 3136 + 4 * ch) * 4)};
   }
-  static __device__ f32x4 load_a_row(const Args&, const Ctx&, const RowA& r, int kb) {
-    return r.p ? ld4(r.p + kb * BK) : zero4();
+  static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
+    return bld4(c.in, r.off + (uint32_t)(kb * BK * 4));
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int nl, int ch) {
-    return {c.p.w + (size_t)(c.n0 + nl) * 3136 + 4 * ch};
+    return {(uint32_t)(((c.n0 + nl) * 3136 + 4 * ch) * 4)};
   }
-  static __device__ f32x4 load_b_row(const Args&, const Ctx&, const RowB& r, int kb) { return ld4(r.p + kb * BK); }
+  static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
+    return bld4(c.w, r.off + (uint32_t)(kb * BK * 4));
+  }
 };
 
 constexpr int kPlaneDw = kPlane / 4;  // 1764 dwords per plane
@@ -1216,6 +1222,8 @@ void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, i
 void check_set(const F32Set& set) {
   if (set.n < 1 || set.n > kMaxProbs) throw std::invalid_argument("f32: 1..3 problems");
   if (set.B <= 0) throw std::invalid_argument("f32: B must be positive");
+  if ((int64_t)(set.B + 128) * 400 * 32 * 4 >= (int64_t)1 << 31)  // 32-bit operand byte offsets (raw buffers)
+    throw std::invalid_argument("f32: batch too large for 32-bit operand offsets");
 }
 
 template <class P>

@@ -16,5 +16,7 @@ done
 grep fused_step $O/micro.log | cut -c1-120
 timeout -k 10 300 python -u bench.py --algo aql --steps 500 --warmup 20 > $O/bench.log 2>&1 || exit $?
 grep '^{' $O/bench.log | cut -c1-400
+timeout -k 10 300 python -u bench.py --algo aql --steps 500 --warmup 20 --aql-overlap > $O/bench_overlap.log 2>&1 || exit $?
+grep -o '"value": [0-9.]*' $O/bench_overlap.log
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run \
    -- python3 $R/bench.py --algo aql --steps 100 --warmup 10 > $O/prof.log 2>&1
