@@ -312,18 +312,23 @@ class AQLLearner:
                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                        if split else None)
         self.post_levels = h.aql_post_set_levels(self.post, r.tree, r.wlist.data_ptr(), B) if split else None
-        self.S = None
+        self.S = self.S_draw = None
         if cfg.fused_step and not cfg.fork_tree and B <= 64:
             self.bar = torch.zeros(4, dtype=torch.int32, device=dev)  # arrivals, generation, error flag
-            self.step_desc = torch.zeros(h.aql_step_nbytes(), dtype=torch.uint8, device=dev)
-            self.S = h.make_aql_step(
-                self.L, self.G, self.post, r.tree, self.hp,
-                dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
-                     norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
-                     bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
-                     loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
-                     max_prio=r.max_prio.data_ptr(), alpha=r.alpha),
-                self.step_desc.data_ptr())
+            nb = h.aql_step_nbytes()
+            self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
+            kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
+                      norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
+                      bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
+                      loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
+                      max_prio=r.max_prio.data_ptr(), alpha=r.alpha)
+            self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
+            if self.Ls is not None:  # + the next step's draw (the stream of the forward's fused sampling)
+                self.S_draw = h.make_aql_step(
+                    self.L, self.G, self.post, r.tree, self.hp,
+                    dict(kw, draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=replay.seed ^ 0x51A7,
+                         exclude_last=0 if cfg.exact_mass else 1),
+                    self.step_desc[1].data_ptr())
         self.refresh()
 
     def refresh(self) -> None:
@@ -382,10 +387,18 @@ class AQLLearner:
             torch.cuda.current_stream().wait_stream(self.tree_stream)
             self._tree_pending = False
 
-    def step(self) -> None:
+    def step(self, drawn: bool = False, draw_next: bool = False) -> None:
+        """One SGD step.  ``drawn``: this step's rows were sampled by the previous step's fused
+        tail (``draw_next`` there) -- the forward skips its tree descent; both need the fused
+        step tail and fused sampling (:meth:`AQLEngine.learn_steps` pairs them within an
+        iteration)."""
         self.join()  # the sampler reads the tree the previous step's forked write updated
         h, r, s = self.hip, self.replay, self._s()
-        if self.Ls is not None:  # the forward samples its own rows (one launch fewer)
+        if drawn or draw_next:
+            assert self.S_draw is not None, "pre-drawn rows need the fused step tail and fused sampling"
+        if drawn:
+            h.aql_learn_fwd(self.L, s)
+        elif self.Ls is not None:  # the forward samples its own rows (one launch fewer)
             h.aql_learn_fwd(self.Ls, s)
         else:
             excl = 0 if self.cfg.exact_mass else 1
@@ -393,7 +406,7 @@ class AQLLearner:
                          self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
             h.aql_learn_fwd(self.L, s)
         if self.S is not None:  # backward, priority write, gradients, optimizers, noise: one launch
-            h.aql_step_tail(self.S, s)
+            h.aql_step_tail(self.S_draw if draw_next else self.S, s)
             self._track_losses()
             return
         h.aql_learn_bwd(self.L, s)
@@ -619,8 +632,11 @@ class AQLEngine:
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, 0, 0, s)
 
     def learn_steps(self) -> None:
-        for _ in range(self.K):
-            self.learner.step()
+        """The iteration's K SGD steps; with the fused tail, each step but the last also draws the
+        next step's rows (nothing inserts between them), so only the first forward samples."""
+        pre = self.learner.S_draw is not None
+        for k in range(self.K):
+            self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K)
         self.learner.join()  # (a captured graph must end joined)
 
     def fill(self, threshold: int | None = None) -> None:

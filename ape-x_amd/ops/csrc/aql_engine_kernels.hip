@@ -717,7 +717,7 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
 
 // ------------------------------------------------------------------ fused step tail
 // aql_step_tail_k: everything of one learner step after the candidate forward, in ONE launch
-// of grid = max(gradient blocks, B + 1) + 1 workgroups, all co-resident (the launcher checks
+// of grid = max(gradient blocks, B + 1) + 1 + 8 workgroups, all co-resident (the launcher checks
 // the occupancy), in three phases separated by grid barriers (grid_sync.h):
 //
 //   A  blocks [0, B): the per-sample backward (aql_bwd_block)
@@ -731,6 +731,8 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
 //                     reset (the thread owning a sigma element also updates its mu partner,
 //                     then draws the new epsilon and writes mu + sigma eps), the proposal
 //                     hard copy online -> target; the last block bumps the step counter
+//      8 blocks before the last (AqlStep::draw): the NEXT step's PER draw, so that forward
+//                     skips its tree descent (the tree is final after phase A)
 //
 // Same arithmetic as the separate launches (aql_learn_bwd_k, aql_grad_k, opt_step2_k,
 // aql_post_k): the gradient partials keep aql_grad_k's block layout, so the clip norms and
@@ -777,6 +779,8 @@ __device__ __forceinline__ void step_tree_block(const AqlStep& D) {
   batch_leaves_block(D.tree, w, 1, tred, sids);
 }
 
+constexpr int kStepDrawBlocks = 8;  // phase C workgroups of the next step's draw (4 waves each)
+
 __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
   const AqlStep& D = *Dp;
   const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
@@ -785,7 +789,7 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
   // ---- phase A
   if (bid < B) {
     aql_bwd_block(D.L, bid);
-  } else if (bid == G - 1) {
+  } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
     step_tree_block(D);
   } else {
     const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
@@ -853,6 +857,22 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
           z.beps[e] = ep;
           z.beff[e] = fmaf(pn, ep, mun);
         }
+      }
+    }
+  }
+  const int d0 = G - 1 - kStepDrawBlocks;
+  if (D.draw && bid >= d0 && bid < G - 1) {  // block-uniform: the next step's rows, one wave per sample
+    const int lane = t & 63;
+    const TreeDesc& tr = D.tree;
+    const int64_t f = D.filled[0];
+    const int length = (int)(f < (int64_t)tr.size[0] ? f : (int64_t)tr.size[0]);
+    const float pmin = tr.node_min[tr.levels - 1][0], beta = D.beta[0];
+    for (int b = (bid - d0) * 4 + (t >> 6); b < B; b += 4 * kStepDrawBlocks) {  // wave-uniform
+      float pr;
+      const int node = tree_sample_leaf(tr, b, B, length, D.exclude_last, D.seed, st + 1, lane, &pr);
+      if (lane == 0) {  // (as aql_learn_fwd_k's fused draw writes them)
+        const_cast<int*>(D.L.idx)[b] = node;
+        const_cast<float*>(D.L.w)[b] = (pr > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(pr / pmin, -beta) : 1.f;
       }
     }
   }
@@ -1110,7 +1130,7 @@ void aql_post(const AqlPost& p, int regen, hipStream_t s) {
   LAUNCH_CHECK();
 }
 
-int aql_step_grid(const AqlStep& d) { return std::max(d.nblk, d.L.B + 1) + 1; }
+int aql_step_grid(const AqlStep& d) { return std::max(d.nblk, d.L.B + 1) + 1 + kStepDrawBlocks; }
 
 void aql_step_check(const AqlStep& d) {
   check_net(d.L.on);
@@ -1124,6 +1144,8 @@ void aql_step_check(const AqlStep& d) {
     throw std::invalid_argument("aql_step: barrier / counter / proposal copy");
   if (!d.bw.idx || d.bw.B != d.L.B || d.bw.E != 0 || !d.bw.owner || !d.bw.list || !d.bw.max_prio)
     throw std::invalid_argument("aql_step: priority write");
+  if (d.draw && (!d.filled || !d.beta || !d.L.idx || !d.L.w))
+    throw std::invalid_argument("aql_step: the next step's draw needs filled / beta / idx / w");
   for (int k = 0; k < 2; ++k) {
     const int64_t nw = (int64_t)d.P.layer[k].out * d.P.layer[k].in, nb = d.P.layer[k].out;
     for (int64_t o : {d.mu_w[k], d.sig_w[k]})

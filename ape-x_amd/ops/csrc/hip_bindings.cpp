@@ -752,6 +752,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     w.max_prio = P<float>(g("max_prio"));
     w.alpha = p["alpha"].cast<float>();
     d.bw = w;
+    if (p.contains("draw") && p["draw"].cast<int>()) {  // + the next step's PER draw (same stream as
+      d.draw = 1;                                       // aql_learn_set_sample's)
+      d.filled = P<const int64_t>(g("filled"));
+      d.beta = P<const float>(g("beta"));
+      d.seed = g("seed");
+      d.exclude_last = p["exclude_last"].cast<int>();
+    }
     aql_step_check(d);
     HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));
     return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), aql_step_grid(d)};

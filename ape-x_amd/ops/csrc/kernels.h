@@ -529,6 +529,15 @@ struct AqlStep {
   unsigned* bar;           // [2] grid barrier (arrivals, generation), zero-initialised
   int* err;                // set if a barrier wait timed out (grid not co-resident)
   int nblk;                // gradient workgroups (aql_grad_blocks(n))
+  // the NEXT step's PER draw (draw = 1): in phase C the draw workgroups sample step st + 1's
+  // rows into L.idx / L.w -- what the next forward's fused sampling would draw (same tree,
+  // counter, mass, beta) -- and that forward runs on the plain descriptor, without its descent.
+  // An iteration's last step does not draw (the actors insert before the next one).
+  int draw;
+  const int64_t* filled;
+  const float* beta;
+  uint64_t seed;
+  int exclude_last;
 };
 int aql_step_grid(const AqlStep& d);
 void aql_step_check(const AqlStep& d);  // shapes, pointers, and that the grid fits co-resident

@@ -25,19 +25,23 @@ def main():
     L = eng.learner
     L.step()
     torch.cuda.synchronize()
+    pre = L.S_draw is not None  # the engine's schedule: each step draws the next one's rows
+
+    def steps():
+        for k in range(a.iters):
+            L.step(drawn=pre and k > 0, draw_next=pre and k + 1 < a.iters)
+
     if a.graph:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(a.iters):
-                L.step()
+            steps()
         g.replay()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g.replay()
     else:
         t0 = time.perf_counter()
-        for _ in range(a.iters):
-            L.step()
+        steps()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print(f"fused_step={a.fused_step} {a.iters} learner steps: {1e6 * dt / a.iters:.1f} us/step", L.stats())
