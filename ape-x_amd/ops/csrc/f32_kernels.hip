@@ -1241,19 +1241,26 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
+// tile: 0 = the measured default (below); 1 = 128 x 64 tiles, BK 16 (4 waves of 64 x 32: every B
+// fragment read feeds two MFMAs), 2 = 128 x 64, BK 32 -- per-call variants for the microbench
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int tile) {
   check_set(set);
+  if (tile < 0 || tile > 2) throw std::invalid_argument("f32_conv_fwd_multi: tile 0..2");
   switch (layer) {
     case 1:
       f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
     case 2:
-      if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      if (tile == 1) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
+      else if (tile == 2) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:
-      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      if (tile == 1) fwd_launch<Conv3FwdT<128, 64, 16, 2>>(set, s);
+      else if (tile == 2) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");

@@ -25,6 +25,7 @@ ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
+ap.add_argument("--fwd-tiles", default="", help="extra conv2/conv3 forward cases at these tile variants (1, 2)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -99,6 +100,16 @@ for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
             (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tg=tg: hip.f32_conv_bwd(
                 L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
                 getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), target=tg)), flop)
+mismatch = set()
+for tv in [int(x) for x in a.fwd_tiles.split(",") if x]:  # same k order: bit-identical to the default tiles
+    for L in (2, 3):
+        hip.f32_conv_fwd_multi(L, set3(L), B, S())
+        ref = [(w.a2 if L == 2 else w.a3).clone() for w in wss]
+        hip.f32_conv_fwd_multi(L, set3(L), B, S(), tile=tv)
+        if not all(torch.equal(r, (w.a2 if L == 2 else w.a3)) for r, w in zip(ref, wss)):
+            mismatch.add(f"conv{L}_fwd@t{tv}")
+    cases[f"conv2_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=tv)), 2 * P * 81 * 64 * 512)
+    cases[f"conv3_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=tv)), 2 * P * 49 * 64 * 576)
 res = {}
 runs = [(name, fn, flop) for name, (fn, flop) in cases.items() if not a.only or a.only in name]
 for name, fn, flop in runs:
@@ -124,7 +135,8 @@ for name, fn, flop in runs:
     us = 1000.0 * e0.elapsed_time(e1) / a.iters
     res[name] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1), "pct_peak": round(flop / us / 1e6 / 1.573, 1)}
     if not a.json:
-        print(f"{name:12s} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)")
+        mm = " MISMATCH" if name in mismatch else ""
+        print(f"{name:12s}{mm} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)")
 if a.json:
     print(json.dumps(res))
 tot = sum(r["us"] for r in res.values())
