@@ -1057,9 +1057,10 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 // the conv3 dgrad MFMA work (21 of 27 (ky, iy) pairs in range per axis) and 19% of conv2's.
 // BM x BN tiles of (samples at one input position) x (input channels): 128 x 32 (two n-tiles;
 // 64 x 64 with each dy3 row staged once measured no better)
-template <int BM_, int BN_, int WM_>
+template <int BM_, int BN_, int WM_, int BK_ = 32>
 struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b][pi - tap][co] w3t[tap][ci][co]
-  static constexpr int BM = BM_, BN = BN_, BK = 32, WM = WM_;
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_;
+  static constexpr int KPT = 64 / BK;  // k-blocks per tap (64 output channels)
   static constexpr int NT = 64 / BN;
   static_assert(NT * BN == 64, "n-tiles cover the 64 input channels");
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
@@ -1083,12 +1084,12 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
     const int nky = min(2, c.iy) - c.ky0 + 1;
     c.nkx = min(2, c.ix) - c.kx0 + 1;
     c.kb0 = 0;
-    c.kb1 = 2 * nky * c.nkx;
+    c.kb1 = KPT * nky * c.nkx;
     c.dy = make_rsrc(a.dy, (uint32_t)a.B * 49 * 64 * 4);
     c.w = make_rsrc(a.w, 9 * 64 * 64 * 4);
   }
   static __device__ void tap_of(const Ctx& c, int kb, int& ky, int& kx) {
-    const int ti = kb >> 1, r = ti / c.nkx;
+    const int ti = kb / KPT, r = ti / c.nkx;
     ky = c.ky0 + r;
     kx = c.kx0 + ti - r * c.nkx;
   }
@@ -1102,7 +1103,7 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
   static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     int ky, kx;
     tap_of(c, kb, ky, kx);
-    return bld4(c.dy, r.off + (uint32_t)((((c.iy - ky) * 7 + c.ix - kx) * 64 + (kb & 1) * 32) * 4));
+    return bld4(c.dy, r.off + (uint32_t)((((c.iy - ky) * 7 + c.ix - kx) * 64 + (kb % KPT) * BK) * 4));
   }
   static __device__ RowB row_b(const Args&, const Ctx& c, int n, int ch) {
     return {(uint32_t)((c.n0 + n) * 64 + 4 * ch) * 4};
@@ -1110,7 +1111,7 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
   static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
     int ky, kx;
     tap_of(c, kb, ky, kx);
-    return bld4(c.w, r.off + (uint32_t)(((ky * 3 + kx) * 64 * 64 + (kb & 1) * 32) * 4));
+    return bld4(c.w, r.off + (uint32_t)(((ky * 3 + kx) * 64 * 64 + (kb % KPT) * BK) * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int b = c.b0 + ml;
@@ -1121,11 +1122,14 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
 };
 
 using Conv3DgradP = Conv3DgradPT<128, 32, 4>;
+using Conv3DgradP16 = Conv3DgradPT<128, 32, 4, 16>;
 
 // conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
 // output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
-struct Conv2DgradP {
-  static constexpr int BM = 128, BN = 32, BK = 32, WM = 4;
+template <int BK_ = 32>
+struct Conv2DgradPT {
+  static constexpr int BM = 128, BN = 32, BK = BK_, WM = 4;
+  static constexpr int KPT = 64 / BK;  // k-blocks per tap (64 output channels)
   static constexpr bool A_KMAJ = true, B_KMAJ = true, SMEM = false;
   using Args = BwdArgs;
   using Smem = NoSmem;
@@ -1147,12 +1151,12 @@ struct Conv2DgradP {
     const int nty = (c.jy == 0 ? 0 : 1) - c.ty0 + 1;
     c.ntx = (c.jx == 0 ? 0 : 1) - c.tx0 + 1;
     c.kb0 = 0;
-    c.kb1 = 2 * nty * c.ntx;
+    c.kb1 = KPT * nty * c.ntx;
     c.dy = make_rsrc(a.dy, (uint32_t)a.B * 81 * 64 * 4);
     c.w = make_rsrc(a.w, 16 * 32 * 64 * 4);
   }
   static __device__ void tap_of(const Ctx& c, int kb, int& ty, int& tx) {
-    const int ti = kb >> 1, r = c.ntx == 2 ? ti >> 1 : ti;
+    const int ti = kb / KPT, r = c.ntx == 2 ? ti >> 1 : ti;
     ty = c.ty0 + r;
     tx = c.tx0 + ti - r * c.ntx;
   }
@@ -1164,14 +1168,14 @@ struct Conv2DgradP {
   static __device__ f32x4 load_a_row(const Args&, const Ctx& c, const RowA& r, int kb) {
     int ty, tx;
     tap_of(c, kb, ty, tx);
-    return bld4(c.dy, r.off + (uint32_t)((((c.jy - ty) * 9 + c.jx - tx) * 64 + (kb & 1) * 32) * 4));
+    return bld4(c.dy, r.off + (uint32_t)((((c.jy - ty) * 9 + c.jx - tx) * 64 + (kb % KPT) * BK) * 4));
   }
   static __device__ RowB row_b(const Args&, const Ctx&, int n, int ch) { return {(uint32_t)(n * 64 + 4 * ch) * 4}; }
   static __device__ f32x4 load_b_row(const Args&, const Ctx& c, const RowB& r, int kb) {
     int ty, tx;
     tap_of(c, kb, ty, tx);
     const int ky = (c.cls >> 1) + 2 * ty, kx = (c.cls & 1) + 2 * tx;
-    return bld4(c.w, r.off + (uint32_t)(((ky * 4 + kx) * 32 * 64 + (kb & 1) * 32) * 4));
+    return bld4(c.w, r.off + (uint32_t)(((ky * 4 + kx) * 32 * 64 + (kb % KPT) * BK) * 4));
   }
   static __device__ void store(const Args& a, const Ctx& c, int ml, int n, float v) {
     const int b = c.b0 + ml;
@@ -1181,6 +1185,8 @@ struct Conv2DgradP {
     a.out[o] = a.mask[o] > 0.f ? v : 0.f;
   }
 };
+using Conv2DgradP = Conv2DgradPT<32>;
+using Conv2DgradP16 = Conv2DgradPT<16>;
 
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
@@ -1331,8 +1337,9 @@ size_t f32_wgrad_workspace_floats(int layer, int B, int target) {
 
 // wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target) {
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target, int tile) {
   if (B <= 0) return;
+  if (tile < 0 || tile > 1) throw std::invalid_argument("f32_conv_bwd: tile 0 (default) or 1 (input-gradient BK 16)");
   check_bwd_batch(B);
   const SplitPlan p = wgrad_plan(layer, B, target);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
@@ -1354,10 +1361,12 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.B = B;
   switch (layer) {
     case 3:
-      launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
+      if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP16>(g, (576 / 64) * p.splits, d, Conv3DgradP16::tiles(B), s);
+      else launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
       break;
     case 2:
-      launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
+      if (tile == 1) launch2<ConvWgrad<2>, Conv2DgradP16>(g, (512 / 64) * p.splits, d, Conv2DgradP16::tiles(B), s);
+      else launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
       break;
     case 1:
       f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);
