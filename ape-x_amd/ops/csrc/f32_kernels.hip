@@ -688,17 +688,21 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       y.w = fmaxf(ah[3] + (am[3] + al[3]) + bias4.w, 0.f);
       *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
     };
-    // ping-pong fragment buffers: the next tile's LDS reads are in flight during this tile's MFMAs
+    // ping-pong fragment buffers: the next tile's LDS reads are in flight during this tile's MFMAs.
+    // Wave parity t0 owns tiles t0, t0 + 2, ...: 6 pairs (+ tile 24 for t0 = 0); every fragment
+    // load is unconditional (the one past parity 1's last tile re-reads tile 24, unused), so the
+    // buffers keep fixed registers (guarded loads + a mid-loop exit made the compiler copy them)
     bfx8 fa[8], fb[8];
-    int tile = wave & 1;
-    frags(tile, fa);
-    for (; tile < 25; tile += 4) {
-      if (tile + 2 < 25) frags(tile + 2, fb);
+    const int t0 = wave & 1;
+    frags(t0, fa);
+    for (int pr = 0; pr < 6; ++pr) {
+      const int tile = t0 + 4 * pr;
+      frags(tile + 2, fb);
       tile_mfma(tile, fa);
-      if (tile + 2 >= 25) break;
-      if (tile + 4 < 25) frags(tile + 4, fa);
+      frags(min(tile + 4, 24), fa);
       tile_mfma(tile + 2, fb);
     }
+    if (t0 == 0) tile_mfma(24, fa);
   }
 }
 
