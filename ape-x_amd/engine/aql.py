@@ -42,6 +42,7 @@ from __future__ import annotations
 import collections
 import math
 import os
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -322,8 +323,11 @@ class AQLLearner:
                       bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
                       loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
                       max_prio=r.max_prio.data_ptr(), alpha=r.alpha)
-            self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
-            if self.Ls is not None:  # + the next step's draw (the stream of the forward's fused sampling)
+            try:
+                self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
+            except RuntimeError as e:  # the grid cannot be co-resident on this device: separate launches
+                warnings.warn(f"AQL fused step tail unavailable ({e}); using the separate launches")
+            if self.S is not None and self.Ls is not None:  # + the next step's draw (the forward's sampling stream)
                 self.S_draw = h.make_aql_step(
                     self.L, self.G, self.post, r.tree, self.hp,
                     dict(kw, draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=replay.seed ^ 0x51A7,

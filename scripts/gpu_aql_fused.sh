@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   > $O/pytest.log 2>&1; rc=$?
 tail -5 $O/pytest.log
 [ $rc -ne 0 ] && exit $rc
-for f in 0 1 0 1; do
+for f in 0 1; do
   timeout -k 10 120 python -u scripts/bench_aql.py --iters 200 --fused-step $f >> $O/micro.log 2>&1 || exit $?
 done
 grep fused_step $O/micro.log | cut -c1-120
@@ -18,5 +18,6 @@ timeout -k 10 300 python -u bench.py --algo aql --steps 500 --warmup 20 > $O/ben
 grep '^{' $O/bench.log | cut -c1-400
 timeout -k 10 300 python -u bench.py --algo aql --steps 500 --warmup 20 --aql-overlap > $O/bench_overlap.log 2>&1 || exit $?
 grep -o '"value": [0-9.]*' $O/bench_overlap.log
+[ -z "$PROF" ] && exit 0
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run \
    -- python3 $R/bench.py --algo aql --steps 100 --warmup 10 > $O/prof.log 2>&1
