@@ -629,6 +629,14 @@ __device__ __forceinline__ void c1x_store(const uint4 (&v)[kC1xPer], uint32_t* x
 // Software-pipelined over the workgroup's samples: the next sample's frame chunks are
 // loaded into registers before this sample's MFMA loop, so the frame-ring (HBM) latency
 // hides behind compute; they are converted into LDS after the loop.
+// SplitReads: the two 8-byte halves of a fragment as two ds_read_b64 (2 LDS cycles each, 256 B/clk)
+// instead of the ds_read2_b64 the compiler forms from them (8 cycles, 128 B/clk): the second
+// address is hidden from the load/store merger (one v_add per fragment)
+__device__ __forceinline__ int opaque_i(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+template <bool SplitReads>
 __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
   const int B = set.B, total = set.n * B;
@@ -668,7 +676,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
         const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
-        const uint2 lo = ap[0], hi = ap[1];
+        const uint2 lo = ap[0], hi = SplitReads ? ap[opaque_i(1)] : ap[1];
         a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
     };
@@ -1257,8 +1265,9 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int tile) {
   check_set(set);
   if (tile < 0 || tile > 2) throw std::invalid_argument("f32_conv_fwd_multi: tile 0..2");
   switch (layer) {
-    case 1:
-      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+    case 1:  // tile 1: split fragment reads
+      if (tile == 1) f32_conv1_fwd_x3_k<true><<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+      else f32_conv1_fwd_x3_k<false><<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
     case 2:

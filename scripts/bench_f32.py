@@ -123,6 +123,13 @@ for tv in [int(x) for x in a.fwd_tiles.split(",") if x]:  # same k order: bit-id
         hip.f32_conv_fwd_multi(L, set3(L), B, S(), tile=tv)
         if not all(torch.equal(r, (w.a2 if L == 2 else w.a3)) for r, w in zip(ref, wss)):
             mismatch.add(f"conv{L}_fwd@t{tv}")
+    if tv == 1:  # conv1: split fragment reads
+        hip.f32_conv_fwd_multi(1, set3(1), B, S())
+        ref = [w.a1.clone() for w in wss]
+        hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=1)
+        if not all(torch.equal(r, w.a1) for r, w in zip(ref, wss)):
+            mismatch.add("conv1_fwd@t1")
+        cases["conv1_fwd@t1"] = ((lambda: hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=1)), 2 * P * 400 * 32 * 256)
     cases[f"conv2_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=tv)), 2 * P * 81 * 64 * 512)
     cases[f"conv3_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=tv)), 2 * P * 49 * 64 * 576)
 res = {}
