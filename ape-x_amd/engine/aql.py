@@ -198,8 +198,10 @@ class AQLEngineConfig:
                              # "scalar" = one wave per candidate item (aql_candidate_q)
     # everything after the forward in ONE launch (aql_step_tail_k: backward + priority write +
     # target noise | gradients | Adam x2 + online noise + proposal copy, grid barriers between
-    # the phases) instead of four; batch <= 64, not with fork_tree
-    fused_step: bool = True
+    # the phases; batch <= 64, not with fork_tree).  Measured SLOWER on MI355X: 82.1 vs 54.7 us
+    # per learner step (bit-identical results) -- each grid barrier (~9 us: agent-scope fences
+    # write back / invalidate the XCD L2s) costs more than the ~1.5 us kernel boundary it replaces
+    fused_step: bool = False
     seed: int = 0
 
 

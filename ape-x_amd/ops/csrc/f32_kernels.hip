@@ -629,14 +629,14 @@ __device__ __forceinline__ void c1x_store(const uint4 (&v)[kC1xPer], uint32_t* x
 // Software-pipelined over the workgroup's samples: the next sample's frame chunks are
 // loaded into registers before this sample's MFMA loop, so the frame-ring (HBM) latency
 // hides behind compute; they are converted into LDS after the loop.
-// SplitReads: the two 8-byte halves of a fragment as two ds_read_b64 (2 LDS cycles each, 256 B/clk)
-// instead of the ds_read2_b64 the compiler forms from them (8 cycles, 128 B/clk): the second
-// address is hidden from the load/store merger (one v_add per fragment)
+// The two 8-byte halves of a pixel fragment load as two ds_read_b64 (2 LDS cycles each,
+// 256 B/clk) instead of the ds_read2_b64 the compiler would merge them into (8 cycles,
+// 128 B/clk): the second address is hidden from the load/store merger (one v_add per fragment;
+// MI355X, 3 x 512 samples: 44.6 vs 46.5 us)
 __device__ __forceinline__ int opaque_i(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-template <bool SplitReads>
 __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
   const int B = set.B, total = set.n * B;
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
         const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
-        const uint2 lo = ap[0], hi = SplitReads ? ap[opaque_i(1)] : ap[1];
+        const uint2 lo = ap[0], hi = ap[opaque_i(1)];
         a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
     };
@@ -1133,8 +1133,9 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
   }
 };
 
-using Conv3DgradP = Conv3DgradPT<128, 32, 4>;
-using Conv3DgradP16 = Conv3DgradPT<128, 32, 4, 16>;
+// BK 16 (half the LDS: more workgroups per CU beside the weight-gradient ones of the same
+// launch): conv3 backward 47.2 vs 50.0 us, conv2 65.3 vs 68.8 us at BK 32 (B = 512)
+using Conv3DgradP = Conv3DgradPT<128, 32, 4, 16>;
 
 // conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
 // output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
@@ -1197,8 +1198,7 @@ struct Conv2DgradPT {
     a.out[o] = a.mask[o] > 0.f ? v : 0.f;
   }
 };
-using Conv2DgradP = Conv2DgradPT<32>;
-using Conv2DgradP16 = Conv2DgradPT<16>;
+using Conv2DgradP = Conv2DgradPT<16>;
 
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
@@ -1259,27 +1259,20 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-// tile: 0 = the measured default (below); 1 = 128 x 64 tiles, BK 16 (4 waves of 64 x 32: every B
-// fragment read feeds two MFMAs), 2 = 128 x 64, BK 32 -- per-call variants for the microbench
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int tile) {
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
   check_set(set);
-  if (tile < 0 || tile > 2) throw std::invalid_argument("f32_conv_fwd_multi: tile 0..2");
   switch (layer) {
-    case 1:  // tile 1: split fragment reads
-      if (tile == 1) f32_conv1_fwd_x3_k<true><<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
-      else f32_conv1_fwd_x3_k<false><<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+    case 1:
+      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
-    case 2:
-      if (tile == 1) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
-      else if (tile == 2) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+    case 2:  // learner: 128 x 64 tiles at BK 16 (4 waves of 64 x 32, each B fragment read feeds two
+             // MFMAs): 77.6 us vs 82.9 (64 x 64, BK 32) and 78.6 (128 x 64, BK 32), 3 x 512 samples
+      if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
-    case 3:
-      if (tile == 1) fwd_launch<Conv3FwdT<128, 64, 16, 2>>(set, s);
-      else if (tile == 2) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+    case 3:  // learner: 64 x 64 (65.0 us vs 66.6 / 70.2 for the 128 x 64 tiles at BK 16 / 32)
+      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
@@ -1350,9 +1343,8 @@ size_t f32_wgrad_workspace_floats(int layer, int B, int target) {
 
 // wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target, int tile) {
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target) {
   if (B <= 0) return;
-  if (tile < 0 || tile > 1) throw std::invalid_argument("f32_conv_bwd: tile 0 (default) or 1 (input-gradient BK 16)");
   check_bwd_batch(B);
   const SplitPlan p = wgrad_plan(layer, B, target);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
@@ -1374,12 +1366,10 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.B = B;
   switch (layer) {
     case 3:
-      if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP16>(g, (576 / 64) * p.splits, d, Conv3DgradP16::tiles(B), s);
-      else launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
+      launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
       break;
     case 2:
-      if (tile == 1) launch2<ConvWgrad<2>, Conv2DgradP16>(g, (512 / 64) * p.splits, d, Conv2DgradP16::tiles(B), s);
-      else launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
+      launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
       break;
     case 1:
       f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);

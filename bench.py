@@ -70,8 +70,6 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps after timing (for rocprof)")
     ap.add_argument("--no-reserve", dest="reserve", action="store_false",
                     help="do not take the actor stream from the pool before the process group")
-    ap.add_argument("--learner-priority", action="store_true",
-                    help="run the learner on a high-priority stream (the actor graph keeps normal priority)")
     ap.add_argument("--roctx", action="store_true", help="roctx ranges around engine phases (rocprofv3 --marker-trace)")
     ap.add_argument("--topology", default="auto", choices=["auto", "central", "sharded"],
                     help="auto (default): one GPU = the single-GPU engine, N>1 = central (BASELINE config 3, the "
@@ -210,9 +208,6 @@ def main():
         from apex_amd.engine.apex import reserve_actor_stream
 
         reserve_actor_stream(device)  # before the process group draws its pool streams
-    if args.learner_priority:  # the learner chain on a high-priority HIP stream (its queue dispatches
-        # first when CUs free up), the actor graph on its normal-priority stream beside it
-        torch.cuda.set_stream(torch.cuda.Stream(device=device, priority=-1))
     if world > 1 or args.force_dp:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if args.backend == "nccl":

@@ -25,9 +25,6 @@ ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
-ap.add_argument("--fwd-tiles", default="", help="extra conv2/conv3 forward cases at these tile variants (1, 2)")
-ap.add_argument("--bwd-tiles", default="", help="extra conv2/conv3 backward cases at these input-gradient tile "
-                                                "variants (1: BK 16)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
@@ -95,19 +92,6 @@ cases = {
                                              0, 0, 0, w1.data_ptr(), B, S()), 2 * B * 400 * 32 * 256),
 }
 mismatch = set()
-for tv in [int(x) for x in a.bwd_tiles.split(",") if x]:  # (same k order: bit-identical input gradients)
-    for L, xin, dyin, wt, dx, wsx in ((3, "a2", "dy3", net.w3t, "dy2", w3), (2, "a1", "dy2", net.w2t, "dy1", w2)):
-        flop = 2 * 2 * B * (49 * 64 * 576 if L == 3 else 81 * 64 * 512)
-        fn = (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tv=tv: hip.f32_conv_bwd(
-            L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
-            getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), tile=tv))
-        hip.f32_conv_bwd(L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
-                         getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S())
-        ref = getattr(ws, dx).clone()
-        fn()
-        if not torch.equal(ref, getattr(ws, dx)):
-            mismatch.add(f"conv{L}_bwd@t{tv}")
-        cases[f"conv{L}_bwd@t{tv}"] = (fn, flop)
 for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
     for L, xin, dyin, wt, dx in ((3, "a2", "dy3", net.w3t, "dy2"), (2, "a1", "dy2", net.w2t, "dy1")):
         wsx = torch.empty(hip.f32_wgrad_workspace_floats(L, B, tg), dtype=torch.float32, device=dev)
@@ -116,22 +100,6 @@ for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
             (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tg=tg: hip.f32_conv_bwd(
                 L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
                 getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), target=tg)), flop)
-for tv in [int(x) for x in a.fwd_tiles.split(",") if x]:  # same k order: bit-identical to the default tiles
-    for L in (2, 3):
-        hip.f32_conv_fwd_multi(L, set3(L), B, S())
-        ref = [(w.a2 if L == 2 else w.a3).clone() for w in wss]
-        hip.f32_conv_fwd_multi(L, set3(L), B, S(), tile=tv)
-        if not all(torch.equal(r, (w.a2 if L == 2 else w.a3)) for r, w in zip(ref, wss)):
-            mismatch.add(f"conv{L}_fwd@t{tv}")
-    if tv == 1:  # conv1: split fragment reads
-        hip.f32_conv_fwd_multi(1, set3(1), B, S())
-        ref = [w.a1.clone() for w in wss]
-        hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=1)
-        if not all(torch.equal(r, w.a1) for r, w in zip(ref, wss)):
-            mismatch.add("conv1_fwd@t1")
-        cases["conv1_fwd@t1"] = ((lambda: hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=1)), 2 * P * 400 * 32 * 256)
-    cases[f"conv2_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=tv)), 2 * P * 81 * 64 * 512)
-    cases[f"conv3_fwd@t{tv}"] = ((lambda tv=tv: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=tv)), 2 * P * 49 * 64 * 576)
 res = {}
 runs = [(name, fn, flop) for name, (fn, flop) in cases.items() if not a.only or a.only in name]
 for name, fn, flop in runs:

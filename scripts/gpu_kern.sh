@@ -9,7 +9,7 @@ timeout -k 10 500 python -u -m pytest tests/test_gpu_f32_net.py tests/test_gpu_l
   --timeout 240 --timeout-method thread > gpurun_out/pytest_kern.log 2>&1
 rc=$?; echo "== tests rc=$rc"; tail -4 gpurun_out/pytest_kern.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python scripts/bench_f32.py --wgrad-targets 512,1024 --fwd-tiles 1,2 --bwd-tiles 1 > gpurun_out/bench_f32.log 2>&1
+timeout -k 10 200 python scripts/bench_f32.py > gpurun_out/bench_f32.log 2>&1
 rc=$?; echo "== bench_f32 rc=$rc"; cat gpurun_out/bench_f32.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py --steps 2000 --warmup 50 > gpurun_out/bench1.log 2>&1
