@@ -36,6 +36,7 @@ def main():
 
     m64, t64 = clone(L.model, torch.float64), clone(L.target, torch.float64)
     m32, t32 = clone(L.model, torch.float32), clone(L.target, torch.float32)
+    p_before = {n: p.detach().double().clone() for n, p in L.model.named_parameters()}
     L.step()
     torch.cuda.synchronize()
     B = a.B
@@ -89,6 +90,13 @@ def main():
               f"t32 rel {(acts['t32']['delta'] - ref).norm().item() / ref.norm().item():.3g}  "
               f"hip max abs {(L.delta.double() - ref).abs().max().item():.3g}")
         print(f"gamma_n used {L.gamma_n!r} vs {lc.gamma ** lc.n_step!r}")
+        am64 = acts["t64"]["q2"].argmax(1)
+        print(f"argmax Q(s') differs from fp64: hip {int((hip_acts['q2'].argmax(1) != am64).sum())} "
+              f"t32 {int((acts['t32']['q2'].argmax(1) != am64).sum())} of {B}")
+        hd = (L.delta.double() - ref).abs()
+        k = int(hd.argmax())
+        print(f"worst delta sample {k}: hip {float(L.delta[k]):.7g} fp64 {float(ref[k]):.7g} "
+              f"t32 {float(acts['t32']['delta'][k]):.7g}")
     st = L.stats()
     n64 = torch.sqrt(sum((g ** 2).sum() for g in grads["t64"].values())).item()
     print(f"grad norm: hip {st['grad_norm_l2']:.9g}  fp64 {n64:.9g}  (clip 40)")
@@ -102,6 +110,22 @@ def main():
         s3 = int(((torch.sign(g32) != torch.sign(g64)) & big).sum())
         print(f"{n:28s} {(g - g64).norm().item() / den:10.3g} {(g32 - g64).norm().item() / den:10.3g} "
               f"{sh:9d} {s3:9d} {den:10.3g}")
+    # the first centered-RMSprop update from each gradient (clip inactive below 40), per tensor:
+    # where do the HIP and fp64 updates differ, and how large are the gradients there
+    lr, al, eps = lc.lr, lc.rms_alpha, lc.rms_eps
+    print("update diff per tensor: ||dp_hip - dp_64|| / ||dp_64||, elements off by > 0.05 lr, their |g64| median")
+    tot = 0.0
+    for n, p in L.model.named_parameters():
+        g64 = grads["t64"][n]
+        sq, ga = (1 - al) * g64 * g64, (1 - al) * g64
+        dp64 = -lr * g64 / (torch.sqrt(torch.clamp(sq - ga * ga, min=0)) + eps)
+        dph = p.detach().double() - p_before[n]
+        diff = (dph - dp64)
+        off = diff.abs() > 0.05 * lr
+        tot += float((diff ** 2).sum())
+        med = float(g64[off].abs().median()) if off.any() else float("nan")
+        print(f"{n:28s} {diff.norm().item() / (dp64.norm().item() + 1e-30):10.3g} {int(off.sum()):8d} {med:10.3g}")
+    print(f"total update diff {tot ** 0.5:.4g}")
 
 
 if __name__ == "__main__":
