@@ -93,6 +93,19 @@ def main():
         am64 = acts["t64"]["q2"].argmax(1)
         print(f"argmax Q(s') differs from fp64: hip {int((hip_acts['q2'].argmax(1) != am64).sum())} "
               f"t32 {int((acts['t32']['q2'].argmax(1) != am64).sum())} of {B}")
+        small = ref < 1.0  # the Huber-quadratic samples: their |td| IS the loss gradient
+        yv, qa = {}, {}
+        for name in ("t64", "t32", "hip"):
+            src = acts[name] if name != "hip" else hip_acts
+            q, q2, q2t = src["q"], src["q2"], src["q2t"]
+            yv[name] = r.double() + (lc.gamma ** lc.n_step) * q2t[ar, q2.argmax(1)] * (1 - d.double())
+            qa[name] = q[ar, act.long()]
+        for name in ("hip", "t32"):
+            dd = (yv[name] - qa[name]) - (yv["t64"] - qa["t64"])
+            print(f"{name}: small-td samples {int(small.sum())}: |err td| rms {dd[small].pow(2).mean().sqrt().item():.3g} "
+                  f"|err qa| rms {(qa[name] - qa['t64'])[small].pow(2).mean().sqrt().item():.3g} "
+                  f"|err y| rms {(yv[name] - yv['t64'])[small].pow(2).mean().sqrt().item():.3g}")
+        print(f"|Q| mean {qa['t64'].abs().mean().item():.4g}, |td| mean over small {ref[small].mean().item():.4g}")
         hd = (L.delta.double() - ref).abs()
         k = int(hd.argmax())
         print(f"worst delta sample {k}: hip {float(L.delta[k]):.7g} fp64 {float(ref[k]):.7g} "
