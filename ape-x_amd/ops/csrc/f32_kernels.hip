@@ -566,11 +566,14 @@ struct W1Split {
   bfx8 hi[8], mid[8], lo[8];
 };
 
-// this lane's B fragments for all 8 k-blocks: W1[row][32 kb + 8q + j], split into 3 terms
+// this lane's weight fragments for all 8 k-blocks, split into 3 terms.  k order inside a
+// k-block (input channel kb >> 1, kernel rows 4 (kb & 1) .. +3): lane group q = 2 p + h holds
+// rows 2p, 2p + 1 (j >> 2) x columns 4h .. 4h + 3 (j & 3) -- see f32_conv1_fwd_x3_k's fragments;
+// wrow = W1 row + (2p) * 8 + 4h
 __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
 #pragma unroll
   for (int kb = 0; kb < 8; ++kb) {
-    const f32x4 v0 = ld4(wrow + 32 * kb), v1 = ld4(wrow + 32 * kb + 4);
+    const f32x4 v0 = ld4(wrow + 32 * kb), v1 = ld4(wrow + 32 * kb + 8);
     const float x[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     uint32_t h[4], m[4], l[4];
 #pragma unroll
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
     const F32Prob p = pick(set, prob);
     if (prob != cur) {  // block-uniform
       cur = prob;
-      split_w1(p.w + (nh * 16 + i) * 256 + 8 * q, w);
+      split_w1(p.w + (nh * 16 + i) * 256 + (q >> 1) * 16 + (q & 1) * 4, w);
     }
     __syncthreads();  // the previous sample's tiles are done with xs
     c1x_store(v, xs);
@@ -670,13 +673,18 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
     bias4.y = p.bias[nh * 16 + 4 * q + 1];
     bias4.z = p.bias[nh * 16 + 4 * q + 2];
     bias4.w = p.bias[nh * 16 + 4 * q + 3];
+    // pixel fragments: lane (i, q = 2p + h) reads 4 columns 4 ox + 4h .. +3 of kernel rows 2p and
+    // 2p + 1 (two ds_read_b64, 42 dwords apart).  Within a 32-lane LDS group (q = 0, 1) lane
+    // (ox, h = 1) reads the same dwords as lane (ox + 1, h = 0) -- stride-4 windows overlap by 4
+    // columns -- so the group touches ~34 consecutive dwords and broadcasts the rest: no bank
+    // conflicts (rows in the lane groups gave 1.84 conflict cycles per LDS cycle)
     auto frags = [&](int tile, bfx8 (&a)[8]) {
       const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
-      const __bf16* a0 = xb + (4 * oy + q) * 84 + 4 * ox;
+      const __bf16* a0 = xb + (4 * oy + 2 * (q >> 1)) * 84 + 4 * ox + 4 * (q & 1);
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
         const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
-        const uint2 lo = ap[0], hi = ap[opaque_i(1)];
+        const uint2 lo = ap[0], hi = ap[opaque_i(21)];  // next kernel row (84 bf16 = 21 x 8 bytes)
         a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
     };
@@ -920,6 +928,21 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int col = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
   const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
+  // this wave's quarter of every k-step's dy: co = 16 hq + col, slots j0 .. j0 + 3 of group g.
+  // All 15 k-steps' values are loaded up front (60 registers), in flight with the plane
+  // staging: loaded one k-step ahead, each k-step (~400 MFMA cycles) waited out most of a
+  // global round trip
+  const int hq = c >> 1, j0 = 4 * (c & 1);
+  const bool live = sl < ns;  // a missing second sample (odd batch tail): zero dy, barriers kept
+  const float* dy = a.dy + (size_t)(b0 + (live ? sl : 0)) * 400 * 32 + 16 * hq + col;
+  float dyv[15][4];
+#pragma unroll
+  for (int ks = 0; ks < 15; ++ks) {  // unconditional loads from clamped pixel slots, zeroed at use
+    const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
+    const float* dp = dy + (oy * 20 + ox0) * 32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dyv[ks][j] = dp[min(j0 + j, nv - 1) * 32];
+  }
   {  // stage both samples' planes (u8): 2 x 4 x 441 16-byte chunks
     const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
     constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
@@ -951,24 +974,13 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int i = 0; i < 4; ++i) ah[h][i] = am[h][i] = al[h][i] = zero4();
-  // this wave's quarter of every k-step's dy: co = 16 hq + col, slots j0 .. j0 + 3 of group g
-  const int hq = c >> 1, j0 = 4 * (c & 1);
-  const bool live = sl < ns;  // a missing second sample (odd batch tail): zero dy, barriers kept
-  const float* dy = a.dy + (size_t)(b0 + (live ? sl : 0)) * 400 * 32 + 16 * hq + col;
   float bs = 0.f;  // bias partial of co = 16 hq + col over this wave's slots
-  float nv4[4];
-  auto load_dy = [&](int ks) {  // unconditional loads from clamped pixel slots, zeroed at use
-    const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
-    const float* dp = dy + (oy * 20 + ox0) * 32;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) nv4[j] = dp[min(j0 + j, nv - 1) * 32];
-  };
   auto split_store = [&](int ks, int buf) {
     const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy), nv = min(8, 20 - ox0);
     float d[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      d[j] = (live && j0 + j < nv) ? nv4[j] : 0.f;
+      d[j] = (live && j0 + j < nv) ? dyv[ks][j] : 0.f;
       bs += d[j];
     }
     uint32_t hw[2], mw[2], lw[2];
@@ -988,12 +1000,11 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
     *reinterpret_cast<uint2*>(base + 2 * 64 * 4) = make_uint2(lw[0], lw[1]);
   };
   const uint32_t* pc = pl + (sl * 4 + c) * kPlaneDw + (col >> 1) * 21 + (col & 1);
-  load_dy(0);
   split_store(0, 0);
   __syncthreads();  // the planes and the first k-step's fragments are staged
-  for (int ks = 0; ks < 15; ++ks) {
+#pragma unroll
+  for (int ks = 0; ks < 15; ++ks) {  // unrolled: dyv[ks] stays in registers
     const int cur = ks & 1;
-    if (ks + 1 < 15) load_dy(ks + 1);  // in flight under this k-step's MFMAs
     const int g = 4 * ks + q, oy = g / 3, ox0 = 8 * (g - 3 * oy);
     bfx8 A[2][3];
 #pragma unroll
