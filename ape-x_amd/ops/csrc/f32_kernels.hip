@@ -1270,11 +1270,12 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s) {
+// c1_grid: conv1 workgroups (<= 0: kC1xGrid); a per-call microbench parameter
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid) {
   check_set(set);
   switch (layer) {
     case 1:
-      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, kC1xGrid), 256, 0, s>>>(set);
+      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
     case 2:  // learner: 128 x 64 tiles at BK 16 (4 waves of 64 x 32, each B fragment read feeds two

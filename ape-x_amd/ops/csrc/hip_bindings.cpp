@@ -454,7 +454,8 @@ PYBIND11_MODULE(_apex_hip, m) {
   };
   // probs: (in, ids, idx, w, w2, bias, out)
   m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::vector<uint64_t>>& probs, int B,
-                                       uint64_t s) { f32_conv_fwd_multi(layer, f32set(probs, B), S(s)); });
+                                       uint64_t s, int c1_grid) { f32_conv_fwd_multi(layer, f32set(probs, B), S(s), c1_grid); },
+        py::arg("layer"), py::arg("probs"), py::arg("B"), py::arg("s"), py::arg("c1_grid") = 0);
   m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::vector<uint64_t>>& probs, int B, uint64_t s) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });

@@ -377,7 +377,7 @@ struct F32Set {
   F32Prob p[kMaxProbs];
   int n, B;
 };
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s);
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0);
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
 // target: conv2 / conv3 weight-gradient workgroups (<= 0: the default); the workspace, the

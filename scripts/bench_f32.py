@@ -23,6 +23,7 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
 a = ap.parse_args()
@@ -100,6 +101,9 @@ for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
             (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tg=tg: hip.f32_conv_bwd(
                 L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
                 getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), target=tg)), flop)
+for cg in [int(x) for x in a.c1_grids.split(",") if x]:
+    cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
+                                 2 * P * 400 * 32 * 256)
 res = {}
 runs = [(name, fn, flop) for name, (fn, flop) in cases.items() if not a.only or a.only in name]
 for name, fn, flop in runs:
