@@ -904,9 +904,12 @@ struct ConvWgrad {
 // both co halves: 8 independent accumulators per 4 pixels.  The two samples' partials are
 // added through LDS (fixed order) into partial g: ws[g][co][kk] + bias partials ws_b[g][co]
 // (sum of dy1 over the pixels), reduced over g by grad_finalize like the other layers.
-constexpr int kConv1WgradS = 2;  // samples per workgroup (partials = ceil(B / 2))
-// staging dump (dwords): the 512-thread chunk loop's tail past 2 samples' 3528 chunks
-constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) / 512) * 512 - kConv1WgradS * 4 * (kPlane / 16));
+constexpr int kConv1WgradS = 2;  // default samples per workgroup (partials = ceil(B / 2))
+// staging dump (dwords): the chunk loop's tail past S samples' 1764 S chunks (256 S threads)
+template <int S>
+constexpr int c1w_dump() {
+  return 4 * (((S * 4 * (kPlane / 16) + 256 * S - 1) / (256 * S)) * 256 * S - S * 4 * (kPlane / 16));
+}
 // conv1 weight gradient at reference precision on bf16 MFMA (the exact split of the
 // forward above, applied to dy): the u8 frame operand is exact in bf16 and each dy value
 // splits exactly into hi + mid + lo bf16, so every product is exact and only the fp32
@@ -924,14 +927,17 @@ constexpr int kConv1WgradDump = 4 * (((kConv1WgradS * 4 * (kPlane / 16) + 511) /
 // per lane), one workgroup barrier per k-step -- the split (~5 VALU per value) was 4x redundant
 // and bounded the kernel (9.7 VALU per MFMA, 15 % MFMA busy, round 3).  One workgroup per CU
 // either way (~180 VGPRs: 2 waves per SIMD), so the 82 KB of LDS cost no occupancy.
+// S = samples per workgroup (4 S waves); S = 1 writes one partial per sample.
 constexpr int kC1wAf = 2 * 3 * 64;  // uint4 per (buffer, sample): [half][term][lane]
-__global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t pl[kConv1WgradS * 4 * kPlaneDw + 16 + kConv1WgradDump];  // + pad: row-end groups
-  __shared__ uint4 af[2][kConv1WgradS][kC1wAf];  // split dy fragments, double-buffered over k-steps
-  __shared__ int64_t wplanes[kConv1WgradS * 4];  // plane byte offsets from the frames base
+template <int S>
+__global__ __launch_bounds__(256 * S) void f32_conv1_wgrad_x3_k(BwdArgs a) {
+  constexpr int NT = 256 * S;
+  __shared__ __attribute__((aligned(16))) uint32_t pl[S * 4 * kPlaneDw + 16 + c1w_dump<S>()];  // + pad: row-end groups
+  __shared__ uint4 af[2][S][kC1wAf];  // split dy fragments, double-buffered over k-steps
+  __shared__ int64_t wplanes[S * 4];  // plane byte offsets from the frames base
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int col = lane & 15, q = lane >> 4, sl = wave >> 2, c = wave & 3;
-  const int b0 = blockIdx.x * kConv1WgradS, ns = min(kConv1WgradS, a.B - b0);
+  const int b0 = blockIdx.x * S, ns = min(S, a.B - b0);
   // this wave's quarter of every k-step's dy: co = 16 hq + col, slots j0 .. j0 + 3 of group g.
   // All 15 k-steps' values are loaded up front (60 registers), in flight with the plane
   // staging: loaded one k-step ahead, each k-step (~400 MFMA cycles) waited out most of a
@@ -947,30 +953,30 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) dyv[ks][j] = dp[min(j0 + j, nv - 1) * 32];
   }
-  {  // stage both samples' planes (u8): 2 x 4 x 441 16-byte chunks
+  {  // stage the samples' planes (u8): S x 4 x 441 16-byte chunks
     const FrameSrc f{static_cast<const uint8_t*>(a.x), a.ids, a.idx};
-    constexpr int kChunks = 4 * (kPlane / 16), kPer = (kConv1WgradS * kChunks + 511) / 512;
+    constexpr int kChunks = 4 * (kPlane / 16), kPer = (S * kChunks + NT - 1) / NT;
     // the 8 plane addresses once (frame_plane reads idx then ids: two dependent round trips,
     // paid per chunk when resolved inside the loop below)
     // (kept as offsets from the kernel-argument base: a pointer read back from LDS is a flat
     // pointer, and flat loads may alias the LDS stores below -- each waited out before its store)
     const uint8_t* fb = static_cast<const uint8_t*>(a.x);
-    if (t < kConv1WgradS * 4) wplanes[t] = frame_plane(f, b0 + min(t >> 2, ns - 1), t & 3, kPlane) - fb;
+    if (t < S * 4) wplanes[t] = frame_plane(f, b0 + min(t >> 2, ns - 1), t & 3, kPlane) - fb;
     __syncthreads();
     uint4 v[kPer];
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      const int e = min(t + 512 * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
+      const int e = min(t + NT * i, ns * kChunks - 1), s2 = e / kChunks, r = e - s2 * kChunks, ch = r / 441;
       v[i] = reinterpret_cast<const uint4*>(fb + wplanes[s2 * 4 + ch])[r - ch * 441];
     }
     // unconditional stores (a guarded store sank its load into the branch: one round trip per
     // chunk); the tail chunks past both samples land in the dump past the planes (and pad)
 #pragma unroll
     for (int i = 0; i < kPer; ++i) {
-      const int e = t + 512 * i;
-      reinterpret_cast<uint4*>(pl)[e < kConv1WgradS * kChunks ? e : e + 4] = v[i];
+      const int e = t + NT * i;
+      reinterpret_cast<uint4*>(pl)[e < S * kChunks ? e : e + 4] = v[i];
     }
-    if (t < 16) pl[kConv1WgradS * 4 * kPlaneDw + t] = 0u;
+    if (t < 16) pl[S * 4 * kPlaneDw + t] = 0u;
   }
   // hi / mid / lo products in three accumulators: no MFMA waits on its predecessor's result
   f32x4 ah[2][4], am[2][4], al[2][4];
@@ -1043,10 +1049,10 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
   // (c & 1) of the half and the two samples through LDS (fixed order)
   bs += __shfl_xor(bs, 16, 64);
   bs += __shfl_xor(bs, 32, 64);
-  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [2 samples][4 waves][16]
-  float* bred = red + 4 * 32 * 64;
+  float* red = reinterpret_cast<float*>(pl);  // [4 waves][8 tiles x 4 regs][64 lanes] + bias [S samples][4 waves][16]
+  float* bred = red + (S == 2 ? 4 * 32 * 64 : 0);
   if (q == 0) bred[(sl * 4 + c) * 16 + col] = bs;
-  if (sl == 1) {
+  if (S == 2 && sl == 1) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -1064,15 +1070,16 @@ __global__ __launch_bounds__(512) void f32_conv1_wgrad_x3_k(BwdArgs a) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float v = (ah[h][i][e] + (am[h][i][e] + al[h][i][e])) + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane];
+          const float own = ah[h][i][e] + (am[h][i][e] + al[h][i][e]);
+          const float v = S == 2 ? own + red[((c * 8 + h * 4 + i) * 4 + e) * 64 + lane] : own;
           const int co = h * 16 + 4 * q + e, kk = c * 64 + (col >> 1) * 8 + 4 * (col & 1) + i;
           out[co * 256 + kk] = v;
         }
-    if (t < 32) {  // co = t: half t >> 4, waves 2 (t >> 4) and +1 of both samples
+    if (t < 32) {  // co = t: half t >> 4, waves 2 (t >> 4) and +1 of every sample
       const int h = t >> 4, cc = t & 15;
       float v = 0.f;
 #pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) v += bred[(s2 * 4 + 2 * h) * 16 + cc] + bred[(s2 * 4 + 2 * h + 1) * 16 + cc];
+      for (int s2 = 0; s2 < S; ++s2) v += bred[(s2 * 4 + 2 * h) * 16 + cc] + bred[(s2 * 4 + 2 * h + 1) * 16 + cc];
       a.out2[blockIdx.x * 32 + t] = v;
     }
   }
@@ -1231,7 +1238,10 @@ SplitPlan plan_splits(int kbt, int ntiles, int target_blocks) {
 // target <= 0: the default (~one per CU)
 SplitPlan wgrad_plan(int layer, int B, int target) {
   switch (layer) {
-    case 1: return {(B + kConv1WgradS - 1) / kConv1WgradS, kConv1WgradS};  // f32_conv1_wgrad_x3_k workgroups
+    case 1: {  // f32_conv1_wgrad_x3_k<S> workgroups (target 1: one sample per workgroup)
+      const int S = target == 1 ? 1 : kConv1WgradS;
+      return {(B + S - 1) / S, S};
+    }
     case 2: return plan_splits(ConvWgrad<2>::kblocks(B), 512 / 64, target > 0 ? target : 256);
     case 3: return plan_splits(ConvWgrad<3>::kblocks(B), 576 / 64, target > 0 ? target : 252);
     default: throw std::invalid_argument("f32 wgrad layer");
@@ -1388,7 +1398,8 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
       launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
       break;
     case 1:
-      f32_conv1_wgrad_x3_k<<<p.splits, 512, 0, s>>>(g);
+      if (p.kbps == 1) f32_conv1_wgrad_x3_k<1><<<p.splits, 256, 0, s>>>(g);
+      else f32_conv1_wgrad_x3_k<2><<<p.splits, 512, 0, s>>>(g);
       LAUNCH_CHECK();
       break;
     default: throw std::invalid_argument("f32_conv_bwd: layer must be 1, 2 or 3");

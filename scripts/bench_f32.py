@@ -23,6 +23,7 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
@@ -101,6 +102,15 @@ for tg in [int(x) for x in a.wgrad_targets.split(",") if x]:
             (lambda L=L, xin=xin, dyin=dyin, wt=wt, dx=dx, wsx=wsx, tg=tg: hip.f32_conv_bwd(
                 L, getattr(ws, xin).data_ptr(), 0, 0, getattr(ws, dyin).data_ptr(), wt.data_ptr(),
                 getattr(ws, xin).data_ptr(), getattr(ws, dx).data_ptr(), wsx.data_ptr(), B, S(), target=tg)), flop)
+if a.c1_wgrad_s1:  # conv1 weight gradient, one sample per workgroup (+ its finalize)
+    w1s = torch.empty(hip.f32_wgrad_workspace_floats(1, B, 1), dtype=torch.float32, device=dev)
+    cases["conv1_wgrad@s1"] = ((lambda: hip.f32_conv_bwd(1, frames.data_ptr(), ids.data_ptr(), idx.data_ptr(),
+                                                         ws.dy1.data_ptr(), 0, 0, 0, w1s.data_ptr(), B, S(), target=1)),
+                               2 * B * 400 * 32 * 256)
+    cases["finalize1@s1"] = ((lambda: hip.grad_finalize([hip.f32_conv_finalize_job(
+        1, B, w1s.data_ptr(), f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr(), target=1)], S(), 0)), 1)
+    cases["finalize1"] = ((lambda: hip.grad_finalize([hip.f32_conv_finalize_job(
+        1, B, w1.data_ptr(), f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr())], S(), 0)), 1)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)
