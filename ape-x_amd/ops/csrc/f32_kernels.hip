@@ -592,11 +592,10 @@ __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
   }
 }
 
-// one sample per workgroup: the persistent walk (2 workgroups per CU, 3 samples each, next
-// sample prefetched) measured slower -- 45.5 us vs 40.9 us for 3 x 512 samples (384 / 768 /
-// 1024 workgroups: 44.1 / 44.1 / 43.8, 256: 50.6): resident workgroups overlap one another's
-// staging better than a workgroup overlaps its own
-constexpr int kC1xGrid = 1 << 30;
+// two workgroups per CU, each walking a contiguous run of samples (next sample prefetched):
+// 512 / 1024 workgroups 42.2 / 41.5-43.9 us, one sample per workgroup (1536) 44.4-45.0 us
+// (3 x 512 samples, interleaved on one box)
+constexpr int kC1xGrid = 512;
 constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
 
 // the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on)
