@@ -1157,6 +1157,7 @@ struct Conv3DgradPT {  // dy2[b][pi][ci] = (a2 > 0) * sum_{valid taps, co} dy3[b
 // BK 16 (half the LDS: more workgroups per CU beside the weight-gradient ones of the same
 // launch): conv3 backward 47.2 vs 50.0 us, conv2 65.3 vs 68.8 us at BK 32 (B = 512)
 using Conv3DgradP = Conv3DgradPT<128, 32, 4, 16>;
+using Conv3DgradP32 = Conv3DgradPT<128, 32, 4, 32>;
 
 // conv2: input pixel (iy, ix) = (2 jy + py, 2 jx + px) takes taps (py + 2 ty, px + 2 tx) from
 // output pixel (jy - ty, jx - tx); rows = (class, jy, jx, sample), only in-range (ty, tx)
@@ -1220,6 +1221,7 @@ struct Conv2DgradPT {
   }
 };
 using Conv2DgradP = Conv2DgradPT<16>;
+using Conv2DgradP32 = Conv2DgradPT<32>;
 
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
@@ -1283,17 +1285,19 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-// c1_grid: conv1 workgroups (<= 0: kC1xGrid); a per-call microbench parameter
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid) {
+// c1_grid: conv1 workgroups (<= 0: kC1xGrid); tile 1: the learner's conv2 on 128 x 64 tiles at
+// BK 16 (the alternative to the default) -- per-call microbench parameters
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid, int tile) {
   check_set(set);
   switch (layer) {
     case 1:
       f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
-    case 2:  // learner: 128 x 64 tiles at BK 16 (4 waves of 64 x 32, each B fragment read feeds two
-             // MFMAs): 77.6 us vs 82.9 (64 x 64, BK 32) and 78.6 (128 x 64, BK 32), 3 x 512 samples
-      if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
+    case 2:  // learner: 64 x 64 tiles at BK 32: 79.0-80.4 us vs 87.0-88.5 for 128 x 64 at BK 16
+             // (3 x 512 samples, interleaved on one box; the BK-16 pitch conflicts on the stores)
+      if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:  // learner: 64 x 64 (65.0 us vs 66.6 / 70.2 for the 128 x 64 tiles at BK 16 / 32)
@@ -1368,7 +1372,7 @@ size_t f32_wgrad_workspace_floats(int layer, int B, int target) {
 
 // wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target) {
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target, int tile) {
   if (B <= 0) return;
   check_bwd_batch(B);
   const SplitPlan p = wgrad_plan(layer, B, target);
@@ -1390,11 +1394,13 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.out = dx;
   d.B = B;
   switch (layer) {
-    case 3:
-      launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
+    case 3:  // tile 1: input gradient at BK 32 (the alternative to the default)
+      if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP32>(g, (576 / 64) * p.splits, d, Conv3DgradP32::tiles(B), s);
+      else launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
       break;
     case 2:
-      launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
+      if (tile == 1) launch2<ConvWgrad<2>, Conv2DgradP32>(g, (512 / 64) * p.splits, d, Conv2DgradP32::tiles(B), s);
+      else launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
       break;
     case 1:
       if (p.kbps == 1) f32_conv1_wgrad_x3_k<1><<<p.splits, 256, 0, s>>>(g);

@@ -454,8 +454,9 @@ PYBIND11_MODULE(_apex_hip, m) {
   };
   // probs: (in, ids, idx, w, w2, bias, out)
   m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::vector<uint64_t>>& probs, int B,
-                                       uint64_t s, int c1_grid) { f32_conv_fwd_multi(layer, f32set(probs, B), S(s), c1_grid); },
-        py::arg("layer"), py::arg("probs"), py::arg("B"), py::arg("s"), py::arg("c1_grid") = 0);
+                                       uint64_t s, int c1_grid, int tile) {
+    f32_conv_fwd_multi(layer, f32set(probs, B), S(s), c1_grid, tile);
+  }, py::arg("layer"), py::arg("probs"), py::arg("B"), py::arg("s"), py::arg("c1_grid") = 0, py::arg("tile") = 0);
   m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::vector<uint64_t>>& probs, int B, uint64_t s) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
@@ -475,11 +476,11 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("f32_wgrad_workspace_floats", &f32_wgrad_workspace_floats, py::arg("layer"), py::arg("B"),
         py::arg("target") = 0);
   m.def("f32_conv_bwd", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t w, uint64_t mask,
-                           uint64_t dx, uint64_t ws, int B, uint64_t s, int target) {
+                           uint64_t dx, uint64_t ws, int B, uint64_t s, int target, int tile) {
     f32_conv_bwd(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const float>(dy), P<const float>(w),
-                 P<const float>(mask), P<float>(dx), P<float>(ws), B, S(s), target);
+                 P<const float>(mask), P<float>(dx), P<float>(ws), B, S(s), target, tile);
   }, py::arg("layer"), py::arg("x"), py::arg("ids"), py::arg("idx"), py::arg("dy"), py::arg("w"), py::arg("mask"),
-     py::arg("dx"), py::arg("ws"), py::arg("B"), py::arg("s"), py::arg("target") = 0);
+     py::arg("dx"), py::arg("ws"), py::arg("B"), py::arg("s"), py::arg("target") = 0, py::arg("tile") = 0);
   m.def("f32_conv_finalize_job", [](int layer, int B, uint64_t ws, uint64_t grad, uint64_t bgrad, int target) {
     return f32_conv_finalize_job(layer, B, P<const float>(ws), P<float>(grad), P<float>(bgrad), target);
   }, py::arg("layer"), py::arg("B"), py::arg("ws"), py::arg("grad"), py::arg("bgrad"), py::arg("target") = 0);

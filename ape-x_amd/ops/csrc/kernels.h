@@ -377,7 +377,7 @@ struct F32Set {
   F32Prob p[kMaxProbs];
   int n, B;
 };
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0);
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0);
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
 // target: conv2 / conv3 weight-gradient workgroups (<= 0: the default); the workspace, the
@@ -393,7 +393,7 @@ void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, flo
 // conv backward: layers 3/2 = wgrad partials + dgrad (w = w3t / w2t, masked by `mask`) in
 // one launch, layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target = 0);
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target = 0, int tile = 0);
 FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad, int target = 0);
 // grad_finalize job that only adds sum(g^2) of g[0..n) to the norm partials
 FinalizeJob norm_only_job(const float* g, int n);

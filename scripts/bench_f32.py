@@ -24,6 +24,8 @@ ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
+ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 128x64 BK 16, "
+                                                   "conv2/conv3 input gradient BK 32")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
@@ -111,6 +113,14 @@ if a.c1_wgrad_s1:  # conv1 weight gradient, one sample per workgroup (+ its fina
         1, B, w1s.data_ptr(), f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr(), target=1)], S(), 0)), 1)
     cases["finalize1"] = ((lambda: hip.grad_finalize([hip.f32_conv_finalize_job(
         1, B, w1.data_ptr(), f[0].weight.grad.data_ptr(), f[0].bias.grad.data_ptr())], S(), 0)), 1)
+if a.tile1:
+    cases["conv2_fwd@t1"] = ((lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=1)), 2 * P * 81 * 64 * 512)
+    cases["conv3_bwd@t1"] = ((lambda: hip.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), net.w3t.data_ptr(),
+                                                       ws.a2.data_ptr(), ws.dy2.data_ptr(), w3.data_ptr(), B, S(),
+                                                       tile=1)), 2 * 2 * B * 49 * 64 * 576)
+    cases["conv2_bwd@t1"] = ((lambda: hip.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), net.w2t.data_ptr(),
+                                                       ws.a1.data_ptr(), ws.dy1.data_ptr(), w2.data_ptr(), B, S(),
+                                                       tile=1)), 2 * 2 * B * 81 * 64 * 512)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)
