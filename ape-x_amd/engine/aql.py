@@ -191,6 +191,10 @@ class AQLEngineConfig:
     # (MI355X, batch 32: 14758-14771 vs 13882-13899 SGD steps/s with the write as its own launch,
     # one box, interleaved; scripts/ab/aql_split_tree.sh)
     split_tree: bool = True
+    # priority write as an extra workgroup of the BACKWARD launch (it recomputes the B TD terms
+    # from the forward's Q rows): the leaves and the level walk run beside the per-sample
+    # backward instead of bounding the gradient / noise-reset launches (replaces split_tree)
+    bwd_tree: bool = False
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
     act_blocks: int = 0
@@ -309,7 +313,11 @@ class AQLLearner:
                                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
                                               r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                           if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
-        split = cfg.split_tree and self.post_tree is None and not cfg.fork_tree and B <= 64
+        self.L_tree = (h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
+                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
+                       if cfg.bwd_tree and self.post_tree is None and not cfg.fork_tree and B <= 64 else None)
+        split = (cfg.split_tree and self.post_tree is None and self.L_tree is None and not cfg.fork_tree
+                 and B <= 64)
         self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
                                            self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
@@ -415,7 +423,7 @@ class AQLLearner:
             h.aql_step_tail(self.S_draw if draw_next else self.S, s)
             self._track_losses()
             return
-        h.aql_learn_bwd(self.L, s)
+        h.aql_learn_bwd(self.L if self.L_tree is None else self.L_tree, s)
         # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
         # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
         # forked onto the tree stream (cfg.fork_tree): it only feeds the NEXT step's sampler, so
@@ -425,8 +433,8 @@ class AQLLearner:
                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
                               r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), ts)
 
-        if self.post_tree is not None or self.G_tree is not None:
-            pass  # folded into the launches below (aql_post_set_tree | aql_grad_set_tree + aql_post_set_levels)
+        if self.post_tree is not None or self.G_tree is not None or self.L_tree is not None:
+            pass  # folded into a launch (aql_learn_set_tree | aql_post_set_tree | aql_grad_set_tree + levels)
         elif self.cfg.fork_tree:
             self.tree_stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self.tree_stream):

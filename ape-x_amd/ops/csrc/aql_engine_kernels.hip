@@ -574,7 +574,35 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   AQL_STAMP(L, 7);
 }
 
-__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) { aql_bwd_block(L, blockIdx.x); }
+// this step's priority write by one workgroup: the B TD terms recomputed from the forward's Q
+// rows (aql_td: the formula the backward writes L.delta / L.lw with), then the batched tree
+// write (leaves, mix, loss mean, every level).  Only the next step's sampler reads the tree.
+__device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc& tree, BatchWrite w) {
+  __shared__ float s_dl[64], s_lw[64], tred[16];
+  __shared__ int sids[64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, T = L.on.T;
+  for (int b = wave; b < L.B; b += (int)(blockDim.x >> 6)) {  // wave-uniform
+    const int s_next = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
+    if (lane == 0) {
+      const int row = L.idx[b];
+      const AqlTd td = aql_td(L, b, row, L.act[row], s_next);
+      s_dl[b] = td.dl;
+      s_lw[b] = td.lw;
+    }
+  }
+  __syncthreads();
+  w.mix.delta = s_dl;
+  w.mix.lw = s_lw;
+  batch_leaves_block(tree, w, 1, tred, sids);
+}
+
+__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
+  if (L.bwd_tree && blockIdx.x == L.B) {  // block-uniform: the priority write (aql_learn_set_tree)
+    td_tree_block(L, L.tree, L.bw);
+    return;
+  }
+  aql_bwd_block(L, blockIdx.x);
+}
 
 // ------------------------------------------------------------------ weight gradients
 constexpr int kGradThreads = 256;
@@ -758,27 +786,6 @@ __device__ __forceinline__ void noise_elem(const AqlNoise& z, int l, int64_t i, 
   }
 }
 
-__device__ __forceinline__ void step_tree_block(const AqlStep& D) {
-  __shared__ float s_dl[64], s_lw[64], tred[16];
-  __shared__ int sids[64];
-  const AqlLearn& L = D.L;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, T = L.on.T;
-  for (int b = wave; b < L.B; b += (int)(blockDim.x >> 6)) {  // wave-uniform
-    const int s_next = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
-    if (lane == 0) {
-      const int row = L.idx[b];
-      const AqlTd td = aql_td(L, b, row, L.act[row], s_next);
-      s_dl[b] = td.dl;
-      s_lw[b] = td.lw;
-    }
-  }
-  __syncthreads();
-  BatchWrite w = D.bw;
-  w.mix.delta = s_dl;
-  w.mix.lw = s_lw;
-  batch_leaves_block(D.tree, w, 1, tred, sids);
-}
-
 constexpr int kStepDrawBlocks = 8;  // phase C workgroups of the next step's draw (4 waves each)
 
 __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
@@ -790,7 +797,7 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
   if (bid < B) {
     aql_bwd_block(D.L, bid);
   } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
-    step_tree_block(D);
+    td_tree_block(D.L, D.tree, D.bw);
   } else {
     const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
     const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
@@ -1099,7 +1106,10 @@ void aql_act_q(const AqlLearn& L, hipStream_t s) {
 void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
   check_net(L.on);
   if (L.B < 1) return;
-  aql_learn_bwd_k<<<L.B, 256, 0, s>>>(L);
+  if (L.bwd_tree && (L.B > 64 || L.bw.B != L.B || L.bw.E != 0 || !L.bw.idx || !L.bw.list || !L.bw.owner ||
+                     !L.bw.max_prio || !L.act || !L.idx))
+    throw std::invalid_argument("aql_learn_bwd: the priority write needs B <= 64 and every pointer");
+  aql_learn_bwd_k<<<L.B + (L.bwd_tree ? 1 : 0), 256, 0, s>>>(L);
   LAUNCH_CHECK();
 }
 

@@ -613,6 +613,25 @@ PYBIND11_MODULE(_apex_hip, m) {
     if (!L.filled || !L.beta || !L.ctr || !L.idx_out || !L.w_out) throw std::invalid_argument("aql_learn_set_sample");
     return L;
   });
+  // the priority write as an extra workgroup of the backward launch (replaces the split write)
+  m.def("aql_learn_set_tree", [](const AqlLearn& L0, const TreeHandle& t, uint64_t prio_out, uint64_t loss_out,
+                                 uint64_t owner, uint64_t list, uint64_t max_prio, float alpha) {
+    AqlLearn L = L0;
+    BatchWrite w{};
+    w.idx = L.idx;
+    w.B = L.B;
+    w.mix = PrioMix{nullptr, nullptr, P<float>(prio_out), P<float>(loss_out)};  // delta / lw: the block's LDS
+    w.owner = P<int>(owner);
+    w.list = P<int>(list);
+    w.max_prio = P<float>(max_prio);
+    w.alpha = alpha;
+    if (!w.idx || !w.owner || !w.list || !w.max_prio || L.B < 1 || L.B > 64)
+      throw std::invalid_argument("aql_learn_set_tree: 1 <= B <= 64 and every pointer");
+    L.bwd_tree = 1;
+    L.tree = t.d;
+    L.bw = w;
+    return L;
+  });
   m.def("aql_noisy_eff", [](const AQLNet& net, uint64_t ws, uint64_t s) { aql_noisy_eff(net, P<float>(ws), S(s)); });
   m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
   m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });

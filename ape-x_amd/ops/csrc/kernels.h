@@ -452,6 +452,11 @@ struct AqlLearn {
   uint64_t seed;
   int* idx_out;
   float* w_out;
+  // priority write in the backward launch (aql_learn_set_tree): one extra workgroup recomputes
+  // the B TD terms from the forward's Q rows (aql_td, the backward's own formula) and runs the
+  // batched tree write (leaves + every level, B <= 64) beside the per-sample backward
+  int bwd_tree;
+  BatchWrite bw;
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
 // acting on the learner's MFMA forward: q_s[b][t] = Q_on(st[b], amu[b][t]) for B states

@@ -93,6 +93,8 @@ def parse():
                     help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
                          "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
+    ap.add_argument("--aql-bwd-tree", type=int, default=None,
+                    help="AQL: priority write in the backward launch (1) or split over grad/post (0)")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=560.0,
@@ -379,6 +381,8 @@ def aql(args, rank, world, device):
     cap = min(args.capacity, 1_000_000)
     cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed + rank,
                           actor_offset=rank * args.envs, total_actors=world * args.envs, overlap=args.aql_overlap)
+    if args.aql_bwd_tree is not None:
+        cfg.bwd_tree = bool(args.aql_bwd_tree)
     eng = AQLEngine(cfg, device)
     t_fill = time.perf_counter()
     eng.fill(max(1024, 4 * args.envs))
