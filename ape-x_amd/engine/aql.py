@@ -195,6 +195,9 @@ class AQLEngineConfig:
     # from the forward's Q rows): the leaves and the level walk run beside the per-sample
     # backward instead of bounding the gradient / noise-reset launches (replaces split_tree)
     bwd_tree: bool = False
+    # learner forward: candidate-tile groups per (sample, net) workgroup (0 = about one workgroup
+    # per CU: the ~110 KB weight staging, the PER draw and the state MLP serve a group of tiles)
+    fwd_tile_groups: int = 0
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
     act_blocks: int = 0
@@ -287,6 +290,8 @@ class AQLLearner:
             p["dbg"] = self.dbg.data_ptr()
         self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
                                   float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
+        if cfg.fwd_tile_groups:
+            self.L = h.aql_learn_set_groups(self.L, int(cfg.fwd_tile_groups))
         # fused sampling: the same stratified draw (seed, counter, mass) as per_sample inside the forward
         self.Ls = (h.aql_learn_set_sample(self.L, replay.tree, replay.filled.data_ptr(), self.beta.data_ptr(),
                                           self.step_ctr.data_ptr(), replay.seed ^ 0x51A7,

@@ -202,16 +202,17 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       qb2[t] = N.qf_b2[t];
     }
   }
-  // work items (sample b, candidate tile rt): one per workgroup for the learner; the acting
-  // launch (act_mode) runs a small grid that loops, so the weights staged above (~110 KB of
-  // LDS, one workgroup per CU) are loaded once per workgroup and most CUs stay free for the
-  // learner's kernels running beside it
-  for (int item = blockIdx.x; item < L.B * RT; item += gridDim.x) {
-  const int b = item / RT, rt = item - b * RT;
+  // work items (sample b, group g of its candidate tiles: tiles [g RT / NG, (g + 1) RT / NG)): the
+  // staged weights (~110 KB of LDS, one workgroup per CU), the PER draw and the state half serve
+  // every tile of the group.  The acting launch (act_mode) runs a small grid that loops over the
+  // items, so most CUs stay free for the learner's kernels running beside it
+  const int NG = L.tile_groups > 0 ? min(L.tile_groups, RT) : RT;
+  for (int item = blockIdx.x; item < L.B * NG; item += gridDim.x) {
+  const int b = item / NG, g = item - b * NG, rt0 = g * RT / NG, rt1 = (g + 1) * RT / NG;
   __syncthreads();  // the staging / the previous item is done with sv / xt / stp / qpart / srow
   if (item == blockIdx.x) AQL_STAMP(L, 9);
   if (L.fused_sample) {
-    if (wave == 0) draw(b, rt);
+    if (wave == 0) draw(b, rt0);
     __syncthreads();
   }
   if (item == blockIdx.x) AQL_STAMP(L, 10);
@@ -230,6 +231,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
     __builtin_amdgcn_wave_barrier();
     stp[wave][lane] = lds_dot64(w1 + lane * kP132 + kH, qf[wave], b1e[lane]);
   }
+  for (int rt = rt0; rt < rt1; ++rt) {
   // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
   const int n = 16 * wave + j;
   if (cont) {
@@ -297,6 +299,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       out[(size_t)b * T + tt] = qv;
     }
   }
+  }  // tiles
   }  // work items
   AQL_STAMP(L, 14);
 }
@@ -1086,7 +1089,18 @@ void aql_learn_fwd(const AqlLearn& L, hipStream_t s) {
     throw std::invalid_argument("aql learner: online / target shapes differ");
   if (L.B < 1) return;
   const int RT = (L.on.T + 15) / 16;
-  aql_learn_fwd_k<<<dim3(L.B * RT, 2), 256, 0, s>>>(L);
+  AqlLearn Lk = L;
+  if (Lk.tile_groups <= 0) {  // about one workgroup per CU for the two nets (LDS: one per CU)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      HIP_CHECK(hipGetDevice(&dev));
+      HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    Lk.tile_groups = std::max(1, std::min(RT, cus / (2 * L.B)));
+  }
+  Lk.tile_groups = std::min(Lk.tile_groups, RT);
+  aql_learn_fwd_k<<<dim3(L.B * Lk.tile_groups, 2), 256, 0, s>>>(Lk);
   LAUNCH_CHECK();
 }
 

@@ -632,6 +632,11 @@ PYBIND11_MODULE(_apex_hip, m) {
     L.bw = w;
     return L;
   });
+  m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups) {  // 0: the launcher picks
+    AqlLearn L = L0;
+    L.tile_groups = groups;
+    return L;
+  });
   m.def("aql_noisy_eff", [](const AQLNet& net, uint64_t ws, uint64_t s) { aql_noisy_eff(net, P<float>(ws), S(s)); });
   m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
   m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });

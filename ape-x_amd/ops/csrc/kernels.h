@@ -457,6 +457,9 @@ struct AqlLearn {
   // batched tree write (leaves + every level, B <= 64) beside the per-sample backward
   int bwd_tree;
   BatchWrite bw;
+  // learner forward: candidate-tile groups per (sample, net) workgroup item (0 = about one
+  // workgroup per CU; act_mode: 0 = one tile per item)
+  int tile_groups;
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
 // acting on the learner's MFMA forward: q_s[b][t] = Q_on(st[b], amu[b][t]) for B states

@@ -1,13 +1,20 @@
 #!/bin/bash
-# AQL priority write: extra workgroup of the backward launch (bwd_tree) vs split over the
-# gradient / noise-reset launches -- bit-identity test, then interleaved benches, then a
-# kernel trace of the bwd_tree configuration.
+# AQL learner A/B: priority write in the backward launch (bwd_tree) vs split over the gradient /
+# noise-reset launches, and the forward's tile groups (13 = one tile per workgroup, the old
+# split; 0 = the launcher's choice) -- bit-identity tests, learner-step microbench with phase
+# stamps, interleaved whole-engine benches, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k fused_sampling --timeout 240 \
-  --timeout-method thread > gpurun_out/ab/test.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fused_sampling or tile_groups" \
+  --timeout 240 --timeout-method thread > gpurun_out/ab/test.log 2>&1
 rc=$?; echo "== test rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc
+for g in 13 0 4 2; do
+  APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 0 --groups $g
+  rc=$?; [ $rc -ne 0 ] && exit $rc
+done
+APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 1
+rc=$?; [ $rc -ne 0 ] && exit $rc
 for k in 1 2; do
   for t in 0 1; do
     timeout -k 10 200 python bench.py --algo aql --steps 500 --warmup 20 --aql-bwd-tree $t > gpurun_out/ab/b$t.$k.log 2>&1

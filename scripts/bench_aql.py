@@ -15,12 +15,18 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--fused-step", type=int, default=1, help="one-launch step tail (aql_step_tail_k) or four")
+    ap.add_argument("--bwd-tree", type=int, default=None, help="priority write in the backward launch (1) or not (0)")
+    ap.add_argument("--groups", type=int, default=0, help="forward tile groups per sample (0: the launcher picks)")
     a = ap.parse_args()
     import torch
 
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
-    eng = AQLEngine(AQLEngineConfig(env_id=a.env, capacity=1_000_000, fused_step=bool(a.fused_step)), "cuda:0")
+    cfg = AQLEngineConfig(env_id=a.env, capacity=1_000_000, fused_step=bool(a.fused_step))
+    cfg.fwd_tile_groups = a.groups
+    if a.bwd_tree is not None:
+        cfg.bwd_tree = bool(a.bwd_tree)
+    eng = AQLEngine(cfg, "cuda:0")
     eng.fill(4096)
     L = eng.learner
     L.step()

@@ -317,3 +317,24 @@ def test_fused_sampling_equals_per_sample(cuda):
     for k, other in enumerate(out[1:], 1):
         for name, x, y in zip(names, out[0], other):
             assert torch.equal(x, y), (variants[k], name, (x.double() - y.double()).abs().max().item())
+
+
+def test_forward_tile_groups_bit_identical(cuda):
+    """The learner forward's work split (candidate tiles per workgroup: one, a few, all of a
+    sample's) changes only which workgroup computes a tile: same Q rows, same training."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    out = []
+    for groups in (0, 1, 3, 13):
+        cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=5,
+                              fwd_tile_groups=groups)
+        eng = AQLEngine(cfg, cuda)
+        eng.fill(1024)
+        for _ in range(4):
+            eng.iteration()
+        torch.cuda.synchronize()
+        L = eng.learner
+        out.append((L.q_s.clone(), L.q_s2.clone(), L.qt_s2.clone(), L.idx.clone(), L.flat.clone()))
+    for k in range(1, len(out)):
+        for name, x, y in zip(("q_s", "q_s2", "qt_s2", "idx", "flat"), out[0], out[k]):
+            assert torch.equal(x, y), (k, name)
