@@ -209,6 +209,11 @@ class AQLEngineConfig:
     # per learner step (bit-identical results) -- each grid barrier (~9 us: agent-scope fences
     # write back / invalidate the XCD L2s) costs more than the ~1.5 us kernel boundary it replaces
     fused_step: bool = False
+    # the step's update as ONE launch after the gradient contraction (aql_update_k: both clipped
+    # Adam steps, noise reset of both critics, proposal copy, step bump and the NEXT step's PER
+    # draw, so that forward skips its descent), with the priority write in the backward launch
+    # (implies bwd_tree): four launches per step, no grid barrier
+    fused_update: bool = False
     seed: int = 0
 
 
@@ -320,7 +325,8 @@ class AQLLearner:
                           if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
         self.L_tree = (h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
                                             r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
-                       if cfg.bwd_tree and self.post_tree is None and not cfg.fork_tree and B <= 64 else None)
+                       if (cfg.bwd_tree or cfg.fused_update) and self.post_tree is None and not cfg.fork_tree
+                       and B <= 64 else None)
         split = (cfg.split_tree and self.post_tree is None and self.L_tree is None and not cfg.fork_tree
                  and B <= 64)
         self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
@@ -328,27 +334,37 @@ class AQLLearner:
                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                        if split else None)
         self.post_levels = h.aql_post_set_levels(self.post, r.tree, r.wlist.data_ptr(), B) if split else None
-        self.S = self.S_draw = None
+        self.S = self.S_draw = self.U = self.U_draw = None
+        self.bar = torch.zeros(4, dtype=torch.int32, device=dev)  # arrivals, generation, error flag
+        kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
+                  norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
+                  bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
+                  loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
+                  max_prio=r.max_prio.data_ptr(), alpha=r.alpha)
+        draw_kw = dict(draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=replay.seed ^ 0x51A7,
+                       exclude_last=0 if cfg.exact_mass else 1)
+        nb = h.aql_step_nbytes()
+        self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
         if cfg.fused_step and not cfg.fork_tree and B <= 64:
-            self.bar = torch.zeros(4, dtype=torch.int32, device=dev)  # arrivals, generation, error flag
-            nb = h.aql_step_nbytes()
-            self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
-            kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
-                      norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
-                      bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
-                      loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
-                      max_prio=r.max_prio.data_ptr(), alpha=r.alpha)
             try:
                 self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
             except RuntimeError as e:  # the grid cannot be co-resident on this device: separate launches
                 warnings.warn(f"AQL fused step tail unavailable ({e}); using the separate launches")
             if self.S is not None and self.Ls is not None:  # + the next step's draw (the forward's sampling stream)
-                self.S_draw = h.make_aql_step(
-                    self.L, self.G, self.post, r.tree, self.hp,
-                    dict(kw, draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=replay.seed ^ 0x51A7,
-                         exclude_last=0 if cfg.exact_mass else 1),
-                    self.step_desc[1].data_ptr())
+                self.S_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, dict(kw, **draw_kw),
+                                              self.step_desc[1].data_ptr())
+        if cfg.fused_update and self.S is None and self.L_tree is not None:
+            self.U = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, dict(kw, update=1),
+                                     self.step_desc[0].data_ptr())
+            if self.Ls is not None:
+                self.U_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp,
+                                              dict(kw, update=1, **draw_kw), self.step_desc[1].data_ptr())
         self.refresh()
+
+    @property
+    def predraw(self) -> bool:
+        """Whether a step can draw the next step's rows (fused tail or update launch + fused sampling)."""
+        return self.S_draw is not None or self.U_draw is not None
 
     def refresh(self) -> None:
         """Recompute the effective NoisyLinear weights (mu + sigma * eps) of both networks
@@ -414,7 +430,7 @@ class AQLLearner:
         self.join()  # the sampler reads the tree the previous step's forked write updated
         h, r, s = self.hip, self.replay, self._s()
         if drawn or draw_next:
-            assert self.S_draw is not None, "pre-drawn rows need the fused step tail and fused sampling"
+            assert self.predraw, "pre-drawn rows need the fused step tail / update launch and fused sampling"
         if drawn:
             h.aql_learn_fwd(self.L, s)
         elif self.Ls is not None:  # the forward samples its own rows (one launch fewer)
@@ -448,6 +464,10 @@ class AQLLearner:
         else:
             tree_write(s)
         h.aql_grad(self.G if self.G_tree is None else self.G_tree, s)
+        if self.U is not None:  # optimizers, noise of both critics, proposal copy, next draw: one launch
+            h.aql_update(self.U_draw if draw_next else self.U, s)
+            self._track_losses()
+            return
         Pq, o = self.P_q, 4 * self.P_q
         # the two optimizers (critic, proposal; own clip norms) in one launch
         h.adam_step2((self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
@@ -653,7 +673,7 @@ class AQLEngine:
     def learn_steps(self) -> None:
         """The iteration's K SGD steps; with the fused tail, each step but the last also draws the
         next step's rows (nothing inserts between them), so only the first forward samples."""
-        pre = self.learner.S_draw is not None
+        pre = self.learner.predraw
         for k in range(self.K):
             self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K)
         self.learner.join()  # (a captured graph must end joined)

@@ -791,30 +791,12 @@ __device__ __forceinline__ void noise_elem(const AqlNoise& z, int l, int64_t i, 
 
 constexpr int kStepDrawBlocks = 8;  // phase C workgroups of the next step's draw (4 waves each)
 
-__global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
-  const AqlStep& D = *Dp;
-  const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
-  const int B = D.L.B;
-  const uint64_t st = (uint64_t)D.P.step[0];
-  // ---- phase A
-  if (bid < B) {
-    aql_bwd_block(D.L, bid);
-  } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
-    td_tree_block(D.L, D.tree, D.bw);
-  } else {
-    const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
-    const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
-    for (int64_t i = (int64_t)(bid - B) * 256 + t; i < n2 + n3; i += (int64_t)(G - 1 - B) * 256) {
-      if (i < n2) noise_elem(D.P.layer[2], 2, i, D.P.seed, st);
-      else noise_elem(D.P.layer[3], 3, i - n2, D.P.seed, st);
-    }
-  }
-  grid_sync(D.bar, (unsigned)G, D.err);
-  // ---- phase B
-  float g = 0.f;
-  if (bid < D.nblk) g = aql_grad_block(D.G, bid, D.nblk);
-  grid_sync(D.bar, (unsigned)G, D.err);
-  // ---- phase C
+// phase C of the step for workgroup bid (< nblk: its parameter elements, thread gradient g):
+// both clipped Adam steps, the online noise reset (the thread owning a sigma element also
+// updates its mu partner, then draws the new epsilon and writes mu + sigma eps) and the
+// proposal hard copy online -> target.  Shared by aql_step_tail_k and aql_update_k.
+__device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g, uint64_t st) {
+  const int t = threadIdx.x;
   float lr;
   const AdamRule rule = make_rule(D.hp, (int64_t)st, lr);
   const NormInfo nq = reduce_norms(D.G.part, D.nblk, D.hp.max_norm, D.hp.grad_scale);
@@ -870,14 +852,18 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
       }
     }
   }
-  const int d0 = G - 1 - kStepDrawBlocks;
-  if (D.draw && bid >= d0 && bid < G - 1) {  // block-uniform: the next step's rows, one wave per sample
+}
+
+// the NEXT step's PER draw by draw workgroup k of kStepDrawBlocks (one wave per sample)
+__device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st) {
+  const int t = threadIdx.x, B = D.L.B;
+  if (D.draw && k >= 0 && k < kStepDrawBlocks) {  // block-uniform
     const int lane = t & 63;
     const TreeDesc& tr = D.tree;
     const int64_t f = D.filled[0];
     const int length = (int)(f < (int64_t)tr.size[0] ? f : (int64_t)tr.size[0]);
     const float pmin = tr.node_min[tr.levels - 1][0], beta = D.beta[0];
-    for (int b = (bid - d0) * 4 + (t >> 6); b < B; b += 4 * kStepDrawBlocks) {  // wave-uniform
+    for (int b = k * 4 + (t >> 6); b < B; b += 4 * kStepDrawBlocks) {  // wave-uniform
       float pr;
       const int node = tree_sample_leaf(tr, b, B, length, D.exclude_last, D.seed, st + 1, lane, &pr);
       if (lane == 0) {  // (as aql_learn_fwd_k's fused draw writes them)
@@ -886,16 +872,79 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
       }
     }
   }
-  // the step counter (Adam's bias correction, the noise stream) advances once every block is done
+}
+
+// the step counter (Adam's bias correction, the noise stream) advances once all G workgroups are done
+__device__ __forceinline__ void step_ticket(const AqlPost& P, int G, uint64_t st) {
+  const int t = threadIdx.x;
   __syncthreads();
   if (t == 0) {
     __threadfence();
-    const int tk = atomicAdd(D.P.ticket, 1);
+    const int tk = atomicAdd(P.ticket, 1);
     if (tk == G - 1) {
-      D.P.step[0] = (int64_t)st + 1;
-      D.P.ticket[0] = 0;
+      P.step[0] = (int64_t)st + 1;
+      P.ticket[0] = 0;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
+  const AqlStep& D = *Dp;
+  const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  const int B = D.L.B;
+  const uint64_t st = (uint64_t)D.P.step[0];
+  // ---- phase A
+  if (bid < B) {
+    aql_bwd_block(D.L, bid);
+  } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
+    td_tree_block(D.L, D.tree, D.bw);
+  } else {
+    const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
+    const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
+    for (int64_t i = (int64_t)(bid - B) * 256 + t; i < n2 + n3; i += (int64_t)(G - 1 - B) * 256) {
+      if (i < n2) noise_elem(D.P.layer[2], 2, i, D.P.seed, st);
+      else noise_elem(D.P.layer[3], 3, i - n2, D.P.seed, st);
+    }
+  }
+  grid_sync(D.bar, (unsigned)G, D.err);
+  // ---- phase B
+  float g = 0.f;
+  if (bid < D.nblk) g = aql_grad_block(D.G, bid, D.nblk);
+  grid_sync(D.bar, (unsigned)G, D.err);
+  // ---- phase C
+  update_block(D, bid, g, st);
+  if (D.draw && bid >= G - 1 - kStepDrawBlocks && bid < G - 1) draw_block(D, bid - (G - 1 - kStepDrawBlocks), st);
+  step_ticket(D.P, G, st);
+}
+
+// The step's update as its own launch after aql_grad_k (no grid barrier): blocks [0, nblk) the
+// clipped Adam steps + online noise + proposal copy (update_block, gradients from G.grad), then
+// the target critic's noise reset, then (AqlStep::draw) the next step's PER draw -- the tree is
+// final (the backward launch's priority write, aql_learn_set_tree).  Replaces opt_step2_k +
+// aql_post_k with the same arithmetic (bit-identical, tests/test_gpu_aql_engine.py).
+int aql_update_noise_blocks(const AqlStep& d) {
+  const int64_t n = (int64_t)d.P.layer[2].out * d.P.layer[2].in + d.P.layer[2].out +
+                    (int64_t)d.P.layer[3].out * d.P.layer[3].in + d.P.layer[3].out;
+  return (int)((n + 255) / 256);
+}
+
+__global__ __launch_bounds__(256) void aql_update_k(const AqlStep* __restrict__ Dp, int noise_blocks) {
+  const AqlStep& D = *Dp;
+  const int bid = blockIdx.x, t = threadIdx.x;
+  const uint64_t st = (uint64_t)D.P.step[0];
+  if (bid < D.nblk) {
+    const int64_t i = (int64_t)bid * 256 + t;
+    update_block(D, bid, i < D.n ? D.G.grad[i] : 0.f, st);
+  } else if (bid < D.nblk + noise_blocks) {
+    const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
+    const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
+    const int64_t i = (int64_t)(bid - D.nblk) * 256 + t;
+    if (i < n2) noise_elem(D.P.layer[2], 2, i, D.P.seed, st);
+    else if (i < n2 + n3) noise_elem(D.P.layer[3], 3, i - n2, D.P.seed, st);
+  } else {
+    draw_block(D, bid - D.nblk - noise_blocks, st);
+  }
+  step_ticket(D.P, (int)gridDim.x, st);
 }
 
 // ------------------------------------------------------------------ vector envs
@@ -1156,7 +1205,7 @@ void aql_post(const AqlPost& p, int regen, hipStream_t s) {
 
 int aql_step_grid(const AqlStep& d) { return std::max(d.nblk, d.L.B + 1) + 1 + kStepDrawBlocks; }
 
-void aql_step_check(const AqlStep& d) {
+void aql_step_check(const AqlStep& d, bool coresident) {
   check_net(d.L.on);
   const AqlGrad& G = d.G;
   if (d.nblk != aql_grad_blocks(G.n) || d.n != G.n || G.tree_leaves)
@@ -1177,6 +1226,7 @@ void aql_step_check(const AqlStep& d) {
     for (int64_t o : {d.mu_b[k], d.sig_b[k]})
       if (o < 0 || o + nb > d.P_q) throw std::invalid_argument("aql_step: online noisy biases outside the critic");
   }
+  if (!coresident) return;  // (aql_update: an ordinary grid)
   int dev = 0, cus = 0, per_cu = 0;
   HIP_CHECK(hipGetDevice(&dev));
   HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -1188,6 +1238,17 @@ void aql_step_check(const AqlStep& d) {
 
 void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s) {
   aql_step_tail_k<<<grid, 256, 0, s>>>(dev);
+  LAUNCH_CHECK();
+}
+
+int aql_update_grid(const AqlStep& d, int* noise_blocks) {
+  const int nb = aql_update_noise_blocks(d);
+  if (noise_blocks) *noise_blocks = nb;
+  return d.nblk + nb + (d.draw ? kStepDrawBlocks : 0);
+}
+
+void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s) {
+  aql_update_k<<<grid, 256, 0, s>>>(dev, noise_blocks);
   LAUNCH_CHECK();
 }
 

@@ -747,8 +747,11 @@ PYBIND11_MODULE(_apex_hip, m) {
   struct AqlStepHandle {
     const AqlStep* dev;
     int grid;
+    int update;        // 1: the separate update launch (aql_update), not the fused tail
+    int noise_blocks;  // aql_update: target-noise workgroups
   };
-  py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid);
+  py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid)
+      .def_readonly("update", &AqlStepHandle::update);
   m.def("aql_step_nbytes", []() { return sizeof(AqlStep); });
   m.def("make_aql_step", [](const AqlLearn& L, const AqlGrad& G, const AqlPost& Pst, const TreeHandle& t,
                             const AdamParams& hp, py::dict p, uint64_t desc) {
@@ -785,11 +788,21 @@ PYBIND11_MODULE(_apex_hip, m) {
       d.seed = g("seed");
       d.exclude_last = p["exclude_last"].cast<int>();
     }
-    aql_step_check(d);
+    const int upd = p.contains("update") ? p["update"].cast<int>() : 0;
+    aql_step_check(d, !upd);
     HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));
-    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), aql_step_grid(d)};
+    int nb = 0;
+    const int grid = upd ? aql_update_grid(d, &nb) : aql_step_grid(d);
+    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, upd, nb};
   });
-  m.def("aql_step_tail", [](const AqlStepHandle& h, uint64_t s) { aql_step_tail(h.dev, h.grid, S(s)); });
+  m.def("aql_step_tail", [](const AqlStepHandle& h, uint64_t s) {
+    if (h.update) throw std::invalid_argument("aql_step_tail: an update handle (use aql_update)");
+    aql_step_tail(h.dev, h.grid, S(s));
+  });
+  m.def("aql_update", [](const AqlStepHandle& h, uint64_t s) {
+    if (!h.update) throw std::invalid_argument("aql_update: a fused-tail handle (use aql_step_tail)");
+    aql_update(h.dev, h.grid, h.noise_blocks, S(s));
+  });
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

@@ -548,8 +548,14 @@ struct AqlStep {
   int exclude_last;
 };
 int aql_step_grid(const AqlStep& d);
-void aql_step_check(const AqlStep& d);  // shapes, pointers, and that the grid fits co-resident
+// shapes, pointers, and (coresident) that the fused tail's grid fits co-resident
+void aql_step_check(const AqlStep& d, bool coresident = true);
 void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s);
+// The step's update as its own launch after aql_grad (aql_update_k: both clipped Adam steps,
+// noise reset of both critics, proposal copy, optional next-step draw, step bump) -- replaces
+// adam_step2 + aql_post when the priority write ran in the backward launch
+int aql_update_grid(const AqlStep& d, int* noise_blocks);
+void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s);
 struct AqlEnv {
   int kind;            // 0 BipedalWalker-shaped, 1 CartPole, 2 Pendulum
   int E, obs, adim, T, max_steps;

@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
     ap.add_argument("--aql-bwd-tree", type=int, default=None,
                     help="AQL: priority write in the backward launch (1) or split over grad/post (0)")
+    ap.add_argument("--aql-fused-update", type=int, default=None,
+                    help="AQL: optimizers + noise + next draw as one launch after the gradients (1) or not (0)")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=560.0,
@@ -383,6 +385,8 @@ def aql(args, rank, world, device):
                           actor_offset=rank * args.envs, total_actors=world * args.envs, overlap=args.aql_overlap)
     if args.aql_bwd_tree is not None:
         cfg.bwd_tree = bool(args.aql_bwd_tree)
+    if args.aql_fused_update is not None:
+        cfg.fused_update = bool(args.aql_fused_update)
     eng = AQLEngine(cfg, device)
     t_fill = time.perf_counter()
     eng.fill(max(1024, 4 * args.envs))

@@ -1,28 +1,27 @@
 #!/bin/bash
-# AQL learner A/B: priority write in the backward launch (bwd_tree) vs split over the gradient /
-# noise-reset launches, and the forward's tile groups (13 = one tile per workgroup, the old
-# split; 0 = the launcher's choice) -- bit-identity tests, learner-step microbench with phase
-# stamps, interleaved whole-engine benches, then a kernel trace.
+# AQL learner A/B: priority write in the backward launch (bwd_tree), the optimizers + noise +
+# next draw as one launch (fused_update), the forward's tile groups (13 = one tile per
+# workgroup, the old split; 0 = the launcher's choice) -- bit-identity tests, learner-step
+# microbench with phase stamps, interleaved whole-engine benches, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/ab
 timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fused_sampling or tile_groups" \
   --timeout 240 --timeout-method thread > gpurun_out/ab/test.log 2>&1
 rc=$?; echo "== test rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc
-for g in 13 0 4 2; do
-  APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 0 --groups $g
+for v in "--groups 13" "--groups 0" "--groups 4" "--groups 2" "--bwd-tree 1" "--fused-update 1"; do
+  echo "== bench_aql $v"
+  APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 0 $v
   rc=$?; [ $rc -ne 0 ] && exit $rc
 done
-APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 1
-rc=$?; [ $rc -ne 0 ] && exit $rc
 for k in 1 2; do
-  for t in 0 1; do
-    timeout -k 10 200 python bench.py --algo aql --steps 500 --warmup 20 --aql-bwd-tree $t > gpurun_out/ab/b$t.$k.log 2>&1
-    rc=$?; [ $rc -ne 0 ] && { echo "bench rc=$rc"; tail -5 gpurun_out/ab/b$t.$k.log; exit $rc; }
-    echo "bwd_tree=$t: $(grep -o '"value": [0-9.]*' gpurun_out/ab/b$t.$k.log)"
+  for v in "--aql-fused-update 0 --aql-bwd-tree 0" "--aql-fused-update 0 --aql-bwd-tree 1" "--aql-fused-update 1"; do
+    timeout -k 10 200 python bench.py --algo aql --steps 500 --warmup 20 $v > gpurun_out/ab/b.log 2>&1
+    rc=$?; [ $rc -ne 0 ] && { echo "bench rc=$rc"; tail -5 gpurun_out/ab/b.log; exit $rc; }
+    echo "$v: $(grep -o '"value": [0-9.]*' gpurun_out/ab/b.log)"
   done
 done
 R=$(pwd)
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/ab/prof -o run -- \
-  python3 $R/bench.py --algo aql --steps 200 --warmup 10 --aql-bwd-tree 1 > $R/gpurun_out/ab/prof.log 2>&1
+  python3 $R/bench.py --algo aql --steps 200 --warmup 10 --aql-fused-update 1 > $R/gpurun_out/ab/prof.log 2>&1

@@ -274,21 +274,24 @@ def test_fused_sampling_equals_per_sample(cuda):
     """The learner forward's own PER draw (fused_sample) == per_sample + forward, the priority
     write folded into the noise-reset launch (fused_tree) or split over the gradient and
     noise-reset launches (split_tree) or run as an extra workgroup of the backward (bwd_tree)
-    == its own launch, and the whole step tail in one
+    == its own launch, the optimizers + noise + proposal copy + next draw as one launch
+    (fused_update) == the separate launches, and the whole step tail in one
     grid-synchronised launch (fused_step: backward, tree write, gradients, both Adam steps,
     noise reset, proposal copy) == the separate launches: same rows, IS weights, tree, loss,
     parameters, moments, noise and target after several iterations, bit for bit."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    variants = ((False, False, False, False, False), (True, False, False, False, False),
-                (True, True, False, False, False), (True, False, True, False, False),
-                (True, False, False, True, False), (False, False, False, True, False),
-                (True, False, False, False, True), (False, False, False, False, True))
-    for fused_sample, fused_tree, split_tree, fused_step, bwd_tree in variants:
+    # (fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update)
+    variants = ((False, False, False, False, False, False), (True, False, False, False, False, False),
+                (True, True, False, False, False, False), (True, False, True, False, False, False),
+                (True, False, False, True, False, False), (False, False, False, True, False, False),
+                (True, False, False, False, True, False), (False, False, False, False, True, False),
+                (True, False, False, False, False, True), (False, False, False, False, False, True))
+    for fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update in variants:
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
                               fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree,
-                              fused_step=fused_step, bwd_tree=bwd_tree)
+                              fused_step=fused_step, bwd_tree=bwd_tree, fused_update=fused_update)
         eng = AQLEngine(cfg, cuda)
         L = eng.learner
         assert (L.Ls is not None) == fused_sample
@@ -296,7 +299,9 @@ def test_fused_sampling_equals_per_sample(cuda):
         if not fused_step:
             assert (L.post_tree is not None) == fused_tree
             assert (L.G_tree is not None) == split_tree
-            assert (L.L_tree is not None) == bwd_tree
+            assert (L.L_tree is not None) == (bwd_tree or fused_update)
+            assert (L.U is not None) == fused_update
+            assert L.predraw == (fused_update and fused_sample)
         else:
             assert L.S.grid >= max(L.nblk, L.B + 1) + 1
         eng.fill(1024)
