@@ -643,6 +643,9 @@ __device__ __forceinline__ int opaque_i(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
+// kDiag (microbench diagnostics only, scripts/bench_f32.py --c1-diag): 1 = no MFMA (fragments
+// folded by one VALU op each), 2 = no output stores, 3 = no frame staging (stale LDS)
+template <int kDiag>
 __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
   const int B = set.B, total = set.n * B;
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   // problem boundary (a grid-strided walk crossed one at every sample: ~25 % of the VALU)
   const int per = (total + gridDim.x - 1) / gridDim.x;
   const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
-  if (s0 < s1) c1x_load(set, s0, v);
+  if (kDiag != 3 && s0 < s1) c1x_load(set, s0, v);
   for (int smp = s0; smp < s1; ++smp) {
     const int prob = smp / B, b = smp - prob * B;
     const F32Prob p = pick(set, prob);
@@ -665,9 +668,9 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       split_w1(p.w + (nh * 16 + i) * 256 + (q >> 1) * 16 + (q & 1) * 4, w);
     }
     __syncthreads();  // the previous sample's tiles are done with xs
-    c1x_store(v, xs);
+    if (kDiag != 3) c1x_store(v, xs);
     __syncthreads();
-    if (smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
+    if (kDiag != 3 && smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
     // roles swapped on the MFMA (A = the weight slice, B = the pixels: identical lane maps),
     // so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte store
     float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
@@ -696,6 +699,10 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       f32x4 ah = zero4(), am = zero4(), al = zero4();
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
+        if (kDiag == 1) {
+          ah[kb & 3] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, a[kb]).x);
+          continue;
+        }
         ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.hi[kb], a[kb], ah, 0, 0, 0);
         am = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.mid[kb], a[kb], am, 0, 0, 0);
         al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.lo[kb], a[kb], al, 0, 0, 0);
@@ -705,7 +712,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       y.y = fmaxf(ah[1] + (am[1] + al[1]) + bias4.y, 0.f);
       y.z = fmaxf(ah[2] + (am[2] + al[2]) + bias4.z, 0.f);
       y.w = fmaxf(ah[3] + (am[3] + al[3]) + bias4.w, 0.f);
-      *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
+      if (kDiag != 2 || y.x == 12345.678f) *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
     };
     // ping-pong fragment buffers: the next tile's LDS reads are in flight during this tile's MFMAs.
     // Wave parity t0 owns tiles t0, t0 + 2, ...: 6 pairs (+ tile 24 for t0 = 0); every fragment
@@ -1291,8 +1298,14 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
   check_set(set);
   switch (layer) {
     case 1:
-      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
+    {
+      const int g = std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid);
+      if (tile == 11) f32_conv1_fwd_x3_k<1><<<g, 256, 0, s>>>(set);
+      else if (tile == 12) f32_conv1_fwd_x3_k<2><<<g, 256, 0, s>>>(set);
+      else if (tile == 13) f32_conv1_fwd_x3_k<3><<<g, 256, 0, s>>>(set);
+      else f32_conv1_fwd_x3_k<0><<<g, 256, 0, s>>>(set);
       LAUNCH_CHECK();
+    }
       break;
     case 2:  // learner: 64 x 64 tiles at BK 32: 79.0-80.4 us vs 87.0-88.5 for 128 x 64 at BK 16
              // (3 x 512 samples, interleaved on one box; the BK-16 pitch conflicts on the stores)
