@@ -652,10 +652,11 @@ class AQLEngine:
 
     def _act(self, h, s, E) -> None:
         """Proposal, candidate Q and epsilon-greedy selection for all E envs."""
+        mfma = self.cfg.act_q == "mfma"  # (the effective weights ride along in the proposal launch)
         h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
-                      self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s)
-        if self.cfg.act_q == "mfma":
-            h.aql_noisy_eff(self.actor_net, self.ws.data_ptr(), s)
+                      self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s,
+                      self.ws.data_ptr() if mfma else 0)
+        if mfma:
             h.aql_act_q(self.actL, s)
         else:
             h.aql_candidate_q(self.actor_net, self.ws.data_ptr(), self.obs_buf.data_ptr(), self.amu.data_ptr(), E,

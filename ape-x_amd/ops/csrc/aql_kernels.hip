@@ -19,6 +19,7 @@
 
 namespace apex {
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int AQ_H = 64;        // hidden units of q_feature / action_out / advantage1
 constexpr int AQ_CAT = 128;     // concat width
 constexpr int AQ_PITCH = 129;   // LDS row pitch (floats) for 128-wide rows
@@ -27,16 +28,10 @@ constexpr int kAqGroup = 8;     // candidates per work item of aql_candidate_q_k
 // workspace layout (floats): W1eff [64][128] | b1eff [64] | w2eff [64] | b2eff [1]
 size_t aql_workspace_floats() { return AQ_H * AQ_CAT + AQ_H + AQ_H + 1; }
 
+__device__ __forceinline__ void noisy_eff_elem(const AQLNet& net, float* __restrict__ ws, int i);
+
 __global__ void aql_noisy_eff_k(AQLNet net, float* __restrict__ ws) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n1 = AQ_H * AQ_CAT;
-  auto eff = [&](const float* mu, const float* sg, const float* ep, int k) {
-    return net.noisy ? mu[k] + sg[k] * ep[k] : mu[k];
-  };
-  if (i < n1) ws[i] = eff(net.a1_wmu, net.a1_wsig, net.a1_weps, i);
-  else if (i < n1 + AQ_H) ws[i] = eff(net.a1_bmu, net.a1_bsig, net.a1_beps, i - n1);
-  else if (i < n1 + 2 * AQ_H) ws[i] = eff(net.a2_wmu, net.a2_wsig, net.a2_weps, i - n1 - AQ_H);
-  else if (i == n1 + 2 * AQ_H) ws[i] = eff(net.a2_bmu, net.a2_bsig, net.a2_beps, 0);
+  noisy_eff_elem(net, ws, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 __global__ __launch_bounds__(256) void aql_candidate_q_k(AQLNet net, const float* __restrict__ ws,
@@ -114,80 +109,137 @@ __global__ __launch_bounds__(256) void aql_candidate_q_k(AQLNet net, const float
   }
 }
 
-__global__ __launch_bounds__(64) void aql_propose_k(AQLNet net, const float* __restrict__ state, int B,
-                                                    const float* __restrict__ low, const float* __restrict__ high,
-                                                    const float* __restrict__ var, uint64_t seed,
-                                                    const int64_t* __restrict__ counter, float* __restrict__ a_mu,
-                                                    float* __restrict__ mu_out) {
-  __shared__ float emb[AQ_CAT];
-  __shared__ float hid[AQ_CAT];
-  __shared__ float mu[64];
-  __shared__ int perm[64];
-  const int b = blockIdx.x, lane = threadIdx.x;
-  if (b >= B) return;
-  const float* s = state + (size_t)b * net.obs;
-  // state embedding: features = Linear(obs -> 128) + ReLU (model.py:289-291)
-  for (int j = lane; j < AQ_CAT; j += 64) {
+// Four states per 256-thread workgroup: dist_feature.0's weight [128][128] is staged in LDS once
+// per workgroup (pitch 132: lane j's 16-byte row reads cover all 64 banks per 16 lanes) -- one
+// wave per state read it from global with a 512-byte lane stride (64 cache lines per load,
+// ~14 us for 256 states).  Same fma order as the one-wave-per-state version: bit-identical.
+// Blocks past prop_blocks compute the acting net's effective NoisyLinear weights (aql_noisy_eff)
+// into eff_ws when it is given, so the acting chain has one launch fewer.
+constexpr int kPropStates = 4, kPropPitch = 132;
+
+__device__ __forceinline__ void noisy_eff_elem(const AQLNet& net, float* __restrict__ ws, int i) {
+  const int n1 = AQ_H * AQ_CAT;
+  auto eff = [&](const float* mu, const float* sg, const float* ep, int k) {
+    return net.noisy ? mu[k] + sg[k] * ep[k] : mu[k];
+  };
+  if (i < 0) return;
+  if (i < n1) ws[i] = eff(net.a1_wmu, net.a1_wsig, net.a1_weps, i);
+  else if (i < n1 + AQ_H) ws[i] = eff(net.a1_bmu, net.a1_bsig, net.a1_beps, i - n1);
+  else if (i < n1 + 2 * AQ_H) ws[i] = eff(net.a2_wmu, net.a2_wsig, net.a2_weps, i - n1 - AQ_H);
+  else if (i == n1 + 2 * AQ_H) ws[i] = eff(net.a2_bmu, net.a2_bsig, net.a2_beps, 0);
+}
+
+__global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __restrict__ state, int B,
+                                                     const float* __restrict__ low, const float* __restrict__ high,
+                                                     const float* __restrict__ var, uint64_t seed,
+                                                     const int64_t* __restrict__ counter, float* __restrict__ a_mu,
+                                                     float* __restrict__ mu_out, float* __restrict__ eff_ws,
+                                                     int prop_blocks) {
+  if ((int)blockIdx.x >= prop_blocks) {  // block-uniform: the fused effective-weight blocks
+    noisy_eff_elem(net, eff_ws, ((int)blockIdx.x - prop_blocks) * 256 + (int)threadIdx.x);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) float w1[AQ_CAT * kPropPitch];
+  __shared__ __attribute__((aligned(16))) float emb[kPropStates][AQ_CAT], hid[kPropStates][AQ_CAT];
+  __shared__ float mu[kPropStates][64];
+  __shared__ int perm[kPropStates][64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b0 = blockIdx.x * kPropStates;
+  {  // stage dist_feature.0 [128][128]: every load in flight before the stores
+    if ((reinterpret_cast<uintptr_t>(net.df_w1) & 15) == 0) {  // block-uniform
+      const f32x4* src = reinterpret_cast<const f32x4*>(net.df_w1);
+      f32x4 v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = src[t + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e4 = t + 256 * k, r = e4 >> 5, c = (e4 & 31) * 4;
+        *reinterpret_cast<f32x4*>(&w1[r * kPropPitch + c]) = v[k];
+      }
+    } else {
+      for (int e = t; e < AQ_CAT * AQ_CAT; e += 256) w1[(e >> 7) * kPropPitch + (e & 127)] = net.df_w1[e];
+    }
+  }
+  // state embedding: features = Linear(obs -> 128) + ReLU (model.py:289-291); thread (j, half):
+  // states half, half + 2 of the workgroup (clamped past B: computed, never written out)
+  const int j = t & 127, hs = t >> 7;
+#pragma unroll
+  for (int s2 = hs; s2 < kPropStates; s2 += 2) {
+    const float* sp = state + (size_t)min(b0 + s2, B - 1) * net.obs;
     float acc = net.f_b[j];
-    for (int i = 0; i < net.obs; ++i) acc += net.f_w[j * net.obs + i] * s[i];
-    emb[j] = fmaxf(acc, 0.f);
+    for (int i = 0; i < net.obs; ++i) acc += net.f_w[j * net.obs + i] * sp[i];
+    emb[s2][j] = fmaxf(acc, 0.f);
   }
   __syncthreads();
   // dist_feature: Linear(128 -> 128) + ReLU + Linear(128 -> A)
-  for (int j = lane; j < AQ_CAT; j += 64) {
-    float acc = net.df_b1[j];
-    for (int i = 0; i < AQ_CAT; ++i) acc += net.df_w1[j * AQ_CAT + i] * emb[i];
-    hid[j] = fmaxf(acc, 0.f);
+  {
+    const float bj = net.df_b1[j];
+    float a0 = bj, a1 = bj;
+    const float* wr = w1 + j * kPropPitch;
+#pragma unroll 8
+    for (int i = 0; i < AQ_CAT; i += 4) {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(wr + i);
+      const f32x4 e0 = *reinterpret_cast<const f32x4*>(&emb[hs][i]);
+      const f32x4 e1 = *reinterpret_cast<const f32x4*>(&emb[hs + 2][i]);
+      a0 += w[0] * e0[0]; a0 += w[1] * e0[1]; a0 += w[2] * e0[2]; a0 += w[3] * e0[3];
+      a1 += w[0] * e1[0]; a1 += w[1] * e1[1]; a1 += w[2] * e1[2]; a1 += w[3] * e1[3];
+    }
+    hid[hs][j] = fmaxf(a0, 0.f);
+    hid[hs + 2][j] = fmaxf(a1, 0.f);
   }
   __syncthreads();
   const int A = net.na;  // continuous: action dim; discrete: number of actions
+  const int b = b0 + wave;  // sampling: one wave per state
+  const bool valid = b < B;
   if (lane < A) {
     float acc = net.df_b2[lane];
-    for (int i = 0; i < AQ_CAT; ++i) acc += net.df_w2[lane * AQ_CAT + i] * hid[i];
-    mu[lane] = acc;
-    if (mu_out) mu_out[(size_t)b * A + lane] = acc;
+    for (int i = 0; i < AQ_CAT; ++i) acc += net.df_w2[lane * AQ_CAT + i] * hid[wave][i];
+    mu[wave][lane] = acc;
+    if (mu_out && valid) mu_out[(size_t)b * A + lane] = acc;
   }
   __syncthreads();
   const uint64_t ctr = counter ? (uint64_t)counter[0] : 0ull;
-  const int U = net.uniform, P = net.propose, T = net.T;
+  const int U = net.uniform, T = net.T;
   float u[4];
   if (net.cont) {
+    if (!valid) return;
     float* out = a_mu + (size_t)b * T * A;
     for (int e = lane; e < T * A; e += 64) {
-      const int t = e / A, d = e % A;
+      const int tt = e / A, d = e % A;
       uniform4(seed, (uint64_t)b * 4096 + e, ctr, u);
-      out[e] = t < U ? low[d] + (high[d] - low[d]) * u[0] : mu[d] + sqrtf(var[d]) * std_normal(u[1], u[2]);
+      out[e] = tt < U ? low[d] + (high[d] - low[d]) * u[0] : mu[wave][d] + sqrtf(var[d]) * std_normal(u[1], u[2]);
     }
   } else {
-    float* out = a_mu + (size_t)b * T;
-    if (lane == 0) {  // uniform without replacement: partial Fisher-Yates over 0..A-1
-      for (int i = 0; i < A; ++i) perm[i] = i;
+    if (lane == 0 && valid) {  // uniform without replacement: partial Fisher-Yates over 0..A-1
+      for (int i = 0; i < A; ++i) perm[wave][i] = i;
       for (int i = 0; i < U; ++i) {
         uniform4(seed, (uint64_t)b * 4096 + 4000 + i, ctr, u);
-        const int j = i + min((int)(u[0] * (float)(A - i)), A - i - 1);
-        const int tmp = perm[i];
-        perm[i] = perm[j];
-        perm[j] = tmp;
+        const int jj = i + min((int)(u[0] * (float)(A - i)), A - i - 1);
+        const int tmp = perm[wave][i];
+        perm[wave][i] = perm[wave][jj];
+        perm[wave][jj] = tmp;
       }
     }
     __syncthreads();
+    if (!valid) return;
+    float* out = a_mu + (size_t)b * T;
     float mx = -INFINITY;
-    for (int i = 0; i < A; ++i) mx = fmaxf(mx, mu[i]);
+    for (int i = 0; i < A; ++i) mx = fmaxf(mx, mu[wave][i]);
     float z = 0.f;
-    for (int i = 0; i < A; ++i) z += expf(mu[i] - mx);
-    for (int t = lane; t < T; t += 64) {
-      if (t < U) {
-        out[t] = (float)perm[t];
+    for (int i = 0; i < A; ++i) z += expf(mu[wave][i] - mx);
+    for (int tt = lane; tt < T; tt += 64) {
+      if (tt < U) {
+        out[tt] = (float)perm[wave][tt];
       } else {  // inverse-CDF categorical sample of softmax(logits)
-        uniform4(seed, (uint64_t)b * 4096 + t, ctr, u);
+        uniform4(seed, (uint64_t)b * 4096 + tt, ctr, u);
         const float target = u[0] * z;
         float c = 0.f;
         int k = A - 1;
         for (int i = 0; i < A; ++i) {
-          c += expf(mu[i] - mx);
+          c += expf(mu[wave][i] - mx);
           if (c > target) { k = i; break; }
         }
-        out[t] = (float)k;
+        out[tt] = (float)k;
       }
     }
   }
@@ -237,11 +289,13 @@ void aql_noisy_eff(const AQLNet& net, float* ws, hipStream_t s) {
 }
 
 void aql_propose(const AQLNet& net, const float* state, int B, const float* low, const float* high, const float* var,
-                 uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s) {
+                 uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s, float* eff_ws) {
   if (B <= 0) return;
   if (net.na < 1 || net.na > 64) throw std::invalid_argument("aql_propose: 1 <= actions <= 64");
   if (!net.cont && net.uniform > net.na) throw std::invalid_argument("aql_propose: uniform > actions (discrete)");
-  aql_propose_k<<<B, 64, 0, s>>>(net, state, B, low, high, var, seed, counter, a_mu, mu_out);
+  const int pb = (B + kPropStates - 1) / kPropStates;
+  const int eb = eff_ws ? (int)((aql_workspace_floats() + 255) / 256) : 0;
+  aql_propose_k<<<pb + eb, 256, 0, s>>>(net, state, B, low, high, var, seed, counter, a_mu, mu_out, eff_ws, pb);
   LAUNCH_CHECK();
 }
 

@@ -556,11 +556,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     aql_candidate_q(n, P<float>(ws), P<const float>(state), P<const float>(a_mu), B, P<float>(q), S(s));
   });
   m.def("aql_propose", [](const AQLNet& n, uint64_t state, int B, uint64_t low, uint64_t high, uint64_t var,
-                          uint64_t seed, uint64_t counter, uint64_t a_mu, uint64_t mu_out, uint64_t s) {
+                          uint64_t seed, uint64_t counter, uint64_t a_mu, uint64_t mu_out, uint64_t s,
+                          uint64_t eff_ws) {
     if (!n.f_w || !n.df_w1 || !n.df_w2) throw std::invalid_argument("aql_propose: proposal weights missing");
     aql_propose(n, P<const float>(state), B, P<const float>(low), P<const float>(high), P<const float>(var), seed,
-                P<const int64_t>(counter), P<float>(a_mu), P<float>(mu_out), S(s));
-  });
+                P<const int64_t>(counter), P<float>(a_mu), P<float>(mu_out), S(s), P<float>(eff_ws));
+  }, py::arg("net"), py::arg("state"), py::arg("B"), py::arg("low"), py::arg("high"), py::arg("var"), py::arg("seed"),
+     py::arg("counter"), py::arg("a_mu"), py::arg("mu_out"), py::arg("s"), py::arg("eff_ws") = 0);
   // ---- GPU AQL engine (aql_engine_kernels.hip): descriptors built once, per-step calls take a stream
   py::class_<AqlLearn>(m, "AqlLearn");
   m.def("make_aql_learn", [](const AQLNet& on, const AQLNet& tg, py::dict p, int B, float gamma_n, float ent_lam) {

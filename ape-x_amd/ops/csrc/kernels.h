@@ -413,7 +413,8 @@ void aql_noisy_eff(const AQLNet& net, float* ws, hipStream_t s);  // W_eff = mu 
 void aql_candidate_q(const AQLNet& net, float* ws, const float* state, const float* a_mu, int B, float* q,
                      hipStream_t s);
 void aql_propose(const AQLNet& net, const float* state, int B, const float* low, const float* high, const float* var,
-                 uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s);
+                 uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s,
+                 float* eff_ws = nullptr);  // + aql_noisy_eff into eff_ws (extra workgroups)
 void aql_select(const float* q, const float* a_mu, int B, int T, int adim, const float* eps, uint64_t seed,
                 const int64_t* counter, int* act_idx, float* env_act, hipStream_t s);
 

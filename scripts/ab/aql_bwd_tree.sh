@@ -5,7 +5,7 @@
 # microbench with phase stamps, interleaved whole-engine benches, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fused_sampling or tile_groups" \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fused_sampling or tile_groups or propose or acting" \
   --timeout 240 --timeout-method thread > gpurun_out/ab/test.log 2>&1
 rc=$?; echo "== test rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc

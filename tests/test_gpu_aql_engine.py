@@ -343,3 +343,31 @@ def test_forward_tile_groups_bit_identical(cuda):
     for k in range(1, len(out)):
         for name, x, y in zip(("q_s", "q_s2", "qt_s2", "idx", "flat"), out[0], out[k]):
             assert torch.equal(x, y), (k, name)
+
+
+@pytest.mark.parametrize("env_id", ["BipedalWalker-v3", "CartPole-v0"])
+def test_propose_mu_matches_fp64_and_fused_eff(cuda, env_id):
+    """aql_propose (four states per workgroup, dist_feature.0 staged in LDS): the proposal mean
+    against the fp64 reference Proposal_Network, and the effective-weight workgroups riding in
+    the same launch == aql_noisy_eff, with the candidate sets unchanged by them."""
+    eng = _engine(cuda, env_id, fill=256)
+    h, s = eng.hip, torch.cuda.current_stream().cuda_stream
+    E = eng.E
+    ref = copy.deepcopy(eng.actor_model).double()
+    with torch.no_grad():
+        mu64 = ref.proposal.dist_feature(ref.q.embedding_feature(eng.obs_buf.double()))
+    A = mu64.shape[1]
+    mu = torch.zeros(E, A, device=cuda)
+    h.aql_propose(eng.actor_net, eng.obs_buf.data_ptr(), E, eng.low.data_ptr(), eng.high.data_ptr(),
+                  eng.var.data_ptr(), 77, eng.actor_ctr.data_ptr(), eng.amu.data_ptr(), mu.data_ptr(), s)
+    h.aql_noisy_eff(eng.actor_net, eng.ws.data_ptr(), s)
+    torch.cuda.synchronize()
+    am0, ws0 = eng.amu.clone(), eng.ws.clone()
+    err = float((mu.double() - mu64).abs().max() / mu64.abs().max().clamp_min(1e-30))
+    assert err < 1e-5, err
+    eng.ws.zero_()
+    h.aql_propose(eng.actor_net, eng.obs_buf.data_ptr(), E, eng.low.data_ptr(), eng.high.data_ptr(),
+                  eng.var.data_ptr(), 77, eng.actor_ctr.data_ptr(), eng.amu.data_ptr(), 0, s, eng.ws.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(eng.amu, am0)
+    assert torch.equal(eng.ws, ws0)
