@@ -368,13 +368,16 @@ __device__ __forceinline__ float lds_row_dot(const float* Wl, int n8, const floa
 struct AqlTd {
   float dl, lw, gq;
 };
-__device__ __forceinline__ AqlTd aql_td(const AqlLearn& L, int b, int row, int a_idx, int s_next) {
-  const int T = L.on.T;
-  const float qa = L.q_s[(size_t)b * T + a_idx], qt = L.qt_s2[(size_t)b * T + s_next];
-  const float y = L.rew[row] + L.gamma_n * qt * (1.f - L.done[row]);
-  const float diff = y - qa, dl = fabsf(diff), wb = L.w[b];
+__device__ __forceinline__ AqlTd aql_td_vals(const AqlLearn& L, float qa, float qt, float r, float dn, float wb) {
+  const float y = r + L.gamma_n * qt * (1.f - dn);
+  const float diff = y - qa, dl = fabsf(diff);
   const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
   return AqlTd{dl, wb * (dl < 1.f ? 0.5f * dl * dl : dl - 0.5f), -sg * fminf(dl, 1.f) * wb / (float)L.B};
+}
+__device__ __forceinline__ AqlTd aql_td(const AqlLearn& L, int b, int row, int a_idx, int s_next) {
+  const int T = L.on.T;
+  return aql_td_vals(L, L.q_s[(size_t)b * T + a_idx], L.qt_s2[(size_t)b * T + s_next], L.rew[row], L.done[row],
+                     L.w[b]);
 }
 
 // the backward of sample b by one workgroup (aql_learn_bwd_k, or phase A of aql_step_tail_k)
@@ -581,17 +584,57 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
 // rows (aql_td: the formula the backward writes L.delta / L.lw with), then the batched tree
 // write (leaves, mix, loss mean, every level).  Only the next step's sampler reads the tree.
 __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc& tree, BatchWrite w) {
-  __shared__ float s_dl[64], s_lw[64], tred[16];
-  __shared__ int sids[64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, T = L.on.T;
-  for (int b = wave; b < L.B; b += (int)(blockDim.x >> 6)) {  // wave-uniform
-    const int s_next = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
-    if (lane == 0) {
-      const int row = L.idx[b];
-      const AqlTd td = aql_td(L, b, row, L.act[row], s_next);
-      s_dl[b] = td.dl;
-      s_lw[b] = td.lw;
+  __shared__ float s_dl[64], s_lw[64], tred[16], s_qa[64], s_r[64], s_dn[64], s_wb[64];
+  __shared__ int sids[64], s_next[64];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = (int)(blockDim.x >> 6), T = L.on.T, B = L.B;
+  // the B TD terms with every sample's loads in flight together (a wave-per-sample loop paid ~4
+  // dependent round trips per sample, ~29 us for 32 samples): the scalar chains idx -> act ->
+  // Q(s, a) on one thread per sample, the argmaxes of Q(s', .) 4 samples per wave at a time
+  if (t < B) {
+    const int row = L.idx[t];
+    s_qa[t] = L.q_s[(size_t)t * T + L.act[row]];
+    s_r[t] = L.rew[row];
+    s_dn[t] = L.done[row];
+    s_wb[t] = L.w[t];
+  }
+  if (T <= 256) {
+    for (int b0 = wave * 4; b0 < B; b0 += 4 * nw) {  // wave-uniform
+      float v[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* row = L.q_s2 + (size_t)min(b0 + j, B - 1) * T;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[j][k] = row[min(lane + 64 * k, T - 1)];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // ascending t per lane, as wave_argmax
+          const int tt = lane + 64 * k;
+          if (tt < T && (v[j][k] > bv || (v[j][k] == bv && tt < bi))) { bv = v[j][k]; bi = tt; }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ov = __shfl_xor(bv, o, 64);
+          const int oi = __shfl_xor(bi, o, 64);
+          if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        }
+        if (lane == 0 && b0 + j < B) s_next[b0 + j] = bi == 0x7fffffff ? 0 : bi;
+      }
     }
+  } else {
+    for (int b = wave; b < B; b += nw) {
+      const int sn = wave_argmax(L.q_s2 + (size_t)b * T, T, lane);
+      if (lane == 0) s_next[b] = sn;
+    }
+  }
+  __syncthreads();
+  if (t < B) {
+    const AqlTd td = aql_td_vals(L, s_qa[t], L.qt_s2[(size_t)t * T + s_next[t]], s_r[t], s_dn[t], s_wb[t]);
+    s_dl[t] = td.dl;
+    s_lw[t] = td.lw;
   }
   __syncthreads();
   w.mix.delta = s_dl;

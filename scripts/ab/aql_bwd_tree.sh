@@ -1,7 +1,6 @@
 #!/bin/bash
 # AQL learner A/B: priority write in the backward launch (bwd_tree), the optimizers + noise +
-# next draw as one launch (fused_update), the forward's tile groups (13 = one tile per
-# workgroup, the old split; 0 = the launcher's choice) -- bit-identity tests, learner-step
+# next draw as one launch (fused_update) vs the split write -- bit-identity tests, learner-step
 # microbench with phase stamps, interleaved whole-engine benches, then a kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/ab
@@ -9,9 +8,9 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fus
   --timeout 240 --timeout-method thread > gpurun_out/ab/test.log 2>&1
 rc=$?; echo "== test rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc
-for v in "--groups 13" "--groups 0" "--groups 4" "--groups 2" "--bwd-tree 1" "--fused-update 1"; do
+for v in "--bwd-tree 0" "--bwd-tree 1" "--fused-update 1"; do
   echo "== bench_aql $v"
-  APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 --bwd-tree 0 $v
+  APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 $v
   rc=$?; [ $rc -ne 0 ] && exit $rc
 done
 for k in 1 2; do
