@@ -598,15 +598,30 @@ __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
 constexpr int kC1xGrid = 512;
 constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
 
-// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on)
-__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer]) {
-  const int B = set.B, prob = smp / B, b = smp - prob * B, t = threadIdx.x;
+// plane byte offsets (from the problem's frame base) of up to kC1xWin samples, resolved by
+// 4 kC1xWin threads at once: frame_plane's idx -> ids chain is two dependent round trips, which
+// paid per sample in front of the next sample's chunk loads stalled every wave ~29 of the
+// kernel's 49 us (no-staging diagnostic: 20 us)
+constexpr int kC1xWin = 17;  // a 16-sample window + the next window's first sample (prefetched)
+__device__ __forceinline__ void c1x_resolve(const F32Set& set, int smp, int s1, int64_t* planes) {
+  const int t = threadIdx.x, sm = smp + (t >> 2);
+  if (t < 4 * kC1xWin && sm < s1) {
+    const int B = set.B, prob = sm / B, b = sm - prob * B;
+    const F32Prob p = pick(set, prob);
+    const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
+    planes[t] = frame_plane(f, b, t & 3, kPlane) - static_cast<const uint8_t*>(p.in);
+  }
+}
+
+// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on); pl: its 4 plane offsets
+__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer], const int64_t* pl) {
+  const int B = set.B, prob = smp / B, t = threadIdx.x;
   const F32Prob p = pick(set, prob);
-  const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
-  const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
-  const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
-  const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
-  const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
+  const uint8_t* base = static_cast<const uint8_t*>(p.in);
+  const uint4* s0 = reinterpret_cast<const uint4*>(base + pl[0]);
+  const uint4* s1 = reinterpret_cast<const uint4*>(base + pl[1]);
+  const uint4* s2 = reinterpret_cast<const uint4*>(base + pl[2]);
+  const uint4* s3 = reinterpret_cast<const uint4*>(base + pl[3]);
 #pragma unroll
   for (int k = 0; k < kC1xPer; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
     const int e = min(t + 256 * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
@@ -648,6 +663,7 @@ __device__ __forceinline__ int opaque_i(int x) {
 template <int kDiag>
 __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
+  __shared__ int64_t planes[4 * kC1xWin];
   const int B = set.B, total = set.n * B;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int i = lane & 15, q = lane >> 4, nh = wave >> 1;
@@ -659,7 +675,10 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
   // problem boundary (a grid-strided walk crossed one at every sample: ~25 % of the VALU)
   const int per = (total + gridDim.x - 1) / gridDim.x;
   const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
-  if (kDiag != 3 && s0 < s1) c1x_load(set, s0, v);
+  int win = s0;  // first sample of the resolved plane window
+  c1x_resolve(set, s0, s1, planes);
+  __syncthreads();
+  if (kDiag != 3 && s0 < s1) c1x_load(set, s0, v, planes);
   for (int smp = s0; smp < s1; ++smp) {
     const int prob = smp / B, b = smp - prob * B;
     const F32Prob p = pick(set, prob);
@@ -667,10 +686,15 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       cur = prob;
       split_w1(p.w + (nh * 16 + i) * 256 + (q >> 1) * 16 + (q & 1) * 4, w);
     }
-    __syncthreads();  // the previous sample's tiles are done with xs
+    if (smp + 1 - win >= kC1xWin) {  // block-uniform: the next window (this sample and on)
+      __syncthreads();  // every wave is past its last read of the old window
+      win = smp;
+      c1x_resolve(set, win, s1, planes);
+    }
+    __syncthreads();  // the previous sample's tiles are done with xs (and the window is written)
     if (kDiag != 3) c1x_store(v, xs);
     __syncthreads();
-    if (kDiag != 3 && smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
+    if (kDiag != 3 && smp + 1 < s1) c1x_load(set, smp + 1, v, planes + 4 * (smp + 1 - win));  // in flight during the MFMA loop
     // roles swapped on the MFMA (A = the weight slice, B = the pixels: identical lane maps),
     // so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte store
     float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
