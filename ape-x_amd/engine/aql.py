@@ -193,7 +193,9 @@ class AQLEngineConfig:
     split_tree: bool = True
     # priority write as an extra workgroup of the BACKWARD launch (it recomputes the B TD terms
     # from the forward's Q rows): the leaves and the level walk run beside the per-sample
-    # backward instead of bounding the gradient / noise-reset launches (replaces split_tree)
+    # backward instead of bounding the gradient / noise-reset launches (replaces split_tree).
+    # Alone it measured even with split_tree (14825-14850 vs 14751-14754 SGD steps/s); it is what
+    # lets fused_update draw the next step's rows
     bwd_tree: bool = False
     # learner forward: candidate-tile groups per (sample, net) workgroup (0 = about one workgroup
     # per CU: the ~110 KB weight staging, the PER draw and the state MLP serve a group of tiles)
@@ -212,8 +214,10 @@ class AQLEngineConfig:
     # the step's update as ONE launch after the gradient contraction (aql_update_k: both clipped
     # Adam steps, noise reset of both critics, proposal copy, step bump and the NEXT step's PER
     # draw, so that forward skips its descent), with the priority write in the backward launch
-    # (implies bwd_tree): four launches per step, no grid barrier
-    fused_update: bool = False
+    # (implies bwd_tree): four launches per step, no grid barrier.  MI355X, batch 32, interleaved:
+    # 15577-15580 vs 14751-14754 SGD steps/s for the split write + separate launches
+    # (scripts/ab/aql_bwd_tree.sh; learner step 51.4 vs 55.7 us in scripts/bench_aql.py)
+    fused_update: bool = True
     seed: int = 0
 
 
