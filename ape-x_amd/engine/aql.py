@@ -218,6 +218,10 @@ class AQLEngineConfig:
     # 15577-15580 vs 14751-14754 SGD steps/s for the split write + separate launches
     # (scripts/ab/aql_bwd_tree.sh; learner step 51.4 vs 55.7 us in scripts/bench_aql.py)
     fused_update: bool = True
+    # with the priority write in the backward launch: its extra workgroup writes the leaves only
+    # and the gradient launch's extra workgroup walks the levels (the whole write on one
+    # workgroup outlasted the backward: 23.4 vs 13.6 us)
+    tree_levels_in_grad: bool = True
     seed: int = 0
 
 
@@ -327,10 +331,12 @@ class AQLLearner:
                                               self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
                                               r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
                           if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
+        bwd = (cfg.bwd_tree or cfg.fused_update) and self.post_tree is None and not cfg.fork_tree and B <= 64
+        lv = bwd and cfg.tree_levels_in_grad
         self.L_tree = (h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
-                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
-                       if (cfg.bwd_tree or cfg.fused_update) and self.post_tree is None and not cfg.fork_tree
-                       and B <= 64 else None)
+                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha,
+                                            levels=0 if lv else 1) if bwd else None)
+        self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B) if lv else None
         split = (cfg.split_tree and self.post_tree is None and self.L_tree is None and not cfg.fork_tree
                  and B <= 64)
         self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
@@ -467,7 +473,7 @@ class AQLLearner:
             self._tree_pending = True
         else:
             tree_write(s)
-        h.aql_grad(self.G if self.G_tree is None else self.G_tree, s)
+        h.aql_grad(self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G), s)
         if self.U is not None:  # optimizers, noise of both critics, proposal copy, next draw: one launch
             h.aql_update(self.U_draw if draw_next else self.U, s)
             self._track_losses()

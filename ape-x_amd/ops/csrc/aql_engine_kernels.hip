@@ -583,7 +583,7 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
 // this step's priority write by one workgroup: the B TD terms recomputed from the forward's Q
 // rows (aql_td: the formula the backward writes L.delta / L.lw with), then the batched tree
 // write (leaves, mix, loss mean, every level).  Only the next step's sampler reads the tree.
-__device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc& tree, BatchWrite w) {
+__device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc& tree, BatchWrite w, int levels) {
   __shared__ float s_dl[64], s_lw[64], tred[16], s_qa[64], s_r[64], s_dn[64], s_wb[64];
   __shared__ int sids[64], s_next[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = (int)(blockDim.x >> 6), T = L.on.T, B = L.B;
@@ -639,12 +639,12 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   __syncthreads();
   w.mix.delta = s_dl;
   w.mix.lw = s_lw;
-  batch_leaves_block(tree, w, 1, tred, sids);
+  batch_leaves_block(tree, w, levels, tred, sids);
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   if (L.bwd_tree && blockIdx.x == L.B) {  // block-uniform: the priority write (aql_learn_set_tree)
-    td_tree_block(L, L.tree, L.bw);
+    td_tree_block(L, L.tree, L.bw, L.bwd_tree == 1);
     return;
   }
   aql_bwd_block(L, blockIdx.x);
@@ -719,10 +719,15 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   if (G.tree_leaves && blockIdx.x == gridDim.x - 1) {  // block-uniform: the split tree write's leaves
     __shared__ float tred[16];
     __shared__ int sids[64];
-    batch_leaves_block(G.tree, G.bw, 0, tred, sids);
+    if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
+      for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
+      update_levels_block(G.tree, sids, G.bw.B, 1, G.tree.levels);
+    } else {
+      batch_leaves_block(G.tree, G.bw, 0, tred, sids);
+    }
     return;
   }
-  aql_grad_block(G, blockIdx.x, (int)gridDim.x - G.tree_leaves);
+  aql_grad_block(G, blockIdx.x, (int)gridDim.x - (G.tree_leaves ? 1 : 0));
 }
 
 // ------------------------------------------------------------------ noise reset + proposal copy
@@ -763,6 +768,22 @@ __device__ __forceinline__ void aql_post_block(const AqlPost& P, int regen, uint
   if (i >= 0 && i < P.n_copy) P.dst[i] = P.src[i];
 }
 
+// the step counter (Adam's bias correction, the noise stream) advances once all G workgroups are
+// done with it.  No fence before the ticket: a workgroup's only obligation is to have READ the
+// counter (consumed long before), and the new value reaches later launches at the kernel
+// boundary -- an agent-scope release per workgroup wrote the XCD L2s back every step
+__device__ __forceinline__ void step_ticket(const AqlPost& P, int G, uint64_t st) {
+  const int t = threadIdx.x;
+  __syncthreads();
+  if (t == 0) {
+    const int tk = atomicAdd(P.ticket, 1);
+    if (tk == G - 1) {
+      P.step[0] = (int64_t)st + 1;
+      P.ticket[0] = 0;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
   const uint64_t st = (uint64_t)P.step[0];
   if (regen && P.tree_write && blockIdx.x == gridDim.x - 1) {  // block-uniform: the fused tree write
@@ -778,15 +799,7 @@ __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
     aql_post_block(P, regen, st);
   }
   if (!regen) return;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const int tk = atomicAdd(P.ticket, 1);
-    if (tk == (int)gridDim.x - 1) {
-      P.step[0] = (int64_t)st + 1;
-      P.ticket[0] = 0;
-    }
-  }
+  step_ticket(P, (int)gridDim.x, st);
 }
 
 // ------------------------------------------------------------------ fused step tail
@@ -917,20 +930,6 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
   }
 }
 
-// the step counter (Adam's bias correction, the noise stream) advances once all G workgroups are done
-__device__ __forceinline__ void step_ticket(const AqlPost& P, int G, uint64_t st) {
-  const int t = threadIdx.x;
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    const int tk = atomicAdd(P.ticket, 1);
-    if (tk == G - 1) {
-      P.step[0] = (int64_t)st + 1;
-      P.ticket[0] = 0;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
   const AqlStep& D = *Dp;
   const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
@@ -940,7 +939,7 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
   if (bid < B) {
     aql_bwd_block(D.L, bid);
   } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
-    td_tree_block(D.L, D.tree, D.bw);
+    td_tree_block(D.L, D.tree, D.bw, 1);
   } else {
     const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
     const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
@@ -1230,7 +1229,7 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
     if (J.goff < 0 || J.goff + J.rows > aqlv::STRIDE || J.xoff + J.cols > aqlv::STRIDE)
       throw std::invalid_argument("aql_grad: vector offsets");
   }
-  if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || g.bw.E != 0 || !g.bw.idx || !g.bw.list))
+  if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || g.bw.E != 0 || (g.tree_leaves == 1 && !g.bw.idx) || !g.bw.list))
     throw std::invalid_argument("aql_grad: the split tree write takes 1..64 learner rows and no actor rows");
   aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), kGradThreads, 0, s>>>(g);
   LAUNCH_CHECK();

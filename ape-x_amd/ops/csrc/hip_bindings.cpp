@@ -617,7 +617,7 @@ PYBIND11_MODULE(_apex_hip, m) {
   });
   // the priority write as an extra workgroup of the backward launch (replaces the split write)
   m.def("aql_learn_set_tree", [](const AqlLearn& L0, const TreeHandle& t, uint64_t prio_out, uint64_t loss_out,
-                                 uint64_t owner, uint64_t list, uint64_t max_prio, float alpha) {
+                                 uint64_t owner, uint64_t list, uint64_t max_prio, float alpha, int levels) {
     AqlLearn L = L0;
     BatchWrite w{};
     w.idx = L.idx;
@@ -629,10 +629,22 @@ PYBIND11_MODULE(_apex_hip, m) {
     w.alpha = alpha;
     if (!w.idx || !w.owner || !w.list || !w.max_prio || L.B < 1 || L.B > 64)
       throw std::invalid_argument("aql_learn_set_tree: 1 <= B <= 64 and every pointer");
-    L.bwd_tree = 1;
+    L.bwd_tree = levels ? 1 : 2;
     L.tree = t.d;
     L.bw = w;
     return L;
+  }, py::arg("L"), py::arg("tree"), py::arg("prio_out"), py::arg("loss_out"), py::arg("owner"), py::arg("list"),
+     py::arg("max_prio"), py::arg("alpha"), py::arg("levels") = 1);
+  m.def("aql_grad_set_levels", [](const AqlGrad& g0, const TreeHandle& t, uint64_t list, int B) {
+    AqlGrad g = g0;
+    BatchWrite w{};
+    w.list = P<int>(list);
+    w.B = B;
+    if (!w.list || B < 1 || B > 64) throw std::invalid_argument("aql_grad_set_levels: 1 <= B <= 64 and a list");
+    g.tree_leaves = 2;
+    g.tree = t.d;
+    g.bw = w;
+    return g;
   });
   m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups) {  // 0: the launcher picks
     AqlLearn L = L0;

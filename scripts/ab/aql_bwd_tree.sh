@@ -8,13 +8,13 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_aql_engine.py -x -q -k "fus
   --timeout 240 --timeout-method thread > gpurun_out/ab/test.log 2>&1
 rc=$?; echo "== test rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc
-for v in "--bwd-tree 0" "--bwd-tree 1" "--fused-update 1"; do
+for v in "--fused-update 0" "--fused-update 1 --levels-in-grad 0" "--fused-update 1 --levels-in-grad 1"; do
   echo "== bench_aql $v"
   APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 $v
   rc=$?; [ $rc -ne 0 ] && exit $rc
 done
 for k in 1 2; do
-  for v in "--aql-fused-update 0 --aql-bwd-tree 0" "--aql-fused-update 0 --aql-bwd-tree 1" "--aql-fused-update 1"; do
+  for v in "--aql-fused-update 0" "--aql-fused-update 1 --aql-levels-in-grad 0" "--aql-fused-update 1 --aql-levels-in-grad 1"; do
     timeout -k 10 200 python bench.py --algo aql --steps 500 --warmup 20 $v > gpurun_out/ab/b.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "bench rc=$rc"; tail -5 gpurun_out/ab/b.log; exit $rc; }
     echo "$v: $(grep -o '"value": [0-9.]*' gpurun_out/ab/b.log)"

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--fused-step", type=int, default=1, help="one-launch step tail (aql_step_tail_k) or four")
     ap.add_argument("--bwd-tree", type=int, default=None, help="priority write in the backward launch (1) or not (0)")
     ap.add_argument("--fused-update", type=int, default=None, help="update launch after the gradients (1) or not")
+    ap.add_argument("--levels-in-grad", type=int, default=None, help="tree levels in the gradient launch (1) or not")
     ap.add_argument("--groups", type=int, default=0, help="forward tile groups per sample (0: the launcher picks)")
     a = ap.parse_args()
     import torch
@@ -25,6 +26,8 @@ def main():
 
     cfg = AQLEngineConfig(env_id=a.env, capacity=1_000_000, fused_step=bool(a.fused_step))
     cfg.fwd_tile_groups = a.groups
+    if a.levels_in_grad is not None:
+        cfg.tree_levels_in_grad = bool(a.levels_in_grad)
     if a.fused_update is not None:
         cfg.fused_update = bool(a.fused_update)
     if a.bwd_tree is not None:
