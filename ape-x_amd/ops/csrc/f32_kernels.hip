@@ -603,9 +603,10 @@ constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256
 // paid per sample in front of the next sample's chunk loads stalled every wave ~29 of the
 // kernel's 49 us (no-staging diagnostic: 20 us)
 constexpr int kC1xWin = 17;  // a 16-sample window + the next window's first sample (prefetched)
+template <int WIN = kC1xWin>
 __device__ __forceinline__ void c1x_resolve(const F32Set& set, int smp, int s1, int64_t* planes) {
   const int t = threadIdx.x, sm = smp + (t >> 2);
-  if (t < 4 * kC1xWin && sm < s1) {
+  if (t < 4 * WIN && sm < s1) {
     const int B = set.B, prob = sm / B, b = sm - prob * B;
     const F32Prob p = pick(set, prob);
     const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
@@ -613,8 +614,10 @@ __device__ __forceinline__ void c1x_resolve(const F32Set& set, int smp, int s1, 
   }
 }
 
-// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on); pl: its 4 plane offsets
-__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer], const int64_t* pl) {
+// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on); pl: its 4 plane
+// offsets; NT threads, ceil(1764 / NT) chunks each
+template <int NT = 256, int PER = (kC1xChunks + NT - 1) / NT>
+__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[PER], const int64_t* pl) {
   const int B = set.B, prob = smp / B, t = threadIdx.x;
   const F32Prob p = pick(set, prob);
   const uint8_t* base = static_cast<const uint8_t*>(p.in);
@@ -623,19 +626,20 @@ __device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[
   const uint4* s2 = reinterpret_cast<const uint4*>(base + pl[2]);
   const uint4* s3 = reinterpret_cast<const uint4*>(base + pl[3]);
 #pragma unroll
-  for (int k = 0; k < kC1xPer; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
-    const int e = min(t + 256 * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
+  for (int k = 0; k < PER; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
+    const int e = min(t + NT * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
     const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
     v[k] = sc[e - c * 441];
   }
 }
 
 // registers -> LDS as bf16: chunk e = bf16 elements 16e .. 16e + 15 (7056 = 441 x 16)
-__device__ __forceinline__ void c1x_store(const uint4 (&v)[kC1xPer], uint32_t* xs) {
+template <int NT = 256, int PER = (kC1xChunks + NT - 1) / NT>
+__device__ __forceinline__ void c1x_store(const uint4 (&v)[PER], uint32_t* xs) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < kC1xPer; ++k) {
-    const int e = t + 256 * k;
+  for (int k = 0; k < PER; ++k) {
+    const int e = t + NT * k;
     if (e < kC1xChunks) {
       const f32x4 a = u8x4(v[k].x), bq = u8x4(v[k].y), c = u8x4(v[k].z), d = u8x4(v[k].w);
       uint4* dst = reinterpret_cast<uint4*>(xs) + 2 * e;
@@ -753,6 +757,96 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
       tile_mfma(tile + 2, fb);
     }
     if (t0 == 0) tile_mfma(24, fa);
+  }
+}
+
+// Double-buffered variant: one 512-thread workgroup per CU (2 x 56 KB of planes), 8 waves =
+// 2 channel halves x 4 tile residues (tiles r, r + 4, ...: 7 / 6 each), 2 waves per SIMD.  The
+// NEXT sample's planes are converted into the other buffer from inside this sample's MFMA loop
+// (after the first tile: the VALU conversion and the LDS stores issue between MFMAs of the same
+// wave), and the sample after that is loaded right behind them -- the single-buffered kernel
+// staged between two barriers with the MFMAs idle (no-staging diagnostic: 20 of its 46 us).
+constexpr int kC1dGrid = 256, kC1dWin = 18;  // window: 16 samples + the two prefetched
+__global__ __launch_bounds__(512, 1) void f32_conv1_fwd_db_k(F32Set set) {
+  __shared__ __attribute__((aligned(16))) uint32_t xs[2][2 * kPlaneDw * 4];  // 2 x 4 planes of bf16
+  __shared__ int64_t planes[4 * kC1dWin];
+  constexpr int NT = 512, PER = (kC1xChunks + NT - 1) / NT;
+  const int B = set.B, total = set.n * B;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i = lane & 15, q = lane >> 4, nh = wave & 1, part = wave >> 1;
+  const int nt = part == 0 ? 7 : 6;  // this wave's tiles: part + 4k, k < nt (25 tiles)
+  W1Split w;
+  int cur = -1;
+  uint4 v[PER];
+  const int per = (total + gridDim.x - 1) / gridDim.x;
+  const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
+  if (s0 >= s1) return;  // block-uniform
+  int win = s0;
+  c1x_resolve<kC1dWin>(set, s0, s1, planes);
+  __syncthreads();
+  c1x_load<NT>(set, s0, v, planes);
+  c1x_store<NT>(v, xs[0]);
+  if (s0 + 1 < s1) c1x_load<NT>(set, s0 + 1, v, planes + 4);
+  __syncthreads();
+  for (int smp = s0; smp < s1; ++smp) {
+    const int prob = smp / B, b = smp - prob * B, buf = (smp - s0) & 1;
+    const F32Prob p = pick(set, prob);
+    if (prob != cur) {  // block-uniform
+      cur = prob;
+      split_w1(p.w + (nh * 16 + i) * 256 + (q >> 1) * 16 + (q & 1) * 4, w);
+    }
+    if (smp + 2 - win >= kC1dWin) {  // block-uniform: the next window (this sample and on)
+      win = smp;
+      c1x_resolve<kC1dWin>(set, win, s1, planes);
+      __syncthreads();
+    }
+    const __bf16* xb = reinterpret_cast<const __bf16*>(xs[buf]);
+    float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
+    float4 bias4;
+    bias4.x = p.bias[nh * 16 + 4 * q];
+    bias4.y = p.bias[nh * 16 + 4 * q + 1];
+    bias4.z = p.bias[nh * 16 + 4 * q + 2];
+    bias4.w = p.bias[nh * 16 + 4 * q + 3];
+    auto frags = [&](int tile, bfx8 (&a)[8]) {  // as f32_conv1_fwd_x3_k
+      const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
+      const __bf16* a0 = xb + (4 * oy + 2 * (q >> 1)) * 84 + 4 * ox + 4 * (q & 1);
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
+        const uint2 lo = ap[0], hi = ap[opaque_i(21)];
+        a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    };
+    auto tile_mfma = [&](int tile, const bfx8 (&a)[8]) {
+      f32x4 ah = zero4(), am = zero4(), al = zero4();
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.hi[kb], a[kb], ah, 0, 0, 0);
+        am = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.mid[kb], a[kb], am, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.lo[kb], a[kb], al, 0, 0, 0);
+      }
+      float4 y;
+      y.x = fmaxf(ah[0] + (am[0] + al[0]) + bias4.x, 0.f);
+      y.y = fmaxf(ah[1] + (am[1] + al[1]) + bias4.y, 0.f);
+      y.z = fmaxf(ah[2] + (am[2] + al[2]) + bias4.z, 0.f);
+      y.w = fmaxf(ah[3] + (am[3] + al[3]) + bias4.w, 0.f);
+      *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
+    };
+    bfx8 fa[8], fb[8];
+    frags(part, fa);
+#pragma unroll
+    for (int pr = 0; pr < 3; ++pr) {
+      frags(part + 4 * (2 * pr + 1), fb);
+      tile_mfma(part + 4 * (2 * pr), fa);
+      if (pr == 0 && smp + 1 < s1) {  // block-uniform: stage the next sample, load the one after
+        c1x_store<NT>(v, xs[buf ^ 1]);
+        if (smp + 2 < s1) c1x_load<NT>(set, smp + 2, v, planes + 4 * (smp + 2 - win));
+      }
+      frags(part + 4 * min(2 * pr + 2, nt - 1), fa);  // (parts 1-3 re-read their last tile at the end: unused)
+      tile_mfma(part + 4 * (2 * pr + 1), fb);
+    }
+    if (nt == 7) tile_mfma(part + 24, fa);
+    __syncthreads();  // the next sample's buffer is complete; this one's reads are done
   }
 }
 
@@ -1324,7 +1418,8 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
     case 1:
     {
       const int g = std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid);
-      if (tile == 11) f32_conv1_fwd_x3_k<1><<<g, 256, 0, s>>>(set);
+      if (tile == 20) f32_conv1_fwd_db_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1dGrid), 512, 0, s>>>(set);
+      else if (tile == 11) f32_conv1_fwd_x3_k<1><<<g, 256, 0, s>>>(set);
       else if (tile == 12) f32_conv1_fwd_x3_k<2><<<g, 256, 0, s>>>(set);
       else if (tile == 13) f32_conv1_fwd_x3_k<3><<<g, 256, 0, s>>>(set);
       else f32_conv1_fwd_x3_k<0><<<g, 256, 0, s>>>(set);
