@@ -152,54 +152,61 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   // (measured: drawing on wave 0 WHILE waves 1-3 stage the weights was slower than the two in
   // sequence -- 25.4k vs 18.0k cycles: the descent's dependent loads queue behind the staging
   // traffic in the CU's memory pipeline)
-  {  // stage the two 64x128 matrices with 16-byte loads, all in flight before the stores
+  {  // stage every weight with ALL loads in flight before the first store (in separate groups,
+     // each group's stores waited out its loads before the next group's loads issued: ~3 serial
+     // global round trips): the two 64x128 matrices as 16-byte loads, q_feature.0 / .2 (clamped
+     // column index: unconditional loads; .0's columns past obs stored as zeros), action_out.0
+     // and the bias vectors
     const f32x4* a4 = reinterpret_cast<const f32x4*>(N.ao_w2);
     const f32x4* w4 = reinterpret_cast<const f32x4*>(eff);
+    const int nao1 = cont ? kCat : kH;
     f32x4 va[8], vw[8];
+    float x1[16], x2[16], y1[4];  // action_out.0: nao1 * adim <= 128 x 8
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (cont) va[k] = a4[t + 256 * k];
       vw[k] = w4[t + 256 * k];
     }
 #pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      x1[k] = N.qf_w1[r * obs + min(i, obs - 1)];
+      x2[k] = N.qf_w2[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) y1[k] = N.ao_w1[min(t + 256 * k, nao1 * adim - 1)];
+    const float b_ao1 = N.ao_b1[min(t, nao1 - 1)], b_ao2 = cont ? N.ao_b2[t & 63] : 0.f;
+    const float b_w2 = eff[kEffW2 + (t & 63)], b_b1 = eff[kEffB1 + (t & 63)];
+    const float b_q1 = N.qf_b1[t & 63], b_q2 = N.qf_b2[t & 63];
+#pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int e4 = t + 256 * k, r = e4 >> 5, c = (e4 & 31) * 4;
       if (cont) *reinterpret_cast<f32x4*>(&ao2[r * kP132 + c]) = va[k];
       *reinterpret_cast<f32x4*>(&w1[r * kP132 + c]) = vw[k];
     }
-  }
-  {
-    // first-layer rows zero-padded to whole 8-column blocks (branch-free, unrolled dot
-    // products: a runtime-length loop of LDS loads serialised one LDS latency per term)
-    {  // both 64-row matrices, every load in flight before the stores (clamped column index:
-       // unconditional loads; q_feature.0's columns past obs stored as zeros)
-      float x1[16], x2[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = t + 256 * k, r = e >> 6, i = e & 63;
-        x1[k] = N.qf_w1[r * obs + min(i, obs - 1)];
-        x2[k] = N.qf_w2[e];
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int e = t + 256 * k, r = e >> 6, i = e & 63;
-        qw1[r * kP68 + i] = i < obs ? x1[k] : 0.f;
-        qw2[r * kP68 + i] = x2[k];
-      }
+    for (int k = 0; k < 16; ++k) {
+      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+      qw1[r * kP68 + i] = i < obs ? x1[k] : 0.f;
+      qw2[r * kP68 + i] = x2[k];
     }
-    const int nao1 = cont ? kCat : kH;
-    for (int e = t; e < nao1 * adim; e += 256) ao1w[(e / adim) * kMaxAdim + e % adim] = N.ao_w1[e];
+    // action_out.0 [n][adim] -> [n][8] zero-padded
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = t + 256 * k;
+      if (e < nao1 * adim) ao1w[(e / adim) * kMaxAdim + e % adim] = y1[k];
+    }
     for (int e = t; e < nao1 * (kMaxAdim - adim); e += 256) {
       const int r = e / (kMaxAdim - adim);
       ao1w[r * kMaxAdim + adim + (e - r * (kMaxAdim - adim))] = 0.f;
     }
-    if (t < nao1) ao1b[t] = N.ao_b1[t];
+    if (t < nao1) ao1b[t] = b_ao1;
     if (t < kH) {
-      if (cont) ao2b[t] = N.ao_b2[t];
-      w2e[t] = eff[kEffW2 + t];
-      b1e[t] = eff[kEffB1 + t];
-      qb1[t] = N.qf_b1[t];
-      qb2[t] = N.qf_b2[t];
+      if (cont) ao2b[t] = b_ao2;
+      w2e[t] = b_w2;
+      b1e[t] = b_b1;
+      qb1[t] = b_q1;
+      qb2[t] = b_q2;
     }
   }
   // work items (sample b, group g of its candidate tiles: tiles [g RT / NG, (g + 1) RT / NG)): the
@@ -223,6 +230,16 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   }
   __syncthreads();
   if (item == blockIdx.x) AQL_STAMP(L, 11);
+  // continuous candidates: this lane's action row of a tile (clamped, unconditional loads; zeroed
+  // past adim at use), loaded one tile ahead -- the first before the state MLP, so no tile waits
+  // out a global round trip in front of its encoder
+  float avn[kMaxAdim];
+  auto load_av = [&](int rtx) {
+    const float* am = L.amu + ((size_t)row * T + min(rtx * 16 + j, T - 1)) * adim;
+#pragma unroll
+    for (int d = 0; d < kMaxAdim; ++d) avn[d] = am[min(d, adim - 1)];
+  };
+  if (cont) load_av(rt0);
   // state halves, from LDS: wave si < nst handles state si (q_feature MLP, W1[:, 64:] . qf + b1)
   if (wave < nst) {
     hq[wave][lane] = relu(lds_dot64(qw1 + lane * kP68, sv[wave], qb1[lane]));  // (zero past obs)
@@ -234,12 +251,11 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   for (int rt = rt0; rt < rt1; ++rt) {
   // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
   const int n = 16 * wave + j;
-  if (cont) {
-    const int r = min(rt * 16 + j, T - 1);  // tail rows recompute a valid candidate (discarded)
-    const float* am = L.amu + ((size_t)row * T + r) * adim;
+  if (cont) {  // (tail rows recompute a valid candidate, discarded)
     float av[kMaxAdim];
 #pragma unroll
-    for (int d = 0; d < kMaxAdim; ++d) av[d] = d < adim ? am[d] : 0.f;
+    for (int d = 0; d < kMaxAdim; ++d) av[d] = d < adim ? avn[d] : 0.f;
+    if (rt + 1 < rt1) load_av(rt + 1);
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll 4
     for (int k0 = 0; k0 < kCat; k0 += 8) {
