@@ -26,8 +26,6 @@ ap.add_argument("--json", action="store_true")
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 128x64 BK 16, "
                                                    "conv2/conv3 input gradient BK 32")
-ap.add_argument("--c1-db", action="store_true", help="+ conv1 forward double-buffered (bit-identity checked)")
-ap.add_argument("--c1-diag", action="store_true", help="+ conv1 forward diagnostics (no MFMA / stores / staging)")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
@@ -124,13 +122,6 @@ if a.tile1:
     cases["conv2_bwd@t1"] = ((lambda: hip.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), net.w2t.data_ptr(),
                                                        ws.a1.data_ptr(), ws.dy1.data_ptr(), w2.data_ptr(), B, S(),
                                                        tile=1)), 2 * 2 * B * 81 * 64 * 512)
-if a.c1_db:  # conv1 forward, double-buffered 512-thread workgroups
-    cases["conv1_fwd@db"] = ((lambda: hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=20)), 2 * P * 400 * 32 * 256)
-    mismatch_check.append(("conv1_fwd", "conv1_fwd@db", lambda: wss[0].a1))
-if a.c1_diag:  # conv1 forward without MFMA / without stores / without staging (results garbage)
-    for code, nm in ((11, "nomfma"), (12, "nostore"), (13, "nostage")):
-        cases[f"conv1_fwd@{nm}"] = ((lambda code=code: hip.f32_conv_fwd_multi(1, set3(1), B, S(), tile=code)),
-                                   2 * P * 400 * 32 * 256)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)
