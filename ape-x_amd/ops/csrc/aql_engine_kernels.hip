@@ -737,7 +737,7 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
     __shared__ int sids[64];
     if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
       for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
-      update_levels_block(G.tree, sids, G.bw.B, 1, G.tree.levels);
+      update_levels_fast(G.tree, sids, G.bw.B);
     } else {
       batch_leaves_block(G.tree, G.bw, 0, tred, sids);
     }

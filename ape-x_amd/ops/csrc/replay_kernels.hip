@@ -306,7 +306,7 @@ __global__ void bump_counter_k(int64_t* c, int n, int64_t by) {
 __global__ __launch_bounds__(1024) void per_batch_leaves_k(TreeDesc t, BatchWrite w, int small_levels_in_block) {
   __shared__ float red[16];
   __shared__ int sids[2048];
-  batch_leaves_block(t, w, small_levels_in_block, red, sids);
+  batch_leaves_block<4>(t, w, small_levels_in_block, red, sids);  // (1024 threads: 128 VGPRs)
 }
 
 // One wave per listed slot: recompute its level-`level` ancestor.  With `top_from` > 0

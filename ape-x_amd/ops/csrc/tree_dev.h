@@ -155,11 +155,132 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
   }
 }
 
+// Every level of the dirty paths of sids[0, n) (any order, duplicates allowed; n <= 64) in ONE
+// memory round trip: the children of every ancestor to recompute, at every level, are
+// loaded up front -- all but the dirty ones are final already, and the dirty ones are the
+// nodes this workgroup recomputes one level below, substituted from LDS -- then the levels
+// are reduced bottom-up through LDS only.  The level-synchronous walk (update_levels_ilp)
+// paid a load round trip and a store drain per level (~14 us for a 1M-slot tree, 4 levels).
+// Same per-node arithmetic (wave_sum of the 64 children as doubles, wave_min): the sums are
+// bit-identical.  K: nodes per wave per level (distinct ancestors per level <= K x waves);
+// LP: the deepest tree handled (levels <= LP).
+template <int K, int LP>
+__device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const int* sids, int n) {
+  __shared__ int s_first[LP][64];  // per level: candidate index of each distinct ancestor's first
+  __shared__ int s_nfirst[LP];
+  __shared__ int s_head[64], s_next[64];    // per level: dirty-children list of each ancestor
+  __shared__ double s_ns[2][64];            // new sums / mins by first-rank, ping-pong over levels
+  __shared__ float s_nm[2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tid = threadIdx.x;
+  const int L = t.levels, n0 = t.size[0];
+  __syncthreads();  // the caller's leaf writes (workgroup scope) and sids are in place
+  // 1) the distinct ancestors per level: one wave per level, lane = candidate; compacted in
+  //    candidate order (ballot), so the work split is deterministic
+  for (int l = 1 + wave; l <= L; l += nw) {
+    const int sh = kTreeLog2Fanout * l;
+    const int id = lane < n ? sids[lane] : -1;
+    const bool ok = id >= 0 && id < n0;
+    const int anc = ok ? id >> sh : -1;
+    bool first = ok;
+    for (int v = 0; v < n; ++v) {  // wave-uniform
+      const int iv = sids[v];
+      if (v < lane && iv >= 0 && iv < n0 && (iv >> sh) == anc) first = false;
+    }
+    const uint64_t m = __ballot(first);
+    if (first) s_first[l - 1][__popcll(m & ((1ull << lane) - 1ull))] = lane;
+    if (lane == 0) s_nfirst[l - 1] = __popcll(m);
+  }
+  __syncthreads();
+  // 2) every level's children, all loads in flight (clamped addresses; selected at use)
+  double ps[LP][K];
+  float pm[LP][K];
+#pragma unroll
+  for (int l = 1; l <= LP; ++l) {
+    if (l > L) break;  // uniform
+    const int sh = kTreeLog2Fanout * l, csize = t.size[l - 1], nf = s_nfirst[l - 1];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int r = wave + k * nw;
+      const int node = r < nf ? sids[s_first[l - 1][r]] >> sh : 0;
+      const int c = min(node * kTreeFanout + lane, csize - 1);
+      if (l == 1) {
+        ps[0][k] = (double)__hip_atomic_load(t.leaf_sum + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pm[0][k] = __hip_atomic_load(t.leaf_min + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        ps[l - 1][k] = __hip_atomic_load(t.node_sum[l - 2] + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pm[l - 1][k] = __hip_atomic_load(t.node_min[l - 2] + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
+  // 3) bottom-up through LDS
+#pragma unroll
+  for (int l = 1; l <= LP; ++l) {
+    if (l > L) break;  // uniform
+    const int sh = kTreeLog2Fanout * l, csize = t.size[l - 1], nf = s_nfirst[l - 1];
+    if (l >= 2) {  // the dirty children of each level-l ancestor: the level-(l-1) firsts below it
+      if (tid < 64) s_head[tid] = -1;
+      __syncthreads();
+      const int nfc = s_nfirst[l - 2];
+      if (tid < nfc) {
+        const int a = sids[s_first[l - 2][tid]] >> sh;
+        int rep = 0;
+        for (int r = 0; r < nf; ++r)
+          if ((sids[s_first[l - 1][r]] >> sh) == a) { rep = r; break; }
+        s_next[tid] = atomicExch(&s_head[rep], tid);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int r = wave + k * nw;
+      if (r < nf) {  // wave-uniform
+        const int node = sids[s_first[l - 1][r]] >> sh;
+        const bool okc = node * kTreeFanout + lane < csize;
+        double sv = okc ? ps[l - 1][k] : 0.0;
+        float mv = okc ? pm[l - 1][k] : INFINITY;
+        if (l >= 2) {
+          for (int e = s_head[r]; e >= 0; e = s_next[e]) {  // wave-uniform walk
+            const int slot = (sids[s_first[l - 2][e]] >> (sh - kTreeLog2Fanout)) & (kTreeFanout - 1);
+            if (lane == slot) {
+              sv = s_ns[(l - 2) & 1][e];
+              mv = s_nm[(l - 2) & 1][e];
+            }
+          }
+        }
+        sv = wave_sum(sv);
+        mv = wave_min(mv);
+        if (lane == 0) {
+          t.node_sum[l - 1][node] = sv;
+          t.node_min[l - 1][node] = mv;
+          s_ns[(l - 1) & 1][r] = sv;
+          s_nm[(l - 1) & 1][r] = mv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// update_levels_oneshot when the batch and the tree fit it, else the level-synchronous walk.
+// KMAX caps the per-wave node count compiled in (its prefetch registers: 3 LP KMAX VGPRs),
+// e.g. 4 for 1024-thread workgroups (128 VGPRs)
+template <int KMAX = 16>
+__device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int* sids, int n) {
+  const int nw = blockDim.x >> 6;
+  if (n >= 1 && n <= 64 && t.levels <= 5) {  // block-uniform
+    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n);
+    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n);
+    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n);
+  }
+  update_levels_block(t, sids, n, 1, t.levels);
+}
+
 // The batched tree write of one workgroup (any block size >= 64 and >= B): the actor rows'
 // leaves, the learner priority mix + loss mean, deduplicated learner leaves, the running max
 // and counters; with ``small_levels_in_block`` every level of the dirty paths too.  ``red``:
 // 16 floats, ``sids``: E + B ints of LDS.  Used by per_batch_leaves_k and by the AQL learner's
 // noise-reset launch (aql_post_k), which runs it in one extra workgroup.
+template <int KMAX = 16>
 __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const BatchWrite& w, int small_levels_in_block,
                                                    float* red, int* sids) {
   const int k = threadIdx.x;
@@ -207,7 +328,7 @@ __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const Batc
     if (w.bump) *w.bump += 1;
   }
   if (small_levels_in_block) {  // tiny trees: every level in this block
-    update_levels_block(t, sids, w.E + w.B, 1, t.levels);
+    update_levels_fast<KMAX>(t, sids, w.E + w.B);
   }
 }
 
