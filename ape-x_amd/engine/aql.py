@@ -200,6 +200,7 @@ class AQLEngineConfig:
     # learner forward: candidate-tile groups per (sample, net) workgroup (0 = about one workgroup
     # per CU: the ~110 KB weight staging, the PER draw and the state MLP serve a group of tiles)
     fwd_tile_groups: int = 0
+    fwd_halves: int = 0  # learner forward workgroup: 0 = default (2: 512 threads), 1 = 256 threads
     # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
     # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
     act_blocks: int = 0
@@ -303,8 +304,8 @@ class AQLLearner:
             p["dbg"] = self.dbg.data_ptr()
         self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
                                   float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
-        if cfg.fwd_tile_groups:
-            self.L = h.aql_learn_set_groups(self.L, int(cfg.fwd_tile_groups))
+        if cfg.fwd_tile_groups or cfg.fwd_halves:
+            self.L = h.aql_learn_set_groups(self.L, int(cfg.fwd_tile_groups), int(cfg.fwd_halves))
         # fused sampling: the same stratified draw (seed, counter, mass) as per_sample inside the forward
         self.Ls = (h.aql_learn_set_sample(self.L, replay.tree, replay.filled.data_ptr(), self.beta.data_ptr(),
                                           self.step_ctr.data_ptr(), replay.seed ^ 0x51A7,

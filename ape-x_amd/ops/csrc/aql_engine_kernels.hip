@@ -111,18 +111,22 @@ __device__ __forceinline__ int wave_argmax(const float* row, int T, int lane) {
 // update): the forward reads one array per layer instead of three.
 constexpr int kEffB1 = kH * kCat, kEffW2 = kEffB1 + kH, kEffB2 = kEffW2 + kH;
 
-__global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
+// H = 2: 512 threads, the two halves take alternate candidate tiles of the item (2 waves per
+// SIMD instead of 1: the tile's dependent MFMA chains overlap); the staging and the state MLP
+// stay on the first half
+template <int H>
+__global__ __launch_bounds__(256 * H) void aql_learn_fwd_k(AqlLearn L) {
   __shared__ __attribute__((aligned(16))) float ao2[kH * kP132];  // action_out.2 weight [n][k]
   __shared__ __attribute__((aligned(16))) float w1[kH * kP132];   // advantage1 effective weight [n][k]
   // q_feature.0 [n][obs -> 64, zero-padded], .2 [n][k]: pitch 68 = 4 x odd, so the 16-byte row
   // reads of 16 lanes (one row each) cover all 64 banks
   __shared__ __attribute__((aligned(16))) float qw1[kH * kP68], qw2[kH * kP68];
-  __shared__ float xt[16 * kP68];                                  // ao_out tile [16 candidates][64]
+  __shared__ float xt[H][16 * kP68];                               // ao_out tile [16 candidates][64]
   __shared__ __attribute__((aligned(16))) float ao1w[kCat * kMaxAdim];  // [k][8], zero-padded past adim
   __shared__ float ao1b[kCat], ao2b[kH], w2e[kH], b1e[kH], qb1[kH], qb2[kH];
   __shared__ __attribute__((aligned(16))) float sv[2][64], hq[2][kH], qf[2][kH];
   __shared__ float stp[2][kH];
-  __shared__ float qpart[4][2][16];
+  __shared__ float qpart[H][4][2][16];
   __shared__ int srow;
   const bool tgt = blockIdx.y != 0;
   const AQLNet& N = tgt ? L.tg : L.on;
@@ -130,6 +134,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   const int T = N.T, RT = (T + 15) >> 4;
   const int nst = (tgt || L.act_mode) ? 1 : 2;  // online: {s, s'} (acting: {s}), target: {s'}
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, j = lane & 15, q = lane >> 4;
+  const int half = H == 2 ? t >> 8 : 0, wl = wave & 3, t8 = t & 255;
   const int obs = N.obs, adim = N.adim, cont = N.cont;
   AQL_STAMP(L, 8);
   // the PER draw of sample b (fused sampling) by wave 0: identical in every workgroup of b (same
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   // (measured: drawing on wave 0 WHILE waves 1-3 stage the weights was slower than the two in
   // sequence -- 25.4k vs 18.0k cycles: the descent's dependent loads queue behind the staging
   // traffic in the CU's memory pipeline)
-  {  // stage every weight with ALL loads in flight before the first store (in separate groups,
+  if (t < 256) {  // stage every weight with ALL loads in flight before the first store (in separate groups,
      // each group's stores waited out its loads before the next group's loads issued: ~3 serial
      // global round trips): the two 64x128 matrices as 16-byte loads, q_feature.0 / .2 (clamped
      // column index: unconditional loads; .0's columns past obs stored as zeros), action_out.0
@@ -239,7 +244,7 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
 #pragma unroll
     for (int d = 0; d < kMaxAdim; ++d) avn[d] = am[min(d, adim - 1)];
   };
-  if (cont) load_av(rt0);
+  if (cont) load_av(rt0 + half);
   // state halves, from LDS: wave si < nst handles state si (q_feature MLP, W1[:, 64:] . qf + b1)
   if (wave < nst) {
     hq[wave][lane] = relu(lds_dot64(qw1 + lane * kP68, sv[wave], qb1[lane]));  // (zero past obs)
@@ -248,14 +253,18 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
     __builtin_amdgcn_wave_barrier();
     stp[wave][lane] = lds_dot64(w1 + lane * kP132 + kH, qf[wave], b1e[lane]);
   }
-  for (int rt = rt0; rt < rt1; ++rt) {
+  for (int rb = rt0; rb < rt1; rb += H) {
+  const int rt = rb + half;
+  const bool live = rt < rt1;  // wave-uniform (the barriers below are kept)
+  float* xth = xt[half];
   // action encodings of candidates rt*16 .. +15: wave w computes columns 16w .. 16w+15
-  const int n = 16 * wave + j;
-  if (cont) {  // (tail rows recompute a valid candidate, discarded)
+  const int n = 16 * wl + j;
+  if (!live) {
+  } else if (cont) {  // (tail rows recompute a valid candidate, discarded)
     float av[kMaxAdim];
 #pragma unroll
     for (int d = 0; d < kMaxAdim; ++d) av[d] = d < adim ? avn[d] : 0.f;
-    if (rt + 1 < rt1) load_av(rt + 1);
+    if (rt + H < rt1) load_av(rt + H);
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
 #pragma unroll 4
     for (int k0 = 0; k0 < kCat; k0 += 8) {
@@ -277,12 +286,12 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       acc1 = mfma4(relu(h1), ao2[n * kP132 + k0 + 4 + q], acc1);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xt[(4 * q + i) * kP68 + n] = relu(acc0[i] + acc1[i] + ao2b[n]);
+    for (int i = 0; i < 4; ++i) xth[(4 * q + i) * kP68 + n] = relu(acc0[i] + acc1[i] + ao2b[n]);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int r = min(rt * 16 + 4 * q + i, T - 1);
-      xt[(4 * q + i) * kP68 + n] = relu(fmaf(ao1w[n * kMaxAdim], L.amu[(size_t)row * T + r], ao1b[n]));
+      xth[(4 * q + i) * kP68 + n] = relu(fmaf(ao1w[n * kMaxAdim], L.amu[(size_t)row * T + r], ao1b[n]));
     }
   }
   __syncthreads();
@@ -291,10 +300,10 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
   f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
   for (int k0 = 0; k0 < kH; k0 += 8) {
-    c0 = mfma4(xt[j * kP68 + k0 + q], w1[n * kP132 + k0 + q], c0);
-    c1 = mfma4(xt[j * kP68 + k0 + 4 + q], w1[n * kP132 + k0 + 4 + q], c1);
+    c0 = mfma4(xth[j * kP68 + k0 + q], w1[n * kP132 + k0 + q], c0);
+    c1 = mfma4(xth[j * kP68 + k0 + 4 + q], w1[n * kP132 + k0 + 4 + q], c1);
   }
-  for (int si = 0; si < nst; ++si) {
+  for (int si = 0; si < (live ? nst : 0); ++si) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float v = w2e[n] * relu(c0[i] + c1[i] + stp[si][n]);
@@ -302,15 +311,16 @@ __global__ __launch_bounds__(256) void aql_learn_fwd_k(AqlLearn L) {
       v += __shfl_xor(v, 2, 64);
       v += __shfl_xor(v, 4, 64);
       v += __shfl_xor(v, 8, 64);
-      if (j == 0) qpart[wave][si][4 * q + i] = v;
+      if (j == 0) qpart[half][wl][si][4 * q + i] = v;
     }
   }
   __syncthreads();
   if (item == blockIdx.x) AQL_STAMP(L, 13);
-  if (t < 16 * nst) {
-    const int m = t & 15, si = t >> 4, tt = rt * 16 + m;
+  if (live && t8 < 16 * nst) {
+    const int m = t8 & 15, si = t8 >> 4, tt = rt * 16 + m;
     if (tt < T) {
-      const float qv = ((qpart[0][si][m] + qpart[1][si][m]) + (qpart[2][si][m] + qpart[3][si][m])) + eff[kEffB2];
+      const float (*qp)[2][16] = qpart[half];
+      const float qv = ((qp[0][si][m] + qp[1][si][m]) + (qp[2][si][m] + qp[3][si][m])) + eff[kEffB2];
       float* out = tgt ? L.qt_s2 : (si ? L.q_s2 : L.q_s);
       out[(size_t)b * T + tt] = qv;
     }
@@ -1207,7 +1217,8 @@ void aql_learn_fwd(const AqlLearn& L, hipStream_t s) {
     Lk.tile_groups = std::max(1, std::min(RT, cus / (2 * L.B)));
   }
   Lk.tile_groups = std::min(Lk.tile_groups, RT);
-  aql_learn_fwd_k<<<dim3(L.B * Lk.tile_groups, 2), 256, 0, s>>>(Lk);
+  if (Lk.fwd_halves == 1) aql_learn_fwd_k<1><<<dim3(L.B * Lk.tile_groups, 2), 256, 0, s>>>(Lk);
+  else aql_learn_fwd_k<2><<<dim3(L.B * Lk.tile_groups, 2), 512, 0, s>>>(Lk);
   LAUNCH_CHECK();
 }
 
@@ -1220,7 +1231,7 @@ void aql_act_q(const AqlLearn& L, hipStream_t s) {
   if (L.B < 1) return;
   const int RT = (L.on.T + 15) / 16;
   const int blocks = std::max(1, std::min(L.B * RT, L.act_blocks > 0 ? L.act_blocks : L.B * RT));
-  aql_learn_fwd_k<<<dim3(blocks, 1), 256, 0, s>>>(L);  // grid.y = 1: the online net only
+  aql_learn_fwd_k<1><<<dim3(blocks, 1), 256, 0, s>>>(L);  // grid.y = 1: the online net only
   LAUNCH_CHECK();
 }
 

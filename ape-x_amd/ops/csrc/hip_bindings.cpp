@@ -646,11 +646,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     g.bw = w;
     return g;
   });
-  m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups) {  // 0: the launcher picks
+  m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups, int halves) {  // groups 0: the launcher picks
+    if (halves != 0 && halves != 1 && halves != 2) throw std::invalid_argument("aql_learn_set_groups: halves 0, 1 or 2");
     AqlLearn L = L0;
     L.tile_groups = groups;
+    L.fwd_halves = halves;
     return L;
-  });
+  }, py::arg("L"), py::arg("groups"), py::arg("halves") = 0);
   m.def("aql_noisy_eff", [](const AQLNet& net, uint64_t ws, uint64_t s) { aql_noisy_eff(net, P<float>(ws), S(s)); });
   m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
   m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });

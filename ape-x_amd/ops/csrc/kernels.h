@@ -461,6 +461,7 @@ struct AqlLearn {
   // learner forward: candidate-tile groups per (sample, net) workgroup item (0 = about one
   // workgroup per CU; act_mode: 0 = one tile per item)
   int tile_groups;
+  int fwd_halves;  // learner forward workgroup: 2 = 512 threads (alternate tiles per half), 1 = 256
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
 // acting on the learner's MFMA forward: q_s[b][t] = Q_on(st[b], amu[b][t]) for B states

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--bwd-tree", type=int, default=None, help="priority write in the backward launch (1) or not (0)")
     ap.add_argument("--fused-update", type=int, default=None, help="update launch after the gradients (1) or not")
     ap.add_argument("--levels-in-grad", type=int, default=None, help="tree levels in the gradient launch (1) or not")
+    ap.add_argument("--halves", type=int, default=0, help="forward workgroup halves (0 default, 1, 2)")
     ap.add_argument("--groups", type=int, default=0, help="forward tile groups per sample (0: the launcher picks)")
     a = ap.parse_args()
     import torch
@@ -26,6 +27,7 @@ def main():
 
     cfg = AQLEngineConfig(env_id=a.env, capacity=1_000_000, fused_step=bool(a.fused_step))
     cfg.fwd_tile_groups = a.groups
+    cfg.fwd_halves = a.halves
     if a.levels_in_grad is not None:
         cfg.tree_levels_in_grad = bool(a.levels_in_grad)
     if a.fused_update is not None:

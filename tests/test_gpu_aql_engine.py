@@ -329,13 +329,14 @@ def test_fused_sampling_equals_per_sample(cuda):
 
 def test_forward_tile_groups_bit_identical(cuda):
     """The learner forward's work split (candidate tiles per workgroup: one, a few, all of a
-    sample's) changes only which workgroup computes a tile: same Q rows, same training."""
+    sample's; 256- or 512-thread workgroups) changes only which waves compute a tile: same Q
+    rows, same training."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    for groups in (0, 1, 3, 13):
+    for groups, halves in ((0, 0), (1, 1), (3, 2), (13, 1), (13, 2), (4, 1)):
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=5,
-                              fwd_tile_groups=groups)
+                              fwd_tile_groups=groups, fwd_halves=halves)
         eng = AQLEngine(cfg, cuda)
         eng.fill(1024)
         for _ in range(4):
