@@ -166,7 +166,9 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
 // LP: the deepest tree handled (levels <= LP).
 template <int K, int LP>
 __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const int* sids, int n) {
-  __shared__ int s_first[LP][64];  // per level: candidate index of each distinct ancestor's first
+  __shared__ int s_first[LP][64];    // per level: rank -> candidate index of each distinct ancestor's first
+  __shared__ int s_rank[LP][64];     // per level: first candidate -> its rank
+  __shared__ int s_firstof[LP][64];  // per level: candidate -> the first candidate of its ancestor
   __shared__ int s_nfirst[LP];
   __shared__ int s_head[64], s_next[64];    // per level: dirty-children list of each ancestor
   __shared__ double s_ns[2][64];            // new sums / mins by first-rank, ping-pong over levels
@@ -174,20 +176,27 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tid = threadIdx.x;
   const int L = t.levels, n0 = t.size[0];
   __syncthreads();  // the caller's leaf writes (workgroup scope) and sids are in place
-  // 1) the distinct ancestors per level: one wave per level, lane = candidate; compacted in
-  //    candidate order (ballot), so the work split is deterministic
+  // 1) the distinct ancestors per level: one wave per level, lane = candidate, the ancestors
+  //    compared through readlane (no LDS round trips); compacted in candidate order (ballot),
+  //    so the work split is deterministic
   for (int l = 1 + wave; l <= L; l += nw) {
     const int sh = kTreeLog2Fanout * l;
     const int id = lane < n ? sids[lane] : -1;
     const bool ok = id >= 0 && id < n0;
-    const int anc = ok ? id >> sh : -1;
-    bool first = ok;
+    const int anc = ok ? id >> sh : -1 - lane;  // (invalid candidates match nothing)
+    int fo = lane;
     for (int v = 0; v < n; ++v) {  // wave-uniform
-      const int iv = sids[v];
-      if (v < lane && iv >= 0 && iv < n0 && (iv >> sh) == anc) first = false;
+      const int av = __builtin_amdgcn_readlane(anc, v);
+      if (v < fo && av == anc) fo = v;
     }
+    const bool first = ok && fo == lane;
     const uint64_t m = __ballot(first);
-    if (first) s_first[l - 1][__popcll(m & ((1ull << lane) - 1ull))] = lane;
+    const int rank = __popcll(m & ((1ull << lane) - 1ull));
+    if (first) {
+      s_first[l - 1][rank] = lane;
+      s_rank[l - 1][lane] = rank;
+    }
+    s_firstof[l - 1][lane] = fo;
     if (lane == 0) s_nfirst[l - 1] = __popcll(m);
   }
   __syncthreads();
@@ -221,11 +230,8 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
       if (tid < 64) s_head[tid] = -1;
       __syncthreads();
       const int nfc = s_nfirst[l - 2];
-      if (tid < nfc) {
-        const int a = sids[s_first[l - 2][tid]] >> sh;
-        int rep = 0;
-        for (int r = 0; r < nf; ++r)
-          if ((sids[s_first[l - 1][r]] >> sh) == a) { rep = r; break; }
+      if (tid < nfc) {  // level-(l-1) first -> the rank of its level-l ancestor's first
+        const int rep = s_rank[l - 1][s_firstof[l - 1][s_first[l - 2][tid]]];
         s_next[tid] = atomicExch(&s_head[rep], tid);
       }
       __syncthreads();
