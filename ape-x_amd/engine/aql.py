@@ -220,9 +220,13 @@ class AQLEngineConfig:
     # (scripts/ab/aql_bwd_tree.sh; learner step 51.4 vs 55.7 us in scripts/bench_aql.py)
     fused_update: bool = True
     # with the priority write in the backward launch: its extra workgroup writes the leaves only
-    # and the gradient launch's extra workgroup walks the levels (the whole write on one
-    # workgroup outlasted the backward: 23.4 vs 13.6 us)
-    tree_levels_in_grad: bool = True
+    # and the gradient launch's extra workgroup walks the levels.  Measured slower than the whole
+    # write (leaves + one-round-trip level walk) in the backward's workgroup: 16.58k vs 16.82-16.86k
+    # SGD steps/s (the levels workgroup bounded the gradient launch: 15.1 vs ~5.5 us)
+    tree_levels_in_grad: bool = False
+    # fused_update: the next step's PER draw in extra workgroups of the gradient launch (its
+    # tree descent hides behind the contraction) instead of the update launch
+    draw_in_grad: bool = True
     seed: int = 0
 
 
@@ -474,11 +478,17 @@ class AQLLearner:
             self._tree_pending = True
         else:
             tree_write(s)
-        h.aql_grad(self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G), s)
-        if self.U is not None:  # optimizers, noise of both critics, proposal copy, next draw: one launch
-            h.aql_update(self.U_draw if draw_next else self.U, s)
+        G = self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G)
+        if self.U is not None:  # optimizers, noise of both critics, proposal copy (+ next draw): one launch
+            if draw_next and self.cfg.draw_in_grad:
+                h.aql_grad_draw(G, self.U_draw, s)
+                h.aql_update(self.U, s)
+            else:
+                h.aql_grad(G, s)
+                h.aql_update(self.U_draw if draw_next else self.U, s)
             self._track_losses()
             return
+        h.aql_grad(G, s)
         Pq, o = self.P_q, 4 * self.P_q
         # the two optimizers (critic, proposal; own clip norms) in one launch
         h.adam_step2((self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,

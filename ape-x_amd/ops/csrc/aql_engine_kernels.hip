@@ -741,21 +741,6 @@ __device__ __forceinline__ float aql_grad_block(const AqlGrad& G, int bid, int n
   return g;
 }
 
-__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
-  if (G.tree_leaves && blockIdx.x == gridDim.x - 1) {  // block-uniform: the split tree write's leaves
-    __shared__ float tred[16];
-    __shared__ int sids[64];
-    if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
-      for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
-      update_levels_fast(G.tree, sids, G.bw.B);
-    } else {
-      batch_leaves_block(G.tree, G.bw, 0, tred, sids);
-    }
-    return;
-  }
-  aql_grad_block(G, blockIdx.x, (int)gridDim.x - (G.tree_leaves ? 1 : 0));
-}
-
 // ------------------------------------------------------------------ noise reset + proposal copy
 __device__ __forceinline__ float scaled_noise(uint64_t seed, int layer, int kind, int i, uint64_t ctr) {
   float u[4];
@@ -954,6 +939,30 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
       }
     }
   }
+}
+
+// aql_grad_k: the gradient blocks, then the optional tree workgroup (G.tree_leaves), then the
+// optional NEXT step's PER draw (kStepDrawBlocks workgroups; `draw`: the update descriptor) --
+// the tree is final once the backward launch's priority write is done, and the draw's tree
+// descent hides behind the contraction instead of bounding the update launch
+__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G, const AqlStep* __restrict__ draw) {
+  const int nd = draw ? kStepDrawBlocks : 0, ng = (int)gridDim.x - nd - (G.tree_leaves ? 1 : 0);
+  if ((int)blockIdx.x >= ng + (G.tree_leaves ? 1 : 0)) {  // block-uniform: the draw
+    draw_block(*draw, (int)blockIdx.x - ((int)gridDim.x - nd), (uint64_t)draw->P.step[0]);
+    return;
+  }
+  if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the split tree write
+    __shared__ float tred[16];
+    __shared__ int sids[64];
+    if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
+      for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
+      update_levels_fast(G.tree, sids, G.bw.B);
+    } else {
+      batch_leaves_block(G.tree, G.bw, 0, tred, sids);
+    }
+    return;
+  }
+  aql_grad_block(G, blockIdx.x, ng);
 }
 
 __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
@@ -1256,7 +1265,7 @@ void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
 
 int aql_grad_blocks(int64_t n) { return (int)((n + kGradThreads - 1) / kGradThreads); }
 
-void aql_grad(const AqlGrad& g, hipStream_t s) {
+void aql_grad(const AqlGrad& g, hipStream_t s, const AqlStep* draw) {
   if (g.njobs < 1 || g.njobs > kAqlMaxJobs || g.job[0].off != 0) throw std::invalid_argument("aql_grad: jobs");
   for (int k = 0; k < g.njobs; ++k) {
     const AqlGradJob& J = g.job[k];
@@ -1267,7 +1276,8 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
   }
   if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || g.bw.E != 0 || (g.tree_leaves == 1 && !g.bw.idx) || !g.bw.list))
     throw std::invalid_argument("aql_grad: the split tree write takes 1..64 learner rows and no actor rows");
-  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), kGradThreads, 0, s>>>(g);
+  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0) + (draw ? kStepDrawBlocks : 0), kGradThreads, 0, s>>>(
+      g, draw);
   LAUNCH_CHECK();
 }
 

@@ -765,6 +765,7 @@ PYBIND11_MODULE(_apex_hip, m) {
     int grid;
     int update;        // 1: the separate update launch (aql_update), not the fused tail
     int noise_blocks;  // aql_update: target-noise workgroups
+    int draw;          // the descriptor carries the next step's draw
   };
   py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid)
       .def_readonly("update", &AqlStepHandle::update);
@@ -809,11 +810,15 @@ PYBIND11_MODULE(_apex_hip, m) {
     HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));
     int nb = 0;
     const int grid = upd ? aql_update_grid(d, &nb) : aql_step_grid(d);
-    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, upd, nb};
+    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, upd, nb, d.draw};
   });
   m.def("aql_step_tail", [](const AqlStepHandle& h, uint64_t s) {
     if (h.update) throw std::invalid_argument("aql_step_tail: an update handle (use aql_update)");
     aql_step_tail(h.dev, h.grid, S(s));
+  });
+  m.def("aql_grad_draw", [](const AqlGrad& G, const AqlStepHandle& h, uint64_t s) {
+    if (!h.update || !h.draw) throw std::invalid_argument("aql_grad_draw: an update handle with the draw");
+    aql_grad(G, S(s), h.dev);
   });
   m.def("aql_update", [](const AqlStepHandle& h, uint64_t s) {
     if (!h.update) throw std::invalid_argument("aql_update: a fused-tail handle (use aql_step_tail)");

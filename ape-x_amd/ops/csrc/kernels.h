@@ -493,7 +493,10 @@ struct AqlGrad {
   BatchWrite bw;
 };
 int aql_grad_blocks(int64_t n);
-void aql_grad(const AqlGrad& g, hipStream_t s);
+struct AqlStep;
+// draw: an update descriptor with AqlStep::draw (device memory) -- the next step's PER draw
+// runs in extra workgroups of this launch
+void aql_grad(const AqlGrad& g, hipStream_t s, const AqlStep* draw = nullptr);
 struct AqlNoise {
   float *weps, *beps;                    // NoisyLinear epsilon buffers [out][in], [out]
   const float *wmu, *wsig, *bmu, *bsig;  // parameters (post-update)

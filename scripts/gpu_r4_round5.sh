@@ -9,7 +9,7 @@ rc=$?; echo "== tests rc=$rc"; tail -3 gpurun_out/ab/test.log
 [ $rc -ne 0 ] && exit $rc
 APEX_AQL_DBG=1 timeout -k 10 120 python scripts/bench_aql.py --fused-step 0 --iters 200 || exit $?
 for k in 1 2; do
-  for v in "--aql-fused-update 0" "--aql-fused-update 1 --aql-levels-in-grad 0" "--aql-fused-update 1"; do
+  for v in "--aql-fused-update 0" "--aql-fused-update 1 --aql-draw-in-grad 0" "--aql-fused-update 1"; do
     timeout -k 10 200 python bench.py --algo aql --steps 500 --warmup 20 $v > gpurun_out/ab/b.log 2>&1
     rc=$?; [ $rc -ne 0 ] && { echo "bench rc=$rc"; tail -5 gpurun_out/ab/b.log; exit $rc; }
     echo "$v: $(grep -o '"value": [0-9.]*' gpurun_out/ab/b.log)"

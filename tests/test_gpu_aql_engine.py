@@ -288,12 +288,13 @@ def test_fused_sampling_equals_per_sample(cuda):
                 (True, False, False, True, False, False, False), (False, False, False, True, False, False, False),
                 (True, False, False, False, True, False, False), (False, False, False, False, True, False, True),
                 (True, False, False, False, False, True, True), (False, False, False, False, False, True, True),
-                (True, False, False, False, False, True, False))
+                (True, False, False, False, False, True, False), (True, False, False, False, False, True, None))
     for fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update, lv in variants:
+        # lv None: draw in the update launch (draw_in_grad off), levels in the backward's workgroup
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
                               fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree,
                               fused_step=fused_step, bwd_tree=bwd_tree, fused_update=fused_update,
-                              tree_levels_in_grad=lv)
+                              tree_levels_in_grad=bool(lv), draw_in_grad=lv is not None)
         eng = AQLEngine(cfg, cuda)
         L = eng.learner
         assert (L.Ls is not None) == fused_sample
@@ -304,7 +305,7 @@ def test_fused_sampling_equals_per_sample(cuda):
             assert (L.L_tree is not None) == (bwd_tree or fused_update)
             assert (L.U is not None) == fused_update
             assert L.predraw == (fused_update and fused_sample)
-            assert (L.G_levels is not None) == ((bwd_tree or fused_update) and lv)
+            assert (L.G_levels is not None) == bool((bwd_tree or fused_update) and lv)
         else:
             assert L.S.grid >= max(L.nblk, L.B + 1) + 1
         eng.fill(1024)
