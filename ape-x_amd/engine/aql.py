@@ -225,7 +225,8 @@ class AQLEngineConfig:
     # SGD steps/s (the levels workgroup bounded the gradient launch: 15.1 vs ~5.5 us)
     tree_levels_in_grad: bool = False
     # fused_update: the next step's PER draw in extra workgroups of the gradient launch (its
-    # tree descent hides behind the contraction) instead of the update launch
+    # tree descent hides behind the contraction) instead of the update launch; not with
+    # tree_levels_in_grad (the draw would read levels being written)
     draw_in_grad: bool = True
     seed: int = 0
 
@@ -480,7 +481,7 @@ class AQLLearner:
             tree_write(s)
         G = self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G)
         if self.U is not None:  # optimizers, noise of both critics, proposal copy (+ next draw): one launch
-            if draw_next and self.cfg.draw_in_grad:
+            if draw_next and self.cfg.draw_in_grad and self.G_levels is None:  # (levels in that launch: racy)
                 h.aql_grad_draw(G, self.U_draw, s)
                 h.aql_update(self.U, s)
             else:
