@@ -170,7 +170,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
   __shared__ int s_rank[LP][64];     // per level: first candidate -> its rank
   __shared__ int s_firstof[LP][64];  // per level: candidate -> the first candidate of its ancestor
   __shared__ int s_nfirst[LP];
-  __shared__ int s_head[64], s_next[64];    // per level: dirty-children list of each ancestor
+  __shared__ int s_inv[64][64];             // per node rank: child slot -> dirty child's first-rank (-1)
   __shared__ double s_ns[2][64];            // new sums / mins by first-rank, ping-pong over levels
   __shared__ float s_nm[2][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tid = threadIdx.x;
@@ -221,46 +221,58 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
       }
     }
   }
-  // 3) bottom-up through LDS
+  // 3) bottom-up through LDS.  The dirty children of a wave's K nodes are substituted by
+  //    scatter / gather through a per-wave slot map (all K nodes' LDS traffic batched: a
+  //    per-node list walk paid several dependent LDS latencies per node, ~10 us per write)
 #pragma unroll
   for (int l = 1; l <= LP; ++l) {
     if (l > L) break;  // uniform
     const int sh = kTreeLog2Fanout * l, csize = t.size[l - 1], nf = s_nfirst[l - 1];
-    if (l >= 2) {  // the dirty children of each level-l ancestor: the level-(l-1) firsts below it
-      if (tid < 64) s_head[tid] = -1;
-      __syncthreads();
+    double sv[K];
+    float mv[K];
+    int node[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int r = wave + k * nw;
+      node[k] = r < nf ? sids[s_first[l - 1][r]] >> sh : 0;
+      const bool okc = r < nf && node[k] * kTreeFanout + lane < csize;
+      sv[k] = okc ? ps[l - 1][k] : 0.0;
+      mv[k] = okc ? pm[l - 1][k] : INFINITY;
+    }
+    if (l >= 2) {
       const int nfc = s_nfirst[l - 2];
-      if (tid < nfc) {  // level-(l-1) first -> the rank of its level-l ancestor's first
-        const int rep = s_rank[l - 1][s_firstof[l - 1][s_first[l - 2][tid]]];
-        s_next[tid] = atomicExch(&s_head[rep], tid);
+#pragma unroll
+      for (int k = 0; k < K; ++k) s_inv[wave + k * nw][lane] = -1;
+      __syncthreads();
+      // one lane per level-(l-1) first: its parent's rank (-> owning wave, k) and child slot
+      for (int e = tid; e < nfc; e += blockDim.x) {
+        const int w1 = s_first[l - 2][e];
+        const int rep = s_rank[l - 1][s_firstof[l - 1][w1]];
+        s_inv[rep][(sids[w1] >> (sh - kTreeLog2Fanout)) & (kTreeFanout - 1)] = e;
       }
       __syncthreads();
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int e = s_inv[wave + k * nw][lane];
+        if (e >= 0) {
+          sv[k] = s_ns[(l - 2) & 1][e];
+          mv[k] = s_nm[(l - 2) & 1][e];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      sv[k] = wave_sum(sv[k]);
+      mv[k] = wave_min(mv[k]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int r = wave + k * nw;
-      if (r < nf) {  // wave-uniform
-        const int node = sids[s_first[l - 1][r]] >> sh;
-        const bool okc = node * kTreeFanout + lane < csize;
-        double sv = okc ? ps[l - 1][k] : 0.0;
-        float mv = okc ? pm[l - 1][k] : INFINITY;
-        if (l >= 2) {
-          for (int e = s_head[r]; e >= 0; e = s_next[e]) {  // wave-uniform walk
-            const int slot = (sids[s_first[l - 2][e]] >> (sh - kTreeLog2Fanout)) & (kTreeFanout - 1);
-            if (lane == slot) {
-              sv = s_ns[(l - 2) & 1][e];
-              mv = s_nm[(l - 2) & 1][e];
-            }
-          }
-        }
-        sv = wave_sum(sv);
-        mv = wave_min(mv);
-        if (lane == 0) {
-          t.node_sum[l - 1][node] = sv;
-          t.node_min[l - 1][node] = mv;
-          s_ns[(l - 1) & 1][r] = sv;
-          s_nm[(l - 1) & 1][r] = mv;
-        }
+      if (r < nf && lane == 0) {
+        t.node_sum[l - 1][node[k]] = sv[k];
+        t.node_min[l - 1][node[k]] = mv[k];
+        s_ns[(l - 1) & 1][r] = sv[k];
+        s_nm[(l - 1) & 1][r] = mv[k];
       }
     }
     __syncthreads();
