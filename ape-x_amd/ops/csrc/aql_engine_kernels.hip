@@ -613,6 +613,10 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   __shared__ float s_dl[64], s_lw[64], tred[16], s_qa[64], s_r[64], s_dn[64], s_wb[64];
   __shared__ int sids[64], s_next[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = (int)(blockDim.x >> 6), T = L.on.T, B = L.B;
+  auto stamp = [&](int k) {  // diagnostics (APEX_AQL_DBG): tree-workgroup phase timestamps
+    if (L.dbg && t == 0) L.dbg[16 + k] = (long long)clock64();
+  };
+  stamp(0);
   // the B TD terms with every sample's loads in flight together (a wave-per-sample loop paid ~4
   // dependent round trips per sample, ~29 us for 32 samples): the scalar chains idx -> act ->
   // Q(s, a) on one thread per sample, the argmaxes of Q(s', .) 4 samples per wave at a time
@@ -663,9 +667,13 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
     s_lw[t] = td.lw;
   }
   __syncthreads();
+  stamp(1);
   w.mix.delta = s_dl;
   w.mix.lw = s_lw;
-  batch_leaves_block(tree, w, levels, tred, sids);
+  batch_leaves_block(tree, w, 0, tred, sids);
+  stamp(2);
+  if (levels) update_levels_fast(tree, sids, B);
+  stamp(3);
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {

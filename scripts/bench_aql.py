@@ -64,6 +64,9 @@ def main():
         print("bwd phase cycles:", [d[k + 1] - d[k] for k in range(7)], "total", d[7] - d[0])
         print("fwd phase cycles (staging, sampling, state load, encodings, adv1, out):",
               [d[k + 1] - d[k] for k in range(8, 14)], "total", d[14] - d[8])
+        if d[16]:
+            print("tree workgroup cycles (td, leaves, levels):", [d[k + 1] - d[k] for k in range(16, 19)],
+                  "start after bwd start", d[16] - d[0])
 
 
 if __name__ == "__main__":
