@@ -300,7 +300,7 @@ class AQLLearner:
         nws = h.aql_workspace_floats()  # effective NoisyLinear weights: W1 [64][128] | b1 | w2 | b2
         self.eff_on = torch.zeros(nws, **f32)
         self.eff_tg = torch.zeros(nws, **f32)
-        self.dbg = torch.zeros(24, dtype=torch.int64, device=dev) if os.environ.get("APEX_AQL_DBG") else None
+        self.dbg = torch.zeros(32, dtype=torch.int64, device=dev) if os.environ.get("APEX_AQL_DBG") else None
         p = dict(replay.table_ptrs(), eff_on=self.eff_on.data_ptr(), eff_tg=self.eff_tg.data_ptr(), idx=self.idx.data_ptr(), w=self.w.data_ptr(), var=self.var.data_ptr(),
                  q_s=self.q_s.data_ptr(), q_s2=self.q_s2.data_ptr(), qt_s2=self.qt_s2.data_ptr(),
                  vec=self.vec.data_ptr(), delta=self.delta.data_ptr(), lw=self.lw.data_ptr(),

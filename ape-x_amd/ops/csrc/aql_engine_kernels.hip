@@ -672,7 +672,7 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   w.mix.lw = s_lw;
   batch_leaves_block(tree, w, 0, tred, sids);
   stamp(2);
-  if (levels) update_levels_fast(tree, sids, B);
+  if (levels) update_levels_fast(tree, sids, B, L.dbg ? L.dbg + 24 : nullptr);  // (dbg[24..29]: walk phases)
   stamp(3);
 }
 

@@ -165,7 +165,8 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
 // bit-identical.  K: nodes per wave per level (distinct ancestors per level <= K x waves);
 // LP: the deepest tree handled (levels <= LP).
 template <int K, int LP>
-__device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const int* sids, int n) {
+__device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const int* sids, int n,
+                                                      long long* dbg = nullptr) {
   __shared__ int s_first[LP][64];    // per level: rank -> candidate index of each distinct ancestor's first
   __shared__ int s_rank[LP][64];     // per level: first candidate -> its rank
   __shared__ int s_firstof[LP][64];  // per level: candidate -> the first candidate of its ancestor
@@ -200,6 +201,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
     if (lane == 0) s_nfirst[l - 1] = __popcll(m);
   }
   __syncthreads();
+  if (dbg && threadIdx.x == 0) dbg[0] = (long long)clock64();
   // 2) every level's children, all loads in flight (clamped addresses; selected at use)
   double ps[LP][K];
   float pm[LP][K];
@@ -276,6 +278,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
       }
     }
     __syncthreads();
+    if (dbg && threadIdx.x == 0) dbg[l] = (long long)clock64();
   }
 }
 
@@ -283,12 +286,12 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
 // KMAX caps the per-wave node count compiled in (its prefetch registers: 3 LP KMAX VGPRs),
 // e.g. 4 for 1024-thread workgroups (128 VGPRs)
 template <int KMAX = 16>
-__device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int* sids, int n) {
+__device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int* sids, int n, long long* dbg = nullptr) {
   const int nw = blockDim.x >> 6;
   if (n >= 1 && n <= 64 && t.levels <= 5) {  // block-uniform
-    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n);
-    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n);
-    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n);
+    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n, dbg);
+    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n, dbg);
+    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n, dbg);
   }
   update_levels_block(t, sids, n, 1, t.levels);
 }

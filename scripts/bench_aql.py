@@ -67,6 +67,9 @@ def main():
         if d[16]:
             print("tree workgroup cycles (td, leaves, levels):", [d[k + 1] - d[k] for k in range(16, 19)],
                   "start after bwd start", d[16] - d[0])
+            if d[24]:
+                print("level walk cycles (dedup | level 1..):", d[24] - d[18],
+                      [d[25 + k] - d[24 + k] for k in range(5) if d[25 + k]])
 
 
 if __name__ == "__main__":
