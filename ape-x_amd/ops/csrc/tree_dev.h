@@ -174,6 +174,8 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
   __shared__ int s_inv[64][64];             // per node rank: child slot -> dirty child's first-rank (-1)
   __shared__ double s_ns[2][64];            // new sums / mins by first-rank, ping-pong over levels
   __shared__ float s_nm[2][64];
+  __shared__ double s_os[LP][64];           // every level's new values, stored at the end
+  __shared__ float s_om[LP][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tid = threadIdx.x;
   const int L = t.levels, n0 = t.size[0];
   __syncthreads();  // the caller's leaf writes (workgroup scope) and sids are in place
@@ -270,15 +272,24 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int r = wave + k * nw;
-      if (r < nf && lane == 0) {
-        t.node_sum[l - 1][node[k]] = sv[k];
-        t.node_min[l - 1][node[k]] = mv[k];
+      if (r < nf && lane == 0) {  // (global stores deferred: a barrier waits out pending stores)
         s_ns[(l - 1) & 1][r] = sv[k];
         s_nm[(l - 1) & 1][r] = mv[k];
+        s_os[l - 1][r] = sv[k];
+        s_om[l - 1][r] = mv[k];
       }
     }
     __syncthreads();
     if (dbg && threadIdx.x == 0) dbg[l] = (long long)clock64();
+  }
+  // 4) every new node value out at once (nothing in this workgroup reads them back)
+  for (int l = 1; l <= L; ++l) {
+    const int sh = kTreeLog2Fanout * l;
+    for (int r = tid; r < s_nfirst[l - 1]; r += blockDim.x) {
+      const int node = sids[s_first[l - 1][r]] >> sh;
+      t.node_sum[l - 1][node] = s_os[l - 1][r];
+      t.node_min[l - 1][node] = s_om[l - 1][r];
+    }
   }
 }
 
