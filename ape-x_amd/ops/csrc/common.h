@@ -60,6 +60,32 @@ __device__ __forceinline__ T wave_min(T v) {
   return v;
 }
 
+// K independent wave reductions, step-major: every value's exchange of one butterfly step is
+// issued before the next step (one LDS-permute latency per step instead of one per value and
+// step), each value's arithmetic exactly as wave_sum / wave_min
+template <int K, typename T>
+__device__ __forceinline__ void wave_sum_k(T (&v)[K]) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = __shfl_xor(v[k], o, 64);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += w[k];
+  }
+}
+template <int K, typename T>
+__device__ __forceinline__ void wave_min_k(T (&v)[K]) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = __shfl_xor(v[k], o, 64);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = w[k] < v[k] ? w[k] : v[k];
+  }
+}
+
 // inclusive prefix sum across the 64 lanes (Hillis-Steele, fixed order => deterministic)
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_scan(T v, int lane) {

@@ -119,13 +119,13 @@ __device__ __forceinline__ void update_levels_ilp(const TreeDesc& t, const int* 
         m[j] = ok ? dm[j] : INFINITY;
       }
     }
+    wave_sum_k<K>(s);
+    wave_min_k<K>(m);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const double sj = wave_sum(s[j]);
-      const float mj = wave_min(m[j]);
       if (node[j] >= 0 && lane == 0) {
-        t.node_sum[level - 1][node[j]] = sj;
-        t.node_min[level - 1][node[j]] = mj;
+        t.node_sum[level - 1][node[j]] = s[j];
+        t.node_min[level - 1][node[j]] = m[j];
       }
     }
   }
@@ -264,10 +264,24 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
         }
       }
     }
+    // the reductions, step-major over the wave's nodes; only as many as this level has per wave
+    // (levels near the root have 1-4 nodes)
+    const int kn = nf > wave ? (nf - wave + nw - 1) / nw : 0;  // wave-uniform
+    if (kn > K / 2) {
+      wave_sum_k<K>(sv);
+      wave_min_k<K>(mv);
+    } else if (kn > 1) {
+      double s2[(K / 2 > 0 ? K / 2 : 1)];
+      float m2[(K / 2 > 0 ? K / 2 : 1)];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      sv[k] = wave_sum(sv[k]);
-      mv[k] = wave_min(mv[k]);
+      for (int k = 0; k < K / 2; ++k) { s2[k] = sv[k]; m2[k] = mv[k]; }
+      wave_sum_k<(K / 2 > 0 ? K / 2 : 1)>(s2);
+      wave_min_k<(K / 2 > 0 ? K / 2 : 1)>(m2);
+#pragma unroll
+      for (int k = 0; k < K / 2; ++k) { sv[k] = s2[k]; mv[k] = m2[k]; }
+    } else if (kn == 1) {
+      sv[0] = wave_sum(sv[0]);
+      mv[0] = wave_min(mv[0]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
