@@ -86,6 +86,88 @@ __device__ __forceinline__ void wave_min_k(T (&v)[K]) {
   }
 }
 
+// Tree-node reductions on DPP lane moves (VALU, no LDS permute round trips): quad xor 1, xor
+// 2, half-row mirror, row mirror (every lane of a row then holds the row's value), row
+// broadcasts 15 / 31 into the next rows; the result is read from lane 63.  A fixed association
+// order (not wave_sum's butterfly): every priority-tree kernel reduces node children with
+// these, so all tree paths agree bit for bit.  K values step-major, as wave_sum_k.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_id, double fill) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v), f = __builtin_bit_cast(uint64_t, fill);
+  const int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+  const int flo = (int)(uint32_t)f, fhi = (int)(uint32_t)(f >> 32);
+  int rlo, rhi;
+  switch (ctrl_id) {  // (the DPP control must be a compile-time constant)
+    case 0: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0xB1, 0xF, 0xF, false);
+            rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0xB1, 0xF, 0xF, false); break;
+    case 1: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0x4E, 0xF, 0xF, false);
+            rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0x4E, 0xF, 0xF, false); break;
+    case 2: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0x141, 0xF, 0xF, false);
+            rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0x141, 0xF, 0xF, false); break;
+    case 3: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0x140, 0xF, 0xF, false);
+            rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0x140, 0xF, 0xF, false); break;
+    case 4: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0x142, 0xA, 0xF, false);
+            rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0x142, 0xA, 0xF, false); break;
+    default: rlo = __builtin_amdgcn_update_dpp(flo, lo, 0x143, 0xC, 0xF, false);
+             rhi = __builtin_amdgcn_update_dpp(fhi, hi, 0x143, 0xC, 0xF, false); break;
+  }
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)rhi << 32) | (uint32_t)rlo);
+}
+__device__ __forceinline__ float dpp_f32(float v, int ctrl_id, float fill) {
+  const int x = __builtin_bit_cast(int, v), f = __builtin_bit_cast(int, fill);
+  int r;
+  switch (ctrl_id) {
+    case 0: r = __builtin_amdgcn_update_dpp(f, x, 0xB1, 0xF, 0xF, false); break;
+    case 1: r = __builtin_amdgcn_update_dpp(f, x, 0x4E, 0xF, 0xF, false); break;
+    case 2: r = __builtin_amdgcn_update_dpp(f, x, 0x141, 0xF, 0xF, false); break;
+    case 3: r = __builtin_amdgcn_update_dpp(f, x, 0x140, 0xF, 0xF, false); break;
+    case 4: r = __builtin_amdgcn_update_dpp(f, x, 0x142, 0xA, 0xF, false); break;
+    default: r = __builtin_amdgcn_update_dpp(f, x, 0x143, 0xC, 0xF, false); break;
+  }
+  return __builtin_bit_cast(float, r);
+}
+__device__ __forceinline__ double lane63_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <int K>
+__device__ __forceinline__ void tree_sum_k(double (&v)[K]) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    double w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = dpp_f64(v[k], c, 0.0);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] += w[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = lane63_f64(v[k]);
+}
+template <int K>
+__device__ __forceinline__ void tree_min_k(float (&v)[K]) {
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    float w[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) w[k] = dpp_f32(v[k], c, INFINITY);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = w[k] < v[k] ? w[k] : v[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v[k]), 63));
+}
+__device__ __forceinline__ double tree_sum(double v) {
+  double a[1] = {v};
+  tree_sum_k<1>(a);
+  return a[0];
+}
+__device__ __forceinline__ float tree_min(float v) {
+  float a[1] = {v};
+  tree_min_k<1>(a);
+  return a[0];
+}
+
 // inclusive prefix sum across the 64 lanes (Hillis-Steele, fixed order => deterministic)
 template <typename T>
 __device__ __forceinline__ T wave_inclusive_scan(T v, int lane) {

@@ -142,8 +142,8 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
       m = t.node_min[level - 2][child];
     }
   }
-  s = wave_sum(s);
-  m = wave_min(m);
+  s = tree_sum(s);
+  m = tree_min(m);
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;

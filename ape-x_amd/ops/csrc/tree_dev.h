@@ -52,8 +52,8 @@ __device__ __forceinline__ void recompute_node(const TreeDesc& t, int level, int
       m = __hip_atomic_load(t.node_min[level - 2] + child, __ATOMIC_RELAXED, Scope);
     }
   }
-  s = wave_sum(s);
-  m = wave_min(m);
+  s = tree_sum(s);
+  m = tree_min(m);
   if (lane == 0) {
     t.node_sum[level - 1][node] = s;
     t.node_min[level - 1][node] = m;
@@ -119,8 +119,8 @@ __device__ __forceinline__ void update_levels_ilp(const TreeDesc& t, const int* 
         m[j] = ok ? dm[j] : INFINITY;
       }
     }
-    wave_sum_k<K>(s);
-    wave_min_k<K>(m);
+    tree_sum_k<K>(s);
+    tree_min_k<K>(m);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       if (node[j] >= 0 && lane == 0) {
@@ -161,7 +161,7 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
 // nodes this workgroup recomputes one level below, substituted from LDS -- then the levels
 // are reduced bottom-up through LDS only.  The level-synchronous walk (update_levels_ilp)
 // paid a load round trip and a store drain per level (~14 us for a 1M-slot tree, 4 levels).
-// Same per-node arithmetic (wave_sum of the 64 children as doubles, wave_min): the sums are
+// Same per-node arithmetic (tree_sum of the 64 children as doubles, tree_min): the sums are
 // bit-identical.  K: nodes per wave per level (distinct ancestors per level <= K x waves);
 // LP: the deepest tree handled (levels <= LP).
 template <int K, int LP>
@@ -268,20 +268,20 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
     // (levels near the root have 1-4 nodes)
     const int kn = nf > wave ? (nf - wave + nw - 1) / nw : 0;  // wave-uniform
     if (kn > K / 2) {
-      wave_sum_k<K>(sv);
-      wave_min_k<K>(mv);
+      tree_sum_k<K>(sv);
+      tree_min_k<K>(mv);
     } else if (kn > 1) {
       double s2[(K / 2 > 0 ? K / 2 : 1)];
       float m2[(K / 2 > 0 ? K / 2 : 1)];
 #pragma unroll
       for (int k = 0; k < K / 2; ++k) { s2[k] = sv[k]; m2[k] = mv[k]; }
-      wave_sum_k<(K / 2 > 0 ? K / 2 : 1)>(s2);
-      wave_min_k<(K / 2 > 0 ? K / 2 : 1)>(m2);
+      tree_sum_k<(K / 2 > 0 ? K / 2 : 1)>(s2);
+      tree_min_k<(K / 2 > 0 ? K / 2 : 1)>(m2);
 #pragma unroll
       for (int k = 0; k < K / 2; ++k) { sv[k] = s2[k]; mv[k] = m2[k]; }
     } else if (kn == 1) {
-      sv[0] = wave_sum(sv[0]);
-      mv[0] = wave_min(mv[0]);
+      sv[0] = tree_sum(sv[0]);
+      mv[0] = tree_min(mv[0]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
