@@ -220,10 +220,10 @@ class AQLEngineConfig:
     # (scripts/ab/aql_bwd_tree.sh; learner step 51.4 vs 55.7 us in scripts/bench_aql.py)
     fused_update: bool = True
     # with the priority write in the backward launch: its extra workgroup writes the leaves only
-    # and the gradient launch's extra workgroup walks the levels.  Measured slower than the whole
-    # write (leaves + one-round-trip level walk) in the backward's workgroup: 16.58k vs 16.82-16.86k
-    # SGD steps/s (the levels workgroup bounded the gradient launch: 15.1 vs ~5.5 us)
-    tree_levels_in_grad: bool = False
+    # and the gradient launch's extra workgroup walks the levels (the one-round-trip walk with
+    # DPP node reductions, tree_dev.h).  MI355X, interleaved: 17496-17518 vs 17358-17376 SGD
+    # steps/s with the whole write in the backward's workgroup (which outlasts the backward)
+    tree_levels_in_grad: bool = True
     # fused_update: the next step's PER draw in extra workgroups of the gradient launch (its
     # tree descent hides behind the contraction) instead of the update launch; not with
     # tree_levels_in_grad (the draw would read levels being written)
