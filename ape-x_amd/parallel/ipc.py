@@ -169,8 +169,16 @@ class IpcLearnerLinks:
 
     def __init__(self, R: int, D: int, E: int, P: int, store, prefix: str, device, *, packet_nbytes: int,
                  tables: dict, tree_write, cap: int | None = None, dead_after: float = 30.0,
-                 mode: int = MODE_UNCACHED, log=print, open_timeout: float = 300.0):
+                 mode: int = MODE_UNCACHED, log=print, open_timeout: float = 300.0,
+                 min_publish_interval: float = 0.002):
         self.hip = h = ops.hip()
+        # conflation floor between parameter publishes: a reader's copy of half v & 1 is clean
+        # unless the writer starts v + 2 before it lands; with the writer publishing every
+        # learner iteration (~0.2 ms for AQL) and the reader's copy queued behind the learner's
+        # kernels on a shared GPU, every seqlock retry could fail and an actor never install
+        # weights -- two publishes are now >= 2 x this apart
+        self.min_publish_interval = float(min_publish_interval)
+        self._pub_t = -1e30
         self.R, self.D, self.E, self.P = int(R), int(D), int(E), int(P)
         self.cap = self.D if cap is None else max(1, min(int(cap), self.D))
         self.device = torch.device(device)
@@ -275,14 +283,20 @@ class IpcLearnerLinks:
         n = self.slots_out.numel() if drain else self._n_out
         self.tree_write(self.slots_out[:n], self.prio_out[:n])
 
-    def publish(self, flat: torch.Tensor) -> None:
+    def publish(self, flat: torch.Tensor, force: bool = False) -> bool:
         """Conflated versioned publish (seqlock writer, all on the current stream): announce
-        ``v`` as being written, copy into params[v & 1], then release ``v`` as published."""
+        ``v`` as being written, copy into params[v & 1], then release ``v`` as published.
+        Skipped (False) within ``min_publish_interval`` of the previous one unless ``force``."""
+        now = time.monotonic()
+        if not force and now - self._pub_t < self.min_publish_interval:
+            return False
+        self._pub_t = now
         self.version += 1
         v, s = self.version, self._s()
         self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 4, v, s)
         self.hip.memcpy_async(self.arena + self.par_off + (v & 1) * 4 * self.P, flat.data_ptr(), 4 * self.P, s)
         self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 2, v, s)
+        return True
 
     def drop(self, r: int, why: str) -> None:
         if r in self.live:
