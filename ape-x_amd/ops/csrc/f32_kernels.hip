@@ -557,8 +557,11 @@ constexpr int kPlaneDw = kPlane / 4;  // 1764 dwords per plane
 //  fp32 chain's scale (error vs fp64: tests/test_gpu_f32_net.py).  On v_mfma_f32_16x16x32_bf16
 //  (16 cycles per 16x16x32) the 3 terms cost 48 cycles where v_mfma_f32_16x16x4_f32 pays
 //  8 x 32 = 256 for the same 16x16x32 of fp32: 5.3x fewer MFMA cycles.
-//  The sample's four planes are staged in LDS as bf16 (converted once); the layout of the
-//  workgroup, the waves and the fragments is described at f32_conv1_fwd_x3_k.
+//  Persistent over samples, two workgroups per CU (56 KB of LDS each: the sample's four
+//  planes as bf16, converted once while staging); the weight split is redone only when
+//  the problem changes.  Wave w: channels 16 (w >> 1) .. +15, output tiles w & 1, +2, ...
+//  of 16 pixels; lane (i = l & 15, q = l >> 4) holds A[pixel i][k = 8q + j] = plane c =
+//  kb >> 1, row 4 oy + 4 (kb & 1) + q, columns 4 ox + j: 8 consecutive bf16 of one row.
 struct W1Split {
   bfx8 hi[8], mid[8], lo[8];
 };
@@ -589,48 +592,39 @@ __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
   }
 }
 
-constexpr int kC1xChunks = 4 * (kPlane / 16);  // 16-byte u8 chunks of a sample's 4 planes
+// (A double-buffered 512-thread variant -- one workgroup per CU, the next sample staged from
+// inside the MFMA loop -- timed 42.9-43.5 vs 46.4-47.4 us alone but cost the whole learner step
+// ~3 % (2063-2067 vs 2125-2131 steps/s, scripts/ab/conv1_fullstep_ab.sh): its 113 KB of LDS per
+// CU leave no room for the actor graph's kernels running beside it.)
+// two workgroups per CU, each walking a contiguous run of samples (next sample prefetched):
+// 512 / 1024 workgroups 42.2 / 41.5-43.9 us, one sample per workgroup (1536) 44.4-45.0 us
+// (3 x 512 samples, interleaved on one box)
+constexpr int kC1xGrid = 512;
+constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
 
-// plane byte offsets (from the problem's frame base) of up to WIN samples, resolved by 4 WIN
-// threads at once (frame_plane's idx -> ids chain is two dependent round trips: not paid per
-// sample in front of its chunk loads)
-template <int WIN>
-__device__ __forceinline__ void c1x_resolve(const F32Set& set, int smp, int s1, int64_t* planes) {
-  const int t = threadIdx.x, sm = smp + (t >> 2);
-  if (t < 4 * WIN && sm < s1) {
-    const int B = set.B, prob = sm / B, b = sm - prob * B;
-    const F32Prob p = pick(set, prob);
-    const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
-    planes[t] = frame_plane(f, b, t & 3, kPlane) - static_cast<const uint8_t*>(p.in);
-  }
-}
-
-// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on); pl: its 4 plane
-// offsets; NT threads, ceil(1764 / NT) chunks each
-template <int NT = 256, int PER = (kC1xChunks + NT - 1) / NT>
-__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[PER], const int64_t* pl) {
-  const int B = set.B, prob = smp / B, t = threadIdx.x;
+// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on)
+__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer]) {
+  const int B = set.B, prob = smp / B, b = smp - prob * B, t = threadIdx.x;
   const F32Prob p = pick(set, prob);
-  const uint8_t* base = static_cast<const uint8_t*>(p.in);
-  const uint4* s0 = reinterpret_cast<const uint4*>(base + pl[0]);
-  const uint4* s1 = reinterpret_cast<const uint4*>(base + pl[1]);
-  const uint4* s2 = reinterpret_cast<const uint4*>(base + pl[2]);
-  const uint4* s3 = reinterpret_cast<const uint4*>(base + pl[3]);
+  const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
+  const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
+  const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
+  const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
+  const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
-    const int e = min(t + NT * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
+  for (int k = 0; k < kC1xPer; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
+    const int e = min(t + 256 * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
     const uint4* sc = c == 0 ? s0 : (c == 1 ? s1 : (c == 2 ? s2 : s3));
     v[k] = sc[e - c * 441];
   }
 }
 
 // registers -> LDS as bf16: chunk e = bf16 elements 16e .. 16e + 15 (7056 = 441 x 16)
-template <int NT = 256, int PER = (kC1xChunks + NT - 1) / NT>
-__device__ __forceinline__ void c1x_store(const uint4 (&v)[PER], uint32_t* xs) {
+__device__ __forceinline__ void c1x_store(const uint4 (&v)[kC1xPer], uint32_t* xs) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int e = t + NT * k;
+  for (int k = 0; k < kC1xPer; ++k) {
+    const int e = t + 256 * k;
     if (e < kC1xChunks) {
       const f32x4 a = u8x4(v[k].x), bq = u8x4(v[k].y), c = u8x4(v[k].z), d = u8x4(v[k].w);
       uint4* dst = reinterpret_cast<uint4*>(xs) + 2 * e;
@@ -642,6 +636,9 @@ __device__ __forceinline__ void c1x_store(const uint4 (&v)[PER], uint32_t* xs) {
   }
 }
 
+// Software-pipelined over the workgroup's samples: the next sample's frame chunks are
+// loaded into registers before this sample's MFMA loop, so the frame-ring (HBM) latency
+// hides behind compute; they are converted into LDS after the loop.
 // The two 8-byte halves of a pixel fragment load as two ds_read_b64 (2 LDS cycles each,
 // 256 B/clk) instead of the ds_read2_b64 the compiler would merge them into (8 cycles,
 // 128 B/clk): the second address is hidden from the load/store merger (one v_add per fragment;
@@ -650,55 +647,33 @@ __device__ __forceinline__ int opaque_i(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-
-// Persistent over a contiguous run of samples (the weight split is redone only at a problem
-// boundary), one 512-thread workgroup per CU with the sample planes double-buffered in LDS
-// (2 x 56 KB, bf16), 8 waves = 2 channel halves x 4 tile residues (tiles r, r + 4, ...: 7 / 6
-// of the 25 16-pixel tiles), 2 waves per SIMD.  Lane (i = l & 15, q = l >> 4) holds B[k][pixel
-// i] fragments of 8 consecutive bf16 of one kernel row (the roles are swapped on the MFMA: A =
-// the weight slice, so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte
-// store).  The NEXT sample's planes are converted into the other buffer from inside this
-// sample's MFMA loop (after the first tile: the conversion VALU and LDS stores issue between
-// the wave's MFMAs) and the sample after that is loaded right behind them.  MI355X, 3 x 512
-// samples: 42.9-43.5 us vs 46.4-47.4 for two single-buffered 256-thread workgroups per CU that
-// staged between two barriers (diagnostics of that kernel: 20 us without the staging, 31 us
-// without the output stores, 22 us without the MFMAs -- frame reads + 79 MB of fp32 output
-// make the kernel HBM-heavy).
-constexpr int kC1dGrid = 256, kC1dWin = 18;  // window: 16 samples + the two prefetched
-__global__ __launch_bounds__(512, 1) void f32_conv1_fwd_x3_k(F32Set set) {
-  __shared__ __attribute__((aligned(16))) uint32_t xs[2][2 * kPlaneDw * 4];  // 2 x 4 planes of bf16
-  __shared__ int64_t planes[4 * kC1dWin];
-  constexpr int NT = 512, PER = (kC1xChunks + NT - 1) / NT;
+__global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
+  __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
   const int B = set.B, total = set.n * B;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int i = lane & 15, q = lane >> 4, nh = wave & 1, part = wave >> 1;
-  const int nt = part == 0 ? 7 : 6;  // this wave's tiles: part + 4k, k < nt (25 tiles)
+  const int i = lane & 15, q = lane >> 4, nh = wave >> 1;
+  const __bf16* xb = reinterpret_cast<const __bf16*>(xs);
   W1Split w;
   int cur = -1;
-  uint4 v[PER];
+  uint4 v[kC1xPer];
+  // a contiguous run of samples per workgroup: the weight split is redone only at a
+  // problem boundary (a grid-strided walk crossed one at every sample: ~25 % of the VALU)
   const int per = (total + gridDim.x - 1) / gridDim.x;
   const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
-  if (s0 >= s1) return;  // block-uniform
-  int win = s0;
-  c1x_resolve<kC1dWin>(set, s0, s1, planes);
-  __syncthreads();
-  c1x_load<NT>(set, s0, v, planes);
-  c1x_store<NT>(v, xs[0]);
-  if (s0 + 1 < s1) c1x_load<NT>(set, s0 + 1, v, planes + 4);
-  __syncthreads();
+  if (s0 < s1) c1x_load(set, s0, v);
   for (int smp = s0; smp < s1; ++smp) {
-    const int prob = smp / B, b = smp - prob * B, buf = (smp - s0) & 1;
+    const int prob = smp / B, b = smp - prob * B;
     const F32Prob p = pick(set, prob);
     if (prob != cur) {  // block-uniform
       cur = prob;
       split_w1(p.w + (nh * 16 + i) * 256 + (q >> 1) * 16 + (q & 1) * 4, w);
     }
-    if (smp + 2 - win >= kC1dWin) {  // block-uniform: the next window (this sample and on)
-      win = smp;
-      c1x_resolve<kC1dWin>(set, win, s1, planes);
-      __syncthreads();
-    }
-    const __bf16* xb = reinterpret_cast<const __bf16*>(xs[buf]);
+    __syncthreads();  // the previous sample's tiles are done with xs
+    c1x_store(v, xs);
+    __syncthreads();
+    if (smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
+    // roles swapped on the MFMA (A = the weight slice, B = the pixels: identical lane maps),
+    // so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte store
     float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
     float4 bias4;
     bias4.x = p.bias[nh * 16 + 4 * q];
@@ -707,19 +682,21 @@ __global__ __launch_bounds__(512, 1) void f32_conv1_fwd_x3_k(F32Set set) {
     bias4.w = p.bias[nh * 16 + 4 * q + 3];
     // pixel fragments: lane (i, q = 2p + h) reads 4 columns 4 ox + 4h .. +3 of kernel rows 2p and
     // 2p + 1 (two ds_read_b64, 42 dwords apart).  Within a 32-lane LDS group (q = 0, 1) lane
-    // (ox, h = 1) reads the same dwords as lane (ox + 1, h = 0), so the group touches ~34
-    // consecutive dwords and broadcasts the rest: no bank conflicts
+    // (ox, h = 1) reads the same dwords as lane (ox + 1, h = 0) -- stride-4 windows overlap by 4
+    // columns -- so the group touches ~34 consecutive dwords and broadcasts the rest: no bank
+    // conflicts (rows in the lane groups gave 1.84 conflict cycles per LDS cycle)
     auto frags = [&](int tile, bfx8 (&a)[8]) {
       const int m = tile * 16 + i, oy = m / 20, ox = m - oy * 20;
       const __bf16* a0 = xb + (4 * oy + 2 * (q >> 1)) * 84 + 4 * ox + 4 * (q & 1);
 #pragma unroll
-      for (int kb = 0; kb < 8; ++kb) {
+      for (int kb = 0; kb < 8; ++kb) {  // 8-byte aligned: two ds_read_b64
         const uint2* ap = reinterpret_cast<const uint2*>(a0 + (kb >> 1) * kPlane + (kb & 1) * 4 * 84);
-        const uint2 lo = ap[0], hi = ap[opaque_i(21)];
+        const uint2 lo = ap[0], hi = ap[opaque_i(21)];  // next kernel row (84 bf16 = 21 x 8 bytes)
         a[kb] = __builtin_bit_cast(bfx8, make_uint4(lo.x, lo.y, hi.x, hi.y));
       }
     };
     auto tile_mfma = [&](int tile, const bfx8 (&a)[8]) {
+      // three accumulators (hi / mid / lo products): no MFMA waits on its predecessor's result
       f32x4 ah = zero4(), am = zero4(), al = zero4();
 #pragma unroll
       for (int kb = 0; kb < 8; ++kb) {
@@ -734,21 +711,21 @@ __global__ __launch_bounds__(512, 1) void f32_conv1_fwd_x3_k(F32Set set) {
       y.w = fmaxf(ah[3] + (am[3] + al[3]) + bias4.w, 0.f);
       *reinterpret_cast<float4*>(out + (size_t)(tile * 16 + i) * 32) = y;
     };
+    // ping-pong fragment buffers: the next tile's LDS reads are in flight during this tile's MFMAs.
+    // Wave parity t0 owns tiles t0, t0 + 2, ...: 6 pairs (+ tile 24 for t0 = 0); every fragment
+    // load is unconditional (the one past parity 1's last tile re-reads tile 24, unused), so the
+    // buffers keep fixed registers (guarded loads + a mid-loop exit made the compiler copy them)
     bfx8 fa[8], fb[8];
-    frags(part, fa);
-#pragma unroll
-    for (int pr = 0; pr < 3; ++pr) {
-      frags(part + 4 * (2 * pr + 1), fb);
-      tile_mfma(part + 4 * (2 * pr), fa);
-      if (pr == 0 && smp + 1 < s1) {  // block-uniform: stage the next sample, load the one after
-        c1x_store<NT>(v, xs[buf ^ 1]);
-        if (smp + 2 < s1) c1x_load<NT>(set, smp + 2, v, planes + 4 * (smp + 2 - win));
-      }
-      frags(part + 4 * min(2 * pr + 2, nt - 1), fa);  // (parts 1-3 re-read their last tile at the end: unused)
-      tile_mfma(part + 4 * (2 * pr + 1), fb);
+    const int t0 = wave & 1;
+    frags(t0, fa);
+    for (int pr = 0; pr < 6; ++pr) {
+      const int tile = t0 + 4 * pr;
+      frags(tile + 2, fb);
+      tile_mfma(tile, fa);
+      frags(min(tile + 4, 24), fa);
+      tile_mfma(tile + 2, fb);
     }
-    if (nt == 7) tile_mfma(part + 24, fa);
-    __syncthreads();  // the next sample's buffer is complete; this one's reads are done
+    if (t0 == 0) tile_mfma(24, fa);
   }
 }
 
@@ -1312,13 +1289,13 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-// c1_grid: conv1 workgroups (<= 0: kC1dGrid); tile 1: the learner's conv2 on 128 x 64 tiles at
+// c1_grid: conv1 workgroups (<= 0: kC1xGrid); tile 1: the learner's conv2 on 128 x 64 tiles at
 // BK 16 (the alternative to the default) -- per-call microbench parameters
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid, int tile) {
   check_set(set);
   switch (layer) {
     case 1:
-      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1dGrid), 512, 0, s>>>(set);
+      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
     case 2:  // learner: 64 x 64 tiles at BK 32: 79.0-80.4 us vs 87.0-88.5 for 128 x 64 at BK 16
