@@ -265,8 +265,7 @@ class DQNLearner:
             after = self._fork_point()
             n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
                                         sumsq=self.fin_partials if self.allreduce is None else None,
-                                        after_first=after,
-                                        **({"fc1_stream": self.fc1_stream} if self.fc1_stream is not None else {}))
+                                        after_first=after, fc1_stream=self.fc1_stream)
             if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n
