@@ -52,9 +52,6 @@ class LearnerConfig:
     # private buffers that the forward, loss and backward read: writers of the replay tables
     # may then run beside the step (the central topology's ingest, engine/central.py)
     private_rows: bool = False
-    # fp32 HIP net, single-process learner: the FC1 gradient finalize on a forked stream beside
-    # the conv backward (same partial slots: the grad norm is unchanged bit for bit)
-    fc1_finalize_fork: bool = True
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -162,8 +159,6 @@ class DQNLearner:
                                        device=dev)
             self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
             self.tree_stream = torch.cuda.Stream(device=dev)
-            # the FC1 gradient finalize forked beside the conv backward (fp32 HIP net)
-            self.fc1_stream = (torch.cuda.Stream(device=dev) if cfg.fc1_finalize_fork and self.fp32 else None)
             # single-process learner: grad_finalize writes the grad-norm partials (every
             # gradient passes through it), so no separate sum-of-squares pass; with an
             # all-reduce the norm must be taken after it (grad_sumsq)
@@ -265,7 +260,7 @@ class DQNLearner:
             after = self._fork_point()
             n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
                                         sumsq=self.fin_partials if self.allreduce is None else None,
-                                        after_first=after, fc1_stream=self.fc1_stream)
+                                        after_first=after)
             if self.allreduce is None:
                 assert n <= self.fin_partials.numel()
                 self.n_fin_partials = n

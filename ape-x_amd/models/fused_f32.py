@@ -240,42 +240,18 @@ class F32DuelingNet:
 
     def trunk_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
                        idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None,
-                       after_first=None, fc1_stream: torch.cuda.Stream | None = None) -> int:
+                       after_first=None) -> int:
         """FC1 + conv backward from ``ws.dz`` (fp32 dL/dz).  The conv weight-gradient
         partials (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes the
         per-workgroup sum-of-squares partials of EVERY gradient into ``sumsq`` (fp64) when
-        given; returns the partial count.  ``after_first()`` runs right after the first launch.
-        ``fc1_stream``: the FC1 slices' finalize (the largest: 1.6M weights transposed) runs
-        there, forked right after the FC1 backward, beside the conv chain, writing the same
-        partial slots it would in the single launch (same norm, bit for bit); joined before
-        returning."""
+        given; returns the partial count.  ``after_first()`` runs right after the first launch."""
         self.enable_backward(ws.B)
         fc1_jobs = self._fc1_bwd(ws)
         if after_first is not None:
             after_first()
-        h, s = self.hip, self._s()
-        if fc1_stream is None:
-            jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs) + fc1_jobs
-            return h.grad_finalize(jobs, s, 0 if sumsq is None else sumsq.data_ptr())
-        main = torch.cuda.current_stream()
-        fc1_stream.wait_stream(main)
-        conv_jobs = self._conv_jobs(ws)
-        n_main = h.grad_finalize_blocks(conv_jobs + list(extra_jobs))
-        with torch.cuda.stream(fc1_stream):
-            n_fc1 = h.grad_finalize(fc1_jobs, fc1_stream.cuda_stream,
-                                    0 if sumsq is None else sumsq.data_ptr() + 8 * n_main)
-        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs)
-        n = h.grad_finalize(jobs, s, 0 if sumsq is None else sumsq.data_ptr())
-        assert n == n_main
-        main.wait_stream(fc1_stream)
-        return n + n_fc1
-
-    def _conv_jobs(self, ws: F32Workspace) -> list:
-        """The finalize jobs :meth:`_conv_chain` returns (for counting their partials ahead)."""
-        B, f = ws.B, self.model.features
-        w1, w2, w3 = self._wgrad_wss
-        return [self.hip.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
-                                               f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
+        h = self.hip
+        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs) + fc1_jobs
+        return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr())
 
 
 def forward_multi_f32(passes, act: tuple | None = None) -> None:

@@ -398,13 +398,6 @@ PYBIND11_MODULE(_apex_hip, m) {
     fs.sumsq = P<double>(sumsq);
     return grad_finalize(fs, S(s));
   }, py::arg("jobs"), py::arg("s"), py::arg("sumsq") = 0);
-  m.def("grad_finalize_blocks", [](const std::vector<FinalizeJob>& jobs) {  // its sumsq partial count
-    if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..6 jobs");
-    FinalizeSet fs{};
-    for (size_t i = 0; i < jobs.size(); ++i) fs.job[i] = jobs[i];
-    fs.n = (int)jobs.size();
-    return grad_finalize_blocks(fs);
-  });
   m.def("wgrad_grid", &wgrad_grid);
   m.def("dqn_heads_bwd_blocks", &dqn_heads_bwd_blocks);
   m.def("dqn_heads_bwd", [](py::dict d, int B, int A, float gamma_n, uint64_t s) {

@@ -101,8 +101,6 @@ def parse():
                     help="AQL: tree levels walked in the gradient launch (1) or in the backward's tree workgroup (0)")
     ap.add_argument("--aql-draw-in-grad", type=int, default=None,
                     help="AQL: the next step's draw in the gradient launch (1) or the update launch (0)")
-    ap.add_argument("--fc1-fork", type=int, default=None,
-                    help="FC1 gradient finalize forked beside the conv backward (1, default) or in line (0)")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=560.0,
@@ -241,8 +239,6 @@ def main():
         raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
     rank_batch = args.batch // world if args.scaling == "strong" else args.batch
     lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank)
-    if args.fc1_fork is not None:
-        lc.fc1_finalize_fork = bool(args.fc1_fork)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
