@@ -140,6 +140,7 @@ __global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __
     return;
   }
   __shared__ __attribute__((aligned(16))) float w1[AQ_CAT * kPropPitch];
+  __shared__ __attribute__((aligned(16))) float w2[64 * kPropPitch];  // dist_feature.2 [na <= 64][128]
   __shared__ __attribute__((aligned(16))) float emb[kPropStates][AQ_CAT], hid[kPropStates][AQ_CAT];
   __shared__ float mu[kPropStates][64];
   __shared__ int perm[kPropStates][64];
@@ -159,6 +160,9 @@ __global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __
     } else {
       for (int e = t; e < AQ_CAT * AQ_CAT; e += 256) w1[(e >> 7) * kPropPitch + (e & 127)] = net.df_w1[e];
     }
+    // dist_feature.2 [na][128] (a row per lane below: one wave read 64 rows 512 bytes apart per
+    // load, 128 loads deep)
+    for (int e = t; e < net.na * AQ_CAT; e += 256) w2[(e >> 7) * kPropPitch + (e & 127)] = net.df_w2[e];
   }
   // state embedding: features = Linear(obs -> 128) + ReLU (model.py:289-291); thread (j, half):
   // states half, half + 2 of the workgroup (clamped past B: computed, never written out)
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __
   const bool valid = b < B;
   if (lane < A) {
     float acc = net.df_b2[lane];
-    for (int i = 0; i < AQ_CAT; ++i) acc += net.df_w2[lane * AQ_CAT + i] * hid[wave][i];
+    for (int i = 0; i < AQ_CAT; ++i) acc += w2[lane * kPropPitch + i] * hid[wave][i];
     mu[wave][lane] = acc;
     if (mu_out && valid) mu_out[(size_t)b * A + lane] = acc;
   }

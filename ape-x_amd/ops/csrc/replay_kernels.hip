@@ -174,7 +174,23 @@ __global__ __launch_bounds__(1024) void per_write_ring_fused_k(TreeDesc t, const
     if (bump0) *bump0 += d0;
     if (bump1) *bump1 += d1;
   }
-  update_levels_block(t, sids, B, 1, t.levels);
+  // a ring chunk dirties ~B / 64 level-1 nodes: one representative slot per distinct level-1
+  // node (ring order: duplicates are adjacent), then the one-round-trip walk over those
+  __shared__ int comp[64];
+  __shared__ int ncomp;
+  if (threadIdx.x == 0) ncomp = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < B; i += blockDim.x) {
+    const int id = sids[i];
+    if (id < 0 || id >= t.size[0]) continue;
+    const int prev = i > 0 ? sids[i - 1] : -1;
+    if (prev >= 0 && prev < t.size[0] && (prev >> kTreeLog2Fanout) == (id >> kTreeLog2Fanout)) continue;
+    const int k = atomicAdd(&ncomp, 1);
+    if (k < 64) comp[k] = id;
+  }
+  __syncthreads();
+  if (ncomp <= 64) update_levels_fast<4>(t, comp, ncomp);  // (order-free: node values deterministic)
+  else update_levels_block(t, sids, B, 1, t.levels);
 }
 
 // The small top levels of a batched (random-slot) update in one workgroup.
