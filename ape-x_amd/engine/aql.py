@@ -224,6 +224,9 @@ class AQLEngineConfig:
     # DPP node reductions, tree_dev.h).  MI355X, interleaved: 17496-17518 vs 17358-17376 SGD
     # steps/s with the whole write in the backward's workgroup (which outlasts the backward)
     tree_levels_in_grad: bool = True
+    # with tree_levels_in_grad: the lowest levels still walked by the backward's workgroup (it
+    # has slack behind the per-sample backward), the rest by the gradient launch
+    tree_levels_in_bwd: int = 1
     # fused_update: the next step's PER draw in extra workgroups of the gradient launch (its
     # tree descent hides behind the contraction) instead of the update launch; not with
     # tree_levels_in_grad (the draw would read levels being written)
@@ -339,10 +342,11 @@ class AQLLearner:
                           if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
         bwd = (cfg.bwd_tree or cfg.fused_update) and self.post_tree is None and not cfg.fork_tree and B <= 64
         lv = bwd and cfg.tree_levels_in_grad
+        nb = int(cfg.tree_levels_in_bwd) if lv else -1  # levels the backward's workgroup walks (-1: all)
         self.L_tree = (h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
                                             r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha,
-                                            levels=0 if lv else 1) if bwd else None)
-        self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B) if lv else None
+                                            levels=nb) if bwd else None)
+        self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B, lo=nb + 1) if lv else None
         split = (cfg.split_tree and self.post_tree is None and self.L_tree is None and not cfg.fork_tree
                  and B <= 64)
         self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),

@@ -672,13 +672,14 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   w.mix.lw = s_lw;
   batch_leaves_block(tree, w, 0, tred, sids);
   stamp(2);
-  if (levels) update_levels_fast(tree, sids, B, L.dbg ? L.dbg + 24 : nullptr);  // (dbg[24..29]: walk phases)
+  if (levels > 0)  // levels 1..levels (dbg[24..29]: walk phases)
+    update_levels_fast(tree, sids, B, L.dbg ? L.dbg + 24 : nullptr, 1, levels);
   stamp(3);
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
   if (L.bwd_tree && blockIdx.x == L.B) {  // block-uniform: the priority write (aql_learn_set_tree)
-    td_tree_block(L, L.tree, L.bw, L.bwd_tree == 1);
+    td_tree_block(L, L.tree, L.bw, L.bwd_tree == 1 ? 1 << 30 : L.bwd_levels);
     return;
   }
   aql_bwd_block(L, blockIdx.x);
@@ -964,7 +965,7 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G, const AqlS
     __shared__ int sids[64];
     if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
       for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
-      update_levels_fast(G.tree, sids, G.bw.B);
+      update_levels_fast(G.tree, sids, G.bw.B, nullptr, max(G.levels_lo, 1));
     } else {
       batch_leaves_block(G.tree, G.bw, 0, tred, sids);
     }
@@ -982,7 +983,7 @@ __global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict
   if (bid < B) {
     aql_bwd_block(D.L, bid);
   } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
-    td_tree_block(D.L, D.tree, D.bw, 1);
+    td_tree_block(D.L, D.tree, D.bw, 1 << 30);
   } else {
     const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
     const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;

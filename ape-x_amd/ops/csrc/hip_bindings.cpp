@@ -629,23 +629,25 @@ PYBIND11_MODULE(_apex_hip, m) {
     w.alpha = alpha;
     if (!w.idx || !w.owner || !w.list || !w.max_prio || L.B < 1 || L.B > 64)
       throw std::invalid_argument("aql_learn_set_tree: 1 <= B <= 64 and every pointer");
-    L.bwd_tree = levels ? 1 : 2;
+    L.bwd_tree = levels < 0 ? 1 : 2;  // levels < 0: every level; else levels 1..levels (0: leaves only)
+    L.bwd_levels = levels < 0 ? 0 : levels;
     L.tree = t.d;
     L.bw = w;
     return L;
   }, py::arg("L"), py::arg("tree"), py::arg("prio_out"), py::arg("loss_out"), py::arg("owner"), py::arg("list"),
-     py::arg("max_prio"), py::arg("alpha"), py::arg("levels") = 1);
-  m.def("aql_grad_set_levels", [](const AqlGrad& g0, const TreeHandle& t, uint64_t list, int B) {
+     py::arg("max_prio"), py::arg("alpha"), py::arg("levels") = -1);
+  m.def("aql_grad_set_levels", [](const AqlGrad& g0, const TreeHandle& t, uint64_t list, int B, int lo) {
     AqlGrad g = g0;
     BatchWrite w{};
     w.list = P<int>(list);
     w.B = B;
     if (!w.list || B < 1 || B > 64) throw std::invalid_argument("aql_grad_set_levels: 1 <= B <= 64 and a list");
     g.tree_leaves = 2;
+    g.levels_lo = lo;
     g.tree = t.d;
     g.bw = w;
     return g;
-  });
+  }, py::arg("G"), py::arg("tree"), py::arg("list"), py::arg("B"), py::arg("lo") = 1);
   m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups, int halves) {  // groups 0: the launcher picks
     if (halves != 0 && halves != 1 && halves != 2) throw std::invalid_argument("aql_learn_set_groups: halves 0, 1 or 2");
     AqlLearn L = L0;

@@ -456,7 +456,8 @@ struct AqlLearn {
   // priority write in the backward launch (aql_learn_set_tree): one extra workgroup recomputes
   // the B TD terms from the forward's Q rows (aql_td, the backward's own formula) and runs the
   // batched tree write (leaves + every level, B <= 64) beside the per-sample backward
-  int bwd_tree;  // 1: leaves + every level, 2: leaves only (aql_grad_set_levels walks the levels)
+  int bwd_tree;  // 1: leaves + every level, 2: leaves + levels 1..bwd_levels (aql_grad_set_levels walks the rest)
+  int bwd_levels;
   BatchWrite bw;
   // learner forward: candidate-tile groups per (sample, net) workgroup item (0 = about one
   // workgroup per CU; act_mode: 0 = one tile per item)
@@ -488,7 +489,8 @@ struct AqlGrad {
   // split priority write (aql_grad_set_tree): one extra workgroup writes this step's leaves
   // (per_write_batch's leaves part, B <= 64) and the dirty list; the noise-reset launch's
   // extra workgroup then walks the levels (AqlPost::tree_write = 2)
-  int tree_leaves;  // 1: the leaves; 2: the levels only (the backward launch wrote the leaves + list)
+  int tree_leaves;  // 1: the leaves; 2: levels levels_lo.. only (the backward launch wrote the leaves + list)
+  int levels_lo;
   TreeDesc tree;
   BatchWrite bw;
 };

@@ -166,7 +166,7 @@ __device__ __forceinline__ void update_levels_block(const TreeDesc& t, const int
 // LP: the deepest tree handled (levels <= LP).
 template <int K, int LP>
 __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const int* sids, int n,
-                                                      long long* dbg = nullptr) {
+                                                      long long* dbg = nullptr, int lo = 1, int hi = 1 << 30) {
   __shared__ int s_first[LP][64];    // per level: rank -> candidate index of each distinct ancestor's first
   __shared__ int s_rank[LP][64];     // per level: first candidate -> its rank
   __shared__ int s_firstof[LP][64];  // per level: candidate -> the first candidate of its ancestor
@@ -177,12 +177,14 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
   __shared__ double s_os[LP][64];           // every level's new values, stored at the end
   __shared__ float s_om[LP][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, tid = threadIdx.x;
-  const int L = t.levels, n0 = t.size[0];
+  // levels lo..L of the walk (lo > 1: levels below are final in memory -- written by an earlier
+  // launch -- so level lo substitutes nothing, as level 1 over the leaves)
+  const int L = min(t.levels, hi), n0 = t.size[0];
   __syncthreads();  // the caller's leaf writes (workgroup scope) and sids are in place
   // 1) the distinct ancestors per level: one wave per level, lane = candidate, the ancestors
   //    compared through readlane (no LDS round trips); compacted in candidate order (ballot),
   //    so the work split is deterministic
-  for (int l = 1 + wave; l <= L; l += nw) {
+  for (int l = lo + wave; l <= L; l += nw) {
     const int sh = kTreeLog2Fanout * l;
     const int id = lane < n ? sids[lane] : -1;
     const bool ok = id >= 0 && id < n0;
@@ -210,6 +212,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
 #pragma unroll
   for (int l = 1; l <= LP; ++l) {
     if (l > L) break;  // uniform
+    if (l < lo) continue;
     const int sh = kTreeLog2Fanout * l, csize = t.size[l - 1], nf = s_nfirst[l - 1];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -231,6 +234,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
 #pragma unroll
   for (int l = 1; l <= LP; ++l) {
     if (l > L) break;  // uniform
+    if (l < lo) continue;
     const int sh = kTreeLog2Fanout * l, csize = t.size[l - 1], nf = s_nfirst[l - 1];
     double sv[K];
     float mv[K];
@@ -243,7 +247,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
       sv[k] = okc ? ps[l - 1][k] : 0.0;
       mv[k] = okc ? pm[l - 1][k] : INFINITY;
     }
-    if (l >= 2) {
+    if (l > lo) {
       const int nfc = s_nfirst[l - 2];
 #pragma unroll
       for (int k = 0; k < K; ++k) s_inv[wave + k * nw][lane] = -1;
@@ -297,7 +301,7 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
     if (dbg && threadIdx.x == 0) dbg[l] = (long long)clock64();
   }
   // 4) every new node value out at once (nothing in this workgroup reads them back)
-  for (int l = 1; l <= L; ++l) {
+  for (int l = lo; l <= L; ++l) {
     const int sh = kTreeLog2Fanout * l;
     for (int r = tid; r < s_nfirst[l - 1]; r += blockDim.x) {
       const int node = sids[s_first[l - 1][r]] >> sh;
@@ -311,14 +315,17 @@ __device__ __forceinline__ void update_levels_oneshot(const TreeDesc& t, const i
 // KMAX caps the per-wave node count compiled in (its prefetch registers: 3 LP KMAX VGPRs),
 // e.g. 4 for 1024-thread workgroups (128 VGPRs)
 template <int KMAX = 16>
-__device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int* sids, int n, long long* dbg = nullptr) {
+__device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int* sids, int n, long long* dbg = nullptr,
+                                                   int lo = 1, int hi = 1 << 30) {
   const int nw = blockDim.x >> 6;
+  hi = min(hi, t.levels);
+  if (lo > hi) return;
   if (n >= 1 && n <= 64 && t.levels <= 5) {  // block-uniform
-    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n, dbg);
-    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n, dbg);
-    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n, dbg);
+    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n, dbg, lo, hi);
+    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n, dbg, lo, hi);
+    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n, dbg, lo, hi);
   }
-  update_levels_block(t, sids, n, 1, t.levels);
+  update_levels_block(t, sids, n, lo, hi);
 }
 
 // The batched tree write of one workgroup (any block size >= 64 and >= B): the actor rows'

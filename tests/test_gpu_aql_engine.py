@@ -288,13 +288,15 @@ def test_fused_sampling_equals_per_sample(cuda):
                 (True, False, False, True, False, False, False), (False, False, False, True, False, False, False),
                 (True, False, False, False, True, False, False), (False, False, False, False, True, False, True),
                 (True, False, False, False, False, True, True), (False, False, False, False, False, True, True),
-                (True, False, False, False, False, True, False), (True, False, False, False, False, True, None))
+                (True, False, False, False, False, True, False), (True, False, False, False, False, True, None),
+                (True, False, False, False, False, True, 2))
     for fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update, lv in variants:
         # lv None: draw in the update launch (draw_in_grad off), levels in the backward's workgroup
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
                               fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree,
                               fused_step=fused_step, bwd_tree=bwd_tree, fused_update=fused_update,
-                              tree_levels_in_grad=bool(lv), draw_in_grad=lv is not None)
+                              tree_levels_in_grad=bool(lv), draw_in_grad=lv is not None,
+                              tree_levels_in_bwd=2 if lv == 2 else (1 if lv else 0))
         eng = AQLEngine(cfg, cuda)
         L = eng.learner
         assert (L.Ls is not None) == fused_sample
