@@ -141,6 +141,8 @@ __global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __
   }
   __shared__ __attribute__((aligned(16))) float w1[AQ_CAT * kPropPitch];
   __shared__ __attribute__((aligned(16))) float w2[64 * kPropPitch];  // dist_feature.2 [na <= 64][128]
+  __shared__ float fw[AQ_CAT * 65];                                  // q.features [128][obs <= 64] (pitch 65)
+  __shared__ float sst[kPropStates][64];                             // the workgroup's states
   __shared__ __attribute__((aligned(16))) float emb[kPropStates][AQ_CAT], hid[kPropStates][AQ_CAT];
   __shared__ float mu[kPropStates][64];
   __shared__ int perm[kPropStates][64];
@@ -163,15 +165,22 @@ __global__ __launch_bounds__(256) void aql_propose_k(AQLNet net, const float* __
     // dist_feature.2 [na][128] (a row per lane below: one wave read 64 rows 512 bytes apart per
     // load, 128 loads deep)
     for (int e = t; e < net.na * AQ_CAT; e += 256) w2[(e >> 7) * kPropPitch + (e & 127)] = net.df_w2[e];
+    // q.features and the states: a runtime-length loop of global loads feeding FMAs waited out
+    // one L2 round trip per input (obs of them) for the embedding
+    for (int e = t; e < AQ_CAT * net.obs; e += 256) fw[(e / net.obs) * 65 + e % net.obs] = net.f_w[e];
+    for (int e = t; e < kPropStates * net.obs; e += 256) {
+      const int s2 = e / net.obs;
+      sst[s2][e - s2 * net.obs] = state[(size_t)min(b0 + s2, B - 1) * net.obs + (e - s2 * net.obs)];
+    }
   }
+  __syncthreads();
   // state embedding: features = Linear(obs -> 128) + ReLU (model.py:289-291); thread (j, half):
   // states half, half + 2 of the workgroup (clamped past B: computed, never written out)
   const int j = t & 127, hs = t >> 7;
 #pragma unroll
   for (int s2 = hs; s2 < kPropStates; s2 += 2) {
-    const float* sp = state + (size_t)min(b0 + s2, B - 1) * net.obs;
     float acc = net.f_b[j];
-    for (int i = 0; i < net.obs; ++i) acc += net.f_w[j * net.obs + i] * sp[i];
+    for (int i = 0; i < net.obs; ++i) acc += fw[j * 65 + i] * sst[s2][i];
     emb[s2][j] = fmaxf(acc, 0.f);
   }
   __syncthreads();
@@ -296,6 +305,7 @@ void aql_propose(const AQLNet& net, const float* state, int B, const float* low,
                  uint64_t seed, const int64_t* counter, float* a_mu, float* mu_out, hipStream_t s, float* eff_ws) {
   if (B <= 0) return;
   if (net.na < 1 || net.na > 64) throw std::invalid_argument("aql_propose: 1 <= actions <= 64");
+  if (net.obs < 1 || net.obs > 64) throw std::invalid_argument("aql_propose: 1 <= obs <= 64");
   if (!net.cont && net.uniform > net.na) throw std::invalid_argument("aql_propose: uniform > actions (discrete)");
   const int pb = (B + kPropStates - 1) / kPropStates;
   const int eb = eff_ws ? (int)((aql_workspace_floats() + 255) / 256) : 0;
