@@ -610,8 +610,8 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
 // rows (aql_td: the formula the backward writes L.delta / L.lw with), then the batched tree
 // write (leaves, mix, loss mean, every level).  Only the next step's sampler reads the tree.
 __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc& tree, BatchWrite w, int levels) {
-  __shared__ float s_dl[64], s_lw[64], tred[16], s_qa[64], s_r[64], s_dn[64], s_wb[64];
-  __shared__ int sids[64], s_next[64];
+  __shared__ float s_dl[64], s_lw[64], tred[16], s_r[64], s_dn[64], s_wb[64];
+  __shared__ int sids[64], s_next[64], s_act[64];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = (int)(blockDim.x >> 6), T = L.on.T, B = L.B;
   auto stamp = [&](int k) {  // diagnostics (APEX_AQL_DBG): tree-workgroup phase timestamps
     if (L.dbg && t == 0) L.dbg[16 + k] = (long long)clock64();
@@ -620,12 +620,13 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   // the B TD terms with every sample's loads in flight together (a wave-per-sample loop paid ~4
   // dependent round trips per sample, ~29 us for 32 samples): the scalar chains idx -> act ->
   // Q(s, a) on one thread per sample, the argmaxes of Q(s', .) 4 samples per wave at a time
-  if (t < B) {
-    const int row = L.idx[t];
-    s_qa[t] = L.q_s[(size_t)t * T + L.act[row]];
-    s_r[t] = L.rew[row];
-    s_dn[t] = L.done[row];
-    s_wb[t] = L.w[t];
+  const int tc = t - ((int)blockDim.x - 64);  // the last wave: its chain beside the others' argmaxes
+  if (tc >= 0 && tc < B) {  // (Q(s, a) is loaded after the barrier, beside Q_tgt(s', argmax): one round trip)
+    const int row = L.idx[tc];
+    s_act[tc] = L.act[row];
+    s_r[tc] = L.rew[row];
+    s_dn[tc] = L.done[row];
+    s_wb[tc] = L.w[tc];
   }
   if (T <= 256) {
     for (int b0 = wave * 4; b0 < B; b0 += 4 * nw) {  // wave-uniform
@@ -662,7 +663,8 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   }
   __syncthreads();
   if (t < B) {
-    const AqlTd td = aql_td_vals(L, s_qa[t], L.qt_s2[(size_t)t * T + s_next[t]], s_r[t], s_dn[t], s_wb[t]);
+    const float qa = L.q_s[(size_t)t * T + s_act[t]], qt = L.qt_s2[(size_t)t * T + s_next[t]];
+    const AqlTd td = aql_td_vals(L, qa, qt, s_r[t], s_dn[t], s_wb[t]);
     s_dl[t] = td.dl;
     s_lw[t] = td.lw;
   }
