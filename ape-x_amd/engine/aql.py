@@ -365,6 +365,9 @@ class AQLLearner:
                        exclude_last=0 if cfg.exact_mass else 1)
         nb = h.aql_step_nbytes()
         self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
+        self.pub_desc = torch.zeros(nb, dtype=torch.uint8, device=dev)
+        self._step_kw = kw
+        self.U_pub = None
         if cfg.fused_step and not cfg.fork_tree and B <= 64:
             try:
                 self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
@@ -380,6 +383,22 @@ class AQLLearner:
                 self.U_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp,
                                               dict(kw, update=1, **draw_kw), self.step_desc[1].data_ptr())
         self.refresh()
+
+    def set_publish(self, actor_flat: torch.Tensor, actor_eps: torch.Tensor) -> None:
+        """The iteration's last step can write the acting copies (weights + online noise) from
+        its update launch (``step(publish=True)``) instead of two copy launches after it."""
+        if self.U is None:
+            return
+        e0 = self.eps.data_ptr()
+        sub = lambda buf: actor_eps.data_ptr() + (buf.data_ptr() - e0)  # noqa: E731
+        a1, a2 = self.model.q.advantage1, self.model.q.advantage2
+        assert actor_flat.numel() == self.P and actor_eps.numel() == self.eps.numel()
+        self._pub_keep = (actor_flat, actor_eps)
+        self.U_pub = self.hip.make_aql_step(
+            self.L, self.G, self.post, self.replay.tree, self.hp,
+            dict(self._step_kw, update=1, pub_p=actor_flat.data_ptr(), pub_weps0=sub(a1.weight_epsilon),
+                 pub_beps0=sub(a1.bias_epsilon), pub_weps1=sub(a2.weight_epsilon), pub_beps1=sub(a2.bias_epsilon)),
+            self.pub_desc.data_ptr())
 
     @property
     def predraw(self) -> bool:
@@ -442,7 +461,7 @@ class AQLLearner:
             torch.cuda.current_stream().wait_stream(self.tree_stream)
             self._tree_pending = False
 
-    def step(self, drawn: bool = False, draw_next: bool = False) -> None:
+    def step(self, drawn: bool = False, draw_next: bool = False, publish: bool = False) -> bool:
         """One SGD step.  ``drawn``: this step's rows were sampled by the previous step's fused
         tail (``draw_next`` there) -- the forward skips its tree descent; both need the fused
         step tail and fused sampling (:meth:`AQLEngine.learn_steps` pairs them within an
@@ -485,14 +504,15 @@ class AQLLearner:
             tree_write(s)
         G = self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G)
         if self.U is not None:  # optimizers, noise of both critics, proposal copy (+ next draw): one launch
+            pub = publish and not draw_next and self.U_pub is not None
             if draw_next and self.cfg.draw_in_grad and self.G_levels is None:  # (levels in that launch: racy)
                 h.aql_grad_draw(G, self.U_draw, s)
                 h.aql_update(self.U, s)
             else:
                 h.aql_grad(G, s)
-                h.aql_update(self.U_draw if draw_next else self.U, s)
+                h.aql_update(self.U_draw if draw_next else (self.U_pub if pub else self.U), s)
             self._track_losses()
-            return
+            return pub
         h.aql_grad(G, s)
         Pq, o = self.P_q, 4 * self.P_q
         # the two optimizers (critic, proposal; own clip norms) in one launch
@@ -618,6 +638,11 @@ class AQLEngine:
         # the learner's graph applies the other half (the previous acting step's) to the ring
         # before its first sample, so acting never touches a table or tree the learner reads
         self.overlap = bool(cfg.overlap)
+        # serial mode: the iteration's last SGD step writes the acting copies from its update
+        # launch (no publish copies after it); overlap mode publishes after the acting step
+        if not self.overlap:
+            self.learner.set_publish(self.actor_flat, self.actor_eps)
+        self._pub_in_graph = False
         self._half = 0
         if self.overlap:
             assert not cfg.fork_tree, "overlap and fork_tree are exclusive"
@@ -697,13 +722,17 @@ class AQLEngine:
         h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, 0, 0, s)
 
-    def learn_steps(self) -> None:
+    def learn_steps(self, publish: bool = False) -> bool:
         """The iteration's K SGD steps; with the fused tail, each step but the last also draws the
-        next step's rows (nothing inserts between them), so only the first forward samples."""
+        next step's rows (nothing inserts between them), so only the first forward samples.
+        ``publish``: the last step also writes the acting copies (returns whether it did)."""
         pre = self.learner.predraw
+        pub = False
         for k in range(self.K):
-            self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K)
+            pub = bool(self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K,
+                                         publish=publish and k + 1 == self.K))
         self.learner.join()  # (a captured graph must end joined)
+        return pub
 
     def fill(self, threshold: int | None = None) -> None:
         """Act until the replay holds more than ``threshold`` transitions (AQL_dis.py:120:
@@ -748,7 +777,7 @@ class AQLEngine:
             self.actor_step()
         self._g_learn = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_learn):
-            self.learn_steps()
+            self._pub_in_graph = self.learn_steps(publish=True)
         torch.cuda.synchronize(self.device)
 
     def _beta(self) -> float:
@@ -766,9 +795,11 @@ class AQLEngine:
             self.actor_step()
         if self._g_learn is not None:
             self._g_learn.replay()
+            pub = self._pub_in_graph
         else:
-            self.learn_steps()
-        self.publish()
+            pub = self.learn_steps(publish=True)
+        if not pub:
+            self.publish()
         before = self.learner_steps
         self.learner_steps += self.K
         if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):

@@ -908,6 +908,7 @@ __device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g,
       D.m[i] = a;
       D.v[i] = b;
       D.p[i] = pn;
+      if (D.pub_p) D.pub_p[i] = pn;
       if (prop) D.P.dst[i - D.P_q] = pn;
       if (kind >= 2) {
         const AqlNoise& z = D.P.layer[l];
@@ -917,14 +918,17 @@ __device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g,
         D.m[im] = a2;
         D.v[im] = b2;
         D.p[im] = mun;
+        if (D.pub_p) D.pub_p[im] = mun;
         if (kind == 2) {
           const int o = (int)(e / z.in), c = (int)(e - (int64_t)o * z.in);
           const float ep = noise_w(D.P.seed, l, o, c, st);
           z.weps[e] = ep;
+          if (D.pub_weps[l]) D.pub_weps[l][e] = ep;
           z.weff[e] = fmaf(pn, ep, mun);
         } else {
           const float ep = scaled_noise(D.P.seed, l, 2, (int)e, st);
           z.beps[e] = ep;
+          if (D.pub_beps[l]) D.pub_beps[l][e] = ep;
           z.beff[e] = fmaf(pn, ep, mun);
         }
       }

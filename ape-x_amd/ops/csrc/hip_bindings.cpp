@@ -807,6 +807,11 @@ PYBIND11_MODULE(_apex_hip, m) {
       d.seed = g("seed");
       d.exclude_last = p["exclude_last"].cast<int>();
     }
+    if (p.contains("pub_p")) {  // the acting copies (the iteration's last step publishes)
+      d.pub_p = P<float>(g("pub_p"));
+      d.pub_weps[0] = P<float>(g("pub_weps0")); d.pub_weps[1] = P<float>(g("pub_weps1"));
+      d.pub_beps[0] = P<float>(g("pub_beps0")); d.pub_beps[1] = P<float>(g("pub_beps1"));
+    }
     const int upd = p.contains("update") ? p["update"].cast<int>() : 0;
     aql_step_check(d, !upd);
     HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));

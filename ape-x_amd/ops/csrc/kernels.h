@@ -553,6 +553,11 @@ struct AqlStep {
   const float* beta;
   uint64_t seed;
   int exclude_last;
+  // optional publish (the iteration's last step): every updated parameter and the online noise
+  // also written into the acting copies (set_worker_weights without the two copy launches)
+  float* pub_p;
+  float* pub_weps[2];
+  float* pub_beps[2];
 };
 int aql_step_grid(const AqlStep& d);
 // shapes, pointers, and (coresident) that the fused tail's grid fits co-resident

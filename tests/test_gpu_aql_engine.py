@@ -378,3 +378,22 @@ def test_propose_mu_matches_fp64_and_fused_eff(cuda, env_id):
     torch.cuda.synchronize()
     assert torch.equal(eng.amu, am0)
     assert torch.equal(eng.ws, ws0)
+
+
+def test_last_step_publishes_acting_copies(cuda):
+    """Serial engine: the iteration's last SGD step writes the acting weights and online noise
+    from its update launch (no publish copies) -- they equal the learner's after every
+    iteration, eager and graph-replayed."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    eng = AQLEngine(AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=4), cuda)
+    L = eng.learner
+    assert L.U_pub is not None
+    eng.fill(1024)
+    for it in range(6):
+        if it == 3:
+            eng.capture()
+        eng.iteration()
+        torch.cuda.synchronize()
+        assert torch.equal(eng.actor_flat, L.flat), it
+        assert torch.equal(eng.actor_eps, L.eps), it
