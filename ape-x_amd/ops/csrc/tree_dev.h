@@ -367,24 +367,12 @@ __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const Batc
     sids[w.E + k] = id;
     w.list[w.E + k] = id;
   }
-  if (w.E == 0 && w.B <= 64) {  // block-uniform: the rows sit in wave 0 -- last write wins by readlane
-    bool win = ok;                // (no claim round trips through the global owner array)
-    if (k < 64) {
-      for (int v = 0; v < w.B; ++v)  // wave-uniform
-        if (v > k && __builtin_amdgcn_readlane(id, v) == id) win = false;
-    }
-    if (win) {
-      const float wp = write_leaf(t, id, p, w.alpha);
-      if (w.mix.delta != nullptr || w.prio != nullptr) pmax = fmaxf(pmax, wp);
-    }
-  } else {
-    if (ok) atomicMax(w.owner + id, k);  // device atomics: performed at L2
-    __syncthreads();
-    if (ok && __hip_atomic_load(w.owner + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
-      const float wp = write_leaf(t, id, p, w.alpha);
-      if (w.mix.delta != nullptr || w.prio != nullptr) pmax = fmaxf(pmax, wp);
-      w.owner[id] = -1;  // release the claim (only the winner writes; losers never touch it again)
-    }
+  if (ok) atomicMax(w.owner + id, k);  // device atomics: performed at L2
+  __syncthreads();
+  if (ok && __hip_atomic_load(w.owner + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k) {
+    const float wp = write_leaf(t, id, p, w.alpha);
+    if (w.mix.delta != nullptr || w.prio != nullptr) pmax = fmaxf(pmax, wp);
+    w.owner[id] = -1;  // release the claim (only the winner writes; losers never touch it again)
   }
   pmax = block_reduce_1024(pmax, red, true);
   if (k == 0 && pmax > 0.f) atomic_max_pos_float(w.max_prio, pmax);
