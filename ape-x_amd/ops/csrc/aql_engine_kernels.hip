@@ -875,6 +875,38 @@ constexpr int kStepDrawBlocks = 8;  // phase C workgroups of the next step's dra
 // proposal hard copy online -> target.  Shared by aql_step_tail_k and aql_update_k.
 __device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g, uint64_t st) {
   const int t = threadIdx.x;
+  // this thread's element (and, for an online sigma, its mu partner): its parameter / moments /
+  // partner gradient loaded and its new noise drawn BEFORE the grad-norm reduction (which
+  // barriers), so their latency and the Philox work overlap the partials' round trip
+  const int64_t i = (int64_t)bid * 256 + t;
+  const bool live = bid < D.nblk && i < D.n;
+  int kind = 0, l = 0;
+  int64_t e = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // online noisy tensors: mu elements are updated by their sigma partner's thread
+    const int64_t nw = (int64_t)D.P.layer[k].out * D.P.layer[k].in, nb = D.P.layer[k].out;
+    if ((i >= D.mu_w[k] && i < D.mu_w[k] + nw) || (i >= D.mu_b[k] && i < D.mu_b[k] + nb)) kind = 1;
+    if (i >= D.sig_w[k] && i < D.sig_w[k] + nw) { kind = 2; l = k; e = i - D.sig_w[k]; }
+    if (i >= D.sig_b[k] && i < D.sig_b[k] + nb) { kind = 3; l = k; e = i - D.sig_b[k]; }
+  }
+  const bool upd = live && kind != 1;
+  const int64_t ic = upd ? i : 0;
+  float a = D.m[ic], b = D.v[ic], pv = D.p[ic];
+  const int64_t im = kind >= 2 ? (kind == 2 ? D.mu_w[l] : D.mu_b[l]) + e : 0;
+  float a2 = 0.f, b2 = 0.f, pm = 0.f, gm = 0.f, ep = 0.f;
+  if (upd && kind >= 2) {
+    a2 = D.m[im];
+    b2 = D.v[im];
+    pm = D.p[im];
+    gm = D.G.grad[im];
+    if (kind == 2) {
+      const AqlNoise& z = D.P.layer[l];
+      const int o = (int)(e / z.in), c = (int)(e - (int64_t)o * z.in);
+      ep = noise_w(D.P.seed, l, o, c, st);
+    } else {
+      ep = scaled_noise(D.P.seed, l, 2, (int)e, st);
+    }
+  }
   float lr;
   const AdamRule rule = make_rule(D.hp, (int64_t)st, lr);
   const NormInfo nq = reduce_norms(D.G.part, D.nblk, D.hp.max_norm, D.hp.grad_scale);
@@ -889,49 +921,29 @@ __device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g,
     D.norms_p[2] = fminf(mn > 0.f ? mn / (np.l2 + 1e-6f) : 1.f, 1.f);
     D.norms_p[3] = lr;
   }
-  const int64_t i = (int64_t)bid * 256 + t;
-  if (bid < D.nblk && i < D.n) {
-    // online noisy tensors: mu elements are updated by their sigma partner's thread
-    int kind = 0, l = 0;
-    int64_t e = 0;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int64_t nw = (int64_t)D.P.layer[k].out * D.P.layer[k].in, nb = D.P.layer[k].out;
-      if ((i >= D.mu_w[k] && i < D.mu_w[k] + nw) || (i >= D.mu_b[k] && i < D.mu_b[k] + nb)) kind = 1;
-      if (i >= D.sig_w[k] && i < D.sig_w[k] + nw) { kind = 2; l = k; e = i - D.sig_w[k]; }
-      if (i >= D.sig_b[k] && i < D.sig_b[k] + nb) { kind = 3; l = k; e = i - D.sig_b[k]; }
-    }
-    if (kind != 1) {
-      const bool prop = i >= D.P_q;
-      float a = D.m[i], b = D.v[i];
-      const float pn = rule(D.p[i], opaque(g * (prop ? np.clip : nq.clip)), a, b);
-      D.m[i] = a;
-      D.v[i] = b;
-      D.p[i] = pn;
-      if (D.pub_p) D.pub_p[i] = pn;
-      if (prop) D.P.dst[i - D.P_q] = pn;
-      if (kind >= 2) {
-        const AqlNoise& z = D.P.layer[l];
-        const int64_t im = (kind == 2 ? D.mu_w[l] : D.mu_b[l]) + e;
-        float a2 = D.m[im], b2 = D.v[im];
-        const float mun = rule(D.p[im], opaque(D.G.grad[im] * nq.clip), a2, b2);
-        D.m[im] = a2;
-        D.v[im] = b2;
-        D.p[im] = mun;
-        if (D.pub_p) D.pub_p[im] = mun;
-        if (kind == 2) {
-          const int o = (int)(e / z.in), c = (int)(e - (int64_t)o * z.in);
-          const float ep = noise_w(D.P.seed, l, o, c, st);
-          z.weps[e] = ep;
-          if (D.pub_weps[l]) D.pub_weps[l][e] = ep;
-          z.weff[e] = fmaf(pn, ep, mun);
-        } else {
-          const float ep = scaled_noise(D.P.seed, l, 2, (int)e, st);
-          z.beps[e] = ep;
-          if (D.pub_beps[l]) D.pub_beps[l][e] = ep;
-          z.beff[e] = fmaf(pn, ep, mun);
-        }
-      }
+  if (!upd) return;
+  const bool prop = i >= D.P_q;
+  const float pn = rule(pv, opaque(g * (prop ? np.clip : nq.clip)), a, b);
+  D.m[i] = a;
+  D.v[i] = b;
+  D.p[i] = pn;
+  if (D.pub_p) D.pub_p[i] = pn;
+  if (prop) D.P.dst[i - D.P_q] = pn;
+  if (kind >= 2) {
+    const AqlNoise& z = D.P.layer[l];
+    const float mun = rule(pm, opaque(gm * nq.clip), a2, b2);
+    D.m[im] = a2;
+    D.v[im] = b2;
+    D.p[im] = mun;
+    if (D.pub_p) D.pub_p[im] = mun;
+    if (kind == 2) {
+      z.weps[e] = ep;
+      if (D.pub_weps[l]) D.pub_weps[l][e] = ep;
+      z.weff[e] = fmaf(pn, ep, mun);
+    } else {
+      z.beps[e] = ep;
+      if (D.pub_beps[l]) D.pub_beps[l][e] = ep;
+      z.beff[e] = fmaf(pn, ep, mun);
     }
   }
 }
