@@ -103,6 +103,8 @@ def parse():
                     help="AQL: the next step's draw in the gradient launch (1) or the update launch (0)")
     ap.add_argument("--aql-levels-in-bwd", type=int, default=None,
                     help="AQL: tree levels walked by the backward's workgroup before the gradient launch's")
+    ap.add_argument("--aql-fwd-halves", type=int, default=None,
+                    help="AQL: learner forward workgroups of 512 threads (2) or 256 (1)")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=560.0,
@@ -399,6 +401,8 @@ def aql(args, rank, world, device):
         cfg.draw_in_grad = bool(args.aql_draw_in_grad)
     if args.aql_levels_in_bwd is not None:
         cfg.tree_levels_in_bwd = int(args.aql_levels_in_bwd)
+    if args.aql_fwd_halves is not None:
+        cfg.fwd_halves = int(args.aql_fwd_halves)
     eng = AQLEngine(cfg, device)
     t_fill = time.perf_counter()
     eng.fill(max(1024, 4 * args.envs))
