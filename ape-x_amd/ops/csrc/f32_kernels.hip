@@ -159,7 +159,45 @@ __device__ __forceinline__ int xcd_chunk(int b, int G) {
   return b >= G8 ? b : (b & 7) * (G8 >> 3) + (b >> 3);
 }
 
-template <class P>
+// bf16 helpers of the exact-split conv1 kernels below (every fp32 term split by truncation)
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
+  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
+}
+__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
+
+// Exact three-term split of 8 fp32 values (two 4-element k-runs of a fragment) into bf16
+// hi / mid / lo vectors, x = hi + mid + lo EXACTLY (truncation: 8 + 8 + 8 significant bits).
+// The products of every pair of terms are exact in fp32; the six kept pairs (hi.hi, hi.mid,
+// mid.hi, hi.lo, mid.mid, lo.hi) leave out terms below 2^-23 |a||b| -- the size of the fp32
+// rounding of the product itself -- so the GEMM is fp32-class on the bf16 matrix cores
+// (1024 FLOP/clk/SIMD vs 64 for v_mfma_f32_32x32x2_f32: six of them still run 2.7x faster).
+struct Split8 {
+  bfx8 h, m, l;
+};
+__device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
+  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = x[2 * j], b = x[2 * j + 1];
+    const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
+    const float am = trunc_bf16(ar), bm = trunc_bf16(br);
+    h[j] = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
+    m[j] = pack_bf16_hi(am, bm);
+    l[j] = pack_bf16_hi(ar - am, br - bm);  // exact: <= 8 significant bits
+  }
+  return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
+          __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
+          __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
+}
+
+// fp32 GEMM arithmetic of gemm_body: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 fma chain),
+// 1 = the exact-split bf16 form (split8, six v_mfma_f32_32x32x16_bf16 per 16 k)
+int g_f32_x6 = 1;
+
+template <class P, bool X6>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
@@ -237,9 +275,68 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
   };
   using S0 = std::integral_constant<int, 0>;
+  // X6: the cross terms accumulate apart from hi.hi (summed in the epilogue)
+  f32x16 accx[X6 ? G::TM : 1][X6 ? G::TN : 1];
+  if constexpr (X6) {
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) accx[i][j][e] = 0.f;
+  }
+  auto frag_a = [&](const float* As, int mi, int kc) {
+    const int m = wm * G::WTM + mi * 32 + r;
+    f32x4 v;
+    if constexpr (P::A_KMAJ) {
+      v = *reinterpret_cast<const f32x4*>(As + m * G::PA + kc * 8 + 4 * h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = As[(kc * 8 + 4 * h + i) * G::PA + m];
+    }
+    return v;
+  };
+  auto frag_b = [&](const float* Bs, int ni, int kc) {
+    const int n = wn * G::WTN + ni * 32 + r;
+    f32x4 v;
+    if constexpr (P::B_KMAJ) {
+      v = *reinterpret_cast<const f32x4*>(Bs + n * G::PB + kc * 8 + 4 * h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = Bs[(kc * 8 + 4 * h + i) * G::PB + n];
+    }
+    return v;
+  };
   auto compute = [&](int buf) {
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
+    if constexpr (X6) {
+      static_assert(G::BK % 16 == 0, "X6: k-blocks of 16");
+      // 16 k per step: lane (r, h) holds k = 4h..4h+3 of chunk kc and of chunk kc + 1 -> bf16
+      // k-slots 8h..8h+7 of the 32x32x16 MFMA (the same slot map for A and B)
+#pragma unroll
+      for (int kc = 0; kc < G::BK / 8; kc += 2) {
+        Split8 a[G::TM], b[G::TN];
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi) a[mi] = split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
+#pragma unroll
+        for (int ni = 0; ni < G::TN; ++ni) b[ni] = split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < G::TN; ++ni) {
+            f32x16 x = accx[mi][ni];
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].l, b[ni].h, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].m, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].l, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].h, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].m, x, 0, 0, 0);
+            accx[mi][ni] = x;
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].h, acc[mi][ni], 0, 0, 0);
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int kc = 0; kc < G::BK / 8; ++kc) {
       f32x4 a[G::TM], b[G::TN];
@@ -292,6 +389,12 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     __syncthreads();
     cur ^= 1;
   }
+  if constexpr (X6) {
+#pragma unroll
+    for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < G::TN; ++ni) acc[mi][ni] += accx[mi][ni];
+  }
 
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi)
@@ -318,19 +421,12 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   }
 }
 
-// bf16 helpers of the exact-split conv1 kernels below (every fp32 term split by truncation)
-typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two exact bf16 halves
-  return __builtin_amdgcn_perm(__float_as_uint(hi), __float_as_uint(lo), 0x07060302u);
-}
-__device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
-
-template <class P>
+template <class P, bool X6>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
-  gemm_body<P>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
+  gemm_body<P, X6>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
 
 template <int A, int B>
@@ -340,7 +436,7 @@ struct MaxI {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2>
+template <class P1, class P2, bool X6>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
   __shared__ union {
@@ -348,9 +444,9 @@ __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1, X6>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2, X6>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -1256,14 +1352,16 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  gemm_k<P><<<blocks, 256, 0, s>>>(a);
+  if (g_f32_x6) gemm_k<P, true><<<blocks, 256, 0, s>>>(a);
+  else gemm_k<P, false><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  if (g_f32_x6) gemm2_k<P1, P2, true><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else gemm2_k<P1, P2, false><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
 
@@ -1311,6 +1409,8 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
   }
 }
+
+void f32_set_x6(int on) { g_f32_x6 = on; }
 
 int f32_fc1_splits() { return kFcSplits; }
 

@@ -25,7 +25,10 @@ update per step) and ``learner_samples_per_sec`` are reported separately; ``--sc
 strong`` keeps the reference's single-learner global batch of 512 (512/N per rank), so
 ``value`` equals the update rate.  Actor frames/s (4 emulator frames per env step) is
 reported alongside.  ``--dtype fp32`` (default) is the reference's precision
-(origin_repo/learner.py:139-145: fp32 modules, no autocast) on fp32 MFMA kernels;
+(origin_repo/learner.py:139-145: fp32 modules, no autocast): fp32 operands and activations,
+the GEMMs on the bf16 matrix cores through an exact three-term split of every fp32 operand
+(six products per 16 k, dropped terms below 2^-23 |a b|; per-layer error vs fp64 within the
+fp32 dot-product bound, tests/test_gpu_f32_net.py::test_gemm_layers_are_fp32_class);
 ``--dtype bf16`` is the opt-in bf16-operand mode.  Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1
 under torch.distributed.run, one process per GPU).
 """
@@ -348,7 +351,7 @@ def main():
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
                 "batch_pipeline": "sampled at the step start, 3-pass forward",
                 "forward": args.forward,
-                "fp32_forward_gemms": "fp32 MFMA" if args.dtype == "fp32" else None,
+                "fp32_gemms": "exact 3-term bf16 split (x6) on MFMA, fp32 accumulate" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
                 "actor_learner_overlap": args.overlap,
                 "dp_graph": eng._g_dp is not None,

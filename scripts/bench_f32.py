@@ -23,6 +23,7 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--x6", type=int, default=1, help="1: exact-split bf16 MFMA GEMMs, 0: f32 MFMA")
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 128x64 BK 16, "
                                                    "conv2/conv3 input gradient BK 32")
@@ -32,6 +33,7 @@ ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward 
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
+hip.f32_set_x6(a.x6)
 B, A = a.B, 18
 m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
 m.flatten_parameters()

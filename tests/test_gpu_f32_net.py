@@ -230,3 +230,73 @@ def test_f32_packed_arena_stays_exact_under_training(cuda):
         net.repack()
         assert torch.equal(fwd, net.arena[:net.fwd_numel])
     assert int(L.step_counter.item()) == 2 + 3 + 4
+
+
+@pytest.mark.parametrize("x6", [1, 0])
+def test_gemm_layers_are_fp32_class(cuda, x6):
+    """Every gemm_body layer (conv2 / conv3 / FC1 forward; FC1, conv3, conv2 input and weight
+    gradients) against fp64 on the SAME layer inputs, per element scaled by the fp32
+    dot-product error scale sum_k |a_k b_k|.  ``x6`` = 1: the exact three-term bf16 split on
+    v_mfma_f32_32x32x16_bf16 (six products per 16 k, every dropped term below 2^-23 |a b|),
+    0: v_mfma_f32_32x32x2_f32.  Both must stay within a few fp32 ulps of that scale."""
+    from apex_amd import ops
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    h = ops.hip()
+    h.f32_set_x6(x6)
+    try:
+        B, A = 96, 18
+        m = _model(cuda, A=A, seed=7)
+        for p in m.parameters():
+            p.grad = torch.zeros_like(p)
+        net = F32DuelingNet(m)
+        x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+        ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+        net(x, ws)
+        dq = torch.randn(B, A, device=cuda) / B
+        net.backward(dq, x, ws)
+        torch.cuda.synchronize()
+    finally:
+        h.f32_set_x6(1)
+    f = m.features
+    d = lambda t: t.detach().double()  # noqa: E731
+    errs = {}
+
+    def scaled(name, got, ref, scale):
+        errs[name] = float(((got.double() - ref).abs() / scale.clamp_min(1e-30)).max())
+
+    g1, g2, g3 = _nchw(ws.a1, B, 32, 20), _nchw(ws.a2, B, 64, 9), _nchw(ws.a3, B, 64, 7)
+    for name, xin, L, out in (("conv2", g1, 2, g2), ("conv3", g2, 4, g3)):
+        st = 2 if L == 2 else 1
+        pre = F.conv2d(xin, d(f[L].weight), d(f[L].bias), stride=st)
+        sc = F.conv2d(xin.abs(), d(f[L].weight).abs(), d(f[L].bias).abs(), stride=st)
+        mask = pre > 1e-6 * sc  # ReLU-active outputs (the clamped ones are exact zeros)
+        scaled(name + "_fwd", out[mask], pre[mask], sc[mask])
+    hflat = g3.reshape(B, -1)
+    W = torch.cat([d(m.advantage[0].weight), d(m.value[0].weight)])
+    bb = torch.cat([d(m.advantage[0].bias), d(m.value[0].bias)])
+    pre = hflat @ W.t() + bb
+    sc = hflat.abs() @ W.abs().t() + bb.abs()
+    mask = pre > 1e-6 * sc
+    scaled("fc1_fwd", ws.h.double()[mask], pre[mask], sc[mask])
+    # backward: weight gradients from the kernels' own output gradients
+    dz = ws.dz.double()  # [B, 256] (post-ReLU-mask FC1 output gradient)
+    gW = torch.cat([m.advantage[0].weight.grad, m.value[0].weight.grad]).double()
+    scaled("fc1_wgrad", gW, dz.t() @ hflat, dz.abs().t() @ hflat.abs())
+    dy3 = _nchw(ws.dy3, B, 64, 7)
+    ref = (dz @ W).view(B, 64, 7, 7) * (g3 > 0)
+    sc = (dz.abs() @ W.abs()).view(B, 64, 7, 7)
+    mask = g3 > 0
+    scaled("fc1_dgrad", dy3[mask], ref[mask], sc[mask])
+    for name, xin, L, dy, st in (("conv3", g2, 4, dy3, 1), ("conv2", g1, 2, _nchw(ws.dy2, B, 64, 9), 2)):
+        ref = torch.nn.grad.conv2d_weight(xin, f[L].weight.shape, dy, stride=st)
+        sc = torch.nn.grad.conv2d_weight(xin.abs(), f[L].weight.shape, dy.abs(), stride=st)
+        scaled(name + "_wgrad", f[L].weight.grad, ref, sc)
+        dx = torch.nn.grad.conv2d_input(xin.shape, d(f[L].weight), dy, stride=st)
+        dxs = torch.nn.grad.conv2d_input(xin.shape, d(f[L].weight).abs(), dy.abs(), stride=st)
+        got = _nchw(ws.dy2 if L == 4 else ws.dy1, B, xin.shape[1], xin.shape[2])
+        mask = xin > 0
+        scaled(name + "_dgrad", got[mask], dx[mask], dxs[mask])
+    print(f"x6={x6}", {k: f"{v:.2e}" for k, v in errs.items()})
+    # fp32 unit roundoff 6e-8: K <= 3136 accumulations stay within a few ulps of sum |a b|
+    assert max(errs.values()) < 1e-6, errs
