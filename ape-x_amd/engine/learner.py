@@ -319,10 +319,14 @@ class DQNLearner:
             for fn in hooks:
                 fn()
             pre, self.pre_writes = self.pre_writes, []
-            for slots, prios, filled in pre:
+            for slots, prios, filled in pre[:-1]:  # (more than one staged actor step per learner step)
                 self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
-            self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
-                                         mix=(self.delta, self.lw, self.prio, self.loss))
+            # the last actor step's rows + this step's mixed priorities (last write wins) in one
+            # batched write: a one-workgroup leaves launch, then one wide launch per big tree level
+            # (the last one finishing the small top levels) -- the single-workgroup level walks
+            # took ~130 us beside the backward
+            self.replay.write_batch(pre=pre[-1] if pre else None, idx=self.idx, bump=self.step_counter,
+                                    mix=(self.delta, self.lw, self.prio, self.loss))
             tail, self.tree_tail = self.tree_tail, []
             for fn in tail:
                 fn()

@@ -74,7 +74,13 @@ def check_ipc(hip, store, rank: int, world: int, device: int, prefix: str, timeo
     """IPC round trip (see the module docstring).  Collective over the store."""
     key = lambda s: f"{prefix}/preflight/{s}"  # noqa: E731
     if rank == 0:
-        arena = hip.ipc_alloc(world * BLOCK, mode)
+        try:
+            arena = hip.ipc_alloc(world * BLOCK, mode)
+        except Exception as e:  # every rank learns it through the verdict (an empty handle: skip)
+            msg = f"rank 0 on GPU {device}: IPC export failed: {type(e).__name__}: {e}"[:400]
+            store.set(key("handle"), b"")
+            store.set(key("verdict"), json.dumps({"0": msg}))
+            raise PreflightError(f"preflight: IPC round trip failed: {msg}") from e
         try:
             store.set(key("handle"), hip.ipc_handle(arena))
             _wait(store, [key(f"wrote/{r}") for r in range(1, world)], timeout, "IPC peer writes")
@@ -104,7 +110,10 @@ def check_ipc(hip, store, rank: int, world: int, device: int, prefix: str, timeo
     status = "ok"
     remote = 0
     try:
-        remote = hip.ipc_open(store.get(key("handle")), device)
+        handle = store.get(key("handle"))
+        if not handle:
+            raise PreflightError("rank 0 exported no IPC handle")
+        remote = hip.ipc_open(handle, device)
         buf, host = _host_buf(pattern(rank))
         hip.memcpy_sync(remote + rank * BLOCK, host, BLOCK)
     except Exception as e:
@@ -123,6 +132,43 @@ def check_ipc(hip, store, rank: int, world: int, device: int, prefix: str, timeo
         raise PreflightError(f"preflight: IPC round trip failed"
                              + (f" for this rank: {mine}" if mine else f" on rank(s) {sorted(map(int, verdict))}"))
     return {"ipc": "ok"}
+
+
+def ipc_or_fallback(hip, store, rank: int, world: int, device: int, peer_device: int, prefix: str,
+                    timeout: float, mode: int = MODE_UNCACHED) -> dict:
+    """Peer access + IPC round trip, deciding the experience transport instead of failing
+    the job: every actor rank reports its peer-access verdict through the store; rank 0
+    decides.  A refused peer mapping or a failed round trip selects the ``p2p`` transport
+    (torch.distributed send/recv links, parallel/experience.py -- the reference's links
+    work over any path too, origin_repo/actor.py:28-37); every rank returns the SAME
+    decision.  A rank that never answers still raises (timeouts are not a transport
+    problem)."""
+    key = lambda s: f"{prefix}/transport/{s}"  # noqa: E731
+    rep = {}
+    if rank != 0:
+        try:
+            rep.update(check_peer_access(hip, rank, device, peer_device))
+            st = "ok"
+        except PreflightError as e:
+            st = str(e)[:400]
+        store.set(key(f"peer/{rank}"), st)
+    else:
+        _wait(store, [key(f"peer/{r}") for r in range(1, world)], timeout, "peer-access reports")
+        bad = {r: store.get(key(f"peer/{r}")).decode(errors="replace") for r in range(1, world)}
+        bad = {r: v for r, v in bad.items() if v != "ok"}
+        store.set(key("decision"), json.dumps(
+            {"transport": "p2p", "reason": "; ".join(bad[r] for r in sorted(bad))} if bad else {"transport": "ipc"}))
+    _wait(store, [key("decision")], timeout, "rank 0's transport decision")
+    d = json.loads(store.get(key("decision")))
+    if d["transport"] == "p2p":
+        return {**rep, "ipc": "skipped", "transport": "p2p", "transport_fallback": d["reason"]}
+    try:
+        rep.update(check_ipc(hip, store, rank, world, device, prefix, timeout, mode))
+    except PreflightError as e:
+        if "timed out" in str(e):
+            raise
+        return {**rep, "ipc": "failed", "transport": "p2p", "transport_fallback": str(e)[:600]}
+    return {**rep, "transport": "ipc", "transport_fallback": None}
 
 
 def check_collective(rank: int, world: int, allreduce, comm_count=None) -> dict:
@@ -192,10 +238,13 @@ def _gloo_allreduce(vec):
     return t.tolist()
 
 
-def run(device, *, ipc: bool = True, timeout: float = 60.0, hip=None, log=None) -> dict:
+def run(device, *, ipc: bool = True, timeout: float = 60.0, hip=None, log=None, fallback: bool = False) -> dict:
     """Run the preflight on this rank of the initialised default process group (every
     rank must call it).  ``ipc``: also check the IPC round trip (the central topology's
-    data plane).  Returns this rank's report; raises :class:`PreflightError`."""
+    data plane); with ``fallback`` a failed peer-access or IPC step selects the p2p
+    transport instead of raising (``rep["transport"]``, ``rep["transport_fallback"]``).
+    Returns this rank's report; raises :class:`PreflightError` (the collective check
+    always does)."""
     import torch
     import torch.distributed as dist
 
@@ -219,10 +268,13 @@ def run(device, *, ipc: bool = True, timeout: float = 60.0, hip=None, log=None) 
 
         hip = ops.hip()
     rep = {"rank": rank, "world": world, "device": idx}
-    if rank != 0:
-        rep.update(check_peer_access(hip, rank, idx, dev0))
-    if ipc:
-        rep.update(check_ipc(hip, store, rank, world, idx, prefix, timeout))
+    if ipc and fallback:
+        rep.update(ipc_or_fallback(hip, store, rank, world, idx, dev0, prefix, timeout))
+    else:
+        if rank != 0:
+            rep.update(check_peer_access(hip, rank, idx, dev0))
+        if ipc:
+            rep.update(check_ipc(hip, store, rank, world, idx, prefix, timeout))
     if dist.get_backend() == "nccl":
         ar, count, close = _rccl_allreduce(hip, store, prefix, rank, world, dev, timeout)
         try:

@@ -5,11 +5,15 @@ the reference's replay.py + learner.py + N x actor.py deployment 
 one rank per GPU, launched directly (1 GPU) or under ``torch.distributed.run`` (any
 number of GPUs and nodes; RCCL over xGMI inside a node):
 
-* ``--topology sharded`` (default for N > 1): every rank runs an actor shard, its HBM
-  replay shard and a data-parallel learner replica; gradients are all-reduced and the
-  shards are sampled as one global prioritized buffer (``apex_amd.parallel.sharded``).
-* ``--topology central``: rank 0 is the learner with the one replay; ranks 1.. are
-  actor GPUs pushing experience over RCCL (``apex_amd.engine.central``).
+* ``--topology central`` (default for N > 1, ``config.py``): rank 0 is THE learner with the
+  one replay (the reference's single learner, origin_repo/learner.py:134-175); ranks 1..
+  are actor GPUs pushing experience into rank 0's HBM over HIP IPC rings (xGMI peer
+  copies, ``apex_amd.parallel.ipc``).  A multi-GPU preflight runs first: if peer access
+  or the IPC round trip fails, the experience links fall back to torch.distributed
+  send/recv (RCCL, ``apex_amd.parallel.experience``) instead of failing the job.
+* ``--topology sharded``: every rank runs an actor shard, its HBM replay shard and a
+  data-parallel learner replica; gradients are all-reduced over RCCL and the shards are
+  sampled as one global prioritized buffer (``apex_amd.parallel.sharded``).
 
 Reference cadences and tags are kept: target sync every ``--target_update_interval``
 (learner.py:163-165), weights published every ``--publish_param_interval``
@@ -127,6 +131,15 @@ def main(argv=None) -> int:
         kw = {"device_id": device} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     topology = cfg.replay.topology if world > 1 else "single"
+    transport = "auto"
+    if topology == "central":  # prove the cross-device paths; IPC -> p2p fallback (parallel/preflight.py)
+        from .parallel import preflight
+
+        rep = preflight.run(device, ipc=True, timeout=90.0, fallback=True)
+        transport = rep["transport"]
+        if rep.get("transport_fallback") and rank == 0:
+            print(f"preflight: IPC experience links unavailable ({rep['transport_fallback']}); using p2p links",
+                  file=sys.stderr)
 
     from .engine.apex import ApexEngine, EngineConfig
     from .engine.learner import LearnerConfig
@@ -148,7 +161,7 @@ def main(argv=None) -> int:
     if topology == "central":
         from .engine.central import CentralApexEngine
 
-        eng = CentralApexEngine(ecfg, device, rank, world)
+        eng = CentralApexEngine(ecfg, device, rank, world, transport=transport)
         learner = eng.learner if rank == 0 else None
         if args.resume and rank == 0:
             counters = load_engine(learner, args.resume)

@@ -186,9 +186,19 @@ def run_preflight(args, topo: str, device, wd: "Watchdog") -> dict | None:
     from apex_amd.parallel import preflight
 
     ipc = topo == "central" and args.transport in ("auto", "ipc")
-    rep = preflight.run(device, ipc=ipc, timeout=90.0)
+    rep = preflight.run(device, ipc=ipc, timeout=90.0, fallback=args.transport == "auto")
     wd.kick()
     return rep
+
+
+def resolve_transport(requested: str, pre: dict | None) -> tuple[str, str | None]:
+    """The central topology's experience transport after the preflight: ``auto`` takes the
+    preflight's decision -- HIP IPC, or the torch.distributed p2p links (RCCL send/recv)
+    with the reason when peer access or the IPC round trip failed.  An explicit choice
+    stands (``ipc`` then fails in the preflight, by request)."""
+    if requested != "auto" or not pre or "transport" not in pre:
+        return requested, None
+    return pre["transport"], pre.get("transport_fallback")
 
 
 def main():
@@ -231,7 +241,13 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
     wd.kick()
     pre = run_preflight(args, topo, device, wd) if world > 1 else None
+    args.transport, args.transport_fallback = resolve_transport(args.transport, pre)
+    if args.transport_fallback and rank == 0:
+        print(f"preflight: IPC experience links unavailable ({args.transport_fallback}); "
+              f"using the {args.transport} transport", file=sys.stderr)
     if args.algo == "aql":
+        if topo == "central" and args.transport == "p2p":
+            raise SystemExit(f"AQL central topology needs the HIP IPC links: {args.transport_fallback}")
         if topo == "central":
             return aql_central(args, rank, world, device, wd, pre)
         return aql(args, rank, world, device)
@@ -610,6 +626,7 @@ def central(args, rank, world, device, wd, pre=None):
         "packets_applied_per_learner_step": round(packets / args.steps, 3),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
         "links_complete": all(links["applied"][r] == links.get("sent", {}).get(r, links["applied"][r]) for r in links["live"]),
+        "transport": eng.transport, "transport_fallback": args.transport_fallback,
         "preflight": pre,
         "timing": "rank 0 (the one learner) between two device syncs; actor ranks act continuously",
         "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
