@@ -22,12 +22,17 @@ parameter publish, for actor GPUs on the same node (xGMI):
   credit window, actor.py:105-115: at most ``D`` packets in flight), the published
   parameter version, per-link heartbeat counters, drop flags, the stop flag and stop
   acknowledgements.  The actors read and write it with plain CPU loads / stores.
-* **Parameters** (conflated, learner.py:57-68 PUB/SUB CONFLATE=1): rank 0 copies its master
-  weights into ``params[v & 1]`` on its stream, then stores ``v`` into the control block
-  (release), having announced ``v`` in a *begin* word before the copy (seqlock writer).  An
-  actor that sees a newer version pulls that half with one peer copy and then re-reads the
-  begin word: if version ``v + 2`` was announced meanwhile the half may have been
-  rewritten, and the pull is retried.  Slow actors simply skip versions.
+* **Parameters** (conflated, learner.py:57-68 PUB/SUB CONFLATE=1): ``K = R + 2`` parameter
+  buffers; version ``v`` lives in buffer ``v % K``.  A reader *pins* the version it is about
+  to pull (its pin word in the control block), pulls buffer ``v % K`` with one peer copy,
+  then checks that buffer's *begin* word -- stored by rank 0's stream just before it starts
+  writing a buffer -- still reads ``v`` (nobody began rewriting it during the pull).  The
+  writer never targets a pinned buffer or the newest one: it skips version numbers until
+  ``v % K`` is free (at most R buffers are pinned, so one always is).  Once its pin is
+  visible a reader's buffer cannot be rewritten, however slow its copy: publishing every
+  learner iteration never starves a reader (a pull fails only if ``K`` versions are
+  enqueued between reading the version word and storing the pin -- microseconds -- and is
+  then retried).  Readers simply skip versions.
 * **Liveness** (SURVEY §5.3): actors bump a heartbeat word on a wall-clock period (also
   while waiting for credit); rank 0 drops a link whose word stopped moving for
   ``dead_after`` s: its ingest mask goes to 0 and its drop flag tells a live-but-stuck actor
@@ -69,15 +74,56 @@ def packet_bytes(E: int) -> int:
     return E * (FRAME_BYTES + META_COLS * 4)
 
 
-class ControlBlock:
-    """int64 words in /dev/shm: header | consumed[R] | heartbeat[R] | drop[R] | sent[R] | ack[R]."""
+def param_buffers(R: int) -> int:
+    """Parameter buffers of the pinned publish protocol: one per reader that may hold a pin,
+    plus the newest version, plus one the writer can always take."""
+    return int(R) + 2
 
-    FIELDS = ("consumed", "heartbeat", "drop", "sent", "ack")
+
+def pick_version(last: int, pins, K: int) -> int:
+    """Writer side of the pinned protocol: the next version number ``> last`` whose buffer
+    ``v % K`` is neither pinned by a reader nor the newest version's (``last % K``)."""
+    busy = {int(p) % K for p in pins if int(p) > 0} | {last % K}
+    v = last + 1
+    while v % K in busy:
+        v += 1
+    return v
+
+
+def pinned_pull(ctrl: "ControlBlock", i: int, have: int, pull, retries: int = 8) -> tuple[int | None, int]:
+    """Reader side of the pinned protocol for reader ``i``: pin the newest published version,
+    ``pull(buffer)`` it (synchronously), keep it if the buffer's begin word still reads that
+    version.  Returns (installed version or None, failed pulls)."""
+    v = ctrl.param_version
+    if v <= have:
+        return None, 0
+    pin = ctrl.view("pin")
+    failed = 0
+    try:
+        for _ in range(retries):
+            pin[i] = v  # from here on the writer leaves buffer v % K alone
+            b = v % ctrl.K
+            pull(b)
+            if int(ctrl.w[ctrl.begin_off(b)]) == v:  # nobody began rewriting it during the pull: clean
+                return v, failed
+            failed += 1
+            v = ctrl.param_version
+        return None, failed
+    finally:
+        pin[i] = 0
+
+
+class ControlBlock:
+    """int64 words in /dev/shm: header | consumed[R] | heartbeat[R] | drop[R] | sent[R] | ack[R]
+    | pin[R] | begin[K] (K = param_buffers(R): the version each parameter buffer last began)."""
+
+    FIELDS = ("consumed", "heartbeat", "drop", "sent", "ack", "pin")
 
     def __init__(self, name: str, R: int, create: bool):
         self.name, self.R = name, int(R)
+        self.K = param_buffers(self.R)
         self.path = f"/dev/shm/{name}"
-        self.nbytes = _align(8 * (_HDR + len(self.FIELDS) * self.R), 4096)
+        self.nbytes = _align(8 * (_HDR + len(self.FIELDS) * self.R + self.K), 4096)
         if create:
             fd = os.open(self.path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
             os.ftruncate(fd, self.nbytes)
@@ -106,13 +152,13 @@ class ControlBlock:
         o = self.off(field)
         return self.w[o:o + self.R]
 
+    def begin_off(self, b: int) -> int:
+        """Word offset of parameter buffer ``b``'s begin word."""
+        return _HDR + len(self.FIELDS) * self.R + int(b)
+
     @property
     def param_version(self) -> int:
         return int(self.w[2])
-
-    @property
-    def param_begin(self) -> int:
-        return int(self.w[4])
 
     @property
     def stop(self) -> bool:
@@ -169,17 +215,10 @@ class IpcLearnerLinks:
 
     def __init__(self, R: int, D: int, E: int, P: int, store, prefix: str, device, *, packet_nbytes: int,
                  tables: dict, tree_write, cap: int | None = None, dead_after: float = 30.0,
-                 mode: int = MODE_UNCACHED, log=print, open_timeout: float = 300.0,
-                 min_publish_interval: float = 0.002):
+                 mode: int = MODE_UNCACHED, log=print, open_timeout: float = 300.0):
         self.hip = h = ops.hip()
-        # conflation floor between parameter publishes: a reader's copy of half v & 1 is clean
-        # unless the writer starts v + 2 before it lands; with the writer publishing every
-        # learner iteration (~0.2 ms for AQL) and the reader's copy queued behind the learner's
-        # kernels on a shared GPU, every seqlock retry could fail and an actor never install
-        # weights -- two publishes are now >= 2 x this apart
-        self.min_publish_interval = float(min_publish_interval)
-        self._pub_t = -1e30
         self.R, self.D, self.E, self.P = int(R), int(D), int(E), int(P)
+        self.K = param_buffers(self.R)
         self.cap = self.D if cap is None else max(1, min(int(cap), self.D))
         self.device = torch.device(device)
         self.store, self.prefix, self.log = store, prefix, log
@@ -189,7 +228,7 @@ class IpcLearnerLinks:
         self.pkt = _align(self.packet_nbytes)
         self.seq_off = _align(self.R * self.D * self.pkt)
         self.par_off = _align(self.seq_off + 8 * self.R * self.D)
-        self.nbytes = self.par_off + 2 * 4 * self.P
+        self.nbytes = self.par_off + self.K * 4 * self.P
         self.arena = h.ipc_alloc(self.nbytes, mode)
         self.ctrl = ControlBlock(f"apex_ipc_{prefix.replace('/', '_')}_{os.getpid()}", R, create=True)
         self.ctrl.register(h)
@@ -283,20 +322,17 @@ class IpcLearnerLinks:
         n = self.slots_out.numel() if drain else self._n_out
         self.tree_write(self.slots_out[:n], self.prio_out[:n])
 
-    def publish(self, flat: torch.Tensor, force: bool = False) -> bool:
-        """Conflated versioned publish (seqlock writer, all on the current stream): announce
-        ``v`` as being written, copy into params[v & 1], then release ``v`` as published.
-        Skipped (False) within ``min_publish_interval`` of the previous one unless ``force``."""
-        now = time.monotonic()
-        if not force and now - self._pub_t < self.min_publish_interval:
-            return False
-        self._pub_t = now
-        self.version += 1
-        v, s = self.version, self._s()
-        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 4, v, s)
-        self.hip.memcpy_async(self.arena + self.par_off + (v & 1) * 4 * self.P, flat.data_ptr(), 4 * self.P, s)
+    def publish(self, flat: torch.Tensor) -> int:
+        """Conflated versioned publish (pinned protocol, module docstring), all on the current
+        stream: pick a version whose buffer no reader has pinned, mark the buffer as begun,
+        copy, release the version.  Returns the version."""
+        v = pick_version(self.version, self.ctrl.view("pin"), self.K)
+        b, s = v % self.K, self._s()
+        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * self.ctrl.begin_off(b), v, s)
+        self.hip.memcpy_async(self.arena + self.par_off + b * 4 * self.P, flat.data_ptr(), 4 * self.P, s)
         self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 2, v, s)
-        return True
+        self.version = v
+        return v
 
     def drop(self, r: int, why: str) -> None:
         if r in self.live:
@@ -386,6 +422,7 @@ class IpcActorLink:
         store.wait([f"{prefix}/ipc/handle", f"{prefix}/ipc/geometry"], timedelta(seconds=timeout))
         geo = json.loads(store.get(f"{prefix}/ipc/geometry"))
         self.R, self.D, self.E, self.P = geo["R"], geo["D"], geo["E"], geo["P"]
+        self.K = param_buffers(self.R)
         self.pkt, self.seq_off, self.par_off = geo["pkt"], geo["seq_off"], geo["par_off"]
         want = geo.get("packet_nbytes", packet_bytes(self.E))
         if packet.numel() * packet.element_size() != want or not packet.is_contiguous():
@@ -402,6 +439,7 @@ class IpcActorLink:
         self._hb_t = 0.0
         self.sent = 0
         self.version = 0
+        self.pulls_retried = 0
         self.stopped = False
         self.dropped = False
         self._ev = torch.cuda.Event()
@@ -465,23 +503,21 @@ class IpcActorLink:
         return True
 
     def poll_params(self, retries: int = 8):
-        """None (nothing new), STOP, or the version just installed into ``flat``."""
+        """None (nothing new), STOP, or the version just installed into ``flat`` (the
+        pinned protocol's reader, module docstring)."""
         if self.check_stop():
             return STOP
-        v = self.ctrl.param_version
-        if v <= self.version:
-            return None
-        for _ in range(retries):
-            s = self._s()
-            self.hip.memcpy_async(self.flat.data_ptr(), self.remote + self.par_off + (v & 1) * 4 * self.P,
-                                  4 * self.P, s)
+        def pull(b: int) -> None:
+            self.hip.memcpy_async(self.flat.data_ptr(), self.remote + self.par_off + b * 4 * self.P, 4 * self.P,
+                                  self._s())
             self._ev.record(torch.cuda.current_stream(self.device))
             self._ev.synchronize()
-            if self.ctrl.param_begin < v + 2:  # rank 0 had not started rewriting half (v & 1): clean
-                self.version = v
-                return v
-            v = self.ctrl.param_version
-        return None
+
+        v, failed = pinned_pull(self.ctrl, self.i, self.version, pull, retries)
+        self.pulls_retried += failed
+        if v is not None:
+            self.version = v
+        return v
 
     def finish(self) -> None:
         if self.stopped:

@@ -105,3 +105,88 @@ def test_ipc_arena_peer_copy_and_shm_control(cuda):
             p.kill()
     assert out[0] is True, out[0]   # the peer's bytes landed before its sequence word
     assert out[1] is True, out[1]   # the owner's kernel store reached the other process's CPU
+
+
+def _params_body(rank, port, q, seconds, delay_cycles):
+    import time
+    import traceback
+    from datetime import timedelta
+
+    try:
+        import torch.distributed as dist
+
+        from apex_amd.engine.aql import AQLReplay
+        from apex_amd.parallel.experience import STOP
+        from apex_amd.parallel.ipc import IpcActorLink, IpcLearnerLinks, aql_packet_floats
+
+        torch.cuda.set_device(0)
+        store = dist.TCPStore("127.0.0.1", port, 2, rank == 0, timedelta(seconds=60))
+        E, P, obs, T, adim = 8, 1 << 20, 4, 3, 1
+        flat = torch.zeros(P, dtype=torch.float32, device="cuda")
+        if rank == 0:  # the writer: a new parameter version every "iteration", no clock floor
+            rp = AQLReplay(1024, obs, T, adim, device="cuda")
+            links = IpcLearnerLinks.for_aql(1, 3, E, P, rp, store, "pt", "cuda", log=None)
+            store.set("ready", "1")
+            n, t_end = 0, time.monotonic() + seconds
+            while time.monotonic() < t_end:
+                flat.fill_(float(n))
+                links.publish(flat)
+                torch.cuda._sleep(20000)  # ~10 us of "learner iteration"
+                n += 1
+                if n % 64 == 0:
+                    torch.cuda.synchronize()
+            st = links.close(timeout=60)
+            q.put((0, {"published": n, "version": st["params_version"]}))
+        else:  # the reader: every pull queued behind ~ms of other work on its stream
+            store.wait(["ready"], timedelta(seconds=60))
+            pkt = torch.zeros(aql_packet_floats(E, obs, T * adim), dtype=torch.float32, device="cuda")
+            link = IpcActorLink(1, store, "pt", flat, pkt, "cuda")
+            polls, installs, torn, last = 0, 0, 0, 0
+            while True:
+                torch.cuda._sleep(delay_cycles)  # queued work ahead of the parameter copy
+                v = link.poll_params()
+                polls += 1
+                if v == STOP:
+                    break
+                if v is None:
+                    continue
+                lo, hi = float(flat.min()), float(flat.max())
+                torn += int(lo != hi)
+                assert v > last
+                last, installs = v, installs + 1
+            q.put((1, {"polls": polls, "installs": installs, "torn": torn, "retried": link.pulls_retried}))
+    except Exception:
+        q.put((rank, "ERROR " + traceback.format_exc()))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_ipc_params_delayed_reader_installs_while_writer_publishes_every_iteration(cuda):
+    """with the pinned K-buffer protocol (parallel/ipc.py) a reader whose
+    copies sit behind ~2 ms of queued work still installs a clean (untorn) version on
+    practically every poll while rank 0 publishes a new version every ~10 us -- no publish
+    floor, no starvation."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_params_body, args=(r, port, q, 3.0, 4_000_000)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        r, res = q.get(timeout=150)
+        out[r] = res
+    for p in procs:
+        p.join(30)
+        if p.is_alive():
+            p.kill()
+    for r, res in out.items():
+        assert not (isinstance(res, str) and res.startswith("ERROR")), f"rank {r}: {res}"
+    w, rd = out[0], out[1]
+    print(w, rd)
+    assert w["published"] > 10 * rd["installs"]       # the writer ran far ahead of the reader
+    assert rd["torn"] == 0 and rd["installs"] >= 20
+    assert rd["retried"] <= 2 and rd["installs"] >= rd["polls"] - 3  # bounded polls per install
