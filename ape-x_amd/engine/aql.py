@@ -41,8 +41,6 @@ from __future__ import annotations
 
 import collections
 import math
-import os
-import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -175,62 +173,26 @@ class AQLEngineConfig:
     threshold: int | None = None       # transitions before learning (default batch_size + 1)
     exact_mass: bool = False           # False = reference sampling mass (Q5)
     use_graphs: bool = True
-    fork_tree: bool = False  # tree write on a forked stream: measured 9851 vs 11769 steps/s (two cross-queue
-                             # hand-offs per ~85 us step cost more than the 11 us they hide)
+    # The learner step's launch sequence.  True (default): four launches per SGD step --
+    #   aql_learn_fwd   (draws its own PER rows, or uses the rows the previous step drew)
+    #   aql_learn_bwd   (+ one workgroup: priority mix, loss mean, deduplicated leaves, tree level 1)
+    #   aql_grad        (+ one workgroup: tree levels 2..)
+    #   aql_update      (both clipped Adam steps, noise reset of both critics, proposal copy,
+    #                    step bump, the NEXT step's PER draw; the iteration's last step also
+    #                    writes the acting copies)
+    # MI355X, batch 32: 19.0k SGD steps/s (profiles/r4_aql_engine.md).  False: the reference
+    # sequence of separate launches (per_sample, forward, backward, per_write_batch, gradients,
+    # adam_step2, noise reset) -- the bit-identity baseline of tests/test_gpu_aql_engine.py.
+    # (Round 4 alternatives measured slower and removed: a forked tree stream, the whole step
+    # tail in one grid-barrier launch, the tree write in the noise-reset launch.)
+    fused: bool = True
     # acting on its own HIP stream beside the learner steps (staged transitions); MI355X, B 32:
     # 12978-13005 vs 13161 SGD steps/s serial -- the learner's chain of small kernels slows by
     # about what the hidden acting step saves, so serial stays the default
     overlap: bool = False
-    fused_sample: bool = True  # PER draw inside aql_learn_fwd
-    # priority write as an extra workgroup of the noise-reset launch: measured 12936-12958 vs 13117
-    # SGD steps/s (the one-workgroup tree write, ~15 us in a 256-thread block, then bounds that launch)
-    fused_tree: bool = False
-    # priority write split over the two launches that follow the backward: the leaves (claims,
-    # mix, loss mean, dirty list) as an extra workgroup of the gradient contraction, the level
-    # walk as an extra workgroup of the noise reset -- no launch of its own on the chain
-    # (MI355X, batch 32: 14758-14771 vs 13882-13899 SGD steps/s with the write as its own launch,
-    # one box, interleaved; scripts/ab/aql_split_tree.sh)
-    split_tree: bool = True
-    # priority write as an extra workgroup of the BACKWARD launch (it recomputes the B TD terms
-    # from the forward's Q rows): the leaves and the level walk run beside the per-sample
-    # backward instead of bounding the gradient / noise-reset launches (replaces split_tree).
-    # Alone it measured even with split_tree (14825-14850 vs 14751-14754 SGD steps/s); it is what
-    # lets fused_update draw the next step's rows
-    bwd_tree: bool = False
     # learner forward: candidate-tile groups per (sample, net) workgroup (0 = about one workgroup
     # per CU: the ~110 KB weight staging, the PER draw and the state MLP serve a group of tiles)
     fwd_tile_groups: int = 0
-    fwd_halves: int = 0  # learner forward workgroup: 0 = default (2: 512 threads), 1 = 256 threads
-    # acting-Q workgroups (each loops over its (state, 16-candidate) items); 0 = one per item,
-    # or 64 with ``overlap`` (so the acting launch leaves most CUs to the learner beside it)
-    act_blocks: int = 0
-    act_q: str = "mfma"  # acting Q: "mfma" = the learner's fp32-MFMA candidate forward (aql_act_q),
-                             # "scalar" = one wave per candidate item (aql_candidate_q)
-    # everything after the forward in ONE launch (aql_step_tail_k: backward + priority write +
-    # target noise | gradients | Adam x2 + online noise + proposal copy, grid barriers between
-    # the phases; batch <= 64, not with fork_tree).  Measured SLOWER on MI355X: 82.1 vs 54.7 us
-    # per learner step (bit-identical results) -- each grid barrier (~9 us: agent-scope fences
-    # write back / invalidate the XCD L2s) costs more than the ~1.5 us kernel boundary it replaces
-    fused_step: bool = False
-    # the step's update as ONE launch after the gradient contraction (aql_update_k: both clipped
-    # Adam steps, noise reset of both critics, proposal copy, step bump and the NEXT step's PER
-    # draw, so that forward skips its descent), with the priority write in the backward launch
-    # (implies bwd_tree): four launches per step, no grid barrier.  MI355X, batch 32, interleaved:
-    # 15577-15580 vs 14751-14754 SGD steps/s for the split write + separate launches
-    # (scripts/ab/aql_bwd_tree.sh; learner step 51.4 vs 55.7 us in scripts/bench_aql.py)
-    fused_update: bool = True
-    # with the priority write in the backward launch: its extra workgroup writes the leaves only
-    # and the gradient launch's extra workgroup walks the levels (the one-round-trip walk with
-    # DPP node reductions, tree_dev.h).  MI355X, interleaved: 17496-17518 vs 17358-17376 SGD
-    # steps/s with the whole write in the backward's workgroup (which outlasts the backward)
-    tree_levels_in_grad: bool = True
-    # with tree_levels_in_grad: the lowest levels still walked by the backward's workgroup (it
-    # has slack behind the per-sample backward), the rest by the gradient launch
-    tree_levels_in_bwd: int = 1
-    # fused_update: the next step's PER draw in extra workgroups of the gradient launch (its
-    # tree descent hides behind the contraction) instead of the update launch; not with
-    # tree_levels_in_grad (the draw would read levels being written)
-    draw_in_grad: bool = True
     seed: int = 0
 
 
@@ -254,8 +216,6 @@ class AQLLearner:
         self.cfg, self.model, self.target, self.replay = cfg, model, target, replay
         dev = replay.device
         self.device = dev
-        self.tree_stream = torch.cuda.Stream(device=dev) if cfg.fork_tree else None
-        self._tree_pending = False
         self.flat = flatten_module_params(model)
         self.tflat = flatten_module_params(target)
         self.eps = flatten_noise(model)
@@ -303,21 +263,14 @@ class AQLLearner:
         nws = h.aql_workspace_floats()  # effective NoisyLinear weights: W1 [64][128] | b1 | w2 | b2
         self.eff_on = torch.zeros(nws, **f32)
         self.eff_tg = torch.zeros(nws, **f32)
-        self.dbg = torch.zeros(32, dtype=torch.int64, device=dev) if os.environ.get("APEX_AQL_DBG") else None
         p = dict(replay.table_ptrs(), eff_on=self.eff_on.data_ptr(), eff_tg=self.eff_tg.data_ptr(), idx=self.idx.data_ptr(), w=self.w.data_ptr(), var=self.var.data_ptr(),
                  q_s=self.q_s.data_ptr(), q_s2=self.q_s2.data_ptr(), qt_s2=self.qt_s2.data_ptr(),
                  vec=self.vec.data_ptr(), delta=self.delta.data_ptr(), lw=self.lw.data_ptr(),
                  lossp=self.lossp.data_ptr())
-        if self.dbg is not None:  # phase timestamps of the backward kernel (diagnostics)
-            p["dbg"] = self.dbg.data_ptr()
         self.L = h.make_aql_learn(self.fused_on._net(), self.fused_tg._net(), p, B,
                                   float(cfg.gamma ** cfg.n_steps), float(cfg.ent_lam))
-        if cfg.fwd_tile_groups or cfg.fwd_halves:
-            self.L = h.aql_learn_set_groups(self.L, int(cfg.fwd_tile_groups), int(cfg.fwd_halves))
-        # fused sampling: the same stratified draw (seed, counter, mass) as per_sample inside the forward
-        self.Ls = (h.aql_learn_set_sample(self.L, replay.tree, replay.filled.data_ptr(), self.beta.data_ptr(),
-                                          self.step_ctr.data_ptr(), replay.seed ^ 0x51A7,
-                                          0 if cfg.exact_mass else 1) if cfg.fused_sample else None)
+        if cfg.fwd_tile_groups:
+            self.L = h.aql_learn_set_groups(self.L, int(cfg.fwd_tile_groups), 0)
         self.G = h.make_aql_grad(self._grad_jobs(), self.P, self.vec.data_ptr(), B, self.grad.data_ptr(),
                                  self.part.data_ptr(), self.lossp.data_ptr(), self.loss_p.data_ptr())
         layers = []
@@ -332,56 +285,32 @@ class AQLLearner:
         self.post = h.make_aql_post(layers, self.flat[self.P_q:].data_ptr(), self.tflat[self.P_q:].data_ptr(),
                                     self.P_p, self.step_ctr.data_ptr(), self.ticket.data_ptr(),
                                     (cfg.seed * 0x9E3779B1 + 0x5EED) & 0xFFFFFFFFFFFF)
-        # the priority write (0.9 max + 0.1 |td| + 1e-6, loss mean) as one extra workgroup of the
-        # noise-reset launch: it only feeds the NEXT step's sampling, and the gradient contraction,
-        # the optimizers and the noise reset read none of the tree
         r = replay
-        self.post_tree = (h.aql_post_set_tree(self.post, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
-                                              self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
-                                              r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
-                          if cfg.fused_tree and not cfg.fork_tree and B <= 64 else None)
-        bwd = (cfg.bwd_tree or cfg.fused_update) and self.post_tree is None and not cfg.fork_tree and B <= 64
-        lv = bwd and cfg.tree_levels_in_grad
-        nb = int(cfg.tree_levels_in_bwd) if lv else -1  # levels the backward's workgroup walks (-1: all)
-        self.L_tree = (h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
-                                            r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha,
-                                            levels=nb) if bwd else None)
-        self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B, lo=nb + 1) if lv else None
-        split = (cfg.split_tree and self.post_tree is None and self.L_tree is None and not cfg.fork_tree
-                 and B <= 64)
-        self.G_tree = (h.aql_grad_set_tree(self.G, r.tree, self.idx.data_ptr(), B, self.delta.data_ptr(),
-                                           self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(),
-                                           r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha)
-                       if split else None)
-        self.post_levels = h.aql_post_set_levels(self.post, r.tree, r.wlist.data_ptr(), B) if split else None
-        self.S = self.S_draw = self.U = self.U_draw = None
-        self.bar = torch.zeros(4, dtype=torch.int32, device=dev)  # arrivals, generation, error flag
-        kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
-                  norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(),
-                  bar=self.bar.data_ptr(), err=self.bar[2:].data_ptr(), prio=self.prio.data_ptr(),
-                  loss_q=self.loss_q.data_ptr(), owner=r.owner.data_ptr(), list=r.wlist.data_ptr(),
-                  max_prio=r.max_prio.data_ptr(), alpha=r.alpha)
-        draw_kw = dict(draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=replay.seed ^ 0x51A7,
-                       exclude_last=0 if cfg.exact_mass else 1)
-        nb = h.aql_step_nbytes()
-        self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
-        self.pub_desc = torch.zeros(nb, dtype=torch.uint8, device=dev)
-        self._step_kw = kw
-        self.U_pub = None
-        if cfg.fused_step and not cfg.fork_tree and B <= 64:
-            try:
-                self.S = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
-            except RuntimeError as e:  # the grid cannot be co-resident on this device: separate launches
-                warnings.warn(f"AQL fused step tail unavailable ({e}); using the separate launches")
-            if self.S is not None and self.Ls is not None:  # + the next step's draw (the forward's sampling stream)
-                self.S_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, dict(kw, **draw_kw),
-                                              self.step_desc[1].data_ptr())
-        if cfg.fused_update and self.S is None and self.L_tree is not None:
-            self.U = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, dict(kw, update=1),
-                                     self.step_desc[0].data_ptr())
-            if self.Ls is not None:
-                self.U_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp,
-                                              dict(kw, update=1, **draw_kw), self.step_desc[1].data_ptr())
+        self.fused = bool(cfg.fused) and B <= 64  # (the tree workgroups stage <= 64 dirty paths)
+        self.Ls = self.L_tree = self.G_levels = self.U = self.U_draw = self.U_pub = None
+        if self.fused:
+            # the forward's own stratified draw (same seed, counter and mass as per_sample)
+            self.Ls = h.aql_learn_set_sample(self.L, r.tree, r.filled.data_ptr(), self.beta.data_ptr(),
+                                             self.step_ctr.data_ptr(), r.seed ^ 0x51A7, 0 if cfg.exact_mass else 1)
+            # the backward's extra workgroup recomputes the B TD terms from the forward's Q rows and
+            # writes the priorities (0.9 max + 0.1 |td| + 1e-6), the loss mean, the deduplicated
+            # leaves and tree level 1; the gradient launch's extra workgroup walks levels 2..
+            self.L_tree = h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
+                                               r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha,
+                                               levels=1)
+            self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B, lo=2)
+            kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
+                      norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(), update=1)
+            nb = h.aql_step_nbytes()
+            self.step_desc = torch.zeros(2, nb, dtype=torch.uint8, device=dev)
+            self.pub_desc = torch.zeros(nb, dtype=torch.uint8, device=dev)
+            self._step_kw = kw
+            self.U = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw, self.step_desc[0].data_ptr())
+            # + the NEXT step's draw (the tree is final once the backward launch's write is done)
+            self.U_draw = h.make_aql_step(self.L, self.G, self.post, r.tree, self.hp,
+                                          dict(kw, draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(),
+                                               seed=r.seed ^ 0x51A7, exclude_last=0 if cfg.exact_mass else 1),
+                                          self.step_desc[1].data_ptr())
         self.refresh()
 
     def set_publish(self, actor_flat: torch.Tensor, actor_eps: torch.Tensor) -> None:
@@ -402,8 +331,8 @@ class AQLLearner:
 
     @property
     def predraw(self) -> bool:
-        """Whether a step can draw the next step's rows (fused tail or update launch + fused sampling)."""
-        return self.S_draw is not None or self.U_draw is not None
+        """Whether a step can draw the next step's rows (the fused sequence's update launch)."""
+        return self.U_draw is not None
 
     def refresh(self) -> None:
         """Recompute the effective NoisyLinear weights (mu + sigma * eps) of both networks
@@ -455,65 +384,34 @@ class AQLLearner:
     def _s() -> int:
         return torch.cuda.current_stream().cuda_stream
 
-    def join(self) -> None:
-        """Order the caller's stream after the forked priority-tree write (if one is pending)."""
-        if self._tree_pending:
-            torch.cuda.current_stream().wait_stream(self.tree_stream)
-            self._tree_pending = False
-
     def step(self, drawn: bool = False, draw_next: bool = False, publish: bool = False) -> bool:
-        """One SGD step.  ``drawn``: this step's rows were sampled by the previous step's fused
-        tail (``draw_next`` there) -- the forward skips its tree descent; both need the fused
-        step tail and fused sampling (:meth:`AQLEngine.learn_steps` pairs them within an
-        iteration)."""
-        self.join()  # the sampler reads the tree the previous step's forked write updated
+        """One SGD step.  ``drawn``: this step's rows were drawn by the previous step's update
+        launch (``draw_next`` there) -- the forward skips its tree descent (:meth:`AQLEngine.
+        learn_steps` pairs them within an iteration).  ``publish``: the update launch also writes
+        the acting copies (returns whether it did)."""
         h, r, s = self.hip, self.replay, self._s()
         if drawn or draw_next:
-            assert self.predraw, "pre-drawn rows need the fused step tail / update launch and fused sampling"
-        if drawn:
-            h.aql_learn_fwd(self.L, s)
-        elif self.Ls is not None:  # the forward samples its own rows (one launch fewer)
-            h.aql_learn_fwd(self.Ls, s)
-        else:
-            excl = 0 if self.cfg.exact_mass else 1
-            h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
-                         self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
-            h.aql_learn_fwd(self.L, s)
-        if self.S is not None:  # backward, priority write, gradients, optimizers, noise: one launch
-            h.aql_step_tail(self.S_draw if draw_next else self.S, s)
-            self._track_losses()
-            return
-        h.aql_learn_bwd(self.L if self.L_tree is None else self.L_tree, s)
-        # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
-        # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
-        # forked onto the tree stream (cfg.fork_tree): it only feeds the NEXT step's sampler, so
-        # it runs beside the gradient contraction, the optimizers and the noise reset
-        def tree_write(ts):
-            h.per_write_batch(r.tree, 0, 0, 0, 0, self.idx.data_ptr(), 0, self.B, self.delta.data_ptr(),
-                              self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
-                              r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), ts)
-
-        if self.post_tree is not None or self.G_tree is not None or self.L_tree is not None:
-            pass  # folded into a launch (aql_learn_set_tree | aql_post_set_tree | aql_grad_set_tree + levels)
-        elif self.cfg.fork_tree:
-            self.tree_stream.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self.tree_stream):
-                tree_write(self._s())
-            self._tree_pending = True
-        else:
-            tree_write(s)
-        G = self.G_tree if self.G_tree is not None else (self.G_levels if self.G_levels is not None else self.G)
-        if self.U is not None:  # optimizers, noise of both critics, proposal copy (+ next draw): one launch
+            assert self.predraw, "pre-drawn rows need the fused sequence"
+        if self.fused:
+            h.aql_learn_fwd(self.L if drawn else self.Ls, s)
+            h.aql_learn_bwd(self.L_tree, s)
+            h.aql_grad(self.G_levels, s)
             pub = publish and not draw_next and self.U_pub is not None
-            if draw_next and self.cfg.draw_in_grad and self.G_levels is None:  # (levels in that launch: racy)
-                h.aql_grad_draw(G, self.U_draw, s)
-                h.aql_update(self.U, s)
-            else:
-                h.aql_grad(G, s)
-                h.aql_update(self.U_draw if draw_next else (self.U_pub if pub else self.U), s)
+            h.aql_update(self.U_draw if draw_next else (self.U_pub if pub else self.U), s)
             self._track_losses()
             return pub
-        h.aql_grad(G, s)
+        # the reference sequence
+        excl = 0 if self.cfg.exact_mass else 1
+        h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
+                     self.step_ctr.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), excl, s)
+        h.aql_learn_fwd(self.L, s)
+        h.aql_learn_bwd(self.L, s)
+        # priorities 0.9 max|td| + 0.1 |td| + 1e-6 (utils.py:55) and the loss mean, written with the
+        # batched tree kernels (leaves + one wide launch per big level; duplicates last-write-wins)
+        h.per_write_batch(r.tree, 0, 0, 0, 0, self.idx.data_ptr(), 0, self.B, self.delta.data_ptr(),
+                          self.lw.data_ptr(), self.prio.data_ptr(), self.loss_q.data_ptr(), 0, r.owner.data_ptr(),
+                          r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha, r.ticket.data_ptr(), s)
+        h.aql_grad(self.G, s)
         Pq, o = self.P_q, 4 * self.P_q
         # the two optimizers (critic, proposal; own clip norms) in one launch
         h.adam_step2((self.flat.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), Pq,
@@ -522,9 +420,9 @@ class AQLLearner:
                       self.v.data_ptr() + o, self.P_p, self.part.data_ptr() + 8 * self.nblk, self.nblk,
                       self.norms_p.data_ptr()),
                      self.hp, self.step_ctr.data_ptr(), s)
-        h.aql_post(self.post_tree if self.post_tree is not None else
-                   (self.post_levels if self.post_levels is not None else self.post), 1, s)
+        h.aql_post(self.post, 1, s)
         self._track_losses()
+        return False
 
     def _track_losses(self) -> None:
         if self.cfg.track_losses:  # device-side running sums; read (one sync) only when logging
@@ -534,7 +432,6 @@ class AQLLearner:
 
     def take_loss_means(self) -> tuple[float, float, int]:
         """(mean loss_q, mean loss_proposal, steps) since the previous call; resets the sums."""
-        self.join()
         q, p, n = (float(x) for x in self.loss_acc.tolist())
         self.loss_acc.zero_()
         n = int(round(n))
@@ -547,15 +444,7 @@ class AQLLearner:
         self.hip.copy_f32(self.teps.data_ptr(), self.eps.data_ptr(), self.eps.numel(), s)
         self.refresh()
 
-    def check_fused(self) -> None:
-        """Raise if a grid barrier of the fused step tail ever timed out (host sync)."""
-        if self.S is not None and int(self.bar[2].item()) != 0:
-            raise RuntimeError("aql_step_tail: a grid barrier timed out (the grid was not co-resident); "
-                               "results since then are invalid")
-
     def stats(self) -> dict:
-        self.join()
-        self.check_fused()
         return {"loss_q": float(self.loss_q.item()), "loss_proposal": float(self.loss_p.item()),
                 "grad_norm_q": float(self.norms_q[0].item()), "grad_norm_proposal": float(self.norms_p[0].item()),
                 "steps": int(self.step_ctr.item())}
@@ -645,7 +534,6 @@ class AQLEngine:
         self._pub_in_graph = False
         self._half = 0
         if self.overlap:
-            assert not cfg.fork_tree, "overlap and fork_tree are exclusive"
             self._zero64 = torch.zeros(1, dtype=torch.int64, device=dev)
             self._stage_slots = torch.zeros(E, dtype=torch.int32, device=dev)
             self._stage = []
@@ -664,8 +552,9 @@ class AQLEngine:
             self._ev_learn = torch.cuda.Event()
         self.actor_net = FusedAQL(self.actor_model)._net()
         # acting on the learner's MFMA candidate forward (online net, s only, row = env index)
+        # (64 acting workgroups beside the learner in overlap mode: most CUs stay the learner's)
         self.actL = h.make_aql_act(self.actor_net, self.obs_buf.data_ptr(), self.amu.data_ptr(), self.ws.data_ptr(),
-                                   self.qbuf.data_ptr(), E, int(cfg.act_blocks) or (64 if cfg.overlap else 0))
+                                   self.qbuf.data_ptr(), E, 64 if cfg.overlap else 0)
         h.aql_env_reset(self.env, self._s())
         self.iterations = 0
         self.learner_steps = 0
@@ -689,7 +578,6 @@ class AQLEngine:
         staging half ``half`` instead of the ring (see :meth:`apply_staged`); ``into``: an
         ``AqlInsert`` of E rows (C = E) to write them to instead -- e.g. a central-topology
         actor rank's packet buffer (engine.central_aql); no tree write then."""
-        self.learner.join()  # the actor's tree writes follow the learner's forked one
         h, s, E, r = self.hip, self._s(), self.E, self.replay
         self._act(h, s, E)
         if into is not None or half is not None:
@@ -702,16 +590,13 @@ class AQLEngine:
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
 
     def _act(self, h, s, E) -> None:
-        """Proposal, candidate Q and epsilon-greedy selection for all E envs."""
-        mfma = self.cfg.act_q == "mfma"  # (the effective weights ride along in the proposal launch)
+        """Proposal, candidate Q (the learner's MFMA candidate forward on the online net, s only)
+        and epsilon-greedy selection for all E envs."""
+        # (the effective NoisyNet weights ride along in the proposal launch)
         h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
                       self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s,
-                      self.ws.data_ptr() if mfma else 0)
-        if mfma:
-            h.aql_act_q(self.actL, s)
-        else:
-            h.aql_candidate_q(self.actor_net, self.ws.data_ptr(), self.obs_buf.data_ptr(), self.amu.data_ptr(), E,
-                              self.qbuf.data_ptr(), s)
+                      self.ws.data_ptr())
+        h.aql_act_q(self.actL, s)
         h.aql_select(self.qbuf.data_ptr(), self.amu.data_ptr(), E, self.T, self.adim, self.eps.data_ptr(),
                      self.seed ^ 0xA9C1, self.actor_ctr.data_ptr(), self.act_idx.data_ptr(), self.env_act.data_ptr(), s)
 
@@ -731,7 +616,6 @@ class AQLEngine:
         for k in range(self.K):
             pub = bool(self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K,
                                          publish=publish and k + 1 == self.K))
-        self.learner.join()  # (a captured graph must end joined)
         return pub
 
     def fill(self, threshold: int | None = None) -> None:

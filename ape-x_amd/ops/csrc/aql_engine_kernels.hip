@@ -40,7 +40,6 @@
 #include <algorithm>
 
 #include "common.h"
-#include "grid_sync.h"
 #include "kernels.h"
 #include "opt_dev.h"
 #include "tree_dev.h"
@@ -406,7 +405,7 @@ __device__ __forceinline__ AqlTd aql_td(const AqlLearn& L, int b, int row, int a
                      L.w[b]);
 }
 
-// the backward of sample b by one workgroup (aql_learn_bwd_k, or phase A of aql_step_tail_k)
+// the backward of sample b by one workgroup (aql_learn_bwd_k)
 __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   __shared__ __attribute__((aligned(16))) float s_s[64];
   __shared__ float s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
@@ -691,7 +690,7 @@ __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
 constexpr int kGradThreads = 256;
 
 // the weight gradients of flat elements [bid * 256, +256) and the block's per-group sums of
-// squares (aql_grad_k, or phase B of aql_step_tail_k); returns the thread's gradient
+// squares (aql_grad_k); returns the thread's gradient
 __device__ __forceinline__ float aql_grad_block(const AqlGrad& G, int bid, int nblk) {
   __shared__ double red[2][4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -808,44 +807,12 @@ __device__ __forceinline__ void step_ticket(const AqlPost& P, int G, uint64_t st
 
 __global__ __launch_bounds__(256) void aql_post_k(AqlPost P, int regen) {
   const uint64_t st = (uint64_t)P.step[0];
-  if (regen && P.tree_write && blockIdx.x == gridDim.x - 1) {  // block-uniform: the fused tree write
-    __shared__ float red[16];
-    __shared__ int sids[64];
-    if (P.tree_write == 2) {  // levels only: aql_grad_k wrote the leaves and the dirty list
-      for (int i = threadIdx.x; i < P.bw.B; i += blockDim.x) sids[i] = P.bw.list[i];
-      update_levels_block(P.tree, sids, P.bw.B, 1, P.tree.levels);
-    } else {
-      batch_leaves_block(P.tree, P.bw, 1, red, sids);
-    }
-  } else {
-    aql_post_block(P, regen, st);
-  }
+  aql_post_block(P, regen, st);
   if (!regen) return;
   step_ticket(P, (int)gridDim.x, st);
 }
 
-// ------------------------------------------------------------------ fused step tail
-// aql_step_tail_k: everything of one learner step after the candidate forward, in ONE launch
-// of grid = max(gradient blocks, B + 1) + 1 + 8 workgroups, all co-resident (the launcher checks
-// the occupancy), in three phases separated by grid barriers (grid_sync.h):
-//
-//   A  blocks [0, B): the per-sample backward (aql_bwd_block)
-//      last block:    this step's priority write -- it recomputes the B TD terms itself
-//                     (aql_td: the same formula the backward uses) from the forward's Q
-//                     rows, so the leaves AND every level run here, beside the backward,
-//                     instead of after it (the next step's sampler is the only reader)
-//      other blocks:  the TARGET critic's noise reset (reads target parameters only)
-//   B  blocks [0, nblk): the weight-gradient contraction (aql_grad_block) + norm partials
-//   C  every block:   both clipped Adam steps over the flat parameters, the ONLINE noise
-//                     reset (the thread owning a sigma element also updates its mu partner,
-//                     then draws the new epsilon and writes mu + sigma eps), the proposal
-//                     hard copy online -> target; the last block bumps the step counter
-//      8 blocks before the last (AqlStep::draw): the NEXT step's PER draw, so that forward
-//                     skips its tree descent (the tree is final after phase A)
-//
-// Same arithmetic as the separate launches (aql_learn_bwd_k, aql_grad_k, opt_step2_k,
-// aql_post_k): the gradient partials keep aql_grad_k's block layout, so the clip norms and
-// every update are bit-identical (tests/test_gpu_aql_engine.py).
+// ------------------------------------------------------------------ update launch helpers
 __device__ __forceinline__ float noise_w(uint64_t seed, int l, int o, int c, uint64_t st) {
   return scaled_noise(seed, l, 0, o, st) * scaled_noise(seed, l, 1, c, st);
 }
@@ -867,12 +834,12 @@ __device__ __forceinline__ void noise_elem(const AqlNoise& z, int l, int64_t i, 
   }
 }
 
-constexpr int kStepDrawBlocks = 8;  // phase C workgroups of the next step's draw (4 waves each)
+constexpr int kStepDrawBlocks = 8;  // update-launch workgroups of the next step's draw (4 waves each)
 
-// phase C of the step for workgroup bid (< nblk: its parameter elements, thread gradient g):
-// both clipped Adam steps, the online noise reset (the thread owning a sigma element also
-// updates its mu partner, then draws the new epsilon and writes mu + sigma eps) and the
-// proposal hard copy online -> target.  Shared by aql_step_tail_k and aql_update_k.
+// the update of workgroup bid (< nblk: its parameter elements, thread gradient g): both clipped
+// Adam steps, the online noise reset (the thread owning a sigma element also updates its mu
+// partner, then draws the new epsilon and writes mu + sigma eps) and the proposal hard copy
+// online -> target.
 __device__ __forceinline__ void update_block(const AqlStep& D, int bid, float g, uint64_t st) {
   const int t = threadIdx.x;
   // this thread's element (and, for an online sigma, its mu partner): its parameter / moments /
@@ -968,57 +935,18 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
   }
 }
 
-// aql_grad_k: the gradient blocks, then the optional tree workgroup (G.tree_leaves), then the
-// optional NEXT step's PER draw (kStepDrawBlocks workgroups; `draw`: the update descriptor) --
-// the tree is final once the backward launch's priority write is done, and the draw's tree
-// descent hides behind the contraction instead of bounding the update launch
-__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G, const AqlStep* __restrict__ draw) {
-  const int nd = draw ? kStepDrawBlocks : 0, ng = (int)gridDim.x - nd - (G.tree_leaves ? 1 : 0);
-  if ((int)blockIdx.x >= ng + (G.tree_leaves ? 1 : 0)) {  // block-uniform: the draw
-    draw_block(*draw, (int)blockIdx.x - ((int)gridDim.x - nd), (uint64_t)draw->P.step[0]);
-    return;
-  }
-  if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the split tree write
-    __shared__ float tred[16];
+// aql_grad_k: the gradient blocks, then (G.tree_leaves) one workgroup walking the priority
+// tree's levels levels_lo.. of this step's dirty list -- the backward launch's tree workgroup
+// wrote the leaves, the list and the lowest levels
+__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+  const int ng = (int)gridDim.x - (G.tree_leaves ? 1 : 0);
+  if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the level walk
     __shared__ int sids[64];
-    if (G.tree_leaves == 2) {  // levels only: the backward launch wrote the leaves and the dirty list
-      for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
-      update_levels_fast(G.tree, sids, G.bw.B, nullptr, max(G.levels_lo, 1));
-    } else {
-      batch_leaves_block(G.tree, G.bw, 0, tred, sids);
-    }
+    for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
+    update_levels_fast(G.tree, sids, G.bw.B, nullptr, max(G.levels_lo, 1));
     return;
   }
   aql_grad_block(G, blockIdx.x, ng);
-}
-
-__global__ __launch_bounds__(256) void aql_step_tail_k(const AqlStep* __restrict__ Dp) {
-  const AqlStep& D = *Dp;
-  const int bid = blockIdx.x, G = gridDim.x, t = threadIdx.x;
-  const int B = D.L.B;
-  const uint64_t st = (uint64_t)D.P.step[0];
-  // ---- phase A
-  if (bid < B) {
-    aql_bwd_block(D.L, bid);
-  } else if (bid == G - 1) {  // (the draw workgroups [G - 1 - kStepDrawBlocks, G - 1) join the noise below)
-    td_tree_block(D.L, D.tree, D.bw, 1 << 30);
-  } else {
-    const int64_t n2 = (int64_t)D.P.layer[2].out * D.P.layer[2].in + D.P.layer[2].out;
-    const int64_t n3 = (int64_t)D.P.layer[3].out * D.P.layer[3].in + D.P.layer[3].out;
-    for (int64_t i = (int64_t)(bid - B) * 256 + t; i < n2 + n3; i += (int64_t)(G - 1 - B) * 256) {
-      if (i < n2) noise_elem(D.P.layer[2], 2, i, D.P.seed, st);
-      else noise_elem(D.P.layer[3], 3, i - n2, D.P.seed, st);
-    }
-  }
-  grid_sync(D.bar, (unsigned)G, D.err);
-  // ---- phase B
-  float g = 0.f;
-  if (bid < D.nblk) g = aql_grad_block(D.G, bid, D.nblk);
-  grid_sync(D.bar, (unsigned)G, D.err);
-  // ---- phase C
-  update_block(D, bid, g, st);
-  if (D.draw && bid >= G - 1 - kStepDrawBlocks && bid < G - 1) draw_block(D, bid - (G - 1 - kStepDrawBlocks), st);
-  step_ticket(D.P, G, st);
 }
 
 // The step's update as its own launch after aql_grad_k (no grid barrier): blocks [0, nblk) the
@@ -1292,7 +1220,7 @@ void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
 
 int aql_grad_blocks(int64_t n) { return (int)((n + kGradThreads - 1) / kGradThreads); }
 
-void aql_grad(const AqlGrad& g, hipStream_t s, const AqlStep* draw) {
+void aql_grad(const AqlGrad& g, hipStream_t s) {
   if (g.njobs < 1 || g.njobs > kAqlMaxJobs || g.job[0].off != 0) throw std::invalid_argument("aql_grad: jobs");
   for (int k = 0; k < g.njobs; ++k) {
     const AqlGradJob& J = g.job[k];
@@ -1301,37 +1229,28 @@ void aql_grad(const AqlGrad& g, hipStream_t s, const AqlStep* draw) {
     if (J.goff < 0 || J.goff + J.rows > aqlv::STRIDE || J.xoff + J.cols > aqlv::STRIDE)
       throw std::invalid_argument("aql_grad: vector offsets");
   }
-  if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || g.bw.E != 0 || (g.tree_leaves == 1 && !g.bw.idx) || !g.bw.list))
-    throw std::invalid_argument("aql_grad: the split tree write takes 1..64 learner rows and no actor rows");
-  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0) + (draw ? kStepDrawBlocks : 0), kGradThreads, 0, s>>>(
-      g, draw);
+  if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || !g.bw.list))
+    throw std::invalid_argument("aql_grad: the level walk takes a list of 1..64 learner rows");
+  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), kGradThreads, 0, s>>>(g);
   LAUNCH_CHECK();
 }
 
 void aql_post(const AqlPost& p, int regen, hipStream_t s) {
   int64_t n = regen ? p.n_copy : 0;
   for (int l = 0; l < 4; ++l) n += (int64_t)p.layer[l].out * p.layer[l].in + p.layer[l].out;
-  const int extra = (regen && p.tree_write) ? 1 : 0;  // the fused tree-write workgroup
-  if (extra && (p.bw.B < 1 || p.bw.B > 64 || p.bw.E != 0 || (p.tree_write == 1 && !p.bw.idx) || !p.bw.list))
-    throw std::invalid_argument("aql_post: the fused tree write takes <= 64 learner rows and no actor rows");
-  aql_post_k<<<(int)((n + 255) / 256) + extra, 256, 0, s>>>(p, regen);
+  aql_post_k<<<(int)((n + 255) / 256), 256, 0, s>>>(p, regen);
   LAUNCH_CHECK();
 }
 
-int aql_step_grid(const AqlStep& d) { return std::max(d.nblk, d.L.B + 1) + 1 + kStepDrawBlocks; }
-
-void aql_step_check(const AqlStep& d, bool coresident) {
+void aql_step_check(const AqlStep& d) {
   check_net(d.L.on);
   const AqlGrad& G = d.G;
-  if (d.nblk != aql_grad_blocks(G.n) || d.n != G.n || G.tree_leaves)
-    throw std::invalid_argument("aql_step: gradient blocks / parameter count / split tree write");
-  if (d.L.B < 1 || d.L.B > 64) throw std::invalid_argument("aql_step: 1 <= batch <= 64 (one-workgroup tree write)");
+  if (d.nblk != aql_grad_blocks(G.n) || d.n != G.n)
+    throw std::invalid_argument("aql_step: gradient blocks / parameter count");
   if (d.P_q <= 0 || d.P_q > d.n || !d.p || !d.m || !d.v || !d.norms_q || !d.norms_p || !G.grad || !G.part)
     throw std::invalid_argument("aql_step: optimizer tensors");
-  if (!d.bar || !d.err || !d.P.step || !d.P.ticket || !d.P.dst || d.P.n_copy != d.n - d.P_q)
-    throw std::invalid_argument("aql_step: barrier / counter / proposal copy");
-  if (!d.bw.idx || d.bw.B != d.L.B || d.bw.E != 0 || !d.bw.owner || !d.bw.list || !d.bw.max_prio)
-    throw std::invalid_argument("aql_step: priority write");
+  if (!d.P.step || !d.P.ticket || !d.P.dst || d.P.n_copy != d.n - d.P_q)
+    throw std::invalid_argument("aql_step: counter / proposal copy");
   if (d.draw && (!d.filled || !d.beta || !d.L.idx || !d.L.w))
     throw std::invalid_argument("aql_step: the next step's draw needs filled / beta / idx / w");
   for (int k = 0; k < 2; ++k) {
@@ -1341,19 +1260,6 @@ void aql_step_check(const AqlStep& d, bool coresident) {
     for (int64_t o : {d.mu_b[k], d.sig_b[k]})
       if (o < 0 || o + nb > d.P_q) throw std::invalid_argument("aql_step: online noisy biases outside the critic");
   }
-  if (!coresident) return;  // (aql_update: an ordinary grid)
-  int dev = 0, cus = 0, per_cu = 0;
-  HIP_CHECK(hipGetDevice(&dev));
-  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, aql_step_tail_k, 256, 0));
-  if ((int64_t)cus * per_cu < aql_step_grid(d))
-    throw std::runtime_error("aql_step: the grid does not fit co-resident (" + std::to_string(cus) + " CUs x " +
-                             std::to_string(per_cu) + " workgroups < " + std::to_string(aql_step_grid(d)) + ")");
-}
-
-void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s) {
-  aql_step_tail_k<<<grid, 256, 0, s>>>(dev);
-  LAUNCH_CHECK();
 }
 
 int aql_update_grid(const AqlStep& d, int* noise_blocks) {

@@ -711,67 +711,15 @@ PYBIND11_MODULE(_apex_hip, m) {
     return p;
   });
   m.def("aql_post", [](const AqlPost& p, int regen, uint64_t s) { aql_post(p, regen, S(s)); });
-  // the learner step's batched priority write folded into the noise-reset launch
-  m.def("aql_post_set_tree", [](const AqlPost& p0, const TreeHandle& t, uint64_t idx, int B, uint64_t delta,
-                                uint64_t lw, uint64_t prio_out, uint64_t loss_out, uint64_t owner, uint64_t list,
-                                uint64_t max_prio, float alpha) {
-    AqlPost p = p0;
-    BatchWrite w{};
-    w.idx = P<const int>(idx);
-    w.B = B;
-    w.mix = PrioMix{P<const float>(delta), P<const float>(lw), P<float>(prio_out), P<float>(loss_out)};
-    w.owner = P<int>(owner);
-    w.list = P<int>(list);
-    w.max_prio = P<float>(max_prio);
-    w.alpha = alpha;
-    if (!w.idx || !w.mix.delta || !w.mix.lw || !w.owner || !w.list || !w.max_prio || B < 1 || B > 64)
-      throw std::invalid_argument("aql_post_set_tree: 1 <= B <= 64 and every pointer");
-    p.tree_write = 1;
-    p.tree = t.d;
-    p.bw = w;
-    return p;
-  });
-  m.def("aql_grad_set_tree", [](const AqlGrad& g0, const TreeHandle& t, uint64_t idx, int B, uint64_t delta,
-                                uint64_t lw, uint64_t prio_out, uint64_t loss_out, uint64_t owner, uint64_t list,
-                                uint64_t max_prio, float alpha) {
-    AqlGrad g = g0;
-    BatchWrite w{};
-    w.idx = P<const int>(idx);
-    w.B = B;
-    w.mix = PrioMix{P<const float>(delta), P<const float>(lw), P<float>(prio_out), P<float>(loss_out)};
-    w.owner = P<int>(owner);
-    w.list = P<int>(list);
-    w.max_prio = P<float>(max_prio);
-    w.alpha = alpha;
-    if (!w.idx || !w.mix.delta || !w.mix.lw || !w.owner || !w.list || !w.max_prio || B < 1 || B > 64)
-      throw std::invalid_argument("aql_grad_set_tree: 1 <= B <= 64 and every pointer");
-    g.tree_leaves = 1;
-    g.tree = t.d;
-    g.bw = w;
-    return g;
-  });
-  m.def("aql_post_set_levels", [](const AqlPost& p0, const TreeHandle& t, uint64_t list, int B) {
-    AqlPost p = p0;
-    BatchWrite w{};
-    w.list = P<int>(list);
-    w.B = B;
-    if (!w.list || B < 1 || B > 64) throw std::invalid_argument("aql_post_set_levels: 1 <= B <= 64 and a list");
-    p.tree_write = 2;
-    p.tree = t.d;
-    p.bw = w;
-    return p;
-  });
-  // fused step tail: the descriptor is validated, copied into `desc` (device memory of
-  // aql_step_nbytes() bytes, owned by the caller) and launched from there
+  // the learner step's update launch: the descriptor is validated, copied into `desc` (device
+  // memory of aql_step_nbytes() bytes, owned by the caller) and launched from there
   struct AqlStepHandle {
     const AqlStep* dev;
     int grid;
-    int update;        // 1: the separate update launch (aql_update), not the fused tail
-    int noise_blocks;  // aql_update: target-noise workgroups
+    int noise_blocks;  // target-noise workgroups
     int draw;          // the descriptor carries the next step's draw
   };
-  py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid)
-      .def_readonly("update", &AqlStepHandle::update);
+  py::class_<AqlStepHandle>(m, "AqlStepHandle").def_readonly("grid", &AqlStepHandle::grid);
   m.def("aql_step_nbytes", []() { return sizeof(AqlStep); });
   m.def("make_aql_step", [](const AqlLearn& L, const AqlGrad& G, const AqlPost& Pst, const TreeHandle& t,
                             const AdamParams& hp, py::dict p, uint64_t desc) {
@@ -786,21 +734,11 @@ PYBIND11_MODULE(_apex_hip, m) {
     d.p = P<float>(g("p")); d.m = P<float>(g("m")); d.v = P<float>(g("v"));
     d.n = gi("n"); d.P_q = gi("P_q");
     d.norms_q = P<float>(g("norms_q")); d.norms_p = P<float>(g("norms_p"));
-    d.bar = P<unsigned>(g("bar")); d.err = P<int>(g("err"));
     d.nblk = aql_grad_blocks(d.n);
     for (int k = 0; k < 2; ++k) {  // offsets of the online noisy tensors in the flat buffer
       const AqlNoise& z = Pst.layer[k];
       d.mu_w[k] = z.wmu - d.p; d.sig_w[k] = z.wsig - d.p; d.mu_b[k] = z.bmu - d.p; d.sig_b[k] = z.bsig - d.p;
     }
-    BatchWrite w{};
-    w.idx = L.idx;
-    w.B = L.B;
-    w.mix = PrioMix{L.delta, L.lw, P<float>(g("prio")), P<float>(g("loss_q"))};  // delta / lw: LDS at run time
-    w.owner = P<int>(g("owner"));
-    w.list = P<int>(g("list"));
-    w.max_prio = P<float>(g("max_prio"));
-    w.alpha = p["alpha"].cast<float>();
-    d.bw = w;
     if (p.contains("draw") && p["draw"].cast<int>()) {  // + the next step's PER draw (same stream as
       d.draw = 1;                                       // aql_learn_set_sample's)
       d.filled = P<const int64_t>(g("filled"));
@@ -813,25 +751,13 @@ PYBIND11_MODULE(_apex_hip, m) {
       d.pub_weps[0] = P<float>(g("pub_weps0")); d.pub_weps[1] = P<float>(g("pub_weps1"));
       d.pub_beps[0] = P<float>(g("pub_beps0")); d.pub_beps[1] = P<float>(g("pub_beps1"));
     }
-    const int upd = p.contains("update") ? p["update"].cast<int>() : 0;
-    aql_step_check(d, !upd);
+    aql_step_check(d);
     HIP_CHECK(hipMemcpy(reinterpret_cast<void*>(desc), &d, sizeof(AqlStep), hipMemcpyHostToDevice));
     int nb = 0;
-    const int grid = upd ? aql_update_grid(d, &nb) : aql_step_grid(d);
-    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, upd, nb, d.draw};
+    const int grid = aql_update_grid(d, &nb);
+    return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, nb, d.draw};
   });
-  m.def("aql_step_tail", [](const AqlStepHandle& h, uint64_t s) {
-    if (h.update) throw std::invalid_argument("aql_step_tail: an update handle (use aql_update)");
-    aql_step_tail(h.dev, h.grid, S(s));
-  });
-  m.def("aql_grad_draw", [](const AqlGrad& G, const AqlStepHandle& h, uint64_t s) {
-    if (!h.update || !h.draw) throw std::invalid_argument("aql_grad_draw: an update handle with the draw");
-    aql_grad(G, S(s), h.dev);
-  });
-  m.def("aql_update", [](const AqlStepHandle& h, uint64_t s) {
-    if (!h.update) throw std::invalid_argument("aql_update: a fused-tail handle (use aql_step_tail)");
-    aql_update(h.dev, h.grid, h.noise_blocks, S(s));
-  });
+  m.def("aql_update", [](const AqlStepHandle& h, uint64_t s) { aql_update(h.dev, h.grid, h.noise_blocks, S(s)); });
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

@@ -487,19 +487,15 @@ struct AqlGrad {
   double* part;        // [2][blocks] sum of squares per group
   const float* lossp;  // [B]
   float* lossp_out;    // [1] proposal loss mean
-  // split priority write (aql_grad_set_tree): one extra workgroup writes this step's leaves
-  // (per_write_batch's leaves part, B <= 64) and the dirty list; the noise-reset launch's
-  // extra workgroup then walks the levels (AqlPost::tree_write = 2)
-  int tree_leaves;  // 1: the leaves; 2: levels levels_lo.. only (the backward launch wrote the leaves + list)
+  // the priority tree's level walk (aql_grad_set_levels): one extra workgroup walks levels
+  // levels_lo.. of the dirty list the backward launch's tree workgroup wrote (with the leaves)
+  int tree_leaves;  // 0 / 2 (the walk)
   int levels_lo;
   TreeDesc tree;
   BatchWrite bw;
 };
 int aql_grad_blocks(int64_t n);
-struct AqlStep;
-// draw: an update descriptor with AqlStep::draw (device memory) -- the next step's PER draw
-// runs in extra workgroups of this launch
-void aql_grad(const AqlGrad& g, hipStream_t s, const AqlStep* draw = nullptr);
+void aql_grad(const AqlGrad& g, hipStream_t s);
 struct AqlNoise {
   float *weps, *beps;                    // NoisyLinear epsilon buffers [out][in], [out]
   const float *wmu, *wsig, *bmu, *bsig;  // parameters (post-update)
@@ -514,38 +510,28 @@ struct AqlPost {
   int64_t* step;       // learner step counter (+1 by the last block)
   int* ticket;
   uint64_t seed;
-  // fused priority write (aql_post_set_tree): one extra workgroup of the regen launch runs
-  // this step's batched tree write (per_write_batch's leaves + all levels, B <= 64) beside
-  // the noise reset -- neither reads what the other writes; the next step's sampling follows.
-  // tree_write = 2 (aql_post_set_levels): the levels only, the leaves ran in aql_grad_k
-  int tree_write;
-  TreeDesc tree;
-  BatchWrite bw;
 };
 // regen = 1: fresh factorised noise for all four layers (reset_noise), effective weights,
 // proposal copy, step + 1.  regen = 0: effective weights from the current noise only
 // (after initialisation / a target sync).
 void aql_post(const AqlPost& p, int regen, hipStream_t s);
-// Fused learner-step tail (aql_engine_kernels.hip: aql_step_tail_k): backward + priority
-// write + target noise reset | weight gradients | both clipped Adam steps + online noise reset
-// + proposal copy + step bump -- three phases of ONE launch separated by grid barriers
-// (grid_sync.h), replacing aql_learn_bwd + aql_grad + adam_step2 + aql_post.  The descriptor
-// lives in device memory (too large for kernel arguments).
+// The learner step's update (aql_engine_kernels.hip: aql_update_k) after the gradient launch:
+// both clipped Adam steps + the noise reset of both critics + the proposal copy + the step bump
+// (+ the next step's PER draw, + the acting copies), replacing adam_step2 + aql_post when the
+// priority write ran in the backward launch.  The descriptor lives in device memory (too large
+// for kernel arguments).
 struct AqlStep {
   AqlLearn L;              // the backward's view (online net, replay tables, per-sample outputs)
   AqlGrad G;               // gradient jobs, grad, partials [2][nblk], proposal loss mean
   AqlPost P;               // noisy layers (online 0-1, target 2-3), proposal copy, step, ticket
-  BatchWrite bw;           // this step's priority write (learner rows; the mix inputs come from LDS)
   TreeDesc tree;
   AdamParams hp;
   float *p, *m, *v;        // flat parameters and Adam moments
   int64_t n, P_q;          // critic [0, P_q), proposal [P_q, n)
   float *norms_q, *norms_p;
   int64_t mu_w[2], sig_w[2], mu_b[2], sig_b[2];  // flat offsets of the online noisy layers' tensors
-  unsigned* bar;           // [2] grid barrier (arrivals, generation), zero-initialised
-  int* err;                // set if a barrier wait timed out (grid not co-resident)
   int nblk;                // gradient workgroups (aql_grad_blocks(n))
-  // the NEXT step's PER draw (draw = 1): in phase C the draw workgroups sample step st + 1's
+  // the NEXT step's PER draw (draw = 1): extra workgroups sample step st + 1's
   // rows into L.idx / L.w -- what the next forward's fused sampling would draw (same tree,
   // counter, mass, beta) -- and that forward runs on the plain descriptor, without its descent.
   // An iteration's last step does not draw (the actors insert before the next one).
@@ -560,13 +546,7 @@ struct AqlStep {
   float* pub_weps[2];
   float* pub_beps[2];
 };
-int aql_step_grid(const AqlStep& d);
-// shapes, pointers, and (coresident) that the fused tail's grid fits co-resident
-void aql_step_check(const AqlStep& d, bool coresident = true);
-void aql_step_tail(const AqlStep* dev, int grid, hipStream_t s);
-// The step's update as its own launch after aql_grad (aql_update_k: both clipped Adam steps,
-// noise reset of both critics, proposal copy, optional next-step draw, step bump) -- replaces
-// adam_step2 + aql_post when the priority write ran in the backward launch
+void aql_step_check(const AqlStep& d);
 int aql_update_grid(const AqlStep& d, int* noise_blocks);
 void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s);
 struct AqlEnv {

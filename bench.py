@@ -96,18 +96,6 @@ def parse():
                     help="apex: the headline Ape-X DQN bench; aql: the GPU AQL engine (BASELINE config 4, "
                          "AQL_dis BipedalWalker-shaped; one step = one actor step of --envs envs + envs/32 SGD steps)")
     ap.add_argument("--aql-env", default="BipedalWalker-v3")
-    ap.add_argument("--aql-bwd-tree", type=int, default=None,
-                    help="AQL: priority write in the backward launch (1) or split over grad/post (0)")
-    ap.add_argument("--aql-fused-update", type=int, default=None,
-                    help="AQL: optimizers + noise + next draw as one launch after the gradients (1) or not (0)")
-    ap.add_argument("--aql-levels-in-grad", type=int, default=None,
-                    help="AQL: tree levels walked in the gradient launch (1) or in the backward's tree workgroup (0)")
-    ap.add_argument("--aql-draw-in-grad", type=int, default=None,
-                    help="AQL: the next step's draw in the gradient launch (1) or the update launch (0)")
-    ap.add_argument("--aql-levels-in-bwd", type=int, default=None,
-                    help="AQL: tree levels walked by the backward's workgroup before the gradient launch's")
-    ap.add_argument("--aql-fwd-halves", type=int, default=None,
-                    help="AQL: learner forward workgroups of 512 threads (2) or 256 (1)")
     ap.add_argument("--aql-overlap", action="store_true",
                     help="--algo aql: acting on its own HIP stream beside the learner steps (staged transitions)")
     ap.add_argument("--launch-timeout", type=float, default=560.0,
@@ -410,18 +398,6 @@ def aql(args, rank, world, device):
     cap = min(args.capacity, 1_000_000)
     cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed + rank,
                           actor_offset=rank * args.envs, total_actors=world * args.envs, overlap=args.aql_overlap)
-    if args.aql_bwd_tree is not None:
-        cfg.bwd_tree = bool(args.aql_bwd_tree)
-    if args.aql_fused_update is not None:
-        cfg.fused_update = bool(args.aql_fused_update)
-    if args.aql_levels_in_grad is not None:
-        cfg.tree_levels_in_grad = bool(args.aql_levels_in_grad)
-    if args.aql_draw_in_grad is not None:
-        cfg.draw_in_grad = bool(args.aql_draw_in_grad)
-    if args.aql_levels_in_bwd is not None:
-        cfg.tree_levels_in_bwd = int(args.aql_levels_in_bwd)
-    if args.aql_fwd_halves is not None:
-        cfg.fwd_halves = int(args.aql_fwd_halves)
     eng = AQLEngine(cfg, device)
     t_fill = time.perf_counter()
     eng.fill(max(1024, 4 * args.envs))
@@ -464,7 +440,8 @@ def aql(args, rank, world, device):
                        "parallelism": f"independent x{world}", "env": cfg.env_id, "envs_per_gpu": eng.E,
                        "sgd_steps_per_iteration": eng.K, "replay_capacity_per_gpu": cap,
                        "acting": ("own HIP stream beside the learner (staged transitions)" if eng.overlap
-                                  else "serial before the learner steps") + f", Q on {cfg.act_q}",
+                                  else "serial before the learner steps"),
+                       "learner_launches_per_step": 4 if eng.learner.fused else 7,
                        "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
             "actor_env_steps_per_sec": round(env_steps, 1),
             "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 check (one gpurun call): the multi-rank IPC tests first (stop-while-credit-blocked
+# Full check (one gpurun call): the multi-rank IPC tests first (stop-while-credit-blocked
 # regression), the whole GPU suite, smoke, a 1-GPU bench, the 3-rank same-device central
 # bench (preflight + links), then a kernel + HIP-runtime trace of the 1-GPU step.
 # Every GPU step has its own limit; the first failure ends the call.
@@ -29,7 +29,7 @@ timeout -k 10 400 python bench.py --gpus 3 --same-device --backend gloo --steps 
 rc=$?; step bench3_central $rc; grep '^{' gpurun_out/bench3_central.log | cut -c1-3000; tail -3 gpurun_out/bench3_central.log | cut -c1-600
 [ $rc -ne 0 ] && exit $rc
 if [ -z "$SKIP_TRACE" ]; then
-O=$R/gpurun_out/r4trace
+O=$R/gpurun_out/trace
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $O -o t \

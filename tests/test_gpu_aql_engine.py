@@ -270,46 +270,22 @@ def test_overlapped_acting_graphs_equal_eager(cuda):
         assert torch.equal(x, y)
 
 
-def test_fused_sampling_equals_per_sample(cuda):
-    """The learner forward's own PER draw (fused_sample) == per_sample + forward, the priority
-    write folded into the noise-reset launch (fused_tree) or split over the gradient and
-    noise-reset launches (split_tree) or run as an extra workgroup of the backward (bwd_tree)
-    == its own launch, the optimizers + noise + proposal copy + next draw as one launch
-    (fused_update) == the separate launches, and the whole step tail in one
-    grid-synchronised launch (fused_step: backward, tree write, gradients, both Adam steps,
-    noise reset, proposal copy) == the separate launches: same rows, IS weights, tree, loss,
-    parameters, moments, noise and target after several iterations, bit for bit."""
+def test_fused_sequence_equals_reference_sequence(cuda):
+    """The engine's four-launch step (the forward draws its own PER rows or uses the rows the
+    previous step's update launch drew; the priority write as extra workgroups of the backward
+    and gradient launches; both Adam steps + noise reset + proposal copy + next draw in one
+    update launch) == the reference sequence of separate launches (per_sample, forward,
+    backward, per_write_batch, gradients, adam_step2, noise reset): same rows, IS weights,
+    tree, loss, parameters, moments, noise and target after several iterations, eager and
+    graph-captured, bit for bit."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    # (fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update, tree_levels_in_grad)
-    variants = ((False, False, False, False, False, False, False), (True, False, False, False, False, False, False),
-                (True, True, False, False, False, False, False), (True, False, True, False, False, False, False),
-                (True, False, False, True, False, False, False), (False, False, False, True, False, False, False),
-                (True, False, False, False, True, False, False), (False, False, False, False, True, False, True),
-                (True, False, False, False, False, True, True), (False, False, False, False, False, True, True),
-                (True, False, False, False, False, True, False), (True, False, False, False, False, True, None),
-                (True, False, False, False, False, True, 2))
-    for fused_sample, fused_tree, split_tree, fused_step, bwd_tree, fused_update, lv in variants:
-        # lv None: draw in the update launch (draw_in_grad off), levels in the backward's workgroup
-        cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9,
-                              fused_sample=fused_sample, fused_tree=fused_tree, split_tree=split_tree,
-                              fused_step=fused_step, bwd_tree=bwd_tree, fused_update=fused_update,
-                              tree_levels_in_grad=bool(lv), draw_in_grad=lv is not None,
-                              tree_levels_in_bwd=2 if lv == 2 else (1 if lv else 0))
+    for fused in (False, True):
+        cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=9, fused=fused)
         eng = AQLEngine(cfg, cuda)
         L = eng.learner
-        assert (L.Ls is not None) == fused_sample
-        assert (L.S is not None) == fused_step
-        if not fused_step:
-            assert (L.post_tree is not None) == fused_tree
-            assert (L.G_tree is not None) == split_tree
-            assert (L.L_tree is not None) == (bwd_tree or fused_update)
-            assert (L.U is not None) == fused_update
-            assert L.predraw == (fused_update and fused_sample)
-            assert (L.G_levels is not None) == bool((bwd_tree or fused_update) and lv)
-        else:
-            assert L.S.grid >= max(L.nblk, L.B + 1) + 1
+        assert L.fused == fused and L.predraw == fused and (L.U is not None) == fused
         eng.fill(1024)
         for _ in range(5):
             eng.iteration()
@@ -317,7 +293,6 @@ def test_fused_sampling_equals_per_sample(cuda):
         for _ in range(3):
             eng.iteration()
         torch.cuda.synchronize()
-        L.check_fused()
         r = eng.replay
         out.append((L.idx.clone(), L.w.clone(), L.flat.clone(), L.m.clone(), L.v.clone(), L.eps.clone(),
                     L.teps.clone(), L.tflat.clone(), L.eff_on.clone(), L.eff_tg.clone(), L.loss_q.clone(),
@@ -325,21 +300,19 @@ def test_fused_sampling_equals_per_sample(cuda):
                     r.leaf_sum.clone(), r.node_sum[-1].clone(), r.max_prio.clone()))
     names = ("idx", "w", "flat", "m", "v", "eps", "teps", "tflat", "eff_on", "eff_tg", "loss_q", "loss_p", "prio",
              "norms_q", "norms_p", "step", "leaf_sum", "root", "max_prio")
-    for k, other in enumerate(out[1:], 1):
-        for name, x, y in zip(names, out[0], other):
-            assert torch.equal(x, y), (variants[k], name, (x.double() - y.double()).abs().max().item())
+    for name, x, y in zip(names, out[0], out[1]):
+        assert torch.equal(x, y), (name, (x.double() - y.double()).abs().max().item())
 
 
 def test_forward_tile_groups_bit_identical(cuda):
     """The learner forward's work split (candidate tiles per workgroup: one, a few, all of a
-    sample's; 256- or 512-thread workgroups) changes only which waves compute a tile: same Q
-    rows, same training."""
+    sample's) changes only which waves compute a tile: same Q rows, same training."""
     from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
 
     out = []
-    for groups, halves in ((0, 0), (1, 1), (3, 2), (13, 1), (13, 2), (4, 1)):
+    for groups in (0, 1, 3, 13, 4):
         cfg = AQLEngineConfig(env_id="BipedalWalker-v3", n_envs=64, capacity=8192, batch_size=32, seed=5,
-                              fwd_tile_groups=groups, fwd_halves=halves)
+                              fwd_tile_groups=groups)
         eng = AQLEngine(cfg, cuda)
         eng.fill(1024)
         for _ in range(4):
