@@ -288,6 +288,7 @@ class AQLLearner:
         r = replay
         self.fused = bool(cfg.fused) and B <= 64  # (the tree workgroups stage <= 64 dirty paths)
         self.Ls = self.L_tree = self.G_levels = self.U = self.U_draw = self.U_pub = None
+        self.U_gate = self.U_gate_draw = self._gate_ptr = None
         if self.fused:
             # the forward's own stratified draw (same seed, counter and mass as per_sample)
             self.Ls = h.aql_learn_set_sample(self.L, r.tree, r.filled.data_ptr(), self.beta.data_ptr(),
@@ -328,6 +329,19 @@ class AQLLearner:
             dict(self._step_kw, update=1, pub_p=actor_flat.data_ptr(), pub_weps0=sub(a1.weight_epsilon),
                  pub_beps0=sub(a1.bias_epsilon), pub_weps1=sub(a2.weight_epsilon), pub_beps1=sub(a2.bias_epsilon)),
             self.pub_desc.data_ptr())
+
+    def _make_gated(self, gate: torch.Tensor) -> None:
+        """Update-launch descriptors that honour the step gate ``gate``."""
+        r = self.replay
+        kw = dict(self._step_kw, gate=gate.data_ptr())
+        self._gate_ptr, self._gate_keep = gate.data_ptr(), gate
+        self.gate_desc = torch.zeros_like(self.step_desc)
+        self.U_gate = self.hip.make_aql_step(self.L, self.G, self.post, r.tree, self.hp, kw,
+                                             self.gate_desc[0].data_ptr())
+        self.U_gate_draw = self.hip.make_aql_step(
+            self.L, self.G, self.post, r.tree, self.hp,
+            dict(kw, draw=1, filled=r.filled.data_ptr(), beta=self.beta.data_ptr(), seed=r.seed ^ 0x51A7,
+                 exclude_last=0 if self.cfg.exact_mass else 1), self.gate_desc[1].data_ptr())
 
     @property
     def predraw(self) -> bool:
@@ -384,22 +398,31 @@ class AQLLearner:
     def _s() -> int:
         return torch.cuda.current_stream().cuda_stream
 
-    def step(self, drawn: bool = False, draw_next: bool = False, publish: bool = False) -> bool:
+    def step(self, drawn: bool = False, draw_next: bool = False, publish: bool = False,
+             gate: torch.Tensor | None = None, j: int = 0) -> bool:
         """One SGD step.  ``drawn``: this step's rows were drawn by the previous step's update
         launch (``draw_next`` there) -- the forward skips its tree descent (:meth:`AQLEngine.
         learn_steps` pairs them within an iteration).  ``publish``: the update launch also writes
-        the acting copies (returns whether it did)."""
+        the acting copies (returns whether it did).  ``gate`` (int32 [1], device): the step is
+        step ``j`` of its iteration and runs only if ``j < gate`` -- every launch of a gated-off
+        step returns at once (the central learner's rows-applied replay ratio)."""
         h, r, s = self.hip, self.replay, self._s()
         if drawn or draw_next:
             assert self.predraw, "pre-drawn rows need the fused sequence"
         if self.fused:
-            h.aql_learn_fwd(self.L if drawn else self.Ls, s)
-            h.aql_learn_bwd(self.L_tree, s)
-            h.aql_grad(self.G_levels, s)
-            pub = publish and not draw_next and self.U_pub is not None
-            h.aql_update(self.U_draw if draw_next else (self.U_pub if pub else self.U), s)
+            g = 0 if gate is None else gate.data_ptr()
+            if g and (self.U_gate is None or self._gate_ptr != g):
+                self._make_gated(gate)
+            U, U_draw = (self.U_gate, self.U_gate_draw) if g else (self.U, self.U_draw)
+            h.aql_learn_fwd(self.L if drawn else self.Ls, s, g, j)
+            h.aql_learn_bwd(self.L_tree, s, g, j)
+            h.aql_grad(self.G_levels, s, g, j)
+            pub = publish and not draw_next and self.U_pub is not None and not g
+            h.aql_update(U_draw if draw_next else (self.U_pub if pub else U), s, j)
             self._track_losses()
             return pub
+        if gate is not None:
+            raise ValueError("the step gate needs the fused launch sequence")
         # the reference sequence
         excl = 0 if self.cfg.exact_mass else 1
         h.per_sample(r.tree, self.B, r.filled.data_ptr(), 0, self.beta.data_ptr(), 0.0, r.seed ^ 0x51A7,
@@ -607,15 +630,16 @@ class AQLEngine:
         h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, 0, 0, s)
 
-    def learn_steps(self, publish: bool = False) -> bool:
-        """The iteration's K SGD steps; with the fused tail, each step but the last also draws the
-        next step's rows (nothing inserts between them), so only the first forward samples.
-        ``publish``: the last step also writes the acting copies (returns whether it did)."""
+    def learn_steps(self, publish: bool = False, gate: torch.Tensor | None = None) -> bool:
+        """The iteration's K SGD steps; in the fused sequence each step but the last also draws
+        the next step's rows (nothing inserts between them), so only the first forward samples.
+        ``publish``: the last step also writes the acting copies (returns whether it did).
+        ``gate``: only the first ``gate[0]`` of the K steps run (:meth:`AQLLearner.step`)."""
         pre = self.learner.predraw
         pub = False
         for k in range(self.K):
             pub = bool(self.learner.step(drawn=pre and k > 0, draw_next=pre and k + 1 < self.K,
-                                         publish=publish and k + 1 == self.K))
+                                         publish=publish and k + 1 == self.K, gate=gate, j=k))
         return pub
 
     def fill(self, threshold: int | None = None) -> None:

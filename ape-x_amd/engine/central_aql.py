@@ -9,10 +9,13 @@ SGD steps and broadcasts its weights every iteration.  Here:
 * **rank 0** = the AQL learner and the one HBM replay (:class:`AQLEngine` with no acting).
   Its captured iteration graph = IPC ingest (every ready packet of every live link, paced
   at one per link: rows appended to the replay ring in (link, packet) order at its cursor,
-  then one max-priority leaf write; ipc_kernels.hip ``ipc_apply_aql_k``) + ``K`` fused
-  learner steps (the reference replay ratio: one SGD step per ``batch_size`` transitions,
-  ``K = R * E // batch``).  After each iteration it publishes ``[weights | NoisyNet eps]``
-  conflated over the IPC parameter block and syncs the target on the reference cadence.
+  then one max-priority leaf write; ipc_kernels.hip ``ipc_apply_aql_k``) + up to ``K = R * E
+  // batch`` fused learner steps.  The ingest turns the rows it ACTUALLY applied into a
+  device step gate (carry kept): only ``(carry + rows) // batch`` of the K captured steps
+  run, the others return at once -- the reference replay ratio, ``total_ep_len // batch``
+  SGD steps per recorded batch (AQL_dis.py:117-118), however fast or slow the actors are.
+  After each iteration it publishes ``[weights | NoisyNet eps]`` conflated over the IPC
+  parameter block and syncs the target on the reference cadence.
 * **ranks 1..R** = AQL actor GPUs: E vectorised envs, on-device proposal + candidate
   critic + epsilon-greedy on the global worker ladder (actor ids ``(r-1) E ..``).  One
   actor step writes its E rows straight into the packet buffer (structure of arrays, see
@@ -53,6 +56,13 @@ class CentralAQLEngine:
             lc = copy.copy(cfg)
             # the reference replay ratio over everything the links can deliver per iteration
             lc.learner_steps = cfg.learner_steps or max(1, self.R * self.E // cfg.batch_size)
+            if cfg.target_update_steps:
+                raise ValueError("central AQL: the step gate decides the step count on the device; "
+                                 "use the iteration cadence (target_update_interval)")
+            depth_rows = self.R * depth * self.E
+            if cfg.capacity < depth_rows:
+                raise ValueError(f"central AQL: replay capacity {cfg.capacity} < links x ring depth x envs = "
+                                 f"{self.R} x {depth} x {self.E} = {depth_rows} (raise --capacity or lower --n-envs)")
             self.eng = AQLEngine(lc, self.device)
             self.cfg = lc
             self.K = self.eng.K
@@ -60,9 +70,13 @@ class CentralAQLEngine:
             self.pub = torch.zeros(L.P + L.eps.numel(), dtype=torch.float32, device=self.device)
             self._pack_params()
             self._broadcast_initial()
+            # the step gate: rows applied -> SGD steps this iteration (carry in budget)
+            self.budget = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self.gate = torch.zeros(1, dtype=torch.int32, device=self.device)
             self.links = IpcLearnerLinks.for_aql(self.R, depth, self.E, self.pub.numel(), self.eng.replay, self.store,
                                                  self.prefix, self.device, cap=1 if paced else None,
-                                                 dead_after=dead_after)
+                                                 dead_after=dead_after,
+                                                 gate=(self.budget, self.gate, cfg.batch_size, self.K))
         else:
             ac = copy.copy(cfg)
             # an actor rank keeps no replay of its own: a minimal ring, never sampled
@@ -137,8 +151,8 @@ class CentralAQLEngine:
 
     # ------------------------------------------------------------------ learner rank
     def _learner_body(self) -> None:
-        self.links.ingest()     # <= 1 packet per live link (paced) -> replay ring + max-priority leaves
-        self.eng.learn_steps()  # K fused SGD steps
+        self.links.ingest()                   # <= 1 packet per live link (paced) -> ring + leaves + gate
+        self.eng.learn_steps(gate=self.gate)  # the first gate[0] of K fused SGD steps
 
     def fill(self, timeout: float = 300.0) -> None:
         """rank 0: ingest until the replay holds more than ``threshold`` transitions
@@ -155,6 +169,7 @@ class CentralAQLEngine:
             torch.cuda.synchronize(self.device)
             self.links.check_heartbeats()
             time.sleep(0.0005)
+        self.budget.zero_()  # the warm-up rows pay for no SGD step (learning starts now)
 
     def capture(self) -> None:
         """hipGraph of the compute body (actor: one acting step into the packet; rank 0:
@@ -175,10 +190,14 @@ class CentralAQLEngine:
                 self._actor_body()
         torch.cuda.synchronize(self.device)
 
+    def sgd_steps(self) -> int:
+        """SGD steps taken so far (the device step counter; one host sync)."""
+        return int(self.eng.learner.step_ctr.item()) if self.is_learner else 0
+
     def _after_iteration(self) -> None:
         e = self.eng
         before = self.learner_steps
-        self.learner_steps += self.K
+        self.learner_steps += self.K  # (an upper bound: the gate decides on the device, see sgd_steps)
         e.learner_steps = self.learner_steps
         if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):
             e.learner.sync_target()

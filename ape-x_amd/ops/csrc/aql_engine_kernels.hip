@@ -127,6 +127,7 @@ __global__ __launch_bounds__(256 * H) void aql_learn_fwd_k(AqlLearn L) {
   __shared__ float stp[2][kH];
   __shared__ float qpart[H][4][2][16];
   __shared__ int srow;
+  if (L.gate && L.gate_j >= *L.gate) return;  // (grid-uniform) a gated-off step
   const bool tgt = blockIdx.y != 0;
   const AQLNet& N = tgt ? L.tg : L.on;
   const float* eff = tgt ? L.eff_tg : L.eff_on;
@@ -679,6 +680,7 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
 }
 
 __global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
+  if (L.gate && L.gate_j >= *L.gate) return;  // (grid-uniform) a gated-off step
   if (L.bwd_tree && blockIdx.x == L.B) {  // block-uniform: the priority write (aql_learn_set_tree)
     td_tree_block(L, L.tree, L.bw, L.bwd_tree == 1 ? 1 << 30 : L.bwd_levels);
     return;
@@ -939,6 +941,7 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
 // tree's levels levels_lo.. of this step's dirty list -- the backward launch's tree workgroup
 // wrote the leaves, the list and the lowest levels
 __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+  if (G.gate && G.gate_j >= *G.gate) return;  // (grid-uniform) a gated-off step
   const int ng = (int)gridDim.x - (G.tree_leaves ? 1 : 0);
   if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the level walk
     __shared__ int sids[64];
@@ -960,8 +963,9 @@ int aql_update_noise_blocks(const AqlStep& d) {
   return (int)((n + 255) / 256);
 }
 
-__global__ __launch_bounds__(256) void aql_update_k(const AqlStep* __restrict__ Dp, int noise_blocks) {
+__global__ __launch_bounds__(256) void aql_update_k(const AqlStep* __restrict__ Dp, int noise_blocks, int gate_j) {
   const AqlStep& D = *Dp;
+  if (D.gate && gate_j >= *D.gate) return;  // (grid-uniform) a gated-off step
   const int bid = blockIdx.x, t = threadIdx.x;
   const uint64_t st = (uint64_t)D.P.step[0];
   if (bid < D.nblk) {
@@ -1268,8 +1272,8 @@ int aql_update_grid(const AqlStep& d, int* noise_blocks) {
   return d.nblk + nb + (d.draw ? kStepDrawBlocks : 0);
 }
 
-void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s) {
-  aql_update_k<<<grid, 256, 0, s>>>(dev, noise_blocks);
+void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s, int gate_j) {
+  aql_update_k<<<grid, 256, 0, s>>>(dev, noise_blocks, gate_j);
   LAUNCH_CHECK();
 }
 

@@ -657,8 +657,17 @@ PYBIND11_MODULE(_apex_hip, m) {
     return L;
   }, py::arg("L"), py::arg("groups"), py::arg("halves") = 0);
   m.def("aql_noisy_eff", [](const AQLNet& net, uint64_t ws, uint64_t s) { aql_noisy_eff(net, P<float>(ws), S(s)); });
-  m.def("aql_learn_fwd", [](const AqlLearn& L, uint64_t s) { aql_learn_fwd(L, S(s)); });
-  m.def("aql_learn_bwd", [](const AqlLearn& L, uint64_t s) { aql_learn_bwd(L, S(s)); });
+  // gate / j: the step gate (kernels.h AqlLearn::gate) -- a by-value copy per launch
+  m.def("aql_learn_fwd", [](AqlLearn L, uint64_t s, uint64_t gate, int j) {
+    L.gate = P<const int>(gate);
+    L.gate_j = j;
+    aql_learn_fwd(L, S(s));
+  }, py::arg("L"), py::arg("s"), py::arg("gate") = 0, py::arg("j") = 0);
+  m.def("aql_learn_bwd", [](AqlLearn L, uint64_t s, uint64_t gate, int j) {
+    L.gate = P<const int>(gate);
+    L.gate_j = j;
+    aql_learn_bwd(L, S(s));
+  }, py::arg("L"), py::arg("s"), py::arg("gate") = 0, py::arg("j") = 0);
   m.def("aql_vec_layout", []() {
     py::dict d;
     d["GQ"] = aqlv::GQ; d["H"] = aqlv::H; d["GH"] = aqlv::GH; d["X"] = aqlv::X; d["GX"] = aqlv::GX;
@@ -688,7 +697,11 @@ PYBIND11_MODULE(_apex_hip, m) {
     G.lossp_out = P<float>(lossp_out);
     return G;
   });
-  m.def("aql_grad", [](const AqlGrad& G, uint64_t s) { aql_grad(G, S(s)); });
+  m.def("aql_grad", [](AqlGrad G, uint64_t s, uint64_t gate, int j) {
+    G.gate = P<const int>(gate);
+    G.gate_j = j;
+    aql_grad(G, S(s));
+  }, py::arg("G"), py::arg("s"), py::arg("gate") = 0, py::arg("j") = 0);
   m.def("aql_grad_blocks", &aql_grad_blocks);
   py::class_<AqlPost>(m, "AqlPost");
   // layers: 4 x (weps, beps, wmu, wsig, bmu, bsig, weff, beff, out, in)
@@ -746,6 +759,7 @@ PYBIND11_MODULE(_apex_hip, m) {
       d.seed = g("seed");
       d.exclude_last = p["exclude_last"].cast<int>();
     }
+    if (p.contains("gate")) d.gate = P<const int>(g("gate"));  // the step gate (aql_update's j)
     if (p.contains("pub_p")) {  // the acting copies (the iteration's last step publishes)
       d.pub_p = P<float>(g("pub_p"));
       d.pub_weps[0] = P<float>(g("pub_weps0")); d.pub_weps[1] = P<float>(g("pub_weps1"));
@@ -757,7 +771,9 @@ PYBIND11_MODULE(_apex_hip, m) {
     const int grid = aql_update_grid(d, &nb);
     return AqlStepHandle{reinterpret_cast<const AqlStep*>(desc), grid, nb, d.draw};
   });
-  m.def("aql_update", [](const AqlStepHandle& h, uint64_t s) { aql_update(h.dev, h.grid, h.noise_blocks, S(s)); });
+  m.def("aql_update", [](const AqlStepHandle& h, uint64_t s, int j) {
+    aql_update(h.dev, h.grid, h.noise_blocks, S(s), j);
+  }, py::arg("h"), py::arg("s"), py::arg("j") = 0);
   py::class_<AqlEnv>(m, "AqlEnv");
   m.def("make_aql_env", [](py::dict d) {
     auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };

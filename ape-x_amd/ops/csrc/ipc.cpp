@@ -142,6 +142,10 @@ void register_ipc(py::module_& m) {
     g.slot_base = P<const int64_t>(p("slot_base"));
     g.slots_out = P<int32_t>(p("slots_out"));
     g.prio_out = P<float>(p("prio_out"));
+    g.budget = P<int64_t>(p("budget"));
+    g.gate = P<int>(p("gate"));
+    g.gate_batch = d.contains("gate_batch") ? (int)i("gate_batch") : 0;
+    g.gate_max = d.contains("gate_max") ? (int)i("gate_max") : 0;
     return h;
   });
   m.def("ipc_ingest", [](const IpcIngestHandle& h, uint64_t s) { apex::ipc_ingest(h.g, S(s)); });

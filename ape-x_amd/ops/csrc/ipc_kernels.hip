@@ -185,6 +185,12 @@ __global__ void ipc_release_k(IpcIngest g) {
   }
   __syncthreads();
   if (threadIdx.x == 0 && g.kind == 1 && g.filled && total) g.filled[0] += (int64_t)total * g.E;
+  if (threadIdx.x == 0 && g.gate) {  // the SGD steps this ingest's rows pay for (carry kept in budget)
+    const int64_t b = g.budget[0] + (int64_t)total * g.E;
+    const int64_t n = b / g.gate_batch < (int64_t)g.gate_max ? b / g.gate_batch : (int64_t)g.gate_max;
+    g.budget[0] = b - n * g.gate_batch;
+    g.gate[0] = (int)n;
+  }
 }
 
 __global__ void ipc_flag_k(int64_t* p, int64_t v) {
@@ -215,6 +221,8 @@ void ipc_ingest(const IpcIngest& g, hipStream_t s) {
   } else {
     throw std::invalid_argument("ipc_ingest: kind must be 0 (DQN) or 1 (AQL)");
   }
+  if (g.gate && (g.kind != 1 || !g.budget || g.gate_batch < 1 || g.gate_max < 0))
+    throw std::invalid_argument("ipc_ingest: the step gate needs AQL rows, a budget, batch >= 1");
   const int thr = ((g.R + 63) / 64) * 64;
   ipc_scan_k<<<1, thr, 0, s>>>(g);
   LAUNCH_CHECK();

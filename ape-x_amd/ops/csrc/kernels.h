@@ -464,6 +464,10 @@ struct AqlLearn {
   // workgroup per CU; act_mode: 0 = one tile per item)
   int tile_groups;
   int fwd_halves;  // learner forward workgroup: 2 = 512 threads (alternate tiles per half), 1 = 256
+  // step gate (central AQL learner): this launch belongs to step gate_j of the iteration and
+  // does nothing unless gate_j < *gate (the steps the ingest's new rows paid for, IpcIngest)
+  const int* gate;
+  int gate_j;
 };
 void aql_learn_fwd(const AqlLearn& L, hipStream_t s);
 // acting on the learner's MFMA forward: q_s[b][t] = Q_on(st[b], amu[b][t]) for B states
@@ -493,6 +497,8 @@ struct AqlGrad {
   int levels_lo;
   TreeDesc tree;
   BatchWrite bw;
+  const int* gate;  // step gate (AqlLearn::gate)
+  int gate_j;
 };
 int aql_grad_blocks(int64_t n);
 void aql_grad(const AqlGrad& g, hipStream_t s);
@@ -545,10 +551,11 @@ struct AqlStep {
   float* pub_p;
   float* pub_weps[2];
   float* pub_beps[2];
+  const int* gate;  // step gate (AqlLearn::gate); the step index is aql_update's gate_j
 };
 void aql_step_check(const AqlStep& d);
 int aql_update_grid(const AqlStep& d, int* noise_blocks);
-void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s);
+void aql_update(const AqlStep* dev, int grid, int noise_blocks, hipStream_t s, int gate_j = 0);
 struct AqlEnv {
   int kind;            // 0 BipedalWalker-shaped, 1 CartPole, 2 Pendulum
   int E, obs, adim, T, max_steps;
@@ -599,6 +606,12 @@ struct IpcIngest {
   const int64_t *frame_base, *slot_base;  // [R] region offsets
   int32_t* slots_out;               // [R * cap * E] global slot or -1 (tree write input)
   float* prio_out;                  // [R * cap * E]
+  // AQL step gate (optional): the reference trains total_rows // batch SGD steps per recorded
+  // batch (AQL_dis.py:117-118) -- budget += rows applied, gate = min(gate_max, budget // batch),
+  // budget -= gate * batch; the learner's step j runs iff j < gate (AqlLearn::gate)
+  int64_t* budget;
+  int* gate;
+  int gate_batch, gate_max;
 };
 void ipc_ingest(const IpcIngest& g, hipStream_t s);
 void ipc_flag(int64_t* p, int64_t v, hipStream_t s);  // system-scope release store of v (one thread)

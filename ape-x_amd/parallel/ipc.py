@@ -283,15 +283,23 @@ class IpcLearnerLinks:
         return links
 
     @classmethod
-    def for_aql(cls, R: int, D: int, E: int, P: int, replay, store, prefix: str, device, **kw):
+    def for_aql(cls, R: int, D: int, E: int, P: int, replay, store, prefix: str, device, gate: tuple | None = None,
+                **kw):
         """AQL links (AQL_dis.py:109-126 over xGMI): packets of E raw (s, s', a_mu, a, r, d)
         rows appended to ``replay``'s ring (engine.aql.AQLReplay) at max priority
-        (CustomPrioritizedReplayBuffer_AQL.add, memory.py:368-378)."""
+        (CustomPrioritizedReplayBuffer_AQL.add, memory.py:368-378).  ``gate`` = (budget i64 [1],
+        gate i32 [1], batch, max steps): every ingest turns the rows it applied into the SGD
+        steps they pay for (kernels.h IpcIngest)."""
         rp = replay
         TA = rp.T * rp.adim
+        if rp.capacity < R * D * E:  # the drain ingests up to D packets per link into the ring
+            raise ValueError(f"AQL links: replay capacity {rp.capacity} < R x D x E = {R} x {D} x {E}")
         tables = dict(kind=1, obs=rp.obs, TA=TA, aql_st=rp.st.data_ptr(), aql_st2=rp.st2.data_ptr(),
                       aql_amu=rp.a_mu.data_ptr(), aql_act=rp.action.data_ptr(), aql_rew=rp.reward.data_ptr(),
                       aql_done=rp.done.data_ptr(), aql_C=rp.capacity, filled=rp.filled.data_ptr())
+        if gate is not None:
+            tables.update(budget=gate[0].data_ptr(), gate=gate[1].data_ptr(), gate_batch=int(gate[2]),
+                          gate_max=int(gate[3]))
         h = ops.hip()
 
         def tree_write(slots, _prios):  # every new row at the running max priority (ring order, -1 skipped)

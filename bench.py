@@ -460,9 +460,10 @@ def aql_central(args, rank, world, device, wd, pre=None):
     THE AQL learner (batch 32, AQL_dis.py:31-47) + the one replay, ranks 1.. = actor GPUs
     with ``--envs`` envs each pushing raw (s, a, r, s', d, a_mu) rows over HIP IPC
     (engine/central_aql.py; AQL_dis.py:50-53,109-126).  One rank-0 iteration = ingest (<= one
-    packet per actor) + K = (N-1) * envs / 32 SGD steps (the reference replay ratio) + a
-    weight publish.  ``value`` = learner SGD steps/s; actor env steps/s = rows that reached
-    the replay during the timed window."""
+    packet per actor) + the SGD steps its rows pay for (at most K = (N-1) * envs / 32: the
+    reference replay ratio, one step per 32 recorded transitions) + a weight publish.  ``value`` = learner SGD steps/s (the device step counter: the ingest's
+    step gate runs only the steps the applied rows pay for); actor env steps/s = rows that
+    reached the replay during the timed window."""
     import torch
     import torch.distributed as dist
 
@@ -494,14 +495,15 @@ def aql_central(args, rank, world, device, wd, pre=None):
     torch.cuda.synchronize(device)
     wd.kick()
     a0 = sum(eng.applied.values())
-    s0 = eng.learner_steps
+    s0 = eng.sgd_steps()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.iteration()
     torch.cuda.synchronize(device)
     dt = time.perf_counter() - t0
     packets = sum(eng.applied.values()) - a0
-    sgd = (eng.learner_steps - s0) / dt
+    n_sgd = eng.sgd_steps() - s0
+    sgd = n_sgd / dt
     wd.kick()
     st = eng.eng.learner.stats()
     links = eng.close()
@@ -521,6 +523,9 @@ def aql_central(args, rank, world, device, wd, pre=None):
                    "replay_capacity": cap, "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
         "actor_env_steps_per_sec": round(packets * eng.E / dt, 1),
         "packets_applied_per_iteration": round(packets / args.steps, 3),
+        # the reference replay ratio is one SGD step per `batch` recorded transitions
+        # (AQL_dis.py:117-118); the device step gate holds it whatever the actors' pace
+        "sgd_steps_per_transition_x_batch": round(n_sgd * cfg.batch_size / max(1, packets * eng.E), 4),
         "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
         "links_complete": all(links["applied"][r] == links["sent"][r] for r in links["live"]),

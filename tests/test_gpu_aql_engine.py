@@ -304,6 +304,37 @@ def test_fused_sequence_equals_reference_sequence(cuda):
         assert torch.equal(x, y), (name, (x.double() - y.double()).abs().max().item())
 
 
+def test_step_gate_runs_only_the_paid_steps(cuda):
+    """The device step gate (the central learner's rows-applied replay ratio): K = 4 captured
+    steps with gate = 2 train exactly like K = 2 ungated steps -- the gated-off steps' launches
+    change nothing (parameters, moments, tree, step counter), eager and graph-captured."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    def run(K, n):
+        cfg = AQLEngineConfig(env_id="CartPole-v0", n_envs=64, capacity=8192, batch_size=32, seed=3, learner_steps=K)
+        eng = AQLEngine(cfg, cuda)
+        eng.fill(1024)
+        gate = None if n is None else torch.full((1,), n, dtype=torch.int32, device=cuda)
+        for _ in range(3):
+            eng.actor_step()
+            eng.learn_steps(gate=gate)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            eng.learn_steps(gate=gate)
+        for _ in range(2):
+            eng.actor_step()
+            g.replay()
+        torch.cuda.synchronize()
+        L = eng.learner
+        return (L.flat.clone(), L.m.clone(), L.v.clone(), L.eps.clone(), eng.replay.leaf_sum.clone(),
+                L.step_ctr.clone())
+
+    a, b = run(4, 2), run(2, None)
+    assert int(a[-1].item()) == 5 * 2
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_forward_tile_groups_bit_identical(cuda):
     """The learner forward's work split (candidate tiles per workgroup: one, a few, all of a
     sample's) changes only which waves compute a tile: same Q rows, same training."""

@@ -1,8 +1,9 @@
 """Distributed AQL_dis over HIP IPC (engine/central_aql.py) on ONE MI355X: rank 0 = the AQL
 learner + replay, ranks 1..2 = actor GPUs (here: processes on the same device, gloo control
 plane).  Every transition an actor pushed must be in rank 0's replay ring exactly once, at
-max priority, and the learner must have trained on them (BASELINE config 4; reference
-AQL_dis.py:109-126, batchrecoder_AQL.py:109-132)."""
+max priority, and the learner must have trained on them -- exactly one SGD step per 32 rows
+that reached the replay (the device step gate; reference AQL_dis.py:109-126,117-118,
+batchrecoder_AQL.py:109-132)."""
 import pytest
 import torch
 
@@ -36,10 +37,12 @@ def _central_aql_body(rank, world, iters):
         dist.send(allp, 0)
         return {"steps": eng.actor_steps, "sent": eng.link.n_sent, "version": eng.param_version}
     eng.fill()
+    a0, s0 = sum(eng.applied.values()), eng.sgd_steps()
     eng.capture()
     for _ in range(iters):
         eng.iteration()
     torch.cuda.synchronize(dev)
+    a1, s1 = sum(eng.applied.values()), eng.sgd_steps()
     st = eng.eng.learner.stats()
     links = eng.close()
     rp = eng.eng.replay
@@ -71,7 +74,7 @@ def _central_aql_body(rank, world, iters):
     live_leaves = int((rp.leaf_sum[:n] > 0).sum().item())
     return {"links": links, "filled": n, "want_rows": want.shape[0], "same_rows": key(have) == key(want),
             "live_leaves": live_leaves, "learner_steps": eng.learner_steps, "K": eng.K,
-            "loss_q": st["loss_q"], "sgd_steps": st["steps"]}
+            "loss_q": st["loss_q"], "sgd_steps": st["steps"], "gate_packets": a1 - a0, "gate_steps": s1 - s0}
 
 
 def test_central_aql_every_transition_reaches_the_learner(cuda):
@@ -86,5 +89,7 @@ def test_central_aql_every_transition_reaches_the_learner(cuda):
     assert o["filled"] == 64 * (L["applied"][1] + L["applied"][2]) == o["want_rows"]
     assert o["same_rows"], "rank 0's replay rows differ from what the actors pushed"
     assert o["live_leaves"] == o["filled"]  # every row inserted at (max) priority
-    assert o["K"] == 2 * 64 // 32 and o["learner_steps"] >= 30 * o["K"] and o["sgd_steps"] >= o["learner_steps"]
+    assert o["K"] == 2 * 64 // 32
+    # the replay ratio: one SGD step per 32 rows that reached the replay (64-row packets: 2 each)
+    assert o["gate_packets"] >= 30 and o["gate_steps"] == 2 * o["gate_packets"]
     assert o["loss_q"] == o["loss_q"]
