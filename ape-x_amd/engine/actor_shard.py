@@ -105,11 +105,14 @@ class ActorShard:
         draw as ``select_actions``); then call :meth:`act_and_step` with ``selected=True``."""
         return (self.eps.data_ptr(), self.seed ^ 0x5E1EC7, self.step_counter.data_ptr(), self.actions.data_ptr())
 
-    def act_and_step(self, q: torch.Tensor | None = None, parity: int | None = None, selected: bool = False) -> None:
+    def act_and_step(self, q: torch.Tensor | None = None, parity: int | None = None, selected: bool = False,
+                     tree: bool = True) -> None:
         """Given Q for the current observations (in ``self.q`` or ``q``), act, step the
         envs and push the emitted transitions into the replay (staged mode: into staging
         set ``parity``; :meth:`apply_staged` moves them into the replay).  ``selected``:
-        ``self.actions`` already holds this step's eps-greedy actions (see :meth:`act_args`)."""
+        ``self.actions`` already holds this step's eps-greedy actions (see :meth:`act_args`).
+        ``tree=False``: rows only, no priority-tree write (a central actor rank's local mirror:
+        the priorities travel in its packet to rank 0's tree)."""
         if q is not None and q.data_ptr() != self.q.data_ptr():
             self.q.copy_(q)
         s = self._stream()
@@ -129,8 +132,9 @@ class ActorShard:
             return  # the kernel advanced step_counter
         h.nstep_emit(self.nstep, self.q.data_ptr(), self.actions.data_ptr(), self.reward.data_ptr(),
                      self.done.data_ptr(), self.new_frame.data_ptr(), self.step_counter.data_ptr(),
-                     self.slot.data_ptr(), self.prio.data_ptr(), s)
-        self.replay.write_batch(pre=(self.slot, self.prio, self.replay.filled), bump=self.step_counter)
+                     self.slot.data_ptr(), self.prio.data_ptr(), s, not tree)  # (no tree: the kernel bumps)
+        if tree:
+            self.replay.write_batch(pre=(self.slot, self.prio, self.replay.filled), bump=self.step_counter)
 
     def apply_staged(self, parity: int) -> None:
         """Scatter staging set ``parity`` into the replay tables and write its

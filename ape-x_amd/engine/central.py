@@ -32,19 +32,67 @@ from __future__ import annotations
 
 import dataclasses
 import time
+from types import SimpleNamespace
+
 import torch
 import torch.distributed as dist
 
 from ..models.dqn import DuelingDQN
 from ..models.fused import make_hip_net, make_workspace
+from .. import ops
 from ..parallel.experience import (META_COLS, STOP, ActorLink, Dropped, LearnerLinks, Region, apply_packets,
-                                   engine_nonce, link_groups, pack_meta)
+                                   engine_nonce, link_groups)
 from ..parallel.ipc import IpcActorLink, IpcLearnerLinks, packet_bytes
 from ..roles.common import maybe_fault
 from .actor_shard import ActorShard
 from .apex import EngineConfig
 from .hbm_replay import FRAME_BYTES, HBMReplay
 from .learner import DQNLearner
+
+
+def stage_packet(hip, replay: HBMReplay, actor: ActorShard, packet: torch.Tensor, E: int, initial: bool = False):
+    """ipc_stage_dqn over an actor shard's local replay mirror into ``packet`` (current stream)."""
+    rp, a = replay, actor
+    d = dict(frames=rp.frames.data_ptr(), new_frame=a.new_frame.data_ptr(), packet=packet.data_ptr(), E=E,
+             initial=int(initial))
+    if initial:
+        d.update(hist=a.st["hist"].data_ptr(), actions=a.actions.data_ptr())
+    else:
+        d.update(s_ids=rp.s_ids.data_ptr(), s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(),
+                 reward=rp.reward.data_ptr(), done=rp.done.data_ptr(), slot=a.slot.data_ptr(), prio=a.prio.data_ptr())
+    hip.ipc_stage_dqn(d, torch.cuda.current_stream().cuda_stream)
+
+
+def build_actor_rank(cfg: EngineConfig, device, rank: int, R: int, C_r: int, F_r: int,
+                     model: DuelingDQN | None = None) -> SimpleNamespace:
+    """An actor GPU's state (central topology rank ``rank`` of R actor ranks): the local
+    replay mirror of its region (frame ring + transition rows, no sampling), the
+    :class:`ActorShard` on the global epsilon ladder, the acting network (packed HIP copy of
+    ``model``) and its workspace."""
+    lc, E = cfg.learner, cfg.n_envs
+    replay = HBMReplay(C_r, E, lc.n_step, cfg.alpha, device, frame_capacity=F_r, exact_mass=cfg.exact_mass,
+                       seed=cfg.seed + rank)
+    actor = ActorShard(replay, E, cfg.n_actions, lc.n_step, lc.gamma, cfg.eps_base, cfg.eps_alpha,
+                       actor_offset=(rank - 1) * E, total_actors=R * E, seed=cfg.seed + 7919 * rank,
+                       mode=cfg.nstep_mode)
+    model = (model if model is not None else DuelingDQN.from_shapes((4, 84, 84), cfg.n_actions)).to(device)
+    flat = model.flatten_parameters()
+    for p in model.parameters():
+        p.requires_grad_(False)
+    net = make_hip_net(model, lc.dtype)
+    ws = make_workspace(E, cfg.n_actions, device, lc.dtype)
+    ws.q = actor.q  # the heads kernel writes Q (and picks the actions) in place
+    return SimpleNamespace(replay=replay, actor=actor, model=model, flat=flat, net=net, ws=ws, E=E)
+
+
+def actor_rank_step(hip, a, packet: torch.Tensor) -> None:
+    """One actor step of an actor rank's E envs into its packet (``a``: :func:`build_actor_rank`
+    fields): the forward (conv1 reads the stacks from the local frame ring; the heads kernel
+    writes Q and picks the eps-greedy actions), env step + n-step rows into the local mirror
+    (no local tree: the priorities travel with the rows), then the one staging launch."""
+    a.net(a.replay.frames, a.ws, a.actor.st["hist"], act=a.actor.act_args())
+    a.actor.act_and_step(None, selected=True, tree=False)
+    stage_packet(hip, a.replay, a.actor, packet, a.E)
 
 
 def region_geometry(cfg: EngineConfig, n_actor_ranks: int) -> tuple[int, int]:
@@ -58,14 +106,24 @@ def region_geometry(cfg: EngineConfig, n_actor_ranks: int) -> tuple[int, int]:
 class CentralApexEngine:
     def __init__(self, cfg: EngineConfig, device, rank: int | None = None, world: int | None = None,
                  depth: int = 3, dead_after: float = 30.0, heartbeat_every: float = 0.5, paced: bool = True,
-                 transport: str = "auto"):
+                 transport: str = "auto", emulate_links: int = 0):
         """``transport``: "ipc" (HIP IPC rings in rank 0's HBM, parallel/ipc.py; the default on
         GPUs), "p2p" (torch.distributed isend/irecv links, parallel/experience.py; CPU tests and
-        the host-staged gloo rehearsal) or "auto"."""
+        the host-staged gloo rehearsal) or "auto".  ``emulate_links`` = R > 0: THIS process is
+        rank 0 of a virtual world of R + 1 whose R actor links are emulated in-process
+        (parallel.ipc.EmulatedActorLinks: synthetic packets written into the real IPC ring,
+        ingested by the real in-graph ingest) -- the central learner's load at N = R + 1 GPUs,
+        measured on one."""
         self.cfg = cfg
+        self.hip = ops.hip()
         self.device = torch.device(device)
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
+        self.emu = None
+        if emulate_links:
+            if dist.get_world_size() != 1 or transport not in ("ipc", "auto"):
+                raise ValueError("emulate_links: one process (a world-1 process group) over the IPC transport")
+            self.rank, self.world = 0, int(emulate_links) + 1
         if self.world < 2:
             raise ValueError("the central topology needs >= 2 ranks (rank 0 learner, ranks 1.. actors)")
         self.R = self.world - 1
@@ -108,27 +166,31 @@ class CentralApexEngine:
             self.tables = {"frames": rp.frames, "s_ids": rp.s_ids, "s2_ids": rp.s2_ids, "action": rp.action,
                            "reward": rp.reward, "done": rp.done}
         else:
-            self.replay = HBMReplay(self.C_r, E, lc.n_step, cfg.alpha, self.device, frame_capacity=self.F_r,
-                                    exact_mass=cfg.exact_mass, seed=cfg.seed + self.rank)
-            self.actor = ActorShard(self.replay, E, cfg.n_actions, lc.n_step, lc.gamma, cfg.eps_base, cfg.eps_alpha,
-                                    actor_offset=(self.rank - 1) * E, total_actors=self.R * E,
-                                    seed=cfg.seed + 7919 * self.rank, mode=cfg.nstep_mode)
-            model = model.to(self.device)
-            self.flat = model.flatten_parameters()
-            for p in model.parameters():
-                p.requires_grad_(False)
-            self.model = model
-            self.net = make_hip_net(model, cfg.learner.dtype)
-            self.ws = make_workspace(E, cfg.n_actions, self.device, cfg.learner.dtype)
+            a = build_actor_rank(cfg, self.device, self.rank, self.R, self.C_r, self.F_r, model)
+            self.replay, self.actor, self.model, self.flat, self.net, self.ws = (a.replay, a.actor, a.model, a.flat,
+                                                                                 a.net, a.ws)
         self._initial_params()
         if self.is_learner:
             self._setup_learner_links(dead_after)
+            if emulate_links:
+                from ..parallel.ipc import EmulatedActorLinks
+
+                self.emu = EmulatedActorLinks(self.links, self.C_r, self.F_r, cfg.n_actions, seed=cfg.seed)
+                self._estream = torch.cuda.Stream(device=self.device)
         else:
             self._setup_actor_link()
 
     # ------------------------------------------------------------------ setup
+    def _emu_push(self) -> None:
+        """Emulated links: every link's next paced packet, on the emulators' own stream."""
+        if self.emu is not None:
+            with torch.cuda.stream(self._estream):
+                self.emu.push()
+
     def _initial_params(self) -> None:
         """Identical weights everywhere before the links start (one collective broadcast)."""
+        if dist.get_world_size() == 1:
+            return
         if dist.get_backend() != "nccl":
             h = self.flat.cpu()
             dist.broadcast(h, src=0)
@@ -160,22 +222,20 @@ class CentralApexEngine:
         self._sel_k = 0
 
     def _setup_actor_link(self) -> None:
+        # one contiguous packet (E frames | E x 14 meta) that ONE staging launch fills per actor step
+        E, FB = self.E, FRAME_BYTES
+        self.pkt = torch.empty(packet_bytes(E), dtype=torch.uint8, device=self.device)
+        self.pkt_frames = self.pkt[:E * FB].view(E, FB)
+        self.pkt_meta = self.pkt[E * FB:].view(torch.int32).view(E, META_COLS)
+        self.param_version = 0
         if self.transport == "ipc":
-            E, FB = self.E, FRAME_BYTES
-            self.pkt = torch.empty(packet_bytes(E), dtype=torch.uint8, device=self.device)
-            self.pkt_frames = self.pkt[:E * FB].view(E, FB)
-            self.pkt_meta = self.pkt[E * FB:].view(torch.int32).view(E, META_COLS)
             self.link = IpcActorLink(self.rank, self.store, self.prefix, self.flat, self.pkt, self.device,
                                      self.heartbeat_every)
-            self.param_version = 0
             self._stage_packet(initial=True)  # the reset frames are the first packet
             self.link.push()
             return
         self.link = ActorLink(self.rank, self.groups[self.rank], self.store, self.flat, self.E, FRAME_BYTES,
                               self.depth, self.heartbeat_every, prefix=self.prefix)
-        self.pkt_frames = torch.empty(self.E, FRAME_BYTES, dtype=torch.uint8, device=self.device)
-        self.pkt_meta = torch.empty(self.E, META_COLS, dtype=torch.int32, device=self.device)
-        self.param_version = 0
         self._stage_packet(initial=True)  # the reset frames are the first packet
         self.link.push(self.pkt_frames, self.pkt_meta)
 
@@ -198,22 +258,15 @@ class CentralApexEngine:
 
     # ------------------------------------------------------------------ actor ranks
     def _stage_packet(self, initial: bool = False) -> None:
+        """The actor step's packet in ONE launch (ipc_kernels.hip ipc_stage_dqn_k): the E new
+        frames out of the local frame ring + the E rows the n-step kernel just wrote into the
+        local mirror (make_batch of memory.py:466-469, actor.py:105-115).  ``initial``: the
+        reset frames only, every row a filler (slot -1: no transition row is written)."""
         a, rp = self.actor, self.replay
-        if initial:  # reset frames only: every row is a filler (slot -1: no transition row is written)
-            z = torch.zeros(self.E, dtype=torch.float32, device=self.device)
-            slot = torch.full((self.E,), -1, dtype=torch.int32, device=self.device)
-            pack_meta(a.st["hist"], a.st["hist"], a.actions, z, z, z, slot, a.new_frame, out=self.pkt_meta)
-        else:
-            sl = a.slot.long()
-            pack_meta(rp.s_ids.index_select(0, sl), rp.s2_ids.index_select(0, sl), rp.action.index_select(0, sl),
-                      rp.reward.index_select(0, sl), rp.done.index_select(0, sl), a.prio, a.slot, a.new_frame,
-                      out=self.pkt_meta)
-        torch.index_select(rp.frames, 0, a.new_frame.long(), out=self.pkt_frames)
+        stage_packet(self.hip, rp, a, self.pkt, self.E, initial)
 
     def _actor_body(self) -> None:
-        q = self.net(self.replay.frames, self.ws, self.actor.st["hist"])
-        self.actor.act_and_step(q)
-        self._stage_packet()
+        actor_rank_step(self.hip, self, self.pkt)
 
     def actor_step(self) -> bool:
         """One actor step + push; False once the learner has stopped or dropped this actor."""
@@ -276,7 +329,10 @@ class CentralApexEngine:
         meta = self.rx_meta.view(self.R * D, E, META_COLS).index_select(0, idx)
         slots, prio = apply_packets(self.tables, frames, meta, self._fbase.index_select(0, idx),
                                     self._sbase.index_select(0, idx))
-        self.replay.write_priorities(slots, prio, dedup=False, bumps=((self.replay.filled, len(ready) * E),))
+        # the fill counter advances by the real transition rows (filler rows, e.g. the
+        # reset-frame packet's, carry frames only -- as the IPC ingest counts them)
+        self.replay.filled.add_((slots >= 0).sum())
+        self.replay.write_priorities(slots, prio, dedup=False)
 
     def ingest(self, cap: int | None = None) -> int:
         if self.transport == "ipc":  # device-side (normally captured in the learner graph)
@@ -313,6 +369,8 @@ class CentralApexEngine:
         """Stop every live actor and drain its link (bounded).  Returns link stats."""
         if not self.is_learner:
             return {}
+        if self.emu is not None:
+            self.emu.finish()
         st = self.links.close(timeout)
         torch.cuda.synchronize(self.device)
         return st
@@ -326,10 +384,13 @@ class CentralApexEngine:
         need = -(-self.cfg.threshold_size // self.E)
         deadline = time.monotonic() + timeout
         if self.transport == "ipc":
-            while sum(self.applied.values()) < need + len(self.live):
+            # (+ every real actor's reset-frame packet; emulated links send none)
+            while sum(self.applied.values()) < need + (0 if self.emu is not None else len(self.live)):
                 if not self.live or time.monotonic() > deadline:
                     raise RuntimeError(f"central fill: {sum(self.applied.values())} packets after {timeout}s, "
                                        f"live actors {sorted(self.live)}")
+                self._emu_push()
+                torch.cuda.synchronize(self.device)
                 self.links.ingest(drain=True)
                 torch.cuda.synchronize(self.device)
                 self.links.check_heartbeats()
@@ -347,6 +408,7 @@ class CentralApexEngine:
         """hipGraphs of the compute bodies (the links stay eager around them)."""
         pool = torch.cuda.graph_pool_handle()
         if self.is_learner:
+            self._emu_push()
             self._learner_body()  # eager warm-up (a real step)
             self.learn_steps += 1
             torch.cuda.synchronize(self.device)
@@ -370,6 +432,7 @@ class CentralApexEngine:
                 if not self.actor_step():
                     return False
             return True
+        self._emu_push()
         self.learner_step()
         if self.transport == "p2p":
             self.ingest(self.ingest_cap)

@@ -150,4 +150,42 @@ void register_ipc(py::module_& m) {
   });
   m.def("ipc_ingest", [](const IpcIngestHandle& h, uint64_t s) { apex::ipc_ingest(h.g, S(s)); });
   m.def("ipc_flag", [](uint64_t p, int64_t v, uint64_t s) { apex::ipc_flag(P<int64_t>(p), v, S(s)); });
+  m.def("ipc_stage_dqn", [](py::dict d, uint64_t s) {
+    auto p = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
+    apex::IpcStage st{};
+    st.frames = P<const uint8_t>(p("frames"));
+    st.new_frame = P<const int32_t>(p("new_frame"));
+    st.s_ids = P<const int32_t>(p("s_ids"));
+    st.s2_ids = P<const int32_t>(p("s2_ids"));
+    st.action = P<const int32_t>(p("action"));
+    st.reward = P<const float>(p("reward"));
+    st.done = P<const float>(p("done"));
+    st.slot = P<const int32_t>(p("slot"));
+    st.prio = P<const float>(p("prio"));
+    st.hist = P<const int32_t>(p("hist"));
+    st.actions = P<const int32_t>(p("actions"));
+    st.packet = P<uint8_t>(p("packet"));
+    st.E = d["E"].cast<int>();
+    st.initial = d.contains("initial") ? d["initial"].cast<int>() : 0;
+    apex::ipc_stage_dqn(st, S(s));
+  });
+  py::class_<apex::IpcEmu>(m, "IpcEmu");
+  m.def("make_ipc_emu", [](py::dict d) {
+    auto p = [&](const char* k) { return d[k].cast<uint64_t>(); };
+    auto i = [&](const char* k) { return d[k].cast<int64_t>(); };
+    apex::IpcEmu g{};
+    g.ring = P<uint8_t>(p("ring"));
+    g.seq = P<int64_t>(p("seq"));
+    g.consumed = P<const int64_t>(p("consumed"));
+    g.sent = P<int64_t>(p("sent"));
+    g.go = P<int32_t>(p("go"));
+    g.pool = P<const uint8_t>(p("pool"));
+    g.pool_n = (int)i("pool_n");
+    g.R = (int)i("R"); g.D = (int)i("D"); g.E = (int)i("E");
+    g.C_r = (int)i("C_r"); g.F_r = (int)i("F_r"); g.n_actions = (int)i("n_actions");
+    g.pkt = i("pkt");
+    g.seed = p("seed");
+    return g;
+  });
+  m.def("ipc_emu_push", [](const apex::IpcEmu& g, uint64_t s) { apex::ipc_emu_push(g, S(s)); });
 }

@@ -193,6 +193,85 @@ __global__ void ipc_release_k(IpcIngest g) {
   }
 }
 
+// one workgroup per env row: its new frame (441 x 16 B) and its 14 metadata words
+__global__ __launch_bounds__(128) void ipc_stage_dqn_k(IpcStage st) {
+  const int e = blockIdx.x, t = threadIdx.x;
+  const int32_t nf = st.new_frame[e];
+  const uint4* src = reinterpret_cast<const uint4*>(st.frames + (int64_t)nf * kFrameBytes);
+  uint4* dst = reinterpret_cast<uint4*>(st.packet + (int64_t)e * kFrameBytes);
+  for (int w = t; w < kFrameVec; w += 128) dst[w] = src[w];
+  if (t >= kMetaCols) return;
+  int32_t* m = reinterpret_cast<int32_t*>(st.packet + (int64_t)st.E * kFrameBytes) + e * kMetaCols;
+  int32_t v = 0;
+  if (st.initial) {
+    if (t < 8) v = st.hist[e * 4 + (t & 3)];
+    else if (t == 8) v = st.actions[e];
+    else if (t == 12) v = -1;
+    else if (t == 13) v = nf;
+  } else {
+    const int32_t j = st.slot[e];
+    if (t == 12) v = j;
+    else if (t == 13) v = nf;
+    else if (t == 11) v = __float_as_int(st.prio[e]);
+    else if (j >= 0) {
+      if (t < 4) v = st.s_ids[j * 4 + t];
+      else if (t < 8) v = st.s2_ids[j * 4 + t - 4];
+      else if (t == 8) v = st.action[j];
+      else if (t == 9) v = __float_as_int(st.reward[j]);
+      else v = __float_as_int(st.done[j]);
+    }
+  }
+  m[t] = v;
+}
+
+// --- link emulation (IpcEmu): decide per link, write the packets, then publish them
+__global__ void ipc_emu_decide_k(IpcEmu g) {
+  const int r = threadIdx.x;
+  if (r < g.R) g.go[r] = g.sent[r] - __hip_atomic_load(g.consumed + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g.D;
+}
+
+__device__ __forceinline__ uint32_t emu_hash(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// grid R * E blocks of 128 threads: (link r, env e)
+__global__ __launch_bounds__(128) void ipc_emu_write_k(IpcEmu g) {
+  const int r = blockIdx.x / g.E, e = blockIdx.x % g.E, t = threadIdx.x;
+  if (!g.go[r]) return;
+  const int64_t n = g.sent[r];
+  uint8_t* pkt = g.ring + ((int64_t)r * g.D + n % g.D) * g.pkt;
+  const int64_t q = n * g.E + e;
+  const uint4* src = reinterpret_cast<const uint4*>(g.pool + (q % g.pool_n) * kFrameBytes);
+  uint4* dst = reinterpret_cast<uint4*>(pkt + (int64_t)e * kFrameBytes);
+  for (int w = t; w < kFrameVec; w += 128) dst[w] = src[w];
+  if (t >= kMetaCols) return;
+  const int32_t fs = (int32_t)(q % g.F_r), ls = (int32_t)(q % g.C_r);
+  const uint32_t h = emu_hash(g.seed ^ ((uint64_t)r << 40) ^ (uint64_t)q);
+  int32_t v;
+  if (t < 4) v = (int32_t)((q + g.F_r - 4 + t) % g.F_r);          // the stack ending before the new frame
+  else if (t < 8) v = (int32_t)((q + g.F_r - 4 + (t - 4) + 3) % g.F_r);  // n-step later (any frames in the region)
+  else if (t == 8) v = (int32_t)(h % (uint32_t)g.n_actions);
+  else if (t == 9) v = __float_as_int((float)((int)(h >> 8) % 3 - 1));
+  else if (t == 10) v = __float_as_int((h >> 4) % 100 == 0 ? 1.f : 0.f);
+  else if (t == 11) v = __float_as_int(0.05f + (float)(h >> 12) * (1.f / 1048576.f));
+  else if (t == 12) v = ls;
+  else v = fs;
+  reinterpret_cast<int32_t*>(pkt + (int64_t)g.E * kFrameBytes)[e * kMetaCols + t] = v;
+}
+
+__global__ void ipc_emu_publish_k(IpcEmu g) {
+  const int r = threadIdx.x;
+  if (r >= g.R || !g.go[r]) return;
+  const int64_t n = g.sent[r];
+  store_release_sys(g.seq + (int64_t)r * g.D + n % g.D, n + 1);  // after the packet (kernel boundary)
+  g.sent[r] = n + 1;
+}
+
 __global__ void ipc_flag_k(int64_t* p, int64_t v) {
   if (threadIdx.x == 0 && blockIdx.x == 0) store_release_sys(p, v);
 }
@@ -230,6 +309,29 @@ void ipc_ingest(const IpcIngest& g, hipStream_t s) {
   else ipc_apply_aql_k<<<g.R * g.cap * (g.E / kAqlRows), 256, 0, s>>>(g);
   LAUNCH_CHECK();
   ipc_release_k<<<1, thr, 0, s>>>(g);
+  LAUNCH_CHECK();
+}
+
+void ipc_stage_dqn(const IpcStage& st, hipStream_t s) {
+  if (st.E < 1 || !st.frames || !st.new_frame || !st.packet) throw std::invalid_argument("ipc_stage_dqn: frames");
+  if (st.initial ? (!st.hist || !st.actions)
+                 : (!st.s_ids || !st.s2_ids || !st.action || !st.reward || !st.done || !st.slot || !st.prio))
+    throw std::invalid_argument("ipc_stage_dqn: row sources");
+  ipc_stage_dqn_k<<<st.E, 128, 0, s>>>(st);
+  LAUNCH_CHECK();
+}
+
+void ipc_emu_push(const IpcEmu& g, hipStream_t s) {
+  if (g.R < 1 || g.R > 1024 || g.D < 1 || g.E < 1 || g.C_r < g.E || g.F_r < g.C_r || g.pool_n < 1 || g.n_actions < 1 ||
+      g.pkt < (int64_t)g.E * (kFrameBytes + kMetaCols * 4))
+    throw std::invalid_argument("ipc_emu_push: geometry");
+  if (!g.ring || !g.seq || !g.consumed || !g.sent || !g.go || !g.pool) throw std::invalid_argument("ipc_emu_push: null");
+  const int thr = ((g.R + 63) / 64) * 64;
+  ipc_emu_decide_k<<<1, thr, 0, s>>>(g);
+  LAUNCH_CHECK();
+  ipc_emu_write_k<<<g.R * g.E, 128, 0, s>>>(g);
+  LAUNCH_CHECK();
+  ipc_emu_publish_k<<<1, thr, 0, s>>>(g);
   LAUNCH_CHECK();
 }
 

@@ -614,6 +614,41 @@ struct IpcIngest {
   int gate_batch, gate_max;
 };
 void ipc_ingest(const IpcIngest& g, hipStream_t s);
+// An actor rank's packet for one actor step (Ape-X DQN, ONE launch): E new frames copied out of
+// the local frame ring + E metadata rows gathered from the local mirror's transition tables at
+// the rows' slots (kMetaCols = 14: s_ids 4 | s2_ids 4 | action | reward | done | priority | slot
+// | new-frame slot).  initial = 1: the reset-frame packet (rows from `hist` / `actions`, slot -1).
+struct IpcStage {
+  const uint8_t* frames;            // local frame ring [F][7056]
+  const int32_t* new_frame;         // [E] local frame slot of each env's new frame
+  const int32_t *s_ids, *s2_ids;    // local mirror tables [C][4]
+  const int32_t* action;            // [C]
+  const float *reward, *done;       // [C]
+  const int32_t* slot;              // [E] local transition slot of each env's row (-1: none)
+  const float* prio;                // [E] actor priority
+  const int32_t* hist;              // initial: [E][4] current stacks (both s and s')
+  const int32_t* actions;           // initial: [E]
+  uint8_t* packet;                  // E frames | E x 14 meta
+  int E, initial;
+};
+void ipc_stage_dqn(const IpcStage& st, hipStream_t s);
+// In-process emulation of R actor links (bench.py --emulate-links): every call pushes one
+// synthetic packet per link whose credit window (D) allows it, straight into the learner's ring
+// slot (the bytes an actor's xGMI peer copy would land), then stores the slot's sequence word --
+// the same release protocol the ingest acquires.  Packet n of link r: frames from a pool,
+// rows at local slots (n E + e) mod C_r with frame ids inside the link's region.
+struct IpcEmu {
+  uint8_t* ring;                    // [R][D] packet slots (stride pkt)
+  int64_t* seq;                     // [R][D]
+  const int64_t* consumed;          // [R] the ingest's device counters (credit)
+  int64_t* sent;                    // [R] packets pushed (device)
+  int32_t* go;                      // [R] scratch: this call's decision per link
+  const uint8_t* pool;              // [pool_n][7056] frame pool
+  int pool_n, R, D, E, C_r, F_r, n_actions;
+  int64_t pkt;                      // ring slot stride
+  uint64_t seed;
+};
+void ipc_emu_push(const IpcEmu& e, hipStream_t s);
 void ipc_flag(int64_t* p, int64_t v, hipStream_t s);  // system-scope release store of v (one thread)
 
 }  // namespace apex

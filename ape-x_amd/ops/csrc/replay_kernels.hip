@@ -355,7 +355,8 @@ __global__ __launch_bounds__(256) void per_batch_level_k(TreeDesc t, const int* 
 void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStream_t s) {
   const int n = w.E + w.B;
   if (n <= 0) return;
-  if (w.B > 1024 || w.E > 1024) throw std::invalid_argument("per_write_batch: E, B must be <= 1024");
+  // (the leaves workgroup stages E + B slots in LDS; its learner rows are one per thread)
+  if (w.B > 1024 || w.E + w.B > 2048) throw std::invalid_argument("per_write_batch: B <= 1024, E + B <= 2048");
   if (w.B > 0 && !w.idx) throw std::invalid_argument("per_write_batch: learner slots missing");
   if (w.E > 0 && (!w.pre_idx || !w.pre_prio)) throw std::invalid_argument("per_write_batch: actor rows missing");
   if (w.mix.delta && !w.mix.lw) throw std::invalid_argument("per_write_batch: mixing needs lw");

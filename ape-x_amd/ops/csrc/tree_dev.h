@@ -320,10 +320,14 @@ __device__ __forceinline__ void update_levels_fast(const TreeDesc& t, const int*
   const int nw = blockDim.x >> 6;
   hi = min(hi, t.levels);
   if (lo > hi) return;
+  // (the one-shot walk's per-wave slot maps index rows wave + k nw < K nw of its 64-row LDS
+  // tables: only a K with K nw <= 64 is safe for this workgroup size)
   if (n >= 1 && n <= 64 && t.levels <= 5) {  // block-uniform
-    if (n <= 4 * nw) return update_levels_oneshot<4, 5>(t, sids, n, dbg, lo, hi);
-    if (KMAX >= 8 && n <= 8 * nw) return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n, dbg, lo, hi);
-    if (KMAX >= 16 && n <= 16 * nw) return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n, dbg, lo, hi);
+    if (n <= 4 * nw && 4 * nw <= 64) return update_levels_oneshot<4, 5>(t, sids, n, dbg, lo, hi);
+    if (KMAX >= 8 && n <= 8 * nw && 8 * nw <= 64)
+      return update_levels_oneshot<(KMAX >= 8 ? 8 : 4), 5>(t, sids, n, dbg, lo, hi);
+    if (KMAX >= 16 && n <= 16 * nw && 16 * nw <= 64)
+      return update_levels_oneshot<(KMAX >= 16 ? 16 : 4), 5>(t, sids, n, dbg, lo, hi);
   }
   update_levels_block(t, sids, n, lo, hi);
 }

@@ -277,8 +277,14 @@ class IpcLearnerLinks:
         tables = dict(kind=0, filled=rp.filled.data_ptr(), frames=rp.frames.data_ptr(), s_ids=rp.s_ids.data_ptr(),
                       s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
                       done=rp.done.data_ptr(), frame_base=fb.data_ptr(), slot_base=sb.data_ptr())
+        def tree_write(slots, prios):  # ring-ordered new rows (slot -1: nothing there)
+            if slots.numel() <= 2048:  # (the paced ingest: R x E rows) batched leaves + one wide launch per level
+                rp.write_batch(pre=(slots, prios, None))
+            else:  # (the drain's R x D x E rows, untimed)
+                rp.write_priorities(slots, prios, dedup=False)
+
         links = cls(R, D, E, P, store, prefix, device, packet_nbytes=packet_bytes(E), tables=tables,
-                    tree_write=lambda slots, prios: rp.write_priorities(slots, prios, dedup=False), **kw)
+                    tree_write=tree_write, **kw)
         links.replay, links.frame_base, links.slot_base = rp, fb, sb  # (kept alive: the kernel reads them)
         return links
 
@@ -535,3 +541,42 @@ class IpcActorLink:
         self.ctrl.view("ack")[self.i] = 1
         self.hip.ipc_close(self.remote)
         self.remote = 0
+
+
+class EmulatedActorLinks:
+    """R actor links emulated inside rank 0's process (``bench.py --emulate-links R``): a
+    one-GPU model of the central learner's load at N = R + 1 GPUs.  Every :meth:`push` writes,
+    for each link whose credit window allows it, one synthetic Ape-X packet (E frames + E rows
+    at the link's next local slots) straight into the learner's IPC ring slot and then stores
+    the slot's sequence word -- the bytes and the release protocol an actor GPU's xGMI peer copy
+    delivers (ipc_kernels.hip ``ipc_emu_*``).  The learner side is the real one: the in-graph
+    ``ipc_ingest``, the batched tree write, the credit counters, the stop / drain handshake
+    (the emulated actors acknowledge a stop in :meth:`finish`)."""
+
+    def __init__(self, links: IpcLearnerLinks, C_r: int, F_r: int, n_actions: int, seed: int = 0,
+                 pool_frames: int = 4096):
+        self.links, self.hip = links, links.hip
+        dev = links.device
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.pool = torch.randint(0, 256, (pool_frames, FRAME_BYTES), dtype=torch.uint8, device=dev, generator=g)
+        self.sent = torch.zeros(links.R, dtype=torch.int64, device=dev)
+        self.go = torch.zeros(links.R, dtype=torch.int32, device=dev)
+        self.handle = self.hip.make_ipc_emu(dict(
+            ring=links.arena, seq=links.arena + links.seq_off, consumed=links.consumed.data_ptr(),
+            sent=self.sent.data_ptr(), go=self.go.data_ptr(), pool=self.pool.data_ptr(), pool_n=pool_frames,
+            R=links.R, D=links.D, E=links.E, C_r=int(C_r), F_r=int(F_r), n_actions=int(n_actions), pkt=links.pkt,
+            seed=(seed * 0x9E3779B97F4A7C15 + 1) & 0xFFFFFFFFFFFFFFFF))
+        for r in range(1, links.R + 1):  # every "actor" has mapped the control block
+            links.store.set(f"{links.prefix}/ipc/opened/{r}", "1")
+        self._hb = links.ctrl.view("heartbeat")
+
+    def push(self) -> None:
+        """One paced actor step of every link (credit permitting), on the current stream."""
+        self.hip.ipc_emu_push(self.handle, torch.cuda.current_stream().cuda_stream)
+        self._hb += 1  # alive
+
+    def finish(self) -> None:
+        """Acknowledge the stop: the final sent counts, then the acks (the learner drains them)."""
+        torch.cuda.synchronize(self.links.device)
+        self.links.ctrl.view("sent")[:] = self.sent.cpu().numpy()
+        self.links.ctrl.view("ack")[:] = 1

@@ -109,6 +109,12 @@ def parse():
                     help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
+    ap.add_argument("--emulate-links", type=int, default=0, metavar="R",
+                    help="one GPU: the central learner (rank 0) with R actor links emulated in-process (synthetic "
+                         "packets into the real IPC ring, the real in-graph ingest): its load at N = R + 1 GPUs")
+    ap.add_argument("--actor-only", default="", metavar="E,E,..",
+                    help="one GPU: an actor rank's own throughput, unpaced (act + n-step rows + packet staging + the "
+                         "packet copy), at each env count, e.g. 256,1024,4096")
     ap.add_argument("--unpaced", action="store_true",
                     help="central topology: actors run free (default: paced at --actor-steps packets per learner "
                          "step per actor through the credit window)")
@@ -202,6 +208,11 @@ def main():
     wd = Watchdog(args.watchdog)
     import torch
     import torch.distributed as dist
+
+    if args.actor_only:
+        return actor_only(args, wd)
+    if args.emulate_links:
+        return central_emulated(args, wd)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -536,7 +547,7 @@ def aql_central(args, rank, world, device, wd, pre=None):
     dist.destroy_process_group()
 
 
-def central(args, rank, world, device, wd, pre=None):
+def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
     """Central-replay topology (BASELINE config 3; the default for N>1), asynchronous:
     rank 0 = THE learner (batch 512, the reference's single learner, origin_repo/learner.py:
     134-175) + the one replay, ranks 1.. = actor GPUs pushing experience over their own
@@ -557,7 +568,8 @@ def central(args, rank, world, device, wd, pre=None):
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
-    eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport)
+    eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport,
+                            emulate_links=emulate)
     wd.kick()
     if rank != 0:  # actor GPU: act and push until the learner stops this link
         if not args.no_graphs:
@@ -594,12 +606,13 @@ def central(args, rank, world, device, wd, pre=None):
     print(json.dumps({
         "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
         "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": 1 if emulate else world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": args.dtype,
         "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
         "config": {"model": "Ape-X dueling double DQN, Nature-CNN trunk, 128-hidden dueling heads, 18 actions",
-                   "global_batch": args.batch, "seq_len": 3, "parallelism": f"central1+actors{world - 1}",
+                   "global_batch": args.batch, "seq_len": 3,
+                   "parallelism": (f"central1+emulated_links{emulate}" if emulate else f"central1+actors{world - 1}"),
                    "topology": "central replay on rank 0, async experience links over "
                                + ("HIP IPC (xGMI peer copies)" if eng.transport == "ipc" else args.backend),
                    "actor_pacing": "free" if args.unpaced else f"{args.actor_steps} packet/learner step/actor",
@@ -614,6 +627,97 @@ def central(args, rank, world, device, wd, pre=None):
         "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
     }), flush=True)
     dist.destroy_process_group()
+
+
+
+
+def central_emulated(args, wd):
+    """``--emulate-links R``: BASELINE config 3's rank 0 on one GPU -- the central learner
+    with R actor links emulated in-process (parallel.ipc.EmulatedActorLinks: one synthetic
+    packet per link per learner step, credit permitting, written into the real IPC ring and
+    applied by the real in-graph ingest + batched tree write).  Not a scaling number: the
+    learner's steps/s under the ingest load of N = R + 1 GPUs (is rank 0 still
+    at the 1-GPU rate with 7 links?)."""
+    import torch
+    import torch.distributed as dist
+
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) > 1:
+        raise SystemExit("--emulate-links runs in ONE process")
+    torch.cuda.set_device(0)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(29000 + os.getpid() % 1000))
+    dist.init_process_group("gloo", rank=0, world_size=1)  # (the store the IPC handshake keys live in)
+    return central(args, 0, args.emulate_links + 1, torch.device("cuda", 0), wd, None, emulate=args.emulate_links)
+
+
+def actor_only(args, wd):
+    """``--actor-only E,..``: what one actor GPU of the central topology generates unpaced --
+    per actor step: batched inference of its E envs (eps-greedy in the heads kernel), the env
+    step, the n-step rows + priorities into its local mirror, the packet staging launch and a
+    device copy of the packet (standing in for the xGMI push) -- graph-captured and timed
+    back to back.  Frames/s = 4 emulator frames per env step (action repeat 4)."""
+    import torch
+
+    from apex_amd import ops
+    from apex_amd.engine.apex import EngineConfig
+    from apex_amd.engine.central import actor_rank_step, build_actor_rank, region_geometry
+    from apex_amd.engine.learner import LearnerConfig
+    from apex_amd.parallel.ipc import packet_bytes
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    hip = ops.hip()
+    rows = []
+    for E in [int(x) for x in args.actor_only.split(",") if x]:
+        cfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=args.capacity, seed=args.seed,
+                           learner=LearnerConfig(batch_size=args.batch, forward="hip", dtype=args.dtype))
+        R = 7  # the actor ranks of one 8-GPU node: each rank's region of the central replay
+        C_r, F_r = region_geometry(cfg, R)
+        a = build_actor_rank(cfg, dev, 1, R, C_r, F_r)
+        pkt = torch.empty(packet_bytes(E), dtype=torch.uint8, device=dev)
+        dst = torch.empty_like(pkt)
+
+        def step():
+            actor_rank_step(hip, a, pkt)
+            dst.copy_(pkt)
+
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        for _ in range(args.warmup):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        wd.kick()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        wd.kick()
+        rows.append({"envs": E, "actor_steps_per_sec": round(args.steps / dt, 1),
+                     "frames_per_sec": round(args.steps * E * 4 / dt, 1),
+                     "us_per_actor_step": round(1e6 * dt / args.steps, 2),
+                     "packet_bytes": packet_bytes(E)})
+        del a, g
+        torch.cuda.empty_cache()
+    wd.off()
+    best = max(rows, key=lambda r: r["frames_per_sec"])
+    print(json.dumps({
+        "metric": "actor frames/sec of one central-topology actor GPU (unpaced)",
+        "value": best["frames_per_sec"], "unit": "emulator frames/s (4 per env step) of one actor rank",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "vs_baseline": None,
+        "dtype": args.dtype, "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
+        "config": {"model": "Ape-X dueling double DQN actor (Nature-CNN, 18 actions)", "parallelism": "actor rank",
+                   "work_per_step": "inference + eps-greedy, env step, n-step rows + priorities, packet staging, "
+                                    "packet copy"},
+        "per_envs": rows,
+    }), flush=True)
 
 
 if __name__ == "__main__":

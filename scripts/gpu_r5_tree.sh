@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 700 python -u -m pytest -s -x -v --timeout 120 --timeout-method thread tests/test_gpu_replay.py \
-  tests/test_gpu_fused_bwd.py tests/test_gpu_learner.py tests/test_gpu_overlap.py tests/test_gpu_learning.py tests/test_gpu_ipc.py tests/test_gpu_multirank.py \
+  tests/test_gpu_fused_bwd.py tests/test_gpu_learner.py tests/test_gpu_overlap.py tests/test_gpu_learning.py tests/test_gpu_ipc.py tests/test_gpu_multirank.py tests/test_gpu_aql_engine.py tests/test_gpu_central_aql.py tests/test_gpu_f32_net.py \
   > gpurun_out/r5_tree_test.log 2>&1; rc=$?; echo "== tests rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/r5_tree_test.log | tail -15
 [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do
