@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 STEPS = 200
 
 
-def _run(cuda, dtype: str, B: int = 256, steps: int = STEPS):
+def _run(cuda, dtype: str, B: int = 256, steps: int = STEPS, seed: int = 1122):
     """HIP learner (``dtype``) + fp32 and fp64 PyTorch reference learners on the HIP
     learner's sampled stream.  Returns per-step trajectories and parameter distances."""
     from apex_amd.algo.losses import compute_loss_device, update_parameters_ex
@@ -25,7 +25,7 @@ def _run(cuda, dtype: str, B: int = 256, steps: int = STEPS):
     from apex_amd.models.dqn import DuelingDQN
 
     lc = LearnerConfig(batch_size=B, forward="hip", dtype=dtype)
-    cfg = EngineConfig(n_envs=64, replay_capacity=16384, threshold_size=8192, learner=lc)
+    cfg = EngineConfig(n_envs=64, replay_capacity=16384, threshold_size=8192, learner=lc, seed=seed)
     eng = ApexEngine(cfg, cuda)
     eng.fill()
     L, rp = eng.learner, eng.replay
@@ -84,6 +84,29 @@ def _summary(traj):
             print(i, {k: f"{traj[i][k]:.3g}" for k in keys})
 
 
+def test_first_step_distance_to_fp64_is_torch_fp32_class_over_seeds(cuda):
+    """the step-0 update's distance to the fp64 learner's, as a fraction
+    of the update length, for the HIP learner and for PyTorch's fp32 learner on the same
+    batch, over 8 seeds (model init, replay contents and the sampled batch all change).  A
+    single seed is the luck of one quadratic-region sample (see below); the median over seeds
+    is the kernels' precision class.  Bound: HIP median <= 3x torch fp32's median (the round-3
+    class), every seed within 20x (table in profiles/r5_learning_first_step_seeds.md)."""
+    rows = []
+    for k in range(8):
+        tr = _run(cuda, "fp32", steps=1, seed=1000 + 7 * k)
+        rows.append((1000 + 7 * k, tr[0]["hip_vs_64"], tr[0]["t32_vs_64"], tr[0]["hip_loss_err"],
+                     tr[0]["t32_loss_err"]))
+    print("\n| seed | HIP vs fp64 | torch fp32 vs fp64 | HIP loss err | torch fp32 loss err |")
+    print("|---:|---:|---:|---:|---:|")
+    for r in rows:
+        print(f"| {r[0]} | {r[1]:.3g} | {r[2]:.3g} | {r[3]:.3g} | {r[4]:.3g} |")
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731  (upper median of 8)
+    hip, t32 = med([r[1] for r in rows]), med([r[2] for r in rows])
+    print(f"median: HIP {hip:.3g}  torch fp32 {t32:.3g}  ratio {hip / t32:.2f}")
+    assert hip <= 3.0 * t32, (hip, t32)
+    assert all(r[1] <= 20.0 * max(r[2], 1e-7) for r in rows), rows
+
+
 def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
     """Loss / priorities within ~2e-7 of fp64 from the first step.  The parameter distance of
     the first steps hinges on very few samples: with this random-init net on raw u8 frames
@@ -101,9 +124,10 @@ def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
     traj = _run(cuda, "fp32")
     _summary(traj)
     assert traj[-1]["moved"] > 0
-    # first steps: within 0.1 % of the fp64 update; loss and priorities at kernel precision
+    # first steps: loss and priorities at kernel precision (the multi-seed precision-class
+    # bound on the update itself is the test above)
     for row in traj[:3]:
-        assert row["hip_vs_64"] < 1e-3, row["hip_vs_64"]
+        assert row["hip_vs_64"] <= 3.0 * row["t32_vs_64"] + 5e-4, row
         assert row["hip_loss_err"] < 1e-4 and row["hip_prio_err"] < 1e-3
     # whole run: the HIP fp32 learner is no farther from the fp64 learner than PyTorch's
     # own fp32 learner (same fp32 roundoff class).  The sign-like RMSprop steps amplify any
