@@ -168,39 +168,84 @@ __device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two e
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
 
 // Exact three-term split of 8 fp32 values (two 4-element k-runs of a fragment) into bf16
-// hi / mid / lo vectors, x = hi + mid + lo EXACTLY (truncation: 8 + 8 + 8 significant bits).
-// The products of every pair of terms are exact in fp32; the six kept pairs (hi.hi, hi.mid,
-// mid.hi, hi.lo, mid.mid, lo.hi) leave out terms below 2^-23 |a||b| -- the size of the fp32
-// rounding of the product itself -- so the GEMM is fp32-class on the bf16 matrix cores
-// (1024 FLOP/clk/SIMD vs 64 for v_mfma_f32_32x32x2_f32: six of them still run 2.7x faster).
+// hi / mid / lo vectors with x = hi + mid + lo EXACTLY: hi = rne(x), mid = rne(x - hi),
+// lo = rne(x - hi - mid) -- each residual is exact in fp32, and round-to-nearest leaves at most
+// 24 - 8 - 9 - 9 < 0 bits for a fourth term.  The products of every pair of terms are exact in
+// fp32; the six kept pairs (hi.hi, hi.mid, mid.hi, hi.lo, mid.mid, lo.hi) leave out terms below
+// 2^-26 |a||b| -- under the fp32 rounding of the product itself -- so the GEMM is fp32-class on
+// the bf16 matrix cores (1024 FLOP/clk/SIMD vs 64 for v_mfma_f32_32x32x2_f32: six of them still
+// run 2.7x faster).  Per pair of values: 3 v_cvt_pk_bf16_f32, 2 v_pk_add_f32, 4 unpacks.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 struct Split8 {
   bfx8 h, m, l;
 };
+__device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const bf16x2 hb = __builtin_convertvector(v, bf16x2);
+  const f32x2 r = v - __builtin_convertvector(hb, f32x2);
+  const bf16x2 mb = __builtin_convertvector(r, bf16x2);
+  const f32x2 r2 = r - __builtin_convertvector(mb, f32x2);
+  h = __builtin_bit_cast(uint32_t, hb);
+  m = __builtin_bit_cast(uint32_t, mb);
+  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2));
+}
 __device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
-  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
   uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float a = x[2 * j], b = x[2 * j + 1];
-    const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
-    const float am = trunc_bf16(ar), bm = trunc_bf16(br);
-    h[j] = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
-    m[j] = pack_bf16_hi(am, bm);
-    l[j] = pack_bf16_hi(ar - am, br - bm);  // exact: <= 8 significant bits
-  }
+  split2(f32x2{x0[0], x0[1]}, h[0], m[0], l[0]);
+  split2(f32x2{x0[2], x0[3]}, h[1], m[1], l[1]);
+  split2(f32x2{x1[0], x1[1]}, h[2], m[2], l[2]);
+  split2(f32x2{x1[2], x1[3]}, h[3], m[3], l[3]);
   return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
           __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
           __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
 }
 
 // fp32 GEMM arithmetic of gemm_body: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 fma chain),
-// 1 = the exact-split bf16 form (split8, six v_mfma_f32_32x32x16_bf16 per 16 k)
+// 1 = the exact-split bf16 form (split8 of every fragment a wave reads, six
+// v_mfma_f32_32x32x16_bf16 per 16 k), 2 = the same products with K-major operands split ONCE
+// while staging into LDS (three bf16 planes; MN-major operands as in 1) -- bit-identical to 1
 int g_f32_x6 = 1;
 
-template <class P, bool X6>
+// LDS layout of gemm_body<P, X>: a K-major operand staged as split planes (X == 2) holds three
+// bf16 planes [hi | mid | lo][rows][BK + 8], each 16-k group of a row permuted to k order
+// {0-3, 8-11, 4-7, 12-15} so lane half h reads its 8 fragment values (k 4h..4h+3, 8+4h..8+4h+3,
+// the register-split slot map) with ONE 16-byte read per plane; the 80-byte pitch (BK 32) keeps
+// 16 consecutive lanes' 16-byte reads on distinct banks.
+template <class P, int X>
+struct Lay {
+  using G = Geo<P>;
+  static constexpr bool A2 = X == 2 && P::A_KMAJ, B2 = X == 2 && P::B_KMAJ;
+  static constexpr int P2 = G::BK + 8;  // bf16 per plane row
+  static constexpr int SA = A2 ? 3 * G::BM * P2 / 2 : G::SA;  // floats
+  static constexpr int SB = B2 ? 3 * G::BN * P2 / 2 : G::SB;
+  static constexpr int FLOATS = 2 * (SA + SB) > 4 * 256 ? 2 * (SA + SB) : 4 * 256;
+};
+
+// the 4-element k-run `v` (chunk ch of a row) split into the three planes of row `row`
+template <int ROWS, int P2>
+__device__ __forceinline__ void store_split(float* base, int row, int ch, f32x4 v) {
+  uint16_t* d = reinterpret_cast<uint16_t*>(base) + row * P2 + (ch >> 2) * 16 + ((ch & 1) << 3) + ((ch & 2) << 1);
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split2(f32x2{v[0], v[1]}, h0, m0, l0);
+  split2(f32x2{v[2], v[3]}, h1, m1, l1);
+  *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+  *reinterpret_cast<uint2*>(d + ROWS * P2) = make_uint2(m0, m1);
+  *reinterpret_cast<uint2*>(d + 2 * ROWS * P2) = make_uint2(l0, l1);
+}
+// 16-k step s of row `row`: lane half h's 8 values of each plane
+template <int ROWS, int P2>
+__device__ __forceinline__ Split8 load_split(const float* base, int row, int s, int h) {
+  const uint16_t* p = reinterpret_cast<const uint16_t*>(base) + row * P2 + s * 16 + h * 8;
+  return {__builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p)),
+          __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + ROWS * P2)),
+          __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + 2 * ROWS * P2))};
+}
+
+template <class P, int X6>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
+  using L = Lay<P, X6>;
   constexpr bool COLSUM = HasColsum<P>::value;
   static_assert(!COLSUM || (!P::A_KMAJ && 256 % G::RA == 0), "colsum needs MN-major A");
   typename P::Ctx ctx;
@@ -257,21 +302,24 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   };
   auto sstore = [&](int buf, auto S) {
     constexpr int st = decltype(S)::value;
-    float* As = lds + buf * (G::SA + G::SB);
-    float* Bs = As + G::SA;
+    float* As = lds + buf * (L::SA + L::SB);
+    float* Bs = As + L::SA;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int q = t + 256 * j;
       if (G::CA % 256 == 0 || q < G::CA) {
-        *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[st][j];
+        if constexpr (L::A2) store_split<G::BM, L::P2>(As, q / G::RA, q % G::RA, ra[st][j]);
+        else *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[st][j];
         if constexpr (COLSUM) csum += ra[st][j];
       }
     }
 #pragma unroll
     for (int j = 0; j < G::NB; ++j) {
       const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB)
-        *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[st][j];
+      if (G::CB % 256 == 0 || q < G::CB) {
+        if constexpr (L::B2) store_split<G::BN, L::P2>(Bs, q / G::RB, q % G::RB, rb[st][j]);
+        else *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[st][j];
+      }
     }
   };
   using S0 = std::integral_constant<int, 0>;
@@ -307,9 +355,17 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
     return v;
   };
+  auto split_a = [&](const float* As, int mi, int kc) {
+    if constexpr (L::A2) return load_split<G::BM, L::P2>(As, wm * G::WTM + mi * 32 + r, kc >> 1, h);
+    else return split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
+  };
+  auto split_b = [&](const float* Bs, int ni, int kc) {
+    if constexpr (L::B2) return load_split<G::BN, L::P2>(Bs, wn * G::WTN + ni * 32 + r, kc >> 1, h);
+    else return split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
+  };
   auto compute = [&](int buf) {
-    const float* As = lds + buf * (G::SA + G::SB);
-    const float* Bs = As + G::SA;
+    const float* As = lds + buf * (L::SA + L::SB);
+    const float* Bs = As + L::SA;
     if constexpr (X6) {
       static_assert(G::BK % 16 == 0, "X6: k-blocks of 16");
       // 16 k per step: lane (r, h) holds k = 4h..4h+3 of chunk kc and of chunk kc + 1 -> bf16
@@ -318,9 +374,9 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
       for (int kc = 0; kc < G::BK / 8; kc += 2) {
         Split8 a[G::TM], b[G::TN];
 #pragma unroll
-        for (int mi = 0; mi < G::TM; ++mi) a[mi] = split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
+        for (int mi = 0; mi < G::TM; ++mi) a[mi] = split_a(As, mi, kc);
 #pragma unroll
-        for (int ni = 0; ni < G::TN; ++ni) b[ni] = split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
+        for (int ni = 0; ni < G::TN; ++ni) b[ni] = split_b(Bs, ni, kc);
 #pragma unroll
         for (int mi = 0; mi < G::TM; ++mi)
 #pragma unroll
@@ -422,9 +478,9 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 }
 
 
-template <class P, bool X6>
+template <class P, int X6>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
-  __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[Lay<P, X6>::FLOATS];
   __shared__ typename P::Smem sm;
   gemm_body<P, X6>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
@@ -436,9 +492,9 @@ struct MaxI {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2, bool X6>
+template <class P1, class P2, int X6>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
-  __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
+  __shared__ __attribute__((aligned(16))) float lds[MaxI<Lay<P1, X6>::FLOATS, Lay<P2, X6>::FLOATS>::value];
   __shared__ union {
     typename P1::Smem s1;
     typename P2::Smem s2;
@@ -1352,16 +1408,18 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  if (g_f32_x6) gemm_k<P, true><<<blocks, 256, 0, s>>>(a);
-  else gemm_k<P, false><<<blocks, 256, 0, s>>>(a);
+  if (g_f32_x6 == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a);
+  else if (g_f32_x6) gemm_k<P, 1><<<blocks, 256, 0, s>>>(a);
+  else gemm_k<P, 0><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  if (g_f32_x6) gemm2_k<P1, P2, true><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else gemm2_k<P1, P2, false><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  if (g_f32_x6 == 2) gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else if (g_f32_x6) gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else gemm2_k<P1, P2, 0><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
 

@@ -27,7 +27,7 @@ strong`` keeps the reference's single-learner global batch of 512 (512/N per ran
 reported alongside.  ``--dtype fp32`` (default) is the reference's precision
 (origin_repo/learner.py:139-145: fp32 modules, no autocast): fp32 operands and activations,
 the GEMMs on the bf16 matrix cores through an exact three-term split of every fp32 operand
-(six products per 16 k, dropped terms below 2^-23 |a b|; per-layer error vs fp64 within the
+(six products per 16 k, dropped terms below 2^-26 |a b|; per-layer error vs fp64 within the
 fp32 dot-product bound, tests/test_gpu_f32_net.py::test_gemm_layers_are_fp32_class);
 ``--dtype bf16`` is the opt-in bf16-operand mode.  Run: ``python bench.py [--gpus N --steps K --warmup W]`` (N>1
 under torch.distributed.run, one process per GPU).
