@@ -10,7 +10,7 @@ timeout -k 10 300 python -u -m pytest -x -v -s --timeout 120 --timeout-method th
   > $O/f32_test.log 2>&1; rc=$?; echo "== f32 tests rc=$rc"; grep -E "x6=|passed|failed|Error" $O/f32_test.log | head -30
 [ $rc -ne 0 ] && exit $rc
 for x in 1 2 1 2; do
-  timeout -k 10 120 python scripts/bench_f32.py --x6 $x > $O/bench_f32_x$x.log 2>&1 || exit $?
+  timeout -k 10 120 python scripts/bench_f32.py --x6 $x --tile2 > $O/bench_f32_x$x.log 2>&1 || exit $?
   echo "== bench_f32 x6=$x"; cat $O/bench_f32_x$x.log | grep -v amdgpu.ids
 done
 for x in 1 2 1 2; do
