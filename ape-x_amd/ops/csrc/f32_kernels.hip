@@ -202,50 +202,32 @@ __device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
 
 // fp32 GEMM arithmetic of gemm_body: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 fma chain),
 // 1 = the exact-split bf16 form (split8 of every fragment a wave reads, six
-// v_mfma_f32_32x32x16_bf16 per 16 k), 2 = the same products with K-major operands split ONCE
-// while staging into LDS (three bf16 planes; MN-major operands as in 1) -- bit-identical to 1
+// v_mfma_f32_32x32x16_bf16 per 16 k), 2 = the same with the truncation split (A/B)
 int g_f32_x6 = 1;
 
-// LDS layout of gemm_body<P, X>: a K-major operand staged as split planes (X == 2) holds three
-// bf16 planes [hi | mid | lo][rows][BK + 8], each 16-k group of a row permuted to k order
-// {0-3, 8-11, 4-7, 12-15} so lane half h reads its 8 fragment values (k 4h..4h+3, 8+4h..8+4h+3,
-// the register-split slot map) with ONE 16-byte read per plane; the 80-byte pitch (BK 32) keeps
-// 16 consecutive lanes' 16-byte reads on distinct banks.
-template <class P, int X>
-struct Lay {
-  using G = Geo<P>;
-  static constexpr bool A2 = X == 2 && P::A_KMAJ, B2 = X == 2 && P::B_KMAJ;
-  static constexpr int P2 = G::BK + 8;  // bf16 per plane row
-  static constexpr int SA = A2 ? 3 * G::BM * P2 / 2 : G::SA;  // floats
-  static constexpr int SB = B2 ? 3 * G::BN * P2 / 2 : G::SB;
-  static constexpr int FLOATS = 2 * (SA + SB) > 4 * 256 ? 2 * (SA + SB) : 4 * 256;
-};
-
-// the 4-element k-run `v` (chunk ch of a row) split into the three planes of row `row`
-template <int ROWS, int P2>
-__device__ __forceinline__ void store_split(float* base, int row, int ch, f32x4 v) {
-  uint16_t* d = reinterpret_cast<uint16_t*>(base) + row * P2 + (ch >> 2) * 16 + ((ch & 1) << 3) + ((ch & 2) << 1);
-  uint32_t h0, m0, l0, h1, m1, l1;
-  split2(f32x2{v[0], v[1]}, h0, m0, l0);
-  split2(f32x2{v[2], v[3]}, h1, m1, l1);
-  *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
-  *reinterpret_cast<uint2*>(d + ROWS * P2) = make_uint2(m0, m1);
-  *reinterpret_cast<uint2*>(d + 2 * ROWS * P2) = make_uint2(l0, l1);
-}
-// 16-k step s of row `row`: lane half h's 8 values of each plane
-template <int ROWS, int P2>
-__device__ __forceinline__ Split8 load_split(const float* base, int row, int s, int h) {
-  const uint16_t* p = reinterpret_cast<const uint16_t*>(base) + row * P2 + s * 16 + h * 8;
-  return {__builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p)),
-          __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + ROWS * P2)),
-          __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + 2 * ROWS * P2))};
+// the same split by truncation (hi = the upper 16 bits, mid / lo of the exact residuals): the
+// round-4 form, kept as mode 2 for the same-box A/B against the round-to-nearest split8
+__device__ __forceinline__ Split8 split8_trunc(f32x4 x0, f32x4 x1) {
+  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  uint32_t h[4], m[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float a = x[2 * j], b = x[2 * j + 1];
+    const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
+    const float am = trunc_bf16(ar), bm = trunc_bf16(br);
+    h[j] = pack_bf16_hi(a, b);
+    m[j] = pack_bf16_hi(am, bm);
+    l[j] = pack_bf16_hi(ar - am, br - bm);
+  }
+  return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
+          __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
+          __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
 }
 
 template <class P, int X6>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
-  using L = Lay<P, X6>;
   constexpr bool COLSUM = HasColsum<P>::value;
   static_assert(!COLSUM || (!P::A_KMAJ && 256 % G::RA == 0), "colsum needs MN-major A");
   typename P::Ctx ctx;
@@ -302,24 +284,21 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
   };
   auto sstore = [&](int buf, auto S) {
     constexpr int st = decltype(S)::value;
-    float* As = lds + buf * (L::SA + L::SB);
-    float* Bs = As + L::SA;
+    float* As = lds + buf * (G::SA + G::SB);
+    float* Bs = As + G::SA;
 #pragma unroll
     for (int j = 0; j < G::NA; ++j) {
       const int q = t + 256 * j;
       if (G::CA % 256 == 0 || q < G::CA) {
-        if constexpr (L::A2) store_split<G::BM, L::P2>(As, q / G::RA, q % G::RA, ra[st][j]);
-        else *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[st][j];
+        *reinterpret_cast<f32x4*>(As + (q / G::RA) * G::PA + 4 * (q % G::RA)) = ra[st][j];
         if constexpr (COLSUM) csum += ra[st][j];
       }
     }
 #pragma unroll
     for (int j = 0; j < G::NB; ++j) {
       const int q = t + 256 * j;
-      if (G::CB % 256 == 0 || q < G::CB) {
-        if constexpr (L::B2) store_split<G::BN, L::P2>(Bs, q / G::RB, q % G::RB, rb[st][j]);
-        else *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[st][j];
-      }
+      if (G::CB % 256 == 0 || q < G::CB)
+        *reinterpret_cast<f32x4*>(Bs + (q / G::RB) * G::PB + 4 * (q % G::RB)) = rb[st][j];
     }
   };
   using S0 = std::integral_constant<int, 0>;
@@ -356,16 +335,16 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     return v;
   };
   auto split_a = [&](const float* As, int mi, int kc) {
-    if constexpr (L::A2) return load_split<G::BM, L::P2>(As, wm * G::WTM + mi * 32 + r, kc >> 1, h);
+    if constexpr (X6 == 2) return split8_trunc(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
     else return split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
   };
   auto split_b = [&](const float* Bs, int ni, int kc) {
-    if constexpr (L::B2) return load_split<G::BN, L::P2>(Bs, wn * G::WTN + ni * 32 + r, kc >> 1, h);
+    if constexpr (X6 == 2) return split8_trunc(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
     else return split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
   };
   auto compute = [&](int buf) {
-    const float* As = lds + buf * (L::SA + L::SB);
-    const float* Bs = As + L::SA;
+    const float* As = lds + buf * (G::SA + G::SB);
+    const float* Bs = As + G::SA;
     if constexpr (X6) {
       static_assert(G::BK % 16 == 0, "X6: k-blocks of 16");
       // 16 k per step: lane (r, h) holds k = 4h..4h+3 of chunk kc and of chunk kc + 1 -> bf16
@@ -480,7 +459,7 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 
 template <class P, int X6>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
-  __shared__ __attribute__((aligned(16))) float lds[Lay<P, X6>::FLOATS];
+  __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
   gemm_body<P, X6>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
@@ -494,7 +473,7 @@ struct MaxI {
 // longer per-block problem starts early).
 template <class P1, class P2, int X6>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
-  __shared__ __attribute__((aligned(16))) float lds[MaxI<Lay<P1, X6>::FLOATS, Lay<P2, X6>::FLOATS>::value];
+  __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
   __shared__ union {
     typename P1::Smem s1;
     typename P2::Smem s2;

@@ -26,6 +26,10 @@ template <typename T>
 T* P(uint64_t v) {
   return reinterpret_cast<T*>(static_cast<uintptr_t>(v));
 }
+template <typename T>
+T* P_(uint64_t v) {  // (P names a parameter count in some bindings)
+  return P<T>(v);
+}
 uint64_t U(const void* p) { return (uint64_t)reinterpret_cast<uintptr_t>(p); }
 hipStream_t S(uint64_t v) { return reinterpret_cast<hipStream_t>(static_cast<uintptr_t>(v)); }
 
@@ -166,6 +170,11 @@ void register_ipc(py::module_& m) {
   });
   m.def("ipc_ingest", [](const IpcIngestHandle& h, uint64_t s) { apex::ipc_ingest(h.g, S(s)); });
   m.def("ipc_flag", [](uint64_t p, int64_t v, uint64_t s) { apex::ipc_flag(P<int64_t>(p), v, S(s)); });
+  m.def("ipc_param_publish", [](uint64_t ctrl, int pin_off, int R, int begin_off, int K, uint64_t params,
+                                int64_t stride_f, uint64_t src, int64_t P, int64_t v, uint64_t pick, uint64_t s) {
+    apex::ipc_param_publish(P_<int64_t>(ctrl), pin_off, R, begin_off, K, P_<float>(params), stride_f,
+                            P_<const float>(src), P, v, P_<int>(pick), S(s));
+  });
   m.def("ipc_stage_dqn", [](py::dict d, uint64_t s) {
     auto p = [&](const char* k) -> uint64_t { return d.contains(k) ? d[k].cast<uint64_t>() : 0; };
     apex::IpcStage st{};

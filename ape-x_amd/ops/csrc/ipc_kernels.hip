@@ -28,6 +28,8 @@
 //   * parameters: rank 0 copies the master weights into params[v & 1] on its stream, then
 //     ipc_flag_k publishes v to the control block; actors read v there and pull the slot
 //     (seqlock check on the version around the copy).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -272,6 +274,34 @@ __global__ void ipc_emu_publish_k(IpcEmu g) {
   g.sent[r] = n + 1;
 }
 
+// --- pinned parameter publish
+__global__ void ipc_param_pick_k(int64_t* ctrl, int pin_off, int R, int begin_off, int K, int64_t v, int* pick) {
+  if (threadIdx.x != 0) return;
+  uint64_t busy = 1ull << (__hip_atomic_load(ctrl + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) & 0xFF);
+  for (int r = 0; r < R; ++r) {
+    const int64_t p = __hip_atomic_load(ctrl + pin_off + r, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (p != 0) busy |= 1ull << (p & 0xFF);
+  }
+  int b = 0;
+  while (b < K - 1 && ((busy >> b) & 1ull)) ++b;  // (K = R + 2 > #busy: a free one exists)
+  pick[0] = b;
+  store_release_sys(ctrl + begin_off + b, v);  // begun: a reader whose pull overlaps sees it
+}
+
+__global__ __launch_bounds__(256) void ipc_param_copy_k(float* params, const float* __restrict__ src, int64_t P,
+                                                        int64_t stride_f, const int* __restrict__ pick) {
+  float* dst = params + (int64_t)pick[0] * stride_f;
+  const int64_t n4 = P >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) dst[i] = src[i];
+}
+
+__global__ void ipc_param_release_k(int64_t* ctrl, int64_t v, const int* __restrict__ pick) {
+  if (threadIdx.x == 0) store_release_sys(ctrl + 2, (v << 8) | (int64_t)pick[0]);
+}
+
 __global__ void ipc_flag_k(int64_t* p, int64_t v) {
   if (threadIdx.x == 0 && blockIdx.x == 0) store_release_sys(p, v);
 }
@@ -332,6 +362,22 @@ void ipc_emu_push(const IpcEmu& g, hipStream_t s) {
   ipc_emu_write_k<<<g.R * g.E, 128, 0, s>>>(g);
   LAUNCH_CHECK();
   ipc_emu_publish_k<<<1, thr, 0, s>>>(g);
+  LAUNCH_CHECK();
+}
+
+void ipc_param_publish(int64_t* ctrl, int pin_off, int R, int begin_off, int K, float* params, int64_t stride_f,
+                       const float* src, int64_t P, int64_t v, int* pick, hipStream_t s) {
+  if (!ctrl || !params || !src || !pick || R < 1 || K < R + 2 || K > 64 || P < 1 || v < 1 || stride_f < P)
+    throw std::invalid_argument("ipc_param_publish: K in [R + 2, 64], pointers, P and v positive, stride >= P");
+  if ((reinterpret_cast<uintptr_t>(params) | reinterpret_cast<uintptr_t>(src)) & 15 || stride_f % 4)
+    throw std::invalid_argument("ipc_param_publish: 16-byte aligned buffers and stride");
+  ipc_param_pick_k<<<1, 64, 0, s>>>(ctrl, pin_off, R, begin_off, K, v, pick);
+  LAUNCH_CHECK();
+  const int64_t n4 = P / 4;
+  const int blocks = (int)std::min<int64_t>(1024, (n4 + 255) / 256);
+  ipc_param_copy_k<<<std::max(blocks, 1), 256, 0, s>>>(params, src, P, stride_f, pick);
+  LAUNCH_CHECK();
+  ipc_param_release_k<<<1, 64, 0, s>>>(ctrl, v, pick);
   LAUNCH_CHECK();
 }
 

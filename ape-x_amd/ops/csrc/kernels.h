@@ -650,5 +650,11 @@ struct IpcEmu {
 };
 void ipc_emu_push(const IpcEmu& e, hipStream_t s);
 void ipc_flag(int64_t* p, int64_t v, hipStream_t s);  // system-scope release store of v (one thread)
+// The pinned parameter publish (parallel/ipc.py): at execution time pick buffer b of K -- not
+// the current word's (word & 0xFF), not any reader's pinned word's -- store begin[b] = v, copy
+// src [P] into params + b stride_f, then release word = v << 8 | b.  ctrl: the control block's
+// device address (int64 words); pin_off / begin_off / word 2: word offsets.
+void ipc_param_publish(int64_t* ctrl, int pin_off, int R, int begin_off, int K, float* params, int64_t stride_f,
+                       const float* src, int64_t P, int64_t v, int* pick, hipStream_t s);
 
 }  // namespace apex

@@ -23,16 +23,17 @@ parameter publish, for actor GPUs on the same node (xGMI):
   parameter version, per-link heartbeat counters, drop flags, the stop flag and stop
   acknowledgements.  The actors read and write it with plain CPU loads / stores.
 * **Parameters** (conflated, learner.py:57-68 PUB/SUB CONFLATE=1): ``K = R + 2`` parameter
-  buffers; version ``v`` lives in buffer ``v % K``.  A reader *pins* the version it is about
-  to pull (its pin word in the control block), pulls buffer ``v % K`` with one peer copy,
-  then checks that buffer's *begin* word -- stored by rank 0's stream just before it starts
-  writing a buffer -- still reads ``v`` (nobody began rewriting it during the pull).  The
-  writer never targets a pinned buffer or the newest one: it skips version numbers until
-  ``v % K`` is free (at most R buffers are pinned, so one always is).  Once its pin is
-  visible a reader's buffer cannot be rewritten, however slow its copy: publishing every
-  learner iteration never starves a reader (a pull fails only if ``K`` versions are
-  enqueued between reading the version word and storing the pin -- microseconds -- and is
-  then retried).  Readers simply skip versions.
+  buffers.  The published word in the control block is ``v << 8 | b``: version ``v`` lives in
+  buffer ``b``.  A reader *pins* the word it is about to pull (its pin slot), pulls buffer ``b``
+  with one peer copy, then checks that buffer's *begin* word still reads ``v`` (nobody began
+  rewriting it during the pull).  The writer picks the buffer ON THE GPU, when the publish
+  executes (ipc_kernels.hip ``ipc_param_publish``): neither the newest version's buffer nor
+  any pinned one -- at most R are pinned, so one of K is always free -- marks it begun, copies,
+  then releases the new word.  Once its pin is visible a reader's buffer is never rewritten,
+  however slow its copy and however far the learner's host runs ahead of its GPU: publishing
+  every learner iteration never starves a reader (a pull fails only if two versions are
+  published between reading the word and storing the pin -- microseconds -- and is retried).
+  Readers simply skip versions.
 * **Liveness** (SURVEY §5.3): actors bump a heartbeat word on a wall-clock period (also
   while waiting for credit); rank 0 drops a link whose word stopped moving for
   ``dead_after`` s: its ingest mask goes to 0 and its drop flag tells a live-but-stuck actor
@@ -62,7 +63,7 @@ FRAME_BYTES = 84 * 84
 MODE_UNCACHED = 2
 
 # control block layout (int64 words)
-_HDR = 8          # magic, R, param_version, stop, param_begin, (reserved)
+_HDR = 8          # magic, R, param word (version << 8 | buffer), stop, (reserved)
 _MAGIC = 0x4150455849504331  # "APEXIPC1"
 
 
@@ -80,34 +81,32 @@ def param_buffers(R: int) -> int:
     return int(R) + 2
 
 
-def pick_version(last: int, pins, K: int) -> int:
-    """Writer side of the pinned protocol: the next version number ``> last`` whose buffer
-    ``v % K`` is neither pinned by a reader nor the newest version's (``last % K``)."""
-    busy = {int(p) % K for p in pins if int(p) > 0} | {last % K}
-    v = last + 1
-    while v % K in busy:
-        v += 1
-    return v
+def pick_buffer(word: int, pins, K: int) -> int:
+    """Writer side of the pinned protocol (what ``ipc_param_publish`` computes on the GPU):
+    the lowest buffer that is neither the current word's nor pinned by a reader (pins hold the
+    words the readers pinned; 0 = none)."""
+    busy = {int(word) & 0xFF} | {int(p) & 0xFF for p in pins if int(p) != 0}
+    return next(b for b in range(K) if b not in busy)
 
 
 def pinned_pull(ctrl: "ControlBlock", i: int, have: int, pull, retries: int = 8) -> tuple[int | None, int]:
-    """Reader side of the pinned protocol for reader ``i``: pin the newest published version,
+    """Reader side of the pinned protocol for reader ``i``: pin the newest published word,
     ``pull(buffer)`` it (synchronously), keep it if the buffer's begin word still reads that
     version.  Returns (installed version or None, failed pulls)."""
-    v = ctrl.param_version
-    if v <= have:
+    w = ctrl.param_word
+    if (w >> 8) <= have:
         return None, 0
     pin = ctrl.view("pin")
     failed = 0
     try:
         for _ in range(retries):
-            pin[i] = v  # from here on the writer leaves buffer v % K alone
-            b = v % ctrl.K
+            pin[i] = w  # from here on the writer leaves this buffer alone
+            v, b = w >> 8, w & 0xFF
             pull(b)
             if int(ctrl.w[ctrl.begin_off(b)]) == v:  # nobody began rewriting it during the pull: clean
                 return v, failed
             failed += 1
-            v = ctrl.param_version
+            w = ctrl.param_word
         return None, failed
     finally:
         pin[i] = 0
@@ -157,8 +156,13 @@ class ControlBlock:
         return _HDR + len(self.FIELDS) * self.R + int(b)
 
     @property
-    def param_version(self) -> int:
+    def param_word(self) -> int:
+        """The published parameter word: version << 8 | buffer."""
         return int(self.w[2])
+
+    @property
+    def param_version(self) -> int:
+        return int(self.w[2]) >> 8
 
     @property
     def stop(self) -> bool:
@@ -228,7 +232,9 @@ class IpcLearnerLinks:
         self.pkt = _align(self.packet_nbytes)
         self.seq_off = _align(self.R * self.D * self.pkt)
         self.par_off = _align(self.seq_off + 8 * self.R * self.D)
-        self.nbytes = self.par_off + self.K * 4 * self.P
+        self.PS = _align(4 * self.P) // 4  # parameter buffer stride (floats; 256-byte aligned buffers)
+        self.nbytes = self.par_off + self.K * 4 * self.PS
+        self._pick = torch.zeros(1, dtype=torch.int32, device=device)  # the publish's buffer (scratch)
         self.arena = h.ipc_alloc(self.nbytes, mode)
         self.ctrl = ControlBlock(f"apex_ipc_{prefix.replace('/', '_')}_{os.getpid()}", R, create=True)
         self.ctrl.register(h)
@@ -257,7 +263,7 @@ class IpcLearnerLinks:
         self._hb = {r: (None, time.monotonic()) for r in self.live}
         self._hb_t = time.monotonic()
         self.closed = False
-        geo = dict(R=R, D=D, E=E, P=P, pkt=self.pkt, packet_nbytes=self.packet_nbytes, seq_off=self.seq_off,
+        geo = dict(R=R, D=D, E=E, P=P, PS=self.PS, pkt=self.pkt, packet_nbytes=self.packet_nbytes, seq_off=self.seq_off,
                    par_off=self.par_off, shm=self.ctrl.name, device=self.device.index or 0)
         store.set(f"{prefix}/ipc/handle", h.ipc_handle(self.arena))
         store.set(f"{prefix}/ipc/geometry", json.dumps(geo))
@@ -337,16 +343,15 @@ class IpcLearnerLinks:
         self.tree_write(self.slots_out[:n], self.prio_out[:n])
 
     def publish(self, flat: torch.Tensor) -> int:
-        """Conflated versioned publish (pinned protocol, module docstring), all on the current
-        stream: pick a version whose buffer no reader has pinned, mark the buffer as begun,
-        copy, release the version.  Returns the version."""
-        v = pick_version(self.version, self.ctrl.view("pin"), self.K)
-        b, s = v % self.K, self._s()
-        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * self.ctrl.begin_off(b), v, s)
-        self.hip.memcpy_async(self.arena + self.par_off + b * 4 * self.P, flat.data_ptr(), 4 * self.P, s)
-        self.hip.ipc_flag(self.ctrl.dev_ptr + 8 * 2, v, s)
-        self.version = v
-        return v
+        """Conflated versioned publish (pinned protocol, module docstring), on the current
+        stream: the GPU picks a buffer neither current nor pinned when the publish executes,
+        marks it begun, copies ``flat`` into it and releases the new word.  Returns the version."""
+        self.version += 1
+        c = self.ctrl
+        self.hip.ipc_param_publish(c.dev_ptr, c.off("pin"), self.R, c.begin_off(0), self.K,
+                                   self.arena + self.par_off, self.PS, flat.data_ptr(), self.P, self.version,
+                                   self._pick.data_ptr(), self._s())
+        return self.version
 
     def drop(self, r: int, why: str) -> None:
         if r in self.live:
@@ -435,7 +440,7 @@ class IpcActorLink:
         self.flat, self.packet = flat, packet
         store.wait([f"{prefix}/ipc/handle", f"{prefix}/ipc/geometry"], timedelta(seconds=timeout))
         geo = json.loads(store.get(f"{prefix}/ipc/geometry"))
-        self.R, self.D, self.E, self.P = geo["R"], geo["D"], geo["E"], geo["P"]
+        self.R, self.D, self.E, self.P, self.PS = geo["R"], geo["D"], geo["E"], geo["P"], geo["PS"]
         self.K = param_buffers(self.R)
         self.pkt, self.seq_off, self.par_off = geo["pkt"], geo["seq_off"], geo["par_off"]
         want = geo.get("packet_nbytes", packet_bytes(self.E))
@@ -522,7 +527,7 @@ class IpcActorLink:
         if self.check_stop():
             return STOP
         def pull(b: int) -> None:
-            self.hip.memcpy_async(self.flat.data_ptr(), self.remote + self.par_off + b * 4 * self.P, 4 * self.P,
+            self.hip.memcpy_async(self.flat.data_ptr(), self.remote + self.par_off + b * 4 * self.PS, 4 * self.P,
                                   self._s())
             self._ev.record(torch.cuda.current_stream(self.device))
             self._ev.synchronize()

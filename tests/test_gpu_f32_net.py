@@ -301,34 +301,3 @@ def test_gemm_layers_are_fp32_class(cuda, x6):
     # fp32 unit roundoff 6e-8: K <= 3136 accumulations stay within a few ulps of sum |a b|
     assert max(errs.values()) < 1e-6, errs
 
-
-def test_staged_split_equals_register_split(cuda):
-    """gemm_body mode 2 (K-major operands split once while staging into LDS as bf16 planes)
-    == mode 1 (every fragment split in registers): the same terms, the same products, the
-    same accumulation order -- bit for bit, forward and backward."""
-    from apex_amd import ops
-    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
-
-    h = ops.hip()
-    outs = []
-    try:
-        for mode in (1, 2):
-            h.f32_set_x6(mode)
-            B, A = 70, 18
-            m = _model(cuda, A=A, seed=11)
-            for p in m.parameters():
-                p.grad = torch.zeros_like(p)
-            net = F32DuelingNet(m)
-            g = torch.Generator(device=cuda).manual_seed(5)
-            x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda, generator=g)
-            ws = F32Workspace(B, A, cuda, keep_for_backward=True)
-            net(x, ws)
-            dq = torch.randn(B, A, device=cuda, generator=g) / B
-            net.backward(dq, x, ws)
-            torch.cuda.synchronize()
-            outs.append([ws.a2.clone(), ws.a3.clone(), ws.h.clone(), ws.q.clone(), ws.dy3.clone(), ws.dy2.clone(),
-                         ws.dy1.clone()] + [p.grad.clone() for p in m.parameters()])
-    finally:
-        h.f32_set_x6(1)
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
