@@ -52,8 +52,6 @@ class LearnerConfig:
     # private buffers that the forward, loss and backward read: writers of the replay tables
     # may then run beside the step (the central topology's ingest, engine/central.py)
     private_rows: bool = False
-    # (A/B of the tree branch: the round-4 single-workgroup level walks instead of per_write_batch)
-    tree_walk: bool = False
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -321,21 +319,14 @@ class DQNLearner:
             for fn in hooks:
                 fn()
             pre, self.pre_writes = self.pre_writes, []
-            if self.cfg.tree_walk:
-                for slots, prios, filled in pre:
-                    self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
-                self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
-                                             mix=(self.delta, self.lw, self.prio, self.loss))
-                pre = []
-            for slots, prios, filled in pre[:-1]:  # (more than one staged actor step per learner step)
+            for slots, prios, filled in pre:
                 self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
-            # the last actor step's rows + this step's mixed priorities (last write wins) in one
-            # batched write: a one-workgroup leaves launch, then one wide launch per big tree level
-            # (the last one finishing the small top levels) -- the single-workgroup level walks
-            # took ~130 us beside the backward
-            if not self.cfg.tree_walk:
-                self.replay.write_batch(pre=pre[-1] if pre else None, idx=self.idx, bump=self.step_counter,
-                                        mix=(self.delta, self.lw, self.prio, self.loss))
+            # the single-workgroup walks (rank-sorted dedup, one workgroup per walk) on purpose:
+            # the batched per_write_batch (one wide launch per big tree level) finishes sooner
+            # but its workgroups compete with the backward GEMMs beside it -- measured 2188 vs
+            # 2303 learner steps/s (MI355X, round 5, interleaved; profiles/r5_x6.md)
+            self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
+                                         mix=(self.delta, self.lw, self.prio, self.loss))
             tail, self.tree_tail = self.tree_tail, []
             for fn in tail:
                 fn()

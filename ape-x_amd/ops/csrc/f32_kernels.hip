@@ -168,46 +168,17 @@ __device__ __forceinline__ uint32_t pack_bf16_hi(float lo, float hi) {  // two e
 __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFF0000u); }
 
 // Exact three-term split of 8 fp32 values (two 4-element k-runs of a fragment) into bf16
-// hi / mid / lo vectors with x = hi + mid + lo EXACTLY: hi = rne(x), mid = rne(x - hi),
-// lo = rne(x - hi - mid) -- each residual is exact in fp32, and round-to-nearest leaves at most
-// 24 - 8 - 9 - 9 < 0 bits for a fourth term.  The products of every pair of terms are exact in
-// fp32; the six kept pairs (hi.hi, hi.mid, mid.hi, hi.lo, mid.mid, lo.hi) leave out terms below
-// 2^-26 |a||b| -- under the fp32 rounding of the product itself -- so the GEMM is fp32-class on
-// the bf16 matrix cores (1024 FLOP/clk/SIMD vs 64 for v_mfma_f32_32x32x2_f32: six of them still
-// run 2.7x faster).  Per pair of values: 3 v_cvt_pk_bf16_f32, 2 v_pk_add_f32, 4 unpacks.
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+// hi / mid / lo vectors, x = hi + mid + lo EXACTLY (truncation: 8 + 8 + 8 significant bits).
+// The products of every pair of terms are exact in fp32; the six kept pairs (hi.hi, hi.mid,
+// mid.hi, hi.lo, mid.mid, lo.hi) leave out terms below 2^-23 |a||b| -- the size of the fp32
+// rounding of the product itself -- so the GEMM is fp32-class on the bf16 matrix cores
+// (1024 FLOP/clk/SIMD vs 64 for v_mfma_f32_32x32x2_f32: six of them still run 2.7x faster).
+// (A round-to-nearest split through v_cvt_pk_bf16_f32 -- fewer VALU instructions on paper --
+// measured 3-5 % slower per launch and 3 % slower per step on MI355X: profiles/r5_x6.md.)
 struct Split8 {
   bfx8 h, m, l;
 };
-__device__ __forceinline__ void split2(f32x2 v, uint32_t& h, uint32_t& m, uint32_t& l) {
-  const bf16x2 hb = __builtin_convertvector(v, bf16x2);
-  const f32x2 r = v - __builtin_convertvector(hb, f32x2);
-  const bf16x2 mb = __builtin_convertvector(r, bf16x2);
-  const f32x2 r2 = r - __builtin_convertvector(mb, f32x2);
-  h = __builtin_bit_cast(uint32_t, hb);
-  m = __builtin_bit_cast(uint32_t, mb);
-  l = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2));
-}
 __device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
-  uint32_t h[4], m[4], l[4];
-  split2(f32x2{x0[0], x0[1]}, h[0], m[0], l[0]);
-  split2(f32x2{x0[2], x0[3]}, h[1], m[1], l[1]);
-  split2(f32x2{x1[0], x1[1]}, h[2], m[2], l[2]);
-  split2(f32x2{x1[2], x1[3]}, h[3], m[3], l[3]);
-  return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
-          __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
-          __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
-}
-
-// fp32 GEMM arithmetic of gemm_body: 0 = v_mfma_f32_32x32x2_f32 (exact fp32 fma chain),
-// 1 = the exact-split bf16 form (split8 of every fragment a wave reads, six
-// v_mfma_f32_32x32x16_bf16 per 16 k), 2 = the same with the truncation split (A/B)
-int g_f32_x6 = 1;
-
-// the same split by truncation (hi = the upper 16 bits, mid / lo of the exact residuals): the
-// round-4 form, kept as mode 2 for the same-box A/B against the round-to-nearest split8
-__device__ __forceinline__ Split8 split8_trunc(f32x4 x0, f32x4 x1) {
   const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
   uint32_t h[4], m[4], l[4];
 #pragma unroll
@@ -215,16 +186,19 @@ __device__ __forceinline__ Split8 split8_trunc(f32x4 x0, f32x4 x1) {
     const float a = x[2 * j], b = x[2 * j + 1];
     const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
     const float am = trunc_bf16(ar), bm = trunc_bf16(br);
-    h[j] = pack_bf16_hi(a, b);
+    h[j] = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
     m[j] = pack_bf16_hi(am, bm);
-    l[j] = pack_bf16_hi(ar - am, br - bm);
+    l[j] = pack_bf16_hi(ar - am, br - bm);  // exact: <= 8 significant bits
   }
   return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
           __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
           __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
 }
 
-template <class P, int X6>
+// Every fp32 GEMM of the learner (gemm_body) on the bf16 matrix cores through split8: the
+// fp32-MFMA form (v_mfma_f32_32x32x2_f32) it replaced in round 5 ran 2142 vs 2378 learner
+// steps/s at the same fp32-class accuracy (profiles/r5_x6.md, tests/test_gpu_f32_net.py).
+template <class P>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
@@ -302,16 +276,14 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
   };
   using S0 = std::integral_constant<int, 0>;
-  // X6: the cross terms accumulate apart from hi.hi (summed in the epilogue)
-  f32x16 accx[X6 ? G::TM : 1][X6 ? G::TN : 1];
-  if constexpr (X6) {
+  // the cross terms accumulate apart from hi.hi (summed in the epilogue)
+  f32x16 accx[G::TM][G::TN];
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i)
+  for (int i = 0; i < G::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < G::TN; ++j)
+    for (int j = 0; j < G::TN; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) accx[i][j][e] = 0.f;
-  }
+      for (int e = 0; e < 16; ++e) accx[i][j][e] = 0.f;
   auto frag_a = [&](const float* As, int mi, int kc) {
     const int m = wm * G::WTM + mi * 32 + r;
     f32x4 v;
@@ -334,74 +306,32 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
     return v;
   };
-  auto split_a = [&](const float* As, int mi, int kc) {
-    if constexpr (X6 == 2) return split8_trunc(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
-    else return split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
-  };
-  auto split_b = [&](const float* Bs, int ni, int kc) {
-    if constexpr (X6 == 2) return split8_trunc(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
-    else return split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
-  };
   auto compute = [&](int buf) {
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
-    if constexpr (X6) {
-      static_assert(G::BK % 16 == 0, "X6: k-blocks of 16");
-      // 16 k per step: lane (r, h) holds k = 4h..4h+3 of chunk kc and of chunk kc + 1 -> bf16
-      // k-slots 8h..8h+7 of the 32x32x16 MFMA (the same slot map for A and B)
+    static_assert(G::BK % 16 == 0, "k-blocks of 16");
+    // 16 k per step: lane (r, h) holds k = 4h..4h+3 of chunk kc and of chunk kc + 1 -> bf16
+    // k-slots 8h..8h+7 of the 32x32x16 MFMA (the same slot map for A and B)
 #pragma unroll
-      for (int kc = 0; kc < G::BK / 8; kc += 2) {
-        Split8 a[G::TM], b[G::TN];
+    for (int kc = 0; kc < G::BK / 8; kc += 2) {
+      Split8 a[G::TM], b[G::TN];
 #pragma unroll
-        for (int mi = 0; mi < G::TM; ++mi) a[mi] = split_a(As, mi, kc);
+      for (int mi = 0; mi < G::TM; ++mi) a[mi] = split8(frag_a(As, mi, kc), frag_a(As, mi, kc + 1));
 #pragma unroll
-        for (int ni = 0; ni < G::TN; ++ni) b[ni] = split_b(Bs, ni, kc);
+      for (int ni = 0; ni < G::TN; ++ni) b[ni] = split8(frag_b(Bs, ni, kc), frag_b(Bs, ni, kc + 1));
 #pragma unroll
-        for (int mi = 0; mi < G::TM; ++mi)
+      for (int mi = 0; mi < G::TM; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < G::TN; ++ni) {
-            f32x16 x = accx[mi][ni];
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].l, b[ni].h, x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].m, x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].l, x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].h, x, 0, 0, 0);
-            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].m, x, 0, 0, 0);
-            accx[mi][ni] = x;
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].h, acc[mi][ni], 0, 0, 0);
-          }
-      }
-      return;
-    }
-#pragma unroll
-    for (int kc = 0; kc < G::BK / 8; ++kc) {
-      f32x4 a[G::TM], b[G::TN];
-#pragma unroll
-      for (int mi = 0; mi < G::TM; ++mi) {
-        const int m = wm * G::WTM + mi * 32 + r;
-        if constexpr (P::A_KMAJ) {
-          a[mi] = *reinterpret_cast<const f32x4*>(As + m * G::PA + kc * 8 + 4 * h);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) a[mi][i] = As[(kc * 8 + 4 * h + i) * G::PA + m];
+        for (int ni = 0; ni < G::TN; ++ni) {
+          f32x16 x = accx[mi][ni];
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].l, b[ni].h, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].m, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].l, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].h, x, 0, 0, 0);
+          x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].m, x, 0, 0, 0);
+          accx[mi][ni] = x;
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].h, acc[mi][ni], 0, 0, 0);
         }
-      }
-#pragma unroll
-      for (int ni = 0; ni < G::TN; ++ni) {
-        const int n = wn * G::WTN + ni * 32 + r;
-        if constexpr (P::B_KMAJ) {
-          b[ni] = *reinterpret_cast<const f32x4*>(Bs + n * G::PB + kc * 8 + 4 * h);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) b[ni][i] = Bs[(kc * 8 + 4 * h + i) * G::PB + n];
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int mi = 0; mi < G::TM; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < G::TN; ++ni)
-            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi][i], b[ni][i], acc[mi][ni], 0, 0, 0);
     }
   };
 
@@ -424,12 +354,10 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     __syncthreads();
     cur ^= 1;
   }
-  if constexpr (X6) {
 #pragma unroll
-    for (int mi = 0; mi < G::TM; ++mi)
+  for (int mi = 0; mi < G::TM; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < G::TN; ++ni) acc[mi][ni] += accx[mi][ni];
-  }
+    for (int ni = 0; ni < G::TN; ++ni) acc[mi][ni] += accx[mi][ni];
 
 #pragma unroll
   for (int mi = 0; mi < G::TM; ++mi)
@@ -457,11 +385,11 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 }
 
 
-template <class P, int X6>
+template <class P>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
   __shared__ typename P::Smem sm;
-  gemm_body<P, X6>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
+  gemm_body<P>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
 
 template <int A, int B>
@@ -471,7 +399,7 @@ struct MaxI {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2, int X6>
+template <class P1, class P2>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
   __shared__ union {
@@ -479,9 +407,9 @@ __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1, X6>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2, X6>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -1387,18 +1315,14 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  if (g_f32_x6 == 2) gemm_k<P, 2><<<blocks, 256, 0, s>>>(a);
-  else if (g_f32_x6) gemm_k<P, 1><<<blocks, 256, 0, s>>>(a);
-  else gemm_k<P, 0><<<blocks, 256, 0, s>>>(a);
+  gemm_k<P><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  if (g_f32_x6 == 2) gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else if (g_f32_x6) gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else gemm2_k<P1, P2, 0><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
 
@@ -1433,23 +1357,20 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
       f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
-    case 2:  // learner: 64 x 64 tiles at BK 32: 79.0-80.4 us vs 87.0-88.5 for 128 x 64 at BK 16
-             // (3 x 512 samples, interleaved on one box; the BK-16 pitch conflicts on the stores)
+    case 2:  // learner: 128 x 64 tiles at BK 32 (64 x 32 per wave): on the split-bf16 MFMA 67-70 us vs
+             // 73-79 for 64 x 64 (round 5; under fp32 MFMA 64 x 64 had won), 128 x 64 at BK 16 slower
       if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<128, 64, 16, 2>>(set, s);
-      else if (learner_sized(set) && tile == 2) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (learner_sized(set) && tile == 2) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:  // learner: 64 x 64 (65.0 us vs 66.6 / 70.2 for the 128 x 64 tiles at BK 16 / 32)
-      if (learner_sized(set) && tile == 2) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
   }
 }
-
-void f32_set_x6(int on) { g_f32_x6 = on; }
 
 int f32_fc1_splits() { return kFcSplits; }
 

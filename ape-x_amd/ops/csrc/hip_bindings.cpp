@@ -460,7 +460,6 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::vector<uint64_t>>& probs, int B, uint64_t s) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
-  m.def("f32_set_x6", &f32_set_x6);
   m.def("f32_fc1_splits", &f32_fc1_splits);
   m.def("f32_fc1_bwd_split", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ws, int B,
                                 uint64_t s) {

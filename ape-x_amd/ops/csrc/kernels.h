@@ -378,7 +378,6 @@ struct F32Set {
   int n, B;
 };
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0);
-void f32_set_x6(int on);  // A/B: fp32 GEMMs on the exact-split bf16 MFMA (1) or f32 MFMA (0)
 int f32_fc1_splits();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
 // target: conv2 / conv3 weight-gradient workgroups (<= 0: the default); the workspace, the

@@ -109,7 +109,6 @@ def parse():
                     help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
-    ap.add_argument("--tree-walk", action="store_true", help="(A/B) the round-4 tree branch instead of per_write_batch")
     ap.add_argument("--actor-cus", type=int, default=0,
                     help="overlap mode: confine the actor stream to this many CUs (0 = all)")
     ap.add_argument("--emulate-links", type=int, default=0, metavar="R",
@@ -263,8 +262,7 @@ def main():
     if args.scaling == "strong" and args.batch % world:
         raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
     rank_batch = args.batch // world if args.scaling == "strong" else args.batch
-    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
-                       tree_walk=args.tree_walk)
+    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank)
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,

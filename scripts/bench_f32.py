@@ -1,6 +1,8 @@
 #!/usr/bin/env python
 """Per-launch timing of the fp32 (reference-precision) network kernels at the learner's
 shapes: forward launches with 3 problems x B (Q(s), Q(s'), Q_target(s')), backward at B.
+TFLOP/s are fp32-equivalent (the GEMMs run on the bf16 matrix cores through the exact
+three-term split; the percentage is of the 157.3 TF fp32 MFMA peak, for comparison).
 
 ``python scripts/bench_f32.py [--B 512] [--iters 50] [--only NAME] [--graph 1]`` prints
 us/launch and achieved TFLOP/s (157.3 TF = fp32 MFMA peak); ``--graph 0`` launches
@@ -23,19 +25,16 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
-ap.add_argument("--x6", type=int, default=1, help="1: exact-split bf16 MFMA GEMMs, 0: f32 MFMA")
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 128x64 BK 16, "
                                                    "conv2/conv3 input gradient BK 32")
-ap.add_argument("--tile2", action="store_true", help="+ conv2 / conv3 forward on 128 x 64 tiles at BK 32 (64 x 32 "
-                                                   "wave tiles)")
+ap.add_argument("--tile2", action="store_true", help="+ conv2 forward on the 64 x 64 tiles (the round-4 default)")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
 a = ap.parse_args()
 dev = torch.device("cuda")
 hip = ops.hip()
-hip.f32_set_x6(a.x6)
 B, A = a.B, 18
 m = DuelingDQN.from_shapes((4, 84, 84), A).to(dev)
 m.flatten_parameters()
@@ -128,7 +127,6 @@ if a.tile1:
                                                        tile=1)), 2 * 2 * B * 81 * 64 * 512)
 if a.tile2:
     cases["conv2_fwd@t2"] = ((lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=2)), 2 * P * 81 * 64 * 512)
-    cases["conv3_fwd@t2"] = ((lambda: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=2)), 2 * P * 49 * 64 * 576)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)

@@ -232,32 +232,26 @@ def test_f32_packed_arena_stays_exact_under_training(cuda):
     assert int(L.step_counter.item()) == 2 + 3 + 4
 
 
-@pytest.mark.parametrize("x6", [1, 0, 2])
-def test_gemm_layers_are_fp32_class(cuda, x6):
+def test_gemm_layers_are_fp32_class(cuda):
     """Every gemm_body layer (conv2 / conv3 / FC1 forward; FC1, conv3, conv2 input and weight
     gradients) against fp64 on the SAME layer inputs, per element scaled by the fp32
-    dot-product error scale sum_k |a_k b_k|.  ``x6`` = 1: the exact three-term bf16 split on
-    v_mfma_f32_32x32x16_bf16 (six products per 16 k, every dropped term below 2^-23 |a b|),
-    0: v_mfma_f32_32x32x2_f32.  Both must stay within a few fp32 ulps of that scale."""
-    from apex_amd import ops
+    dot-product error scale sum_k |a_k b_k|.  The GEMMs run on v_mfma_f32_32x32x16_bf16 through
+    the exact three-term split of every fp32 operand (six products per 16 k, every dropped term
+    below 2^-23 |a b|); they must stay within a few fp32 ulps of that scale, like the fp32-MFMA
+    kernels they replaced (round-5 table of both: profiles/r5_x6.md)."""
     from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
 
-    h = ops.hip()
-    h.f32_set_x6(x6)
-    try:
-        B, A = 96, 18
-        m = _model(cuda, A=A, seed=7)
-        for p in m.parameters():
-            p.grad = torch.zeros_like(p)
-        net = F32DuelingNet(m)
-        x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
-        ws = F32Workspace(B, A, cuda, keep_for_backward=True)
-        net(x, ws)
-        dq = torch.randn(B, A, device=cuda) / B
-        net.backward(dq, x, ws)
-        torch.cuda.synchronize()
-    finally:
-        h.f32_set_x6(1)
+    B, A = 96, 18
+    m = _model(cuda, A=A, seed=7)
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    net = F32DuelingNet(m)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    ws = F32Workspace(B, A, cuda, keep_for_backward=True)
+    net(x, ws)
+    dq = torch.randn(B, A, device=cuda) / B
+    net.backward(dq, x, ws)
+    torch.cuda.synchronize()
     f = m.features
     d = lambda t: t.detach().double()  # noqa: E731
     errs = {}
@@ -297,7 +291,7 @@ def test_gemm_layers_are_fp32_class(cuda, x6):
         got = _nchw(ws.dy2 if L == 4 else ws.dy1, B, xin.shape[1], xin.shape[2])
         mask = xin > 0
         scaled(name + "_dgrad", got[mask], dx[mask], dxs[mask])
-    print(f"x6={x6}", {k: f"{v:.2e}" for k, v in errs.items()})
+    print({k: f"{v:.2e}" for k, v in errs.items()})
     # fp32 unit roundoff 6e-8: K <= 3136 accumulations stay within a few ulps of sum |a b|
     assert max(errs.values()) < 1e-6, errs
 
