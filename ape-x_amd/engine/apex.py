@@ -60,9 +60,6 @@ class EngineConfig:
     # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
     # staging half, instead of three phase graphs with eager collectives in between
     dp_graph: bool = False
-    # overlap mode: the actor stream confined to this many CUs (spread evenly over the XCDs;
-    # 0 = every CU) so its small-grid kernels stop stretching the learner's
-    actor_cus: int = 0
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
 
@@ -80,20 +77,6 @@ def reserve_actor_stream(device) -> None:
     dev = torch.device(device)
     if dev not in _RESERVED:
         _RESERVED[dev] = torch.cuda.Stream(device=dev)
-
-
-def cu_masked_stream(device, n_cus: int):
-    """A torch stream over a HIP stream restricted to ``n_cus`` CUs, spread evenly over the
-    device's CUs (the XCDs' share kept equal).  The stream lives as long as the process."""
-    dev = torch.device(device)
-    total = torch.cuda.get_device_properties(dev).multi_processor_count
-    n = max(1, min(int(n_cus), total))
-    words = [0] * (-(-total // 32))
-    for k in range(n):
-        c = (k * total) // n
-        words[c // 32] |= 1 << (c % 32)
-    h = ops.hip().stream_with_cu_mask(dev.index or 0, words)
-    return torch.cuda.ExternalStream(h, device=dev)
 
 
 class ApexEngine:
@@ -147,8 +130,6 @@ class ApexEngine:
         # its pool streams, else the next pool stream
         self._astream = (_RESERVED.pop(self.device, None) or torch.cuda.Stream(device=self.device)) if self.overlap \
             else None
-        if self.overlap and cfg.actor_cus:
-            self._astream = cu_masked_stream(self.device, cfg.actor_cus)
         self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()] if self.overlap else None
         self._ev_learn = torch.cuda.Event() if self.overlap else None
 

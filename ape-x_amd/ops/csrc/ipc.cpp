@@ -40,20 +40,6 @@ struct IpcIngestHandle {
 }  // namespace
 
 void register_ipc(py::module_& m) {
-  // a stream whose kernels run only on the CUs set in `mask` (bit i = CU i; 32 CUs per word):
-  // the overlapped actor graph confined to a CU subset beside the learner (engine/apex.py)
-  m.def("stream_with_cu_mask", [](int device, std::vector<uint32_t> mask) {
-    if (mask.empty()) throw std::invalid_argument("stream_with_cu_mask: empty mask");
-    int prev = 0;
-    hip_ok(hipGetDevice(&prev), "hipGetDevice");
-    hip_ok(hipSetDevice(device), "hipSetDevice");
-    hipStream_t s = nullptr;
-    const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
-    hip_ok(hipSetDevice(prev), "hipSetDevice");
-    hip_ok(e, "hipExtStreamCreateWithCUMask");
-    return U(s);
-  });
-  m.def("stream_destroy", [](uint64_t s) { hip_ok(hipStreamDestroy(S(s)), "hipStreamDestroy"); });
   // mode 0: plain device memory (L2-cached), 1: fine-grained, 2: uncached (every access
   // bypasses L2: the right mode for memory that peers write over xGMI while this GPU reads it)
   m.def("ipc_alloc", [](int64_t bytes, int mode) {

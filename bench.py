@@ -109,8 +109,6 @@ def parse():
                     help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
-    ap.add_argument("--actor-cus", type=int, default=0,
-                    help="overlap mode: confine the actor stream to this many CUs (0 = all)")
     ap.add_argument("--emulate-links", type=int, default=0, metavar="R",
                     help="one GPU: the central learner (rank 0) with R actor links emulated in-process (synthetic "
                          "packets into the real IPC ring, the real in-graph ingest): its load at N = R + 1 GPUs")
@@ -267,7 +265,7 @@ def main():
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
                        use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
-                       actor_cus=args.actor_cus, learner=lc)
+                       learner=lc)
     dp = world > 1 or args.force_dp
     allreduce = None
     if dp and args.comm == "rccl" and args.backend == "nccl":
@@ -370,7 +368,7 @@ def main():
                 "forward": args.forward,
                 "fp32_gemms": "exact 3-term bf16 split (x6) on MFMA, fp32 accumulate" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
-                "actor_learner_overlap": args.overlap, "actor_cus": args.actor_cus or None,
+                "actor_learner_overlap": args.overlap,
                 "dp_graph": eng._g_dp is not None,
                 # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
                 # gradient communicator, else the torch.distributed group size

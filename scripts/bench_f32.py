@@ -29,6 +29,7 @@ ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradi
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 128x64 BK 16, "
                                                    "conv2/conv3 input gradient BK 32")
 ap.add_argument("--tile2", action="store_true", help="+ conv2 forward on the 64 x 64 tiles (the round-4 default)")
+ap.add_argument("--tiles", default="", help="extra conv2 / conv3 forward cases at these tile ids, e.g. 3,4,5")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
@@ -127,6 +128,9 @@ if a.tile1:
                                                        tile=1)), 2 * 2 * B * 81 * 64 * 512)
 if a.tile2:
     cases["conv2_fwd@t2"] = ((lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=2)), 2 * P * 81 * 64 * 512)
+for t in [int(x) for x in a.tiles.split(",") if x]:  # forward tile alternatives (f32_conv_fwd_multi ``tile``)
+    cases[f"conv2_fwd@t{t}"] = ((lambda t=t: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=t)), 2 * P * 81 * 64 * 512)
+    cases[f"conv3_fwd@t{t}"] = ((lambda t=t: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=t)), 2 * P * 49 * 64 * 576)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)

@@ -6,6 +6,15 @@ R=$(pwd)
 O=$R/gpurun_out/r5b
 mkdir -p $O
 export PYTHONUNBUFFERED=1
+timeout -k 10 300 python -u -m pytest -x -q -s --timeout 120 --timeout-method thread tests/test_gpu_f32_net.py tests/test_gpu_learner.py \
+  > $O/test.log 2>&1; rc=$?; echo "== tests rc=$rc"; grep -E "conv2_fwd|passed|failed|Error" $O/test.log | head
+[ $rc -ne 0 ] && exit $rc
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --steps 2000 --warmup 50 > $O/bench_$i.log 2>&1 || exit $?
+  echo "== bench $i $(grep '^{' $O/bench_$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+done
+timeout -k 10 120 python scripts/bench_f32.py --tile2 > $O/bench_f32.log 2>&1 || exit $?
+grep -v amdgpu.ids $O/bench_f32.log
 bash scripts/gpu_pmc_r4.sh > $O/pmc.log 2>&1; rc=$?; echo "== pmc rc=$rc"; tail -14 $O/pmc.log
 [ $rc -ne 0 ] && exit $rc
 for rep in 1 2; do
