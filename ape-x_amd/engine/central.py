@@ -177,13 +177,18 @@ class CentralApexEngine:
 
                 self.emu = EmulatedActorLinks(self.links, self.C_r, self.F_r, cfg.n_actions, seed=cfg.seed)
                 self._estream = torch.cuda.Stream(device=self.device)
+                self._ev_step = torch.cuda.Event()  # the previous learner step (its ingest freed credit)
+                self._ev_step.record(torch.cuda.current_stream(self.device))
         else:
             self._setup_actor_link()
 
     # ------------------------------------------------------------------ setup
     def _emu_push(self) -> None:
-        """Emulated links: every link's next paced packet, on the emulators' own stream."""
+        """Emulated links: every link's next packet, on the emulators' own stream, after the
+        previous learner step (whose ingest returned the credit) -- a paced actor pushes as
+        soon as its credit window opens, so each link delivers one packet per learner step."""
         if self.emu is not None:
+            self._estream.wait_event(self._ev_step)
             with torch.cuda.stream(self._estream):
                 self.emu.push()
 
@@ -361,6 +366,8 @@ class CentralApexEngine:
             self._g_learn.replay()
         else:
             self._learner_body()
+        if self.emu is not None:
+            self._ev_step.record(torch.cuda.current_stream(self.device))
         self.learn_steps += 1
         if self.learn_steps % self.cfg.target_update_interval == 0:
             self.learner.sync_target()

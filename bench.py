@@ -621,7 +621,7 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
         "packets_applied_per_learner_step": round(packets / args.steps, 3),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
         "links_complete": all(links["applied"][r] == links.get("sent", {}).get(r, links["applied"][r]) for r in links["live"]),
-        "transport": eng.transport, "transport_fallback": args.transport_fallback,
+        "transport": eng.transport, "transport_fallback": getattr(args, "transport_fallback", None),
         "preflight": pre,
         "timing": "rank 0 (the one learner) between two device syncs; actor ranks act continuously",
         "last_loss": round(st["loss"], 6), "last_grad_norm_l2": round(st["grad_norm_l2"], 6),
