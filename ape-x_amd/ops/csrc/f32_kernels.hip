@@ -1357,18 +1357,15 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
       f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
       LAUNCH_CHECK();
       break;
-    case 2:  // learner: 256 x 64 tiles at BK 16 (64 x 64 per wave: each split fragment feeds 12 MFMAs);
-             // on the split-bf16 MFMA 64.4-65.4 us vs 66-70 for 128 x 64 at BK 32 (64 x 32 per wave) and
-             // 73-79 for 64 x 64 (round 5; under fp32 MFMA 64 x 64 had won); BK 32 the same time at
-             // twice the LDS (92 KB)
-      if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else if (learner_sized(set) && tile == 2) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv2FwdT<256, 64, 16, 4>>(set, s);
+    case 2:  // learner: 128 x 64 tiles at BK 32 (64 x 32 per wave): on the split-bf16 MFMA 66.6-67.5 us
+             // vs 73-79 for 64 x 64 (under fp32 MFMA 64 x 64 had won) and 76-88 for 256 x 64 (64 x 64
+             // per wave: one wave per SIMD); whole step 2456-2466 vs 2193-2200 steps/s for 256 x 64
+      if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
-    case 3:  // learner: 256 x 64 at BK 16 (48.0-48.3 us vs 49.1-49.8 for 64 x 64; 128 x 64 48.0-48.4)
-      if (learner_sized(set) && tile == 2) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
-      else if (learner_sized(set)) fwd_launch<Conv3FwdT<256, 64, 16, 4>>(set, s);
+    case 3:  // learner: 64 x 64 (46.7-46.8 us vs 80.6-84.5 for 256 x 64)
+      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");

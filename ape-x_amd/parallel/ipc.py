@@ -284,10 +284,11 @@ class IpcLearnerLinks:
                       s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
                       done=rp.done.data_ptr(), frame_base=fb.data_ptr(), slot_base=sb.data_ptr())
         def tree_write(slots, prios):  # ring-ordered new rows (slot -1: nothing there)
-            if slots.numel() <= 2048:  # (the paced ingest: R x E rows) batched leaves + one wide launch per level
-                rp.write_batch(pre=(slots, prios, None))
-            else:  # (the drain's R x D x E rows, untimed)
-                rp.write_priorities(slots, prios, dedup=False)
+            # one-workgroup fused writes (leaves + every level) of <= 1024 rows each: they run on
+            # the learner's tree stream beside the conv backward, where wide per-level launches
+            # slow the backward's GEMMs (profiles/r5_x6.md, learner tree branch)
+            for k in range(0, slots.numel(), 1024):
+                rp.write_priorities(slots[k:k + 1024], prios[k:k + 1024], dedup=False)
 
         links = cls(R, D, E, P, store, prefix, device, packet_nbytes=packet_bytes(E), tables=tables,
                     tree_write=tree_write, **kw)
