@@ -36,12 +36,19 @@ def _central_aql_body(rank, world, iters):
         dist.send(torch.tensor([allp.shape[0]]), 0)
         dist.send(allp, 0)
         return {"steps": eng.actor_steps, "sent": eng.link.n_sent, "version": eng.param_version}
+    import time
+
     eng.fill()
     a0, s0 = sum(eng.applied.values()), eng.sgd_steps()
     eng.capture()
-    for _ in range(iters):
+    # the learner never waits for data (a ~0.2 ms iteration outruns the actor processes): run
+    # until the links have delivered enough packets, paced a little so the actors keep up
+    deadline, it = time.monotonic() + 90, 0
+    while it < iters or (sum(eng.applied.values()) - a0 < iters and time.monotonic() < deadline):
         eng.iteration()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        time.sleep(0.002)
+        it += 1
     a1, s1 = sum(eng.applied.values()), eng.sgd_steps()
     st = eng.eng.learner.stats()
     links = eng.close()
