@@ -25,6 +25,7 @@ ap.add_argument("--only", default=None)
 ap.add_argument("--B", type=int, default=512)
 ap.add_argument("--graph", type=int, default=1)
 ap.add_argument("--json", action="store_true")
+ap.add_argument("--rounds", type=int, default=1, help="time every case this many times, round-robin; report the median")
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 64x64, "
                                                    "conv2/conv3 input gradient BK 32")
@@ -142,31 +143,42 @@ for _ in range(5):  # clocks up and caches warm before the first timed case (it 
     for name, fn, flop in runs:
         fn()
 torch.cuda.synchronize()
-for name, fn, flop in runs:
-    fn()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if a.graph:
+graphs = {}
+if a.graph:
+    for name, fn, flop in runs:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             for _ in range(a.iters):
                 fn()
         g.replay()
-        torch.cuda.synchronize()
-        e0.record()
-        g.replay()
-        e1.record()
-    else:
-        e0.record()
-        for _ in range(a.iters):
-            fn()
-        e1.record()
+        graphs[name] = g
     torch.cuda.synchronize()
-    us = 1000.0 * e0.elapsed_time(e1) / a.iters
+times = {name: [] for name, _, _ in runs}
+for _ in range(a.rounds):  # round-robin: clock / thermal drift hits every case alike
+    for name, fn, flop in runs:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if a.graph:
+            e0.record()
+            graphs[name].replay()
+            e1.record()
+        else:
+            fn()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.iters):
+                fn()
+            e1.record()
+        torch.cuda.synchronize()
+        times[name].append(1000.0 * e0.elapsed_time(e1) / a.iters)
+for name, fn, flop in runs:
+    ts = sorted(times[name])
+    us = ts[len(ts) // 2]
     res[name] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1), "pct_peak": round(flop / us / 1e6 / 1.573, 1)}
     if not a.json:
         mm = " MISMATCH" if name in mismatch else ""
-        print(f"{name:12s}{mm} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)")
+        spread = f"  [{ts[0]:.1f}-{ts[-1]:.1f}]" if len(ts) > 1 else ""
+        print(f"{name:12s}{mm} {us:8.2f} us  {flop / us / 1e6:6.1f} TFLOP/s  ({flop / us / 1e6 / 1.573:4.1f}% of 157.3)"
+              f"{spread}")
 if a.json:
     print(json.dumps(res))
 tot = sum(r["us"] for r in res.values())
