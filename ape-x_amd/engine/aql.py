@@ -193,6 +193,10 @@ class AQLEngineConfig:
     # learner forward: candidate-tile groups per (sample, net) workgroup (0 = about one workgroup
     # per CU: the ~110 KB weight staging, the PER draw and the state MLP serve a group of tiles)
     fwd_tile_groups: int = 0
+    # serial acting tail in one launch (aql_act_tail: eps-greedy select + env step + ring tree
+    # write + counter bumps + the learner's PER beta) instead of select, env step, ring write
+    # and a host beta fill; False = the separate launches (the bit-identity baseline)
+    fused_acting: bool = True
     seed: int = 0
 
 
@@ -573,6 +577,20 @@ class AQLEngine:
             self._astream = torch.cuda.Stream(device=dev)
             self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()]
             self._ev_learn = torch.cuda.Event()
+        # the serial engine's fused acting tail (aql_act_tail); it also writes the learner's PER
+        # beta for the iteration from a device iteration counter (AQL_dis.py:59)
+        self._tail = None
+        if cfg.fused_acting and not self.overlap and E <= 1024:
+            r = self.replay
+            self._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._iter_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._tail = h.make_aql_tail(self.env, self.ins, r.tree, dict(
+                q=self.qbuf.data_ptr(), amu=self.amu.data_ptr(), eps=self.eps.data_ptr(), sel_seed=self.seed ^ 0xA9C1,
+                act_idx=self.act_idx.data_ptr(), env_act=self.env_act.data_ptr(), alpha=float(r.alpha),
+                max_prio=r.max_prio.data_ptr(), filled=r.filled.data_ptr(), counter=self.actor_ctr.data_ptr(),
+                ticket=self._ticket.data_ptr(), beta_out=self.learner.beta.data_ptr(), iter=self._iter_dev.data_ptr(),
+                beta0=float(cfg.beta_start), beta_omb=1.0 - cfg.beta_start, beta_max_step=float(cfg.max_step),
+                beta_workers=float(cfg.n_workers)))
         self.actor_net = FusedAQL(self.actor_model)._net()
         # acting on the learner's MFMA candidate forward (online net, s only, row = env index)
         # (64 acting workgroups beside the learner in overlap mode: most CUs stay the learner's)
@@ -602,6 +620,10 @@ class AQLEngine:
         ``AqlInsert`` of E rows (C = E) to write them to instead -- e.g. a central-topology
         actor rank's packet buffer (engine.central_aql); no tree write then."""
         h, s, E, r = self.hip, self._s(), self.E, self.replay
+        if into is None and half is None and self._tail is not None:
+            self._propose_q(h, s, E)
+            h.aql_act_tail(self._tail, s)
+            return
         self._act(h, s, E)
         if into is not None or half is not None:
             dst = into if into is not None else self._stage_ins[half]
@@ -612,14 +634,18 @@ class AQLEngine:
         h.per_write_leaves(r.tree, self.slots.data_ptr(), 0, E, r.alpha, r.max_prio.data_ptr(), 0,
                            r.sorted_scratch.data_ptr(), r.filled.data_ptr(), E, self.actor_ctr.data_ptr(), 1, s)
 
-    def _act(self, h, s, E) -> None:
-        """Proposal, candidate Q (the learner's MFMA candidate forward on the online net, s only)
-        and epsilon-greedy selection for all E envs."""
+    def _propose_q(self, h, s, E) -> None:
+        """Proposal and candidate Q (the learner's MFMA candidate forward on the online net, s
+        only) for all E envs."""
         # (the effective NoisyNet weights ride along in the proposal launch)
         h.aql_propose(self.actor_net, self.obs_buf.data_ptr(), E, self.low.data_ptr(), self.high.data_ptr(),
                       self.var.data_ptr(), self.seed ^ 0x9909, self.actor_ctr.data_ptr(), self.amu.data_ptr(), 0, s,
                       self.ws.data_ptr())
         h.aql_act_q(self.actL, s)
+
+    def _act(self, h, s, E) -> None:
+        """Proposal, candidate Q and epsilon-greedy selection for all E envs."""
+        self._propose_q(h, s, E)
         h.aql_select(self.qbuf.data_ptr(), self.amu.data_ptr(), E, self.T, self.adim, self.eps.data_ptr(),
                      self.seed ^ 0xA9C1, self.actor_ctr.data_ptr(), self.act_idx.data_ptr(), self.env_act.data_ptr(), s)
 
@@ -657,6 +683,8 @@ class AQLEngine:
             return
         for _ in range(n):
             self.actor_step()
+        if self._tail is not None:  # the device iteration counter of the fused tail's beta
+            self._iter_dev.fill_(self.iterations)
         self.publish()
 
     def capture(self) -> None:
@@ -696,7 +724,8 @@ class AQLEngine:
         """One actor step of all envs, weight publish, K learner steps."""
         if self.overlap:
             return self._iteration_overlap()
-        self.learner.beta.fill_(self._beta())
+        if self._tail is None:  # (the fused acting tail writes it on the device)
+            self.learner.beta.fill_(self._beta())
         if self._g_actor is not None:
             self._g_actor.replay()
         else:

@@ -1031,14 +1031,12 @@ __global__ __launch_bounds__(256) void aql_env_reset_k(AqlEnv V) {
   env_reset_one(V, e, threadIdx.x & 63, 0xFFFFFFFFull);
 }
 
-__global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __restrict__ act,
-                                                      const int* __restrict__ act_idx, const float* __restrict__ amu,
-                                                      AqlInsert I) {
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= V.E) return;
-  const uint64_t ctr = (uint64_t)V.counter[0];
-  const int64_t slot = (I.filled[0] + e) % I.C;
+// One env's step by one wave: dynamics, reward, the raw transition into replay slot `slot`,
+// episode bookkeeping / reset.  `a`: this env's action vector (adim floats; the discrete envs'
+// action index as a float), `aidx`: its candidate index.
+__device__ __forceinline__ void env_step_wave(const AqlEnv& V, int e, int lane, const float* a_in, int aidx,
+                                              const float* __restrict__ amu, const AqlInsert& I, int64_t slot,
+                                              uint64_t ctr) {
   const int obs = V.obs;
   const float* s = V.obs_buf + (size_t)e * obs;
   float s2 = 0.f, r = 0.f;
@@ -1047,7 +1045,7 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
     float a[kBwAct], pen = 0.f;
 #pragma unroll
     for (int d = 0; d < kBwAct; ++d) {
-      a[d] = fminf(fmaxf(act[(size_t)e * kBwAct + d], -1.f), 1.f);
+      a[d] = fminf(fmaxf(a_in[d], -1.f), 1.f);
       pen += fabsf(a[d]);
     }
     if (lane < kBwObs) {
@@ -1067,7 +1065,7 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
   } else if (V.kind == 1) {  // CartPole (Barto et al. 1983; envs/classic.py CartPoleEnv)
     float* ph = V.phys + (size_t)e * 4;
     const float x = ph[0], xd = ph[1], th = ph[2], thd = ph[3];
-    const float force = ((int)act[e] == 1) ? 10.f : -10.f;
+    const float force = ((int)a_in[0] == 1) ? 10.f : -10.f;
     const float ct = cosf(th), sn = sinf(th);
     const float tmp = (force + 0.05f * thd * thd * sn) / 1.1f;
     const float tha = (9.8f * sn - ct * tmp) / (0.5f * (4.f / 3.f - 0.1f * ct * ct / 1.1f));
@@ -1081,7 +1079,7 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
   } else {  // Pendulum (envs/classic.py PendulumEnv)
     float* ph = V.phys + (size_t)e * 4;
     const float th = ph[0], thd = ph[1];
-    const float u = fminf(fmaxf(act[e], -2.f), 2.f);
+    const float u = fminf(fmaxf(a_in[0], -2.f), 2.f);
     const float an = remainderf(th, 6.2831853f);  // normalised angle in [-pi, pi]
     const float cost = an * an + 0.1f * thd * thd + 0.001f * u * u;
     float nthd = thd + (-3.f * 10.f / 2.f * sinf(th + 3.14159265f) + 3.f * u) * 0.05f;
@@ -1106,7 +1104,7 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
   const int TA = V.T * V.adim;
   for (int k = lane; k < TA; k += 64) I.amu[slot * TA + k] = amu[(size_t)e * TA + k];
   if (lane == 0) {
-    I.act[slot] = act_idx[e];
+    I.act[slot] = aidx;
     I.rew[slot] = r;
     I.done[slot] = done ? 1.f : 0.f;
     I.slots[e] = (int)slot;
@@ -1126,6 +1124,103 @@ __global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __r
     if (lane == 0) {
       V.ep_len[e] = len;
       V.ep_ret[e] += r;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void aql_env_step_k(AqlEnv V, const float* __restrict__ act,
+                                                      const int* __restrict__ act_idx, const float* __restrict__ amu,
+                                                      AqlInsert I) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= V.E) return;
+  env_step_wave(V, e, lane, act + (size_t)e * V.adim, act_idx[e], amu, I, (I.filled[0] + e) % I.C,
+                (uint64_t)V.counter[0]);
+}
+
+// The serial engine's acting tail in ONE launch (aql_act_tail): a wave per env picks its
+// candidate (eps-greedy, aql_select_k's draw) and steps the env into its ring slot; one extra
+// workgroup writes the E ring leaves at the max priority and walks their levels (the
+// per_write_ring_fused_k write: it needs only the slots, (filled + e) mod C); the last
+// workgroup to finish advances `filled` by E and the acting counter by 1 (every workgroup has
+// read both by then) and writes the learner's PER beta for this iteration.  Replaces
+// select + env step + ring write + the host's beta fill (4 launches).
+__global__ __launch_bounds__(256) void aql_act_tail_k(AqlTail A) {
+  const AqlEnv& V = A.V;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nenv = (V.E + 3) / 4;
+  if ((int)blockIdx.x < nenv) {
+    __shared__ float s_act[4][kMaxAdim];
+    const int e = blockIdx.x * 4 + wave;
+    if (e < V.E) {  // wave-uniform
+      const uint64_t ctr = (uint64_t)A.counter[0];
+      const int T = V.T, adim = V.adim;
+      float best = -INFINITY;
+      int arg = 0x7fffffff;
+      for (int c = lane; c < T; c += 64) {
+        const float v = A.q[(size_t)e * T + c];
+        if (v > best || (v == best && c < arg)) { best = v; arg = c; }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o, 64);
+        const int oa = __shfl_xor(arg, o, 64);
+        if (ov > best || (ov == best && oa < arg)) { best = ov; arg = oa; }
+      }
+      float u[4];
+      uniform4(A.sel_seed, (uint64_t)e, ctr, u);
+      if (u[0] <= A.eps[e]) arg = min((int)(u[1] * (float)T), T - 1);  // random candidate (model.py:331-333)
+      if (lane == 0) A.act_idx[e] = arg;
+      if (lane < adim) {
+        const float av = A.amu[((size_t)e * T + arg) * adim + lane];
+        A.env_act[(size_t)e * adim + lane] = av;
+        s_act[wave][lane] = av;
+      }
+      __builtin_amdgcn_wave_barrier();
+      env_step_wave(V, e, lane, s_act[wave], arg, A.amu, A.I, (A.filled[0] + e) % A.I.C, ctr);
+    }
+  } else {
+    __shared__ int sids[1024];
+    __shared__ int comp[64];
+    __shared__ int ncomp;
+    const TreeDesc& tr = A.tree;
+    const int64_t f = A.filled[0];
+    const float p = *A.max_prio;
+    for (int i = t; i < V.E; i += blockDim.x) {
+      const int id = (int)((f + i) % A.I.C);
+      sids[i] = id;
+      if (id < tr.size[0]) write_leaf(tr, id, p, A.alpha);
+    }
+    if (t == 0) {
+      ncomp = 0;
+      if (A.beta_out) {  // AQL_dis.py:59 in the host's double arithmetic, then to fp32
+#pragma clang fp contract(off)
+        const double it = (double)A.iter[0];
+        const double r = A.beta0 + it * A.beta_omb / A.beta_max_step * A.beta_workers;
+        A.beta_out[0] = (float)(r < 1.0 ? r : 1.0);
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < V.E; i += blockDim.x) {  // one slot per distinct level-1 node (ring order)
+      const int id = sids[i];
+      if (id >= tr.size[0]) continue;
+      const int prev = i > 0 ? sids[i - 1] : -1;
+      if (prev >= 0 && prev < tr.size[0] && (prev >> kTreeLog2Fanout) == (id >> kTreeLog2Fanout)) continue;
+      const int k = atomicAdd(&ncomp, 1);
+      if (k < 64) comp[k] = id;
+    }
+    __syncthreads();
+    if (ncomp <= 64) update_levels_fast<4>(tr, comp, ncomp);
+    else update_levels_block(tr, sids, V.E, 1, tr.levels);
+  }
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    if (atomicAdd(A.ticket, 1) == (int)gridDim.x - 1) {  // the last workgroup: every read of the counters is done
+      A.filled[0] += V.E;
+      A.counter[0] += 1;
+      if (A.iter) A.iter[0] += 1;
+      A.ticket[0] = 0;
     }
   }
 }
@@ -1292,6 +1387,24 @@ void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, con
   if (ins.C < e.E) throw std::invalid_argument("aql env: replay capacity < envs");
   if (e.E < 1) return;
   aql_env_step_k<<<(e.E + 3) / 4, 256, 0, s>>>(e, env_act, act_idx, amu, ins);
+  LAUNCH_CHECK();
+}
+
+void aql_act_tail(const AqlTail& a, hipStream_t s) {
+  static const int obs_of[3] = {kBwObs, 4, 3}, adim_of[3] = {kBwAct, 1, 1};
+  const AqlEnv& e = a.V;
+  if (e.kind < 0 || e.kind > 2) throw std::invalid_argument("aql env: kind");
+  if (e.obs != obs_of[e.kind] || e.adim != adim_of[e.kind]) throw std::invalid_argument("aql env: obs/action dims");
+  if (a.I.C < e.E) throw std::invalid_argument("aql env: replay capacity < envs");
+  if (e.E > 1024) throw std::invalid_argument("aql_act_tail: at most 1024 envs (one tree workgroup)");
+  if (e.adim > kMaxAdim) throw std::invalid_argument("aql_act_tail: action dim");
+  if (a.I.C > ((int64_t)1 << 31) || a.tree.size[0] < a.I.C)
+    throw std::invalid_argument("aql_act_tail: the tree must cover the ring");
+  if (!a.q || !a.amu || !a.eps || !a.act_idx || !a.env_act || !a.max_prio || !a.filled || !a.counter || !a.ticket ||
+      (a.beta_out && !a.iter))
+    throw std::invalid_argument("aql_act_tail: missing buffers");
+  if (e.E < 1) return;
+  aql_act_tail_k<<<(e.E + 3) / 4 + 1, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 

@@ -803,6 +803,28 @@ PYBIND11_MODULE(_apex_hip, m) {
                            uint64_t s) {
     aql_env_step(e, P<const float>(env_act), P<const int>(act_idx), P<const float>(amu), ins, S(s));
   });
+  py::class_<AqlTail>(m, "AqlTail");
+  m.def("make_aql_tail", [](const AqlEnv& env, const AqlInsert& ins, const TreeHandle& tree, py::dict d) {
+    auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+    auto opt = [&](const char* k) { return d.contains(k) ? d[k].cast<uint64_t>() : (uint64_t)0; };
+    AqlTail a{};
+    a.V = env;
+    a.I = ins;
+    a.tree = tree.d;
+    a.q = P<const float>(g("q")); a.amu = P<const float>(g("amu")); a.eps = P<const float>(g("eps"));
+    a.sel_seed = g("sel_seed"); a.act_idx = P<int>(g("act_idx")); a.env_act = P<float>(g("env_act"));
+    a.alpha = d["alpha"].cast<float>(); a.max_prio = P<const float>(g("max_prio"));
+    a.filled = P<int64_t>(g("filled")); a.counter = P<int64_t>(g("counter")); a.ticket = P<int>(g("ticket"));
+    a.beta_out = P<float>(opt("beta_out")); a.iter = P<int64_t>(opt("iter"));
+    a.beta0 = d.contains("beta0") ? d["beta0"].cast<double>() : 0.0;
+    a.beta_omb = d.contains("beta_omb") ? d["beta_omb"].cast<double>() : 0.0;
+    a.beta_max_step = d.contains("beta_max_step") ? d["beta_max_step"].cast<double>() : 1.0;
+    a.beta_workers = d.contains("beta_workers") ? d["beta_workers"].cast<double>() : 0.0;
+    if ((const void*)a.counter != (const void*)env.counter || (const void*)a.filled != (const void*)ins.filled)
+      throw std::invalid_argument("make_aql_tail: counter / filled must be the env's and the ring's");
+    return a;
+  });
+  m.def("aql_act_tail", [](const AqlTail& a, uint64_t s) { aql_act_tail(a, S(s)); });
   m.def("aql_select", [](uint64_t q, uint64_t a_mu, int B, int T, int adim, uint64_t eps, uint64_t seed,
                          uint64_t counter, uint64_t act_idx, uint64_t env_act, uint64_t s) {
     aql_select(P<const float>(q), P<const float>(a_mu), B, T, adim, P<const float>(eps), seed,

@@ -579,6 +579,26 @@ struct AqlInsert {
 void aql_env_reset(const AqlEnv& e, hipStream_t s);
 void aql_env_step(const AqlEnv& e, const float* env_act, const int* act_idx, const float* amu, const AqlInsert& ins,
                   hipStream_t s);
+// the serial engine's acting tail: eps-greedy select + env step + ring tree write + counter bumps
+// (+ the learner's PER beta) in one launch (aql_engine_kernels.hip aql_act_tail_k)
+struct AqlTail {
+  AqlEnv V;
+  AqlInsert I;         // the replay ring (I.filled is read; `filled` below is bumped)
+  TreeDesc tree;
+  const float *q, *amu, *eps;  // candidate Q [E][T], candidates [E][T][adim], per-env epsilon
+  uint64_t sel_seed;
+  int* act_idx;
+  float* env_act;
+  float alpha;
+  const float* max_prio;
+  int64_t* filled;     // += E by the last workgroup
+  int64_t* counter;    // acting counter (V.counter), += 1 by the last workgroup
+  int* ticket;         // zero between launches
+  float* beta_out;     // optional: beta_start + iter (1 - beta_start) / max_step * workers, min 1
+  int64_t* iter;       // iterations so far (+= 1 by the last workgroup)
+  double beta0, beta_omb, beta_max_step, beta_workers;
+};
+void aql_act_tail(const AqlTail& a, hipStream_t s);
 // rows 0..E-1 of the staging tables ``src`` -> ring slots (dst.filled + e) % dst.C (slot list in dst.slots)
 void aql_apply_staged(const AqlInsert& src, const AqlInsert& dst, int E, int obs, int TA, hipStream_t s);
 

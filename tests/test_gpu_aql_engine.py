@@ -401,3 +401,37 @@ def test_last_step_publishes_acting_copies(cuda):
         torch.cuda.synchronize()
         assert torch.equal(eng.actor_flat, L.flat), it
         assert torch.equal(eng.actor_eps, L.eps), it
+
+
+@pytest.mark.parametrize("env_id", ["BipedalWalker-v3", "CartPole-v0"])
+def test_fused_acting_tail_equals_separate_launches(cuda, env_id):
+    """The serial engine's one-launch acting tail (aql_act_tail: eps-greedy select + env step +
+    ring tree write + counter bumps + the learner's PER beta from a device iteration counter)
+    == select, env step, per_write_leaves and the host's beta fill as separate launches: same
+    replay rows, tree, counters, env state, beta and learner after fill + eager and
+    graph-captured iterations, bit for bit."""
+    from apex_amd.engine.aql import AQLEngine, AQLEngineConfig
+
+    out = []
+    for fused in (False, True):
+        cfg = AQLEngineConfig(env_id=env_id, n_envs=96, capacity=8192, batch_size=32, seed=13, fused_acting=fused,
+                              max_step=40)  # (a short beta horizon: beta moves every iteration)
+        eng = AQLEngine(cfg, cuda)
+        assert (eng._tail is not None) == fused
+        eng.fill(1024)
+        for _ in range(4):
+            eng.iteration()
+        eng.capture()
+        for _ in range(3):
+            eng.iteration()
+        torch.cuda.synchronize()
+        r, L = eng.replay, eng.learner
+        out.append((r.st.clone(), r.st2.clone(), r.action.clone(), r.reward.clone(), r.done.clone(), r.a_mu.clone(),
+                    r.leaf_sum.clone(), r.node_sum[0].clone(), r.node_sum[-1].clone(), r.filled.clone(),
+                    eng.actor_ctr.clone(), eng.obs_buf.clone(), eng.ep_len.clone(), eng.ep_ret.clone(),
+                    eng.ep_count.clone(), L.beta.clone(), L.idx.clone(), L.flat.clone()))
+    names = ("st", "st2", "action", "reward", "done", "a_mu", "leaf_sum", "level1", "root", "filled", "actor_ctr",
+             "obs", "ep_len", "ep_ret", "ep_count", "beta", "idx", "flat")
+    for name, x, y in zip(names, out[0], out[1]):
+        assert torch.equal(x, y), (name, (x.double() - y.double()).abs().max().item())
+    assert out[1][15].item() != AQLEngineConfig().beta_start  # the device beta moved
