@@ -248,10 +248,14 @@ class ApexEngine:
             fn()
         return g
 
-    def capture(self, warmup_iters: int = 3) -> None:
+    def capture(self, warmup_iters: int = 3, warm_replays: int = 0) -> None:
         """Warm up on a side stream, then capture actor and learner steps as hipGraphs.
         The warm-up iterations are real train steps and are counted as such.  Collectives
-        stay eager, between the learner's phase graphs (unless ``dp_graph``)."""
+        stay eager, between the learner's phase graphs (unless ``dp_graph``).
+        ``warm_replays``: real train steps through the captured graphs right after capture,
+        back to back (also counted): after a pause the MI355X runs the first ~30 steps 4-8 %
+        slower than steady state (clock / power ramp, scripts/diag/warmup_curve.py), so a
+        caller that times a short window right after setup starts from the sustained state."""
         self._drain_mass()
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
@@ -276,6 +280,8 @@ class ApexEngine:
         torch.cuda.synchronize(self.device)
         if self.overlap:
             self._ev_learn.record(torch.cuda.current_stream(self.device))
+        for _ in range(warm_replays):
+            self.train_step()
 
     def _capture_overlap_graphs(self, apool) -> None:
         """Overlap mode: graphs per staging half (actor: fill half h; learner: apply half

@@ -66,6 +66,10 @@ def parse():
     ap.add_argument("--actions", type=int, default=18)
     ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--graph-warm", type=int, default=48,
+                    help="real train steps replayed back to back right after graph capture, before the --warmup "
+                         "steps (untimed, counted as training): the GPU reaches its sustained clock after ~30 "
+                         "steps of load, so a short timed window right after setup is not a ramp measurement")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
@@ -296,7 +300,7 @@ def main():
     t_fill = time.perf_counter() - t_fill
     wd.kick()
     if not args.no_graphs:
-        eng.capture()
+        eng.capture(warm_replays=args.graph_warm)
     wd.kick()
     for _ in range(args.warmup):
         eng.train_step()
@@ -368,6 +372,7 @@ def main():
                 "forward": args.forward,
                 "fp32_gemms": "exact 3-term bf16 split (x6) on MFMA, fp32 accumulate" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
+                "graph_warm_replays": 0 if args.no_graphs else args.graph_warm,
                 "actor_learner_overlap": args.overlap,
                 "dp_graph": eng._g_dp is not None,
                 # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
