@@ -592,6 +592,8 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
     wd.kick()
     if not args.no_graphs:
         eng.capture()
+        for _ in range(args.graph_warm):  # real steps, back to back (see --graph-warm)
+            eng.train_step()
     for _ in range(args.warmup):
         eng.train_step()
     torch.cuda.synchronize(device)
@@ -612,6 +614,7 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
         "metric": "learner SGD steps/sec + actor frames/sec, Ape-X DQN Atari at 1/2/4/8 MI355X",
         "value": round(steps_per_s, 3), "unit": "learner SGD steps/s (one central learner, batch 512)",
         "n_gpus": 1 if emulate else world, "steps": args.steps, "warmup": args.warmup,
+        "graph_warm_replays": 0 if args.no_graphs else args.graph_warm,
         "ms_per_step": round(1000.0 * dt / args.steps, 4), "higher_is_better": True, "scaling": "strong",
         "vs_baseline": round(steps_per_s / REFERENCE_BATCHES_PER_S, 2), "dtype": args.dtype,
         "data": "synthetic (GPU-rendered Atari-shaped 84x84x4 u8 frames, random-init weights)",
