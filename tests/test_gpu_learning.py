@@ -134,15 +134,17 @@ def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
         assert row["hip_loss_err"] < 1e-4 and row["hip_prio_err"] < 1e-3
     # whole run: the HIP fp32 learner is no farther from the fp64 learner than PyTorch's
     # own fp32 learner (same fp32 roundoff class).  The sign-like RMSprop steps amplify any
-    # roundoff difference chaotically, and the torch fp32 reference is NOT run-to-run
-    # deterministic (its conv backward): measured on MI355X (scripts/det_check.py, 4 runs)
-    # the HIP trajectory is bit-identical every run while torch fp32's own distance to fp64
-    # at step 15 was 0.071 / 0.072 / 0.073 / 0.27 -- so a single reference run bounds each
-    # step only loosely and the tight comparison is on the steady tail's mean.
-    for row in traj:
-        assert row["hip_vs_64"] <= 3.0 * row["t32_vs_64"] + 0.02, row
-        assert row["param_rel"] <= 3.0 * row["t32_param_rel"] + 2e-4, row
+    # roundoff difference chaotically from step ~3 on, and the torch fp32 reference is NOT
+    # run-to-run deterministic (its conv backward): three runs of this seed in one process
+    # (scripts/diag/learning_determinism.py, MI355X) gave the HIP learner 0.0681 at step 10
+    # every time (bit-identical trajectory) and torch fp32 0.057 / 0.0029 / 4.3e-5 -- the
+    # step at which torch's copy leaves fp64 is a coin toss, so steps of the divergence onset
+    # are not compared one by one (a per-step bound there passed or failed with torch's luck).
+    # Once both have saturated (the second half) every step is compared, and the tail means.
     tail = traj[len(traj) // 2:]
+    for row in tail:
+        assert row["hip_vs_64"] <= 1.5 * row["t32_vs_64"] + 0.05, row
+        assert row["param_rel"] <= 3.0 * row["t32_param_rel"] + 2e-4, row
     mean = lambda k: sum(r[k] for r in tail) / len(tail)  # noqa: E731
     assert mean("hip_vs_64") <= 1.5 * mean("t32_vs_64")
     assert mean("hip_loss_err") <= 2.0 * mean("t32_loss_err") + 0.02
