@@ -599,7 +599,7 @@ class AQLEngine:
         h.aql_env_reset(self.env, self._s())
         self.iterations = 0
         self.learner_steps = 0
-        self._g_actor = self._g_learn = None
+        self._g_actor = self._g_learn = self._g_iter = None
         self._ep_read = 0
         self.target_syncs = collections.deque(maxlen=4096)  # iterations after which the target was synced
 
@@ -688,8 +688,8 @@ class AQLEngine:
         self.publish()
 
     def capture(self) -> None:
-        """Actor step and the K learner steps each as one hipGraph (same stream order); overlap
-        mode: one actor graph and one learner graph (apply + K steps) per staging half."""
+        """The iteration (actor step + the K learner steps) as one hipGraph; overlap mode: one
+        actor graph and one learner graph (apply + K steps) per staging half."""
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):  # warm the launch paths outside capture
@@ -708,11 +708,11 @@ class AQLEngine:
             torch.cuda.synchronize(self.device)
             self._ev_learn.record(torch.cuda.current_stream(self.device))
             return
-        self._g_actor = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_actor):
+        # the whole serial iteration (acting + K steps) as ONE graph: one graph launch per
+        # iteration instead of two (19.32-19.35k vs 19.10-19.13k SGD steps/s, one box)
+        self._g_iter = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._g_iter):
             self.actor_step()
-        self._g_learn = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_learn):
             self._pub_in_graph = self.learn_steps(publish=True)
         torch.cuda.synchronize(self.device)
 
@@ -726,14 +726,11 @@ class AQLEngine:
             return self._iteration_overlap()
         if self._tail is None:  # (the fused acting tail writes it on the device)
             self.learner.beta.fill_(self._beta())
-        if self._g_actor is not None:
-            self._g_actor.replay()
-        else:
-            self.actor_step()
-        if self._g_learn is not None:
-            self._g_learn.replay()
+        if self._g_iter is not None:
+            self._g_iter.replay()
             pub = self._pub_in_graph
         else:
+            self.actor_step()
             pub = self.learn_steps(publish=True)
         if not pub:
             self.publish()
