@@ -675,7 +675,7 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   batch_leaves_block(tree, w, 0, tred, sids);
   stamp(2);
   if (levels > 0)  // levels 1..levels (dbg[24..29]: walk phases)
-    update_levels_fast(tree, sids, B, L.dbg ? L.dbg + 24 : nullptr, 1, levels);
+    update_levels_fast<8>(tree, sids, B, L.dbg ? L.dbg + 24 : nullptr, 1, levels);
   stamp(3);
 }
 
@@ -946,7 +946,7 @@ __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the level walk
     __shared__ int sids[64];
     for (int i = threadIdx.x; i < G.bw.B; i += blockDim.x) sids[i] = G.bw.list[i];
-    update_levels_fast(G.tree, sids, G.bw.B, nullptr, max(G.levels_lo, 1));
+    update_levels_fast<8>(G.tree, sids, G.bw.B, nullptr, max(G.levels_lo, 1));
     return;
   }
   aql_grad_block(G, blockIdx.x, ng);
