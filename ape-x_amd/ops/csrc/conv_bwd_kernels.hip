@@ -663,12 +663,24 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   if (jb.kind == 2) {  // FC1 weight rows: natural [n][p*64 + c] -> reference [n][c*49 + p]
     const int n = (int)blockIdx.x - jb.block0;
     const float* src = jb.part + (size_t)n * kRowLen;
+    // the thread's 13 elements of each slice loaded together (clamped index, zeroed after):
+    // a loop load -> store per element paid a round trip each
+    constexpr int kPer = (kRowLen + 255) / 256;
+    float t[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) t[i] = src[min((int)threadIdx.x + 256 * i, kRowLen - 1)];
+    for (int g = 1; g < jb.G; ++g) {
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) t[i] += src[(size_t)g * jb.pstride + min((int)threadIdx.x + 256 * i, kRowLen - 1)];
+    }
     float q = 0.f;
-    for (int k = threadIdx.x; k < kRowLen; k += 256) {
-      float t = 0.f;
-      for (int g = 0; g < jb.G; ++g) t += src[(size_t)g * jb.pstride + k];
-      row[(k & 63) * 49 + (k >> 6)] = t;
-      q += t * t;
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      const int k = threadIdx.x + 256 * i;
+      if (k < kRowLen) {
+        row[(k & 63) * 49 + (k >> 6)] = t[i];
+        q += t[i] * t[i];
+      }
     }
     __syncthreads();
     float* dst = jb.out[0] + (size_t)n * kRowLen;

@@ -237,7 +237,6 @@ __device__ __forceinline__ void opt_body(float* __restrict__ p, const float* __r
     return;
   }
   // generic part: every element outside the FC1 ranges, scalar, through the scatter maps
-  const NormInfo ni = norms();
   const int gb = bid - n_fc_blocks, ngb = nblk - n_fc_blocks;
   const int64_t stride = (int64_t)ngb * kOptThreads;
   int64_t lo[3], hi[3];
@@ -252,6 +251,47 @@ __device__ __forceinline__ void opt_body(float* __restrict__ p, const float* __r
   } else {
     lo[0] = 0; hi[0] = n; nr = 1;
   }
+  bool one_pass = true;  // (grid-uniform) the grid covers every range in one element per thread
+  for (int k = 0; k < nr; ++k) one_pass = one_pass && hi[k] - lo[k] <= stride;
+  if (one_pass) {
+    // every load of the thread's (<= 3) elements and their packed-copy slots in flight before
+    // the norm reduction: the grid-stride loop below pays a dependent round trip per element
+    // (MI355X, fp32 DQN learner: 9.9 -> 8.3 us per optimizer launch, scripts/diag/opt_tail.py)
+    float vp[3], vg[3], va[3], vb[3];
+    int64_t vi[3];
+    int d1[3], d2[3];
+    const bool packed = pk.arena_f32 != nullptr || pk.arena != nullptr;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      vi[k] = k < nr ? lo[k] + (int64_t)gb * kOptThreads + threadIdx.x : -1;
+      const int64_t c = k < nr && vi[k] < hi[k] ? vi[k] : 0;  // clamp: the idle lanes reload element 0
+      vp[k] = p[c];
+      vg[k] = g[c];
+      va[k] = s1[c];
+      vb[k] = s2[c];
+      d1[k] = packed ? pk.dst1[c] : -1;
+      d2[k] = packed ? pk.dst2[c] : -1;
+    }
+    const NormInfo ni = norms();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k >= nr || vi[k] >= hi[k]) continue;
+      const float np = rule(vp[k], opaque(vg[k] * ni.clip), va[k], vb[k]);
+      s1[vi[k]] = va[k];
+      s2[vi[k]] = vb[k];
+      p[vi[k]] = np;
+      if (pk.arena_f32) {
+        if (d1[k] >= 0) pk.arena_f32[d1[k]] = np;
+        if (d2[k] >= 0) pk.arena_f32[d2[k]] = np;
+      } else if (pk.arena) {
+        const uint16_t b = f2bf(np);
+        if (d1[k] >= 0) pk.arena[d1[k]] = b;
+        if (d2[k] >= 0) pk.arena[d2[k]] = b;
+      }
+    }
+    return;
+  }
+  const NormInfo ni = norms();
   for (int k = 0; k < nr; ++k)
     for (int64_t i = lo[k] + (int64_t)gb * kOptThreads + threadIdx.x; i < hi[k]; i += stride)
       opt_elem(p, g, s1, s2, i, ni.clip, rule, pk);
@@ -298,7 +338,8 @@ static void launch_opt(float* p, const float* g, float* s1, float* s2, int64_t n
     nfc = 2 * kFcTilesPerMat;
   }
   const int64_t gen = n - (nfc ? 2 * (int64_t)kFcN * kFcC * kFcP : 0);
-  const int ngb = (int)std::max<int64_t>(1, std::min<int64_t>((gen + 4 * kOptThreads - 1) / (4 * kOptThreads),
+  // one element per thread (the one-pass path) up to kOptGenBlocksMax workgroups
+  const int ngb = (int)std::max<int64_t>(1, std::min<int64_t>((gen + kOptThreads - 1) / kOptThreads,
                                                                kOptGenBlocksMax));
   opt_step_k<Params><<<nfc + ngb, kOptThreads, 0, s>>>(p, g, s1, s2, n, partials, n_partials, hp, step, norms_out,
                                                        pk, f, nfc);
