@@ -66,10 +66,12 @@ def parse():
     ap.add_argument("--actions", type=int, default=18)
     ap.add_argument("--forward", default="hip", choices=["torch", "hip"])
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--graph-warm", type=int, default=48,
+    ap.add_argument("--graph-warm", type=int, default=200,
                     help="real train steps replayed back to back right after graph capture, before the --warmup "
-                         "steps (untimed, counted as training): the GPU reaches its sustained clock after ~30 "
-                         "steps of load, so a short timed window right after setup is not a ramp measurement")
+                         "steps (untimed, counted as training; ~0.1 s): the GPU reaches its sustained clock only "
+                         "after a stretch of load, so a short timed window right after setup is not a ramp "
+                         "measurement (20-step windows, one box: 2276-2318 steps/s after 48, 2310-2345 after "
+                         "200, 2345 sustained over 2000 steps; profiles/r5_short_window.txt)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
