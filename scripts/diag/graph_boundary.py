@@ -46,6 +46,14 @@ def main():
                                                  act=eng.actor.act_args()))
     g_env = actor_graphs(lambda h: eng.actor.act_and_step(None, h, selected=True))
     torch.cuda.synchronize()
+    # (g) timing probe only: the learner graphs WITHOUT the forked priority-tree branch (no tree
+    # writes at all -- wrong replay semantics, kept out of every other case): its fork/join cost
+    L = eng.learner
+    fork, join = L._fork_point, L._tree_fork_end
+    L._fork_point, L._tree_fork_end = (lambda: None), (lambda: None)
+    g_notree = [eng._graph(lambda h=h: (eng._learn_a(1 - h), eng._learn_b()), eng._pool) for h in (0, 1)]
+    L._fork_point, L._tree_fork_end = fork, join
+    torch.cuda.synchronize()
     eng._ev_learn.record(torch.cuda.current_stream())
 
     def step_with(gA, n):  # _train_step_overlap's event pattern (no publish / target sync)
@@ -86,7 +94,8 @@ def main():
              "(c) two learner steps per graph": two_step,
              "(d) learner || whole actor graph": lambda n: step_with(eng._g_actor, n),
              "(e) learner || actor forward only": lambda n: step_with(g_fwd, n),
-             "(f) learner || actor env step + staging only": lambda n: step_with(g_env, n)}
+             "(f) learner || actor env step + staging only": lambda n: step_with(g_env, n),
+             "(g) learner graphs alone, no tree branch (probe)": lambda n: [g_notree[i & 1].replay() for i in range(n)]}
     res = {k: [] for k in cases}
     for _ in range(a.rounds):
         for k, fn in cases.items():
