@@ -5,8 +5,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/central5
 export PYTHONUNBUFFERED=1 HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/central5
-timeout -k 10 150 python scripts/bench_f32.py --tile1 --tile2 > $O/tiles.log 2>&1 || exit $?
-grep -v amdgpu.ids $O/tiles.log
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_central_emulated.py \
   > $O/test.log 2>&1; rc=$?; echo "== tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/test.log | tail -8
 [ $rc -ne 0 ] && exit $rc
