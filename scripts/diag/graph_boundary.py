@@ -52,6 +52,19 @@ def main():
     fork, join = L._fork_point, L._tree_fork_end
     L._fork_point, L._tree_fork_end = (lambda: None), (lambda: None)
     g_notree = [eng._graph(lambda h=h: (eng._learn_a(1 - h), eng._learn_b()), eng._pool) for h in (0, 1)]
+
+    # (h) timing probe only: the tree branch forked at the graph's start (it would write the
+    # PREVIOUS step's priorities; here it races the sampling -- timing only) and joined after
+    # the optimizer, i.e. no fork / join in the middle of the learner chain
+    def root_fork(h):
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        L._tree_fork_begin(ev)
+        eng._learn_a(1 - h)
+        eng._learn_b()
+        torch.cuda.current_stream().wait_stream(L.tree_stream)
+
+    g_rootfork = [eng._graph(lambda h=h: root_fork(h), eng._pool) for h in (0, 1)]
     L._fork_point, L._tree_fork_end = fork, join
     torch.cuda.synchronize()
     eng._ev_learn.record(torch.cuda.current_stream())
@@ -95,7 +108,9 @@ def main():
              "(d) learner || whole actor graph": lambda n: step_with(eng._g_actor, n),
              "(e) learner || actor forward only": lambda n: step_with(g_fwd, n),
              "(f) learner || actor env step + staging only": lambda n: step_with(g_env, n),
-             "(g) learner graphs alone, no tree branch (probe)": lambda n: [g_notree[i & 1].replay() for i in range(n)]}
+             "(g) learner graphs alone, no tree branch (probe)": lambda n: [g_notree[i & 1].replay() for i in range(n)],
+             "(h) learner graphs alone, tree branch forked at the start (probe)":
+                 lambda n: [g_rootfork[i & 1].replay() for i in range(n)]}
     res = {k: [] for k in cases}
     for _ in range(a.rounds):
         for k, fn in cases.items():
