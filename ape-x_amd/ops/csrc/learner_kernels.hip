@@ -324,6 +324,8 @@ static void launch_opt(float* p, const float* g, float* s1, float* s2, int64_t n
                        int n_partials, const Params& hp, const int64_t* step, float* norms_out, const PackMap* pack,
                        const FcPack* fc, hipStream_t s) {
   const PackMap pk = pack ? *pack : PackMap{nullptr, nullptr, nullptr, nullptr};
+  if ((pk.arena || pk.arena_f32) && (!pk.dst1 || !pk.dst2))
+    throw std::invalid_argument("opt_step: packed copies need both scatter maps (dst1, dst2)");
   FcPack f{};
   int nfc = 0;
   if (fc && (fc->wp || fc->wp_f32)) {
