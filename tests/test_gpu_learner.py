@@ -50,11 +50,16 @@ def _seg_handle(hip, shapes):
 
 
 @pytest.mark.parametrize("centered", [True, False])
-def test_rmsprop_clip_matches_torch(cuda, centered):
+@pytest.mark.parametrize("size", ["full", "small"])
+def test_rmsprop_clip_matches_torch(cuda, centered, size):
+    """``small`` (~43k parameters) runs the optimizer's one-pass path (one element per thread,
+    every load in flight before the norm reduce), ``full`` (~445k) its grid-stride loop."""
     from apex_amd import ops
 
     hip = ops.hip()
     shapes = [(32, 4, 8, 8), (32,), (64, 32, 4, 4), (64,), (128, 3136), (128,), (18, 128), (18,)]
+    if size == "small":
+        shapes = [sh for sh in shapes if sh != (128, 3136)]
     seg, P = _seg_handle(hip, shapes)
     g = torch.Generator(device="cpu").manual_seed(3)
     params = [torch.randn(*sh, generator=g).to(cuda) for sh in shapes]
@@ -141,4 +146,23 @@ def test_learner_step_end_to_end(cuda):
     sd = eng.learner.model.state_dict()
     assert list(sd)[:2] == ["features.0.weight", "features.0.bias"]
     assert sd["advantage.0.weight"].shape == (128, 3136) and sd["advantage.2.weight"].shape == (18, 128)
+
+
+def test_optimizer_refuses_packed_copies_without_maps(cuda):
+    """Packed copies (an arena) need both scatter maps: the launch is refused on the host
+    instead of dereferencing a null map on the device."""
+    from apex_amd import ops
+
+    hip = ops.hip()
+    P = 1024
+    x = [torch.zeros(P, device=cuda) for _ in range(4)]
+    partials = torch.zeros(hip.grad_norm_partials(), dtype=torch.float64, device=cuda)
+    norms = torch.zeros(4, device=cuda)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda)
+    arena = torch.zeros(P, device=cuda)
+    hp = hip.RMSpropParams(6.25e-5, 0.95, 1.5e-7, 40.0, 1.0, 0, 0, True)
+    with pytest.raises(ValueError, match="scatter maps"):
+        hip.rmsprop_step(x[0].data_ptr(), x[1].data_ptr(), x[2].data_ptr(), x[3].data_ptr(), P, partials.data_ptr(),
+                         partials.numel(), hp, step.data_ptr(), norms.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                         arena_f32=arena.data_ptr())
 
