@@ -303,6 +303,10 @@ class AQLLearner:
             self.L_tree = h.aql_learn_set_tree(self.L, r.tree, self.prio.data_ptr(), self.loss_q.data_ptr(),
                                                r.owner.data_ptr(), r.wlist.data_ptr(), r.max_prio.data_ptr(), r.alpha,
                                                levels=1)
+            # the gradient launch snapshots the step counter for the update launch, which then
+            # bumps it from one workgroup instead of a last-workgroup ticket
+            self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.G = h.aql_grad_set_step_snap(self.G, self.step_snap.data_ptr(), self.step_ctr.data_ptr())
             self.G_levels = h.aql_grad_set_levels(self.G, r.tree, r.wlist.data_ptr(), B, lo=2)
             kw = dict(p=self.flat.data_ptr(), m=self.m.data_ptr(), v=self.v.data_ptr(), n=self.P, P_q=self.P_q,
                       norms_q=self.norms_q.data_ptr(), norms_p=self.norms_p.data_ptr(), update=1)

@@ -942,6 +942,7 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
 // wrote the leaves, the list and the lowest levels
 __global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
   if (G.gate && G.gate_j >= *G.gate) return;  // (grid-uniform) a gated-off step
+  if (G.step_snap && blockIdx.x == 0 && threadIdx.x == 0) *G.step_snap = *G.step_src;
   const int ng = (int)gridDim.x - (G.tree_leaves ? 1 : 0);
   if (G.tree_leaves && (int)blockIdx.x == ng) {  // block-uniform: the level walk
     __shared__ int sids[64];
@@ -967,7 +968,10 @@ __global__ __launch_bounds__(256) void aql_update_k(const AqlStep* __restrict__ 
   const AqlStep& D = *Dp;
   if (D.gate && gate_j >= *D.gate) return;  // (grid-uniform) a gated-off step
   const int bid = blockIdx.x, t = threadIdx.x;
-  const uint64_t st = (uint64_t)D.P.step[0];
+  // the step from the gradient launch's copy when there is one (then block 0 bumps the counter:
+  // no block of this launch reads it), else from the counter (bumped by the last block)
+  const int64_t* snap = D.G.step_snap;
+  const uint64_t st = (uint64_t)(snap ? snap[0] : D.P.step[0]);
   if (bid < D.nblk) {
     const int64_t i = (int64_t)bid * 256 + t;
     update_block(D, bid, i < D.n ? D.G.grad[i] : 0.f, st);
@@ -980,7 +984,8 @@ __global__ __launch_bounds__(256) void aql_update_k(const AqlStep* __restrict__ 
   } else {
     draw_block(D, bid - D.nblk - noise_blocks, st);
   }
-  step_ticket(D.P, (int)gridDim.x, st);
+  if (!snap) step_ticket(D.P, (int)gridDim.x, st);
+  else if (bid == 0 && t == 0) D.P.step[0] = (int64_t)st + 1;
 }
 
 // ------------------------------------------------------------------ vector envs

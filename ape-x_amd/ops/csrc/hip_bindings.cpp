@@ -648,6 +648,13 @@ PYBIND11_MODULE(_apex_hip, m) {
     g.bw = w;
     return g;
   }, py::arg("G"), py::arg("tree"), py::arg("list"), py::arg("B"), py::arg("lo") = 1);
+  m.def("aql_grad_set_step_snap", [](const AqlGrad& g0, uint64_t snap, uint64_t step) {
+    AqlGrad g = g0;
+    if (!snap || !step) throw std::invalid_argument("aql_grad_set_step_snap: both pointers");
+    g.step_snap = P<int64_t>(snap);
+    g.step_src = P<const int64_t>(step);
+    return g;
+  }, py::arg("G"), py::arg("snap"), py::arg("step"));
   m.def("aql_learn_set_groups", [](const AqlLearn& L0, int groups, int halves) {  // groups 0: the launcher picks
     if (halves != 0 && halves != 1 && halves != 2) throw std::invalid_argument("aql_learn_set_groups: halves 0, 1 or 2");
     AqlLearn L = L0;

@@ -498,6 +498,11 @@ struct AqlGrad {
   BatchWrite bw;
   const int* gate;  // step gate (AqlLearn::gate)
   int gate_j;
+  // (aql_grad_set_step_snap) block 0 copies the learner step counter here: the update launch
+  // that follows reads its step from the copy, so one of its blocks can bump the counter
+  // without a last-block ticket (an atomic round trip at the end of every update workgroup)
+  int64_t* step_snap = nullptr;
+  const int64_t* step_src = nullptr;
 };
 int aql_grad_blocks(int64_t n);
 void aql_grad(const AqlGrad& g, hipStream_t s);
