@@ -44,6 +44,7 @@
 // conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.  conv1 (forward
 // and weight gradient) has its own sample-resident kernels: u8 frame planes staged in LDS.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -178,30 +179,92 @@ __device__ __forceinline__ float trunc_bf16(float x) { return __uint_as_float(__
 struct Split8 {
   bfx8 h, m, l;
 };
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// One pair (a, b) -> packed bf16 words of its hi / mid / lo terms.  The two residual
+// subtractions run as one v_pk_add_f32 each (the same IEEE operations as two v_sub_f32: the
+// terms are bit-identical), 9 VALU per pair instead of 11.
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const f32x2 v = {a, b};
+  const f32x2 r = v - f32x2{trunc_bf16(a), trunc_bf16(b)};
+  const f32x2 rl = r - f32x2{trunc_bf16(r[0]), trunc_bf16(r[1])};
+  h = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
+  m = pack_bf16_hi(r[0], r[1]);
+  l = pack_bf16_hi(rl[0], rl[1]);  // exact: <= 8 significant bits
+}
 __device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
-  const float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
   uint32_t h[4], m[4], l[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float a = x[2 * j], b = x[2 * j + 1];
-    const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
-    const float am = trunc_bf16(ar), bm = trunc_bf16(br);
-    h[j] = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
-    m[j] = pack_bf16_hi(am, bm);
-    l[j] = pack_bf16_hi(ar - am, br - bm);  // exact: <= 8 significant bits
-  }
+  split_pair(x0[0], x0[1], h[0], m[0], l[0]);
+  split_pair(x0[2], x0[3], h[1], m[1], l[1]);
+  split_pair(x1[0], x1[1], h[2], m[2], l[2]);
+  split_pair(x1[2], x1[3], h[3], m[3], l[3]);
   return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
           __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
           __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
 }
 
+// Stage-split LDS image (gemm_body<P, true>): each fp32 operand chunk is split ONCE, by the
+// thread that stages it, into three bf16 planes (hi / mid / lo) in LDS; the waves read the
+// planes back as ready MFMA fragments.  In the register-split form every wave splits every
+// fragment it reads -- each element 2x (2 x 2 wave grids) to 4x (the shared B operand of a
+// 4 x 1 grid), 44 VALU per fragment and 16 k -- which bounds the GEMMs on the VALU
+// (14-20 VALU per MFMA, 15-29 % MFMA busy: profiles/r5_fp32_pmc.md).  Same terms, same
+// k-slot of every product (bit-identical results):
+//  * K-major operand: plane rows [row][BK] bf16; the 4-element staging chunk u of a 16-k
+//    block lands in 16-byte chunk (u & 1), 8-byte half (u >> 1) -- so lane (r, h) reads slots
+//    8h..8h+7 = k {4h..4h+3, 8+4h..8+4h+3} (split8's map) as ONE ds_read_b128 per plane;
+//    chunks XOR-swizzled by row so a read's 16-lane groups hit 64 distinct banks.
+//  * MN-major operand: plane rows [k][BM] bf16 (the staged chunk's 4 m at one k, natural
+//    order); a fragment is two ds_read_b64_tr_b16 per plane (k rows 4h..+3 and 8+4h..+3:
+//    lane 4q + p of a 16-lane group addresses k row q, columns 4p..4p+3; lane i receives
+//    column i) -- the hardware transpose; chunks XOR-swizzled so a 32-lane half's four k rows
+//    hit distinct banks.
+template <class P>
+struct GeoS {
+  using G = Geo<P>;
+  static constexpr int BM = P::BM, BN = P::BN, BK = P::BK;
+  static constexpr int RBA = P::A_KMAJ ? BK * 2 : BM * 2;  // plane row bytes (no padding)
+  static constexpr int RBB = P::B_KMAJ ? BK * 2 : BN * 2;
+  static constexpr int PLA = (P::A_KMAJ ? BM : BK) * RBA;  // plane bytes
+  static constexpr int PLB = (P::B_KMAJ ? BN : BK) * RBB;
+  static constexpr int SA = 3 * PLA, SB = 3 * PLB;
+  static constexpr int LDS_BYTES = 2 * (SA + SB);
+  static_assert(BK == 16 || BK == 32, "K-major swizzle: 2 or 4 chunks per row");
+  static_assert((P::A_KMAJ || BM == 32 || BM == 64 || BM == 128) && (P::B_KMAJ || BN == 32 || BN == 64 || BN == 128),
+                "MN-major swizzle");
+};
+// K-major: row of NC = BK / 8 16-byte chunks; 16 / NC rows share a 256-byte bank line
+template <int BK>
+__device__ __forceinline__ int swz_k(int row) {
+  constexpr int NC = BK / 8;
+  return (row / (16 / NC)) & (NC - 1);
+}
+// MN-major: row of W bf16 (W / 8 chunks); a half-wave transposed read takes 4 rows x 4 chunks
+template <int W>
+__device__ __forceinline__ int swz_m(int row) {
+  if constexpr (W == 32) return 0;
+  else if constexpr (W == 64) return 4 * ((row >> 1) & 1);
+  else return 4 * (row & 3);
+}
+// one staged fp32 chunk (4 values) -> its hi / mid / lo bf16 words (split_pair: split8's terms)
+__device__ __forceinline__ void split4(f32x4 x, uint2& h, uint2& m, uint2& l) {
+  split_pair(x[0], x[1], h.x, m.x, l.x);
+  split_pair(x[2], x[3], h.y, m.y, l.y);
+}
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+__device__ __forceinline__ uint2 ds_tr16(const char* p) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+  return __builtin_bit_cast(uint2, v);
+}
+
 // Every fp32 GEMM of the learner (gemm_body) on the bf16 matrix cores through split8: the
 // fp32-MFMA form (v_mfma_f32_32x32x2_f32) it replaced in round 5 ran 2142 vs 2378 learner
 // steps/s at the same fp32-class accuracy (profiles/r5_x6.md, tests/test_gpu_f32_net.py).
-template <class P>
+template <class P, bool SS>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
+  using GS = GeoS<P>;
   constexpr bool COLSUM = HasColsum<P>::value;
   static_assert(!COLSUM || (!P::A_KMAJ && 256 % G::RA == 0), "colsum needs MN-major A");
   typename P::Ctx ctx;
@@ -256,8 +319,50 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
       }
     }
   };
+  // stage-split store: chunk q of a K-major operand = row q / R, k 4 (q % R) .. +3; of an
+  // MN-major operand = k row q / R, m 4 (q % R) .. +3 (R: fp32 chunks per row)
+  auto ss_store = [&](char* base, int plane, auto KMAJ, auto W, int R, int q, f32x4 v) {
+    uint2 hi, mi, lo;
+    split4(v, hi, mi, lo);
+    const int row = q / R, ch = q % R;
+    int off;
+    if constexpr (decltype(KMAJ)::value) {
+      constexpr int BK = decltype(W)::value;
+      const int u = ch & 3, pc = ((ch >> 2) * 2 + (u & 1)) ^ swz_k<BK>(row);
+      off = row * (BK * 2) + pc * 16 + (u >> 1) * 8;
+    } else {
+      constexpr int Wd = decltype(W)::value;
+      const int pc = (ch >> 1) ^ swz_m<Wd>(row);
+      off = row * (Wd * 2) + pc * 16 + (ch & 1) * 8;
+    }
+    *reinterpret_cast<uint2*>(base + off) = hi;
+    *reinterpret_cast<uint2*>(base + plane + off) = mi;
+    *reinterpret_cast<uint2*>(base + 2 * plane + off) = lo;
+  };
   auto sstore = [&](int buf, auto S) {
     constexpr int st = decltype(S)::value;
+    if constexpr (SS) {
+      char* As = reinterpret_cast<char*>(lds) + buf * (GS::SA + GS::SB);
+      char* Bs = As + GS::SA;
+      using KA = std::integral_constant<bool, P::A_KMAJ>;
+      using KB = std::integral_constant<bool, P::B_KMAJ>;
+      using WA = std::integral_constant<int, P::A_KMAJ ? G::BK : G::BM>;
+      using WB = std::integral_constant<int, P::B_KMAJ ? G::BK : G::BN>;
+#pragma unroll
+      for (int j = 0; j < G::NA; ++j) {
+        const int q = t + 256 * j;
+        if (G::CA % 256 == 0 || q < G::CA) {
+          ss_store(As, GS::PLA, KA{}, WA{}, G::RA, q, ra[st][j]);
+          if constexpr (COLSUM) csum += ra[st][j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < G::NB; ++j) {
+        const int q = t + 256 * j;
+        if (G::CB % 256 == 0 || q < G::CB) ss_store(Bs, GS::PLB, KB{}, WB{}, G::RB, q, rb[st][j]);
+      }
+      return;
+    }
     float* As = lds + buf * (G::SA + G::SB);
     float* Bs = As + G::SA;
 #pragma unroll
@@ -306,7 +411,67 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     }
     return v;
   };
+  // stage-split fragment of 16 k (k16 step s) for MFMA row/column `mn` of the wave tile
+  auto ss_frag = [&](const char* base, int plane, auto KMAJ, auto W, int mn0, int s) {
+    Split8 f;
+    if constexpr (decltype(KMAJ)::value) {
+      constexpr int BK = decltype(W)::value;
+      const int row = mn0 + r;
+      const char* p = base + row * (BK * 2) + (((2 * s + h) ^ swz_k<BK>(row)) * 16);
+      f.h = __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p));
+      f.m = __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + plane));
+      f.l = __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p + 2 * plane));
+    } else {
+      constexpr int Wd = decltype(W)::value;
+      const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+      const int col = mn0 + 16 * (g & 1) + 4 * pp, c = col >> 3, hb = ((col >> 2) & 1) * 8;
+      const int k1 = 16 * s + 4 * (g >> 1) + qq, k2 = k1 + 8;
+      const char* p1 = base + k1 * (Wd * 2) + ((c ^ swz_m<Wd>(k1)) * 16) + hb;
+      const char* p2 = base + k2 * (Wd * 2) + ((c ^ swz_m<Wd>(k2)) * 16) + hb;
+      uint2 x1, x2;
+      x1 = ds_tr16(p1);
+      x2 = ds_tr16(p2);
+      f.h = __builtin_bit_cast(bfx8, make_uint4(x1.x, x1.y, x2.x, x2.y));
+      x1 = ds_tr16(p1 + plane);
+      x2 = ds_tr16(p2 + plane);
+      f.m = __builtin_bit_cast(bfx8, make_uint4(x1.x, x1.y, x2.x, x2.y));
+      x1 = ds_tr16(p1 + 2 * plane);
+      x2 = ds_tr16(p2 + 2 * plane);
+      f.l = __builtin_bit_cast(bfx8, make_uint4(x1.x, x1.y, x2.x, x2.y));
+    }
+    return f;
+  };
   auto compute = [&](int buf) {
+    if constexpr (SS) {
+      const char* As = reinterpret_cast<const char*>(lds) + buf * (GS::SA + GS::SB);
+      const char* Bs = As + GS::SA;
+      using KA = std::integral_constant<bool, P::A_KMAJ>;
+      using KB = std::integral_constant<bool, P::B_KMAJ>;
+      using WA = std::integral_constant<int, P::A_KMAJ ? G::BK : G::BM>;
+      using WB = std::integral_constant<int, P::B_KMAJ ? G::BK : G::BN>;
+#pragma unroll
+      for (int s = 0; s < G::BK / 16; ++s) {
+        Split8 a[G::TM], b[G::TN];
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi) a[mi] = ss_frag(As, GS::PLA, KA{}, WA{}, wm * G::WTM + mi * 32, s);
+#pragma unroll
+        for (int ni = 0; ni < G::TN; ++ni) b[ni] = ss_frag(Bs, GS::PLB, KB{}, WB{}, wn * G::WTN + ni * 32, s);
+#pragma unroll
+        for (int mi = 0; mi < G::TM; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < G::TN; ++ni) {
+            f32x16 x = accx[mi][ni];
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].l, b[ni].h, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].m, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].l, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].m, b[ni].h, x, 0, 0, 0);
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].m, x, 0, 0, 0);
+            accx[mi][ni] = x;
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi].h, b[ni].h, acc[mi][ni], 0, 0, 0);
+          }
+      }
+      return;
+    }
     const float* As = lds + buf * (G::SA + G::SB);
     const float* Bs = As + G::SA;
     static_assert(G::BK % 16 == 0, "k-blocks of 16");
@@ -385,31 +550,35 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
 }
 
 
-template <class P>
-__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
-  __shared__ __attribute__((aligned(16))) float lds[Geo<P>::LDS_FLOATS];
-  __shared__ typename P::Smem sm;
-  gemm_body<P>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
-}
-
 template <int A, int B>
 struct MaxI {
   static constexpr int value = A > B ? A : B;
 };
+template <class P, bool SS>
+struct LdsFloats {
+  static constexpr int value = SS ? MaxI<GeoS<P>::LDS_BYTES / 4, 4 * 256>::value : Geo<P>::LDS_FLOATS;
+};
+
+template <class P, bool SS>
+__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
+  __shared__ __attribute__((aligned(16))) float lds[LdsFloats<P, SS>::value];
+  __shared__ typename P::Smem sm;
+  gemm_body<P, SS>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
+}
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2>
+template <class P1, class P2, bool SS>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
-  __shared__ __attribute__((aligned(16))) float lds[MaxI<Geo<P1>::LDS_FLOATS, Geo<P2>::LDS_FLOATS>::value];
+  __shared__ __attribute__((aligned(16))) float lds[MaxI<LdsFloats<P1, SS>::value, LdsFloats<P2, SS>::value>::value];
   __shared__ union {
     typename P1::Smem s1;
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1, SS>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2, SS>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -1286,6 +1455,8 @@ struct Conv2DgradPT {
 using Conv2DgradP = Conv2DgradPT<16>;
 using Conv2DgradP32 = Conv2DgradPT<32>;
 
+constexpr int kStageSplitDefault = 0;
+
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
   int splits, kbps;
@@ -1312,17 +1483,30 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
   }
 }
 
+// stage-split selection (bit 0: forward GEMMs, bit 1: backward pairs), read at launch time:
+// a captured graph keeps the form it was captured with.  Both forms give bit-identical results.
+int g_stage_split = -1;
+int stage_split_mask() {
+  if (g_stage_split < 0) {
+    const char* e = std::getenv("APEX_F32_STAGE_SPLIT");
+    g_stage_split = e ? std::atoi(e) : kStageSplitDefault;
+  }
+  return g_stage_split;
+}
+
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  gemm_k<P><<<blocks, 256, 0, s>>>(a);
+  if (stage_split_mask() & 1) gemm_k<P, true><<<blocks, 256, 0, s>>>(a);
+  else gemm_k<P, false><<<blocks, 256, 0, s>>>(a);
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  gemm2_k<P1, P2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  if (stage_split_mask() & 2) gemm2_k<P1, P2, true><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  else gemm2_k<P1, P2, false><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   LAUNCH_CHECK();
 }
 
@@ -1339,6 +1523,9 @@ void fwd_launch(const F32Set& set, hipStream_t s) {
 }
 
 }  // namespace
+
+void f32_set_stage_split(int mask) { g_stage_split = mask; }
+int f32_stage_split() { return stage_split_mask(); }
 
 // ------------------------------------------------------------------ host launchers
 // Tiles (MI355X, measured): the learner's launches (2-3 passes of its batch: >= 1024 rows) on

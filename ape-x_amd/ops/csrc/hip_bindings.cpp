@@ -461,6 +461,8 @@ PYBIND11_MODULE(_apex_hip, m) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });
   m.def("f32_fc1_splits", &f32_fc1_splits);
+  m.def("f32_set_stage_split", &f32_set_stage_split);
+  m.def("f32_stage_split", &f32_stage_split);
   m.def("f32_fc1_bwd_split", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ws, int B,
                                 uint64_t s) {
     f32_fc1_bwd_split(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ws), B,

@@ -379,6 +379,11 @@ struct F32Set {
 };
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0);
 int f32_fc1_splits();
+// GEMM form: bit 0 forward, bit 1 backward pairs use the stage-split LDS image (split once
+// per staged element) instead of the per-wave register split; -1 reads APEX_F32_STAGE_SPLIT.
+// Bit-identical either way; read at launch (graphs keep the form they captured).
+void f32_set_stage_split(int mask);
+int f32_stage_split();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count
 // target: conv2 / conv3 weight-gradient workgroups (<= 0: the default); the workspace, the
 // launch and the finalize job of one gradient must use the same value

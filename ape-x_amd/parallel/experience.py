@@ -511,6 +511,7 @@ class LearnerLinks:
         self.live = set(range(1, world))
         self.dropped: dict[int, str] = {}
         self.applied = {r: 0 for r in range(1, world)}
+        self.sent: dict[int, int] = {}  # packets each actor reported sending (stop handshake)
         self.version = 0
         self._hb_t = time.monotonic()
         self.closed = False
@@ -595,6 +596,7 @@ class LearnerLinks:
             try:
                 self.store.wait([f"{self.prefix}/sent/{r}"], timedelta(seconds=timeout))
                 sent = int(self.store.get(f"{self.prefix}/sent/{r}"))
+                self.sent[r] = sent
             except Exception as e:
                 self.drop(r, f"no packet count: {e!r}")
                 continue
@@ -617,8 +619,9 @@ class LearnerLinks:
         return self.stats()
 
     def stats(self) -> dict:
-        return {"applied": dict(self.applied), "dropped": dict(self.dropped), "live": sorted(self.live),
-                "params_skipped": {r: p.skipped for r, p in self.params.items()}}
+        return {"applied": dict(self.applied), "sent": dict(self.sent), "dropped": dict(self.dropped),
+                "live": sorted(self.live), "params_skipped": {r: p.skipped for r, p in self.params.items()},
+                "transport": "p2p"}
 
 
 class ActorLink:

@@ -89,6 +89,9 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--same-device", action="store_true", help="--gpus N on one GPU (every rank on cuda:0)")
     p.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
                    help="control-plane backend of the multi-rank form (the data plane is HIP IPC)")
+    p.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
+                   help="the multi-rank form's experience links: HIP IPC rings, or torch.distributed p2p "
+                        "(auto: IPC on GPUs)")
     p.add_argument("--launch-timeout", type=float, default=3600.0, help="--gpus N self-launch wall limit")
     return p
 
@@ -225,7 +228,7 @@ def train_central(a, rank: int, world: int) -> dict:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    ceng = CentralAQLEngine(config_from_args(a), dev, rank, world)
+    ceng = CentralAQLEngine(config_from_args(a), dev, rank, world, transport=a.transport)
     last = {}
     try:
         if rank != 0:
@@ -240,7 +243,7 @@ def train_central(a, rank: int, world: int) -> dict:
             if idx is None:
                 raise SystemExit(f"--resume latest: no model*.pth in {a.save_dir}")
             load_engine(ceng.eng, model_path(a.save_dir, idx), idx)
-            ceng.iterations, ceng.learner_steps = ceng.eng.iterations, ceng.eng.learner_steps
+            ceng.restore(ceng.eng.iterations, ceng.eng.learner_steps)
         writer = NullWriter() if a.no_tb else SummaryWriter(a.log_dir, comment=f"-{a.env}-learner-central")
         ceng.fill()
         if not a.no_graphs:
@@ -256,23 +259,47 @@ def train_central(a, rank: int, world: int) -> dict:
     return last
 
 
+def _crossed(lo: int, hi: int, every: int, offset: int = 0) -> bool:
+    """Some k in [lo, hi] with (k + offset) % every == 0."""
+    if hi < lo or every <= 0:
+        return False
+    return (hi + offset) // every * every >= lo + offset
+
+
 def _loop(a, eng: AQLEngine, iterate, envs_per_iter: int, episodes, start: int, writer, central=None) -> dict:
     """The training loop: ``iterate()`` per iteration (act + K SGD steps + publish + target
-    cadence, or its central form), checkpoints, metrics and greedy evaluations."""
+    cadence, or its central form), checkpoints, metrics and greedy evaluations.
+
+    Central: one ``iterate()`` is a learner SPIN (ingest + the SGD steps the applied rows
+    pay for); the iteration count, checkpoint / log / eval cadences and ``max_step`` follow
+    the recorded batches that reached the replay (CentralAQLEngine.data_iterations), and the
+    logged step counts / rates read the device SGD counter (one sync per log window)."""
     ep_idx, last = 0, {}
     t_win, it_win, steps_win = time.perf_counter(), start, eng.learner_steps
     jl = open(a.json_log, "a") if a.json_log else None
+    it = start  # the next iteration to complete
     try:
-        for it in range(start, a.max_step):
+        while it < a.max_step:
             iterate()   # act + K SGD steps + publish + (it % 20 == 0) target sync
             if central is not None:
-                eng.iterations, eng.learner_steps = central.iterations, central.learner_steps
-            if it % a.save_interval == 0 or it == a.max_step - 1:
-                save_engine(eng, model_path(a.save_dir, it))
-            log_now = (it + 1 - start) % a.log_interval == 0 or it == a.max_step - 1
-            ev = a.eval_interval > 0 and ((it + 1) % a.eval_interval == 0 or it == a.max_step - 1)
+                done = min(central.iterations, a.max_step)  # iterations completed so far
+                if done <= it:
+                    continue  # a spin that completed no recorded batch
+                lo, hi = it, done - 1
+                eng.iterations = done
+            else:
+                lo = hi = it
+            it = hi + 1
+            if _crossed(lo, hi, a.save_interval) or hi == a.max_step - 1:
+                if central is not None:
+                    central.refresh_steps()
+                save_engine(eng, model_path(a.save_dir, hi))
+            log_now = _crossed(lo, hi, a.log_interval, 1 - start) or hi == a.max_step - 1
+            ev = a.eval_interval > 0 and (_crossed(lo, hi, a.eval_interval, 1) or hi == a.max_step - 1)
             if not (log_now or ev):
                 continue
+            if central is not None:
+                central.refresh_steps()
             lq, lp, n = eng.learner.take_loss_means()
             eps = episodes()
             now = time.perf_counter()
@@ -286,14 +313,15 @@ def _loop(a, eng: AQLEngine, iterate, envs_per_iter: int, episodes, start: int, 
                 ep_idx += 1
             sps = (eng.learner_steps - steps_win) / dt
             writer.add_scalar("learner/steps_per_sec", sps, eng.learner_steps)
-            writer.add_scalar("actor/env_steps_per_sec", (it + 1 - it_win) * envs_per_iter / dt, eng.learner_steps)
-            last = {"iteration": it, "learner_steps": eng.learner_steps, "loss_q": lq, "loss_proposal": lp,
+            writer.add_scalar("actor/env_steps_per_sec", (hi + 1 - it_win) * envs_per_iter / dt, eng.learner_steps)
+            last = {"iteration": hi, "learner_steps": eng.learner_steps, "loss_q": lq, "loss_proposal": lp,
                     "episodes": len(eps), "actor_mean_return": float(np.mean([r for r, _ in eps])) if eps else None,
                     "sgd_steps_per_s": round(sps, 1), "target_syncs": len(eng.target_syncs)}
             if central is not None:
                 last["packets_applied"] = sum(central.applied.values())
+                last["learner_spins"] = central.spins
             if ev:
-                ret = greedy_eval(eng, a.eval_episodes, seed=a.seed + 7 * it)
+                ret = greedy_eval(eng, a.eval_episodes, seed=a.seed + 7 * hi)
                 for k, r in enumerate(ret):
                     writer.add_scalar("evaluator/episode_reward", r, eng.learner_steps)
                 last["greedy_mean_return"] = float(np.mean(ret))
@@ -301,7 +329,7 @@ def _loop(a, eng: AQLEngine, iterate, envs_per_iter: int, episodes, start: int, 
             if jl:
                 jl.write(json.dumps(last) + "\n")
                 jl.flush()
-            t_win, it_win, steps_win = time.perf_counter(), it + 1, eng.learner_steps
+            t_win, it_win, steps_win = time.perf_counter(), hi + 1, eng.learner_steps
     finally:
         writer.flush()
         if jl:

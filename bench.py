@@ -251,8 +251,6 @@ def main():
         print(f"preflight: IPC experience links unavailable ({args.transport_fallback}); "
               f"using the {args.transport} transport", file=sys.stderr)
     if args.algo == "aql":
-        if topo == "central" and args.transport == "p2p":
-            raise SystemExit(f"AQL central topology needs the HIP IPC links: {args.transport_fallback}")
         if topo == "central":
             return aql_central(args, rank, world, device, wd, pre)
         return aql(args, rank, world, device)
@@ -490,7 +488,7 @@ def aql_central(args, rank, world, device, wd, pre=None):
 
     cap = min(args.capacity, 1_000_000)
     cfg = AQLEngineConfig(env_id=args.aql_env, n_envs=args.envs, capacity=cap, seed=args.seed)
-    eng = CentralAQLEngine(cfg, device, rank, world, paced=not args.unpaced)
+    eng = CentralAQLEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport)
     wd.kick()
     if rank != 0:
         if not args.no_graphs:
@@ -536,7 +534,8 @@ def aql_central(args, rank, world, device, wd, pre=None):
         "data": "synthetic (GPU BipedalWalker-shaped env, random-init weights)",
         "config": {"model": f"AQL NoisyNet critic + proposal, {e.obs}-d obs, {e.adim}-d action, T={e.T} candidates",
                    "global_batch": cfg.batch_size, "seq_len": 1, "parallelism": f"central1+actors{world - 1}",
-                   "topology": "AQL learner + replay on rank 0, actor GPUs push rows over HIP IPC",
+                   "topology": "AQL learner + replay on rank 0, actor GPUs push rows over "
+                               + ("HIP IPC" if eng.transport == "ipc" else "torch.distributed p2p links"),
                    "env": cfg.env_id, "envs_per_actor_gpu": args.envs, "sgd_steps_per_iteration": eng.K,
                    "replay_capacity": cap, "optimizer": "Adam lr 1e-3 x2 (critic, proposal), clip 40 each"},
         "actor_env_steps_per_sec": round(packets * eng.E / dt, 1),
@@ -546,7 +545,10 @@ def aql_central(args, rank, world, device, wd, pre=None):
         "sgd_steps_per_transition_x_batch": round(n_sgd * cfg.batch_size / max(1, packets * eng.E), 4),
         "learner_samples_per_sec": round(sgd * cfg.batch_size, 1),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
-        "links_complete": all(links["applied"][r] == links["sent"][r] for r in links["live"]),
+        "links_complete": all(links["applied"][r] == links.get("sent", {}).get(r, links["applied"][r])
+                              for r in links["live"]),
+        "transport": eng.transport, "transport_fallback": getattr(args, "transport_fallback", None),
+        "iterations": eng.iterations, "learner_spins": eng.spins, "target_syncs": len(e.target_syncs),
         "preflight": pre,
         "timing": "rank 0 (the one learner) between two device syncs; actor ranks act continuously",
         "last_loss_q": round(st["loss_q"], 6), "last_loss_proposal": round(st["loss_proposal"], 6),

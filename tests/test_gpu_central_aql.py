@@ -15,16 +15,17 @@ pytestmark = pytest.mark.gpu
 def _cfg():
     from apex_amd.engine.aql import AQLEngineConfig
 
-    return AQLEngineConfig(env_id="CartPole-v0", n_envs=64, capacity=65536, batch_size=32, seed=3)
+    return AQLEngineConfig(env_id="CartPole-v0", n_envs=64, capacity=65536, batch_size=32, seed=3,
+                           target_update_interval=4)
 
 
-def _central_aql_body(rank, world, iters):
+def _central_aql_body(rank, world, iters, transport="ipc"):
     import torch.distributed as dist
 
     from apex_amd.engine.central_aql import CentralAQLEngine
 
     dev = torch.device("cuda", 0)
-    eng = CentralAQLEngine(_cfg(), dev, rank, world, heartbeat_every=0.05)
+    eng = CentralAQLEngine(_cfg(), dev, rank, world, heartbeat_every=0.05, transport=transport)
     if rank != 0:
         log = []
         eng.capture()  # (pushes the eager warm-up step)
@@ -50,6 +51,9 @@ def _central_aql_body(rank, world, iters):
         time.sleep(0.002)
         it += 1
     a1, s1 = sum(eng.applied.values()), eng.sgd_steps()
+    cadence = {"iterations": eng.iterations, "spins": eng.spins, "syncs": list(eng.eng.target_syncs),
+               "data_iterations": eng.data_iterations(), "packets_since_fill": a1 - eng._pk0 if transport == "p2p"
+               else eng._packets_consumed() - eng._pk0}
     st = eng.eng.learner.stats()
     links = eng.close()
     rp = eng.eng.replay
@@ -81,11 +85,15 @@ def _central_aql_body(rank, world, iters):
     live_leaves = int((rp.leaf_sum[:n] > 0).sum().item())
     return {"links": links, "filled": n, "want_rows": want.shape[0], "same_rows": key(have) == key(want),
             "live_leaves": live_leaves, "learner_steps": eng.learner_steps, "K": eng.K,
-            "loss_q": st["loss_q"], "sgd_steps": st["steps"], "gate_packets": a1 - a0, "gate_steps": s1 - s0}
+            "loss_q": st["loss_q"], "sgd_steps": st["steps"], "gate_packets": a1 - a0, "gate_steps": s1 - s0,
+            "cadence": cadence, "transport": eng.transport}
 
 
-def test_central_aql_every_transition_reaches_the_learner(cuda):
-    out, codes = _run(_central_aql_body, 3, (30,), timeout=240)
+@pytest.mark.parametrize("transport", ["ipc", "p2p"])
+def test_central_aql_every_transition_reaches_the_learner(cuda, transport):
+    """Both experience transports: the HIP IPC rings, and the torch.distributed p2p links the
+    bench's preflight falls back to when IPC is unusable (here host-staged over gloo)."""
+    out, codes = _run(_central_aql_body, 3, (30, transport), timeout=240)
     assert codes == [0, 0, 0]
     o = out[0]
     L = o["links"]
@@ -100,3 +108,14 @@ def test_central_aql_every_transition_reaches_the_learner(cuda):
     # the replay ratio: one SGD step per 32 rows that reached the replay (64-row packets: 2 each)
     assert o["gate_packets"] >= 30 and o["gate_steps"] == 2 * o["gate_packets"]
     assert o["loss_q"] == o["loss_q"]
+    assert o["transport"] == transport
+    # the reference cadence counts recorded batches (R = 2 packets each), not learner spins:
+    # the learner outruns the actors (more spins than iterations), and the target syncs once
+    # per completed iteration i with i % 4 == 0 (AQL_dis.py:127-129)
+    c = o["cadence"]
+    assert c["data_iterations"] == c["packets_since_fill"] // 2 >= 10
+    # (ipc: the host reads the consumed words the ingest publishes, so its count may trail
+    # the GPU by the last spin)
+    assert c["data_iterations"] - (1 if o["transport"] == "ipc" else 0) <= c["iterations"] <= c["data_iterations"]
+    assert c["spins"] > c["iterations"]
+    assert len(c["syncs"]) == -(-c["iterations"] // 4), c

@@ -295,3 +295,42 @@ def test_gemm_layers_are_fp32_class(cuda):
     # fp32 unit roundoff 6e-8: K <= 3136 accumulations stay within a few ulps of sum |a b|
     assert max(errs.values()) < 1e-6, errs
 
+
+
+@pytest.mark.parametrize("B", [96, 384])
+def test_stage_split_gemms_bit_identical(cuda, B):
+    """The stage-split GEMM form (each staged fp32 element split once into bf16 hi / mid / lo
+    planes in LDS, fragments read back as ready MFMA operands -- ds_read_b128 for K-major,
+    ds_read_b64_tr_b16 for MN-major operands) against the per-wave register split: the same
+    terms in the same MFMA k-slots, so every forward activation (3-problem learner launch:
+    B = 384 takes the learner-sized tiles), every input gradient and every weight gradient is
+    BIT-identical."""
+    from apex_amd import ops
+    from apex_amd.models.fused import forward_multi
+    from apex_amd.models.fused_f32 import F32DuelingNet, F32Workspace
+
+    hip = ops.hip()
+    A = 18
+    m, mt = _model(cuda, A=A, seed=11), _model(cuda, A=A, seed=12)
+    for p in m.parameters():
+        p.grad = torch.zeros_like(p)
+    net, tnet = F32DuelingNet(m), F32DuelingNet(mt)
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    x2 = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    dq = torch.randn(B, A, device=cuda) / B
+    prev = hip.f32_stage_split()
+    outs = []
+    try:
+        for mode in (0, 3):
+            hip.f32_set_stage_split(mode)
+            wss = [F32Workspace(B, A, cuda, keep_for_backward=(i == 0)) for i in range(3)]
+            forward_multi([(net, x, wss[0], None, None), (net, x2, wss[1], None, None), (tnet, x2, wss[2], None, None)])
+            net.backward(dq, x, wss[0])
+            torch.cuda.synchronize()
+            ws = wss[0]
+            outs.append([t.clone() for t in (ws.a1, ws.a2, ws.a3, ws.h, ws.q, wss[1].q, wss[2].q, ws.dz, ws.dy3,
+                                              ws.dy2, ws.dy1)] + [p.grad.clone() for p in m.parameters()])
+    finally:
+        hip.f32_set_stage_split(prev)
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), (i, float((a - b).abs().max()))
