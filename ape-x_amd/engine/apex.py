@@ -60,6 +60,11 @@ class EngineConfig:
     # gradient all-reduces (direct communicator, parallel/rccl.py) as one hipGraph per
     # staging half, instead of three phase graphs with eager collectives in between
     dp_graph: bool = False
+    # overlap mode, single process: where the actor graph starts within the learner step --
+    # "start" (with the step) or "loss" (after the fused loss + heads backward: the actor's
+    # forward then co-runs with the trunk backward and the optimizer instead of the
+    # learner's forward GEMMs; the learner graph is split there, one launch boundary)
+    actor_at: str = "start"
     seed: int = 1122
     learner: LearnerConfig = field(default_factory=LearnerConfig)
 
@@ -132,6 +137,12 @@ class ApexEngine:
             else None
         self._ev_actor = [torch.cuda.Event(), torch.cuda.Event()] if self.overlap else None
         self._ev_learn = torch.cuda.Event() if self.overlap else None
+        if cfg.actor_at not in ("start", "loss"):
+            raise ValueError("EngineConfig.actor_at must be 'start' or 'loss'")
+        # the learner graph split at the loss (the actor launches between its two halves)
+        self._split_at_loss = (self.overlap and cfg.actor_at == "loss" and self.hip_net and allreduce is None
+                               and not lc.private_rows)
+        self._g_learn_front = None
 
     # ------------------------------------------------------------------ eager bodies
     def publish_params(self) -> None:
@@ -180,6 +191,17 @@ class ApexEngine:
                     self.actor.apply_rows(apply_half * k + i)
             self.learner.pre_writes = [self.actor.staged_prio_write(apply_half * k + i) for i in range(k)]
         self.learner.forward_phase()
+
+    def _learn_front(self, apply_half: int) -> None:
+        """Split-at-loss learner graph, first half: staged actor rows + sample + forward x3 +
+        the fused loss / heads backward."""
+        self._stage_rows(apply_half)
+        self.learner.forward_phase(part="a")
+
+    def _stage_rows(self, apply_half: int) -> None:
+        k = self.cfg.actor_steps_per_learner_step
+        self.learner.pre_rows = [self.actor.staged_rows(apply_half * k + i) for i in range(k)]
+        self.learner.pre_writes = [self.actor.staged_prio_write(apply_half * k + i) for i in range(k)]
 
     def _learn_b(self):
         self.learner.optimize()
@@ -306,6 +328,15 @@ class ApexEngine:
                 self._g_dp = None
                 torch.cuda.synchronize(self.device)
                 apool = torch.cuda.graph_pool_handle()
+        if self._split_at_loss:
+            L = self.learner
+            self._g_learn_front = []
+            for h in (0, 1):
+                self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
+                self._g_learn_front.append(self._graph(lambda h=h: self._learn_front(1 - h), self._pool))
+                self._g_learn_a.append(self._graph(lambda: (L.forward_phase(part="b"), self._learn_b()), self._pool))
+            self._g_learn_b = None
+            return
         for h in (0, 1):
             self._g_actor.append(self._graph(lambda h=h: self._actor_half(h), apool))
             if self._dp:
@@ -358,6 +389,9 @@ class ApexEngine:
         h = self._half
         L = torch.cuda.current_stream(self.device)
         A = self._astream
+        if self._g_learn_front is not None:
+            self._train_step_split(h, L, A)
+            return
         with trace.range("actor.launch"):
             A.wait_event(self._ev_learn)
             with torch.cuda.stream(A):
@@ -382,6 +416,31 @@ class ApexEngine:
         if self.learn_steps % self.cfg.target_update_interval == 0:
             self.learner.sync_target()
         self._ev_learn.record(L)
+        self._half ^= 1
+
+    def _train_step_split(self, h: int, L, A) -> None:
+        """actor_at="loss": learner front (sample .. loss + heads backward) | actor half h on
+        the actor stream from there, beside the learner's trunk backward + optimizer.  Same
+        ordering as :meth:`_train_step_overlap`: actor step t follows learner step t-1 (L is in
+        order, the front of step t comes after it) and learner step t waits for actor t-1."""
+        with trace.range("apex.learner"):
+            L.wait_event(self._ev_actor[1 - h])
+            self._g_learn_front[h].replay()
+        with trace.range("actor.launch"):
+            self._ev_learn.record(L)
+            A.wait_event(self._ev_learn)
+            with torch.cuda.stream(A):
+                self._g_actor[h].replay()
+            self._ev_actor[h].record(A)
+        with trace.range("apex.learner"):
+            self._g_learn_a[h].replay()
+        self.learn_steps += 1
+        self.actor_steps += self.cfg.actor_steps_per_learner_step
+        if self.learn_steps % self.cfg.publish_param_interval == 0:
+            L.wait_event(self._ev_actor[h])  # the actor is not reading its weights
+            self.publish_params()
+        if self.learn_steps % self.cfg.target_update_interval == 0:
+            self.learner.sync_target()
         self._half ^= 1
 
     # ------------------------------------------------------------------ steps

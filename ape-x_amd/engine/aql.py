@@ -180,7 +180,7 @@ class AQLEngineConfig:
     #   aql_update      (both clipped Adam steps, noise reset of both critics, proposal copy,
     #                    step bump, the NEXT step's PER draw; the iteration's last step also
     #                    writes the acting copies)
-    # MI355X, batch 32: 19.0k SGD steps/s (profiles/r4_aql_engine.md).  False: the reference
+    # MI355X, batch 32: 19.0k SGD steps/s (profiles/archive_r4.md (r4_aql_engine.md)).  False: the reference
     # sequence of separate launches (per_sample, forward, backward, per_write_batch, gradients,
     # adam_step2, noise reset) -- the bit-identity baseline of tests/test_gpu_aql_engine.py.
     # (Round 4 alternatives measured slower and removed: a forked tree stream, the whole step

@@ -69,6 +69,8 @@ class GPUEvaluator:
         self._seen = torch.zeros(E)
         self.episodes = 0
         self.steps = 0
+        self.max_episode_steps = int(max_episode_steps)
+        self._graph, self._graph_steps = None, 0
 
     @staticmethod
     def _stream() -> int:
@@ -107,8 +109,34 @@ class GPUEvaluator:
         self.steps += 1
 
     def run(self, n_steps: int) -> None:
+        """``n_steps`` greedy steps of every env: whole replays of the captured chunk graph
+        (:meth:`capture`) while they fit, eager steps for the rest."""
+        if self._graph is not None:
+            for _ in range(n_steps // self._graph_steps):
+                self._graph.replay()
+                self.steps += self._graph_steps
+            n_steps %= self._graph_steps
         for _ in range(n_steps):
             self.step()
+
+    def capture(self, steps: int = 100) -> None:
+        """Capture ``steps`` greedy steps as one hipGraph on the current stream (the
+        evaluator's ~8 launches per step are host-bound when eager: a budget that finishes
+        capped episodes is thousands of steps per log window)."""
+        self.step()  # (a real step: every kernel's first launch happens outside the capture)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            for _ in range(steps):
+                self.step()
+        self.steps -= steps  # the captured steps did not run
+        self._graph, self._graph_steps = g, int(steps)
+
+    def running(self) -> tuple[torch.Tensor, torch.Tensor]:
+        """(return so far, steps so far) of every env's episode in progress (one host read):
+        the explicit marker for episodes still running at a log line."""
+        st = self.env_state[:, 25:27].cpu()  # S_EPRET, S_EPLEN (actor_kernels.hip)
+        return st[:, 0], st[:, 1]
 
     def poll(self) -> list[tuple[float, float]]:
         """(episode_reward, episode_length) of the episodes finished since the last poll

@@ -211,9 +211,15 @@ class DQNLearner:
         if self.dp_split:
             self.backward_phase()
 
-    def forward_phase(self) -> None:
+    def forward_phase(self, part: str | None = None) -> None:
         """Sample, forward x3, loss + heads backward; single-process: the whole backward
-        too; data-parallel split: up to the FC1 backward and its finalize."""
+        too; data-parallel split: up to the FC1 backward and its finalize.
+        ``part`` (single-process HIP learner): "a" = up to the fused loss + heads backward,
+        "b" = the trunk backward (+ the priority-tree branch) -- the two halves of the step
+        around the point where the overlapped engine may start its actor graph."""
+        if part == "b":
+            self._trunk_phase()
+            return
         s = self._stream()
         glob = shard = None
         if self.sharded is not None:  # gathered shard masses -> global pmin + weight scale
@@ -253,18 +259,12 @@ class DQNLearner:
                  "step_snap": self.step_snap.data_ptr(),
                  **({"dzx": self.ws_s.dzx.data_ptr(), "dzx_ps": self.ws_s.dzx.shape[1]}
                     if getattr(self.ws_s, "dzx", None) is not None else {})}, self.B, self.A, self.gamma_n, s)
-            heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
             if self.dp_split:
+                heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
                 self.net.fc_backward(self.ws_s, extra_jobs=[heads_job])
                 return
-            after = self._fork_point()
-            n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
-                                        sumsq=self.fin_partials if self.allreduce is None else None,
-                                        after_first=after)
-            if self.allreduce is None:
-                assert n <= self.fin_partials.numel()
-                self.n_fin_partials = n
-            self._tree_fork_end()
+            if part != "a":
+                self._trunk_phase()
             return
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
@@ -283,6 +283,22 @@ class DQNLearner:
                           self.dq.data_ptr(), self.prio.data_ptr(), s)
         self.flat_grad.zero_()
         q.backward(self.dq)
+
+    def _trunk_phase(self) -> None:
+        """Single-process HIP learner: FC1 + conv backward and the finalize (the heads'
+        partials folded in), the priority-tree branch forked beside it and joined at the end."""
+        assert self.hip_net and not self.dp_split
+        rp = self.replay
+        ids_s, _, jdx, _ = self._src
+        heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
+        after = self._fork_point()
+        n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
+                                    sumsq=self.fin_partials if self.allreduce is None else None,
+                                    after_first=after)
+        if self.allreduce is None:
+            assert n <= self.fin_partials.numel()
+            self.n_fin_partials = n
+        self._tree_fork_end()
 
     def backward_phase(self, after_first=None) -> None:
         """Data-parallel split, part 2: priority-tree writes on the forked tree stream beside

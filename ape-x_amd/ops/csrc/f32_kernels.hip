@@ -180,23 +180,34 @@ struct Split8 {
   bfx8 h, m, l;
 };
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-// One pair (a, b) -> packed bf16 words of its hi / mid / lo terms.  The two residual
-// subtractions run as one v_pk_add_f32 each (the same IEEE operations as two v_sub_f32: the
-// terms are bit-identical), 9 VALU per pair instead of 11.
+// One pair (a, b) -> packed bf16 words of its hi / mid / lo terms.  PK: the two residual
+// subtractions as one v_pk_add_f32 each (the same IEEE operations: bit-identical terms),
+// 9 VALU per pair instead of 11 -- measured 3.5 % SLOWER per step inside the register-split
+// GEMM loop (register pairs constrain the allocation, profiles/archive_r5.md (r5_ab_split_packed_sub.txt)),
+// so only the stage-split store (outside the MFMA loop) uses it.
+template <bool PK>
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& h, uint32_t& m, uint32_t& l) {
-  const f32x2 v = {a, b};
-  const f32x2 r = v - f32x2{trunc_bf16(a), trunc_bf16(b)};
-  const f32x2 rl = r - f32x2{trunc_bf16(r[0]), trunc_bf16(r[1])};
-  h = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
-  m = pack_bf16_hi(r[0], r[1]);
-  l = pack_bf16_hi(rl[0], rl[1]);  // exact: <= 8 significant bits
+  if constexpr (PK) {
+    const f32x2 v = {a, b};
+    const f32x2 r = v - f32x2{trunc_bf16(a), trunc_bf16(b)};
+    const f32x2 rl = r - f32x2{trunc_bf16(r[0]), trunc_bf16(r[1])};
+    h = pack_bf16_hi(a, b);  // (the perm takes the upper halves: truncation)
+    m = pack_bf16_hi(r[0], r[1]);
+    l = pack_bf16_hi(rl[0], rl[1]);  // exact: <= 8 significant bits
+  } else {
+    const float ar = a - trunc_bf16(a), br = b - trunc_bf16(b);
+    const float am = trunc_bf16(ar), bm = trunc_bf16(br);
+    h = pack_bf16_hi(a, b);
+    m = pack_bf16_hi(am, bm);
+    l = pack_bf16_hi(ar - am, br - bm);
+  }
 }
 __device__ __forceinline__ Split8 split8(f32x4 x0, f32x4 x1) {
   uint32_t h[4], m[4], l[4];
-  split_pair(x0[0], x0[1], h[0], m[0], l[0]);
-  split_pair(x0[2], x0[3], h[1], m[1], l[1]);
-  split_pair(x1[0], x1[1], h[2], m[2], l[2]);
-  split_pair(x1[2], x1[3], h[3], m[3], l[3]);
+  split_pair<false>(x0[0], x0[1], h[0], m[0], l[0]);
+  split_pair<false>(x0[2], x0[3], h[1], m[1], l[1]);
+  split_pair<false>(x1[0], x1[1], h[2], m[2], l[2]);
+  split_pair<false>(x1[2], x1[3], h[3], m[3], l[3]);
   return {__builtin_bit_cast(bfx8, make_uint4(h[0], h[1], h[2], h[3])),
           __builtin_bit_cast(bfx8, make_uint4(m[0], m[1], m[2], m[3])),
           __builtin_bit_cast(bfx8, make_uint4(l[0], l[1], l[2], l[3]))};
@@ -247,8 +258,8 @@ __device__ __forceinline__ int swz_m(int row) {
 }
 // one staged fp32 chunk (4 values) -> its hi / mid / lo bf16 words (split_pair: split8's terms)
 __device__ __forceinline__ void split4(f32x4 x, uint2& h, uint2& m, uint2& l) {
-  split_pair(x[0], x[1], h.x, m.x, l.x);
-  split_pair(x[2], x[3], h.y, m.y, l.y);
+  split_pair<true>(x[0], x[1], h.x, m.x, l.x);
+  split_pair<true>(x[2], x[3], h.y, m.y, l.y);
 }
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -260,7 +271,7 @@ __device__ __forceinline__ uint2 ds_tr16(const char* p) {
 // Every fp32 GEMM of the learner (gemm_body) on the bf16 matrix cores through split8: the
 // fp32-MFMA form (v_mfma_f32_32x32x2_f32) it replaced in round 5 ran 2142 vs 2378 learner
 // steps/s at the same fp32-class accuracy (profiles/r5_x6.md, tests/test_gpu_f32_net.py).
-template <class P, bool SS>
+template <class P, int SS>
 __device__ __forceinline__ void gemm_body(const typename P::Args& args, int block, float* lds,
                                           typename P::Smem& sm) {
   using G = Geo<P>;
@@ -507,6 +518,20 @@ __device__ __forceinline__ void gemm_body(const typename P::Args& args, int bloc
     sstore(0, S0{});
   }
   __syncthreads();
+  if constexpr (SS == 2) {  // one LDS image (half the footprint): the next k-block waits in
+                            // registers and is stored after a second barrier
+    for (; kb < ctx.kb1; ++kb) {
+      const bool more = kb + 1 < ctx.kb1;
+      if (more) gload(kb + 1, S0{});
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      if (more) {
+        __syncthreads();
+        sstore(0, S0{});
+      }
+      __syncthreads();
+    }
+  } else
   for (; kb < ctx.kb1; ++kb) {
     const bool more = kb + 1 < ctx.kb1;
     if (more) gload(kb + 1, S0{});
@@ -554,12 +579,14 @@ template <int A, int B>
 struct MaxI {
   static constexpr int value = A > B ? A : B;
 };
-template <class P, bool SS>
+// SS: 0 = register split (Geo image), 1 = stage-split double buffer, 2 = stage-split single buffer
+template <class P, int SS>
 struct LdsFloats {
-  static constexpr int value = SS ? MaxI<GeoS<P>::LDS_BYTES / 4, 4 * 256>::value : Geo<P>::LDS_FLOATS;
+  static constexpr int value =
+      SS ? MaxI<GeoS<P>::LDS_BYTES / (SS == 2 ? 8 : 4), 4 * 256>::value : Geo<P>::LDS_FLOATS;
 };
 
-template <class P, bool SS>
+template <class P, int SS>
 __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[LdsFloats<P, SS>::value];
   __shared__ typename P::Smem sm;
@@ -568,7 +595,7 @@ __global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
-template <class P1, class P2, bool SS>
+template <class P1, class P2, int SS>
 __global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<LdsFloats<P1, SS>::value, LdsFloats<P2, SS>::value>::value];
   __shared__ union {
@@ -1483,8 +1510,10 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
   }
 }
 
-// stage-split selection (bit 0: forward GEMMs, bit 1: backward pairs), read at launch time:
-// a captured graph keeps the form it was captured with.  Both forms give bit-identical results.
+// GEMM form per direction, read at launch time (a captured graph keeps the form it was
+// captured with): mask = forward form + 4 x backward-pair form, form 0 = register split,
+// 1 = stage-split (double-buffered LDS image), 2 = stage-split, single LDS image.  Every
+// form gives bit-identical results.
 int g_stage_split = -1;
 int stage_split_mask() {
   if (g_stage_split < 0) {
@@ -1497,16 +1526,22 @@ int stage_split_mask() {
 template <class P>
 void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   if (blocks <= 0) return;
-  if (stage_split_mask() & 1) gemm_k<P, true><<<blocks, 256, 0, s>>>(a);
-  else gemm_k<P, false><<<blocks, 256, 0, s>>>(a);
+  switch (stage_split_mask() & 3) {
+    case 1: gemm_k<P, 1><<<blocks, 256, 0, s>>>(a); break;
+    case 2: gemm_k<P, 2><<<blocks, 256, 0, s>>>(a); break;
+    default: gemm_k<P, 0><<<blocks, 256, 0, s>>>(a);
+  }
   LAUNCH_CHECK();
 }
 
 template <class P1, class P2>
 void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
   if (n1 + n2 <= 0) return;
-  if (stage_split_mask() & 2) gemm2_k<P1, P2, true><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
-  else gemm2_k<P1, P2, false><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  switch ((stage_split_mask() >> 2) & 3) {
+    case 1: gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
+    case 2: gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
+    default: gemm2_k<P1, P2, 0><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+  }
   LAUNCH_CHECK();
 }
 

@@ -379,9 +379,10 @@ struct F32Set {
 };
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0);
 int f32_fc1_splits();
-// GEMM form: bit 0 forward, bit 1 backward pairs use the stage-split LDS image (split once
-// per staged element) instead of the per-wave register split; -1 reads APEX_F32_STAGE_SPLIT.
-// Bit-identical either way; read at launch (graphs keep the form they captured).
+// GEMM form: mask = forward form + 4 x backward-pair form; form 0 = per-wave register split,
+// 1 = stage-split LDS image (split once per staged element, double-buffered), 2 = the same
+// with one LDS image; -1 reads APEX_F32_STAGE_SPLIT.  Bit-identical in every form; read at
+// launch (graphs keep the form they captured).
 void f32_set_stage_split(int mask);
 int f32_stage_split();
 int f32_fc1_fwd_multi(const F32Set& set, hipStream_t s);  // returns the slab count

@@ -50,7 +50,11 @@ def parser():
     p.add_argument("--eval-envs", type=int, default=8,
                    help="greedy evaluator envs on rank 0 (eps 0, unclipped rewards, origin_repo/eval.py); 0 = off")
     p.add_argument("--eval-interval", type=int, default=50, help="learner steps between evaluator chunks")
-    p.add_argument("--eval-steps", type=int, default=25, help="evaluator env steps per chunk")
+    p.add_argument("--eval-steps", default="25",
+                   help="evaluator env steps per chunk, or 'auto': enough that every evaluator env can finish a "
+                        "capped episode (max_episode_length steps) inside each log window of --bps_interval "
+                        "learner steps (run as captured graphs of 100 steps; slows training wall-clock, not "
+                        "its per-step dynamics)")
     return p
 
 
@@ -227,6 +231,17 @@ def main(argv=None) -> int:
                                  episode_life=bool(cfg.env.episode_life), max_episode_steps=cfg.env.max_episode_length)
         eval_stream = torch.cuda.Stream(device=device)
         ev_loaded = torch.cuda.Event()
+        if str(args.eval_steps) == "auto":
+            chunks = max(1, L.bps_interval // max(1, args.eval_interval))
+            eval_steps = -(-int(cfg.env.max_episode_length) // chunks)
+        else:
+            eval_steps = int(args.eval_steps)
+        if cfg.kernel.use_graphs and eval_steps >= 100:
+            with torch.cuda.stream(eval_stream):
+                evaluator.capture(100)
+            torch.cuda.synchronize(device)
+        print(f"evaluator: {args.eval_envs} envs, {eval_steps} greedy steps per {args.eval_interval} learner steps "
+              f"(episode cap {int(cfg.env.max_episode_length)})", flush=True)
 
     def eval_chunk():
         """Latest published weights -> evaluator (ordered after the publish on the training
@@ -239,7 +254,7 @@ def main(argv=None) -> int:
             else:
                 evaluator.load(learner.flat, getattr(learner, "net", None))
             ev_loaded.record(eval_stream)
-            evaluator.run(args.eval_steps)
+            evaluator.run(eval_steps)
         cur.wait_event(ev_loaded)
 
     max_step = int(L.max_step)
@@ -282,7 +297,13 @@ def main(argv=None) -> int:
                         line["evaluator/episode_reward"] = sum(eval_rets) / len(eval_rets)
                         line["evaluator/episode_length"] = sum(eval_lens) / len(eval_lens)
                         line["evaluator/episodes"] = float(evaluator.episodes)
+                        # episodes that ended at the step cap (eval.py:77's max_episode_length)
+                        line["evaluator/capped_episodes"] = float(sum(n >= evaluator.max_episode_steps
+                                                                      for n in eval_lens))
                         eval_rets, eval_lens = [], []
+                    run_ret, run_len = evaluator.running()  # episodes still in progress
+                    line["evaluator/running_return"] = float(run_ret.mean())
+                    line["evaluator/running_length"] = float(run_len.mean())
                 shard = getattr(eng, "actor", None)
                 if shard is not None:
                     ret, length, count = shard.episode_stats()

@@ -71,7 +71,10 @@ def parse():
                          "steps (untimed, counted as training; ~0.1 s): the GPU reaches its sustained clock only "
                          "after a stretch of load, so a short timed window right after setup is not a ramp "
                          "measurement (20-step windows, one box: 2276-2318 steps/s after 48, 2310-2345 after "
-                         "200, 2345 sustained over 2000 steps; profiles/r5_short_window.txt)")
+                         "200, 2345 sustained over 2000 steps; profiles/archive_r5.md (r5_short_window.txt))")
+    ap.add_argument("--actor-at", default="start", choices=["start", "loss"],
+                    help="overlapped engine: start the actor graph with the learner step, or after its fused "
+                         "loss + heads backward (beside the trunk backward)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="run the actor graph after the learner step on the same stream (default: the actor "
                          "graph runs on its own HIP stream, concurrent with the learner step)")
@@ -269,6 +272,7 @@ def main():
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
                        use_graphs=not args.no_graphs, overlap=args.overlap, seed=args.seed + 7919 * rank,
+                       actor_at=args.actor_at,
                        learner=lc)
     dp = world > 1 or args.force_dp
     allreduce = None
@@ -373,7 +377,7 @@ def main():
                 "fp32_gemms": "exact 3-term bf16 split (x6) on MFMA, fp32 accumulate" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
                 "graph_warm_replays": 0 if args.no_graphs else args.graph_warm,
-                "actor_learner_overlap": args.overlap,
+                "actor_learner_overlap": args.overlap, "actor_at": args.actor_at,
                 "dp_graph": eng._g_dp is not None,
                 # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
                 # gradient communicator, else the torch.distributed group size

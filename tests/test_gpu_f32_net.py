@@ -321,7 +321,7 @@ def test_stage_split_gemms_bit_identical(cuda, B):
     prev = hip.f32_stage_split()
     outs = []
     try:
-        for mode in (0, 3):
+        for mode in (0, 1 + 4, 2 + 8):  # register split | stage-split, 2 LDS images | 1 image
             hip.f32_set_stage_split(mode)
             wss = [F32Workspace(B, A, cuda, keep_for_backward=(i == 0)) for i in range(3)]
             forward_multi([(net, x, wss[0], None, None), (net, x2, wss[1], None, None), (tnet, x2, wss[2], None, None)])
