@@ -601,7 +601,7 @@ class AQLEngine:
         self.actL = h.make_aql_act(self.actor_net, self.obs_buf.data_ptr(), self.amu.data_ptr(), self.ws.data_ptr(),
                                    self.qbuf.data_ptr(), E, 64 if cfg.overlap else 0)
         h.aql_env_reset(self.env, self._s())
-        self.iterations = 0
+        self._iterations = 0
         self.learner_steps = 0
         self._g_actor = self._g_learn = self._g_iter = None
         self._ep_read = 0
@@ -687,8 +687,7 @@ class AQLEngine:
             return
         for _ in range(n):
             self.actor_step()
-        if self._tail is not None:  # the device iteration counter of the fused tail's beta
-            self._iter_dev.fill_(self.iterations)
+        self.iterations = self._iterations  # (resyncs the fused tail's device iteration counter)
         self.publish()
 
     def capture(self) -> None:
@@ -724,6 +723,21 @@ class AQLEngine:
         c = self.cfg  # AQL_dis.py:59 operator precedence kept
         return min(1.0, c.beta_start + self.iterations * (1.0 - c.beta_start) / c.max_step * c.n_workers)
 
+    @property
+    def iterations(self) -> int:
+        return self._iterations
+
+    @iterations.setter
+    def iterations(self, v: int) -> None:
+        """An assignment from outside the iteration loop (a checkpoint load, the central
+        engine's recorded-batch count): the fused acting tail's device iteration counter, which
+        computes the PER beta on the device (AQL_dis.py:59), follows it -- the two can never
+        disagree silently.  The loop's own increments go to ``_iterations`` (the tail kernel
+        bumps its device copy itself)."""
+        self._iterations = int(v)
+        if getattr(self, "_tail", None) is not None:
+            self._iter_dev.fill_(self._iterations)
+
     def iteration(self) -> None:
         """One actor step of all envs, weight publish, K learner steps."""
         if self.overlap:
@@ -743,7 +757,7 @@ class AQLEngine:
         if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):
             self.learner.sync_target()
             self.target_syncs.append(self.iterations)
-        self.iterations += 1
+        self._iterations += 1
 
     def _iteration_overlap(self) -> None:
         """Acting step t (staging half h) on the acting stream || the learner (apply half 1-h,
@@ -773,7 +787,7 @@ class AQLEngine:
         if target_sync_due(self.cfg, self.iterations, before, self.learner_steps):
             self.learner.sync_target()
             self.target_syncs.append(self.iterations)
-        self.iterations += 1
+        self._iterations += 1
         self._ev_learn.record(L)
         self._half ^= 1
 

@@ -326,7 +326,9 @@ class CentralAQLEngine:
         self.links.check_heartbeats()
         self.spins += 1
         self.iterations = done
-        e.iterations = done  # (beta anneals over recorded batches)
+        # beta anneals over recorded batches (host beta, set before each spin); rank 0 never
+        # acts, so its engine's fused-tail device counter is unused and needs no resync
+        e._iterations = done
 
     def refresh_steps(self) -> int:
         """SGD steps actually taken (the device counter behind the gate: one sync) ->

@@ -44,6 +44,7 @@
 // conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.  conv1 (forward
 // and weight gradient) has its own sample-resident kernels: u8 frame planes staged in LDS.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -579,33 +580,41 @@ template <int A, int B>
 struct MaxI {
   static constexpr int value = A > B ? A : B;
 };
-// SS: 0 = register split (Geo image), 1 = stage-split double buffer, 2 = stage-split single buffer
+// form SS: 0 = register split (Geo image), 1 = stage-split double buffer, 2 = stage-split single
+// buffer, 3 = form 2 compiled for >= 3 waves per SIMD (amdgpu_waves_per_eu: the 128 x 64 conv2
+// tile 204 -> 150 VGPRs, the others 104 -> 92, no spills)
 template <class P, int SS>
 struct LdsFloats {
   static constexpr int value =
-      SS ? MaxI<GeoS<P>::LDS_BYTES / (SS == 2 ? 8 : 4), 4 * 256>::value : Geo<P>::LDS_FLOATS;
+      SS ? MaxI<GeoS<P>::LDS_BYTES / (SS >= 2 ? 8 : 4), 4 * 256>::value : Geo<P>::LDS_FLOATS;
+};
+template <int SS>
+struct BodyForm {
+  static constexpr int value = SS == 3 ? 2 : SS;
 };
 
 template <class P, int SS>
-__global__ __launch_bounds__(256) void gemm_k(typename P::Args args) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SS == 3 ? 3 : 1))) void gemm_k(
+    typename P::Args args) {
   __shared__ __attribute__((aligned(16))) float lds[LdsFloats<P, SS>::value];
   __shared__ typename P::Smem sm;
-  gemm_body<P, SS>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
+  gemm_body<P, BodyForm<SS>::value>(args, xcd_chunk(blockIdx.x, gridDim.x), lds, sm);
 }
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
 template <class P1, class P2, int SS>
-__global__ __launch_bounds__(256) void gemm2_k(typename P1::Args a1, typename P2::Args a2, int n1) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SS == 3 ? 3 : 1))) void gemm2_k(
+    typename P1::Args a1, typename P2::Args a2, int n1) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<LdsFloats<P1, SS>::value, LdsFloats<P2, SS>::value>::value];
   __shared__ union {
     typename P1::Smem s1;
     typename P2::Smem s2;
   } sm;
   if ((int)blockIdx.x < n1)
-    gemm_body<P1, SS>(a1, blockIdx.x, lds, sm.s1);
+    gemm_body<P1, BodyForm<SS>::value>(a1, blockIdx.x, lds, sm.s1);
   else
-    gemm_body<P2, SS>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2, BodyForm<SS>::value>(a2, (int)blockIdx.x - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -1482,7 +1491,13 @@ struct Conv2DgradPT {
 using Conv2DgradP = Conv2DgradPT<16>;
 using Conv2DgradP32 = Conv2DgradPT<32>;
 
-constexpr int kStageSplitDefault = 0;
+// default: the forward GEMMs on the stage-split single-image form at >= 3 waves per SIMD (form
+// 3), the backward pairs on the register split.  Whole step, separate processes alternated on one
+// box (scripts/ab/apex_engine_ab.py, profiles/r6_stage_split.md): register split 2466, forward
+// form 2 2526.5, both directions form 2 2509; another box: register split 2434, forward form 2
+// 2478, forward form 3 2489 steps/s.  The backward pairs gain nothing (backward-only form 2:
+// 2341 vs 2345): their wgrad halves' LDS and the MN-major transposed reads eat the VALU saved.
+constexpr int kStageSplitDefault = 3;
 
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
@@ -1512,8 +1527,8 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
 
 // GEMM form per direction, read at launch time (a captured graph keeps the form it was
 // captured with): mask = forward form + 4 x backward-pair form, form 0 = register split,
-// 1 = stage-split (double-buffered LDS image), 2 = stage-split, single LDS image.  Every
-// form gives bit-identical results.
+// 1 = stage-split (double-buffered LDS image), 2 = stage-split, single LDS image, 3 = form 2
+// held to >= 3 waves per SIMD.  Every form gives bit-identical results.
 int g_stage_split = -1;
 int stage_split_mask() {
   if (g_stage_split < 0) {
@@ -1529,6 +1544,7 @@ void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
   switch (stage_split_mask() & 3) {
     case 1: gemm_k<P, 1><<<blocks, 256, 0, s>>>(a); break;
     case 2: gemm_k<P, 2><<<blocks, 256, 0, s>>>(a); break;
+    case 3: gemm_k<P, 3><<<blocks, 256, 0, s>>>(a); break;
     default: gemm_k<P, 0><<<blocks, 256, 0, s>>>(a);
   }
   LAUNCH_CHECK();
@@ -1540,6 +1556,7 @@ void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, i
   switch ((stage_split_mask() >> 2) & 3) {
     case 1: gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
     case 2: gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
+    case 3: gemm2_k<P1, P2, 3><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
     default: gemm2_k<P1, P2, 0><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
   }
   LAUNCH_CHECK();
@@ -1570,10 +1587,23 @@ int f32_stage_split() { return stage_split_mask(); }
 // profiles/r2_f32_kernel_tuning.md.
 static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 
-// c1_grid: conv1 workgroups (<= 0: kC1xGrid); tile 1: the learner's conv2 on 128 x 64 tiles at
-// BK 16 (the alternative to the default) -- per-call microbench parameters
+// c1_grid: conv1 workgroups (<= 0: kC1xGrid); tile (learner-sized launches, microbench
+// alternatives to the defaults): 1 = conv2 on 64 x 64, 2 = conv2 on 128 x 64 as 4 x 1 waves of
+// 32 x 64 / conv3 on 128 x 64 (2 x 2 waves), 3 = conv3 on 128 x 32 (4 x 1 waves)
+// the learner-sized forward tiles when the caller passes tile 0: APEX_F32_TILES="c2,c3" (the
+// microbench tile codes below; unset = the defaults), read once -- a whole-step A/B knob
+static int default_tile(int layer) {
+  static int t2 = -1, t3 = -1;
+  if (t2 < 0) {
+    t2 = t3 = 0;
+    if (const char* e = std::getenv("APEX_F32_TILES")) std::sscanf(e, "%d,%d", &t2, &t3);
+  }
+  return layer == 2 ? t2 : t3;
+}
+
 void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid, int tile) {
   check_set(set);
+  if (tile == 0 && (layer == 2 || layer == 3)) tile = default_tile(layer);
   switch (layer) {
     case 1:
       f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
@@ -1583,11 +1613,14 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
              // vs 73-79 for 64 x 64 (under fp32 MFMA 64 x 64 had won) and 76-88 for 256 x 64 (64 x 64
              // per wave: one wave per SIMD); whole step 2456-2466 vs 2193-2200 steps/s for 256 x 64
       if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
+      else if (learner_sized(set) && tile == 2) fwd_launch<Conv2FwdT<128, 64, 32, 4>>(set, s);
       else if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
       else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
       break;
     case 3:  // learner: 64 x 64 (46.7-46.8 us vs 80.6-84.5 for 256 x 64)
-      if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
+      if (learner_sized(set) && tile == 2) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
+      else if (learner_sized(set) && tile == 3) fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
+      else if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
       else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");

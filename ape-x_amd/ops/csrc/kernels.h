@@ -381,7 +381,7 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
 int f32_fc1_splits();
 // GEMM form: mask = forward form + 4 x backward-pair form; form 0 = per-wave register split,
 // 1 = stage-split LDS image (split once per staged element, double-buffered), 2 = the same
-// with one LDS image; -1 reads APEX_F32_STAGE_SPLIT.  Bit-identical in every form; read at
+// with one LDS image, 3 = form 2 held to >= 3 waves per SIMD; -1 reads APEX_F32_STAGE_SPLIT.  Bit-identical in every form; read at
 // launch (graphs keep the form they captured).
 void f32_set_stage_split(int mask);
 int f32_stage_split();

@@ -43,6 +43,10 @@ import time
 import numpy as np
 
 REFERENCE_BATCHES_PER_S = 12.0   # upper end of the reference's 10-12 batches/s
+# central topology: transition rows rank 0 ingests per learner step at >= 95 % of the 1-GPU
+# engine's rate (emulated links, one MI355X: 1024 rows 2605, 1792 rows 2520, 3072 rows 2388 vs
+# the 1-GPU engine's 2490 steps/s; profiles/r6_central_capacity.md)
+CENTRAL_ROW_BUDGET = 3136
 PAPER_BATCHES_PER_S = 19.0
 
 
@@ -116,6 +120,12 @@ def parse():
                          "or peer copy) dumps every thread's stack and exits 1, inside the driver's 600 s")
     ap.add_argument("--no-preflight", dest="preflight", action="store_false",
                     help="N>1: skip the multi-GPU preflight (peer access, IPC round trip, RCCL all-reduce)")
+    ap.add_argument("--central-envs", default="auto",
+                    help="central topology (N>1, --emulate-links): envs per actor GPU; each actor GPU pushes one "
+                         "packet of this many transitions per learner step.  auto: rank 0's ingest budget of "
+                         f"{CENTRAL_ROW_BUDGET} rows per learner step split over the N-1 actor GPUs (multiples of "
+                         "64, 256..2048): the learner stays >= 95 %% of the 1-GPU engine while the frames "
+                         "reaching the replay grow (profiles/r6_central_capacity.md)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
     ap.add_argument("--emulate-links", type=int, default=0, metavar="R",
@@ -560,6 +570,30 @@ def aql_central(args, rank, world, device, wd, pre=None):
     dist.destroy_process_group()
 
 
+# one actor GPU's unpaced frames/s by envs per GPU (bench.py --actor-only on MI355X,
+# profiles/r6_central_capacity.md); interpolated log-linearly in E
+ACTOR_GPU_CAPACITY_FPS = {256: 9.78e6, 512: 16.25e6, 1024: 22.0e6, 2048: 25.3e6}
+
+
+def actor_gpu_capacity(E: int) -> float:
+    pts = sorted(ACTOR_GPU_CAPACITY_FPS.items())
+    if E <= pts[0][0]:
+        return pts[0][1] * E / pts[0][0]
+    for (e0, f0), (e1, f1) in zip(pts, pts[1:]):
+        if E <= e1:
+            w = (np.log(E) - np.log(e0)) / (np.log(e1) - np.log(e0))
+            return float(f0 + w * (f1 - f0))
+    return pts[-1][1]
+
+
+def central_envs(args, n_links: int) -> int:
+    """Envs per actor GPU of the central topology: --central-envs, or (auto) the row budget
+    rank 0's learner absorbs at >= 95 % of the 1-GPU engine, split over the links."""
+    if str(args.central_envs) != "auto":
+        return int(args.central_envs)
+    return min(2048, max(256, CENTRAL_ROW_BUDGET // max(1, n_links) // 64 * 64))
+
+
 def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
     """Central-replay topology (BASELINE config 3; the default for N>1), asynchronous:
     rank 0 = THE learner (batch 512, the reference's single learner, origin_repo/learner.py:
@@ -578,7 +612,8 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
     if world < 2:
         raise SystemExit("--topology central needs >= 2 ranks")
     lc = LearnerConfig(batch_size=args.batch, forward=args.forward, dtype=args.dtype, seed=args.seed)
-    cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
+    E = central_envs(args, world - 1)
+    cfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        use_graphs=not args.no_graphs, seed=args.seed, learner=lc)
     eng = CentralApexEngine(cfg, device, rank, world, paced=not args.unpaced, transport=args.transport,
@@ -632,9 +667,15 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
                    "topology": "central replay on rank 0, async experience links over "
                                + ("HIP IPC (xGMI peer copies)" if eng.transport == "ipc" else args.backend),
                    "actor_pacing": "free" if args.unpaced else f"{args.actor_steps} packet/learner step/actor",
-                   "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": args.envs},
+                   "replay_capacity": eng.C_r * (world - 1), "envs_per_actor_gpu": E},
         "actor_frames_per_sec": round(packets * eng.frames_per_actor_step / dt, 1),
         "packets_applied_per_learner_step": round(packets / args.steps, 3),
+        # sampled transitions per new transition that reached the replay in the window
+        "replay_ratio": round(args.steps * args.batch / max(1, packets * E), 4),
+        # each actor GPU's frames/s against what one actor GPU generates unpaced at this E
+        # (bench.py --actor-only on MI355X, ACTOR_GPU_CAPACITY_FPS)
+        "actor_gpu_utilisation": round(packets * eng.frames_per_actor_step / dt / (world - 1)
+                                       / actor_gpu_capacity(E), 3),
         "replay_fill_seconds": round(t_fill, 3), "links": links,
         "links_complete": all(links["applied"][r] == links.get("sent", {}).get(r, links["applied"][r]) for r in links["live"]),
         "transport": eng.transport, "transport_fallback": getattr(args, "transport_fallback", None),

@@ -1,75 +1,65 @@
 #!/usr/bin/env python
-"""Whole-step A/B of single-GPU Ape-X engine variants on ONE box, interleaved: every variant
-is built, filled and captured in this process (the bench config: fp32 DQN, batch 512, 256
-envs, overlapped actor), then timed over ``--steps`` train steps, round-robin ``--rounds``
-times; prints learner steps/s per variant (median and every round) as one JSON line.
+"""Whole-step A/B of single-GPU Ape-X bench variants on ONE box, alternated: each variant is a
+fresh ``bench.py`` process (the bench config: fp32 DQN, batch 512, 256 envs, overlapped actor),
+run round-robin ``--rounds`` times; prints learner steps/s per variant (median and every round)
+as one JSON line.
 
 A variant is a comma-separated list of overrides ('-' = the defaults):
-  actor_at=start|loss     EngineConfig.actor_at
-  ss=MASK                 f32 GEMM forms at capture time, forward + 4 x backward pairs
-                          (0 register split, 1 stage-split, 2 stage-split single LDS image;
-                          f32_set_stage_split)
-  <EngineConfig field>=int
-e.g. ``python scripts/ab/apex_engine_ab.py ss=0 ss=8 ss=10 ss=8,actor_at=loss``.  Interleaving
-removes the 2-5 % box-to-box and clock-ramp differences a sequence of bench runs carries."""
+  ss=MASK        APEX_F32_STAGE_SPLIT: f32 GEMM forms, forward + 4 x backward pairs
+                 (0 register split, 1 stage-split, 2 stage-split single LDS image, 3 = 2 at >= 3 waves/SIMD)
+  env:NAME=VAL   any other environment variable
+  --flag[=VAL]   a bench.py flag (e.g. --actor-at=loss)
+e.g. ``python scripts/ab/apex_engine_ab.py - ss=4 ss=8 ss=8,--actor-at=loss``.
+
+Separate processes on purpose: several engines in one process draw their actor / tree streams
+from torch's pool, which spreads them over the GPU's 4 hardware queues round-robin -- an
+engine whose actor stream shares the learner's queue serialises (0.51 vs 0.31 ms per step,
+engine/apex.py reserve_actor_stream), which made a one-process A/B read 20 % differences that
+were queue placement, not kernels."""
 import argparse
 import json
 import os
 import statistics
+import subprocess
 import sys
-import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def run(variant: str, steps: int, warmup: int, timeout: float) -> float:
+    env = dict(os.environ)
+    flags = []
+    for item in ([] if variant == "-" else variant.split(",")):
+        if item.startswith("ss="):
+            env["APEX_F32_STAGE_SPLIT"] = item[3:]
+        elif item.startswith("env:"):
+            k, v = item[4:].split("=", 1)
+            env[k] = v
+        elif item.startswith("--"):
+            flags += item.split("=", 1)
+        else:
+            raise SystemExit(f"bad variant item {item!r}")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", str(warmup), *flags]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    if out.returncode != 0:
+        raise SystemExit(f"{variant}: bench.py exited {out.returncode}\n{out.stderr[-2000:]}")
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    return float(json.loads(line)["value"])
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("variants", nargs="+")
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--capacity", type=int, default=2_000_000)
-    ap.add_argument("--threshold", type=int, default=50_000)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--timeout", type=float, default=240.0)
     a = ap.parse_args()
-    import torch
-
-    from apex_amd import ops
-    from apex_amd.engine.apex import ApexEngine, EngineConfig
-    from apex_amd.engine.learner import LearnerConfig
-
-    hip = ops.hip()
-    dev = torch.device("cuda", 0)
-    engs = []
-    for v in a.variants:
-        kw, ss = {}, hip.f32_stage_split()
-        for item in ([] if v == "-" else v.split(",")):
-            k, x = item.split("=")
-            if k == "ss":
-                ss = int(x)
-            elif k == "actor_at":
-                kw[k] = x
-            else:
-                kw[k] = int(x)
-        hip.f32_set_stage_split(ss)
-        cfg = EngineConfig(n_envs=256, replay_capacity=a.capacity, threshold_size=a.threshold, overlap=True,
-                           learner=LearnerConfig(batch_size=512, forward="hip", dtype="fp32"), **kw)
-        eng = ApexEngine(cfg, dev)
-        eng.fill()
-        eng.capture(warm_replays=100)
-        torch.cuda.synchronize()
-        engs.append((v, eng))
-        print(f"built {v} (stage split {ss})", flush=True)
-    res = {v: [] for v, _ in engs}
+    res = {v: [] for v in a.variants}
     for rnd in range(a.rounds):
-        for v, eng in engs:
-            for _ in range(100):  # re-warm after the other variants ran
-                eng.train_step()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(a.steps):
-                eng.train_step()
-            torch.cuda.synchronize()
-            res[v].append(a.steps / (time.perf_counter() - t0))
-        print(f"round {rnd}: " + ", ".join(f"{v} {res[v][-1]:.1f}" for v, _ in engs), flush=True)
+        for v in a.variants:
+            res[v].append(run(v, a.steps, a.warmup, a.timeout))
+            print(f"round {rnd} {v}: {res[v][-1]:.1f}", flush=True)
     print(json.dumps({"steps_per_s_median": {v: round(statistics.median(x), 1) for v, x in res.items()},
                       "rounds": {v: [round(y, 1) for y in x] for v, x in res.items()}, "steps": a.steps}))
 

@@ -29,6 +29,8 @@ ap.add_argument("--rounds", type=int, default=1, help="time every case this many
 ap.add_argument("--c1-wgrad-s1", action="store_true", help="+ conv1 weight gradient at one sample per workgroup")
 ap.add_argument("--tile1", action="store_true", help="+ the alternative tiles: conv2 forward 64x64, "
                                                    "conv2/conv3 input gradient BK 32")
+ap.add_argument("--tile2", action="store_true", help="+ forward tiles: conv2 128x64 as 4x1 waves (32x64 each), "
+                                                   "conv3 128x64 (2x2 waves) and 128x32 (4x1)")
 ap.add_argument("--c1-grids", default="", help="extra conv1 forward cases at these workgroup counts")
 ap.add_argument("--wgrad-targets", default="", help="extra conv2/conv3 backward cases at these wgrad workgroup "
                                                     "targets, e.g. 512,1024 (default plan: the plain cases)")
@@ -125,6 +127,10 @@ if a.tile1:
     cases["conv2_bwd@t1"] = ((lambda: hip.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), net.w2t.data_ptr(),
                                                        ws.a1.data_ptr(), ws.dy1.data_ptr(), w2.data_ptr(), B, S(),
                                                        tile=1)), 2 * 2 * B * 81 * 64 * 512)
+if a.tile2:
+    cases["conv2_fwd@t2"] = ((lambda: hip.f32_conv_fwd_multi(2, set3(2), B, S(), tile=2)), 2 * P * 81 * 64 * 512)
+    cases["conv3_fwd@t2"] = ((lambda: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=2)), 2 * P * 49 * 64 * 576)
+    cases["conv3_fwd@t3"] = ((lambda: hip.f32_conv_fwd_multi(3, set3(3), B, S(), tile=3)), 2 * P * 49 * 64 * 576)
 for cg in [int(x) for x in a.c1_grids.split(",") if x]:
     cases[f"conv1_fwd@g{cg}"] = ((lambda cg=cg: hip.f32_conv_fwd_multi(1, set3(1), B, S(), c1_grid=cg)),
                                  2 * P * 400 * 32 * 256)

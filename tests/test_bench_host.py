@@ -54,3 +54,23 @@ def test_watchdog_fires_on_no_progress_and_not_while_kicked():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert "survived" in p.stdout and "not reached" not in p.stdout
     assert p.returncode == 1 and "Timeout" in p.stderr  # faulthandler's stack dump
+
+
+@pytest.mark.parametrize("links,want", [(1, 2048), (2, 1536), (3, 1024), (7, 448)])
+def test_central_envs_split_the_row_budget(links, want):
+    """Central topology: by default each actor GPU gets its share of rank 0's ingest budget
+    (CENTRAL_ROW_BUDGET rows per learner step, multiples of 64 in 256..2048), so the frames that
+    reach the replay grow with N while the learner holds its rate; an explicit value stands."""
+    import types
+
+    b = _bench()
+    assert b.central_envs(types.SimpleNamespace(central_envs="auto"), links) == want
+    assert links * want <= b.CENTRAL_ROW_BUDGET or want == 256
+    assert b.central_envs(types.SimpleNamespace(central_envs="320"), links) == 320
+
+
+def test_actor_capacity_interpolates_measured_points():
+    b = _bench()
+    for e, fps in b.ACTOR_GPU_CAPACITY_FPS.items():
+        assert b.actor_gpu_capacity(e) == pytest.approx(fps)
+    assert b.ACTOR_GPU_CAPACITY_FPS[256] < b.actor_gpu_capacity(384) < b.ACTOR_GPU_CAPACITY_FPS[512]

@@ -86,7 +86,9 @@ def _central_aql_body(rank, world, iters, transport="ipc"):
     return {"links": links, "filled": n, "want_rows": want.shape[0], "same_rows": key(have) == key(want),
             "live_leaves": live_leaves, "learner_steps": eng.learner_steps, "K": eng.K,
             "loss_q": st["loss_q"], "sgd_steps": st["steps"], "gate_packets": a1 - a0, "gate_steps": s1 - s0,
-            "cadence": cadence, "transport": eng.transport}
+            "cadence": cadence, "transport": eng.transport,
+            "inbox": ({r: (ib.n_posted, ib.n_done) for r, ib in eng.links.inbox.items()}
+                      if transport == "p2p" else None)}
 
 
 @pytest.mark.parametrize("transport", ["ipc", "p2p"])
@@ -99,7 +101,9 @@ def test_central_aql_every_transition_reaches_the_learner(cuda, transport):
     L = o["links"]
     assert L["dropped"] == {} and L["live"] == [1, 2]
     for r in (1, 2):  # every pushed packet applied; the actor logged exactly what it pushed
-        assert L["applied"][r] == L["sent"][r] == out[r]["sent"] == out[r]["steps"]
+        assert L["applied"][r] == L["sent"][r] == out[r]["steps"], (L, out[r], o["inbox"])
+        # (p2p: the actor's send count also holds the filler packets of the stop handshake)
+        assert out[r]["sent"] == out[r]["steps"] if transport == "ipc" else out[r]["sent"] >= out[r]["steps"]
         assert out[r]["version"] >= 1  # conflated weights reached the actor
     assert o["filled"] == 64 * (L["applied"][1] + L["applied"][2]) == o["want_rows"]
     assert o["same_rows"], "rank 0's replay rows differ from what the actors pushed"
@@ -109,13 +113,15 @@ def test_central_aql_every_transition_reaches_the_learner(cuda, transport):
     assert o["gate_packets"] >= 30 and o["gate_steps"] == 2 * o["gate_packets"]
     assert o["loss_q"] == o["loss_q"]
     assert o["transport"] == transport
-    # the reference cadence counts recorded batches (R = 2 packets each), not learner spins:
-    # the learner outruns the actors (more spins than iterations), and the target syncs once
-    # per completed iteration i with i % 4 == 0 (AQL_dis.py:127-129)
+    # the reference cadence counts recorded batches (R = 2 packets each), not learner spins
+    # (a spin that ingested nothing completes no iteration), and the target syncs once per
+    # completed iteration i with i % 4 == 0 (AQL_dis.py:127-129)
     c = o["cadence"]
     assert c["data_iterations"] == c["packets_since_fill"] // 2 >= 10
     # (ipc: the host reads the consumed words the ingest publishes, so its count may trail
     # the GPU by the last spin)
     assert c["data_iterations"] - (1 if o["transport"] == "ipc" else 0) <= c["iterations"] <= c["data_iterations"]
-    assert c["spins"] > c["iterations"]
+    # (ipc: the paced learner outruns the actor processes -- spins that ran no SGD step do not
+    # advance the cadence; the host-staged p2p links are slower, one packet per spin)
+    assert c["spins"] > c["iterations"] if transport == "ipc" else c["spins"] >= c["iterations"]
     assert len(c["syncs"]) == -(-c["iterations"] // 4), c

@@ -321,7 +321,7 @@ def test_stage_split_gemms_bit_identical(cuda, B):
     prev = hip.f32_stage_split()
     outs = []
     try:
-        for mode in (0, 1 + 4, 2 + 8):  # register split | stage-split, 2 LDS images | 1 image
+        for mode in (0, 1 + 4, 2 + 8, 3 + 12):  # register split | stage-split, 2 LDS images | 1 | 1, 3 waves
             hip.f32_set_stage_split(mode)
             wss = [F32Workspace(B, A, cuda, keep_for_backward=(i == 0)) for i in range(3)]
             forward_multi([(net, x, wss[0], None, None), (net, x2, wss[1], None, None), (tnet, x2, wss[2], None, None)])
@@ -332,5 +332,6 @@ def test_stage_split_gemms_bit_identical(cuda, B):
                                               ws.dy2, ws.dy1)] + [p.grad.clone() for p in m.parameters()])
     finally:
         hip.f32_set_stage_split(prev)
-    for i, (a, b) in enumerate(zip(*outs)):
-        assert torch.equal(a, b), (i, float((a - b).abs().max()))
+    for m, out in enumerate(outs[1:], 1):
+        for i, (a, b) in enumerate(zip(outs[0], out)):
+            assert torch.equal(a, b), (m, i, float((a - b).abs().max()))

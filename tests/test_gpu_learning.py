@@ -77,8 +77,8 @@ def _run(cuda, dtype: str, B: int = 256, steps: int = STEPS, seed: int = 1122):
 
 
 def _summary(traj):
-    keys = ("moved", "hip_vs_64", "t32_vs_64", "hip_vs_t32", "param_rel", "hip_loss_err", "t32_loss_err",
-            "hip_prio_err", "t32_prio_err")
+    keys = ("moved", "hip_vs_64", "t32_vs_64", "hip_vs_t32", "param_rel", "t32_param_rel", "hip_loss_err",
+            "t32_loss_err", "hip_prio_err", "t32_prio_err")
     for i in (0, 1, 2, 5, 10, 25, 50, 100, len(traj) - 1):
         if i < len(traj):
             print(i, {k: f"{traj[i][k]:.3g}" for k in keys})
@@ -129,8 +129,11 @@ def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
     assert traj[-1]["moved"] > 0
     # first steps: loss and priorities at kernel precision (the multi-seed precision-class
     # bound on the update itself is the test above)
+    # (multiplicative against torch fp32's own value on the same step -- measured, round 6:
+    # HIP 1.2e-4 / 1.1e-4 / 1.4e-4 vs torch 2.8e-5 / 2.7e-5 / 2.5e-5; the 8-seed test above shows
+    # which learner lands nearer fp64 is a per-seed coin toss)
     for row in traj[:3]:
-        assert row["hip_vs_64"] <= 3.0 * row["t32_vs_64"] + 5e-4, row
+        assert row["hip_vs_64"] <= 10.0 * row["t32_vs_64"], row
         assert row["hip_loss_err"] < 1e-4 and row["hip_prio_err"] < 1e-3
     # whole run: the HIP fp32 learner is no farther from the fp64 learner than PyTorch's
     # own fp32 learner (same fp32 roundoff class).  The sign-like RMSprop steps amplify any
@@ -141,14 +144,19 @@ def test_fp32_hip_learner_tracks_torch_fp32_learner(cuda):
     # step at which torch's copy leaves fp64 is a coin toss, so steps of the divergence onset
     # are not compared one by one (a per-step bound there passed or failed with torch's luck).
     # Once both have saturated (the second half) every step is compared, and the tail means.
+    # Every bound is multiplicative against torch fp32's own tail (no additive floors; measured,
+    # round 6, steps 100 / 199: distance to fp64 HIP 0.60 / 0.74 vs torch 0.60 / 0.70, loss error
+    # 0.019 / 0.045 vs 0.12 / 0.25, priority error 0.080 / 0.086 vs 0.13 / 0.076).
     tail = traj[len(traj) // 2:]
-    for row in tail:
-        assert row["hip_vs_64"] <= 1.5 * row["t32_vs_64"] + 0.05, row
-        assert row["param_rel"] <= 3.0 * row["t32_param_rel"] + 2e-4, row
     mean = lambda k: sum(r[k] for r in tail) / len(tail)  # noqa: E731
+    med = lambda k: sorted(r[k] for r in tail)[len(tail) // 2]  # noqa: E731
+    for row in tail:
+        assert row["hip_vs_64"] <= 1.5 * med("t32_vs_64"), row
+        assert row["param_rel"] <= 3.0 * med("t32_param_rel"), row
     assert mean("hip_vs_64") <= 1.5 * mean("t32_vs_64")
-    assert mean("hip_loss_err") <= 2.0 * mean("t32_loss_err") + 0.02
-    assert mean("hip_prio_err") <= 2.0 * mean("t32_prio_err") + 0.02
+    assert mean("param_rel") <= 2.0 * mean("t32_param_rel")
+    assert mean("hip_loss_err") <= 3.0 * mean("t32_loss_err")
+    assert mean("hip_prio_err") <= 2.0 * mean("t32_prio_err")
 
 
 def test_bf16_hip_learner_stays_in_band(cuda):
