@@ -158,6 +158,8 @@ class DQNLearner:
             self.lh_part = torch.zeros(self.lh_blocks * ((A + 1) * 128 + (A + 1) + 256), dtype=torch.float32,
                                        device=dev)
             self.step_snap = torch.zeros(1, dtype=torch.int64, device=dev)
+            # (a high-priority tree stream -- its single-workgroup kernels otherwise wait for CU
+            # room beside the backward -- measured 1011 vs 2492 learner steps/s: not used)
             self.tree_stream = torch.cuda.Stream(device=dev)
             # single-process learner: grad_finalize writes the grad-norm partials (every
             # gradient passes through it), so no separate sum-of-squares pass; with an
@@ -221,6 +223,7 @@ class DQNLearner:
             self._trunk_phase()
             return
         s = self._stream()
+        rp = self.replay
         glob = shard = None
         if self.sharded is not None:  # gathered shard masses -> global pmin + weight scale
             if self.sharded.in_kernel:
@@ -232,13 +235,17 @@ class DQNLearner:
         for extra in rows[:-1]:  # more than one staged actor step per learner step
             self.hip.apply_staged_rows(extra[0], self.replay.trans_ptrs(), extra[1].data_ptr(), extra[2].data_ptr(),
                                        extra[1].numel(), s)
-        rp = self.replay
         self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
                                    rows=rows[-1] if rows else None, out_rows=self.rows)
         if self.rows is not None:  # the batch reads its private rows (no idx indirection)
             self._src = (self.rows["s_ids"], self.rows["s2_ids"], None, SimpleNamespace(**self.rows))
         else:
             self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
+        self._forward_and_loss(s, part)
+
+    def _forward_and_loss(self, s: int, part: str | None = None) -> None:
+        """Forward x3 + loss (+ the backward: single process) of the batch in ``_src``."""
+        rp = self.replay
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
             # the loss reads (a, r, d) straight out of the transition table.  The three passes
@@ -331,21 +338,25 @@ class DQNLearner:
         the single-workgroup level walk: it occupies few CUs beside the backward GEMMs."""
         self.tree_stream.wait_event(ev)
         with torch.cuda.stream(self.tree_stream):
-            hooks, self.tree_hooks = self.tree_hooks, []
-            for fn in hooks:
-                fn()
-            pre, self.pre_writes = self.pre_writes, []
-            for slots, prios, filled in pre:
-                self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
-            # the single-workgroup walks (rank-sorted dedup, one workgroup per walk) on purpose:
-            # the batched per_write_batch (one wide launch per big tree level) finishes sooner
-            # but its workgroups compete with the backward GEMMs beside it -- measured 2188 vs
-            # 2303 learner steps/s (MI355X, round 5, interleaved; profiles/r5_x6.md)
-            self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
-                                         mix=(self.delta, self.lw, self.prio, self.loss))
-            tail, self.tree_tail = self.tree_tail, []
-            for fn in tail:
-                fn()
+            self.tree_phase()
+
+    def tree_phase(self) -> None:
+        """The priority-tree work of this step on the CURRENT stream (the forked branch's body)."""
+        hooks, self.tree_hooks = self.tree_hooks, []
+        for fn in hooks:
+            fn()
+        pre, self.pre_writes = self.pre_writes, []
+        for slots, prios, filled in pre:
+            self.replay.write_priorities(slots, prios, dedup=False, bumps=((filled, slots.numel()),))
+        # the single-workgroup walks (rank-sorted dedup, one workgroup per walk) on purpose:
+        # the batched per_write_batch (one wide launch per big tree level) finishes sooner
+        # but its workgroups compete with the backward GEMMs beside it -- measured 2188 vs
+        # 2303 learner steps/s (MI355X, round 5, interleaved; profiles/r5_x6.md)
+        self.replay.write_priorities(self.idx, None, dedup=True, bumps=((self.step_counter, 1),),
+                                     mix=(self.delta, self.lw, self.prio, self.loss))
+        tail, self.tree_tail = self.tree_tail, []
+        for fn in tail:
+            fn()
 
     def _tree_fork_end(self) -> None:
         torch.cuda.current_stream().wait_stream(self.tree_stream)  # join: the next sample reads the tree

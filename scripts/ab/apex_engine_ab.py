@@ -8,8 +8,8 @@ A variant is a comma-separated list of overrides ('-' = the defaults):
   ss=MASK        APEX_F32_STAGE_SPLIT: f32 GEMM forms, forward + 4 x backward pairs
                  (0 register split, 1 stage-split, 2 stage-split single LDS image, 3 = 2 at >= 3 waves/SIMD)
   env:NAME=VAL   any other environment variable
-  --flag[=VAL]   a bench.py flag (e.g. --actor-at=loss)
-e.g. ``python scripts/ab/apex_engine_ab.py - ss=4 ss=8 ss=8,--actor-at=loss``.
+  arg:--flag[=VAL]  a bench.py flag (e.g. arg:--actor-at=loss)
+e.g. ``python scripts/ab/apex_engine_ab.py - ss=4 ss=8 ss=8,arg:--actor-at=loss``.
 
 Separate processes on purpose: several engines in one process draw their actor / tree streams
 from torch's pool, which spreads them over the GPU's 4 hardware queues round-robin -- an
@@ -35,8 +35,8 @@ def run(variant: str, steps: int, warmup: int, timeout: float) -> float:
         elif item.startswith("env:"):
             k, v = item[4:].split("=", 1)
             env[k] = v
-        elif item.startswith("--"):
-            flags += item.split("=", 1)
+        elif item.startswith("arg:"):
+            flags += item[4:].split("=", 1)
         else:
             raise SystemExit(f"bad variant item {item!r}")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup", str(warmup), *flags]

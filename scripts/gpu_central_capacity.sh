@@ -25,7 +25,7 @@ for E in ${CENTRAL_ENVS:-256 512 1024}; do
     python - "$O/emu_R${R}_E${E}.log" "$R" "$E" <<'EOF'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-print(json.dumps({"R": int(sys.argv[2]), "E": int(sys.argv[3]), "steps_per_s": d["value"],
+print(json.dumps({"R": int(sys.argv[2]), "E": d["config"]["envs_per_actor_gpu"], "steps_per_s": d["value"],
                   "frames_per_s": d["actor_frames_per_sec"], "replay_ratio": d.get("replay_ratio"),
                   "actor_gpu_utilisation": d.get("actor_gpu_utilisation"),
                   "packets_per_step": d["packets_applied_per_learner_step"], "links_complete": d["links_complete"]}))

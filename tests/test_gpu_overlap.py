@@ -38,12 +38,12 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start"):
+def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start", capacity=4096):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
-    cfg = EngineConfig(n_envs=64, replay_capacity=4096, threshold_size=2048, overlap=overlap, use_graphs=graphs,
+    cfg = EngineConfig(n_envs=64, replay_capacity=capacity, threshold_size=2048, overlap=overlap, use_graphs=graphs,
                        publish_param_interval=4, target_update_interval=6, actor_at=actor_at,
                        learner=LearnerConfig(batch_size=256, forward="hip"))
     torch.manual_seed(0)
@@ -58,7 +58,7 @@ def test_graphs_equal_sequential_schedule(cuda, overlap, actor_at):
     launched with the step or -- actor_at="loss" -- between the two halves of the split
     learner graph) replays exactly like the same schedule run eagerly on one stream."""
     eng_g = _engine(cuda, overlap, True, actor_at=actor_at)
-    assert (eng_g._split_at_loss) == (actor_at == "loss")
+    assert eng_g._split_at_loss == (actor_at == "loss")
     eng_e = _engine(cuda, overlap, False)
     for eng in (eng_g, eng_e):
         eng.fill()
