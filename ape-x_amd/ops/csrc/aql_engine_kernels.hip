@@ -39,6 +39,8 @@
 // -(1/B) sum_k cnt_k log p_jk - ent_lam H_j with cnt_k = #{i : best_i = k}.
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "opt_dev.h"
@@ -406,8 +408,16 @@ __device__ __forceinline__ AqlTd aql_td(const AqlLearn& L, int b, int row, int a
                      L.w[b]);
 }
 
-// the backward of sample b by one workgroup (aql_learn_bwd_k)
+// the backward of sample b by one workgroup (aql_learn_bwd_k) of NT = 256 or 512 threads.  The
+// computing phases map thread tt < 256 to a row / column; with 512 threads the second half
+// shares the staging that dominates the workgroup (the ~110 KB of layer weights it reads:
+// 13k of ~30k cycles at 256 threads, profiles/r5_aql_engine.md): half the first-layer loads
+// per thread and half of every prefetched second-layer row, whose two partial dot products
+// are added through LDS.
+template <int NT>
 __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
+  static_assert(NT == 256 || NT == 512, "256 or 512 threads");
+  constexpr int NH = NT / 256;  // thread halves
   __shared__ __attribute__((aligned(16))) float s_s[64];
   __shared__ float s_a[kMaxAdim], qfh[kH], aoh[kCat], x[kCat], pre[kH], gh[kH], gx[kCat];
   __shared__ float emb[kCat], hid[kCat], mu[64], gmu[64];
@@ -418,9 +428,10 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   // row reads, conflict-free), action_out.0 zero-padded to 8 at pitch 9
   __shared__ __attribute__((aligned(16))) float sw_qf1[kH * kP68], sw_f[kCat * kP68];
   __shared__ float sw_ao1[kCat * (kMaxAdim + 1)];
+  __shared__ float red2[NH > 1 ? 256 : 1];  // the second half's partial second-layer dots
   const AQLNet& N = L.on;
   const float* eff = L.eff_on;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, tt = t & 255, hf = t >> 8;
   const int T = N.T, obs = N.obs, adim = N.adim, na = N.na, B = L.B, cont = N.cont;
   const int row = L.idx[b];
   const int a_idx = L.act[row];
@@ -428,47 +439,49 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   // the second-layer row this thread contracts later (q_feature.2 / action_out.2 /
   // dist_feature.0), prefetched now: its loads fly under the staging and the first layers
   // instead of opening a phase of their own
-  const float* w2row = t < kH ? N.qf_w2 + (size_t)t * kH
-                              : (t < 2 * kH ? (cont ? N.ao_w2 + (size_t)(t - kH) * kCat : nullptr)
-                                            : N.df_w1 + (size_t)(t - 2 * kH) * kCat);
-  f32x4 xr[kCat / 4];
+  const float* w2row = tt < kH ? N.qf_w2 + (size_t)tt * kH
+                               : (tt < 2 * kH ? (cont ? N.ao_w2 + (size_t)(tt - kH) * kCat : nullptr)
+                                              : N.df_w1 + (size_t)(tt - 2 * kH) * kCat);
+  constexpr int XR = kCat / 4 / NH;  // 16-byte chunks of the (half) row per thread
+  const int myN4 = (tt < kH ? kH / 4 : kCat / 4) / NH;
+  f32x4 xr[XR];
   if (w2row) {
 #pragma unroll
-    for (int k = 0; k < kCat / 4; ++k)
-      if (t >= kH || k < kH / 4) xr[k] = reinterpret_cast<const f32x4*>(w2row)[k];
+    for (int k = 0; k < XR; ++k)
+      if (k < myN4) xr[k] = reinterpret_cast<const f32x4*>(w2row)[hf * myN4 + k];
   }
   const int pa = kMaxAdim + 1, nao1 = cont ? kCat : kH;
   {  // first layers, every load in flight before the stores (clamped column index:
      // unconditional loads; columns past obs / adim stored as zeros)
-    float y1[16], y2[32], y3[4];
+    float y1[16 / NH], y2[32 / NH], y3[4 / NH];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+    for (int k = 0; k < 16 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 6, i = e & 63;
       y1[k] = N.qf_w1[r * obs + min(i, obs - 1)];
     }
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+    for (int k = 0; k < 32 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 6, i = e & 63;
       y2[k] = N.f_w[r * obs + min(i, obs - 1)];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = t + 256 * k, r = e >> 3, i = e & 7;
+    for (int k = 0; k < 4 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 3, i = e & 7;
       y3[k] = N.ao_w1[min(r, nao1 - 1) * adim + min(i, adim - 1)];
     }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+    for (int k = 0; k < 16 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 6, i = e & 63;
       sw_qf1[r * kP68 + i] = i < obs ? y1[k] : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int e = t + 256 * k, r = e >> 6, i = e & 63;
+    for (int k = 0; k < 32 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 6, i = e & 63;
       sw_f[r * kP68 + i] = i < obs ? y2[k] : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int e = t + 256 * k, r = e >> 3, i = e & 7;
+    for (int k = 0; k < 4 / NH; ++k) {
+      const int e = t + NT * k, r = e >> 3, i = e & 7;
       if (r < nao1) sw_ao1[r * pa + i] = i < adim ? y3[k] : 0.f;
     }
   }
@@ -485,7 +498,7 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   __syncthreads();
   AQL_STAMP(L, 1);
   if (!cont) {  // counts of every sample's best candidate (the [B, B] log-prob broadcast)
-    for (int i = wave; i < B; i += 4) {
+    for (int i = wave; i < B; i += NT / 64) {
       const int ri = L.idx[i];
       const int bi = wave_argmax(L.q_s + (size_t)i * T, T, lane);
       if (lane == 0) {
@@ -502,32 +515,54 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   }
   // forward of the taken candidate (s, a_mu[a]) + the proposal trunk.  First layers from
   // the LDS-staged matrices (thread per row), then the 64/128-wide layers wave-per-row.
-  if (t < kH) {
-    qfh[t] = relu(lds_dot64(sw_qf1 + t * kP68, s_s, N.qf_b1[t]));  // (zero past obs)
-  } else if (t < kH + (cont ? kCat : kH)) {
-    const int k = t - kH;
-    aoh[k] = relu(lds_row_dot(sw_ao1 + k * pa, kMaxAdim, s_a, N.ao_b1[k]));
-  }
-  if (t >= 2 * kH) {
-    const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
-    emb[k] = relu(lds_dot64(sw_f + k * kP68, s_s, N.f_b[k]));
+  if (hf == 0) {
+    if (t < kH) {
+      qfh[t] = relu(lds_dot64(sw_qf1 + t * kP68, s_s, N.qf_b1[t]));  // (zero past obs)
+    } else if (t < kH + (cont ? kCat : kH)) {
+      const int k = t - kH;
+      aoh[k] = relu(lds_row_dot(sw_ao1 + k * pa, kMaxAdim, s_a, N.ao_b1[k]));
+    }
+    if (t >= 2 * kH) {
+      const int k = t - 2 * kH;  // state embedding q.features (model.py:289-291)
+      emb[k] = relu(lds_dot64(sw_f + k * kP68, s_s, N.f_b[k]));
+    }
   }
   __syncthreads();
   AQL_STAMP(L, 2);
-  if (t < kH) {  // q_feature.2 (from the prefetched row)
-    x[kH + t] = relu(regs_dot4<kH / 4>(xr, qfh) + N.qf_b2[t]);
-  } else if (t < 2 * kH) {  // action_out.2 (continuous) / identity (discrete)
-    const int nn = t - kH;
-    x[nn] = cont ? relu(regs_dot4<kCat / 4>(xr, aoh) + N.ao_b2[nn]) : aoh[nn];
-  } else {  // proposal dist_feature.0
-    const int k = t - 2 * kH;
-    hid[k] = relu(regs_dot4<kCat / 4>(xr, emb) + N.df_b1[k]);
+  if constexpr (NH == 1) {
+    if (t < kH) {  // q_feature.2 (from the prefetched row)
+      x[kH + t] = relu(regs_dot4<kH / 4>(xr, qfh) + N.qf_b2[t]);
+    } else if (t < 2 * kH) {  // action_out.2 (continuous) / identity (discrete)
+      const int nn = t - kH;
+      x[nn] = cont ? relu(regs_dot4<kCat / 4>(xr, aoh) + N.ao_b2[nn]) : aoh[nn];
+    } else {  // proposal dist_feature.0
+      const int k = t - 2 * kH;
+      hid[k] = relu(regs_dot4<kCat / 4>(xr, emb) + N.df_b1[k]);
+    }
+  } else {  // each half contracts its half of the row; the first half adds the second's
+    float part = 0.f;
+    if (tt < kH) part = regs_dot4<kH / 8>(xr, qfh + hf * (kH / 2));
+    else if (tt < 2 * kH) part = cont ? regs_dot4<kCat / 8>(xr, aoh + hf * (kCat / 2)) : 0.f;
+    else part = regs_dot4<kCat / 8>(xr, emb + hf * (kCat / 2));
+    if (hf == 1) red2[tt] = part;
+    __syncthreads();
+    if (hf == 0) {
+      const float a = part + red2[tt];
+      if (tt < kH) {
+        x[kH + tt] = relu(a + N.qf_b2[tt]);
+      } else if (tt < 2 * kH) {
+        const int nn = tt - kH;
+        x[nn] = cont ? relu(a + N.ao_b2[nn]) : aoh[nn];
+      } else {
+        hid[tt - 2 * kH] = relu(a + N.df_b1[tt - 2 * kH]);
+      }
+    }
   }
   __syncthreads();
   AQL_STAMP(L, 3);
   if (t < kH) {  // advantage1 pre-activation (effective noisy weight)
     pre[t] = row_dot4<kCat / 4>(eff, t, x) + eff[kEffB1 + t];
-  } else if (t >= 2 * kH && t - 2 * kH < na) {  // proposal mean / logits
+  } else if (t >= 2 * kH && t < 256 && t - 2 * kH < na) {  // proposal mean / logits
     const int d = t - 2 * kH;
     mu[d] = row_dot4<kCat / 4>(N.df_w2, d, hid) + N.df_b2[d];
   }
@@ -572,7 +607,7 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   if (t < kCat) {  // advantage1 input gradient
     const float a = cols_dot<kH>(eff, kCat, kH, gh, t);
     gx[t] = x[t] > 0.f ? a : 0.f;
-  } else {  // proposal hidden gradient
+  } else if (t < 256) {  // proposal hidden gradient
     const int k = t - kCat;
     const float a = cols_dot<64>(N.df_w2, kCat, na, gmu, k);
     V[aqlv::GHID + k] = hid[k] > 0.f ? a : 0.f;
@@ -596,7 +631,7 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
     V[aqlv::QFH + k] = qfh[k];
     V[aqlv::H + k] = relu(pre[k]);
     V[aqlv::GH + k] = gh[k];
-  } else {
+  } else if (t < 256) {
     const int k = t - kCat - kH;
     if (k < na) V[aqlv::GMU + k] = gmu[k];
     if (k < obs) V[aqlv::S + k] = s_s[k];
@@ -679,13 +714,14 @@ __device__ __forceinline__ void td_tree_block(const AqlLearn& L, const TreeDesc&
   stamp(3);
 }
 
-__global__ __launch_bounds__(256) void aql_learn_bwd_k(AqlLearn L) {
+template <int NT>
+__global__ __launch_bounds__(NT) void aql_learn_bwd_k(AqlLearn L) {
   if (L.gate && L.gate_j >= *L.gate) return;  // (grid-uniform) a gated-off step
   if (L.bwd_tree && blockIdx.x == L.B) {  // block-uniform: the priority write (aql_learn_set_tree)
     td_tree_block(L, L.tree, L.bw, L.bwd_tree == 1 ? 1 << 30 : L.bwd_levels);
     return;
   }
-  aql_bwd_block(L, blockIdx.x);
+  aql_bwd_block<NT>(L, blockIdx.x);
 }
 
 // ------------------------------------------------------------------ weight gradients
@@ -1312,13 +1348,21 @@ void aql_act_q(const AqlLearn& L, hipStream_t s) {
   LAUNCH_CHECK();
 }
 
+constexpr int kAqlBwdThreadsDefault = 256;
+
 void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
   check_net(L.on);
   if (L.B < 1) return;
   if (L.bwd_tree && (L.B > 64 || L.bw.B != L.B || L.bw.E != 0 || !L.bw.idx || !L.bw.list || !L.bw.owner ||
                      !L.bw.max_prio || !L.act || !L.idx))
     throw std::invalid_argument("aql_learn_bwd: the priority write needs B <= 64 and every pointer");
-  aql_learn_bwd_k<<<L.B + (L.bwd_tree ? 1 : 0), 256, 0, s>>>(L);
+  // APEX_AQL_BWD_THREADS = 512: two thread halves per sample workgroup (and per tree workgroup)
+  static const int nt = [] {
+    const char* e = std::getenv("APEX_AQL_BWD_THREADS");
+    return e && std::atoi(e) == 512 ? 512 : kAqlBwdThreadsDefault;
+  }();
+  if (nt == 512) aql_learn_bwd_k<512><<<L.B + (L.bwd_tree ? 1 : 0), 512, 0, s>>>(L);
+  else aql_learn_bwd_k<256><<<L.B + (L.bwd_tree ? 1 : 0), 256, 0, s>>>(L);
   LAUNCH_CHECK();
 }
 

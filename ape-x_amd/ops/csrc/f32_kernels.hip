@@ -43,6 +43,17 @@
 // Independent backward GEMMs share one launch (gemm2_k: fc1 dgrad+wgrad, conv3 wgrad+dgrad,
 // conv2 wgrad+dgrad), so the backward is 4 GEMM launches + one grad_finalize.  conv1 (forward
 // and weight gradient) has its own sample-resident kernels: u8 frame planes staged in LDS.
+//
+// Two forms of the same GEMM body (bit-identical results, tests/test_gpu_f32_net.py):
+//  * register split: operands staged as fp32 in LDS; every wave splits every fragment it reads
+//    into bf16 hi / mid / lo (split8, 44 VALU per fragment and 16 k -- 11-18 VALU per MFMA);
+//  * stage split (GeoS): the thread that stages a 4-value chunk splits it ONCE and stores the three
+//    bf16 planes; fragments are read back ready (ds_read_b128 for K-major operands,
+//    ds_read_b64_tr_b16 -- the hardware transpose -- for MN-major ones): 3-8 VALU per MFMA, one
+//    LDS image (the next k-block waits in registers) so the footprint stays at the fp32 form's.
+// The forward launches run the stage split (co-running with the actor's forward, they gain most
+// from the VALU they no longer issue); the backward pairs keep the register split (measured no
+// faster staged: profiles/r6_stage_split.md).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>

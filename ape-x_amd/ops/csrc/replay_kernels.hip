@@ -152,13 +152,17 @@ __global__ void per_update_level_k(TreeDesc t, const int* __restrict__ ids, int 
 
 
 
-// Actor inserts: B (<= 1024) unique ring-ordered slots -> leaves AND every level in one
-// launch (a ring chunk dirties only a handful of nodes per level).
+// Actor inserts: B (<= kRingFusedMax) unique ring-ordered slots -> leaves AND every level in
+// one launch (a ring chunk dirties only a handful of nodes per level).  Up to 4096 slots in one
+// workgroup: the central learner's ingest writes R links x E rows per step (3136 at R = 7, E =
+// 448) on the tree stream beside the backward, where every extra single-workgroup launch of a
+// 1024-slot chunking waited for CU room on its own.
+constexpr int kRingFusedMax = 4096;
 __global__ __launch_bounds__(1024) void per_write_ring_fused_k(TreeDesc t, const int* __restrict__ idx,
                                                                const float* __restrict__ prio, int B, float alpha,
                                                                float* max_prio, int64_t* bump0, int64_t d0,
                                                                int64_t* bump1, int64_t d1) {
-  __shared__ int sids[1024];
+  __shared__ int sids[kRingFusedMax];
   __shared__ float red[16];
   float pmax = 0.f;
   for (int i = threadIdx.x; i < B; i += blockDim.x) {
@@ -395,7 +399,7 @@ void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int 
                                                   d1, mix);
     LAUNCH_CHECK();
     per_update_levels(t, sorted_scratch, B, s);
-  } else if (B <= 1024) {
+  } else if (B <= kRingFusedMax) {
     per_write_ring_fused_k<<<1, 1024, 0, s>>>(t, idx, prio, B, alpha, max_prio, bump0, d0, bump1, d1);
     LAUNCH_CHECK();
   } else {

@@ -284,11 +284,11 @@ class IpcLearnerLinks:
                       s2_ids=rp.s2_ids.data_ptr(), action=rp.action.data_ptr(), reward=rp.reward.data_ptr(),
                       done=rp.done.data_ptr(), frame_base=fb.data_ptr(), slot_base=sb.data_ptr())
         def tree_write(slots, prios):  # ring-ordered new rows (slot -1: nothing there)
-            # one-workgroup fused writes (leaves + every level) of <= 1024 rows each: they run on
+            # one-workgroup fused writes (leaves + every level) of <= 4096 rows each: they run on
             # the learner's tree stream beside the conv backward, where wide per-level launches
             # slow the backward's GEMMs (profiles/r5_x6.md, learner tree branch)
-            for k in range(0, slots.numel(), 1024):
-                rp.write_priorities(slots[k:k + 1024], prios[k:k + 1024], dedup=False)
+            for k in range(0, slots.numel(), 4096):
+                rp.write_priorities(slots[k:k + 4096], prios[k:k + 4096], dedup=False)
 
         links = cls(R, D, E, P, store, prefix, device, packet_nbytes=packet_bytes(E), tables=tables,
                     tree_write=tree_write, **kw)

@@ -68,6 +68,39 @@ def test_tree_ring_writes_fused(cuda):
     assert rp.min_priority() == pytest.approx(np.min(leaf[leaf > 0]), rel=1e-6)
 
 
+@pytest.mark.parametrize("E,R", [(448, 7), (1024, 3), (2048, 2)])
+def test_tree_ring_writes_fused_multi_region(cuda, E, R):
+    """The central learner's ingest write: R links' ring-ordered rows (each link's slots
+    contiguous in its own region, missing packets as -1 holes) as ONE fused launch of up to
+    4096 slots (leaves + every level in one workgroup); tree must equal the fp64 oracle."""
+    from apex_amd.engine.hbm_replay import HBMReplay
+
+    C = 2_000_000
+    rp = HBMReplay(C, n_envs=E, device=cuda, alpha=0.6)
+    rng = np.random.RandomState(E + R)
+    host = np.zeros(C)
+    C_r = C // R
+    for step in range(3):
+        parts = []
+        for r in range(R):
+            base = r * C_r + (step * E + 5 * r) % (C_r - E)
+            idx = (base + np.arange(E)).astype(np.int32)
+            if (r + step) % 4 == 3:  # a link with nothing ready this step
+                idx[:] = -1
+            parts.append(idx)
+        idx = np.concatenate(parts)
+        pr = rng.uniform(0.01, 2.0, size=idx.size).astype(np.float32)
+        ok = idx >= 0
+        host[idx[ok]] = pr[ok].astype(np.float64) ** 0.6
+        rp.write_priorities(torch.from_numpy(idx).to(cuda), torch.from_numpy(pr).to(cuda), dedup=False)
+    torch.cuda.synchronize()
+    leaf = rp.leaf_sum.cpu().numpy()
+    np.testing.assert_allclose(leaf, host, rtol=2e-6, atol=0)
+    levels = _tree_oracle(leaf, rp.level_sizes)
+    for k, t in enumerate(rp.node_sum):
+        np.testing.assert_allclose(t.cpu().numpy(), levels[k + 1], rtol=1e-12, atol=1e-9)
+
+
 def test_sample_stratified_and_weights(cuda):
     from apex_amd.engine.hbm_replay import HBMReplay
 
