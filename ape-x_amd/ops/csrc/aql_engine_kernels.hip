@@ -560,11 +560,37 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   }
   __syncthreads();
   AQL_STAMP(L, 3);
-  if (t < kH) {  // advantage1 pre-activation (effective noisy weight)
-    pre[t] = row_dot4<kCat / 4>(eff, t, x) + eff[kEffB1 + t];
-  } else if (t >= 2 * kH && t < 256 && t - 2 * kH < na) {  // proposal mean / logits
-    const int d = t - 2 * kH;
-    mu[d] = row_dot4<kCat / 4>(N.df_w2, d, hid) + N.df_b2[d];
+  if constexpr (NH == 1) {
+    if (t < kH) {  // advantage1 pre-activation (effective noisy weight)
+      pre[t] = row_dot4<kCat / 4>(eff, t, x) + eff[kEffB1 + t];
+    } else if (t >= 2 * kH && t - 2 * kH < na) {  // proposal mean / logits
+      const int d = t - 2 * kH;
+      mu[d] = row_dot4<kCat / 4>(N.df_w2, d, hid) + N.df_b2[d];
+    }
+  } else {  // half rows, the partial dots added through LDS
+    const float* wrow = nullptr;
+    const float* vin = nullptr;
+    if (tt < kH) {
+      wrow = eff + (size_t)tt * kCat;
+      vin = x;
+    } else if (tt >= 2 * kH && tt - 2 * kH < na) {
+      wrow = N.df_w2 + (size_t)(tt - 2 * kH) * kCat;
+      vin = hid;
+    }
+    float part = 0.f;
+    if (wrow) {
+      f32x4 xw[kCat / 8];
+#pragma unroll
+      for (int k = 0; k < kCat / 8; ++k) xw[k] = reinterpret_cast<const f32x4*>(wrow + hf * (kCat / 2))[k];
+      part = regs_dot4<kCat / 8>(xw, vin + hf * (kCat / 2));
+    }
+    if (hf == 1) red2[tt] = part;
+    __syncthreads();
+    if (hf == 0 && wrow) {
+      const float a = part + red2[tt];
+      if (tt < kH) pre[tt] = a + eff[kEffB1 + tt];
+      else mu[tt - 2 * kH] = a + N.df_b2[tt - 2 * kH];
+    }
   }
   __syncthreads();
   AQL_STAMP(L, 4);
@@ -604,29 +630,59 @@ __device__ __forceinline__ void aql_bwd_block(const AqlLearn& L, int b) {
   __syncthreads();
   AQL_STAMP(L, 5);
   float* V = L.vec + (size_t)b * aqlv::STRIDE;
-  if (t < kCat) {  // advantage1 input gradient
-    const float a = cols_dot<kH>(eff, kCat, kH, gh, t);
-    gx[t] = x[t] > 0.f ? a : 0.f;
-  } else if (t < 256) {  // proposal hidden gradient
-    const int k = t - kCat;
-    const float a = cols_dot<64>(N.df_w2, kCat, na, gmu, k);
-    V[aqlv::GHID + k] = hid[k] > 0.f ? a : 0.f;
-    V[aqlv::HID + k] = hid[k];
-    V[aqlv::EMB + k] = emb[k];
+  // the column contractions over 64 rows: with two halves, rows 32 hf .. 32 hf + 31 each
+  float c5 = 0.f;
+  if (tt < kCat) {  // advantage1 input gradient
+    c5 = NH == 1 ? cols_dot<kH>(eff, kCat, kH, gh, t)
+                 : cols_dot<kH / 2>(eff + (size_t)hf * (kH / 2) * kCat, kCat, kH / 2, gh + hf * (kH / 2), tt);
+  } else {  // proposal hidden gradient
+    const int k = tt - kCat;
+    c5 = NH == 1 ? cols_dot<64>(N.df_w2, kCat, na, gmu, k)
+                 : cols_dot<32>(N.df_w2 + (size_t)hf * 32 * kCat, kCat, max(0, min(32, na - 32 * hf)), gmu + 32 * hf, k);
+  }
+  if (NH > 1) {
+    if (hf == 1) red2[tt] = c5;
+    __syncthreads();
+    if (hf == 0) c5 += red2[tt];
+  }
+  if (hf == 0) {
+    if (t < kCat) {
+      gx[t] = x[t] > 0.f ? c5 : 0.f;
+    } else {
+      const int k = t - kCat;
+      V[aqlv::GHID + k] = hid[k] > 0.f ? c5 : 0.f;
+      V[aqlv::HID + k] = hid[k];
+      V[aqlv::EMB + k] = emb[k];
+    }
   }
   __syncthreads();
   AQL_STAMP(L, 6);
-  if (t < kCat) {
-    if (cont) {  // action_out.0 input gradient
-      const float a = cols_dot<kH>(N.ao_w2, kCat, kH, gx, t);
-      V[aqlv::GAOH + t] = aoh[t] > 0.f ? a : 0.f;
+  float c6 = 0.f;
+  if (tt < kCat) {  // action_out.0 input gradient
+    if (cont)
+      c6 = NH == 1 ? cols_dot<kH>(N.ao_w2, kCat, kH, gx, t)
+                   : cols_dot<kH / 2>(N.ao_w2 + (size_t)hf * (kH / 2) * kCat, kCat, kH / 2, gx + hf * (kH / 2), tt);
+  } else if (tt < kCat + kH) {  // q_feature.0 input gradient
+    const int k = tt - kCat;
+    c6 = NH == 1 ? cols_dot<kH>(N.qf_w2, kH, kH, gx + kH, k)
+                 : cols_dot<kH / 2>(N.qf_w2 + (size_t)hf * (kH / 2) * kH, kH, kH / 2, gx + kH + hf * (kH / 2), k);
+  }
+  if (NH > 1) {
+    if (hf == 1) red2[tt] = c6;
+    __syncthreads();
+    if (hf == 0) c6 += red2[tt];
+  }
+  if (hf == 1) {
+  } else if (t < kCat) {
+    if (cont) {
+      V[aqlv::GAOH + t] = aoh[t] > 0.f ? c6 : 0.f;
       V[aqlv::AOH + t] = aoh[t];
     }
     V[aqlv::X + t] = x[t];
     V[aqlv::GX + t] = gx[t];
-  } else if (t < kCat + kH) {  // q_feature.0 input gradient
+  } else if (t < kCat + kH) {
     const int k = t - kCat;
-    const float a = cols_dot<kH>(N.qf_w2, kH, kH, gx + kH, k);
+    const float a = c6;
     V[aqlv::GQFH + k] = qfh[k] > 0.f ? a : 0.f;
     V[aqlv::QFH + k] = qfh[k];
     V[aqlv::H + k] = relu(pre[k]);

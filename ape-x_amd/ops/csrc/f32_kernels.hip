@@ -1537,9 +1537,10 @@ SplitPlan wgrad_plan(int layer, int B, int target) {
 }
 
 // GEMM form per direction, read at launch time (a captured graph keeps the form it was
-// captured with): mask = forward form + 4 x backward-pair form, form 0 = register split,
-// 1 = stage-split (double-buffered LDS image), 2 = stage-split, single LDS image, 3 = form 2
-// held to >= 3 waves per SIMD.  Every form gives bit-identical results.
+// captured with): mask = forward form + 4 x backward-pair form (+ 16 x (1 + form) of the
+// forward launches below the learner's size, the actor's; unset = the forward form), form 0 =
+// register split, 1 = stage-split (double-buffered LDS image), 2 = stage-split, single LDS
+// image, 3 = form 2 held to >= 3 waves per SIMD.  Every form gives bit-identical results.
 int g_stage_split = -1;
 int stage_split_mask() {
   if (g_stage_split < 0) {
@@ -1549,10 +1550,14 @@ int stage_split_mask() {
   return g_stage_split;
 }
 
+// small: a launch below the learner's size (the actor's / evaluator's forward) -- bits 4-5 of the
+// mask, when set, give those launches a form of their own (form + 1; 0 = the forward form)
 template <class P>
-void launch1(const typename P::Args& a, int blocks, hipStream_t s) {
+void launch1(const typename P::Args& a, int blocks, hipStream_t s, bool small = false) {
   if (blocks <= 0) return;
-  switch (stage_split_mask() & 3) {
+  const int m = stage_split_mask();
+  const int form = small && ((m >> 4) & 3) ? ((m >> 4) & 3) - 1 : m & 3;
+  switch (form) {
     case 1: gemm_k<P, 1><<<blocks, 256, 0, s>>>(a); break;
     case 2: gemm_k<P, 2><<<blocks, 256, 0, s>>>(a); break;
     case 3: gemm_k<P, 3><<<blocks, 256, 0, s>>>(a); break;
@@ -1582,7 +1587,7 @@ void check_set(const F32Set& set) {
 
 template <class P>
 void fwd_launch(const F32Set& set, hipStream_t s) {
-  launch1<P>(set, set.n * P::tiles(set.B), s);
+  launch1<P>(set, set.n * P::tiles(set.B), s, set.n * set.B < 1024);
 }
 
 }  // namespace

@@ -43,10 +43,13 @@ import time
 import numpy as np
 
 REFERENCE_BATCHES_PER_S = 12.0   # upper end of the reference's 10-12 batches/s
-# central topology: transition rows rank 0 ingests per learner step at >= 95 % of the 1-GPU
-# engine's rate (emulated links, one MI355X: 1024 rows 2605, 1792 rows 2520, 3072 rows 2388 vs
-# the 1-GPU engine's 2490 steps/s; profiles/r6_central_capacity.md)
-CENTRAL_ROW_BUDGET = 3136
+# central topology: transition rows rank 0 ingests per learner step, split over the actor GPUs
+# (envs per actor GPU in CENTRAL_MIN_ENVS..2048, multiples of 64): the learner stays >= 95 % of
+# the 1-GPU engine while the frames reaching the replay grow with N (emulated links, one MI355X,
+# vs the 1-GPU engine's 2483 steps/s: R = 1 x 2048 envs 2556, R = 3 x 1344 2409, R = 7 x 640
+# 2377 steps/s; profiles/r6_central_capacity.md)
+CENTRAL_ROW_BUDGET = 4032
+CENTRAL_MIN_ENVS = 640
 PAPER_BATCHES_PER_S = 19.0
 
 
@@ -124,7 +127,7 @@ def parse():
                     help="central topology (N>1, --emulate-links): envs per actor GPU; each actor GPU pushes one "
                          "packet of this many transitions per learner step.  auto: rank 0's ingest budget of "
                          f"{CENTRAL_ROW_BUDGET} rows per learner step split over the N-1 actor GPUs (multiples of "
-                         "64, 256..2048): the learner stays >= 95 %% of the 1-GPU engine while the frames "
+                         f"64, {CENTRAL_MIN_ENVS}..2048): the learner stays >= 95 %% of the 1-GPU engine while the frames "
                          "reaching the replay grow (profiles/r6_central_capacity.md)")
     ap.add_argument("--transport", default="auto", choices=["auto", "ipc", "p2p"],
                     help="central topology: HIP IPC rings in rank 0's HBM (auto on GPUs) or torch.distributed P2P links")
@@ -591,7 +594,7 @@ def central_envs(args, n_links: int) -> int:
     rank 0's learner absorbs at >= 95 % of the 1-GPU engine, split over the links."""
     if str(args.central_envs) != "auto":
         return int(args.central_envs)
-    return min(2048, max(256, CENTRAL_ROW_BUDGET // max(1, n_links) // 64 * 64))
+    return min(2048, max(CENTRAL_MIN_ENVS, CENTRAL_ROW_BUDGET // max(1, n_links) // 64 * 64))
 
 
 def central(args, rank, world, device, wd, pre=None, emulate: int = 0):

@@ -56,16 +56,17 @@ def test_watchdog_fires_on_no_progress_and_not_while_kicked():
     assert p.returncode == 1 and "Timeout" in p.stderr  # faulthandler's stack dump
 
 
-@pytest.mark.parametrize("links,want", [(1, 2048), (2, 1536), (3, 1024), (7, 448)])
+@pytest.mark.parametrize("links,want", [(1, 2048), (2, 1984), (3, 1344), (7, 640)])
 def test_central_envs_split_the_row_budget(links, want):
     """Central topology: by default each actor GPU gets its share of rank 0's ingest budget
     (CENTRAL_ROW_BUDGET rows per learner step, multiples of 64 in 256..2048), so the frames that
-    reach the replay grow with N while the learner holds its rate; an explicit value stands."""
+    reach the replay grow with N while the learner holds its rate (a floor of CENTRAL_MIN_ENVS per
+    actor GPU lets N = 8 deliver more than N = 4); an explicit value stands."""
     import types
 
     b = _bench()
     assert b.central_envs(types.SimpleNamespace(central_envs="auto"), links) == want
-    assert links * want <= b.CENTRAL_ROW_BUDGET or want == 256
+    assert links * want <= b.CENTRAL_ROW_BUDGET or want == b.CENTRAL_MIN_ENVS
     assert b.central_envs(types.SimpleNamespace(central_envs="320"), links) == 320
 
 
