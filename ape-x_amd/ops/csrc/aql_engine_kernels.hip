@@ -785,10 +785,12 @@ constexpr int kGradThreads = 256;
 
 // the weight gradients of flat elements [bid * 256, +256) and the block's per-group sums of
 // squares (aql_grad_k); returns the thread's gradient
+// (a 512-thread launch: waves 4..7 of a gradient block hold no element -- they exist for the
+// launch's level-walk workgroup -- and add zeros to nothing: the partials are bit-identical)
 __device__ __forceinline__ float aql_grad_block(const AqlGrad& G, int bid, int nblk) {
   __shared__ double red[2][4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int64_t i = (int64_t)bid * kGradThreads + t;
+  const int64_t i = t < kGradThreads ? (int64_t)bid * kGradThreads + t : G.n;
   float g = 0.f;
   int grp = -1;
   if (i < G.n) {
@@ -827,7 +829,7 @@ __device__ __forceinline__ float aql_grad_block(const AqlGrad& G, int bid, int n
   double s0 = grp == 0 ? (double)g * (double)g : 0.0, s1 = grp == 1 ? (double)g * (double)g : 0.0;
   s0 = wave_sum(s0);
   s1 = wave_sum(s1);
-  if (lane == 0) {
+  if (lane == 0 && wave < 4) {
     red[0][wave] = s0;
     red[1][wave] = s1;
   }
@@ -1032,7 +1034,11 @@ __device__ __forceinline__ void draw_block(const AqlStep& D, int k, uint64_t st)
 // aql_grad_k: the gradient blocks, then (G.tree_leaves) one workgroup walking the priority
 // tree's levels levels_lo.. of this step's dirty list -- the backward launch's tree workgroup
 // wrote the leaves, the list and the lowest levels
-__global__ __launch_bounds__(kGradThreads) void aql_grad_k(AqlGrad G) {
+// NT = 512: the level-walk workgroup runs 8 waves (update_levels_fast: 4 ancestors per wave per
+// level instead of 8) -- that walk, not the gradient blocks, is the launch's critical path
+// (profiles/r5_aql_engine.md: the walk takes the launch from 5.5 to 9.0 us)
+template <int NT>
+__global__ __launch_bounds__(NT) void aql_grad_k(AqlGrad G) {
   if (G.gate && G.gate_j >= *G.gate) return;  // (grid-uniform) a gated-off step
   if (G.step_snap && blockIdx.x == 0 && threadIdx.x == 0) *G.step_snap = *G.step_src;
   const int ng = (int)gridDim.x - (G.tree_leaves ? 1 : 0);
@@ -1404,7 +1410,9 @@ void aql_act_q(const AqlLearn& L, hipStream_t s) {
   LAUNCH_CHECK();
 }
 
-constexpr int kAqlBwdThreadsDefault = 256;
+// 512 threads per backward workgroup: bench.py --algo aql 19648 -> 20857 SGD steps/s (two
+// alternated processes each, one box; profiles/r6_aql.md)
+constexpr int kAqlBwdThreadsDefault = 512;
 
 void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
   check_net(L.on);
@@ -1412,10 +1420,11 @@ void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
   if (L.bwd_tree && (L.B > 64 || L.bw.B != L.B || L.bw.E != 0 || !L.bw.idx || !L.bw.list || !L.bw.owner ||
                      !L.bw.max_prio || !L.act || !L.idx))
     throw std::invalid_argument("aql_learn_bwd: the priority write needs B <= 64 and every pointer");
-  // APEX_AQL_BWD_THREADS = 512: two thread halves per sample workgroup (and per tree workgroup)
+  // APEX_AQL_BWD_THREADS = 256 | 512: one or two thread halves per sample workgroup (and per tree
+  // workgroup)
   static const int nt = [] {
     const char* e = std::getenv("APEX_AQL_BWD_THREADS");
-    return e && std::atoi(e) == 512 ? 512 : kAqlBwdThreadsDefault;
+    return e ? (std::atoi(e) == 256 ? 256 : 512) : kAqlBwdThreadsDefault;
   }();
   if (nt == 512) aql_learn_bwd_k<512><<<L.B + (L.bwd_tree ? 1 : 0), 512, 0, s>>>(L);
   else aql_learn_bwd_k<256><<<L.B + (L.bwd_tree ? 1 : 0), 256, 0, s>>>(L);
@@ -1423,6 +1432,10 @@ void aql_learn_bwd(const AqlLearn& L, hipStream_t s) {
 }
 
 int aql_grad_blocks(int64_t n) { return (int)((n + kGradThreads - 1) / kGradThreads); }
+
+// 512 threads per gradient workgroup (the level-walk workgroup's extra halves; the gradient rows
+// keep 256): 20843 -> 21726 SGD steps/s (profiles/r6_aql.md)
+constexpr int kAqlGradThreadsDefault = 512;
 
 void aql_grad(const AqlGrad& g, hipStream_t s) {
   if (g.njobs < 1 || g.njobs > kAqlMaxJobs || g.job[0].off != 0) throw std::invalid_argument("aql_grad: jobs");
@@ -1435,7 +1448,12 @@ void aql_grad(const AqlGrad& g, hipStream_t s) {
   }
   if (g.tree_leaves && (g.bw.B < 1 || g.bw.B > 64 || !g.bw.list))
     throw std::invalid_argument("aql_grad: the level walk takes a list of 1..64 learner rows");
-  aql_grad_k<<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), kGradThreads, 0, s>>>(g);
+  static const int nt = [] {  // APEX_AQL_GRAD_THREADS = 256 | 512
+    const char* e = std::getenv("APEX_AQL_GRAD_THREADS");
+    return e ? (std::atoi(e) == 512 ? 512 : 256) : kAqlGradThreadsDefault;
+  }();
+  if (nt == 512) aql_grad_k<512><<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), 512, 0, s>>>(g);
+  else aql_grad_k<256><<<aql_grad_blocks(g.n) + (g.tree_leaves ? 1 : 0), 256, 0, s>>>(g);
   LAUNCH_CHECK();
 }
 

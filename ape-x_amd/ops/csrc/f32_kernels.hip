@@ -1508,7 +1508,9 @@ using Conv2DgradP32 = Conv2DgradPT<32>;
 // form 2 2526.5, both directions form 2 2509; another box: register split 2434, forward form 2
 // 2478, forward form 3 2489 steps/s.  The backward pairs gain nothing (backward-only form 2:
 // 2341 vs 2345): their wgrad halves' LDS and the MN-major transposed reads eat the VALU saved.
-constexpr int kStageSplitDefault = 3;
+// The actor's small forward launches (256 envs, beside the learner's forward) on the register
+// split: 2497 vs 2489 (both rounds of an alternated A/B).
+constexpr int kStageSplitDefault = 3 + 16 * (0 + 1);  // (+ the actor's small launches on form 0)
 
 // wgrad split sizing: ~target blocks over (n-tiles x splits)
 struct SplitPlan {
