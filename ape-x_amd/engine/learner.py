@@ -52,6 +52,11 @@ class LearnerConfig:
     # private buffers that the forward, loss and backward read: writers of the replay tables
     # may then run beside the step (the central topology's ingest, engine/central.py)
     private_rows: bool = False
+    # the step's priority-tree write as extra workgroups of the trunk backward's launches (the
+    # leaves with the FC1 pair, level 1 with the conv3 pair, level 2 + the top with the conv2
+    # pair: ops/csrc/tree_dev.h tree_ride) instead of a forked tree stream joined before the
+    # optimizer -- fp32 HIP learner, single process, no ingest tail
+    tree_ride: bool = True
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -180,6 +185,7 @@ class DQNLearner:
         # staged actor rows scattered into the tables by the sampling launch:
         # (staged table ptr dict, slots, raw priorities)
         self.pre_rows = []
+        self.tree_rides_used = False  # the last traced trunk backward carried the tree riders
 
     @staticmethod
     def _stream() -> int:
@@ -298,14 +304,53 @@ class DQNLearner:
         rp = self.replay
         ids_s, _, jdx, _ = self._src
         heads_job = self.net.heads_finalize_job(self.lh_part, self.lh_blocks)
-        after = self._fork_point()
-        n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job],
-                                    sumsq=self.fin_partials if self.allreduce is None else None,
-                                    after_first=after)
+        sumsq = self.fin_partials if self.allreduce is None else None
+        rides = self._tree_rides()
+        self.tree_rides_used = rides is not None
+        if rides is not None:  # the tree write rides the backward launches: no fork / join
+            n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job], sumsq=sumsq,
+                                        rides=rides)
+        else:
+            after = self._fork_point()
+            n = self.net.trunk_backward(rp.frames, self.ws_s, ids_s, jdx, extra_jobs=[heads_job], sumsq=sumsq,
+                                        after_first=after)
         if self.allreduce is None:
             assert n <= self.fin_partials.numel()
             self.n_fin_partials = n
-        self._tree_fork_end()
+        if rides is None:
+            self._tree_fork_end()
+
+    def _tree_rides(self):
+        """Riders of this step's tree write for the FC1, conv3 and conv2 backward launches and the
+        gradient finalize (leaves, level 1, level 2 or the top walk, the top walk or None) -- the staged actor
+        rows' priorities then the learner's mixed, deduplicated priorities, the same leaves,
+        nodes, max priority and counters as :meth:`tree_phase` -- or None when the write keeps
+        the forked tree stream (no fp32 HIP trunk, hooks / an ingest tail queued, several staged
+        actor writes, or a tree too tall for two wide levels)."""
+        rp = self.replay
+        if not (self.cfg.tree_ride and self.fp32 and hasattr(self.net, "fc1_ride_ok") and not self.tree_hooks
+                and not self.tree_tail and len(self.pre_writes) <= 1):
+            return None
+        stages = self.hip.tree_ride_level_stages(rp.tree)
+        pre = self.pre_writes[0] if self.pre_writes else None
+        E = 0 if pre is None else pre[0].numel()
+        if stages < 0 or E + self.B > rp.wlist.numel():
+            return None
+        self.pre_writes = []
+        ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        common = (ptr(pre[0]) if pre else 0, ptr(pre[1]) if pre else 0, E, ptr(pre[2]) if pre else 0,
+                  self.idx.data_ptr(), self.B, self.delta.data_ptr(), self.lw.data_ptr(), self.prio.data_ptr(),
+                  self.loss.data_ptr(), self.step_counter.data_ptr(), rp.owner.data_ptr(), rp.wlist.data_ptr(),
+                  rp.max_prio.data_ptr(), rp.alpha)
+        L = rp.tree.levels
+        mk = self.hip.make_tree_ride
+        leaves, lv1 = mk(rp.tree, 1, 0, 0, *common), mk(rp.tree, 2, 1, 0, *common)
+        if stages == 1:  # the top walk (levels 2..) with the conv2 pair
+            return leaves, lv1, (mk(rp.tree, 3, 0, 2, *common) if L >= 2 else None), None
+        # level 2 with the conv2 pair, the top walk (levels 3..) with the gradient finalize (as
+        # block 0 of the conv1 weight gradient's 256 one-per-CU workgroups it pushed the last
+        # of them into a second round: +1.8 us)
+        return leaves, lv1, mk(rp.tree, 2, 2, 0, *common), mk(rp.tree, 3, 0, 3, *common)
 
     def backward_phase(self, after_first=None) -> None:
         """Data-parallel split, part 2: priority-tree writes on the forked tree stream beside

@@ -198,30 +198,33 @@ class F32DuelingNet:
                                            m.value[2].bias.grad.data_ptr(), m.advantage[0].bias.grad.data_ptr(),
                                            m.value[0].bias.grad.data_ptr())
 
-    def _fc1_bwd(self, ws: F32Workspace) -> list:
-        """FC1 dgrad + weight gradient (one launch); returns the finalize jobs that complete
-        the weight gradient (sum the slices + transpose to the reference layout, with their
-        sum-of-squares partials)."""
+    fc1_ride_ok = True  # the backward launches take priority-tree riders (ops/csrc/tree_dev.h)
+
+    def _fc1_bwd(self, ws: F32Workspace, ride=None) -> list:
+        """FC1 dgrad + weight gradient (one launch, + the tree-write rider ``ride``); returns
+        the finalize jobs that complete the weight gradient (sum the slices + transpose to the
+        reference layout, with their sum-of-squares partials)."""
         m = self.model
         ga, gv = m.advantage[0].weight.grad, m.value[0].weight.grad
         self.hip.f32_fc1_bwd_split(ws.dz.data_ptr(), ws.a3.data_ptr(), self.wfc1p.data_ptr(), ws.dy3.data_ptr(),
-                                   self._fc1_ws.data_ptr(), ws.B, self._s())
+                                   self._fc1_ws.data_ptr(), ws.B, self._s(), ride=ride)
         return [self.hip.f32_fc1_finalize_job(0, self._fc1_G, self._fc1_ws.data_ptr(), ga.data_ptr()),
                 self.hip.f32_fc1_finalize_job(1, self._fc1_G, self._fc1_ws.data_ptr(), gv.data_ptr())]
 
-    def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None) -> list:
-        """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch); returns the
-        finalize jobs of the three layers."""
+    def _conv_chain(self, x, ws: F32Workspace, ids, idx, after_first=None, rides=(None, None)) -> list:
+        """conv3 .. conv1 backward (wgrad partials + masked dgrad per launch; ``rides``: the
+        tree-write riders of the conv3 / conv2 launches); returns the finalize jobs of the
+        three layers."""
         B = ws.B
         h, s, f = self.hip, self._s(), self.model.features
         xp, ip, jp = self._src(x, ids, idx, B)
         w1, w2, w3 = self._wgrad_wss
         h.f32_conv_bwd(3, ws.a2.data_ptr(), 0, 0, ws.dy3.data_ptr(), self.w3t.data_ptr(), ws.a2.data_ptr(),
-                       ws.dy2.data_ptr(), w3.data_ptr(), B, s)
+                       ws.dy2.data_ptr(), w3.data_ptr(), B, s, ride=rides[0])
         if after_first is not None:
             after_first()
         h.f32_conv_bwd(2, ws.a1.data_ptr(), 0, 0, ws.dy2.data_ptr(), self.w2t.data_ptr(), ws.a1.data_ptr(),
-                       ws.dy1.data_ptr(), w2.data_ptr(), B, s)
+                       ws.dy1.data_ptr(), w2.data_ptr(), B, s, ride=rides[1])
         h.f32_conv_bwd(1, xp, ip, jp, ws.dy1.data_ptr(), 0, 0, 0, w1.data_ptr(), B, s)
         return [h.f32_conv_finalize_job(k, B, wsp.data_ptr(), f[2 * k - 2].weight.grad.data_ptr(),
                                         f[2 * k - 2].bias.grad.data_ptr()) for k, wsp in ((3, w3), (2, w2), (1, w1))]
@@ -240,18 +243,19 @@ class F32DuelingNet:
 
     def trunk_backward(self, x: torch.Tensor, ws: F32Workspace, ids: torch.Tensor | None = None,
                        idx: torch.Tensor | None = None, extra_jobs=(), sumsq: torch.Tensor | None = None,
-                       after_first=None) -> int:
+                       after_first=None, rides=(None, None, None, None)) -> int:
         """FC1 + conv backward from ``ws.dz`` (fp32 dL/dz).  The conv weight-gradient
         partials (+ ``extra_jobs``) are reduced by ONE grad_finalize, which also writes the
         per-workgroup sum-of-squares partials of EVERY gradient into ``sumsq`` (fp64) when
-        given; returns the partial count.  ``after_first()`` runs right after the first launch."""
+        given; returns the partial count.  ``after_first()`` runs right after the first launch;
+        ``rides`` = the priority-tree riders of the FC1, conv3 and conv2 launches and the finalize."""
         self.enable_backward(ws.B)
-        fc1_jobs = self._fc1_bwd(ws)
+        fc1_jobs = self._fc1_bwd(ws, ride=rides[0])
         if after_first is not None:
             after_first()
         h = self.hip
-        jobs = self._conv_chain(x, ws, ids, idx) + list(extra_jobs) + fc1_jobs
-        return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr())
+        jobs = self._conv_chain(x, ws, ids, idx, rides=rides[1:3]) + list(extra_jobs) + fc1_jobs
+        return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr(), ride=rides[3])
 
 
 def forward_multi_f32(passes, act: tuple | None = None) -> None:

@@ -18,6 +18,7 @@
 //   scatters into the reference [N][C][KH][KW] gradient layout.
 #include "common.h"
 #include "kernels.h"
+#include "tree_dev.h"
 
 namespace apex {
 
@@ -623,30 +624,34 @@ __host__ __device__ inline int finalize_blocks(const FinalizeJob& j) {
   return (j.n_main + j.n_bias + per - 1) / per;
 }
 
-__device__ __forceinline__ void finalize_sumsq_q(double q, const FinalizeSet& fs) {
+__device__ __forceinline__ void finalize_sumsq_q(double q, const FinalizeSet& fs, int gb) {
   // block-wide fixed-order sum of the threads' q (all 256 threads call this)
   __shared__ double red[4];
   q = wave_sum(q);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) red[wave] = q;
   __syncthreads();
-  if (threadIdx.x == 0) fs.sumsq[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (threadIdx.x == 0) fs.sumsq[gb] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-__device__ __forceinline__ void finalize_sumsq(float v, const FinalizeSet& fs, bool active) {
-  finalize_sumsq_q(active ? (double)v * (double)v : 0.0, fs);
+__device__ __forceinline__ void finalize_sumsq(float v, const FinalizeSet& fs, bool active, int gb) {
+  finalize_sumsq_q(active ? (double)v * (double)v : 0.0, fs, gb);
 }
 
-__global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
+// r (stage 3): the top walk of the learner's priority-tree write riding the launch as block 0
+// (tree_dev.h tree_ride; the finalize blocks and their sum-of-squares partials keep their index)
+__global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs, TreeRide r) {
   __shared__ float red[4][64];
   __shared__ float row[kRowLen];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int gb = blockIdx.x;
+  if (r.stage && tree_ride(r, r.nhost, &red[0][0], &gb)) return;  // (block-uniform role)
   int j = 0;
-  while (j + 1 < fs.n && (int)blockIdx.x >= fs.job[j + 1].block0) ++j;
+  while (j + 1 < fs.n && gb >= fs.job[j + 1].block0) ++j;
   const FinalizeJob& jb = fs.job[j];
   if (jb.kind == 3) {  // norm only: the gradient was written in place by its producer
     if (!fs.sumsq) return;
-    const int e0 = ((int)blockIdx.x - jb.block0) * kNormOnlyPer + threadIdx.x;
+    const int e0 = (gb - jb.block0) * kNormOnlyPer + threadIdx.x;
     float v[8];
     // unconditional loads from clamped indices, zeroed after: guarded, each load compiled to a
     // branch + wait (8 serial round trips per workgroup)
@@ -657,11 +662,11 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
     double q = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) q += (double)v[k] * (double)v[k];
-    finalize_sumsq_q(q, fs);
+    finalize_sumsq_q(q, fs, gb);
     return;
   }
   if (jb.kind == 2) {  // FC1 weight rows: natural [n][p*64 + c] -> reference [n][c*49 + p]
-    const int n = (int)blockIdx.x - jb.block0;
+    const int n = gb - jb.block0;
     const float* src = jb.part + (size_t)n * kRowLen;
     // the thread's 13 elements of each slice loaded together (clamped index, zeroed after):
     // a loop load -> store per element paid a round trip each
@@ -691,7 +696,7 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
       double d = wave_sum((double)q);
       if (lane == 0) rq[wave] = d;
       __syncthreads();
-      if (threadIdx.x == 0) fs.sumsq[blockIdx.x] = (rq[0] + rq[1]) + (rq[2] + rq[3]);
+      if (threadIdx.x == 0) fs.sumsq[gb] = (rq[0] + rq[1]) + (rq[2] + rq[3]);
     }
     return;
   }
@@ -700,7 +705,7 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   float t = 0.f;
   bool have = false;
   if (jb.G >= kWideG) {
-    e = ((int)blockIdx.x - jb.block0) * 64 + lane;
+    e = (gb - jb.block0) * 64 + lane;
     float s = 0.f;
     // (16 slices per unrolled batch: the loads of a batch are in flight together, the adds
     // stay in slice order)
@@ -716,7 +721,7 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
     have = wave == 0 && e < total;
     if (have) t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   } else {
-    e = ((int)blockIdx.x - jb.block0) * 256 + threadIdx.x;
+    e = (gb - jb.block0) * 256 + threadIdx.x;
     have = e < total;
     if (have) {
       const float* src = e < jb.n_main ? jb.part + e : jb.bpart + (e - jb.n_main);
@@ -733,7 +738,7 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
       t = (s0 + s1) + (s2 + s3);
     }
   }
-  if (fs.sumsq) finalize_sumsq(t, fs, have);
+  if (fs.sumsq) finalize_sumsq(t, fs, have, gb);
   if (!have) return;
   if (jb.kind == 0) {  // conv: [N][KH*KW*C] (c fastest) -> reference [N][C][KH][KW]
     if (e < jb.n_main) {
@@ -755,14 +760,20 @@ __global__ __launch_bounds__(256) void grad_finalize_k(FinalizeSet fs) {
   }
 }
 
-int grad_finalize(FinalizeSet fs, hipStream_t s) {
+int grad_finalize(FinalizeSet fs, hipStream_t s, const TreeRide* ride) {
   if (fs.n < 1 || fs.n > kMaxFinalizeJobs) throw std::invalid_argument("grad_finalize: 1..6 jobs");
   int blocks = 0;
   for (int j = 0; j < fs.n; ++j) {
     fs.job[j].block0 = blocks;
     blocks += finalize_blocks(fs.job[j]);
   }
-  grad_finalize_k<<<blocks, 256, 0, s>>>(fs);
+  TreeRide r{};
+  if (ride && ride->stage) {
+    if (ride->stage != 3) throw std::invalid_argument("grad_finalize: takes the top-walk rider only");
+    r = *ride;
+    r.nhost = blocks;
+  }
+  grad_finalize_k<<<blocks + tree_ride_blocks(r), 256, 0, s>>>(fs, r);
   LAUNCH_CHECK();
   return blocks;
 }

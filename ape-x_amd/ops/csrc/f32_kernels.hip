@@ -61,6 +61,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "tree_dev.h"
 
 namespace apex {
 namespace {
@@ -614,18 +615,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SS == 3 ? 3
 
 // Two independent GEMMs in one launch: blocks [0, n1) run P1, the rest P2 (P1 first: the
 // longer per-block problem starts early).
+// r (stage > 0): the learner's priority-tree write riding the launch as extra workgroups
+// (tree_dev.h tree_ride: the leaves in block 0, a level's recompute past the GEMM tiles).
 template <class P1, class P2, int SS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SS == 3 ? 3 : 1))) void gemm2_k(
-    typename P1::Args a1, typename P2::Args a2, int n1) {
+    typename P1::Args a1, typename P2::Args a2, int n1, TreeRide r) {
   __shared__ __attribute__((aligned(16))) float lds[MaxI<LdsFloats<P1, SS>::value, LdsFloats<P2, SS>::value>::value];
   __shared__ union {
     typename P1::Smem s1;
     typename P2::Smem s2;
   } sm;
-  if ((int)blockIdx.x < n1)
-    gemm_body<P1, BodyForm<SS>::value>(a1, blockIdx.x, lds, sm.s1);
+  int b = blockIdx.x;
+  if (r.stage && tree_ride(r, r.nhost, lds, &b)) return;  // (grid-uniform stage, block-uniform role)
+  if (b < n1)
+    gemm_body<P1, BodyForm<SS>::value>(a1, b, lds, sm.s1);
   else
-    gemm_body<P2, BodyForm<SS>::value>(a2, (int)blockIdx.x - n1, lds, sm.s2);
+    gemm_body<P2, BodyForm<SS>::value>(a2, b - n1, lds, sm.s2);
 }
 
 __device__ __forceinline__ F32Prob pick(const F32Set& s, int i) {
@@ -1569,13 +1574,20 @@ void launch1(const typename P::Args& a, int blocks, hipStream_t s, bool small = 
 }
 
 template <class P1, class P2>
-void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s) {
+void launch2(const typename P1::Args& a1, int n1, const typename P2::Args& a2, int n2, hipStream_t s,
+             const TreeRide* ride = nullptr) {
   if (n1 + n2 <= 0) return;
+  TreeRide r{};
+  if (ride && ride->stage) {
+    r = *ride;
+    r.nhost = n1 + n2;
+  }
+  const int nb = n1 + n2 + tree_ride_blocks(r);
   switch ((stage_split_mask() >> 2) & 3) {
-    case 1: gemm2_k<P1, P2, 1><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
-    case 2: gemm2_k<P1, P2, 2><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
-    case 3: gemm2_k<P1, P2, 3><<<n1 + n2, 256, 0, s>>>(a1, a2, n1); break;
-    default: gemm2_k<P1, P2, 0><<<n1 + n2, 256, 0, s>>>(a1, a2, n1);
+    case 1: gemm2_k<P1, P2, 1><<<nb, 256, 0, s>>>(a1, a2, n1, r); break;
+    case 2: gemm2_k<P1, P2, 2><<<nb, 256, 0, s>>>(a1, a2, n1, r); break;
+    case 3: gemm2_k<P1, P2, 3><<<nb, 256, 0, s>>>(a1, a2, n1, r); break;
+    default: gemm2_k<P1, P2, 0><<<nb, 256, 0, s>>>(a1, a2, n1, r);
   }
   LAUNCH_CHECK();
 }
@@ -1669,7 +1681,7 @@ static void check_bwd_batch(int B) {
 }
 
 void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
-                       hipStream_t s) {
+                       hipStream_t s, const TreeRide* ride) {
   if (B <= 0) return;
   check_bwd_batch(B);
   BwdArgs d{};
@@ -1687,7 +1699,7 @@ void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, flo
   w.splits = std::min(kFc1WgSlices, nkb);
   w.kbps = (nkb + w.splits - 1) / w.splits;
   w.splits = (nkb + w.kbps - 1) / w.kbps;  // every slice non-empty
-  launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B) * w.splits, d, Fc1Dgrad::tiles(B), s);
+  launch2<Fc1Wgrad, Fc1Dgrad>(w, Fc1Wgrad::tiles(B) * w.splits, d, Fc1Dgrad::tiles(B), s, ride);
 }
 
 int f32_fc1_wgrad_slices(int B) {
@@ -1709,9 +1721,11 @@ size_t f32_wgrad_workspace_floats(int layer, int B, int target) {
 
 // wgrad + dgrad of conv layer 3 or 2 in one launch; layer 1: wgrad only (x = frames)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target, int tile) {
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target, int tile,
+                  const TreeRide* ride) {
   if (B <= 0) return;
   check_bwd_batch(B);
+  if (ride && ride->stage && layer == 1) throw std::invalid_argument("f32_conv_bwd: no tree rider on layer 1");
   const SplitPlan p = wgrad_plan(layer, B, target);
   const size_t per = layer == 1 ? 32 * 256 : (layer == 2 ? 64 * 512 : 64 * 576);
   BwdArgs g{};
@@ -1732,12 +1746,12 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.B = B;
   switch (layer) {
     case 3:  // tile 1: input gradient at BK 32 (the alternative to the default)
-      if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP32>(g, (576 / 64) * p.splits, d, Conv3DgradP32::tiles(B), s);
-      else launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s);
+      if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP32>(g, (576 / 64) * p.splits, d, Conv3DgradP32::tiles(B), s, ride);
+      else launch2<ConvWgrad<3>, Conv3DgradP>(g, (576 / 64) * p.splits, d, Conv3DgradP::tiles(B), s, ride);
       break;
     case 2:
-      if (tile == 1) launch2<ConvWgrad<2>, Conv2DgradP32>(g, (512 / 64) * p.splits, d, Conv2DgradP32::tiles(B), s);
-      else launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s);
+      if (tile == 1) launch2<ConvWgrad<2>, Conv2DgradP32>(g, (512 / 64) * p.splits, d, Conv2DgradP32::tiles(B), s, ride);
+      else launch2<ConvWgrad<2>, Conv2DgradP>(g, (512 / 64) * p.splits, d, Conv2DgradP::tiles(B), s, ride);
       break;
     case 1:
       if (p.kbps == 1) f32_conv1_wgrad_x3_k<1><<<p.splits, 256, 0, s>>>(g);

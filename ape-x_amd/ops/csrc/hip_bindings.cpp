@@ -49,6 +49,28 @@ TreeHandle make_tree(uint64_t leaf_sum, uint64_t leaf_min, const std::vector<uin
   return h;
 }
 
+BatchWrite batch_write(uint64_t pre_idx, uint64_t pre_prio, int E, uint64_t pre_bump, uint64_t idx, uint64_t prio,
+                       int B, uint64_t mix_delta, uint64_t mix_lw, uint64_t mix_prio_out, uint64_t mix_loss_out,
+                       uint64_t bump, uint64_t owner, uint64_t list, uint64_t max_prio, float alpha) {
+  BatchWrite w{};
+  w.pre_idx = P<const int>(pre_idx);
+  w.pre_prio = P<const float>(pre_prio);
+  w.E = E;
+  w.pre_bump = P<int64_t>(pre_bump);
+  w.idx = P<const int>(idx);
+  w.prio = P<const float>(prio);
+  w.B = B;
+  w.mix = PrioMix{P<const float>(mix_delta), P<const float>(mix_lw), P<float>(mix_prio_out), P<float>(mix_loss_out)};
+  w.bump = P<int64_t>(bump);
+  w.owner = P<int>(owner);
+  w.list = P<int>(list);
+  w.max_prio = P<float>(max_prio);
+  w.alpha = alpha;
+  return w;
+}
+
+const TreeRide* ride_of(const py::object& o) { return o.is_none() ? nullptr : o.cast<const TreeRide*>(); }
+
 struct NStepHandle {
   NStepParams p{};
   NStepState st{};
@@ -74,22 +96,42 @@ PYBIND11_MODULE(_apex_hip, m) {
                               uint64_t idx, uint64_t prio, int B, uint64_t mix_delta, uint64_t mix_lw,
                               uint64_t mix_prio_out, uint64_t mix_loss_out, uint64_t bump, uint64_t owner,
                               uint64_t list, uint64_t max_prio, float alpha, uint64_t ticket, uint64_t s) {
-    BatchWrite w{};
-    w.pre_idx = P<const int>(pre_idx);
-    w.pre_prio = P<const float>(pre_prio);
-    w.E = E;
-    w.pre_bump = P<int64_t>(pre_bump);
-    w.idx = P<const int>(idx);
-    w.prio = P<const float>(prio);
-    w.B = B;
-    w.mix = PrioMix{P<const float>(mix_delta), P<const float>(mix_lw), P<float>(mix_prio_out), P<float>(mix_loss_out)};
-    w.bump = P<int64_t>(bump);
-    w.owner = P<int>(owner);
-    w.list = P<int>(list);
-    w.max_prio = P<float>(max_prio);
-    w.alpha = alpha;
+    const BatchWrite w = batch_write(pre_idx, pre_prio, E, pre_bump, idx, prio, B, mix_delta, mix_lw, mix_prio_out,
+                                     mix_loss_out, bump, owner, list, max_prio, alpha);
     per_write_batch(t.d, w, P<int>(ticket), S(s));
   });
+  // the batched write as riders of the learner's backward launches (f32_fc1_bwd_split /
+  // f32_conv_bwd ride=): stage 1 leaves, stage 2 level `level`, stage 3 levels top_from.. in
+  // one workgroup
+  py::class_<TreeRide>(m, "TreeRide")
+      .def_readonly("stage", &TreeRide::stage)
+      .def_readonly("level", &TreeRide::level)
+      .def_readonly("top_from", &TreeRide::top_from)
+      .def_property_readonly("blocks", [](const TreeRide& r) { return tree_ride_blocks(r); });
+  m.def("make_tree_ride", [](const TreeHandle& t, int stage, int level, int top_from, uint64_t pre_idx,
+                             uint64_t pre_prio, int E, uint64_t pre_bump, uint64_t idx, int B, uint64_t mix_delta,
+                             uint64_t mix_lw, uint64_t mix_prio_out, uint64_t mix_loss_out, uint64_t bump,
+                             uint64_t owner, uint64_t list, uint64_t max_prio, float alpha) {
+    TreeRide r{};
+    r.t = t.d;
+    r.w = batch_write(pre_idx, pre_prio, E, pre_bump, idx, 0, B, mix_delta, mix_lw, mix_prio_out, mix_loss_out, bump,
+                      owner, list, max_prio, alpha);
+    r.stage = stage;
+    r.level = level;
+    r.top_from = top_from;
+    if (stage < 1 || stage > 3)
+      throw std::invalid_argument("make_tree_ride: stage 1 (leaves), 2 (a level) or 3 (the top levels)");
+    if (stage == 3 && (top_from < 1 || top_from > t.d.levels || t.d.size[top_from] > 64))
+      throw std::invalid_argument("make_tree_ride: the top walk starts at a level in 1..levels of <= 64 nodes");
+    if (E < 0 || B < 0 || E + B > 2048 || (E > 0 && (!pre_idx || !pre_prio)) || (B > 0 && !idx))
+      throw std::invalid_argument("make_tree_ride: 0 <= E + B <= 2048 with their slots / priorities");
+    if (!owner || !list || !max_prio || (mix_delta && !mix_lw) || (B > 0 && !mix_delta))
+      throw std::invalid_argument("make_tree_ride: owner, list, max_prio and the learner mix (delta + lw)");
+    if (stage == 2 && (level < 1 || level > t.d.levels))
+      throw std::invalid_argument("make_tree_ride: level in 1..levels");
+    return r;
+  });
+  m.def("tree_ride_level_stages", [](const TreeHandle& t) { return tree_ride_level_stages(t.d); });
   m.def("pack_shard_slots", [](const TreeHandle& t, uint64_t slots, int world, int rank, uint64_t s) {
     pack_shard_slots(t.d, P<float>(slots), world, rank, S(s));
   });
@@ -390,14 +432,14 @@ PYBIND11_MODULE(_apex_hip, m) {
     fc1_bwd(P<const uint16_t>(dz), P<const uint16_t>(a3), P<const uint16_t>(wt), P<uint16_t>(dy3), P<float>(part), B,
             S(s));
   });
-  m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s, uint64_t sumsq) {
+  m.def("grad_finalize", [](const std::vector<FinalizeJob>& jobs, uint64_t s, uint64_t sumsq, py::object ride) {
     if (jobs.empty() || jobs.size() > (size_t)kMaxFinalizeJobs) throw std::invalid_argument("1..6 jobs");
     FinalizeSet fs{};
     for (size_t i = 0; i < jobs.size(); ++i) fs.job[i] = jobs[i];
     fs.n = (int)jobs.size();
     fs.sumsq = P<double>(sumsq);
-    return grad_finalize(fs, S(s));
-  }, py::arg("jobs"), py::arg("s"), py::arg("sumsq") = 0);
+    return grad_finalize(fs, S(s), ride_of(ride));
+  }, py::arg("jobs"), py::arg("s"), py::arg("sumsq") = 0, py::arg("ride") = py::none());
   m.def("wgrad_grid", &wgrad_grid);
   m.def("dqn_heads_bwd_blocks", &dqn_heads_bwd_blocks);
   m.def("dqn_heads_bwd", [](py::dict d, int B, int A, float gamma_n, uint64_t s) {
@@ -464,10 +506,11 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("f32_set_stage_split", &f32_set_stage_split);
   m.def("f32_stage_split", &f32_stage_split);
   m.def("f32_fc1_bwd_split", [](uint64_t dz, uint64_t a3, uint64_t wfc1p, uint64_t dy3, uint64_t ws, int B,
-                                uint64_t s) {
+                                uint64_t s, py::object ride) {
     f32_fc1_bwd_split(P<const float>(dz), P<const float>(a3), P<const float>(wfc1p), P<float>(dy3), P<float>(ws), B,
-                      S(s));
-  });
+                      S(s), ride_of(ride));
+  }, py::arg("dz"), py::arg("a3"), py::arg("wfc1p"), py::arg("dy3"), py::arg("ws"), py::arg("B"), py::arg("s"),
+     py::arg("ride") = py::none());
   m.def("f32_fc1_wgrad_splits", &f32_fc1_wgrad_splits);
   m.def("f32_fc1_wgrad_slices", &f32_fc1_wgrad_slices);
   m.def("f32_fc1_wgrad_workspace_floats", &f32_fc1_wgrad_workspace_floats);
@@ -478,11 +521,12 @@ PYBIND11_MODULE(_apex_hip, m) {
   m.def("f32_wgrad_workspace_floats", &f32_wgrad_workspace_floats, py::arg("layer"), py::arg("B"),
         py::arg("target") = 0);
   m.def("f32_conv_bwd", [](int layer, uint64_t x, uint64_t ids, uint64_t idx, uint64_t dy, uint64_t w, uint64_t mask,
-                           uint64_t dx, uint64_t ws, int B, uint64_t s, int target, int tile) {
+                           uint64_t dx, uint64_t ws, int B, uint64_t s, int target, int tile, py::object ride) {
     f32_conv_bwd(layer, P<const void>(x), P<const int>(ids), P<const int>(idx), P<const float>(dy), P<const float>(w),
-                 P<const float>(mask), P<float>(dx), P<float>(ws), B, S(s), target, tile);
+                 P<const float>(mask), P<float>(dx), P<float>(ws), B, S(s), target, tile, ride_of(ride));
   }, py::arg("layer"), py::arg("x"), py::arg("ids"), py::arg("idx"), py::arg("dy"), py::arg("w"), py::arg("mask"),
-     py::arg("dx"), py::arg("ws"), py::arg("B"), py::arg("s"), py::arg("target") = 0, py::arg("tile") = 0);
+     py::arg("dx"), py::arg("ws"), py::arg("B"), py::arg("s"), py::arg("target") = 0, py::arg("tile") = 0,
+     py::arg("ride") = py::none());
   m.def("f32_conv_finalize_job", [](int layer, int B, uint64_t ws, uint64_t grad, uint64_t bgrad, int target) {
     return f32_conv_finalize_job(layer, B, P<const float>(ws), P<float>(grad), P<float>(bgrad), target);
   }, py::arg("layer"), py::arg("B"), py::arg("ws"), py::arg("grad"), py::arg("bgrad"), py::arg("target") = 0);

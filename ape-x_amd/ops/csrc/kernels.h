@@ -55,6 +55,23 @@ struct BatchWrite {
   float alpha;
 };
 void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStream_t s);
+// The same batched write riding the learner's backward launches as extra workgroups (no
+// tree stream, no fork / join in the learner graph): stage 1 = the leaves (one workgroup,
+// block 0 of the FC1 backward pair), stage 2 = level `level` of the listed slots (one wave
+// per slot, workgroups after the GEMM tiles), stage 3 = every node of levels top_from.. in one
+// workgroup (block 0).  Each stage reads what an earlier launch wrote: no fences, no tickets.
+// stage 0: no rider.
+struct TreeRide {
+  TreeDesc t;
+  BatchWrite w;
+  int stage, level, top_from;
+  int nhost;  // the host launch's own workgroups (set by the launcher)
+};
+// workgroups a rider adds to its host launch
+int tree_ride_blocks(const TreeRide& r);
+// wide level stages of a ridden write on this tree: 1 (level 1; every level above it in the top
+// walk), 2 (levels 1 and 2; the rest in the top walk), or -1 (a level above 2 has > 64 nodes)
+int tree_ride_level_stages(const TreeDesc& t);
 // Zero `slots` [world][2] and write this shard's (root mass, root min priority) into
 // slot `rank`: after a SUM all-reduce every rank holds all shards' pairs (an all-gather
 // folded into the learner's conv-gradient all-reduce).
@@ -171,7 +188,8 @@ struct FinalizeSet {
   double* sumsq;            // optional: one fp64 partial of sum(g^2) per workgroup (grad norm)
 };
 int wgrad_grid(int layer, int B);
-int grad_finalize(FinalizeSet fs, hipStream_t s);  // returns the workgroup (= sumsq partial) count
+// returns the finalize workgroup (= sumsq partial) count; ride: a stage-3 tree rider (block 0)
+int grad_finalize(FinalizeSet fs, hipStream_t s, const TreeRide* ride = nullptr);
 int grad_finalize_blocks(const FinalizeSet& fs);
 FinalizeJob conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad);
 // FC1 weight half (0: advantage rows 0..127, 1: value rows 128..255) of fc1_bwd's slabs
@@ -395,11 +413,12 @@ int f32_fc1_wgrad_splits();
 int f32_fc1_wgrad_slices(int B);
 size_t f32_fc1_wgrad_workspace_floats();
 void f32_fc1_bwd_split(const float* dz, const float* a3, const float* wfc1p, float* dy3, float* ws, int B,
-                       hipStream_t s);
+                       hipStream_t s, const TreeRide* ride = nullptr);
 // conv backward: layers 3/2 = wgrad partials + dgrad (w = w3t / w2t, masked by `mask`) in
 // one launch, layer 1 = wgrad partials from the u8 frames (x/ids/idx as FrameSrc)
 void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, const float* dy, const float* w,
-                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target = 0, int tile = 0);
+                  const float* mask, float* dx, float* ws, int B, hipStream_t s, int target = 0, int tile = 0,
+                  const TreeRide* ride = nullptr);  // ride: layers 3 / 2 only
 FinalizeJob f32_conv_finalize_job(int layer, int B, const float* ws, float* grad, float* bias_grad, int target = 0);
 // grad_finalize job that only adds sum(g^2) of g[0..n) to the norm partials
 FinalizeJob norm_only_job(const float* g, int n);

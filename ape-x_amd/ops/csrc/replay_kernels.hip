@@ -384,6 +384,19 @@ void per_write_batch(const TreeDesc& t, const BatchWrite& w, int* ticket, hipStr
   }
 }
 
+int tree_ride_blocks(const TreeRide& r) {
+  if (r.stage == 1 || r.stage == 3) return 1;
+  if (r.stage == 2) return (r.w.E + r.w.B + 3) / 4;  // one wave per listed slot, 4 waves per workgroup
+  return 0;
+}
+
+int tree_ride_level_stages(const TreeDesc& t) {
+  int last_big = 0;
+  for (int lv = 1; lv <= t.levels; ++lv)
+    if (t.size[lv] > 64) last_big = lv;
+  return last_big <= 1 ? 1 : (last_big == 2 ? 2 : -1);
+}
+
 // ------------------------------------------------------------------ launchers
 void per_write_leaves(const TreeDesc& t, const int* idx, const float* prio, int B, float alpha, float* max_prio,
                       int dedup, int* sorted_scratch, int64_t* bump0, int64_t d0, int64_t* bump1, int64_t d1,

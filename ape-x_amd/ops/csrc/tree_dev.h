@@ -389,4 +389,157 @@ __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const Batc
   }
 }
 
+// Block reduction of rows v[0, n) in the order of block_reduce_1024 over a 1024-thread block
+// holding one row per thread (wave j sums rows [64 j, 64 j + 64); the wave totals are added in
+// order j = 0, 1, ..): any block size gives the same bits as the one-row-per-thread kernels
+// (per_write_leaves_sorted_k), so a rider workgroup of 256 threads reproduces their loss mean.
+// red: >= (n + 63) / 64 floats.
+__device__ __forceinline__ float block_reduce_rows(const float* __restrict__ v, int n, float* red, bool is_max) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6, nj = (n + 63) >> 6;
+  __syncthreads();
+  for (int j = wave; j < nj; j += nw) {  // wave-uniform
+    const int r = 64 * j + lane;
+    float x = r < n ? v[r] : (is_max ? -INFINITY : 0.f);
+    x = is_max ? wave_max(x) : wave_sum(x);
+    if (lane == 0) red[j] = x;
+  }
+  __syncthreads();
+  float t = is_max ? -INFINITY : 0.f;
+  for (int j = 0; j < nj; ++j) t = is_max ? fmaxf(t, red[j]) : t + red[j];  // fixed order
+  return t;
+}
+
+// Ride stage 1: batch_leaves_block for any block size (rows strided over the threads), with
+// the loss mean / max TD error reduced as the 1024-thread kernels do.  The learner rows' mixed
+// priorities are recomputed where used (prio_mix is a pure function of dmax and delta_i).
+__device__ __forceinline__ void ride_leaves(const TreeDesc& t, const BatchWrite& w, float* red) {
+  const int k = threadIdx.x, nt = blockDim.x;
+  float pmax = 0.f;
+  for (int i = k; i < w.E; i += nt) {  // actor rows first (they precede the learner's in time)
+    const int id = w.pre_idx[i];
+    w.list[i] = id;
+    if (id >= 0 && id < t.size[0]) pmax = fmaxf(pmax, write_leaf(t, id, w.pre_prio[i], w.alpha));
+  }
+  float dmax = 0.f;
+  if (w.mix.delta && w.B > 0) {
+    const float total = block_reduce_rows(w.mix.lw, w.B, red, false);
+    dmax = block_reduce_rows(w.mix.delta, w.B, red, true);
+    if (k == 0 && w.mix.loss_out) w.mix.loss_out[0] = total / (float)w.B;
+  }
+  __syncthreads();  // actor leaves land before any learner leaf (last write wins)
+  for (int i = k; i < w.B; i += nt) {
+    const int id = w.idx[i];
+    w.list[w.E + i] = id;
+    if (id >= 0 && id < t.size[0]) atomicMax(w.owner + id, i);  // device atomics: performed at L2
+  }
+  __syncthreads();
+  for (int i = k; i < w.B; i += nt) {
+    const int id = w.idx[i];
+    const float p = w.mix.delta ? prio_mix(dmax, w.mix.delta[i]) : (w.prio ? w.prio[i] : *w.max_prio);
+    if (w.mix.delta && w.mix.prio_out) w.mix.prio_out[i] = p;
+    if (id >= 0 && id < t.size[0] &&
+        __hip_atomic_load(w.owner + id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == i) {
+      const float wp = write_leaf(t, id, p, w.alpha);
+      if (w.mix.delta != nullptr || w.prio != nullptr) pmax = fmaxf(pmax, wp);
+      w.owner[id] = -1;  // release the claim (only the winner writes; losers never touch it again)
+    }
+  }
+  pmax = block_reduce_1024(pmax, red, true);
+  if (k == 0) {
+    if (pmax > 0.f) atomic_max_pos_float(w.max_prio, pmax);
+    if (w.pre_bump) *w.pre_bump += w.E;
+    if (w.bump) *w.bump += 1;
+  }
+}
+
+// Ride stage 2: rider workgroup `rb` recomputes level `level` of listed slots (one wave per
+// slot; a slot whose predecessor in the list shares the ancestor skips it -- the actor's
+// ring-ordered runs).  No ticket / fence: the level above waits for the next launch.
+__device__ __forceinline__ void ride_level(const TreeDesc& t, const BatchWrite& w, int level, int rb) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int n = w.E + w.B, i = rb * nw + (threadIdx.x >> 6), sh = kTreeLog2Fanout * level;
+  if (i >= n) return;
+  const int id = w.list[i];
+  const int prev = i > 0 ? w.list[i - 1] : -1;
+  const bool dup = prev >= 0 && prev < t.size[0] && id >= 0 && (prev >> sh) == (id >> sh);
+  if (id >= 0 && id < t.size[0] && !dup) recompute_node(t, level, id >> sh, lane);
+}
+
+// Ride stage 3: every node of levels top_from.. in ONE workgroup (the levels below are final:
+// written by earlier launches; level top_from has <= 64 nodes).  One global round trip: each wave
+// loads the children of all its level-top_from nodes together, and the levels above reduce
+// their children out of LDS.  Same per-node arithmetic as recompute_node (tree_sum of the 64
+// children as doubles, tree_min): bit-identical node values.  No device-scope fence (on
+// gfx950 a __threadfence writes back the XCD's whole L2 -- inside a GEMM launch its dirty
+// output tiles: a ticketed top walk riding the conv2 pair took that launch from 55 to 84 us).
+__device__ __forceinline__ void ride_top(const TreeDesc& t, int lo) {
+  __shared__ double s_sum[2][64];
+  __shared__ float s_min[2][64];
+  constexpr int K = 16;  // nodes per wave at level lo (64 nodes over >= 4 waves)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int n = t.size[lo], csize = t.size[lo - 1];
+  double sv[K];
+  float mv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {  // every load in flight (clamped addresses, selected after)
+    const int node = wave + k * nw, c = min(min(node, n - 1) * kTreeFanout + lane, csize - 1);
+    if (lo == 1) {
+      sv[k] = (double)t.leaf_sum[c];
+      mv[k] = t.leaf_min[c];
+    } else {
+      sv[k] = t.node_sum[lo - 2][c];
+      mv[k] = t.node_min[lo - 2][c];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int node = wave + k * nw;
+    if (node >= n) break;  // wave-uniform
+    const bool ok = node * kTreeFanout + lane < csize;
+    const double s = tree_sum(ok ? sv[k] : 0.0);
+    const float m = tree_min(ok ? mv[k] : INFINITY);
+    if (lane == 0) {
+      t.node_sum[lo - 1][node] = s;
+      t.node_min[lo - 1][node] = m;
+      s_sum[lo & 1][node] = s;
+      s_min[lo & 1][node] = m;
+    }
+  }
+  for (int lv = lo + 1; lv <= t.levels; ++lv) {  // <= 64 children per level, from LDS
+    __syncthreads();
+    const int cs = t.size[lv - 1];
+    for (int node = wave; node < t.size[lv]; node += nw) {
+      const int c = node * kTreeFanout + lane;
+      const double s = tree_sum(c < cs ? s_sum[(lv - 1) & 1][c] : 0.0);
+      const float m = tree_min(c < cs ? s_min[(lv - 1) & 1][c] : INFINITY);
+      if (lane == 0) {
+        t.node_sum[lv - 1][node] = s;
+        t.node_min[lv - 1][node] = m;
+        s_sum[lv & 1][node] = s;
+        s_min[lv & 1][node] = m;
+      }
+    }
+  }
+}
+
+// The rider part of a host launch: true when this workgroup was a rider (it has returned from
+// its tree work); *gb = the host kernel's own block index otherwise.  Riders of stages 1 and 3
+// take block 0 (they start with the launch), level riders the blocks past the host's grid.
+__device__ __forceinline__ bool tree_ride(const TreeRide& r, int nhost, float* red, int* gb) {
+  const int b = blockIdx.x;
+  *gb = b;
+  if (r.stage == 1 || r.stage == 3) {
+    if (b == 0) {
+      if (r.stage == 1) ride_leaves(r.t, r.w, red);
+      else ride_top(r.t, r.top_from);
+      return true;
+    }
+    *gb = b - 1;
+  } else if (r.stage == 2 && b >= nhost) {
+    ride_level(r.t, r.w, r.level, b - nhost);
+    return true;
+  }
+  return false;
+}
+
 }  // namespace apex

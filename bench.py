@@ -79,6 +79,9 @@ def parse():
                          "after a stretch of load, so a short timed window right after setup is not a ramp "
                          "measurement (20-step windows, one box: 2276-2318 steps/s after 48, 2310-2345 after "
                          "200, 2345 sustained over 2000 steps; profiles/archive_r5.md (r5_short_window.txt))")
+    ap.add_argument("--tree-ride", type=int, default=1, choices=[0, 1],
+                    help="1: the learner's priority-tree write rides the trunk backward's launches as extra "
+                         "workgroups (no tree stream fork / join); 0: the forked tree stream")
     ap.add_argument("--actor-at", default="start", choices=["start", "loss"],
                     help="overlapped engine: start the actor graph with the learner step, or after its fused "
                          "loss + heads backward (beside the trunk backward)")
@@ -280,7 +283,8 @@ def main():
     if args.scaling == "strong" and args.batch % world:
         raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
     rank_batch = args.batch // world if args.scaling == "strong" else args.batch
-    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank)
+    lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
+                       tree_ride=bool(args.tree_ride))
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
@@ -391,6 +395,8 @@ def main():
                 "hip_graphs": not args.no_graphs,
                 "graph_warm_replays": 0 if args.no_graphs else args.graph_warm,
                 "actor_learner_overlap": args.overlap, "actor_at": args.actor_at,
+                "tree_write": ("riders of the trunk backward's launches" if eng.learner.tree_rides_used
+                               else "forked tree stream"),
                 "dp_graph": eng._g_dp is not None,
                 # ranks the communicators themselves report: RCCL's ncclCommCount on the direct
                 # gradient communicator, else the torch.distributed group size
@@ -614,7 +620,8 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
 
     if world < 2:
         raise SystemExit("--topology central needs >= 2 ranks")
-    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, dtype=args.dtype, seed=args.seed)
+    lc = LearnerConfig(batch_size=args.batch, forward=args.forward, dtype=args.dtype, seed=args.seed,
+                       tree_ride=bool(args.tree_ride))
     E = central_envs(args, world - 1)
     cfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,

@@ -38,14 +38,14 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start", capacity=4096):
+def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start", capacity=4096, tree_ride=True):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=capacity, threshold_size=2048, overlap=overlap, use_graphs=graphs,
                        publish_param_interval=4, target_update_interval=6, actor_at=actor_at,
-                       learner=LearnerConfig(batch_size=256, forward="hip"))
+                       learner=LearnerConfig(batch_size=256, forward="hip", tree_ride=tree_ride))
     torch.manual_seed(0)
     # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
     # pipelined shard-mass exchange) with a world-1 all-reduce -- same code path, 1 GPU
@@ -76,6 +76,35 @@ def test_graphs_equal_sequential_schedule(cuda, overlap, actor_at):
     assert torch.equal(eng_g.learner.flat, eng_e.learner.flat)
     assert torch.equal(eng_g.actor_flat, eng_e.actor_flat)
     assert torch.isfinite(eng_g.learner.flat).all()
+
+
+@pytest.mark.parametrize("capacity", [4096, 8192, 1 << 21])
+def test_tree_riders_equal_forked_tree_stream(cuda, capacity):
+    """The priority-tree write as riders of the trunk backward's launches (leaves with the FC1
+    pair, level 1 with the conv3 pair, level 2 with the conv2 pair, the top walk with the gradient
+    finalize -- or with the conv2 pair when only level 1 is wide) leaves the replay, the
+    counters and the learner exactly as the forked tree stream does (4096: level 1 of 64 nodes;
+    8192: 128; 2M: levels 1 and 2 wide, 512 nodes at level 2)."""
+    engs = [_engine(cuda, True, True, capacity=capacity, tree_ride=r) for r in (True, False)]
+    for eng in engs:
+        eng.fill()
+        eng.capture()
+    assert engs[0].learner.tree_rides_used and not engs[1].learner.tree_rides_used
+    for _ in range(40):
+        for eng in engs:
+            eng.train_step()
+    torch.cuda.synchronize()
+    a, b = (e.replay for e in engs)
+    for name in ("leaf_sum", "leaf_min", "max_prio", "filled", "s_ids", "frames"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    for x, y in zip(a.node_sum + a.node_min, b.node_sum + b.node_min):
+        assert torch.equal(x, y)
+    assert torch.equal(a.owner, torch.full_like(a.owner, -1))  # every dedup claim released
+    la, lb = (e.learner for e in engs)
+    for name in ("flat", "step_counter", "prio", "loss", "idx", "w"):
+        assert torch.equal(getattr(la, name), getattr(lb, name)), name
+    # the tree is consistent: the root holds the sum of the leaves
+    assert torch.allclose(a.node_sum[-1].double(), a.leaf_sum.double().sum(), rtol=1e-9)
 
 
 @pytest.mark.parametrize("overlap,sharded", [(True, False), (False, False), (True, True), (False, True)])
