@@ -57,6 +57,10 @@ class LearnerConfig:
     # pair: ops/csrc/tree_dev.h tree_ride) instead of a forked tree stream joined before the
     # optimizer -- fp32 HIP learner, single process, no ingest tail
     tree_ride: bool = True
+    # the PER draw folded into the fp32 conv1 forward launch (every workgroup draws its own
+    # samples; f32_conv1_fwd_x3_k) instead of its own sampling launch at the chain head --
+    # single replay, no private rows
+    draw_in_conv1: bool = True
 
 
 def forward_q(model: DuelingDQN, x_u8: torch.Tensor, bf16: bool = False) -> torch.Tensor:
@@ -186,6 +190,7 @@ class DQNLearner:
         # (staged table ptr dict, slots, raw priorities)
         self.pre_rows = []
         self.tree_rides_used = False  # the last traced trunk backward carried the tree riders
+        self.draws_in_conv1 = False   # the last traced forward drew its batch inside conv1
 
     @staticmethod
     def _stream() -> int:
@@ -241,16 +246,34 @@ class DQNLearner:
         for extra in rows[:-1]:  # more than one staged actor step per learner step
             self.hip.apply_staged_rows(extra[0], self.replay.trans_ptrs(), extra[1].data_ptr(), extra[2].data_ptr(),
                                        extra[1].numel(), s)
-        self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob, shard=shard,
-                                   rows=rows[-1] if rows else None, out_rows=self.rows)
+        draw = self._conv1_draw(rows[-1] if rows else None) if glob is None and shard is None else None
+        self.draws_in_conv1 = draw is not None
+        if draw is None:
+            self.replay.sample_indices(self.B, self.idx, self.w, self.step_counter, self.beta, glob=glob,
+                                       shard=shard, rows=rows[-1] if rows else None, out_rows=self.rows)
         if self.rows is not None:  # the batch reads its private rows (no idx indirection)
             self._src = (self.rows["s_ids"], self.rows["s2_ids"], None, SimpleNamespace(**self.rows))
         else:
             self._src = (rp.s_ids, rp.s2_ids, self.idx, rp)
-        self._forward_and_loss(s, part)
+        self._forward_and_loss(s, part, draw)
 
-    def _forward_and_loss(self, s: int, part: str | None = None) -> None:
-        """Forward x3 + loss (+ the backward: single process) of the batch in ``_src``."""
+    def _conv1_draw(self, rows):
+        """The PER draw (+ the staged actor rows ``rows`` it scatters) as part of the conv1
+        forward launch -- the slots, IS weights and rows per_sample writes -- or None when the
+        draw keeps its own launch (no fp32 HIP forward, private rows)."""
+        rp = self.replay
+        if not (self.cfg.draw_in_conv1 and self.hip_net and self.fp32 and self.rows is None):
+            return None
+        st = {} if rows is None else {"rows_stage": rows[0], "rows_dst": rp.trans_ptrs(),
+                                      "rows_slot": rows[1].data_ptr(), "rows_prio": rows[2].data_ptr(),
+                                      "rows_E": rows[1].numel()}
+        return self.hip.make_conv_sample(rp.tree, rp.filled.data_ptr(), self.beta.data_ptr(), rp.seed,
+                                         self.step_counter.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(),
+                                         int(not rp.exact_mass), **st)
+
+    def _forward_and_loss(self, s: int, part: str | None = None, draw=None) -> None:
+        """Forward x3 + loss (+ the backward: single process) of the batch in ``_src``
+        (``draw``: the PER draw folded into the conv1 launch)."""
         rp = self.replay
         if self.hip_net:
             # conv1 reads the sampled stacks straight out of the HBM frame ring (no gather),
@@ -258,7 +281,7 @@ class DQNLearner:
             # share each layer's launch (5 kernels, not 15).
             ids_s, ids_s2, jdx, tab = self._src
             forward_multi([(self.net, rp.frames, self.ws_s, ids_s, jdx), (self.net, rp.frames, self.ws_s2, ids_s2, jdx),
-                           (self.tnet, rp.frames, self.ws_t, ids_s2, jdx)])
+                           (self.tnet, rp.frames, self.ws_t, ids_s2, jdx)], draw=draw)
             q2t = self.ws_t.q
             m = self.model
             self.hip.dqn_heads_bwd(
@@ -279,6 +302,7 @@ class DQNLearner:
             if part != "a":
                 self._trunk_phase()
             return
+        assert draw is None, "the folded draw needs the HIP forward"
         hooks, self.tree_hooks = self.tree_hooks, []
         for fn in hooks:  # no tree stream on this path: deferred priorities go right after sampling
             fn()

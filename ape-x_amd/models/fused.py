@@ -292,7 +292,7 @@ class HipDuelingNet:
                 for k, wsp in ((3, w3), (2, w2), (1, w1))]
 
 
-def forward_multi(passes, act: tuple | None = None) -> None:
+def forward_multi(passes, act: tuple | None = None, draw=None) -> None:
     """Run up to 3 forward passes ``(net, x, ws, ids, idx)`` (same batch size and action
     count; the nets may differ, e.g. online and target) with ONE launch per layer: conv1,
     conv2, conv3, FC1, heads = 5 kernels instead of 5 per pass.  Each kernel boundary
@@ -301,7 +301,8 @@ def forward_multi(passes, act: tuple | None = None) -> None:
     passes = list(passes)
     if getattr(passes[0][0], "fp32", False):
         from .fused_f32 import forward_multi_f32
-        return forward_multi_f32(passes, act=act)
+        return forward_multi_f32(passes, act=act, draw=draw)
+    assert draw is None, "the PER draw folds into the fp32 conv1 launch only"
     assert 1 <= len(passes) <= 3
     net0 = passes[0][0]
     B, A = passes[0][2].B, net0.A

@@ -258,9 +258,10 @@ class F32DuelingNet:
         return h.grad_finalize(jobs, self._s(), 0 if sumsq is None else sumsq.data_ptr(), ride=rides[3])
 
 
-def forward_multi_f32(passes, act: tuple | None = None) -> None:
+def forward_multi_f32(passes, act: tuple | None = None, draw=None) -> None:
     """Up to 3 fp32 forward passes ``(net, x, ws, ids, idx)`` (common batch and action
-    count; the nets may differ, e.g. online and target) with ONE launch per layer."""
+    count; the nets may differ, e.g. online and target) with ONE launch per layer.  ``draw``
+    (``make_conv_sample``): the conv1 launch draws the PER rows that ``idx`` then holds."""
     passes = list(passes)
     assert 1 <= len(passes) <= 3
     net0 = passes[0][0]
@@ -276,7 +277,7 @@ def forward_multi_f32(passes, act: tuple | None = None) -> None:
         c3.append((ws.a2.data_ptr(), 0, 0, net.w3p.data_ptr(), 0, f[4].bias.data_ptr(), ws.a3.data_ptr()))
         fc.append((ws.a3.data_ptr(), 0, 0, net.wfc1p.data_ptr(), 0, 0, ws.z.data_ptr()))
         hd.append(net._heads_tuple(ws))
-    h.f32_conv_fwd_multi(1, c1, B, s)
+    h.f32_conv_fwd_multi(1, c1, B, s, draw=draw)
     h.f32_conv_fwd_multi(2, c2, B, s)
     h.f32_conv_fwd_multi(3, c3, B, s)
     nsplit = h.f32_fc1_fwd_multi(fc, B, s)

@@ -880,17 +880,26 @@ __device__ __forceinline__ void split_w1(const float* wrow, W1Split& w) {
 // 512 / 1024 workgroups 42.2 / 41.5-43.9 us, one sample per workgroup (1536) 44.4-45.0 us
 // (3 x 512 samples, interleaved on one box)
 constexpr int kC1xGrid = 512;
+// the learner's 3 x 512 samples on 384 workgroups (4 each): with the PER draw folded in, the
+// 512-workgroup launch filled every CU's LDS (2 x 56 KB) from the step's first microsecond and
+// starved the actor graph's conv1 beside it (the sampling launch used to give it a head start):
+// whole step, alternated on one box, draw folded at 384 / 448 / 320 / 512 workgroups 2546.5 /
+// 2549.8 / 2441.3 / 2446.5 (another box), sampling launch + 512: 2525.3 (profiles/r6_step_kernels.md)
+constexpr int kC1xGridLearner = 384;
+constexpr int kC1xDrawMax = 8;  // samples per workgroup with the folded draw (2 per wave)
 constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
 
-// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on)
-__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer]) {
+// the sample's 4 x 441 16-byte u8 chunks -> registers (issued, not waited on); fid (the folded
+// draw): the sample's 4 frame ids, drawn by this workgroup
+__device__ __forceinline__ void c1x_load(const F32Set& set, int smp, uint4 (&v)[kC1xPer], const int* fid) {
   const int B = set.B, prob = smp / B, b = smp - prob * B, t = threadIdx.x;
   const F32Prob p = pick(set, prob);
-  const FrameSrc f{static_cast<const uint8_t*>(p.in), p.ids, p.idx};
-  const uint4* s0 = reinterpret_cast<const uint4*>(frame_plane(f, b, 0, kPlane));
-  const uint4* s1 = reinterpret_cast<const uint4*>(frame_plane(f, b, 1, kPlane));
-  const uint4* s2 = reinterpret_cast<const uint4*>(frame_plane(f, b, 2, kPlane));
-  const uint4* s3 = reinterpret_cast<const uint4*>(frame_plane(f, b, 3, kPlane));
+  const uint8_t* fr = static_cast<const uint8_t*>(p.in);
+  const FrameSrc f{fr, p.ids, p.idx};
+  const uint4* s0 = reinterpret_cast<const uint4*>(fid ? fr + (size_t)fid[0] * kPlane : frame_plane(f, b, 0, kPlane));
+  const uint4* s1 = reinterpret_cast<const uint4*>(fid ? fr + (size_t)fid[1] * kPlane : frame_plane(f, b, 1, kPlane));
+  const uint4* s2 = reinterpret_cast<const uint4*>(fid ? fr + (size_t)fid[2] * kPlane : frame_plane(f, b, 2, kPlane));
+  const uint4* s3 = reinterpret_cast<const uint4*>(fid ? fr + (size_t)fid[3] * kPlane : frame_plane(f, b, 3, kPlane));
 #pragma unroll
   for (int k = 0; k < kC1xPer; ++k) {  // (no dynamically indexed pointer array: it would live in scratch)
     const int e = min(t + 256 * k, kC1xChunks - 1), c = e / 441;  // tail lanes reload a valid chunk
@@ -927,20 +936,50 @@ __device__ __forceinline__ int opaque_i(int x) {
   asm volatile("" : "+v"(x));
   return x;
 }
-__global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
+// cs.out_idx (the learner): the PER draw folded in -- wave k draws sample s0 + k's slot (the
+// per_sample_k descent, same arithmetic: identical slots and IS weights) and its 4 frame ids go
+// to LDS before the first frame load; workgroups past cs.nhost scatter the staged actor rows.
+__global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set, ConvSample cs) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[2 * kPlaneDw * 4];  // 4 planes of bf16
+  __shared__ int fid[kC1xDrawMax][4];  // (the draw) frame ids of the workgroup's samples
   const int B = set.B, total = set.n * B;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int i = lane & 15, q = lane >> 4, nh = wave >> 1;
+  const bool draw = cs.out_idx != nullptr;  // grid-uniform
+  const int G = draw ? cs.nhost : (int)gridDim.x;
+  if (draw && (int)blockIdx.x >= G) {  // block-uniform: the staged-row scatter
+    staged_scatter(cs.rows, blockIdx.x - G);
+    return;
+  }
   const __bf16* xb = reinterpret_cast<const __bf16*>(xs);
   W1Split w;
   int cur = -1;
   uint4 v[kC1xPer];
   // a contiguous run of samples per workgroup: the weight split is redone only at a
   // problem boundary (a grid-strided walk crossed one at every sample: ~25 % of the VALU)
-  const int per = (total + gridDim.x - 1) / gridDim.x;
+  const int per = (total + G - 1) / G;
   const int s0 = blockIdx.x * per, s1 = min(total, s0 + per);
-  if (s0 < s1) c1x_load(set, s0, v);
+  if (draw) {  // (per <= kC1xDrawMax: checked by the launcher)
+    for (int k = wave; k < s1 - s0; k += 4) {  // wave-uniform
+      const int smp = s0 + k, prob = smp / B, b = smp - prob * B;
+      const int64_t len64 = cs.length[0];
+      const int length = (int)(len64 < (int64_t)cs.t.size[0] ? len64 : (int64_t)cs.t.size[0]);
+      const float pmin = cs.t.node_min[cs.t.levels - 1][0];
+      float p;
+      const int node = tree_sample_leaf(cs.t, b, B, length, cs.exclude_last, cs.seed, (uint64_t)cs.counter[0], lane,
+                                        &p);
+      const int se = staged_row_of(cs.rows, node, lane);
+      const F32Prob pp = pick(set, prob);
+      const int* ids = se < 0 ? pp.ids : (pp.ids == cs.rows.dst.s_ids ? cs.rows.st.s_ids : cs.rows.st.s2_ids);
+      if (lane < 4) fid[k][lane] = ids[4 * (se < 0 ? node : se) + lane];
+      if (prob == 0 && lane == 0) {
+        cs.out_idx[b] = node;
+        cs.out_w[b] = per_is_weight(p, pmin, 1.f, cs.beta[0]);
+      }
+    }
+    __syncthreads();
+  }
+  if (s0 < s1) c1x_load(set, s0, v, draw ? fid[0] : nullptr);
   for (int smp = s0; smp < s1; ++smp) {
     const int prob = smp / B, b = smp - prob * B;
     const F32Prob p = pick(set, prob);
@@ -951,7 +990,7 @@ __global__ __launch_bounds__(256, 2) void f32_conv1_fwd_x3_k(F32Set set) {
     __syncthreads();  // the previous sample's tiles are done with xs
     c1x_store(v, xs);
     __syncthreads();
-    if (smp + 1 < s1) c1x_load(set, smp + 1, v);  // in flight during the MFMA loop
+    if (smp + 1 < s1) c1x_load(set, smp + 1, v, draw ? fid[smp + 1 - s0] : nullptr);  // in flight during the MFMAs
     // roles swapped on the MFMA (A = the weight slice, B = the pixels: identical lane maps),
     // so lane (i, q) ends with channels 4q .. 4q+3 of pixel i -- one 16-byte store
     float* out = p.out + (size_t)b * 400 * 32 + nh * 16 + 4 * q;
@@ -1631,14 +1670,30 @@ static int default_tile(int layer) {
   return layer == 2 ? t2 : t3;
 }
 
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid, int tile) {
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid, int tile, const ConvSample* draw) {
   check_set(set);
+  if (draw && draw->out_idx && layer != 1) throw std::invalid_argument("f32_conv_fwd_multi: the draw folds into conv1");
   if (tile == 0 && (layer == 2 || layer == 3)) tile = default_tile(layer);
   switch (layer) {
-    case 1:
-      f32_conv1_fwd_x3_k<<<std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid), 256, 0, s>>>(set);
+    case 1: {
+      if (c1_grid <= 0 && learner_sized(set)) c1_grid = kC1xGridLearner;
+      const int G = std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid);
+      ConvSample c{};
+      if (draw && draw->out_idx) {
+        c = *draw;
+        c.nhost = G;
+        if ((set.n * set.B + G - 1) / G > kC1xDrawMax)
+          throw std::invalid_argument("f32 conv1 draw: <= 8 samples per workgroup");
+        if (!c.length || !c.beta || !c.counter || !c.out_w || set.p[0].idx != c.out_idx)
+          throw std::invalid_argument("f32 conv1 draw: fill level, beta, counter, weights, and problem 0 reading idx");
+        for (int k = 0; k < set.n; ++k)
+          if (!set.p[k].ids || (c.rows.E > 0 && set.p[k].ids != c.rows.dst.s_ids && set.p[k].ids != c.rows.dst.s2_ids))
+            throw std::invalid_argument("f32 conv1 draw: every problem reads the replay's frame-id tables");
+      }
+      f32_conv1_fwd_x3_k<<<G + (c.out_idx ? (c.rows.E + 255) / 256 : 0), 256, 0, s>>>(set, c);
       LAUNCH_CHECK();
       break;
+    }
     case 2:  // learner: 128 x 64 tiles at BK 32 (64 x 32 per wave): on the split-bf16 MFMA 66.6-67.5 us
              // vs 73-79 for 64 x 64 (under fp32 MFMA 64 x 64 had won) and 76-88 for 256 x 64 (64 x 64
              // per wave: one wave per SIMD); whole step 2456-2466 vs 2193-2200 steps/s for 256 x 64

@@ -71,6 +71,12 @@ BatchWrite batch_write(uint64_t pre_idx, uint64_t pre_prio, int E, uint64_t pre_
 
 const TreeRide* ride_of(const py::object& o) { return o.is_none() ? nullptr : o.cast<const TreeRide*>(); }
 
+TransTable trans_table(py::dict d) {
+  auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
+  return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
+                    P<float>(g("done"))};
+}
+
 struct NStepHandle {
   NStepParams p{};
   NStepState st{};
@@ -153,11 +159,7 @@ PYBIND11_MODULE(_apex_hip, m) {
                          int exclude_last, uint64_t s, uint64_t glob, uint64_t gathered, int world, int rank,
                          py::object rows_stage, py::object rows_dst, uint64_t rows_slot, uint64_t rows_prio,
                          int rows_E, py::object src, py::object out) {
-    auto tab = [](py::dict d) {
-      auto g = [&](const char* k) { return d[k].cast<uint64_t>(); };
-      return TransTable{P<int>(g("s_ids")), P<int>(g("s2_ids")), P<int>(g("action")), P<float>(g("reward")),
-                        P<float>(g("done"))};
-    };
+    auto tab = trans_table;
     StagedRows rows{};
     if (rows_E > 0)
       rows = StagedRows{tab(rows_stage.cast<py::dict>()), tab(rows_dst.cast<py::dict>()), P<const int>(rows_slot),
@@ -496,9 +498,38 @@ PYBIND11_MODULE(_apex_hip, m) {
   };
   // probs: (in, ids, idx, w, w2, bias, out)
   m.def("f32_conv_fwd_multi", [f32set](int layer, const std::vector<std::vector<uint64_t>>& probs, int B,
-                                       uint64_t s, int c1_grid, int tile) {
-    f32_conv_fwd_multi(layer, f32set(probs, B), S(s), c1_grid, tile);
-  }, py::arg("layer"), py::arg("probs"), py::arg("B"), py::arg("s"), py::arg("c1_grid") = 0, py::arg("tile") = 0);
+                                       uint64_t s, int c1_grid, int tile, py::object draw) {
+    f32_conv_fwd_multi(layer, f32set(probs, B), S(s), c1_grid, tile,
+                       draw.is_none() ? nullptr : draw.cast<const ConvSample*>());
+  }, py::arg("layer"), py::arg("probs"), py::arg("B"), py::arg("s"), py::arg("c1_grid") = 0, py::arg("tile") = 0,
+     py::arg("draw") = py::none());
+  // the learner's PER draw folded into the conv1 forward (f32_conv_fwd_multi(1, draw=)): the
+  // per_sample arguments of the plain single-replay path (+ the staged actor rows it scatters)
+  py::class_<ConvSample>(m, "ConvSample");
+  m.def("make_conv_sample", [](const TreeHandle& t, uint64_t length_ptr, uint64_t beta_ptr, uint64_t seed,
+                               uint64_t counter, uint64_t out_idx, uint64_t out_w, int exclude_last,
+                               py::object rows_stage, py::object rows_dst, uint64_t rows_slot, uint64_t rows_prio,
+                               int rows_E) {
+    if (!length_ptr || !beta_ptr || !counter || !out_idx || !out_w)
+      throw std::invalid_argument("make_conv_sample: fill level, beta, counter, idx and weight pointers");
+    ConvSample c{};
+    c.t = t.d;
+    c.length = P<const int64_t>(length_ptr);
+    c.beta = P<const float>(beta_ptr);
+    c.counter = P<const int64_t>(counter);
+    c.seed = seed;
+    c.out_idx = P<int>(out_idx);
+    c.out_w = P<float>(out_w);
+    c.exclude_last = exclude_last;
+    if (rows_E > 0) {
+      if (!rows_slot || !rows_prio) throw std::invalid_argument("make_conv_sample: staged slots / priorities");
+      c.rows = StagedRows{trans_table(rows_stage.cast<py::dict>()), trans_table(rows_dst.cast<py::dict>()),
+                          P<const int>(rows_slot), P<const float>(rows_prio), rows_E};
+    }
+    return c;
+  }, py::arg("t"), py::arg("length_ptr"), py::arg("beta_ptr"), py::arg("seed"), py::arg("counter"),
+     py::arg("out_idx"), py::arg("out_w"), py::arg("exclude_last"), py::arg("rows_stage") = py::none(),
+     py::arg("rows_dst") = py::none(), py::arg("rows_slot") = 0, py::arg("rows_prio") = 0, py::arg("rows_E") = 0);
   m.def("f32_fc1_fwd_multi", [f32set](const std::vector<std::vector<uint64_t>>& probs, int B, uint64_t s) {
     return f32_fc1_fwd_multi(f32set(probs, B), S(s));
   });

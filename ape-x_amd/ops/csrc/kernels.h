@@ -395,7 +395,25 @@ struct F32Set {
   F32Prob p[kMaxProbs];
   int n, B;
 };
-void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0);
+// The learner's PER draw folded into the fp32 conv1 forward (f32_conv1_fwd_x3_k): every
+// workgroup draws the slots of its own samples (one wave each, the per_sample_k descent) before
+// staging their frames, and problem 0's workgroups write out_idx / out_w.  rows.E > 0: the staged
+// actor rows this launch scatters into the tables (extra workgroups, as per_sample_k's); a drawn
+// slot among them is read from the staging rows.  out_idx == nullptr: no draw.
+struct ConvSample {
+  TreeDesc t;
+  const int64_t* length;   // live fill level (replay.filled)
+  const float* beta;
+  const int64_t* counter;  // RNG step counter
+  uint64_t seed;
+  int* out_idx;
+  float* out_w;
+  int exclude_last;
+  StagedRows rows;
+  int nhost;  // set by the launcher
+};
+void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid = 0, int tile = 0,
+                        const ConvSample* draw = nullptr);  // draw: layer 1 only
 int f32_fc1_splits();
 // GEMM form: mask = forward form + 4 x backward-pair form; form 0 = per-wave register split,
 // 1 = stage-split LDS image (split once per staged element, double-buffered), 2 = the same

@@ -214,14 +214,7 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
                              float* __restrict__ out_w, int exclude_last, const float* __restrict__ glob,
                              ShardGlob sg, StagedRows rows, SampleRowsOut ro, int sample_blocks) {
   if ((int)blockIdx.x >= sample_blocks) {  // fused staged-row scatter (apply_staged_rows)
-    const int e = (blockIdx.x - sample_blocks) * blockDim.x + threadIdx.x;
-    if (e >= rows.E || !(rows.prio[e] > 0.f)) return;
-    const int j = rows.slot[e];
-    reinterpret_cast<int4*>(rows.dst.s_ids)[j] = reinterpret_cast<const int4*>(rows.st.s_ids)[e];
-    reinterpret_cast<int4*>(rows.dst.s2_ids)[j] = reinterpret_cast<const int4*>(rows.st.s2_ids)[e];
-    rows.dst.action[j] = rows.st.action[e];
-    rows.dst.reward[j] = rows.st.reward[e];
-    rows.dst.done[j] = rows.st.done[e];
+    staged_scatter(rows, blockIdx.x - sample_blocks);
     return;
   }
   const int lane = threadIdx.x & 63;
@@ -245,14 +238,11 @@ __global__ void per_sample_k(TreeDesc t, int B, const int64_t* length_ptr, int64
   }
   if (lane == 0) {
     out_idx[i] = node;
-    out_w[i] = wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
+    out_w[i] = per_is_weight(p, pmin, wscale, beta);
   }
   if (ro.out.s_ids) {  // private row copy: the staged row if this launch scatters the slot (no race with
                        // the scatter blocks), else the table row (a slot nobody writes in this launch)
-    int se = -1;
-    for (int e = lane; e < rows.E; e += 64)
-      if (rows.slot[e] == node && rows.prio[e] > 0.f) se = e;
-    se = wave_max(se);
+    const int se = staged_row_of(rows, node, lane);
     const TransTable& src = se >= 0 ? rows.st : ro.src;
     const int r = se >= 0 ? se : node;
     if (lane < 4) ro.out.s_ids[4 * i + lane] = src.s_ids[4 * r + lane];

@@ -389,6 +389,32 @@ __device__ __forceinline__ void batch_leaves_block(const TreeDesc& t, const Batc
   }
 }
 
+// IS weight of a drawn leaf (memory.py:284-298 as (p / p_min)^-beta) times the shard scale
+__device__ __forceinline__ float per_is_weight(float p, float pmin, float wscale, float beta) {
+  return wscale * ((p > 0.f && pmin > 0.f && isfinite(pmin)) ? powf(p / pmin, -beta) : 1.f);
+}
+
+// The staging row of slot `node` if this launch scatters it (prio > 0), else -1 (wave-uniform)
+__device__ __forceinline__ int staged_row_of(const StagedRows& rows, int node, int lane) {
+  int se = -1;
+  for (int e = lane; e < rows.E; e += 64)
+    if (rows.slot[e] == node && rows.prio[e] > 0.f) se = e;
+  return wave_max(se);
+}
+
+// One staged actor row per thread into the tables (apply_staged_rows), block `rb` of the
+// scatter workgroups of a sampling launch
+__device__ __forceinline__ void staged_scatter(const StagedRows& rows, int rb) {
+  const int e = rb * blockDim.x + threadIdx.x;
+  if (e >= rows.E || !(rows.prio[e] > 0.f)) return;
+  const int j = rows.slot[e];
+  reinterpret_cast<int4*>(rows.dst.s_ids)[j] = reinterpret_cast<const int4*>(rows.st.s_ids)[e];
+  reinterpret_cast<int4*>(rows.dst.s2_ids)[j] = reinterpret_cast<const int4*>(rows.st.s2_ids)[e];
+  rows.dst.action[j] = rows.st.action[e];
+  rows.dst.reward[j] = rows.st.reward[e];
+  rows.dst.done[j] = rows.st.done[e];
+}
+
 // Block reduction of rows v[0, n) in the order of block_reduce_1024 over a 1024-thread block
 // holding one row per thread (wave j sums rows [64 j, 64 j + 64); the wave totals are added in
 // order j = 0, 1, ..): any block size gives the same bits as the one-row-per-thread kernels

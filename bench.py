@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--tree-ride", type=int, default=1, choices=[0, 1],
                     help="1: the learner's priority-tree write rides the trunk backward's launches as extra "
                          "workgroups (no tree stream fork / join); 0: the forked tree stream")
+    ap.add_argument("--draw-in-conv1", type=int, default=1, choices=[0, 1],
+                    help="1: the learner's PER draw runs inside the conv1 forward launch; 0: its own sampling "
+                         "launch at the chain head")
     ap.add_argument("--actor-at", default="start", choices=["start", "loss"],
                     help="overlapped engine: start the actor graph with the learner step, or after its fused "
                          "loss + heads backward (beside the trunk backward)")
@@ -284,7 +287,7 @@ def main():
         raise SystemExit(f"--scaling strong needs --batch divisible by {world}")
     rank_batch = args.batch // world if args.scaling == "strong" else args.batch
     lc = LearnerConfig(batch_size=rank_batch, forward=args.forward, dtype=args.dtype, seed=args.seed + rank,
-                       tree_ride=bool(args.tree_ride))
+                       tree_ride=bool(args.tree_ride), draw_in_conv1=bool(args.draw_in_conv1))
     cfg = EngineConfig(n_envs=args.envs, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,
                        actor_offset=rank * args.envs, total_actors=world * args.envs,
@@ -389,7 +392,8 @@ def main():
                 "actor_steps_per_learner_step": args.actor_steps,
                 "optimizer": "centered RMSprop lr 6.25e-5 alpha .95 eps 1.5e-7, clip 40",
                 "per": "alpha 0.6 beta 0.4, stratified proportional, fanout-64 HBM tree",
-                "batch_pipeline": "sampled at the step start, 3-pass forward",
+                "batch_pipeline": ("drawn inside the conv1 forward launch" if eng.learner.draws_in_conv1
+                                   else "sampled at the step start") + ", 3-pass forward",
                 "forward": args.forward,
                 "fp32_gemms": "exact 3-term bf16 split (x6) on MFMA, fp32 accumulate" if args.dtype == "fp32" else None,
                 "hip_graphs": not args.no_graphs,
@@ -621,7 +625,7 @@ def central(args, rank, world, device, wd, pre=None, emulate: int = 0):
     if world < 2:
         raise SystemExit("--topology central needs >= 2 ranks")
     lc = LearnerConfig(batch_size=args.batch, forward=args.forward, dtype=args.dtype, seed=args.seed,
-                       tree_ride=bool(args.tree_ride))
+                       tree_ride=bool(args.tree_ride), draw_in_conv1=bool(args.draw_in_conv1))
     E = central_envs(args, world - 1)
     cfg = EngineConfig(n_envs=E, n_actions=args.actions, replay_capacity=args.capacity,
                        threshold_size=args.threshold, actor_steps_per_learner_step=args.actor_steps,

@@ -38,14 +38,16 @@ def test_staged_actor_rows_match_direct_write(cuda, mode):
     assert torch.equal(a.step_counter, b.step_counter)
 
 
-def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start", capacity=4096, tree_ride=True):
+def _engine(dev, overlap, graphs, dp=False, sharded=False, actor_at="start", capacity=4096, tree_ride=True,
+            draw_in_conv1=True):
     from apex_amd.engine.apex import ApexEngine, EngineConfig
     from apex_amd.engine.learner import LearnerConfig
     from apex_amd.parallel.dp import FlatGradAllReduce
 
     cfg = EngineConfig(n_envs=64, replay_capacity=capacity, threshold_size=2048, overlap=overlap, use_graphs=graphs,
                        publish_param_interval=4, target_update_interval=6, actor_at=actor_at,
-                       learner=LearnerConfig(batch_size=256, forward="hip", tree_ride=tree_ride))
+                       learner=LearnerConfig(batch_size=256, forward="hip", tree_ride=tree_ride,
+                                             draw_in_conv1=draw_in_conv1))
     torch.manual_seed(0)
     # dp: the data-parallel phase split (FC1/head all-reduce overlapping the conv backward,
     # pipelined shard-mass exchange) with a world-1 all-reduce -- same code path, 1 GPU
@@ -105,6 +107,30 @@ def test_tree_riders_equal_forked_tree_stream(cuda, capacity):
         assert torch.equal(getattr(la, name), getattr(lb, name)), name
     # the tree is consistent: the root holds the sum of the leaves
     assert torch.allclose(a.node_sum[-1].double(), a.leaf_sum.double().sum(), rtol=1e-9)
+
+
+@pytest.mark.parametrize("capacity", [4096, 1 << 21])
+def test_conv1_draw_equals_sampling_launch(cuda, capacity):
+    """The PER draw folded into the conv1 forward launch (each workgroup draws its samples'
+    slots; problem 0's write idx / IS weights; extra workgroups scatter the staged actor rows and
+    a drawn slot among them is read from the staging rows) gives exactly the batches, replay
+    tables and learner of the separate sampling launch, with the actor rows staged every step."""
+    engs = [_engine(cuda, True, True, capacity=capacity, draw_in_conv1=d) for d in (True, False)]
+    for eng in engs:
+        eng.fill()
+        eng.capture()
+    assert engs[0].learner.draws_in_conv1 and not engs[1].learner.draws_in_conv1
+    for _ in range(40):  # 64 envs x 40 steps > 2048 free slots of the 4096 ring: staged rows overwrite drawn slots
+        for eng in engs:
+            eng.train_step()
+    torch.cuda.synchronize()
+    a, b = (e.replay for e in engs)
+    for name in ("s_ids", "s2_ids", "action", "reward", "done", "leaf_sum", "max_prio", "filled"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    la, lb = (e.learner for e in engs)
+    for name in ("idx", "w", "flat", "prio", "loss", "step_counter"):
+        assert torch.equal(getattr(la, name), getattr(lb, name)), name
+    assert la.idx.unique().numel() > la.B // 2  # real draws, not a constant slot
 
 
 @pytest.mark.parametrize("overlap,sharded", [(True, False), (False, False), (True, True), (False, True)])
