@@ -886,6 +886,9 @@ constexpr int kC1xGrid = 512;
 // whole step, alternated on one box, draw folded at 384 / 448 / 320 / 512 workgroups 2546.5 /
 // 2549.8 / 2441.3 / 2446.5 (another box), sampling launch + 512: 2525.3 (profiles/r6_step_kernels.md)
 constexpr int kC1xGridLearner = 384;
+// small launches (the actor's 256 envs beside the learner's forward) at 2 samples per workgroup:
+// 128 workgroups 2566.9, 256 (one sample each, the round-5 shape) 2466.3, 192 2517.0, 96 2538.1,
+// 64 2492.0 learner steps/s (one box, alternated; profiles/r6_step_kernels.md)
 constexpr int kC1xDrawMax = 8;  // samples per workgroup with the folded draw (2 per wave)
 constexpr int kC1xChunks = 4 * (kPlane / 16), kC1xPer = (kC1xChunks + 255) / 256;  // 16-byte u8 chunks
 
@@ -1676,7 +1679,7 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
   if (tile == 0 && (layer == 2 || layer == 3)) tile = default_tile(layer);
   switch (layer) {
     case 1: {
-      if (c1_grid <= 0 && learner_sized(set)) c1_grid = kC1xGridLearner;
+      if (c1_grid <= 0) c1_grid = learner_sized(set) ? kC1xGridLearner : (set.n * set.B + 1) / 2;
       const int G = std::min(set.n * set.B, c1_grid > 0 ? c1_grid : kC1xGrid);
       ConvSample c{};
       if (draw && draw->out_idx) {
@@ -1700,13 +1703,15 @@ void f32_conv_fwd_multi(int layer, const F32Set& set, hipStream_t s, int c1_grid
       if (learner_sized(set) && tile == 1) fwd_launch<Conv2FwdT<64, 64, 32, 2>>(set, s);
       else if (learner_sized(set) && tile == 2) fwd_launch<Conv2FwdT<128, 64, 32, 4>>(set, s);
       else if (learner_sized(set)) fwd_launch<Conv2FwdT<128, 64, 32, 2>>(set, s);
-      else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);
+      else fwd_launch<Conv2FwdT<128, 32, 32, 4>>(set, s);  // (the actor: 128 x 64 / 64 x 64 measured no better)
       break;
     case 3:  // learner: 64 x 64 (46.7-46.8 us vs 80.6-84.5 for 256 x 64)
       if (learner_sized(set) && tile == 2) fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
       else if (learner_sized(set) && tile == 3) fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
       else if (learner_sized(set)) fwd_launch<Conv3FwdT<64, 64, 32, 2>>(set, s);
-      else fwd_launch<Conv3FwdT<128, 32, 32, 4>>(set, s);
+      // the actor: 128 x 64 tiles (98 workgroups for 256 envs beside the learner's forward):
+      // 2622.6 vs 2564.0 learner steps/s for 128 x 32 (196), 64 x 64 (196) 2558.2 (one box)
+      else fwd_launch<Conv3FwdT<128, 64, 32, 2>>(set, s);
       break;
     default: throw std::invalid_argument("f32_conv_fwd_multi: layer must be 1, 2 or 3");
   }
