@@ -1804,6 +1804,19 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.mask = mask;
   d.out = dx;
   d.B = B;
+  // microbench knob (read once): APEX_F32_BWD_HALF=1 runs only the weight-gradient half of a conv
+  // pair, 2 only the input-gradient half (profiles/r6_sr_dgrad.md: what each half costs alone)
+  static const int halves = [] {
+    const char* e = std::getenv("APEX_F32_BWD_HALF");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (halves && layer != 1) {
+    const int nw = (layer == 2 ? 512 / 64 : 576 / 64) * p.splits;
+    const int nd = layer == 2 ? Conv2DgradP::tiles(B) : Conv3DgradP::tiles(B);
+    if (layer == 2) launch2<ConvWgrad<2>, Conv2DgradP>(g, halves == 1 ? nw : 0, d, halves == 2 ? nd : 0, s, nullptr);
+    else launch2<ConvWgrad<3>, Conv3DgradP>(g, halves == 1 ? nw : 0, d, halves == 2 ? nd : 0, s, nullptr);
+    return;
+  }
   switch (layer) {
     case 3:  // tile 1: input gradient at BK 32 (the alternative to the default)
       if (tile == 1) launch2<ConvWgrad<3>, Conv3DgradP32>(g, (576 / 64) * p.splits, d, Conv3DgradP32::tiles(B), s, ride);
