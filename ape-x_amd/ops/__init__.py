@@ -54,10 +54,21 @@ def cpu():
 
 
 def hip():
-    """Load the gfx950 kernel library (requires ``import torch`` first, done here)."""
+    """Load the gfx950 kernel library (requires ``import torch`` first, done here).
+    ``APEX_HIP_EXT_DIR`` loads it from another directory instead (whole-step A/B of two
+    builds in separate processes on one box: ``scripts/ab/apex_engine_ab.py``)."""
     import torch  # noqa: F401  -- binds libamdhip64.so.7 to torch's copy before our dlopen
     from . import build
 
+    alt = os.environ.get("APEX_HIP_EXT_DIR")
+    if alt:
+        with _lock:
+            if "_apex_hip" not in _mods:
+                spec = importlib.util.spec_from_file_location("_apex_hip", os.path.join(alt, build.hip_target().name))
+                mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(mod)
+                _mods["_apex_hip"] = mod
+            return _mods["_apex_hip"]
     return _load("_apex_hip", lambda: build.build_hip())
 
 

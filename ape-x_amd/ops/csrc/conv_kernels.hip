@@ -21,6 +21,7 @@ namespace apex {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 template <int H_, int W_, int C_, int KH_, int KW_, int S_, int N_>
 struct ConvGeo {
@@ -227,8 +228,11 @@ void conv_fwd(int layer, const void* in, const int* ids, const int* idx, const u
 constexpr int kHeadRows = 4;
 
 __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
-  __shared__ float ws[64 * 129];  // row a (a < A: adv, a == A: value), padded to break bank conflicts
-  __shared__ float hs[4][256];
+  // row a (a < A: adv, a == A: value); pitch 132 floats: 16-byte rows for ds_read_b128, lane
+  // a's read starting at bank 4a (mod 64), so 16 lanes per LDS cycle are conflict-free
+  constexpr int kWp = 132;
+  __shared__ __attribute__((aligned(16))) float ws[64 * kWp];
+  __shared__ __attribute__((aligned(16))) float hs[4][256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int B = set.B, A = set.A, nsplit = set.nsplit, RB = (B + kHeadRows - 1) / kHeadRows;
   int pb, rb;
@@ -248,41 +252,46 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
   }
   const HeadsProb& pr = set.p[pb];
   const float* __restrict__ z = pr.z;
+  static_assert(kHeadRows == 4, "one row per wave");
+  const int b = rb * kHeadRows + wave;
+  const bool valid = b < B;
+  const float* zr = z + (size_t)(valid ? b : 0) * 256;
+  // split-K slabs summed in fixed (slab) order; 4 columns per lane, 8 slabs (32 loads) in
+  // flight ahead of the adds (the actor's 256-row FC1 uses 28 slabs: 2 in flight cost ~12 us).
+  // The first 8 slabs' loads are issued BEFORE the head-weight staging: the two global round
+  // trips overlap instead of following each other.
+  const size_t sstride = (size_t)B * 256;
+  constexpr int U = 8;
+  float v[U][4];
+  auto zload = [&](int sp) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[u][k] = sp + u < nsplit ? zr[(size_t)(sp + u) * sstride + lane + 64 * k] : 0.f;
+  };
+  zload(0);
   // head weights staged 8 loads at a time (a rolled load -> LDS store loop waits out one L2
   // round trip per element: ~10 per thread before the first row)
   const float* __restrict__ wa2 = pr.w_adv2;
   const float* __restrict__ wv2 = pr.w_val2;
   for (int e0 = threadIdx.x; e0 < (A + 1) * 128; e0 += 8 * 256) {
-    float v[8];
+    float wv[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = min(e0 + 256 * u, (A + 1) * 128 - 1), a = e / 128, j = e % 128;
-      v[u] = a < A ? wa2[a * 128 + j] : wv2[j];
+      wv[u] = a < A ? wa2[a * 128 + j] : wv2[j];
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = e0 + 256 * u;
-      if (e < (A + 1) * 128) ws[(e / 128) * 129 + e % 128] = v[u];
+      if (e < (A + 1) * 128) ws[(e / 128) * kWp + e % 128] = wv[u];
     }
   }
   const float bo = lane < A ? pr.b_adv2[lane] : (lane == A ? pr.b_val2[0] : 0.f);
-  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
-    const int b = rb * kHeadRows + rr * 4 + wave;
-    const bool valid = b < B;
-    const float* zr = z + (size_t)(valid ? b : 0) * 256;
-    // split-K slabs summed in fixed (slab) order; 4 columns per lane, 8 slabs (32 loads)
-    // in flight ahead of the adds: the sum is a chain of dependent L2/MALL round trips
-    // (the actor's 256-row FC1 uses 28 slabs: 2 in flight cost ~12 us)
+  {
     float zs[4] = {0.f, 0.f, 0.f, 0.f};
-    const size_t sstride = (size_t)B * 256;
-    constexpr int U = 8;
     for (int sp = 0; sp < nsplit; sp += U) {
-      float v[U][4];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          v[u][k] = sp + u < nsplit ? zr[(size_t)(sp + u) * sstride + lane + 64 * k] : 0.f;
+      if (sp > 0) zload(sp);
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -299,11 +308,17 @@ __global__ __launch_bounds__(256) void heads_fwd_k(HeadsSet set) {
     }
     __syncthreads();
     float o = 0.f;
-    if (lane <= A) {
-      const float* wr = ws + lane * 129;
-      const float* hr = hs[wave] + (lane < A ? 0 : 128);
+    if (lane <= A) {  // 16-byte LDS reads, the same j-ordered fp32 chain as a scalar loop
+      const f32x4v* wr = reinterpret_cast<const f32x4v*>(ws + lane * kWp);
+      const f32x4v* hr = reinterpret_cast<const f32x4v*>(hs[wave] + (lane < A ? 0 : 128));
 #pragma unroll 8
-      for (int j = 0; j < 128; ++j) o += hr[j] * wr[j];
+      for (int j = 0; j < 32; ++j) {
+        const f32x4v hv = hr[j], wv = wr[j];
+        o += hv[0] * wv[0];
+        o += hv[1] * wv[1];
+        o += hv[2] * wv[2];
+        o += hv[3] * wv[3];
+      }
       o += bo;
     }
     const float adv_sum = wave_sum(lane < A ? o : 0.f);

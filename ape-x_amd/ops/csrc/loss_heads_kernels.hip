@@ -37,6 +37,8 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
   __shared__ int as[LH_ROWS];
   __shared__ float dzs[LH_ROWS][256];
   __shared__ float adv[LH_MAXA][128];
+  __shared__ float wadv[LH_MAXA][128];  // W_adv2 (+ W_val2 below): the row's dz reads LDS, not
+  __shared__ float wval[128];           // a global load that waited on the action load
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = threadIdx.x;
   const int B = p.B, A = p.A;
   const int r0 = blockIdx.x * LH_ROWS, nr = min(LH_ROWS, B - r0);
@@ -45,13 +47,17 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
     // 16 loads in flight per batch (the rolled loop waited out one L2 round trip per action:
     // ~18 of them before the first row could start), summed in action order
     float c = 0.f;
+    wval[t] = p.w_val2[t];
     for (int a0 = 0; a0 < A; a0 += 16) {
       float v[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) v[u] = p.w_adv2[min(a0 + u, A - 1) * 128 + t];
 #pragma unroll
       for (int u = 0; u < 16; ++u)
-        if (a0 + u < A) c += v[u];
+        if (a0 + u < A) {
+          c += v[u];
+          wadv[a0 + u][t] = v[u];
+        }
     }
     colsum[t] = c;
   }
@@ -104,7 +110,7 @@ __global__ __launch_bounds__(64 * LH_ROWS) void dqn_heads_bwd_k(LossHeadsArgs p)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int j = lane + 64 * k;
-      float d = j < 128 ? g * p.w_adv2[a * 128 + j] - ga * colsum[j] : g * p.w_val2[j - 128];
+      float d = j < 128 ? g * wadv[a][j] - ga * colsum[j] : g * wval[j - 128];
       d = hr[j] > 0.f ? d : 0.f;
       dzs[rr][j] = d;
       if (p.dz) {
