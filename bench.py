@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--envs", type=int, default=256, help="GPU envs (actors) per GPU")
-    ap.add_argument("--actor-steps", type=int, default=1, help="actor steps per learner step")
+    ap.add_argument("--actor-steps", type=int, default=1, help="actor steps per learner step (>= 1)")
     ap.add_argument("--batch", type=int, default=512, help="global batch at N=1 (per-rank batch under weak scaling)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="learner/actor compute precision: fp32 = the reference's (fp32 MFMA kernels), bf16 = opt-in")
@@ -146,7 +146,10 @@ def parse():
     ap.add_argument("--unpaced", action="store_true",
                     help="central topology: actors run free (default: paced at --actor-steps packets per learner "
                          "step per actor through the credit window)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.actor_steps < 1:
+        ap.error("--actor-steps must be >= 1 (the overlapped engine stages one actor step per learner step)")
+    return args
 
 
 def _host_launch_cost(eng, device, n: int = 20) -> float:
