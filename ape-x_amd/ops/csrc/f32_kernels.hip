@@ -1805,7 +1805,7 @@ void f32_conv_bwd(int layer, const void* x, const int* ids, const int* idx, cons
   d.out = dx;
   d.B = B;
   // microbench knob (read once): APEX_F32_BWD_HALF=1 runs only the weight-gradient half of a conv
-  // pair, 2 only the input-gradient half (profiles/r6_sr_dgrad.md: what each half costs alone)
+  // pair, 2 only the input-gradient half (profiles/r6_ab_ledger.md: what each half costs alone)
   static const int halves = [] {
     const char* e = std::getenv("APEX_F32_BWD_HALF");
     return e ? std::atoi(e) : 0;
