@@ -1663,12 +1663,12 @@ static bool learner_sized(const F32Set& set) { return set.n * set.B >= 1024; }
 // alternatives to the defaults): 1 = conv2 on 64 x 64, 2 = conv2 on 128 x 64 as 4 x 1 waves of
 // 32 x 64 / conv3 on 128 x 64 (2 x 2 waves), 3 = conv3 on 128 x 32 (4 x 1 waves)
 // the learner-sized forward tiles when the caller passes tile 0: APEX_F32_TILES="c2,c3" (the
-// microbench tile codes below; unset = the defaults), read once -- a whole-step A/B knob
+// microbench tile codes below, or "c2/c3"; unset = the defaults), read once -- a whole-step A/B knob
 static int default_tile(int layer) {
   static int t2 = -1, t3 = -1;
   if (t2 < 0) {
     t2 = t3 = 0;
-    if (const char* e = std::getenv("APEX_F32_TILES")) std::sscanf(e, "%d,%d", &t2, &t3);
+    if (const char* e = std::getenv("APEX_F32_TILES")) std::sscanf(e, "%d%*c%d", &t2, &t3);  // "c2,c3" or "c2/c3"
   }
   return layer == 2 ? t2 : t3;
 }
